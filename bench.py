@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""ringdp headline benchmark: MNIST ConvNet DDP training throughput (images/sec, whole job).
+
+Metric/config from BASELINE.json: "images/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; DDP
+scaling efficiency" - reference workload W1 (ref/launch_dist.py: ConvNet, CrossEntropyLoss,
+SGD lr 1e-4, DDP over NCCL, launch-style entrypoint), here on ringdp: bf16 MFMA kernels with fp32
+master weights, C++ reducer + RCCL all-reduce over xGMI, fused SGD, whole step in a hipGraph.
+
+Data: synthetic MNIST-shaped uint8 images + labels generated on the device (no dataset download
+is possible offline); Normalize((0.1307,),(0.3081,)) is fused into the first conv kernel.
+Weights: random init (torch.manual_seed(0), PyTorch default init - identical to the reference).
+Scaling: weak (fixed per-rank batch), like the reference.
+
+Usage:
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-rank B]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+      bench.py --gpus N --steps K --warmup W
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "images/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; DDP scaling efficiency"
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch-per-rank", type=int, default=int(os.environ.get("RINGDP_BENCH_BATCH", "4096")))
+    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--first-bucket-mb", type=float, default=None)
+    ap.add_argument("--comm-hook", type=str, default="allreduce", choices=["allreduce", "bf16_compress", "fp16_compress"])
+    ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph per step")
+    ap.add_argument("--pool", type=int, default=8, help="number of distinct synthetic batches cycled")
+    ap.add_argument("--local-rank", "--local_rank", type=int, default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import ringdp
+    import ringdp.distributed as dist
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+    from ringdp.optim import SGD
+    from ringdp.parallel import DistributedDataParallel as DDP
+    from ringdp.utils.graph import StepGraph
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_env = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", args.local_rank if args.local_rank is not None else 0))
+    torch.cuda.set_device(local_rank)
+    if world_env > 1 or "MASTER_ADDR" in os.environ:
+        dist.init_process_group(backend="nccl")
+    else:
+        dist.init_process_group(backend="nccl", store=dist.HashStore(), rank=0, world_size=1)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but world size is {world}; reporting n_gpus={world}", file=sys.stderr)
+    dev = torch.device("cuda", local_rank)
+    B = args.batch_per_rank
+
+    torch.manual_seed(0)
+    model = ConvNet().to(dev)
+    ddp = DDP(model, device_ids=[local_rank], output_device=local_rank, bucket_cap_mb=args.bucket_mb,
+              first_bucket_mb=args.first_bucket_mb)
+    if args.comm_hook != "allreduce":
+        ddp._set_builtin_hook(args.comm_hook)
+    crit = CrossEntropyLoss()
+    opt = SGD(ddp.parameters(), lr=args.lr)
+
+    pool = [ringdp._C.synth_u8_images(B, 28, 28, 10, 1000 * rank + i, dev) for i in range(args.pool)]
+    static_x = torch.empty_like(pool[0][0])
+    static_y = torch.empty_like(pool[0][1])
+
+    def step_on(x, y):
+        out = ddp(x)
+        loss = crit(out, y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    def static_step():
+        return step_on(static_x, static_y)
+
+    use_graph = not args.no_graph
+    graph = None
+    n_warm = max(args.warmup, 3)
+    if use_graph:
+        # eager warmup (bucket rebuild happens at iteration 1), then capture
+        for i in range(2):
+            x, y = pool[i % args.pool]
+            step_on(x, y)
+        static_x.copy_(pool[0][0])
+        static_y.copy_(pool[0][1])
+        graph = StepGraph(static_step, warmup=2).capture()
+        for i in range(n_warm):
+            x, y = pool[i % args.pool]
+            static_x.copy_(x, non_blocking=True)
+            static_y.copy_(y, non_blocking=True)
+            graph.replay()
+    else:
+        for i in range(n_warm):
+            x, y = pool[i % args.pool]
+            step_on(x, y)
+
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for i in range(args.steps):
+        x, y = pool[i % args.pool]
+        if use_graph:
+            static_x.copy_(x, non_blocking=True)
+            static_y.copy_(y, non_blocking=True)
+            loss = graph.replay()
+        else:
+            loss = step_on(x, y)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max = float(t.item())
+    final_loss = float(loss.item()) if loss is not None else float("nan")
+    ms_per_step = 1000.0 * elapsed_max / args.steps
+    value = world * B * args.steps / elapsed_max
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)",
+            "config": {
+                "model": "MNIST ConvNet (ref/launch_dist.py; 113,674 params)",
+                "global_batch": B * world,
+                "per_rank_batch": B,
+                "seq_len": None,
+                "image_shape": [1, 28, 28],
+                "parallelism": f"dp{world}",
+                "optimizer": f"SGD lr={args.lr}",
+                "comm": f"RCCL all-reduce ({args.comm_hook}), buckets cap {args.bucket_mb} MB",
+                "hipgraph": use_graph,
+                "master_weights": "fp32",
+            },
+            "final_loss": round(final_loss, 5),
+        }
+        print(json.dumps(res), flush=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

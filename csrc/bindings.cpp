@@ -1,0 +1,372 @@
+// pybind11 module `ringdp._C`: stores, process groups, reducer, HIP ops.
+#include <torch/extension.h>
+#include <pybind11/chrono.h>
+#include <pybind11/functional.h>
+#include <pybind11/stl.h>
+
+#include "comm/host_ring.h"
+#include "comm/rccl_pg.h"
+#include "ops/ops.h"
+#include "reducer/reducer.h"
+#include "store/store.h"
+
+namespace py = pybind11;
+using namespace ringdp;
+
+namespace {
+
+std::chrono::milliseconds ms(int64_t v) { return std::chrono::milliseconds(v); }
+
+py::bytes to_bytes(const std::string& s) { return py::bytes(s); }
+
+std::string as_str(const py::object& o) {
+  if (py::isinstance<py::bytes>(o)) return o.cast<std::string>();
+  if (py::isinstance<py::str>(o)) return o.cast<std::string>();
+  return py::str(o).cast<std::string>();
+}
+
+// A Store backed by any Python object exposing set/get/add/wait/check/delete_key/num_keys/
+// compare_set (e.g. torch.distributed.TCPStore when ringdp workers are started by torchrun and
+// must rendezvous through the elastic agent's store instead of hosting their own).
+class PyStore : public Store {
+ public:
+  PyStore(py::object obj, std::chrono::milliseconds timeout) : Store(timeout), obj_(std::move(obj)) {}
+  ~PyStore() override {
+    py::gil_scoped_acquire gil;
+    obj_ = py::object();
+  }
+  void set(const std::string& key, const std::string& value) override {
+    py::gil_scoped_acquire gil;
+    obj_.attr("set")(key, py::bytes(value));
+  }
+  std::string get(const std::string& key) override {
+    py::gil_scoped_acquire gil;
+    return obj_.attr("get")(key).cast<std::string>();
+  }
+  int64_t add(const std::string& key, int64_t delta) override {
+    py::gil_scoped_acquire gil;
+    return obj_.attr("add")(key, delta).cast<int64_t>();
+  }
+  std::string compare_set(const std::string& key, const std::string& expected,
+                          const std::string& desired) override {
+    py::gil_scoped_acquire gil;
+    return obj_.attr("compare_set")(key, py::bytes(expected), py::bytes(desired)).cast<std::string>();
+  }
+  bool check(const std::vector<std::string>& keys) override {
+    py::gil_scoped_acquire gil;
+    return obj_.attr("check")(keys).cast<bool>();
+  }
+  void wait(const std::vector<std::string>& keys, std::chrono::milliseconds timeout) override {
+    py::gil_scoped_acquire gil;
+    obj_.attr("wait")(keys, timeout);
+  }
+  bool delete_key(const std::string& key) override {
+    py::gil_scoped_acquire gil;
+    return obj_.attr("delete_key")(key).cast<bool>();
+  }
+  int64_t num_keys() override {
+    py::gil_scoped_acquire gil;
+    return obj_.attr("num_keys")().cast<int64_t>();
+  }
+
+ private:
+  py::object obj_;
+};
+
+// Adapts a Python object with wait()/result() (e.g. a comm-hook future) to a native Work.
+class PyWork : public Work {
+ public:
+  explicit PyWork(py::object obj) : Work(OpType::COALESCED, 0), obj_(std::move(obj)) {}
+  ~PyWork() override {
+    py::gil_scoped_acquire gil;
+    obj_ = py::object();
+  }
+  void wait(bool /*blocking*/) override {
+    py::gil_scoped_acquire gil;
+    py::object r = obj_.attr("wait")();
+    if (py::hasattr(obj_, "result")) {
+      py::object res = obj_.attr("result")();
+      if (py::isinstance<at::Tensor>(res)) {
+        outputs_ = {res.cast<at::Tensor>()};
+      } else {
+        try {
+          outputs_ = res.cast<std::vector<at::Tensor>>();
+        } catch (const py::cast_error&) {
+        }
+      }
+    } else if (py::isinstance<at::Tensor>(r)) {
+      outputs_ = {r.cast<at::Tensor>()};
+    }
+  }
+  bool is_completed() override {
+    py::gil_scoped_acquire gil;
+    if (py::hasattr(obj_, "is_completed")) return obj_.attr("is_completed")().cast<bool>();
+    if (py::hasattr(obj_, "done")) return obj_.attr("done")().cast<bool>();
+    return false;
+  }
+
+ private:
+  py::object obj_;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "ringdp native runtime for AMD MI355X (gfx950): stores, RCCL/host-ring process "
+            "groups, gradient reducer and CDNA4 HIP kernels";
+
+  py::register_exception<RingdpError>(m, "RingdpError", PyExc_RuntimeError);
+  py::register_exception<TimeoutError>(m, "DistTimeoutError", PyExc_TimeoutError);
+
+  // ---------------------------------------------------------------- stores
+  py::class_<Store, std::shared_ptr<Store>>(m, "Store")
+      .def("set", [](Store& s, const std::string& k, const py::object& v) { s.set(k, as_str(v)); })
+      .def("get",
+           [](Store& s, const std::string& k) {
+             std::string v;
+             {
+               py::gil_scoped_release nogil;
+               v = s.get(k);
+             }
+             return to_bytes(v);
+           })
+      .def("add", &Store::add, py::call_guard<py::gil_scoped_release>())
+      .def("compare_set",
+           [](Store& s, const std::string& k, const py::object& e, const py::object& d) {
+             std::string es = as_str(e), ds = as_str(d), v;
+             {
+               py::gil_scoped_release nogil;
+               v = s.compare_set(k, es, ds);
+             }
+             return to_bytes(v);
+           })
+      .def("check", &Store::check, py::call_guard<py::gil_scoped_release>())
+      .def("wait",
+           [](Store& s, const std::vector<std::string>& keys) {
+             py::gil_scoped_release nogil;
+             s.wait(keys);
+           })
+      .def("wait",
+           [](Store& s, const std::vector<std::string>& keys, const std::chrono::milliseconds& t) {
+             py::gil_scoped_release nogil;
+             s.wait(keys, t);
+           })
+      .def("delete_key", &Store::delete_key, py::call_guard<py::gil_scoped_release>())
+      .def("num_keys", &Store::num_keys, py::call_guard<py::gil_scoped_release>())
+      .def_property("timeout", &Store::timeout, &Store::set_timeout)
+      .def("set_timeout", &Store::set_timeout);
+
+  py::class_<HashStore, Store, std::shared_ptr<HashStore>>(m, "HashStore")
+      .def(py::init([](int64_t timeout_ms) { return std::make_shared<HashStore>(ms(timeout_ms)); }),
+           py::arg("timeout_ms") = 300000);
+
+  py::class_<PrefixStore, Store, std::shared_ptr<PrefixStore>>(m, "PrefixStore")
+      .def(py::init([](const std::string& prefix, std::shared_ptr<Store> base) {
+             return std::make_shared<PrefixStore>(prefix, std::move(base));
+           }),
+           py::arg("prefix"), py::arg("store"))
+      .def_property_readonly("underlying_store", &PrefixStore::underlying)
+      .def_property_readonly("prefix", &PrefixStore::prefix);
+
+  py::class_<TCPStore, Store, std::shared_ptr<TCPStore>>(m, "TCPStore")
+      .def(py::init([](const std::string& host, int port, int world_size, bool is_master,
+                       int64_t timeout_ms, bool wait_for_workers) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<TCPStore>(host, port, is_master, ms(timeout_ms), world_size,
+                                               wait_for_workers);
+           }),
+           py::arg("host_name"), py::arg("port"), py::arg("world_size") = -1,
+           py::arg("is_master") = false, py::arg("timeout_ms") = 300000,
+           py::arg("wait_for_workers") = false)
+      .def_property_readonly("port", &TCPStore::port)
+      .def_property_readonly("host", &TCPStore::host)
+      .def_property_readonly("is_master", &TCPStore::is_master);
+
+  py::class_<FileStore, Store, std::shared_ptr<FileStore>>(m, "FileStore")
+      .def(py::init([](const std::string& path, int world_size, int64_t timeout_ms) {
+             return std::make_shared<FileStore>(path, world_size, ms(timeout_ms));
+           }),
+           py::arg("path"), py::arg("world_size") = -1, py::arg("timeout_ms") = 300000);
+
+  py::class_<PyStore, Store, std::shared_ptr<PyStore>>(m, "PyStore")
+      .def(py::init([](py::object obj, int64_t timeout_ms) {
+             return std::make_shared<PyStore>(std::move(obj), ms(timeout_ms));
+           }),
+           py::arg("store"), py::arg("timeout_ms") = 300000);
+
+  // ---------------------------------------------------------------- process groups
+  py::enum_<ReduceOp>(m, "ReduceOp")
+      .value("SUM", ReduceOp::SUM)
+      .value("PRODUCT", ReduceOp::PRODUCT)
+      .value("MIN", ReduceOp::MIN)
+      .value("MAX", ReduceOp::MAX)
+      .value("AVG", ReduceOp::AVG)
+      .value("BAND", ReduceOp::BAND)
+      .value("BOR", ReduceOp::BOR)
+      .value("BXOR", ReduceOp::BXOR);
+
+  py::class_<Work, std::shared_ptr<Work>>(m, "Work")
+      .def("wait",
+           [](Work& w, bool blocking) {
+             py::gil_scoped_release nogil;
+             w.wait(blocking);
+             return true;
+           },
+           py::arg("blocking") = false)
+      .def("is_completed", &Work::is_completed)
+      .def("synchronize", &Work::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("result", [](Work& w) { return w.result(); })
+      .def_property_readonly("seq", &Work::seq)
+      .def_property_readonly("op", [](Work& w) { return std::string(op_name(w.op())); })
+      .def("duration_us", &Work::duration_us);
+
+  py::class_<ProcessGroup, std::shared_ptr<ProcessGroup>>(m, "ProcessGroup")
+      .def("rank", &ProcessGroup::rank)
+      .def("size", &ProcessGroup::size)
+      .def("backend_name", &ProcessGroup::backend_name)
+      .def("seq", &ProcessGroup::seq)
+      .def("allreduce", &ProcessGroup::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_coalesced", &ProcessGroup::allreduce_coalesced,
+           py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &ProcessGroup::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &ProcessGroup::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("allgather_into_tensor", &ProcessGroup::allgather_into_tensor,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter_tensor", &ProcessGroup::reduce_scatter_tensor,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reduce", &ProcessGroup::reduce, py::call_guard<py::gil_scoped_release>())
+      .def("gather", &ProcessGroup::gather, py::call_guard<py::gil_scoped_release>())
+      .def("scatter", &ProcessGroup::scatter, py::call_guard<py::gil_scoped_release>())
+      .def("alltoall_base",
+           [](ProcessGroup& pg, at::Tensor& out, const at::Tensor& in,
+              std::vector<int64_t> out_splits, std::vector<int64_t> in_splits) {
+             py::gil_scoped_release nogil;
+             AllToAllSplits sp{std::move(out_splits), std::move(in_splits)};
+             return pg.alltoall_base(out, in, sp);
+           })
+      .def("send", &ProcessGroup::send, py::call_guard<py::gil_scoped_release>())
+      .def("recv", &ProcessGroup::recv, py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &ProcessGroup::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("split", &ProcessGroup::split, py::call_guard<py::gil_scoped_release>())
+      .def("shutdown", &ProcessGroup::shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &ProcessGroup::abort, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<HostRingPG, ProcessGroup, std::shared_ptr<HostRingPG>>(m, "HostRingPG")
+      .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int64_t timeout_ms,
+                       const std::string& bind_hint) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<HostRingPG>(std::move(store), rank, size, ms(timeout_ms),
+                                                 bind_hint);
+           }),
+           py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("timeout_ms") = 1800000,
+           py::arg("bind_hint") = "127.0.0.1");
+
+  py::class_<RcclPG, ProcessGroup, std::shared_ptr<RcclPG>>(m, "RcclPG")
+      .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int device,
+                       int64_t timeout_ms) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<RcclPG>(std::move(store), rank, size, device, ms(timeout_ms));
+           }),
+           py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"),
+           py::arg("timeout_ms") = 600000)
+      .def_property_readonly("device", &RcclPG::device)
+      .def("aborted", &RcclPG::aborted)
+      .def("drain", &RcclPG::drain, py::call_guard<py::gil_scoped_release>())
+      .def("error_message", &RcclPG::error_message)
+      .def("set_timing", &RcclPG::set_timing)
+      .def("timing", &RcclPG::timing)
+      .def("set_async_error_handling", &RcclPG::set_async_error_handling)
+      .def("comm_stream_ptr",
+           [](RcclPG& pg) { return reinterpret_cast<uintptr_t>(pg.comm_stream()); });
+
+  m.def("rccl_version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+
+  // ---------------------------------------------------------------- reducer
+  py::enum_<CommHook>(m, "CommHook")
+      .value("ALLREDUCE", CommHook::ALLREDUCE)
+      .value("BF16_COMPRESS", CommHook::BF16_COMPRESS)
+      .value("FP16_COMPRESS", CommHook::FP16_COMPRESS)
+      .value("PYTHON", CommHook::PYTHON)
+      .value("NONE", CommHook::NONE);
+
+  py::class_<BucketStats>(m, "BucketStats")
+      .def_readonly("numel", &BucketStats::numel)
+      .def_readonly("bytes", &BucketStats::bytes)
+      .def_readonly("last_ready_us", &BucketStats::last_ready_us)
+      .def_readonly("last_launch_us", &BucketStats::last_launch_us)
+      .def_readonly("last_comm_us", &BucketStats::last_comm_us)
+      .def_readonly("total_comm_us", &BucketStats::total_comm_us)
+      .def_readonly("comm_samples", &BucketStats::comm_samples);
+
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init<std::vector<at::Tensor>, std::vector<std::vector<int64_t>>,
+                    std::shared_ptr<ProcessGroup>, bool, int64_t>(),
+           py::arg("params"), py::arg("bucket_indices"), py::arg("process_group"),
+           py::arg("find_unused_parameters") = false, py::arg("pad_elems") = 16)
+      .def("prepare_for_forward", &Reducer::prepare_for_forward)
+      .def("prepare_for_backward", &Reducer::prepare_for_backward)
+      .def("set_require_sync", &Reducer::set_require_sync)
+      .def("require_sync", &Reducer::require_sync)
+      .def("set_comm_hook", &Reducer::set_comm_hook)
+      .def("comm_hook", &Reducer::comm_hook)
+      .def("set_python_hook",
+           [](Reducer& r, py::function fn) {
+             auto holder = std::make_shared<py::function>(std::move(fn));
+             r.set_python_hook([holder](int64_t idx, at::Tensor flat) -> std::shared_ptr<Work> {
+               py::gil_scoped_acquire gil;
+               py::object res = (*holder)(idx, flat);
+               if (res.is_none()) return nullptr;
+               if (py::isinstance<Work>(res)) return res.cast<std::shared_ptr<Work>>();
+               return std::make_shared<PyWork>(res);
+             });
+           })
+      .def("grad_slots", &Reducer::grad_slots)
+      .def("flat_buffers", &Reducer::flat_buffers)
+      .def("param_offsets", &Reducer::param_offsets)
+      .def("bucket_indices", &Reducer::bucket_indices)
+      .def("bucket_numels", &Reducer::bucket_numels)
+      .def("ready_order", &Reducer::ready_order)
+      .def("rebuilt", &Reducer::rebuilt)
+      .def("rebuild_buckets", &Reducer::rebuild_buckets)
+      .def("iteration", &Reducer::iteration)
+      .def("stats", &Reducer::stats);
+
+  m.def("compute_bucket_assignment_by_size",
+        [](const std::vector<at::Tensor>& tensors, const std::vector<int64_t>& limits,
+           const std::vector<bool>& expect_sparse, const std::vector<int64_t>& tensor_indices) {
+          return compute_bucket_assignment_by_size(tensors, limits, expect_sparse, tensor_indices);
+        },
+        py::arg("tensors"), py::arg("bucket_size_limits"),
+        py::arg("expect_sparse_gradient") = std::vector<bool>{},
+        py::arg("tensor_indices") = std::vector<int64_t>{});
+
+  // ---------------------------------------------------------------- ops
+  py::class_<ops::SgdHyper>(m, "SgdHyper")
+      .def(py::init<>())
+      .def_readwrite("lr", &ops::SgdHyper::lr)
+      .def_readwrite("momentum", &ops::SgdHyper::momentum)
+      .def_readwrite("dampening", &ops::SgdHyper::dampening)
+      .def_readwrite("weight_decay", &ops::SgdHyper::weight_decay)
+      .def_readwrite("nesterov", &ops::SgdHyper::nesterov)
+      .def_readwrite("maximize", &ops::SgdHyper::maximize);
+  m.def("cast_copy", &ops::cast_copy);
+  m.def("sgd_flat", &ops::sgd_flat, py::arg("param"), py::arg("grad"), py::arg("momentum_buf"),
+        py::arg("hyper"), py::arg("first_step"), py::arg("lr_tensor") = py::none(),
+        py::arg("grad_scale") = py::none());
+  m.def("sgd_multi", &ops::sgd_multi, py::arg("params"), py::arg("grads"), py::arg("bufs"),
+        py::arg("hyper"), py::arg("first_step"), py::arg("lr_tensor") = py::none(),
+        py::arg("grad_scale") = py::none());
+  m.def("cross_entropy_fwd", &ops::cross_entropy_fwd);
+  m.def("cross_entropy_bwd", &ops::cross_entropy_bwd);
+  m.def("convnet_conv1_fwd", &ops::convnet_conv1_fwd);
+  m.def("convnet_conv1_wgrad", &ops::convnet_conv1_wgrad);
+  m.def("convnet_conv_fwd", &ops::convnet_conv_fwd);
+  m.def("convnet_conv_bwd", &ops::convnet_conv_bwd);
+  m.def("convnet_fc_fwd", &ops::convnet_fc_fwd);
+  m.def("convnet_fc_bwd", &ops::convnet_fc_bwd);
+  m.def("synth_u8_images", &ops::synth_u8_images);
+}

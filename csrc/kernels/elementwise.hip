@@ -1,0 +1,338 @@
+// ringdp elementwise / optimizer / loss kernels for CDNA4 (gfx950).
+//
+//  * SGD: one fused, float4-vectorised kernel over the DDP flat parameter range (replaces the
+//    ~5 _foreach_* launches of torch's multi-tensor SGD); the math is
+//    torch/optim/sgd.py:343-380 (wd, momentum/dampening, nesterov, maximize).
+//  * split-K reduction used by every weight-gradient kernel (deterministic slice order).
+//  * cross entropy forward (lse + mean loss, last-arriving workgroup reduces the partials in a
+//    fixed order) and backward (softmax - target).
+#include "device_common.h"
+#include "kernels.h"
+
+namespace ringdp {
+namespace kern {
+
+using namespace ringdp::dev;
+
+namespace {
+
+inline int grid_for(int64_t work, int block, int cap = 4096) {
+  int64_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<int>(g);
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = reinterpret_cast<const float4*>(src)[i];
+    bf16x4 o = {(bf16)v.x, (bf16)v.y, (bf16)v.z, (bf16)v.w};
+    reinterpret_cast<bf16x4*>(dst)[i] = o;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = (bf16)src[i];
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    bf16x4 v = reinterpret_cast<const bf16x4*>(src)[i];
+    reinterpret_cast<float4*>(dst)[i] = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = (float)src[i];
+}
+
+__global__ void cast_f32_f16_kernel(const float* __restrict__ src, _Float16* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = (_Float16)src[i];
+}
+
+__global__ void cast_f16_f32_kernel(const _Float16* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dst[i] = (float)src[i];
+}
+
+struct SgdDev {
+  float lr, momentum, dampening, weight_decay, inv_scale;
+  bool nesterov, maximize, first;
+};
+
+__device__ __forceinline__ SgdDev load_sgd(const SgdArgs& a) {
+  SgdDev d;
+  d.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
+  d.inv_scale = a.grad_scale_ptr ? 1.0f / *a.grad_scale_ptr : 1.0f;
+  d.momentum = a.momentum;
+  d.dampening = a.dampening;
+  d.weight_decay = a.weight_decay;
+  d.nesterov = a.nesterov;
+  d.maximize = a.maximize;
+  d.first = a.first_step;
+  return d;
+}
+
+template <bool MOM>
+__device__ __forceinline__ void sgd_elem(float& p, float g, float& m, const SgdDev& d) {
+  g *= d.inv_scale;
+  if (d.maximize) g = -g;
+  if (d.weight_decay != 0.f) g = fmaf(d.weight_decay, p, g);
+  if (MOM) {
+    m = d.first ? g : fmaf(d.momentum, m, (1.f - d.dampening) * g);
+    g = d.nesterov ? fmaf(d.momentum, m, g) : m;
+  }
+  p = fmaf(-d.lr, g, p);
+}
+
+template <bool MOM>
+__global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ m, int64_t n, SgdArgs a) {
+  const SgdDev d = load_sgd(a);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n / 4;
+  float4 dummy = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = MOM ? reinterpret_cast<float4*>(m)[i] : dummy;
+    sgd_elem<MOM>(pv.x, gv.x, mv.x, d);
+    sgd_elem<MOM>(pv.y, gv.y, mv.y, d);
+    sgd_elem<MOM>(pv.z, gv.z, mv.z, d);
+    sgd_elem<MOM>(pv.w, gv.w, mv.w, d);
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if (MOM) reinterpret_cast<float4*>(m)[i] = mv;
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pv = p[i], mv = MOM ? m[i] : 0.f;
+    sgd_elem<MOM>(pv, g[i], mv, d);
+    p[i] = pv;
+    if (MOM) m[i] = mv;
+  }
+}
+
+template <bool MOM>
+__global__ __launch_bounds__(256) void sgd_multi_kernel(const SgdTensor* __restrict__ table,
+                                                        const int64_t* __restrict__ chunks,
+                                                        int64_t chunk_elems, SgdArgs a) {
+  const SgdDev d = load_sgd(a);
+  const int64_t t = chunks[2 * blockIdx.x];
+  const int64_t start = chunks[2 * blockIdx.x + 1];
+  const SgdTensor T = table[t];
+  const int64_t end = start + chunk_elems < T.n ? start + chunk_elems : T.n;
+  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    float pv = T.p[i], mv = MOM ? T.m[i] : 0.f;
+    sgd_elem<MOM>(pv, T.g[i], mv, d);
+    T.p[i] = pv;
+    if (MOM) T.m[i] = mv;
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ slabs, int S,
+                                                            int64_t n, float* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if ((n & 3) == 0) {
+    const int64_t n4 = n / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+      float4 acc = reinterpret_cast<const float4*>(slabs)[i];
+      for (int s = 1; s < S; ++s) {
+        float4 v = reinterpret_cast<const float4*>(slabs + (int64_t)s * n)[i];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      reinterpret_cast<float4*>(out)[i] = acc;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      float acc = slabs[i];
+      for (int s = 1; s < S; ++s) acc += slabs[(int64_t)s * n + i];
+      out[i] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- cross entropy
+__global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits,
+                                                     const int64_t* __restrict__ labels, int B, int C,
+                                                     int ignore_index, float eps, int reduction,
+                                                     float* __restrict__ lse_out, float* __restrict__ loss,
+                                                     float* __restrict__ partials, unsigned* counter,
+                                                     int nparts) {
+  __shared__ float s_sum[4], s_cnt[4];
+  __shared__ int s_last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float wsum = 0.f, wcnt = 0.f;
+  for (int r = blockIdx.x * 4 + wave; r < B; r += nparts * 4) {
+    const float* x = logits + (int64_t)r * C;
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, x[c]);
+    mx = wave_max(mx);
+    float se = 0.f, sx = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      se += __expf(x[c] - mx);
+      sx += x[c];
+    }
+    se = wave_sum(se);
+    sx = wave_sum(sx);
+    const float lse = mx + __logf(se);
+    const int64_t y = labels[r];
+    float l = 0.f, valid = 0.f;
+    if (y != ignore_index) {
+      l = (1.f - eps) * (lse - x[y]) + eps * (lse - sx / (float)C);
+      valid = 1.f;
+    }
+    if (lane == 0) {
+      lse_out[r] = lse;
+      if (reduction == 0) loss[r] = l;
+    }
+    wsum += l;
+    wcnt += valid;
+  }
+  if (reduction == 0) return;
+  if (lane == 0) {
+    s_sum[wave] = wsum;
+    s_cnt[wave] = wcnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    partials[2 * blockIdx.x + 1] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    // Publish the partial (agent-scope release), then take a ticket; the last arriver reduces.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == (unsigned)nparts - 1);
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    float s = 0.f, c = 0.f;
+    for (int i = 0; i < nparts; ++i) {  // fixed order: deterministic
+      s += __builtin_nontemporal_load(&partials[2 * i]);
+      c += __builtin_nontemporal_load(&partials[2 * i + 1]);
+    }
+    const float denom = reduction == 1 ? c : 1.f;
+    partials[2 * nparts] = denom;
+    loss[0] = reduction == 1 ? s / denom : s;
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(256) void ce_bwd_kernel(const float* __restrict__ logits,
+                                                     const int64_t* __restrict__ labels,
+                                                     const float* __restrict__ lse,
+                                                     const float* __restrict__ grad_out,
+                                                     const float* __restrict__ denom, int B, int C,
+                                                     int ignore_index, float eps, int reduction,
+                                                     float* __restrict__ dlogits) {
+  const int64_t n = (int64_t)B * C;
+  const float scale_all = reduction == 0 ? 1.f : grad_out[0] / denom[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / C), c = (int)(i % C);
+    const int64_t y = labels[r];
+    float g = 0.f;
+    if (y != ignore_index) {
+      const float p = __expf(logits[i] - lse[r]);
+      const float q = (c == y ? (1.f - eps) : 0.f) + eps / (float)C;
+      g = (p - q) * (reduction == 0 ? grad_out[r] : scale_all);
+    }
+    dlogits[i] = g;
+  }
+}
+
+// ---------------------------------------------------------------- synthetic data
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdULL;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ULL;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+__global__ void synth_u8_kernel(uint8_t* __restrict__ x, int64_t* __restrict__ labels, int B, int HW,
+                                int num_classes, uint64_t seed) {
+  const int64_t n = (int64_t)B * HW;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    x[i] = (uint8_t)(hash32(seed * 0x9E3779B97F4A7C15ULL + (uint64_t)i) & 0xff);
+    if (i < B) labels[i] = (int64_t)(hash32(~seed + 0x1234567ULL * (uint64_t)(i + 1)) % num_classes);
+  }
+}
+
+}  // namespace
+
+void cast_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  cast_f32_bf16_kernel<<<grid_for(n / 4 + 1, 256), 256, 0, s>>>(src, static_cast<bf16*>(dst), n);
+}
+void cast_bf16_to_f32(const void* src, float* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  cast_bf16_f32_kernel<<<grid_for(n / 4 + 1, 256), 256, 0, s>>>(static_cast<const bf16*>(src), dst, n);
+}
+void cast_f32_to_f16(const float* src, void* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  cast_f32_f16_kernel<<<grid_for(n, 256), 256, 0, s>>>(src, static_cast<_Float16*>(dst), n);
+}
+void cast_f16_to_f32(const void* src, float* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  cast_f16_f32_kernel<<<grid_for(n, 256), 256, 0, s>>>(static_cast<const _Float16*>(src), dst, n);
+}
+
+void sgd_flat(float* p, const float* g, float* m, int64_t n, const SgdArgs& a, hipStream_t s) {
+  if (n <= 0) return;
+  const int grid = grid_for(n / 4 + 1, 256, 2048);
+  if (m && a.momentum != 0.f)
+    sgd_flat_kernel<true><<<grid, 256, 0, s>>>(p, g, m, n, a);
+  else
+    sgd_flat_kernel<false><<<grid, 256, 0, s>>>(p, g, m, n, a);
+}
+
+void sgd_multi(const SgdTensor* table, const int64_t* chunks, int64_t nchunks, int64_t chunk_elems,
+               const SgdArgs& a, hipStream_t s) {
+  if (nchunks <= 0) return;
+  if (a.momentum != 0.f)
+    sgd_multi_kernel<true><<<(unsigned)nchunks, 256, 0, s>>>(table, chunks, chunk_elems, a);
+  else
+    sgd_multi_kernel<false><<<(unsigned)nchunks, 256, 0, s>>>(table, chunks, chunk_elems, a);
+}
+
+void splitk_reduce(const float* slabs, int nslices, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  splitk_reduce_kernel<<<grid_for(n / 4 + 1, 256, 1024), 256, 0, s>>>(slabs, nslices, n, out);
+}
+
+void cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, int ignore_index,
+                       float label_smoothing, int reduction, float* lse, float* loss,
+                       float* partials, unsigned* counter, int nparts, hipStream_t s) {
+  ce_fwd_kernel<<<nparts, 256, 0, s>>>(logits, labels, B, C, ignore_index, label_smoothing,
+                                       reduction, lse, loss, partials, counter, nparts);
+}
+
+void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* lse,
+                       const float* grad_out, const float* denom, int B, int C, int ignore_index,
+                       float label_smoothing, int reduction, float* dlogits, hipStream_t s) {
+  const int64_t n = (int64_t)B * C;
+  ce_bwd_kernel<<<grid_for(n, 256, 1024), 256, 0, s>>>(logits, labels, lse, grad_out, denom, B, C,
+                                                       ignore_index, label_smoothing, reduction,
+                                                       dlogits);
+}
+
+void synth_u8_images(uint8_t* x, int64_t* labels, int B, int HW, int num_classes, uint64_t seed,
+                     hipStream_t s) {
+  const int64_t n = (int64_t)B * HW;
+  synth_u8_kernel<<<grid_for(n, 256, 2048), 256, 0, s>>>(x, labels, B, HW, num_classes, seed);
+}
+
+}  // namespace kern
+}  // namespace ringdp

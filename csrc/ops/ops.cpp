@@ -1,0 +1,385 @@
+// Tensor-level wrappers around ringdp's HIP kernels.
+#include "ops.h"
+
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+
+#include "../common.h"
+#include "../kernels/kernels.h"
+
+namespace ringdp {
+namespace ops {
+
+namespace {
+
+hipStream_t cur_stream(const at::Tensor& t) {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.get_device()).stream();
+}
+
+void check_cuda(const at::Tensor& t, const char* name) {
+  RINGDP_CHECK(t.defined(), name, ": undefined tensor");
+  RINGDP_CHECK(t.is_cuda(), name, ": expected a GPU tensor (ringdp HIP kernel), got ", t.device());
+  RINGDP_CHECK(t.is_contiguous(), name, ": expected a contiguous tensor");
+}
+
+void check_dtype(const at::Tensor& t, at::ScalarType d, const char* name) {
+  RINGDP_CHECK(t.scalar_type() == d, name, ": expected dtype ", c10::toString(d), ", got ",
+               c10::toString(t.scalar_type()));
+}
+
+void check_shape(const at::Tensor& t, at::IntArrayRef s, const char* name) {
+  RINGDP_CHECK(t.sizes() == s, name, ": expected shape ", s, ", got ", t.sizes());
+}
+
+// Persistent, zero-initialised arrival counters for last-arriver reductions.  Each call takes
+// the next slot; the kernel's last workgroup resets its slot to 0, so no per-call memset launch
+// is needed (and the slot index is stable under hipGraph capture).
+unsigned* next_counter(const at::Tensor& like) {
+  constexpr int kSlots = 4096;
+  static std::mutex mu;
+  static std::map<int, std::pair<at::Tensor, int>> pools;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& e = pools[like.get_device()];
+  if (!e.first.defined()) {
+    e.first = at::zeros({kSlots}, like.options().dtype(at::kInt));
+    e.second = 0;
+  }
+  unsigned* p = reinterpret_cast<unsigned*>(e.first.data_ptr<int>()) + e.second;
+  e.second = (e.second + 16) % kSlots;  // 64-byte spacing between live counters
+  return p;
+}
+
+bool aligned16(const at::Tensor& t) {
+  return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0;
+}
+
+kern::SgdArgs make_args(const SgdHyper& h, bool first, const c10::optional<at::Tensor>& lr_t,
+                        const c10::optional<at::Tensor>& scale_t) {
+  kern::SgdArgs a{};
+  a.lr = static_cast<float>(h.lr);
+  a.momentum = static_cast<float>(h.momentum);
+  a.dampening = static_cast<float>(h.dampening);
+  a.weight_decay = static_cast<float>(h.weight_decay);
+  a.nesterov = h.nesterov;
+  a.maximize = h.maximize;
+  a.first_step = first;
+  a.lr_ptr = nullptr;
+  a.grad_scale_ptr = nullptr;
+  if (lr_t && lr_t->defined()) {
+    check_cuda(*lr_t, "lr tensor");
+    check_dtype(*lr_t, at::kFloat, "lr tensor");
+    a.lr_ptr = lr_t->data_ptr<float>();
+  }
+  if (scale_t && scale_t->defined()) {
+    check_cuda(*scale_t, "grad_scale tensor");
+    check_dtype(*scale_t, at::kFloat, "grad_scale tensor");
+    a.grad_scale_ptr = scale_t->data_ptr<float>();
+  }
+  return a;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ casts
+void cast_copy(at::Tensor dst, const at::Tensor& src) {
+  RINGDP_CHECK(dst.numel() == src.numel(), "cast_copy: numel mismatch");
+  if (!dst.is_cuda()) {
+    dst.copy_(src.view(dst.sizes()));
+    return;
+  }
+  check_cuda(dst, "cast_copy dst");
+  check_cuda(src, "cast_copy src");
+  const int64_t n = src.numel();
+  hipStream_t s = cur_stream(dst);
+  auto sd = src.scalar_type(), dd = dst.scalar_type();
+  const bool vec = aligned16(src) && aligned16(dst);
+  if (sd == at::kFloat && dd == at::kBFloat16 && vec) {
+    kern::cast_f32_to_bf16(src.data_ptr<float>(), dst.data_ptr(), n, s);
+  } else if (sd == at::kBFloat16 && dd == at::kFloat && vec) {
+    kern::cast_bf16_to_f32(src.data_ptr(), dst.data_ptr<float>(), n, s);
+  } else if (sd == at::kFloat && dd == at::kHalf) {
+    kern::cast_f32_to_f16(src.data_ptr<float>(), dst.data_ptr(), n, s);
+  } else if (sd == at::kHalf && dd == at::kFloat) {
+    kern::cast_f16_to_f32(src.data_ptr(), dst.data_ptr<float>(), n, s);
+  } else if (sd == dd) {
+    dst.copy_(src.view(dst.sizes()));
+  } else {
+    RINGDP_CHECK(false, "cast_copy: unsupported conversion ", c10::toString(sd), " -> ",
+                 c10::toString(dd), vec ? "" : " (unaligned)");
+  }
+}
+
+// ------------------------------------------------------------------ SGD
+void sgd_flat(at::Tensor param, const at::Tensor& grad, at::Tensor buf, const SgdHyper& h,
+              bool first_step, const c10::optional<at::Tensor>& lr_t,
+              const c10::optional<at::Tensor>& scale_t) {
+  check_cuda(param, "sgd param");
+  check_cuda(grad, "sgd grad");
+  check_dtype(param, at::kFloat, "sgd param");
+  check_dtype(grad, at::kFloat, "sgd grad");
+  RINGDP_CHECK(param.numel() == grad.numel(), "sgd_flat: param/grad numel mismatch");
+  float* m = nullptr;
+  if (h.momentum != 0.0) {
+    check_cuda(buf, "sgd momentum buffer");
+    RINGDP_CHECK(buf.numel() == param.numel(), "sgd_flat: momentum buffer numel mismatch");
+    m = buf.data_ptr<float>();
+  }
+  RINGDP_CHECK(aligned16(param) && aligned16(grad) && (!m || aligned16(buf)),
+               "sgd_flat: buffers must be 16-byte aligned");
+  kern::sgd_flat(param.data_ptr<float>(), grad.data_ptr<float>(), m, param.numel(),
+                 make_args(h, first_step, lr_t, scale_t), cur_stream(param));
+}
+
+void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
+               std::vector<at::Tensor> bufs, const SgdHyper& h, bool first_step,
+               const c10::optional<at::Tensor>& lr_t, const c10::optional<at::Tensor>& scale_t) {
+  RINGDP_CHECK(params.size() == grads.size(), "sgd_multi: params/grads length mismatch");
+  if (params.empty()) return;
+  const bool mom = h.momentum != 0.0;
+  if (mom) RINGDP_CHECK(bufs.size() == params.size(), "sgd_multi: need one buffer per param");
+  constexpr int64_t kChunk = 65536;
+  std::vector<kern::SgdTensor> table(params.size());
+  std::vector<int64_t> chunks;
+  for (size_t i = 0; i < params.size(); ++i) {
+    check_cuda(params[i], "sgd param");
+    check_cuda(grads[i], "sgd grad");
+    check_dtype(params[i], at::kFloat, "sgd param");
+    check_dtype(grads[i], at::kFloat, "sgd grad");
+    RINGDP_CHECK(params[i].numel() == grads[i].numel(), "sgd_multi: numel mismatch at ", i);
+    table[i] = {params[i].data_ptr<float>(), grads[i].data_ptr<float>(),
+                mom ? bufs[i].data_ptr<float>() : nullptr, params[i].numel()};
+    for (int64_t s = 0; s < params[i].numel(); s += kChunk) {
+      chunks.push_back(static_cast<int64_t>(i));
+      chunks.push_back(s);
+    }
+  }
+  const int64_t tbytes = static_cast<int64_t>(table.size() * sizeof(kern::SgdTensor));
+  const int64_t cbytes = static_cast<int64_t>(chunks.size() * sizeof(int64_t));
+  at::Tensor host = at::empty({tbytes + cbytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  std::memcpy(host.data_ptr(), table.data(), tbytes);
+  std::memcpy(static_cast<char*>(host.data_ptr()) + tbytes, chunks.data(), cbytes);
+  at::Tensor dev = host.to(params[0].device(), /*non_blocking=*/true);
+  auto* dtable = reinterpret_cast<const kern::SgdTensor*>(dev.data_ptr());
+  auto* dchunks = reinterpret_cast<const int64_t*>(static_cast<char*>(dev.data_ptr()) + tbytes);
+  kern::sgd_multi(dtable, dchunks, static_cast<int64_t>(chunks.size() / 2), kChunk,
+                  make_args(h, first_step, lr_t, scale_t), cur_stream(params[0]));
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_fwd(const at::Tensor& logits,
+                                                                 const at::Tensor& labels,
+                                                                 int64_t ignore_index,
+                                                                 double smoothing,
+                                                                 int64_t reduction) {
+  check_cuda(logits, "cross_entropy logits");
+  check_cuda(labels, "cross_entropy labels");
+  check_dtype(logits, at::kFloat, "cross_entropy logits");
+  check_dtype(labels, at::kLong, "cross_entropy labels");
+  RINGDP_CHECK(logits.dim() == 2 && labels.dim() == 1 && labels.size(0) == logits.size(0),
+               "cross_entropy: expected logits [B, C] and labels [B]");
+  const int B = static_cast<int>(logits.size(0)), C = static_cast<int>(logits.size(1));
+  const int nparts = std::max(1, std::min(256, (B + 63) / 64));
+  auto fo = logits.options();
+  at::Tensor lse = at::empty({B}, fo);
+  at::Tensor loss = reduction == 0 ? at::empty({B}, fo) : at::empty({}, fo);
+  // ws: [2*nparts partials][denom][3 pad]
+  at::Tensor ws = at::empty({2 * nparts + 4}, fo);
+  unsigned* counter = next_counter(logits);
+  kern::cross_entropy_fwd(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), B, C,
+                          static_cast<int>(ignore_index), static_cast<float>(smoothing),
+                          static_cast<int>(reduction), lse.data_ptr<float>(),
+                          loss.data_ptr<float>(), ws.data_ptr<float>(), counter, nparts,
+                          cur_stream(logits));
+  return {loss, lse, ws};
+}
+
+at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& labels,
+                             const at::Tensor& lse, const at::Tensor& ws,
+                             const at::Tensor& grad_out, int64_t ignore_index, double smoothing,
+                             int64_t reduction) {
+  check_cuda(grad_out, "cross_entropy grad_out");
+  at::Tensor g = grad_out.to(at::kFloat).contiguous();
+  const int B = static_cast<int>(logits.size(0)), C = static_cast<int>(logits.size(1));
+  const int nparts = static_cast<int>((ws.numel() - 4) / 2);
+  at::Tensor d = at::empty_like(logits);
+  kern::cross_entropy_bwd(logits.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                          lse.data_ptr<float>(), g.data_ptr<float>(),
+                          ws.data_ptr<float>() + 2 * nparts, B, C, static_cast<int>(ignore_index),
+                          static_cast<float>(smoothing), static_cast<int>(reduction),
+                          d.data_ptr<float>(), cur_stream(logits));
+  return d;
+}
+
+// ------------------------------------------------------------------ ConvNet
+namespace {
+void check_input(const at::Tensor& x, int64_t& B, bool& u8) {
+  check_cuda(x, "convnet input");
+  RINGDP_CHECK(x.dim() == 4 && x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28,
+               "convnet input: expected [B, 1, 28, 28], got ", x.sizes());
+  RINGDP_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kByte,
+               "convnet input: expected float32 or uint8");
+  B = x.size(0);
+  u8 = x.scalar_type() == at::kByte;
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> convnet_conv1_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                     const at::Tensor& b, double mean,
+                                                     double std, double in_scale) {
+  int64_t B;
+  bool u8;
+  check_input(x, B, u8);
+  check_cuda(w, "conv1 weight");
+  check_cuda(b, "conv1 bias");
+  check_dtype(w, at::kFloat, "conv1 weight");
+  check_shape(w, {32, 1, 5, 5}, "conv1 weight");
+  check_shape(b, {32}, "conv1 bias");
+  auto opt = x.options();
+  at::Tensor a1 = at::empty({B, 13, 13, 32}, opt.dtype(at::kBFloat16));
+  at::Tensor idx = at::empty({B, 13, 13, 32}, opt.dtype(at::kByte));
+  if (B == 0) return {a1, idx};
+  kern::convnet_conv1_fwd(x.data_ptr(), u8, w.data_ptr<float>(), b.data_ptr<float>(),
+                          a1.data_ptr(), idx.data_ptr<uint8_t>(), static_cast<int>(B),
+                          static_cast<float>(mean), static_cast<float>(1.0 / std),
+                          static_cast<float>(in_scale), cur_stream(x));
+  return {a1, idx};
+}
+
+void convnet_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
+                         const at::Tensor& a1, at::Tensor dw, at::Tensor db, double mean,
+                         double std, double in_scale) {
+  int64_t B;
+  bool u8;
+  check_input(x, B, u8);
+  check_cuda(da1, "conv1 grad");
+  check_dtype(da1, at::kBFloat16, "conv1 grad");
+  check_shape(da1, {B, 13, 13, 32}, "conv1 grad");
+  check_shape(idx1, {B, 13, 13, 32}, "conv1 argmax");
+  check_shape(a1, {B, 13, 13, 32}, "conv1 pooled");
+  check_cuda(dw, "conv1 dw");
+  check_cuda(db, "conv1 db");
+  check_shape(dw, {32, 1, 5, 5}, "conv1 dw");
+  check_shape(db, {32}, "conv1 db");
+  int S = 1;
+  const int64_t nf = kern::convnet_conv1_wgrad_slab_floats(static_cast<int>(B), &S);
+  at::Tensor slabs = at::empty({nf}, dw.options());
+  kern::convnet_conv1_wgrad(x.data_ptr(), u8, da1.data_ptr(), idx1.data_ptr<uint8_t>(),
+                            a1.data_ptr(), static_cast<int>(B), static_cast<float>(mean),
+                            static_cast<float>(1.0 / std), static_cast<float>(in_scale),
+                            slabs.data_ptr<float>(), S, dw.data_ptr<float>(),
+                            db.data_ptr<float>(), cur_stream(x));
+}
+
+namespace {
+struct LayerShape {
+  int64_t cin, cout, ih, ph;
+};
+LayerShape layer_shape(int64_t layer) {
+  RINGDP_CHECK(layer == 2 || layer == 3, "convnet layer must be 2 or 3");
+  return layer == 2 ? LayerShape{32, 64, 13, 10} : LayerShape{64, 128, 10, 4};
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> convnet_conv_fwd(int64_t layer, const at::Tensor& in,
+                                                    const at::Tensor& w, const at::Tensor& b) {
+  auto L = layer_shape(layer);
+  check_cuda(in, "conv input");
+  check_dtype(in, at::kBFloat16, "conv input");
+  RINGDP_CHECK(in.dim() == 4 && in.size(1) == L.ih && in.size(2) == L.ih && in.size(3) == L.cin,
+               "conv", layer, " input: expected [B, ", L.ih, ", ", L.ih, ", ", L.cin, "] got ",
+               in.sizes());
+  check_cuda(w, "conv weight");
+  check_dtype(w, at::kFloat, "conv weight");
+  check_shape(w, {L.cout, L.cin, 3, 3}, "conv weight");
+  check_shape(b, {L.cout}, "conv bias");
+  const int64_t B = in.size(0);
+  at::Tensor out = at::empty({B, L.ph, L.ph, L.cout}, in.options());
+  at::Tensor idx = at::empty({B, L.ph, L.ph, L.cout}, in.options().dtype(at::kByte));
+  if (B == 0) return {out, idx};
+  kern::convnet_conv_fwd(static_cast<int>(layer), in.data_ptr(), w.data_ptr<float>(),
+                         b.data_ptr<float>(), out.data_ptr(), idx.data_ptr<uint8_t>(),
+                         static_cast<int>(B), cur_stream(in));
+  return {out, idx};
+}
+
+at::Tensor convnet_conv_bwd(int64_t layer, const at::Tensor& in, const at::Tensor& w,
+                            const at::Tensor& dout, const at::Tensor& idx, const at::Tensor& out,
+                            bool need_din, at::Tensor dw, at::Tensor db) {
+  auto L = layer_shape(layer);
+  check_cuda(in, "conv input");
+  check_cuda(dout, "conv grad_output");
+  check_dtype(dout, at::kBFloat16, "conv grad_output");
+  const int64_t B = in.size(0);
+  check_shape(dout, {B, L.ph, L.ph, L.cout}, "conv grad_output");
+  check_shape(idx, {B, L.ph, L.ph, L.cout}, "conv argmax");
+  check_shape(out, {B, L.ph, L.ph, L.cout}, "conv pooled output");
+  check_cuda(dw, "conv dw");
+  check_cuda(db, "conv db");
+  check_shape(dw, {L.cout, L.cin, 3, 3}, "conv dw");
+  check_shape(db, {L.cout}, "conv db");
+  at::Tensor din;
+  if (need_din) din = at::empty_like(in);
+  int S = 1;
+  const int64_t nf = kern::convnet_conv_wgrad_slab_floats(static_cast<int>(layer),
+                                                          static_cast<int>(B), &S);
+  at::Tensor slabs = at::empty({nf}, dw.options());
+  kern::convnet_conv_bwd(static_cast<int>(layer), in.data_ptr(), w.data_ptr<float>(),
+                         dout.data_ptr(), idx.data_ptr<uint8_t>(), out.data_ptr(),
+                         need_din ? din.data_ptr() : nullptr, static_cast<int>(B),
+                         slabs.data_ptr<float>(), S, dw.data_ptr<float>(), db.data_ptr<float>(),
+                         cur_stream(in));
+  return din;
+}
+
+at::Tensor convnet_fc_fwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& b) {
+  check_cuda(a3, "fc input");
+  check_dtype(a3, at::kBFloat16, "fc input");
+  RINGDP_CHECK(a3.numel() % 2048 == 0, "fc input: expected [B, 4, 4, 128]");
+  check_shape(w, {10, 2048}, "fc weight");
+  check_shape(b, {10}, "fc bias");
+  const int64_t B = a3.numel() / 2048;
+  at::Tensor logits = at::empty({B, 10}, a3.options().dtype(at::kFloat));
+  if (B == 0) return logits;
+  kern::convnet_fc_fwd(a3.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
+                       logits.data_ptr<float>(), static_cast<int>(B), cur_stream(a3));
+  return logits;
+}
+
+at::Tensor convnet_fc_bwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& dlogits,
+                          at::Tensor dw, at::Tensor db) {
+  const int64_t B = a3.numel() / 2048;
+  check_cuda(dlogits, "fc grad_output");
+  at::Tensor dl = dlogits.to(at::kFloat).contiguous();
+  check_shape(dl, {B, 10}, "fc grad_output");
+  check_shape(dw, {10, 2048}, "fc dw");
+  check_shape(db, {10}, "fc db");
+  at::Tensor da3 = at::empty_like(a3);
+  int S = 1;
+  const int64_t nf = kern::convnet_fc_slab_floats(static_cast<int>(B), &S);
+  at::Tensor slabs = at::empty({nf}, dw.options());
+  kern::convnet_fc_bwd(a3.data_ptr(), w.data_ptr<float>(), dl.data_ptr<float>(), da3.data_ptr(),
+                       static_cast<int>(B), slabs.data_ptr<float>(), S, dw.data_ptr<float>(),
+                       db.data_ptr<float>(), cur_stream(a3));
+  return da3;
+}
+
+std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,
+                                                   int64_t num_classes, int64_t seed,
+                                                   at::Device device) {
+  RINGDP_CHECK(device.is_cuda(), "synth_u8_images: expected a GPU device");
+  c10::DeviceGuard g(device);
+  auto opt = at::TensorOptions().device(device);
+  at::Tensor x = at::empty({B, 1, H, W}, opt.dtype(at::kByte));
+  at::Tensor y = at::empty({B}, opt.dtype(at::kLong));
+  kern::synth_u8_images(x.data_ptr<uint8_t>(), y.data_ptr<int64_t>(), static_cast<int>(B),
+                        static_cast<int>(H * W), static_cast<int>(num_classes),
+                        static_cast<uint64_t>(seed), cur_stream(x));
+  return {x, y};
+}
+
+}  // namespace ops
+}  // namespace ringdp

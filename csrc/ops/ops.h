@@ -1,0 +1,66 @@
+// Tensor-level wrappers around ringdp's HIP kernels (shape/dtype/device checks + launch on the
+// caller's current HIP stream).  Every op fails loudly on bad input instead of falling back.
+#pragma once
+
+#include <ATen/ATen.h>
+
+#include <tuple>
+#include <vector>
+
+namespace ringdp {
+namespace ops {
+
+// dst = src converted (fp32 <-> bf16 / fp16).  GPU: ringdp cast kernel; CPU: ATen copy.
+void cast_copy(at::Tensor dst, const at::Tensor& src);
+
+struct SgdHyper {
+  double lr = 0.01;
+  double momentum = 0.0;
+  double dampening = 0.0;
+  double weight_decay = 0.0;
+  bool nesterov = false;
+  bool maximize = false;
+};
+// One fused SGD step over flat fp32 buffers (momentum_buf may be undefined when momentum == 0).
+void sgd_flat(at::Tensor param, const at::Tensor& grad, at::Tensor momentum_buf,
+              const SgdHyper& h, bool first_step, const c10::optional<at::Tensor>& lr_tensor,
+              const c10::optional<at::Tensor>& grad_scale);
+// Multi-tensor SGD: one launch for lists of (possibly non-adjacent) fp32 tensors.
+void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
+               std::vector<at::Tensor> bufs, const SgdHyper& h, bool first_step,
+               const c10::optional<at::Tensor>& lr_tensor,
+               const c10::optional<at::Tensor>& grad_scale);
+
+// Cross entropy: returns (loss, lse, workspace); workspace holds the denominator for backward.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_fwd(const at::Tensor& logits,
+                                                                 const at::Tensor& labels,
+                                                                 int64_t ignore_index,
+                                                                 double label_smoothing,
+                                                                 int64_t reduction);
+at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& labels,
+                             const at::Tensor& lse, const at::Tensor& ws,
+                             const at::Tensor& grad_out, int64_t ignore_index,
+                             double label_smoothing, int64_t reduction);
+
+// MNIST ConvNet layers (see csrc/kernels/convnet.hip).
+std::tuple<at::Tensor, at::Tensor> convnet_conv1_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                     const at::Tensor& b, double mean,
+                                                     double std, double in_scale);
+void convnet_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
+                         const at::Tensor& a1, at::Tensor dw, at::Tensor db, double mean,
+                         double std, double in_scale);
+std::tuple<at::Tensor, at::Tensor> convnet_conv_fwd(int64_t layer, const at::Tensor& in,
+                                                    const at::Tensor& w, const at::Tensor& b);
+at::Tensor convnet_conv_bwd(int64_t layer, const at::Tensor& in, const at::Tensor& w,
+                            const at::Tensor& dout, const at::Tensor& idx, const at::Tensor& out,
+                            bool need_din, at::Tensor dw, at::Tensor db);
+at::Tensor convnet_fc_fwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& b);
+at::Tensor convnet_fc_bwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& dlogits,
+                          at::Tensor dw, at::Tensor db);
+
+std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,
+                                                   int64_t num_classes, int64_t seed,
+                                                   at::Device device);
+
+}  // namespace ops
+}  // namespace ringdp

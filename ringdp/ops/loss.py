@@ -1,0 +1,33 @@
+"""Cross entropy on ringdp kernels (csrc/kernels/elementwise.hip)."""
+from __future__ import annotations
+
+import torch
+
+from .._native import C
+
+_RED = {"none": 0, "mean": 1, "sum": 2}
+
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target, ignore_index, label_smoothing, reduction):
+        logits = logits.float().contiguous()
+        target = target.long().contiguous()
+        loss, lse, ws = C.cross_entropy_fwd(logits, target, ignore_index, label_smoothing, _RED[reduction])
+        ctx.save_for_backward(logits, target, lse, ws)
+        ctx.cfg = (ignore_index, label_smoothing, _RED[reduction])
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, target, lse, ws = ctx.saved_tensors
+        d = C.cross_entropy_bwd(logits, target, lse, ws, grad_out.contiguous(), *ctx.cfg)
+        return d, None, None, None, None
+
+
+def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int = -100,
+                  label_smoothing: float = 0.0, reduction: str = "mean") -> torch.Tensor:
+    if logits.is_cuda and logits.dim() == 2 and target.dim() == 1:
+        return _CrossEntropy.apply(logits, target, ignore_index, float(label_smoothing), reduction)
+    return torch.nn.functional.cross_entropy(logits, target, ignore_index=ignore_index,
+                                             label_smoothing=label_smoothing, reduction=reduction)

@@ -1,0 +1,390 @@
+"""DistributedDataParallel on ringdp's native reducer + RCCL/host-ring process groups.
+
+API parity target: ``torch.nn.parallel.DistributedDataParallel`` as used by the reference
+(``ref/mpspawn_dist.py:68``, ``ref/launch_dist.py:61``, ``ref/example_mp.py:53``,
+``ref/example_launch.py:29``):
+
+* construction verifies parameter shapes across ranks (C1/C2), broadcasts rank 0's parameters and
+  buffers (C3, coalesced per dtype), and builds one reducer bucket for iteration 0;
+* after iteration 0 the buckets are rebuilt from the observed gradient-ready order with limits
+  ``[first_bucket_mb, bucket_cap_mb]`` and rank 0's assignment is broadcast (C5);
+* every forward with ``broadcast_buffers`` re-broadcasts rank 0's buffers (C4);
+* gradients are all-reduced bucket by bucket, in bucket order, overlapped with backward (C6);
+* ``no_sync()``, ``register_comm_hook`` (allreduce / bf16 / fp16 compression / Python hooks),
+  ``find_unused_parameters``, ``_get_ddp_logging_data()``.
+
+MI355X-first differences (documented, behaviour-preserving):
+* gradients live permanently in the flat bucket buffer (grad-as-bucket-view) and ringdp kernels
+  write into it directly; averaging happens inside the collective (ncclAvg);
+* with ``flatten_parameters=True`` (default) parameters are re-pointed into one flat buffer laid
+  out exactly like the gradient buffer, so ``ringdp.optim.SGD`` updates the whole model with one
+  kernel.  ``state_dict()`` / ``parameters()`` are unchanged for the user.
+"""
+from __future__ import annotations
+
+import sys
+import time
+from contextlib import contextmanager
+from typing import Any, Callable, Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+from .. import distributed as dist
+from .._native import C
+from . import comm_hooks as default_hooks
+
+_DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
+_BROADCAST_BUCKET_BYTES = 250 * 1024 * 1024
+_PAD_ELEMS = 16  # 64-byte alignment of every parameter inside the flat buffers
+
+
+def _device_of(module: nn.Module) -> torch.device:
+    for p in module.parameters():
+        return p.device
+    for b in module.buffers():
+        return b.device
+    return torch.device("cpu")
+
+
+class GradBucket:
+    """Bucket handed to Python communication hooks (torch.distributed.GradBucket subset)."""
+
+    def __init__(self, index: int, buffer: torch.Tensor, params: List[torch.Tensor], is_last: bool):
+        self._index, self._buffer, self._params, self._last = index, buffer, params, is_last
+
+    def index(self) -> int:
+        return self._index
+
+    def buffer(self) -> torch.Tensor:
+        return self._buffer
+
+    def parameters(self) -> List[torch.Tensor]:
+        return self._params
+
+    def gradients(self) -> List[torch.Tensor]:
+        return [p.grad for p in self._params]
+
+    def is_last(self) -> bool:
+        return self._last
+
+    def set_buffer(self, t: torch.Tensor):
+        self._buffer.copy_(t)
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, output_device=None, dim: int = 0,
+                 broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: Optional[float] = None,
+                 find_unused_parameters: bool = False, check_reduction: bool = False,
+                 gradient_as_bucket_view: bool = False, static_graph: bool = False,
+                 delay_all_reduce_named_params=None, param_to_hook_all_reduce=None,
+                 mixed_precision=None, device_mesh=None, *, first_bucket_mb: Optional[float] = None,
+                 comm_hook: Optional[str] = None, flatten_parameters: bool = True,
+                 rebuild_buckets: bool = True):
+        super().__init__()
+        if mixed_precision is not None or device_mesh is not None:
+            raise NotImplementedError("ringdp DDP: mixed_precision/device_mesh are not supported")
+        self.module = module
+        self.process_group = process_group if process_group is not None else dist._default()
+        if process_group is dist.GroupMember.NON_GROUP_MEMBER:
+            raise ValueError("DDP: this rank is not a member of the given process group")
+        self.dim = dim
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.static_graph = static_graph
+        self.gradient_as_bucket_view = True  # always (see module docstring)
+        self.require_backward_grad_sync = True
+        self.require_forward_param_sync = True
+        self._flatten = flatten_parameters
+        self._rebuild_enabled = rebuild_buckets and not find_unused_parameters
+
+        # ---- device placement (U7 :744-790)
+        self.device = _device_of(module)
+        if device_ids is not None:
+            if len(device_ids) != 1:
+                raise ValueError("device_ids can only be None or contain a single element.")
+            d = device_ids[0]
+            dev = d if isinstance(d, torch.device) else torch.device("cuda", int(d))
+            if self.device != dev:
+                raise ValueError(f"DDP: module parameters are on {self.device} but device_ids={device_ids}")
+            self.device_ids = [dev.index]
+            od = output_device if output_device is not None else dev.index
+            self.output_device = od.index if isinstance(od, torch.device) else od
+        else:
+            self.device_ids = None
+            self.output_device = None
+        self._is_gpu = self.device.type == "cuda"
+
+        # ---- parameters (deduplicated, requires_grad only)
+        seen = set()
+        self._params: List[nn.Parameter] = []
+        self._param_names: List[str] = []
+        for name, p in module.named_parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                self._params.append(p)
+                self._param_names.append(name)
+        if not self._params:
+            raise RuntimeError("DistributedDataParallel is not needed when a module doesn't have any parameter that requires a gradient.")
+        if any(p.device != self.device for p in self._params):
+            raise ValueError("DDP: all parameters must live on one device")
+        self._buffers_list = [b for b in module.buffers()]
+
+        self.bucket_bytes_cap = int((25 if bucket_cap_mb is None else bucket_cap_mb) * 1024 * 1024)
+        self.first_bucket_bytes = (int(first_bucket_mb * 1024 * 1024) if first_bucket_mb is not None
+                                   else _DEFAULT_FIRST_BUCKET_BYTES)
+
+        # ---- native communicator for this device
+        self._native_pg = self._native_for(self.device)
+
+        # ---- C1/C2: verify shapes, C3: broadcast module state from rank 0
+        self._verify_params_across_processes()
+        self._sync_module_states()
+
+        # ---- reducer (iteration 0: one bucket unless find_unused_parameters, U7 :1199-1200)
+        limits = [sys.maxsize] if not find_unused_parameters else [self.first_bucket_bytes, self.bucket_bytes_cap]
+        bucket_indices, _ = C.compute_bucket_assignment_by_size(self._params, limits)
+        self.reducer = C.Reducer(self._params, list(reversed(bucket_indices)), self._native_pg,
+                                 find_unused_parameters, _PAD_ELEMS)
+        self._comm_hook_name = "allreduce"
+        if comm_hook is not None:
+            self._set_builtin_hook(comm_hook)
+        self._python_hook = None
+        self._install_layout()
+        self._iteration = 0
+        self._stats = {"forward_ms": 0.0, "iterations": 0}
+
+    # ------------------------------------------------------------------ construction helpers
+    def _native_for(self, device: torch.device):
+        g = self.process_group
+        probe = torch.empty(0, device=device)
+        native, staged = g.native_for(probe)
+        if staged:
+            raise RuntimeError("ringdp DDP: GPU module with a host-only process group; use backend 'nccl'/'rccl'")
+        return native
+
+    def _verify_params_across_processes(self):
+        """C1 all_gather(param count) + C2 broadcast(rank 0 metadata) and compare (U7 :862)."""
+        g = self.process_group
+        if g.size() == 1:
+            return
+        dev = self.device
+        cnt = torch.tensor([len(self._params)], dtype=torch.long, device=dev)
+        counts = [torch.zeros_like(cnt) for _ in range(g.size())]
+        dist.all_gather(counts, cnt, group=g)
+        counts = [int(c.item()) for c in counts]
+        if len(set(counts)) != 1:
+            raise RuntimeError(f"DDP expects the same number of parameters on every rank, got {counts}")
+        meta = []
+        for p in self._params:
+            meta.append(p.dim())
+            meta.extend(p.shape)
+            meta.append(int(_DTYPE_CODES.get(p.dtype, 99)))
+        mine = torch.tensor(meta, dtype=torch.long, device=dev)
+        theirs = mine.clone()
+        dist.broadcast(theirs, src=g.ranks[0], group=g)
+        if not torch.equal(mine, theirs):
+            raise RuntimeError("DDP: parameter shapes/dtypes differ from rank 0's (model mismatch across ranks)")
+
+    def _broadcast_coalesced(self, tensors: List[torch.Tensor]):
+        """Flatten per dtype into <=250 MiB buffers, broadcast from the group's first rank."""
+        g = self.process_group
+        if g.size() == 1 or not tensors:
+            return
+        by_dtype: Dict[torch.dtype, List[torch.Tensor]] = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        for ts in by_dtype.values():
+            chunk: List[torch.Tensor] = []
+            size = 0
+            for t in ts + [None]:
+                if t is not None and size + t.numel() * t.element_size() <= _BROADCAST_BUCKET_BYTES:
+                    chunk.append(t)
+                    size += t.numel() * t.element_size()
+                    continue
+                if chunk:
+                    flat = torch.cat([c.detach().reshape(-1) for c in chunk])
+                    dist.broadcast(flat, src=g.ranks[0], group=g)
+                    off = 0
+                    with torch.no_grad():
+                        for c in chunk:
+                            c.copy_(flat[off:off + c.numel()].view_as(c))
+                            off += c.numel()
+                if t is not None:
+                    chunk, size = [t], t.numel() * t.element_size()
+
+    def _sync_module_states(self):
+        state = [p.data for p in self._params] + [b for b in self._buffers_list]
+        self._broadcast_coalesced(state)
+
+    def _install_layout(self):
+        """Grad slots for ringdp ops + (optionally) flat parameter storage matching the grads."""
+        slots = self.reducer.grad_slots()
+        offsets = self.reducer.param_offsets()
+        flats = self.reducer.flat_buffers()
+        flat_by_dtype = {f.dtype: f for f in flats}
+        for p, s in zip(self._params, slots):
+            p._ringdp_grad_slot = s
+        if not self._flatten:
+            return
+        self._flat_params = {}
+        with torch.no_grad():
+            for dt, fg in flat_by_dtype.items():
+                fp = torch.zeros_like(fg)
+                members = [(p, off) for p, off in zip(self._params, offsets) if p.dtype == dt]
+                for p, off in members:
+                    view = fp[off:off + p.numel()].view_as(p)
+                    view.copy_(p.data)
+                    p.data = view
+                for p, off in members:
+                    p._ringdp_flat = (fp, fg, off, len(members))
+                self._flat_params[dt] = fp
+
+    def _set_builtin_hook(self, name: str):
+        name = name.lower()
+        table = {"allreduce": C.CommHook.ALLREDUCE, "bf16": C.CommHook.BF16_COMPRESS,
+                 "bf16_compress": C.CommHook.BF16_COMPRESS, "fp16": C.CommHook.FP16_COMPRESS,
+                 "fp16_compress": C.CommHook.FP16_COMPRESS, "none": C.CommHook.NONE}
+        if name not in table:
+            raise ValueError(f"unknown builtin comm hook {name!r}")
+        self.reducer.set_comm_hook(table[name])
+        self._comm_hook_name = name
+
+    # ------------------------------------------------------------------ bucket rebuild (C5)
+    def _maybe_rebuild_buckets(self):
+        if not self._rebuild_enabled or self.reducer.rebuilt() or self.reducer.iteration() < 1:
+            return
+        order = list(self.reducer.ready_order())
+        g = self.process_group
+        if len(order) == len(self._params):
+            params_in_order = [self._params[i] for i in order]
+            buckets, _ = C.compute_bucket_assignment_by_size(
+                params_in_order, [self.first_bucket_bytes, self.bucket_bytes_cap], [], order)
+        else:
+            buckets = [list(b) for b in self.reducer.bucket_indices()]
+        # Rank 0's assignment wins (every rank must issue identical collectives).
+        if g.size() > 1:
+            sizes = [len(b) for b in buckets]
+            payload = [len(buckets)] + sizes + [i for b in buckets for i in b]
+            n = torch.tensor([len(payload)], dtype=torch.long, device=self.device)
+            dist.broadcast(n, src=g.ranks[0], group=g)
+            buf = torch.zeros(int(n.item()), dtype=torch.long, device=self.device)
+            if g.rank() == 0:
+                buf.copy_(torch.tensor(payload, dtype=torch.long))
+            dist.broadcast(buf, src=g.ranks[0], group=g)
+            vals = buf.tolist()
+            nb = vals[0]
+            sizes = vals[1:1 + nb]
+            flat = vals[1 + nb:]
+            buckets, off = [], 0
+            for s in sizes:
+                buckets.append(flat[off:off + s])
+                off += s
+        self.reducer.rebuild_buckets(buckets)
+        self._install_layout()
+
+    # ------------------------------------------------------------------ forward
+    def _sync_buffers(self):
+        """C4: broadcast rank 0's buffers every forward (broadcast_buffers=True, U7 :2155-2221)."""
+        if self.process_group.size() > 1 and self._buffers_list:
+            self._broadcast_coalesced(self._buffers_list)
+
+    def _to_device(self, obj):
+        if torch.is_tensor(obj):
+            return obj.to(self.device, non_blocking=True) if obj.device != self.device else obj
+        if isinstance(obj, (list, tuple)):
+            return type(obj)(self._to_device(o) for o in obj)
+        if isinstance(obj, dict):
+            return {k: self._to_device(v) for k, v in obj.items()}
+        return obj
+
+    def forward(self, *inputs, **kwargs):
+        with torch.autograd.profiler.record_function("DistributedDataParallel.forward"):
+            grad = torch.is_grad_enabled() and self.require_backward_grad_sync
+            if grad:
+                self._maybe_rebuild_buckets()
+                self.reducer.prepare_for_forward()
+            if self.broadcast_buffers and self.require_forward_param_sync:
+                self._sync_buffers()
+            if self.device_ids is not None:
+                inputs = self._to_device(inputs)
+                kwargs = self._to_device(kwargs)
+            out = self.module(*inputs, **kwargs)
+            if torch.is_grad_enabled():
+                self.reducer.set_require_sync(self.require_backward_grad_sync)
+                self.reducer.prepare_for_backward()
+            self._iteration += 1
+            return out
+
+    # ------------------------------------------------------------------ public API
+    @contextmanager
+    def no_sync(self):
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def register_comm_hook(self, state: Any, hook: Callable):
+        """Builtin hooks (allreduce / bf16_compress / fp16_compress from
+        ``ringdp.parallel.comm_hooks``) run natively; any other callable is invoked as
+        ``hook(state, GradBucket) -> Work | None`` from the reducer."""
+        builtin = {default_hooks.allreduce_hook: "allreduce",
+                   default_hooks.bf16_compress_hook: "bf16_compress",
+                   default_hooks.fp16_compress_hook: "fp16_compress"}
+        if hook in builtin:
+            self._set_builtin_hook(builtin[hook])
+            return
+        nb = len(self.reducer.bucket_indices())
+        ddp = self
+
+        def call(index, flat):
+            params = [ddp._params[i] for i in ddp.reducer.bucket_indices()[index]]
+            res = hook(state, GradBucket(index, flat, params, index == nb - 1))
+            return res
+
+        self.reducer.set_python_hook(call)
+        self._python_hook = hook
+        self._comm_hook_name = getattr(hook, "__name__", "python_hook")
+
+    def _get_ddp_logging_data(self) -> Dict[str, Any]:
+        stats = self.reducer.stats()
+        return {
+            "world_size": self.process_group.size(),
+            "rank": self.process_group.rank(),
+            "backend_name": self._native_pg.backend_name(),
+            "module_name": type(self.module).__name__,
+            "device_ids": self.device_ids,
+            "output_device": self.output_device,
+            "broadcast_buffers": self.broadcast_buffers,
+            "bucket_cap_bytes": self.bucket_bytes_cap,
+            "first_bucket_bytes": self.first_bucket_bytes,
+            "find_unused_parameters": self.find_unused_parameters,
+            "gradient_as_bucket_view": True,
+            "comm_hook": self._comm_hook_name,
+            "num_parameter_tensors": len(self._params),
+            "total_parameter_size_bytes": sum(p.numel() * p.element_size() for p in self._params),
+            "bucket_sizes": [s.bytes for s in stats],
+            "rebuilt_bucket_sizes": [s.bytes for s in stats] if self.reducer.rebuilt() else [],
+            "rebuilt_per_bucket_param_indices": self.reducer.bucket_indices() if self.reducer.rebuilt() else [],
+            "bucket_ready_us": [s.last_ready_us for s in stats],
+            "bucket_launch_us": [s.last_launch_us for s in stats],
+            "bucket_comm_us": [s.last_comm_us for s in stats],
+            "avg_bucket_comm_us": [s.total_comm_us / s.comm_samples if s.comm_samples else None for s in stats],
+            "iteration": self.reducer.iteration(),
+        }
+
+    def bucket_param_names(self) -> List[List[str]]:
+        return [[self._param_names[i] for i in b] for b in self.reducer.bucket_indices()]
+
+    def state_dict(self, *args, **kwargs):
+        return super().state_dict(*args, **kwargs)
+
+    def train(self, mode: bool = True):
+        super().train(mode)
+        return self
+
+
+_DTYPE_CODES = {torch.float32: 0, torch.float64: 1, torch.float16: 2, torch.bfloat16: 3,
+                torch.int64: 4, torch.int32: 5, torch.uint8: 6, torch.int8: 7, torch.bool: 8}

@@ -1,0 +1,54 @@
+"""hipGraph capture of a whole training step (MI355X-first replacement for a tracing compiler).
+
+A ringdp training step at the reference's shapes is launch-bound: forward,
+backward, the RCCL bucket all-reduces on the side stream and the fused optimizer are a few dozen
+small launches.  ``StepGraph`` warms the step up on a side stream, drains every RCCL watchdog
+queue, then captures one step (including the cross-stream event fork/join of the reducer and
+the RCCL kernels) into a hipGraph that ``replay()`` launches with a single call.
+
+Requirements: inputs the step reads must live in static tensors (copy each new batch into
+them), DDP bucket rebuild must have happened (warmup >= 2 steps), and the optimizer must use
+its graph-safe path (ringdp.optim.SGD flat path: no allocations, lr may be a device tensor).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+from .. import distributed as dist
+
+
+def drain_comms():
+    """Block until every in-flight RCCL op of every group has completed."""
+    w = dist._world
+    for g in list(w.groups.values()):
+        for pg in list(g._rccl.values()):
+            pg.drain()
+
+
+class StepGraph:
+    def __init__(self, step_fn: Callable[[], Optional[torch.Tensor]], warmup: int = 3):
+        self.step_fn = step_fn
+        self.warmup = warmup
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.output = None
+
+    def capture(self):
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):
+                self.step_fn()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        drain_comms()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            self.output = self.step_fn()
+        torch.cuda.synchronize()
+        return self
+
+    def replay(self):
+        self.graph.replay()
+        return self.output
