@@ -576,7 +576,8 @@ __global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restri
   }
 }
 
-// Reduce slabs over slices and scatter to the PyTorch weight layout [co][ci][kh][kw] + bias.
+// Reduce slabs over slices (4 waves x quarter of the slices, fixed combine order) and scatter to
+// the PyTorch weight layout [co][ci][kh][kw] + bias.
 template <int L>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float* __restrict__ slabs,
                                                                      int nslices,
@@ -585,16 +586,29 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float
   using G = Geo<L>;
   using W = WgradGeo<L>;
   constexpr int SL = W::NOUT + G::COUT;
-  for (int i = blockIdx.x * kThreads + threadIdx.x; i < SL; i += gridDim.x * kThreads) {
-    float s = 0.f;
-    for (int k = 0; k < nslices; ++k) s += slabs[(int64_t)k * SL + i];
-    if (i < W::NOUT) {
-      const int n = i / G::COUT, co = i % G::COUT;
-      const int tap = n / G::CIN, ci = n % G::CIN;
-      dw[(co * G::CIN + ci) * 9 + tap] = s;
-    } else {
-      db[i - W::NOUT] = s;
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f;
+  if (i < SL) {
+    const float* p = slabs + i;
+    int k = wave;
+    for (; k + 4 < nslices; k += 8) {
+      a0 += p[(int64_t)k * SL];
+      a1 += p[(int64_t)(k + 4) * SL];
     }
+    for (; k < nslices; k += 4) a0 += p[(int64_t)k * SL];
+  }
+  part[wave][lane] = a0 + a1;
+  __syncthreads();
+  if (wave != 0 || i >= SL) return;
+  const float s = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (i < W::NOUT) {
+    const int n = i / G::COUT, co = i % G::COUT;
+    const int tap = n / G::CIN, ci = n % G::CIN;
+    dw[(co * G::CIN + ci) * 9 + tap] = s;
+  } else {
+    db[i - W::NOUT] = s;
   }
 }
 
@@ -804,25 +818,40 @@ inline int wgrad_slices(int B, int images_per_slice_min, int cap) {
 }  // namespace
 
 namespace {
+// Deterministic split-K reduction, parallel over slices: a workgroup owns 64 consecutive outputs;
+// its 4 waves each sum a quarter of the slices (lane = output, fully coalesced 256-B rows), 4-way
+// unrolled for memory-level parallelism; the 4 partials are combined in a fixed order in LDS.
+// out[i] = sum_s slabs[s * stride + off + i],  i < n.
 __global__ __launch_bounds__(kThreads) void strided_reduce_kernel(const float* __restrict__ slabs,
                                                                   int S, int64_t stride,
                                                                   int64_t off, int64_t n,
                                                                   float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * kThreads) {
-    float acc = 0.f;
-    for (int k = 0; k < S; ++k) acc += slabs[(int64_t)k * stride + off + i];
-    out[i] = acc;
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < n) {
+    const float* p = slabs + off + i;
+    int s = wave;
+    for (; s + 12 < S; s += 16) {
+      a0 += p[(int64_t)s * stride];
+      a1 += p[(int64_t)(s + 4) * stride];
+      a2 += p[(int64_t)(s + 8) * stride];
+      a3 += p[(int64_t)(s + 12) * stride];
+    }
+    for (; s < S; s += 4) a0 += p[(int64_t)s * stride];
   }
+  part[wave][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wave == 0 && i < n) out[i] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 }
 }  // namespace
 
 void strided_reduce(const float* slabs, int S, int64_t stride, int64_t off, int64_t n, float* out,
                     hipStream_t s) {
-  const int grid = clampi((int)cdiv((int)n, kThreads), 1, 1024);
+  const int grid = (int)((n + 63) / 64);
   strided_reduce_kernel<<<grid, kThreads, 0, s>>>(slabs, S, stride, off, n, out);
 }
-
 
 // ================================================================== launchers
 void convnet_conv1_fwd(const void* x, bool x_is_u8, const float* w, const float* b, void* a1,
@@ -838,7 +867,7 @@ void convnet_conv1_fwd(const void* x, bool x_is_u8, const float* w, const float*
 }
 
 int64_t convnet_conv1_wgrad_slab_floats(int B, int* nslices) {
-  const int S = wgrad_slices(B, 2, 4 * num_cus());
+  const int S = wgrad_slices(B, 4, 2 * num_cus());
   if (nslices) *nslices = S;
   return (int64_t)S * C1_SL;
 }
@@ -920,7 +949,7 @@ void convnet_conv_bwd(int layer, const void* in, const float* w, const void* dou
     conv_bwd_kernel<2, NS><<<n_dgrad + n_w, kThreads, 0, s>>>(inb, w, doutb, idx, outb, dinb, B,
                                                              slabs, nslices, n_dgrad);
     constexpr int SL = WgradGeo<2>::NOUT + Geo<2>::COUT;
-    conv_wgrad_reduce_kernel<2><<<cdiv(SL, kThreads), kThreads, 0, s>>>(slabs, nslices, dw, db);
+    conv_wgrad_reduce_kernel<2><<<cdiv(SL, 64), kThreads, 0, s>>>(slabs, nslices, dw, db);
   } else {
     constexpr int NS = bwd_nsplit<3>();
     const int n_dgrad = din ? clampi(B, 1, cdiv(4 * num_cus(), NS)) * NS : 0;
@@ -928,7 +957,7 @@ void convnet_conv_bwd(int layer, const void* in, const float* w, const void* dou
     conv_bwd_kernel<3, NS><<<n_dgrad + n_w, kThreads, 0, s>>>(inb, w, doutb, idx, outb, dinb, B,
                                                              slabs, nslices, n_dgrad);
     constexpr int SL = WgradGeo<3>::NOUT + Geo<3>::COUT;
-    conv_wgrad_reduce_kernel<3><<<cdiv(SL, kThreads), kThreads, 0, s>>>(slabs, nslices, dw, db);
+    conv_wgrad_reduce_kernel<3><<<cdiv(SL, 64), kThreads, 0, s>>>(slabs, nslices, dw, db);
   }
 }
 
@@ -939,7 +968,7 @@ void convnet_fc_fwd(const void* a3, const float* w, const float* b, float* logit
 }
 
 int64_t convnet_fc_slab_floats(int B, int* nslices) {
-  const int S = wgrad_slices(B, 4, num_cus());
+  const int S = wgrad_slices(B, 8, 128);
   if (nslices) *nslices = S;
   return (int64_t)S * (FC_N * FC_K + FC_N);
 }

@@ -114,7 +114,7 @@ void cast_copy(at::Tensor dst, const at::Tensor& src) {
 }
 
 // ------------------------------------------------------------------ SGD
-void sgd_flat(at::Tensor param, const at::Tensor& grad, at::Tensor buf, const SgdHyper& h,
+void sgd_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& buf_opt, const SgdHyper& h,
               bool first_step, const c10::optional<at::Tensor>& lr_t,
               const c10::optional<at::Tensor>& scale_t) {
   check_cuda(param, "sgd param");
@@ -123,6 +123,7 @@ void sgd_flat(at::Tensor param, const at::Tensor& grad, at::Tensor buf, const Sg
   check_dtype(grad, at::kFloat, "sgd grad");
   RINGDP_CHECK(param.numel() == grad.numel(), "sgd_flat: param/grad numel mismatch");
   float* m = nullptr;
+  at::Tensor buf = buf_opt.has_value() ? *buf_opt : at::Tensor();
   if (h.momentum != 0.0) {
     check_cuda(buf, "sgd momentum buffer");
     RINGDP_CHECK(buf.numel() == param.numel(), "sgd_flat: momentum buffer numel mismatch");

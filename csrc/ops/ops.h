@@ -22,7 +22,7 @@ struct SgdHyper {
   bool maximize = false;
 };
 // One fused SGD step over flat fp32 buffers (momentum_buf may be undefined when momentum == 0).
-void sgd_flat(at::Tensor param, const at::Tensor& grad, at::Tensor momentum_buf,
+void sgd_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& momentum_buf,
               const SgdHyper& h, bool first_step, const c10::optional<at::Tensor>& lr_tensor,
               const c10::optional<at::Tensor>& grad_scale);
 // Multi-tensor SGD: one launch for lists of (possibly non-adjacent) fp32 tensors.

@@ -52,8 +52,10 @@ std::pair<std::vector<std::vector<int64_t>>, std::vector<int64_t>> compute_bucke
       if (li + 1 < limits.size()) ++li;
     }
   }
-  for (auto& key : key_order) {
-    auto& b = buckets[key];
+  // Remainder flush: most recently first-seen key first (the iteration order c10d's
+  // unordered_map yields with libstdc++, so mixed-dtype layouts match upstream too).
+  for (auto it = key_order.rbegin(); it != key_order.rend(); ++it) {
+    auto& b = buckets[*it];
     if (!b.indices.empty()) result.push_back({std::move(b.indices), b.limit});
   }
   if (tensor_indices.empty()) {

@@ -31,9 +31,9 @@ struct Writer {
 };
 
 struct Reader {
-  const std::string& buf;
+  std::string buf;  // owned: callers often construct a Reader from a temporary reply
   size_t pos = 0;
-  explicit Reader(const std::string& b) : buf(b) {}
+  explicit Reader(std::string b) : buf(std::move(b)) {}
   void need(size_t n) {
     RINGDP_CHECK(pos + n <= buf.size(), "wire: truncated message");
   }

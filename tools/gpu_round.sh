@@ -18,12 +18,18 @@ step() {  # name timeout cmd...
 : > $OUT/summary.txt
 for s in ${STEPS:-tests smoke bench}; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider -k "not hipgraph" ;;
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
     bench) step bench_b100_eager 300 python bench.py --batch-per-rank 100 --steps 100 --warmup 10 --no-graph
            step bench_b100_graph 300 python bench.py --batch-per-rank 100 --steps 200 --warmup 10
            step bench_b4096_graph 300 python bench.py --batch-per-rank 4096 --steps 100 --warmup 10
            step bench_default 300 python bench.py ;;
+    eager) step bench_b100_eager 300 python bench.py --batch-per-rank 100 --steps 100 --warmup 10 --no-graph
+           step bench_b1024_eager 300 python bench.py --batch-per-rank 1024 --steps 100 --warmup 10 --no-graph
+           step bench_b4096_eager 300 python bench.py --batch-per-rank 4096 --steps 50 --warmup 10 --no-graph
+           step bench_b16384_eager 300 python bench.py --batch-per-rank 16384 --steps 20 --warmup 5 --no-graph ;;
+    graphdiag) for lv in fwd loss bwd full; do step gdiag_$lv 300 env PYTHONPATH=. python tools/graph_diag.py $lv; done
+           step gdiag_full_ddp 300 env PYTHONPATH=. python tools/graph_diag.py full ddp ;;
     prof)  step prof_b100 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_b100 -o run --output-format csv -- python bench.py --batch-per-rank 100 --steps 50 --warmup 5 --no-graph
            step prof_b4096 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_b4096 -o run --output-format csv -- python bench.py --batch-per-rank 4096 --steps 50 --warmup 5 --no-graph ;;
   esac
