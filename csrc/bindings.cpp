@@ -360,6 +360,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_multi", &ops::sgd_multi, py::arg("params"), py::arg("grads"), py::arg("bufs"),
         py::arg("hyper"), py::arg("first_step"), py::arg("lr_tensor") = py::none(),
         py::arg("grad_scale") = py::none());
+  m.def("sgd_multi_build", &ops::sgd_multi_build);
+  m.def("sgd_multi_run", &ops::sgd_multi_run, py::arg("table"), py::arg("nchunks"),
+        py::arg("table_bytes"), py::arg("hyper"), py::arg("first_step"),
+        py::arg("lr_tensor") = py::none(), py::arg("grad_scale") = py::none());
   m.def("cross_entropy_fwd", &ops::cross_entropy_fwd);
   m.def("cross_entropy_bwd", &ops::cross_entropy_bwd);
   m.def("convnet_conv1_fwd", &ops::convnet_conv1_fwd);

@@ -135,14 +135,16 @@ void sgd_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::
                  make_args(h, first_step, lr_t, scale_t), cur_stream(param));
 }
 
-void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
-               std::vector<at::Tensor> bufs, const SgdHyper& h, bool first_step,
-               const c10::optional<at::Tensor>& lr_t, const c10::optional<at::Tensor>& scale_t) {
-  RINGDP_CHECK(params.size() == grads.size(), "sgd_multi: params/grads length mismatch");
-  if (params.empty()) return;
-  const bool mom = h.momentum != 0.0;
+namespace {
+constexpr int64_t kSgdChunk = 65536;
+}
+
+std::tuple<at::Tensor, int64_t, int64_t> sgd_multi_build(std::vector<at::Tensor> params,
+                                                         std::vector<at::Tensor> grads,
+                                                         std::vector<at::Tensor> bufs,
+                                                         bool mom) {
+  RINGDP_CHECK(params.size() == grads.size() && !params.empty(), "sgd_multi: bad tensor lists");
   if (mom) RINGDP_CHECK(bufs.size() == params.size(), "sgd_multi: need one buffer per param");
-  constexpr int64_t kChunk = 65536;
   std::vector<kern::SgdTensor> table(params.size());
   std::vector<int64_t> chunks;
   for (size_t i = 0; i < params.size(); ++i) {
@@ -151,23 +153,39 @@ void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
     check_dtype(params[i], at::kFloat, "sgd param");
     check_dtype(grads[i], at::kFloat, "sgd grad");
     RINGDP_CHECK(params[i].numel() == grads[i].numel(), "sgd_multi: numel mismatch at ", i);
+    if (mom) check_cuda(bufs[i], "sgd momentum buffer");
     table[i] = {params[i].data_ptr<float>(), grads[i].data_ptr<float>(),
                 mom ? bufs[i].data_ptr<float>() : nullptr, params[i].numel()};
-    for (int64_t s = 0; s < params[i].numel(); s += kChunk) {
+    for (int64_t s = 0; s < params[i].numel(); s += kSgdChunk) {
       chunks.push_back(static_cast<int64_t>(i));
       chunks.push_back(s);
     }
   }
   const int64_t tbytes = static_cast<int64_t>(table.size() * sizeof(kern::SgdTensor));
   const int64_t cbytes = static_cast<int64_t>(chunks.size() * sizeof(int64_t));
-  at::Tensor host = at::empty({tbytes + cbytes}, at::TensorOptions().dtype(at::kByte).pinned_memory(true));
+  at::Tensor host = at::empty({tbytes + cbytes}, at::TensorOptions().dtype(at::kByte));
   std::memcpy(host.data_ptr(), table.data(), tbytes);
   std::memcpy(static_cast<char*>(host.data_ptr()) + tbytes, chunks.data(), cbytes);
-  at::Tensor dev = host.to(params[0].device(), /*non_blocking=*/true);
+  at::Tensor dev = host.to(params[0].device());  // synchronous: safe to cache and reuse
+  return {dev, static_cast<int64_t>(chunks.size() / 2), tbytes};
+}
+
+void sgd_multi_run(const at::Tensor& dev, int64_t nchunks, int64_t tbytes, const SgdHyper& h,
+                   bool first_step, const c10::optional<at::Tensor>& lr_t,
+                   const c10::optional<at::Tensor>& scale_t) {
+  check_cuda(dev, "sgd table");
   auto* dtable = reinterpret_cast<const kern::SgdTensor*>(dev.data_ptr());
   auto* dchunks = reinterpret_cast<const int64_t*>(static_cast<char*>(dev.data_ptr()) + tbytes);
-  kern::sgd_multi(dtable, dchunks, static_cast<int64_t>(chunks.size() / 2), kChunk,
-                  make_args(h, first_step, lr_t, scale_t), cur_stream(params[0]));
+  kern::sgd_multi(dtable, dchunks, nchunks, kSgdChunk, make_args(h, first_step, lr_t, scale_t),
+                  cur_stream(dev));
+}
+
+void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
+               std::vector<at::Tensor> bufs, const SgdHyper& h, bool first_step,
+               const c10::optional<at::Tensor>& lr_t, const c10::optional<at::Tensor>& scale_t) {
+  if (params.empty()) return;
+  auto t = sgd_multi_build(params, grads, bufs, h.momentum != 0.0);
+  sgd_multi_run(std::get<0>(t), std::get<1>(t), std::get<2>(t), h, first_step, lr_t, scale_t);
 }
 
 // ------------------------------------------------------------------ cross entropy

@@ -31,6 +31,15 @@ void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
                const c10::optional<at::Tensor>& lr_tensor,
                const c10::optional<at::Tensor>& grad_scale);
 
+// Cached multi-tensor table (graph-capture safe: build once outside capture, run many times).
+std::tuple<at::Tensor, int64_t, int64_t> sgd_multi_build(std::vector<at::Tensor> params,
+                                                         std::vector<at::Tensor> grads,
+                                                         std::vector<at::Tensor> bufs,
+                                                         bool with_momentum);
+void sgd_multi_run(const at::Tensor& table, int64_t nchunks, int64_t table_bytes,
+                   const SgdHyper& h, bool first_step, const c10::optional<at::Tensor>& lr_tensor,
+                   const c10::optional<at::Tensor>& grad_scale);
+
 // Cross entropy: returns (loss, lse, workspace); workspace holds the denominator for backward.
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_fwd(const at::Tensor& logits,
                                                                  const at::Tensor& labels,

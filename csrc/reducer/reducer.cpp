@@ -163,28 +163,53 @@ void Reducer::build(const std::vector<std::vector<int64_t>>& bucket_indices) {
   }
 }
 
+namespace {
+
+// Calls the reducer after the parameter's gradient has been accumulated; chains any hook that was
+// installed before (e.g. a user's register_post_accumulate_grad_hook).
+class ReducerAccHook : public torch::autograd::PostAccumulateGradHook {
+ public:
+  ReducerAccHook(Reducer* r, int64_t index,
+                 std::unique_ptr<torch::autograd::PostAccumulateGradHook> prev)
+      : reducer_(r), index_(index), prev_(std::move(prev)) {}
+  void operator()(const torch::autograd::Variable& tensor) override {
+    if (prev_) (*prev_)(tensor);
+    reducer_->autograd_hook(index_);
+  }
+  std::unique_ptr<torch::autograd::PostAccumulateGradHook> take_prev() { return std::move(prev_); }
+  const Reducer* owner() const { return reducer_; }
+
+ private:
+  Reducer* reducer_;
+  int64_t index_;
+  std::unique_ptr<torch::autograd::PostAccumulateGradHook> prev_;
+};
+
+}  // namespace
+
 void Reducer::install_hooks() {
-  grad_accumulators_.resize(params_.size());
-  hook_keys_.resize(params_.size());
+  hooked_.assign(params_.size(), false);
   for (size_t i = 0; i < params_.size(); ++i) {
-    auto acc = torch::autograd::impl::grad_accumulator(params_[i]);
-    RINGDP_CHECK(acc, "Reducer: parameter ", i, " has no grad accumulator (not a leaf?)");
-    const int64_t index = static_cast<int64_t>(i);
-    hook_keys_[i] = acc->add_post_hook(std::make_unique<torch::autograd::utils::LambdaPostHook>(
-        [this, index](const torch::autograd::variable_list& outputs,
-                      const torch::autograd::variable_list& /*inputs*/) {
-          this->autograd_hook(index);
-          return outputs;
-        }));
-    grad_accumulators_[i] = std::move(acc);
+    RINGDP_CHECK(params_[i].is_leaf(), "Reducer: parameter ", i, " is not a leaf tensor");
+    auto& slot = torch::autograd::impl::post_acc_grad_hooks(params_[i]);
+    std::unique_ptr<torch::autograd::PostAccumulateGradHook> prev = std::move(slot);
+    torch::autograd::impl::set_post_acc_grad_hooks(
+        params_[i], std::make_unique<ReducerAccHook>(this, static_cast<int64_t>(i), std::move(prev)));
+    hooked_[i] = true;
   }
 }
 
 void Reducer::remove_hooks() {
-  for (size_t i = 0; i < grad_accumulators_.size(); ++i) {
-    if (grad_accumulators_[i]) grad_accumulators_[i]->del_post_hook(hook_keys_[i]);
+  for (size_t i = 0; i < hooked_.size(); ++i) {
+    if (!hooked_[i]) continue;
+    auto& slot = torch::autograd::impl::post_acc_grad_hooks(params_[i]);
+    auto* mine = dynamic_cast<ReducerAccHook*>(slot.get());
+    if (mine && mine->owner() == this) {
+      auto prev = mine->take_prev();
+      slot = std::move(prev);
+    }
+    hooked_[i] = false;
   }
-  grad_accumulators_.clear();
 }
 
 std::vector<at::Tensor> Reducer::flat_buffers() const {

@@ -114,8 +114,10 @@ class Reducer {
   std::vector<int64_t> offsets_;       // per param offset in its dtype's flat buffer
   std::map<int, at::Tensor> flat_by_dtype_;
 
-  std::vector<std::shared_ptr<torch::autograd::Node>> grad_accumulators_;
-  std::vector<uintptr_t> hook_keys_;
+  // Tensor-level post-accumulate-grad hooks (one per parameter).  Hooks are attached to the
+  // parameter, not to an AccumulateGrad node, so the reducer never pins a node created on another
+  // stream (which would break hipGraph capture of backward).
+  std::vector<bool> hooked_;
 
   std::mutex mu_;
   CommHook hook_ = CommHook::ALLREDUCE;

@@ -41,6 +41,7 @@ class SGD(Optimizer):
                         nesterov=nesterov, maximize=maximize)
         super().__init__(params, defaults)
         self._flat_cache = {}
+        self._multi_cache = {}
 
     # ------------------------------------------------------------------ helpers
     @staticmethod
@@ -127,8 +128,20 @@ class SGD(Optimizer):
                 if st.get("momentum_buffer") is None:
                     st["momentum_buffer"] = torch.empty_like(p, memory_format=torch.contiguous_format)
                 bufs.append(st["momentum_buffer"])
-        grads = [p.grad if p.grad.is_contiguous() else p.grad.contiguous() for p in params]
-        C.sgd_multi(params, grads, bufs, h, first, lr_t, None)
+        if not all(p.grad.is_contiguous() and p.is_contiguous() for p in params):
+            grads = [p.grad.contiguous() for p in params]
+            C.sgd_multi(params, grads, bufs, h, first, lr_t, None)
+            return
+        # Pointer table cached per (param, grad, buffer) addresses: no host->device copy per step,
+        # so the step is hipGraph-capturable once the table exists.
+        key = tuple(p.data_ptr() for p in params) + tuple(p.grad.data_ptr() for p in params) + \
+            tuple(b.data_ptr() for b in bufs)
+        tab = self._multi_cache.get(id(group))
+        if tab is None or tab[0] != key:
+            dev, nchunks, tbytes = C.sgd_multi_build(params, [p.grad for p in params], bufs, mom_on)
+            tab = (key, dev, nchunks, tbytes)
+            self._multi_cache[id(group)] = tab
+        C.sgd_multi_run(tab[1], tab[2], tab[3], h, first, lr_t, None)
 
     def _step_cpu(self, group, params):
         lr = float(group["lr"])

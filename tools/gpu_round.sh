@@ -18,9 +18,10 @@ step() {  # name timeout cmd...
 : > $OUT/summary.txt
 for s in ${STEPS:-tests smoke bench}; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider -k "not hipgraph" ;;
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
     bench) step bench_b100_eager 300 python bench.py --batch-per-rank 100 --steps 100 --warmup 10 --no-graph
+           step bench_b1024_graph 300 python bench.py --batch-per-rank 1024 --steps 100 --warmup 10
            step bench_b100_graph 300 python bench.py --batch-per-rank 100 --steps 200 --warmup 10
            step bench_b4096_graph 300 python bench.py --batch-per-rank 4096 --steps 100 --warmup 10
            step bench_default 300 python bench.py ;;
