@@ -366,11 +366,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lr_tensor") = py::none(), py::arg("grad_scale") = py::none());
   m.def("cross_entropy_fwd", &ops::cross_entropy_fwd);
   m.def("cross_entropy_bwd", &ops::cross_entropy_bwd);
-  m.def("convnet_conv1_fwd", &ops::convnet_conv1_fwd);
-  m.def("convnet_conv1_wgrad", &ops::convnet_conv1_wgrad);
-  m.def("convnet_conv_fwd", &ops::convnet_conv_fwd);
-  m.def("convnet_conv_bwd", &ops::convnet_conv_bwd);
-  m.def("convnet_fc_fwd", &ops::convnet_fc_fwd);
-  m.def("convnet_fc_bwd", &ops::convnet_fc_bwd);
+  m.def("cn_pack_weights", &ops::cn_pack_weights);
+  m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
+  m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);
+  m.def("cn_conv3_fc_fwd", &ops::cn_conv3_fc_fwd);
+  m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd);
+  m.def("cn_conv2_bwd", &ops::cn_conv2_bwd);
+  m.def("cn_conv1_wgrad", &ops::cn_conv1_wgrad);
   m.def("synth_u8_images", &ops::synth_u8_images);
 }

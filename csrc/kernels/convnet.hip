@@ -5,21 +5,28 @@
 //   conv2 32->64 k3 (13->11)  -> ReLU -> MaxPool(2,1) (10)   [overlapping windows]
 //   conv3 64->128 k3 (10->8)  -> ReLU -> MaxPool(2,2) (4)  -> view(-1, 2048) -> fc1 2048->10
 //
-// Design (MI355X-first, not a translation of cuDNN calls):
-//   * activations stay NHWC bf16 and only the POOLED outputs are stored (+ a 1-byte argmax per
-//     pooled element); ReLU/MaxPool are fused into the conv epilogue (K02/K03/K05/K06/K08/K09);
-//   * conv2/conv3 forward = implicit GEMM on v_mfma_f32_16x16x32_bf16, whole input image staged
-//     in LDS, weights converted fp32->bf16 while staged (no shadow weight copies), workgroups
-//     loop over images so weights are staged once per workgroup;
-//   * backward never materialises d(conv) in HBM: each kernel re-creates it while staging from
-//     d(pooled) + argmax + pooled>0 (unpool+ReLU-mask, deterministic gather form even for the
-//     overlapping k2/s1 pool, K17);
-//   * dgrad = "full" correlation with flipped weights from a zero-ringed LDS image (MFMA);
-//   * wgrad = TN GEMM over (image, position) with operands read by ds_read_b64_tr_b16 straight
-//     from the NHWC LDS images (the transposed read also does the im2col gather), split over
-//     images into fp32 slabs reduced in a fixed order (deterministic);
-//   * conv1 (C_in = 1) forward is fp32 VALU direct convolution; its wgrad is an MFMA GEMM over a
-//     row-padded unpooled grid with per-kw shifted copies of the input to keep reads aligned.
+// Kernel blocks (one autograd Function each, see ringdp/ops/convnet.py):
+//   F1  conv1 + ReLU + pool1                       -> a1 [B,13,13,32] bf16 + argmax
+//   F2  conv2 + ReLU                               -> r2 [B,11,11,64] bf16
+//   F3  pool2 + conv3 + ReLU + pool3 + fc1         -> logits [B,10] fp32 (+ a3, argmax)
+// The overlapping k2/s1 pool lives at the START of F3: its argmax is recomputed from r2 when
+// needed, so no argmax tensor is stored for it and conv2's backward sees a plain ReLU mask.
+//
+// MI355X-first design:
+//   * weight-stationary: weights are packed once per forward (cn_pack_weights) into bf16 MFMA
+//     B-fragment order; every workgroup keeps its fragments in VGPRs for all the images it
+//     processes; images stream through LDS with one-image-ahead register prefetch;
+//   * window-ordered M: the GEMM rows of a conv followed by a 2x2/s2 pool are ordered
+//     (pool window, position-in-window), so each lane's 4 accumulator registers of a
+//     v_mfma_f32_16x16x32_bf16 tile are exactly one pool window -> bias + max + argmax + ReLU are
+//     done in registers (conv1, conv3), no LDS round trip;
+//   * fc1 is fused into the conv3 epilogue (partial logits reduced across lanes and waves);
+//   * backward: dgrad is a weight-stationary full correlation over a zero-ringed LDS image; wgrad is
+//     a TN GEMM whose operands are read with ds_read_b64_tr_b16 (the transposed read also does the
+//     im2col gather), split over images into fp32 slabs reduced in a fixed order (deterministic);
+//   * one multi-segment reduction launch per layer backward.
+#include <vector>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -30,770 +37,1013 @@ using namespace ringdp::dev;
 
 namespace {
 
-constexpr int kThreads = 256;
-
-// ------------------------------------------------------------------ geometry
-template <int L>
-struct Geo;
-template <>
-struct Geo<2> {
-  static constexpr int CIN = 32, COUT = 64, IH = 13, PS = 1, OH = 11, PH = 10;
-};
-template <>
-struct Geo<3> {
-  static constexpr int CIN = 64, COUT = 128, IH = 10, PS = 2, OH = 8, PH = 4;
-};
-
 __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
-__host__ __device__ constexpr int align16(int bytes) { return (bytes + 15) / 16 * 16; }
 
-// 8 channels of d(conv output) at (y, x) from d(pooled), argmax and pooled > 0 (ReLU mask).
-// Gather form: sums over every pooling window that covers (y, x) and selected it.
-template <int OH, int PH, int PS, int C>
-__device__ __forceinline__ void unpool_grad8(const bf16* __restrict__ dout, const uint8_t* __restrict__ idx,
-                                             const bf16* __restrict__ pooled, int y, int x, int c0,
-                                             float (&g)[8]) {
-#pragma unroll
-  for (int j = 0; j < 8; ++j) g[j] = 0.f;
-  const int py_lo = y >= 1 ? (y - 1 + PS - 1) / PS : 0;
-  const int py_hi = min(PH - 1, y / PS);
-  const int px_lo = x >= 1 ? (x - 1 + PS - 1) / PS : 0;
-  const int px_hi = min(PH - 1, x / PS);
-  for (int py = py_lo; py <= py_hi; ++py) {
-    for (int px = px_lo; px <= px_hi; ++px) {
-      const int e = (py * PH + px) * C + c0;
-      const int want = (y - py * PS) * 2 + (x - px * PS);
-      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dout + e);
-      const bf16x8 pv = *reinterpret_cast<const bf16x8*>(pooled + e);
-      const uint2 iv = *reinterpret_cast<const uint2*>(idx + e);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t word = j < 4 ? iv.x : iv.y;
-        const int ij = (word >> (8 * (j & 3))) & 0xff;
-        if (ij == want && (float)pv[j] > 0.f) g[j] += (float)dv[j];
-      }
-    }
-  }
-}
+// ------------------------------------------------------------------ packed weight layout
+// bf16 element offsets inside the packed buffer.  Fragment order: [n-tile][k-step][lane][8].
+constexpr int P1_OFF = 0, P1_N = 2 * 64 * 8;                    // conv1 fwd   (K = 25 -> 32)
+constexpr int P2F_OFF = P1_OFF + P1_N, P2F_N = 4 * 9 * 512;     // conv2 fwd   (N 64, K 288)
+constexpr int P3F_OFF = P2F_OFF + P2F_N, P3F_N = 8 * 18 * 512;  // conv3 fwd   (N 128, K 576)
+constexpr int P2D_OFF = P3F_OFF + P3F_N, P2D_N = 2 * 18 * 512;  // conv2 dgrad (N 32, K 576)
+constexpr int P3D_OFF = P2D_OFF + P2D_N, P3D_N = 4 * 36 * 512;  // conv3 dgrad (N 64, K 1152)
+constexpr int PFC_OFF = P3D_OFF + P3D_N, PFC_N = 16 * 128 * 10; // fc1 [window][co][n]
+constexpr int PACK_TOTAL = PFC_OFF + PFC_N;
 
-// ------------------------------------------------------------------ conv1 forward (VALU fp32)
-// One workgroup loops over images; per image: 30x30 zero-ringed normalised input in LDS.
-// Work item = (channel group of 8, pooled position): 8 ch x 4 conv outputs x 25 taps.
-template <bool U8>
-__global__ __launch_bounds__(kThreads) void conv1_fwd_kernel(const void* __restrict__ xin,
-                                                             const float* __restrict__ w,
-                                                             const float* __restrict__ bias,
-                                                             bf16* __restrict__ a1,
-                                                             uint8_t* __restrict__ idx1, int B,
-                                                             float mean, float inv_std, float in_scale) {
-  __shared__ float xs[30 * 30];
-  __shared__ float ws[32 * 25];
-  __shared__ float bs[32];
-  for (int i = threadIdx.x; i < 800; i += kThreads) ws[i] = w[i];
-  if (threadIdx.x < 32) bs[threadIdx.x] = bias[threadIdx.x];
-  for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < 900; i += kThreads) {
-      const int r = i / 30 - 1, c = i % 30 - 1;
-      float v = 0.f;
-      if (r >= 0 && r < 28 && c >= 0 && c < 28) {
-        const int64_t o = (int64_t)b * 784 + r * 28 + c;
-        const float raw = U8 ? (float)static_cast<const uint8_t*>(xin)[o] * in_scale
-                             : static_cast<const float*>(xin)[o];
-        v = (raw - mean) * inv_std;
-      }
-      xs[i] = v;
-    }
-    __syncthreads();
-    for (int item = threadIdx.x; item < 4 * 169; item += kThreads) {
-      const int cg = item / 169, pp = item % 169;
-      const int ph = pp / 13, pw = pp % 13;
-      float patch[6][6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) patch[r][c] = xs[(2 * ph + r) * 30 + 2 * pw + c];
-      bf16x8 outv;
-      uint32_t iw0 = 0, iw1 = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int co = cg * 8 + j;
-        float acc[4];
-        const float bv = bs[co];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] = bv;
-#pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-          for (int kw = 0; kw < 5; ++kw) {
-            const float wv = ws[co * 25 + kh * 5 + kw];
-            acc[0] = fmaf(wv, patch[kh][kw], acc[0]);
-            acc[1] = fmaf(wv, patch[kh][kw + 1], acc[1]);
-            acc[2] = fmaf(wv, patch[kh + 1][kw], acc[2]);
-            acc[3] = fmaf(wv, patch[kh + 1][kw + 1], acc[3]);
-          }
-        int bi = 0;
-        float bm = acc[0];
-#pragma unroll
-        for (int q = 1; q < 4; ++q)
-          if (acc[q] > bm) {
-            bm = acc[q];
-            bi = q;
-          }
-        outv[j] = (bf16)fmaxf(bm, 0.f);
-        if (j < 4)
-          iw0 |= (uint32_t)bi << (8 * j);
-        else
-          iw1 |= (uint32_t)bi << (8 * (j - 4));
-      }
-      const int64_t o = ((int64_t)b * 169 + pp) * 32 + cg * 8;
-      *reinterpret_cast<bf16x8*>(a1 + o) = outv;
-      *reinterpret_cast<uint2*>(idx1 + o) = make_uint2(iw0, iw1);
-    }
-  }
-}
-
-// ------------------------------------------------------------------ conv3x3 fwd + ReLU + pool
-// Implicit GEMM: M = OH*OH output positions, N = CN output channels (slice `ns` of NSPLIT),
-// K = 9 taps x CIN.  A[m][k] = in[oh+kh][ow+kw][ci] read from the LDS image; B[n][k] = the
-// slice's weights (bf16, k-contiguous rows).  Epilogue: bias -> fp32 LDS tile -> max-pool with
-// argmax -> ReLU -> bf16 pooled output.
-template <int L, int NSPLIT>
-struct FwdCfg {
-  using G = Geo<L>;
-  static constexpr int CN = G::COUT / NSPLIT;
-  static constexpr int K = 9 * G::CIN;
-  static constexpr int KS = K / 32;
-  static constexpr int M = G::OH * G::OH;
-  static constexpr int MT = cdiv(M, 16);
-  static constexpr int NT = CN / 16;
-  static constexpr int A_RS = G::CIN + 8;  // bf16 elements per LDS image row (position)
-  static constexpr int B_RS = K + 8;       // bf16 elements per LDS weight row
-  static constexpr int C_RS = CN + 1;      // floats per epilogue row
-  static constexpr int A_BYTES = align16(G::IH * G::IH * A_RS * 2);
-  static constexpr int B_BYTES = align16(CN * B_RS * 2);
-  static constexpr int C_BYTES = align16(M * C_RS * 4);
-  static constexpr int LDS = B_BYTES + (A_BYTES > C_BYTES ? A_BYTES : C_BYTES);
-  static constexpr int TILES = MT * NT;
-  static constexpr int TPW = cdiv(TILES, 4);  // tiles per wave
-};
-
-template <int L, int NSPLIT>
-__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(const bf16* __restrict__ in,
-                                                            const float* __restrict__ w,
-                                                            const float* __restrict__ bias,
-                                                            bf16* __restrict__ out,
-                                                            uint8_t* __restrict__ idx, int B) {
-  using G = Geo<L>;
-  using F = FwdCfg<L, NSPLIT>;
-  __shared__ __attribute__((aligned(16))) char smem[F::LDS];
-  bf16* Bs = reinterpret_cast<bf16*>(smem);
-  bf16* As = reinterpret_cast<bf16*>(smem + F::B_BYTES);
-  float* Cs = reinterpret_cast<float*>(smem + F::B_BYTES);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ns = blockIdx.x % NSPLIT;
-  const int co0 = ns * F::CN;
-  const int groups = gridDim.x / NSPLIT;
-
-  // Stage this slice's weights once: natural [co][ci][tap] order reads, [co][tap*CIN+ci] writes.
-  for (int e = tid; e < F::CN * G::CIN * 9; e += kThreads) {
-    const int co = e / (G::CIN * 9), r = e % (G::CIN * 9), ci = r / 9, tap = r % 9;
-    Bs[co * F::B_RS + tap * G::CIN + ci] = (bf16)w[(int64_t)co0 * G::CIN * 9 + e];
-  }
-
-  for (int b = blockIdx.x / NSPLIT; b < B; b += groups) {
-    __syncthreads();  // previous image's epilogue done with Cs (aliases As)
-    // Stage the input image (NHWC) with padded rows.
-    constexpr int CH8 = G::CIN / 8;
-    const bf16* src = in + (int64_t)b * G::IH * G::IH * G::CIN;
-    for (int e = tid; e < G::IH * G::IH * CH8; e += kThreads) {
-      const int pos = e / CH8, q = e % CH8;
-      *reinterpret_cast<bf16x8*>(As + pos * F::A_RS + q * 8) =
-          *reinterpret_cast<const bf16x8*>(src + pos * G::CIN + q * 8);
-    }
-    __syncthreads();
-
-    f32x4 acc[F::TPW];
-#pragma unroll
-    for (int t = 0; t < F::TPW; ++t) acc[t] = zero_f32x4();
-    const int r16 = lane & 15, q8 = (lane >> 4) * 8;
-    // Per-tile A-row base (position) for this lane.
-    int arow[F::TPW];
-    bool avalid[F::TPW];
-#pragma unroll
-    for (int t = 0; t < F::TPW; ++t) {
-      const int tile = wave + 4 * t;
-      const int mt = tile % F::MT;
-      const int m = mt * 16 + r16;
-      avalid[t] = tile < F::TILES && m < F::M;
-      const int mm = avalid[t] ? m : 0;
-      arow[t] = (mm / G::OH) * G::IH + (mm % G::OH);
-    }
-#pragma unroll 2
-    for (int ks = 0; ks < F::KS; ++ks) {
-      const int k0 = ks * 32;
-      const int tap = k0 / G::CIN, ci0 = k0 % G::CIN;
-      const int kh = tap / 3, kw = tap % 3;
-      const int shift = kh * G::IH + kw;
-#pragma unroll
-      for (int t = 0; t < F::TPW; ++t) {
-        const int tile = wave + 4 * t;
-        if (tile >= F::TILES) continue;
-        const int nt = tile / F::MT;
-        const bf16x8 bfrag =
-            *reinterpret_cast<const bf16x8*>(Bs + (nt * 16 + r16) * F::B_RS + k0 + q8);
-        bf16x8 afrag = zero_bf16x8();
-        if (avalid[t])
-          afrag = *reinterpret_cast<const bf16x8*>(As + (arow[t] + shift) * F::A_RS + ci0 + q8);
-        acc[t] = mfma16x16x32(afrag, bfrag, acc[t]);
-      }
-    }
-    __syncthreads();  // all waves done reading As before Cs (alias) is written
-#pragma unroll
-    for (int t = 0; t < F::TPW; ++t) {
-      const int tile = wave + 4 * t;
-      if (tile >= F::TILES) continue;
-      const int mt = tile % F::MT, nt = tile / F::MT;
-      const int c = nt * 16 + r16;
-      const float bv = bias[co0 + c];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mt * 16 + (lane >> 4) * 4 + i;
-        if (m < F::M) Cs[m * F::C_RS + c] = acc[t][i] + bv;
-      }
-    }
-    __syncthreads();
-    // Max-pool (k2, stride PS) with first-max argmax, then ReLU; 8 channels per item.
-    constexpr int CG = F::CN / 8;
-    bf16* ob = out + (int64_t)b * G::PH * G::PH * G::COUT;
-    uint8_t* ib = idx + (int64_t)b * G::PH * G::PH * G::COUT;
-    for (int e = tid; e < G::PH * G::PH * CG; e += kThreads) {
-      const int pp = e / CG, cg = e % CG;
-      const int ph = pp / G::PH, pw = pp % G::PH;
-      const int m00 = (ph * G::PS) * G::OH + pw * G::PS;
-      bf16x8 ov;
-      uint32_t w0 = 0, w1 = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = cg * 8 + j;
-        const float v0 = Cs[m00 * F::C_RS + c];
-        const float v1 = Cs[(m00 + 1) * F::C_RS + c];
-        const float v2 = Cs[(m00 + G::OH) * F::C_RS + c];
-        const float v3 = Cs[(m00 + G::OH + 1) * F::C_RS + c];
-        int bi = 0;
-        float bm = v0;
-        if (v1 > bm) { bm = v1; bi = 1; }
-        if (v2 > bm) { bm = v2; bi = 2; }
-        if (v3 > bm) { bm = v3; bi = 3; }
-        ov[j] = (bf16)fmaxf(bm, 0.f);
-        if (j < 4) w0 |= (uint32_t)bi << (8 * j);
-        else w1 |= (uint32_t)bi << (8 * (j - 4));
-      }
-      const int o = pp * G::COUT + co0 + cg * 8;
-      *reinterpret_cast<bf16x8*>(ob + o) = ov;
-      *reinterpret_cast<uint2*>(ib + o) = make_uint2(w0, w1);
-    }
-  }
-}
-
-// ------------------------------------------------------------------ conv3x3 dgrad
-// din[ih][iw][ci] = sum_{kh',kw',co} P[ih+kh'][iw+kw'][co] * W[co][ci][2-kh'][2-kw'], with P the
-// d(conv) image (re-created from d(pooled)) inside a zero ring of width 2.
-template <int L, int NSPLIT>
-struct DgradCfg {
-  using G = Geo<L>;
-  static constexpr int CN = G::CIN / NSPLIT;   // input channels produced per workgroup
-  static constexpr int K = 9 * G::COUT;
-  static constexpr int KS = K / 32;
-  static constexpr int PW = G::OH + 4;         // padded d(conv) width (= IH + 2)
-  static constexpr int M = G::IH * G::IH;
-  static constexpr int MT = cdiv(M, 16);
-  static constexpr int NT = CN / 16;
-  static constexpr int P_RS = G::COUT + 8;
-  static constexpr int B_RS = K + 8;
-  static constexpr int C_RS = CN + 1;
-  static constexpr int P_BYTES = align16(PW * PW * P_RS * 2);
-  static constexpr int B_BYTES = align16(CN * B_RS * 2);
-  static constexpr int C_BYTES = align16(M * C_RS * 4);
-  static constexpr int LDS = B_BYTES + (P_BYTES > C_BYTES ? P_BYTES : C_BYTES);
-  static constexpr int TILES = MT * NT;
-  static constexpr int TPW = cdiv(TILES, 4);
-};
-
-template <int L, int NSPLIT>
-__device__ __forceinline__ void dgrad_body(char* smem, const float* __restrict__ w,
-                                           const bf16* __restrict__ dout,
-                                           const uint8_t* __restrict__ idx,
-                                           const bf16* __restrict__ pooled, bf16* __restrict__ din,
-                                           int B, int block, int nblocks) {
-  using G = Geo<L>;
-  using D = DgradCfg<L, NSPLIT>;
-  bf16* Bs = reinterpret_cast<bf16*>(smem);
-  bf16* Ps = reinterpret_cast<bf16*>(smem + D::B_BYTES);
-  float* Cs = reinterpret_cast<float*>(smem + D::B_BYTES);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ns = block % NSPLIT;
-  const int ci0 = ns * D::CN;
-  const int groups = nblocks / NSPLIT;
-
-  // Flipped, transposed weight slice: Bs[ci][tap'*COUT + co] = W[co][ci0+ci][8 - tap'].
-  for (int e = tid; e < G::COUT * D::CN * 9; e += kThreads) {
-    const int co = e / (D::CN * 9), r = e % (D::CN * 9), ci = r / 9, tap = r % 9;
-    Bs[ci * D::B_RS + (8 - tap) * G::COUT + co] =
-        (bf16)w[(int64_t)co * G::CIN * 9 + (int64_t)(ci0 + ci) * 9 + tap];
-  }
-
-  for (int b = block / NSPLIT; b < B; b += groups) {
-    __syncthreads();
-    // Zero ring + interior re-created from the pooled gradient.
-    constexpr int CG = G::COUT / 8;
-    const int64_t pbase = (int64_t)b * G::PH * G::PH * G::COUT;
-    for (int e = tid; e < D::PW * D::PW * CG; e += kThreads) {
-      const int pos = e / CG, cg = e % CG;
-      const int y = pos / D::PW - 2, x = pos % D::PW - 2;
-      bf16x8 v = zero_bf16x8();
-      if (y >= 0 && y < G::OH && x >= 0 && x < G::OH) {
-        float g[8];
-        unpool_grad8<G::OH, G::PH, G::PS, G::COUT>(dout + pbase, idx + pbase, pooled + pbase, y,
-                                                   x, cg * 8, g);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (bf16)g[j];
-      }
-      *reinterpret_cast<bf16x8*>(Ps + pos * D::P_RS + cg * 8) = v;
-    }
-    __syncthreads();
-
-    f32x4 acc[D::TPW];
-#pragma unroll
-    for (int t = 0; t < D::TPW; ++t) acc[t] = zero_f32x4();
-    const int r16 = lane & 15, q8 = (lane >> 4) * 8;
-    int prow[D::TPW];
-    bool valid[D::TPW];
-#pragma unroll
-    for (int t = 0; t < D::TPW; ++t) {
-      const int tile = wave + 4 * t;
-      const int m = (tile % D::MT) * 16 + r16;
-      valid[t] = tile < D::TILES && m < D::M;
-      const int mm = valid[t] ? m : 0;
-      prow[t] = (mm / G::IH) * D::PW + (mm % G::IH);
-    }
-#pragma unroll 2
-    for (int ks = 0; ks < D::KS; ++ks) {
-      const int k0 = ks * 32;
-      const int tap = k0 / G::COUT, c0 = k0 % G::COUT;
-      const int shift = (tap / 3) * D::PW + (tap % 3);
-#pragma unroll
-      for (int t = 0; t < D::TPW; ++t) {
-        const int tile = wave + 4 * t;
-        if (tile >= D::TILES) continue;
-        const int nt = tile / D::MT;
-        const bf16x8 bfrag =
-            *reinterpret_cast<const bf16x8*>(Bs + (nt * 16 + r16) * D::B_RS + k0 + q8);
-        bf16x8 afrag = zero_bf16x8();
-        if (valid[t])
-          afrag = *reinterpret_cast<const bf16x8*>(Ps + (prow[t] + shift) * D::P_RS + c0 + q8);
-        acc[t] = mfma16x16x32(afrag, bfrag, acc[t]);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < D::TPW; ++t) {
-      const int tile = wave + 4 * t;
-      if (tile >= D::TILES) continue;
-      const int mt = tile % D::MT, nt = tile / D::MT;
-      const int c = nt * 16 + r16;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mt * 16 + (lane >> 4) * 4 + i;
-        if (m < D::M) Cs[m * D::C_RS + c] = acc[t][i];
-      }
-    }
-    __syncthreads();
-    constexpr int OG = D::CN / 8;
-    bf16* db = din + (int64_t)b * D::M * G::CIN;
-    for (int e = tid; e < D::M * OG; e += kThreads) {
-      const int m = e / OG, cg = e % OG;
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)Cs[m * D::C_RS + cg * 8 + j];
-      *reinterpret_cast<bf16x8*>(db + m * G::CIN + ci0 + cg * 8) = v;
-    }
-  }
-}
-
-// ------------------------------------------------------------------ conv3x3 wgrad (split-K)
-// dWt[n = tap*CIN + ci][co] = sum_{b, pos} Dc[b][pos][co] * X[b][pos shifted by tap][ci].
-// Wave grid WM x WN over (co tiles) x (n tiles of this tap group).
-template <int L>
-struct WgradCfg;
-template <>
-struct WgradCfg<2> {
-  static constexpr int TG = 9, WM = 2, WN = 2;
-};
-template <>
-struct WgradCfg<3> {
-  static constexpr int TG = 3, WM = 1, WN = 4;
-};
-
-template <int L>
-struct WgradGeo {
-  using G = Geo<L>;
-  using C = WgradCfg<L>;
-  static constexpr int NPOS = G::OH * G::OH;
-  static constexpr int KP = cdiv(NPOS, 32) * 32;       // K rows per image (zero padded)
-  static constexpr int KS = KP / 32;
-  static constexpr int NGROUPS = 9 / C::TG;
-  static constexpr int NCH = C::TG * G::CIN;           // n columns per workgroup
-  static constexpr int MTW = (G::COUT / 16) / C::WM;   // m tiles per wave
-  static constexpr int NTW = (NCH / 16) / C::WN;       // n tiles per wave
-  static constexpr int D_RS = G::COUT + 8;
-  static constexpr int X_RS = G::CIN + 8;
-  static constexpr int D_BYTES = align16(KP * D_RS * 2);
-  static constexpr int X_BYTES = align16(G::IH * G::IH * X_RS * 2);
-  static constexpr int LDS = D_BYTES + X_BYTES;
-  static constexpr int NOUT = 9 * G::CIN * G::COUT;    // floats per slab (weights)
-  static_assert((G::COUT / 16) % C::WM == 0, "bad WM");
-  static_assert((NCH / 16) % C::WN == 0, "bad WN");
-};
-
-// Slab layout per slice s: [NOUT weights in dWt order (n-major, co fastest)] [COUT bias].
-template <int L>
-__device__ __forceinline__ void wgrad_body(char* smem, const bf16* __restrict__ x,
-                                           const bf16* __restrict__ dout,
-                                           const uint8_t* __restrict__ idx,
-                                           const bf16* __restrict__ pooled,
-                                           float* __restrict__ slabs, int B, int nslices,
-                                           int block) {
-  using G = Geo<L>;
-  using C = WgradCfg<L>;
-  using W = WgradGeo<L>;
-  bf16* Ds = reinterpret_cast<bf16*>(smem);
-  bf16* Xs = reinterpret_cast<bf16*>(smem + W::D_BYTES);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slice = block / W::NGROUPS, tg = block % W::NGROUPS;
-  const int wm = wave / C::WN, wn = wave % C::WN;
-  const int per = cdiv(B, nslices);
-  const int b_lo = slice * per, b_hi = min(B, b_lo + per);
-
-  f32x4 acc[W::MTW][W::NTW];
-#pragma unroll
-  for (int i = 0; i < W::MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < W::NTW; ++j) acc[i][j] = zero_f32x4();
-  float bias_acc = 0.f;  // thread tid < COUT owns channel tid (tap group 0 only)
-
-  const int g16 = lane & 15, grp = lane >> 4;
-  const int q = g16 >> 2, p = g16 & 3;
-
-  for (int b = b_lo; b < b_hi; ++b) {
-    __syncthreads();
-    constexpr int CG = G::COUT / 8;
-    const int64_t pbase = (int64_t)b * G::PH * G::PH * G::COUT;
-    for (int e = tid; e < W::KP * CG; e += kThreads) {
-      const int pos = e / CG, cg = e % CG;
-      bf16x8 v = zero_bf16x8();
-      if (pos < W::NPOS) {
-        float g[8];
-        unpool_grad8<G::OH, G::PH, G::PS, G::COUT>(dout + pbase, idx + pbase, pooled + pbase,
-                                                   pos / G::OH, pos % G::OH, cg * 8, g);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (bf16)g[j];
-      }
-      *reinterpret_cast<bf16x8*>(Ds + pos * W::D_RS + cg * 8) = v;
-    }
-    constexpr int XG = G::CIN / 8;
-    const bf16* xb = x + (int64_t)b * G::IH * G::IH * G::CIN;
-    for (int e = tid; e < G::IH * G::IH * XG; e += kThreads) {
-      const int pos = e / XG, cg = e % XG;
-      *reinterpret_cast<bf16x8*>(Xs + pos * W::X_RS + cg * 8) =
-          *reinterpret_cast<const bf16x8*>(xb + pos * G::CIN + cg * 8);
-    }
-    __syncthreads();
-    if (tg == 0 && tid < G::COUT) {
-      float s = 0.f;
-      for (int pos = 0; pos < W::NPOS; ++pos) s += (float)Ds[pos * W::D_RS + tid];
-      bias_acc += s;
-    }
-    for (int ks = 0; ks < W::KS; ++ks) {
-      const int kb = ks * 32 + grp * 8;  // this lane group's first k row
-      // A fragments (d(conv)^T): rows k, columns co -> transposed reads.
-      bf16x8 af[W::MTW];
-#pragma unroll
-      for (int i = 0; i < W::MTW; ++i) {
-        const int m0 = (wm * W::MTW + i) * 16;
-        const bf16x4 lo = lds_read_tr16(Ds + (kb + q) * W::D_RS + m0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(Ds + (kb + 4 + q) * W::D_RS + m0 + 4 * p);
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      // B rows: the X positions of k rows kb+q and kb+4+q (clamped; D is zero there).
-      const int kr0 = min(kb + q, W::NPOS - 1), kr1 = min(kb + 4 + q, W::NPOS - 1);
-      const int xr0 = (kr0 / G::OH) * G::IH + kr0 % G::OH;
-      const int xr1 = (kr1 / G::OH) * G::IH + kr1 % G::OH;
-#pragma unroll
-      for (int j = 0; j < W::NTW; ++j) {
-        const int n0 = (wn * W::NTW + j) * 16;           // column within this tap group
-        const int tap = tg * C::TG + n0 / G::CIN, c0 = n0 % G::CIN;
-        const int shift = (tap / 3) * G::IH + (tap % 3);
-        const bf16x4 lo = lds_read_tr16(Xs + (xr0 + shift) * W::X_RS + c0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(Xs + (xr1 + shift) * W::X_RS + c0 + 4 * p);
-        const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int i = 0; i < W::MTW; ++i) acc[i][j] = mfma16x16x32(af[i], bf, acc[i][j]);
-      }
-    }
-  }
-  // Write this slice's partial: slab[n][co] (co fastest) for n in this tap group.
-  float* slab = slabs + (int64_t)slice * (W::NOUT + G::COUT);
-#pragma unroll
-  for (int i = 0; i < W::MTW; ++i) {
-#pragma unroll
-    for (int j = 0; j < W::NTW; ++j) {
-      const int co = (wm * W::MTW + i) * 16 + (lane >> 4) * 4;
-      const int n = tg * W::NCH + (wn * W::NTW + j) * 16 + g16;
-      *reinterpret_cast<f32x4*>(slab + (int64_t)n * G::COUT + co) = acc[i][j];
-    }
-  }
-  if (tg == 0 && tid < G::COUT) slab[W::NOUT + tid] = bias_acc;
-}
-
-// Fused backward launch: blocks [0, n_dgrad) compute the data gradient, the rest the weight
-// gradient slabs (horizontal fusion: one launch, both read the same d(pooled)).
-template <int L, int NSPLIT>
-__global__ __launch_bounds__(kThreads) void conv_bwd_kernel(const bf16* __restrict__ in,
-                                                            const float* __restrict__ w,
-                                                            const bf16* __restrict__ dout,
-                                                            const uint8_t* __restrict__ idx,
-                                                            const bf16* __restrict__ pooled,
-                                                            bf16* __restrict__ din, int B,
-                                                            float* __restrict__ slabs,
-                                                            int nslices, int n_dgrad) {
-  constexpr int L1 = DgradCfg<L, NSPLIT>::LDS, L2 = WgradGeo<L>::LDS;
-  __shared__ __attribute__((aligned(16))) char smem[L1 > L2 ? L1 : L2];
-  if ((int)blockIdx.x < n_dgrad) {
-    dgrad_body<L, NSPLIT>(smem, w, dout, idx, pooled, din, B, blockIdx.x, n_dgrad);
+__global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ w1,
+                                                           const float* __restrict__ w2,
+                                                           const float* __restrict__ w3,
+                                                           const float* __restrict__ wfc,
+                                                           bf16* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= PACK_TOTAL) return;
+  float v = 0.f;
+  if (e < P2F_OFF) {
+    const int j = e & 7, lane = (e >> 3) & 63, nt = e >> 9;
+    const int co = nt * 16 + (lane & 15), t = 8 * (lane >> 4) + j;
+    v = t < 25 ? w1[co * 25 + t] : 0.f;
+  } else if (e < P2D_OFF) {  // forward fragments of conv2 / conv3: B[k = tap*CIN + ci][n = co]
+    const bool l2 = e < P3F_OFF;
+    const int r = e - (l2 ? P2F_OFF : P3F_OFF);
+    const int CIN = l2 ? 32 : 64, KS = l2 ? 9 : 18;
+    const float* w = l2 ? w2 : w3;
+    const int j = r & 7, lane = (r >> 3) & 63, ks = (r >> 9) % KS, nt = (r >> 9) / KS;
+    const int co = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
+    v = w[(co * CIN + k % CIN) * 9 + k / CIN];
+  } else if (e < PFC_OFF) {  // dgrad fragments: B[k = tap'*COUT + co][n = ci] = W[co][ci][8 - tap']
+    const bool l2 = e < P3D_OFF;
+    const int r = e - (l2 ? P2D_OFF : P3D_OFF);
+    const int CIN = l2 ? 32 : 64, COUT = l2 ? 64 : 128, KS = l2 ? 18 : 36;
+    const float* w = l2 ? w2 : w3;
+    const int j = r & 7, lane = (r >> 3) & 63, ks = (r >> 9) % KS, nt = (r >> 9) / KS;
+    const int ci = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
+    v = w[((k % COUT) * CIN + ci) * 9 + (8 - k / COUT)];
   } else {
-    wgrad_body<L>(smem, in, dout, idx, pooled, slabs, B, nslices, blockIdx.x - n_dgrad);
+    const int r = e - PFC_OFF;
+    const int n = r % 10, co = (r / 10) % 128, wd = r / 1280;
+    v = wfc[n * 2048 + co * 16 + wd];
+  }
+  out[e] = (bf16)v;
+}
+
+__device__ __forceinline__ bf16x8 bmax8(const bf16x8& a, const bf16x8& b) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (float)a[j] >= (float)b[j] ? a[j] : b[j];
+  return r;
+}
+
+// max over a 2x2 window of an LDS image with row stride rs (in bf16) and width w
+__device__ __forceinline__ bf16x8 window_max8(const bf16* r0, int rs, int w) {
+  return bmax8(bmax8(*reinterpret_cast<const bf16x8*>(r0), *reinterpret_cast<const bf16x8*>(r0 + rs)),
+               bmax8(*reinterpret_cast<const bf16x8*>(r0 + w * rs),
+                     *reinterpret_cast<const bf16x8*>(r0 + (w + 1) * rs)));
+}
+
+// First-max argmax over the 4 registers of a window + bias + ReLU (torch max_pool2d semantics:
+// strict '>' keeps the first maximum in (0,0),(0,1),(1,0),(1,1) order).
+__device__ __forceinline__ float pool4(const f32x4& c, float bias, int& arg) {
+  float bm = c[0];
+  arg = 0;
+#pragma unroll
+  for (int r = 1; r < 4; ++r)
+    if (c[r] > bm) {
+      bm = c[r];
+      arg = r;
+    }
+  return fmaxf(bm + bias, 0.f);
+}
+
+__device__ __forceinline__ int byte_of(const uint2& v, int j) {
+  return (int)(((j < 4 ? v.x : v.y) >> (8 * (j & 3))) & 0xff);
+}
+
+// window-ordered GEMM row r = 4*window + i of a pooled (2x2/s2) 8x8 map -> spatial y*pw + x
+__device__ __forceinline__ int win_pos(int r, int pw) {
+  const int w = r >> 2, i = r & 3;
+  return (2 * (w >> 2) + (i >> 1)) * pw + 2 * (w & 3) + (i & 1);
+}
+
+__device__ __forceinline__ void stage_rows(const bf16* __restrict__ src, bf16* dst, int nchunks,
+                                           int chunks_per_row, int rs, int tid, int nthreads) {
+  for (int c = tid; c < nchunks; c += nthreads)
+    *reinterpret_cast<bf16x8*>(dst + (c / chunks_per_row) * rs + (c % chunks_per_row) * 8) =
+        reinterpret_cast<const bf16x8*>(src)[c];
+}
+
+// Async global -> LDS copy of 16 B per lane (global_load_lds_dwordx4): the LDS destination is the
+// wave-uniform base + lane * 16, so the image it fills is lane-linear (no padding inside a wave's 1 KiB).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// ================================================================== F1: conv1 (MFMA, K 25 -> 32)
+constexpr int C1_XS = 30 * 30 + 12;  // zero-ringed 30x30 bf16 image (+pad)
+
+template <bool U8>
+__device__ __forceinline__ void c1_load(const void* xin, int b, int tid, uint32_t& u, float4& f) {
+  if (tid < 196) {
+    if (U8)
+      u = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(xin) + (int64_t)b * 784)[tid];
+    else
+      f = reinterpret_cast<const float4*>(static_cast<const float*>(xin) + (int64_t)b * 784)[tid];
   }
 }
 
-// Reduce slabs over slices (4 waves x quarter of the slices, fixed combine order) and scatter to
-// the PyTorch weight layout [co][ci][kh][kw] + bias.
-template <int L>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_reduce_kernel(const float* __restrict__ slabs,
-                                                                     int nslices,
-                                                                     float* __restrict__ dw,
-                                                                     float* __restrict__ db) {
-  using G = Geo<L>;
-  using W = WgradGeo<L>;
-  constexpr int SL = W::NOUT + G::COUT;
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + lane;
-  float a0 = 0.f, a1 = 0.f;
-  if (i < SL) {
-    const float* p = slabs + i;
-    int k = wave;
-    for (; k + 4 < nslices; k += 8) {
-      a0 += p[(int64_t)k * SL];
-      a1 += p[(int64_t)(k + 4) * SL];
+template <bool U8>
+__device__ __forceinline__ void c1_store(bf16* xs, int tid, uint32_t u, float4 f, float mean,
+                                         float inv_std, float in_scale) {
+  if (tid < 196) {
+    float v[4];
+    if (U8) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = (float)((u >> (8 * k)) & 0xff) * in_scale;
+    } else {
+      v[0] = f.x;
+      v[1] = f.y;
+      v[2] = f.z;
+      v[3] = f.w;
     }
-    for (; k < nslices; k += 4) a0 += p[(int64_t)k * SL];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int p = 4 * tid + k, r = p / 28, c = p % 28;
+      xs[(r + 1) * 30 + c + 1] = (bf16)((v[k] - mean) * inv_std);
+    }
   }
-  part[wave][lane] = a0 + a1;
+}
+
+template <bool U8>
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__ xin,
+                                                        const bf16* __restrict__ packed,
+                                                        const float* __restrict__ bias,
+                                                        bf16* __restrict__ a1,
+                                                        uint8_t* __restrict__ idx1, int B,
+                                                        float mean, float inv_std, float in_scale) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][C1_XS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P1_OFF);
+  const bf16x8 bw0 = pk[lane], bw1 = pk[64 + lane];
+  const float bias0 = bias[lane & 15], bias1 = bias[16 + (lane & 15)];
+  int toff[8];
+  bool tval[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int t = 8 * (lane >> 4) + j;
+    tval[j] = t < 25;
+    toff[j] = tval[j] ? (t / 5) * 30 + t % 5 : 0;
+  }
+  for (int i = tid; i < 2 * C1_XS; i += 256) (&xs[0][0])[i] = (bf16)0.f;
   __syncthreads();
-  if (wave != 0 || i >= SL) return;
-  const float s = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
-  if (i < W::NOUT) {
-    const int n = i / G::COUT, co = i % G::COUT;
-    const int tap = n / G::CIN, ci = n % G::CIN;
-    dw[(co * G::CIN + ci) * 9 + tap] = s;
-  } else {
-    db[i - W::NOUT] = s;
+  uint32_t pu = 0;
+  float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+  int b = blockIdx.x;
+  if (b < B) {
+    c1_load<U8>(xin, b, tid, pu, pf);
+    c1_store<U8>(xs[0], tid, pu, pf, mean, inv_std, in_scale);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; b < B; b += gridDim.x) {
+    const int nb = b + gridDim.x;
+    if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
+    const bf16* x = xs[cur];
+    for (int mt = wave; mt < 43; mt += 4) {
+      const int r16 = lane & 15;
+      const int w = 4 * mt + (r16 >> 2), i = r16 & 3;
+      bf16x8 a = zero_bf16x8();
+      if (w < 169) {
+        const int base = (2 * (w / 13) + (i >> 1)) * 30 + 2 * (w % 13) + (i & 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] = tval[j] ? x[base + toff[j]] : (bf16)0.f;
+      }
+      const f32x4 c0 = mfma16x16x32(a, bw0, zero_f32x4());
+      const f32x4 c1 = mfma16x16x32(a, bw1, zero_f32x4());
+      const int wc = 4 * mt + (lane >> 4);
+      if (wc < 169) {
+        int g0, g1;
+        const float v0 = pool4(c0, bias0, g0), v1 = pool4(c1, bias1, g1);
+        const int64_t o = ((int64_t)b * 169 + wc) * 32 + (lane & 15);
+        a1[o] = (bf16)v0;
+        a1[o + 16] = (bf16)v1;
+        idx1[o] = (uint8_t)g0;
+        idx1[o + 16] = (uint8_t)g1;
+      }
+    }
+    if (nb < B) c1_store<U8>(xs[cur ^ 1], tid, pu, pf, mean, inv_std, in_scale);
+    __syncthreads();
+    cur ^= 1;
   }
 }
 
-// ------------------------------------------------------------------ conv1 wgrad (MFMA)
-// dW1[co][t] = sum_{b, y, x} Dc[b][y][x][co] * xpad[b][y + kh][x + kw], t = kh*5 + kw.
-// K rows = (y, x) with x padded to 32 per row (26 valid); A = Dc^T staged [co][y*32+x];
-// B[k][n=t] read from per-kw shifted copies of the input rows (aligned 16-byte reads).
-constexpr int C1_KROW = 32;
-constexpr int C1_K = 26 * C1_KROW;       // 832 = 26 k-steps
-constexpr int C1_DT_RS = C1_K + 8;       // bf16 per co row
-constexpr int C1_XS_RS = 40;             // bf16 per shifted input row (>= 32 + 8)
-constexpr int C1_DT_BYTES = align16(32 * C1_DT_RS * 2);
-constexpr int C1_XS_BYTES = align16(5 * 30 * C1_XS_RS * 2);
-constexpr int C1_NOUT = 32 * 25;
-constexpr int C1_SL = C1_NOUT + 32;
+// ================================================================== F2: conv2 + ReLU
+// 256 threads; wave (wm, wn) owns n-tiles {2wn, 2wn+1} x m-tiles {4wm..4wm+3} (121 rows -> 128).
+constexpr int C2_XRS = 40;  // bf16 per LDS row of the a1 image (32 + 8 pad)
+constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 + 8)
 
-template <bool U8>
-__global__ __launch_bounds__(kThreads) void conv1_wgrad_kernel(const void* __restrict__ xin,
-                                                               const bf16* __restrict__ da1,
-                                                               const uint8_t* __restrict__ idx1,
-                                                               const bf16* __restrict__ a1, int B,
-                                                               float mean, float inv_std,
-                                                               float in_scale,
-                                                               float* __restrict__ slabs,
-                                                               int nslices) {
-  __shared__ __attribute__((aligned(16))) char smem[C1_DT_BYTES + C1_XS_BYTES];
-  bf16* Dt = reinterpret_cast<bf16*>(smem);
-  bf16* Xs = reinterpret_cast<bf16*>(smem + C1_DT_BYTES);
+__global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restrict__ a1,
+                                                           const bf16* __restrict__ packed,
+                                                           const float* __restrict__ bias,
+                                                           bf16* __restrict__ r2, int B) {
+  __shared__ __attribute__((aligned(16))) bf16 X[2][169 * C2_XRS];
+  __shared__ __attribute__((aligned(16))) bf16 Cs[121 * C2_CRS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int per = cdiv(B, nslices);
-  const int b_lo = blockIdx.x * per, b_hi = min(B, b_lo + per);
-  // Wave (mt, nt): co tile mt (0..1), tap tile nt (0..1: taps 0-15, 16-31 with 25.. = 0).
-  const int mt = wave >> 1, nt = wave & 1;
-  f32x4 acc = zero_f32x4();
-  float bias_acc = 0.f;
+  const int wm = wave >> 1, wn = wave & 1;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
-  const int t = nt * 16 + r16;  // this lane's B column (tap)
-  const bool tvalid = t < 25;
-  const int kh = tvalid ? t / 5 : 0, kw = tvalid ? t % 5 : 0;
-
-  for (int b = b_lo; b < b_hi; ++b) {
-    __syncthreads();
-    // Zero the transposed d(conv) image, then scatter the pooled gradients.
-    for (int e = tid; e < 32 * C1_DT_RS / 8; e += kThreads)
-      reinterpret_cast<bf16x8*>(Dt)[e] = zero_bf16x8();
-    // Shifted input copies: Xs[kw][r][c] = xpad[r][c + kw], xpad = normalised input, ring of 1.
-    for (int e = tid; e < 5 * 30 * 32; e += kThreads) {
-      const int s = e / (30 * 32), rc = e % (30 * 32), r = rc / 32, c = rc % 32;
-      const int yy = r - 1, xx = c + s - 1;
-      float v = 0.f;
-      if (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) {
-        const int64_t o = (int64_t)b * 784 + yy * 28 + xx;
-        const float raw = U8 ? (float)static_cast<const uint8_t*>(xin)[o] * in_scale
-                             : static_cast<const float*>(xin)[o];
-        v = (raw - mean) * inv_std;
-      }
-      Xs[(s * 30 + r) * C1_XS_RS + c] = (bf16)v;
-    }
-    __syncthreads();
-    for (int e = tid; e < 169 * 32; e += kThreads) {
-      const int pp = e / 32, co = e % 32;
-      const int64_t o = ((int64_t)b * 169 + pp) * 32 + co;
-      const float pv = (float)a1[o];
-      const float g = pv > 0.f ? (float)da1[o] : 0.f;
-      const int i = idx1[o];
-      const int y = (pp / 13) * 2 + (i >> 1), x = (pp % 13) * 2 + (i & 1);
-      Dt[co * C1_DT_RS + y * C1_KROW + x] = (bf16)g;
-    }
-    __syncthreads();
-    if (tid < 32) {
-      float s = 0.f;
-      for (int k = 0; k < C1_K; ++k) s += (float)Dt[tid * C1_DT_RS + k];
-      bias_acc += s;
-    }
-    for (int ks = 0; ks < 26; ++ks) {
-      const int y = ks;  // one padded row of 32 positions per k-step
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Dt + (mt * 16 + r16) * C1_DT_RS + ks * 32 + q8);
-      bf16x8 bf = zero_bf16x8();
-      if (tvalid) bf = *reinterpret_cast<const bf16x8*>(Xs + (kw * 30 + y + kh) * C1_XS_RS + q8);
-      acc = mfma16x16x32(af, bf, acc);
-    }
-  }
-  float* slab = slabs + (int64_t)blockIdx.x * C1_SL;
-  // C layout: col = tap (lane & 15), rows = co (lane >> 4)*4 + i.
+  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P2F_OFF);
+  bf16x8 bw[2][9];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = mt * 16 + (lane >> 4) * 4 + i;
-    if (tvalid) slab[co * 25 + t] = acc[i];
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 9; ++ks) bw[t][ks] = pk[((2 * wn + t) * 9 + ks) * 64 + lane];
+  float bv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) bv[t] = bias[(2 * wn + t) * 16 + r16];
+  int base[4];
+  bool valid[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    const int m = (4 * wm + mt) * 16 + r16;
+    valid[mt] = m < 121;
+    const int mm = valid[mt] ? m : 0;
+    base[mt] = (mm / 11) * 13 + mm % 11;
   }
-  if (tid < 32) slab[C1_NOUT + tid] = bias_acc;
-}
-
-// ------------------------------------------------------------------ fc (2048 -> 10)
-// Activation k' = pos*128 + c (NHWC), weight column k = c*16 + pos (PyTorch CHW flatten).
-constexpr int FC_K = 2048, FC_N = 10;
-__device__ __forceinline__ int fc_wcol(int kp) { return (kp & 127) * 16 + (kp >> 7); }
-
-// One wave per image; W staged once per workgroup in LDS (fp32, activation order).
-__global__ __launch_bounds__(kThreads) void fc_fwd_kernel(const bf16* __restrict__ a3,
-                                                          const float* __restrict__ w,
-                                                          const float* __restrict__ bias,
-                                                          float* __restrict__ logits, int B) {
-  __shared__ __attribute__((aligned(16))) float Ws[FC_N * FC_K];
-  for (int e = threadIdx.x; e < FC_N * FC_K; e += kThreads) {
-    const int n = e / FC_K, kp = e % FC_K;
-    Ws[e] = w[n * FC_K + fc_wcol(kp)];
+  bf16x8 pre[3];
+  auto load = [&](int bb) {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(a1 + (int64_t)bb * 169 * 32);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int c = tid + 256 * k;
+      if (c < 676) pre[k] = src[c];
+    }
+  };
+  auto store = [&](bf16* dst) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int c = tid + 256 * k;
+      if (c < 676) *reinterpret_cast<bf16x8*>(dst + (c >> 2) * C2_XRS + (c & 3) * 8) = pre[k];
+    }
+  };
+  int b = blockIdx.x;
+  if (b < B) {
+    load(b);
+    store(X[0]);
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int b = blockIdx.x * 4 + wave; b < B; b += gridDim.x * 4) {
-    float s[FC_N];
+  int cur = 0;
+  for (; b < B; b += gridDim.x) {
+    const int nb = b + gridDim.x;
+    if (nb < B) load(nb);
+    const bf16* x = X[cur];
+    f32x4 acc[4][2];
 #pragma unroll
-    for (int n = 0; n < FC_N; ++n) s[n] = 0.f;
-    const bf16* xb = a3 + (int64_t)b * FC_K;
+    for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int kp = j * 512 + lane * 8;
-      const bf16x8 xv = *reinterpret_cast<const bf16x8*>(xb + kp);
+    for (int ks = 0; ks < 9; ++ks) {
+      const int shift = (ks / 3) * 13 + ks % 3;
 #pragma unroll
-      for (int n = 0; n < FC_N; ++n) {
-        const float4 w0 = *reinterpret_cast<const float4*>(Ws + n * FC_K + kp);
-        const float4 w1 = *reinterpret_cast<const float4*>(Ws + n * FC_K + kp + 4);
-        s[n] += (float)xv[0] * w0.x + (float)xv[1] * w0.y + (float)xv[2] * w0.z +
-                (float)xv[3] * w0.w + (float)xv[4] * w1.x + (float)xv[5] * w1.y +
-                (float)xv[6] * w1.z + (float)xv[7] * w1.w;
+      for (int mt = 0; mt < 4; ++mt) {
+        bf16x8 a = zero_bf16x8();
+        if (valid[mt]) a = *reinterpret_cast<const bf16x8*>(x + (base[mt] + shift) * C2_XRS + q8);
+        acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
+        acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
       }
     }
+    __syncthreads();  // previous image's copy-out of Cs is complete
 #pragma unroll
-    for (int n = 0; n < FC_N; ++n) s[n] = wave_sum(s[n]);
-    if (lane < FC_N) {
-      float v = 0.f;
+    for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int n = 0; n < FC_N; ++n)
-        if (n == lane) v = s[n];
-      logits[(int64_t)b * FC_N + lane] = v + bias[lane];
-    }
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = (4 * wm + mt) * 16 + (lane >> 4) * 4 + i;
+          if (m < 121) Cs[m * C2_CRS + (2 * wn + t) * 16 + r16] = (bf16)fmaxf(acc[mt][t][i] + bv[t], 0.f);
+        }
+    if (nb < B) store(X[cur ^ 1]);
+    __syncthreads();
+    bf16x8* dst = reinterpret_cast<bf16x8*>(r2 + (int64_t)b * 121 * 64);
+    for (int c = tid; c < 968; c += 256)
+      dst[c] = *reinterpret_cast<const bf16x8*>(Cs + (c >> 3) * C2_CRS + (c & 7) * 8);
+    cur ^= 1;
   }
 }
 
-// Each thread owns 8 activation columns: da3 for those columns per image, and dW partials
-// (80 accumulators) over this slice's images.  Slab: [N*K in PyTorch order][N bias].
-__global__ __launch_bounds__(kThreads) void fc_bwd_kernel(const bf16* __restrict__ a3,
-                                                          const float* __restrict__ w,
-                                                          const float* __restrict__ dlogits,
-                                                          bf16* __restrict__ da3, int B,
-                                                          float* __restrict__ slabs, int nslices) {
-  const int kp0 = threadIdx.x * 8;
-  float wr[FC_N][8];
+// ================================================================== F3: pool2 + conv3 + ReLU + pool3 + fc1
+// 256 threads; wave w owns output channels 32w..32w+31 (n-tiles 2w, 2w+1) for all 16 pool windows.
+constexpr int C3_RRS = 64;  // bf16 per LDS row, r2 image (unpadded: filled by glds)
+constexpr int C3_XRS = 72;  // bf16 per LDS row, pooled conv3 input (64 + 8)
+
+__device__ __forceinline__ void pool2_into(const bf16* R, bf16* X, int tid, int nthreads) {
+  for (int it = tid; it < 800; it += nthreads) {
+    const int p = it >> 3, c = (it & 7) * 8;
+    const int py = p / 10, px = p % 10;
+    *reinterpret_cast<bf16x8*>(X + p * C3_XRS + c) = window_max8(R + (py * 11 + px) * C3_RRS + c, C3_RRS, 11);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __restrict__ r2,
+                                                              const bf16* __restrict__ packed,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ bfc,
+                                                              float* __restrict__ logits,
+                                                              bf16* __restrict__ a3,
+                                                              uint8_t* __restrict__ idx3, int B) {
+  __shared__ __attribute__((aligned(16))) bf16 R[121 * C3_RRS];
+  __shared__ __attribute__((aligned(16))) bf16 X[100 * C3_XRS];
+  __shared__ __attribute__((aligned(16))) bf16 Fc[PFC_N];
+  __shared__ float red[4][10];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, q8 = (lane >> 4) * 8;
+  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3F_OFF);
+  bf16x8 bw[2][18];
 #pragma unroll
-  for (int n = 0; n < FC_N; ++n)
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wr[n][j] = w[n * FC_K + fc_wcol(kp0 + j)];
-  float acc[FC_N][8];
+    for (int ks = 0; ks < 18; ++ks) bw[t][ks] = pk[((2 * wave + t) * 18 + ks) * 64 + lane];
+  float bv[2];
 #pragma unroll
-  for (int n = 0; n < FC_N; ++n)
+  for (int t = 0; t < 2; ++t) bv[t] = bias[32 * wave + 16 * t + r16];
+  int base[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) base[mt] = win_pos(4 * (4 * mt + (r16 >> 2)) + (r16 & 3), 10);
+  {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFC_OFF);
+    for (int c = tid; c < PFC_N / 8; c += 256) reinterpret_cast<bf16x8*>(Fc)[c] = src[c];
+  }
+  // r2 image -> R: 968 16-B chunks = 16 wave-instructions (4 per wave), lane-linear
+  auto stage = [&](int bb) {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(r2 + (int64_t)bb * 121 * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int inst = k * 4 + wave, c = inst * 64 + lane;
+      if (c < 968) glds16(src + c, R + inst * 64 * 8);
+    }
+  };
+  int b = blockIdx.x;
+  if (b < B) stage(b);
+  __syncthreads();
+  for (; b < B; b += gridDim.x) {
+    pool2_into(R, X, tid, 256);
+    __syncthreads();  // X complete, R free
+    const int nb = b + gridDim.x;
+    if (nb < B) stage(nb);  // lands while the MFMAs below run
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int tap = ks >> 1, c0 = (ks & 1) * 32;
+      const int shift = (tap / 3) * 10 + tap % 3;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(X + (base[mt] + shift) * C3_XRS + c0 + q8);
+        acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
+        acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
+      }
+    }
+    float s[10];
+#pragma unroll
+    for (int n = 0; n < 10; ++n) s[n] = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int wc = 4 * mt + (lane >> 4), co = 32 * wave + 16 * t + r16;
+        int g;
+        const bf16 pb = (bf16)pool4(acc[mt][t], bv[t], g);
+        const int64_t o = ((int64_t)b * 16 + wc) * 128 + co;
+        a3[o] = pb;
+        idx3[o] = (uint8_t)g;
+        const float pf = (float)pb;
+        const uint32_t* fw = reinterpret_cast<const uint32_t*>(Fc + (wc * 128 + co) * 10);
+#pragma unroll
+        for (int h = 0; h < 5; ++h) {
+          const uint32_t u = fw[h];
+          s[2 * h] = fmaf(pf, __uint_as_float(u << 16), s[2 * h]);
+          s[2 * h + 1] = fmaf(pf, __uint_as_float(u & 0xffff0000u), s[2 * h + 1]);
+        }
+      }
+#pragma unroll
+    for (int n = 0; n < 10; ++n) s[n] = wave_sum(s[n]);
+    if (lane == 0) {
+#pragma unroll
+      for (int n = 0; n < 10; ++n) red[wave][n] = s[n];
+    }
+    __syncthreads();
+    if (tid < 10)
+      logits[(int64_t)b * 10 + tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) + bfc[tid];
+  }
+}
+
+// ================================================================== F3 backward
+// (1) fc1 backward: da3 = dl . Wfc, scattered to window-ordered d(conv3) rows D3[b][4w + i][co]
+//     (one non-zero per window: the argmax, if the pooled value is > 0) + fc weight-grad slabs.
+constexpr int FC_SLAB = 10 * 2048 + 10;
+
+__global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3,
+                                                     const uint8_t* __restrict__ idx3,
+                                                     const float* __restrict__ wfc,
+                                                     const float* __restrict__ dl,
+                                                     bf16* __restrict__ d3, float* __restrict__ slabs,
+                                                     int nslices, int B) {
+  const int t = threadIdx.x;
+  const int wd = t >> 4, co0 = (t & 15) * 8;  // this thread's 8 activations: window wd, channels co0..
+  float wr[10][8];
+#pragma unroll
+  for (int n = 0; n < 10; ++n)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wr[n][j] = wfc[n * 2048 + (co0 + j) * 16 + wd];
+  float acc[10][8];
+#pragma unroll
+  for (int n = 0; n < 10; ++n)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[n][j] = 0.f;
   float bacc = 0.f;
   const int per = cdiv(B, nslices);
   const int b_lo = blockIdx.x * per, b_hi = min(B, b_lo + per);
   for (int b = b_lo; b < b_hi; ++b) {
-    float dl[FC_N];
+    float g[10];
 #pragma unroll
-    for (int n = 0; n < FC_N; ++n) dl[n] = dlogits[(int64_t)b * FC_N + n];
-    const bf16x8 xv = *reinterpret_cast<const bf16x8*>(a3 + (int64_t)b * FC_K + kp0);
-    bf16x8 dv;
+    for (int n = 0; n < 10; ++n) g[n] = dl[(int64_t)b * 10 + n];
+    const int64_t o = (int64_t)b * 2048 + wd * 128 + co0;
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(a3 + o);
+    const uint2 iv = *reinterpret_cast<const uint2*>(idx3 + o);
+    float da[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float s = 0.f;
+      const float aj = (float)av[j];
 #pragma unroll
-      for (int n = 0; n < FC_N; ++n) {
-        s = fmaf(dl[n], wr[n][j], s);
-        acc[n][j] = fmaf(dl[n], (float)xv[j], acc[n][j]);
+      for (int n = 0; n < 10; ++n) {
+        s = fmaf(g[n], wr[n][j], s);
+        acc[n][j] = fmaf(g[n], aj, acc[n][j]);
       }
-      dv[j] = (bf16)s;
+      da[j] = aj > 0.f ? s : 0.f;
     }
-    *reinterpret_cast<bf16x8*>(da3 + (int64_t)b * FC_K + kp0) = dv;
-    if (threadIdx.x < FC_N) bacc += dl[threadIdx.x];
+    bf16* drow = d3 + ((int64_t)b * 64 + 4 * wd) * 128 + co0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)(byte_of(iv, j) == i ? da[j] : 0.f);
+      *reinterpret_cast<bf16x8*>(drow + i * 128) = v;
+    }
+    if (t < 10) bacc += dl[(int64_t)b * 10 + t];
   }
-  float* slab = slabs + (int64_t)blockIdx.x * (FC_N * FC_K + FC_N);
+  float* slab = slabs + (int64_t)blockIdx.x * FC_SLAB;
 #pragma unroll
-  for (int n = 0; n < FC_N; ++n)
+  for (int n = 0; n < 10; ++n)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) slab[n * FC_K + fc_wcol(kp0 + j)] = acc[n][j];
-  if (threadIdx.x < FC_N) slab[FC_N * FC_K + threadIdx.x] = bacc;
+    for (int j = 0; j < 8; ++j) slab[n * 2048 + (co0 + j) * 16 + wd] = acc[n][j];
+  if (t < 10) slab[20480 + t] = bacc;
+}
+
+// (2) conv3 backward, two roles in one 512-thread launch:
+//   dgrad: da2 = full-corr(D3 image, flipped W3) -> pool2 backward (argmax recomputed from r2)
+//          -> dr2 [B,11,11,64];
+//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a2 = pool2(r2).
+constexpr int C3_PW = 12;    // padded d(conv3) image width (8 + 2*2)
+constexpr int C3_PRS = 136;  // bf16 per padded-image row (128 + 8)
+constexpr int C3_DARS = 68;  // floats per da2 row (64 + 4)
+constexpr int C3_DRS = 136;  // bf16 per D3 row in LDS
+constexpr int C3B_P_BYTES = C3_PW * C3_PW * C3_PRS * 2;  // 39168
+constexpr int C3B_R_BYTES = 121 * C3_RRS * 2;            // 15488
+constexpr int C3B_AM_BYTES = 100 * 64;                   // 6400
+constexpr int C3B_DG_LDS = C3B_P_BYTES + C3B_R_BYTES + C3B_AM_BYTES;
+constexpr int C3B_D_BYTES = 64 * C3_DRS * 2;   // 17408
+constexpr int C3B_X_BYTES = 100 * C3_XRS * 2;  // 14400
+constexpr int C3B_WG_LDS = C3B_D_BYTES + C3B_X_BYTES + C3B_R_BYTES;
+constexpr int C3B_LDS = C3B_DG_LDS > C3B_WG_LDS ? C3B_DG_LDS : C3B_WG_LDS;
+constexpr int C3_WSLAB = 576 * 128 + 128;  // dW3t + db3
+static_assert(100 * C3_DARS * 4 <= C3B_P_BYTES, "da2 must fit in the padded-image region");
+
+__device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ r2, const bf16* __restrict__ d3,
+                                 const bf16* __restrict__ packed, bf16* __restrict__ dr2, int B,
+                                 int block, int nblocks) {
+  bf16* P = reinterpret_cast<bf16*>(smem);
+  float* DA = reinterpret_cast<float*>(smem);  // aliases P after the MFMA phase
+  bf16* R = reinterpret_cast<bf16*>(smem + C3B_P_BYTES);
+  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3B_P_BYTES + C3B_R_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nt = wave & 3, mh = wave >> 2;  // n-tile (16 input channels), m-tile parity
+  const int r16 = lane & 15, q8 = (lane >> 4) * 8;
+  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3D_OFF);
+  bf16x8 bw[36];
+#pragma unroll
+  for (int ks = 0; ks < 36; ++ks) bw[ks] = pk[(nt * 36 + ks) * 64 + lane];
+  int base[4];
+  bool valid[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int mt = mh + 2 * k;
+    const int m = mt * 16 + r16;
+    valid[k] = mt < 7 && m < 100;
+    const int mm = valid[k] ? m : 0;
+    base[k] = (mm / 10) * C3_PW + mm % 10;
+  }
+  const int nk = mh ? 3 : 4;
+  for (int b = block; b < B; b += nblocks) {
+    __syncthreads();
+    // zero the whole padded image (its ring was overwritten by DA), stage r2
+    for (int c = tid; c < C3_PW * C3_PW * C3_PRS / 8; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
+    stage_rows(r2 + (int64_t)b * 121 * 64, R, 968, 8, C3_RRS, tid, 512);
+    __syncthreads();
+    {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(d3 + (int64_t)b * 64 * 128);
+      for (int c = tid; c < 1024; c += 512) {
+        const int r = c >> 4, cc = (c & 15) * 8;
+        *reinterpret_cast<bf16x8*>(P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS + cc) = src[c];
+      }
+    }
+    // pool2 argmax per window (first max), from the r2 image
+    for (int it = tid; it < 800; it += 512) {
+      const int p = it >> 3, c = (it & 7) * 8;
+      const int py = p / 10, px = p % 10;
+      const bf16* r0 = R + (py * 11 + px) * C3_RRS + c;
+      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(r0);
+      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(r0 + C3_RRS);
+      const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(r0 + 11 * C3_RRS);
+      const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(r0 + 12 * C3_RRS);
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float bm = (float)v0[j];
+        uint32_t g = 0;
+        if ((float)v1[j] > bm) {
+          bm = (float)v1[j];
+          g = 1;
+        }
+        if ((float)v2[j] > bm) {
+          bm = (float)v2[j];
+          g = 2;
+        }
+        if ((float)v3[j] > bm) g = 3;
+        if (j < 4)
+          lo |= g << (8 * j);
+        else
+          hi |= g << (8 * (j - 4));
+      }
+      *reinterpret_cast<uint2*>(AM + p * 64 + c) = make_uint2(lo, hi);
+    }
+    __syncthreads();
+    f32x4 acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = zero_f32x4();
+#pragma unroll 4
+    for (int ks = 0; ks < 36; ++ks) {
+      const int tapp = ks >> 2, c0 = (ks & 3) * 32;
+      const int shift = (tapp / 3) * C3_PW + tapp % 3;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < nk) {
+          bf16x8 a = zero_bf16x8();
+          if (valid[k]) a = *reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C3_PRS + c0 + q8);
+          acc[k] = mfma16x16x32(a, bw[ks], acc[k]);
+        }
+      }
+    }
+    __syncthreads();  // P dead -> DA
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int mt = mh + 2 * k;
+      if (k < nk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mt * 16 + (lane >> 4) * 4 + i;
+          if (m < 100) DA[m * C3_DARS + nt * 16 + r16] = acc[k][i];
+        }
+      }
+    }
+    __syncthreads();
+    // pool2 backward (gather): dr2[y][x] = sum of da2 over the windows whose argmax is (y, x)
+    bf16x8* dst = reinterpret_cast<bf16x8*>(dr2 + (int64_t)b * 121 * 64);
+    for (int it = tid; it < 968; it += 512) {
+      const int pos = it >> 3, c = (it & 7) * 8;
+      const int y = pos / 11, x = pos % 11;
+      float g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = 0.f;
+      for (int py = max(0, y - 1); py <= min(9, y); ++py)
+        for (int px = max(0, x - 1); px <= min(9, x); ++px) {
+          const int want = (y - py) * 2 + (x - px);
+          const int p = py * 10 + px;
+          const uint2 am = *reinterpret_cast<const uint2*>(AM + p * 64 + c);
+          const float4 d0 = *reinterpret_cast<const float4*>(DA + p * C3_DARS + c);
+          const float4 d1 = *reinterpret_cast<const float4*>(DA + p * C3_DARS + c + 4);
+          const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (byte_of(am, j) == want) g[j] += dv[j];
+        }
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)g[j];
+      dst[it] = v;
+    }
+  }
+}
+
+__device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ r2, const bf16* __restrict__ d3,
+                                 float* __restrict__ slabs, int B, int nslices, int slice) {
+  bf16* D = reinterpret_cast<bf16*>(smem);
+  bf16* X = reinterpret_cast<bf16*>(smem + C3B_D_BYTES);
+  bf16* R = reinterpret_cast<bf16*>(smem + C3B_D_BYTES + C3B_X_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;  // m-tiles 4wm..4wm+3 (co), n-tiles 9wn..9wn+8
+  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = zero_f32x4();
+  float bacc = 0.f;
+  const int per = cdiv(B, nslices);
+  const int b_lo = slice * per, b_hi = min(B, b_lo + per);
+  for (int b = b_lo; b < b_hi; ++b) {
+    __syncthreads();
+    stage_rows(d3 + (int64_t)b * 64 * 128, D, 1024, 16, C3_DRS, tid, 512);
+    stage_rows(r2 + (int64_t)b * 121 * 64, R, 968, 8, C3_RRS, tid, 512);
+    __syncthreads();
+    pool2_into(R, X, tid, 512);
+    if (tid < 128) {
+      float s = 0.f;
+      for (int r = 0; r < 64; ++r) s += (float)D[r * C3_DRS + tid];
+      bacc += s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kb = ks * 32 + grp * 8;
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m0 = (4 * wm + i) * 16;
+        const bf16x4 lo = lds_read_tr16(D + (kb + q) * C3_DRS + m0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(D + (kb + 4 + q) * C3_DRS + m0 + 4 * p);
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int x0 = win_pos(kb + q, 10), x1 = win_pos(kb + 4 + q, 10);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int n0 = (9 * wn + j) * 16;  // n = tap*64 + ci
+        const int tap = n0 >> 6, c0 = n0 & 63;
+        const int shift = (tap / 3) * 10 + tap % 3;
+        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3_XRS + c0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C3_XRS + c0 + 4 * p);
+        const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16x16x32(af[i], bf, acc[i][j]);
+      }
+    }
+  }
+  float* slab = slabs + (int64_t)slice * C3_WSLAB;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int co = (4 * wm + i) * 16 + grp * 4;
+      const int n = (9 * wn + j) * 16 + g16;
+      *reinterpret_cast<f32x4*>(slab + (int64_t)n * 128 + co) = acc[i][j];
+    }
+  if (tid < 128) slab[576 * 128 + tid] = bacc;
+}
+
+__global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__ r2,
+                                                        const bf16* __restrict__ d3,
+                                                        const bf16* __restrict__ packed,
+                                                        bf16* __restrict__ dr2, int B,
+                                                        float* __restrict__ slabs, int nslices,
+                                                        int n_dgrad) {
+  __shared__ __attribute__((aligned(16))) char smem[C3B_LDS];
+  if ((int)blockIdx.x < n_dgrad)
+    conv3_dgrad_role(smem, r2, d3, packed, dr2, B, blockIdx.x, n_dgrad);
+  else
+    conv3_wgrad_role(smem, r2, d3, slabs, B, nslices, blockIdx.x - n_dgrad);
+}
+
+// ================================================================== F2 backward
+// dconv2 = dr2 * (r2 > 0) (ReLU mask); roles:
+//   dgrad: da1 = full-corr(dconv2 image, flipped W2)  [13x13x32]
+//   wgrad: dW2t[n = tap*32 + ci][co] = sum_pos dconv2[pos][co] * a1[pos + tap][ci]
+constexpr int C2_PW = 15, C2_PRS = 72, C2_ORS = 40, C2_DRS = 72;
+constexpr int C2B_P_BYTES = C2_PW * C2_PW * C2_PRS * 2;  // 32400
+constexpr int C2B_O_BYTES = 169 * C2_ORS * 2;            // 13520
+constexpr int C2B_D_BYTES = 128 * C2_DRS * 2;            // 18432
+constexpr int C2B_X_BYTES = 169 * C2_XRS * 2;            // 13520
+constexpr int C2B_LDS = (C2B_P_BYTES + C2B_O_BYTES) > (C2B_D_BYTES + C2B_X_BYTES)
+                            ? (C2B_P_BYTES + C2B_O_BYTES)
+                            : (C2B_D_BYTES + C2B_X_BYTES);
+constexpr int C2_WSLAB = 288 * 64 + 64;
+
+__device__ __forceinline__ bf16x8 relu_mask8(const bf16x8& g, const bf16x8& r) {
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)r[j] > 0.f ? g[j] : (bf16)0.f;
+  return v;
+}
+
+__device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ r2, const bf16* __restrict__ dr2,
+                                 const bf16* __restrict__ packed, bf16* __restrict__ da1, int B,
+                                 int block, int nblocks) {
+  bf16* P = reinterpret_cast<bf16*>(smem);
+  bf16* O = reinterpret_cast<bf16*>(smem + C2B_P_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nt = wave & 1, mg = wave >> 1;  // n-tile (16 input channels), m-tiles mg, mg+4, mg+8
+  const int r16 = lane & 15, q8 = (lane >> 4) * 8;
+  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P2D_OFF);
+  bf16x8 bw[18];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) bw[ks] = pk[(nt * 18 + ks) * 64 + lane];
+  int base[3];
+  bool valid[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int mt = mg + 4 * k;
+    const int m = mt * 16 + r16;
+    valid[k] = mt < 11 && m < 169;
+    const int mm = valid[k] ? m : 0;
+    base[k] = (mm / 13) * C2_PW + mm % 13;
+  }
+  const int nk = mg == 3 ? 2 : 3;
+  for (int c = tid; c < C2_PW * C2_PW * C2_PRS / 8; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
+  for (int b = block; b < B; b += nblocks) {
+    __syncthreads();
+    {
+      const bf16x8* g = reinterpret_cast<const bf16x8*>(dr2 + (int64_t)b * 121 * 64);
+      const bf16x8* r = reinterpret_cast<const bf16x8*>(r2 + (int64_t)b * 121 * 64);
+      for (int c = tid; c < 968; c += 512) {
+        const int pos = c >> 3, cc = (c & 7) * 8;
+        const int y = pos / 11, x = pos % 11;
+        *reinterpret_cast<bf16x8*>(P + ((y + 2) * C2_PW + x + 2) * C2_PRS + cc) = relu_mask8(g[c], r[c]);
+      }
+    }
+    __syncthreads();
+    f32x4 acc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) acc[k] = zero_f32x4();
+#pragma unroll 2
+    for (int ks = 0; ks < 18; ++ks) {
+      const int tapp = ks >> 1, c0 = (ks & 1) * 32;
+      const int shift = (tapp / 3) * C2_PW + tapp % 3;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        if (k < nk) {
+          bf16x8 a = zero_bf16x8();
+          if (valid[k]) a = *reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C2_PRS + c0 + q8);
+          acc[k] = mfma16x16x32(a, bw[ks], acc[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int mt = mg + 4 * k;
+      if (k < nk) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = mt * 16 + (lane >> 4) * 4 + i;
+          if (m < 169) O[m * C2_ORS + nt * 16 + r16] = (bf16)acc[k][i];
+        }
+      }
+    }
+    __syncthreads();
+    bf16x8* dst = reinterpret_cast<bf16x8*>(da1 + (int64_t)b * 169 * 32);
+    for (int c = tid; c < 676; c += 512) dst[c] = *reinterpret_cast<const bf16x8*>(O + (c >> 2) * C2_ORS + (c & 3) * 8);
+  }
+}
+
+__device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ r2,
+                                 const bf16* __restrict__ dr2, float* __restrict__ slabs, int B,
+                                 int nslices, int slice) {
+  bf16* D = reinterpret_cast<bf16*>(smem);
+  bf16* X = reinterpret_cast<bf16*>(smem + C2B_D_BYTES);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // m-tile wm (co 16wm..), n-tiles 9wn..9wn+8
+  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
+  f32x4 acc[9];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) acc[j] = zero_f32x4();
+  float bacc = 0.f;
+  for (int c = tid; c < 128 * C2_DRS / 8; c += 512) reinterpret_cast<bf16x8*>(D)[c] = zero_bf16x8();
+  const int per = cdiv(B, nslices);
+  const int b_lo = slice * per, b_hi = min(B, b_lo + per);
+  for (int b = b_lo; b < b_hi; ++b) {
+    __syncthreads();
+    {
+      const bf16x8* g = reinterpret_cast<const bf16x8*>(dr2 + (int64_t)b * 121 * 64);
+      const bf16x8* r = reinterpret_cast<const bf16x8*>(r2 + (int64_t)b * 121 * 64);
+      for (int c = tid; c < 968; c += 512)
+        *reinterpret_cast<bf16x8*>(D + (c >> 3) * C2_DRS + (c & 7) * 8) = relu_mask8(g[c], r[c]);
+    }
+    stage_rows(a1 + (int64_t)b * 169 * 32, X, 676, 4, C2_XRS, tid, 512);
+    __syncthreads();
+    if (tid < 64) {
+      float s = 0.f;
+      for (int r = 0; r < 121; ++r) s += (float)D[r * C2_DRS + tid];
+      bacc += s;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kb = ks * 32 + grp * 8;
+      const int m0 = wm * 16;
+      const bf16x4 alo = lds_read_tr16(D + (kb + q) * C2_DRS + m0 + 4 * p);
+      const bf16x4 ahi = lds_read_tr16(D + (kb + 4 + q) * C2_DRS + m0 + 4 * p);
+      const bf16x8 af = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+      const int k0 = min(kb + q, 120), k1 = min(kb + 4 + q, 120);  // rows >= 121 of D are zero
+      const int x0 = (k0 / 11) * 13 + k0 % 11, x1 = (k1 / 11) * 13 + k1 % 11;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int n0 = (9 * wn + j) * 16;  // n = tap*32 + ci
+        const int tap = n0 >> 5, c0 = n0 & 31;
+        const int shift = (tap / 3) * 13 + tap % 3;
+        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C2_XRS + c0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C2_XRS + c0 + 4 * p);
+        const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[j] = mfma16x16x32(af, bf, acc[j]);
+      }
+    }
+  }
+  float* slab = slabs + (int64_t)slice * C2_WSLAB;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int co = wm * 16 + grp * 4;
+    const int n = (9 * wn + j) * 16 + g16;
+    *reinterpret_cast<f32x4*>(slab + (int64_t)n * 64 + co) = acc[j];
+  }
+  if (tid < 64) slab[288 * 64 + tid] = bacc;
+}
+
+__global__ __launch_bounds__(512) void conv2_bwd_kernel(const bf16* __restrict__ a1,
+                                                        const bf16* __restrict__ r2,
+                                                        const bf16* __restrict__ dr2,
+                                                        const bf16* __restrict__ packed,
+                                                        bf16* __restrict__ da1, int B,
+                                                        float* __restrict__ slabs, int nslices,
+                                                        int n_dgrad) {
+  __shared__ __attribute__((aligned(16))) char smem[C2B_LDS];
+  if ((int)blockIdx.x < n_dgrad)
+    conv2_dgrad_role(smem, r2, dr2, packed, da1, B, blockIdx.x, n_dgrad);
+  else
+    conv2_wgrad_role(smem, a1, r2, dr2, slabs, B, nslices, blockIdx.x - n_dgrad);
+}
+
+// ================================================================== F1 backward (conv1 wgrad)
+// dW1[co][t] = sum_{b, k} Dc[b][k][co] * xpad[b][pos(k) + (kh, kw)], K rows in window order
+// (k = 4w + i: one non-zero row per window and channel - the argmax, if the pooled value > 0).
+constexpr int C1W_K = 704;          // 676 rows padded to 22 k-steps
+constexpr int C1W_DRS = C1W_K + 8;  // bf16 per co row of the transposed d(conv1)
+constexpr int C1_WSLAB = 32 * 25 + 32;
+
+template <bool U8>
+__global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict__ xin,
+                                                          const bf16* __restrict__ da1,
+                                                          const uint8_t* __restrict__ idx1,
+                                                          const bf16* __restrict__ a1, int B,
+                                                          float mean, float inv_std, float in_scale,
+                                                          float* __restrict__ slabs, int nslices) {
+  __shared__ __attribute__((aligned(16))) bf16 Dt[32 * C1W_DRS];
+  __shared__ __attribute__((aligned(16))) bf16 xs[C1_XS];
+  __shared__ float bred[32][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int mt = wave >> 1, nt = wave & 1;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int t = nt * 16 + r16;
+  const bool tvalid = t < 25;
+  const int toff = tvalid ? (t / 5) * 30 + t % 5 : 0;
+  f32x4 acc = zero_f32x4();
+  float bpart[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bpart[j] = 0.f;
+  for (int i = tid; i < 32 * C1W_DRS / 8; i += 256) reinterpret_cast<bf16x8*>(Dt)[i] = zero_bf16x8();
+  for (int i = tid; i < C1_XS; i += 256) xs[i] = (bf16)0.f;
+  const int per = cdiv(B, nslices);
+  const int b_lo = blockIdx.x * per, b_hi = min(B, b_lo + per);
+  const int c0 = (tid & 3) * 8;  // fixed channel chunk of this thread in the staging loop
+  for (int b = b_lo; b < b_hi; ++b) {
+    __syncthreads();
+    uint32_t u = 0;
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    c1_load<U8>(xin, b, tid, u, f);
+    c1_store<U8>(xs, tid, u, f, mean, inv_std, in_scale);
+    for (int it = tid; it < 676; it += 256) {
+      const int w = it >> 2;
+      const int64_t o = ((int64_t)b * 169 + w) * 32 + c0;
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(da1 + o);
+      const bf16x8 pv = *reinterpret_cast<const bf16x8*>(a1 + o);
+      const uint2 iv = *reinterpret_cast<const uint2*>(idx1 + o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bf16 gb = (float)pv[j] > 0.f ? g[j] : (bf16)0.f;
+        bpart[j] += (float)gb;
+        const int ij = byte_of(iv, j);
+        bf16x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = i == ij ? gb : (bf16)0.f;
+        *reinterpret_cast<bf16x4*>(Dt + (c0 + j) * C1W_DRS + 4 * w) = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int ks = 0; ks < 22; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Dt + (mt * 16 + r16) * C1W_DRS + ks * 32 + q * 8);
+      bf16x8 bf = zero_bf16x8();
+      if (tvalid) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = min(ks * 32 + q * 8 + j, 675);  // Dt columns >= 676 are zero
+          const int w = k >> 2, i = k & 3;
+          bf[j] = xs[(2 * (w / 13) + (i >> 1)) * 30 + 2 * (w % 13) + (i & 1) + toff];
+        }
+      }
+      acc = mfma16x16x32(af, bf, acc);
+    }
+  }
+  // bias: the 16 lanes of a wave with the same channel chunk (lane & 3) reduce by shuffles,
+  // then the 4 waves through LDS (fixed order)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = bpart[j];
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (lane < 4) bred[c0 + j][wave] = v;
+  }
+  __syncthreads();
+  float* slab = slabs + (int64_t)blockIdx.x * C1_WSLAB;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = mt * 16 + q * 4 + i;
+    if (tvalid) slab[co * 25 + t] = acc[i];
+  }
+  if (tid < 32) slab[800 + tid] = (bred[tid][0] + bred[tid][1]) + (bred[tid][2] + bred[tid][3]);
+}
+
+// ================================================================== fixed-order slab reductions
+struct ReduceSeg {
+  const float* slabs;
+  int64_t stride;  // floats between consecutive slices
+  int64_t off;     // first float of this segment inside a slice
+  int64_t n;       // outputs
+  int nslices;
+  float* out;
+  int mode;  // 0: out[i] = sum; 1: conv transpose dWt[n = tap*cin + ci][co] -> W[co][ci][tap]
+  int cin, cout;
+  int blocks;
+};
+struct ReduceSegs {
+  ReduceSeg seg[4];
+  int count;
+};
+
+// Each workgroup owns 64 outputs of one segment and sums its slices with 4 waves (lane = output,
+// coalesced rows) combined in a fixed order.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(ReduceSegs segs) {
+  __shared__ float part[4][64];
+  int blk = blockIdx.x, sidx = 0;
+  while (sidx < segs.count - 1 && blk >= segs.seg[sidx].blocks) {
+    blk -= segs.seg[sidx].blocks;
+    ++sidx;
+  }
+  const ReduceSeg& sg = segs.seg[sidx];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blk * 64 + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (i < sg.n) {
+    const float* pp = sg.slabs + sg.off + i;
+    int s = wave;
+    for (; s + 12 < sg.nslices; s += 16) {
+      a0 += pp[(int64_t)s * sg.stride];
+      a1 += pp[(int64_t)(s + 4) * sg.stride];
+      a2 += pp[(int64_t)(s + 8) * sg.stride];
+      a3 += pp[(int64_t)(s + 12) * sg.stride];
+    }
+    for (; s < sg.nslices; s += 4) a0 += pp[(int64_t)s * sg.stride];
+  }
+  part[wave][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wave != 0 || i >= sg.n) return;
+  const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (sg.mode == 0) {
+    sg.out[i] = v;
+  } else {
+    const int n = (int)(i / sg.cout), co = (int)(i % sg.cout);
+    sg.out[((int64_t)co * sg.cin + n % sg.cin) * 9 + n / sg.cin] = v;
+  }
+}
+
+ReduceSeg seg(const float* slabs, int64_t stride, int64_t off, int64_t n, int nslices, float* out,
+              int mode = 0, int cin = 0, int cout = 0) {
+  return ReduceSeg{slabs, stride, off, n, nslices, out, mode, cin, cout, (int)((n + 63) / 64)};
+}
+
+void launch_reduce(const std::vector<ReduceSeg>& v, hipStream_t s) {
+  ReduceSegs segs{};
+  int total = 0;
+  segs.count = (int)v.size();
+  for (size_t k = 0; k < v.size(); ++k) {
+    segs.seg[k] = v[k];
+    total += v[k].blocks;
+  }
+  slab_reduce_kernel<<<total, 256, 0, s>>>(segs);
 }
 
 int num_cus() {
@@ -810,176 +1060,89 @@ int num_cus() {
 
 inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Number of weight-gradient slices (images split across workgroups).
-inline int wgrad_slices(int B, int images_per_slice_min, int cap) {
-  return clampi(cdiv(B, images_per_slice_min), 1, cap);
-}
-
 }  // namespace
-
-namespace {
-// Deterministic split-K reduction, parallel over slices: a workgroup owns 64 consecutive outputs;
-// its 4 waves each sum a quarter of the slices (lane = output, fully coalesced 256-B rows), 4-way
-// unrolled for memory-level parallelism; the 4 partials are combined in a fixed order in LDS.
-// out[i] = sum_s slabs[s * stride + off + i],  i < n.
-__global__ __launch_bounds__(kThreads) void strided_reduce_kernel(const float* __restrict__ slabs,
-                                                                  int S, int64_t stride,
-                                                                  int64_t off, int64_t n,
-                                                                  float* __restrict__ out) {
-  __shared__ float part[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (i < n) {
-    const float* p = slabs + off + i;
-    int s = wave;
-    for (; s + 12 < S; s += 16) {
-      a0 += p[(int64_t)s * stride];
-      a1 += p[(int64_t)(s + 4) * stride];
-      a2 += p[(int64_t)(s + 8) * stride];
-      a3 += p[(int64_t)(s + 12) * stride];
-    }
-    for (; s < S; s += 4) a0 += p[(int64_t)s * stride];
-  }
-  part[wave][lane] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (wave == 0 && i < n) out[i] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
-}
-}  // namespace
-
-void strided_reduce(const float* slabs, int S, int64_t stride, int64_t off, int64_t n, float* out,
-                    hipStream_t s) {
-  const int grid = (int)((n + 63) / 64);
-  strided_reduce_kernel<<<grid, kThreads, 0, s>>>(slabs, S, stride, off, n, out);
-}
 
 // ================================================================== launchers
-void convnet_conv1_fwd(const void* x, bool x_is_u8, const float* w, const float* b, void* a1,
-                       uint8_t* idx1, int B, float mean, float inv_std, float in_scale,
-                       hipStream_t s) {
-  const int grid = clampi(B, 1, 8 * num_cus());
-  if (x_is_u8)
-    conv1_fwd_kernel<true><<<grid, kThreads, 0, s>>>(x, w, b, static_cast<bf16*>(a1), idx1, B, mean,
-                                                     inv_std, in_scale);
+int64_t cn_packed_elems() { return PACK_TOTAL; }
+
+void cn_pack_weights(const float* w1, const float* w2, const float* w3, const float* wfc, void* out,
+                     hipStream_t s) {
+  pack_weights_kernel<<<cdiv(PACK_TOTAL, 256), 256, 0, s>>>(w1, w2, w3, wfc, static_cast<bf16*>(out));
+}
+
+void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
+                  int B, float mean, float inv_std, float in_scale, hipStream_t s) {
+  const int grid = clampi(B, 1, 4 * num_cus());
+  const bf16* pk = static_cast<const bf16*>(packed);
+  if (u8)
+    conv1_fwd_kernel<true><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
   else
-    conv1_fwd_kernel<false><<<grid, kThreads, 0, s>>>(x, w, b, static_cast<bf16*>(a1), idx1, B, mean,
-                                                      inv_std, in_scale);
+    conv1_fwd_kernel<false><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
 }
 
-int64_t convnet_conv1_wgrad_slab_floats(int B, int* nslices) {
-  const int S = wgrad_slices(B, 4, 2 * num_cus());
-  if (nslices) *nslices = S;
-  return (int64_t)S * C1_SL;
+void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* r2, int B, hipStream_t s) {
+  const int grid = clampi(B, 1, 2 * num_cus());
+  conv2_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(packed), b2,
+                                        static_cast<bf16*>(r2), B);
 }
 
-void convnet_conv1_wgrad(const void* x, bool x_is_u8, const void* da1, const uint8_t* idx1,
-                         const void* a1, int B, float mean, float inv_std, float in_scale,
-                         float* slabs, int nslices, float* dw, float* db, hipStream_t s) {
-  if (x_is_u8)
-    conv1_wgrad_kernel<true><<<nslices, kThreads, 0, s>>>(x, static_cast<const bf16*>(da1), idx1,
-                                                          static_cast<const bf16*>(a1), B, mean,
-                                                          inv_std, in_scale, slabs, nslices);
-  else
-    conv1_wgrad_kernel<false><<<nslices, kThreads, 0, s>>>(x, static_cast<const bf16*>(da1), idx1,
-                                                           static_cast<const bf16*>(a1), B, mean,
-                                                           inv_std, in_scale, slabs, nslices);
-  // Slab order == PyTorch [co][1][kh][kw], bias follows: two strided fixed-order reductions.
-  strided_reduce(slabs, nslices, C1_SL, 0, C1_NOUT, dw, s);
-  strided_reduce(slabs, nslices, C1_SL, C1_NOUT, 32, db, s);
+void cn_conv3_fc_fwd(const void* r2, const void* packed, const float* b3, const float* bfc, float* logits,
+                     void* a3, uint8_t* idx3, int B, hipStream_t s) {
+  const int grid = clampi(B, 1, 2 * num_cus());
+  conv3_fc_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(r2), static_cast<const bf16*>(packed), b3,
+                                           bfc, logits, static_cast<bf16*>(a3), idx3, B);
 }
 
-namespace {
-template <int L>
-inline int fwd_nsplit(int B) {
-  if (L == 2) return B >= 2048 ? 1 : (B >= 512 ? 2 : 4);
-  return B >= 1024 ? 2 : 4;
-}
-template <int L, int NS>
-void launch_fwd(const void* in, const float* w, const float* b, void* out, uint8_t* idx, int B,
-                hipStream_t s) {
-  const int groups = clampi(B, 1, cdiv(4 * num_cus(), NS));
-  conv_fwd_kernel<L, NS><<<groups * NS, kThreads, 0, s>>>(static_cast<const bf16*>(in), w, b,
-                                                          static_cast<bf16*>(out), idx, B);
-}
-template <int L>
-constexpr int bwd_nsplit() {
-  return L == 2 ? 2 : 4;
-}
-}  // namespace
+static int fc_slices(int B) { return clampi(cdiv(B, 4), 1, 128); }
+static int conv3_wslices(int B) { return clampi(cdiv(B, 8), 1, num_cus()); }
+static int conv2_wslices(int B) { return clampi(cdiv(B, 8), 1, num_cus()); }
+static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 2 * num_cus()); }
+int64_t cn_fc_slab_floats(int B) { return (int64_t)fc_slices(B) * FC_SLAB; }
+int64_t cn_conv3_slab_floats(int B) { return (int64_t)conv3_wslices(B) * C3_WSLAB; }
+int64_t cn_conv2_slab_floats(int B) { return (int64_t)conv2_wslices(B) * C2_WSLAB; }
+int64_t cn_conv1_slab_floats(int B) { return (int64_t)conv1_wslices(B) * C1_WSLAB; }
 
-void convnet_conv_fwd(int layer, const void* in, const float* w, const float* b, void* out,
-                      uint8_t* idx, int B, hipStream_t s) {
-  if (layer == 2) {
-    const int ns = fwd_nsplit<2>(B);
-    if (ns == 1) launch_fwd<2, 1>(in, w, b, out, idx, B, s);
-    else if (ns == 2) launch_fwd<2, 2>(in, w, b, out, idx, B, s);
-    else launch_fwd<2, 4>(in, w, b, out, idx, B, s);
-  } else {
-    const int ns = fwd_nsplit<3>(B);
-    if (ns == 2) launch_fwd<3, 2>(in, w, b, out, idx, B, s);
-    else launch_fwd<3, 4>(in, w, b, out, idx, B, s);
-  }
+void cn_conv3_fc_bwd(const void* r2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
+                     const void* packed, void* d3, void* dr2, int B, float* fc_slabs, float* c3_slabs,
+                     float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s) {
+  const int fs = fc_slices(B);
+  fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), idx3, wfc, dl, static_cast<bf16*>(d3),
+                                   fc_slabs, fs, B);
+  const int ws = conv3_wslices(B);
+  const int nd = dr2 ? clampi(B, 1, num_cus()) : 0;
+  conv3_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(r2), static_cast<const bf16*>(d3),
+                                           static_cast<const bf16*>(packed), static_cast<bf16*>(dr2), B,
+                                           c3_slabs, ws, nd);
+  launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
+                 seg(c3_slabs, C3_WSLAB, 576 * 128, 128, ws, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc),
+                 seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},
+                s);
 }
 
-int64_t convnet_conv_wgrad_slab_floats(int layer, int B, int* nslices) {
-  int S;
-  int64_t per;
-  if (layer == 2) {
-    S = wgrad_slices(B, 2, 2 * num_cus());
-    per = WgradGeo<2>::NOUT + Geo<2>::COUT;
-  } else {
-    S = wgrad_slices(B, 4, (2 * num_cus()) / WgradGeo<3>::NGROUPS);
-    per = WgradGeo<3>::NOUT + Geo<3>::COUT;
-  }
-  if (nslices) *nslices = S;
-  return (int64_t)S * per;
+void cn_conv2_bwd(const void* a1, const void* r2, const void* dr2, const void* packed, void* da1, int B,
+                  float* slabs, float* dw2, float* db2, hipStream_t s) {
+  const int ws = conv2_wslices(B);
+  const int nd = da1 ? clampi(B, 1, num_cus()) : 0;
+  conv2_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(r2),
+                                           static_cast<const bf16*>(dr2), static_cast<const bf16*>(packed),
+                                           static_cast<bf16*>(da1), B, slabs, ws, nd);
+  launch_reduce({seg(slabs, C2_WSLAB, 0, 288 * 64, ws, dw2, 1, 32, 64), seg(slabs, C2_WSLAB, 288 * 64, 64, ws, db2)},
+                s);
 }
 
-void convnet_conv_bwd(int layer, const void* in, const float* w, const void* dout,
-                      const uint8_t* idx, const void* out, void* din, int B, float* slabs,
-                      int nslices, float* dw, float* db, hipStream_t s) {
-  const bf16* inb = static_cast<const bf16*>(in);
-  const bf16* doutb = static_cast<const bf16*>(dout);
-  const bf16* outb = static_cast<const bf16*>(out);
-  bf16* dinb = static_cast<bf16*>(din);
-  if (layer == 2) {
-    constexpr int NS = bwd_nsplit<2>();
-    const int n_dgrad = din ? clampi(B, 1, cdiv(4 * num_cus(), NS)) * NS : 0;
-    const int n_w = nslices * WgradGeo<2>::NGROUPS;
-    conv_bwd_kernel<2, NS><<<n_dgrad + n_w, kThreads, 0, s>>>(inb, w, doutb, idx, outb, dinb, B,
-                                                             slabs, nslices, n_dgrad);
-    constexpr int SL = WgradGeo<2>::NOUT + Geo<2>::COUT;
-    conv_wgrad_reduce_kernel<2><<<cdiv(SL, 64), kThreads, 0, s>>>(slabs, nslices, dw, db);
-  } else {
-    constexpr int NS = bwd_nsplit<3>();
-    const int n_dgrad = din ? clampi(B, 1, cdiv(4 * num_cus(), NS)) * NS : 0;
-    const int n_w = nslices * WgradGeo<3>::NGROUPS;
-    conv_bwd_kernel<3, NS><<<n_dgrad + n_w, kThreads, 0, s>>>(inb, w, doutb, idx, outb, dinb, B,
-                                                             slabs, nslices, n_dgrad);
-    constexpr int SL = WgradGeo<3>::NOUT + Geo<3>::COUT;
-    conv_wgrad_reduce_kernel<3><<<cdiv(SL, 64), kThreads, 0, s>>>(slabs, nslices, dw, db);
-  }
-}
-
-void convnet_fc_fwd(const void* a3, const float* w, const float* b, float* logits, int B,
+void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, const void* a1, int B,
+                    float mean, float inv_std, float in_scale, float* slabs, float* dw1, float* db1,
                     hipStream_t s) {
-  const int grid = clampi(cdiv(B, 4), 1, num_cus());
-  fc_fwd_kernel<<<grid, kThreads, 0, s>>>(static_cast<const bf16*>(a3), w, b, logits, B);
-}
-
-int64_t convnet_fc_slab_floats(int B, int* nslices) {
-  const int S = wgrad_slices(B, 8, 128);
-  if (nslices) *nslices = S;
-  return (int64_t)S * (FC_N * FC_K + FC_N);
-}
-
-void convnet_fc_bwd(const void* a3, const float* w, const float* dlogits, void* da3, int B,
-                    float* slabs, int nslices, float* dw, float* db, hipStream_t s) {
-  fc_bwd_kernel<<<nslices, kThreads, 0, s>>>(static_cast<const bf16*>(a3), w, dlogits,
-                                             static_cast<bf16*>(da3), B, slabs, nslices);
-  constexpr int SL = FC_N * FC_K + FC_N;
-  strided_reduce(slabs, nslices, SL, 0, FC_N * FC_K, dw, s);
-  strided_reduce(slabs, nslices, SL, FC_N * FC_K, FC_N, db, s);
+  const int ws = conv1_wslices(B);
+  if (u8)
+    conv1_wgrad_kernel<true><<<ws, 256, 0, s>>>(x, static_cast<const bf16*>(da1), idx1,
+                                                static_cast<const bf16*>(a1), B, mean, inv_std, in_scale,
+                                                slabs, ws);
+  else
+    conv1_wgrad_kernel<false><<<ws, 256, 0, s>>>(x, static_cast<const bf16*>(da1), idx1,
+                                                 static_cast<const bf16*>(a1), B, mean, inv_std, in_scale,
+                                                 slabs, ws);
+  launch_reduce({seg(slabs, C1_WSLAB, 0, 800, ws, dw1), seg(slabs, C1_WSLAB, 800, 32, ws, db1)}, s);
 }
 
 }  // namespace kern

@@ -52,34 +52,35 @@ void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* 
                        float label_smoothing, int reduction, float* dlogits, hipStream_t s);
 
 // ---------------------------------------------------------------- MNIST ConvNet
-// Activations are NHWC bf16; weights are PyTorch-layout fp32 master weights.
-// conv1 (1->32, k5, pad1) + ReLU + MaxPool(2,2): x [B,28,28] (u8 or f32) -> a1 [B,13,13,32].
-void convnet_conv1_fwd(const void* x, bool x_is_u8, const float* w, const float* b, void* a1,
-                       uint8_t* idx1, int B, float mean, float inv_std, float in_scale,
-                       hipStream_t s);
-// conv1 weight/bias grad from d(a1) (unpool + relu mask via idx1/a1).
-int64_t convnet_conv1_wgrad_slab_floats(int B, int* nslices);
-void convnet_conv1_wgrad(const void* x, bool x_is_u8, const void* da1, const uint8_t* idx1,
-                         const void* a1, int B, float mean, float inv_std, float in_scale,
-                         float* slabs, int nslices, float* dw, float* db, hipStream_t s);
+// Activations are NHWC bf16 (a1 [B,13,13,32], r2 [B,11,11,64], a3 [B,16 windows,128]); weights are
+// PyTorch-layout fp32 masters, packed once per forward into bf16 MFMA fragments.
+int64_t cn_packed_elems();
+void cn_pack_weights(const float* w1, const float* w2, const float* w3, const float* wfc, void* out,
+                     hipStream_t s);
+// F1: conv1 + ReLU + pool1 (x u8 or fp32 [B,28,28]; normalisation fused).
+void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
+                  int B, float mean, float inv_std, float in_scale, hipStream_t s);
+// F2: conv2 + ReLU -> r2.
+void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* r2, int B, hipStream_t s);
+// F3: pool2 + conv3 + ReLU + pool3 + fc1 -> logits (+ a3 / argmax for backward).
+void cn_conv3_fc_fwd(const void* r2, const void* packed, const float* b3, const float* bfc, float* logits,
+                     void* a3, uint8_t* idx3, int B, hipStream_t s);
 
-// layer: 2 -> conv2 (32->64 @13x13, pool k2 s1 -> 10x10), 3 -> conv3 (64->128 @10x10, pool k2 s2
-// -> 4x4).
-void convnet_conv_fwd(int layer, const void* in, const float* w, const float* b, void* out,
-                      uint8_t* idx, int B, hipStream_t s);
-int64_t convnet_conv_wgrad_slab_floats(int layer, int B, int* nslices);
-// Backward of conv+relu+pool: dout = d(pooled output).  Writes din (may be null to skip the
-// data gradient), and dw/db via slabs + reduction.
-void convnet_conv_bwd(int layer, const void* in, const float* w, const void* dout,
-                      const uint8_t* idx, const void* out, void* din, int B, float* slabs,
-                      int nslices, float* dw, float* db, hipStream_t s);
-
-// fc (2048 -> 10) over the NHWC [B,4,4,128] activation; W is PyTorch [10, 2048] (CHW order).
-void convnet_fc_fwd(const void* a3, const float* w, const float* b, float* logits, int B,
+int64_t cn_fc_slab_floats(int B);
+int64_t cn_conv3_slab_floats(int B);
+int64_t cn_conv2_slab_floats(int B);
+int64_t cn_conv1_slab_floats(int B);
+// F3 backward: d3 is a [B,64,128] bf16 workspace; dr2 may be null (skip data grad).
+void cn_conv3_fc_bwd(const void* r2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
+                     const void* packed, void* d3, void* dr2, int B, float* fc_slabs, float* c3_slabs,
+                     float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s);
+// F2 backward: da1 may be null.
+void cn_conv2_bwd(const void* a1, const void* r2, const void* dr2, const void* packed, void* da1, int B,
+                  float* slabs, float* dw2, float* db2, hipStream_t s);
+// F1 backward (weights only: the input needs no gradient).
+void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, const void* a1, int B,
+                    float mean, float inv_std, float in_scale, float* slabs, float* dw1, float* db1,
                     hipStream_t s);
-int64_t convnet_fc_slab_floats(int B, int* nslices);
-void convnet_fc_bwd(const void* a3, const float* w, const float* dlogits, void* da3, int B,
-                    float* slabs, int nslices, float* dw, float* db, hipStream_t s);
 
 // ---------------------------------------------------------------- data
 // Synthetic MNIST-shaped batch (u8 images + labels) from a counter-based hash (deterministic).

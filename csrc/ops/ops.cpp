@@ -246,144 +246,170 @@ void check_input(const at::Tensor& x, int64_t& B, bool& u8) {
 }
 }  // namespace
 
-std::tuple<at::Tensor, at::Tensor> convnet_conv1_fwd(const at::Tensor& x, const at::Tensor& w,
-                                                     const at::Tensor& b, double mean,
-                                                     double std, double in_scale) {
+void check_f32_out(const at::Tensor& t, at::IntArrayRef shape, const char* name) {
+  check_cuda(t, name);
+  check_dtype(t, at::kFloat, name);
+  check_shape(t, shape, name);
+  RINGDP_CHECK(t.is_contiguous(), name, ": must be contiguous");
+}
+
+void check_act(const at::Tensor& t, at::IntArrayRef shape, at::ScalarType d, const char* name) {
+  check_cuda(t, name);
+  check_dtype(t, d, name);
+  check_shape(t, shape, name);
+  RINGDP_CHECK(t.is_contiguous(), name, ": must be contiguous");
+}
+
+void check_packed(const at::Tensor& p) {
+  check_act(p, {kern::cn_packed_elems()}, at::kBFloat16, "packed convnet weights");
+}
+
+at::Tensor cn_pack_weights(const at::Tensor& w1, const at::Tensor& w2, const at::Tensor& w3,
+                           const at::Tensor& wfc) {
+  check_f32_out(w1, {32, 1, 5, 5}, "conv1 weight");
+  check_f32_out(w2, {64, 32, 3, 3}, "conv2 weight");
+  check_f32_out(w3, {128, 64, 3, 3}, "conv3 weight");
+  check_f32_out(wfc, {10, 2048}, "fc1 weight");
+  at::Tensor out = at::empty({kern::cn_packed_elems()}, w1.options().dtype(at::kBFloat16));
+  kern::cn_pack_weights(w1.data_ptr<float>(), w2.data_ptr<float>(), w3.data_ptr<float>(),
+                        wfc.data_ptr<float>(), out.data_ptr(), cur_stream(w1));
+  return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::Tensor& packed,
+                                                const at::Tensor& b1, double mean, double std,
+                                                double in_scale) {
   int64_t B;
   bool u8;
   check_input(x, B, u8);
-  check_cuda(w, "conv1 weight");
-  check_cuda(b, "conv1 bias");
-  check_dtype(w, at::kFloat, "conv1 weight");
-  check_shape(w, {32, 1, 5, 5}, "conv1 weight");
-  check_shape(b, {32}, "conv1 bias");
+  RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
+  check_packed(packed);
+  check_f32_out(b1, {32}, "conv1 bias");
   auto opt = x.options();
   at::Tensor a1 = at::empty({B, 13, 13, 32}, opt.dtype(at::kBFloat16));
   at::Tensor idx = at::empty({B, 13, 13, 32}, opt.dtype(at::kByte));
   if (B == 0) return {a1, idx};
-  kern::convnet_conv1_fwd(x.data_ptr(), u8, w.data_ptr<float>(), b.data_ptr<float>(),
-                          a1.data_ptr(), idx.data_ptr<uint8_t>(), static_cast<int>(B),
-                          static_cast<float>(mean), static_cast<float>(1.0 / std),
-                          static_cast<float>(in_scale), cur_stream(x));
+  kern::cn_conv1_fwd(x.data_ptr(), u8, packed.data_ptr(), b1.data_ptr<float>(), a1.data_ptr(),
+                     idx.data_ptr<uint8_t>(), static_cast<int>(B), static_cast<float>(mean),
+                     static_cast<float>(1.0 / std), static_cast<float>(in_scale), cur_stream(x));
   return {a1, idx};
 }
 
-void convnet_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
-                         const at::Tensor& a1, at::Tensor dw, at::Tensor db, double mean,
-                         double std, double in_scale) {
+at::Tensor cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed, const at::Tensor& b2) {
+  const int64_t B = a1.size(0);
+  check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
+  check_packed(packed);
+  check_f32_out(b2, {64}, "conv2 bias");
+  at::Tensor r2 = at::empty({B, 11, 11, 64}, a1.options());
+  if (B == 0) return r2;
+  kern::cn_conv2_fwd(a1.data_ptr(), packed.data_ptr(), b2.data_ptr<float>(), r2.data_ptr(),
+                     static_cast<int>(B), cur_stream(a1));
+  return r2;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& r2,
+                                                               const at::Tensor& packed,
+                                                               const at::Tensor& b3,
+                                                               const at::Tensor& bfc) {
+  const int64_t B = r2.size(0);
+  check_act(r2, {B, 11, 11, 64}, at::kBFloat16, "conv3 input (relu(conv2))");
+  check_packed(packed);
+  check_f32_out(b3, {128}, "conv3 bias");
+  check_f32_out(bfc, {10}, "fc1 bias");
+  at::Tensor logits = at::empty({B, 10}, r2.options().dtype(at::kFloat));
+  at::Tensor a3 = at::empty({B, 16, 128}, r2.options());
+  at::Tensor idx3 = at::empty({B, 16, 128}, r2.options().dtype(at::kByte));
+  if (B == 0) return {logits, a3, idx3};
+  kern::cn_conv3_fc_fwd(r2.data_ptr(), packed.data_ptr(), b3.data_ptr<float>(), bfc.data_ptr<float>(),
+                        logits.data_ptr<float>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
+                        static_cast<int>(B), cur_stream(r2));
+  return {logits, a3, idx3};
+}
+
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& r2, const at::Tensor& a3, const at::Tensor& idx3,
+                           const at::Tensor& wfc, const at::Tensor& dlogits,
+                           const at::Tensor& packed, bool need_dr2, at::Tensor dw3, at::Tensor db3,
+                           at::Tensor dwfc, at::Tensor dbfc) {
+  const int64_t B = r2.size(0);
+  check_act(r2, {B, 11, 11, 64}, at::kBFloat16, "conv3 input (relu(conv2))");
+  check_act(a3, {B, 16, 128}, at::kBFloat16, "pooled conv3");
+  check_act(idx3, {B, 16, 128}, at::kByte, "conv3 argmax");
+  check_f32_out(wfc, {10, 2048}, "fc1 weight");
+  check_packed(packed);
+  check_f32_out(dw3, {128, 64, 3, 3}, "conv3 dw");
+  check_f32_out(db3, {128}, "conv3 db");
+  check_f32_out(dwfc, {10, 2048}, "fc1 dw");
+  check_f32_out(dbfc, {10}, "fc1 db");
+  check_cuda(dlogits, "logits grad");
+  at::Tensor dl = dlogits.to(at::kFloat).contiguous();
+  check_shape(dl, {B, 10}, "logits grad");
+  at::Tensor dr2;
+  if (need_dr2) dr2 = at::empty_like(r2);
+  if (B == 0) {
+    dw3.zero_();
+    db3.zero_();
+    dwfc.zero_();
+    dbfc.zero_();
+    return dr2;
+  }
+  const int bi = static_cast<int>(B);
+  at::Tensor d3 = at::empty({B, 64, 128}, r2.options());
+  at::Tensor fs = at::empty({kern::cn_fc_slab_floats(bi)}, dw3.options());
+  at::Tensor cs = at::empty({kern::cn_conv3_slab_floats(bi)}, dw3.options());
+  kern::cn_conv3_fc_bwd(r2.data_ptr(), a3.data_ptr(), idx3.data_ptr<uint8_t>(), wfc.data_ptr<float>(),
+                        dl.data_ptr<float>(), packed.data_ptr(), d3.data_ptr(),
+                        need_dr2 ? dr2.data_ptr() : nullptr, bi, fs.data_ptr<float>(),
+                        cs.data_ptr<float>(), dw3.data_ptr<float>(), db3.data_ptr<float>(),
+                        dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), cur_stream(r2));
+  return dr2;
+}
+
+at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& r2, const at::Tensor& dr2,
+                        const at::Tensor& packed, bool need_da1, at::Tensor dw2, at::Tensor db2) {
+  const int64_t B = a1.size(0);
+  check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
+  check_act(r2, {B, 11, 11, 64}, at::kBFloat16, "relu(conv2)");
+  check_act(dr2, {B, 11, 11, 64}, at::kBFloat16, "relu(conv2) grad");
+  check_packed(packed);
+  check_f32_out(dw2, {64, 32, 3, 3}, "conv2 dw");
+  check_f32_out(db2, {64}, "conv2 db");
+  at::Tensor da1;
+  if (need_da1) da1 = at::empty_like(a1);
+  if (B == 0) {
+    dw2.zero_();
+    db2.zero_();
+    return da1;
+  }
+  const int bi = static_cast<int>(B);
+  at::Tensor slabs = at::empty({kern::cn_conv2_slab_floats(bi)}, dw2.options());
+  kern::cn_conv2_bwd(a1.data_ptr(), r2.data_ptr(), dr2.data_ptr(), packed.data_ptr(),
+                     need_da1 ? da1.data_ptr() : nullptr, bi, slabs.data_ptr<float>(),
+                     dw2.data_ptr<float>(), db2.data_ptr<float>(), cur_stream(a1));
+  return da1;
+}
+
+void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
+                    const at::Tensor& a1, at::Tensor dw1, at::Tensor db1, double mean, double std,
+                    double in_scale) {
   int64_t B;
   bool u8;
   check_input(x, B, u8);
-  check_cuda(da1, "conv1 grad");
-  check_dtype(da1, at::kBFloat16, "conv1 grad");
-  check_shape(da1, {B, 13, 13, 32}, "conv1 grad");
-  check_shape(idx1, {B, 13, 13, 32}, "conv1 argmax");
-  check_shape(a1, {B, 13, 13, 32}, "conv1 pooled");
-  check_cuda(dw, "conv1 dw");
-  check_cuda(db, "conv1 db");
-  check_shape(dw, {32, 1, 5, 5}, "conv1 dw");
-  check_shape(db, {32}, "conv1 db");
-  int S = 1;
-  const int64_t nf = kern::convnet_conv1_wgrad_slab_floats(static_cast<int>(B), &S);
-  at::Tensor slabs = at::empty({nf}, dw.options());
-  kern::convnet_conv1_wgrad(x.data_ptr(), u8, da1.data_ptr(), idx1.data_ptr<uint8_t>(),
-                            a1.data_ptr(), static_cast<int>(B), static_cast<float>(mean),
-                            static_cast<float>(1.0 / std), static_cast<float>(in_scale),
-                            slabs.data_ptr<float>(), S, dw.data_ptr<float>(),
-                            db.data_ptr<float>(), cur_stream(x));
-}
-
-namespace {
-struct LayerShape {
-  int64_t cin, cout, ih, ph;
-};
-LayerShape layer_shape(int64_t layer) {
-  RINGDP_CHECK(layer == 2 || layer == 3, "convnet layer must be 2 or 3");
-  return layer == 2 ? LayerShape{32, 64, 13, 10} : LayerShape{64, 128, 10, 4};
-}
-}  // namespace
-
-std::tuple<at::Tensor, at::Tensor> convnet_conv_fwd(int64_t layer, const at::Tensor& in,
-                                                    const at::Tensor& w, const at::Tensor& b) {
-  auto L = layer_shape(layer);
-  check_cuda(in, "conv input");
-  check_dtype(in, at::kBFloat16, "conv input");
-  RINGDP_CHECK(in.dim() == 4 && in.size(1) == L.ih && in.size(2) == L.ih && in.size(3) == L.cin,
-               "conv", layer, " input: expected [B, ", L.ih, ", ", L.ih, ", ", L.cin, "] got ",
-               in.sizes());
-  check_cuda(w, "conv weight");
-  check_dtype(w, at::kFloat, "conv weight");
-  check_shape(w, {L.cout, L.cin, 3, 3}, "conv weight");
-  check_shape(b, {L.cout}, "conv bias");
-  const int64_t B = in.size(0);
-  at::Tensor out = at::empty({B, L.ph, L.ph, L.cout}, in.options());
-  at::Tensor idx = at::empty({B, L.ph, L.ph, L.cout}, in.options().dtype(at::kByte));
-  if (B == 0) return {out, idx};
-  kern::convnet_conv_fwd(static_cast<int>(layer), in.data_ptr(), w.data_ptr<float>(),
-                         b.data_ptr<float>(), out.data_ptr(), idx.data_ptr<uint8_t>(),
-                         static_cast<int>(B), cur_stream(in));
-  return {out, idx};
-}
-
-at::Tensor convnet_conv_bwd(int64_t layer, const at::Tensor& in, const at::Tensor& w,
-                            const at::Tensor& dout, const at::Tensor& idx, const at::Tensor& out,
-                            bool need_din, at::Tensor dw, at::Tensor db) {
-  auto L = layer_shape(layer);
-  check_cuda(in, "conv input");
-  check_cuda(dout, "conv grad_output");
-  check_dtype(dout, at::kBFloat16, "conv grad_output");
-  const int64_t B = in.size(0);
-  check_shape(dout, {B, L.ph, L.ph, L.cout}, "conv grad_output");
-  check_shape(idx, {B, L.ph, L.ph, L.cout}, "conv argmax");
-  check_shape(out, {B, L.ph, L.ph, L.cout}, "conv pooled output");
-  check_cuda(dw, "conv dw");
-  check_cuda(db, "conv db");
-  check_shape(dw, {L.cout, L.cin, 3, 3}, "conv dw");
-  check_shape(db, {L.cout}, "conv db");
-  at::Tensor din;
-  if (need_din) din = at::empty_like(in);
-  int S = 1;
-  const int64_t nf = kern::convnet_conv_wgrad_slab_floats(static_cast<int>(layer),
-                                                          static_cast<int>(B), &S);
-  at::Tensor slabs = at::empty({nf}, dw.options());
-  kern::convnet_conv_bwd(static_cast<int>(layer), in.data_ptr(), w.data_ptr<float>(),
-                         dout.data_ptr(), idx.data_ptr<uint8_t>(), out.data_ptr(),
-                         need_din ? din.data_ptr() : nullptr, static_cast<int>(B),
-                         slabs.data_ptr<float>(), S, dw.data_ptr<float>(), db.data_ptr<float>(),
-                         cur_stream(in));
-  return din;
-}
-
-at::Tensor convnet_fc_fwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& b) {
-  check_cuda(a3, "fc input");
-  check_dtype(a3, at::kBFloat16, "fc input");
-  RINGDP_CHECK(a3.numel() % 2048 == 0, "fc input: expected [B, 4, 4, 128]");
-  check_shape(w, {10, 2048}, "fc weight");
-  check_shape(b, {10}, "fc bias");
-  const int64_t B = a3.numel() / 2048;
-  at::Tensor logits = at::empty({B, 10}, a3.options().dtype(at::kFloat));
-  if (B == 0) return logits;
-  kern::convnet_fc_fwd(a3.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
-                       logits.data_ptr<float>(), static_cast<int>(B), cur_stream(a3));
-  return logits;
-}
-
-at::Tensor convnet_fc_bwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& dlogits,
-                          at::Tensor dw, at::Tensor db) {
-  const int64_t B = a3.numel() / 2048;
-  check_cuda(dlogits, "fc grad_output");
-  at::Tensor dl = dlogits.to(at::kFloat).contiguous();
-  check_shape(dl, {B, 10}, "fc grad_output");
-  check_shape(dw, {10, 2048}, "fc dw");
-  check_shape(db, {10}, "fc db");
-  at::Tensor da3 = at::empty_like(a3);
-  int S = 1;
-  const int64_t nf = kern::convnet_fc_slab_floats(static_cast<int>(B), &S);
-  at::Tensor slabs = at::empty({nf}, dw.options());
-  kern::convnet_fc_bwd(a3.data_ptr(), w.data_ptr<float>(), dl.data_ptr<float>(), da3.data_ptr(),
-                       static_cast<int>(B), slabs.data_ptr<float>(), S, dw.data_ptr<float>(),
-                       db.data_ptr<float>(), cur_stream(a3));
-  return da3;
+  check_act(da1, {B, 13, 13, 32}, at::kBFloat16, "conv1 grad");
+  check_act(idx1, {B, 13, 13, 32}, at::kByte, "conv1 argmax");
+  check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv1 pooled");
+  check_f32_out(dw1, {32, 1, 5, 5}, "conv1 dw");
+  check_f32_out(db1, {32}, "conv1 db");
+  if (B == 0) {
+    dw1.zero_();
+    db1.zero_();
+    return;
+  }
+  const int bi = static_cast<int>(B);
+  at::Tensor slabs = at::empty({kern::cn_conv1_slab_floats(bi)}, dw1.options());
+  kern::cn_conv1_wgrad(x.data_ptr(), u8, da1.data_ptr(), idx1.data_ptr<uint8_t>(), a1.data_ptr(), bi,
+                       static_cast<float>(mean), static_cast<float>(1.0 / std),
+                       static_cast<float>(in_scale), slabs.data_ptr<float>(), dw1.data_ptr<float>(),
+                       db1.data_ptr<float>(), cur_stream(x));
 }
 
 std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,

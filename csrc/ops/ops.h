@@ -51,21 +51,26 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& labels,
                              const at::Tensor& grad_out, int64_t ignore_index,
                              double label_smoothing, int64_t reduction);
 
-// MNIST ConvNet layers (see csrc/kernels/convnet.hip).
-std::tuple<at::Tensor, at::Tensor> convnet_conv1_fwd(const at::Tensor& x, const at::Tensor& w,
-                                                     const at::Tensor& b, double mean,
-                                                     double std, double in_scale);
-void convnet_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
-                         const at::Tensor& a1, at::Tensor dw, at::Tensor db, double mean,
-                         double std, double in_scale);
-std::tuple<at::Tensor, at::Tensor> convnet_conv_fwd(int64_t layer, const at::Tensor& in,
-                                                    const at::Tensor& w, const at::Tensor& b);
-at::Tensor convnet_conv_bwd(int64_t layer, const at::Tensor& in, const at::Tensor& w,
-                            const at::Tensor& dout, const at::Tensor& idx, const at::Tensor& out,
-                            bool need_din, at::Tensor dw, at::Tensor db);
-at::Tensor convnet_fc_fwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& b);
-at::Tensor convnet_fc_bwd(const at::Tensor& a3, const at::Tensor& w, const at::Tensor& dlogits,
-                          at::Tensor dw, at::Tensor db);
+// MNIST ConvNet blocks (see csrc/kernels/convnet.hip for the F1/F2/F3 split).
+at::Tensor cn_pack_weights(const at::Tensor& w1, const at::Tensor& w2, const at::Tensor& w3,
+                           const at::Tensor& wfc);
+std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::Tensor& packed,
+                                                const at::Tensor& b1, double mean, double std,
+                                                double in_scale);
+at::Tensor cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed, const at::Tensor& b2);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& r2,
+                                                               const at::Tensor& packed,
+                                                               const at::Tensor& b3,
+                                                               const at::Tensor& bfc);
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& r2, const at::Tensor& a3, const at::Tensor& idx3,
+                           const at::Tensor& wfc, const at::Tensor& dlogits,
+                           const at::Tensor& packed, bool need_dr2, at::Tensor dw3, at::Tensor db3,
+                           at::Tensor dwfc, at::Tensor dbfc);
+at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& r2, const at::Tensor& dr2,
+                        const at::Tensor& packed, bool need_da1, at::Tensor dw2, at::Tensor db2);
+void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
+                    const at::Tensor& a1, at::Tensor dw1, at::Tensor db1, double mean, double std,
+                    double in_scale);
 
 std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,
                                                    int64_t num_classes, int64_t seed,

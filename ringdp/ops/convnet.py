@@ -1,11 +1,17 @@
 """Autograd Functions for the MNIST ConvNet hot path (csrc/kernels/convnet.hip).
 
-Layer boundaries are chosen so autograd fires parameter hooks as early as possible: fc1's
-gradients are final after ``_FC.backward``, conv3's after ``_ConvReluPool(3).backward``, etc.,
-which is what lets ringdp's reducer start the first bucket all-reduce while conv2/conv1
-backward kernels are still running.
+Forward is three fused blocks (reference layers ref/launch_dist.py:35-41):
 
-Activations are NHWC bf16 pooled outputs; weights are fp32 masters (PyTorch layouts).
+* ``_Conv1``      conv1 + ReLU + pool1 (+ fused ToTensor/Normalize for uint8 input) -> a1
+* ``_Conv2Relu``  conv2 + ReLU -> r2 (the overlapping k2/s1 pool2 is NOT applied here)
+* ``_Conv3FC``    pool2 + conv3 + ReLU + pool3 + view + fc1 -> logits
+
+Placing pool2 at the start of the third block means its argmax never has to be stored (it is
+recomputed from r2 in backward) and conv2's backward only needs a ReLU mask.  Weights are packed
+once per forward into bf16 MFMA fragments (``C.cn_pack_weights``); the fp32 masters stay the
+parameters.  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
+``_Conv3FC.backward`` - so ringdp's reducer starts the first bucket all-reduce while conv2/conv1
+backward kernels still run.
 """
 from __future__ import annotations
 
@@ -18,10 +24,10 @@ MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
 
 
-class _Conv1ReluPool(torch.autograd.Function):
+class _Conv1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, mean, std, in_scale):
-        a1, idx = C.convnet_conv1_fwd(x, w, b, mean, std, in_scale)
+    def forward(ctx, x, w, b, packed, mean, std, in_scale):
+        a1, idx = C.cn_conv1_fwd(x, packed, b, mean, std, in_scale)
         ctx.save_for_backward(x, a1, idx)
         ctx.params = (w, b)
         ctx.norm = (mean, std, in_scale)
@@ -33,48 +39,55 @@ class _Conv1ReluPool(torch.autograd.Function):
         w, b = ctx.params
         need_w, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         if not (need_w or need_b):
-            return None, None, None, None, None, None
+            return (None,) * 7
         dw, db = grad_buffer(w), grad_buffer(b)
-        C.convnet_conv1_wgrad(x, da1.contiguous(), idx, a1, dw, db, *ctx.norm)
-        return None, (dw if need_w else None), (db if need_b else None), None, None, None
+        C.cn_conv1_wgrad(x, da1.contiguous(), idx, a1, dw, db, *ctx.norm)
+        return None, (dw if need_w else None), (db if need_b else None), None, None, None, None
 
 
-class _ConvReluPool(torch.autograd.Function):
+class _Conv2Relu(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, layer, inp, w, b):
-        out, idx = C.convnet_conv_fwd(layer, inp, w, b)
-        ctx.save_for_backward(inp, w, out, idx)
+    def forward(ctx, a1, w, b, packed):
+        r2 = C.cn_conv2_fwd(a1, packed, b)
+        ctx.save_for_backward(a1, r2, packed)
         ctx.params = (w, b)
-        ctx.layer = layer
-        return out
+        return r2
 
     @staticmethod
-    def backward(ctx, dout):
-        inp, w_saved, out, idx = ctx.saved_tensors
+    def backward(ctx, dr2):
+        a1, r2, packed = ctx.saved_tensors
         w, b = ctx.params
         dw, db = grad_buffer(w), grad_buffer(b)
-        need_in = ctx.needs_input_grad[1]
-        din = C.convnet_conv_bwd(ctx.layer, inp, w_saved, dout.contiguous(), idx, out, need_in, dw, db)
-        return (None, din if need_in else None, dw if ctx.needs_input_grad[2] else None,
-                db if ctx.needs_input_grad[3] else None)
+        need_in = ctx.needs_input_grad[0]
+        da1 = C.cn_conv2_bwd(a1, r2, dr2.contiguous(), packed, need_in, dw, db)
+        return (da1 if need_in else None, dw if ctx.needs_input_grad[1] else None,
+                db if ctx.needs_input_grad[2] else None, None)
 
 
-class _FC(torch.autograd.Function):
+class _Conv3FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a3, w, b):
-        logits = C.convnet_fc_fwd(a3, w, b)
-        ctx.save_for_backward(a3, w)
-        ctx.params = (w, b)
+    def forward(ctx, r2, w3, b3, wfc, bfc, packed):
+        logits, a3, idx3 = C.cn_conv3_fc_fwd(r2, packed, b3, bfc)
+        ctx.save_for_backward(r2, a3, idx3, wfc, packed)
+        ctx.params = (w3, b3, wfc, bfc)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
-        a3, w_saved = ctx.saved_tensors
-        w, b = ctx.params
-        dw, db = grad_buffer(w), grad_buffer(b)
-        da3 = C.convnet_fc_bwd(a3, w_saved, dlogits.contiguous(), dw, db)
-        return (da3 if ctx.needs_input_grad[0] else None, dw if ctx.needs_input_grad[1] else None,
-                db if ctx.needs_input_grad[2] else None)
+        r2, a3, idx3, wfc_saved, packed = ctx.saved_tensors
+        w3, b3, wfc, bfc = ctx.params
+        dw3, db3, dwfc, dbfc = (grad_buffer(p) for p in (w3, b3, wfc, bfc))
+        need_in = ctx.needs_input_grad[0]
+        dr2 = C.cn_conv3_fc_bwd(r2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
+                                dw3, db3, dwfc, dbfc)
+        n = ctx.needs_input_grad
+        return (dr2 if need_in else None, dw3 if n[1] else None, db3 if n[2] else None,
+                dwfc if n[3] else None, dbfc if n[4] else None, None)
+
+
+def pack_weights(conv1, conv2, conv3, fc1) -> torch.Tensor:
+    with torch.no_grad():
+        return C.cn_pack_weights(conv1.weight, conv2.weight, conv3.weight, fc1.weight)
 
 
 def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
@@ -88,7 +101,7 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         x = x.float()
         mean, std, scale = 0.0, 1.0, 1.0
     x = x.contiguous()
-    a1 = _Conv1ReluPool.apply(x, conv1.weight, conv1.bias, mean, std, scale)
-    a2 = _ConvReluPool.apply(2, a1, conv2.weight, conv2.bias)
-    a3 = _ConvReluPool.apply(3, a2, conv3.weight, conv3.bias)
-    return _FC.apply(a3, fc1.weight, fc1.bias)
+    packed = pack_weights(conv1, conv2, conv3, fc1)
+    a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
+    r2 = _Conv2Relu.apply(a1, conv2.weight, conv2.bias, packed)
+    return _Conv3FC.apply(r2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)

@@ -31,6 +31,7 @@ for s in ${STEPS:-tests smoke bench}; do
            step bench_b16384_eager 300 python bench.py --batch-per-rank 16384 --steps 20 --warmup 5 --no-graph ;;
     graphdiag) for lv in fwd loss bwd full; do step gdiag_$lv 300 env PYTHONPATH=. python tools/graph_diag.py $lv; done
            step gdiag_full_ddp 300 env PYTHONPATH=. python tools/graph_diag.py full ddp ;;
+    kbench) step kbench 300 python tools/kbench.py ${KB:-100 1024 4096 16384} ;;
     prof)  step prof_b100 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_b100 -o run --output-format csv -- python bench.py --batch-per-rank 100 --steps 50 --warmup 5 --no-graph
            step prof_b4096 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_b4096 -o run --output-format csv -- python bench.py --batch-per-rank 4096 --steps 50 --warmup 5 --no-graph ;;
   esac
