@@ -6,11 +6,11 @@
 //   conv3 64->128 k3 (10->8)  -> ReLU -> MaxPool(2,2) (4)  -> view(-1, 2048) -> fc1 2048->10
 //
 // Kernel blocks (one autograd Function each, see ringdp/ops/convnet.py):
-//   F1  conv1 + ReLU + pool1                       -> a1 [B,13,13,32] bf16 + argmax
-//   F2  conv2 + ReLU                               -> r2 [B,11,11,64] bf16
-//   F3  pool2 + conv3 + ReLU + pool3 + fc1         -> logits [B,10] fp32 (+ a3, argmax)
-// The overlapping k2/s1 pool lives at the START of F3: its argmax is recomputed from r2 when
-// needed, so no argmax tensor is stored for it and conv2's backward sees a plain ReLU mask.
+//   F1  conv1 + ReLU + pool1                       -> a1 [B,13,13,32] bf16 + argmax|relu byte
+//   F2  conv2 (+ bias, no ReLU)                    -> z2 [B,11,11,64] bf16
+//   F3  ReLU + pool2 + conv3 + ReLU + pool3 + fc1  -> logits [B,10] fp32 (+ a3, argmax)
+// conv2's ReLU and the overlapping k2/s1 pool live at the START of F3: their masks/argmax are
+// recomputed from z2 in F3's backward, which hands conv2 a plain linear-layer gradient dz2.
 //
 // MI355X-first design:
 //   * weight-stationary: weights are packed once per forward (cn_pack_weights) into bf16 MFMA
@@ -25,6 +25,8 @@
 //     a TN GEMM whose operands are read with ds_read_b64_tr_b16 (the transposed read also does the
 //     im2col gather), split over images into fp32 slabs reduced in a fixed order (deterministic);
 //   * one multi-segment reduction launch per layer backward.
+#include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #include "device_common.h"
@@ -41,7 +43,7 @@ __host__ __device__ constexpr int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // ------------------------------------------------------------------ packed weight layout
 // bf16 element offsets inside the packed buffer.  Fragment order: [n-tile][k-step][lane][8].
-constexpr int P1_OFF = 0, P1_N = 2 * 64 * 8;                    // conv1 fwd   (K = 25 -> 32)
+constexpr int P1_OFF = 0, P1_N = 2 * 2 * 512;                   // conv1 fwd   (K = kh*8 + kw, 2 k-steps)
 constexpr int P2F_OFF = P1_OFF + P1_N, P2F_N = 4 * 9 * 512;     // conv2 fwd   (N 64, K 288)
 constexpr int P3F_OFF = P2F_OFF + P2F_N, P3F_N = 8 * 18 * 512;  // conv3 fwd   (N 128, K 576)
 constexpr int P2D_OFF = P3F_OFF + P3F_N, P2D_N = 2 * 18 * 512;  // conv2 dgrad (N 32, K 576)
@@ -57,10 +59,10 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= PACK_TOTAL) return;
   float v = 0.f;
-  if (e < P2F_OFF) {
-    const int j = e & 7, lane = (e >> 3) & 63, nt = e >> 9;
-    const int co = nt * 16 + (lane & 15), t = 8 * (lane >> 4) + j;
-    v = t < 25 ? w1[co * 25 + t] : 0.f;
+  if (e < P2F_OFF) {  // [nt][ks][lane][8]: k = ks*32 + 8*(lane>>4) + j -> kh = ks*4 + (lane>>4), kw = j
+    const int j = e & 7, lane = (e >> 3) & 63, ks = (e >> 9) & 1, nt = e >> 10;
+    const int co = nt * 16 + (lane & 15), kh = ks * 4 + (lane >> 4), kw = j;
+    v = (kh < 5 && kw < 5) ? w1[co * 25 + kh * 5 + kw] : 0.f;
   } else if (e < P2D_OFF) {  // forward fragments of conv2 / conv3: B[k = tap*CIN + ci][n = co]
     const bool l2 = e < P3F_OFF;
     const int r = e - (l2 ? P2F_OFF : P3F_OFF);
@@ -97,6 +99,13 @@ __device__ __forceinline__ bf16x8 window_max8(const bf16* r0, int rs, int w) {
   return bmax8(bmax8(*reinterpret_cast<const bf16x8*>(r0), *reinterpret_cast<const bf16x8*>(r0 + rs)),
                bmax8(*reinterpret_cast<const bf16x8*>(r0 + w * rs),
                      *reinterpret_cast<const bf16x8*>(r0 + (w + 1) * rs)));
+}
+
+__device__ __forceinline__ bf16x8 relu8(const bf16x8& a) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (float)a[j] > 0.f ? a[j] : (bf16)0.f;
+  return r;
 }
 
 // First-max argmax over the 4 registers of a window + bias + ReLU (torch max_pool2d semantics:
@@ -137,8 +146,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-// ================================================================== F1: conv1 (MFMA, K 25 -> 32)
-constexpr int C1_XS = 30 * 30 + 12;  // zero-ringed 30x30 bf16 image (+pad)
+// ================================================================== F1: conv1 (MFMA)
+// The zero-ringed 30x30 input is staged as 8 copies shifted by s = 0..7 columns (rows of 32):
+// copy s holds xpad[r][c + s].  Eight consecutive pixels xpad[r][ow .. ow+7] are then ONE aligned
+// ds_read_b128 at copy (ow & 7), column (ow & ~7) - this is the im2col of a 5-wide filter row, so
+// the GEMM K is laid out as k = kh*8 + kw (kw < 5 valid): 2 k-steps of 32, no per-element gather.
+constexpr int XC_W = 32, XC_SZ = 30 * XC_W;  // one shifted copy (bf16)
 
 template <bool U8>
 __device__ __forceinline__ void c1_load(const void* xin, int b, int tid, uint32_t& u, float4& f) {
@@ -150,9 +163,11 @@ __device__ __forceinline__ void c1_load(const void* xin, int b, int tid, uint32_
   }
 }
 
-template <bool U8>
-__device__ __forceinline__ void c1_store(bf16* xs, int tid, uint32_t u, float4 f, float mean,
-                                         float inv_std, float in_scale) {
+// Normalise this thread's 4 pixels and write them into copies 0..NC-1 (positions outside a copy
+// are never written, so the zero ring / tail established once stays zero).
+template <bool U8, int NC>
+__device__ __forceinline__ void c1_store(bf16* xc, int tid, uint32_t u, float4 f, float mean, float inv_std,
+                                         float in_scale) {
   if (tid < 196) {
     float v[4];
     if (U8) {
@@ -166,8 +181,11 @@ __device__ __forceinline__ void c1_store(bf16* xs, int tid, uint32_t u, float4 f
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int p = 4 * tid + k, r = p / 28, c = p % 28;
-      xs[(r + 1) * 30 + c + 1] = (bf16)((v[k] - mean) * inv_std);
+      const int p = 4 * tid + k, pr = p / 28 + 1, pc = p % 28 + 1;
+      const bf16 xv = (bf16)((v[k] - mean) * inv_std);
+#pragma unroll
+      for (int s = 0; s < NC; ++s)
+        if (pc >= s) xc[s * XC_SZ + pr * XC_W + pc - s] = xv;
     }
   }
 }
@@ -179,27 +197,25 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
                                                         bf16* __restrict__ a1,
                                                         uint8_t* __restrict__ idx1, int B,
                                                         float mean, float inv_std, float in_scale) {
-  __shared__ __attribute__((aligned(16))) bf16 xs[2][C1_XS];
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][8 * XC_SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P1_OFF);
-  const bf16x8 bw0 = pk[lane], bw1 = pk[64 + lane];
-  const float bias0 = bias[lane & 15], bias1 = bias[16 + (lane & 15)];
-  int toff[8];
-  bool tval[8];
+  bf16x8 bw[2][2];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int t = 8 * (lane >> 4) + j;
-    tval[j] = t < 25;
-    toff[j] = tval[j] ? (t / 5) * 30 + t % 5 : 0;
-  }
-  for (int i = tid; i < 2 * C1_XS; i += 256) (&xs[0][0])[i] = (bf16)0.f;
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) bw[nt][ks] = pk[(nt * 2 + ks) * 64 + lane];
+  const float bias0 = bias[lane & 15], bias1 = bias[16 + (lane & 15)];
+  const int kh0 = (lane >> 4) * XC_W;  // k-step 0: filter rows 0..3; k-step 1: row 4 (others zero weights)
+  const int kh1 = 4 * XC_W;
+  for (int i = tid; i < 2 * 8 * XC_SZ / 8; i += 256) reinterpret_cast<bf16x8*>(&xs[0][0])[i] = zero_bf16x8();
   __syncthreads();
   uint32_t pu = 0;
   float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
   int b = blockIdx.x;
   if (b < B) {
     c1_load<U8>(xin, b, tid, pu, pf);
-    c1_store<U8>(xs[0], tid, pu, pf, mean, inv_std, in_scale);
+    c1_store<U8, 8>(xs[0], tid, pu, pf, mean, inv_std, in_scale);
   }
   __syncthreads();
   int cur = 0;
@@ -209,15 +225,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
     const bf16* x = xs[cur];
     for (int mt = wave; mt < 43; mt += 4) {
       const int r16 = lane & 15;
-      const int w = 4 * mt + (r16 >> 2), i = r16 & 3;
-      bf16x8 a = zero_bf16x8();
-      if (w < 169) {
-        const int base = (2 * (w / 13) + (i >> 1)) * 30 + 2 * (w % 13) + (i & 1);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) a[j] = tval[j] ? x[base + toff[j]] : (bf16)0.f;
-      }
-      const f32x4 c0 = mfma16x16x32(a, bw0, zero_f32x4());
-      const f32x4 c1 = mfma16x16x32(a, bw1, zero_f32x4());
+      const int w = min(4 * mt + (r16 >> 2), 168), i = r16 & 3;  // rows >= 676: clamped, dropped
+      const int oh = 2 * (w / 13) + (i >> 1), ow = 2 * (w % 13) + (i & 1);
+      const bf16* xr = x + (ow & 7) * XC_SZ + oh * XC_W + (ow & ~7);
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xr + kh0);
+      const bf16x8 a1v = *reinterpret_cast<const bf16x8*>(xr + kh1);
+      f32x4 c0 = mfma16x16x32(a0, bw[0][0], zero_f32x4());
+      c0 = mfma16x16x32(a1v, bw[0][1], c0);
+      f32x4 c1 = mfma16x16x32(a0, bw[1][0], zero_f32x4());
+      c1 = mfma16x16x32(a1v, bw[1][1], c1);
       const int wc = 4 * mt + (lane >> 4);
       if (wc < 169) {
         int g0, g1;
@@ -225,17 +241,17 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
         const int64_t o = ((int64_t)b * 169 + wc) * 32 + (lane & 15);
         a1[o] = (bf16)v0;
         a1[o + 16] = (bf16)v1;
-        idx1[o] = (uint8_t)g0;
-        idx1[o + 16] = (uint8_t)g1;
+        idx1[o] = (uint8_t)(g0 | (v0 > 0.f ? 4 : 0));  // bit 2: ReLU mask for the backward
+        idx1[o + 16] = (uint8_t)(g1 | (v1 > 0.f ? 4 : 0));
       }
     }
-    if (nb < B) c1_store<U8>(xs[cur ^ 1], tid, pu, pf, mean, inv_std, in_scale);
+    if (nb < B) c1_store<U8, 8>(xs[cur ^ 1], tid, pu, pf, mean, inv_std, in_scale);
     __syncthreads();
     cur ^= 1;
   }
 }
 
-// ================================================================== F2: conv2 + ReLU
+// ================================================================== F2: conv2 (pre-activation out)
 // 256 threads; wave (wm, wn) owns n-tiles {2wn, 2wn+1} x m-tiles {4wm..4wm+3} (121 rows -> 128).
 constexpr int C2_XRS = 40;  // bf16 per LDS row of the a1 image (32 + 8 pad)
 constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 + 8)
@@ -243,7 +259,7 @@ constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 +
 __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restrict__ a1,
                                                            const bf16* __restrict__ packed,
                                                            const float* __restrict__ bias,
-                                                           bf16* __restrict__ r2, int B) {
+                                                           bf16* __restrict__ z2, int B) {
   __shared__ __attribute__((aligned(16))) bf16 X[2][169 * C2_XRS];
   __shared__ __attribute__((aligned(16))) bf16 Cs[121 * C2_CRS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -258,13 +274,10 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
   float bv[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) bv[t] = bias[(2 * wn + t) * 16 + r16];
-  int base[4];
-  bool valid[4];
+  int base[4];  // rows >= 121 read a clamped (valid) address; their outputs are dropped
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    const int m = (4 * wm + mt) * 16 + r16;
-    valid[mt] = m < 121;
-    const int mm = valid[mt] ? m : 0;
+    const int mm = min((4 * wm + mt) * 16 + r16, 120);
     base[mt] = (mm / 11) * 13 + mm % 11;
   }
   bf16x8 pre[3];
@@ -302,8 +315,7 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
       const int shift = (ks / 3) * 13 + ks % 3;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        bf16x8 a = zero_bf16x8();
-        if (valid[mt]) a = *reinterpret_cast<const bf16x8*>(x + (base[mt] + shift) * C2_XRS + q8);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + (base[mt] + shift) * C2_XRS + q8);
         acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
         acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
       }
@@ -316,31 +328,31 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int m = (4 * wm + mt) * 16 + (lane >> 4) * 4 + i;
-          if (m < 121) Cs[m * C2_CRS + (2 * wn + t) * 16 + r16] = (bf16)fmaxf(acc[mt][t][i] + bv[t], 0.f);
+          if (m < 121) Cs[m * C2_CRS + (2 * wn + t) * 16 + r16] = (bf16)(acc[mt][t][i] + bv[t]);
         }
     if (nb < B) store(X[cur ^ 1]);
     __syncthreads();
-    bf16x8* dst = reinterpret_cast<bf16x8*>(r2 + (int64_t)b * 121 * 64);
+    bf16x8* dst = reinterpret_cast<bf16x8*>(z2 + (int64_t)b * 121 * 64);
     for (int c = tid; c < 968; c += 256)
       dst[c] = *reinterpret_cast<const bf16x8*>(Cs + (c >> 3) * C2_CRS + (c & 7) * 8);
     cur ^= 1;
   }
 }
 
-// ================================================================== F3: pool2 + conv3 + ReLU + pool3 + fc1
+// ================================================================== F3: ReLU + pool2 + conv3 + ReLU + pool3 + fc1
 // 256 threads; wave w owns output channels 32w..32w+31 (n-tiles 2w, 2w+1) for all 16 pool windows.
-constexpr int C3_RRS = 64;  // bf16 per LDS row, r2 image (unpadded: filled by glds)
+constexpr int C3_RRS = 64;  // bf16 per LDS row, z2 image (unpadded: filled by glds)
 constexpr int C3_XRS = 72;  // bf16 per LDS row, pooled conv3 input (64 + 8)
 
 __device__ __forceinline__ void pool2_into(const bf16* R, bf16* X, int tid, int nthreads) {
   for (int it = tid; it < 800; it += nthreads) {
     const int p = it >> 3, c = (it & 7) * 8;
     const int py = p / 10, px = p % 10;
-    *reinterpret_cast<bf16x8*>(X + p * C3_XRS + c) = window_max8(R + (py * 11 + px) * C3_RRS + c, C3_RRS, 11);
+    *reinterpret_cast<bf16x8*>(X + p * C3_XRS + c) = relu8(window_max8(R + (py * 11 + px) * C3_RRS + c, C3_RRS, 11));
   }
 }
 
-__global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __restrict__ r2,
+__global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __restrict__ z2,
                                                               const bf16* __restrict__ packed,
                                                               const float* __restrict__ bias,
                                                               const float* __restrict__ bfc,
@@ -369,9 +381,9 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
     const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFC_OFF);
     for (int c = tid; c < PFC_N / 8; c += 256) reinterpret_cast<bf16x8*>(Fc)[c] = src[c];
   }
-  // r2 image -> R: 968 16-B chunks = 16 wave-instructions (4 per wave), lane-linear
+  // z2 image -> R: 968 16-B chunks = 16 wave-instructions (4 per wave), lane-linear
   auto stage = [&](int bb) {
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(r2 + (int64_t)bb * 121 * 64);
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(z2 + (int64_t)bb * 121 * 64);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int inst = k * 4 + wave, c = inst * 64 + lane;
@@ -435,94 +447,140 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
 }
 
 // ================================================================== F3 backward
-// (1) fc1 backward: da3 = dl . Wfc, scattered to window-ordered d(conv3) rows D3[b][4w + i][co]
-//     (one non-zero per window: the argmax, if the pooled value is > 0) + fc weight-grad slabs.
-constexpr int FC_SLAB = 10 * 2048 + 10;
+// (1) fc1 backward, one pass over a3: compact data gradient
+//       da3m[b][w][co] = (a3 > 0) * sum_n dl[b][n] * Wfc[n][co*16 + w]     (bf16, Wfc from the pack)
+//     and the fc1 weight/bias gradient of this block's images as an fp32 slab.  The conv3 backward
+//     roles expand da3m to window-ordered rows (row 4w + argmax) in LDS.
+constexpr int FC_IMGS = 16;              // images per workgroup
+constexpr int FC_SLAB = 10 * 2048 + 10;  // dWfc + dbfc
 
 __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3,
-                                                     const uint8_t* __restrict__ idx3,
-                                                     const float* __restrict__ wfc,
+                                                     const bf16* __restrict__ packed,
                                                      const float* __restrict__ dl,
-                                                     bf16* __restrict__ d3, float* __restrict__ slabs,
-                                                     int nslices, int B) {
+                                                     bf16* __restrict__ da3m, float* __restrict__ slabs,
+                                                     int B) {
   const int t = threadIdx.x;
   const int wd = t >> 4, co0 = (t & 15) * 8;  // this thread's 8 activations: window wd, channels co0..
-  float wr[10][8];
+  float wr[8][10];
+  {
+    // Pfc is [w][co][n]: this thread's 80 weights are contiguous (10 x 16 B)
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFC_OFF + (wd * 128 + co0) * 10);
 #pragma unroll
-  for (int n = 0; n < 10; ++n)
+    for (int h = 0; h < 10; ++h) {
+      const bf16x8 v = src[h];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) wr[n][j] = wfc[n * 2048 + (co0 + j) * 16 + wd];
-  float acc[10][8];
+      for (int e = 0; e < 8; ++e) wr[(8 * h + e) / 10][(8 * h + e) % 10] = (float)v[e];
+    }
+  }
+  float acc[8][10];
 #pragma unroll
-  for (int n = 0; n < 10; ++n)
+  for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[n][j] = 0.f;
+    for (int n = 0; n < 10; ++n) acc[j][n] = 0.f;
   float bacc = 0.f;
-  const int per = cdiv(B, nslices);
-  const int b_lo = blockIdx.x * per, b_hi = min(B, b_lo + per);
-  for (int b = b_lo; b < b_hi; ++b) {
-    float g[10];
+  const int b0 = blockIdx.x * FC_IMGS, nimg = min(FC_IMGS, B - b0);
+  for (int k0 = 0; k0 < nimg; k0 += 8) {
+    bf16x8 av[8];
 #pragma unroll
-    for (int n = 0; n < 10; ++n) g[n] = dl[(int64_t)b * 10 + n];
-    const int64_t o = (int64_t)b * 2048 + wd * 128 + co0;
-    const bf16x8 av = *reinterpret_cast<const bf16x8*>(a3 + o);
-    const uint2 iv = *reinterpret_cast<const uint2*>(idx3 + o);
-    float da[8];
+    for (int k = 0; k < 8; ++k)
+      if (k0 + k < nimg) av[k] = *reinterpret_cast<const bf16x8*>(a3 + (int64_t)(b0 + k0 + k) * 2048 + wd * 128 + co0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float s = 0.f;
-      const float aj = (float)av[j];
+    for (int k = 0; k < 8; ++k) {
+      if (k0 + k < nimg) {
+        const int b = b0 + k0 + k;
+        float g[10];
 #pragma unroll
-      for (int n = 0; n < 10; ++n) {
-        s = fmaf(g[n], wr[n][j], s);
-        acc[n][j] = fmaf(g[n], aj, acc[n][j]);
+        for (int n = 0; n < 10; ++n) g[n] = dl[(int64_t)b * 10 + n];
+        bf16x8 v;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float aj = (float)av[k][j];
+          float s = 0.f;
+#pragma unroll
+          for (int n = 0; n < 10; ++n) {
+            s = fmaf(g[n], wr[j][n], s);
+            acc[j][n] = fmaf(g[n], aj, acc[j][n]);
+          }
+          v[j] = aj > 0.f ? (bf16)s : (bf16)0.f;
+        }
+        *reinterpret_cast<bf16x8*>(da3m + (int64_t)b * 2048 + wd * 128 + co0) = v;
+        if (t < 10) bacc += dl[(int64_t)b * 10 + t];
       }
-      da[j] = aj > 0.f ? s : 0.f;
     }
-    bf16* drow = d3 + ((int64_t)b * 64 + 4 * wd) * 128 + co0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)(byte_of(iv, j) == i ? da[j] : 0.f);
-      *reinterpret_cast<bf16x8*>(drow + i * 128) = v;
-    }
-    if (t < 10) bacc += dl[(int64_t)b * 10 + t];
   }
   float* slab = slabs + (int64_t)blockIdx.x * FC_SLAB;
 #pragma unroll
   for (int n = 0; n < 10; ++n)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) slab[n * 2048 + (co0 + j) * 16 + wd] = acc[n][j];
+    for (int j = 0; j < 8; ++j) slab[n * 2048 + (co0 + j) * 16 + wd] = acc[j][n];
   if (t < 10) slab[20480 + t] = bacc;
 }
 
 // (2) conv3 backward, two roles in one 512-thread launch:
-//   dgrad: da2 = full-corr(D3 image, flipped W3) -> pool2 backward (argmax recomputed from r2)
-//          -> dr2 [B,11,11,64];
-//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a2 = pool2(r2).
+//   dgrad: da2 = full-corr(d(conv3) image, flipped W3) -> pool2 + ReLU backward (argmax and mask
+//          recomputed from z2) -> dz2 [B,11,11,64];
+//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a2 = relu(pool2(z2));
+//          db3 via one extra MFMA tile against a ones column.
 constexpr int C3_PW = 12;    // padded d(conv3) image width (8 + 2*2)
 constexpr int C3_PRS = 136;  // bf16 per padded-image row (128 + 8)
 constexpr int C3_DARS = 68;  // floats per da2 row (64 + 4)
 constexpr int C3_DRS = 136;  // bf16 per D3 row in LDS
-constexpr int C3B_P_BYTES = C3_PW * C3_PW * C3_PRS * 2;  // 39168
-constexpr int C3B_R_BYTES = 121 * C3_RRS * 2;            // 15488
-constexpr int C3B_AM_BYTES = 100 * 64;                   // 6400
-constexpr int C3B_DG_LDS = C3B_P_BYTES + C3B_R_BYTES + C3B_AM_BYTES;
-constexpr int C3B_D_BYTES = 64 * C3_DRS * 2;   // 17408
-constexpr int C3B_X_BYTES = 100 * C3_XRS * 2;  // 14400
-constexpr int C3B_WG_LDS = C3B_D_BYTES + C3B_X_BYTES + C3B_R_BYTES;
-constexpr int C3B_LDS = C3B_DG_LDS > C3B_WG_LDS ? C3B_DG_LDS : C3B_WG_LDS;
+constexpr int C3D_P = C3_PW * C3_PW * C3_PRS * 2;  // 39168
+constexpr int C3D_R = 121 * C3_RRS * 2;            // 15488
+constexpr int C3D_AM = 100 * 64;                   // 6400
+constexpr int C3D_DA = 100 * C3_DARS * 4;          // 27200
+constexpr int C3D_LDS = C3D_P + C3D_R + C3D_AM + C3D_DA;
+constexpr int C3W_D = 64 * C3_DRS * 2;   // 17408
+constexpr int C3W_X = 100 * C3_XRS * 2;  // 14400
+constexpr int C3W_LDS = C3W_D + C3W_X + C3D_R;
+constexpr int C3B_LDS = C3D_LDS > C3W_LDS ? C3D_LDS : C3W_LDS;
 constexpr int C3_WSLAB = 576 * 128 + 128;  // dW3t + db3
-static_assert(100 * C3_DARS * 4 <= C3B_P_BYTES, "da2 must fit in the padded-image region");
 
-__device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ r2, const bf16* __restrict__ d3,
-                                 const bf16* __restrict__ packed, bf16* __restrict__ dr2, int B,
-                                 int block, int nblocks) {
+// One image of F3-backward input, held in registers while the previous image is computed on.
+struct C3Pre {
+  bf16x8 da;  // compact d(a3) chunk (threads < 256)
+  uint2 id;   // its pool3 argmax bytes
+  bf16x8 z[2];
+};
+
+__device__ __forceinline__ void c3_load(C3Pre& p, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
+                                        const bf16* __restrict__ z2, int b, int tid) {
+  if (tid < 256) {
+    p.da = reinterpret_cast<const bf16x8*>(da3m + (int64_t)b * 2048)[tid];
+    p.id = reinterpret_cast<const uint2*>(idx3 + (int64_t)b * 2048)[tid];
+  }
+  const bf16x8* zs = reinterpret_cast<const bf16x8*>(z2 + (int64_t)b * 121 * 64);
+  p.z[0] = zs[tid];
+  if (tid + 512 < 968) p.z[1] = zs[tid + 512];
+}
+
+__device__ __forceinline__ void c3_store_R(const C3Pre& p, bf16* R, int tid) {
+  reinterpret_cast<bf16x8*>(R)[tid] = p.z[0];
+  if (tid + 512 < 968) reinterpret_cast<bf16x8*>(R)[tid + 512] = p.z[1];
+}
+
+// Expand compact item tid (window w = tid >> 4, channels cc..cc+7) to the 4 window-ordered rows.
+template <typename RowPtr>
+__device__ __forceinline__ void c3_expand(const C3Pre& p, int tid, RowPtr row_ptr) {
+  if (tid < 256) {
+    const int w = tid >> 4, cc = (tid & 15) * 8;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = byte_of(p.id, j) == i ? p.da[j] : (bf16)0.f;
+      *reinterpret_cast<bf16x8*>(row_ptr(4 * w + i) + cc) = v;
+    }
+  }
+}
+
+__device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ z2, const bf16* __restrict__ da3m,
+                                 const uint8_t* __restrict__ idx3, const bf16* __restrict__ packed,
+                                 bf16* __restrict__ dz2, int B, int block, int nblocks) {
   bf16* P = reinterpret_cast<bf16*>(smem);
-  float* DA = reinterpret_cast<float*>(smem);  // aliases P after the MFMA phase
-  bf16* R = reinterpret_cast<bf16*>(smem + C3B_P_BYTES);
-  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3B_P_BYTES + C3B_R_BYTES);
+  bf16* R = reinterpret_cast<bf16*>(smem + C3D_P);
+  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P + C3D_R);
+  float* DA = reinterpret_cast<float*>(smem + C3D_P + C3D_R + C3D_AM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nt = wave & 3, mh = wave >> 2;  // n-tile (16 input channels), m-tile parity
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
@@ -530,39 +588,58 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ r2, const 
   bf16x8 bw[36];
 #pragma unroll
   for (int ks = 0; ks < 36; ++ks) bw[ks] = pk[(nt * 36 + ks) * 64 + lane];
-  int base[4];
-  bool valid[4];
+  int base[4];  // rows >= 100 read a clamped (valid) address; their outputs are dropped
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int mt = mh + 2 * k;
-    const int m = mt * 16 + r16;
-    valid[k] = mt < 7 && m < 100;
-    const int mm = valid[k] ? m : 0;
+    const int mm = min((mh + 2 * k) * 16 + r16, 99);
     base[k] = (mm / 10) * C3_PW + mm % 10;
   }
-  const int nk = mh ? 3 : 4;
-  for (int b = block; b < B; b += nblocks) {
-    __syncthreads();
-    // zero the whole padded image (its ring was overwritten by DA), stage r2
-    for (int c = tid; c < C3_PW * C3_PW * C3_PRS / 8; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
-    stage_rows(r2 + (int64_t)b * 121 * 64, R, 968, 8, C3_RRS, tid, 512);
-    __syncthreads();
-    {
-      const bf16x8* src = reinterpret_cast<const bf16x8*>(d3 + (int64_t)b * 64 * 128);
-      for (int c = tid; c < 1024; c += 512) {
-        const int r = c >> 4, cc = (c & 15) * 8;
-        *reinterpret_cast<bf16x8*>(P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS + cc) = src[c];
+  // the ring of the padded image stays zero; only the 8x8 interior is rewritten per image
+  for (int c = tid; c < C3D_P / 16; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
+  // m-tiles mh, mh+2, ... < 7: 4 for even waves, 3 for odd (compile-time trip counts)
+  auto mfma_phase = [&](auto nk_c) {
+    constexpr int NK = decltype(nk_c)::value;
+    f32x4 acc[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) acc[k] = zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < 36; ++ks) {
+      const int tapp = ks >> 2, c0 = (ks & 3) * 32;
+      const int shift = (tapp / 3) * C3_PW + tapp % 3;
+#pragma unroll
+      for (int k = 0; k < NK; ++k)
+        acc[k] = mfma16x16x32(*reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C3_PRS + c0 + q8), bw[ks],
+                              acc[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const int mt = mh + 2 * k;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = mt * 16 + (lane >> 4) * 4 + i;
+        if (m < 100) DA[m * C3_DARS + nt * 16 + r16] = acc[k][i];
       }
     }
-    // pool2 argmax per window (first max), from the r2 image
+  };
+  C3Pre pre;
+  int b = block;
+  if (b < B) c3_load(pre, da3m, idx3, z2, b, tid);
+  for (; b < B; b += nblocks) {
+    __syncthreads();  // previous image fully consumed
+    c3_expand(pre, tid, [&](int r) { return P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS; });
+    c3_store_R(pre, R, tid);
+    const int nb = b + nblocks;
+    if (nb < B) c3_load(pre, da3m, idx3, z2, nb, tid);  // lands during the MFMA phase
+    __syncthreads();
+    // pool2 argmax per window (first max of relu(z2): ties at 0 pick the first, like torch)
     for (int it = tid; it < 800; it += 512) {
       const int p = it >> 3, c = (it & 7) * 8;
       const int py = p / 10, px = p % 10;
       const bf16* r0 = R + (py * 11 + px) * C3_RRS + c;
-      const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(r0);
-      const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(r0 + C3_RRS);
-      const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(r0 + 11 * C3_RRS);
-      const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(r0 + 12 * C3_RRS);
+      const bf16x8 v0 = relu8(*reinterpret_cast<const bf16x8*>(r0));
+      const bf16x8 v1 = relu8(*reinterpret_cast<const bf16x8*>(r0 + C3_RRS));
+      const bf16x8 v2 = relu8(*reinterpret_cast<const bf16x8*>(r0 + 11 * C3_RRS));
+      const bf16x8 v3 = relu8(*reinterpret_cast<const bf16x8*>(r0 + 12 * C3_RRS));
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -584,38 +661,13 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ r2, const 
       }
       *reinterpret_cast<uint2*>(AM + p * 64 + c) = make_uint2(lo, hi);
     }
+    if (mh == 0)
+      mfma_phase(std::integral_constant<int, 4>{});
+    else
+      mfma_phase(std::integral_constant<int, 3>{});
     __syncthreads();
-    f32x4 acc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[k] = zero_f32x4();
-#pragma unroll 4
-    for (int ks = 0; ks < 36; ++ks) {
-      const int tapp = ks >> 2, c0 = (ks & 3) * 32;
-      const int shift = (tapp / 3) * C3_PW + tapp % 3;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (k < nk) {
-          bf16x8 a = zero_bf16x8();
-          if (valid[k]) a = *reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C3_PRS + c0 + q8);
-          acc[k] = mfma16x16x32(a, bw[ks], acc[k]);
-        }
-      }
-    }
-    __syncthreads();  // P dead -> DA
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int mt = mh + 2 * k;
-      if (k < nk) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = mt * 16 + (lane >> 4) * 4 + i;
-          if (m < 100) DA[m * C3_DARS + nt * 16 + r16] = acc[k][i];
-        }
-      }
-    }
-    __syncthreads();
-    // pool2 backward (gather): dr2[y][x] = sum of da2 over the windows whose argmax is (y, x)
-    bf16x8* dst = reinterpret_cast<bf16x8*>(dr2 + (int64_t)b * 121 * 64);
+    // pool2 backward (gather over the <= 4 windows covering (y, x)) + ReLU mask (z2 > 0)
+    bf16x8* dst = reinterpret_cast<bf16x8*>(dz2 + (int64_t)b * 121 * 64);
     for (int it = tid; it < 968; it += 512) {
       const int pos = it >> 3, c = (it & 7) * 8;
       const int y = pos / 11, x = pos % 11;
@@ -634,41 +686,48 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ r2, const 
           for (int j = 0; j < 8; ++j)
             if (byte_of(am, j) == want) g[j] += dv[j];
         }
+      const bf16x8 zv = *reinterpret_cast<const bf16x8*>(R + pos * C3_RRS + c);
       bf16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)g[j];
+      for (int j = 0; j < 8; ++j) v[j] = (float)zv[j] > 0.f ? (bf16)g[j] : (bf16)0.f;
       dst[it] = v;
     }
   }
 }
 
-__device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ r2, const bf16* __restrict__ d3,
-                                 float* __restrict__ slabs, int B, int nslices, int slice) {
+__device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
+  const bf16 one = (bf16)((lane & 15) == 0 ? 1.f : 0.f);
+  return bf16x8{one, one, one, one, one, one, one, one};
+}
+
+__device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ z2, const bf16* __restrict__ da3m,
+                                 const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
+                                 int nslices, int slice) {
   bf16* D = reinterpret_cast<bf16*>(smem);
-  bf16* X = reinterpret_cast<bf16*>(smem + C3B_D_BYTES);
-  bf16* R = reinterpret_cast<bf16*>(smem + C3B_D_BYTES + C3B_X_BYTES);
+  bf16* X = reinterpret_cast<bf16*>(smem + C3W_D);
+  bf16* R = reinterpret_cast<bf16*>(smem + C3W_D + C3W_X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;  // m-tiles 4wm..4wm+3 (co), n-tiles 9wn..9wn+8
   const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
-  f32x4 acc[4][9];
+  const bf16x8 onesf = ones_column_frag(lane);
+  f32x4 acc[4][9], accb[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    accb[i] = zero_f32x4();
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = zero_f32x4();
-  float bacc = 0.f;
+  }
   const int per = cdiv(B, nslices);
   const int b_lo = slice * per, b_hi = min(B, b_lo + per);
+  C3Pre pre;
+  if (b_lo < b_hi) c3_load(pre, da3m, idx3, z2, b_lo, tid);
   for (int b = b_lo; b < b_hi; ++b) {
     __syncthreads();
-    stage_rows(d3 + (int64_t)b * 64 * 128, D, 1024, 16, C3_DRS, tid, 512);
-    stage_rows(r2 + (int64_t)b * 121 * 64, R, 968, 8, C3_RRS, tid, 512);
+    c3_expand(pre, tid, [&](int r) { return D + r * C3_DRS; });
+    c3_store_R(pre, R, tid);
+    if (b + 1 < b_hi) c3_load(pre, da3m, idx3, z2, b + 1, tid);
     __syncthreads();
     pool2_into(R, X, tid, 512);
-    if (tid < 128) {
-      float s = 0.f;
-      for (int r = 0; r < 64; ++r) s += (float)D[r * C3_DRS + tid];
-      bacc += s;
-    }
     __syncthreads();
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -693,59 +752,56 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ r2, const 
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][j] = mfma16x16x32(af[i], bf, acc[i][j]);
       }
+      if (wn == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) accb[i] = mfma16x16x32(af[i], onesf, accb[i]);
+      }
     }
   }
   float* slab = slabs + (int64_t)slice * C3_WSLAB;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    const int co = (4 * wm + i) * 16 + grp * 4;
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
-      const int co = (4 * wm + i) * 16 + grp * 4;
       const int n = (9 * wn + j) * 16 + g16;
       *reinterpret_cast<f32x4*>(slab + (int64_t)n * 128 + co) = acc[i][j];
     }
-  if (tid < 128) slab[576 * 128 + tid] = bacc;
+    if (wn == 0 && g16 == 0) *reinterpret_cast<f32x4*>(slab + 576 * 128 + co) = accb[i];
+  }
 }
 
-__global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__ r2,
-                                                        const bf16* __restrict__ d3,
+__global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__ z2,
+                                                        const bf16* __restrict__ da3m,
+                                                        const uint8_t* __restrict__ idx3,
                                                         const bf16* __restrict__ packed,
-                                                        bf16* __restrict__ dr2, int B,
-                                                        float* __restrict__ slabs, int nslices,
+                                                        bf16* __restrict__ dz2, int B,
+                                                        float* __restrict__ slabs, int n_wgrad,
                                                         int n_dgrad) {
   __shared__ __attribute__((aligned(16))) char smem[C3B_LDS];
-  if ((int)blockIdx.x < n_dgrad)
-    conv3_dgrad_role(smem, r2, d3, packed, dr2, B, blockIdx.x, n_dgrad);
+  const int blk = blockIdx.x;
+  if (blk < n_dgrad)
+    conv3_dgrad_role(smem, z2, da3m, idx3, packed, dz2, B, blk, n_dgrad);
   else
-    conv3_wgrad_role(smem, r2, d3, slabs, B, nslices, blockIdx.x - n_dgrad);
+    conv3_wgrad_role(smem, z2, da3m, idx3, slabs, B, n_wgrad, blk - n_dgrad);
 }
 
 // ================================================================== F2 backward
-// dconv2 = dr2 * (r2 > 0) (ReLU mask); roles:
-//   dgrad: da1 = full-corr(dconv2 image, flipped W2)  [13x13x32]
-//   wgrad: dW2t[n = tap*32 + ci][co] = sum_pos dconv2[pos][co] * a1[pos + tap][ci]
+// conv2 is linear here (its ReLU belongs to F3), so dz2 is the conv output gradient directly:
+//   dgrad: da1 = full-corr(dz2 image, flipped W2)  [13x13x32]
+//   wgrad: dW2t[n = tap*32 + ci][co] = sum_pos dz2[pos][co] * a1[pos + tap][ci]; db2 via a ones tile
 constexpr int C2_PW = 15, C2_PRS = 72, C2_ORS = 40, C2_DRS = 72;
-constexpr int C2B_P_BYTES = C2_PW * C2_PW * C2_PRS * 2;  // 32400
-constexpr int C2B_O_BYTES = 169 * C2_ORS * 2;            // 13520
-constexpr int C2B_D_BYTES = 128 * C2_DRS * 2;            // 18432
-constexpr int C2B_X_BYTES = 169 * C2_XRS * 2;            // 13520
-constexpr int C2B_LDS = (C2B_P_BYTES + C2B_O_BYTES) > (C2B_D_BYTES + C2B_X_BYTES)
-                            ? (C2B_P_BYTES + C2B_O_BYTES)
-                            : (C2B_D_BYTES + C2B_X_BYTES);
+constexpr int C2D_P = C2_PW * C2_PW * C2_PRS * 2;  // 32400
+constexpr int C2D_O = 169 * C2_ORS * 2;            // 13520 (x2: double-buffered output tile)
+constexpr int C2W_D = 128 * C2_DRS * 2;            // 18432
+constexpr int C2W_X = 169 * C2_XRS * 2;            // 13520
+constexpr int C2B_LDS = (C2D_P + 2 * C2D_O) > (C2W_D + C2W_X) ? (C2D_P + 2 * C2D_O) : (C2W_D + C2W_X);
 constexpr int C2_WSLAB = 288 * 64 + 64;
 
-__device__ __forceinline__ bf16x8 relu_mask8(const bf16x8& g, const bf16x8& r) {
-  bf16x8 v;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) v[j] = (float)r[j] > 0.f ? g[j] : (bf16)0.f;
-  return v;
-}
-
-__device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ r2, const bf16* __restrict__ dr2,
-                                 const bf16* __restrict__ packed, bf16* __restrict__ da1, int B,
-                                 int block, int nblocks) {
+__device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ dz2, const bf16* __restrict__ packed,
+                                 bf16* __restrict__ da1, int B, int block, int nblocks) {
   bf16* P = reinterpret_cast<bf16*>(smem);
-  bf16* O = reinterpret_cast<bf16*>(smem + C2B_P_BYTES);
+  bf16* O = reinterpret_cast<bf16*>(smem + C2D_P);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nt = wave & 1, mg = wave >> 1;  // n-tile (16 input channels), m-tiles mg, mg+4, mg+8
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
@@ -753,93 +809,110 @@ __device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ r2, const 
   bf16x8 bw[18];
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) bw[ks] = pk[(nt * 18 + ks) * 64 + lane];
-  int base[3];
-  bool valid[3];
+  int base[3];  // rows >= 169 read a clamped (valid) address; their outputs are dropped
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const int mt = mg + 4 * k;
-    const int m = mt * 16 + r16;
-    valid[k] = mt < 11 && m < 169;
-    const int mm = valid[k] ? m : 0;
+    const int mm = min((mg + 4 * k) * 16 + r16, 168);
     base[k] = (mm / 13) * C2_PW + mm % 13;
   }
-  const int nk = mg == 3 ? 2 : 3;
-  for (int c = tid; c < C2_PW * C2_PW * C2_PRS / 8; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
-  for (int b = block; b < B; b += nblocks) {
-    __syncthreads();
-    {
-      const bf16x8* g = reinterpret_cast<const bf16x8*>(dr2 + (int64_t)b * 121 * 64);
-      const bf16x8* r = reinterpret_cast<const bf16x8*>(r2 + (int64_t)b * 121 * 64);
-      for (int c = tid; c < 968; c += 512) {
-        const int pos = c >> 3, cc = (c & 7) * 8;
-        const int y = pos / 11, x = pos % 11;
-        *reinterpret_cast<bf16x8*>(P + ((y + 2) * C2_PW + x + 2) * C2_PRS + cc) = relu_mask8(g[c], r[c]);
-      }
-    }
-    __syncthreads();
-    f32x4 acc[3];
+  for (int c = tid; c < C2D_P / 16; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
+  auto copy_out = [&](int bb, const bf16* src) {
+    bf16x8* dst = reinterpret_cast<bf16x8*>(da1 + (int64_t)bb * 169 * 32);
+    for (int c = tid; c < 676; c += 512) dst[c] = *reinterpret_cast<const bf16x8*>(src + (c >> 2) * C2_ORS + (c & 3) * 8);
+  };
+  bf16x8 pz[2];
+  auto load = [&](int bb) {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
+    pz[0] = src[tid];
+    if (tid + 512 < 968) pz[1] = src[tid + 512];
+  };
+  // m-tiles mg, mg+4, mg+8 < 11: 3 for waves with mg < 3, 2 for mg == 3 (compile-time trip counts)
+  auto mfma_phase = [&](auto nk_c, bf16* Oc) {
+    constexpr int NK = decltype(nk_c)::value;
+    f32x4 acc[NK];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) acc[k] = zero_f32x4();
-#pragma unroll 2
+    for (int k = 0; k < NK; ++k) acc[k] = zero_f32x4();
+#pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int tapp = ks >> 1, c0 = (ks & 1) * 32;
       const int shift = (tapp / 3) * C2_PW + tapp % 3;
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (k < nk) {
-          bf16x8 a = zero_bf16x8();
-          if (valid[k]) a = *reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C2_PRS + c0 + q8);
-          acc[k] = mfma16x16x32(a, bw[ks], acc[k]);
-        }
-      }
+      for (int k = 0; k < NK; ++k)
+        acc[k] = mfma16x16x32(*reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C2_PRS + c0 + q8), bw[ks],
+                              acc[k]);
     }
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < NK; ++k) {
       const int mt = mg + 4 * k;
-      if (k < nk) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = mt * 16 + (lane >> 4) * 4 + i;
-          if (m < 169) O[m * C2_ORS + nt * 16 + r16] = (bf16)acc[k][i];
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int m = mt * 16 + (lane >> 4) * 4 + i;
+        if (m < 169) Oc[m * C2_ORS + nt * 16 + r16] = (bf16)acc[k][i];
       }
     }
+  };
+  int b = block, prev = -1, cur = 0;
+  if (b < B) load(b);
+  for (; b < B; b += nblocks) {
     __syncthreads();
-    bf16x8* dst = reinterpret_cast<bf16x8*>(da1 + (int64_t)b * 169 * 32);
-    for (int c = tid; c < 676; c += 512) dst[c] = *reinterpret_cast<const bf16x8*>(O + (c >> 2) * C2_ORS + (c & 3) * 8);
+    if (prev >= 0) copy_out(prev, O + (cur ^ 1) * 169 * C2_ORS);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + 512 * k;
+      if (c < 968) {
+        const int pos = c >> 3, cc = (c & 7) * 8;
+        *reinterpret_cast<bf16x8*>(P + ((pos / 11 + 2) * C2_PW + pos % 11 + 2) * C2_PRS + cc) = pz[k];
+      }
+    }
+    const int nb = b + nblocks;
+    if (nb < B) load(nb);
+    __syncthreads();
+    bf16* Oc = O + cur * 169 * C2_ORS;
+    if (mg < 3)
+      mfma_phase(std::integral_constant<int, 3>{}, Oc);
+    else
+      mfma_phase(std::integral_constant<int, 2>{}, Oc);
+    prev = b;
+    cur ^= 1;
   }
+  __syncthreads();
+  if (prev >= 0) copy_out(prev, O + (cur ^ 1) * 169 * C2_ORS);
 }
 
-__device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ r2,
-                                 const bf16* __restrict__ dr2, float* __restrict__ slabs, int B,
-                                 int nslices, int slice) {
+__device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ dz2,
+                                 float* __restrict__ slabs, int B, int nslices, int slice) {
   bf16* D = reinterpret_cast<bf16*>(smem);
-  bf16* X = reinterpret_cast<bf16*>(smem + C2B_D_BYTES);
+  bf16* X = reinterpret_cast<bf16*>(smem + C2W_D);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;  // m-tile wm (co 16wm..), n-tiles 9wn..9wn+8
   const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
-  f32x4 acc[9];
+  const bf16x8 onesf = ones_column_frag(lane);
+  f32x4 acc[9], accb = zero_f32x4();
 #pragma unroll
   for (int j = 0; j < 9; ++j) acc[j] = zero_f32x4();
-  float bacc = 0.f;
-  for (int c = tid; c < 128 * C2_DRS / 8; c += 512) reinterpret_cast<bf16x8*>(D)[c] = zero_bf16x8();
+  for (int c = tid; c < C2W_D / 16; c += 512) reinterpret_cast<bf16x8*>(D)[c] = zero_bf16x8();  // rows >= 121 stay 0
   const int per = cdiv(B, nslices);
   const int b_lo = slice * per, b_hi = min(B, b_lo + per);
+  bf16x8 pz[2], pa[2];
+  auto load = [&](int bb) {
+    const bf16x8* zs = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
+    const bf16x8* as = reinterpret_cast<const bf16x8*>(a1 + (int64_t)bb * 169 * 32);
+    pz[0] = zs[tid];
+    if (tid + 512 < 968) pz[1] = zs[tid + 512];
+    pa[0] = as[tid];
+    if (tid + 512 < 676) pa[1] = as[tid + 512];
+  };
+  if (b_lo < b_hi) load(b_lo);
   for (int b = b_lo; b < b_hi; ++b) {
     __syncthreads();
-    {
-      const bf16x8* g = reinterpret_cast<const bf16x8*>(dr2 + (int64_t)b * 121 * 64);
-      const bf16x8* r = reinterpret_cast<const bf16x8*>(r2 + (int64_t)b * 121 * 64);
-      for (int c = tid; c < 968; c += 512)
-        *reinterpret_cast<bf16x8*>(D + (c >> 3) * C2_DRS + (c & 7) * 8) = relu_mask8(g[c], r[c]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = tid + 512 * k;
+      if (c < 968) *reinterpret_cast<bf16x8*>(D + (c >> 3) * C2_DRS + (c & 7) * 8) = pz[k];
+      if (c < 676) *reinterpret_cast<bf16x8*>(X + (c >> 2) * C2_XRS + (c & 3) * 8) = pa[k];
     }
-    stage_rows(a1 + (int64_t)b * 169 * 32, X, 676, 4, C2_XRS, tid, 512);
+    if (b + 1 < b_hi) load(b + 1);
     __syncthreads();
-    if (tid < 64) {
-      float s = 0.f;
-      for (int r = 0; r < 121; ++r) s += (float)D[r * C2_DRS + tid];
-      bacc += s;
-    }
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int kb = ks * 32 + grp * 8;
@@ -859,122 +932,121 @@ __device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const 
         const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         acc[j] = mfma16x16x32(af, bf, acc[j]);
       }
+      if (wn == 0) accb = mfma16x16x32(af, onesf, accb);
     }
   }
   float* slab = slabs + (int64_t)slice * C2_WSLAB;
+  const int co = wm * 16 + grp * 4;
 #pragma unroll
   for (int j = 0; j < 9; ++j) {
-    const int co = wm * 16 + grp * 4;
     const int n = (9 * wn + j) * 16 + g16;
     *reinterpret_cast<f32x4*>(slab + (int64_t)n * 64 + co) = acc[j];
   }
-  if (tid < 64) slab[288 * 64 + tid] = bacc;
+  if (wn == 0 && g16 == 0) *reinterpret_cast<f32x4*>(slab + 288 * 64 + co) = accb;
 }
 
 __global__ __launch_bounds__(512) void conv2_bwd_kernel(const bf16* __restrict__ a1,
-                                                        const bf16* __restrict__ r2,
-                                                        const bf16* __restrict__ dr2,
+                                                        const bf16* __restrict__ dz2,
                                                         const bf16* __restrict__ packed,
                                                         bf16* __restrict__ da1, int B,
                                                         float* __restrict__ slabs, int nslices,
                                                         int n_dgrad) {
   __shared__ __attribute__((aligned(16))) char smem[C2B_LDS];
   if ((int)blockIdx.x < n_dgrad)
-    conv2_dgrad_role(smem, r2, dr2, packed, da1, B, blockIdx.x, n_dgrad);
+    conv2_dgrad_role(smem, dz2, packed, da1, B, blockIdx.x, n_dgrad);
   else
-    conv2_wgrad_role(smem, a1, r2, dr2, slabs, B, nslices, blockIdx.x - n_dgrad);
+    conv2_wgrad_role(smem, a1, dz2, slabs, B, nslices, blockIdx.x - n_dgrad);
 }
 
 // ================================================================== F1 backward (conv1 wgrad)
-// dW1[co][t] = sum_{b, k} Dc[b][k][co] * xpad[b][pos(k) + (kh, kw)], K rows in window order
-// (k = 4w + i: one non-zero row per window and channel - the argmax, if the pooled value > 0).
-constexpr int C1W_K = 704;          // 676 rows padded to 22 k-steps
-constexpr int C1W_DRS = C1W_K + 8;  // bf16 per co row of the transposed d(conv1)
+// dW1[co][t] = sum_{b, oh, ow} dC[b][oh][ow][co] * xpad[b][oh + kh][ow + kw]  as a TN GEMM with
+// K = spatial positions in rows of 32 (k = oh*32 + ow, ow >= 26 zero): the X operand for tap
+// (kh, kw) and 8 consecutive ow is one aligned ds_read_b128 of shifted copy kw; the dC operand is
+// stored [k][co] and read with ds_read_b64_tr_b16.  dC = unpool(da1) * relu-mask, both from the
+// idx1 byte.  Tap column t = 25 of the padded N is a ones column -> db1 for free.
+constexpr int C1W_K = 26 * 32;
 constexpr int C1_WSLAB = 32 * 25 + 32;
 
 template <bool U8>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict__ xin,
                                                           const bf16* __restrict__ da1,
-                                                          const uint8_t* __restrict__ idx1,
-                                                          const bf16* __restrict__ a1, int B,
+                                                          const uint8_t* __restrict__ idx1, int B,
                                                           float mean, float inv_std, float in_scale,
                                                           float* __restrict__ slabs, int nslices) {
-  __shared__ __attribute__((aligned(16))) bf16 Dt[32 * C1W_DRS];
-  __shared__ __attribute__((aligned(16))) bf16 xs[C1_XS];
-  __shared__ float bred[32][4];
+  __shared__ __attribute__((aligned(16))) bf16 Dk[C1W_K * 32];
+  __shared__ __attribute__((aligned(16))) bf16 xs[5 * XC_SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mt = wave >> 1, nt = wave & 1;
-  const int r16 = lane & 15, q = lane >> 4;
-  const int t = nt * 16 + r16;
-  const bool tvalid = t < 25;
-  const int toff = tvalid ? (t / 5) * 30 + t % 5 : 0;
-  f32x4 acc = zero_f32x4();
-  float bpart[8];
+  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
+  const int t = nt * 16 + g16;
+  const bool tvalid = t < 25, tones = t == 25;
+  const int xoff = tvalid ? (t % 5) * XC_SZ + (t / 5) * XC_W + 8 * grp : 0;
+  bf16x8 onesv;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) bpart[j] = 0.f;
-  for (int i = tid; i < 32 * C1W_DRS / 8; i += 256) reinterpret_cast<bf16x8*>(Dt)[i] = zero_bf16x8();
-  for (int i = tid; i < C1_XS; i += 256) xs[i] = (bf16)0.f;
+  for (int j = 0; j < 8; ++j) onesv[j] = (bf16)(tones ? 1.f : 0.f);
+  f32x4 acc = zero_f32x4();
+  for (int i = tid; i < C1W_K * 32 / 8; i += 256) reinterpret_cast<bf16x8*>(Dk)[i] = zero_bf16x8();
+  for (int i = tid; i < 5 * XC_SZ / 8; i += 256) reinterpret_cast<bf16x8*>(xs)[i] = zero_bf16x8();
   const int per = cdiv(B, nslices);
   const int b_lo = blockIdx.x * per, b_hi = min(B, b_lo + per);
   const int c0 = (tid & 3) * 8;  // fixed channel chunk of this thread in the staging loop
-  for (int b = b_lo; b < b_hi; ++b) {
-    __syncthreads();
-    uint32_t u = 0;
-    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
-    c1_load<U8>(xin, b, tid, u, f);
-    c1_store<U8>(xs, tid, u, f, mean, inv_std, in_scale);
-    for (int it = tid; it < 676; it += 256) {
-      const int w = it >> 2;
-      const int64_t o = ((int64_t)b * 169 + w) * 32 + c0;
-      const bf16x8 g = *reinterpret_cast<const bf16x8*>(da1 + o);
-      const bf16x8 pv = *reinterpret_cast<const bf16x8*>(a1 + o);
-      const uint2 iv = *reinterpret_cast<const uint2*>(idx1 + o);
+  uint32_t xu = 0;
+  float4 xf = make_float4(0.f, 0.f, 0.f, 0.f);
+  bf16x8 gv[3];
+  uint2 iv[3];
+  auto load = [&](int bb) {
+    c1_load<U8>(xin, bb, tid, xu, xf);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bf16 gb = (float)pv[j] > 0.f ? g[j] : (bf16)0.f;
-        bpart[j] += (float)gb;
-        const int ij = byte_of(iv, j);
-        bf16x4 v;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = i == ij ? gb : (bf16)0.f;
-        *reinterpret_cast<bf16x4*>(Dt + (c0 + j) * C1W_DRS + 4 * w) = v;
+    for (int k = 0; k < 3; ++k) {
+      const int it = tid + 256 * k;
+      if (it < 676) {
+        const int64_t o = ((int64_t)bb * 169 + (it >> 2)) * 32 + c0;
+        gv[k] = *reinterpret_cast<const bf16x8*>(da1 + o);
+        iv[k] = *reinterpret_cast<const uint2*>(idx1 + o);
       }
     }
+  };
+  if (b_lo < b_hi) load(b_lo);
+  for (int b = b_lo; b < b_hi; ++b) {
     __syncthreads();
-#pragma unroll 2
-    for (int ks = 0; ks < 22; ++ks) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(Dt + (mt * 16 + r16) * C1W_DRS + ks * 32 + q * 8);
-      bf16x8 bf = zero_bf16x8();
-      if (tvalid) {
+    c1_store<U8, 5>(xs, tid, xu, xf, mean, inv_std, in_scale);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int k = min(ks * 32 + q * 8 + j, 675);  // Dt columns >= 676 are zero
-          const int w = k >> 2, i = k & 3;
-          bf[j] = xs[(2 * (w / 13) + (i >> 1)) * 30 + 2 * (w % 13) + (i & 1) + toff];
+    for (int k = 0; k < 3; ++k) {
+      const int it = tid + 256 * k;
+      if (it < 676) {
+        const int w = it >> 2, py = w / 13, px = w % 13;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          bf16x8 v;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int code = byte_of(iv[k], j);
+            v[j] = (code & 4) && (code & 3) == d ? gv[k][j] : (bf16)0.f;
+          }
+          const int pos = (2 * py + (d >> 1)) * 32 + 2 * px + (d & 1);
+          *reinterpret_cast<bf16x8*>(Dk + pos * 32 + c0) = v;
         }
       }
+    }
+    if (b + 1 < b_hi) load(b + 1);
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 26; ++ks) {
+      const int kb = ks * 32 + grp * 8;
+      const bf16x4 lo = lds_read_tr16(Dk + (kb + q) * 32 + mt * 16 + 4 * p);
+      const bf16x4 hi = lds_read_tr16(Dk + (kb + 4 + q) * 32 + mt * 16 + 4 * p);
+      const bf16x8 af = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const bf16x8 bf = tvalid ? *reinterpret_cast<const bf16x8*>(xs + xoff + ks * XC_W) : onesv;
       acc = mfma16x16x32(af, bf, acc);
     }
   }
-  // bias: the 16 lanes of a wave with the same channel chunk (lane & 3) reduce by shuffles,
-  // then the 4 waves through LDS (fixed order)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float v = bpart[j];
-    v += __shfl_xor(v, 4, 64);
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (lane < 4) bred[c0 + j][wave] = v;
-  }
-  __syncthreads();
   float* slab = slabs + (int64_t)blockIdx.x * C1_WSLAB;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int co = mt * 16 + q * 4 + i;
+    const int co = mt * 16 + grp * 4 + i;
     if (tvalid) slab[co * 25 + t] = acc[i];
+    if (tones) slab[800 + co] = acc[i];
   }
-  if (tid < 32) slab[800 + tid] = (bred[tid][0] + bred[tid][1]) + (bred[tid][2] + bred[tid][3]);
 }
 
 // ================================================================== fixed-order slab reductions
@@ -1080,67 +1152,98 @@ void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, v
     conv1_fwd_kernel<false><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
 }
 
-void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* r2, int B, hipStream_t s) {
+void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* z2, int B, hipStream_t s) {
   const int grid = clampi(B, 1, 2 * num_cus());
   conv2_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(packed), b2,
-                                        static_cast<bf16*>(r2), B);
+                                        static_cast<bf16*>(z2), B);
 }
 
-void cn_conv3_fc_fwd(const void* r2, const void* packed, const float* b3, const float* bfc, float* logits,
+void cn_conv3_fc_fwd(const void* z2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s) {
   const int grid = clampi(B, 1, 2 * num_cus());
-  conv3_fc_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(r2), static_cast<const bf16*>(packed), b3,
+  conv3_fc_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(z2), static_cast<const bf16*>(packed), b3,
                                            bfc, logits, static_cast<bf16*>(a3), idx3, B);
 }
 
-static int fc_slices(int B) { return clampi(cdiv(B, 4), 1, 128); }
-static int conv3_wslices(int B) { return clampi(cdiv(B, 8), 1, num_cus()); }
-static int conv2_wslices(int B) { return clampi(cdiv(B, 8), 1, num_cus()); }
+// Work split of the role-fused backward launches.  All blocks of a launch are co-resident (one
+// 512-thread block per CU), so dgrad and wgrad blocks are sized to finish together: dgrad does
+// ~2x (conv3) / ~1.25x (conv2) the MFMA work of wgrad per image.
+static void c3_split(int B, bool dgrad, int& nd, int& ws) {
+  const int cus = num_cus();
+  if (!dgrad) {
+    nd = 0;
+    ws = clampi(cdiv(B, 8), 1, cus);
+    return;
+  }
+  nd = clampi(B, 1, (2 * cus) / 3);
+  const int per = cdiv(B, nd);
+  ws = clampi(cdiv(B, 2 * per), 1, std::max(1, cus - nd));
+}
+
+static void c2_split(int B, bool dgrad, int& nd, int& ws) {
+  const int cus = num_cus();
+  if (!dgrad) {
+    nd = 0;
+    ws = clampi(cdiv(B, 8), 1, cus);
+    return;
+  }
+  nd = clampi(B, 1, (9 * cus) / 16);
+  const int per = cdiv(B, nd);
+  ws = clampi(cdiv(B, per), 1, std::max(1, cus - nd));
+}
+
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 2 * num_cus()); }
-int64_t cn_fc_slab_floats(int B) { return (int64_t)fc_slices(B) * FC_SLAB; }
-int64_t cn_conv3_slab_floats(int B) { return (int64_t)conv3_wslices(B) * C3_WSLAB; }
-int64_t cn_conv2_slab_floats(int B) { return (int64_t)conv2_wslices(B) * C2_WSLAB; }
+
+int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, FC_IMGS) * FC_SLAB; }
+int64_t cn_conv3_slab_floats(int B, bool dgrad) {
+  int nd, ws;
+  c3_split(B, dgrad, nd, ws);
+  return (int64_t)ws * C3_WSLAB;
+}
+int64_t cn_conv2_slab_floats(int B, bool dgrad) {
+  int nd, ws;
+  c2_split(B, dgrad, nd, ws);
+  return (int64_t)ws * C2_WSLAB;
+}
 int64_t cn_conv1_slab_floats(int B) { return (int64_t)conv1_wslices(B) * C1_WSLAB; }
 
-void cn_conv3_fc_bwd(const void* r2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
-                     const void* packed, void* d3, void* dr2, int B, float* fc_slabs, float* c3_slabs,
+void cn_conv3_fc_bwd(const void* z2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
+                     const void* packed, void* da3m, void* dz2, int B, float* fc_slabs, float* c3_slabs,
                      float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s) {
-  const int fs = fc_slices(B);
-  fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), idx3, wfc, dl, static_cast<bf16*>(d3),
-                                   fc_slabs, fs, B);
-  const int ws = conv3_wslices(B);
-  const int nd = dr2 ? clampi(B, 1, num_cus()) : 0;
-  conv3_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(r2), static_cast<const bf16*>(d3),
-                                           static_cast<const bf16*>(packed), static_cast<bf16*>(dr2), B,
-                                           c3_slabs, ws, nd);
+  (void)wfc;  // the data gradient uses the packed bf16 copy, like every other dgrad
+  int nd, ws;
+  c3_split(B, dz2 != nullptr, nd, ws);
+  const int fs = cdiv(B, FC_IMGS);
+  fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
+                                   static_cast<bf16*>(da3m), fc_slabs, B);
+  conv3_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(z2), static_cast<const bf16*>(da3m), idx3,
+                                           static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B, c3_slabs,
+                                           ws, nd);
   launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
                  seg(c3_slabs, C3_WSLAB, 576 * 128, 128, ws, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc),
                  seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},
                 s);
 }
 
-void cn_conv2_bwd(const void* a1, const void* r2, const void* dr2, const void* packed, void* da1, int B,
-                  float* slabs, float* dw2, float* db2, hipStream_t s) {
-  const int ws = conv2_wslices(B);
-  const int nd = da1 ? clampi(B, 1, num_cus()) : 0;
-  conv2_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(r2),
-                                           static_cast<const bf16*>(dr2), static_cast<const bf16*>(packed),
-                                           static_cast<bf16*>(da1), B, slabs, ws, nd);
+void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1, int B, float* slabs,
+                  float* dw2, float* db2, hipStream_t s) {
+  int nd, ws;
+  c2_split(B, da1 != nullptr, nd, ws);
+  conv2_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(dz2),
+                                           static_cast<const bf16*>(packed), static_cast<bf16*>(da1), B, slabs,
+                                           ws, nd);
   launch_reduce({seg(slabs, C2_WSLAB, 0, 288 * 64, ws, dw2, 1, 32, 64), seg(slabs, C2_WSLAB, 288 * 64, 64, ws, db2)},
                 s);
 }
 
-void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, const void* a1, int B,
-                    float mean, float inv_std, float in_scale, float* slabs, float* dw1, float* db1,
-                    hipStream_t s) {
+void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,
+                    float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s) {
   const int ws = conv1_wslices(B);
   if (u8)
-    conv1_wgrad_kernel<true><<<ws, 256, 0, s>>>(x, static_cast<const bf16*>(da1), idx1,
-                                                static_cast<const bf16*>(a1), B, mean, inv_std, in_scale,
+    conv1_wgrad_kernel<true><<<ws, 256, 0, s>>>(x, static_cast<const bf16*>(da1), idx1, B, mean, inv_std, in_scale,
                                                 slabs, ws);
   else
-    conv1_wgrad_kernel<false><<<ws, 256, 0, s>>>(x, static_cast<const bf16*>(da1), idx1,
-                                                 static_cast<const bf16*>(a1), B, mean, inv_std, in_scale,
+    conv1_wgrad_kernel<false><<<ws, 256, 0, s>>>(x, static_cast<const bf16*>(da1), idx1, B, mean, inv_std, in_scale,
                                                  slabs, ws);
   launch_reduce({seg(slabs, C1_WSLAB, 0, 800, ws, dw1), seg(slabs, C1_WSLAB, 800, 32, ws, db1)}, s);
 }

@@ -157,51 +157,84 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }
 
 // ---------------------------------------------------------------- cross entropy
+// Row loss: one lane per row for small C (the MNIST head: C = 10, no cross-lane work at all), one
+// wave per row otherwise.  Per-block partial sums + an agent-scope last-arriver reduction that runs
+// in a fixed order (deterministic, graph-capturable: the counter re-arms itself).
+__device__ __forceinline__ float ce_row_loss(float lse, float xy, float sx, int C, float eps) {
+  return (1.f - eps) * (lse - xy) + eps * (lse - sx / (float)C);
+}
+
+template <bool kSmallC>
 __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ logits,
                                                      const int64_t* __restrict__ labels, int B, int C,
                                                      int ignore_index, float eps, int reduction,
                                                      float* __restrict__ lse_out, float* __restrict__ loss,
                                                      float* __restrict__ partials, unsigned* counter,
                                                      int nparts) {
-  __shared__ float s_sum[4], s_cnt[4];
+  __shared__ float s_sum[256], s_cnt[256];
   __shared__ int s_last;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float wsum = 0.f, wcnt = 0.f;
-  for (int r = blockIdx.x * 4 + wave; r < B; r += nparts * 4) {
-    const float* x = logits + (int64_t)r * C;
-    float mx = -INFINITY;
-    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, x[c]);
-    mx = wave_max(mx);
-    float se = 0.f, sx = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      se += __expf(x[c] - mx);
-      sx += x[c];
-    }
-    se = wave_sum(se);
-    sx = wave_sum(sx);
-    const float lse = mx + __logf(se);
-    const int64_t y = labels[r];
-    float l = 0.f, valid = 0.f;
-    if (y != ignore_index) {
-      l = (1.f - eps) * (lse - x[y]) + eps * (lse - sx / (float)C);
-      valid = 1.f;
-    }
-    if (lane == 0) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float tsum = 0.f, tcnt = 0.f;
+  if (kSmallC) {
+    for (int r = blockIdx.x * 256 + tid; r < B; r += nparts * 256) {
+      const float* x = logits + (int64_t)r * C;
+      const int64_t y = labels[r];
+      float mx = -INFINITY, sx = 0.f, xy = 0.f;
+      for (int c = 0; c < C; ++c) {
+        const float v = x[c];
+        mx = fmaxf(mx, v);
+        sx += v;
+        xy = (c == y) ? v : xy;
+      }
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += __expf(x[c] - mx);
+      const float lse = mx + __logf(se);
+      const bool valid = y != ignore_index;
+      const float l = valid ? ce_row_loss(lse, xy, sx, C, eps) : 0.f;
       lse_out[r] = lse;
       if (reduction == 0) loss[r] = l;
+      tsum += l;
+      tcnt += valid ? 1.f : 0.f;
     }
-    wsum += l;
-    wcnt += valid;
+  } else {
+    for (int r = blockIdx.x * 4 + wave; r < B; r += nparts * 4) {
+      const float* x = logits + (int64_t)r * C;
+      float mx = -INFINITY;
+      for (int c = lane; c < C; c += 64) mx = fmaxf(mx, x[c]);
+      mx = wave_max(mx);
+      float se = 0.f, sx = 0.f;
+      for (int c = lane; c < C; c += 64) {
+        se += __expf(x[c] - mx);
+        sx += x[c];
+      }
+      se = wave_sum(se);
+      sx = wave_sum(sx);
+      const float lse = mx + __logf(se);
+      const int64_t y = labels[r];
+      const bool valid = y != ignore_index;
+      const float l = valid ? ce_row_loss(lse, x[y], sx, C, eps) : 0.f;
+      if (lane == 0) {
+        lse_out[r] = lse;
+        if (reduction == 0) loss[r] = l;
+        tsum += l;
+        tcnt += valid ? 1.f : 0.f;
+      }
+    }
   }
   if (reduction == 0) return;
-  if (lane == 0) {
-    s_sum[wave] = wsum;
-    s_cnt[wave] = wcnt;
-  }
+  s_sum[tid] = tsum;
+  s_cnt[tid] = tcnt;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    partials[2 * blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
-    partials[2 * blockIdx.x + 1] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+  for (int off = 128; off > 0; off >>= 1) {  // fixed-shape tree: deterministic
+    if (tid < off) {
+      s_sum[tid] += s_sum[tid + off];
+      s_cnt[tid] += s_cnt[tid + off];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    partials[2 * blockIdx.x] = s_sum[0];
+    partials[2 * blockIdx.x + 1] = s_cnt[0];
     // Publish the partial (agent-scope release), then take a ticket; the last arriver reduces.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -214,15 +247,25 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
   }
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) {
-    float s = 0.f, c = 0.f;
-    for (int i = 0; i < nparts; ++i) {  // fixed order: deterministic
-      s += __builtin_nontemporal_load(&partials[2 * i]);
-      c += __builtin_nontemporal_load(&partials[2 * i + 1]);
+  float a = 0.f, c = 0.f;
+  for (int i = tid; i < nparts; i += 256) {  // fixed assignment + fixed tree below: deterministic
+    a += __builtin_nontemporal_load(&partials[2 * i]);
+    c += __builtin_nontemporal_load(&partials[2 * i + 1]);
+  }
+  s_sum[tid] = a;
+  s_cnt[tid] = c;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+      s_sum[tid] += s_sum[tid + off];
+      s_cnt[tid] += s_cnt[tid + off];
     }
-    const float denom = reduction == 1 ? c : 1.f;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float denom = reduction == 1 ? s_cnt[0] : 1.f;
     partials[2 * nparts] = denom;
-    loss[0] = reduction == 1 ? s / denom : s;
+    loss[0] = reduction == 1 ? s_sum[0] / denom : s_sum[0];
     __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -315,8 +358,12 @@ void splitk_reduce(const float* slabs, int nslices, int64_t n, float* out, hipSt
 void cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, int ignore_index,
                        float label_smoothing, int reduction, float* lse, float* loss,
                        float* partials, unsigned* counter, int nparts, hipStream_t s) {
-  ce_fwd_kernel<<<nparts, 256, 0, s>>>(logits, labels, B, C, ignore_index, label_smoothing,
-                                       reduction, lse, loss, partials, counter, nparts);
+  if (C <= kCeSmallC)
+    ce_fwd_kernel<true><<<nparts, 256, 0, s>>>(logits, labels, B, C, ignore_index, label_smoothing, reduction,
+                                               lse, loss, partials, counter, nparts);
+  else
+    ce_fwd_kernel<false><<<nparts, 256, 0, s>>>(logits, labels, B, C, ignore_index, label_smoothing, reduction,
+                                                lse, loss, partials, counter, nparts);
 }
 
 void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* lse,

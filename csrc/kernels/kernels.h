@@ -43,7 +43,13 @@ void splitk_reduce(const float* slabs, int nslices, int64_t n, float* out, hipSt
 // ---------------------------------------------------------------- cross entropy
 // logits [B, C] fp32; labels int64 [B]; writes lse [B], loss scalar (or per-row for
 // reduction none), denom (number of non-ignored rows) in ws.
-// reduction: 0 none, 1 mean, 2 sum.
+// reduction: 0 none, 1 mean, 2 sum.  nparts = cross_entropy_parts(B, C) workgroups.
+constexpr int kCeSmallC = 32;  // up to this many classes: one lane per row
+inline int cross_entropy_parts(int B, int C) {
+  const int rows_per_block = C <= kCeSmallC ? 256 : 4;
+  const int n = (B + rows_per_block - 1) / rows_per_block;
+  return n < 1 ? 1 : (n > 1024 ? 1024 : n);
+}
 void cross_entropy_fwd(const float* logits, const int64_t* labels, int B, int C, int ignore_index,
                        float label_smoothing, int reduction, float* lse, float* loss,
                        float* partials, unsigned* counter, int nparts, hipStream_t s);
@@ -60,27 +66,27 @@ void cn_pack_weights(const float* w1, const float* w2, const float* w3, const fl
 // F1: conv1 + ReLU + pool1 (x u8 or fp32 [B,28,28]; normalisation fused).
 void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
                   int B, float mean, float inv_std, float in_scale, hipStream_t s);
-// F2: conv2 + ReLU -> r2.
-void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* r2, int B, hipStream_t s);
-// F3: pool2 + conv3 + ReLU + pool3 + fc1 -> logits (+ a3 / argmax for backward).
-void cn_conv3_fc_fwd(const void* r2, const void* packed, const float* b3, const float* bfc, float* logits,
+// F2: conv2 + bias (pre-activation) -> z2 [B,11,11,64].
+void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* z2, int B, hipStream_t s);
+// F3: ReLU + pool2 + conv3 + ReLU + pool3 + fc1 -> logits (+ a3 [B,16,128] / argmax for backward).
+void cn_conv3_fc_fwd(const void* z2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s);
 
-int64_t cn_fc_slab_floats(int B);
-int64_t cn_conv3_slab_floats(int B);
-int64_t cn_conv2_slab_floats(int B);
+// Workspace sizes (floats) of the backward weight-gradient slabs.
+int64_t cn_fc_slab_floats(int B, bool dgrad);
+int64_t cn_conv3_slab_floats(int B, bool dgrad);
+int64_t cn_conv2_slab_floats(int B, bool dgrad);
 int64_t cn_conv1_slab_floats(int B);
-// F3 backward: d3 is a [B,64,128] bf16 workspace; dr2 may be null (skip data grad).
-void cn_conv3_fc_bwd(const void* r2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
-                     const void* packed, void* d3, void* dr2, int B, float* fc_slabs, float* c3_slabs,
+// F3 backward: da3m is a [B,16,128] bf16 workspace; dz2 may be null (skip the data gradient).
+void cn_conv3_fc_bwd(const void* z2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
+                     const void* packed, void* da3m, void* dz2, int B, float* fc_slabs, float* c3_slabs,
                      float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s);
 // F2 backward: da1 may be null.
-void cn_conv2_bwd(const void* a1, const void* r2, const void* dr2, const void* packed, void* da1, int B,
-                  float* slabs, float* dw2, float* db2, hipStream_t s);
-// F1 backward (weights only: the input needs no gradient).
-void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, const void* a1, int B,
-                    float mean, float inv_std, float in_scale, float* slabs, float* dw1, float* db1,
-                    hipStream_t s);
+void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1, int B, float* slabs,
+                  float* dw2, float* db2, hipStream_t s);
+// F1 backward (weights only: the input needs no gradient).  idx1 bytes carry argmax | relu<<2.
+void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,
+                    float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s);
 
 // ---------------------------------------------------------------- data
 // Synthetic MNIST-shaped batch (u8 images + labels) from a counter-based hash (deterministic).

@@ -200,8 +200,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cross_entropy_fwd(const at::Tenso
   check_dtype(labels, at::kLong, "cross_entropy labels");
   RINGDP_CHECK(logits.dim() == 2 && labels.dim() == 1 && labels.size(0) == logits.size(0),
                "cross_entropy: expected logits [B, C] and labels [B]");
+  RINGDP_CHECK(logits.is_contiguous() && labels.is_contiguous(), "cross_entropy: inputs must be contiguous");
   const int B = static_cast<int>(logits.size(0)), C = static_cast<int>(logits.size(1));
-  const int nparts = std::max(1, std::min(256, (B + 63) / 64));
+  const int nparts = kern::cross_entropy_parts(static_cast<int>(B), static_cast<int>(C));
   auto fo = logits.options();
   at::Tensor lse = at::empty({B}, fo);
   at::Tensor loss = reduction == 0 ? at::empty({B}, fo) : at::empty({}, fo);
@@ -300,38 +301,38 @@ at::Tensor cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed, const at
   check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
   check_packed(packed);
   check_f32_out(b2, {64}, "conv2 bias");
-  at::Tensor r2 = at::empty({B, 11, 11, 64}, a1.options());
-  if (B == 0) return r2;
-  kern::cn_conv2_fwd(a1.data_ptr(), packed.data_ptr(), b2.data_ptr<float>(), r2.data_ptr(),
+  at::Tensor z2 = at::empty({B, 11, 11, 64}, a1.options());
+  if (B == 0) return z2;
+  kern::cn_conv2_fwd(a1.data_ptr(), packed.data_ptr(), b2.data_ptr<float>(), z2.data_ptr(),
                      static_cast<int>(B), cur_stream(a1));
-  return r2;
+  return z2;
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& r2,
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& z2,
                                                                const at::Tensor& packed,
                                                                const at::Tensor& b3,
                                                                const at::Tensor& bfc) {
-  const int64_t B = r2.size(0);
-  check_act(r2, {B, 11, 11, 64}, at::kBFloat16, "conv3 input (relu(conv2))");
+  const int64_t B = z2.size(0);
+  check_act(z2, {B, 11, 11, 64}, at::kBFloat16, "conv2 pre-activation z2");
   check_packed(packed);
   check_f32_out(b3, {128}, "conv3 bias");
   check_f32_out(bfc, {10}, "fc1 bias");
-  at::Tensor logits = at::empty({B, 10}, r2.options().dtype(at::kFloat));
-  at::Tensor a3 = at::empty({B, 16, 128}, r2.options());
-  at::Tensor idx3 = at::empty({B, 16, 128}, r2.options().dtype(at::kByte));
+  at::Tensor logits = at::empty({B, 10}, z2.options().dtype(at::kFloat));
+  at::Tensor a3 = at::empty({B, 16, 128}, z2.options());
+  at::Tensor idx3 = at::empty({B, 16, 128}, z2.options().dtype(at::kByte));
   if (B == 0) return {logits, a3, idx3};
-  kern::cn_conv3_fc_fwd(r2.data_ptr(), packed.data_ptr(), b3.data_ptr<float>(), bfc.data_ptr<float>(),
+  kern::cn_conv3_fc_fwd(z2.data_ptr(), packed.data_ptr(), b3.data_ptr<float>(), bfc.data_ptr<float>(),
                         logits.data_ptr<float>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
-                        static_cast<int>(B), cur_stream(r2));
+                        static_cast<int>(B), cur_stream(z2));
   return {logits, a3, idx3};
 }
 
-at::Tensor cn_conv3_fc_bwd(const at::Tensor& r2, const at::Tensor& a3, const at::Tensor& idx3,
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& z2, const at::Tensor& a3, const at::Tensor& idx3,
                            const at::Tensor& wfc, const at::Tensor& dlogits,
-                           const at::Tensor& packed, bool need_dr2, at::Tensor dw3, at::Tensor db3,
+                           const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
                            at::Tensor dwfc, at::Tensor dbfc) {
-  const int64_t B = r2.size(0);
-  check_act(r2, {B, 11, 11, 64}, at::kBFloat16, "conv3 input (relu(conv2))");
+  const int64_t B = z2.size(0);
+  check_act(z2, {B, 11, 11, 64}, at::kBFloat16, "conv2 pre-activation z2");
   check_act(a3, {B, 16, 128}, at::kBFloat16, "pooled conv3");
   check_act(idx3, {B, 16, 128}, at::kByte, "conv3 argmax");
   check_f32_out(wfc, {10, 2048}, "fc1 weight");
@@ -343,33 +344,32 @@ at::Tensor cn_conv3_fc_bwd(const at::Tensor& r2, const at::Tensor& a3, const at:
   check_cuda(dlogits, "logits grad");
   at::Tensor dl = dlogits.to(at::kFloat).contiguous();
   check_shape(dl, {B, 10}, "logits grad");
-  at::Tensor dr2;
-  if (need_dr2) dr2 = at::empty_like(r2);
+  at::Tensor dz2;
+  if (need_dz2) dz2 = at::empty_like(z2);
   if (B == 0) {
     dw3.zero_();
     db3.zero_();
     dwfc.zero_();
     dbfc.zero_();
-    return dr2;
+    return dz2;
   }
   const int bi = static_cast<int>(B);
-  at::Tensor d3 = at::empty({B, 64, 128}, r2.options());
-  at::Tensor fs = at::empty({kern::cn_fc_slab_floats(bi)}, dw3.options());
-  at::Tensor cs = at::empty({kern::cn_conv3_slab_floats(bi)}, dw3.options());
-  kern::cn_conv3_fc_bwd(r2.data_ptr(), a3.data_ptr(), idx3.data_ptr<uint8_t>(), wfc.data_ptr<float>(),
-                        dl.data_ptr<float>(), packed.data_ptr(), d3.data_ptr(),
-                        need_dr2 ? dr2.data_ptr() : nullptr, bi, fs.data_ptr<float>(),
+  at::Tensor da3m = at::empty({B, 16, 128}, z2.options());
+  at::Tensor fs = at::empty({kern::cn_fc_slab_floats(bi, need_dz2)}, dw3.options());
+  at::Tensor cs = at::empty({kern::cn_conv3_slab_floats(bi, need_dz2)}, dw3.options());
+  kern::cn_conv3_fc_bwd(z2.data_ptr(), a3.data_ptr(), idx3.data_ptr<uint8_t>(), wfc.data_ptr<float>(),
+                        dl.data_ptr<float>(), packed.data_ptr(), da3m.data_ptr(),
+                        need_dz2 ? dz2.data_ptr() : nullptr, bi, fs.data_ptr<float>(),
                         cs.data_ptr<float>(), dw3.data_ptr<float>(), db3.data_ptr<float>(),
-                        dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), cur_stream(r2));
-  return dr2;
+                        dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), cur_stream(z2));
+  return dz2;
 }
 
-at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& r2, const at::Tensor& dr2,
-                        const at::Tensor& packed, bool need_da1, at::Tensor dw2, at::Tensor db2) {
+at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::Tensor& packed,
+                        bool need_da1, at::Tensor dw2, at::Tensor db2) {
   const int64_t B = a1.size(0);
   check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
-  check_act(r2, {B, 11, 11, 64}, at::kBFloat16, "relu(conv2)");
-  check_act(dr2, {B, 11, 11, 64}, at::kBFloat16, "relu(conv2) grad");
+  check_act(dz2, {B, 11, 11, 64}, at::kBFloat16, "conv2 output grad");
   check_packed(packed);
   check_f32_out(dw2, {64, 32, 3, 3}, "conv2 dw");
   check_f32_out(db2, {64}, "conv2 db");
@@ -381,22 +381,21 @@ at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& r2, const at::Te
     return da1;
   }
   const int bi = static_cast<int>(B);
-  at::Tensor slabs = at::empty({kern::cn_conv2_slab_floats(bi)}, dw2.options());
-  kern::cn_conv2_bwd(a1.data_ptr(), r2.data_ptr(), dr2.data_ptr(), packed.data_ptr(),
-                     need_da1 ? da1.data_ptr() : nullptr, bi, slabs.data_ptr<float>(),
-                     dw2.data_ptr<float>(), db2.data_ptr<float>(), cur_stream(a1));
+  at::Tensor slabs = at::empty({kern::cn_conv2_slab_floats(bi, need_da1)}, dw2.options());
+  kern::cn_conv2_bwd(a1.data_ptr(), dz2.data_ptr(), packed.data_ptr(), need_da1 ? da1.data_ptr() : nullptr,
+                     bi, slabs.data_ptr<float>(), dw2.data_ptr<float>(), db2.data_ptr<float>(),
+                     cur_stream(a1));
   return da1;
 }
 
-void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
-                    const at::Tensor& a1, at::Tensor dw1, at::Tensor db1, double mean, double std,
-                    double in_scale) {
+void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1, at::Tensor dw1,
+                    at::Tensor db1, double mean, double std, double in_scale) {
   int64_t B;
   bool u8;
   check_input(x, B, u8);
+  RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
   check_act(da1, {B, 13, 13, 32}, at::kBFloat16, "conv1 grad");
   check_act(idx1, {B, 13, 13, 32}, at::kByte, "conv1 argmax");
-  check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv1 pooled");
   check_f32_out(dw1, {32, 1, 5, 5}, "conv1 dw");
   check_f32_out(db1, {32}, "conv1 db");
   if (B == 0) {
@@ -406,10 +405,9 @@ void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor
   }
   const int bi = static_cast<int>(B);
   at::Tensor slabs = at::empty({kern::cn_conv1_slab_floats(bi)}, dw1.options());
-  kern::cn_conv1_wgrad(x.data_ptr(), u8, da1.data_ptr(), idx1.data_ptr<uint8_t>(), a1.data_ptr(), bi,
-                       static_cast<float>(mean), static_cast<float>(1.0 / std),
-                       static_cast<float>(in_scale), slabs.data_ptr<float>(), dw1.data_ptr<float>(),
-                       db1.data_ptr<float>(), cur_stream(x));
+  kern::cn_conv1_wgrad(x.data_ptr(), u8, da1.data_ptr(), idx1.data_ptr<uint8_t>(), bi, static_cast<float>(mean),
+                       static_cast<float>(1.0 / std), static_cast<float>(in_scale), slabs.data_ptr<float>(),
+                       dw1.data_ptr<float>(), db1.data_ptr<float>(), cur_stream(x));
 }
 
 std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,

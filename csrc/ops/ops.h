@@ -58,19 +58,18 @@ std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::T
                                                 const at::Tensor& b1, double mean, double std,
                                                 double in_scale);
 at::Tensor cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed, const at::Tensor& b2);
-std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& r2,
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& z2,
                                                                const at::Tensor& packed,
                                                                const at::Tensor& b3,
                                                                const at::Tensor& bfc);
-at::Tensor cn_conv3_fc_bwd(const at::Tensor& r2, const at::Tensor& a3, const at::Tensor& idx3,
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& z2, const at::Tensor& a3, const at::Tensor& idx3,
                            const at::Tensor& wfc, const at::Tensor& dlogits,
-                           const at::Tensor& packed, bool need_dr2, at::Tensor dw3, at::Tensor db3,
+                           const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
                            at::Tensor dwfc, at::Tensor dbfc);
-at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& r2, const at::Tensor& dr2,
-                        const at::Tensor& packed, bool need_da1, at::Tensor dw2, at::Tensor db2);
-void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1,
-                    const at::Tensor& a1, at::Tensor dw1, at::Tensor db1, double mean, double std,
-                    double in_scale);
+at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::Tensor& packed,
+                        bool need_da1, at::Tensor dw2, at::Tensor db2);
+void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1, at::Tensor dw1,
+                    at::Tensor db1, double mean, double std, double in_scale);
 
 std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,
                                                    int64_t num_classes, int64_t seed,

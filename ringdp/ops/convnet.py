@@ -2,12 +2,13 @@
 
 Forward is three fused blocks (reference layers ref/launch_dist.py:35-41):
 
-* ``_Conv1``      conv1 + ReLU + pool1 (+ fused ToTensor/Normalize for uint8 input) -> a1
-* ``_Conv2Relu``  conv2 + ReLU -> r2 (the overlapping k2/s1 pool2 is NOT applied here)
-* ``_Conv3FC``    pool2 + conv3 + ReLU + pool3 + view + fc1 -> logits
+* ``_Conv1``  conv1 + ReLU + pool1 (+ fused ToTensor/Normalize for uint8 input) -> a1
+* ``_Conv2``  conv2 + bias -> z2 (pre-activation; conv2's ReLU and pool2 belong to the next block)
+* ``_Conv3FC``  ReLU + pool2 + conv3 + ReLU + pool3 + view + fc1 -> logits
 
-Placing pool2 at the start of the third block means its argmax never has to be stored (it is
-recomputed from r2 in backward) and conv2's backward only needs a ReLU mask.  Weights are packed
+Placing conv2's ReLU and the overlapping pool2 at the start of the third block means their
+mask/argmax are never stored (they are recomputed from z2 in backward) and conv2's backward is a
+plain linear-layer backward.  Weights are packed
 once per forward into bf16 MFMA fragments (``C.cn_pack_weights``); the fp32 masters stay the
 parameters.  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
 ``_Conv3FC.backward`` - so ringdp's reducer starts the first bucket all-reduce while conv2/conv1
@@ -28,60 +29,60 @@ class _Conv1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, packed, mean, std, in_scale):
         a1, idx = C.cn_conv1_fwd(x, packed, b, mean, std, in_scale)
-        ctx.save_for_backward(x, a1, idx)
+        ctx.save_for_backward(x, idx)
         ctx.params = (w, b)
         ctx.norm = (mean, std, in_scale)
         return a1
 
     @staticmethod
     def backward(ctx, da1):
-        x, a1, idx = ctx.saved_tensors
+        x, idx = ctx.saved_tensors
         w, b = ctx.params
         need_w, need_b = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
         if not (need_w or need_b):
             return (None,) * 7
         dw, db = grad_buffer(w), grad_buffer(b)
-        C.cn_conv1_wgrad(x, da1.contiguous(), idx, a1, dw, db, *ctx.norm)
+        C.cn_conv1_wgrad(x, da1.contiguous(), idx, dw, db, *ctx.norm)
         return None, (dw if need_w else None), (db if need_b else None), None, None, None, None
 
 
-class _Conv2Relu(torch.autograd.Function):
+class _Conv2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a1, w, b, packed):
-        r2 = C.cn_conv2_fwd(a1, packed, b)
-        ctx.save_for_backward(a1, r2, packed)
+        z2 = C.cn_conv2_fwd(a1, packed, b)
+        ctx.save_for_backward(a1, packed)
         ctx.params = (w, b)
-        return r2
+        return z2
 
     @staticmethod
-    def backward(ctx, dr2):
-        a1, r2, packed = ctx.saved_tensors
+    def backward(ctx, dz2):
+        a1, packed = ctx.saved_tensors
         w, b = ctx.params
         dw, db = grad_buffer(w), grad_buffer(b)
         need_in = ctx.needs_input_grad[0]
-        da1 = C.cn_conv2_bwd(a1, r2, dr2.contiguous(), packed, need_in, dw, db)
+        da1 = C.cn_conv2_bwd(a1, dz2.contiguous(), packed, need_in, dw, db)
         return (da1 if need_in else None, dw if ctx.needs_input_grad[1] else None,
                 db if ctx.needs_input_grad[2] else None, None)
 
 
 class _Conv3FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, r2, w3, b3, wfc, bfc, packed):
-        logits, a3, idx3 = C.cn_conv3_fc_fwd(r2, packed, b3, bfc)
-        ctx.save_for_backward(r2, a3, idx3, wfc, packed)
+    def forward(ctx, z2, w3, b3, wfc, bfc, packed):
+        logits, a3, idx3 = C.cn_conv3_fc_fwd(z2, packed, b3, bfc)
+        ctx.save_for_backward(z2, a3, idx3, wfc, packed)
         ctx.params = (w3, b3, wfc, bfc)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
-        r2, a3, idx3, wfc_saved, packed = ctx.saved_tensors
+        z2, a3, idx3, wfc_saved, packed = ctx.saved_tensors
         w3, b3, wfc, bfc = ctx.params
         dw3, db3, dwfc, dbfc = (grad_buffer(p) for p in (w3, b3, wfc, bfc))
         need_in = ctx.needs_input_grad[0]
-        dr2 = C.cn_conv3_fc_bwd(r2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
+        dz2 = C.cn_conv3_fc_bwd(z2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
                                 dw3, db3, dwfc, dbfc)
         n = ctx.needs_input_grad
-        return (dr2 if need_in else None, dw3 if n[1] else None, db3 if n[2] else None,
+        return (dz2 if need_in else None, dw3 if n[1] else None, db3 if n[2] else None,
                 dwfc if n[3] else None, dbfc if n[4] else None, None)
 
 
@@ -103,5 +104,5 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
     x = x.contiguous()
     packed = pack_weights(conv1, conv2, conv3, fc1)
     a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
-    r2 = _Conv2Relu.apply(a1, conv2.weight, conv2.bias, packed)
-    return _Conv3FC.apply(r2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)
+    z2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
+    return _Conv3FC.apply(z2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)

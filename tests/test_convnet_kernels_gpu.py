@@ -1,8 +1,8 @@
 """Numerics of ringdp's ConvNet HIP kernels against plain PyTorch fp32 references (same ops,
 inputs rounded to bf16 the way the kernels consume them).
 
-Blocks under test (csrc/kernels/convnet.hip): F1 conv1+relu+pool1, F2 conv2+relu,
-F3 pool2+conv3+relu+pool3+fc1, their backward kernels and the weight packer."""
+Blocks under test (csrc/kernels/convnet.hip): F1 conv1+relu+pool1, F2 conv2 (pre-activation),
+F3 relu+pool2+conv3+relu+pool3+fc1, their backward kernels and the weight packer."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -98,8 +98,10 @@ def test_conv1_forward(B, u8):
     assert a1.shape == (B, 13, 13, 32) and a1.dtype == torch.bfloat16
     assert rel_err(a1, ref) < 1e-2
     yw = y.permute(0, 2, 3, 1).reshape(B, 13, 2, 13, 2, 32).permute(0, 1, 3, 5, 2, 4).reshape(B, 13, 13, 32, 4)
-    picked = torch.gather(yw, 4, idx.long().unsqueeze(-1)).squeeze(-1)
+    picked = torch.gather(yw, 4, (idx.long() & 3).unsqueeze(-1)).squeeze(-1)
     assert torch.all((yw.max(-1).values - picked) <= 1e-3 * (1 + yw.abs().max(-1).values))
+    # bit 2 of the argmax byte is the ReLU mask of the pooled value
+    assert torch.equal((idx & 4) != 0, a1.float() > 0)
 
 
 @pytest.mark.parametrize("B", [1, 5, 100, 600])
@@ -108,15 +110,15 @@ def test_conv2_forward(B):
     dev = torch.device("cuda")
     ws = weights(dev, B + 1)
     a1 = torch.relu(torch.randn(B, 13, 13, 32, device=dev)).bfloat16()
-    r2 = C().cn_conv2_fwd(a1, packed(ws), ws[3])
-    ref = F.relu(F.conv2d(a1.permute(0, 3, 1, 2).float(), bf(ws[2]), ws[3])).permute(0, 2, 3, 1)
-    assert r2.shape == (B, 11, 11, 64) and r2.dtype == torch.bfloat16
-    assert rel_err(r2, ref) < 1e-2
+    z2 = C().cn_conv2_fwd(a1, packed(ws), ws[3])
+    ref = F.conv2d(a1.permute(0, 3, 1, 2).float(), bf(ws[2]), ws[3]).permute(0, 2, 3, 1)
+    assert z2.shape == (B, 11, 11, 64) and z2.dtype == torch.bfloat16
+    assert rel_err(z2, ref) < 1e-2
 
 
-def f3_reference(r2, ws):
+def f3_reference(z2, ws):
     w3, b3, wf, bfc = ws[4], ws[5], ws[6], ws[7]
-    a2 = F.max_pool2d(r2.permute(0, 3, 1, 2).float(), 2, 1)
+    a2 = F.max_pool2d(F.relu(z2.permute(0, 3, 1, 2).float()), 2, 1)
     y = F.conv2d(a2, bf(w3), b3)
     a3 = F.max_pool2d(F.relu(y), 2, 2)
     return y, a3, F.linear(a3.reshape(-1, 2048), bf(wf), bfc)
@@ -127,9 +129,9 @@ def test_conv3_fc_forward(B):
     torch.manual_seed(B)
     dev = torch.device("cuda")
     ws = weights(dev, B + 2)
-    r2 = torch.relu(torch.randn(B, 11, 11, 64, device=dev)).bfloat16()
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(r2, packed(ws), ws[5], ws[7])
-    y, a3_ref, logits_ref = f3_reference(r2, ws)
+    z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(z2, packed(ws), ws[5], ws[7])
+    y, a3_ref, logits_ref = f3_reference(z2, ws)
     assert a3.shape == (B, 16, 128) and idx3.shape == (B, 16, 128)
     a3_nchw = a3.view(B, 4, 4, 128).permute(0, 3, 1, 2)
     assert rel_err(a3_nchw, a3_ref) < 1e-2
@@ -138,35 +140,35 @@ def test_conv3_fc_forward(B):
 
 
 @pytest.mark.parametrize("B", [1, 3, 64, 257])
-@pytest.mark.parametrize("need_dr2", [True, False])
-def test_conv3_fc_backward(B, need_dr2):
+@pytest.mark.parametrize("need_dz2", [True, False])
+def test_conv3_fc_backward(B, need_dz2):
     torch.manual_seed(7 + B)
     dev = torch.device("cuda")
     ws = weights(dev, B + 3)
     w3, b3, wf, bfc = ws[4], ws[5], ws[6], ws[7]
-    r2 = torch.relu(torch.randn(B, 11, 11, 64, device=dev)).bfloat16()
+    z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
     pk = packed(ws)
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(r2, pk, b3, bfc)
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(z2, pk, b3, bfc)
     dl = torch.randn(B, 10, device=dev)
     dw3, db3, dwf, dbf = (torch.empty_like(t) for t in (w3, b3, wf, bfc))
-    dr2 = C().cn_conv3_fc_bwd(r2, a3, idx3, wf, dl, pk, need_dr2, dw3, db3, dwf, dbf)
+    dz2 = C().cn_conv3_fc_bwd(z2, a3, idx3, wf, dl, pk, need_dz2, dw3, db3, dwf, dbf)
     # reference: fc backward in fp32, unpool through the kernel's own pool3 argmax
     a3_flat = a3.view(B, 4, 4, 128).permute(0, 3, 1, 2).reshape(B, 2048).float()
     torch.testing.assert_close(dwf, dl.t() @ a3_flat, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(dbf, dl.sum(0), rtol=1e-5, atol=1e-5)
     da3 = (dl @ wf).view(B, 128, 4, 4).permute(0, 2, 3, 1)
     dconv = bf(unpool2x2(da3, idx3.view(B, 4, 4, 128), a3.view(B, 4, 4, 128), 8)).permute(0, 3, 1, 2)
-    r2f = r2.permute(0, 3, 1, 2).float().requires_grad_()
+    z2f = z2.permute(0, 3, 1, 2).float().requires_grad_()
     w3q = bf(w3).requires_grad_()
     b3q = b3.clone().requires_grad_()
-    F.conv2d(F.max_pool2d(r2f, 2, 1), w3q, b3q).backward(dconv)
+    F.conv2d(F.max_pool2d(F.relu(z2f), 2, 1), w3q, b3q).backward(dconv)
     assert rel_err(dw3, w3q.grad) < 5e-3
     assert rel_err(db3, b3q.grad) < 5e-3
-    if need_dr2:
-        assert dr2.shape == (B, 11, 11, 64)
-        assert rel_err(dr2.permute(0, 3, 1, 2), r2f.grad) < 1.5e-2
+    if need_dz2:
+        assert dz2.shape == (B, 11, 11, 64)
+        assert rel_err(dz2.permute(0, 3, 1, 2), z2f.grad) < 1.5e-2
     else:
-        assert dr2 is None
+        assert dz2 is None
 
 
 @pytest.mark.parametrize("B", [1, 3, 64, 257])
@@ -176,11 +178,10 @@ def test_conv2_backward(B):
     ws = weights(dev, B + 4)
     w2, b2 = ws[2], ws[3]
     a1 = torch.relu(torch.randn(B, 13, 13, 32, device=dev)).bfloat16()
-    r2 = torch.relu(torch.randn(B, 11, 11, 64, device=dev)).bfloat16()
-    dr2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
+    dz2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
     dw2, db2 = torch.empty_like(w2), torch.empty_like(b2)
-    da1 = C().cn_conv2_bwd(a1, r2, dr2, packed(ws), True, dw2, db2)
-    dconv = (dr2.float() * (r2.float() > 0)).permute(0, 3, 1, 2)
+    da1 = C().cn_conv2_bwd(a1, dz2, packed(ws), True, dw2, db2)
+    dconv = dz2.float().permute(0, 3, 1, 2)
     x = a1.permute(0, 3, 1, 2).float().requires_grad_()
     wq = bf(w2).requires_grad_()
     bq = b2.clone().requires_grad_()
@@ -201,8 +202,8 @@ def test_conv1_wgrad(B, u8):
     a1, idx = C().cn_conv1_fwd(x, packed(ws), b1, *norm)
     da1 = torch.randn(B, 13, 13, 32, device=dev).bfloat16()
     dw, db = torch.empty_like(w1), torch.empty_like(b1)
-    C().cn_conv1_wgrad(x, da1, idx, a1, dw, db, *norm)
-    dconv = bf(unpool2x2(da1, idx, a1, 26)).permute(0, 3, 1, 2)
+    C().cn_conv1_wgrad(x, da1, idx, dw, db, *norm)
+    dconv = bf(unpool2x2(da1, idx & 3, a1, 26)).permute(0, 3, 1, 2)
     wq = w1.clone().requires_grad_()
     bq = b1.clone().requires_grad_()
     F.conv2d(bf(xn), wq, bq, padding=1).backward(dconv)
@@ -215,15 +216,15 @@ def test_wgrad_deterministic():
     dev = torch.device("cuda")
     ws = weights(dev, 9)
     B = 333
-    r2 = torch.relu(torch.randn(B, 11, 11, 64, device=dev)).bfloat16()
+    z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
     pk = packed(ws)
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(r2, pk, ws[5], ws[7])
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(z2, pk, ws[5], ws[7])
     dl = torch.randn(B, 10, device=dev)
     outs = []
     for _ in range(2):
         g = [torch.empty_like(t) for t in (ws[4], ws[5], ws[6], ws[7])]
-        dr2 = C().cn_conv3_fc_bwd(r2, a3, idx3, ws[6], dl, pk, True, *g)
-        outs.append(g + [dr2])
+        dz2 = C().cn_conv3_fc_bwd(z2, a3, idx3, ws[6], dl, pk, True, *g)
+        outs.append(g + [dz2])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
 
