@@ -26,6 +26,7 @@
 //     im2col gather), split over images into fp32 slabs reduced in a fixed order (deterministic);
 //   * one multi-segment reduction launch per layer backward.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <vector>
 
@@ -1168,6 +1169,15 @@ void cn_conv3_fc_fwd(const void* z2, const void* packed, const float* b3, const 
 // Work split of the role-fused backward launches.  All blocks of a launch are co-resident (one
 // 512-thread block per CU), so dgrad and wgrad blocks are sized to finish together: dgrad does
 // ~2x (conv3) / ~1.25x (conv2) the MFMA work of wgrad per image.
+// Fraction of the CUs given to the dgrad role (RINGDP_C3_DGRAD_FRAC / RINGDP_C2_DGRAD_FRAC override
+// the measured defaults; used for tuning sweeps).
+static double split_frac(const char* env, double dflt) {
+  const char* v = getenv(env);
+  if (!v) return dflt;
+  const double f = atof(v);
+  return f > 0.05 && f < 0.95 ? f : dflt;
+}
+
 static void c3_split(int B, bool dgrad, int& nd, int& ws) {
   const int cus = num_cus();
   if (!dgrad) {
@@ -1175,9 +1185,10 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
     ws = clampi(cdiv(B, 8), 1, cus);
     return;
   }
-  nd = clampi(B, 1, (2 * cus) / 3);
+  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.68);
+  nd = clampi(B, 1, (int)(frac * cus));
   const int per = cdiv(B, nd);
-  ws = clampi(cdiv(B, 2 * per), 1, std::max(1, cus - nd));
+  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
 }
 
 static void c2_split(int B, bool dgrad, int& nd, int& ws) {
@@ -1187,9 +1198,10 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
     ws = clampi(cdiv(B, 8), 1, cus);
     return;
   }
-  nd = clampi(B, 1, (9 * cus) / 16);
+  static const double frac = split_frac("RINGDP_C2_DGRAD_FRAC", 0.62);
+  nd = clampi(B, 1, (int)(frac * cus));
   const int per = cdiv(B, nd);
-  ws = clampi(cdiv(B, per), 1, std::max(1, cus - nd));
+  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
 }
 
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 2 * num_cus()); }
