@@ -366,6 +366,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lr_tensor") = py::none(), py::arg("grad_scale") = py::none());
   m.def("cross_entropy_fwd", &ops::cross_entropy_fwd);
   m.def("cross_entropy_bwd", &ops::cross_entropy_bwd);
+  m.def("gather_augment", &ops::gather_augment, py::arg("x"), py::arg("labels"), py::arg("idx"),
+        py::arg("pad") = 0, py::arg("flip") = false, py::arg("mean") = std::vector<double>{},
+        py::arg("std") = std::vector<double>{}, py::arg("seed") = 0, py::arg("nhwc") = false,
+        py::arg("out_dtype") = at::kFloat);
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);

@@ -89,6 +89,16 @@ void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1
                     float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s);
 
 // ---------------------------------------------------------------- data
+// Gather B samples of a uint8 (N, H, W, C) dataset by index, random-crop (zero pad) + h-flip, then
+// ToTensor + Normalize; out_kind 0 = fp32, 1 = bf16, 2 = uint8 (no normalisation).  Output NCHW
+// (or NHWC when nhwc).  yout[b] = labels[idx[b]] when labels != nullptr.
+struct AugNorm {
+  float mean[4];
+  float inv_std[4];
+};
+void gather_augment(const uint8_t* x, const int64_t* labels, const int64_t* idx, int B, int H, int W, int C,
+                    int pad, bool flip, const AugNorm& nrm, uint64_t seed, bool nhwc, int out_kind, void* out,
+                    int64_t* yout, hipStream_t s);
 // Synthetic MNIST-shaped batch (u8 images + labels) from a counter-based hash (deterministic).
 void synth_u8_images(uint8_t* x, int64_t* labels, int B, int HW, int num_classes, uint64_t seed,
                      hipStream_t s);

@@ -410,6 +410,50 @@ void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor
                        dw1.data_ptr<float>(), db1.data_ptr<float>(), cur_stream(x));
 }
 
+std::tuple<at::Tensor, at::Tensor> gather_augment(const at::Tensor& x, const c10::optional<at::Tensor>& labels,
+                                                  const at::Tensor& idx, int64_t pad, bool flip,
+                                                  std::vector<double> mean, std::vector<double> std,
+                                                  int64_t seed, bool nhwc, at::ScalarType out_dtype) {
+  check_cuda(x, "dataset images");
+  check_dtype(x, at::kByte, "dataset images");
+  RINGDP_CHECK(x.is_contiguous() && (x.dim() == 3 || x.dim() == 4),
+               "dataset images: expected contiguous uint8 (N, H, W) or (N, H, W, C)");
+  check_cuda(idx, "batch indices");
+  check_dtype(idx, at::kLong, "batch indices");
+  RINGDP_CHECK(idx.dim() == 1 && idx.is_contiguous(), "batch indices: expected 1-D contiguous int64");
+  const int64_t H = x.size(1), W = x.size(2), Cc = x.dim() == 4 ? x.size(3) : 1, B = idx.size(0);
+  RINGDP_CHECK(Cc <= 4, "gather_augment: at most 4 channels");
+  RINGDP_CHECK(pad >= 0 && pad < H && pad < W, "gather_augment: bad padding");
+  RINGDP_CHECK(out_dtype == at::kFloat || out_dtype == at::kBFloat16 || out_dtype == at::kByte,
+               "gather_augment: out dtype must be float32, bfloat16 or uint8");
+  kern::AugNorm nrm{};
+  for (int c = 0; c < 4; ++c) {
+    const double m = mean.empty() ? 0.0 : mean[std::min<size_t>(c, mean.size() - 1)];
+    const double sd = std.empty() ? 1.0 : std[std::min<size_t>(c, std.size() - 1)];
+    RINGDP_CHECK(sd != 0.0, "gather_augment: std must be non-zero");
+    nrm.mean[c] = static_cast<float>(m);
+    nrm.inv_std[c] = static_cast<float>(1.0 / sd);
+  }
+  auto opt = x.options().dtype(out_dtype);
+  at::Tensor out = nhwc ? at::empty({B, H, W, Cc}, opt) : at::empty({B, Cc, H, W}, opt);
+  at::Tensor y;
+  const int64_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    check_cuda(*labels, "dataset labels");
+    check_dtype(*labels, at::kLong, "dataset labels");
+    RINGDP_CHECK(labels->is_contiguous() && labels->size(0) == x.size(0), "dataset labels: shape mismatch");
+    y = at::empty({B}, labels->options());
+    lab = labels->data_ptr<int64_t>();
+  }
+  if (B == 0) return {out, y};
+  const int kind = out_dtype == at::kFloat ? 0 : (out_dtype == at::kBFloat16 ? 1 : 2);
+  kern::gather_augment(x.data_ptr<uint8_t>(), lab, idx.data_ptr<int64_t>(), static_cast<int>(B),
+                       static_cast<int>(H), static_cast<int>(W), static_cast<int>(Cc), static_cast<int>(pad), flip,
+                       nrm, static_cast<uint64_t>(seed), nhwc, kind, out.data_ptr(),
+                       lab ? y.data_ptr<int64_t>() : nullptr, cur_stream(x));
+  return {out, y};
+}
+
 std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,
                                                    int64_t num_classes, int64_t seed,
                                                    at::Device device) {

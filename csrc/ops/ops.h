@@ -71,6 +71,12 @@ at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::T
 void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1, at::Tensor dw1,
                     at::Tensor db1, double mean, double std, double in_scale);
 
+// Device input pipeline: gather + random crop/flip + ToTensor/Normalize in one launch.
+std::tuple<at::Tensor, at::Tensor> gather_augment(const at::Tensor& x, const c10::optional<at::Tensor>& labels,
+                                                  const at::Tensor& idx, int64_t pad, bool flip,
+                                                  std::vector<double> mean, std::vector<double> std,
+                                                  int64_t seed, bool nhwc, at::ScalarType out_dtype);
+
 std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t W,
                                                    int64_t num_classes, int64_t seed,
                                                    at::Device device);
