@@ -6,6 +6,7 @@
 
 #include "comm/host_ring.h"
 #include "comm/rccl_pg.h"
+#include "ops/nn_ops.h"
 #include "ops/ops.h"
 #include "reducer/reducer.h"
 #include "store/store.h"
@@ -370,6 +371,26 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad") = 0, py::arg("flip") = false, py::arg("mean") = std::vector<double>{},
         py::arg("std") = std::vector<double>{}, py::arg("seed") = 0, py::arg("nhwc") = false,
         py::arg("out_dtype") = at::kFloat);
+  // generic GEMM / implicit-GEMM conv / NHWC layers
+  m.def("gemm", &ops::gemm, py::arg("a"), py::arg("b"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("lda"),
+        py::arg("ldb"), py::arg("a_row") = false, py::arg("b_row") = false, py::arg("batch") = 1,
+        py::arg("a_bstride") = 0, py::arg("b_bstride") = 0, py::arg("out_bf16") = true,
+        py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("residual") = py::none(),
+        py::arg("preact") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none());
+  m.def("gemm_splitk_f32", &ops::gemm_splitk_f32);
+  m.def("pack_conv_weight", &ops::pack_conv_weight);
+  m.def("conv2d_fwd", &ops::conv2d_fwd);
+  m.def("conv2d_dgrad", &ops::conv2d_dgrad);
+  m.def("conv2d_wgrad", &ops::conv2d_wgrad);
+  m.def("nchw_to_nhwc", &ops::nchw_to_nhwc);
+  m.def("bn_fwd_train", &ops::bn_fwd_train);
+  m.def("bn_fwd_eval", &ops::bn_fwd_eval);
+  m.def("bn_bwd", &ops::bn_bwd);
+  m.def("maxpool2d_fwd", &ops::maxpool2d_fwd);
+  m.def("maxpool2d_bwd", &ops::maxpool2d_bwd);
+  m.def("avgpool_fwd", &ops::avgpool_fwd);
+  m.def("avgpool_bwd", &ops::avgpool_bwd);
+  m.def("add_bf16", &ops::add_bf16);
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);

@@ -1,0 +1,494 @@
+// Generic bf16 MFMA GEMM core for CDNA4 (gfx950) with gather loaders and fused epilogues.
+//
+// Serves the deep-model families of BASELINE.json (ResNet-18/50 convolutions as implicit GEMM,
+// ViT-B/16 linear layers and attention batches; SURVEY.md §2.4 U14 "cuDNN conv / cuBLAS addmm").
+//
+//   C[b][m][n] = epilogue( sum_k A(b, m, k) * B(b, n, k) )
+//
+// * Operands are described by LOADERS.  A loader is either K-contiguous (8 consecutive k of one
+//   row per 16-B vector: dense row-major, NHWC im2col, transposed-conv gather) or ROW-contiguous
+//   (8 consecutive rows of one k: dense column-major, the dY^T / im2col^T operands of a weight
+//   gradient).  K-contiguous tiles are staged [row][k] and read with ds_read_b128; row-contiguous
+//   tiles are staged [k][row] and read with ds_read_b64_tr_b16 - the transposed LDS read replaces
+//   any explicit transpose pass.
+// * 128x128 block tile, BK = 64, 256 threads = 2x2 waves of 64x64 (4x4 v_mfma_f32_16x16x32_bf16
+//   tiles each), LDS double buffer with register-staged prefetch of the next k-tile (one barrier
+//   per k-tile), XCD-aware block->tile mapping (blocks of one XCD walk the same A row-panel).
+// * The MFMA is issued as C^T = B * A^T so every lane ends with 4 CONSECUTIVE n of one m: the
+//   epilogue stores 8-byte (bf16) / 16-byte (fp32) runs, applies bias / ReLU / GELU / residual,
+//   optionally keeps the pre-activation, and emits deterministic per-channel sum / sum-of-squares
+//   partials (batch-norm statistics) or split-K fp32 partials.
+#include <algorithm>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace ringdp {
+namespace kern {
+
+using namespace ringdp::dev;
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int KPAD = BK + 8;         // K-contiguous stage row (bf16)
+constexpr int RPAD = 128 + 8;        // row-contiguous stage row (bf16)
+constexpr int STAGE_ELEMS = 128 * KPAD;  // >= BK * RPAD: both orientations fit
+static_assert(STAGE_ELEMS >= BK * RPAD, "stage size");
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// ------------------------------------------------------------------ loaders
+struct DenseLoader {  // element (b, r, k): K-contig p[b*bs + r*ld + k]; row-contig p[b*bs + k*ld + r]
+  const bf16* p;
+  int64_t ld, bs;
+  int R, K;
+};
+
+template <bool kRowContig>
+struct Dense {
+  static constexpr bool kRow = kRowContig;
+  DenseLoader d;
+  struct Row {
+    const bf16* base;
+    int r;
+  };
+  __device__ __forceinline__ Row row(int b, int r) const { return Row{d.p + (int64_t)b * d.bs, r}; }
+  __device__ __forceinline__ bf16x8 load(const Row& rw, int k) const {
+    if (rw.r >= d.R || k >= d.K) return zero_bf16x8();
+    if (kRowContig) return *reinterpret_cast<const bf16x8*>(rw.base + (int64_t)k * d.ld + rw.r);
+    return *reinterpret_cast<const bf16x8*>(rw.base + (int64_t)rw.r * d.ld + k);
+  }
+};
+
+// im2col of an NHWC input for the forward conv: row m = (n, p, q), k = (r, s, c) - K-contiguous
+struct ConvFwdA {
+  static constexpr bool kRow = false;
+  const bf16* x;
+  ConvGeom g;
+  int M, Kd;
+  struct Row {
+    const bf16* base;
+    int h0, w0;
+    bool ok;
+  };
+  __device__ __forceinline__ Row row(int, int m) const {
+    if (m >= M) return Row{x, 0, 0, false};
+    const int pq = g.P * g.Q;
+    const int n = m / pq, rem = m - n * pq, p = rem / g.Q, q = rem - p * g.Q;
+    return Row{x + (int64_t)n * g.H * g.W * g.C, p * g.stride - g.pad, q * g.stride - g.pad, true};
+  }
+  __device__ __forceinline__ bf16x8 load(const Row& rw, int k) const {
+    if (!rw.ok || k >= Kd) return zero_bf16x8();
+    const int rs = k / g.C, c = k - rs * g.C, r = rs / g.S, s = rs - r * g.S;
+    const int h = rw.h0 + r * g.dil, w = rw.w0 + s * g.dil;
+    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(rw.base + ((int64_t)h * g.W + w) * g.C + c);
+  }
+};
+
+// transposed-conv gather of dY for the data gradient: row m = (n, h, w) of the INPUT,
+// k = (r, s, kout): dY[n][(h + pad - r*dil)/stride][(w + pad - s*dil)/stride][kout..] when exact
+struct ConvDgradA {
+  static constexpr bool kRow = false;
+  const bf16* dy;
+  ConvGeom g;
+  int M, Kd;
+  struct Row {
+    const bf16* base;
+    int hp, wp;
+    bool ok;
+  };
+  __device__ __forceinline__ Row row(int, int m) const {
+    if (m >= M) return Row{dy, 0, 0, false};
+    const int hw = g.H * g.W;
+    const int n = m / hw, rem = m - n * hw, h = rem / g.W, w = rem - h * g.W;
+    return Row{dy + (int64_t)n * g.P * g.Q * g.K, h + g.pad, w + g.pad, true};
+  }
+  __device__ __forceinline__ bf16x8 load(const Row& rw, int k) const {
+    if (!rw.ok || k >= Kd) return zero_bf16x8();
+    const int rs = k / g.K, ko = k - rs * g.K, r = rs / g.S, s = rs - r * g.S;
+    const int ph = rw.hp - r * g.dil, pw = rw.wp - s * g.dil;
+    if (ph < 0 || pw < 0) return zero_bf16x8();
+    const int p = ph / g.stride, q = pw / g.stride;
+    if (p * g.stride != ph || q * g.stride != pw || p >= g.P || q >= g.Q) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(rw.base + ((int64_t)p * g.Q + q) * g.K + ko);
+  }
+};
+
+// weight-gradient B operand: rows = filter taps kk = (r, s, c), k = output position m = (n, p, q):
+// element = x[n][p*stride - pad + r*dil][q*stride - pad + s*dil][c]; 8 consecutive kk = 8 channels
+struct ConvWgradB {
+  static constexpr bool kRow = true;
+  const bf16* x;
+  ConvGeom g;
+  int Mpos, Kd;  // Mpos = N*P*Q (the GEMM's K), Kd = R*S*C (rows)
+  struct Row {
+    int roff, soff, c;
+    bool ok;
+  };
+  __device__ __forceinline__ Row row(int, int kk) const {
+    if (kk >= Kd) return Row{0, 0, 0, false};
+    const int rs = kk / g.C, c = kk - rs * g.C, r = rs / g.S, s = rs - r * g.S;
+    return Row{r * g.dil - g.pad, s * g.dil - g.pad, c, true};
+  }
+  __device__ __forceinline__ bf16x8 load(const Row& rw, int m) const {
+    if (!rw.ok || m >= Mpos) return zero_bf16x8();
+    const int pq = g.P * g.Q;
+    const int n = m / pq, rem = m - n * pq, p = rem / g.Q, q = rem - p * g.Q;
+    const int h = p * g.stride + rw.roff, w = q * g.stride + rw.soff;
+    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(x + (((int64_t)n * g.H + h) * g.W + w) * g.C + rw.c);
+  }
+};
+
+// ------------------------------------------------------------------ stage helpers
+// K-contiguous operand: tile [128 rows][64 k] = 1024 vectors; thread t owns rows (t>>3) + 32i and
+// the k-vector (t & 7).  Row-contiguous: tile [64 k][128 rows]; thread t owns the row-vector (t & 15)
+// and k = (t >> 4) + 16i.
+template <class L>
+struct Stager {
+  typename L::Row rows[4];
+  bf16x8 v[4];
+  __device__ __forceinline__ void init(const L& ld, int b, int tile_r0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (L::kRow)
+        rows[i] = ld.row(b, tile_r0 + 8 * (tid & 15));
+      else
+        rows[i] = ld.row(b, tile_r0 + (tid >> 3) + 32 * i);
+    }
+  }
+  __device__ __forceinline__ void load(const L& ld, int k0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (L::kRow)
+        v[i] = ld.load(rows[0], k0 + (tid >> 4) + 16 * i);
+      else
+        v[i] = ld.load(rows[i], k0 + 8 * (tid & 7));
+    }
+  }
+  __device__ __forceinline__ void store(bf16* s, int tid) const {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (L::kRow)
+        *reinterpret_cast<bf16x8*>(s + ((tid >> 4) + 16 * i) * RPAD + 8 * (tid & 15)) = v[i];
+      else
+        *reinterpret_cast<bf16x8*>(s + ((tid >> 3) + 32 * i) * KPAD + 8 * (tid & 7)) = v[i];
+    }
+  }
+};
+
+// MFMA operand fragment for rows r0..r0+15 at k-step kk (32-wide) from a staged tile.
+template <bool kRow>
+__device__ __forceinline__ bf16x8 frag(const bf16* s, int r0, int kk, int lane) {
+  if (!kRow) return *reinterpret_cast<const bf16x8*>(s + (r0 + (lane & 15)) * KPAD + kk * 32 + 8 * (lane >> 4));
+  const int q = (lane & 15) >> 2, p = lane & 3, kb = kk * 32 + 8 * (lane >> 4);
+  const bf16x4 lo = lds_read_tr16(s + (kb + q) * RPAD + r0 + 4 * p);
+  const bf16x4 hi = lds_read_tr16(s + (kb + 4 + q) * RPAD + r0 + 4 * p);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// ------------------------------------------------------------------ the kernel
+template <class LA, class LB>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue ep, int M, int N, int K,
+                                                      int tiles_m, int tiles_n, int splits, int k_per_split) {
+  __shared__ __attribute__((aligned(16))) bf16 smem[2][2][STAGE_ELEMS];  // [stage][A|B]
+  __shared__ float red[2][2][BN];                                      // BN-stat cross-wave reduction
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  // block -> (batch*split, tile_m, tile_n); tiles of one XCD walk one A row-panel
+  const int per_z = tiles_m * tiles_n;
+  const int zid = blockIdx.y;
+  const int t = xcd_remap(blockIdx.x, per_z);
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int b = zid / splits, split = zid - b * splits;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
+  const int nkt = (kend - kbeg + BK - 1) / BK;
+
+  Stager<LA> sa;
+  Stager<LB> sb;
+  sa.init(la, b, m0, tid);
+  sb.init(lb, b, n0, tid);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero_f32x4();
+  if (nkt > 0) {
+    sa.load(la, kbeg, tid);
+    sb.load(lb, kbeg, tid);
+    sa.store(smem[0][0], tid);
+    sb.store(smem[0][1], tid);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      sa.load(la, kbeg + (kt + 1) * BK, tid);
+      sb.load(lb, kbeg + (kt + 1) * BK, tid);
+    }
+    const bf16* As = smem[cur][0];
+    const bf16* Bs = smem[cur][1];
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag<LA::kRow>(As, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag<LB::kRow>(Bs, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // C^T tile
+    }
+    if (more) {
+      sa.store(smem[cur ^ 1][0], tid);
+      sb.store(smem[cur ^ 1][1], tid);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue: lane holds C[m][n..n+3], m = m0 + wm*64 + 16i + (lane&15),
+  //                  n = n0 + wn*64 + 16j + 4*(lane>>4)
+  const int mrow = m0 + wm * 64 + (lane & 15);
+  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+  if (ep.mode == GemmEpilogue::kSplitK) {
+    float* out = ep.partial + ((int64_t)zid) * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mrow + 16 * i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = ncol + 16 * j;
+        if (n + 3 < N) {
+          *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) out[(int64_t)m * N + n + e] = acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
+  float ssum[4][4], ssq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ssum[j][e] = ssq[j][e] = 0.f;
+  const int64_t cb = (int64_t)b * ep.c_bstride;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mrow + 16 * i;
+    const bool mok = m < M;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = ncol + 16 * j;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] * ep.alpha;
+        if (ep.bias && n + e < N) v[e] += ep.bias[n + e];
+      }
+      const int64_t off = cb + (int64_t)m * ep.ldc + n;
+      const bool full = mok && n + 3 < N;
+      if (ep.preact && mok) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < N) static_cast<bf16*>(ep.preact)[off + e] = (bf16)v[e];
+      }
+      if (ep.residual && mok) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < N) v[e] += (float)static_cast<const bf16*>(ep.residual)[off + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
+      }
+      if (mok) {
+        if (ep.out_bf16) {
+          bf16* c = static_cast<bf16*>(ep.C) + off;
+          if (full) {
+            *reinterpret_cast<bf16x4*>(c) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < N) c[e] = (bf16)v[e];
+          }
+          // statistics of what was stored (bf16-rounded), like a norm layer reading it back
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (float)(bf16)v[e];
+        } else {
+          float* c = static_cast<float*>(ep.C) + off;
+          if (full) {
+            *reinterpret_cast<f32x4*>(c) = f32x4{v[0], v[1], v[2], v[3]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < N) c[e] = v[e];
+          }
+        }
+        if (ep.stats) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ssum[j][e] += v[e];
+            ssq[j][e] += v[e] * v[e];
+          }
+        }
+      }
+    }
+  }
+  if (!ep.stats) return;
+  // per-channel partials of this block's 128 rows: reduce over the 16 m-lanes, then the 2 m-waves
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        ssum[j][e] += __shfl_xor(ssum[j][e], o, 64);
+        ssq[j][e] += __shfl_xor(ssq[j][e], o, 64);
+      }
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int nl = wn * 64 + 16 * j + 4 * (lane >> 4) + e;
+        red[wm][0][nl] = ssum[j][e];
+        red[wm][1][nl] = ssq[j][e];
+      }
+  }
+  __syncthreads();
+  if (tid < BN) {
+    const int n = n0 + tid;
+    if (n < N) {
+      float* st = ep.stats + ((int64_t)b * tiles_m + tm) * 2 * N;
+      st[n] = red[0][0][tid] + red[1][0][tid];
+      st[N + n] = red[0][1][tid] + red[1][1][tid];
+    }
+  }
+}
+
+template <class LA, class LB>
+void launch(const LA& la, const LB& lb, const GemmEpilogue& ep, int batch, int M, int N, int K, int splits,
+            hipStream_t s) {
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+  splits = std::max(1, splits);
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (K + kps - 1) / kps;
+  dim3 grid(tiles_m * tiles_n, batch * splits);
+  gemm_kernel<LA, LB><<<grid, 256, 0, s>>>(la, lb, ep, M, N, K, tiles_m, tiles_n, splits, kps);
+}
+
+// ------------------------------------------------------------------ reductions
+// out[i] = sum_s part[s][i] (fixed order); optional KRSC -> KCRS permutation for conv weights.
+__global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict__ part, int S, int64_t n,
+                                                         float* __restrict__ out, int perm_k, int perm_c,
+                                                         int perm_rs) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float a = 0.f;
+  for (int s = 0; s < S; ++s) a += part[(int64_t)s * n + i];
+  if (perm_rs > 0) {  // i = ko*(RS*C) + rs*C + c  ->  ko*(C*RS) + c*RS + rs
+    const int64_t per = (int64_t)perm_rs * perm_c;
+    const int64_t ko = i / per, rem = i - ko * per, rs = rem / perm_c, c = rem - rs * perm_c;
+    out[ko * per + c * perm_rs + rs] = a;
+  } else {
+    out[i] = a;
+  }
+  (void)perm_k;
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const float* __restrict__ part, int tiles, int N,
+                                                                float* __restrict__ sums) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f, q = 0.f;
+  for (int t = 0; t < tiles; ++t) {
+    a += part[(int64_t)t * 2 * N + n];
+    q += part[(int64_t)t * 2 * N + N + n];
+  }
+  sums[n] = a;
+  sums[N + n] = q;
+}
+
+}  // namespace
+
+// ================================================================== launchers
+void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K, const GemmEpilogue& ep,
+               int splits, hipStream_t s) {
+  const DenseLoader da{static_cast<const bf16*>(A.p), A.ld, A.bstride, M, K};
+  const DenseLoader db{static_cast<const bf16*>(B.p), B.ld, B.bstride, N, K};
+  if (!A.row_contig && !B.row_contig)
+    launch(Dense<false>{da}, Dense<false>{db}, ep, batch, M, N, K, splits, s);
+  else if (!A.row_contig && B.row_contig)
+    launch(Dense<false>{da}, Dense<true>{db}, ep, batch, M, N, K, splits, s);
+  else if (A.row_contig && !B.row_contig)
+    launch(Dense<true>{da}, Dense<false>{db}, ep, batch, M, N, K, splits, s);
+  else
+    launch(Dense<true>{da}, Dense<true>{db}, ep, batch, M, N, K, splits, s);
+}
+
+void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {
+  const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  const ConvFwdA la{static_cast<const bf16*>(x), g, M, Kd};
+  const DenseLoader db{static_cast<const bf16*>(w_krsc), Kd, 0, g.K, Kd};
+  launch(la, Dense<false>{db}, ep, 1, M, g.K, Kd, 1, s);
+}
+
+void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {
+  const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
+  const ConvDgradA la{static_cast<const bf16*>(dy), g, M, Kd};
+  const DenseLoader db{static_cast<const bf16*>(w_crsk), Kd, 0, g.C, Kd};
+  launch(la, Dense<false>{db}, ep, 1, M, g.C, Kd, 1, s);
+}
+
+void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,
+                     hipStream_t s) {
+  const int Mpos = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  // C[ko][kk] = sum_m dY[m][ko] * X(m, kk):  A = dY^T (row-contiguous, ld = K), B = im2col^T
+  const DenseLoader da{static_cast<const bf16*>(dy), g.K, 0, g.K, Mpos};
+  const ConvWgradB lb{static_cast<const bf16*>(x), g, Mpos, Kd};
+  GemmEpilogue ep{};
+  ep.mode = GemmEpilogue::kSplitK;
+  ep.partial = partial;
+  const int tiles_m = (g.K + BM - 1) / BM, tiles_n = (Kd + BN - 1) / BN;
+  (void)tiles_m;
+  (void)tiles_n;
+  int kps = (Mpos + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  const int S = (Mpos + kps - 1) / kps;
+  launch(Dense<true>{da}, lb, ep, 1, g.K, Kd, Mpos, S, s);
+  const int64_t n = (int64_t)g.K * Kd;
+  splitk_sum_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(partial, S, n, dw_kcrs, g.K, g.C, g.R * g.S);
+}
+
+int conv_wgrad_splits(const ConvGeom& g, int cus) {
+  const int Mpos = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  const int tiles = ((g.K + BM - 1) / BM) * ((Kd + BN - 1) / BN);
+  const int want = std::max(1, (2 * cus + tiles - 1) / tiles);
+  const int max_split = std::max(1, Mpos / (4 * BK));
+  return std::min(want, max_split);
+}
+
+void splitk_sum(const float* part, int S, int64_t n, float* out, hipStream_t s) {
+  splitk_sum_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(part, S, n, out, 0, 0, 0);
+}
+
+void bn_stats_finalize(const float* part, int tiles, int N, float* sums, hipStream_t s) {
+  bn_stats_finalize_kernel<<<(N + 255) / 256, 256, 0, s>>>(part, tiles, N, sums);
+}
+
+int gemm_tiles_m(int M) { return (M + BM - 1) / BM; }
+
+}  // namespace kern
+}  // namespace ringdp

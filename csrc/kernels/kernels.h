@@ -88,6 +88,71 @@ void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1
 void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,
                     float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s);
 
+// ---------------------------------------------------------------- generic GEMM / implicit-GEMM conv
+// (csrc/kernels/gemm.hip)  C[b][m][n] = epilogue(sum_k A(b, m, k) * B(b, n, k)), bf16 in, fp32 acc.
+struct GemmOperand {
+  const void* p;     // bf16
+  int64_t ld;        // row stride (K-contiguous) or k stride (row-contiguous)
+  int64_t bstride;   // batch stride (elements)
+  bool row_contig;   // false: element (r, k) at p[r*ld + k]; true: at p[k*ld + r]
+};
+struct GemmEpilogue {
+  enum Mode : int { kStore = 0, kSplitK = 1 };
+  int mode;
+  void* C;            // fp32 or bf16 [b][m][ldc]
+  int64_t ldc, c_bstride;
+  bool out_bf16;
+  float alpha;
+  const float* bias;  // [N] or null
+  int act;            // 0 none, 1 relu, 2 gelu (erf)
+  void* preact;       // bf16 copy of the value before residual/activation (same layout as C) or null
+  const void* residual;  // bf16, same layout as C, added before the activation
+  float* stats;       // [b][tiles_m][2][N] per-channel sum / sumsq partials of the stored C, or null
+  float* partial;     // split-K fp32 partials [b*splits][M][N]
+};
+struct ConvGeom {
+  int N, H, W, C;   // input NHWC (C padded to a multiple of 8)
+  int K, R, S;      // output channels, filter
+  int P, Q;         // output spatial
+  int stride, pad, dil;
+};
+void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K, const GemmEpilogue& ep,
+               int splits, hipStream_t s);
+void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
+void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
+void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,
+                     hipStream_t s);
+int conv_wgrad_splits(const ConvGeom& g, int cus);
+void splitk_sum(const float* part, int S, int64_t n, float* out, hipStream_t s);
+void bn_stats_finalize(const float* part, int tiles, int N, float* sums, hipStream_t s);
+int gemm_tiles_m(int M);
+
+// ---------------------------------------------------------------- NHWC network layers (nn.hip)
+void pack_conv_weight(const float* w_kcrs, int K, int C, int R, int S, int Cp, void* w_krsc, void* w_crsk,
+                      hipStream_t s);
+void nchw_to_nhwc_pad(const void* x, bool x_bf16, int N, int C, int H, int W, int Cp, void* y, hipStream_t s);
+// batch norm (training): sums = [sum(C), sumsq(C)] over M rows -> scale/shift (+ saved mean/invstd,
+// running-stat update), then y = act(z*scale + shift [+ res])
+void bn_prepare(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+                float momentum, float* running_mean, float* running_var, float* scale_shift, float* save,
+                hipStream_t s);
+void bn_act_fwd(const void* z, const float* scale_shift, const void* res, bool relu, int64_t M, int C, void* y,
+                hipStream_t s);
+// backward part 1: g = dy * (y > 0 if relu); partial sums of g and g*zhat per channel -> part
+int bn_bwd_parts(int64_t M);
+void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
+                   float* part, void* g_out, hipStream_t s);
+// part 2: dgamma/dbeta and dz = scale*(g - mean(g) - zhat*mean(g*zhat))/..., plus d(residual) = g
+void bn_bwd_apply(const float* part, int nparts, const void* g, const void* z, const float* save, const float* gamma,
+                  int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s);
+void maxpool_fwd(const void* x, int N, int H, int W, int C, int k, int stride, int pad, int P, int Q, void* y,
+                 uint8_t* arg, hipStream_t s);
+void maxpool_bwd(const void* dy, const uint8_t* arg, int N, int H, int W, int C, int k, int stride, int pad, int P,
+                 int Q, void* dx, hipStream_t s);
+void avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t s);
+void avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t s);
+void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s);
+
 // ---------------------------------------------------------------- data
 // Gather B samples of a uint8 (N, H, W, C) dataset by index, random-crop (zero pad) + h-flip, then
 // ToTensor + Normalize; out_kind 0 = fp32, 1 = bf16, 2 = uint8 (no normalisation).  Output NCHW

@@ -1,0 +1,374 @@
+// NHWC bf16 network layers around the implicit-GEMM convolutions (ResNet family; SURVEY.md §2.4
+// "U14 ATen BN, add, avgpool (W2)"; ref/example_mp.py:50 resnet18).
+//
+// Batch norm is split MI355X-first: the per-channel sum / sum-of-squares come out of the producing
+// conv's GEMM epilogue (gemm.hip, deterministic per-tile partials), so BN forward is ONE
+// elementwise pass that also fuses the residual add and the ReLU; BN backward is one reduction pass
+// (ReLU mask + the two channel sums) and one apply pass that also emits the residual branch's grad.
+// Every kernel moves 16-B vectors of 8 channels.
+#include <algorithm>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace ringdp {
+namespace kern {
+
+using namespace ringdp::dev;
+
+namespace {
+
+inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + per_block - 1) / per_block, cap));
+}
+
+__global__ __launch_bounds__(256) void pack_conv_weight_kernel(const float* __restrict__ w, int K, int C, int R,
+                                                               int S, int Cp, bf16* __restrict__ krsc,
+                                                               bf16* __restrict__ crsk) {
+  const int64_t total = (int64_t)K * R * S * Cp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    // e indexes KRSC(padded): e = ((k*R + r)*S + s)*Cp + c
+    const int c = (int)(e % Cp);
+    int64_t t = e / Cp;
+    const int s = (int)(t % S);
+    t /= S;
+    const int r = (int)(t % R);
+    const int k = (int)(t / R);
+    const float v = c < C ? w[(((int64_t)k * C + c) * R + r) * S + s] : 0.f;
+    krsc[e] = (bf16)v;
+    crsk[(((int64_t)c * R + r) * S + s) * K + k] = (bf16)v;
+  }
+}
+
+template <bool BF>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restrict__ x, int N, int C, int H, int W,
+                                                           int Cp, bf16* __restrict__ y) {
+  const int64_t total = (int64_t)N * H * W * Cp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c = (int)(e % Cp);
+    const int64_t pix = e / Cp;  // n*H*W + h*W + w
+    const int64_t n = pix / ((int64_t)H * W), hw = pix - n * H * W;
+    float v = 0.f;
+    if (c < C) {
+      const int64_t src = (n * C + c) * H * W + hw;
+      v = BF ? (float)static_cast<const bf16*>(x)[src] : static_cast<const float*>(x)[src];
+    }
+    y[e] = (bf16)v;
+  }
+}
+
+__global__ void bn_prepare_kernel(const float* __restrict__ sums, int64_t M, int C, const float* __restrict__ gamma,
+                                  const float* __restrict__ beta, float eps, float momentum,
+                                  float* __restrict__ running_mean, float* __restrict__ running_var,
+                                  float* __restrict__ ss, float* __restrict__ save) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const double inv = 1.0 / (double)M;
+  const double mean = sums[c] * inv;
+  const double var = fmax(sums[C + c] * inv - mean * mean, 0.0);  // biased (normalisation)
+  const float invstd = (float)(1.0 / sqrt(var + eps));
+  const float sc = gamma[c] * invstd;
+  ss[c] = sc;
+  ss[C + c] = beta[c] - (float)mean * sc;
+  save[c] = (float)mean;
+  save[C + c] = invstd;
+  if (running_mean) {
+    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict__ z, const float* __restrict__ ss,
+                                                         const bf16* __restrict__ res, int relu, int64_t nvec, int C,
+                                                         bf16* __restrict__ y) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((v * 8) % C);
+    const bf16x8 zv = reinterpret_cast<const bf16x8*>(z)[v];
+    bf16x8 rv = zero_bf16x8();
+    if (res) rv = reinterpret_cast<const bf16x8*>(res)[v];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float f = (float)zv[j] * ss[c0 + j] + ss[C + c0 + j];
+      if (res) f += (float)rv[j];
+      if (relu) f = fmaxf(f, 0.f);
+      o[j] = (bf16)f;
+    }
+    reinterpret_cast<bf16x8*>(y)[v] = o;
+  }
+}
+
+// Rows are split over workgroups; each thread owns one 8-channel vector column (C/8 columns, C <= 2048)
+// and walks rows with a stride, accumulating in fp32; partials [part][2][C] (deterministic).
+inline int64_t bn_rows_per_part(int64_t M) { return std::max<int64_t>(64, (M + 1023) / 1024); }
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
+                                                            const bf16* __restrict__ z, const float* __restrict__ save,
+                                                            int relu, int64_t M, int C, int64_t rows_per_part,
+                                                            float* __restrict__ part, bf16* __restrict__ g_out) {
+  const int cv = C / 8;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_part;
+  const int64_t r1 = std::min<int64_t>(M, r0 + rows_per_part);
+  const int lanes_per_row = cv;
+  const int rows_in_flight = max(1, 256 / lanes_per_row);
+  const int col = threadIdx.x % lanes_per_row, rsub = threadIdx.x / lanes_per_row;
+  __shared__ float red[2][256];
+  float sg[8], sgz[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] = sgz[j] = 0.f;
+  if (rsub < rows_in_flight && col < lanes_per_row) {
+    float mean[8], inv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mean[j] = save[col * 8 + j];
+      inv[j] = save[C + col * 8 + j];
+    }
+    for (int64_t r = r0 + rsub; r < r1; r += rows_in_flight) {
+      const int64_t v = r * cv + col;
+      const bf16x8 d = reinterpret_cast<const bf16x8*>(dy)[v];
+      const bf16x8 zz = reinterpret_cast<const bf16x8*>(z)[v];
+      bf16x8 yy = zero_bf16x8();
+      if (relu) yy = reinterpret_cast<const bf16x8*>(y)[v];
+      bf16x8 go;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (relu && !((float)yy[j] > 0.f)) ? 0.f : (float)d[j];
+        go[j] = (bf16)g;
+        const float gq = (float)go[j];
+        sg[j] += gq;
+        sgz[j] += gq * ((float)zz[j] - mean[j]) * inv[j];
+      }
+      reinterpret_cast<bf16x8*>(g_out)[v] = go;
+    }
+  }
+  // combine the rows_in_flight partial rows for each column (fixed order)
+  __syncthreads();
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x] = sg[j];
+    red[1][threadIdx.x] = sgz[j];
+    __syncthreads();
+    if (threadIdx.x < lanes_per_row) {
+      float a = 0.f, q = 0.f;
+      for (int k = 0; k < rows_in_flight; ++k) {
+        a += red[0][k * lanes_per_row + threadIdx.x];
+        q += red[1][k * lanes_per_row + threadIdx.x];
+      }
+      part[((int64_t)blockIdx.x * 2) * C + threadIdx.x * 8 + j] = a;
+      part[((int64_t)blockIdx.x * 2 + 1) * C + threadIdx.x * 8 + j] = q;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_final_kernel(const float* __restrict__ part, int nparts, int C,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float a = 0.f, q = 0.f;
+  for (int p = 0; p < nparts; ++p) {
+    a += part[(int64_t)p * 2 * C + c];
+    q += part[((int64_t)p * 2 + 1) * C + c];
+  }
+  dbeta[c] = a;
+  dgamma[c] = q;
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
+                                                           const float* __restrict__ save,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ dgamma,
+                                                           const float* __restrict__ dbeta, int64_t M, int C,
+                                                           int64_t nvec, bf16* __restrict__ dz) {
+  const float invM = 1.f / (float)M;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const int c0 = (int)((v * 8) % C);
+    const bf16x8 gv = reinterpret_cast<const bf16x8*>(g)[v];
+    const bf16x8 zv = reinterpret_cast<const bf16x8*>(z)[v];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      const float inv = save[C + c];
+      const float zh = ((float)zv[j] - save[c]) * inv;
+      const float d = gamma[c] * inv * ((float)gv[j] - dbeta[c] * invM - zh * dgamma[c] * invM);
+      o[j] = (bf16)d;
+    }
+    reinterpret_cast<bf16x8*>(dz)[v] = o;
+  }
+}
+
+// max pooling (ResNet stem 3x3 s2 p1), NHWC; arg = window offset (dy*k + dx) of the first max
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
+                                                          int k, int stride, int pad, int P, int Q,
+                                                          bf16* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int64_t total = (int64_t)N * P * Q * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    int64_t t = e / C;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float best = -INFINITY;
+    int ba = 0;
+    for (int dy = 0; dy < k; ++dy) {
+      const int h = p * stride - pad + dy;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int dx = 0; dx < k; ++dx) {
+        const int w = q * stride - pad + dx;
+        if ((unsigned)w >= (unsigned)W) continue;
+        const float v = (float)x[(((int64_t)n * H + h) * W + w) * C + c];
+        if (v > best) {
+          best = v;
+          ba = dy * k + dx;
+        }
+      }
+    }
+    y[e] = (bf16)best;
+    arg[e] = (uint8_t)ba;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                          int N, int H, int W, int C, int k, int stride, int pad,
+                                                          int P, int Q, bf16* __restrict__ dx) {
+  const int64_t total = (int64_t)N * H * W * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    int64_t t = e / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float g = 0.f;
+    // windows p with p*stride - pad <= h <= p*stride - pad + k - 1 (gather: deterministic)
+    const int p_lo = max(0, (h + pad - k + stride) / stride), p_hi = min(P - 1, (h + pad) / stride);
+    const int q_lo = max(0, (w + pad - k + stride) / stride), q_hi = min(Q - 1, (w + pad) / stride);
+    for (int p = p_lo; p <= p_hi; ++p)
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int dyy = h - (p * stride - pad), dxx = w - (q * stride - pad);
+        if (dyy < 0 || dyy >= k || dxx < 0 || dxx >= k) continue;
+        const int64_t o = (((int64_t)n * P + p) * Q + q) * C + c;
+        if (arg[o] == dyy * k + dxx) g += (float)dy[o];
+      }
+    dx[e] = (bf16)g;
+  }
+}
+
+// global average pool NHWC [N][HW][C] -> [N][C] (fp32 accumulation); one thread per (n, c)
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16* __restrict__ x, int N, int HW, int C,
+                                                          bf16* __restrict__ y) {
+  const int64_t total = (int64_t)N * C;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t n = e / C;
+    const int c = (int)(e % C);
+    float a = 0.f;
+    for (int i = 0; i < HW; ++i) a += (float)x[(n * HW + i) * C + c];
+    y[e] = (bf16)(a / (float)HW);
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16* __restrict__ dy, int N, int HW, int C,
+                                                          bf16* __restrict__ dx) {
+  const int64_t total = (int64_t)N * HW * C;
+  const float s = 1.f / (float)HW;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int c = (int)(e % C);
+    const int64_t n = e / ((int64_t)HW * C);
+    dx[e] = (bf16)((float)dy[n * C + c] * s);
+  }
+}
+
+__global__ __launch_bounds__(256) void add_bf16_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
+                                                       int64_t nvec, bf16* __restrict__ y) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const bf16x8 x = reinterpret_cast<const bf16x8*>(a)[v], z = reinterpret_cast<const bf16x8*>(b)[v];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)((float)x[j] + (float)z[j]);
+    reinterpret_cast<bf16x8*>(y)[v] = o;
+  }
+}
+
+}  // namespace
+
+void pack_conv_weight(const float* w, int K, int C, int R, int S, int Cp, void* krsc, void* crsk, hipStream_t s) {
+  const int64_t total = (int64_t)K * R * S * Cp;
+  pack_conv_weight_kernel<<<grid_for(total), 256, 0, s>>>(w, K, C, R, S, Cp, static_cast<bf16*>(krsc),
+                                                          static_cast<bf16*>(crsk));
+}
+
+void nchw_to_nhwc_pad(const void* x, bool x_bf16, int N, int C, int H, int W, int Cp, void* y, hipStream_t s) {
+  const int64_t total = (int64_t)N * H * W * Cp;
+  if (x_bf16)
+    nchw_to_nhwc_kernel<true><<<grid_for(total), 256, 0, s>>>(x, N, C, H, W, Cp, static_cast<bf16*>(y));
+  else
+    nchw_to_nhwc_kernel<false><<<grid_for(total), 256, 0, s>>>(x, N, C, H, W, Cp, static_cast<bf16*>(y));
+}
+
+void bn_prepare(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+                float momentum, float* running_mean, float* running_var, float* scale_shift, float* save,
+                hipStream_t s) {
+  bn_prepare_kernel<<<(C + 255) / 256, 256, 0, s>>>(sums, M, C, gamma, beta, eps, momentum, running_mean,
+                                                    running_var, scale_shift, save);
+}
+
+void bn_act_fwd(const void* z, const float* ss, const void* res, bool relu, int64_t M, int C, void* y,
+                hipStream_t s) {
+  const int64_t nvec = M * C / 8;
+  bn_act_fwd_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(z), ss, static_cast<const bf16*>(res),
+                                                   relu ? 1 : 0, nvec, C, static_cast<bf16*>(y));
+}
+
+int bn_bwd_parts(int64_t M) {
+  const int64_t rpp = bn_rows_per_part(M);
+  return (int)((M + rpp - 1) / rpp);
+}
+
+void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
+                   float* part, void* g_out, hipStream_t s) {
+  bn_bwd_reduce_kernel<<<bn_bwd_parts(M), 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(y),
+                                                       static_cast<const bf16*>(z), save, relu ? 1 : 0, M, C,
+                                                       bn_rows_per_part(M), part, static_cast<bf16*>(g_out));
+}
+
+void bn_bwd_apply(const float* part, int nparts, const void* g, const void* z, const float* save, const float* gamma,
+                  int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s) {
+  bn_bwd_final_kernel<<<(C + 255) / 256, 256, 0, s>>>(part, nparts, C, dgamma, dbeta);
+  const int64_t nvec = M * C / 8;
+  bn_bwd_apply_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save,
+                                                     gamma, dgamma, dbeta, M, C, nvec, static_cast<bf16*>(dz));
+}
+
+void maxpool_fwd(const void* x, int N, int H, int W, int C, int k, int stride, int pad, int P, int Q, void* y,
+                 uint8_t* arg, hipStream_t s) {
+  const int64_t total = (int64_t)N * P * Q * C;
+  maxpool_fwd_kernel<<<grid_for(total), 256, 0, s>>>(static_cast<const bf16*>(x), N, H, W, C, k, stride, pad, P, Q,
+                                                     static_cast<bf16*>(y), arg);
+}
+
+void maxpool_bwd(const void* dy, const uint8_t* arg, int N, int H, int W, int C, int k, int stride, int pad, int P,
+                 int Q, void* dx, hipStream_t s) {
+  const int64_t total = (int64_t)N * H * W * C;
+  maxpool_bwd_kernel<<<grid_for(total), 256, 0, s>>>(static_cast<const bf16*>(dy), arg, N, H, W, C, k, stride, pad,
+                                                     P, Q, static_cast<bf16*>(dx));
+}
+
+void avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t s) {
+  avgpool_fwd_kernel<<<grid_for((int64_t)N * C), 256, 0, s>>>(static_cast<const bf16*>(x), N, HW, C,
+                                                              static_cast<bf16*>(y));
+}
+
+void avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t s) {
+  avgpool_bwd_kernel<<<grid_for((int64_t)N * HW * C), 256, 0, s>>>(static_cast<const bf16*>(dy), N, HW, C,
+                                                                   static_cast<bf16*>(dx));
+}
+
+void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s) {
+  add_bf16_kernel<<<grid_for(n / 8), 256, 0, s>>>(static_cast<const bf16*>(a), static_cast<const bf16*>(b), n / 8,
+                                                  static_cast<bf16*>(y));
+}
+
+}  // namespace kern
+}  // namespace ringdp

@@ -1,0 +1,42 @@
+// Tensor-level wrappers: generic GEMM, implicit-GEMM conv, NHWC layers (see nn_ops.cpp).
+#pragma once
+
+#include <ATen/ATen.h>
+
+#include <tuple>
+
+namespace ringdp {
+namespace ops {
+
+at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+                bool a_row, bool b_row, int64_t batch, int64_t a_bstride, int64_t b_bstride, bool out_bf16,
+                const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& residual,
+                const c10::optional<at::Tensor>& preact, double alpha, const c10::optional<at::Tensor>& out);
+at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, int64_t K, int64_t lda,
+                           int64_t ldb, bool a_row, bool b_row, int64_t splits, const at::Tensor& out);
+std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t cpad);
+std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w_krsc, int64_t stride,
+                                              int64_t pad, int64_t dil, bool want_stats);
+at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t H, int64_t W, int64_t stride,
+                        int64_t pad, int64_t dil);
+void conv2d_wgrad(const at::Tensor& dz, const at::Tensor& x, at::Tensor dw, int64_t stride, int64_t pad, int64_t dil);
+at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad);
+std::tuple<at::Tensor, at::Tensor> bn_fwd_train(const at::Tensor& z, const at::Tensor& sums, const at::Tensor& gamma,
+                                                const at::Tensor& beta, const c10::optional<at::Tensor>& running_mean,
+                                                const c10::optional<at::Tensor>& running_var, double eps,
+                                                double momentum, const c10::optional<at::Tensor>& residual,
+                                                bool relu);
+at::Tensor bn_fwd_eval(const at::Tensor& z, const at::Tensor& scale_shift, const c10::optional<at::Tensor>& residual,
+                       bool relu);
+std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& z,
+                                          const at::Tensor& save, const at::Tensor& gamma, bool relu,
+                                          at::Tensor dgamma, at::Tensor dbeta);
+std::tuple<at::Tensor, at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
+at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W, int64_t k,
+                         int64_t stride, int64_t pad);
+at::Tensor avgpool_fwd(const at::Tensor& x);
+at::Tensor avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W);
+at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b);
+
+}  // namespace ops
+}  // namespace ringdp

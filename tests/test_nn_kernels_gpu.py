@@ -1,0 +1,169 @@
+"""Generic MFMA GEMM, implicit-GEMM conv (fwd / dgrad / wgrad), BN, pooling kernels vs PyTorch fp32
+references (inputs rounded to bf16 the way the kernels consume them)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def C():
+    import ringdp
+
+    return ringdp._C
+
+
+def bf(t):
+    return t.bfloat16().float()
+
+
+def rel(a, b):
+    return float((a.float() - b.float()).abs().max() / (b.float().abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("a_row,b_row", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("M,N,K,batch", [(200, 136, 320, 1), (64, 256, 64, 3), (1000, 72, 776, 1)])
+def test_gemm_layouts(a_row, b_row, M, N, K, batch):
+    torch.manual_seed(M + N + K)
+    dev = "cuda"
+    A = torch.randn(batch, M, K, device=dev).bfloat16()
+    B = torch.randn(batch, N, K, device=dev).bfloat16()
+    a_store = A.transpose(1, 2).contiguous() if a_row else A
+    b_store = B.transpose(1, 2).contiguous() if b_row else B
+    lda = M if a_row else K
+    ldb = N if b_row else K
+    out = C().gemm(a_store, b_store, M, N, K, lda, ldb, a_row, b_row, batch, M * K, N * K, False)
+    ref = A.float() @ B.float().transpose(1, 2)
+    assert rel(out, ref) < 2e-3
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_gemm_epilogue(act):
+    torch.manual_seed(act)
+    dev = "cuda"
+    M, N, K = 300, 264, 128
+    A = torch.randn(M, K, device=dev).bfloat16()
+    B = torch.randn(N, K, device=dev).bfloat16()
+    bias = torch.randn(N, device=dev)
+    res = torch.randn(M, N, device=dev).bfloat16()
+    pre = torch.empty(M, N, device=dev).bfloat16()
+    out = C().gemm(A, B, M, N, K, K, K, False, False, 1, 0, 0, True, bias, act, res, pre, 0.5)
+    z = 0.5 * (A.float() @ B.float().t()) + bias
+    assert rel(pre.view(M, N), z) < 1e-2
+    y = z + res.float()
+    y = {0: y, 1: torch.relu(y), 2: F.gelu(y)}[act]
+    assert rel(out.view(M, N), y) < 1e-2
+
+
+def test_gemm_splitk():
+    torch.manual_seed(5)
+    M, N, K = 64, 200, 4096
+    A = torch.randn(K, M, device="cuda").bfloat16()  # row-contiguous A: (m, k) at k*M + m
+    B = torch.randn(K, N, device="cuda").bfloat16()
+    out = torch.empty(M, N, device="cuda")
+    C().gemm_splitk_f32(A, B, M, N, K, M, N, True, True, 8, out)
+    ref = A.float().t() @ B.float()
+    assert rel(out, ref) < 2e-3
+
+
+CONV_CASES = [
+    # N, C, H, K, R, stride, pad
+    (4, 3, 32, 64, 7, 2, 3),   # ResNet stem (C padded to 8)
+    (2, 64, 8, 64, 3, 1, 1),
+    (3, 64, 9, 128, 3, 2, 1),
+    (2, 256, 7, 64, 1, 1, 0),
+    (2, 64, 8, 128, 1, 2, 0),
+]
+
+
+def _nhwc(x, cp):
+    n, c, h, w = x.shape
+    out = torch.zeros(n, h, w, cp, device=x.device)
+    out[..., :c] = x.permute(0, 2, 3, 1)
+    return out.bfloat16().contiguous()
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    N, Cin, H, K, R, stride, pad = case
+    torch.manual_seed(sum(case))
+    dev = "cuda"
+    cp = (Cin + 7) // 8 * 8
+    x = torch.randn(N, Cin, H, H, device=dev)
+    w = torch.randn(K, Cin, R, R, device=dev) * 0.1
+    krsc, crsk = C().pack_conv_weight(w, cp)
+    xh = _nhwc(x, cp)
+    z, sums = C().conv2d_fwd(xh, krsc, stride, pad, 1, True)
+    xr = bf(x).requires_grad_()
+    wr = bf(w).requires_grad_()
+    ref = F.conv2d(xr, wr, stride=stride, padding=pad)
+    assert rel(z.permute(0, 3, 1, 2), ref) < 1e-2
+    zf = z.float().reshape(-1, K)
+    torch.testing.assert_close(sums[0], zf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(sums[1], (zf * zf).sum(0), rtol=1e-3, atol=1e-1)
+    dz = torch.randn_like(ref).bfloat16()
+    ref.backward(dz.float())
+    dzh = dz.permute(0, 2, 3, 1).contiguous()
+    dx = C().conv2d_dgrad(dzh, crsk, H, H, stride, pad, 1)
+    assert rel(dx[..., :Cin].permute(0, 3, 1, 2), xr.grad) < 1e-2
+    dw = torch.empty_like(w)
+    C().conv2d_wgrad(dzh, xh, dw, stride, pad, 1)
+    assert rel(dw, wr.grad) < 5e-3
+
+
+@pytest.mark.parametrize("relu,resid", [(True, False), (True, True), (False, False)])
+def test_batchnorm_fwd_bwd(relu, resid):
+    torch.manual_seed(int(relu) * 2 + int(resid))
+    dev = "cuda"
+    N, H, Cc = 6, 7, 64
+    z = (torch.randn(N, H, H, Cc, device=dev) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(Cc, device=dev) + 0.5
+    beta = torch.randn(Cc, device=dev) * 0.1
+    rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    res = torch.randn(N, H, H, Cc, device=dev).bfloat16() if resid else None
+    zf = z.float().reshape(-1, Cc)
+    sums = torch.stack([zf.sum(0), (zf * zf).sum(0)])
+    y, save = C().bn_fwd_train(z, sums, gamma, beta, rm, rv, 1e-5, 0.1, res, relu)
+    # reference in NCHW fp32
+    zr = z.float().permute(0, 3, 1, 2).requires_grad_()
+    g_ = gamma.clone().requires_grad_()
+    b_ = beta.clone().requires_grad_()
+    rm2, rv2 = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
+    out = F.batch_norm(zr, rm2, rv2, g_, b_, training=True, momentum=0.1, eps=1e-5)
+    if resid:
+        resr = res.float().permute(0, 3, 1, 2).requires_grad_()
+        out = out + resr
+    if relu:
+        out = torch.relu(out)
+    assert rel(y.permute(0, 3, 1, 2), out) < 1e-2
+    torch.testing.assert_close(rm, rm2, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv, rv2, rtol=1e-3, atol=1e-3)
+    dy = torch.randn_like(out).bfloat16()
+    out.backward(dy.float())
+    dgamma, dbeta = torch.empty_like(gamma), torch.empty_like(beta)
+    dz, g = C().bn_bwd(dy.permute(0, 2, 3, 1).contiguous(), y, z, save, gamma, relu, dgamma, dbeta)
+    assert rel(dz.permute(0, 3, 1, 2), zr.grad) < 2e-2
+    assert rel(dgamma, g_.grad) < 1e-2
+    assert rel(dbeta, b_.grad) < 1e-2
+    if resid:
+        assert rel(g.permute(0, 3, 1, 2), resr.grad) < 1e-2
+
+
+def test_pools():
+    torch.manual_seed(0)
+    x = torch.randn(3, 17, 17, 64, device="cuda").bfloat16()
+    y, arg = C().maxpool2d_fwd(x, 3, 2, 1)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_()
+    ref = F.max_pool2d(xr, 3, 2, 1)
+    torch.testing.assert_close(y.float().permute(0, 3, 1, 2), ref)
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    dx = C().maxpool2d_bwd(dy.permute(0, 2, 3, 1).contiguous(), arg, 17, 17, 3, 2, 1)
+    assert rel(dx.permute(0, 3, 1, 2), xr.grad) < 1e-2
+    a = torch.randn(4, 7, 7, 128, device="cuda").bfloat16()
+    ya = C().avgpool_fwd(a)
+    torch.testing.assert_close(ya.float(), a.float().mean((1, 2)), rtol=1e-2, atol=1e-2)
+    dya = torch.randn(4, 128, device="cuda").bfloat16()
+    dxa = C().avgpool_bwd(dya, 7, 7)
+    torch.testing.assert_close(dxa.float(), (dya.float() / 49).view(4, 1, 1, 128).expand(4, 7, 7, 128), rtol=1e-2,
+                               atol=1e-3)
