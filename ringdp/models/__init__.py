@@ -1,4 +1,5 @@
 """ringdp.models - the reference's model families, MI355X-native."""
 from .convnet import ConvNet  # noqa: F401
+from .resnet import ResNet, resnet18, resnet34, resnet50  # noqa: F401
 
-__all__ = ["ConvNet"]
+__all__ = ["ConvNet", "ResNet", "resnet18", "resnet34", "resnet50"]

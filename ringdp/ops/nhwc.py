@@ -1,0 +1,136 @@
+"""Autograd Functions for NHWC bf16 conv nets on ringdp's implicit-GEMM kernels (ResNet family).
+
+Reference layers: torchvision ``resnet18`` as used by ``ref/example_mp.py:50`` /
+``ref/example_launch.py:26`` (SURVEY.md §2.2 R2, §2.6 K30+).  The fused unit is
+``conv -> BatchNorm (batch statistics) [-> + residual] [-> ReLU]``:
+
+* forward: one implicit-GEMM launch writes the conv output z (bf16) AND the per-channel
+  sum / sum-of-squares partials from its epilogue; one elementwise launch applies the normalisation,
+  the residual add and the ReLU;
+* backward: one reduction launch (ReLU mask, the two channel sums, the residual branch's gradient),
+  one apply launch (dz), then the data-gradient GEMM (transposed-conv gather) and the
+  weight-gradient GEMM (split-K over output positions, fixed-order reduction that also converts
+  KRSC back to the parameter's KCRS layout).
+
+Weights stay fp32 masters in PyTorch layout (state_dict-compatible with torchvision); each forward
+packs them once to bf16 KRSC (forward) and CRSK (data gradient).
+"""
+from __future__ import annotations
+
+import torch
+
+from .._native import C
+from . import grad_buffer
+
+
+def _cpad(c: int) -> int:
+    return (c + 7) // 8 * 8
+
+
+def to_nhwc(x: torch.Tensor) -> torch.Tensor:
+    """NCHW fp32/bf16 images -> NHWC bf16 with channels padded to a multiple of 8 (no gradient)."""
+    return C.nchw_to_nhwc(x.contiguous(), _cpad(x.shape[1]))
+
+
+class ConvBNAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, stride: int, pad: int, relu: bool,
+                training: bool, momentum: float, eps: float):
+        krsc, crsk = C.pack_conv_weight(w, x.shape[-1])
+        if training:
+            z, sums = C.conv2d_fwd(x, krsc, stride, pad, 1, True)
+            y, save = C.bn_fwd_train(z, sums, gamma, beta, running_mean, running_var, eps, momentum, residual, relu)
+        else:
+            z, _ = C.conv2d_fwd(x, krsc, stride, pad, 1, False)
+            scale = gamma * torch.rsqrt(running_var + eps)
+            ss = torch.stack([scale, beta - running_mean * scale]).contiguous()
+            y = C.bn_fwd_eval(z, ss, residual, relu)
+            save = ss
+        ctx.save_for_backward(x, z, y, save, crsk)
+        ctx.params = (w, gamma, beta)
+        ctx.cfg = (stride, pad, relu, residual is not None, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, z, y, save, crsk = ctx.saved_tensors
+        w, gamma, beta = ctx.params
+        stride, pad, relu, has_res, training = ctx.cfg
+        if not training:
+            raise RuntimeError("ConvBNAct: backward through eval-mode batch norm is not supported")
+        dgamma, dbeta = grad_buffer(gamma), grad_buffer(beta)
+        dz, g = C.bn_bwd(dy.contiguous(), y, z, save, gamma, relu, dgamma, dbeta)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = C.conv2d_dgrad(dz, crsk, x.shape[1], x.shape[2], stride, pad, 1)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = grad_buffer(w)
+            C.conv2d_wgrad(dz, x, dw, stride, pad, 1)
+        dres = g if (has_res and ctx.needs_input_grad[4]) else None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+
+
+class MaxPoolNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k: int, stride: int, pad: int):
+        y, arg = C.maxpool2d_fwd(x, k, stride, pad)
+        ctx.save_for_backward(arg)
+        ctx.cfg = (x.shape[1], x.shape[2], k, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        H, W, k, s, p = ctx.cfg
+        return C.maxpool2d_bwd(dy.contiguous(), arg, H, W, k, s, p), None, None, None
+
+
+def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
+    if t.shape[0] == rows:
+        return t.contiguous()
+    out = torch.zeros((rows,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    out[: t.shape[0]] = t
+    return out
+
+
+class AvgPoolLinear(torch.autograd.Function):
+    """Global average pool (NHWC bf16) + fully connected head -> fp32 logits."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        n, h, wd, c = x.shape
+        pooled = C.avgpool_fwd(x)  # [N, C] bf16
+        ncls = w.shape[0]
+        npad = _cpad(ncls)
+        wb = _pad_rows(w.detach().to(torch.bfloat16), npad)
+        logits = C.gemm(pooled, wb, n, npad, c, c, c, False, False, 1, 0, 0, False, _pad_rows(b.detach(), npad))
+        ctx.save_for_backward(pooled, wb)
+        ctx.params = (w, b)
+        ctx.cfg = (h, wd, ncls, npad)
+        logits = logits.view(n, npad)
+        return logits if npad == ncls else logits[:, :ncls].contiguous()
+
+    @staticmethod
+    def backward(ctx, dl):
+        pooled, wb = ctx.saved_tensors
+        w, b = ctx.params
+        h, wd, ncls, npad = ctx.cfg
+        n, c = pooled.shape
+        n8 = _cpad(n)  # the weight-gradient GEMM reduces over the batch: K % 8 == 0
+        dlp = torch.zeros(n8, npad, device=dl.device, dtype=torch.bfloat16)
+        dlp[:n, :ncls] = dl
+        # d(pooled)[n][c] = sum_j dl[n][j] W[j][c]:  A = dl (K-contig over classes), B = W^T (row-contig)
+        dpooled = C.gemm(dlp, wb, n, c, npad, npad, c, False, True, 1, 0, 0, True)
+        dx = C.avgpool_bwd(dpooled.view(n, c), h, wd)
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            # dW[j][c] = sum_n dl[n][j] pooled[n][c]:  A = dl^T (row-contig), B = pooled^T (row-contig)
+            full = torch.empty(npad, c, device=dl.device, dtype=torch.float32)
+            C.gemm_splitk_f32(dlp, _pad_rows(pooled, n8), npad, c, n8, npad, c, True, True, max(1, n8 // 256), full)
+            dw = grad_buffer(w)
+            dw.copy_(full[:ncls])
+        if ctx.needs_input_grad[2]:
+            db = grad_buffer(b)
+            db.copy_(dl.float().sum(0))
+        return dx, dw, db

@@ -167,3 +167,97 @@ def test_pools():
     dxa = C().avgpool_bwd(dya, 7, 7)
     torch.testing.assert_close(dxa.float(), (dya.float() / 49).view(4, 1, 1, 128).expand(4, 7, 7, 128), rtol=1e-2,
                                atol=1e-3)
+
+
+def _cos(a, b):
+    return float(F.cosine_similarity(a.reshape(1, -1).float(), b.reshape(1, -1).float()))
+
+
+class _RoundBF16(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+def _emulate_bf16(model):
+    """Round weights once and every conv / BN / ReLU output (and its gradient) to bf16, the points
+    where the fused NHWC kernels round - so only accumulation order differs from the oracle."""
+    for mod in model.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.weight.data = mod.weight.data.bfloat16().float()
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.BatchNorm2d, torch.nn.ReLU)):
+            mod.register_forward_hook(lambda m, i, o: _RoundBF16.apply(o))
+
+
+@pytest.mark.parametrize("kind", ["basic", "basic_ds", "bottleneck_ds", "bottleneck"])
+def test_resnet_block_matches_aten(kind):
+    """One residual block, same input to both paths: isolates kernel error from the chaotic
+    amplification of rounding differences that a deep random-init BN network shows."""
+    import copy
+
+    from ringdp.models.resnet import BasicBlock, Bottleneck, conv1x1
+
+    torch.manual_seed(1)
+    nn = torch.nn
+    if kind == "basic":
+        blk = BasicBlock(64, 64)
+    elif kind == "basic_ds":
+        blk = BasicBlock(64, 128, 2, nn.Sequential(conv1x1(64, 128, 2), nn.BatchNorm2d(128)))
+    elif kind == "bottleneck_ds":
+        blk = Bottleneck(64, 64, 2, nn.Sequential(conv1x1(64, 256, 2), nn.BatchNorm2d(256)))
+    else:
+        blk = Bottleneck(256, 64)
+    blk = blk.cuda()
+    for mod in blk.modules():
+        if isinstance(mod, nn.Conv2d):
+            mod.weight.data = mod.weight.data.bfloat16().float()
+    ref = copy.deepcopy(blk)
+    _emulate_bf16(ref)
+    cin = 256 if kind == "bottleneck" else 64
+    x = torch.randn(16, cin, 14, 14, device="cuda").bfloat16().float()
+    xh = x.permute(0, 2, 3, 1).contiguous().bfloat16().requires_grad_()
+    xr = x.clone().requires_grad_()
+    out = blk.forward_nhwc(xh)
+    out_ref = ref(xr)
+    assert _cos(out.detach().permute(0, 3, 1, 2), out_ref.detach()) > 0.9999
+    g = torch.randn_like(out_ref).bfloat16()
+    out.backward(g.permute(0, 2, 3, 1).contiguous())
+    out_ref.backward(g.float())
+    assert _cos(xh.grad.permute(0, 3, 1, 2), xr.grad) > 0.999
+    for (n, p), (_, q) in zip(blk.named_parameters(), ref.named_parameters()):
+        assert _cos(p.grad, q.grad) > 0.999, n
+
+
+@pytest.mark.parametrize("arch,res", [("resnet18", 32), ("resnet50", 64)])
+def test_resnet_matches_aten(arch, res):
+    """Whole network, zero-init residual branches (a stable, near-identity net at init)."""
+    import copy
+
+    from ringdp import models
+
+    torch.manual_seed(0)
+    m = getattr(models, arch)(num_classes=10, zero_init_residual=True).cuda()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d):
+            mod.weight.data = mod.weight.data.bfloat16().float()
+    ref = copy.deepcopy(m)
+    _emulate_bf16(ref)
+    x = torch.randn(32, 3, res, res, device="cuda")
+    y = torch.randint(0, 10, (32,), device="cuda")
+    out = m(x)
+    out_ref = ref.reference_forward(x)
+    assert out.shape == (32, 10)
+    assert _cos(out.detach(), out_ref.detach()) > 0.995
+    F.cross_entropy(out, y).backward()
+    F.cross_entropy(out_ref, y).backward()
+    cos = {n: _cos(p.grad, q.grad) for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters())
+           if q.grad is not None and float(q.grad.abs().max()) > 0}
+    bad = {n: round(c, 4) for n, c in cos.items() if c < 0.98}
+    assert not bad, bad
+    for (n, b), (_, c) in zip(m.named_buffers(), ref.named_buffers()):
+        if b.dtype.is_floating_point:
+            torch.testing.assert_close(b, c, rtol=5e-2, atol=5e-2), n
