@@ -29,14 +29,26 @@ import torch
 
 METRIC = "images/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; DDP scaling efficiency"
 
+# Extra BASELINE.json configs (--model): the deeper families, synthetic data of the named shape.
+MODELS = {
+    "convnet": dict(batch=4096, shape=(1, 28, 28), lr=1e-4, momentum=0.0, nesterov=False, wd=0.0,
+                    desc="MNIST ConvNet (ref/launch_dist.py; 113,674 params)"),
+    "resnet18": dict(batch=256, shape=(3, 32, 32), lr=0.02, momentum=0.9, nesterov=True, wd=1e-4,
+                     desc="ResNet-18 CIFAR-shape (ref/example_mp.py; torchvision tree, 11,181,642 params)"),
+    "resnet50": dict(batch=256, shape=(3, 224, 224), lr=0.02, momentum=0.9, nesterov=True, wd=1e-4,
+                     desc="ResNet-50 ImageNet-shape (25,557,032 params)"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch-per-rank", type=int, default=int(os.environ.get("RINGDP_BENCH_BATCH", "4096")))
-    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--model", type=str, default="convnet", choices=sorted(MODELS))
+    ap.add_argument("--batch-per-rank", type=int, default=None,
+                    help="per-rank batch (default: 4096 for the ConvNet, RINGDP_BENCH_BATCH overrides)")
+    ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--first-bucket-mb", type=float, default=None)
     ap.add_argument("--comm-hook", type=str, default="allreduce", choices=["allreduce", "bf16_compress", "fp16_compress"])
@@ -50,7 +62,7 @@ def main():
     args = parse()
     import ringdp
     import ringdp.distributed as dist
-    from ringdp.models import ConvNet
+    from ringdp import models
     from ringdp.nn import CrossEntropyLoss
     from ringdp.optim import SGD
     from ringdp.parallel import DistributedDataParallel as DDP
@@ -68,18 +80,30 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but world size is {world}; reporting n_gpus={world}", file=sys.stderr)
     dev = torch.device("cuda", local_rank)
-    B = args.batch_per_rank
+    spec = MODELS[args.model]
+    B = args.batch_per_rank or int(os.environ.get("RINGDP_BENCH_BATCH", spec["batch"]))
+    lr = args.lr if args.lr is not None else spec["lr"]
 
     torch.manual_seed(0)
-    model = ConvNet().to(dev)
+    if args.model == "convnet":
+        model = models.ConvNet().to(dev)
+    else:
+        model = getattr(models, args.model)(num_classes=1000 if args.model == "resnet50" else 10).to(dev)
     ddp = DDP(model, device_ids=[local_rank], output_device=local_rank, bucket_cap_mb=args.bucket_mb,
               first_bucket_mb=args.first_bucket_mb)
     if args.comm_hook != "allreduce":
         ddp._set_builtin_hook(args.comm_hook)
     crit = CrossEntropyLoss()
-    opt = SGD(ddp.parameters(), lr=args.lr)
+    opt = SGD(ddp.parameters(), lr=lr, momentum=spec["momentum"], nesterov=spec["nesterov"],
+              weight_decay=spec["wd"])
 
-    pool = [ringdp._C.synth_u8_images(B, 28, 28, 10, 1000 * rank + i, dev) for i in range(args.pool)]
+    if args.model == "convnet":
+        pool = [ringdp._C.synth_u8_images(B, 28, 28, 10, 1000 * rank + i, dev) for i in range(args.pool)]
+    else:
+        g = torch.Generator(device=dev).manual_seed(1000 * rank)
+        ncls = 1000 if args.model == "resnet50" else 10
+        pool = [(torch.randn((B,) + spec["shape"], device=dev, generator=g),
+                 torch.randint(0, ncls, (B,), device=dev, generator=g)) for _ in range(min(args.pool, 4))]
     static_x = torch.empty_like(pool[0][0])
     static_y = torch.empty_like(pool[0][1])
 
@@ -100,19 +124,19 @@ def main():
     if use_graph:
         # eager warmup (bucket rebuild happens at iteration 1), then capture
         for i in range(2):
-            x, y = pool[i % args.pool]
+            x, y = pool[i % len(pool)]
             step_on(x, y)
         static_x.copy_(pool[0][0])
         static_y.copy_(pool[0][1])
         graph = StepGraph(static_step, warmup=2).capture()
         for i in range(n_warm):
-            x, y = pool[i % args.pool]
+            x, y = pool[i % len(pool)]
             static_x.copy_(x, non_blocking=True)
             static_y.copy_(y, non_blocking=True)
             graph.replay()
     else:
         for i in range(n_warm):
-            x, y = pool[i % args.pool]
+            x, y = pool[i % len(pool)]
             step_on(x, y)
 
     torch.cuda.synchronize()
@@ -121,7 +145,7 @@ def main():
     t0 = time.perf_counter()
     loss = None
     for i in range(args.steps):
-        x, y = pool[i % args.pool]
+        x, y = pool[i % len(pool)]
         if use_graph:
             static_x.copy_(x, non_blocking=True)
             static_y.copy_(y, non_blocking=True)
@@ -140,8 +164,13 @@ def main():
     ms_per_step = 1000.0 * elapsed_max / args.steps
     value = world * B * args.steps / elapsed_max
     if rank == 0:
+        metric = METRIC if args.model == "convnet" else \
+            f"images/sec (whole node) {args.model} synthetic DDP training at 1/2/4/8 MI355X"
+        data = ("synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)"
+                if args.model == "convnet" else
+                f"synthetic (on-device N(0,1) {spec['shape']} images + labels; random-init weights)")
         res = {
-            "metric": METRIC,
+            "metric": metric,
             "value": round(value, 1),
             "unit": "images/sec",
             "n_gpus": world,
@@ -152,15 +181,15 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)",
+            "data": data,
             "config": {
-                "model": "MNIST ConvNet (ref/launch_dist.py; 113,674 params)",
+                "model": spec["desc"],
                 "global_batch": B * world,
                 "per_rank_batch": B,
                 "seq_len": None,
-                "image_shape": [1, 28, 28],
+                "image_shape": list(spec["shape"]),
                 "parallelism": f"dp{world}",
-                "optimizer": f"SGD lr={args.lr}",
+                "optimizer": f"SGD lr={lr} momentum={spec['momentum']} nesterov={spec['nesterov']} wd={spec['wd']}",
                 "comm": f"RCCL all-reduce ({args.comm_hook}), buckets cap {args.bucket_mb} MB",
                 "hipgraph": use_graph,
                 "master_weights": "fp32",

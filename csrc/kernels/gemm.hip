@@ -408,17 +408,43 @@ __global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict
   (void)perm_k;
 }
 
-__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const float* __restrict__ part, int tiles, int N,
-                                                                float* __restrict__ sums) {
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= N) return;
+// Two-level fixed-order reduction of per-tile channel partials part[tile][2][N] -> out0/out1[N]:
+// level 1: block (64 channels, tile group) - lane = channel, 4 waves stride the group's tiles;
+// level 2: one thread per channel sums the G group results in order.
+constexpr int PR_GROUPS = 128;
+
+__global__ __launch_bounds__(256) void reduce_parts_l1_kernel(const float* __restrict__ part, int nparts, int N,
+                                                              int per_group, float* __restrict__ mid) {
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, g = blockIdx.y;
+  const int t0 = g * per_group, t1 = min(nparts, t0 + per_group);
   float a = 0.f, q = 0.f;
-  for (int t = 0; t < tiles; ++t) {
-    a += part[(int64_t)t * 2 * N + n];
-    q += part[(int64_t)t * 2 * N + N + n];
+  if (c < N)
+    for (int t = t0 + wave; t < t1; t += 4) {
+      a += part[(int64_t)t * 2 * N + c];
+      q += part[(int64_t)t * 2 * N + N + c];
+    }
+  red[wave][0][lane] = a;
+  red[wave][1][lane] = q;
+  __syncthreads();
+  if (wave == 0 && c < N) {
+    mid[(int64_t)g * 2 * N + c] = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
+    mid[(int64_t)g * 2 * N + N + c] = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
   }
-  sums[n] = a;
-  sums[N + n] = q;
+}
+
+__global__ __launch_bounds__(256) void reduce_parts_l2_kernel(const float* __restrict__ mid, int G, int N,
+                                                              float* __restrict__ out0, float* __restrict__ out1) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  float a = 0.f, q = 0.f;
+  for (int g = 0; g < G; ++g) {
+    a += mid[(int64_t)g * 2 * N + c];
+    q += mid[(int64_t)g * 2 * N + N + c];
+  }
+  out0[c] = a;
+  out1[c] = q;
 }
 
 }  // namespace
@@ -484,8 +510,16 @@ void splitk_sum(const float* part, int S, int64_t n, float* out, hipStream_t s) 
   splitk_sum_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(part, S, n, out, 0, 0, 0);
 }
 
-void bn_stats_finalize(const float* part, int tiles, int N, float* sums, hipStream_t s) {
-  bn_stats_finalize_kernel<<<(N + 255) / 256, 256, 0, s>>>(part, tiles, N, sums);
+int reduce_parts_scratch_floats(int nparts, int N) {
+  const int G = std::min(PR_GROUPS, std::max(1, (nparts + 31) / 32));
+  return 2 * N * G;
+}
+
+void reduce_parts(const float* part, int nparts, int N, float* scratch, float* out0, float* out1, hipStream_t s) {
+  const int G = std::min(PR_GROUPS, std::max(1, (nparts + 31) / 32));
+  const int per = (nparts + G - 1) / G;
+  reduce_parts_l1_kernel<<<dim3((N + 63) / 64, G), 256, 0, s>>>(part, nparts, N, per, scratch);
+  reduce_parts_l2_kernel<<<(N + 255) / 256, 256, 0, s>>>(scratch, G, N, out0, out1);
 }
 
 int gemm_tiles_m(int M) { return (M + BM - 1) / BM; }

@@ -124,7 +124,9 @@ void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int split
                      hipStream_t s);
 int conv_wgrad_splits(const ConvGeom& g, int cus);
 void splitk_sum(const float* part, int S, int64_t n, float* out, hipStream_t s);
-void bn_stats_finalize(const float* part, int tiles, int N, float* sums, hipStream_t s);
+// out0[c] = sum_t part[t][0][c], out1[c] = sum_t part[t][1][c]  (two-level, fixed order)
+int reduce_parts_scratch_floats(int nparts, int N);
+void reduce_parts(const float* part, int nparts, int N, float* scratch, float* out0, float* out1, hipStream_t s);
 int gemm_tiles_m(int M);
 
 // ---------------------------------------------------------------- NHWC network layers (nn.hip)
@@ -143,8 +145,8 @@ int bn_bwd_parts(int64_t M);
 void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
                    float* part, void* g_out, hipStream_t s);
 // part 2: dgamma/dbeta and dz = scale*(g - mean(g) - zhat*mean(g*zhat))/..., plus d(residual) = g
-void bn_bwd_apply(const float* part, int nparts, const void* g, const void* z, const float* save, const float* gamma,
-                  int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s);
+void bn_bwd_apply(const float* part, int nparts, float* scratch, const void* g, const void* z, const float* save,
+                  const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s);
 void maxpool_fwd(const void* x, int N, int H, int W, int C, int k, int stride, int pad, int P, int Q, void* y,
                  uint8_t* arg, hipStream_t s);
 void maxpool_bwd(const void* dy, const uint8_t* arg, int N, int H, int W, int C, int k, int stride, int pad, int P,

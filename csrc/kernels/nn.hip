@@ -161,19 +161,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
   }
 }
 
-__global__ __launch_bounds__(256) void bn_bwd_final_kernel(const float* __restrict__ part, int nparts, int C,
-                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float a = 0.f, q = 0.f;
-  for (int p = 0; p < nparts; ++p) {
-    a += part[(int64_t)p * 2 * C + c];
-    q += part[((int64_t)p * 2 + 1) * C + c];
-  }
-  dbeta[c] = a;
-  dgamma[c] = q;
-}
-
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
                                                            const float* __restrict__ save,
                                                            const float* __restrict__ gamma,
@@ -198,50 +185,68 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16* __restric
   }
 }
 
-// max pooling (ResNet stem 3x3 s2 p1), NHWC; arg = window offset (dy*k + dx) of the first max
+// max pooling (ResNet stem 3x3 s2 p1), NHWC, 8 channels per thread; arg = window offset (dy*k + dx)
+// of the first max, one byte per channel
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16* __restrict__ x, int N, int H, int W, int C,
                                                           int k, int stride, int pad, int P, int Q,
                                                           bf16* __restrict__ y, uint8_t* __restrict__ arg) {
-  const int64_t total = (int64_t)N * P * Q * C;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * P * Q * cv;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int c = (int)(e % C);
-    int64_t t = e / C;
+    const int c8 = (int)(e % cv);
+    int64_t t = e / cv;
     const int q = (int)(t % Q);
     t /= Q;
     const int p = (int)(t % P);
     const int n = (int)(t / P);
-    float best = -INFINITY;
-    int ba = 0;
+    float best[8];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) best[j] = -INFINITY;
     for (int dy = 0; dy < k; ++dy) {
       const int h = p * stride - pad + dy;
       if ((unsigned)h >= (unsigned)H) continue;
       for (int dx = 0; dx < k; ++dx) {
         const int w = q * stride - pad + dx;
         if ((unsigned)w >= (unsigned)W) continue;
-        const float v = (float)x[(((int64_t)n * H + h) * W + w) * C + c];
-        if (v > best) {
-          best = v;
-          ba = dy * k + dx;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8);
+        const uint32_t a = (uint32_t)(dy * k + dx);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = (float)v[j];
+          if (f > best[j]) {
+            best[j] = f;
+            if (j < 4)
+              lo = (lo & ~(0xffu << (8 * j))) | (a << (8 * j));
+            else
+              hi = (hi & ~(0xffu << (8 * (j - 4)))) | (a << (8 * (j - 4)));
+          }
         }
       }
     }
-    y[e] = (bf16)best;
-    arg[e] = (uint8_t)ba;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)best[j];
+    reinterpret_cast<bf16x8*>(y)[e] = o;
+    reinterpret_cast<uint2*>(arg)[e] = make_uint2(lo, hi);
   }
 }
 
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16* __restrict__ dy, const uint8_t* __restrict__ arg,
                                                           int N, int H, int W, int C, int k, int stride, int pad,
                                                           int P, int Q, bf16* __restrict__ dx) {
-  const int64_t total = (int64_t)N * H * W * C;
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * H * W * cv;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int c = (int)(e % C);
-    int64_t t = e / C;
+    const int c8 = (int)(e % cv);
+    int64_t t = e / cv;
     const int w = (int)(t % W);
     t /= W;
     const int h = (int)(t % H);
     const int n = (int)(t / H);
-    float g = 0.f;
+    float g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = 0.f;
     // windows p with p*stride - pad <= h <= p*stride - pad + k - 1 (gather: deterministic)
     const int p_lo = max(0, (h + pad - k + stride) / stride), p_hi = min(P - 1, (h + pad) / stride);
     const int q_lo = max(0, (w + pad - k + stride) / stride), q_hi = min(Q - 1, (w + pad) / stride);
@@ -249,10 +254,20 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16* __restrict
       for (int q = q_lo; q <= q_hi; ++q) {
         const int dyy = h - (p * stride - pad), dxx = w - (q * stride - pad);
         if (dyy < 0 || dyy >= k || dxx < 0 || dxx >= k) continue;
-        const int64_t o = (((int64_t)n * P + p) * Q + q) * C + c;
-        if (arg[o] == dyy * k + dxx) g += (float)dy[o];
+        const int want = dyy * k + dxx;
+        const int64_t o = (((int64_t)n * P + p) * Q + q) * cv + c8;
+        const uint2 am = reinterpret_cast<const uint2*>(arg)[o];
+        const bf16x8 d = reinterpret_cast<const bf16x8*>(dy)[o];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int aj = (int)(((j < 4 ? am.x : am.y) >> (8 * (j & 3))) & 0xff);
+          if (aj == want) g[j] += (float)d[j];
+        }
       }
-    dx[e] = (bf16)g;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)g[j];
+    reinterpret_cast<bf16x8*>(dx)[e] = o;
   }
 }
 
@@ -333,9 +348,9 @@ void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* sa
                                                        bn_rows_per_part(M), part, static_cast<bf16*>(g_out));
 }
 
-void bn_bwd_apply(const float* part, int nparts, const void* g, const void* z, const float* save, const float* gamma,
-                  int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s) {
-  bn_bwd_final_kernel<<<(C + 255) / 256, 256, 0, s>>>(part, nparts, C, dgamma, dbeta);
+void bn_bwd_apply(const float* part, int nparts, float* scratch, const void* g, const void* z, const float* save,
+                  const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s) {
+  reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);  // part[p][0] = sum g, part[p][1] = sum g*zhat
   const int64_t nvec = M * C / 8;
   bn_bwd_apply_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save,
                                                      gamma, dgamma, dbeta, M, C, nvec, static_cast<bf16*>(dz));
@@ -343,14 +358,14 @@ void bn_bwd_apply(const float* part, int nparts, const void* g, const void* z, c
 
 void maxpool_fwd(const void* x, int N, int H, int W, int C, int k, int stride, int pad, int P, int Q, void* y,
                  uint8_t* arg, hipStream_t s) {
-  const int64_t total = (int64_t)N * P * Q * C;
+  const int64_t total = (int64_t)N * P * Q * C / 8;
   maxpool_fwd_kernel<<<grid_for(total), 256, 0, s>>>(static_cast<const bf16*>(x), N, H, W, C, k, stride, pad, P, Q,
                                                      static_cast<bf16*>(y), arg);
 }
 
 void maxpool_bwd(const void* dy, const uint8_t* arg, int N, int H, int W, int C, int k, int stride, int pad, int P,
                  int Q, void* dx, hipStream_t s) {
-  const int64_t total = (int64_t)N * H * W * C;
+  const int64_t total = (int64_t)N * H * W * C / 8;
   maxpool_bwd_kernel<<<grid_for(total), 256, 0, s>>>(static_cast<const bf16*>(dy), arg, N, H, W, C, k, stride, pad,
                                                      P, Q, static_cast<bf16*>(dx));
 }

@@ -148,9 +148,12 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Ten
     sums = at::empty({2, g.K}, part.options());
   }
   kern::conv_fwd_bf16(x.data_ptr(), w_krsc.data_ptr(), g, e, stream_of(x));
-  if (want_stats)
-    kern::bn_stats_finalize(part.data_ptr<float>(), kern::gemm_tiles_m(M), g.K, sums.data_ptr<float>(),
-                            stream_of(x));
+  if (want_stats) {
+    const int tiles = kern::gemm_tiles_m(M);
+    at::Tensor scratch = at::empty({kern::reduce_parts_scratch_floats(tiles, g.K)}, part.options());
+    kern::reduce_parts(part.data_ptr<float>(), tiles, g.K, scratch.data_ptr<float>(), sums.data_ptr<float>(),
+                       sums.data_ptr<float>() + g.K, stream_of(x));
+  }
   return {z, sums};
 }
 
@@ -264,7 +267,9 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor
   kern::bn_bwd_reduce(dy.data_ptr(), relu ? y.data_ptr() : nullptr, z.data_ptr(), save.data_ptr<float>(), relu, M,
                       (int)C, part.data_ptr<float>(), g.data_ptr(), stream_of(z));
   at::Tensor dz = at::empty_like(z);
-  kern::bn_bwd_apply(part.data_ptr<float>(), nparts, g.data_ptr(), z.data_ptr(), save.data_ptr<float>(),
+  at::Tensor scratch = at::empty({kern::reduce_parts_scratch_floats(nparts, (int)C)}, part.options());
+  kern::bn_bwd_apply(part.data_ptr<float>(), nparts, scratch.data_ptr<float>(), g.data_ptr(), z.data_ptr(),
+                     save.data_ptr<float>(),
                      gamma.data_ptr<float>(), M, (int)C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
                      dz.data_ptr(), stream_of(z));
   return {dz, g};
@@ -273,6 +278,7 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor
 std::tuple<at::Tensor, at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad) {
   bf16_gpu(x, "maxpool input");
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  RINGDP_CHECK(C % 8 == 0 && k * k <= 255, "maxpool: channels must be a multiple of 8");
   const int64_t P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
   at::Tensor y = at::empty({N, P, Q, C}, x.options());
   at::Tensor arg = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));

@@ -1,0 +1,65 @@
+"""Throughput of the generic MFMA GEMM core: dense layouts and ResNet-50 conv shapes (B=256)."""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+import ringdp  # noqa: E402
+
+C = ringdp._C
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / iters * 1000.0  # us
+
+
+def dense(M, N, K, a_row=False, b_row=False):
+    A = torch.randn(K * M, device="cuda").bfloat16()
+    B = torch.randn(K * N, device="cuda").bfloat16()
+    lda = M if a_row else K
+    ldb = N if b_row else K
+    us = timeit(lambda: C.gemm(A, B, M, N, K, lda, ldb, a_row, b_row, 1, 0, 0, True))
+    return {"shape": f"dense {M}x{N}x{K} a_row={a_row} b_row={b_row}", "us": round(us, 1),
+            "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+
+
+def conv(n, h, c, k, r, stride):
+    pad = r // 2
+    x = torch.randn(n, h, h, c, device="cuda").bfloat16()
+    w = torch.randn(k, c, r, r, device="cuda") * 0.05
+    krsc, crsk = C.pack_conv_weight(w, c)
+    z, _ = C.conv2d_fwd(x, krsc, stride, pad, 1, False)
+    p = z.shape[1]
+    flops = 2 * n * p * p * k * c * r * r
+    f = timeit(lambda: C.conv2d_fwd(x, krsc, stride, pad, 1, False))
+    fs = timeit(lambda: C.conv2d_fwd(x, krsc, stride, pad, 1, True))
+    d = timeit(lambda: C.conv2d_dgrad(z, crsk, h, h, stride, pad, 1))
+    dw = torch.empty_like(w)
+    wg = timeit(lambda: C.conv2d_wgrad(z, x, dw, stride, pad, 1))
+    return {"shape": f"conv n{n} {h}x{h} c{c}->k{k} r{r} s{stride}",
+            "fwd": [round(f, 1), round(flops / f / 1e6, 1)], "fwd+stats_us": round(fs, 1),
+            "dgrad": [round(d, 1), round(flops / d / 1e6, 1)], "wgrad": [round(wg, 1), round(flops / wg / 1e6, 1)]}
+
+
+if __name__ == "__main__":
+    out = []
+    for args in [(4096, 4096, 4096), (4096, 4096, 4096, True, False), (4096, 4096, 4096, False, True),
+                 (4096, 4096, 4096, True, True), (8192, 768, 3072)]:
+        out.append(dense(*args))
+        print(json.dumps(out[-1]), flush=True)
+    for args in [(256, 56, 64, 64, 1, 1), (256, 56, 64, 64, 3, 1), (256, 56, 64, 256, 1, 1), (256, 56, 256, 64, 1, 1),
+                 (256, 28, 128, 128, 3, 1), (256, 14, 256, 256, 3, 1), (256, 7, 512, 512, 3, 1),
+                 (256, 14, 1024, 256, 1, 1), (256, 224, 8, 64, 7, 2)]:
+        out.append(conv(*args))
+        print(json.dumps(out[-1]), flush=True)
