@@ -37,7 +37,10 @@ MODELS = {
                      desc="ResNet-18 CIFAR-shape (ref/example_mp.py; torchvision tree, 11,181,642 params)"),
     "resnet50": dict(batch=256, shape=(3, 224, 224), lr=0.02, momentum=0.9, nesterov=True, wd=1e-4,
                      desc="ResNet-50 ImageNet-shape (25,557,032 params)"),
+    "vit_b_16": dict(batch=128, shape=(3, 224, 224), lr=0.01, momentum=0.9, nesterov=False, wd=0.0,
+                     desc="ViT-B/16 ImageNet-shape (86,567,656 params, seq 197)"),
 }
+NUM_CLASSES = {"convnet": 10, "resnet18": 10, "resnet50": 1000, "vit_b_16": 1000}
 
 
 def parse():
@@ -88,7 +91,7 @@ def main():
     if args.model == "convnet":
         model = models.ConvNet().to(dev)
     else:
-        model = getattr(models, args.model)(num_classes=1000 if args.model == "resnet50" else 10).to(dev)
+        model = getattr(models, args.model)(num_classes=NUM_CLASSES[args.model]).to(dev)
     ddp = DDP(model, device_ids=[local_rank], output_device=local_rank, bucket_cap_mb=args.bucket_mb,
               first_bucket_mb=args.first_bucket_mb)
     if args.comm_hook != "allreduce":
@@ -101,7 +104,7 @@ def main():
         pool = [ringdp._C.synth_u8_images(B, 28, 28, 10, 1000 * rank + i, dev) for i in range(args.pool)]
     else:
         g = torch.Generator(device=dev).manual_seed(1000 * rank)
-        ncls = 1000 if args.model == "resnet50" else 10
+        ncls = NUM_CLASSES[args.model]
         pool = [(torch.randn((B,) + spec["shape"], device=dev, generator=g),
                  torch.randint(0, ncls, (B,), device=dev, generator=g)) for _ in range(min(args.pool, 4))]
     static_x = torch.empty_like(pool[0][0])

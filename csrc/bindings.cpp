@@ -391,6 +391,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool_fwd", &ops::avgpool_fwd);
   m.def("avgpool_bwd", &ops::avgpool_bwd);
   m.def("add_bf16", &ops::add_bf16);
+  m.def("layernorm_fwd", &ops::layernorm_fwd);
+  m.def("layernorm_bwd", &ops::layernorm_bwd);
+  m.def("qkv_split", &ops::qkv_split);
+  m.def("qkv_merge", &ops::qkv_merge);
+  m.def("heads_to_rows", &ops::heads_to_rows);
+  m.def("rows_to_heads", &ops::rows_to_heads);
+  m.def("softmax_fwd", &ops::softmax_fwd);
+  m.def("softmax_bwd", &ops::softmax_bwd);
+  m.def("gelu_bwd", &ops::gelu_bwd);
+  m.def("assemble_tokens", &ops::assemble_tokens);
+  m.def("assemble_tokens_bwd", &ops::assemble_tokens_bwd);
+  m.def("cls_rows", &ops::cls_rows);
+  m.def("patchify", &ops::patchify);
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);

@@ -155,6 +155,27 @@ void avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t s);
 void avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t s);
 void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s);
 
+// ---------------------------------------------------------------- transformer layers (vit.hip)
+void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, void* y,
+                   float* stats, hipStream_t s);
+int layernorm_bwd_scratch_floats(int64_t rows, int D);
+void layernorm_bwd(const void* dy, const void* x, const float* stats, const float* w, const void* dres, int64_t rows,
+                   int D, void* dx, float* scratch, float* dw, float* db, hipStream_t s);
+void qkv_split(const void* qkv, int B, int T, int H, int Dh, int Tp, void* q, void* k, void* v, hipStream_t s);
+void qkv_merge(const void* dq, const void* dk, const void* dv, int B, int T, int H, int Dh, int Tp, void* dqkv,
+               hipStream_t s);
+void heads_to_rows(const void* o, int B, int T, int H, int Dh, int Tp, void* rows, hipStream_t s);
+void rows_to_heads(const void* rows, int B, int T, int H, int Dh, int Tp, void* o, hipStream_t s);
+void softmax_fwd(const float* scores, int64_t rows, int T, int Tp, float scale, void* p, hipStream_t s);
+void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);
+void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s);
+void assemble_tokens(const void* patches, const float* cls, const float* pos, int B, int NP, int D, void* out,
+                     hipStream_t s);
+void assemble_tokens_bwd(const void* dout, int B, int NP, int D, void* dpatches, float* dpos, float* dcls,
+                         hipStream_t s);
+void cls_rows(const void* x, int B, int T, int D, void* y, bool reverse, hipStream_t s);
+void patchify(const void* x, bool x_bf16, int B, int C, int H, int W, int P, void* out, hipStream_t s);
+
 // ---------------------------------------------------------------- data
 // Gather B samples of a uint8 (N, H, W, C) dataset by index, random-crop (zero pad) + h-flip, then
 // ToTensor + Normalize; out_kind 0 = fp32, 1 = bf16, 2 = uint8 (no normalisation).  Output NCHW

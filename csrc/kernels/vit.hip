@@ -1,0 +1,460 @@
+// Transformer (ViT-B/16) layer kernels around the generic MFMA GEMM (BASELINE.json config 5).
+//
+// Token activations are row-major bf16 [rows][D].  Attention is computed on head-major tensors
+// padded to a multiple-of-16 sequence (Tp >= T; padded keys are masked, padded queries are zero)
+// so every attention matmul is one batched GEMM of the generic core (QK^T, PV and the four
+// backward products), and the softmax lives in its own row kernel with the 1/sqrt(d) scale and
+// the key mask fused.  LayerNorm keeps fp32 statistics; its backward fuses the residual-stream
+// gradient add.
+#include <algorithm>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace ringdp {
+namespace kern {
+
+using namespace ringdp::dev;
+
+namespace {
+
+inline int grid_for(int64_t n, int per_block = 256, int cap = 8192) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + per_block - 1) / per_block, cap));
+}
+
+// ---------------------------------------------------------------- LayerNorm (one wave per row)
+// D <= 64 * 8 * 4 = 2048, D % 8 == 0
+template <int VPL>  // 8-element vectors per lane
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ b, int64_t rows, int D,
+                                                            float eps, bf16* __restrict__ y,
+                                                            float* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = D / 8;
+  const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row * D);
+  float v[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + 64 * i;
+    if (vi < nv) {
+      const bf16x8 t = xr[vi];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = (float)t[j];
+        s += v[i][j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+    if (lane + 64 * i < nv)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+  bf16x8* yr = reinterpret_cast<bf16x8*>(y + row * D);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int vi = lane + 64 * i;
+    if (vi < nv) {
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = vi * 8 + j;
+        o[j] = (bf16)((v[i][j] - mean) * rstd * w[c] + b[c]);
+      }
+      yr[vi] = o;
+    }
+  }
+  if (lane == 0) {
+    stats[2 * row] = mean;
+    stats[2 * row + 1] = rstd;
+  }
+}
+
+// dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)) (+ dres);  dw/db partials per block
+template <int VPL>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                            const float* __restrict__ stats,
+                                                            const float* __restrict__ w, const bf16* __restrict__ dres,
+                                                            int64_t rows, int D, int rows_per_block,
+                                                            bf16* __restrict__ dx, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nv = D / 8;
+  float dw[VPL][8], db[VPL][8];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dw[i][j] = db[i][j] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = std::min<int64_t>(rows, r0 + rows_per_block);
+  for (int64_t row = r0 + wave; row < r1; row += 4) {
+    const float mean = stats[2 * row], rstd = stats[2 * row + 1];
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row * D);
+    const bf16x8* gr = reinterpret_cast<const bf16x8*>(dy + row * D);
+    float xh[VPL][8], gw[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nv) {
+        const bf16x8 xv = xr[vi], gv = gr[vi];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = vi * 8 + j;
+          xh[i][j] = ((float)xv[j] - mean) * rstd;
+          const float g = (float)gv[j];
+          gw[i][j] = g * w[c];
+          s1 += gw[i][j];
+          s2 += gw[i][j] * xh[i][j];
+          dw[i][j] += g * xh[i][j];
+          db[i][j] += g;
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)D, m2 = wave_sum(s2) / (float)D;
+    bf16x8* dxr = reinterpret_cast<bf16x8*>(dx + row * D);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nv) {
+        bf16x8 rv = zero_bf16x8();
+        if (dres) rv = reinterpret_cast<const bf16x8*>(dres + row * D)[vi];
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)(rstd * (gw[i][j] - m1 - xh[i][j] * m2) + (float)rv[j]);
+        dxr[vi] = o;
+      }
+    }
+  }
+  // combine the 4 waves (fixed order) and write this block's partial dw/db
+  __shared__ float red[4][2048];
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nv)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wave][vi * 8 + j] = pass == 0 ? dw[i][j] : db[i][j];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < D; c += 256)
+      part[((int64_t)blockIdx.x * 2 + pass) * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- attention layout
+// qkv [B*T][3*H*Dh] (Linear output) -> q/k/v [B*H][Tp][Dh] (rows >= T zero)
+__global__ __launch_bounds__(256) void qkv_split_kernel(const bf16* __restrict__ qkv, int B, int T, int H, int Dh,
+                                                        int Tp, bf16* __restrict__ q, bf16* __restrict__ k,
+                                                        bf16* __restrict__ v) {
+  const int dv = Dh / 8;
+  const int64_t total = (int64_t)3 * B * H * Tp * dv;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int d8 = (int)(e % dv);
+    int64_t r = e / dv;
+    const int t = (int)(r % Tp);
+    r /= Tp;
+    const int h = (int)(r % H);
+    r /= H;
+    const int b = (int)(r % B);
+    const int which = (int)(r / B);
+    bf16x8 val = zero_bf16x8();
+    if (t < T)
+      val = *reinterpret_cast<const bf16x8*>(qkv + ((int64_t)b * T + t) * 3 * H * Dh + which * H * Dh + h * Dh + d8 * 8);
+    bf16* dst = which == 0 ? q : (which == 1 ? k : v);
+    *reinterpret_cast<bf16x8*>(dst + (((int64_t)b * H + h) * Tp + t) * Dh + d8 * 8) = val;
+  }
+}
+
+// inverse: q/k/v grads [B*H][Tp][Dh] -> dqkv [B*T][3*H*Dh]
+__global__ __launch_bounds__(256) void qkv_merge_kernel(const bf16* __restrict__ dq, const bf16* __restrict__ dk,
+                                                        const bf16* __restrict__ dv_, int B, int T, int H, int Dh,
+                                                        int Tp, bf16* __restrict__ dqkv) {
+  const int dv = Dh / 8;
+  const int64_t total = (int64_t)B * T * 3 * H * dv;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int d8 = (int)(e % dv);
+    int64_t r = e / dv;
+    const int h = (int)(r % H);
+    r /= H;
+    const int which = (int)(r % 3);
+    r /= 3;
+    const int t = (int)(r % T);
+    const int b = (int)(r / T);
+    const bf16* src = which == 0 ? dq : (which == 1 ? dk : dv_);
+    *reinterpret_cast<bf16x8*>(dqkv + ((int64_t)b * T + t) * 3 * H * Dh + which * H * Dh + h * Dh + d8 * 8) =
+        *reinterpret_cast<const bf16x8*>(src + (((int64_t)b * H + h) * Tp + t) * Dh + d8 * 8);
+  }
+}
+
+// o [B*H][Tp][Dh] -> [B*T][H*Dh]   (and the reverse for the gradient)
+template <bool TO_HEADS>
+__global__ __launch_bounds__(256) void heads_kernel(const bf16* __restrict__ src, int B, int T, int H, int Dh, int Tp,
+                                                    bf16* __restrict__ dst) {
+  const int dv = Dh / 8;
+  const int64_t total = TO_HEADS ? (int64_t)B * H * Tp * dv : (int64_t)B * T * H * dv;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int d8 = (int)(e % dv);
+    int64_t r = e / dv;
+    if (TO_HEADS) {  // dst [B*H][Tp][Dh] from src [B*T][H*Dh]
+      const int t = (int)(r % Tp);
+      r /= Tp;
+      const int h = (int)(r % H);
+      const int b = (int)(r / H);
+      bf16x8 val = zero_bf16x8();
+      if (t < T) val = *reinterpret_cast<const bf16x8*>(src + ((int64_t)b * T + t) * H * Dh + h * Dh + d8 * 8);
+      *reinterpret_cast<bf16x8*>(dst + (((int64_t)b * H + h) * Tp + t) * Dh + d8 * 8) = val;
+    } else {  // dst [B*T][H*Dh] from src [B*H][Tp][Dh]
+      const int h = (int)(r % H);
+      r /= H;
+      const int t = (int)(r % T);
+      const int b = (int)(r / T);
+      *reinterpret_cast<bf16x8*>(dst + ((int64_t)b * T + t) * H * Dh + h * Dh + d8 * 8) =
+          *reinterpret_cast<const bf16x8*>(src + (((int64_t)b * H + h) * Tp + t) * Dh + d8 * 8);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- softmax over keys (one wave per row)
+// s [rows][Tp] fp32 scores (unscaled) -> p bf16 = softmax(scale * s) over the first T keys; padded
+// keys get 0.  Rows t >= T (padded queries) are written as zeros.
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* __restrict__ s, int64_t rows, int T, int Tp,
+                                                          float scale, bf16* __restrict__ p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bool qpad = (int)(row % Tp) >= T;
+  const float* sr = s + row * Tp;
+  bf16* pr = p + row * Tp;
+  if (qpad) {
+    for (int c = lane; c < Tp; c += 64) pr[c] = (bf16)0.f;
+    return;
+  }
+  float mx = -INFINITY;
+  for (int c = lane; c < T; c += 64) mx = fmaxf(mx, sr[c] * scale);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int c = lane; c < T; c += 64) sum += __expf(sr[c] * scale - mx);
+  const float inv = 1.f / wave_sum(sum);
+  for (int c = lane; c < Tp; c += 64) pr[c] = (bf16)(c < T ? __expf(sr[c] * scale - mx) * inv : 0.f);
+}
+
+// ds = scale * p * (dp - sum_j dp_j p_j)  (bf16 out; padded keys / queries -> 0)
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16* __restrict__ p, const float* __restrict__ dp,
+                                                          int64_t rows, int T, int Tp, float scale,
+                                                          bf16* __restrict__ ds) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16* pr = p + row * Tp;
+  const float* dr = dp + row * Tp;
+  bf16* o = ds + row * Tp;
+  float dot = 0.f;
+  for (int c = lane; c < T; c += 64) dot += (float)pr[c] * dr[c];
+  dot = wave_sum(dot);
+  for (int c = lane; c < Tp; c += 64) o[c] = (bf16)(c < T ? scale * (float)pr[c] * (dr[c] - dot) : 0.f);
+}
+
+// ---------------------------------------------------------------- misc
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ pre,
+                                                       int64_t nvec, bf16* __restrict__ dx) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const bf16x8 g = reinterpret_cast<const bf16x8*>(dy)[v], z = reinterpret_cast<const bf16x8*>(pre)[v];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = (float)z[j];
+      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+      o[j] = (bf16)((float)g[j] * (cdf + x * pdf));
+    }
+    reinterpret_cast<bf16x8*>(dx)[v] = o;
+  }
+}
+
+// tokens [B][1+NP][D] = concat(cls, patches [B][NP][D]) + pos [1+NP][D]
+__global__ __launch_bounds__(256) void assemble_tokens_kernel(const bf16* __restrict__ patches,
+                                                              const float* __restrict__ cls,
+                                                              const float* __restrict__ pos, int B, int NP, int D,
+                                                              bf16* __restrict__ out) {
+  const int T = NP + 1;
+  const int64_t total = (int64_t)B * T * D;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int d = (int)(e % D);
+    const int64_t r = e / D;
+    const int t = (int)(r % T);
+    const int64_t b = r / T;
+    const float base = t == 0 ? cls[d] : (float)patches[(b * NP + t - 1) * D + d];
+    out[e] = (bf16)(base + pos[(int64_t)t * D + d]);
+  }
+}
+
+// gradients of assemble_tokens: dpatches (bf16) and per-block partial sums for dcls / dpos
+__global__ __launch_bounds__(256) void assemble_tokens_bwd_kernel(const bf16* __restrict__ dout, int B, int NP, int D,
+                                                                  bf16* __restrict__ dpatches,
+                                                                  float* __restrict__ dpos, float* __restrict__ dcls) {
+  const int T = NP + 1;
+  // one thread per (t, d): sum over the batch in a fixed order
+  const int64_t total = (int64_t)T * D;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int d = (int)(e % D);
+    const int t = (int)(e / D);
+    float acc = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float g = (float)dout[((int64_t)b * T + t) * D + d];
+      acc += g;
+      if (t > 0) dpatches[((int64_t)b * NP + t - 1) * D + d] = (bf16)g;
+    }
+    dpos[e] = acc;
+    if (t == 0) dcls[d] = acc;
+  }
+}
+
+// rows [B][T][D] -> the class-token rows [B][D] (and the reverse scatter for the gradient)
+__global__ __launch_bounds__(256) void cls_rows_kernel(const bf16* __restrict__ x, int B, int T, int D,
+                                                       bf16* __restrict__ y, int reverse) {
+  const int64_t total = (int64_t)B * D;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t b = e / D;
+    const int d = (int)(e % D);
+    if (!reverse)
+      y[e] = x[b * T * D + d];
+    else
+      y[b * T * D + d] = x[e];
+  }
+}
+
+// NCHW fp32/bf16 images -> non-overlapping patch rows [B*NP][C*P*P] bf16 (column order c, kh, kw:
+// the flattened conv_proj weight), i.e. the im2col of a stride-P PxP convolution.
+template <bool BF>
+__global__ __launch_bounds__(256) void patchify_kernel(const void* __restrict__ x, int B, int Cc, int H, int W,
+                                                       int P, bf16* __restrict__ out) {
+  const int gh = H / P, gw = W / P, K = Cc * P * P;
+  const int64_t total = (int64_t)B * gh * gw * K;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int k = (int)(e % K);
+    const int64_t r = e / K;
+    const int pw = (int)(r % gw);
+    const int ph = (int)((r / gw) % gh);
+    const int64_t b = r / ((int64_t)gw * gh);
+    const int c = k / (P * P), kh = (k / P) % P, kw = k % P;
+    const int64_t src = ((b * Cc + c) * H + ph * P + kh) * W + pw * P + kw;
+    out[e] = BF ? static_cast<const bf16*>(x)[src] : (bf16)static_cast<const float*>(x)[src];
+  }
+}
+
+}  // namespace
+
+void patchify(const void* x, bool x_bf16, int B, int C, int H, int W, int P, void* out, hipStream_t s) {
+  const int64_t total = (int64_t)B * (H / P) * (W / P) * C * P * P;
+  if (x_bf16)
+    patchify_kernel<true><<<grid_for(total), 256, 0, s>>>(x, B, C, H, W, P, static_cast<bf16*>(out));
+  else
+    patchify_kernel<false><<<grid_for(total), 256, 0, s>>>(x, B, C, H, W, P, static_cast<bf16*>(out));
+}
+
+int layernorm_bwd_blocks(int64_t rows) { return (int)std::min<int64_t>(1024, std::max<int64_t>(1, (rows + 15) / 16)); }
+
+void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, void* y,
+                   float* stats, hipStream_t s) {
+  const int nv = D / 8;
+  const int grid = (int)((rows + 3) / 4);
+  if (nv <= 64)
+    layernorm_fwd_kernel<1><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, static_cast<bf16*>(y), stats);
+  else if (nv <= 128)
+    layernorm_fwd_kernel<2><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, static_cast<bf16*>(y), stats);
+  else
+    layernorm_fwd_kernel<4><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, static_cast<bf16*>(y), stats);
+}
+
+void layernorm_bwd(const void* dy, const void* x, const float* stats, const float* w, const void* dres, int64_t rows,
+                   int D, void* dx, float* part, float* dw, float* db, hipStream_t s) {
+  const int nb = layernorm_bwd_blocks(rows);
+  const int rpb = (int)((rows + nb - 1) / nb);
+  const int nv = D / 8;
+  auto args = [&](auto kern) {
+    kern<<<nb, 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(x), stats, w,
+                            static_cast<const bf16*>(dres), rows, D, rpb, static_cast<bf16*>(dx), part);
+  };
+  if (nv <= 64)
+    args(layernorm_bwd_kernel<1>);
+  else if (nv <= 128)
+    args(layernorm_bwd_kernel<2>);
+  else
+    args(layernorm_bwd_kernel<4>);
+  // part [nb][2][D] -> dw = sum part[.][0], db = sum part[.][1]
+  reduce_parts(part, nb, D, part + (int64_t)nb * 2 * D, dw, db, s);
+}
+
+int layernorm_bwd_scratch_floats(int64_t rows, int D) {
+  const int nb = layernorm_bwd_blocks(rows);
+  return nb * 2 * D + reduce_parts_scratch_floats(nb, D);
+}
+
+void qkv_split(const void* qkv, int B, int T, int H, int Dh, int Tp, void* q, void* k, void* v, hipStream_t s) {
+  qkv_split_kernel<<<grid_for((int64_t)3 * B * H * Tp * Dh / 8), 256, 0, s>>>(
+      static_cast<const bf16*>(qkv), B, T, H, Dh, Tp, static_cast<bf16*>(q), static_cast<bf16*>(k), static_cast<bf16*>(v));
+}
+
+void qkv_merge(const void* dq, const void* dk, const void* dv, int B, int T, int H, int Dh, int Tp, void* dqkv,
+               hipStream_t s) {
+  qkv_merge_kernel<<<grid_for((int64_t)B * T * 3 * H * Dh / 8), 256, 0, s>>>(
+      static_cast<const bf16*>(dq), static_cast<const bf16*>(dk), static_cast<const bf16*>(dv), B, T, H, Dh, Tp,
+      static_cast<bf16*>(dqkv));
+}
+
+void heads_to_rows(const void* o, int B, int T, int H, int Dh, int Tp, void* rows, hipStream_t s) {
+  heads_kernel<false><<<grid_for((int64_t)B * T * H * Dh / 8), 256, 0, s>>>(static_cast<const bf16*>(o), B, T, H, Dh, Tp,
+                                                                            static_cast<bf16*>(rows));
+}
+
+void rows_to_heads(const void* rows, int B, int T, int H, int Dh, int Tp, void* o, hipStream_t s) {
+  heads_kernel<true><<<grid_for((int64_t)B * H * Tp * Dh / 8), 256, 0, s>>>(static_cast<const bf16*>(rows), B, T, H, Dh,
+                                                                            Tp, static_cast<bf16*>(o));
+}
+
+void softmax_fwd(const float* scores, int64_t rows, int T, int Tp, float scale, void* p, hipStream_t s) {
+  softmax_fwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(scores, rows, T, Tp, scale, static_cast<bf16*>(p));
+}
+
+void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s) {
+  softmax_bwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(static_cast<const bf16*>(p), dp, rows, T, Tp, scale,
+                                                           static_cast<bf16*>(ds));
+}
+
+void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s) {
+  gelu_bwd_kernel<<<grid_for(n / 8), 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(pre), n / 8,
+                                                  static_cast<bf16*>(dx));
+}
+
+void assemble_tokens(const void* patches, const float* cls, const float* pos, int B, int NP, int D, void* out,
+                     hipStream_t s) {
+  assemble_tokens_kernel<<<grid_for((int64_t)B * (NP + 1) * D), 256, 0, s>>>(static_cast<const bf16*>(patches), cls, pos,
+                                                                             B, NP, D, static_cast<bf16*>(out));
+}
+
+void assemble_tokens_bwd(const void* dout, int B, int NP, int D, void* dpatches, float* dpos, float* dcls,
+                         hipStream_t s) {
+  assemble_tokens_bwd_kernel<<<grid_for((int64_t)(NP + 1) * D), 256, 0, s>>>(static_cast<const bf16*>(dout), B, NP, D,
+                                                                             static_cast<bf16*>(dpatches), dpos, dcls);
+}
+
+void cls_rows(const void* x, int B, int T, int D, void* y, bool reverse, hipStream_t s) {
+  cls_rows_kernel<<<grid_for((int64_t)B * D), 256, 0, s>>>(static_cast<const bf16*>(x), B, T, D, static_cast<bf16*>(y),
+                                                           reverse ? 1 : 0);
+}
+
+}  // namespace kern
+}  // namespace ringdp

@@ -54,7 +54,9 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, 
                 const c10::optional<at::Tensor>& preact, double alpha, const c10::optional<at::Tensor>& out) {
   bf16_gpu(a, "gemm A");
   bf16_gpu(b, "gemm B");
-  RINGDP_CHECK(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "gemm: K and leading dims must be multiples of 8");
+  // 16-B vectors run along K for K-contiguous operands and along the rows otherwise
+  RINGDP_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: leading dims must be multiples of 8");
+  RINGDP_CHECK((a_row && b_row) || K % 8 == 0, "gemm: K must be a multiple of 8 for a K-contiguous operand");
   RINGDP_CHECK(!a_row || M % 8 == 0, "gemm: a row-contiguous A needs M % 8 == 0");
   RINGDP_CHECK(!b_row || N % 8 == 0, "gemm: a row-contiguous B needs N % 8 == 0");
   // bounds: the last element each operand touches must be inside its storage
@@ -101,7 +103,8 @@ at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, 
   bf16_gpu(b, "gemm B");
   f32_gpu(out, "gemm out");
   RINGDP_CHECK(out.numel() == M * N, "gemm_splitk_f32: out must have M*N elements");
-  RINGDP_CHECK(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0, "gemm: K and leading dims must be multiples of 8");
+  RINGDP_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: leading dims must be multiples of 8");
+  RINGDP_CHECK((a_row && b_row) || K % 8 == 0, "gemm: K must be a multiple of 8 for a K-contiguous operand");
   RINGDP_CHECK((!a_row || M % 8 == 0) && (!b_row || N % 8 == 0), "gemm: row-contiguous operand needs 8-multiple");
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 64)));
   at::Tensor part = at::empty({splits, M, N}, out.options());
@@ -320,6 +323,153 @@ at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b) {
   at::Tensor y = at::empty_like(a);
   kern::add_bf16(a.data_ptr(), b.data_ptr(), a.numel(), y.data_ptr(), stream_of(a));
   return y;
+}
+
+// ------------------------------------------------------------------ transformer layers
+std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                                 double eps) {
+  bf16_gpu(x, "layernorm input");
+  f32_gpu(w, "layernorm weight");
+  f32_gpu(b, "layernorm bias");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  RINGDP_CHECK(D % 8 == 0 && D <= 2048 && w.numel() == D && b.numel() == D, "layernorm: bad shapes");
+  at::Tensor y = at::empty_like(x);
+  at::Tensor stats = at::empty({rows, 2}, w.options());
+  kern::layernorm_fwd(x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), rows, (int)D, (float)eps, y.data_ptr(),
+                      stats.data_ptr<float>(), stream_of(x));
+  return {y, stats};
+}
+
+at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats, const at::Tensor& w,
+                         const c10::optional<at::Tensor>& dres, at::Tensor dw, at::Tensor db) {
+  bf16_gpu(dy, "layernorm output grad");
+  bf16_gpu(x, "layernorm input");
+  f32_gpu(stats, "layernorm stats");
+  f32_gpu(dw, "layernorm dweight");
+  f32_gpu(db, "layernorm dbias");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  RINGDP_CHECK(dy.sizes() == x.sizes(), "layernorm backward: shape mismatch");
+  const void* dr = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    bf16_gpu(*dres, "layernorm residual grad");
+    RINGDP_CHECK(dres->sizes() == x.sizes(), "layernorm residual grad: shape mismatch");
+    dr = dres->data_ptr();
+  }
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor scratch = at::empty({kern::layernorm_bwd_scratch_floats(rows, (int)D)}, w.options());
+  kern::layernorm_bwd(dy.data_ptr(), x.data_ptr(), stats.data_ptr<float>(), w.data_ptr<float>(), dr, rows, (int)D,
+                      dx.data_ptr(), scratch.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                      stream_of(x));
+  return dx;
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> qkv_split(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H,
+                                                         int64_t Tp) {
+  bf16_gpu(qkv, "qkv");
+  const int64_t D3 = qkv.size(-1), Dh = D3 / 3 / H;
+  RINGDP_CHECK(qkv.numel() == B * T * D3 && Dh * 3 * H == D3 && Dh % 8 == 0 && Tp >= T, "qkv_split: bad shapes");
+  auto opt = qkv.options();
+  at::Tensor q = at::empty({B * H, Tp, Dh}, opt), k = at::empty({B * H, Tp, Dh}, opt), v = at::empty({B * H, Tp, Dh}, opt);
+  kern::qkv_split(qkv.data_ptr(), (int)B, (int)T, (int)H, (int)Dh, (int)Tp, q.data_ptr(), k.data_ptr(), v.data_ptr(),
+                  stream_of(qkv));
+  return {q, k, v};
+}
+
+at::Tensor qkv_merge(const at::Tensor& dq, const at::Tensor& dk, const at::Tensor& dv, int64_t B, int64_t T) {
+  bf16_gpu(dq, "dq");
+  bf16_gpu(dk, "dk");
+  bf16_gpu(dv, "dv");
+  const int64_t BH = dq.size(0), Tp = dq.size(1), Dh = dq.size(2), H = BH / B;
+  at::Tensor out = at::empty({B * T, 3 * H * Dh}, dq.options());
+  kern::qkv_merge(dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), (int)B, (int)T, (int)H, (int)Dh, (int)Tp,
+                  out.data_ptr(), stream_of(dq));
+  return out;
+}
+
+at::Tensor heads_to_rows(const at::Tensor& o, int64_t B, int64_t T) {
+  bf16_gpu(o, "attention output");
+  const int64_t BH = o.size(0), Tp = o.size(1), Dh = o.size(2), H = BH / B;
+  at::Tensor out = at::empty({B * T, H * Dh}, o.options());
+  kern::heads_to_rows(o.data_ptr(), (int)B, (int)T, (int)H, (int)Dh, (int)Tp, out.data_ptr(), stream_of(o));
+  return out;
+}
+
+at::Tensor rows_to_heads(const at::Tensor& rows, int64_t B, int64_t T, int64_t H, int64_t Tp) {
+  bf16_gpu(rows, "token rows");
+  const int64_t D = rows.size(-1), Dh = D / H;
+  at::Tensor out = at::empty({B * H, Tp, Dh}, rows.options());
+  kern::rows_to_heads(rows.data_ptr(), (int)B, (int)T, (int)H, (int)Dh, (int)Tp, out.data_ptr(), stream_of(rows));
+  return out;
+}
+
+at::Tensor softmax_fwd(const at::Tensor& scores, int64_t T, double scale) {
+  f32_gpu(scores, "attention scores");
+  const int64_t Tp = scores.size(-1), rows = scores.numel() / Tp;
+  at::Tensor p = at::empty(scores.sizes(), scores.options().dtype(at::kBFloat16));
+  kern::softmax_fwd(scores.data_ptr<float>(), rows, (int)T, (int)Tp, (float)scale, p.data_ptr(), stream_of(scores));
+  return p;
+}
+
+at::Tensor softmax_bwd(const at::Tensor& p, const at::Tensor& dp, int64_t T, double scale) {
+  bf16_gpu(p, "attention probs");
+  f32_gpu(dp, "attention probs grad");
+  const int64_t Tp = p.size(-1), rows = p.numel() / Tp;
+  at::Tensor ds = at::empty_like(p);
+  kern::softmax_bwd(p.data_ptr(), dp.data_ptr<float>(), rows, (int)T, (int)Tp, (float)scale, ds.data_ptr(),
+                    stream_of(p));
+  return ds;
+}
+
+at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& pre) {
+  bf16_gpu(dy, "gelu output grad");
+  bf16_gpu(pre, "gelu input");
+  RINGDP_CHECK(dy.numel() == pre.numel() && dy.numel() % 8 == 0, "gelu_bwd: shape mismatch");
+  at::Tensor dx = at::empty_like(pre);
+  kern::gelu_bwd(dy.data_ptr(), pre.data_ptr(), dy.numel(), dx.data_ptr(), stream_of(dy));
+  return dx;
+}
+
+at::Tensor assemble_tokens(const at::Tensor& patches, const at::Tensor& cls, const at::Tensor& pos) {
+  bf16_gpu(patches, "patch embeddings");
+  f32_gpu(cls, "class token");
+  f32_gpu(pos, "position embedding");
+  const int64_t B = patches.size(0), D = patches.size(-1), NP = patches.numel() / (B * D);
+  RINGDP_CHECK(pos.numel() == (NP + 1) * D && cls.numel() == D, "assemble_tokens: bad shapes");
+  at::Tensor out = at::empty({B, NP + 1, D}, patches.options());
+  kern::assemble_tokens(patches.data_ptr(), cls.data_ptr<float>(), pos.data_ptr<float>(), (int)B, (int)NP, (int)D,
+                        out.data_ptr(), stream_of(patches));
+  return out;
+}
+
+at::Tensor assemble_tokens_bwd(const at::Tensor& dout, at::Tensor dpos, at::Tensor dcls) {
+  bf16_gpu(dout, "token grad");
+  f32_gpu(dpos, "position grad");
+  f32_gpu(dcls, "class token grad");
+  const int64_t B = dout.size(0), T = dout.size(1), D = dout.size(2);
+  at::Tensor dp = at::empty({B, T - 1, D}, dout.options());
+  kern::assemble_tokens_bwd(dout.data_ptr(), (int)B, (int)(T - 1), (int)D, dp.data_ptr(), dpos.data_ptr<float>(),
+                            dcls.data_ptr<float>(), stream_of(dout));
+  return dp;
+}
+
+at::Tensor cls_rows(const at::Tensor& x, int64_t B, int64_t T, bool reverse) {
+  bf16_gpu(x, "token rows");
+  const int64_t D = x.size(-1);
+  at::Tensor y = reverse ? at::zeros({B, T, D}, x.options()) : at::empty({B, D}, x.options());
+  kern::cls_rows(x.data_ptr(), (int)B, (int)T, (int)D, y.data_ptr(), reverse, stream_of(x));
+  return y;
+}
+
+at::Tensor patchify(const at::Tensor& x, int64_t P) {
+  gpu(x, "images");
+  RINGDP_CHECK(x.dim() == 4 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+               "patchify: expected NCHW float/bf16 images");
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  RINGDP_CHECK(H % P == 0 && W % P == 0 && (C * P * P) % 8 == 0, "patchify: bad patch size");
+  at::Tensor out = at::empty({B * (H / P) * (W / P), C * P * P}, x.options().dtype(at::kBFloat16));
+  kern::patchify(x.data_ptr(), x.scalar_type() == at::kBFloat16, (int)B, (int)C, (int)H, (int)W, (int)P,
+                 out.data_ptr(), stream_of(x));
+  return out;
 }
 
 }  // namespace ops

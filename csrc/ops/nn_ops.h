@@ -38,5 +38,22 @@ at::Tensor avgpool_fwd(const at::Tensor& x);
 at::Tensor avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W);
 at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b);
 
+std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
+                                                 double eps);
+at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats, const at::Tensor& w,
+                         const c10::optional<at::Tensor>& dres, at::Tensor dw, at::Tensor db);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> qkv_split(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H,
+                                                         int64_t Tp);
+at::Tensor qkv_merge(const at::Tensor& dq, const at::Tensor& dk, const at::Tensor& dv, int64_t B, int64_t T);
+at::Tensor heads_to_rows(const at::Tensor& o, int64_t B, int64_t T);
+at::Tensor rows_to_heads(const at::Tensor& rows, int64_t B, int64_t T, int64_t H, int64_t Tp);
+at::Tensor softmax_fwd(const at::Tensor& scores, int64_t T, double scale);
+at::Tensor softmax_bwd(const at::Tensor& p, const at::Tensor& dp, int64_t T, double scale);
+at::Tensor gelu_bwd(const at::Tensor& dy, const at::Tensor& pre);
+at::Tensor assemble_tokens(const at::Tensor& patches, const at::Tensor& cls, const at::Tensor& pos);
+at::Tensor assemble_tokens_bwd(const at::Tensor& dout, at::Tensor dpos, at::Tensor dcls);
+at::Tensor cls_rows(const at::Tensor& x, int64_t B, int64_t T, bool reverse);
+at::Tensor patchify(const at::Tensor& x, int64_t P);
+
 }  // namespace ops
 }  // namespace ringdp

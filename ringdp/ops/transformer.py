@@ -1,0 +1,208 @@
+"""Autograd Functions for transformer blocks (ViT-B/16, BASELINE.json config 5) on ringdp kernels.
+
+Token activations are row-major bf16 ``[rows, D]``.  Every matmul - the linear layers and all six
+attention products - is the generic MFMA GEMM core (``csrc/kernels/gemm.hip``) with its fused
+epilogue (bias, GELU with the pre-activation kept for backward, residual add); weight gradients use
+its split-K fp32 mode straight into the parameter's gradient slot; LayerNorm, softmax, GELU backward
+and the head/token layout moves are the row kernels of ``csrc/kernels/vit.hip``.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from .._native import C
+from . import grad_buffer
+
+_ONES: Dict[Tuple[int, torch.device], torch.Tensor] = {}
+
+
+def _ones_col(rows: int, device) -> torch.Tensor:
+    """[rows, 8] bf16 with column 0 = 1: a GEMM against it yields column sums (bias gradients)."""
+    key = (rows, torch.device(device))
+    t = _ONES.get(key)
+    if t is None:
+        t = torch.zeros(rows, 8, device=device, dtype=torch.bfloat16)
+        t[:, 0] = 1
+        _ONES[key] = t
+    return t
+
+
+def _bf16(w: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(w.shape, device=w.device, dtype=torch.bfloat16)
+    C.cast_copy(out, w.detach().contiguous())
+    return out
+
+
+def _splits(k: int) -> int:
+    return max(1, min(64, k // 512))
+
+
+class LinearF(torch.autograd.Function):
+    """y = act(x W^T + b) [+ residual]; act 0 = identity, 2 = GELU (erf)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, residual, act: int, out_f32: bool):
+        M, K = x.shape
+        N = w.shape[0]
+        Np = (N + 7) // 8 * 8  # the weight-gradient GEMM walks rows of W in 16-B vectors
+        wb = _bf16(w)
+        bb = b
+        if Np != N:
+            if residual is not None or act:
+                raise ValueError("LinearF: output features must be a multiple of 8 with residual/activation")
+            wb = torch.cat([wb, wb.new_zeros(Np - N, K)])
+            bb = None if b is None else torch.cat([b.detach(), b.new_zeros(Np - N)])
+        pre = torch.empty(M, Np, device=x.device, dtype=torch.bfloat16) if act == 2 else None
+        y = C.gemm(x, wb, M, Np, K, K, K, False, False, 1, 0, 0, not out_f32, bb, act, residual, pre).view(M, Np)
+        if Np != N:
+            y = y[:, :N].contiguous()
+        ctx.save_for_backward(x, wb, pre)
+        ctx.params = (w, b)
+        ctx.cfg = (act, residual is not None, N)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb, pre = ctx.saved_tensors
+        w, b = ctx.params
+        act, has_res, n_out = ctx.cfg
+        M, K = x.shape
+        N = wb.shape[0]
+        if N != n_out:
+            dyp = torch.zeros(M, N, device=dy.device, dtype=torch.bfloat16)
+            dyp[:, :n_out] = dy
+            dy = dyp
+        dyb = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
+        dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
+        dx = None
+        if ctx.needs_input_grad[0]:
+            # dX[m][k] = sum_n dz[m][n] W[n][k]:  A = dz (K-contiguous over n), B = W^T (row-contiguous)
+            dx = C.gemm(dz, wb, M, K, N, N, K, False, True).view(M, K)
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            # dW[n][k] = sum_m dz[m][n] x[m][k]:  A = dz^T, B = x^T (both row-contiguous), split over m
+            dw = grad_buffer(w)
+            if N == n_out:
+                C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M), dw)
+            else:
+                full_w = torch.empty(N, K, device=dy.device, dtype=torch.float32)
+                C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M), full_w)
+                dw.copy_(full_w[:n_out])
+        if b is not None and ctx.needs_input_grad[2]:
+            full = torch.empty(N, 8, device=dy.device, dtype=torch.float32)
+            C.gemm_splitk_f32(dz, _ones_col(M, dy.device), N, 8, M, N, 8, True, True, _splits(M), full)
+            db = grad_buffer(b)
+            db.copy_(full[:n_out, 0])
+        dres = dyb if has_res and ctx.needs_input_grad[3] else None
+        return dx, dw, db, dres, None, None
+
+
+class LayerNormF(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float):
+        y, stats = C.layernorm_fwd(x, w, b, eps)
+        ctx.save_for_backward(x, stats)
+        ctx.params = (w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, stats = ctx.saved_tensors
+        w, b = ctx.params
+        dw, db = grad_buffer(w), grad_buffer(b)
+        dx = C.layernorm_bwd(dy.contiguous(), x, stats, w, None, dw, db)
+        return dx, dw, db, None
+
+
+def _tp(t: int) -> int:
+    return (t + 15) // 16 * 16
+
+
+class AttentionF(torch.autograd.Function):
+    """Multi-head self-attention core on the packed qkv rows [B*T, 3*D] -> [B*T, D]."""
+
+    @staticmethod
+    def forward(ctx, qkv, B: int, T: int, H: int):
+        Tp = _tp(T)
+        q, k, v = C.qkv_split(qkv, B, T, H, Tp)
+        BH, _, Dh = q.shape
+        scale = 1.0 / math.sqrt(Dh)
+        # S = Q K^T (fp32), P = softmax(scale * S) over the T real keys
+        s = C.gemm(q, k, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
+        p = C.softmax_fwd(s, T, scale)
+        # O = P V:  A = P (K-contiguous over keys), B = V^T (row-contiguous: element (d, t) = V[t][d])
+        o = C.gemm(p, v, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
+        ctx.save_for_backward(q, k, v, p)
+        ctx.cfg = (B, T, H, Tp, scale)
+        return C.heads_to_rows(o.view(BH, Tp, Dh), B, T)
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, p = ctx.saved_tensors
+        B, T, H, Tp, scale = ctx.cfg
+        BH, _, Dh = q.shape
+        do = C.rows_to_heads(dout.contiguous(), B, T, H, Tp)
+        # dP = dO V^T (fp32) -> dS = scale * P * (dP - rowsum(dP * P))
+        dp = C.gemm(do, v, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
+        ds = C.softmax_bwd(p, dp, T, scale)
+        # dQ = dS K ; dK = dS^T Q ; dV = P^T dO
+        dq = C.gemm(ds, k, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
+        dk = C.gemm(ds, q, Tp, Dh, Tp, Tp, Dh, True, True, BH, Tp * Tp, Tp * Dh, True)
+        dv = C.gemm(p, do, Tp, Dh, Tp, Tp, Dh, True, True, BH, Tp * Tp, Tp * Dh, True)
+        dqkv = C.qkv_merge(dq.view(BH, Tp, Dh), dk.view(BH, Tp, Dh), dv.view(BH, Tp, Dh), B, T)
+        return dqkv, None, None, None
+
+
+class PatchTokensF(torch.autograd.Function):
+    """Patch embedding (stride = kernel conv as one GEMM over the patch rows) + class token +
+    position embedding -> token rows [B*T, D]."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, cls, pos, patch: int):
+        Bn = x.shape[0]
+        D = w.shape[0]
+        rows = C.patchify(x.contiguous(), patch)  # [B*NP, C*P*P]
+        wb = _bf16(w.reshape(D, -1))
+        emb = C.gemm(rows, wb, rows.shape[0], D, rows.shape[1], rows.shape[1], rows.shape[1], False, False, 1, 0, 0,
+                     True, b)
+        NP = rows.shape[0] // Bn
+        tokens = C.assemble_tokens(emb.view(Bn, NP, D), cls.reshape(-1), pos.reshape(-1))
+        ctx.save_for_backward(rows)
+        ctx.params = (w, b, cls, pos)
+        ctx.cfg = (Bn, NP, D)
+        return tokens.view(Bn * (NP + 1), D)
+
+    @staticmethod
+    def backward(ctx, dtok):
+        (rows,) = ctx.saved_tensors
+        w, b, cls, pos = ctx.params
+        Bn, NP, D = ctx.cfg
+        dpos, dcls = grad_buffer(pos), grad_buffer(cls)
+        demb = C.assemble_tokens_bwd(dtok.contiguous().view(Bn, NP + 1, D), dpos, dcls).view(Bn * NP, D)
+        M, K = rows.shape
+        dw = grad_buffer(w)
+        C.gemm_splitk_f32(demb, rows, D, K, M, D, K, True, True, _splits(M), dw)
+        full = torch.empty(D, 8, device=dtok.device, dtype=torch.float32)
+        C.gemm_splitk_f32(demb, _ones_col(M, dtok.device), D, 8, M, D, 8, True, True, _splits(M), full)
+        db = grad_buffer(b)
+        db.copy_(full[:, 0])
+        return None, dw, db, dcls, dpos, None
+
+
+class ClassRowsF(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, B: int, T: int):
+        ctx.cfg = (B, T)
+        return C.cls_rows(x, B, T, False)
+
+    @staticmethod
+    def backward(ctx, dy):
+        B, T = ctx.cfg
+        return C.cls_rows(dy.contiguous().to(torch.bfloat16), B, T, True).view(B * T, -1), None, None
+
+
+def linear(x, lin, act: int = 0, residual: Optional[torch.Tensor] = None, out_f32: bool = False):
+    return LinearF.apply(x, lin.weight, lin.bias, residual, act, out_f32)

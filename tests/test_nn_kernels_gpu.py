@@ -261,3 +261,53 @@ def test_resnet_matches_aten(arch, res):
     for (n, b), (_, c) in zip(m.named_buffers(), ref.named_buffers()):
         if b.dtype.is_floating_point:
             torch.testing.assert_close(b, c, rtol=5e-2, atol=5e-2), n
+
+
+def test_layernorm_softmax_kernels():
+    torch.manual_seed(3)
+    x = torch.randn(300, 768, device="cuda").bfloat16()
+    w = torch.rand(768, device="cuda") + 0.5
+    b = torch.randn(768, device="cuda")
+    y, stats = C().layernorm_fwd(x, w, b, 1e-6)
+    xr = x.float().requires_grad_()
+    wr, br = w.clone().requires_grad_(), b.clone().requires_grad_()
+    ref = F.layer_norm(xr, (768,), wr, br, 1e-6)
+    assert rel(y, ref) < 1e-2
+    dy = torch.randn_like(ref).bfloat16()
+    ref.backward(dy.float())
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    dx = C().layernorm_bwd(dy, x, stats, w, None, dw, db)
+    assert rel(dx, xr.grad) < 2e-2 and rel(dw, wr.grad) < 1e-2 and rel(db, br.grad) < 1e-2
+    T, Tp = 197, 208
+    s = torch.randn(6, Tp, Tp, device="cuda")
+    p = C().softmax_fwd(s, T, 0.125)
+    sr = s[:, :T, :T].clone().requires_grad_()
+    pr = torch.softmax(sr * 0.125, -1)
+    assert rel(p[:, :T, :T], pr) < 1e-2
+    assert float(p[:, T:, :].abs().max()) == 0 and float(p[:, :, T:].abs().max()) == 0
+    dp = torch.randn(6, Tp, Tp, device="cuda")
+    pr.backward(dp[:, :T, :T])
+    ds = C().softmax_bwd(p, dp, T, 0.125)
+    assert rel(ds[:, :T, :T], sr.grad) < 2e-2
+
+
+def test_vit_matches_aten():
+    import copy
+
+    from ringdp.models import vit_tiny
+
+    torch.manual_seed(0)
+    m = vit_tiny(num_classes=16).cuda()
+    torch.nn.init.normal_(m.heads.head.weight, std=0.05)
+    ref = copy.deepcopy(m)
+    x = torch.randn(8, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 16, (8,), device="cuda")
+    out = m(x)
+    out_ref = ref.reference_forward(x)
+    assert out.shape == (8, 16) and out.dtype == torch.float32
+    assert _cos(out.detach(), out_ref.detach()) > 0.995
+    F.cross_entropy(out, y).backward()
+    F.cross_entropy(out_ref, y).backward()
+    cos = {n: _cos(p.grad, q.grad) for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters())}
+    bad = {n: round(c, 4) for n, c in cos.items() if c < 0.98}
+    assert not bad, bad
