@@ -10,6 +10,7 @@
 #include "ops/ops.h"
 #include "reducer/reducer.h"
 #include "store/store.h"
+#include "trace/trace.h"
 
 namespace py = pybind11;
 using namespace ringdp;
@@ -367,6 +368,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lr_tensor") = py::none(), py::arg("grad_scale") = py::none());
   m.def("cross_entropy_fwd", &ops::cross_entropy_fwd);
   m.def("cross_entropy_bwd", &ops::cross_entropy_bwd);
+  // roctx tracing (rocprofv3 --marker-trace)
+  m.def("trace_enabled", &trace::enabled);
+  m.def("trace_set_enabled", &trace::set_enabled);
+  m.def("trace_push", [](const std::string& n) { trace::push(n.c_str()); });
+  m.def("trace_pop", &trace::pop);
+  m.def("trace_mark", [](const std::string& n) { trace::mark(n.c_str()); });
   m.def("gather_augment", &ops::gather_augment, py::arg("x"), py::arg("labels"), py::arg("idx"),
         py::arg("pad") = 0, py::arg("flip") = false, py::arg("mean") = std::vector<double>{},
         py::arg("std") = std::vector<double>{}, py::arg("seed") = 0, py::arg("nhwc") = false,

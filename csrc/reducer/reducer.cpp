@@ -1,6 +1,8 @@
 // ringdp gradient Reducer implementation (see reducer.h).
 #include "reducer.h"
 
+#include "../trace/trace.h"
+
 #include <torch/csrc/autograd/engine.h>
 #include <torch/csrc/autograd/functions/accumulate_grad.h>
 #include <torch/csrc/autograd/utils/lambda_post_hook.h>
@@ -308,6 +310,10 @@ void Reducer::launch_ready_buckets() {
 
 void Reducer::launch_bucket(Bucket& b, int64_t index) {
   b.launched = true;
+  if (trace::enabled()) {
+    const std::string tag = "ringdp.bucket" + std::to_string(index) + ".launch";
+    trace::mark(tag.c_str());
+  }
   b.st.last_launch_us = static_cast<double>(now_us() - backward_start_us_);
   if (pg_->size() == 1 || hook_ == CommHook::NONE) {
     b.work.reset();

@@ -36,8 +36,12 @@ def _bf16(w: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _splits(k: int) -> int:
-    return max(1, min(64, k // 512))
+def _splits(k: int, m: int = 128, n: int = 128, cus: int = 256) -> int:
+    """Split-K count for an (m x n) weight-gradient GEMM reducing over k rows: enough workgroups to
+    cover the chip twice, but few fp32 partial planes (each is m*n*4 bytes of traffic)."""
+    tiles = ((m + 127) // 128) * ((n + 127) // 128)
+    want = max(1, (2 * cus + tiles - 1) // tiles)
+    return max(1, min(want, k // 256, 32))
 
 
 class LinearF(torch.autograd.Function):
@@ -86,14 +90,14 @@ class LinearF(torch.autograd.Function):
             # dW[n][k] = sum_m dz[m][n] x[m][k]:  A = dz^T, B = x^T (both row-contiguous), split over m
             dw = grad_buffer(w)
             if N == n_out:
-                C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M), dw)
+                C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M, N, K), dw)
             else:
                 full_w = torch.empty(N, K, device=dy.device, dtype=torch.float32)
-                C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M), full_w)
+                C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M, N, K), full_w)
                 dw.copy_(full_w[:n_out])
         if b is not None and ctx.needs_input_grad[2]:
             full = torch.empty(N, 8, device=dy.device, dtype=torch.float32)
-            C.gemm_splitk_f32(dz, _ones_col(M, dy.device), N, 8, M, N, 8, True, True, _splits(M), full)
+            C.gemm_splitk_f32(dz, _ones_col(M, dy.device), N, 8, M, N, 8, True, True, _splits(M, N, 8), full)
             db = grad_buffer(b)
             db.copy_(full[:n_out, 0])
         dres = dyb if has_res and ctx.needs_input_grad[3] else None
@@ -184,9 +188,9 @@ class PatchTokensF(torch.autograd.Function):
         demb = C.assemble_tokens_bwd(dtok.contiguous().view(Bn, NP + 1, D), dpos, dcls).view(Bn * NP, D)
         M, K = rows.shape
         dw = grad_buffer(w)
-        C.gemm_splitk_f32(demb, rows, D, K, M, D, K, True, True, _splits(M), dw)
+        C.gemm_splitk_f32(demb, rows, D, K, M, D, K, True, True, _splits(M, D, K), dw)
         full = torch.empty(D, 8, device=dtok.device, dtype=torch.float32)
-        C.gemm_splitk_f32(demb, _ones_col(M, dtok.device), D, 8, M, D, 8, True, True, _splits(M), full)
+        C.gemm_splitk_f32(demb, _ones_col(M, dtok.device), D, 8, M, D, 8, True, True, _splits(M, D, 8), full)
         db = grad_buffer(b)
         db.copy_(full[:, 0])
         return None, dw, db, dcls, dpos, None

@@ -21,6 +21,7 @@ import torch
 from torch.optim.optimizer import Optimizer
 
 from .._native import C
+from ..utils import tracing as _tracing
 
 
 class SGD(Optimizer):
@@ -40,6 +41,12 @@ class SGD(Optimizer):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay,
                         nesterov=nesterov, maximize=maximize)
         super().__init__(params, defaults)
+        self._flat_cache = {}
+        self._multi_cache = {}
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        # drop the fused-kernel layouts: the next step re-adopts the loaded momentum buffers
         self._flat_cache = {}
         self._multi_cache = {}
 
@@ -96,6 +103,7 @@ class SGD(Optimizer):
 
     # ------------------------------------------------------------------ step
     @torch.no_grad()
+    @_tracing.annotate("ringdp.SGD.step")
     def step(self, closure=None):
         loss = None
         if closure is not None:

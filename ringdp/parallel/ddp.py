@@ -33,6 +33,7 @@ import torch.nn as nn
 from .. import distributed as dist
 from .._native import C
 from . import comm_hooks as default_hooks
+from ..utils import tracing as _tracing
 
 _DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
 _BROADCAST_BUCKET_BYTES = 250 * 1024 * 1024
@@ -299,7 +300,8 @@ class DistributedDataParallel(nn.Module):
         return obj
 
     def forward(self, *inputs, **kwargs):
-        with torch.autograd.profiler.record_function("DistributedDataParallel.forward"):
+        with torch.autograd.profiler.record_function("DistributedDataParallel.forward"), \
+                _tracing.range("ringdp.DDP.forward"):
             grad = torch.is_grad_enabled() and self.require_backward_grad_sync
             if grad:
                 self._maybe_rebuild_buckets()

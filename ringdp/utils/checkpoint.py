@@ -1,0 +1,63 @@
+"""Checkpoint / resume for DDP training (absent in the reference, optional here).
+
+* ``save(path, model, optimizer, **meta)``: rank 0 writes ``{model, optimizer, meta}`` with
+  ``torch.save`` (DDP wrappers are unwrapped, so the file loads into a bare model too), then all ranks
+  meet at a barrier so nobody races ahead of a half-written file.  The write goes to ``path.tmp`` and
+  is renamed, so an interrupted save never leaves a truncated checkpoint behind.
+* ``load(path, model, optimizer=None, broadcast=True)``: reads with ``weights_only=True`` (no code
+  execution from the file).  With ``broadcast`` only rank 0 reads; parameters, buffers and optimizer
+  state are then broadcast from rank 0, which also guarantees identical replicas after resume.
+  Returns the ``meta`` dict (epoch, step, sampler epoch, ...).
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+
+import torch
+
+from .. import distributed as dist
+
+
+def _unwrap(model):
+    return getattr(model, "module", model)
+
+
+def _rank() -> int:
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
+def save(path: str, model, optimizer=None, **meta: Any) -> None:
+    if _rank() == 0:
+        state = {"model": _unwrap(model).state_dict(), "meta": dict(meta)}
+        if optimizer is not None:
+            state["optimizer"] = optimizer.state_dict()
+        tmp = path + ".tmp"
+        torch.save(state, tmp)
+        os.replace(tmp, path)
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def load(path: str, model, optimizer=None, broadcast: bool = True, map_location=None) -> Dict[str, Any]:
+    m = _unwrap(model)
+    dev = next(m.parameters()).device
+    reader = (not broadcast) or _rank() == 0 or not dist.is_initialized()
+    meta: Dict[str, Any] = {}
+    if reader:
+        state = torch.load(path, map_location=map_location or dev, weights_only=True)
+        m.load_state_dict(state["model"])
+        if optimizer is not None and "optimizer" in state:
+            optimizer.load_state_dict(state["optimizer"])
+        meta = state.get("meta", {})
+    if broadcast and dist.is_initialized() and dist.get_world_size() > 1:
+        with torch.no_grad():
+            for t in list(m.parameters()) + list(m.buffers()):
+                dist.broadcast(t.data, src=0)
+        if optimizer is not None:
+            box = [optimizer.state_dict() if _rank() == 0 else None, meta]
+            dist.broadcast_object_list(box, src=0)
+            if _rank() != 0:
+                optimizer.load_state_dict(box[0])
+                meta = box[1]
+    return meta

@@ -270,3 +270,50 @@ def spawn_exit(i):
     if i == 0:
         sys.exit(7)
     time.sleep(30)
+
+
+def checkpoint_resume_worker(rank, world, init_file, out_dir):
+    """Train 2 steps, save, 2 more; then a fresh model+optimizer resumes from the checkpoint and
+    runs the same 2 steps: the parameters must match bit for bit."""
+    import os
+
+    import torch
+
+    import ringdp
+    import ringdp.distributed as dist
+    from ringdp.models import ConvNet
+    from ringdp.optim import SGD
+    from ringdp.utils import checkpoint
+
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(rank)
+    xs = [torch.randn(4, 1, 28, 28, generator=g) for _ in range(4)]
+    ys = [torch.randint(0, 10, (4,), generator=g) for _ in range(4)]
+
+    def make():
+        torch.manual_seed(0)
+        m = ringdp.DistributedDataParallel(ConvNet())
+        return m, SGD(m.parameters(), lr=0.05, momentum=0.9, nesterov=True, weight_decay=1e-4)
+
+    def step(m, o, i):
+        loss = torch.nn.functional.cross_entropy(m(xs[i]), ys[i])
+        o.zero_grad()
+        loss.backward()
+        o.step()
+
+    ckpt = os.path.join(out_dir, "ck.pt")
+    m, o = make()
+    step(m, o, 0)
+    step(m, o, 1)
+    checkpoint.save(ckpt, m, o, epoch=3, step=2)
+    step(m, o, 2)
+    step(m, o, 3)
+    ref = [p.detach().clone() for p in m.parameters()]
+    m2, o2 = make()
+    meta = checkpoint.load(ckpt, m2, o2)
+    assert meta == {"epoch": 3, "step": 2}, meta
+    step(m2, o2, 2)
+    step(m2, o2, 3)
+    for a, b in zip(ref, m2.parameters()):
+        assert torch.equal(a, b.detach()), (a - b).abs().max()
+    dist.destroy_process_group()

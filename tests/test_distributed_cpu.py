@@ -104,3 +104,9 @@ def test_spawn_propagates_exit_code():
     with pytest.raises(ProcessExitedException) as ei:
         spawn(W.spawn_exit, nprocs=2)
     assert ei.value.exit_code == 7 and ei.value.error_index == 0
+
+
+def test_checkpoint_resume_bitwise(tmp_path):
+    from ringdp.multiprocessing import spawn
+
+    spawn(W.checkpoint_resume_worker, args=(2, str(tmp_path / "init"), str(tmp_path)), nprocs=2)
