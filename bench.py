@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--comm-hook", type=str, default="allreduce", choices=["allreduce", "bf16_compress", "fp16_compress"])
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph per step")
     ap.add_argument("--pool", type=int, default=8, help="number of distinct synthetic batches cycled")
+    ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: e4m3 linear-layer GEMMs on the block-scaled MFMA (vit_b_16)")
     ap.add_argument("--local-rank", "--local_rank", type=int, default=None)
     return ap.parse_args()
 
@@ -87,6 +89,11 @@ def main():
     B = args.batch_per_rank or int(os.environ.get("RINGDP_BENCH_BATCH", spec["batch"]))
     lr = args.lr if args.lr is not None else spec["lr"]
 
+    if args.dtype == "fp8":
+        if args.model != "vit_b_16":
+            raise SystemExit("--dtype fp8 is implemented for --model vit_b_16")
+        from ringdp.ops.transformer import set_fp8
+        set_fp8(True)
     torch.manual_seed(0)
     if args.model == "convnet":
         model = models.ConvNet().to(dev)
@@ -183,7 +190,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype if args.dtype == "bf16" else "fp8 (e4m3 linear GEMMs, bf16 attention/norms)",
             "data": data,
             "config": {
                 "model": spec["desc"],

@@ -411,6 +411,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("assemble_tokens_bwd", &ops::assemble_tokens_bwd);
   m.def("cls_rows", &ops::cls_rows);
   m.def("patchify", &ops::patchify);
+  m.def("fp8_quantize", &ops::fp8_quantize);
+  m.def("fp8_quantize_both", &ops::fp8_quantize_both);
+  m.def("gemm_fp8", &ops::gemm_fp8, py::arg("a"), py::arg("b"), py::arg("scale_a"), py::arg("scale_b"), py::arg("M"),
+        py::arg("N"), py::arg("K"), py::arg("out_bf16") = true, py::arg("bias") = py::none(), py::arg("act") = 0,
+        py::arg("residual") = py::none(), py::arg("preact") = py::none());
+  m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);

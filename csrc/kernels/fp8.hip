@@ -1,0 +1,118 @@
+// Per-tensor e4m3 (OCP, gfx950-native) quantisation for the fp8 GEMM path (BASELINE.json config 5,
+// "ViT-B/16 ... fp8: CDNA4 fp8 MFMA GEMM path").
+//   amax  : |x|max over a bf16 tensor (atomicMax on the float bits of non-negative values:
+//           order-independent, so deterministic)
+//   quant : scale = max(amax, tiny) / 448 (written to device memory for the GEMM epilogue),
+//           q = cvt_e4m3(x / scale); optional transpose through a 64x64 LDS tile so every GEMM
+//           operand (x^T, w^T, dy^T) is K-contiguous.  No host synchronisation anywhere.
+#include <algorithm>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace ringdp {
+namespace kern {
+
+using namespace ringdp::dev;
+
+namespace {
+
+constexpr float kE4M3Max = 448.f;
+
+__global__ __launch_bounds__(256) void amax_kernel(const bf16* __restrict__ x, int64_t nvec,
+                                                   unsigned* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const bf16x8 t = reinterpret_cast<const bf16x8*>(x)[v];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)t[j]));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+__device__ __forceinline__ float qscale(const float* amax) { return fmaxf(amax[0], 1e-12f) / kE4M3Max; }
+
+__device__ __forceinline__ uint32_t pack4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+__global__ __launch_bounds__(256) void quant_kernel(const bf16* __restrict__ x, int64_t nvec,
+                                                    const float* __restrict__ amax, uint8_t* __restrict__ out,
+                                                    float* __restrict__ scale) {
+  const float inv = 1.f / qscale(amax);
+  if (blockIdx.x == 0 && threadIdx.x == 0) scale[0] = qscale(amax);
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const bf16x8 t = reinterpret_cast<const bf16x8*>(x)[v];
+    uint2 o;
+    o.x = pack4((float)t[0] * inv, (float)t[1] * inv, (float)t[2] * inv, (float)t[3] * inv);
+    o.y = pack4((float)t[4] * inv, (float)t[5] * inv, (float)t[6] * inv, (float)t[7] * inv);
+    reinterpret_cast<uint2*>(out)[v] = o;
+  }
+}
+
+// x [rows][cols] bf16 -> out [cols][rows] e4m3 (and, when out_rm != null, the row-major copy too:
+// one read of x for both GEMM orientations); 64x64 tiles through LDS (rows, cols % 16 == 0)
+__global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
+                                                      const float* __restrict__ amax, uint8_t* __restrict__ out,
+                                                      float* __restrict__ scale, uint8_t* __restrict__ out_rm) {
+  __shared__ float tile[64][65];
+  const float inv = 1.f / qscale(amax);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) scale[0] = qscale(amax);
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int t = threadIdx.x;
+  // load: 64 rows x 8 vectors of 8 -> thread t: row t/4 (+0, +64..) -> use 2 passes of 32 rows
+  for (int pass = 0; pass < 2; ++pass) {
+    const int r = (t >> 3) + 32 * pass, cv = t & 7;
+    const int64_t gr = r0 + r, gc = c0 + cv * 8;
+    bf16x8 v = zero_bf16x8();
+    if (gr < rows && gc < cols) v = *reinterpret_cast<const bf16x8*>(x + gr * cols + gc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[r][cv * 8 + j] = (float)v[j] * inv;
+    if (out_rm && gr < rows && gc < cols) {
+      uint2 o;
+      o.x = pack4(tile[r][cv * 8 + 0], tile[r][cv * 8 + 1], tile[r][cv * 8 + 2], tile[r][cv * 8 + 3]);
+      o.y = pack4(tile[r][cv * 8 + 4], tile[r][cv * 8 + 5], tile[r][cv * 8 + 6], tile[r][cv * 8 + 7]);
+      *reinterpret_cast<uint2*>(out_rm + gr * cols + gc) = o;
+    }
+  }
+  __syncthreads();
+  // store: out row = column c of x, 64 rows x 64 bytes -> thread t: out row t/4, 16 bytes
+  const int oc = t >> 2, seg = (t & 3) * 16;
+  const int64_t gr = c0 + oc;
+  if (gr < cols && r0 + seg < rows) {
+    uint4 o;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      w[q] = pack4(tile[seg + 4 * q][oc], tile[seg + 4 * q + 1][oc], tile[seg + 4 * q + 2][oc], tile[seg + 4 * q + 3][oc]);
+    *reinterpret_cast<uint4*>(out + gr * rows + r0 + seg) = o;
+  }
+}
+
+}  // namespace
+
+void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s) {
+  hipMemsetAsync(amax, 0, sizeof(float), s);
+  const int64_t nvec = n / 8;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nvec + 255) / 256, 2048));
+  amax_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), nvec, reinterpret_cast<unsigned*>(amax));
+}
+
+void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, const float* amax, void* out,
+                  float* scale, hipStream_t s, void* out_rowmajor) {
+  if (!transpose) {
+    const int64_t nvec = rows * cols / 8;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nvec + 255) / 256, 8192));
+    quant_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), nvec, amax, static_cast<uint8_t*>(out), scale);
+  } else {
+    dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+    quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, amax, static_cast<uint8_t*>(out),
+                                        scale, static_cast<uint8_t*>(out_rowmajor));
+  }
+}
+
+}  // namespace kern
+}  // namespace ringdp

@@ -190,7 +190,27 @@ __device__ __forceinline__ bf16x8 frag(const bf16* s, int r0, int kk, int lane) 
 }
 
 // ------------------------------------------------------------------ the kernel
-template <class LA, class LB>
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// fp8 (e4m3, OCP) operand fragment for v_mfma_scale_f32_16x16x128_f8f6f4: lane l holds row l&15,
+// k = 32*(l>>4) + j (j < 32) = 32 bytes = two 16-B reads of a K-contiguous stage.  In the stage,
+// one bf16 "slot" is 2 fp8 bytes, so a 64-slot stage row is 128 fp8 values = one MFMA k-step.
+__device__ __forceinline__ i32x8 frag_fp8(const bf16* s, int r0, int lane) {
+  const bf16* p = s + (r0 + (lane & 15)) * KPAD + 16 * (lane >> 4);
+  const bf16x8 lo = *reinterpret_cast<const bf16x8*>(p);
+  const bf16x8 hi = *reinterpret_cast<const bf16x8*>(p + 8);
+  i32x8 r;
+  const int* a = reinterpret_cast<const int*>(&lo);
+  const int* b = reinterpret_cast<const int*>(&hi);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    r[i] = a[i];
+    r[4 + i] = b[i];
+  }
+  return r;
+}
+
+template <class LA, class LB, bool kFp8 = false>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue ep, int M, int N, int K,
                                                       int tiles_m, int tiles_n, int splits, int k_per_split) {
   __shared__ __attribute__((aligned(16))) bf16 smem[2][2][STAGE_ELEMS];  // [stage][A|B]
@@ -232,17 +252,31 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
     }
     const bf16* As = smem[cur][0];
     const bf16* Bs = smem[cur][1];
+    if constexpr (kFp8) {
+      static_assert(!LA::kRow && !LB::kRow, "fp8 GEMM: K-contiguous operands only");
+      i32x8 fa[4], fb[4];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 fa[4], fb[4];
+      for (int i = 0; i < 4; ++i) fa[i] = frag_fp8(As, wm * 64 + 16 * i, lane);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag<LA::kRow>(As, wm * 64 + 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag<LB::kRow>(Bs, wn * 64 + 16 * j, kk, lane);
+      for (int j = 0; j < 4; ++j) fb[j] = frag_fp8(Bs, wn * 64 + 16 * j, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // C^T tile
+        for (int j = 0; j < 4; ++j)  // e4m3 x e4m3, unit block scales (2^0 = e8m0 127): per-tensor scales in the epilogue
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[j], fa[i], acc[i][j], 0, 0, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag<LA::kRow>(As, wm * 64 + 16 * i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag<LB::kRow>(Bs, wn * 64 + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // C^T tile
+      }
     }
     if (more) {
       sa.store(smem[cur ^ 1][0], tid);
@@ -255,6 +289,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
   //                  n = n0 + wn*64 + 16j + 4*(lane>>4)
   const int mrow = m0 + wm * 64 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+  const float dscale = (ep.scale_a ? ep.scale_a[0] : 1.f) * (ep.scale_b ? ep.scale_b[0] : 1.f);
+  if (dscale != 1.f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] *= dscale;
+  }
   if (ep.mode == GemmEpilogue::kSplitK) {
     float* out = ep.partial + ((int64_t)zid) * M * N;
 #pragma unroll
@@ -377,7 +418,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
   }
 }
 
-template <class LA, class LB>
+template <class LA, class LB, bool kFp8 = false>
 void launch(const LA& la, const LB& lb, const GemmEpilogue& ep, int batch, int M, int N, int K, int splits,
             hipStream_t s) {
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
@@ -386,7 +427,7 @@ void launch(const LA& la, const LB& lb, const GemmEpilogue& ep, int batch, int M
   kps = (kps + BK - 1) / BK * BK;
   splits = (K + kps - 1) / kps;
   dim3 grid(tiles_m * tiles_n, batch * splits);
-  gemm_kernel<LA, LB><<<grid, 256, 0, s>>>(la, lb, ep, M, N, K, tiles_m, tiles_n, splits, kps);
+  gemm_kernel<LA, LB, kFp8><<<grid, 256, 0, s>>>(la, lb, ep, M, N, K, tiles_m, tiles_n, splits, kps);
 }
 
 // ------------------------------------------------------------------ reductions
@@ -462,6 +503,14 @@ void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int
     launch(Dense<true>{da}, Dense<false>{db}, ep, batch, M, N, K, splits, s);
   else
     launch(Dense<true>{da}, Dense<true>{db}, ep, batch, M, N, K, splits, s);
+}
+
+void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes, const GemmEpilogue& ep,
+              int splits, hipStream_t s) {
+  // K-contiguous e4m3 operands viewed as bf16 "slots" of 2 bytes for the 16-B stagers
+  const DenseLoader da{static_cast<const bf16*>(A.p), A.ld / 2, A.bstride / 2, M, Kbytes / 2};
+  const DenseLoader db{static_cast<const bf16*>(B.p), B.ld / 2, B.bstride / 2, N, Kbytes / 2};
+  launch<Dense<false>, Dense<false>, true>(Dense<false>{da}, Dense<false>{db}, ep, batch, M, N, Kbytes / 2, splits, s);
 }
 
 void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {

@@ -109,6 +109,8 @@ struct GemmEpilogue {
   const void* residual;  // bf16, same layout as C, added before the activation
   float* stats;       // [b][tiles_m][2][N] per-channel sum / sumsq partials of the stored C, or null
   float* partial;     // split-K fp32 partials [b*splits][M][N]
+  const float* scale_a;  // optional device per-tensor dequant scales (fp8 GEMM): C *= scale_a[0]*scale_b[0]
+  const float* scale_b;
 };
 struct ConvGeom {
   int N, H, W, C;   // input NHWC (C padded to a multiple of 8)
@@ -118,6 +120,14 @@ struct ConvGeom {
 };
 void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K, const GemmEpilogue& ep,
                int splits, hipStream_t s);
+// e4m3 x e4m3 (both K-contiguous; ld / bstride / K in BYTES, multiples of 16) on the block-scaled
+// MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales; per-tensor scales via ep.scale_a/b).
+void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes, const GemmEpilogue& ep,
+              int splits, hipStream_t s);
+// per-tensor fp8 quantisation (fp8.hip): amax -> scale = amax / 448 -> e4m3, optionally transposed
+void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s);
+void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, const float* amax, void* out,
+                  float* scale, hipStream_t s, void* out_rowmajor = nullptr);
 void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,

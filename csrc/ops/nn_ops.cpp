@@ -460,6 +460,90 @@ at::Tensor cls_rows(const at::Tensor& x, int64_t B, int64_t T, bool reverse) {
   return y;
 }
 
+// ------------------------------------------------------------------ fp8 (e4m3) GEMM path
+std::tuple<at::Tensor, at::Tensor> fp8_quantize(const at::Tensor& x, bool transpose) {
+  bf16_gpu(x, "fp8 quantize input");
+  RINGDP_CHECK(x.dim() == 2, "fp8_quantize: expected a 2-D tensor");
+  const int64_t R = x.size(0), Cc = x.size(1);
+  RINGDP_CHECK(Cc % 16 == 0 && (!transpose || R % 16 == 0), "fp8_quantize: dims must be multiples of 16");
+  auto f = x.options().dtype(at::kFloat);
+  at::Tensor amax = at::empty({1}, f), scale = at::empty({1}, f);
+  at::Tensor q = transpose ? at::empty({Cc, R}, x.options().dtype(at::kByte)) : at::empty({R, Cc}, x.options().dtype(at::kByte));
+  kern::fp8_amax(x.data_ptr(), x.numel(), amax.data_ptr<float>(), stream_of(x));
+  kern::fp8_quantize(x.data_ptr(), R, Cc, transpose, amax.data_ptr<float>(), q.data_ptr(), scale.data_ptr<float>(),
+                     stream_of(x));
+  return {q, scale};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both(const at::Tensor& x) {
+  bf16_gpu(x, "fp8 quantize input");
+  RINGDP_CHECK(x.dim() == 2 && x.size(0) % 16 == 0 && x.size(1) % 16 == 0,
+               "fp8_quantize_both: expected a 2-D tensor with dims % 16 == 0");
+  const int64_t R = x.size(0), Cc = x.size(1);
+  auto f = x.options().dtype(at::kFloat);
+  at::Tensor amax = at::empty({1}, f), scale = at::empty({1}, f);
+  at::Tensor q = at::empty({R, Cc}, x.options().dtype(at::kByte)), qt = at::empty({Cc, R}, x.options().dtype(at::kByte));
+  kern::fp8_amax(x.data_ptr(), x.numel(), amax.data_ptr<float>(), stream_of(x));
+  kern::fp8_quantize(x.data_ptr(), R, Cc, true, amax.data_ptr<float>(), qt.data_ptr(), scale.data_ptr<float>(),
+                     stream_of(x), q.data_ptr());
+  return {q, qt, scale};
+}
+
+at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
+                    int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,
+                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& preact) {
+  gpu(a, "fp8 A");
+  gpu(b, "fp8 B");
+  dtype(a, at::kByte, "fp8 A");
+  dtype(b, at::kByte, "fp8 B");
+  f32_gpu(scale_a, "fp8 scale A");
+  f32_gpu(scale_b, "fp8 scale B");
+  RINGDP_CHECK(K % 16 == 0, "gemm_fp8: K must be a multiple of 16");
+  RINGDP_CHECK(a.numel() >= M * K && b.numel() >= N * K, "gemm_fp8: operand smaller than described");
+  at::Tensor c = at::empty({M, N}, a.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  auto e = make_epi(c.data_ptr(), N, 0, out_bf16);
+  e.act = static_cast<int>(act);
+  e.scale_a = scale_a.data_ptr<float>();
+  e.scale_b = scale_b.data_ptr<float>();
+  if (bias.has_value() && bias->defined()) {
+    f32_gpu(*bias, "gemm bias");
+    e.bias = bias->data_ptr<float>();
+  }
+  if (residual.has_value() && residual->defined()) {
+    bf16_gpu(*residual, "gemm residual");
+    e.residual = residual->data_ptr();
+  }
+  if (preact.has_value() && preact->defined()) {
+    bf16_gpu(*preact, "gemm preact");
+    e.preact = preact->data_ptr();
+  }
+  kern::GemmOperand A{a.data_ptr(), K, 0, false}, B{b.data_ptr(), K, 0, false};
+  kern::gemm_fp8(A, B, 1, (int)M, (int)N, (int)K, e, 1, stream_of(a));
+  return c;
+}
+
+void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a,
+                         const at::Tensor& scale_b, int64_t M, int64_t N, int64_t K, int64_t splits, at::Tensor out) {
+  gpu(a, "fp8 A");
+  gpu(b, "fp8 B");
+  f32_gpu(out, "fp8 gemm out");
+  RINGDP_CHECK(K % 16 == 0 && out.numel() == M * N, "gemm_fp8_splitk_f32: bad shapes");
+  splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 128)));
+  at::Tensor part = at::empty({splits, M, N}, out.options());
+  kern::GemmEpilogue e{};
+  e.mode = kern::GemmEpilogue::kSplitK;
+  e.partial = part.data_ptr<float>();
+  e.scale_a = scale_a.data_ptr<float>();
+  e.scale_b = scale_b.data_ptr<float>();
+  kern::GemmOperand A{a.data_ptr(), K, 0, false}, B{b.data_ptr(), K, 0, false};
+  kern::gemm_fp8(A, B, 1, (int)M, (int)N, (int)K, e, (int)splits, stream_of(a));
+  // split boundaries are in 64-slot (128-byte) units; sum only the planes that were written
+  const int64_t kslots = K / 2;
+  const int64_t kps = ((kslots + splits - 1) / splits + 63) / 64 * 64;
+  const int64_t used = (kslots + kps - 1) / kps;
+  kern::splitk_sum(part.data_ptr<float>(), (int)used, M * N, out.data_ptr<float>(), stream_of(a));
+}
+
 at::Tensor patchify(const at::Tensor& x, int64_t P) {
   gpu(x, "images");
   RINGDP_CHECK(x.dim() == 4 && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),

@@ -54,6 +54,13 @@ at::Tensor assemble_tokens(const at::Tensor& patches, const at::Tensor& cls, con
 at::Tensor assemble_tokens_bwd(const at::Tensor& dout, at::Tensor dpos, at::Tensor dcls);
 at::Tensor cls_rows(const at::Tensor& x, int64_t B, int64_t T, bool reverse);
 at::Tensor patchify(const at::Tensor& x, int64_t P);
+std::tuple<at::Tensor, at::Tensor> fp8_quantize(const at::Tensor& x, bool transpose);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both(const at::Tensor& x);
+at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
+                    int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,
+                    const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& preact);
+void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a,
+                         const at::Tensor& scale_b, int64_t M, int64_t N, int64_t K, int64_t splits, at::Tensor out);
 
 }  // namespace ops
 }  // namespace ringdp

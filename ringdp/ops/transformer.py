@@ -17,6 +17,17 @@ from .._native import C
 from . import grad_buffer
 
 _ONES: Dict[Tuple[int, torch.device], torch.Tensor] = {}
+_FP8 = {"on": False}
+
+
+def set_fp8(on: bool = True) -> None:
+    """Run the linear layers' forward, data-gradient and weight-gradient GEMMs in e4m3 on the
+    block-scaled MFMA (per-tensor current scaling; attention products stay bf16)."""
+    _FP8["on"] = bool(on)
+
+
+def fp8_enabled() -> bool:
+    return _FP8["on"]
 
 
 def _ones_col(rows: int, device) -> torch.Tensor:
@@ -51,6 +62,9 @@ class LinearF(torch.autograd.Function):
     def forward(ctx, x, w, b, residual, act: int, out_f32: bool):
         M, K = x.shape
         N = w.shape[0]
+        if _FP8["on"] and M % 16 == 0 and N % 16 == 0 and K % 16 == 0:
+            return _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32)
+        ctx.fp8 = False
         Np = (N + 7) // 8 * 8  # the weight-gradient GEMM walks rows of W in 16-B vectors
         wb = _bf16(w)
         bb = b
@@ -70,6 +84,8 @@ class LinearF(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.fp8:
+            return _linear_fp8_bwd(ctx, dy)
         x, wb, pre = ctx.saved_tensors
         w, b = ctx.params
         act, has_res, n_out = ctx.cfg
@@ -102,6 +118,45 @@ class LinearF(torch.autograd.Function):
             db.copy_(full[:n_out, 0])
         dres = dyb if has_res and ctx.needs_input_grad[3] else None
         return dx, dw, db, dres, None, None
+
+
+def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
+    M, K = x.shape
+    N = w.shape[0]
+    wb = _bf16(w)
+    xq, xtq, sx = C.fp8_quantize_both(x)   # row-major for this GEMM, transposed for the weight grad
+    wq, wtq, sw = C.fp8_quantize_both(wb)  # ... and for the data grad
+    pre = torch.empty(M, N, device=x.device, dtype=torch.bfloat16) if act == 2 else None
+    y = C.gemm_fp8(xq, wq, sx, sw, M, N, K, not out_f32, b, act, residual, pre)
+    ctx.fp8 = True
+    ctx.save_for_backward(xtq, sx, wtq, sw, pre)
+    ctx.shape = (M, K)
+    ctx.params = (w, b)
+    ctx.cfg = (act, residual is not None, N)
+    return y
+
+
+def _linear_fp8_bwd(ctx, dy):
+    xtq, sx, wtq, sw, pre = ctx.saved_tensors
+    w, b = ctx.params
+    act, has_res, N = ctx.cfg
+    M, K = ctx.shape
+    dyb = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
+    dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
+    dx = dw = db = None
+    dzq, dztq, sdz = C.fp8_quantize_both(dz)  # [M][N] for the data grad, [N][M] for the weight grad
+    if ctx.needs_input_grad[0]:
+        dx = C.gemm_fp8(dzq, wtq, sdz, sw, M, K, N, True)
+    if ctx.needs_input_grad[1]:
+        dw = grad_buffer(w)
+        C.gemm_fp8_splitk_f32(dztq, xtq, sdz, sx, N, K, M, _splits(M, N, K), dw)
+    if b is not None and ctx.needs_input_grad[2]:
+        full = torch.empty(N, 8, device=dy.device, dtype=torch.float32)
+        C.gemm_splitk_f32(dz, _ones_col(M, dy.device), N, 8, M, N, 8, True, True, _splits(M, N, 8), full)
+        db = grad_buffer(b)
+        db.copy_(full[:, 0])
+    dres = dyb if has_res and ctx.needs_input_grad[3] else None
+    return dx, dw, db, dres, None, None
 
 
 class LayerNormF(torch.autograd.Function):

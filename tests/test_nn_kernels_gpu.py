@@ -311,3 +311,68 @@ def test_vit_matches_aten():
     cos = {n: _cos(p.grad, q.grad) for (n, p), (_, q) in zip(m.named_parameters(), ref.named_parameters())}
     bad = {n: round(c, 4) for n, c in cos.items() if c < 0.98}
     assert not bad, bad
+
+
+def _fp8_ref(x):
+    """e4m3 round trip with the same per-tensor scale the kernel uses."""
+    s = x.float().abs().max().clamp_min(1e-12) / 448.0
+    return (x.float() / s).to(torch.float8_e4m3fn).float() * s, s
+
+
+def test_fp8_quantize_and_gemm():
+    """References in float64: fp32 torch matmuls on this ROCm build are not full-precision."""
+    torch.manual_seed(0)
+    M, N, K = 320, 272, 768
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, K, device="cuda").bfloat16()
+    qa, sa = C().fp8_quantize(a, False)
+    qb, sb = C().fp8_quantize(b, False)
+    ra, sra = _fp8_ref(a)
+    torch.testing.assert_close(sa[0], sra, rtol=1e-6, atol=0)
+    deq = qa.view(torch.float8_e4m3fn).float() * sa
+    torch.testing.assert_close(deq, ra, rtol=0, atol=0)  # bit-exact e4m3 encoding (OCP)
+    qt, st = C().fp8_quantize(a, True)
+    assert torch.equal(qt, qa.t().contiguous())
+    out = C().gemm_fp8(qa, qb, sa, sb, M, N, K, False)
+    # reference on the kernel's own quantised operands (x*(1/s) vs x/s may differ by one e4m3 ulp)
+    da = qa.view(torch.float8_e4m3fn).double() * sa.double()
+    db_ = qb.view(torch.float8_e4m3fn).double() * sb.double()
+    ref = da @ db_.t()
+    assert rel(out.double(), ref) < 1e-4  # only accumulation order differs
+    assert rel(out.double(), a.double() @ b.double().t()) < 8e-2
+    bias = torch.randn(N, device="cuda")
+    out2 = C().gemm_fp8(qa, qb, sa, sb, M, N, K, True, bias, 2)
+    assert rel(out2.double(), F.gelu(ref + bias.double())) < 2e-2
+    part = torch.empty(N, K, device="cuda")
+    qat, sat = C().fp8_quantize(a, True)  # [K][M]
+    g = torch.randn(M, N, device="cuda").bfloat16()
+    qgt, sgt = C().fp8_quantize(g, True)  # [N][M]
+    C().gemm_fp8_splitk_f32(qgt, qat, sgt, sat, N, K, M, 4, part)
+    dg = qgt.view(torch.float8_e4m3fn).double() * sgt.double()  # [N][M]
+    dat = qat.view(torch.float8_e4m3fn).double() * sat.double()  # [K][M]
+    assert rel(part.double(), dg @ dat.t()) < 1e-4
+
+
+def test_vit_fp8_close_to_bf16():
+    import copy
+
+    from ringdp.models import vit_tiny
+    from ringdp.ops.transformer import set_fp8
+
+    torch.manual_seed(0)
+    m = vit_tiny(num_classes=16).cuda()
+    torch.nn.init.normal_(m.heads.head.weight, std=0.05)
+    m8 = copy.deepcopy(m)
+    x = torch.randn(16, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 16, (16,), device="cuda")
+    out = m(x)
+    F.cross_entropy(out, y).backward()
+    set_fp8(True)
+    try:
+        out8 = m8(x)
+        F.cross_entropy(out8, y).backward()
+    finally:
+        set_fp8(False)
+    assert _cos(out.detach(), out8.detach()) > 0.98
+    for (n, p), (_, q) in zip(m.named_parameters(), m8.named_parameters()):
+        assert _cos(p.grad, q.grad) > 0.9, n

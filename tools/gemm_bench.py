@@ -34,6 +34,14 @@ def dense(M, N, K, a_row=False, b_row=False):
             "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
 
 
+def dense_fp8(M, N, K):
+    A = torch.randn(M, K, device="cuda").to(torch.float8_e4m3fn).view(torch.uint8)
+    B = torch.randn(N, K, device="cuda").to(torch.float8_e4m3fn).view(torch.uint8)
+    one = torch.ones(1, device="cuda")
+    us = timeit(lambda: C.gemm_fp8(A, B, one, one, M, N, K, True))
+    return {"shape": f"fp8 dense {M}x{N}x{K}", "us": round(us, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+
+
 def conv(n, h, c, k, r, stride):
     pad = r // 2
     x = torch.randn(n, h, h, c, device="cuda").bfloat16()
@@ -56,6 +64,12 @@ if __name__ == "__main__":
     out = []
     for args in [(4096, 4096, 4096), (4096, 4096, 4096, True, False), (4096, 4096, 4096, False, True),
                  (4096, 4096, 4096, True, True), (8192, 768, 3072)]:
+        out.append(dense(*args))
+        print(json.dumps(out[-1]), flush=True)
+    for args in [(4096, 4096, 4096), (8192, 8192, 8192), (25216, 3072, 768), (25216, 768, 3072)]:
+        out.append(dense_fp8(*args))
+        print(json.dumps(out[-1]), flush=True)
+    for args in [(8192, 8192, 8192), (25216, 3072, 768), (25216, 768, 3072), (25216, 2304, 768)]:
         out.append(dense(*args))
         print(json.dumps(out[-1]), flush=True)
     for args in [(256, 56, 64, 64, 1, 1), (256, 56, 64, 64, 3, 1), (256, 56, 64, 256, 1, 1), (256, 56, 256, 64, 1, 1),
