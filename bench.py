@@ -32,6 +32,9 @@ METRIC = "images/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; DDP scaling e
 # Extra BASELINE.json configs (--model): the deeper families, synthetic data of the named shape.
 MODELS = {
     "convnet": dict(batch=4096, shape=(1, 28, 28), lr=1e-4, momentum=0.0, nesterov=False, wd=0.0,
+                    # 455 KB of fp32 grads in two buckets: [fc1 + conv3] is all-reduced while conv2/conv1
+                    # backward still run; only the small [conv2 + conv1] bucket is exposed at the end.
+                    bucket_mb=0.3, first_bucket_mb=0.3,
                     desc="MNIST ConvNet (ref/launch_dist.py; 113,674 params)"),
     "resnet18": dict(batch=256, shape=(3, 32, 32), lr=0.02, momentum=0.9, nesterov=True, wd=1e-4,
                      desc="ResNet-18 CIFAR-shape (ref/example_mp.py; torchvision tree, 11,181,642 params)"),
@@ -52,7 +55,7 @@ def parse():
     ap.add_argument("--batch-per-rank", type=int, default=None,
                     help="per-rank batch (default: 4096 for the ConvNet, RINGDP_BENCH_BATCH overrides)")
     ap.add_argument("--lr", type=float, default=None)
-    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--bucket-mb", type=float, default=None, help="bucket cap (default: per model, else 25)")
     ap.add_argument("--first-bucket-mb", type=float, default=None)
     ap.add_argument("--comm-hook", type=str, default="allreduce", choices=["allreduce", "bf16_compress", "fp16_compress"])
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph per step")
@@ -88,6 +91,10 @@ def main():
     spec = MODELS[args.model]
     B = args.batch_per_rank or int(os.environ.get("RINGDP_BENCH_BATCH", spec["batch"]))
     lr = args.lr if args.lr is not None else spec["lr"]
+    if args.bucket_mb is None:
+        args.bucket_mb = spec.get("bucket_mb", 25.0)
+    if args.first_bucket_mb is None:
+        args.first_bucket_mb = spec.get("first_bucket_mb")
 
     if args.dtype == "fp8":
         if args.model != "vit_b_16":
@@ -138,7 +145,14 @@ def main():
             step_on(x, y)
         static_x.copy_(pool[0][0])
         static_y.copy_(pool[0][1])
-        graph = StepGraph(static_step, warmup=2).capture()
+        try:
+            graph = StepGraph(static_step, warmup=2).capture()
+        except Exception as e:  # fall back to eager steps rather than report nothing
+            print(f"[bench] rank {rank}: hipGraph capture failed ({type(e).__name__}: {e}); running eager",
+                  file=sys.stderr, flush=True)
+            torch.cuda.synchronize()
+            use_graph, graph = False, None
+    if use_graph:
         for i in range(n_warm):
             x, y = pool[i % len(pool)]
             static_x.copy_(x, non_blocking=True)
@@ -170,6 +184,7 @@ def main():
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max = float(t.item())
+    n_buckets = len(ddp.reducer.bucket_indices())
     final_loss = float(loss.item()) if loss is not None else float("nan")
     ms_per_step = 1000.0 * elapsed_max / args.steps
     value = world * B * args.steps / elapsed_max
@@ -200,7 +215,7 @@ def main():
                 "image_shape": list(spec["shape"]),
                 "parallelism": f"dp{world}",
                 "optimizer": f"SGD lr={lr} momentum={spec['momentum']} nesterov={spec['nesterov']} wd={spec['wd']}",
-                "comm": f"RCCL all-reduce ({args.comm_hook}), buckets cap {args.bucket_mb} MB",
+                "comm": f"RCCL all-reduce ({args.comm_hook}), {n_buckets} bucket(s), cap {args.bucket_mb} MB",
                 "hipgraph": use_graph,
                 "master_weights": "fp32",
             },

@@ -121,7 +121,7 @@ RcclPG::RcclPG(std::shared_ptr<Store> store, int rank, int size, int device,
     : ProcessGroup(rank, size),
       device_(device),
       timeout_(timeout),
-      comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(true, device)) {
+      comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(env_flag("RINGDP_COMM_HIGH_PRIORITY", false), device)) {
   DeviceScope ds(device_);
   ncclUniqueId uid;
   if (rank == 0) {
@@ -141,7 +141,7 @@ RcclPG::RcclPG(ncclComm_t comm, int rank, int size, int device, std::chrono::mil
       comm_(comm),
       device_(device),
       timeout_(timeout),
-      comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(true, device)) {
+      comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(env_flag("RINGDP_COMM_HIGH_PRIORITY", false), device)) {
   init_common();
 }
 

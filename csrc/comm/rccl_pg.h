@@ -1,4 +1,4 @@
-// RCCL process group: GPU collectives over xGMI, issued on a high-priority side HIP stream.
+// RCCL process group: GPU collectives over xGMI, issued on a side HIP stream.
 //
 // Parity target: c10d ProcessGroupNCCL (c10d/ProcessGroupNCCL.hpp:318; SURVEY.md §2.3 U4,
 // §2.4): comm-per-PG created eagerly from a store-exchanged unique id, dedicated comm stream
@@ -101,6 +101,9 @@ class RcclPG : public ProcessGroup {
   ncclComm_t comm_ = nullptr;
   int device_;
   std::chrono::milliseconds timeout_;
+  // Normal priority by default: on gfx950 an eager step with its collectives on a high-priority
+  // stream measured 1.26 ms vs 0.55 ms (ConvNet B=4096, one rank, forced comm); graph replay is
+  // unaffected.  RINGDP_COMM_HIGH_PRIORITY=1 restores the high-priority stream.
   HipStream comm_stream_;
   hipEvent_t ready_ = nullptr;
   bool timing_ = false;

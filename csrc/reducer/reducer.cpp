@@ -9,6 +9,7 @@
 #include <torch/csrc/autograd/variable.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <unordered_map>
 
 #include "../ops/ops.h"
@@ -308,6 +309,15 @@ void Reducer::launch_ready_buckets() {
   }
 }
 
+namespace {
+// RINGDP_DDP_FORCE_COMM=1: issue the bucket collectives even on a one-rank group, so a single-GPU
+// run exercises the whole communication path (side stream, events, RCCL inside a hipGraph).
+bool force_comm() {
+  const char* e = std::getenv("RINGDP_DDP_FORCE_COMM");  // read per bucket: tests toggle it
+  return e != nullptr && e[0] != '\0' && e[0] != '0';
+}
+}  // namespace
+
 void Reducer::launch_bucket(Bucket& b, int64_t index) {
   b.launched = true;
   if (trace::enabled()) {
@@ -315,7 +325,7 @@ void Reducer::launch_bucket(Bucket& b, int64_t index) {
     trace::mark(tag.c_str());
   }
   b.st.last_launch_us = static_cast<double>(now_us() - backward_start_us_);
-  if (pg_->size() == 1 || hook_ == CommHook::NONE) {
+  if ((pg_->size() == 1 && !force_comm()) || hook_ == CommHook::NONE) {
     b.work.reset();
     return;
   }

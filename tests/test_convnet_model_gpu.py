@@ -142,3 +142,67 @@ def test_hipgraph_step_matches_eager(world1):
     torch.cuda.synchronize()
     for pa, pb in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("hook", ["allreduce", "bf16"])
+def test_forced_comm_eager_and_graph(world1, monkeypatch, hook):
+    """RINGDP_DDP_FORCE_COMM=1 runs the bucket all-reduces on the one-rank RCCL group: the side
+    stream, the event fork/join and RCCL inside hipGraph capture are exercised on one GPU, and the
+    result must match the no-communication run (AVG over one rank is the identity)."""
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+    from ringdp.optim import SGD
+    from ringdp.parallel import DistributedDataParallel as DDP
+    from ringdp.utils.graph import StepGraph
+
+    crit = CrossEntropyLoss()
+    data = [(torch.randint(0, 256, (64, 1, 28, 28), dtype=torch.uint8, device="cuda"),
+             torch.randint(0, 10, (64,), device="cuda")) for _ in range(7)]
+
+    def make(force):
+        monkeypatch.setenv("RINGDP_DDP_FORCE_COMM", "1" if force else "0")
+        torch.manual_seed(3)
+        m = ConvNet().cuda()
+        # small buckets: several collectives per step, launched while backward is still running
+        d = DDP(m, device_ids=[0], bucket_cap_mb=0.05, first_bucket_mb=0.05)
+        if hook != "allreduce":
+            d._set_builtin_hook(hook)
+        return m, d, SGD(d.parameters(), lr=0.05, momentum=0.9)
+
+    m0, d0, o0 = make(False)
+    for x, y in data:
+        loss = crit(d0(x), y)
+        o0.zero_grad(set_to_none=True)
+        loss.backward()
+        o0.step()
+
+    m1, d1, o1 = make(True)
+    assert len(d1.reducer.flat_buffers()) >= 1
+    sx = torch.empty_like(data[0][0])
+    sy = torch.empty_like(data[0][1])
+
+    def step():
+        loss = crit(d1(sx), sy)
+        o1.zero_grad(set_to_none=True)
+        loss.backward()
+        o1.step()
+        return loss
+
+    for x, y in data[:3]:  # eager, with comm (bucket rebuild after iteration 0)
+        sx.copy_(x)
+        sy.copy_(y)
+        step()
+    g = StepGraph(step, warmup=0).capture()
+    for x, y in data[3:]:
+        sx.copy_(x)
+        sy.copy_(y)
+        g.replay()
+    torch.cuda.synchronize()
+    stats = d1._get_ddp_logging_data()
+    assert stats["iteration"] >= 3
+    for pa, pb in zip(m0.parameters(), m1.parameters()):
+        if hook == "allreduce":
+            torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
+        else:  # gradients went over the wire in bf16
+            assert torch.isfinite(pb).all()
+            torch.testing.assert_close(pa, pb, rtol=2e-2, atol=2e-3)
