@@ -4,6 +4,7 @@
 #include <pybind11/functional.h>
 #include <pybind11/stl.h>
 
+#include "comm/fake_pg.h"
 #include "comm/host_ring.h"
 #include "comm/rccl_pg.h"
 #include "ops/nn_ops.h"
@@ -252,6 +253,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("split", &ProcessGroup::split, py::call_guard<py::gil_scoped_release>())
       .def("shutdown", &ProcessGroup::shutdown, py::call_guard<py::gil_scoped_release>())
       .def("abort", &ProcessGroup::abort, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<FakePG, ProcessGroup, std::shared_ptr<FakePG>>(m, "FakePG")
+      .def(py::init<int, int>(), py::arg("rank"), py::arg("size"));
 
   py::class_<HostRingPG, ProcessGroup, std::shared_ptr<HostRingPG>>(m, "HostRingPG")
       .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int64_t timeout_ms,

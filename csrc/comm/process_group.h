@@ -68,6 +68,7 @@ class Work {
   std::vector<at::Tensor> outputs_;
   friend class HostRingPG;
   friend class RcclPG;
+  friend class FakePG;
 };
 
 // A Work completed on a host thread (promise-style).

@@ -56,6 +56,7 @@ class Backend:
     RCCL = "rccl"
     GLOO = "gloo"
     HOST = "host"
+    FAKE = "fake"  # collectives are no-ops (upstream fake_pg.py): single-process tests as rank r of N
 
     @staticmethod
     def normalize(backend: Optional[str]) -> Dict[str, str]:
@@ -73,7 +74,9 @@ class Backend:
             return {"cuda": "rccl"}
         if b in _CPU_BACKENDS:
             return {"cpu": "host", "cuda": "host"}
-        raise ValueError(f"ringdp: unknown backend {backend!r} (use 'nccl', 'rccl', 'gloo', 'host')")
+        if b == "fake":
+            return {"cpu": "fake", "cuda": "fake"}
+        raise ValueError(f"ringdp: unknown backend {backend!r} (use 'nccl', 'rccl', 'gloo', 'host', 'fake')")
 
 
 def _to_reduce_op(op) -> "C.ReduceOp":
@@ -112,6 +115,7 @@ class ProcessGroup:
         self.group_name = name
         self._bind_hint = bind_hint
         self._host = None
+        self._fake = None
         self._rccl: Dict[int, Any] = {}
         self._lock = threading.Lock()
         self._coll_count = 0
@@ -142,6 +146,8 @@ class ProcessGroup:
 
     # -- native communicators
     def host(self):
+        if self._backends.get("cpu") == "fake":
+            return self.native_for(torch.empty(0))[0]
         with self._lock:
             if self._host is None:
                 sub = C.PrefixStore(f"{self.group_name}/host", self._store)
@@ -167,6 +173,11 @@ class ProcessGroup:
             raise RuntimeError(
                 f"ringdp: process group {self.group_name} has no backend for {dev} tensors "
                 f"(backends={self._backends}); e.g. rccl/nccl only reduces GPU tensors")
+        if kind == "fake":
+            with self._lock:
+                if self._fake is None:
+                    self._fake = C.FakePG(self._rank, self._size)
+            return self._fake, False
         if kind == "rccl":
             return self.rccl(tensor.device.index if tensor.device.index is not None else torch.cuda.current_device()), False
         return self.host(), tensor.is_cuda
@@ -179,6 +190,7 @@ class ProcessGroup:
 
     def shutdown(self):
         with self._lock:
+            self._fake = None
             for pg in self._rccl.values():
                 pg.shutdown()
             self._rccl.clear()
@@ -303,6 +315,11 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     backends = Backend.normalize(backend)
     if timeout is None:
         timeout = default_pg_nccl_timeout if set(backends.values()) == {"rccl"} else default_pg_timeout
+    if set(backends.values()) == {"fake"} and store is None and init_method is None:
+        # upstream: init_process_group("fake") short-circuits the rendezvous
+        if rank < 0 or world_size <= 0:
+            raise ValueError("ringdp: the fake backend needs explicit rank and world_size")
+        store = C.HashStore()
     if store is not None:
         if init_method is not None:
             raise ValueError("ringdp: cannot specify both init_method and store")
@@ -388,6 +405,8 @@ def get_backend(group: Optional[ProcessGroup] = None) -> str:
         return "nccl"
     if kinds == {"host"}:
         return "gloo"
+    if kinds == {"fake"}:
+        return "fake"
     return "cpu:gloo,cuda:nccl"
 
 
@@ -814,6 +833,8 @@ def get_default_store():
 def native_group(group=None, device: Optional[int] = None):
     """The native communicator that serves ``group`` on ``device`` (GPU) or the host."""
     g = _resolve(group)
+    if "fake" in g._backends.values():
+        return g.host()
     if device is None:
         return g.host()
     return g.rccl(device)

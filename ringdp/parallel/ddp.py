@@ -11,7 +11,7 @@ API parity target: ``torch.nn.parallel.DistributedDataParallel`` as used by the 
 * every forward with ``broadcast_buffers`` re-broadcasts rank 0's buffers (C4);
 * gradients are all-reduced bucket by bucket, in bucket order, overlapped with backward (C6);
 * ``no_sync()``, ``register_comm_hook`` (allreduce / bf16 / fp16 compression / Python hooks),
-  ``find_unused_parameters``, ``_get_ddp_logging_data()``.
+  ``find_unused_parameters``, ``join()`` for uneven inputs, ``_get_ddp_logging_data()``.
 
 MI355X-first differences (documented, behaviour-preserving):
 * gradients live permanently in the flat bucket buffer (grad-as-bucket-view) and ringdp kernels
@@ -153,6 +153,7 @@ class DistributedDataParallel(nn.Module):
         self._python_hook = None
         self._install_layout()
         self._iteration = 0
+        self._join_cfg: Optional[Dict[str, Any]] = None
         self._stats = {"forward_ms": 0.0, "iterations": 0}
 
     # ------------------------------------------------------------------ construction helpers
@@ -187,11 +188,13 @@ class DistributedDataParallel(nn.Module):
         if not torch.equal(mine, theirs):
             raise RuntimeError("DDP: parameter shapes/dtypes differ from rank 0's (model mismatch across ranks)")
 
-    def _broadcast_coalesced(self, tensors: List[torch.Tensor]):
-        """Flatten per dtype into <=250 MiB buffers, broadcast from the group's first rank."""
+    def _broadcast_coalesced(self, tensors: List[torch.Tensor], src: Optional[int] = None):
+        """Flatten per dtype into <=250 MiB buffers, broadcast from ``src`` (a global rank; default:
+        the group's first rank)."""
         g = self.process_group
         if g.size() == 1 or not tensors:
             return
+        src = g.ranks[0] if src is None else src
         by_dtype: Dict[torch.dtype, List[torch.Tensor]] = {}
         for t in tensors:
             by_dtype.setdefault(t.dtype, []).append(t)
@@ -205,7 +208,7 @@ class DistributedDataParallel(nn.Module):
                     continue
                 if chunk:
                     flat = torch.cat([c.detach().reshape(-1) for c in chunk])
-                    dist.broadcast(flat, src=g.ranks[0], group=g)
+                    dist.broadcast(flat, src=src, group=g)
                     off = 0
                     with torch.no_grad():
                         for c in chunk:
@@ -270,7 +273,7 @@ class DistributedDataParallel(nn.Module):
             n = torch.tensor([len(payload)], dtype=torch.long, device=self.device)
             dist.broadcast(n, src=g.ranks[0], group=g)
             buf = torch.zeros(int(n.item()), dtype=torch.long, device=self.device)
-            if g.rank() == 0:
+            if len(payload) == buf.numel():  # the root's copy is what counts; others get overwritten
                 buf.copy_(torch.tensor(payload, dtype=torch.long))
             dist.broadcast(buf, src=g.ranks[0], group=g)
             vals = buf.tolist()
@@ -303,6 +306,8 @@ class DistributedDataParallel(nn.Module):
         with torch.autograd.profiler.record_function("DistributedDataParallel.forward"), \
                 _tracing.range("ringdp.DDP.forward"):
             grad = torch.is_grad_enabled() and self.require_backward_grad_sync
+            if self._join_cfg is not None:
+                self._join_notify(grad)
             if grad:
                 self._maybe_rebuild_buckets()
                 self.reducer.prepare_for_forward()
@@ -327,6 +332,78 @@ class DistributedDataParallel(nn.Module):
             yield
         finally:
             self.require_backward_grad_sync = old
+
+    @contextmanager
+    def join(self, divide_by_initial_world_size: bool = True, enable: bool = True,
+             throw_on_early_termination: bool = False):
+        """Train with uneven inputs across ranks (U7 ``join`` ``torch/nn/parallel/distributed.py:1765``).
+
+        While inside the context every forward first all-reduces ``[1, grad_sync]`` so ranks can
+        tell how many peers are still training.  A rank whose input is exhausted leaves the
+        ``with`` body and *shadows* the others: per remaining iteration it joins that count
+        all-reduce, the bucket rebuild and buffer broadcast, and all-reduces zero-filled buckets of
+        the same sizes/dtypes in bucket order, so every rank issues an identical collective
+        sequence.  Gradients are therefore averaged over the initial world size.  When no rank is
+        active any more, the parameters and buffers of the last rank to join (the one that ran the
+        most iterations) are broadcast to everyone.
+        """
+        g = self.process_group
+        if not enable or g.size() == 1:
+            yield
+            return
+        if not divide_by_initial_world_size:
+            raise NotImplementedError("ringdp DDP.join: only divide_by_initial_world_size=True is supported")
+        if self._comm_hook_name not in ("allreduce", "bf16_compress", "fp16_compress"):
+            raise NotImplementedError("ringdp DDP.join: custom Python comm hooks cannot be shadowed")
+        self._join_cfg = {"throw": throw_on_early_termination}
+        try:
+            yield
+            self._join_shadow()
+        finally:
+            self._join_cfg = None
+
+    def _join_device(self) -> torch.device:
+        return self.device if self.device is not None else torch.device("cpu")
+
+    def _join_notify(self, grad_sync: bool):
+        g = self.process_group
+        flag = torch.tensor([1.0, 1.0 if grad_sync else 0.0], dtype=torch.float32, device=self._join_device())
+        dist.all_reduce(flag, group=g)
+        if self._join_cfg["throw"] and int(flag[0].item()) < g.size():
+            raise RuntimeError(f"ringdp DDP.join: rank {g.rank()} detected that another rank exhausted its "
+                               "inputs (throw_on_early_termination=True)")
+
+    def _join_shadow(self):
+        g = self.process_group
+        dev = self._join_device()
+        joined_at = self._iteration
+        wire = {"bf16_compress": torch.bfloat16, "fp16_compress": torch.float16}.get(self._comm_hook_name)
+        while True:
+            flag = torch.zeros(2, dtype=torch.float32, device=dev)
+            dist.all_reduce(flag, group=g)
+            n_active, n_sync = int(flag[0].item()), int(flag[1].item())
+            if n_active == 0:
+                break
+            if self._join_cfg["throw"]:
+                raise RuntimeError(f"ringdp DDP.join: rank {g.rank()} exhausted its inputs "
+                                   "(throw_on_early_termination=True)")
+            if n_sync:
+                self._maybe_rebuild_buckets()
+            if self.broadcast_buffers and self.require_forward_param_sync:
+                self._sync_buffers()
+            if n_sync:
+                idx = self.reducer.bucket_indices()
+                for b, numel in enumerate(self.reducer.bucket_numels()):
+                    dt = wire or self._params[idx[b][0]].dtype
+                    z = torch.zeros(numel, dtype=dt, device=dev)
+                    # the reducer's collectives go straight to the native PG; mirror that exactly
+                    self._native_pg.allreduce([z], C.ReduceOp.AVG).wait(True)
+        # last joiner = most iterations (ties: highest rank); its model becomes everyone's
+        key = torch.tensor([float(joined_at * g.size() + g.rank())], dtype=torch.float64, device=dev)
+        dist.all_reduce(key, op=dist.ReduceOp.MAX, group=g)
+        src = g.ranks[int(key.item()) % g.size()]
+        with torch.no_grad():
+            self._broadcast_coalesced([p.data for p in self._params] + list(self._buffers_list), src=src)
 
     def register_comm_hook(self, state: Any, hook: Callable):
         """Builtin hooks (allreduce / bf16_compress / fp16_compress from

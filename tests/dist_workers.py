@@ -317,3 +317,58 @@ def checkpoint_resume_worker(rank, world, init_file, out_dir):
     for a, b in zip(ref, m2.parameters()):
         assert torch.equal(a, b.detach()), (a - b).abs().max()
     dist.destroy_process_group()
+
+
+JOIN_BATCHES = (5, 3, 4, 2)
+
+
+def join_worker(rank, world, port, result_dir, hook):
+    """Uneven inputs under DDP.join(): rank r trains on JOIN_BATCHES[r] batches."""
+    dist = _init(rank, world, port)
+    from ringdp.models import ConvNet
+    from ringdp.optim import SGD
+    from ringdp.parallel import DistributedDataParallel as DDP
+    from ringdp.parallel import comm_hooks
+
+    B = 4
+    torch.manual_seed(5)
+    model = ConvNet()
+    ddp = DDP(model, bucket_cap_mb=0.1, first_bucket_mb=0.05)
+    if hook == "bf16":
+        ddp.register_comm_hook(None, comm_hooks.bf16_compress_hook)
+    opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9)
+    steps = max(JOIN_BATCHES[:world])
+    xs, ys = _convnet_batches(world, B, steps)
+    with ddp.join():
+        for i in range(JOIN_BATCHES[rank]):
+            x = xs[i][rank * B:(rank + 1) * B]
+            y = ys[i][rank * B:(rank + 1) * B]
+            loss = torch.nn.functional.cross_entropy(ddp(x), y)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    allp = [torch.zeros_like(flat) for _ in range(world)]
+    dist.all_gather(allp, flat)
+    same = all(torch.equal(allp[0], a) for a in allp)
+    torch.save({"flat": flat, "same": same}, os.path.join(result_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def join_throw_worker(rank, world, port, result_dir):
+    dist = _init(rank, world, port)
+    from ringdp.models import ConvNet
+    from ringdp.parallel import DistributedDataParallel as DDP
+
+    torch.manual_seed(5)
+    ddp = DDP(ConvNet())
+    xs, ys = _convnet_batches(world, 2, 3)
+    raised = False
+    try:
+        with ddp.join(throw_on_early_termination=True):
+            for i in range(1 if rank == 0 else 3):
+                torch.nn.functional.cross_entropy(ddp(xs[i][:2]), ys[i][:2]).backward()
+    except RuntimeError as e:
+        raised = "throw_on_early_termination" in str(e)
+    torch.save({"raised": raised}, os.path.join(result_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()

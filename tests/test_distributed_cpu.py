@@ -57,6 +57,46 @@ def test_ddp_equivalence(tmp_path, world, momentum, hook, bucket_mb, first_mb):
         assert len(res[0]["buckets"]) > 1
 
 
+def _reference_join(world, hook):
+    """One process: iteration i averages the gradients of the ranks that still have data over the
+    initial world size (the semantics of DDP.join(divide_by_initial_world_size=True))."""
+    from ringdp.models import ConvNet
+    from ringdp.optim import SGD
+
+    B = 4
+    torch.manual_seed(5)
+    model = ConvNet()
+    opt = SGD(model.parameters(), lr=0.01, momentum=0.9)
+    n = W.JOIN_BATCHES[:world]
+    xs, ys = W._convnet_batches(world, B, max(n))
+    for i in range(max(n)):
+        loss = 0
+        for r in range(world):
+            if i < n[r]:
+                loss = loss + torch.nn.functional.cross_entropy(model(xs[i][r * B:(r + 1) * B]),
+                                                                ys[i][r * B:(r + 1) * B]) / world
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+
+
+@pytest.mark.parametrize("world,hook", [(2, "allreduce"), (3, "allreduce"), (2, "bf16")])
+def test_join_uneven_inputs(tmp_path, world, hook):
+    spawn(W.join_worker, args=(world, free_port(), str(tmp_path), hook), nprocs=world)
+    res = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
+    assert all(r["same"] for r in res), "final model sync from the last joiner failed"
+    ref = _reference_join(world, hook)
+    err = float((res[0]["flat"] - ref).abs().max())
+    assert err < (2e-2 if hook == "bf16" else 1e-4), err
+
+
+def test_join_throw_on_early_termination(tmp_path):
+    spawn(W.join_throw_worker, args=(2, free_port(), str(tmp_path)), nprocs=2)
+    res = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(2)]
+    assert all(r["raised"] for r in res)
+
+
 def test_no_sync_accumulates(tmp_path):
     spawn(W.no_sync_worker, args=(2, free_port(), str(tmp_path)), nprocs=2)
     r0, r1 = (torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(2))
