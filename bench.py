@@ -31,7 +31,7 @@ METRIC = "images/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; DDP scaling e
 
 # Extra BASELINE.json configs (--model): the deeper families, synthetic data of the named shape.
 MODELS = {
-    "convnet": dict(batch=4096, shape=(1, 28, 28), lr=1e-4, momentum=0.0, nesterov=False, wd=0.0,
+    "convnet": dict(batch=16384, shape=(1, 28, 28), lr=1e-4, momentum=0.0, nesterov=False, wd=0.0,
                     # 455 KB of fp32 grads in two buckets: [fc1 + conv3] is all-reduced while conv2/conv1
                     # backward still run; only the small [conv2 + conv1] bucket is exposed at the end.
                     bucket_mb=0.3, first_bucket_mb=0.3,
@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", type=str, default="convnet", choices=sorted(MODELS))
     ap.add_argument("--batch-per-rank", type=int, default=None,
-                    help="per-rank batch (default: 4096 for the ConvNet, RINGDP_BENCH_BATCH overrides)")
+                    help="per-rank batch (default: 16384 for the ConvNet, RINGDP_BENCH_BATCH overrides)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--bucket-mb", type=float, default=None, help="bucket cap (default: per model, else 25)")
     ap.add_argument("--first-bucket-mb", type=float, default=None)

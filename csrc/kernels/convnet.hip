@@ -7,10 +7,11 @@
 //
 // Kernel blocks (one autograd Function each, see ringdp/ops/convnet.py):
 //   F1  conv1 + ReLU + pool1                       -> a1 [B,13,13,32] bf16 + argmax|relu byte
-//   F2  conv2 (+ bias, no ReLU)                    -> z2 [B,11,11,64] bf16
-//   F3  ReLU + pool2 + conv3 + ReLU + pool3 + fc1  -> logits [B,10] fp32 (+ a3, argmax)
-// conv2's ReLU and the overlapping k2/s1 pool live at the START of F3: their masks/argmax are
-// recomputed from z2 in F3's backward, which hands conv2 a plain linear-layer gradient dz2.
+//   F2  conv2 + ReLU + pool2 (2x2/s1)              -> a2 [B,10,10,64] bf16 + pool2 code byte
+//   F3  conv3 + ReLU + pool3 + fc1                 -> logits [B,10] fp32 (+ a3, argmax)
+// conv2's pre-activation z2 is never materialised: F2 keeps only what F3 and the backward need
+// (a2 = relu(pool2(z2)) and, per pooled value, the first-max position or "no gradient"), and F3's
+// backward scatters d(a2) through those codes into dz2, a plain linear-layer gradient for conv2.
 //
 // MI355X-first design:
 //   * weight-stationary: weights are packed once per forward (cn_pack_weights) into bf16 MFMA
@@ -88,25 +89,34 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
   out[e] = (bf16)v;
 }
 
-__device__ __forceinline__ bf16x8 bmax8(const bf16x8& a, const bf16x8& b) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (float)a[j] >= (float)b[j] ? a[j] : b[j];
-  return r;
-}
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned char u8x8 __attribute__((ext_vector_type(8)));
 
-// max over a 2x2 window of an LDS image with row stride rs (in bf16) and width w
-__device__ __forceinline__ bf16x8 window_max8(const bf16* r0, int rs, int w) {
-  return bmax8(bmax8(*reinterpret_cast<const bf16x8*>(r0), *reinterpret_cast<const bf16x8*>(r0 + rs)),
-               bmax8(*reinterpret_cast<const bf16x8*>(r0 + w * rs),
-                     *reinterpret_cast<const bf16x8*>(r0 + (w + 1) * rs)));
-}
-
-__device__ __forceinline__ bf16x8 relu8(const bf16x8& a) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (float)a[j] > 0.f ? a[j] : (bf16)0.f;
-  return r;
+// relu(max over a 2x2 window) of 8 bf16 channels, plus the pool2 code byte per channel:
+// 0..3 = first maximum in (0,0),(0,1),(1,0),(1,1) order (torch max_pool2d semantics), bit 2 set =
+// the pooled value is 0 (no gradient flows).  Done on the raw bf16 bit patterns with packed int16
+// ops (v_pk_max_i16 & co, 2 channels per instruction): for values >= 0 the integer order is the float
+// order and any negative value is a negative int16, so max(v0..v3, 0) over int16 IS relu(max).
+__device__ __forceinline__ void pool2_code8(const bf16* r0, int rs, int w, bf16x8& out, uint2& code) {
+  const s16x8 v0 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0));
+  const s16x8 v1 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0 + rs));
+  const s16x8 v2 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0 + w * rs));
+  const s16x8 v3 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0 + (w + 1) * rs));
+  const s16x8 zero = (s16x8)0;
+  const s16x8 m = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_elementwise_max(v0, v1),
+                                                                      __builtin_elementwise_max(v2, v3)),
+                                            zero);
+  const u16x8 mu = __builtin_bit_cast(u16x8, m), one = (u16x8)1;
+  // k_i = 0 iff v_i == m (u16 difference; a negative v_i wraps to a non-zero value)
+  const u16x8 k0 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v0), one);
+  const u16x8 k1 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v1), one);
+  const u16x8 k2 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v2), one);
+  const u16x8 t1 = k0 * k1;
+  const u16x8 idx = k0 + t1 + t1 * k2;                                    // first i with v_i == m
+  const u16x8 none = (one - __builtin_elementwise_min(mu, one)) << 2;     // 4 iff m == 0
+  out = __builtin_bit_cast(bf16x8, m);
+  code = __builtin_bit_cast(uint2, __builtin_convertvector(idx | none, u8x8));
 }
 
 // First-max argmax over the 4 registers of a window + bias + ReLU (torch max_pool2d semantics:
@@ -131,13 +141,6 @@ __device__ __forceinline__ int byte_of(const uint2& v, int j) {
 __device__ __forceinline__ int win_pos(int r, int pw) {
   const int w = r >> 2, i = r & 3;
   return (2 * (w >> 2) + (i >> 1)) * pw + 2 * (w & 3) + (i & 1);
-}
-
-__device__ __forceinline__ void stage_rows(const bf16* __restrict__ src, bf16* dst, int nchunks,
-                                           int chunks_per_row, int rs, int tid, int nthreads) {
-  for (int c = tid; c < nchunks; c += nthreads)
-    *reinterpret_cast<bf16x8*>(dst + (c / chunks_per_row) * rs + (c % chunks_per_row) * 8) =
-        reinterpret_cast<const bf16x8*>(src)[c];
 }
 
 // Async global -> LDS copy of 16 B per lane (global_load_lds_dwordx4): the LDS destination is the
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
   }
 }
 
-// ================================================================== F2: conv2 (pre-activation out)
+// ================================================================== F2: conv2 + ReLU + pool2
 // 256 threads; wave (wm, wn) owns n-tiles {2wn, 2wn+1} x m-tiles {4wm..4wm+3} (121 rows -> 128).
 constexpr int C2_XRS = 40;  // bf16 per LDS row of the a1 image (32 + 8 pad)
 constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 + 8)
@@ -260,7 +263,8 @@ constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 +
 __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restrict__ a1,
                                                            const bf16* __restrict__ packed,
                                                            const float* __restrict__ bias,
-                                                           bf16* __restrict__ z2, int B) {
+                                                           bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
+                                                           int B) {
   __shared__ __attribute__((aligned(16))) bf16 X[2][169 * C2_XRS];
   __shared__ __attribute__((aligned(16))) bf16 Cs[121 * C2_CRS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -272,9 +276,14 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int ks = 0; ks < 9; ++ks) bw[t][ks] = pk[((2 * wn + t) * 9 + ks) * 64 + lane];
-  float bv[2];
+  // operands swapped (weights = A): a lane's 4 accumulators are 4 consecutive channels of one
+  // position, staged with one 8-byte LDS store
+  const int c4 = (lane >> 4) * 4;
+  f32x4 bv[2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) bv[t] = bias[(2 * wn + t) * 16 + r16];
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[t][i] = bias[(2 * wn + t) * 16 + c4 + i];
   int base[4];  // rows >= 121 read a clamped (valid) address; their outputs are dropped
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
@@ -317,50 +326,70 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(x + (base[mt] + shift) * C2_XRS + q8);
-        acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
-        acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
+        acc[mt][0] = mfma16x16x32(bw[0][ks], a, acc[mt][0]);
+        acc[mt][1] = mfma16x16x32(bw[1][ks], a, acc[mt][1]);
       }
     }
-    __syncthreads();  // previous image's copy-out of Cs is complete
+    __syncthreads();  // previous image's pooling reads of Cs are complete
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < 4; ++mt) {
+      const int m = (4 * wm + mt) * 16 + r16;
+      if (m < 121) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = (4 * wm + mt) * 16 + (lane >> 4) * 4 + i;
-          if (m < 121) Cs[m * C2_CRS + (2 * wn + t) * 16 + r16] = (bf16)(acc[mt][t][i] + bv[t]);
+        for (int t = 0; t < 2; ++t) {
+          const f32x4 v = acc[mt][t] + bv[t];
+          *reinterpret_cast<bf16x4*>(Cs + m * C2_CRS + (2 * wn + t) * 16 + c4) =
+              bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         }
+      }
+    }
     if (nb < B) store(X[cur ^ 1]);
     __syncthreads();
-    bf16x8* dst = reinterpret_cast<bf16x8*>(z2 + (int64_t)b * 121 * 64);
-    for (int c = tid; c < 968; c += 256)
-      dst[c] = *reinterpret_cast<const bf16x8*>(Cs + (c >> 3) * C2_CRS + (c & 7) * 8);
+    // relu + overlapping 2x2/s1 pool of the staged z2 tile -> a2 and the pool2 codes
+    bf16x8* da = reinterpret_cast<bf16x8*>(a2 + (int64_t)b * 6400);
+    uint2* di = reinterpret_cast<uint2*>(idx2 + (int64_t)b * 6400);
+    for (int it = tid; it < 800; it += 256) {
+      const int p = it >> 3, c = (it & 7) * 8;
+      bf16x8 v;
+      uint2 code;
+      pool2_code8(Cs + ((p / 10) * 11 + p % 10) * C2_CRS + c, C2_CRS, 11, v, code);
+      da[it] = v;
+      di[it] = code;
+    }
     cur ^= 1;
   }
 }
 
-// ================================================================== F3: ReLU + pool2 + conv3 + ReLU + pool3 + fc1
+// ================================================================== F3: conv3 + ReLU + pool3 + fc1
 // 256 threads; wave w owns output channels 32w..32w+31 (n-tiles 2w, 2w+1) for all 16 pool windows.
-constexpr int C3_RRS = 64;  // bf16 per LDS row, z2 image (unpadded: filled by glds)
-constexpr int C3_XRS = 72;  // bf16 per LDS row, pooled conv3 input (64 + 8)
+constexpr int C3_XRS = 72;  // bf16 per padded LDS row of a2 (backward wgrad role)
 
-__device__ __forceinline__ void pool2_into(const bf16* R, bf16* X, int tid, int nthreads) {
-  for (int it = tid; it < 800; it += nthreads) {
-    const int p = it >> 3, c = (it & 7) * 8;
-    const int py = p / 10, px = p % 10;
-    *reinterpret_cast<bf16x8*>(X + p * C3_XRS + c) = relu8(window_max8(R + (py * 11 + px) * C3_RRS + c, C3_RRS, 11));
+// a2 image -> LDS staging buffer R (lane-linear 16-B chunks, LDS-DMA: no VGPRs, lands while the
+// previous image computes); nthreads threads issue the 13 wave-instructions (the last half full).
+__device__ __forceinline__ void a2_glds(const bf16* __restrict__ a2, int b, bf16* R, int wave, int lane,
+                                        int nwaves) {
+  const bf16* src = a2 + (int64_t)b * 6400;
+  for (int k = wave; k < 13; k += nwaves) {
+    const int slot = k * 64 + lane;
+    if (slot < 800) glds16(src + slot * 8, R + k * 512);
   }
 }
 
-__global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __restrict__ z2,
+// staging buffer -> padded MFMA rows (C3_XRS): the padding keeps the 16 rows of a fragment read on
+// distinct banks, which a lane-linear DMA image cannot have
+__device__ __forceinline__ void a2_relayout(const bf16* R, bf16* X, int tid, int nthreads) {
+  for (int c = tid; c < 800; c += nthreads)
+    *reinterpret_cast<bf16x8*>(X + (c >> 3) * C3_XRS + (c & 7) * 8) = reinterpret_cast<const bf16x8*>(R)[c];
+}
+
+__global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __restrict__ a2,
                                                               const bf16* __restrict__ packed,
                                                               const float* __restrict__ bias,
                                                               const float* __restrict__ bfc,
                                                               float* __restrict__ logits,
                                                               bf16* __restrict__ a3,
                                                               uint8_t* __restrict__ idx3, int B) {
-  __shared__ __attribute__((aligned(16))) bf16 R[121 * C3_RRS];
+  __shared__ __attribute__((aligned(16))) bf16 R[100 * 64];
   __shared__ __attribute__((aligned(16))) bf16 X[100 * C3_XRS];
   __shared__ __attribute__((aligned(16))) bf16 Fc[PFC_N];
   __shared__ float red[4][10];
@@ -382,23 +411,14 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
     const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFC_OFF);
     for (int c = tid; c < PFC_N / 8; c += 256) reinterpret_cast<bf16x8*>(Fc)[c] = src[c];
   }
-  // z2 image -> R: 968 16-B chunks = 16 wave-instructions (4 per wave), lane-linear
-  auto stage = [&](int bb) {
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(z2 + (int64_t)bb * 121 * 64);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int inst = k * 4 + wave, c = inst * 64 + lane;
-      if (c < 968) glds16(src + c, R + inst * 64 * 8);
-    }
-  };
   int b = blockIdx.x;
-  if (b < B) stage(b);
-  __syncthreads();
+  if (b < B) a2_glds(a2, b, R, wave, lane, 4);
   for (; b < B; b += gridDim.x) {
-    pool2_into(R, X, tid, 256);
+    __syncthreads();  // R has landed; the previous image's X and red reads are done
+    a2_relayout(R, X, tid, 256);
     __syncthreads();  // X complete, R free
     const int nb = b + gridDim.x;
-    if (nb < B) stage(nb);  // lands while the MFMAs below run
+    if (nb < B) a2_glds(a2, nb, R, wave, lane, 4);  // lands while the MFMAs below run
     f32x4 acc[4][2];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
@@ -518,47 +538,38 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
 }
 
 // (2) conv3 backward, two roles in one 512-thread launch:
-//   dgrad: da2 = full-corr(d(conv3) image, flipped W3) -> pool2 + ReLU backward (argmax and mask
-//          recomputed from z2) -> dz2 [B,11,11,64];
-//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a2 = relu(pool2(z2));
+//   dgrad: da2 = full-corr(d(conv3) image, flipped W3), then pool2 + ReLU backward: each da2 value goes
+//          to the z2 position its pool2 code names (F2 forward) -> dz2 [B,11,11,64];
+//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci];
 //          db3 via one extra MFMA tile against a ones column.
 constexpr int C3_PW = 12;    // padded d(conv3) image width (8 + 2*2)
 constexpr int C3_PRS = 136;  // bf16 per padded-image row (128 + 8)
-constexpr int C3_DARS = 68;  // floats per da2 row (64 + 4)
+constexpr int C3_DARS = 68;  // floats per da2 partial-sum row (64 + 4)
 constexpr int C3_DRS = 136;  // bf16 per D3 row in LDS
 constexpr int C3D_P = C3_PW * C3_PW * C3_PRS * 2;  // 39168
-constexpr int C3D_R = 121 * C3_RRS * 2;            // 15488
-constexpr int C3D_AM = 100 * 64;                   // 6400
-constexpr int C3D_DA = 100 * C3_DARS * 4;          // 27200
-constexpr int C3D_LDS = C3D_P + C3D_R + C3D_AM + C3D_DA;
+constexpr int C3D_AM = 100 * 64;                   // 6400: pool2 codes
+constexpr int C3D_DA = 100 * C3_DARS * 4;          // 27200 (x2: partial sums of two k-group pairs)
+constexpr int C3D_LDS = C3D_P + C3D_AM + 2 * C3D_DA;
 constexpr int C3W_D = 64 * C3_DRS * 2;   // 17408
 constexpr int C3W_X = 100 * C3_XRS * 2;  // 14400
-constexpr int C3W_LDS = C3W_D + C3W_X + C3D_R;
+constexpr int C3W_R = 100 * 64 * 2;      // 12800: DMA staging of the next a2 image
+constexpr int C3W_LDS = C3W_D + C3W_X + C3W_R;
 constexpr int C3B_LDS = C3D_LDS > C3W_LDS ? C3D_LDS : C3W_LDS;
 constexpr int C3_WSLAB = 576 * 128 + 128;  // dW3t + db3
 
-// One image of F3-backward input, held in registers while the previous image is computed on.
+// The compact F3-backward input of one image, held in registers while the previous image is
+// computed on: d(a3) chunk + its pool3 argmax bytes (threads < 256).
 struct C3Pre {
-  bf16x8 da;  // compact d(a3) chunk (threads < 256)
-  uint2 id;   // its pool3 argmax bytes
-  bf16x8 z[2];
-};
-
-__device__ __forceinline__ void c3_load(C3Pre& p, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
-                                        const bf16* __restrict__ z2, int b, int tid) {
-  if (tid < 256) {
-    p.da = reinterpret_cast<const bf16x8*>(da3m + (int64_t)b * 2048)[tid];
-    p.id = reinterpret_cast<const uint2*>(idx3 + (int64_t)b * 2048)[tid];
+  bf16x8 da;
+  uint2 id;
+  __device__ __forceinline__ void load(const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3, int b,
+                                       int tid) {
+    if (tid < 256) {
+      da = reinterpret_cast<const bf16x8*>(da3m + (int64_t)b * 2048)[tid];
+      id = reinterpret_cast<const uint2*>(idx3 + (int64_t)b * 2048)[tid];
+    }
   }
-  const bf16x8* zs = reinterpret_cast<const bf16x8*>(z2 + (int64_t)b * 121 * 64);
-  p.z[0] = zs[tid];
-  if (tid + 512 < 968) p.z[1] = zs[tid + 512];
-}
-
-__device__ __forceinline__ void c3_store_R(const C3Pre& p, bf16* R, int tid) {
-  reinterpret_cast<bf16x8*>(R)[tid] = p.z[0];
-  if (tid + 512 < 968) reinterpret_cast<bf16x8*>(R)[tid + 512] = p.z[1];
-}
+};
 
 // Expand compact item tid (window w = tid >> 4, channels cc..cc+7) to the 4 window-ordered rows.
 template <typename RowPtr>
@@ -575,123 +586,127 @@ __device__ __forceinline__ void c3_expand(const C3Pre& p, int tid, RowPtr row_pt
   }
 }
 
-__device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ z2, const bf16* __restrict__ da3m,
-                                 const uint8_t* __restrict__ idx3, const bf16* __restrict__ packed,
+// dgrad GEMM per image, operands swapped so the output lands channel-contiguous:
+//   C[c = 64 input channels][m = 100 positions] = sum_k W3d[c][k] * Pimg[k][m],  K = 9 taps x 128.
+// 8 waves = 4 K-groups (9 of the 36 k-steps each) x 2 channel halves; a wave keeps the weight
+// fragments of its K-group and 2 channel tiles in VGPRs (72) for every image, covers all 7 position
+// tiles, and uses each image fragment it reads from LDS for 2 MFMAs (half the LDS reads of one
+// channel tile per wave).  K-group partials are combined in a fixed order ((g0 + g1) + (g2 + g3)):
+// deterministic.
+__device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
+                                 const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ dz2, int B, int block, int nblocks) {
   bf16* P = reinterpret_cast<bf16*>(smem);
-  bf16* R = reinterpret_cast<bf16*>(smem + C3D_P);
-  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P + C3D_R);
-  float* DA = reinterpret_cast<float*>(smem + C3D_P + C3D_R + C3D_AM);
+  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P);
+  float* DA0 = reinterpret_cast<float*>(smem + C3D_P + C3D_AM);
+  float* DA1 = DA0 + 100 * C3_DARS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nt = wave & 3, mh = wave >> 2;  // n-tile (16 input channels), m-tile parity
-  const int r16 = lane & 15, q8 = (lane >> 4) * 8;
+  const int kg = wave >> 1, nh = wave & 1;
+  const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3D_OFF);
-  bf16x8 bw[36];
+  bf16x8 aw[2][9];
 #pragma unroll
-  for (int ks = 0; ks < 36; ++ks) bw[ks] = pk[(nt * 36 + ks) * 64 + lane];
-  int base[4];  // rows >= 100 read a clamped (valid) address; their outputs are dropped
+  for (int t = 0; t < 2; ++t)
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int mm = min((mh + 2 * k) * 16 + r16, 99);
-    base[k] = (mm / 10) * C3_PW + mm % 10;
+    for (int j = 0; j < 9; ++j) aw[t][j] = pk[((2 * nh + t) * 36 + 9 * kg + j) * 64 + lane];
+  int base[7];  // positions >= 100 read a clamped (valid) address; their outputs are dropped
+#pragma unroll
+  for (int mt = 0; mt < 7; ++mt) {
+    const int mm = min(mt * 16 + r16, 99);
+    base[mt] = (mm / 10) * C3_PW + mm % 10;
   }
   // the ring of the padded image stays zero; only the 8x8 interior is rewritten per image
   for (int c = tid; c < C3D_P / 16; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
-  // m-tiles mh, mh+2, ... < 7: 4 for even waves, 3 for odd (compile-time trip counts)
-  auto mfma_phase = [&](auto nk_c) {
-    constexpr int NK = decltype(nk_c)::value;
-    f32x4 acc[NK];
+  // the K-group is a template parameter, so every fragment address is a per-lane base plus an
+  // immediate offset (no hoisted address VGPRs)
+  auto mfma_phase = [&](auto kg_c) {
+    constexpr int KG = decltype(kg_c)::value;
+    f32x4 acc[7][2];
 #pragma unroll
-    for (int k = 0; k < NK; ++k) acc[k] = zero_f32x4();
+    for (int mt = 0; mt < 7; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
 #pragma unroll
-    for (int ks = 0; ks < 36; ++ks) {
+    for (int j = 0; j < 9; ++j) {
+      const int ks = 9 * KG + j;
       const int tapp = ks >> 2, c0 = (ks & 3) * 32;
       const int shift = (tapp / 3) * C3_PW + tapp % 3;
 #pragma unroll
-      for (int k = 0; k < NK; ++k)
-        acc[k] = mfma16x16x32(*reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C3_PRS + c0 + q8), bw[ks],
-                              acc[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < NK; ++k) {
-      const int mt = mh + 2 * k;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = mt * 16 + (lane >> 4) * 4 + i;
-        if (m < 100) DA[m * C3_DARS + nt * 16 + r16] = acc[k][i];
+      for (int mt = 0; mt < 7; ++mt) {
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(P + (base[mt] + shift) * C3_PRS + c0 + q8);
+        acc[mt][0] = mfma16x16x32(aw[0][j], bfr, acc[mt][0]);
+        acc[mt][1] = mfma16x16x32(aw[1][j], bfr, acc[mt][1]);
       }
+    }
+    // round 1: groups 1 and 3 publish; round 2: groups 0 and 2 fold theirs in
+    auto publish = [&](float* D, bool add) {
+#pragma unroll
+      for (int mt = 0; mt < 7; ++mt) {
+        const int m = mt * 16 + r16;
+        if (m < 100) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            f32x4* d = reinterpret_cast<f32x4*>(D + m * C3_DARS + (2 * nh + t) * 16 + c4);
+            *d = add ? *d + acc[mt][t] : acc[mt][t];
+          }
+        }
+      }
+    };
+    if (KG & 1) publish(KG == 1 ? DA0 : DA1, false);
+    __syncthreads();
+    if (!(KG & 1)) publish(KG == 0 ? DA0 : DA1, true);
+  };
+  auto run_phase = [&]() {
+    switch (kg) {
+      case 0: mfma_phase(std::integral_constant<int, 0>{}); break;
+      case 1: mfma_phase(std::integral_constant<int, 1>{}); break;
+      case 2: mfma_phase(std::integral_constant<int, 2>{}); break;
+      default: mfma_phase(std::integral_constant<int, 3>{}); break;
     }
   };
   C3Pre pre;
+  uint4 code = make_uint4(0, 0, 0, 0);
   int b = block;
-  if (b < B) c3_load(pre, da3m, idx3, z2, b, tid);
+  if (b < B) {
+    pre.load(da3m, idx3, b, tid);
+    if (tid < 400) code = reinterpret_cast<const uint4*>(idx2 + (int64_t)b * 6400)[tid];
+  }
   for (; b < B; b += nblocks) {
-    __syncthreads();  // previous image fully consumed
+    __syncthreads();  // previous image fully consumed (P, AM, DA)
     c3_expand(pre, tid, [&](int r) { return P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS; });
-    c3_store_R(pre, R, tid);
+    if (tid < 400) reinterpret_cast<uint4*>(AM)[tid] = code;
     const int nb = b + nblocks;
-    if (nb < B) c3_load(pre, da3m, idx3, z2, nb, tid);  // lands during the MFMA phase
-    __syncthreads();
-    // pool2 argmax per window (first max of relu(z2): ties at 0 pick the first, like torch)
-    for (int it = tid; it < 800; it += 512) {
-      const int p = it >> 3, c = (it & 7) * 8;
-      const int py = p / 10, px = p % 10;
-      const bf16* r0 = R + (py * 11 + px) * C3_RRS + c;
-      const bf16x8 v0 = relu8(*reinterpret_cast<const bf16x8*>(r0));
-      const bf16x8 v1 = relu8(*reinterpret_cast<const bf16x8*>(r0 + C3_RRS));
-      const bf16x8 v2 = relu8(*reinterpret_cast<const bf16x8*>(r0 + 11 * C3_RRS));
-      const bf16x8 v3 = relu8(*reinterpret_cast<const bf16x8*>(r0 + 12 * C3_RRS));
-      uint32_t lo = 0, hi = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float bm = (float)v0[j];
-        uint32_t g = 0;
-        if ((float)v1[j] > bm) {
-          bm = (float)v1[j];
-          g = 1;
-        }
-        if ((float)v2[j] > bm) {
-          bm = (float)v2[j];
-          g = 2;
-        }
-        if ((float)v3[j] > bm) g = 3;
-        if (j < 4)
-          lo |= g << (8 * j);
-        else
-          hi |= g << (8 * (j - 4));
-      }
-      *reinterpret_cast<uint2*>(AM + p * 64 + c) = make_uint2(lo, hi);
+    if (nb < B) {  // lands during the MFMA phase
+      pre.load(da3m, idx3, nb, tid);
+      if (tid < 400) code = reinterpret_cast<const uint4*>(idx2 + (int64_t)nb * 6400)[tid];
     }
-    if (mh == 0)
-      mfma_phase(std::integral_constant<int, 4>{});
-    else
-      mfma_phase(std::integral_constant<int, 3>{});
     __syncthreads();
-    // pool2 backward (gather over the <= 4 windows covering (y, x)) + ReLU mask (z2 > 0)
-    bf16x8* dst = reinterpret_cast<bf16x8*>(dz2 + (int64_t)b * 121 * 64);
-    for (int it = tid; it < 968; it += 512) {
-      const int pos = it >> 3, c = (it & 7) * 8;
+    run_phase();
+    __syncthreads();
+    // pool2 + ReLU backward as a gather: item (position, 4-channel quad) sums da2 = DA0 + DA1 of the
+    // (<= 4) windows covering it, in a fixed window order, where the window's code names this
+    // position (a code with bit 2 set - no gradient - never matches).  16 consecutive lanes share a
+    // position: every LDS read is a contiguous 256 B (conflict-free) and every store is coalesced.
+    bf16x4* dst = reinterpret_cast<bf16x4*>(dz2 + (int64_t)b * 121 * 64);
+    for (int it = tid; it < 121 * 16; it += 512) {
+      const int pos = it >> 4, cq = (it & 15) * 4;
       const int y = pos / 11, x = pos % 11;
-      float g[8];
+      f32x4 g = zero_f32x4();
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = 0.f;
-      for (int py = max(0, y - 1); py <= min(9, y); ++py)
-        for (int px = max(0, x - 1); px <= min(9, x); ++px) {
-          const int want = (y - py) * 2 + (x - px);
-          const int p = py * 10 + px;
-          const uint2 am = *reinterpret_cast<const uint2*>(AM + p * 64 + c);
-          const float4 d0 = *reinterpret_cast<const float4*>(DA + p * C3_DARS + c);
-          const float4 d1 = *reinterpret_cast<const float4*>(DA + p * C3_DARS + c + 4);
-          const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+      for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (byte_of(am, j) == want) g[j] += dv[j];
+        for (int dx = 0; dx < 2; ++dx) {
+          const int py = y - dy, px = x - dx;
+          if (py >= 0 && py < 10 && px >= 0 && px < 10) {
+            const int p = py * 10 + px;
+            const uint32_t cw = *reinterpret_cast<const uint32_t*>(AM + p * 64 + cq);
+            const f32x4 d = *reinterpret_cast<const f32x4*>(DA0 + p * C3_DARS + cq) +
+                            *reinterpret_cast<const f32x4*>(DA1 + p * C3_DARS + cq);
+            const uint32_t want = (uint32_t)(dy * 2 + dx);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (((cw >> (8 * j)) & 0xffu) == want) g[j] += d[j];
+          }
         }
-      const bf16x8 zv = *reinterpret_cast<const bf16x8*>(R + pos * C3_RRS + c);
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (float)zv[j] > 0.f ? (bf16)g[j] : (bf16)0.f;
-      dst[it] = v;
+      dst[it] = bf16x4{(bf16)g[0], (bf16)g[1], (bf16)g[2], (bf16)g[3]};
     }
   }
 }
@@ -701,12 +716,11 @@ __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
   return bf16x8{one, one, one, one, one, one, one, one};
 }
 
-__device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ z2, const bf16* __restrict__ da3m,
+__device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
                                  const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
                                  int nslices, int slice) {
   bf16* D = reinterpret_cast<bf16*>(smem);
   bf16* X = reinterpret_cast<bf16*>(smem + C3W_D);
-  bf16* R = reinterpret_cast<bf16*>(smem + C3W_D + C3W_X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;  // m-tiles 4wm..4wm+3 (co), n-tiles 9wn..9wn+8
   const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
@@ -720,16 +734,21 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ z2, const 
   }
   const int per = cdiv(B, nslices);
   const int b_lo = slice * per, b_hi = min(B, b_lo + per);
+  bf16* R = reinterpret_cast<bf16*>(smem + C3W_D + C3W_X);
   C3Pre pre;
-  if (b_lo < b_hi) c3_load(pre, da3m, idx3, z2, b_lo, tid);
+  if (b_lo < b_hi) {
+    pre.load(da3m, idx3, b_lo, tid);
+    a2_glds(a2, b_lo, R, wave, lane, 8);
+  }
   for (int b = b_lo; b < b_hi; ++b) {
-    __syncthreads();
+    __syncthreads();  // R has landed; the previous image's D / X reads are done
     c3_expand(pre, tid, [&](int r) { return D + r * C3_DRS; });
-    c3_store_R(pre, R, tid);
-    if (b + 1 < b_hi) c3_load(pre, da3m, idx3, z2, b + 1, tid);
-    __syncthreads();
-    pool2_into(R, X, tid, 512);
-    __syncthreads();
+    a2_relayout(R, X, tid, 512);
+    __syncthreads();  // D, X complete; R free
+    if (b + 1 < b_hi) {  // lands during the MFMAs
+      pre.load(da3m, idx3, b + 1, tid);
+      a2_glds(a2, b + 1, R, wave, lane, 8);
+    }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = ks * 32 + grp * 8;
@@ -772,7 +791,8 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ z2, const 
   }
 }
 
-__global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__ z2,
+__global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__ a2,
+                                                        const uint8_t* __restrict__ idx2,
                                                         const bf16* __restrict__ da3m,
                                                         const uint8_t* __restrict__ idx3,
                                                         const bf16* __restrict__ packed,
@@ -782,9 +802,9 @@ __global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__
   __shared__ __attribute__((aligned(16))) char smem[C3B_LDS];
   const int blk = blockIdx.x;
   if (blk < n_dgrad)
-    conv3_dgrad_role(smem, z2, da3m, idx3, packed, dz2, B, blk, n_dgrad);
+    conv3_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, B, blk, n_dgrad);
   else
-    conv3_wgrad_role(smem, z2, da3m, idx3, slabs, B, n_wgrad, blk - n_dgrad);
+    conv3_wgrad_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, blk - n_dgrad);
 }
 
 // ================================================================== F2 backward
@@ -1153,16 +1173,17 @@ void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, v
     conv1_fwd_kernel<false><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
 }
 
-void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* z2, int B, hipStream_t s) {
+void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,
+                  hipStream_t s) {
   const int grid = clampi(B, 1, 2 * num_cus());
   conv2_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(packed), b2,
-                                        static_cast<bf16*>(z2), B);
+                                        static_cast<bf16*>(a2), idx2, B);
 }
 
-void cn_conv3_fc_fwd(const void* z2, const void* packed, const float* b3, const float* bfc, float* logits,
+void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s) {
   const int grid = clampi(B, 1, 2 * num_cus());
-  conv3_fc_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(z2), static_cast<const bf16*>(packed), b3,
+  conv3_fc_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a2), static_cast<const bf16*>(packed), b3,
                                            bfc, logits, static_cast<bf16*>(a3), idx3, B);
 }
 
@@ -1185,7 +1206,7 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
     ws = clampi(cdiv(B, 8), 1, cus);
     return;
   }
-  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.68);
+  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.72);
   nd = clampi(B, 1, (int)(frac * cus));
   const int per = cdiv(B, nd);
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
@@ -1219,18 +1240,18 @@ int64_t cn_conv2_slab_floats(int B, bool dgrad) {
 }
 int64_t cn_conv1_slab_floats(int B) { return (int64_t)conv1_wslices(B) * C1_WSLAB; }
 
-void cn_conv3_fc_bwd(const void* z2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
-                     const void* packed, void* da3m, void* dz2, int B, float* fc_slabs, float* c3_slabs,
-                     float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s) {
+void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const uint8_t* idx3, const float* wfc,
+                     const float* dl, const void* packed, void* da3m, void* dz2, int B, float* fc_slabs,
+                     float* c3_slabs, float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s) {
   (void)wfc;  // the data gradient uses the packed bf16 copy, like every other dgrad
   int nd, ws;
   c3_split(B, dz2 != nullptr, nd, ws);
   const int fs = cdiv(B, FC_IMGS);
   fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
                                    static_cast<bf16*>(da3m), fc_slabs, B);
-  conv3_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(z2), static_cast<const bf16*>(da3m), idx3,
-                                           static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B, c3_slabs,
-                                           ws, nd);
+  conv3_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
+                                           idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
+                                           c3_slabs, ws, nd);
   launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
                  seg(c3_slabs, C3_WSLAB, 576 * 128, 128, ws, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc),
                  seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},

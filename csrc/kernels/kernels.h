@@ -58,7 +58,7 @@ void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* 
                        float label_smoothing, int reduction, float* dlogits, hipStream_t s);
 
 // ---------------------------------------------------------------- MNIST ConvNet
-// Activations are NHWC bf16 (a1 [B,13,13,32], r2 [B,11,11,64], a3 [B,16 windows,128]); weights are
+// Activations are NHWC bf16 (a1 [B,13,13,32], a2 [B,10,10,64], a3 [B,16 windows,128]); weights are
 // PyTorch-layout fp32 masters, packed once per forward into bf16 MFMA fragments.
 int64_t cn_packed_elems();
 void cn_pack_weights(const float* w1, const float* w2, const float* w3, const float* wfc, void* out,
@@ -66,10 +66,12 @@ void cn_pack_weights(const float* w1, const float* w2, const float* w3, const fl
 // F1: conv1 + ReLU + pool1 (x u8 or fp32 [B,28,28]; normalisation fused).
 void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
                   int B, float mean, float inv_std, float in_scale, hipStream_t s);
-// F2: conv2 + bias (pre-activation) -> z2 [B,11,11,64].
-void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* z2, int B, hipStream_t s);
-// F3: ReLU + pool2 + conv3 + ReLU + pool3 + fc1 -> logits (+ a3 [B,16,128] / argmax for backward).
-void cn_conv3_fc_fwd(const void* z2, const void* packed, const float* b3, const float* bfc, float* logits,
+// F2: conv2 + bias + ReLU + pool2 (2x2/s1) -> a2 [B,10,10,64] + pool2 codes idx2 [B,10,10,64]
+// (0..3 = first-max position in the window, bit 2 = pooled value 0 / no gradient).
+void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,
+                  hipStream_t s);
+// F3: conv3 + ReLU + pool3 + fc1 on a2 -> logits (+ a3 [B,16,128] / argmax for backward).
+void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s);
 
 // Workspace sizes (floats) of the backward weight-gradient slabs.
@@ -77,10 +79,11 @@ int64_t cn_fc_slab_floats(int B, bool dgrad);
 int64_t cn_conv3_slab_floats(int B, bool dgrad);
 int64_t cn_conv2_slab_floats(int B, bool dgrad);
 int64_t cn_conv1_slab_floats(int B);
-// F3 backward: da3m is a [B,16,128] bf16 workspace; dz2 may be null (skip the data gradient).
-void cn_conv3_fc_bwd(const void* z2, const void* a3, const uint8_t* idx3, const float* wfc, const float* dl,
-                     const void* packed, void* da3m, void* dz2, int B, float* fc_slabs, float* c3_slabs,
-                     float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s);
+// F3 backward: da3m is a [B,16,128] bf16 workspace; dz2 [B,11,11,64] (the gradient of conv2's
+// pre-activation, through pool2 + ReLU) may be null (skip the data gradient).
+void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const uint8_t* idx3, const float* wfc,
+                     const float* dl, const void* packed, void* da3m, void* dz2, int B, float* fc_slabs,
+                     float* c3_slabs, float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s);
 // F2 backward: da1 may be null.
 void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1, int B, float* slabs,
                   float* dw2, float* db2, hipStream_t s);

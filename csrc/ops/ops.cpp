@@ -296,43 +296,46 @@ std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::T
   return {a1, idx};
 }
 
-at::Tensor cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed, const at::Tensor& b2) {
+std::tuple<at::Tensor, at::Tensor> cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed,
+                                                const at::Tensor& b2) {
   const int64_t B = a1.size(0);
   check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
   check_packed(packed);
   check_f32_out(b2, {64}, "conv2 bias");
-  at::Tensor z2 = at::empty({B, 11, 11, 64}, a1.options());
-  if (B == 0) return z2;
-  kern::cn_conv2_fwd(a1.data_ptr(), packed.data_ptr(), b2.data_ptr<float>(), z2.data_ptr(),
-                     static_cast<int>(B), cur_stream(a1));
-  return z2;
+  at::Tensor a2 = at::empty({B, 10, 10, 64}, a1.options());
+  at::Tensor idx2 = at::empty({B, 10, 10, 64}, a1.options().dtype(at::kByte));
+  if (B == 0) return {a2, idx2};
+  kern::cn_conv2_fwd(a1.data_ptr(), packed.data_ptr(), b2.data_ptr<float>(), a2.data_ptr(),
+                     idx2.data_ptr<uint8_t>(), static_cast<int>(B), cur_stream(a1));
+  return {a2, idx2};
 }
 
-std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& z2,
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& a2,
                                                                const at::Tensor& packed,
                                                                const at::Tensor& b3,
                                                                const at::Tensor& bfc) {
-  const int64_t B = z2.size(0);
-  check_act(z2, {B, 11, 11, 64}, at::kBFloat16, "conv2 pre-activation z2");
+  const int64_t B = a2.size(0);
+  check_act(a2, {B, 10, 10, 64}, at::kBFloat16, "pooled conv2 activation a2");
   check_packed(packed);
   check_f32_out(b3, {128}, "conv3 bias");
   check_f32_out(bfc, {10}, "fc1 bias");
-  at::Tensor logits = at::empty({B, 10}, z2.options().dtype(at::kFloat));
-  at::Tensor a3 = at::empty({B, 16, 128}, z2.options());
-  at::Tensor idx3 = at::empty({B, 16, 128}, z2.options().dtype(at::kByte));
+  at::Tensor logits = at::empty({B, 10}, a2.options().dtype(at::kFloat));
+  at::Tensor a3 = at::empty({B, 16, 128}, a2.options());
+  at::Tensor idx3 = at::empty({B, 16, 128}, a2.options().dtype(at::kByte));
   if (B == 0) return {logits, a3, idx3};
-  kern::cn_conv3_fc_fwd(z2.data_ptr(), packed.data_ptr(), b3.data_ptr<float>(), bfc.data_ptr<float>(),
+  kern::cn_conv3_fc_fwd(a2.data_ptr(), packed.data_ptr(), b3.data_ptr<float>(), bfc.data_ptr<float>(),
                         logits.data_ptr<float>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
-                        static_cast<int>(B), cur_stream(z2));
+                        static_cast<int>(B), cur_stream(a2));
   return {logits, a3, idx3};
 }
 
-at::Tensor cn_conv3_fc_bwd(const at::Tensor& z2, const at::Tensor& a3, const at::Tensor& idx3,
-                           const at::Tensor& wfc, const at::Tensor& dlogits,
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
+                           const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& dlogits,
                            const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
                            at::Tensor dwfc, at::Tensor dbfc) {
-  const int64_t B = z2.size(0);
-  check_act(z2, {B, 11, 11, 64}, at::kBFloat16, "conv2 pre-activation z2");
+  const int64_t B = a2.size(0);
+  check_act(a2, {B, 10, 10, 64}, at::kBFloat16, "pooled conv2 activation a2");
+  check_act(idx2, {B, 10, 10, 64}, at::kByte, "pool2 codes");
   check_act(a3, {B, 16, 128}, at::kBFloat16, "pooled conv3");
   check_act(idx3, {B, 16, 128}, at::kByte, "conv3 argmax");
   check_f32_out(wfc, {10, 2048}, "fc1 weight");
@@ -345,7 +348,7 @@ at::Tensor cn_conv3_fc_bwd(const at::Tensor& z2, const at::Tensor& a3, const at:
   at::Tensor dl = dlogits.to(at::kFloat).contiguous();
   check_shape(dl, {B, 10}, "logits grad");
   at::Tensor dz2;
-  if (need_dz2) dz2 = at::empty_like(z2);
+  if (need_dz2) dz2 = at::empty({B, 11, 11, 64}, a2.options());
   if (B == 0) {
     dw3.zero_();
     db3.zero_();
@@ -354,14 +357,14 @@ at::Tensor cn_conv3_fc_bwd(const at::Tensor& z2, const at::Tensor& a3, const at:
     return dz2;
   }
   const int bi = static_cast<int>(B);
-  at::Tensor da3m = at::empty({B, 16, 128}, z2.options());
+  at::Tensor da3m = at::empty({B, 16, 128}, a2.options());
   at::Tensor fs = at::empty({kern::cn_fc_slab_floats(bi, need_dz2)}, dw3.options());
   at::Tensor cs = at::empty({kern::cn_conv3_slab_floats(bi, need_dz2)}, dw3.options());
-  kern::cn_conv3_fc_bwd(z2.data_ptr(), a3.data_ptr(), idx3.data_ptr<uint8_t>(), wfc.data_ptr<float>(),
-                        dl.data_ptr<float>(), packed.data_ptr(), da3m.data_ptr(),
+  kern::cn_conv3_fc_bwd(a2.data_ptr(), idx2.data_ptr<uint8_t>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
+                        wfc.data_ptr<float>(), dl.data_ptr<float>(), packed.data_ptr(), da3m.data_ptr(),
                         need_dz2 ? dz2.data_ptr() : nullptr, bi, fs.data_ptr<float>(),
                         cs.data_ptr<float>(), dw3.data_ptr<float>(), db3.data_ptr<float>(),
-                        dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), cur_stream(z2));
+                        dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), cur_stream(a2));
   return dz2;
 }
 

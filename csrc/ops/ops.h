@@ -57,13 +57,14 @@ at::Tensor cn_pack_weights(const at::Tensor& w1, const at::Tensor& w2, const at:
 std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::Tensor& packed,
                                                 const at::Tensor& b1, double mean, double std,
                                                 double in_scale);
-at::Tensor cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed, const at::Tensor& b2);
-std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& z2,
+std::tuple<at::Tensor, at::Tensor> cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed,
+                                                const at::Tensor& b2);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& a2,
                                                                const at::Tensor& packed,
                                                                const at::Tensor& b3,
                                                                const at::Tensor& bfc);
-at::Tensor cn_conv3_fc_bwd(const at::Tensor& z2, const at::Tensor& a3, const at::Tensor& idx3,
-                           const at::Tensor& wfc, const at::Tensor& dlogits,
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
+                           const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& dlogits,
                            const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
                            at::Tensor dwfc, at::Tensor dbfc);
 at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::Tensor& packed,

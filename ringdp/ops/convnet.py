@@ -3,12 +3,14 @@
 Forward is three fused blocks (reference layers ref/launch_dist.py:35-41):
 
 * ``_Conv1``  conv1 + ReLU + pool1 (+ fused ToTensor/Normalize for uint8 input) -> a1
-* ``_Conv2``  conv2 + bias -> z2 (pre-activation; conv2's ReLU and pool2 belong to the next block)
-* ``_Conv3FC``  ReLU + pool2 + conv3 + ReLU + pool3 + view + fc1 -> logits
+* ``_Conv2``  conv2 + bias + ReLU + overlapping pool2 -> a2 and one pool2 code byte per value
+* ``_Conv3FC``  conv3 + ReLU + pool3 + view + fc1 -> logits
 
-Placing conv2's ReLU and the overlapping pool2 at the start of the third block means their
-mask/argmax are never stored (they are recomputed from z2 in backward) and conv2's backward is a
-plain linear-layer backward.  Weights are packed
+conv2's pre-activation z2 is never materialised.  ``_Conv2`` returns a zero-stride placeholder
+for it (autograd's handle on "the gradient of conv2's output") next to the real activations;
+``_Conv3FC``'s backward scatters d(a2) through the pool2 codes straight into dz2, so conv2's
+backward is a plain linear-layer backward and pool2/ReLU backward costs no extra pass over
+memory.  Weights are packed
 once per forward into bf16 MFMA fragments (``C.cn_pack_weights``); the fp32 masters stay the
 parameters.  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
 ``_Conv3FC.backward`` - so ringdp's reducer starts the first bucket all-reduce while conv2/conv1
@@ -49,13 +51,16 @@ class _Conv1(torch.autograd.Function):
 class _Conv2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, a1, w, b, packed):
-        z2 = C.cn_conv2_fwd(a1, packed, b)
+        a2, idx2 = C.cn_conv2_fwd(a1, packed, b)
+        z2 = a2.new_empty((1, 1, 1, 1)).expand(a1.shape[0], 11, 11, 64)  # placeholder, never read
+        ctx.mark_non_differentiable(a2, idx2)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(a1, packed)
         ctx.params = (w, b)
-        return z2
+        return z2, a2, idx2
 
     @staticmethod
-    def backward(ctx, dz2):
+    def backward(ctx, dz2, _da2, _didx2):
         a1, packed = ctx.saved_tensors
         w, b = ctx.params
         dw, db = grad_buffer(w), grad_buffer(b)
@@ -67,23 +72,23 @@ class _Conv2(torch.autograd.Function):
 
 class _Conv3FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z2, w3, b3, wfc, bfc, packed):
-        logits, a3, idx3 = C.cn_conv3_fc_fwd(z2, packed, b3, bfc)
-        ctx.save_for_backward(z2, a3, idx3, wfc, packed)
+    def forward(ctx, z2, a2, idx2, w3, b3, wfc, bfc, packed):
+        logits, a3, idx3 = C.cn_conv3_fc_fwd(a2, packed, b3, bfc)
+        ctx.save_for_backward(a2, idx2, a3, idx3, wfc, packed)
         ctx.params = (w3, b3, wfc, bfc)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
-        z2, a3, idx3, wfc_saved, packed = ctx.saved_tensors
+        a2, idx2, a3, idx3, wfc_saved, packed = ctx.saved_tensors
         w3, b3, wfc, bfc = ctx.params
         dw3, db3, dwfc, dbfc = (grad_buffer(p) for p in (w3, b3, wfc, bfc))
         need_in = ctx.needs_input_grad[0]
-        dz2 = C.cn_conv3_fc_bwd(z2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
+        dz2 = C.cn_conv3_fc_bwd(a2, idx2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
                                 dw3, db3, dwfc, dbfc)
         n = ctx.needs_input_grad
-        return (dz2 if need_in else None, dw3 if n[1] else None, db3 if n[2] else None,
-                dwfc if n[3] else None, dbfc if n[4] else None, None)
+        return (dz2 if need_in else None, None, None, dw3 if n[3] else None, db3 if n[4] else None,
+                dwfc if n[5] else None, dbfc if n[6] else None, None)
 
 
 def pack_weights(conv1, conv2, conv3, fc1) -> torch.Tensor:
@@ -104,5 +109,5 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
     x = x.contiguous()
     packed = pack_weights(conv1, conv2, conv3, fc1)
     a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
-    z2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
-    return _Conv3FC.apply(z2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)
+    z2, a2, idx2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
+    return _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)

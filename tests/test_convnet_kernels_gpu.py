@@ -1,8 +1,8 @@
 """Numerics of ringdp's ConvNet HIP kernels against plain PyTorch fp32 references (same ops,
 inputs rounded to bf16 the way the kernels consume them).
 
-Blocks under test (csrc/kernels/convnet.hip): F1 conv1+relu+pool1, F2 conv2 (pre-activation),
-F3 relu+pool2+conv3+relu+pool3+fc1, their backward kernels and the weight packer."""
+Blocks under test (csrc/kernels/convnet.hip): F1 conv1+relu+pool1, F2 conv2+relu+pool2 (with pool2
+codes), F3 conv3+relu+pool3+fc1, their backward kernels and the weight packer."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -104,22 +104,44 @@ def test_conv1_forward(B, u8):
     assert torch.equal((idx & 4) != 0, a1.float() > 0)
 
 
+def pool2_ref(z2):
+    """relu + 2x2/s1 max pool of a bf16 z2 [B,11,11,64] with the kernel's code byte: first maximum in
+    (0,0),(0,1),(1,0),(1,1) order, bit 2 set where the pooled value is 0."""
+    z = z2.float()
+    v = torch.stack([z[:, :-1, :-1], z[:, :-1, 1:], z[:, 1:, :-1], z[:, 1:, 1:]], -1)
+    m = v.max(-1).values.clamp_min(0)
+    first = torch.argmax((v == m.unsqueeze(-1)).to(torch.int8), -1)
+    code = torch.where(m > 0, first, torch.full_like(first, 4)).to(torch.uint8)
+    return m.bfloat16(), code
+
+
 @pytest.mark.parametrize("B", [1, 5, 100, 600])
 def test_conv2_forward(B):
     torch.manual_seed(B)
     dev = torch.device("cuda")
     ws = weights(dev, B + 1)
     a1 = torch.relu(torch.randn(B, 13, 13, 32, device=dev)).bfloat16()
-    z2 = C().cn_conv2_fwd(a1, packed(ws), ws[3])
-    ref = F.conv2d(a1.permute(0, 3, 1, 2).float(), bf(ws[2]), ws[3]).permute(0, 2, 3, 1)
-    assert z2.shape == (B, 11, 11, 64) and z2.dtype == torch.bfloat16
-    assert rel_err(z2, ref) < 1e-2
+    a2, idx2 = C().cn_conv2_fwd(a1, packed(ws), ws[3])
+    z = F.conv2d(a1.permute(0, 3, 1, 2).float(), bf(ws[2]), ws[3]).permute(0, 2, 3, 1)
+    ref = F.max_pool2d(F.relu(z.permute(0, 3, 1, 2)), 2, 1).permute(0, 2, 3, 1)
+    assert a2.shape == (B, 10, 10, 64) and a2.dtype == torch.bfloat16 and idx2.dtype == torch.uint8
+    assert rel_err(a2, ref) < 1e-2
+    # codes: bit 2 <=> pooled value 0; otherwise the named position holds the window maximum
+    assert torch.equal((idx2 & 4) != 0, a2.float() == 0)
+    v = torch.stack([z[:, :-1, :-1], z[:, :-1, 1:], z[:, 1:, :-1], z[:, 1:, 1:]], -1)
+    picked = torch.gather(v, 4, (idx2.long() & 3).unsqueeze(-1)).squeeze(-1)
+    live = (idx2 & 4) == 0
+    tol = 1e-2 * (1 + v.abs().amax(-1))
+    assert torch.all(((v.amax(-1) - picked) <= tol)[live])
+    # on bf16-exact inputs the codes are exactly torch's first-max argmax
+    za, zc = pool2_ref(z.bfloat16())
+    kc = torch.where((idx2 & 4) != 0, torch.full_like(idx2, 4), idx2)  # bits 0-1 are free when bit 2 is set
+    assert float((zc == kc).float().mean()) > 0.99
 
 
-def f3_reference(z2, ws):
+def f3_reference(a2, ws):
     w3, b3, wf, bfc = ws[4], ws[5], ws[6], ws[7]
-    a2 = F.max_pool2d(F.relu(z2.permute(0, 3, 1, 2).float()), 2, 1)
-    y = F.conv2d(a2, bf(w3), b3)
+    y = F.conv2d(a2.permute(0, 3, 1, 2).float(), bf(w3), b3)
     a3 = F.max_pool2d(F.relu(y), 2, 2)
     return y, a3, F.linear(a3.reshape(-1, 2048), bf(wf), bfc)
 
@@ -129,9 +151,9 @@ def test_conv3_fc_forward(B):
     torch.manual_seed(B)
     dev = torch.device("cuda")
     ws = weights(dev, B + 2)
-    z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(z2, packed(ws), ws[5], ws[7])
-    y, a3_ref, logits_ref = f3_reference(z2, ws)
+    a2 = torch.relu(torch.randn(B, 10, 10, 64, device=dev)).bfloat16()
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(a2, packed(ws), ws[5], ws[7])
+    y, a3_ref, logits_ref = f3_reference(a2, ws)
     assert a3.shape == (B, 16, 128) and idx3.shape == (B, 16, 128)
     a3_nchw = a3.view(B, 4, 4, 128).permute(0, 3, 1, 2)
     assert rel_err(a3_nchw, a3_ref) < 1e-2
@@ -147,11 +169,12 @@ def test_conv3_fc_backward(B, need_dz2):
     ws = weights(dev, B + 3)
     w3, b3, wf, bfc = ws[4], ws[5], ws[6], ws[7]
     z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
+    a2, idx2 = pool2_ref(z2)
     pk = packed(ws)
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(z2, pk, b3, bfc)
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(a2, pk, b3, bfc)
     dl = torch.randn(B, 10, device=dev)
     dw3, db3, dwf, dbf = (torch.empty_like(t) for t in (w3, b3, wf, bfc))
-    dz2 = C().cn_conv3_fc_bwd(z2, a3, idx3, wf, dl, pk, need_dz2, dw3, db3, dwf, dbf)
+    dz2 = C().cn_conv3_fc_bwd(a2, idx2, a3, idx3, wf, dl, pk, need_dz2, dw3, db3, dwf, dbf)
     # reference: fc backward in fp32, unpool through the kernel's own pool3 argmax
     a3_flat = a3.view(B, 4, 4, 128).permute(0, 3, 1, 2).reshape(B, 2048).float()
     torch.testing.assert_close(dwf, dl.t() @ a3_flat, rtol=1e-4, atol=1e-4)
@@ -212,18 +235,19 @@ def test_conv1_wgrad(B, u8):
 
 
 def test_wgrad_deterministic():
-    """Slab reductions run in a fixed order: two identical backward calls are bitwise equal."""
+    """Slab reductions and the dgrad K-group sums run in a fixed order: two identical backward calls
+    are bitwise equal."""
     dev = torch.device("cuda")
     ws = weights(dev, 9)
     B = 333
-    z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
+    a2, idx2 = pool2_ref(torch.randn(B, 11, 11, 64, device=dev).bfloat16())
     pk = packed(ws)
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(z2, pk, ws[5], ws[7])
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(a2, pk, ws[5], ws[7])
     dl = torch.randn(B, 10, device=dev)
     outs = []
     for _ in range(2):
         g = [torch.empty_like(t) for t in (ws[4], ws[5], ws[6], ws[7])]
-        dz2 = C().cn_conv3_fc_bwd(z2, a3, idx3, ws[6], dl, pk, True, *g)
+        dz2 = C().cn_conv3_fc_bwd(a2, idx2, a3, idx3, ws[6], dl, pk, True, *g)
         outs.append(g + [dz2])
     for a, b in zip(*outs):
         assert torch.equal(a, b)

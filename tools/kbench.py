@@ -46,10 +46,10 @@ def run(B):
     norm = (0.1307, 0.3081, 1 / 255.0)
     pk = C.cn_pack_weights(w1, w2, w3, wf)
     a1, i1 = C.cn_conv1_fwd(x, pk, b1, *norm)
-    z2 = C.cn_conv2_fwd(a1, pk, b2)
-    logits, a3, i3 = C.cn_conv3_fc_fwd(z2, pk, b3, bfc)
+    a2, i2 = C.cn_conv2_fwd(a1, pk, b2)
+    logits, a3, i3 = C.cn_conv3_fc_fwd(a2, pk, b3, bfc)
     dl = torch.randn(B, 10, device=dev)
-    dz2 = torch.randn_like(z2)
+    dz2 = torch.randn(a2.shape[0], 11, 11, 64, device=a2.device).bfloat16()
     da1 = torch.randn_like(a1)
     dw1, db1 = torch.empty_like(w1), torch.empty_like(b1)
     dw2, db2 = torch.empty_like(w2), torch.empty_like(b2)
@@ -65,10 +65,10 @@ def run(B):
     res["pack"] = timeit(lambda: C.cn_pack_weights(w1, w2, w3, wf))
     res["conv1_fwd"] = timeit(lambda: C.cn_conv1_fwd(x, pk, b1, *norm))
     res["conv2_fwd"] = timeit(lambda: C.cn_conv2_fwd(a1, pk, b2))
-    res["conv3_fc_fwd"] = timeit(lambda: C.cn_conv3_fc_fwd(z2, pk, b3, bfc))
+    res["conv3_fc_fwd"] = timeit(lambda: C.cn_conv3_fc_fwd(a2, pk, b3, bfc))
     res["ce_fwd"] = timeit(lambda: C.cross_entropy_fwd(logits, y, -100, 0.0, 1))
-    res["conv3_fc_bwd"] = timeit(lambda: C.cn_conv3_fc_bwd(z2, a3, i3, wf, dl, pk, True, dw3, db3, dwf, dbf))
-    res["conv3_fc_bwd_w"] = timeit(lambda: C.cn_conv3_fc_bwd(z2, a3, i3, wf, dl, pk, False, dw3, db3, dwf, dbf))
+    res["conv3_fc_bwd"] = timeit(lambda: C.cn_conv3_fc_bwd(a2, i2, a3, i3, wf, dl, pk, True, dw3, db3, dwf, dbf))
+    res["conv3_fc_bwd_w"] = timeit(lambda: C.cn_conv3_fc_bwd(a2, i2, a3, i3, wf, dl, pk, False, dw3, db3, dwf, dbf))
     res["conv2_bwd"] = timeit(lambda: C.cn_conv2_bwd(a1, dz2, pk, True, dw2, db2))
     res["conv2_bwd_w"] = timeit(lambda: C.cn_conv2_bwd(a1, dz2, pk, False, dw2, db2))
     res["conv1_wgrad"] = timeit(lambda: C.cn_conv1_wgrad(x, da1, i1, dw1, db1, *norm))
