@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
 //       da3m[b][w][co] = (a3 > 0) * sum_n dl[b][n] * Wfc[n][co*16 + w]     (bf16, Wfc from the pack)
 //     and the fc1 weight/bias gradient of this block's images as an fp32 slab.  The conv3 backward
 //     roles expand da3m to window-ordered rows (row 4w + argmax) in LDS.
-constexpr int FC_IMGS = 16;              // images per workgroup
+constexpr int FC_IMGS = 32;              // images per workgroup
 constexpr int FC_SLAB = 10 * 2048 + 10;  // dWfc + dbfc
 
 __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3,
@@ -529,11 +529,13 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
       }
     }
   }
+  // slab in thread order (coalesced): element (n*8 + j)*256 + t; the reduction (mode 2) maps it back
+  // to dWfc[n][co*16 + w]
   float* slab = slabs + (int64_t)blockIdx.x * FC_SLAB;
 #pragma unroll
   for (int n = 0; n < 10; ++n)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) slab[n * 2048 + (co0 + j) * 16 + wd] = acc[j][n];
+    for (int j = 0; j < 8; ++j) slab[(n * 8 + j) * 256 + t] = acc[j][n];
   if (t < 10) slab[20480 + t] = bacc;
 }
 
@@ -1078,7 +1080,8 @@ struct ReduceSeg {
   int64_t n;       // outputs
   int nslices;
   float* out;
-  int mode;  // 0: out[i] = sum; 1: conv transpose dWt[n = tap*cin + ci][co] -> W[co][ci][tap]
+  int mode;  // 0: out[i] = sum; 1: conv transpose dWt[n = tap*cin + ci][co] -> W[co][ci][tap];
+             // 2: fc1 slab in fc_bwd thread order (n*8 + j)*256 + t -> dWfc[n][co*16 + w]
   int cin, cout;
   int blocks;
 };
@@ -1117,6 +1120,9 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(ReduceSegs segs) {
   const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
   if (sg.mode == 0) {
     sg.out[i] = v;
+  } else if (sg.mode == 2) {
+    const int t = (int)(i & 255), nj = (int)(i >> 8), n = nj >> 3, j = nj & 7;
+    sg.out[n * 2048 + ((t & 15) * 8 + j) * 16 + (t >> 4)] = v;
   } else {
     const int n = (int)(i / sg.cout), co = (int)(i % sg.cout);
     sg.out[((int64_t)co * sg.cin + n % sg.cin) * 9 + n / sg.cin] = v;
@@ -1253,7 +1259,7 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
                                            idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
                                            c3_slabs, ws, nd);
   launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
-                 seg(c3_slabs, C3_WSLAB, 576 * 128, 128, ws, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc),
+                 seg(c3_slabs, C3_WSLAB, 576 * 128, 128, ws, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
                  seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},
                 s);
 }
