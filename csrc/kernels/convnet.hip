@@ -473,7 +473,8 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
 //     and the fc1 weight/bias gradient of this block's images as an fp32 slab.  The conv3 backward
 //     roles expand da3m to window-ordered rows (row 4w + argmax) in LDS.
 constexpr int FC_IMGS = 32;              // images per workgroup
-constexpr int FC_SLAB = 10 * 2048 + 10;  // dWfc + dbfc
+constexpr int FC_SLAB = 10 * 2048 + 10 + 128;  // dWfc + dbfc + db3 (the conv3 bias gradient is the sum of
+                                                // d(a3) over windows: no MFMA tile needed for it)
 
 __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3,
                                                      const bf16* __restrict__ packed,
@@ -498,7 +499,9 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
   for (int j = 0; j < 8; ++j)
 #pragma unroll
     for (int n = 0; n < 10; ++n) acc[j][n] = 0.f;
-  float bacc = 0.f;
+  float bacc = 0.f, dsum[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dsum[j] = 0.f;
   const int b0 = blockIdx.x * FC_IMGS, nimg = min(FC_IMGS, B - b0);
   for (int k0 = 0; k0 < nimg; k0 += 8) {
     bf16x8 av[8];
@@ -522,7 +525,9 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
             s = fmaf(g[n], wr[j][n], s);
             acc[j][n] = fmaf(g[n], aj, acc[j][n]);
           }
-          v[j] = aj > 0.f ? (bf16)s : (bf16)0.f;
+          const float m = aj > 0.f ? s : 0.f;
+          dsum[j] += m;
+          v[j] = (bf16)m;
         }
         *reinterpret_cast<bf16x8*>(da3m + (int64_t)b * 2048 + wd * 128 + co0) = v;
         if (t < 10) bacc += dl[(int64_t)b * 10 + t];
@@ -537,27 +542,43 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
 #pragma unroll
     for (int j = 0; j < 8; ++j) slab[(n * 8 + j) * 256 + t] = acc[j][n];
   if (t < 10) slab[20480 + t] = bacc;
+  // db3 partial: sum the 16 windows (4 per wave via lane shuffles, then the 4 waves) per channel
+  __shared__ float red[4][128];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float v = dsum[j];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    dsum[j] = v;
+  }
+  if ((t & 63) < 16) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[t >> 6][co0 + j] = dsum[j];
+  }
+  __syncthreads();
+  if (t < 128) slab[20490 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
 }
 
-// (2) conv3 backward, two roles in one 512-thread launch:
+// (2) conv3 backward, two roles in one launch of 256-thread workgroups, two per CU (a CU usually
+//     hosts one of each, so one role's barrier-separated phases overlap the other's MFMA stream):
 //   dgrad: da2 = full-corr(d(conv3) image, flipped W3), then pool2 + ReLU backward: each da2 value goes
 //          to the z2 position its pool2 code names (F2 forward) -> dz2 [B,11,11,64];
-//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci];
-//          db3 via one extra MFMA tile against a ones column.
+//   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a workgroup pair per
+//          image slice (one half of the 576 n columns each).  db3 comes from fc1's backward.
 constexpr int C3_PW = 12;    // padded d(conv3) image width (8 + 2*2)
 constexpr int C3_PRS = 136;  // bf16 per padded-image row (128 + 8)
-constexpr int C3_DARS = 68;  // floats per da2 partial-sum row (64 + 4)
+constexpr int C3_DARS = 68;  // floats per da2 row (64 + 4)
 constexpr int C3_DRS = 136;  // bf16 per D3 row in LDS
 constexpr int C3D_P = C3_PW * C3_PW * C3_PRS * 2;  // 39168
-constexpr int C3D_AM = 100 * 64;                   // 6400: pool2 codes
-constexpr int C3D_DA = 100 * C3_DARS * 4;          // 27200 (x2: partial sums of two k-group pairs)
-constexpr int C3D_LDS = C3D_P + C3D_AM + 2 * C3D_DA;
+constexpr int C3D_AM = 100 * 64;                   // 6400: pool2 codes (x2: the next image lands by DMA)
+constexpr int C3D_DA = 100 * C3_DARS * 4;          // 27200
+constexpr int C3D_LDS = C3D_P + 2 * C3D_AM + C3D_DA;
 constexpr int C3W_D = 64 * C3_DRS * 2;   // 17408
 constexpr int C3W_X = 100 * C3_XRS * 2;  // 14400
 constexpr int C3W_R = 100 * 64 * 2;      // 12800: DMA staging of the next a2 image
 constexpr int C3W_LDS = C3W_D + C3W_X + C3W_R;
 constexpr int C3B_LDS = C3D_LDS > C3W_LDS ? C3D_LDS : C3W_LDS;
-constexpr int C3_WSLAB = 576 * 128 + 128;  // dW3t + db3
+constexpr int C3_WSLAB = 576 * 128;  // dW3t
 
 // The compact F3-backward input of one image, held in registers while the previous image is
 // computed on: d(a3) chunk + its pool3 argmax bytes (threads < 256).
@@ -588,29 +609,37 @@ __device__ __forceinline__ void c3_expand(const C3Pre& p, int tid, RowPtr row_pt
   }
 }
 
+// pool2 codes of one image (6400 B = 400 x 16 B) -> LDS by DMA (4 waves, 7 wave-instructions)
+__device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int b, uint8_t* AM, int wave,
+                                           int lane) {
+  const uint8_t* src = idx2 + (int64_t)b * 6400;
+  for (int k = wave; k < 7; k += 4) {
+    const int slot = k * 64 + lane;
+    if (slot < 400) glds16(src + slot * 16, AM + k * 1024);
+  }
+}
+
 // dgrad GEMM per image, operands swapped so the output lands channel-contiguous:
 //   C[c = 64 input channels][m = 100 positions] = sum_k W3d[c][k] * Pimg[k][m],  K = 9 taps x 128.
-// 8 waves = 4 K-groups (9 of the 36 k-steps each) x 2 channel halves; a wave keeps the weight
-// fragments of its K-group and 2 channel tiles in VGPRs (72) for every image, covers all 7 position
-// tiles, and uses each image fragment it reads from LDS for 2 MFMAs (half the LDS reads of one
-// channel tile per wave).  K-group partials are combined in a fixed order ((g0 + g1) + (g2 + g3)):
-// deterministic.
+// 4 waves = 2 K-groups (18 of the 36 k-steps each) x 2 channel halves; a wave keeps the weight
+// fragments of its K-group and 2 channel tiles in VGPRs (144) for every image, covers all 7 position
+// tiles, and uses each image fragment it reads from LDS for 2 MFMAs.  The two K-group partials are
+// combined in a fixed order (deterministic).
 __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ dz2, int B, int block, int nblocks) {
   bf16* P = reinterpret_cast<bf16*>(smem);
-  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P);
-  float* DA0 = reinterpret_cast<float*>(smem + C3D_P + C3D_AM);
-  float* DA1 = DA0 + 100 * C3_DARS;
+  uint8_t* AMb = reinterpret_cast<uint8_t*>(smem + C3D_P);
+  float* DA = reinterpret_cast<float*>(smem + C3D_P + 2 * C3D_AM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = wave >> 1, nh = wave & 1;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3D_OFF);
-  bf16x8 aw[2][9];
+  bf16x8 aw[2][18];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int j = 0; j < 9; ++j) aw[t][j] = pk[((2 * nh + t) * 36 + 9 * kg + j) * 64 + lane];
+    for (int j = 0; j < 18; ++j) aw[t][j] = pk[((2 * nh + t) * 36 + 18 * kg + j) * 64 + lane];
   int base[7];  // positions >= 100 read a clamped (valid) address; their outputs are dropped
 #pragma unroll
   for (int mt = 0; mt < 7; ++mt) {
@@ -618,7 +647,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
     base[mt] = (mm / 10) * C3_PW + mm % 10;
   }
   // the ring of the padded image stays zero; only the 8x8 interior is rewritten per image
-  for (int c = tid; c < C3D_P / 16; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
+  for (int c = tid; c < C3D_P / 16; c += 256) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
   // the K-group is a template parameter, so every fragment address is a per-lane base plus an
   // immediate offset (no hoisted address VGPRs)
   auto mfma_phase = [&](auto kg_c) {
@@ -627,8 +656,8 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
 #pragma unroll
     for (int mt = 0; mt < 7; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int ks = 9 * KG + j;
+    for (int j = 0; j < 18; ++j) {
+      const int ks = 18 * KG + j;
       const int tapp = ks >> 2, c0 = (ks & 3) * 32;
       const int shift = (tapp / 3) * C3_PW + tapp % 3;
 #pragma unroll
@@ -638,57 +667,51 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
         acc[mt][1] = mfma16x16x32(aw[1][j], bfr, acc[mt][1]);
       }
     }
-    // round 1: groups 1 and 3 publish; round 2: groups 0 and 2 fold theirs in
-    auto publish = [&](float* D, bool add) {
+    // K-group 1 publishes, K-group 0 folds its partial in
+    auto publish = [&](bool add) {
 #pragma unroll
       for (int mt = 0; mt < 7; ++mt) {
         const int m = mt * 16 + r16;
         if (m < 100) {
 #pragma unroll
           for (int t = 0; t < 2; ++t) {
-            f32x4* d = reinterpret_cast<f32x4*>(D + m * C3_DARS + (2 * nh + t) * 16 + c4);
-            *d = add ? *d + acc[mt][t] : acc[mt][t];
+            f32x4* d = reinterpret_cast<f32x4*>(DA + m * C3_DARS + (2 * nh + t) * 16 + c4);
+            *d = add ? acc[mt][t] + *d : acc[mt][t];
           }
         }
       }
     };
-    if (KG & 1) publish(KG == 1 ? DA0 : DA1, false);
+    if (KG == 1) publish(false);
     __syncthreads();
-    if (!(KG & 1)) publish(KG == 0 ? DA0 : DA1, true);
-  };
-  auto run_phase = [&]() {
-    switch (kg) {
-      case 0: mfma_phase(std::integral_constant<int, 0>{}); break;
-      case 1: mfma_phase(std::integral_constant<int, 1>{}); break;
-      case 2: mfma_phase(std::integral_constant<int, 2>{}); break;
-      default: mfma_phase(std::integral_constant<int, 3>{}); break;
-    }
+    if (KG == 0) publish(true);
   };
   C3Pre pre;
-  uint4 code = make_uint4(0, 0, 0, 0);
-  int b = block;
+  int b = block, cur = 0;
   if (b < B) {
     pre.load(da3m, idx3, b, tid);
-    if (tid < 400) code = reinterpret_cast<const uint4*>(idx2 + (int64_t)b * 6400)[tid];
+    codes_glds(idx2, b, AMb, wave, lane);
   }
-  for (; b < B; b += nblocks) {
-    __syncthreads();  // previous image fully consumed (P, AM, DA)
+  for (; b < B; b += nblocks, cur ^= 1) {
+    __syncthreads();  // previous image fully consumed (P, DA); this image's codes have landed
     c3_expand(pre, tid, [&](int r) { return P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS; });
-    if (tid < 400) reinterpret_cast<uint4*>(AM)[tid] = code;
     const int nb = b + nblocks;
     if (nb < B) {  // lands during the MFMA phase
       pre.load(da3m, idx3, nb, tid);
-      if (tid < 400) code = reinterpret_cast<const uint4*>(idx2 + (int64_t)nb * 6400)[tid];
+      codes_glds(idx2, nb, AMb + (cur ^ 1) * C3D_AM, wave, lane);
     }
     __syncthreads();
-    run_phase();
+    if (kg == 0)
+      mfma_phase(std::integral_constant<int, 0>{});
+    else
+      mfma_phase(std::integral_constant<int, 1>{});
     __syncthreads();
-    // pool2 + ReLU backward as a gather: item (position, 4-channel quad) sums da2 = DA0 + DA1 of the
-    // (<= 4) windows covering it, in a fixed window order, where the window's code names this
-    // position (a code with bit 2 set - no gradient - never matches).  16 consecutive lanes share a
-    // position: every LDS read is a contiguous 256 B (conflict-free) and every store is coalesced.
+    // pool2 + ReLU backward as a gather: item (position, 4-channel quad) sums da2 of the (<= 4)
+    // windows covering it, in a fixed window order, where the window's code names this position (a
+    // code with bit 2 set - no gradient - never matches).  16 consecutive lanes share a position:
+    // every LDS read is a contiguous 256 B (conflict-free) and every store is coalesced.
+    const uint8_t* AM = AMb + cur * C3D_AM;
     bf16x4* dst = reinterpret_cast<bf16x4*>(dz2 + (int64_t)b * 121 * 64);
-    for (int it = tid; it < 121 * 16; it += 512) {
+    for (int it = tid; it < 121 * 16; it += 256) {
       const int pos = it >> 4, cq = (it & 15) * 4;
       const int y = pos / 11, x = pos % 11;
       f32x4 g = zero_f32x4();
@@ -700,8 +723,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
           if (py >= 0 && py < 10 && px >= 0 && px < 10) {
             const int p = py * 10 + px;
             const uint32_t cw = *reinterpret_cast<const uint32_t*>(AM + p * 64 + cq);
-            const f32x4 d = *reinterpret_cast<const f32x4*>(DA0 + p * C3_DARS + cq) +
-                            *reinterpret_cast<const f32x4*>(DA1 + p * C3_DARS + cq);
+            const f32x4 d = *reinterpret_cast<const f32x4*>(DA + p * C3_DARS + cq);
             const uint32_t want = (uint32_t)(dy * 2 + dx);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -713,43 +735,38 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
   }
 }
 
-__device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
-  const bf16 one = (bf16)((lane & 15) == 0 ? 1.f : 0.f);
-  return bf16x8{one, one, one, one, one, one, one, one};
-}
-
+// wgrad: workgroup half h of an image slice covers n-tiles 18h..18h+17 of dW3t [576][128];
+// wave (wm, wn) owns m-tiles (co) 4wm..4wm+3 x n-tiles 18h + 9wn .. +8.
 __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
                                  const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
-                                 int nslices, int slice) {
+                                 int nslices, int slice, int h) {
   bf16* D = reinterpret_cast<bf16*>(smem);
   bf16* X = reinterpret_cast<bf16*>(smem + C3W_D);
+  bf16* R = reinterpret_cast<bf16*>(smem + C3W_D + C3W_X);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;  // m-tiles 4wm..4wm+3 (co), n-tiles 9wn..9wn+8
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nt0 = 18 * h + 9 * wn;
   const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
-  const bf16x8 onesf = ones_column_frag(lane);
-  f32x4 acc[4][9], accb[4];
+  f32x4 acc[4][9];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    accb[i] = zero_f32x4();
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = zero_f32x4();
-  }
   const int per = cdiv(B, nslices);
   const int b_lo = slice * per, b_hi = min(B, b_lo + per);
-  bf16* R = reinterpret_cast<bf16*>(smem + C3W_D + C3W_X);
   C3Pre pre;
   if (b_lo < b_hi) {
     pre.load(da3m, idx3, b_lo, tid);
-    a2_glds(a2, b_lo, R, wave, lane, 8);
+    a2_glds(a2, b_lo, R, wave, lane, 4);
   }
   for (int b = b_lo; b < b_hi; ++b) {
     __syncthreads();  // R has landed; the previous image's D / X reads are done
     c3_expand(pre, tid, [&](int r) { return D + r * C3_DRS; });
-    a2_relayout(R, X, tid, 512);
+    a2_relayout(R, X, tid, 256);
     __syncthreads();  // D, X complete; R free
     if (b + 1 < b_hi) {  // lands during the MFMAs
       pre.load(da3m, idx3, b + 1, tid);
-      a2_glds(a2, b + 1, R, wave, lane, 8);
+      a2_glds(a2, b + 1, R, wave, lane, 4);
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -765,7 +782,7 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const 
       const int x0 = win_pos(kb + q, 10), x1 = win_pos(kb + 4 + q, 10);
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
-        const int n0 = (9 * wn + j) * 16;  // n = tap*64 + ci
+        const int n0 = (nt0 + j) * 16;  // n = tap*64 + ci
         const int tap = n0 >> 6, c0 = n0 & 63;
         const int shift = (tap / 3) * 10 + tap % 3;
         const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3_XRS + c0 + 4 * p);
@@ -773,10 +790,6 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const 
         const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int i = 0; i < 4; ++i) acc[i][j] = mfma16x16x32(af[i], bf, acc[i][j]);
-      }
-      if (wn == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) accb[i] = mfma16x16x32(af[i], onesf, accb[i]);
       }
     }
   }
@@ -786,27 +799,33 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const 
     const int co = (4 * wm + i) * 16 + grp * 4;
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
-      const int n = (9 * wn + j) * 16 + g16;
+      const int n = (nt0 + j) * 16 + g16;
       *reinterpret_cast<f32x4*>(slab + (int64_t)n * 128 + co) = acc[i][j];
     }
-    if (wn == 0 && g16 == 0) *reinterpret_cast<f32x4*>(slab + 576 * 128 + co) = accb[i];
   }
 }
 
-__global__ __launch_bounds__(512) void conv3_bwd_kernel(const bf16* __restrict__ a2,
-                                                        const uint8_t* __restrict__ idx2,
-                                                        const bf16* __restrict__ da3m,
-                                                        const uint8_t* __restrict__ idx3,
-                                                        const bf16* __restrict__ packed,
-                                                        bf16* __restrict__ dz2, int B,
-                                                        float* __restrict__ slabs, int n_wgrad,
-                                                        int n_dgrad) {
+__global__ __launch_bounds__(256, 2) void conv3_bwd_kernel(const bf16* __restrict__ a2,
+                                                           const uint8_t* __restrict__ idx2,
+                                                           const bf16* __restrict__ da3m,
+                                                           const uint8_t* __restrict__ idx3,
+                                                           const bf16* __restrict__ packed,
+                                                           bf16* __restrict__ dz2, int B,
+                                                           float* __restrict__ slabs, int n_wgrad,
+                                                           int n_dgrad) {
   __shared__ __attribute__((aligned(16))) char smem[C3B_LDS];
   const int blk = blockIdx.x;
-  if (blk < n_dgrad)
+  if (blk < n_dgrad) {
     conv3_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, B, blk, n_dgrad);
-  else
-    conv3_wgrad_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, blk - n_dgrad);
+  } else {
+    const int w = blk - n_dgrad;
+    conv3_wgrad_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w >> 1, w & 1);
+  }
+}
+
+__device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
+  const bf16 one = (bf16)((lane & 15) == 0 ? 1.f : 0.f);
+  return bf16x8{one, one, one, one, one, one, one, one};
 }
 
 // ================================================================== F2 backward
@@ -1206,16 +1225,17 @@ static double split_frac(const char* env, double dflt) {
 }
 
 static void c3_split(int B, bool dgrad, int& nd, int& ws) {
-  const int cus = num_cus();
+  // 256-thread workgroups, two per CU; ws = image slices, each served by a pair of workgroups
+  const int slots = 2 * num_cus();
   if (!dgrad) {
     nd = 0;
-    ws = clampi(cdiv(B, 8), 1, cus);
+    ws = clampi(cdiv(B, 8), 1, slots / 2);
     return;
   }
-  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.72);
-  nd = clampi(B, 1, (int)(frac * cus));
+  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.70);
+  nd = clampi(B, 1, (int)(frac * slots));
   const int per = cdiv(B, nd);
-  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
+  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, (slots - nd) / 2));  // >= 2 images per slab
 }
 
 static void c2_split(int B, bool dgrad, int& nd, int& ws) {
@@ -1255,11 +1275,11 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
   const int fs = cdiv(B, FC_IMGS);
   fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
                                    static_cast<bf16*>(da3m), fc_slabs, B);
-  conv3_bwd_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
+  conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
                                            idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
                                            c3_slabs, ws, nd);
   launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
-                 seg(c3_slabs, C3_WSLAB, 576 * 128, 128, ws, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
+                 seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
                  seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},
                 s);
 }
