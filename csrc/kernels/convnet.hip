@@ -829,7 +829,7 @@ __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
 }
 
 // ================================================================== F2 backward
-// conv2 is linear here (its ReLU belongs to F3), so dz2 is the conv output gradient directly:
+// conv2's ReLU and pool2 are undone by F3's backward, so dz2 is the conv output gradient directly:
 //   dgrad: da1 = full-corr(dz2 image, flipped W2)  [13x13x32]
 //   wgrad: dW2t[n = tap*32 + ci][co] = sum_pos dz2[pos][co] * a1[pos + tap][ci]; db2 via a ones tile
 constexpr int C2_PW = 15, C2_PRS = 72, C2_ORS = 40, C2_DRS = 72;
