@@ -8,7 +8,7 @@
 // Kernel blocks (one autograd Function each, see ringdp/ops/convnet.py):
 //   F1  conv1 + ReLU + pool1                       -> a1 [B,13,13,32] bf16 + argmax|relu byte
 //   F2  conv2 + ReLU + pool2 (2x2/s1)              -> a2 [B,10,10,64] bf16 + pool2 code byte
-//   F3  conv3 + ReLU + pool3 + fc1                 -> logits [B,10] fp32 (+ a3, argmax)
+//   F3  conv3 + ReLU + pool3, then fc1 (MFMA GEMM)  -> logits [B,10] fp32 (+ a3, argmax)
 // conv2's pre-activation z2 is never materialised: F2 keeps only what F3 and the backward need
 // (a2 = relu(pool2(z2)) and, per pooled value, the first-max position or "no gradient"), and F3's
 // backward scatters d(a2) through those codes into dz2, a plain linear-layer gradient for conv2.
@@ -21,7 +21,7 @@
 //     (pool window, position-in-window), so each lane's 4 accumulator registers of a
 //     v_mfma_f32_16x16x32_bf16 tile are exactly one pool window -> bias + max + argmax + ReLU are
 //     done in registers (conv1, conv3), no LDS round trip;
-//   * fc1 is fused into the conv3 epilogue (partial logits reduced across lanes and waves);
+//   * fc1 runs as a small MFMA GEMM over a3 (cheaper than reducing 10 logits across a workgroup);
 //   * backward: dgrad is a weight-stationary full correlation over a zero-ringed LDS image; wgrad is
 //     a TN GEMM whose operands are read with ds_read_b64_tr_b16 (the transposed read also does the
 //     im2col gather), split over images into fp32 slabs reduced in a fixed order (deterministic);
@@ -50,8 +50,9 @@ constexpr int P2F_OFF = P1_OFF + P1_N, P2F_N = 4 * 9 * 512;     // conv2 fwd   (
 constexpr int P3F_OFF = P2F_OFF + P2F_N, P3F_N = 8 * 18 * 512;  // conv3 fwd   (N 128, K 576)
 constexpr int P2D_OFF = P3F_OFF + P3F_N, P2D_N = 2 * 18 * 512;  // conv2 dgrad (N 32, K 576)
 constexpr int P3D_OFF = P2D_OFF + P2D_N, P3D_N = 4 * 36 * 512;  // conv3 dgrad (N 64, K 1152)
-constexpr int PFC_OFF = P3D_OFF + P3D_N, PFC_N = 16 * 128 * 10; // fc1 [window][co][n]
-constexpr int PACK_TOTAL = PFC_OFF + PFC_N;
+constexpr int PFC_OFF = P3D_OFF + P3D_N, PFC_N = 16 * 128 * 10; // fc1 [window][co][n] (backward)
+constexpr int PFF_OFF = PFC_OFF + PFC_N, PFF_N = 64 * 64 * 8;    // fc1 fwd B fragments, k = w*128 + co
+constexpr int PACK_TOTAL = PFF_OFF + PFF_N;
 
 __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ w1,
                                                            const float* __restrict__ w2,
@@ -81,10 +82,15 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
     const int j = r & 7, lane = (r >> 3) & 63, ks = (r >> 9) % KS, nt = (r >> 9) / KS;
     const int ci = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
     v = w[((k % COUT) * CIN + ci) * 9 + (8 - k / COUT)];
-  } else {
+  } else if (e < PFF_OFF) {
     const int r = e - PFC_OFF;
     const int n = r % 10, co = (r / 10) % 128, wd = r / 1280;
     v = wfc[n * 2048 + co * 16 + wd];
+  } else {  // [ks][lane][8]: B[k = ks*32 + 8*(lane>>4) + j][n = lane & 15], k = window*128 + co
+    const int r = e - PFF_OFF;
+    const int j = r & 7, lane = (r >> 3) & 63, ks = r >> 9;
+    const int n = lane & 15, k = ks * 32 + 8 * (lane >> 4) + j;
+    v = n < 10 ? wfc[n * 2048 + (k & 127) * 16 + (k >> 7)] : 0.f;
   }
   out[e] = (bf16)v;
 }
@@ -382,17 +388,13 @@ __device__ __forceinline__ void a2_relayout(const bf16* R, bf16* X, int tid, int
     *reinterpret_cast<bf16x8*>(X + (c >> 3) * C3_XRS + (c & 7) * 8) = reinterpret_cast<const bf16x8*>(R)[c];
 }
 
-__global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __restrict__ a2,
-                                                              const bf16* __restrict__ packed,
-                                                              const float* __restrict__ bias,
-                                                              const float* __restrict__ bfc,
-                                                              float* __restrict__ logits,
-                                                              bf16* __restrict__ a3,
-                                                              uint8_t* __restrict__ idx3, int B) {
+__global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restrict__ a2,
+                                                           const bf16* __restrict__ packed,
+                                                           const float* __restrict__ bias,
+                                                           bf16* __restrict__ a3,
+                                                           uint8_t* __restrict__ idx3, int B) {
   __shared__ __attribute__((aligned(16))) bf16 R[100 * 64];
   __shared__ __attribute__((aligned(16))) bf16 X[100 * C3_XRS];
-  __shared__ __attribute__((aligned(16))) bf16 Fc[PFC_N];
-  __shared__ float red[4][10];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3F_OFF);
@@ -407,14 +409,10 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
   int base[4];
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) base[mt] = win_pos(4 * (4 * mt + (r16 >> 2)) + (r16 & 3), 10);
-  {
-    const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFC_OFF);
-    for (int c = tid; c < PFC_N / 8; c += 256) reinterpret_cast<bf16x8*>(Fc)[c] = src[c];
-  }
   int b = blockIdx.x;
   if (b < B) a2_glds(a2, b, R, wave, lane, 4);
   for (; b < B; b += gridDim.x) {
-    __syncthreads();  // R has landed; the previous image's X and red reads are done
+    __syncthreads();  // R has landed; the previous image's X reads are done
     a2_relayout(R, X, tid, 256);
     __syncthreads();  // X complete, R free
     const int nb = b + gridDim.x;
@@ -433,9 +431,6 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
         acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
       }
     }
-    float s[10];
-#pragma unroll
-    for (int n = 0; n < 10; ++n) s[n] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -446,24 +441,38 @@ __global__ __launch_bounds__(256, 2) void conv3_fc_fwd_kernel(const bf16* __rest
         const int64_t o = ((int64_t)b * 16 + wc) * 128 + co;
         a3[o] = pb;
         idx3[o] = (uint8_t)g;
-        const float pf = (float)pb;
-        const uint32_t* fw = reinterpret_cast<const uint32_t*>(Fc + (wc * 128 + co) * 10);
-#pragma unroll
-        for (int h = 0; h < 5; ++h) {
-          const uint32_t u = fw[h];
-          s[2 * h] = fmaf(pf, __uint_as_float(u << 16), s[2 * h]);
-          s[2 * h + 1] = fmaf(pf, __uint_as_float(u & 0xffff0000u), s[2 * h + 1]);
-        }
       }
+  }
+}
+
+// fc1 as its own MFMA GEMM: logits[b][n] = sum_k a3[b][k] * Wfc'[k][n] + bfc[n], k = window*128 + co.
+// One wave per 16 images; A fragments stream straight from global (16 B per lane, no LDS), the
+// 64 B-fragments (N = 10 padded to 16) sit in LDS.  Unfused from conv3 because reducing 10 logits
+// across 256 lanes per image cost the conv3 kernel more than this whole pass over a3.
+__global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ a3,
+                                                      const bf16* __restrict__ packed,
+                                                      const float* __restrict__ bfc,
+                                                      float* __restrict__ logits, int B) {
+  __shared__ __attribute__((aligned(16))) bf16x8 Wl[64 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFF_OFF);
+  for (int c = tid; c < 64 * 64; c += 256) Wl[c] = src[c];
+  __syncthreads();
+  const int b0 = (blockIdx.x * 4 + wave) * 16;
+  if (b0 >= B) return;
+  const int row = min(b0 + (lane & 15), B - 1);
+  const bf16x8* ap = reinterpret_cast<const bf16x8*>(a3 + (int64_t)row * 2048) + (lane >> 4);
+  f32x4 acc = zero_f32x4();
+#pragma unroll 16
+  for (int ks = 0; ks < 64; ++ks) acc = mfma16x16x32(ap[ks * 4], Wl[ks * 64 + lane], acc);
+  const int n = lane & 15;
+  if (n < 10) {
+    const float bn = bfc[n];
 #pragma unroll
-    for (int n = 0; n < 10; ++n) s[n] = wave_sum(s[n]);
-    if (lane == 0) {
-#pragma unroll
-      for (int n = 0; n < 10; ++n) red[wave][n] = s[n];
+    for (int i = 0; i < 4; ++i) {
+      const int bb = b0 + (lane >> 4) * 4 + i;
+      if (bb < B) logits[(int64_t)bb * 10 + n] = acc[i] + bn;
     }
-    __syncthreads();
-    if (tid < 10)
-      logits[(int64_t)b * 10 + tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) + bfc[tid];
   }
 }
 
@@ -1208,8 +1217,10 @@ void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2,
 void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s) {
   const int grid = clampi(B, 1, 2 * num_cus());
-  conv3_fc_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a2), static_cast<const bf16*>(packed), b3,
-                                           bfc, logits, static_cast<bf16*>(a3), idx3, B);
+  conv3_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a2), static_cast<const bf16*>(packed), b3,
+                                        static_cast<bf16*>(a3), idx3, B);
+  fc1_fwd_kernel<<<cdiv(B, 64), 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), bfc,
+                                             logits, B);
 }
 
 // Work split of the role-fused backward launches.  All blocks of a launch are co-resident (one
