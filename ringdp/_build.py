@@ -9,7 +9,8 @@ Everything is compiled in-tree so the built object travels with the repository s
 * link                     -> one shared object against torch's bundled HIP runtime + RCCL.
 
 Incremental: an object is rebuilt only when its source or any header under ``csrc/`` is newer.
-Usage: ``python -m ringdp._build [--force] [-j N]``.
+Usage: ``python __graft_entry__.py build`` (the package import needs the built extension, so the
+driver is loaded by file path there).
 """
 from __future__ import annotations
 

@@ -29,7 +29,7 @@ def load():
         else:
             raise ImportError(
                 "ringdp native extension (ringdp/_C*.so) is not built: run "
-                "`python -m ringdp._build` (or set RINGDP_AUTOBUILD=1)"
+                "`python __graft_entry__.py build` (or set RINGDP_AUTOBUILD=1)"
             ) from e
     return _C
 
