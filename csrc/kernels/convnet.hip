@@ -63,8 +63,9 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
   if (e >= PACK_TOTAL) return;
   float v = 0.f;
   if (e < P2F_OFF) {  // [nt][ks][lane][8]: k = ks*32 + 8*(lane>>4) + j -> kh = ks*4 + (lane>>4), kw = j
+    // n-tile nt, column c = channel 2c + nt: a lane's two accumulator tiles are a channel pair
     const int j = e & 7, lane = (e >> 3) & 63, ks = (e >> 9) & 1, nt = e >> 10;
-    const int co = nt * 16 + (lane & 15), kh = ks * 4 + (lane >> 4), kw = j;
+    const int co = 2 * (lane & 15) + nt, kh = ks * 4 + (lane >> 4), kw = j;
     v = (kh < 5 && kw < 5) ? w1[co * 25 + kh * 5 + kw] : 0.f;
   } else if (e < P2D_OFF) {  // forward fragments of conv2 / conv3: B[k = tap*CIN + ci][n = co]
     const bool l2 = e < P3F_OFF;
@@ -173,9 +174,14 @@ __device__ __forceinline__ void c1_load(const void* xin, int b, int tid, uint32_
   }
 }
 
-// Normalise this thread's 4 pixels and write them into copies 0..NC-1 (positions outside a copy
-// are never written, so the zero ring / tail established once stays zero).
-template <bool U8, int NC>
+// Normalise this thread's 4 pixels (one row segment: columns pc0 .. pc0+3, pc0 = 4*(tid%7) + 1) and
+// write them into copies 0..NC-1.  pc0 = 1 (mod 4), so each copy's alignment is known at compile time:
+// one ds_write_b64 (s = 1 mod 4), two b32 (s = 3 mod 4) or b16 + b32 + b16 - instead of 4 b16 per copy.
+// A segment starting at pc0 = 1 writes columns 1-s .. < 0 of copy s "before" its row, i.e. into columns
+// 33-s+k of the previous row: those are only ever read as filter columns kw >= 5 (zero weights in the
+// forward, zero dC rows >= 26 in wgrad), so the spill is harmless and the zero ring (copy column 29-s,
+// column 0 of copy 0, rows 0/29) is never written.
+template <bool U8, int NC, int RS = XC_W, int CS = XC_SZ>
 __device__ __forceinline__ void c1_store(bf16* xc, int tid, uint32_t u, float4 f, float mean, float inv_std,
                                          float in_scale) {
   if (tid < 196) {
@@ -189,17 +195,63 @@ __device__ __forceinline__ void c1_store(bf16* xc, int tid, uint32_t u, float4 f
       v[2] = f.z;
       v[3] = f.w;
     }
+    bf16 xv[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int p = 4 * tid + k, pr = p / 28 + 1, pc = p % 28 + 1;
-      const bf16 xv = (bf16)((v[k] - mean) * inv_std);
+    for (int k = 0; k < 4; ++k) xv[k] = (bf16)((v[k] - mean) * inv_std);
+    const uint32_t lo16 = __builtin_bit_cast(uint16_t, xv[0]), m1 = __builtin_bit_cast(uint16_t, xv[1]),
+                   m2 = __builtin_bit_cast(uint16_t, xv[2]), hi16 = __builtin_bit_cast(uint16_t, xv[3]);
+    const uint32_t p01 = lo16 | (m1 << 16), p23 = m2 | (hi16 << 16), p12 = m1 | (m2 << 16);
+    const int pr = tid / 7 + 1, pc0 = 4 * (tid % 7) + 1;
 #pragma unroll
-      for (int s = 0; s < NC; ++s)
-        if (pc >= s) xc[s * XC_SZ + pr * XC_W + pc - s] = xv;
+    for (int s = 0; s < NC; ++s) {
+      bf16* d = xc + s * CS + pr * RS + pc0 - s;  // may point before the row (see above)
+      if ((s & 3) == 1) {
+        *reinterpret_cast<uint2*>(d) = make_uint2(p01, p23);
+      } else if ((s & 3) == 3) {
+        reinterpret_cast<uint32_t*>(d)[0] = p01;
+        reinterpret_cast<uint32_t*>(d)[1] = p23;
+      } else {
+        d[0] = xv[0];
+        *reinterpret_cast<uint32_t*>(d + 1) = p12;
+        d[3] = xv[3];
+      }
     }
   }
 }
 
+// conv1 pool/ReLU codes for the backward: [B][py 13][co/2 16][px 16][co&1] bytes (px 13..15 zero), each
+// 1 << argmax (dy*2+dx) if the pooled value is > 0, else 0 (the gradient's destination, one-hot).  Window rows per channel pair let conv1 wgrad read the
+// codes of 4 neighbouring windows of one channel as one 8-byte load.
+constexpr int C1I_IMG = 13 * 512;      // 6656 bytes per image
+constexpr int C1A_IMG = 169 * 32;      // a1 elements per image
+
+// relu(max) + argmax of a 2x2 window (the 4 accumulator registers of a window-ordered m-tile, bias
+// included), as one signed-integer max over keys (bits(c_i) with the low 2 bits replaced by 3 - i): for
+// positive values the int order is the float order, ties keep the first index (torch semantics), and a
+// window whose maximum is <= 0 has no gradient, so its argmax is irrelevant.  Returns the pooled value's
+// bits (<= 2 ulp of fp32 below the exact value) and the code byte (one-hot argmax, 0 if the ReLU is off).
+__device__ __forceinline__ uint32_t pool4_key(const f32x4& c, uint32_t& code) {
+  // v_bitop3_b32 0xBA = (S0 & ~S1) | S2: one instruction per key
+  const int k0 = (int)__builtin_amdgcn_bitop3_b32(__float_as_uint(c[0]), 3u, 3u, 0xBA);
+  const int k1 = (int)__builtin_amdgcn_bitop3_b32(__float_as_uint(c[1]), 3u, 2u, 0xBA);
+  const int k2 = (int)__builtin_amdgcn_bitop3_b32(__float_as_uint(c[2]), 3u, 1u, 0xBA);
+  const int k3 = (int)(__float_as_uint(c[3]) & ~3u);
+  const int km = max(max(k0, k1), max(k2, k3));
+  code = km > 0 ? 1u << (~(uint32_t)km & 3u) : 0u;  // one-hot: bit dy*2+dx = where the gradient goes
+  return (uint32_t)max(km, 0);
+}
+
+// F1: 4 waves; per image 43 m-tiles of 16 window-ordered rows (169 windows), 2 n-tiles (channel pairs),
+// K = 2 k-steps (filter rows 0-3 | 4).  Wave w owns m-tiles w, w+4, ..: their LDS offsets are
+// computed once per workgroup and kept in registers.  Pooled outputs (one dword = 2 channels) and codes
+// (2 bytes) are collected in LDS and written with 16-B stores; the next image's pixels are loaded into
+// registers while this one computes.
+constexpr int C1F_MT = 11;  // m-tiles per wave (wave 3: 10)
+// copy stride padded 960 -> 1048 elements: the 16 A-row reads of a ds_read_b128 lane group then hit
+// 2x fewer conflicting bank slots (modelled: 11.9 -> 8.2 LDS cycles per read, ideal 4)
+constexpr int C1F_CS = 1048;
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 template <bool U8>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__ xin,
                                                         const bf16* __restrict__ packed,
@@ -207,25 +259,39 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
                                                         bf16* __restrict__ a1,
                                                         uint8_t* __restrict__ idx1, int B,
                                                         float mean, float inv_std, float in_scale) {
-  __shared__ __attribute__((aligned(16))) bf16 xs[2][8 * XC_SZ];
+  __shared__ __attribute__((aligned(16))) bf16 xs[2][8 * C1F_CS];
+  __shared__ __attribute__((aligned(16))) uint32_t ot[172 * 16];      // rows >= 169: dropped tiles
+  __shared__ __attribute__((aligned(16))) uint8_t ct[C1I_IMG + 512];  // + a dump row for them
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, gq = lane >> 4;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P1_OFF);
   bf16x8 bw[2][2];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) bw[nt][ks] = pk[(nt * 2 + ks) * 64 + lane];
-  const float bias0 = bias[lane & 15], bias1 = bias[16 + (lane & 15)];
-  const int kh0 = (lane >> 4) * XC_W;  // k-step 0: filter rows 0..3; k-step 1: row 4 (others zero weights)
-  const int kh1 = 4 * XC_W;
-  for (int i = tid; i < 2 * 8 * XC_SZ / 8; i += 256) reinterpret_cast<bf16x8*>(&xs[0][0])[i] = zero_bf16x8();
+  const float bias0 = bias[2 * r16], bias1 = bias[2 * r16 + 1];
+  const f32x4 bias0v = {bias0, bias0, bias0, bias0}, bias1v = {bias1, bias1, bias1, bias1};
+  // per m-tile: A-row offset inside a copy buffer (elements; kh row added per k-step) and code offset
+  int aoff[C1F_MT], coff[C1F_MT];
+#pragma unroll
+  for (int j = 0; j < C1F_MT; ++j) {
+    const int mt = wave + 4 * j;
+    const int w = min(4 * mt + (r16 >> 2), 168), i = r16 & 3;  // rows >= 676: clamped, dropped
+    const int oh = 2 * (w / 13) + (i >> 1), ow = 2 * (w % 13) + (i & 1);
+    aoff[j] = (ow & 7) * C1F_CS + oh * XC_W + (ow & ~7) + gq * XC_W;
+    const int wc = 4 * mt + gq;
+    coff[j] = wc < 169 ? (wc / 13) * 512 + r16 * 32 + (wc % 13) * 2 : C1I_IMG + 2 * lane;
+  }
+  for (int i = tid; i < 2 * 8 * C1F_CS / 8; i += 256) reinterpret_cast<bf16x8*>(&xs[0][0])[i] = zero_bf16x8();
+  for (int i = tid; i < C1I_IMG / 16; i += 256) reinterpret_cast<uint4*>(ct)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   uint32_t pu = 0;
   float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
   int b = blockIdx.x;
   if (b < B) {
     c1_load<U8>(xin, b, tid, pu, pf);
-    c1_store<U8, 8>(xs[0], tid, pu, pf, mean, inv_std, in_scale);
+    c1_store<U8, 8, XC_W, C1F_CS>(xs[0], tid, pu, pf, mean, inv_std, in_scale);
   }
   __syncthreads();
   int cur = 0;
@@ -233,30 +299,42 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
     const int nb = b + gridDim.x;
     if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
     const bf16* x = xs[cur];
-    for (int mt = wave; mt < 43; mt += 4) {
-      const int r16 = lane & 15;
-      const int w = min(4 * mt + (r16 >> 2), 168), i = r16 & 3;  // rows >= 676: clamped, dropped
-      const int oh = 2 * (w / 13) + (i >> 1), ow = 2 * (w % 13) + (i & 1);
-      const bf16* xr = x + (ow & 7) * XC_SZ + oh * XC_W + (ow & ~7);
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xr + kh0);
-      const bf16x8 a1v = *reinterpret_cast<const bf16x8*>(xr + kh1);
-      f32x4 c0 = mfma16x16x32(a0, bw[0][0], zero_f32x4());
-      c0 = mfma16x16x32(a1v, bw[0][1], c0);
-      f32x4 c1 = mfma16x16x32(a0, bw[1][0], zero_f32x4());
-      c1 = mfma16x16x32(a1v, bw[1][1], c1);
-      const int wc = 4 * mt + (lane >> 4);
-      if (wc < 169) {
-        int g0, g1;
-        const float v0 = pool4(c0, bias0, g0), v1 = pool4(c1, bias1, g1);
-        const int64_t o = ((int64_t)b * 169 + wc) * 32 + (lane & 15);
-        a1[o] = (bf16)v0;
-        a1[o + 16] = (bf16)v1;
-        idx1[o] = (uint8_t)(g0 | (v0 > 0.f ? 4 : 0));  // bit 2: ReLU mask for the backward
-        idx1[o + 16] = (uint8_t)(g1 | (v1 > 0.f ? 4 : 0));
+    // software-pipelined: the MFMAs of tile j are issued before the epilogue of tile j-1
+    auto epilogue = [&](int j, const f32x4& c0, const f32x4& c1) {
+      uint32_t g0, g1;
+      const uint32_t v0 = pool4_key(c0, g0), v1 = pool4_key(c1, g1);
+      const bf16x2v pv = __builtin_convertvector(f32x2v{__uint_as_float(v0), __uint_as_float(v1)}, bf16x2v);
+      ot[(4 * (wave + 4 * j) + gq) * 16 + r16] = __builtin_bit_cast(uint32_t, pv);  // v_cvt_pk_bf16_f32
+      *reinterpret_cast<uint16_t*>(ct + coff[j]) = (uint16_t)(g0 | (g1 << 8));
+    };
+    f32x4 p0 = zero_f32x4(), p1 = zero_f32x4();
+#pragma unroll
+    for (int j = 0; j < C1F_MT; ++j) {
+      f32x4 c0 = bias0v, c1 = bias1v;  // the bias rides in the accumulator (one channel per lane)
+      const bool live = j < C1F_MT - 1 || wave < 3;  // wave-uniform
+      if (live) {
+        const bf16* xr = x + aoff[j];
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xr);
+        const bf16x8 a1v = *reinterpret_cast<const bf16x8*>(xr + (4 - gq) * XC_W);  // filter row 4
+        c0 = mfma16x16x32(a0, bw[0][0], c0);
+        c1 = mfma16x16x32(a0, bw[1][0], c1);
+        c0 = mfma16x16x32(a1v, bw[0][1], c0);
+        c1 = mfma16x16x32(a1v, bw[1][1], c1);
       }
+      if (j > 0) epilogue(j - 1, p0, p1);
+      if (live && j == C1F_MT - 1) epilogue(j, c0, c1);
+      p0 = c0;
+      p1 = c1;
     }
-    if (nb < B) c1_store<U8, 8>(xs[cur ^ 1], tid, pu, pf, mean, inv_std, in_scale);
-    __syncthreads();
+    if (nb < B) c1_store<U8, 8, XC_W, C1F_CS>(xs[cur ^ 1], tid, pu, pf, mean, inv_std, in_scale);
+    __syncthreads();  // output tile complete; next image's copies written
+    const uint4* os = reinterpret_cast<const uint4*>(ot);
+    uint4* og = reinterpret_cast<uint4*>(a1 + (int64_t)b * C1A_IMG);
+    for (int c = tid; c < C1A_IMG / 8; c += 256) og[c] = os[c];
+    const uint4* cs = reinterpret_cast<const uint4*>(ct);
+    uint4* cg = reinterpret_cast<uint4*>(idx1 + (int64_t)b * C1I_IMG);
+    for (int c = tid; c < C1I_IMG / 16; c += 256) cg[c] = cs[c];
+    __syncthreads();  // output tile read out before the next image overwrites it
     cur ^= 1;
   }
 }
@@ -1012,11 +1090,21 @@ __global__ __launch_bounds__(512) void conv2_bwd_kernel(const bf16* __restrict__
 // ================================================================== F1 backward (conv1 wgrad)
 // dW1[co][t] = sum_{b, oh, ow} dC[b][oh][ow][co] * xpad[b][oh + kh][ow + kw]  as a TN GEMM with
 // K = spatial positions in rows of 32 (k = oh*32 + ow, ow >= 26 zero): the X operand for tap
-// (kh, kw) and 8 consecutive ow is one aligned ds_read_b128 of shifted copy kw; the dC operand is
-// stored [k][co] and read with ds_read_b64_tr_b16.  dC = unpool(da1) * relu-mask, both from the
-// idx1 byte.  Tap column t = 25 of the padded N is a ones column -> db1 for free.
-constexpr int C1W_K = 26 * 32;
+// (kh, kw) and 8 consecutive ow is one aligned ds_read_b128 of shifted copy kw.  dC = unpool(da1) *
+// relu-mask is never materialised: the A fragment of lane (co, 8 positions ow..ow+7 of row oh) covers 4
+// pool windows px..px+3 of window row oh/2, so it is built in registers from ONE ds_read_b64_tr_b16 of
+// the compact da1 image (4 windows x 16 channels) and ONE 8-byte read of the code rows: element
+// (window k, dx) = da1 if bit (oh&1)*2 + dx of the window's one-hot code is set, else 0.  Tap column t = 25 of the padded N is a ones
+// column -> db1 for free.  The 4 waves split K (rows oh = wave mod 4) and cover all 2x2 output tiles,
+// so every A and B fragment feeds 2 MFMAs; da1 and the codes of the next image land by LDS-DMA while
+// the current one computes.
 constexpr int C1_WSLAB = 32 * 25 + 32;
+constexpr int C1W_RS = 48, C1W_CS = 1520;          // padded copies: B-operand reads 16 -> 6 LDS cycles
+constexpr int C1W_XS = 0;                          // 5 shifted copies of the input image (bf16)
+constexpr int C1W_D = 5 * C1W_CS * 2;              // 15200: da1 image [169 (+3 zero) windows][32] bf16, x2
+constexpr int C1W_DSZ = 172 * 32 * 2;              // 11008
+constexpr int C1W_C = C1W_D + 2 * C1W_DSZ;         // 37216: code rows [13][16][16][2] bytes, x2
+constexpr int C1W_LDS = C1W_C + 2 * C1I_IMG;       // 50528 -> 3 workgroups per CU
 
 template <bool U8>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict__ xin,
@@ -1024,79 +1112,108 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict
                                                           const uint8_t* __restrict__ idx1, int B,
                                                           float mean, float inv_std, float in_scale,
                                                           float* __restrict__ slabs, int nslices) {
-  __shared__ __attribute__((aligned(16))) bf16 Dk[C1W_K * 32];
-  __shared__ __attribute__((aligned(16))) bf16 xs[5 * XC_SZ];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[C1W_LDS];  // one array: keeps the DMA in flight
+  bf16* xs = reinterpret_cast<bf16*>(lds + C1W_XS);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int mt = wave >> 1, nt = wave & 1;
-  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
-  const int t = nt * 16 + g16;
-  const bool tvalid = t < 25, tones = t == 25;
-  const int xoff = tvalid ? (t % 5) * XC_SZ + (t / 5) * XC_W + 8 * grp : 0;
-  bf16x8 onesv;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) onesv[j] = (bf16)(tones ? 1.f : 0.f);
-  f32x4 acc = zero_f32x4();
-  for (int i = tid; i < C1W_K * 32 / 8; i += 256) reinterpret_cast<bf16x8*>(Dk)[i] = zero_bf16x8();
-  for (int i = tid; i < 5 * XC_SZ / 8; i += 256) reinterpret_cast<bf16x8*>(xs)[i] = zero_bf16x8();
+  const int i16 = lane & 15, g = lane >> 4, q = i16 >> 2, p = i16 & 3;
+  // B operand (x) per n-tile: lane column t = 16 nt + i16; t = 25 is the ones column, t > 25 zero
+  const int t1 = 16 + i16;
+  const int xoff0 = (i16 % 5) * C1W_CS + (i16 / 5) * C1W_RS + 8 * g;
+  const int xoff1 = t1 < 25 ? (t1 % 5) * C1W_CS + (t1 / 5) * C1W_RS + 8 * g : 0;
+  const uint32_t b1fill = t1 == 25 ? 0x3f803f80u : 0u;  // bf16 1.0 pairs
+  for (int i = tid; i < C1W_C / 16; i += 256) reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
   const int per = cdiv(B, nslices);
-  const int b_lo = blockIdx.x * per, b_hi = min(B, b_lo + per);
-  const int c0 = (tid & 3) * 8;  // fixed channel chunk of this thread in the staging loop
-  uint32_t xu = 0;
-  float4 xf = make_float4(0.f, 0.f, 0.f, 0.f);
-  bf16x8 gv[3];
-  uint2 iv[3];
-  auto load = [&](int bb) {
-    c1_load<U8>(xin, bb, tid, xu, xf);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int it = tid + 256 * k;
-      if (it < 676) {
-        const int64_t o = ((int64_t)bb * 169 + (it >> 2)) * 32 + c0;
-        gv[k] = *reinterpret_cast<const bf16x8*>(da1 + o);
-        iv[k] = *reinterpret_cast<const uint2*>(idx1 + o);
-      }
+  const int b_lo = min(B, blockIdx.x * per), b_hi = min(B, b_lo + per);
+  auto dma = [&](int bb, int k) {
+    const bf16* src = da1 + (int64_t)bb * C1A_IMG;
+    uint8_t* dd = lds + C1W_D + k * C1W_DSZ;
+    for (int i = wave; i < 11; i += 4) {
+      const int c = i * 64 + lane;
+      if (c < C1A_IMG / 8) glds16(src + c * 8, dd + i * 1024);
+    }
+    const uint8_t* cs = idx1 + (int64_t)bb * C1I_IMG;
+    uint8_t* cd = lds + C1W_C + k * C1I_IMG;
+    for (int i = wave; i < 7; i += 4) {
+      const int c = i * 64 + lane;
+      if (c < C1I_IMG / 16) glds16(cs + c * 16, cd + i * 1024);
     }
   };
-  if (b_lo < b_hi) load(b_lo);
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) acc[m][0] = acc[m][1] = zero_f32x4();
+  uint32_t xu = 0;
+  float4 xf = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();  // zero fill done before any DMA / copy write lands
+  if (b_lo < b_hi) {
+    c1_load<U8>(xin, b_lo, tid, xu, xf);
+    dma(b_lo, 0);
+    c1_store<U8, 5, C1W_RS, C1W_CS>(xs, tid, xu, xf, mean, inv_std, in_scale);
+  }
+  int cur = 0;
   for (int b = b_lo; b < b_hi; ++b) {
-    __syncthreads();
-    c1_store<U8, 5>(xs, tid, xu, xf, mean, inv_std, in_scale);
+    __syncthreads();  // copies of image b written, its da1 / codes landed
+    if (b + 1 < b_hi) {
+      c1_load<U8>(xin, b + 1, tid, xu, xf);
+      dma(b + 1, cur ^ 1);
+    }
+    const bf16* D = reinterpret_cast<const bf16*>(lds + C1W_D + cur * C1W_DSZ);
+    const uint8_t* CB = lds + C1W_C + cur * C1I_IMG;
+    const int dy = wave & 1;  // ks = wave (mod 4): every k-step of a wave is the same window row half
+    for (int ks = wave; ks < 26; ks += 4) {
+      const int py = ks >> 1;
+      bf16x8 A[2];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int it = tid + 256 * k;
-      if (it < 676) {
-        const int w = it >> 2, py = w / 13, px = w % 13;
+      for (int m = 0; m < 2; ++m) {
+        // (bit-cast the whole vector: __builtin_bit_cast of a single vector element miscompiles to element 0)
+        const uint2 d = __builtin_bit_cast(uint2, lds_read_tr16(D + (py * 13 + 4 * g + q) * 32 + m * 16 + 4 * p));
+        const int co = m * 16 + i16;
+        const uint2 cu = *reinterpret_cast<const uint2*>(CB + py * 512 + (co >> 1) * 32 + 8 * g);
+        const int csh = 8 * (co & 1) + 2 * dy;
+        uint32_t pr[4];
 #pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          bf16x8 v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int code = byte_of(iv[k], j);
-            v[j] = (code & 4) && (code & 3) == d ? gv[k][j] : (bf16)0.f;
-          }
-          const int pos = (2 * py + (d >> 1)) * 32 + 2 * px + (d & 1);
-          *reinterpret_cast<bf16x8*>(Dk + pos * 32 + c0) = v;
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t dv = k & 1 ? (k < 2 ? d.x : d.y) >> 16 : (k < 2 ? d.x : d.y) & 0xffffu;
+          // the two one-hot bits of window row dy: 1 -> dx = 0, 2 -> dx = 1, 0 -> no gradient
+          const uint32_t sel = __builtin_amdgcn_ubfe(k < 2 ? cu.x : cu.y, 16 * (k & 1) + csh, 2);
+          pr[k] = dv * ((sel * 0x8001u) & 0x10001u);  // dv, dv << 16 or 0
         }
+        A[m] = __builtin_bit_cast(bf16x8, make_uint4(pr[0], pr[1], pr[2], pr[3]));
+      }
+      const bf16x8 B0 = *reinterpret_cast<const bf16x8*>(xs + xoff0 + ks * C1W_RS);
+      bf16x8 B1 = *reinterpret_cast<const bf16x8*>(xs + xoff1 + ks * C1W_RS);
+      if (t1 >= 25) B1 = __builtin_bit_cast(bf16x8, make_uint4(b1fill, b1fill, b1fill, b1fill));
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        acc[m][0] = mfma16x16x32(A[m], B0, acc[m][0]);
+        acc[m][1] = mfma16x16x32(A[m], B1, acc[m][1]);
       }
     }
-    if (b + 1 < b_hi) load(b + 1);
-    __syncthreads();
-#pragma unroll
-    for (int ks = 0; ks < 26; ++ks) {
-      const int kb = ks * 32 + grp * 8;
-      const bf16x4 lo = lds_read_tr16(Dk + (kb + q) * 32 + mt * 16 + 4 * p);
-      const bf16x4 hi = lds_read_tr16(Dk + (kb + 4 + q) * 32 + mt * 16 + 4 * p);
-      const bf16x8 af = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const bf16x8 bf = tvalid ? *reinterpret_cast<const bf16x8*>(xs + xoff + ks * XC_W) : onesv;
-      acc = mfma16x16x32(af, bf, acc);
+    if (b + 1 < b_hi) {
+      __syncthreads();  // every wave is done reading the copies of image b
+      c1_store<U8, 5, C1W_RS, C1W_CS>(xs, tid, xu, xf, mean, inv_std, in_scale);
     }
+    cur ^= 1;
   }
-  float* slab = slabs + (int64_t)blockIdx.x * C1_WSLAB;
+  // combine the 4 K-groups in a fixed order (deterministic) and write this workgroup's slab
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);  // [wave][tile][lane][4]: 16 KiB
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = mt * 16 + grp * 4 + i;
-    if (tvalid) slab[co * 25 + t] = acc[i];
-    if (tones) slab[800 + co] = acc[i];
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      *reinterpret_cast<f32x4*>(red + ((wave * 4 + m * 2 + n) * 64 + lane) * 4) = acc[m][n];
+  __syncthreads();
+  const int tile = tid >> 6;
+  f32x4 sum = *reinterpret_cast<const f32x4*>(red + (tile * 64 + lane) * 4);
+#pragma unroll
+  for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(red + ((w * 4 + tile) * 64 + lane) * 4);
+  float* slab = slabs + (int64_t)blockIdx.x * C1_WSLAB;
+  const int tap = (tile & 1) * 16 + i16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = (tile >> 1) * 16 + g * 4 + r;
+    if (tap < 25) slab[co * 25 + tap] = sum[r];
+    if (tap == 25) slab[800 + co] = sum[r];
   }
 }
 
@@ -1199,7 +1316,7 @@ void cn_pack_weights(const float* w1, const float* w2, const float* w3, const fl
 
 void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
                   int B, float mean, float inv_std, float in_scale, hipStream_t s) {
-  const int grid = clampi(B, 1, 4 * num_cus());
+  const int grid = clampi(B, 1, 3 * num_cus());  // 48 KiB LDS: 3 workgroups per CU
   const bf16* pk = static_cast<const bf16*>(packed);
   if (u8)
     conv1_fwd_kernel<true><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
@@ -1262,7 +1379,7 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
 }
 
-static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 2 * num_cus()); }
+static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 3 * num_cus()); }
 
 int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, FC_IMGS) * FC_SLAB; }
 int64_t cn_conv3_slab_floats(int B, bool dgrad) {

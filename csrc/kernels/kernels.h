@@ -87,7 +87,8 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
 // F2 backward: da1 may be null.
 void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1, int B, float* slabs,
                   float* dw2, float* db2, hipStream_t s);
-// F1 backward (weights only: the input needs no gradient).  idx1 bytes carry argmax | relu<<2.
+// F1 backward (weights only: the input needs no gradient).  idx1 bytes carry argmax | relu<<2, laid
+// out [B][13 py][16 co/2][16 px][co&1] (px 13..15 zero).
 void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,
                     float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s);
 
