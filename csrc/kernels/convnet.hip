@@ -919,10 +919,18 @@ __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
 // conv2's ReLU and pool2 are undone by F3's backward, so dz2 is the conv output gradient directly:
 //   dgrad: da1 = full-corr(dz2 image, flipped W2)  [13x13x32]
 //   wgrad: dW2t[n = tap*32 + ci][co] = sum_pos dz2[pos][co] * a1[pos + tap][ci]; db2 via a ones tile
-constexpr int C2_PW = 15, C2_PRS = 72, C2_ORS = 40, C2_DRS = 72;
+constexpr int C2_PW = 15, C2_PRS = 80, C2_ORS = 40, C2_DRS = 72;
+// dgrad m-tile -> output position map (255 = padding row).  Each full tile holds two positions of every
+// residue (y*15 + x) mod 8, one among lanes {0-3,12-15} and one among lanes {4-11}: with 160-B rows
+// (C2_PRS 80) the 16 rows of every ds_read_b128 lane group then land on 16 distinct 16-B bank slots
+// (modelled 11.3 -> 4.7 LDS cycles per A-fragment read, ideal 4; generator: tools/lds_bank_model.py).
+__constant__ uint8_t c2d_tile_pos[176] = {0,1,2,3,8,9,10,11,12,19,20,13,4,5,6,7,14,15,16,17,22,23,24,25,32,39,34,27,18,33,26,21,28,29,30,31,36,37,38,45,52,53,48,41,46,47,40,35,42,43,44,59,50,51,58,65,66,67,62,55,60,61,54,49,56,57,72,73,64,71,78,79,80,81,76,69,74,75,68,63,70,85,86,87,84,91,92,93,94,95,90,83,88,89,82,77,98,99,100,101,104,105,106,107,108,109,110,111,102,103,96,97,112,113,114,115,118,119,120,121,122,137,130,125,116,123,124,117,126,127,128,129,132,133,134,135,150,151,144,139,136,143,138,131,140,141,142,149,146,147,148,163,164,165,158,153,156,157,152,145,154,155,162,168,160,161,255,255,255,255,255,167,255,255,166,159};
 constexpr int C2D_P = C2_PW * C2_PW * C2_PRS * 2;  // 32400
 constexpr int C2D_O = 169 * C2_ORS * 2;            // 13520 (x2: double-buffered output tile)
-constexpr int C2W_D = 128 * C2_DRS * 2;            // 18432
+// wgrad dz2 tile: rows k in blocks of 8 (80-element rows, 704-element blocks): the 8 rows of a tr16
+// 32-lane group (k, k+1, k+2, k+3, k+8, ..) then cover the 8 32-B bank slots once (modelled 4 -> 2)
+__device__ __forceinline__ int c2_drow(int r) { return (r >> 3) * 704 + (r & 7) * 80; }
+constexpr int C2W_D = 16 * 704 * 2;                // 22528
 constexpr int C2W_X = 169 * C2_XRS * 2;            // 13520
 constexpr int C2B_LDS = (C2D_P + 2 * C2D_O) > (C2W_D + C2W_X) ? (C2D_P + 2 * C2D_O) : (C2W_D + C2W_X);
 constexpr int C2_WSLAB = 288 * 64 + 64;
@@ -938,11 +946,15 @@ __device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ dz2, const
   bf16x8 bw[18];
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) bw[ks] = pk[(nt * 18 + ks) * 64 + lane];
-  int base[3];  // rows >= 169 read a clamped (valid) address; their outputs are dropped
+  int base[3];  // padding rows read a valid address; their outputs are dropped
+  int opos[3][4];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
-    const int mm = min((mg + 4 * k) * 16 + r16, 168);
+    const int mt = min(mg + 4 * k, 10);
+    const int mm = c2d_tile_pos[mt * 16 + r16] == 255 ? 0 : c2d_tile_pos[mt * 16 + r16];
     base[k] = (mm / 13) * C2_PW + mm % 13;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) opos[k][i] = c2d_tile_pos[mt * 16 + (lane >> 4) * 4 + i];
   }
   for (int c = tid; c < C2D_P / 16; c += 512) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
   auto copy_out = [&](int bb, const bf16* src) {
@@ -972,10 +984,9 @@ __device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ dz2, const
     }
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const int mt = mg + 4 * k;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = mt * 16 + (lane >> 4) * 4 + i;
+        const int m = opos[k][i];
         if (m < 169) Oc[m * C2_ORS + nt * 16 + r16] = (bf16)acc[k][i];
       }
     }
@@ -1037,7 +1048,7 @@ __device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const 
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int c = tid + 512 * k;
-      if (c < 968) *reinterpret_cast<bf16x8*>(D + (c >> 3) * C2_DRS + (c & 7) * 8) = pz[k];
+      if (c < 968) *reinterpret_cast<bf16x8*>(D + c2_drow(c >> 3) + (c & 7) * 8) = pz[k];
       if (c < 676) *reinterpret_cast<bf16x8*>(X + (c >> 2) * C2_XRS + (c & 3) * 8) = pa[k];
     }
     if (b + 1 < b_hi) load(b + 1);
@@ -1046,8 +1057,8 @@ __device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const 
     for (int ks = 0; ks < 4; ++ks) {
       const int kb = ks * 32 + grp * 8;
       const int m0 = wm * 16;
-      const bf16x4 alo = lds_read_tr16(D + (kb + q) * C2_DRS + m0 + 4 * p);
-      const bf16x4 ahi = lds_read_tr16(D + (kb + 4 + q) * C2_DRS + m0 + 4 * p);
+      const bf16x4 alo = lds_read_tr16(D + c2_drow(kb + q) + m0 + 4 * p);
+      const bf16x4 ahi = lds_read_tr16(D + c2_drow(kb + 4 + q) + m0 + 4 * p);
       const bf16x8 af = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
       const int k0 = min(kb + q, 120), k1 = min(kb + 4 + q, 120);  // rows >= 121 of D are zero
       const int x0 = (k0 / 11) * 13 + k0 % 11, x1 = (k1 / 11) * 13 + k1 % 11;
@@ -1373,7 +1384,7 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
     ws = clampi(cdiv(B, 8), 1, cus);
     return;
   }
-  static const double frac = split_frac("RINGDP_C2_DGRAD_FRAC", 0.62);
+  static const double frac = split_frac("RINGDP_C2_DGRAD_FRAC", 0.55);
   nd = clampi(B, 1, (int)(frac * cus));
   const int per = cdiv(B, nd);
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
