@@ -341,7 +341,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
 
 // ================================================================== F2: conv2 + ReLU + pool2
 // 256 threads; wave (wm, wn) owns n-tiles {2wn, 2wn+1} x m-tiles {4wm..4wm+3} (121 rows -> 128).
-constexpr int C2_XRS = 40;  // bf16 per LDS row of the a1 image (32 + 8 pad)
+constexpr int C2_XRS = 48;  // bf16 per LDS row of the a1 image (32 + 16 pad): 96-B rows, see c2f_tile_pos
+// forward m-tile -> output position map (255 = padding row): every full tile holds two positions of
+// each residue (y*13 + x) mod 8, one among lanes {0-3,12-15} and one among {4-11}, so with 96-B rows
+// the 16 rows of a ds_read_b128 lane group land on 16 distinct 16-B bank slots (modelled 10.5 -> 4
+// LDS cycles per operand read; generator: tools/lds_bank_model.py)
+__constant__ uint8_t c2f_tile_pos[128] = {0,3,6,1,8,17,12,9,18,13,10,11,4,7,2,5,14,23,20,15,28,31,26,29,32,27,22,25,24,21,16,19,34,37,40,35,42,51,46,43,44,41,36,45,38,33,30,39,48,57,54,49,62,65,60,55,58,61,56,59,52,47,50,53,68,71,66,63,76,77,74,69,78,75,70,79,72,67,64,73,82,85,80,83,88,91,94,89,92,95,90,93,86,81,84,87,96,105,100,97,102,111,108,103,112,109,104,107,106,101,98,99,116,119,114,117,255,255,255,255,255,255,118,255,120,115,110,113};
 constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 + 8)
 
 __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restrict__ a1,
@@ -368,10 +373,11 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) bv[t][i] = bias[(2 * wn + t) * 16 + c4 + i];
-  int base[4];  // rows >= 121 read a clamped (valid) address; their outputs are dropped
+  int base[4], opos[4];  // padding rows read a valid address; their outputs are dropped
 #pragma unroll
   for (int mt = 0; mt < 4; ++mt) {
-    const int mm = min((4 * wm + mt) * 16 + r16, 120);
+    opos[mt] = c2f_tile_pos[(4 * wm + mt) * 16 + r16];
+    const int mm = opos[mt] == 255 ? 0 : opos[mt];
     base[mt] = (mm / 11) * 13 + mm % 11;
   }
   bf16x8 pre[3];
@@ -417,7 +423,7 @@ __global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restric
     __syncthreads();  // previous image's pooling reads of Cs are complete
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      const int m = (4 * wm + mt) * 16 + r16;
+      const int m = opos[mt];
       if (m < 121) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
