@@ -19,16 +19,33 @@ namespace {
 
 constexpr float kE4M3Max = 448.f;
 
+// One atomic per workgroup (not per wave) and at most 2 workgroups per CU: thousands of atomics on one
+// address serialise in the L2 atomic unit (measured 82 us per call at 8192 wave-atomics).  Two
+// 16-B loads in flight per thread.
 __global__ __launch_bounds__(256) void amax_kernel(const bf16* __restrict__ x, int64_t nvec,
                                                    unsigned* __restrict__ out) {
-  float m = 0.f;
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
-    const bf16x8 t = reinterpret_cast<const bf16x8*>(x)[v];
+  __shared__ float red[4];
+  float m0 = 0.f, m1 = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {
+    const bf16x8 t0 = reinterpret_cast<const bf16x8*>(x)[v];
+    const bf16x8 t1 = reinterpret_cast<const bf16x8*>(x)[v + stride];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf((float)t[j]));
+    for (int j = 0; j < 8; ++j) {
+      m0 = fmaxf(m0, fabsf((float)t0[j]));
+      m1 = fmaxf(m1, fabsf((float)t1[j]));
+    }
   }
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+  if (v < nvec) {
+    const bf16x8 t0 = reinterpret_cast<const bf16x8*>(x)[v];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m0 = fmaxf(m0, fabsf((float)t0[j]));
+  }
+  float m = wave_max(fmaxf(m0, m1));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 __device__ __forceinline__ float qscale(const float* amax) { return fmaxf(amax[0], 1e-12f) / kE4M3Max; }
@@ -97,7 +114,7 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
 void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s) {
   hipMemsetAsync(amax, 0, sizeof(float), s);
   const int64_t nvec = n / 8;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nvec + 255) / 256, 2048));
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((nvec + 255) / 256, 512));
   amax_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), nvec, reinterpret_cast<unsigned*>(amax));
 }
 

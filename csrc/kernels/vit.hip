@@ -251,6 +251,40 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* __restric
   for (int c = lane; c < Tp; c += 64) pr[c] = (bf16)(c < T ? __expf(sr[c] * scale - mx) * inv : 0.f);
 }
 
+// Register-resident variant for Tp <= 256 (ViT-B/16: Tp = 208): lane l owns columns 4l..4l+3, loaded once
+// as a float4 and written once as 4 bf16 (the scalar kernel above streams each row 3 times).
+__global__ __launch_bounds__(256) void softmax_fwd_vec_kernel(const float* __restrict__ s, int64_t rows, int T,
+                                                              int Tp, float scale, bf16* __restrict__ p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int c0 = 4 * lane;
+  const bool live = c0 < Tp;
+  uint2* out = reinterpret_cast<uint2*>(p + row * Tp + c0);
+  if ((int)(row % Tp) >= T) {  // padded query row
+    if (live) *out = make_uint2(0u, 0u);
+    return;
+  }
+  float4 v = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+  if (live) v = *reinterpret_cast<const float4*>(s + row * Tp + c0);
+  float x[4] = {v.x * scale, v.y * scale, v.z * scale, v.w * scale};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (c0 + j >= T) x[j] = -INFINITY;
+  const float mx = wave_max(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+  float e[4], sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    e[j] = c0 + j < T ? __expf(x[j] - mx) : 0.f;
+    sum += e[j];
+  }
+  const float inv = 1.f / wave_sum(sum);
+  if (live) {
+    const bf16x4 o = bf16x4{(bf16)(e[0] * inv), (bf16)(e[1] * inv), (bf16)(e[2] * inv), (bf16)(e[3] * inv)};
+    *out = __builtin_bit_cast(uint2, o);
+  }
+}
+
 // ds = scale * p * (dp - sum_j dp_j p_j)  (bf16 out; padded keys / queries -> 0)
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16* __restrict__ p, const float* __restrict__ dp,
                                                           int64_t rows, int T, int Tp, float scale,
@@ -265,6 +299,41 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const bf16* __restrict
   for (int c = lane; c < T; c += 64) dot += (float)pr[c] * dr[c];
   dot = wave_sum(dot);
   for (int c = lane; c < Tp; c += 64) o[c] = (bf16)(c < T ? scale * (float)pr[c] * (dr[c] - dot) : 0.f);
+}
+
+__global__ __launch_bounds__(256) void softmax_bwd_vec_kernel(const bf16* __restrict__ p,
+                                                              const float* __restrict__ dp, int64_t rows, int T,
+                                                              int Tp, float scale, bf16* __restrict__ ds) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int c0 = 4 * lane;
+  const bool live = c0 < Tp;
+  float pv[4] = {0.f, 0.f, 0.f, 0.f}, dv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
+    const bf16x4 pb = __builtin_bit_cast(bf16x4, *reinterpret_cast<const uint2*>(p + row * Tp + c0));
+    const float4 d = *reinterpret_cast<const float4*>(dp + row * Tp + c0);
+    pv[0] = (float)pb[0];
+    pv[1] = (float)pb[1];
+    pv[2] = (float)pb[2];
+    pv[3] = (float)pb[3];
+    dv[0] = d.x;
+    dv[1] = d.y;
+    dv[2] = d.z;
+    dv[3] = d.w;
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (c0 + j < T) dot += pv[j] * dv[j];
+  dot = wave_sum(dot);
+  if (live) {
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = c0 + j < T ? scale * pv[j] * (dv[j] - dot) : 0.f;
+    *reinterpret_cast<uint2*>(ds + row * Tp + c0) =
+        __builtin_bit_cast(uint2, bf16x4{(bf16)o[0], (bf16)o[1], (bf16)o[2], (bf16)o[3]});
+  }
 }
 
 // ---------------------------------------------------------------- misc
@@ -426,11 +495,18 @@ void rows_to_heads(const void* rows, int B, int T, int H, int Dh, int Tp, void* 
 }
 
 void softmax_fwd(const float* scores, int64_t rows, int T, int Tp, float scale, void* p, hipStream_t s) {
-  softmax_fwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(scores, rows, T, Tp, scale, static_cast<bf16*>(p));
+  if (Tp <= 256 && Tp % 4 == 0)
+    softmax_fwd_vec_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(scores, rows, T, Tp, scale, static_cast<bf16*>(p));
+  else
+    softmax_fwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(scores, rows, T, Tp, scale, static_cast<bf16*>(p));
 }
 
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s) {
-  softmax_bwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(static_cast<const bf16*>(p), dp, rows, T, Tp, scale,
+  if (Tp <= 256 && Tp % 4 == 0)
+    softmax_bwd_vec_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(static_cast<const bf16*>(p), dp, rows, T, Tp, scale,
+                                                             static_cast<bf16*>(ds));
+  else
+    softmax_bwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(static_cast<const bf16*>(p), dp, rows, T, Tp, scale,
                                                            static_cast<bf16*>(ds));
 }
 

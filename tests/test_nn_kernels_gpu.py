@@ -278,17 +278,17 @@ def test_layernorm_softmax_kernels():
     dw, db = torch.empty_like(w), torch.empty_like(b)
     dx = C().layernorm_bwd(dy, x, stats, w, None, dw, db)
     assert rel(dx, xr.grad) < 2e-2 and rel(dw, wr.grad) < 1e-2 and rel(db, br.grad) < 1e-2
-    T, Tp = 197, 208
-    s = torch.randn(6, Tp, Tp, device="cuda")
-    p = C().softmax_fwd(s, T, 0.125)
-    sr = s[:, :T, :T].clone().requires_grad_()
-    pr = torch.softmax(sr * 0.125, -1)
-    assert rel(p[:, :T, :T], pr) < 1e-2
-    assert float(p[:, T:, :].abs().max()) == 0 and float(p[:, :, T:].abs().max()) == 0
-    dp = torch.randn(6, Tp, Tp, device="cuda")
-    pr.backward(dp[:, :T, :T])
-    ds = C().softmax_bwd(p, dp, T, 0.125)
-    assert rel(ds[:, :T, :T], sr.grad) < 2e-2
+    for T, Tp in ((197, 208), (300, 304)):  # register-resident (Tp <= 256) and streaming kernels
+        s = torch.randn(6, Tp, Tp, device="cuda")
+        p = C().softmax_fwd(s, T, 0.125)
+        sr = s[:, :T, :T].clone().requires_grad_()
+        pr = torch.softmax(sr * 0.125, -1)
+        assert rel(p[:, :T, :T], pr) < 1e-2
+        assert float(p[:, T:, :].abs().max()) == 0 and float(p[:, :, T:].abs().max()) == 0
+        dp = torch.randn(6, Tp, Tp, device="cuda")
+        pr.backward(dp[:, :T, :T])
+        ds = C().softmax_bwd(p, dp, T, 0.125)
+        assert rel(ds[:, :T, :T], sr.grad) < 2e-2
 
 
 def test_vit_matches_aten():
