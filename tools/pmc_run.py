@@ -43,6 +43,8 @@ def main():
         "conv2_fwd": lambda: C.cn_conv2_fwd(a1, pk, b2),
         "conv3_fc_fwd": lambda: C.cn_conv3_fc_fwd(a2, pk, b3, bfc),
         "conv3_fc_bwd": lambda: C.cn_conv3_fc_bwd(a2, i2, a3, i3, wf, dl, pk, True, *g3),
+        "conv3_fc_bwd_w": lambda: C.cn_conv3_fc_bwd(a2, i2, a3, i3, wf, dl, pk, False, *g3),
+        "conv2_bwd_w": lambda: C.cn_conv2_bwd(a1, dz2, pk, False, *g2),
         "conv2_bwd": lambda: C.cn_conv2_bwd(a1, dz2, pk, True, *g2),
         "conv1_wgrad": lambda: C.cn_conv1_wgrad(x, da1, i1, *g1, *norm),
     }
