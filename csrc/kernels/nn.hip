@@ -99,6 +99,102 @@ __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict_
   }
 }
 
+// Column-stationary variants (C/8 divides 256: every ResNet width 64..2048): thread t owns the 8-channel
+// column t % (C/8) for its whole life, so the per-channel coefficients are loaded once into registers
+// (the grid-stride kernels above recompute a 64-bit modulo and reload 16-24 scalars per vector), and
+// each thread keeps 4 rows of 16-B loads in flight.
+constexpr int kBnUnroll = 4;
+
+__device__ __forceinline__ void load8(const float* p, float (&o)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+
+template <bool kRes, bool kRelu>
+__global__ __launch_bounds__(256) void bn_act_fwd_col_kernel(const bf16* __restrict__ z, const float* __restrict__ ss,
+                                                             const bf16* __restrict__ res, int64_t M, int C,
+                                                             bf16* __restrict__ y) {
+  const int cv = C >> 3, rpb = 256 / cv;
+  const int col = threadIdx.x % cv, rsub = threadIdx.x / cv;
+  float sc[8], sh[8];
+  load8(ss + col * 8, sc);
+  load8(ss + C + col * 8, sh);
+  const int64_t rstride = (int64_t)gridDim.x * rpb;
+  for (int64_t r = (int64_t)blockIdx.x * rpb + rsub; r < M; r += kBnUnroll * rstride) {
+    bf16x8 zv[kBnUnroll], rv[kBnUnroll];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      const int64_t rr = r + u * rstride;
+      if (rr < M) {
+        zv[u] = reinterpret_cast<const bf16x8*>(z)[rr * cv + col];
+        if (kRes) rv[u] = reinterpret_cast<const bf16x8*>(res)[rr * cv + col];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      const int64_t rr = r + u * rstride;
+      if (rr < M) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float f = fmaf((float)zv[u][j], sc[j], sh[j]);
+          if (kRes) f += (float)rv[u][j];
+          if (kRelu) f = fmaxf(f, 0.f);
+          o[j] = (bf16)f;
+        }
+        reinterpret_cast<bf16x8*>(y)[rr * cv + col] = o;
+      }
+    }
+  }
+}
+
+// dz = A*g + Bz*z + Cc per channel (A = gamma*invstd, Bz = -A*invstd*dgamma/M,
+// Cc = -A*dbeta/M - Bz*mean): the coefficients are formed once per thread in registers.
+__global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
+                                                               const float* __restrict__ save,
+                                                               const float* __restrict__ gamma,
+                                                               const float* __restrict__ dgamma,
+                                                               const float* __restrict__ dbeta, int64_t M, int C,
+                                                               bf16* __restrict__ dz) {
+  const int cv = C >> 3, rpb = 256 / cv;
+  const int col = threadIdx.x % cv, rsub = threadIdx.x / cv;
+  const float invM = 1.f / (float)M;
+  float mean[8], inv[8], ga[8], dg[8], db[8], A[8], Bz[8], Cc[8];
+  load8(save + col * 8, mean);
+  load8(save + C + col * 8, inv);
+  load8(gamma + col * 8, ga);
+  load8(dgamma + col * 8, dg);
+  load8(dbeta + col * 8, db);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A[j] = ga[j] * inv[j];
+    Bz[j] = -A[j] * inv[j] * dg[j] * invM;
+    Cc[j] = -A[j] * db[j] * invM - Bz[j] * mean[j];
+  }
+  const int64_t rstride = (int64_t)gridDim.x * rpb;
+  for (int64_t r = (int64_t)blockIdx.x * rpb + rsub; r < M; r += kBnUnroll * rstride) {
+    bf16x8 gv[kBnUnroll], zv[kBnUnroll];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      const int64_t rr = r + u * rstride;
+      if (rr < M) {
+        gv[u] = reinterpret_cast<const bf16x8*>(g)[rr * cv + col];
+        zv[u] = reinterpret_cast<const bf16x8*>(z)[rr * cv + col];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      const int64_t rr = r + u * rstride;
+      if (rr < M) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (bf16)fmaf(A[j], (float)gv[u][j], fmaf(Bz[j], (float)zv[u][j], Cc[j]));
+        reinterpret_cast<bf16x8*>(dz)[rr * cv + col] = o;
+      }
+    }
+  }
+}
+
 // Rows are split over workgroups; each thread owns one 8-channel vector column (C/8 columns, C <= 2048)
 // and walks rows with a stride, accumulating in fp32; partials [part][2][C] (deterministic).
 inline int64_t bn_rows_per_part(int64_t M) { return std::max<int64_t>(64, (M + 1023) / 1024); }
@@ -124,22 +220,35 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
       mean[j] = save[col * 8 + j];
       inv[j] = save[C + col * 8 + j];
     }
-    for (int64_t r = r0 + rsub; r < r1; r += rows_in_flight) {
-      const int64_t v = r * cv + col;
-      const bf16x8 d = reinterpret_cast<const bf16x8*>(dy)[v];
-      const bf16x8 zz = reinterpret_cast<const bf16x8*>(z)[v];
-      bf16x8 yy = zero_bf16x8();
-      if (relu) yy = reinterpret_cast<const bf16x8*>(y)[v];
-      bf16x8 go;
+    // kBnUnroll rows per step: 12 16-B loads in flight per thread (rows accumulate in a fixed order)
+    for (int64_t r = r0 + rsub; r < r1; r += kBnUnroll * rows_in_flight) {
+      bf16x8 d[kBnUnroll], zz[kBnUnroll], yy[kBnUnroll];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float g = (relu && !((float)yy[j] > 0.f)) ? 0.f : (float)d[j];
-        go[j] = (bf16)g;
-        const float gq = (float)go[j];
-        sg[j] += gq;
-        sgz[j] += gq * ((float)zz[j] - mean[j]) * inv[j];
+      for (int u = 0; u < kBnUnroll; ++u) {
+        const int64_t rr = r + u * rows_in_flight;
+        if (rr < r1) {
+          const int64_t v = rr * cv + col;
+          d[u] = reinterpret_cast<const bf16x8*>(dy)[v];
+          zz[u] = reinterpret_cast<const bf16x8*>(z)[v];
+          yy[u] = relu ? reinterpret_cast<const bf16x8*>(y)[v] : zero_bf16x8();
+        }
       }
-      reinterpret_cast<bf16x8*>(g_out)[v] = go;
+#pragma unroll
+      for (int u = 0; u < kBnUnroll; ++u) {
+        const int64_t rr = r + u * rows_in_flight;
+        if (rr < r1) {
+          bf16x8 go;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float g = (relu && !((float)yy[u][j] > 0.f)) ? 0.f : (float)d[u][j];
+            go[j] = (bf16)g;
+            const float gq = (float)go[j];
+            sg[j] += gq;
+            sgz[j] += gq * ((float)zz[u][j] - mean[j]) * inv[j];
+          }
+          reinterpret_cast<bf16x8*>(g_out)[rr * cv + col] = go;
+        }
+      }
     }
   }
   // combine the rows_in_flight partial rows for each column (fixed order)
@@ -332,6 +441,18 @@ void bn_prepare(const float* sums, int64_t M, int C, const float* gamma, const f
 void bn_act_fwd(const void* z, const float* ss, const void* res, bool relu, int64_t M, int C, void* y,
                 hipStream_t s) {
   const int64_t nvec = M * C / 8;
+  if (C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0) {
+    const int rpb = 256 / (C / 8);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((M + rpb * kBnUnroll - 1) / (rpb * kBnUnroll), 2048));
+    const bf16* zb = static_cast<const bf16*>(z);
+    const bf16* rb = static_cast<const bf16*>(res);
+    bf16* yb = static_cast<bf16*>(y);
+    if (res && relu) bn_act_fwd_col_kernel<true, true><<<grid, 256, 0, s>>>(zb, ss, rb, M, C, yb);
+    else if (res) bn_act_fwd_col_kernel<true, false><<<grid, 256, 0, s>>>(zb, ss, rb, M, C, yb);
+    else if (relu) bn_act_fwd_col_kernel<false, true><<<grid, 256, 0, s>>>(zb, ss, rb, M, C, yb);
+    else bn_act_fwd_col_kernel<false, false><<<grid, 256, 0, s>>>(zb, ss, rb, M, C, yb);
+    return;
+  }
   bn_act_fwd_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(z), ss, static_cast<const bf16*>(res),
                                                    relu ? 1 : 0, nvec, C, static_cast<bf16*>(y));
 }
@@ -352,6 +473,13 @@ void bn_bwd_apply(const float* part, int nparts, float* scratch, const void* g, 
                   const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s) {
   reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);  // part[p][0] = sum g, part[p][1] = sum g*zhat
   const int64_t nvec = M * C / 8;
+  if (C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0) {
+    const int rpb = 256 / (C / 8);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((M + rpb * kBnUnroll - 1) / (rpb * kBnUnroll), 2048));
+    bn_bwd_apply_col_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save, gamma,
+                                                 dgamma, dbeta, M, C, static_cast<bf16*>(dz));
+    return;
+  }
   bn_bwd_apply_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save,
                                                      gamma, dgamma, dbeta, M, C, nvec, static_cast<bf16*>(dz));
 }
