@@ -157,6 +157,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// The same copy issued from inline asm.  With the builtin, the compiler sees an LDS write on the VM counter
+// and drains it (s_waitcnt vmcnt(0)) before the next LDS read, however unrelated - the prefetch then never
+// overlaps the compute it was issued ahead of (seen in the ISA of conv1_wgrad / conv3_fwd).  Here the copy
+// is invisible to the compiler: the consumer must `s_waitcnt vmcnt(0)` itself before the barrier that
+// publishes the buffer (c_dma_wait).  M0 is set inside the asm; no kernel using this sets M0 otherwise
+// (the ISA of these kernels has no other M0 writer: checked when this was introduced).
+__device__ __forceinline__ void glds16_async(const void* gsrc, void* lds_wave_base) {
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)((__attribute__((address_space(3))) char*)(lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
+}
+__device__ __forceinline__ void c_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // ================================================================== F1: conv1 (MFMA)
 // The zero-ringed 30x30 input is staged as 8 copies shifted by s = 0..7 columns (rows of 32):
 // copy s holds xpad[r][c + s].  Eight consecutive pixels xpad[r][ow .. ow+7] are then ONE aligned
@@ -461,7 +474,7 @@ __device__ __forceinline__ void a2_glds(const bf16* __restrict__ a2, int b, bf16
   const bf16* src = a2 + (int64_t)b * 6400;
   for (int k = wave; k < 13; k += nwaves) {
     const int slot = k * 64 + lane;
-    if (slot < 800) glds16(src + slot * 8, R + k * 512);
+    if (slot < 800) glds16_async(src + slot * 8, R + k * 512);
   }
 }
 
@@ -496,6 +509,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
   int b = blockIdx.x;
   if (b < B) a2_glds(a2, b, R, wave, lane, 4);
   for (; b < B; b += gridDim.x) {
+    c_dma_wait();
     __syncthreads();  // R has landed; the previous image's X reads are done
     a2_relayout(R, X, tid, 256);
     __syncthreads();  // X complete, R free
@@ -708,7 +722,7 @@ __device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int
   const uint8_t* src = idx2 + (int64_t)b * 6400;
   for (int k = wave; k < 7; k += 4) {
     const int slot = k * 64 + lane;
-    if (slot < 400) glds16(src + slot * 16, AM + k * 1024);
+    if (slot < 400) glds16_async(src + slot * 16, AM + k * 1024);
   }
 }
 
@@ -785,6 +799,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
     codes_glds(idx2, b, AMb, wave, lane);
   }
   for (; b < B; b += nblocks, cur ^= 1) {
+    c_dma_wait();
     __syncthreads();  // previous image fully consumed (P, DA); this image's codes have landed
     c3_expand(pre, tid, [&](int r) { return P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS; });
     const int nb = b + nblocks;
@@ -853,6 +868,7 @@ __device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const 
     a2_glds(a2, b_lo, R, wave, lane, 4);
   }
   for (int b = b_lo; b < b_hi; ++b) {
+    c_dma_wait();
     __syncthreads();  // R has landed; the previous image's D / X reads are done
     c3_expand(pre, tid, [&](int r) { return D + r * C3_DRS; });
     a2_relayout(R, X, tid, 256);
@@ -1146,13 +1162,13 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict
     uint8_t* dd = lds + C1W_D + k * C1W_DSZ;
     for (int i = wave; i < 11; i += 4) {
       const int c = i * 64 + lane;
-      if (c < C1A_IMG / 8) glds16(src + c * 8, dd + i * 1024);
+      if (c < C1A_IMG / 8) glds16_async(src + c * 8, dd + i * 1024);
     }
     const uint8_t* cs = idx1 + (int64_t)bb * C1I_IMG;
     uint8_t* cd = lds + C1W_C + k * C1I_IMG;
     for (int i = wave; i < 7; i += 4) {
       const int c = i * 64 + lane;
-      if (c < C1I_IMG / 16) glds16(cs + c * 16, cd + i * 1024);
+      if (c < C1I_IMG / 16) glds16_async(cs + c * 16, cd + i * 1024);
     }
   };
   f32x4 acc[2][2];
@@ -1168,6 +1184,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict
   }
   int cur = 0;
   for (int b = b_lo; b < b_hi; ++b) {
+    c_dma_wait();
     __syncthreads();  // copies of image b written, its da1 / codes landed
     if (b + 1 < b_hi) {
       c1_load<U8>(xin, b + 1, tid, xu, xf);
