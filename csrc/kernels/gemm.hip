@@ -31,10 +31,24 @@ using namespace ringdp::dev;
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int KPAD = BK + 8;         // K-contiguous stage row (bf16)
-constexpr int RPAD = 128 + 8;        // row-contiguous stage row (bf16)
-constexpr int STAGE_ELEMS = 128 * KPAD;  // >= BK * RPAD: both orientations fit
-static_assert(STAGE_ELEMS >= BK * RPAD, "stage size");
+// Stage images are unpadded and XOR-swizzled (modelled with tools/lds_bank_model.py; the previous
+// 8-element row padding cost 2x on both fragment reads and needed 9 KiB more LDS; measured +3-5 %):
+//  * K-contiguous [128 rows][64 k]: 16-B chunk c of row r lives at chunk c ^ (r & 7), so the 16 rows of a
+//    ds_read_b128 lane group cover 16 distinct bank slots (8 -> 4 LDS cycles per read);
+//  * row-contiguous [64 k][128 rows]: 32-B slot s of k-row R lives at slot s ^ f(R), f(R) = (R & 3) |
+//    ((R >> 1) & 4), so the 8 k-rows of a ds_read_b64_tr_b16 32-lane half (R..R+3, R+8..R+11) cover the
+//    8 slots of a 256-B bank row once (4 -> 2 cycles).
+// (A 2-tile-deep register prefetch was tried on top: +32 VGPRs, no measurable gain - the loop is not
+// waiting on global latency at 2 workgroups per CU.)
+constexpr int KROW = BK;     // K-contiguous stage row (bf16)
+constexpr int RROW = 128;    // row-contiguous stage row (bf16)
+constexpr int STAGE_ELEMS = 128 * KROW;
+static_assert(STAGE_ELEMS == BK * RROW, "stage size");
+__device__ __forceinline__ int ksw(int r, int chunk) { return r * KROW + 8 * (chunk ^ (r & 7)); }
+__device__ __forceinline__ int rsw(int kr, int col) {  // col: element column (multiple of 4)
+  const int f = (kr & 3) | ((kr >> 1) & 4);
+  return kr * RROW + (((col >> 4) ^ f) << 4) + (col & 15);
+}
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
@@ -172,9 +186,9 @@ struct Stager {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       if (L::kRow)
-        *reinterpret_cast<bf16x8*>(s + ((tid >> 4) + 16 * i) * RPAD + 8 * (tid & 15)) = v[i];
+        *reinterpret_cast<bf16x8*>(s + rsw((tid >> 4) + 16 * i, 8 * (tid & 15))) = v[i];
       else
-        *reinterpret_cast<bf16x8*>(s + ((tid >> 3) + 32 * i) * KPAD + 8 * (tid & 7)) = v[i];
+        *reinterpret_cast<bf16x8*>(s + ksw((tid >> 3) + 32 * i, tid & 7)) = v[i];
     }
   }
 };
@@ -182,10 +196,10 @@ struct Stager {
 // MFMA operand fragment for rows r0..r0+15 at k-step kk (32-wide) from a staged tile.
 template <bool kRow>
 __device__ __forceinline__ bf16x8 frag(const bf16* s, int r0, int kk, int lane) {
-  if (!kRow) return *reinterpret_cast<const bf16x8*>(s + (r0 + (lane & 15)) * KPAD + kk * 32 + 8 * (lane >> 4));
+  if (!kRow) return *reinterpret_cast<const bf16x8*>(s + ksw(r0 + (lane & 15), kk * 4 + (lane >> 4)));
   const int q = (lane & 15) >> 2, p = lane & 3, kb = kk * 32 + 8 * (lane >> 4);
-  const bf16x4 lo = lds_read_tr16(s + (kb + q) * RPAD + r0 + 4 * p);
-  const bf16x4 hi = lds_read_tr16(s + (kb + 4 + q) * RPAD + r0 + 4 * p);
+  const bf16x4 lo = lds_read_tr16(s + rsw(kb + q, r0 + 4 * p));
+  const bf16x4 hi = lds_read_tr16(s + rsw(kb + 4 + q, r0 + 4 * p));
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
@@ -196,9 +210,9 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 // k = 32*(l>>4) + j (j < 32) = 32 bytes = two 16-B reads of a K-contiguous stage.  In the stage,
 // one bf16 "slot" is 2 fp8 bytes, so a 64-slot stage row is 128 fp8 values = one MFMA k-step.
 __device__ __forceinline__ i32x8 frag_fp8(const bf16* s, int r0, int lane) {
-  const bf16* p = s + (r0 + (lane & 15)) * KPAD + 16 * (lane >> 4);
-  const bf16x8 lo = *reinterpret_cast<const bf16x8*>(p);
-  const bf16x8 hi = *reinterpret_cast<const bf16x8*>(p + 8);
+  const int row = r0 + (lane & 15);
+  const bf16x8 lo = *reinterpret_cast<const bf16x8*>(s + ksw(row, 2 * (lane >> 4)));
+  const bf16x8 hi = *reinterpret_cast<const bf16x8*>(s + ksw(row, 2 * (lane >> 4) + 1));
   i32x8 r;
   const int* a = reinterpret_cast<const int*>(&lo);
   const int* b = reinterpret_cast<const int*>(&hi);
