@@ -1269,10 +1269,12 @@ struct ReduceSegs {
   int count;
 };
 
-// Each workgroup owns 64 outputs of one segment and sums its slices with 4 waves (lane = output,
-// coalesced rows) combined in a fixed order.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(ReduceSegs segs) {
-  __shared__ float part[4][64];
+// Each workgroup owns 64 outputs of one segment and sums its slices with 16 waves (lane = output,
+// coalesced rows), combined in a fixed order.  16 (not 4) waves: the conv1 / fc1 segments have few
+// outputs (13-20 workgroups) and hundreds of slices, so the per-wave slice chains were the whole cost.
+constexpr int kRedWaves = 16;
+__global__ __launch_bounds__(1024) void slab_reduce_kernel(ReduceSegs segs) {
+  __shared__ float part[kRedWaves][64];
   int blk = blockIdx.x, sidx = 0;
   while (sidx < segs.count - 1 && blk >= segs.seg[sidx].blocks) {
     blk -= segs.seg[sidx].blocks;
@@ -1285,18 +1287,20 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(ReduceSegs segs) {
   if (i < sg.n) {
     const float* pp = sg.slabs + sg.off + i;
     int s = wave;
-    for (; s + 12 < sg.nslices; s += 16) {
+    for (; s + 3 * kRedWaves < sg.nslices; s += 4 * kRedWaves) {
       a0 += pp[(int64_t)s * sg.stride];
-      a1 += pp[(int64_t)(s + 4) * sg.stride];
-      a2 += pp[(int64_t)(s + 8) * sg.stride];
-      a3 += pp[(int64_t)(s + 12) * sg.stride];
+      a1 += pp[(int64_t)(s + kRedWaves) * sg.stride];
+      a2 += pp[(int64_t)(s + 2 * kRedWaves) * sg.stride];
+      a3 += pp[(int64_t)(s + 3 * kRedWaves) * sg.stride];
     }
-    for (; s < sg.nslices; s += 4) a0 += pp[(int64_t)s * sg.stride];
+    for (; s < sg.nslices; s += kRedWaves) a0 += pp[(int64_t)s * sg.stride];
   }
   part[wave][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (wave != 0 || i >= sg.n) return;
-  const float v = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  float v = 0.f;
+#pragma unroll
+  for (int w = 0; w < kRedWaves; ++w) v += part[w][lane];
   if (sg.mode == 0) {
     sg.out[i] = v;
   } else if (sg.mode == 2) {
@@ -1321,7 +1325,7 @@ void launch_reduce(const std::vector<ReduceSeg>& v, hipStream_t s) {
     segs.seg[k] = v[k];
     total += v[k].blocks;
   }
-  slab_reduce_kernel<<<total, 256, 0, s>>>(segs);
+  slab_reduce_kernel<<<total, 64 * kRedWaves, 0, s>>>(segs);
 }
 
 int num_cus() {
