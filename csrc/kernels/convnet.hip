@@ -547,30 +547,47 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
 // One wave per 16 images; A fragments stream straight from global (16 B per lane, no LDS), the
 // 64 B-fragments (N = 10 padded to 16) sit in LDS.  Unfused from conv3 because reducing 10 logits
 // across 256 lanes per image cost the conv3 kernel more than this whole pass over a3.
+constexpr int FC1_G = 2;  // 16-image groups per workgroup
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ a3,
                                                       const bf16* __restrict__ packed,
                                                       const float* __restrict__ bfc,
                                                       float* __restrict__ logits, int B) {
-  __shared__ __attribute__((aligned(16))) bf16x8 Wl[64 * 64];
+  // The 4 waves split K (512 each) and hold their 16 B-fragments in VGPRs, loaded once from the
+  // L2-resident pack: no 64 KiB LDS fill per workgroup (which dominated the old one-wave-per-group
+  // kernel), 8 waves per CU instead of 4.  Partials are summed in a fixed order.
+  __shared__ f32x4 red[3][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFF_OFF);
-  for (int c = tid; c < 64 * 64; c += 256) Wl[c] = src[c];
-  __syncthreads();
-  const int b0 = (blockIdx.x * 4 + wave) * 16;
-  if (b0 >= B) return;
-  const int row = min(b0 + (lane & 15), B - 1);
-  const bf16x8* ap = reinterpret_cast<const bf16x8*>(a3 + (int64_t)row * 2048) + (lane >> 4);
-  f32x4 acc = zero_f32x4();
-#pragma unroll 16
-  for (int ks = 0; ks < 64; ++ks) acc = mfma16x16x32(ap[ks * 4], Wl[ks * 64 + lane], acc);
-  const int n = lane & 15;
-  if (n < 10) {
-    const float bn = bfc[n];
+  bf16x8 w[16];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int bb = b0 + (lane >> 4) * 4 + i;
-      if (bb < B) logits[(int64_t)bb * 10 + n] = acc[i] + bn;
+  for (int j = 0; j < 16; ++j) w[j] = src[(wave * 16 + j) * 64 + lane];
+  for (int g = 0; g < FC1_G; ++g) {
+    const int b0 = (blockIdx.x * FC1_G + g) * 16;  // uniform over the workgroup
+    if (b0 >= B) break;
+    const int row = min(b0 + (lane & 15), B - 1);
+    const bf16x8* ap = reinterpret_cast<const bf16x8*>(a3 + (int64_t)row * 2048) + (lane >> 4) + wave * 64;
+    f32x4 acc0 = zero_f32x4(), acc1 = zero_f32x4();
+#pragma unroll
+    for (int j = 0; j < 16; j += 2) {
+      acc0 = mfma16x16x32(ap[j * 4], w[j], acc0);
+      acc1 = mfma16x16x32(ap[(j + 1) * 4], w[j + 1], acc1);
     }
+    const f32x4 acc = acc0 + acc1;
+    if (wave > 0) red[wave - 1][lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      const f32x4 t = acc + red[0][lane] + red[1][lane] + red[2][lane];
+      const int n = lane & 15;
+      if (n < 10) {
+        const float bn = bfc[n];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int bb = b0 + (lane >> 4) * 4 + i;
+          if (bb < B) logits[(int64_t)bb * 10 + n] = t[i] + bn;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1374,7 +1391,7 @@ void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const 
   const int grid = clampi(B, 1, 2 * num_cus());
   conv3_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a2), static_cast<const bf16*>(packed), b3,
                                         static_cast<bf16*>(a3), idx3, B);
-  fc1_fwd_kernel<<<cdiv(B, 64), 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), bfc,
+  fc1_fwd_kernel<<<cdiv(B, 16 * FC1_G), 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), bfc,
                                              logits, B);
 }
 
