@@ -587,10 +587,23 @@ void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int 
     launch<Dense<false>, Dense<false>, true>(Dense<false>{da}, Dense<false>{db}, ep, batch, M, N, Kbytes / 2, splits, s);
 }
 
+static bool is_pointwise(const ConvGeom& g) {
+  return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0 && g.P == g.H && g.Q == g.W;
+}
+
 void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   const ConvFwdA la{static_cast<const bf16*>(x), g, M, Kd};
   const DenseLoader db{static_cast<const bf16*>(w_krsc), Kd, 0, g.K, Kd};
+  if (Kd % BK == 0) {
+    if (is_pointwise(g)) {  // 1x1 / stride 1 / pad 0: the im2col IS the NHWC activation matrix
+      const DenseLoader da{static_cast<const bf16*>(x), g.C, 0, M, Kd};
+      launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
+    } else {
+      launch(la, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
+    }
+    return;
+  }
   launch(la, Dense<false>{db}, ep, 1, M, g.K, Kd, 1, s);
 }
 
@@ -598,6 +611,15 @@ void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, cons
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   const ConvDgradA la{static_cast<const bf16*>(dy), g, M, Kd};
   const DenseLoader db{static_cast<const bf16*>(w_crsk), Kd, 0, g.C, Kd};
+  if (Kd % BK == 0) {
+    if (is_pointwise(g)) {  // dX = dY W: dY is the dense [N*H*W][K] matrix
+      const DenseLoader da{static_cast<const bf16*>(dy), g.K, 0, M, Kd};
+      launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
+    } else {
+      launch(la, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
+    }
+    return;
+  }
   launch(la, Dense<false>{db}, ep, 1, M, g.C, Kd, 1, s);
 }
 
@@ -616,7 +638,16 @@ void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int split
   int kps = (Mpos + splits - 1) / splits;
   kps = (kps + BK - 1) / BK * BK;
   const int S = (Mpos + kps - 1) / kps;
-  launch(Dense<true>{da}, lb, ep, 1, g.K, Kd, Mpos, S, s);
+  if (Mpos % BK == 0 && g.K % 8 == 0) {
+    if (is_pointwise(g) && Kd % 8 == 0) {  // B = X^T: row-contiguous view of the NHWC activation
+      const DenseLoader db{static_cast<const bf16*>(x), g.C, 0, Kd, Mpos};
+      launch(DenseAligned<true>{da}, DenseAligned<true>{db}, ep, 1, g.K, Kd, Mpos, S, s);
+    } else {
+      launch(DenseAligned<true>{da}, lb, ep, 1, g.K, Kd, Mpos, S, s);
+    }
+  } else {
+    launch(Dense<true>{da}, lb, ep, 1, g.K, Kd, Mpos, S, s);
+  }
   const int64_t n = (int64_t)g.K * Kd;
   splitk_sum_kernel<<<(int)((n + 255) / 256), 256, 0, s>>>(partial, S, n, dw_kcrs, g.K, g.C, g.R * g.S);
 }
