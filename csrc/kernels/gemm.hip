@@ -83,7 +83,7 @@ struct Dense {
 template <bool kRowContig>
 struct DenseAligned {
   static constexpr bool kRow = kRowContig;
-  static constexpr bool kFast = true;
+  static constexpr int kKind = 1;
   DenseLoader d;
 };
 
@@ -173,6 +173,11 @@ struct ConvWgradB {
 // the k-vector (t & 7).  Row-contiguous: tile [64 k][128 rows]; thread t owns the row-vector (t & 15)
 // and k = (t >> 4) + 16i.
 template <class L, class = void>
+struct loader_kind : std::integral_constant<int, 0> {};
+template <class L>
+struct loader_kind<L, std::void_t<decltype(L::kKind)>> : std::integral_constant<int, L::kKind> {};
+
+template <class L, class = void>
 struct StagerRows {  // checked loaders: row descriptors
   typename L::Row rows[4];
   __device__ __forceinline__ void init(const L& ld, int b, int tile_r0, int tid) {
@@ -190,7 +195,7 @@ struct StagerRows {  // checked loaders: row descriptors
   }
 };
 template <class L>
-struct StagerRows<L, std::enable_if_t<L::kFast>> {  // aligned dense: per-vector pointers
+struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 1>> {  // aligned dense: per-vector pointers
   const bf16* ptr[4];
   int64_t kstep;  // elements per unit of k
   __device__ __forceinline__ void init(const L& ld, int b, int tile_r0, int tid) {
@@ -211,6 +216,88 @@ struct StagerRows<L, std::enable_if_t<L::kFast>> {  // aligned dense: per-vector
   }
   __device__ __forceinline__ bf16x8 get(const L&, int i, int k0, int) const {
     return *reinterpret_cast<const bf16x8*>(ptr[i] + (int64_t)k0 * kstep);
+  }
+};
+
+// Implicit-GEMM conv forward with C % 64 == 0: a 64-wide k-tile lies inside one filter tap, so the tap
+// (r, s) and channel base are computed once per k-tile from the uniform k0 (scalar ALU) instead of two
+// integer divisions per 16-B load; each staged row keeps its image pointer and input origin.
+struct ConvFwdA64 {
+  static constexpr bool kRow = false;
+  static constexpr int kKind = 2;
+  const bf16* x;
+  ConvGeom g;
+  int M, Kd;
+};
+template <class L>
+struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 2>> {
+  const bf16* base[4];
+  int h0[4], w0[4];
+  __device__ __forceinline__ void init(const L& ld, int, int tile_r0, int tid) {
+    const ConvGeom& g = ld.g;
+    const int pq = g.P * g.Q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = tile_r0 + (tid >> 3) + 32 * i;
+      if (m < ld.M) {
+        const int n = m / pq, rem = m - n * pq, p = rem / g.Q, q = rem - p * g.Q;
+        base[i] = ld.x + (int64_t)n * g.H * g.W * g.C + 8 * (tid & 7);
+        h0[i] = p * g.stride - g.pad;
+        w0[i] = q * g.stride - g.pad;
+      } else {
+        base[i] = ld.x;
+        h0[i] = -(1 << 20);  // always out of bounds -> zero
+        w0[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ bf16x8 get(const L& ld, int i, int k0, int) const {
+    const ConvGeom& g = ld.g;
+    const int rs = k0 / g.C, c0 = k0 - rs * g.C, r = rs / g.S, sx = rs - r * g.S;  // uniform
+    const int h = h0[i] + r * g.dil, w = w0[i] + sx * g.dil;
+    if ((unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(base[i] + ((int64_t)h * g.W + w) * g.C + c0);
+  }
+};
+
+// Transposed-conv gather of dY (data gradient) with K % 64 == 0: tap and output-channel base per k-tile.
+struct ConvDgradA64 {
+  static constexpr bool kRow = false;
+  static constexpr int kKind = 3;
+  const bf16* dy;
+  ConvGeom g;
+  int M, Kd;
+};
+template <class L>
+struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 3>> {
+  const bf16* base[4];
+  int hp[4], wp[4];
+  __device__ __forceinline__ void init(const L& ld, int, int tile_r0, int tid) {
+    const ConvGeom& g = ld.g;
+    const int hw = g.H * g.W;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = tile_r0 + (tid >> 3) + 32 * i;
+      if (m < ld.M) {
+        const int n = m / hw, rem = m - n * hw, h = rem / g.W, w = rem - h * g.W;
+        base[i] = ld.dy + (int64_t)n * g.P * g.Q * g.K + 8 * (tid & 7);
+        hp[i] = h + g.pad;
+        wp[i] = w + g.pad;
+      } else {
+        base[i] = ld.dy;
+        hp[i] = -(1 << 20);
+        wp[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ bf16x8 get(const L& ld, int i, int k0, int) const {
+    const ConvGeom& g = ld.g;
+    const int rs = k0 / g.K, ko = k0 - rs * g.K, r = rs / g.S, sx = rs - r * g.S;  // uniform
+    const int ph = hp[i] - r * g.dil, pw = wp[i] - sx * g.dil;
+    if (ph < 0 || pw < 0) return zero_bf16x8();
+    const int p = ph / g.stride, q = pw / g.stride;
+    if (p * g.stride != ph || q * g.stride != pw || p >= g.P || q >= g.Q) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(base[i] + ((int64_t)p * g.Q + q) * g.K + ko);
   }
 };
 
@@ -599,6 +686,8 @@ void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const G
     if (is_pointwise(g)) {  // 1x1 / stride 1 / pad 0: the im2col IS the NHWC activation matrix
       const DenseLoader da{static_cast<const bf16*>(x), g.C, 0, M, Kd};
       launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
+    } else if (g.C % BK == 0) {
+      launch(ConvFwdA64{static_cast<const bf16*>(x), g, M, Kd}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
     } else {
       launch(la, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
     }
@@ -615,6 +704,8 @@ void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, cons
     if (is_pointwise(g)) {  // dX = dY W: dY is the dense [N*H*W][K] matrix
       const DenseLoader da{static_cast<const bf16*>(dy), g.K, 0, M, Kd};
       launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
+    } else if (g.K % BK == 0) {
+      launch(ConvDgradA64{static_cast<const bf16*>(dy), g, M, Kd}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
     } else {
       launch(la, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
     }
