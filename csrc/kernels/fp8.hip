@@ -71,12 +71,19 @@ __global__ __launch_bounds__(256) void quant_kernel(const bf16* __restrict__ x, 
 }
 
 // x [rows][cols] bf16 -> out [cols][rows] e4m3 (and, when out_rm != null, the row-major copy too:
-// one read of x for both GEMM orientations); 64x64 tiles through LDS (rows, cols % 16 == 0)
+// one read of x for both GEMM orientations); 64x64 tiles through LDS (rows, cols % 16 == 0).
+// Delayed scaling (amax_next != null): the scale comes from a previous amax, so values are clamped to
+// the e4m3 range before conversion, and this tensor's |x|max is folded into *amax_next (one atomic per
+// workgroup) for the next call - no separate amax pass over x.
 __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
                                                       const float* __restrict__ amax, uint8_t* __restrict__ out,
-                                                      float* __restrict__ scale, uint8_t* __restrict__ out_rm) {
+                                                      float* __restrict__ scale, uint8_t* __restrict__ out_rm,
+                                                      unsigned* __restrict__ amax_next) {
   __shared__ float tile[64][65];
+  __shared__ float red[4];
   const float inv = 1.f / qscale(amax);
+  const float lim = amax_next ? kE4M3Max : INFINITY;
+  float bmax = 0.f;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) scale[0] = qscale(amax);
   const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
   const int t = threadIdx.x;
@@ -87,7 +94,11 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
     bf16x8 v = zero_bf16x8();
     if (gr < rows && gc < cols) v = *reinterpret_cast<const bf16x8*>(x + gr * cols + gc);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) tile[r][cv * 8 + j] = (float)v[j] * inv;
+    for (int j = 0; j < 8; ++j) {
+      const float f = (float)v[j];
+      bmax = fmaxf(bmax, fabsf(f));
+      tile[r][cv * 8 + j] = fminf(fmaxf(f * inv, -lim), lim);
+    }
     if (out_rm && gr < rows && gc < cols) {
       uint2 o;
       o.x = pack4(tile[r][cv * 8 + 0], tile[r][cv * 8 + 1], tile[r][cv * 8 + 2], tile[r][cv * 8 + 3]);
@@ -106,6 +117,28 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
     for (int q = 0; q < 4; ++q)
       w[q] = pack4(tile[seg + 4 * q][oc], tile[seg + 4 * q + 1][oc], tile[seg + 4 * q + 2][oc], tile[seg + 4 * q + 3][oc]);
     *reinterpret_cast<uint4*>(out + gr * rows + r0 + seg) = o;
+  }
+  if (amax_next) {  // this tile's |x|max -> its own slot (thousands of same-address atomics serialise)
+    bmax = wave_max(bmax);
+    if ((t & 63) == 0) red[t >> 6] = bmax;
+    __syncthreads();
+    if (t == 0)
+      amax_next[blockIdx.y * gridDim.x + blockIdx.x] = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+  }
+}
+
+// Delayed-scaling roll: hist[0] (the amax the next quantisation scales by) <- max of the per-tile maxima
+// hist[1 .. 1+n) the previous call of this site wrote (kept if they are all zero).
+__global__ __launch_bounds__(256) void amax_roll_kernel(float* __restrict__ hist, int n) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, hist[1 + i]);
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float a = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (a > 0.f) hist[0] = a;
   }
 }
 
@@ -127,8 +160,19 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
   } else {
     dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
     quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, amax, static_cast<uint8_t*>(out),
-                                        scale, static_cast<uint8_t*>(out_rowmajor));
+                                        scale, static_cast<uint8_t*>(out_rowmajor), nullptr);
   }
+}
+
+void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
+                          float* scale, void* out_rowmajor, hipStream_t s) {
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
+  if (init)
+    fp8_amax(x, rows * cols, hist, s);  // first use of the site: the exact amax of this tensor
+  else
+    amax_roll_kernel<<<1, 256, 0, s>>>(hist, (int)(grid.x * grid.y));
+  quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, hist, static_cast<uint8_t*>(out_t),
+                                      scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1));
 }
 
 }  // namespace kern

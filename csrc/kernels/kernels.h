@@ -132,6 +132,11 @@ void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int 
 void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s);
 void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, const float* amax, void* out,
                   float* scale, hipStream_t s, void* out_rowmajor = nullptr);
+// delayed scaling: hist = {amax to scale by, per-64x64-tile |x|max of the last call...}; hist[0] is
+// rolled from the tile maxima (or, init = first call of a site, measured exactly), then x is quantised
+// (q^T into out_t, q into out_rowmajor) while its tile maxima are written for the next call.
+void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
+                          float* scale, void* out_rowmajor, hipStream_t s);
 void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,

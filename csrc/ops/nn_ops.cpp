@@ -489,6 +489,24 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both(const at::Tenso
   return {q, qt, scale};
 }
 
+int64_t fp8_delayed_slots(int64_t rows, int64_t cols) { return ((rows + 63) / 64) * ((cols + 63) / 64); }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const at::Tensor& x, at::Tensor hist,
+                                                                        bool init) {
+  bf16_gpu(x, "fp8 quantize input");
+  RINGDP_CHECK(x.dim() == 2 && x.size(0) % 16 == 0 && x.size(1) % 16 == 0,
+               "fp8_quantize_both_delayed: expected a 2-D tensor with dims % 16 == 0");
+  f32_gpu(hist, "fp8 amax history");
+  const int64_t R = x.size(0), Cc = x.size(1);
+  RINGDP_CHECK(hist.is_contiguous() && hist.numel() == 1 + fp8_delayed_slots(R, Cc),
+               "fp8 amax history: expected 1 + fp8_delayed_slots(rows, cols) contiguous floats");
+  at::Tensor scale = at::empty({1}, x.options().dtype(at::kFloat));
+  at::Tensor q = at::empty({R, Cc}, x.options().dtype(at::kByte)), qt = at::empty({Cc, R}, x.options().dtype(at::kByte));
+  kern::fp8_quantize_delayed(x.data_ptr(), R, Cc, hist.data_ptr<float>(), init, qt.data_ptr(), scale.data_ptr<float>(),
+                             q.data_ptr(), stream_of(x));
+  return {q, qt, scale};
+}
+
 at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
                     int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,
                     const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& preact) {

@@ -9,6 +9,7 @@ and the head/token layout moves are the row kernels of ``csrc/kernels/vit.hip``.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -120,11 +121,33 @@ class LinearF(torch.autograd.Function):
         return dx, dw, db, dres, None, None
 
 
+_FP8_DELAYED = os.environ.get("RINGDP_FP8_DELAYED", "1") == "1"
+
+
+def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int):
+    """fp8 quantisation of an activation (slot 0: the linear's input x) or output gradient (slot 1: dz)
+    with per-site delayed scaling (TransformerEngine-style, history length 1), state kept on the weight:
+    the first quantisation of a site measures its exact amax; later ones scale by the amax the previous
+    step measured (values clamped to the e4m3 range) and record the current one inside the same pass,
+    which removes the separate amax pass over the tensor."""
+    if not _FP8_DELAYED:
+        return C.fp8_quantize_both(t)
+    sites = getattr(w, "_ringdp_fp8", None)
+    if sites is None:
+        sites = w._ringdp_fp8 = [None, None]
+    n = 1 + C.fp8_delayed_slots(t.shape[0], t.shape[1])
+    hist = sites[slot]
+    init = hist is None or hist.numel() != n
+    if init:
+        hist = sites[slot] = torch.zeros(n, device=t.device, dtype=torch.float32)
+    return C.fp8_quantize_both_delayed(t, hist, init)
+
+
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
     M, K = x.shape
     N = w.shape[0]
     wb = _bf16(w)
-    xq, xtq, sx = C.fp8_quantize_both(x)   # row-major for this GEMM, transposed for the weight grad
+    xq, xtq, sx = _quant_act(x, w, 0)    # row-major for this GEMM, transposed for the weight grad
     wq, wtq, sw = C.fp8_quantize_both(wb)  # ... and for the data grad
     pre = torch.empty(M, N, device=x.device, dtype=torch.bfloat16) if act == 2 else None
     y = C.gemm_fp8(xq, wq, sx, sw, M, N, K, not out_f32, b, act, residual, pre)
@@ -144,7 +167,7 @@ def _linear_fp8_bwd(ctx, dy):
     dyb = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
     dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
     dx = dw = db = None
-    dzq, dztq, sdz = C.fp8_quantize_both(dz)  # [M][N] for the data grad, [N][M] for the weight grad
+    dzq, dztq, sdz = _quant_act(dz, w, 1)  # [M][N] for the data grad, [N][M] for the weight grad
     if ctx.needs_input_grad[0]:
         dx = C.gemm_fp8(dzq, wtq, sdz, sw, M, K, N, True)
     if ctx.needs_input_grad[1]:

@@ -319,6 +319,30 @@ def _fp8_ref(x):
     return (x.float() / s).to(torch.float8_e4m3fn).float() * s, s
 
 
+def test_fp8_delayed_scaling():
+    """Delayed scaling: the first call of a site is exact (measured amax), later calls scale by the
+    previous call's amax, saturate instead of overflowing, and record their own amax."""
+    torch.manual_seed(1)
+    a = torch.randn(320, 768, device="cuda").bfloat16()
+    hist = torch.zeros(1 + C().fp8_delayed_slots(320, 768), device="cuda")
+    q0, qt0, s0 = C().fp8_quantize_both(a)
+    q1, qt1, s1 = C().fp8_quantize_both_delayed(a, hist, True)
+    assert torch.equal(q1, q0) and torch.equal(qt1, qt0) and torch.equal(s1, s0)
+    amax = float(a.float().abs().max())
+    assert float(hist[0]) == amax and float(hist[1:].max()) == amax  # tile maxima recorded
+    b = a * 2  # larger than the scale in use
+    q2, qt2, s2 = C().fp8_quantize_both_delayed(b, hist, False)
+    assert torch.equal(s2, s1)  # scaled by the previous amax
+    deq = q2.view(torch.float8_e4m3fn).float() * s2
+    assert torch.isfinite(deq).all()
+    assert float(deq.abs().max()) <= amax * (1 + 1e-6)  # saturated at 448 * scale
+    assert torch.equal(qt2, q2.t().contiguous())
+    assert float(hist[1:].max()) == float(b.float().abs().max())
+    _, _, s3 = C().fp8_quantize_both_delayed(b, hist, False)  # rolls to b's amax
+    assert float(hist[0]) == float(b.float().abs().max())
+    torch.testing.assert_close(s3[0], hist[0] / 448.0, rtol=1e-6, atol=0)
+
+
 def test_fp8_quantize_and_gemm():
     """References in float64: fp32 torch matmuls on this ROCm build are not full-precision."""
     torch.manual_seed(0)
