@@ -129,15 +129,21 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
 
 // Delayed-scaling roll: hist[0] (the amax the next quantisation scales by) <- max of the per-tile maxima
 // hist[1 .. 1+n) the previous call of this site wrote (kept if they are all zero).
-__global__ __launch_bounds__(256) void amax_roll_kernel(float* __restrict__ hist, int n) {
-  __shared__ float red[4];
-  float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, hist[1 + i]);
-  m = wave_max(m);
+__global__ __launch_bounds__(1024) void amax_roll_kernel(float* __restrict__ hist, int n) {
+  __shared__ float red[16];
+  float m0 = 0.f, m1 = 0.f;  // 1024 threads, two loads in flight each (n is up to ~20k tile maxima)
+  int i = threadIdx.x;
+  for (; i + 1024 < n; i += 2048) {
+    m0 = fmaxf(m0, hist[1 + i]);
+    m1 = fmaxf(m1, hist[1 + i + 1024]);
+  }
+  if (i < n) m0 = fmaxf(m0, hist[1 + i]);
+  const float m = wave_max(fmaxf(m0, m1));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float a = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float a = 0.f;
+    for (int w = 0; w < 16; ++w) a = fmaxf(a, red[w]);
     if (a > 0.f) hist[0] = a;
   }
 }
@@ -170,7 +176,7 @@ void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist
   if (init)
     fp8_amax(x, rows * cols, hist, s);  // first use of the site: the exact amax of this tensor
   else
-    amax_roll_kernel<<<1, 256, 0, s>>>(hist, (int)(grid.x * grid.y));
+    amax_roll_kernel<<<1, 1024, 0, s>>>(hist, (int)(grid.x * grid.y));
   quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, hist, static_cast<uint8_t*>(out_t),
                                       scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1));
 }

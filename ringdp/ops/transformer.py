@@ -125,8 +125,8 @@ _FP8_DELAYED = os.environ.get("RINGDP_FP8_DELAYED", "1") == "1"
 
 
 def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int):
-    """fp8 quantisation of an activation (slot 0: the linear's input x) or output gradient (slot 1: dz)
-    with per-site delayed scaling (TransformerEngine-style, history length 1), state kept on the weight:
+    """fp8 quantisation of an activation (slot 0: the linear's input x), output gradient (slot 1: dz) or
+    the bf16 copy of the weight (slot 2) with per-site delayed scaling (TransformerEngine-style, history length 1), state kept on the weight:
     the first quantisation of a site measures its exact amax; later ones scale by the amax the previous
     step measured (values clamped to the e4m3 range) and record the current one inside the same pass,
     which removes the separate amax pass over the tensor."""
@@ -134,7 +134,7 @@ def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int):
         return C.fp8_quantize_both(t)
     sites = getattr(w, "_ringdp_fp8", None)
     if sites is None:
-        sites = w._ringdp_fp8 = [None, None]
+        sites = w._ringdp_fp8 = [None, None, None]
     n = 1 + C.fp8_delayed_slots(t.shape[0], t.shape[1])
     hist = sites[slot]
     init = hist is None or hist.numel() != n
@@ -148,7 +148,7 @@ def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
     N = w.shape[0]
     wb = _bf16(w)
     xq, xtq, sx = _quant_act(x, w, 0)    # row-major for this GEMM, transposed for the weight grad
-    wq, wtq, sw = C.fp8_quantize_both(wb)  # ... and for the data grad
+    wq, wtq, sw = _quant_act(wb, w, 2)   # ... and for the data grad
     pre = torch.empty(M, N, device=x.device, dtype=torch.bfloat16) if act == 2 else None
     y = C.gemm_fp8(xq, wq, sx, sw, M, N, K, not out_f32, b, act, residual, pre)
     ctx.fp8 = True
