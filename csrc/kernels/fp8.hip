@@ -5,6 +5,8 @@
 //   quant : scale = max(amax, tiny) / 448 (written to device memory for the GEMM epilogue),
 //           q = cvt_e4m3(x / scale); optional transpose through a 64x64 LDS tile so every GEMM
 //           operand (x^T, w^T, dy^T) is K-contiguous.  No host synchronisation anywhere.
+//   delayed: (the training path, ringdp/ops/transformer.py) scale from the previous call's amax, rolled
+//           from the per-tile maxima that call recorded; values clamped to +-448.
 #include <algorithm>
 
 #include "device_common.h"
@@ -73,8 +75,8 @@ __global__ __launch_bounds__(256) void quant_kernel(const bf16* __restrict__ x, 
 // x [rows][cols] bf16 -> out [cols][rows] e4m3 (and, when out_rm != null, the row-major copy too:
 // one read of x for both GEMM orientations); 64x64 tiles through LDS (rows, cols % 16 == 0).
 // Delayed scaling (amax_next != null): the scale comes from a previous amax, so values are clamped to
-// the e4m3 range before conversion, and this tensor's |x|max is folded into *amax_next (one atomic per
-// workgroup) for the next call - no separate amax pass over x.
+// the e4m3 range before conversion, and each 64x64 tile's |x|max is stored to amax_next[tile] for the
+// next call's roll - no separate amax pass over x.
 __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
                                                       const float* __restrict__ amax, uint8_t* __restrict__ out,
                                                       float* __restrict__ scale, uint8_t* __restrict__ out_rm,
