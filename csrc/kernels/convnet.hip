@@ -100,9 +100,9 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned char u8x8 __attribute__((ext_vector_type(8)));
 
-// relu(max over a 2x2 window) of 8 bf16 channels, plus the pool2 code byte per channel:
-// 0..3 = first maximum in (0,0),(0,1),(1,0),(1,1) order (torch max_pool2d semantics), bit 2 set =
-// the pooled value is 0 (no gradient flows).  Done on the raw bf16 bit patterns with packed int16
+// relu(max over a 2x2 window) of 8 bf16 channels, plus the pool2 code byte per channel: one-hot bit
+// dy*2+dx of the first maximum in (0,0),(0,1),(1,0),(1,1) order (torch max_pool2d semantics), 0 = the
+// pooled value is 0 (no gradient flows).  Done on the raw bf16 bit patterns with packed int16
 // ops (v_pk_max_i16 & co, 2 channels per instruction): for values >= 0 the integer order is the float
 // order and any negative value is a negative int16, so max(v0..v3, 0) over int16 IS relu(max).
 __device__ __forceinline__ void pool2_code8(const bf16* r0, int rs, int w, bf16x8& out, uint2& code) {
@@ -121,9 +121,9 @@ __device__ __forceinline__ void pool2_code8(const bf16* r0, int rs, int w, bf16x
   const u16x8 k2 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v2), one);
   const u16x8 t1 = k0 * k1;
   const u16x8 idx = k0 + t1 + t1 * k2;                                    // first i with v_i == m
-  const u16x8 none = (one - __builtin_elementwise_min(mu, one)) << 2;     // 4 iff m == 0
+  const u16x8 live = __builtin_elementwise_min(mu, one);                  // 0 iff m == 0
   out = __builtin_bit_cast(bf16x8, m);
-  code = __builtin_bit_cast(uint2, __builtin_convertvector(idx | none, u8x8));
+  code = __builtin_bit_cast(uint2, __builtin_convertvector((one << idx) * live, u8x8));
 }
 
 // First-max argmax over the 4 registers of a window + bias + ReLU (torch max_pool2d semantics:
@@ -689,14 +689,19 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
 //          to the z2 position its pool2 code names (F2 forward) -> dz2 [B,11,11,64];
 //   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a workgroup pair per
 //          image slice (one half of the 576 n columns each).  db3 comes from fc1's backward.
-constexpr int C3_PW = 12;    // padded d(conv3) image width (8 + 2*2)
-constexpr int C3_PRS = 136;  // bf16 per padded-image row (128 + 8)
+// Padded d(conv3) image (12x12 positions, 8x8 interior, ring of 2 zeros) in LDS: position (Y, X) at
+// Y*C3_PY + X*C3_PX bf16.  These strides (tools/lds_bank_model_conv3.py: 288-B positions, 3648-B rows)
+// make every B-fragment read of the dgrad GEMM conflict-free (4 LDS cycles per ds_read_b128, was 7.7
+// with 136-element rows) while each read stays a per-lane base plus an immediate tap offset.
+constexpr int C3_PX = 144;   // bf16 per position (128 + 16)
+constexpr int C3_PY = 1824;  // bf16 per row of positions (12 * 144 + 96)
 constexpr int C3_DARS = 68;  // floats per da2 row (64 + 4)
 constexpr int C3_DRS = 136;  // bf16 per D3 row in LDS
-constexpr int C3D_P = C3_PW * C3_PW * C3_PRS * 2;  // 39168
-constexpr int C3D_AM = 100 * 64;                   // 6400: pool2 codes (x2: the next image lands by DMA)
-constexpr int C3D_DA = 100 * C3_DARS * 4;          // 27200
-constexpr int C3D_LDS = C3D_P + 2 * C3D_AM + C3D_DA;
+constexpr int C3D_P = (11 * C3_PY + 11 * C3_PX + 128) * 2;  // 43552
+constexpr int C3D_AM = 100 * 64;                            // 6400: pool2 codes of the current image
+constexpr int C3D_DA = 100 * C3_DARS * 4;                   // 27200
+constexpr int C3D_LDS = C3D_P + C3D_AM + C3D_DA;
+static_assert(C3D_P % 16 == 0 && C3D_LDS <= 81920, "two conv3 backward workgroups per CU");
 constexpr int C3W_D = 64 * C3_DRS * 2;   // 17408
 constexpr int C3W_X = 100 * C3_XRS * 2;  // 14400
 constexpr int C3W_R = 100 * 64 * 2;      // 12800: DMA staging of the next a2 image
@@ -753,8 +758,8 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ dz2, int B, int block, int nblocks) {
   bf16* P = reinterpret_cast<bf16*>(smem);
-  uint8_t* AMb = reinterpret_cast<uint8_t*>(smem + C3D_P);
-  float* DA = reinterpret_cast<float*>(smem + C3D_P + 2 * C3D_AM);
+  uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P);
+  float* DA = reinterpret_cast<float*>(smem + C3D_P + C3D_AM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int kg = wave >> 1, nh = wave & 1;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
@@ -768,7 +773,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
 #pragma unroll
   for (int mt = 0; mt < 7; ++mt) {
     const int mm = min(mt * 16 + r16, 99);
-    base[mt] = (mm / 10) * C3_PW + mm % 10;
+    base[mt] = (mm / 10) * C3_PY + (mm % 10) * C3_PX;
   }
   // the ring of the padded image stays zero; only the 8x8 interior is rewritten per image
   for (int c = tid; c < C3D_P / 16; c += 256) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
@@ -783,10 +788,10 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
     for (int j = 0; j < 18; ++j) {
       const int ks = 18 * KG + j;
       const int tapp = ks >> 2, c0 = (ks & 3) * 32;
-      const int shift = (tapp / 3) * C3_PW + tapp % 3;
+      const int shift = (tapp / 3) * C3_PY + (tapp % 3) * C3_PX;
 #pragma unroll
       for (int mt = 0; mt < 7; ++mt) {
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(P + (base[mt] + shift) * C3_PRS + c0 + q8);
+        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(P + base[mt] + shift + c0 + q8);
         acc[mt][0] = mfma16x16x32(aw[0][j], bfr, acc[mt][0]);
         acc[mt][1] = mfma16x16x32(aw[1][j], bfr, acc[mt][1]);
       }
@@ -809,53 +814,67 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
     __syncthreads();
     if (KG == 0) publish(true);
   };
+  // pool2 + ReLU backward, one item per (output row y, channel quad), sliding along x: window (py, px)
+  // covers outputs (py..py+1, px..px+1) and its one-hot code bit dy*2+dx names the one that receives
+  // its gradient, so output (y, x) sums, in a fixed order, the windows (y, x), (y, x-1), (y-1, x),
+  // (y-1, x-1) masked by code bits 0, 1, 2, 3.  Each window of a row is loaded once per item and used
+  // for x and x+1; a missing window row (y = 0 or 10) reads a valid one under a mask of bit 4 (never set).
+  const int gy = tid >> 4, gq = (tid & 15) * 4;
+  const int rowA = min(gy, 9), rowB = max(gy - 1, 0);  // dy = 0 and dy = 1 window rows
+  const int sA = gy <= 9 ? 0 : 4, sB = gy >= 1 ? 2 : 4;
+  auto masked_add = [](f32x4& g, uint32_t cw, int sh, const f32x4& d) {
+    const uint32_t m = (cw >> sh) & 0x01010101u;  // byte j = 1 iff channel j's window picked this output
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = fmaf(d[j], (float)((m >> (8 * j)) & 0xffu), g[j]);
+  };
   C3Pre pre;
-  int b = block, cur = 0;
-  if (b < B) {
-    pre.load(da3m, idx3, b, tid);
-    codes_glds(idx2, b, AMb, wave, lane);
-  }
-  for (; b < B; b += nblocks, cur ^= 1) {
-    c_dma_wait();
-    __syncthreads();  // previous image fully consumed (P, DA); this image's codes have landed
-    c3_expand(pre, tid, [&](int r) { return P + (win_pos(r, C3_PW) + 2 * C3_PW + 2) * C3_PRS; });
+  int b = block;
+  if (b < B) pre.load(da3m, idx3, b, tid);
+  for (; b < B; b += nblocks) {
+    __syncthreads();  // previous image fully consumed (P, DA, AM)
+    c3_expand(pre, tid, [&](int r) {
+      const int w = r >> 2, i = r & 3;
+      return P + (2 * (w >> 2) + (i >> 1) + 2) * C3_PY + (2 * (w & 3) + (i & 1) + 2) * C3_PX;
+    });
+    codes_glds(idx2, b, AM, wave, lane);  // this image's codes land during the MFMA phase
     const int nb = b + nblocks;
-    if (nb < B) {  // lands during the MFMA phase
-      pre.load(da3m, idx3, nb, tid);
-      codes_glds(idx2, nb, AMb + (cur ^ 1) * C3D_AM, wave, lane);
-    }
+    if (nb < B) pre.load(da3m, idx3, nb, tid);
     __syncthreads();
     if (kg == 0)
       mfma_phase(std::integral_constant<int, 0>{});
     else
       mfma_phase(std::integral_constant<int, 1>{});
+    c_dma_wait();
     __syncthreads();
-    // pool2 + ReLU backward as a gather: item (position, 4-channel quad) sums da2 of the (<= 4)
-    // windows covering it, in a fixed window order, where the window's code names this position (a
-    // code with bit 2 set - no gradient - never matches).  16 consecutive lanes share a position:
-    // every LDS read is a contiguous 256 B (conflict-free) and every store is coalesced.
-    const uint8_t* AM = AMb + cur * C3D_AM;
-    bf16x4* dst = reinterpret_cast<bf16x4*>(dz2 + (int64_t)b * 121 * 64);
-    for (int it = tid; it < 121 * 16; it += 256) {
-      const int pos = it >> 4, cq = (it & 15) * 4;
-      const int y = pos / 11, x = pos % 11;
-      f32x4 g = zero_f32x4();
+    if (tid < 176) {
+      const uint32_t* cA = reinterpret_cast<const uint32_t*>(AM + rowA * 640 + gq);
+      const uint32_t* cB = reinterpret_cast<const uint32_t*>(AM + rowB * 640 + gq);
+      const f32x4* dA = reinterpret_cast<const f32x4*>(DA + rowA * 10 * C3_DARS + gq);
+      const f32x4* dB = reinterpret_cast<const f32x4*>(DA + rowB * 10 * C3_DARS + gq);
+      bf16x4* dst = reinterpret_cast<bf16x4*>(dz2 + ((int64_t)b * 121 + gy * 11) * 64 + gq);
+      uint32_t pa = 0, pb = 0;  // window (., x-1)
+      f32x4 qa = zero_f32x4(), qb = zero_f32x4();
 #pragma unroll
-      for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-        for (int dx = 0; dx < 2; ++dx) {
-          const int py = y - dy, px = x - dx;
-          if (py >= 0 && py < 10 && px >= 0 && px < 10) {
-            const int p = py * 10 + px;
-            const uint32_t cw = *reinterpret_cast<const uint32_t*>(AM + p * 64 + cq);
-            const f32x4 d = *reinterpret_cast<const f32x4*>(DA + p * C3_DARS + cq);
-            const uint32_t want = (uint32_t)(dy * 2 + dx);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (((cw >> (8 * j)) & 0xffu) == want) g[j] += d[j];
-          }
+      for (int x = 0; x < 11; ++x) {
+        uint32_t na = 0, nb2 = 0;
+        f32x4 ea = zero_f32x4(), eb = zero_f32x4();
+        if (x < 10) {
+          na = cA[x * 16];
+          nb2 = cB[x * 16];
+          ea = dA[x * (C3_DARS / 4)];
+          eb = dB[x * (C3_DARS / 4)];
         }
-      dst[it] = bf16x4{(bf16)g[0], (bf16)g[1], (bf16)g[2], (bf16)g[3]};
+        f32x4 g = zero_f32x4();
+        if (x < 10) masked_add(g, na, sA, ea);
+        if (x > 0) masked_add(g, pa, sA + 1, qa);
+        if (x < 10) masked_add(g, nb2, sB, eb);
+        if (x > 0) masked_add(g, pb, sB + 1, qb);
+        dst[x * 16] = bf16x4{(bf16)g[0], (bf16)g[1], (bf16)g[2], (bf16)g[3]};
+        pa = na;
+        pb = nb2;
+        qa = ea;
+        qb = eb;
+      }
     }
   }
 }

@@ -119,13 +119,13 @@ def test_conv1_forward(B, u8):
 
 
 def pool2_ref(z2):
-    """relu + 2x2/s1 max pool of a bf16 z2 [B,11,11,64] with the kernel's code byte: first maximum in
-    (0,0),(0,1),(1,0),(1,1) order, bit 2 set where the pooled value is 0."""
+    """relu + 2x2/s1 max pool of a bf16 z2 [B,11,11,64] with the kernel's code byte: one-hot bit
+    dy*2+dx of the first maximum in (0,0),(0,1),(1,0),(1,1) order, 0 where the pooled value is 0."""
     z = z2.float()
     v = torch.stack([z[:, :-1, :-1], z[:, :-1, 1:], z[:, 1:, :-1], z[:, 1:, 1:]], -1)
     m = v.max(-1).values.clamp_min(0)
     first = torch.argmax((v == m.unsqueeze(-1)).to(torch.int8), -1)
-    code = torch.where(m > 0, first, torch.full_like(first, 4)).to(torch.uint8)
+    code = torch.where(m > 0, 1 << first, torch.zeros_like(first)).to(torch.uint8)
     return m.bfloat16(), code
 
 
@@ -140,17 +140,19 @@ def test_conv2_forward(B):
     ref = F.max_pool2d(F.relu(z.permute(0, 3, 1, 2)), 2, 1).permute(0, 2, 3, 1)
     assert a2.shape == (B, 10, 10, 64) and a2.dtype == torch.bfloat16 and idx2.dtype == torch.uint8
     assert rel_err(a2, ref) < 1e-2
-    # codes: bit 2 <=> pooled value 0; otherwise the named position holds the window maximum
-    assert torch.equal((idx2 & 4) != 0, a2.float() == 0)
+    # codes: one-hot (a single bit of 0..3) where the pooled value is > 0, else 0; the named position
+    # holds the window maximum
+    live = idx2 != 0
+    assert torch.equal(live, a2.float() != 0)
+    assert torch.all((idx2 & (idx2 - 1)) == 0) and int(idx2.max()) <= 8
     v = torch.stack([z[:, :-1, :-1], z[:, :-1, 1:], z[:, 1:, :-1], z[:, 1:, 1:]], -1)
-    picked = torch.gather(v, 4, (idx2.long() & 3).unsqueeze(-1)).squeeze(-1)
-    live = (idx2 & 4) == 0
+    arg = torch.log2(idx2.clamp_min(1).float()).long()
+    picked = torch.gather(v, 4, arg.unsqueeze(-1)).squeeze(-1)
     tol = 1e-2 * (1 + v.abs().amax(-1))
     assert torch.all(((v.amax(-1) - picked) <= tol)[live])
     # on bf16-exact inputs the codes are exactly torch's first-max argmax
     za, zc = pool2_ref(z.bfloat16())
-    kc = torch.where((idx2 & 4) != 0, torch.full_like(idx2, 4), idx2)  # bits 0-1 are free when bit 2 is set
-    assert float((zc == kc).float().mean()) > 0.99
+    assert float((zc == idx2).float().mean()) > 0.99
 
 
 def f3_reference(a2, ws):

@@ -60,8 +60,23 @@ def conv(n, h, c, k, r, stride):
             "dgrad": [round(d, 1), round(flops / d / 1e6, 1)], "wgrad": [round(wg, 1), round(flops / wg / 1e6, 1)]}
 
 
+def attention(BH=1536, Tp=208, Dh=64):
+    """ViT-B/16 attention batched GEMMs (B=128 x 12 heads, Tp=208 padded tokens, head dim 64)."""
+    q = torch.randn(BH * Tp * Dh, device="cuda").bfloat16()
+    k = torch.randn(BH * Tp * Dh, device="cuda").bfloat16()
+    p = torch.randn(BH * Tp * Tp, device="cuda").bfloat16()
+    res = {}
+    res["QK^T"] = timeit(lambda: C.gemm(q, k, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False))
+    res["PV"] = timeit(lambda: C.gemm(p, k, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True))
+    res["dS^T Q"] = timeit(lambda: C.gemm(p, q, Tp, Dh, Tp, Tp, Dh, True, True, BH, Tp * Tp, Tp * Dh, True))
+    return {"shape": f"attention BH{BH} Tp{Tp} Dh{Dh}", **{n: round(v, 1) for n, v in res.items()}}
+
+
 if __name__ == "__main__":
     out = []
+    if "--attention" in sys.argv:
+        print(json.dumps(attention()), flush=True)
+        sys.exit(0)
     for args in [(4096, 4096, 4096), (4096, 4096, 4096, True, False), (4096, 4096, 4096, False, True),
                  (4096, 4096, 4096, True, True), (8192, 768, 3072)]:
         out.append(dense(*args))
@@ -77,3 +92,4 @@ if __name__ == "__main__":
                  (256, 14, 1024, 256, 1, 1), (256, 224, 8, 64, 7, 2)]:
         out.append(conv(*args))
         print(json.dumps(out[-1]), flush=True)
+
