@@ -423,6 +423,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("out_bf16") = true, py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("residual") = py::none(), py::arg("preact") = py::none());
   m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
+  m.def("set_fp8_tile_mode", &ops::set_fp8_tile_mode,
+        "fp8 GEMM kernel choice: 0 auto, 128 the generic 128x128 core, 256 the 256x256 DMA-pipelined kernel");
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);

@@ -662,8 +662,56 @@ void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int
     launch(Dense<true>{da}, Dense<true>{db}, ep, batch, M, N, K, splits, s);
 }
 
+// 256x256 fp8 kernel (gemm_fp8_256.hip): one workgroup per CU, so it pays when the tile count fills
+// whole rounds of the 256 CUs; RINGDP_FP8_TILE=128 / 256 forces a path (A/B measurements).
+static int g_fp8_tile = -1;  // -1: not read yet; 0 auto; 128 / 256 forced
+static int fp8_tile_mode() {
+  if (g_fp8_tile < 0) {
+    const char* v = getenv("RINGDP_FP8_TILE");
+    g_fp8_tile = v ? atoi(v) : 0;
+  }
+  return g_fp8_tile;
+}
+void set_fp8_tile_mode(int mode) { g_fp8_tile = mode; }
+static double fp8_256_fill(int64_t tiles) {
+  const int64_t rounds = (tiles + 255) / 256;
+  return rounds > 0 ? (double)tiles / (256.0 * rounds) : 0.0;
+}
+// Measured (tools/gemm_bench.py --vit-fp8, ViT-B/16 shapes): the 256 kernel wins on the long-K split-K
+// weight gradients (K = 25216 tokens: 74-86 us vs 95-118 us at >= 27 output tiles) and on K >= 4096
+// (8192^3: 1.95 vs 1.67 PF/s), and loses on short-K single-pass GEMMs (K = 768 / 3072 over 25216 rows:
+// 6-24 k-steps per tile do not amortise its one-workgroup-per-CU prologue and epilogue).
+static bool fp8_use_256(int M, int N, int Kbytes, int batch, int splits) {
+  const int mode = fp8_tile_mode();
+  if (mode == 128) return false;
+  if (mode == 256) return true;
+  const int64_t out_tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
+  const int64_t tiles = out_tiles * std::max(1, splits);
+  if (tiles < 192 || fp8_256_fill(tiles) < 0.75) return false;
+  return splits > 1 ? out_tiles >= 16 : Kbytes >= 4096;
+}
+
+int gemm_fp8_pick_splits(int M, int N, int Kbytes, int requested) {
+  if (requested <= 1 || fp8_tile_mode() == 128) return std::max(1, requested);
+  const int64_t tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  const int maxs = std::max(1, std::min(32, Kbytes / 256));  // >= 2 k-steps per split
+  int best = 0;
+  double best_fill = 0.0;
+  for (int sp = 1; sp <= maxs; ++sp) {
+    const int64_t t = tiles * sp;
+    if (t < 192) continue;
+    const double f = fp8_256_fill(t) - 0.002 * sp;  // prefer fewer fp32 partial planes on a tie
+    if (f > best_fill) {
+      best_fill = f;
+      best = sp;
+    }
+  }
+  return best > 0 && fp8_use_256(M, N, Kbytes, 1, best) ? best : requested;
+}
+
 void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes, const GemmEpilogue& ep,
               int splits, hipStream_t s) {
+  if (fp8_use_256(M, N, Kbytes, batch, splits) && gemm_fp8_256(A, B, batch, M, N, Kbytes, ep, splits, s)) return;
   // K-contiguous e4m3 operands viewed as bf16 "slots" of 2 bytes for the 16-B stagers
   const DenseLoader da{static_cast<const bf16*>(A.p), A.ld / 2, A.bstride / 2, M, Kbytes / 2};
   const DenseLoader db{static_cast<const bf16*>(B.p), B.ld / 2, B.bstride / 2, N, Kbytes / 2};

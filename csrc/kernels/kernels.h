@@ -128,6 +128,12 @@ void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int
 // MFMA (v_mfma_scale_f32_16x16x128_f8f6f4, unit block scales; per-tensor scales via ep.scale_a/b).
 void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes, const GemmEpilogue& ep,
               int splits, hipStream_t s);
+// the 256x256 e4m3 kernel behind gemm_fp8 (false = shape not supported, nothing launched)
+bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes,
+                  const GemmEpilogue& ep, int splits, hipStream_t s);
+// split-K count gemm_fp8 should be called with for an (M x N) fp32-partial GEMM (fills whole CU rounds)
+int gemm_fp8_pick_splits(int M, int N, int Kbytes, int requested);
+void set_fp8_tile_mode(int mode);  // 0 auto, 128 / 256 force a kernel (tests, A/B runs)
 // per-tensor fp8 quantisation (fp8.hip): amax -> scale = amax / 448 -> e4m3, optionally transposed
 void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s);
 void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, const float* amax, void* out,

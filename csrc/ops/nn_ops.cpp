@@ -540,6 +540,8 @@ at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
   return c;
 }
 
+void set_fp8_tile_mode(int64_t mode) { kern::set_fp8_tile_mode((int)mode); }
+
 void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a,
                          const at::Tensor& scale_b, int64_t M, int64_t N, int64_t K, int64_t splits, at::Tensor out) {
   gpu(a, "fp8 A");
@@ -547,6 +549,7 @@ void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Ten
   f32_gpu(out, "fp8 gemm out");
   RINGDP_CHECK(K % 16 == 0 && out.numel() == M * N, "gemm_fp8_splitk_f32: bad shapes");
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 128)));
+  splits = kern::gemm_fp8_pick_splits((int)M, (int)N, (int)K, (int)splits);
   at::Tensor part = at::empty({splits, M, N}, out.options());
   kern::GemmEpilogue e{};
   e.mode = kern::GemmEpilogue::kSplitK;

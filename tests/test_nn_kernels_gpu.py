@@ -343,10 +343,20 @@ def test_fp8_delayed_scaling():
     torch.testing.assert_close(s3[0], hist[0] / 448.0, rtol=1e-6, atol=0)
 
 
-def test_fp8_quantize_and_gemm():
-    """References in float64: fp32 torch matmuls on this ROCm build are not full-precision."""
+@pytest.mark.parametrize("tile", [128, 256])
+def test_fp8_quantize_and_gemm(tile):
+    """References in float64: fp32 torch matmuls on this ROCm build are not full-precision.  Both fp8
+    kernels (generic 128x128 core, 256x256 DMA-pipelined) on shapes with partial edge tiles."""
+    C().set_fp8_tile_mode(tile)
+    try:
+        _fp8_gemm_checks()
+    finally:
+        C().set_fp8_tile_mode(0)
+
+
+def _fp8_gemm_checks():
     torch.manual_seed(0)
-    M, N, K = 320, 272, 768
+    M, N, K = 384, 272, 768
     a = torch.randn(M, K, device="cuda").bfloat16()
     b = torch.randn(N, K, device="cuda").bfloat16()
     qa, sa = C().fp8_quantize(a, False)
@@ -367,6 +377,11 @@ def test_fp8_quantize_and_gemm():
     bias = torch.randn(N, device="cuda")
     out2 = C().gemm_fp8(qa, qb, sa, sb, M, N, K, True, bias, 2)
     assert rel(out2.double(), F.gelu(ref + bias.double())) < 2e-2
+    res = torch.randn(M, N, device="cuda").bfloat16()
+    pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    out3 = C().gemm_fp8(qa, qb, sa, sb, M, N, K, True, bias, 2, res, pre)
+    assert rel(pre.double(), ref + bias.double()) < 1e-2
+    assert rel(out3.double(), F.gelu(ref + bias.double() + res.double())) < 2e-2
     part = torch.empty(N, K, device="cuda")
     qat, sat = C().fp8_quantize(a, True)  # [K][M]
     g = torch.randn(M, N, device="cuda").bfloat16()

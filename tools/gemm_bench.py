@@ -72,8 +72,33 @@ def attention(BH=1536, Tp=208, Dh=64):
     return {"shape": f"attention BH{BH} Tp{Tp} Dh{Dh}", **{n: round(v, 1) for n, v in res.items()}}
 
 
+def vit_fp8_layer(M=25216, D=768, F=3072):
+    """The 12 fp8 GEMMs of one ViT-B/16 block as ringdp/ops/transformer.py issues them (us each)."""
+    from ringdp.ops.transformer import _splits
+    one = torch.ones(1, device="cuda")
+    q = lambda r, c: torch.randn(r, c, device="cuda").to(torch.float8_e4m3fn).view(torch.uint8)
+    res = {}
+    for name, n_out, k_in in (("qkv", 3 * D, D), ("proj", D, D), ("fc1", F, D), ("fc2", D, F)):
+        x, w, wt, dz = q(M, k_in), q(n_out, k_in), q(k_in, n_out), q(M, n_out)
+        xt, dzt = q(k_in, M), q(n_out, M)
+        dw = torch.empty(n_out, k_in, device="cuda")
+        f = timeit(lambda: C.gemm_fp8(x, w, one, one, M, n_out, k_in, True))
+        d = timeit(lambda: C.gemm_fp8(dz, wt, one, one, M, k_in, n_out, True))
+        sp = _splits(M, n_out, k_in)
+        g = timeit(lambda: C.gemm_fp8_splitk_f32(dzt, xt, one, one, n_out, k_in, M, sp, dw))
+        fl = 2 * M * n_out * k_in / 1e6
+        res[name] = {"fwd": [round(f, 1), round(fl / f, 0)], "dgrad": [round(d, 1), round(fl / d, 0)],
+                     "wgrad": [round(g, 1), round(fl / g, 0)], "splits": sp}
+    return res
+
+
 if __name__ == "__main__":
     out = []
+    if "--vit-fp8" in sys.argv:
+        print(json.dumps(vit_fp8_layer()), flush=True)
+        for args in [(4096, 4096, 4096), (8192, 8192, 8192)]:
+            print(json.dumps(dense_fp8(*args)), flush=True)
+        sys.exit(0)
     if "--attention" in sys.argv:
         print(json.dumps(attention()), flush=True)
         sys.exit(0)
