@@ -192,6 +192,10 @@ void qkv_merge(const void* dq, const void* dk, const void* dv, int B, int T, int
 void heads_to_rows(const void* o, int B, int T, int H, int Dh, int Tp, void* rows, hipStream_t s);
 void rows_to_heads(const void* rows, int B, int T, int H, int Dh, int Tp, void* o, hipStream_t s);
 void softmax_fwd(const float* scores, int64_t rows, int T, int Tp, float scale, void* p, hipStream_t s);
+// fused attention forward (head dim 64, Tp % 16 == 0, Tp <= 256): P = softmax(scale Q K^T) over the T real
+// keys (bf16 [BH][Tp][Tp], padded query rows 0) and O = P V (bf16 [BH][Tp][64]); false = unsupported shape
+bool attn_fwd(const void* q, const void* k, const void* v, int BH, int T, int Tp, int Dh, float scale, void* p,
+              void* o, hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);
 void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s);
 void assemble_tokens(const void* patches, const float* cls, const float* pos, int B, int NP, int D, void* out,

@@ -501,6 +501,138 @@ void softmax_fwd(const float* scores, int64_t rows, int T, int Tp, float scale, 
     softmax_fwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(scores, rows, T, Tp, scale, static_cast<bf16*>(p));
 }
 
+namespace {
+
+// Fused attention forward for head dim 64 and Tp <= 256 (ViT-B/16: Tp = 208): per (batch, head) one
+// 256-thread workgroup holds K and V in LDS (2 x Tp x 128 B, XOR-swizzled) and each wave walks 16-query
+// tiles.  S^T = K Q^T is computed tile by tile (v_mfma_f32_16x16x32_bf16, keys as rows), so lane (g, q)
+// holds keys 16t + 4g .. +3 of query q = lane & 15 in every key tile: the softmax over a query's keys is an
+// in-lane reduction plus two xor-shuffles, and the same registers, as bf16, ARE the B operand of
+// O^T = V^T P^T when the MFMA's k index is permuted to (tile pair, 4g + j) - the V^T fragment reads that
+// same key order with ds_read_b64_tr_b16.  S never leaves registers (the unfused path wrote it as fp32:
+// 2 x Tp^2 x 4 B per head of HBM traffic plus a softmax pass); P is still stored (bf16) for the backward.
+// Semantics match softmax_fwd + the P V GEMM: keys >= T get probability 0, padded query rows are 0.
+constexpr int ATT_D = 64;
+__device__ __forceinline__ int att_ksw(int r, int d) { return r * ATT_D + ((((d >> 3) ^ (r & 7))) << 3) + (d & 7); }
+__device__ __forceinline__ int att_vsw(int r, int d) {
+  return r * ATT_D + ((((d >> 4) ^ ((r >> 1) & 3))) << 4) + (d & 15);
+}
+
+template <int NT>  // key tiles of 16 (Tp = 16 * NT)
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ q, const bf16* __restrict__ k,
+                                                       const bf16* __restrict__ v, int T, float scale,
+                                                       bf16* __restrict__ p, bf16* __restrict__ o) {
+  constexpr int Tp = 16 * NT;
+  __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
+  __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t bh = blockIdx.x;
+  const bf16* kb = k + bh * Tp * ATT_D;
+  const bf16* vb = v + bh * Tp * ATT_D;
+  for (int c = tid; c < Tp * 8; c += 256) {  // 16-B chunks: row c >> 3, columns 8 (c & 7) ..
+    const int r = c >> 3, d = (c & 7) * 8;
+    *reinterpret_cast<bf16x8*>(Ks + att_ksw(r, d)) = reinterpret_cast<const bf16x8*>(kb)[c];
+    *reinterpret_cast<bf16x8*>(Vs + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(vb)[c];
+  }
+  __syncthreads();
+  const int g = lane >> 4, qi = lane & 15;
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int qrow = qt * 16 + qi;
+    const bf16* qp = q + (bh * Tp + qrow) * ATT_D + 8 * g;
+    const bf16x8 qf0 = *reinterpret_cast<const bf16x8*>(qp);
+    const bf16x8 qf1 = *reinterpret_cast<const bf16x8*>(qp + 32);
+    f32x4 st[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int kr = 16 * t + qi;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ks + att_ksw(kr, 8 * g));
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ks + att_ksw(kr, 32 + 8 * g));
+      st[t] = mfma16x16x32(a1, qf1, mfma16x16x32(a0, qf0, zero_f32x4()));
+    }
+    // softmax over keys for query qrow: lane holds keys 16t + 4g + i
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float x = 16 * t + 4 * g + i < T ? st[t][i] * scale : -INFINITY;
+        st[t][i] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = 16 * t + 4 * g + i < T ? __expf(st[t][i] - mx) : 0.f;
+        st[t][i] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = qrow < T ? 1.f / sum : 0.f;  // padded query rows: P = 0
+    bf16x4 pb[NT];
+    bf16* prow = p + (bh * Tp + qrow) * Tp + 4 * g;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      pb[t] = bf16x4{(bf16)(st[t][0] * inv), (bf16)(st[t][1] * inv), (bf16)(st[t][2] * inv), (bf16)(st[t][3] * inv)};
+      *reinterpret_cast<bf16x4*>(prow + 16 * t) = pb[t];
+    }
+    // O^T[d][q] = sum over key pairs (t0, t1) of V^T (keys 16t + 4g + j) x P^T
+    f32x4 ot[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) ot[dt] = zero_f32x4();
+    const int q4 = qi >> 2, p4 = qi & 3;  // tr16 lane roles inside the 16-lane group
+#pragma unroll
+    for (int ks = 0; ks < (NT + 1) / 2; ++ks) {
+      const int t0 = 2 * ks, t1 = 2 * ks + 1 < NT ? 2 * ks + 1 : t0;  // odd NT: the missing tile has P = 0
+      const bf16x4 p1 = 2 * ks + 1 < NT ? pb[2 * ks + 1] : bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      const bf16x8 bfr = bf16x8{pb[t0][0], pb[t0][1], pb[t0][2], pb[t0][3], p1[0], p1[1], p1[2], p1[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x4 lo = lds_read_tr16(Vs + att_vsw(16 * t0 + 4 * g + q4, 16 * dt + 4 * p4));
+        const bf16x4 hi = lds_read_tr16(Vs + att_vsw(16 * t1 + 4 * g + q4, 16 * dt + 4 * p4));
+        const bf16x8 afr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        ot[dt] = mfma16x16x32(afr, bfr, ot[dt]);
+      }
+    }
+    bf16* orow = o + (bh * Tp + qrow) * ATT_D + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      *reinterpret_cast<bf16x4*>(orow + 16 * dt) =
+          bf16x4{(bf16)ot[dt][0], (bf16)ot[dt][1], (bf16)ot[dt][2], (bf16)ot[dt][3]};
+  }
+}
+
+template <int NT>
+void attn_fwd_launch(const void* q, const void* k, const void* v, int BH, int T, float scale, void* p, void* o,
+                     hipStream_t s) {
+  attn_fwd_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(q), static_cast<const bf16*>(k),
+                                         static_cast<const bf16*>(v), T, scale, static_cast<bf16*>(p),
+                                         static_cast<bf16*>(o));
+}
+
+}  // namespace
+
+bool attn_fwd(const void* q, const void* k, const void* v, int BH, int T, int Tp, int Dh, float scale, void* p,
+              void* o, hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
+  switch (Tp / 16) {
+#define RINGDP_ATT_CASE(n) \
+  case n:                 \
+    attn_fwd_launch<n>(q, k, v, BH, T, scale, p, o, s); \
+    return true;
+    RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
+    RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)
+    RINGDP_ATT_CASE(11) RINGDP_ATT_CASE(12) RINGDP_ATT_CASE(13) RINGDP_ATT_CASE(14) RINGDP_ATT_CASE(15)
+    RINGDP_ATT_CASE(16)
+#undef RINGDP_ATT_CASE
+  }
+  return false;
+}
+
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s) {
   if (Tp <= 256 && Tp % 4 == 0)
     softmax_bwd_vec_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(static_cast<const bf16*>(p), dp, rows, T, Tp, scale,

@@ -410,6 +410,23 @@ at::Tensor softmax_fwd(const at::Tensor& scores, int64_t T, double scale) {
   return p;
 }
 
+std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t T,
+                                 double scale) {
+  bf16_gpu(q, "attention q");
+  bf16_gpu(k, "attention k");
+  bf16_gpu(v, "attention v");
+  RINGDP_CHECK(q.dim() == 3 && q.sizes() == k.sizes() && q.sizes() == v.sizes() && q.is_contiguous() &&
+                   k.is_contiguous() && v.is_contiguous(),
+               "attn_fwd: q, k, v must be contiguous [BH, Tp, Dh]");
+  const int64_t BH = q.size(0), Tp = q.size(1), Dh = q.size(2);
+  at::Tensor p = at::empty({BH, Tp, Tp}, q.options());
+  at::Tensor o = at::empty({BH, Tp, Dh}, q.options());
+  const bool ok = kern::attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), (int)BH, (int)T, (int)Tp, (int)Dh,
+                                 (float)scale, p.data_ptr(), o.data_ptr(), stream_of(q));
+  RINGDP_CHECK(ok, "attn_fwd: unsupported shape (needs head dim 64, Tp % 16 == 0, Tp <= 256)");
+  return {p, o};
+}
+
 at::Tensor softmax_bwd(const at::Tensor& p, const at::Tensor& dp, int64_t T, double scale) {
   bf16_gpu(p, "attention probs");
   f32_gpu(dp, "attention probs grad");

@@ -18,6 +18,8 @@ from .._native import C
 from . import grad_buffer
 
 _ONES: Dict[Tuple[int, torch.device], torch.Tensor] = {}
+# RINGDP_ATTN_UNFUSED=1: attention forward as two GEMMs + a softmax pass (the path the fused kernel replaced)
+_ATTN_UNFUSED = os.environ.get("RINGDP_ATTN_UNFUSED", "0") == "1"
 _FP8 = {"on": False}
 
 
@@ -212,11 +214,15 @@ class AttentionF(torch.autograd.Function):
         q, k, v = C.qkv_split(qkv, B, T, H, Tp)
         BH, _, Dh = q.shape
         scale = 1.0 / math.sqrt(Dh)
-        # S = Q K^T (fp32), P = softmax(scale * S) over the T real keys
-        s = C.gemm(q, k, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
-        p = C.softmax_fwd(s, T, scale)
-        # O = P V:  A = P (K-contiguous over keys), B = V^T (row-contiguous: element (d, t) = V[t][d])
-        o = C.gemm(p, v, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
+        if Dh == 64 and Tp <= 256 and not _ATTN_UNFUSED:
+            # one kernel: S stays in registers, P (for the backward) and O are written
+            p, o = C.attn_fwd(q, k, v, T, scale)
+        else:
+            # S = Q K^T (fp32), P = softmax(scale * S) over the T real keys
+            s = C.gemm(q, k, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
+            p = C.softmax_fwd(s, T, scale)
+            # O = P V:  A = P (K-contiguous over keys), B = V^T (row-contiguous: element (d, t) = V[t][d])
+            o = C.gemm(p, v, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
         ctx.save_for_backward(q, k, v, p)
         ctx.cfg = (B, T, H, Tp, scale)
         return C.heads_to_rows(o.view(BH, Tp, Dh), B, T)

@@ -415,3 +415,29 @@ def test_vit_fp8_close_to_bf16():
     assert _cos(out.detach(), out8.detach()) > 0.98
     for (n, p), (_, q) in zip(m.named_parameters(), m8.named_parameters()):
         assert _cos(p.grad, q.grad) > 0.9, n
+
+
+@pytest.mark.parametrize("T", [197, 16, 33, 60])
+def test_fused_attention_forward(T):
+    """attn_fwd (one kernel: S in registers) against an fp32 reference and the unfused GEMM path."""
+    torch.manual_seed(T)
+    BH, Dh = 6, 64
+    Tp = (T + 15) // 16 * 16
+    q, k, v = (torch.randn(BH, Tp, Dh, device="cuda").bfloat16() for _ in range(3))
+    scale = 1.0 / Dh ** 0.5
+    p, o = C().attn_fwd(q, k, v, T, scale)
+    s = (q.float() @ k.float().transpose(1, 2)) * scale
+    s[:, :, T:] = -float("inf")
+    pr = torch.softmax(s, -1)
+    pr[:, T:, :] = 0
+    assert (p[:, :, T:] == 0).all() and (p[:, T:, :] == 0).all()
+    torch.testing.assert_close(p.float(), pr, atol=4e-3, rtol=2e-2)
+    ref_o = p.float() @ v.float()  # on the kernel's own bf16 P: only accumulation order differs
+    torch.testing.assert_close(o.float(), ref_o, atol=2e-2, rtol=2e-2)
+    assert rel(o.float(), pr @ v.float()) < 1e-2
+    # the unfused path this kernel replaces (two GEMMs + softmax) gives the same P and O
+    s2 = C().gemm(q, k, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
+    p2 = C().softmax_fwd(s2, T, scale)
+    o2 = C().gemm(p2, v, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
+    assert (p.float() - p2.float()).abs().max() <= 1.6e-2
+    assert rel(o.float(), o2.float()) < 1e-2
