@@ -196,6 +196,9 @@ void softmax_fwd(const float* scores, int64_t rows, int T, int Tp, float scale, 
 // keys (bf16 [BH][Tp][Tp], padded query rows 0) and O = P V (bf16 [BH][Tp][64]); false = unsupported shape
 bool attn_fwd(const void* q, const void* k, const void* v, int BH, int T, int Tp, int Dh, float scale, void* p,
               void* o, hipStream_t s);
+// fused dP = dO V^T + softmax backward: dS = scale * P * (dP - rowsum(dP * P)) (bf16 [BH][Tp][Tp])
+bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp, int Dh, float scale, void* ds,
+                 hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);
 void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s);
 void assemble_tokens(const void* patches, const float* cls, const float* pos, int B, int NP, int D, void* out,

@@ -606,6 +606,67 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// Fused attention backward front half: dS = scale * P * (dP - rowsum(dP * P)) with dP = dO V^T computed
+// per 16-query tile as dP^T = V dO^T in registers (same lane layout as the forward's S^T: lane (g, q) holds
+// keys 16t + 4g .. +3 of query q), so the fp32 dP never goes to memory (the unfused path wrote and re-read
+// 2 x Tp^2 x 4 B per head).  Same semantics as softmax_bwd: padded keys / queries get dS = 0.
+template <int NT>
+__global__ __launch_bounds__(256) void attn_bwd_ds_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ v,
+                                                          const bf16* __restrict__ p, float scale,
+                                                          bf16* __restrict__ ds) {
+  constexpr int Tp = 16 * NT;
+  __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t bh = blockIdx.x;
+  const bf16* vb = v + bh * Tp * ATT_D;
+  for (int c = tid; c < Tp * 8; c += 256) {
+    const int r = c >> 3, d = (c & 7) * 8;
+    *reinterpret_cast<bf16x8*>(Vs + att_ksw(r, d)) = reinterpret_cast<const bf16x8*>(vb)[c];
+  }
+  __syncthreads();
+  const int g = lane >> 4, qi = lane & 15;
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int qrow = qt * 16 + qi;
+    const bf16* dp_ = dout + (bh * Tp + qrow) * ATT_D + 8 * g;
+    const bf16x8 of0 = *reinterpret_cast<const bf16x8*>(dp_);
+    const bf16x8 of1 = *reinterpret_cast<const bf16x8*>(dp_ + 32);
+    const bf16* prow = p + (bh * Tp + qrow) * Tp + 4 * g;
+    bf16x4 pv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) pv[t] = *reinterpret_cast<const bf16x4*>(prow + 16 * t);
+    f32x4 dpt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int vr = 16 * t + qi;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Vs + att_ksw(vr, 8 * g));
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Vs + att_ksw(vr, 32 + 8 * g));
+      dpt[t] = mfma16x16x32(a1, of1, mfma16x16x32(a0, of0, zero_f32x4()));
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dot = fmaf(dpt[t][i], (float)pv[t][i], dot);
+    dot += __shfl_xor(dot, 16, 64);
+    dot += __shfl_xor(dot, 32, 64);
+    bf16* drow = ds + (bh * Tp + qrow) * Tp + 4 * g;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      bf16x4 r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = (bf16)(scale * (float)pv[t][i] * (dpt[t][i] - dot));
+      *reinterpret_cast<bf16x4*>(drow + 16 * t) = r;
+    }
+  }
+}
+
+template <int NT>
+void attn_bwd_ds_launch(const void* dout, const void* v, const void* p, int BH, float scale, void* ds,
+                        hipStream_t s) {
+  attn_bwd_ds_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(dout), static_cast<const bf16*>(v),
+                                            static_cast<const bf16*>(p), scale, static_cast<bf16*>(ds));
+}
+
 template <int NT>
 void attn_fwd_launch(const void* q, const void* k, const void* v, int BH, int T, float scale, void* p, void* o,
                      hipStream_t s) {
@@ -623,6 +684,23 @@ bool attn_fwd(const void* q, const void* k, const void* v, int BH, int T, int Tp
 #define RINGDP_ATT_CASE(n) \
   case n:                 \
     attn_fwd_launch<n>(q, k, v, BH, T, scale, p, o, s); \
+    return true;
+    RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
+    RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)
+    RINGDP_ATT_CASE(11) RINGDP_ATT_CASE(12) RINGDP_ATT_CASE(13) RINGDP_ATT_CASE(14) RINGDP_ATT_CASE(15)
+    RINGDP_ATT_CASE(16)
+#undef RINGDP_ATT_CASE
+  }
+  return false;
+}
+
+bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp, int Dh, float scale, void* ds,
+                 hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16) return false;
+  switch (Tp / 16) {
+#define RINGDP_ATT_CASE(n) \
+  case n:                 \
+    attn_bwd_ds_launch<n>(dout, v, p, BH, scale, ds, s); \
     return true;
     RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
     RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)

@@ -427,6 +427,21 @@ std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const
   return {p, o};
 }
 
+at::Tensor attn_bwd_ds(const at::Tensor& dout, const at::Tensor& v, const at::Tensor& p, double scale) {
+  bf16_gpu(dout, "attention dO");
+  bf16_gpu(v, "attention v");
+  bf16_gpu(p, "attention probs");
+  RINGDP_CHECK(dout.dim() == 3 && dout.sizes() == v.sizes() && p.dim() == 3 && p.size(0) == v.size(0) &&
+                   p.size(1) == v.size(1) && p.size(2) == v.size(1) && dout.is_contiguous() && v.is_contiguous() &&
+                   p.is_contiguous(),
+               "attn_bwd_ds: expected contiguous dO, V [BH, Tp, Dh] and P [BH, Tp, Tp]");
+  at::Tensor ds = at::empty_like(p);
+  const bool ok = kern::attn_bwd_ds(dout.data_ptr(), v.data_ptr(), p.data_ptr(), (int)v.size(0), (int)v.size(1),
+                                    (int)v.size(2), (float)scale, ds.data_ptr(), stream_of(p));
+  RINGDP_CHECK(ok, "attn_bwd_ds: unsupported shape (needs head dim 64, Tp % 16 == 0, Tp <= 256)");
+  return ds;
+}
+
 at::Tensor softmax_bwd(const at::Tensor& p, const at::Tensor& dp, int64_t T, double scale) {
   bf16_gpu(p, "attention probs");
   f32_gpu(dp, "attention probs grad");

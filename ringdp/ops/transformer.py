@@ -234,8 +234,11 @@ class AttentionF(torch.autograd.Function):
         BH, _, Dh = q.shape
         do = C.rows_to_heads(dout.contiguous(), B, T, H, Tp)
         # dP = dO V^T (fp32) -> dS = scale * P * (dP - rowsum(dP * P))
-        dp = C.gemm(do, v, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
-        ds = C.softmax_bwd(p, dp, T, scale)
+        if Dh == 64 and Tp <= 256 and not _ATTN_UNFUSED:
+            ds = C.attn_bwd_ds(do, v, p, scale)  # dP stays in registers
+        else:
+            dp = C.gemm(do, v, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
+            ds = C.softmax_bwd(p, dp, T, scale)
         # dQ = dS K ; dK = dS^T Q ; dV = P^T dO
         dq = C.gemm(ds, k, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
         dk = C.gemm(ds, q, Tp, Dh, Tp, Tp, Dh, True, True, BH, Tp * Tp, Tp * Dh, True)

@@ -441,3 +441,13 @@ def test_fused_attention_forward(T):
     o2 = C().gemm(p2, v, Tp, Dh, Tp, Tp, Dh, False, True, BH, Tp * Tp, Tp * Dh, True)
     assert (p.float() - p2.float()).abs().max() <= 1.6e-2
     assert rel(o.float(), o2.float()) < 1e-2
+    # backward front half: fused dS against the unfused dP GEMM + softmax_bwd
+    do = torch.randn(BH, Tp, Dh, device="cuda").bfloat16()
+    ds = C().attn_bwd_ds(do, v, p, scale)
+    dp = C().gemm(do, v, Tp, Tp, Dh, Dh, Dh, False, False, BH, Tp * Dh, Tp * Dh, False)
+    ds2 = C().softmax_bwd(p, dp, T, scale)
+    dpr = do.float() @ v.float().transpose(1, 2)
+    dsr = scale * p.float() * (dpr - (dpr * p.float()).sum(-1, keepdim=True))
+    assert (ds[:, :, T:] == 0).all() and (ds[:, T:, :] == 0).all()
+    assert rel(ds.float(), dsr) < 1e-2
+    assert rel(ds.float(), ds2.float()) < 1e-2
