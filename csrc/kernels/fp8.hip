@@ -77,12 +77,15 @@ __global__ __launch_bounds__(256) void quant_kernel(const bf16* __restrict__ x, 
 // Delayed scaling (amax_next != null): the scale comes from a previous amax, so values are clamped to
 // the e4m3 range before conversion, and each 64x64 tile's |x|max is stored to amax_next[tile] for the
 // next call's roll - no separate amax pass over x.
+// colsum != null: also this tile's 64 column sums of x (fp32, over its 64 rows; a fixed-order tree) to
+// colsum[blockIdx.y][cols] - the bias gradient of a linear layer rides on the quantisation of dz.
 __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
                                                       const float* __restrict__ amax, uint8_t* __restrict__ out,
                                                       float* __restrict__ scale, uint8_t* __restrict__ out_rm,
-                                                      unsigned* __restrict__ amax_next) {
+                                                      unsigned* __restrict__ amax_next, float* __restrict__ colsum) {
   __shared__ float tile[64][65];
   __shared__ float red[4];
+  __shared__ float csum[4][64];
   const float inv = 1.f / qscale(amax);
   const float lim = amax_next ? kE4M3Max : INFINITY;
   float bmax = 0.f;
@@ -90,6 +93,7 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
   const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
   const int t = threadIdx.x;
   // load: 64 rows x 8 vectors of 8 -> thread t: row t/4 (+0, +64..) -> use 2 passes of 32 rows
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int pass = 0; pass < 2; ++pass) {
     const int r = (t >> 3) + 32 * pass, cv = t & 7;
     const int64_t gr = r0 + r, gc = c0 + cv * 8;
@@ -99,6 +103,7 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
     for (int j = 0; j < 8; ++j) {
       const float f = (float)v[j];
       bmax = fmaxf(bmax, fabsf(f));
+      cs[j] += f;
       tile[r][cv * 8 + j] = fminf(fmaxf(f * inv, -lim), lim);
     }
     if (out_rm && gr < rows && gc < cols) {
@@ -119,6 +124,21 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
     for (int q = 0; q < 4; ++q)
       w[q] = pack4(tile[seg + 4 * q][oc], tile[seg + 4 * q + 1][oc], tile[seg + 4 * q + 2][oc], tile[seg + 4 * q + 3][oc]);
     *reinterpret_cast<uint4*>(out + gr * rows + r0 + seg) = o;
+  }
+  if (colsum) {  // lanes with equal t & 7 hold the same 8 columns: xor 8 / 16 / 32, then the 4 waves
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cs[j] += __shfl_xor(cs[j], 8, 64);
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+    }
+    if ((t & 63) < 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) csum[t >> 6][(t & 7) * 8 + j] = cs[j];
+    }
+    __syncthreads();
+    if (t < 64 && c0 + t < cols)
+      colsum[(int64_t)blockIdx.y * cols + c0 + t] = (csum[0][t] + csum[1][t]) + (csum[2][t] + csum[3][t]);
   }
   if (amax_next) {  // this tile's |x|max -> its own slot (thousands of same-address atomics serialise)
     bmax = wave_max(bmax);
@@ -150,7 +170,76 @@ __global__ __launch_bounds__(1024) void amax_roll_kernel(float* __restrict__ his
   }
 }
 
+// part[blockIdx.y][c] = sum of x[r][c] over rows [blockIdx.y * rows_per, +rows_per): 64 columns per block,
+// 32 row lanes x 8 columns per thread, a fixed-order tree at the end (deterministic).
+__global__ __launch_bounds__(256) void colsum_part_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
+                                                          int64_t rows_per, float* __restrict__ part) {
+  __shared__ float csum[4][64];
+  const int t = threadIdx.x, cv = t & 7;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cv * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per, r1 = min(rows, r0 + rows_per);
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cols) {
+    for (int64_t r = r0 + (t >> 3); r < r1; r += 32) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + r * cols + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) cs[j] += (float)v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    cs[j] += __shfl_xor(cs[j], 8, 64);
+    cs[j] += __shfl_xor(cs[j], 16, 64);
+    cs[j] += __shfl_xor(cs[j], 32, 64);
+  }
+  if ((t & 63) < 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) csum[t >> 6][cv * 8 + j] = cs[j];
+  }
+  __syncthreads();
+  const int64_t cc = (int64_t)blockIdx.x * 64 + t;
+  if (t < 64 && cc < cols) part[(int64_t)blockIdx.y * cols + cc] = (csum[0][t] + csum[1][t]) + (csum[2][t] + csum[3][t]);
+}
+
+// out[c] = sum over s < S of part[s][c]: 64 columns per block as 16 float4 lanes x 16 row lanes (many
+// partial rows - splitk_sum walks them serially per column), then a fixed-order tree (deterministic).
+__global__ __launch_bounds__(256) void rowsum_f32_kernel(const float* __restrict__ part, int S, int64_t n,
+                                                         float* __restrict__ out) {
+  __shared__ f32x4 red[16][16];
+  const int t = threadIdx.x, cl = t & 15, rl = t >> 4;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl * 4;
+  f32x4 a0 = zero_f32x4(), a1 = zero_f32x4();
+  if (c < n) {
+    int s = rl;
+    for (; s + 16 < S; s += 32) {
+      a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)s * n + c);
+      a1 += *reinterpret_cast<const f32x4*>(part + (int64_t)(s + 16) * n + c);
+    }
+    if (s < S) a0 += *reinterpret_cast<const f32x4*>(part + (int64_t)s * n + c);
+  }
+  red[rl][cl] = a0 + a1;
+  __syncthreads();
+  if (t < 16 && (int64_t)blockIdx.x * 64 + t * 4 < n) {
+    f32x4 v = red[0][t];
+    for (int r = 1; r < 16; ++r) v += red[r][t];
+    *reinterpret_cast<f32x4*>(out + (int64_t)blockIdx.x * 64 + t * 4) = v;
+  }
+}
+
 }  // namespace
+
+void rowsum_f32(const float* part, int S, int64_t n, float* out, hipStream_t s) {
+  rowsum_f32_kernel<<<(unsigned)((n + 63) / 64), 256, 0, s>>>(part, S, n, out);
+}
+
+int colsum_parts(int64_t rows) { return (int)std::max<int64_t>(1, std::min<int64_t>(64, (rows + 255) / 256)); }
+
+void colsum_bf16(const void* x, int64_t rows, int64_t cols, float* part, hipStream_t s) {
+  const int parts = colsum_parts(rows);
+  const int64_t rows_per = (rows + parts - 1) / parts;
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)parts);
+  colsum_part_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, rows_per, part);
+}
 
 void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s) {
   hipMemsetAsync(amax, 0, sizeof(float), s);
@@ -168,19 +257,20 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
   } else {
     dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
     quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, amax, static_cast<uint8_t*>(out),
-                                        scale, static_cast<uint8_t*>(out_rowmajor), nullptr);
+                                        scale, static_cast<uint8_t*>(out_rowmajor), nullptr, nullptr);
   }
 }
 
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
-                          float* scale, void* out_rowmajor, hipStream_t s) {
+                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part) {
   dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
   if (init)
     fp8_amax(x, rows * cols, hist, s);  // first use of the site: the exact amax of this tensor
   else
     amax_roll_kernel<<<1, 1024, 0, s>>>(hist, (int)(grid.x * grid.y));
   quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, hist, static_cast<uint8_t*>(out_t),
-                                      scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1));
+                                      scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1),
+                                      colsum_part);
 }
 
 }  // namespace kern

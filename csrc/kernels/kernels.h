@@ -142,7 +142,13 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
 // rolled from the tile maxima (or, init = first call of a site, measured exactly), then x is quantised
 // (q^T into out_t, q into out_rowmajor) while its tile maxima are written for the next call.
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
-                          float* scale, void* out_rowmajor, hipStream_t s);
+                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part = nullptr);
+// column sums of a bf16 [rows][cols] matrix as colsum_parts(rows) fp32 partial rows (sum them with splitk_sum;
+// fp8_quantize_delayed's colsum_part has one partial row per 64-row tile instead)
+int colsum_parts(int64_t rows);
+void colsum_bf16(const void* x, int64_t rows, int64_t cols, float* part, hipStream_t s);
+// out[c] = sum_s part[s][c] for many partial rows (n % 4 == 0), fixed order
+void rowsum_f32(const float* part, int S, int64_t n, float* out, hipStream_t s);
 void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,

@@ -524,7 +524,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both(const at::Tenso
 int64_t fp8_delayed_slots(int64_t rows, int64_t cols) { return ((rows + 63) / 64) * ((cols + 63) / 64); }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const at::Tensor& x, at::Tensor hist,
-                                                                        bool init) {
+                                                                        bool init,
+                                                                        const c10::optional<at::Tensor>& colsum) {
   bf16_gpu(x, "fp8 quantize input");
   RINGDP_CHECK(x.dim() == 2 && x.size(0) % 16 == 0 && x.size(1) % 16 == 0,
                "fp8_quantize_both_delayed: expected a 2-D tensor with dims % 16 == 0");
@@ -534,9 +535,29 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const a
                "fp8 amax history: expected 1 + fp8_delayed_slots(rows, cols) contiguous floats");
   at::Tensor scale = at::empty({1}, x.options().dtype(at::kFloat));
   at::Tensor q = at::empty({R, Cc}, x.options().dtype(at::kByte)), qt = at::empty({Cc, R}, x.options().dtype(at::kByte));
+  at::Tensor part;
+  if (colsum.has_value() && colsum->defined()) {  // column sums of x (a bias gradient) from the same pass
+    f32_gpu(*colsum, "fp8 quantize colsum");
+    RINGDP_CHECK(colsum->numel() == Cc && colsum->is_contiguous(), "fp8 quantize colsum: expected [cols] floats");
+    part = at::empty({(R + 63) / 64, Cc}, x.options().dtype(at::kFloat));
+  }
   kern::fp8_quantize_delayed(x.data_ptr(), R, Cc, hist.data_ptr<float>(), init, qt.data_ptr(), scale.data_ptr<float>(),
-                             q.data_ptr(), stream_of(x));
+                             q.data_ptr(), stream_of(x), part.defined() ? part.data_ptr<float>() : nullptr);
+  if (part.defined())
+    kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), Cc, colsum->data_ptr<float>(), stream_of(x));
   return {q, qt, scale};
+}
+
+void colsum_f32(const at::Tensor& x, at::Tensor out) {
+  bf16_gpu(x, "colsum input");
+  f32_gpu(out, "colsum output");
+  RINGDP_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(1) % 8 == 0 && out.numel() == x.size(1) &&
+                   out.is_contiguous(),
+               "colsum_f32: expected contiguous bf16 [rows, cols % 8 == 0] and fp32 [cols]");
+  const int64_t R = x.size(0), Cc = x.size(1);
+  at::Tensor part = at::empty({kern::colsum_parts(R), Cc}, out.options());
+  kern::colsum_bf16(x.data_ptr(), R, Cc, part.data_ptr<float>(), stream_of(x));
+  kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), Cc, out.data_ptr<float>(), stream_of(x));
 }
 
 at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,

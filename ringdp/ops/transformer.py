@@ -17,7 +17,6 @@ import torch
 from .._native import C
 from . import grad_buffer
 
-_ONES: Dict[Tuple[int, torch.device], torch.Tensor] = {}
 # RINGDP_ATTN_UNFUSED=1: attention forward as two GEMMs + a softmax pass (the path the fused kernel replaced)
 _ATTN_UNFUSED = os.environ.get("RINGDP_ATTN_UNFUSED", "0") == "1"
 _FP8 = {"on": False}
@@ -31,17 +30,6 @@ def set_fp8(on: bool = True) -> None:
 
 def fp8_enabled() -> bool:
     return _FP8["on"]
-
-
-def _ones_col(rows: int, device) -> torch.Tensor:
-    """[rows, 8] bf16 with column 0 = 1: a GEMM against it yields column sums (bias gradients)."""
-    key = (rows, torch.device(device))
-    t = _ONES.get(key)
-    if t is None:
-        t = torch.zeros(rows, 8, device=device, dtype=torch.bfloat16)
-        t[:, 0] = 1
-        _ONES[key] = t
-    return t
 
 
 def _bf16(w: torch.Tensor) -> torch.Tensor:
@@ -115,10 +103,13 @@ class LinearF(torch.autograd.Function):
                 C.gemm_splitk_f32(dz, x, N, K, M, N, K, True, True, _splits(M, N, K), full_w)
                 dw.copy_(full_w[:n_out])
         if b is not None and ctx.needs_input_grad[2]:
-            full = torch.empty(N, 8, device=dy.device, dtype=torch.float32)
-            C.gemm_splitk_f32(dz, _ones_col(M, dy.device), N, 8, M, N, 8, True, True, _splits(M, N, 8), full)
             db = grad_buffer(b)
-            db.copy_(full[:n_out, 0])
+            if N == n_out:
+                C.colsum_f32(dz, db)  # bias gradient = column sums of dz (one read of dz)
+            else:
+                full = torch.empty(N, device=dy.device, dtype=torch.float32)
+                C.colsum_f32(dz, full)
+                db.copy_(full[:n_out])
         dres = dyb if has_res and ctx.needs_input_grad[3] else None
         return dx, dw, db, dres, None, None
 
@@ -126,7 +117,7 @@ class LinearF(torch.autograd.Function):
 _FP8_DELAYED = os.environ.get("RINGDP_FP8_DELAYED", "1") == "1"
 
 
-def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int):
+def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[torch.Tensor] = None):
     """fp8 quantisation of an activation (slot 0: the linear's input x), output gradient (slot 1: dz) or
     the bf16 copy of the weight (slot 2) with per-site delayed scaling (TransformerEngine-style, history length 1), state kept on the weight:
     the first quantisation of a site measures its exact amax; later ones scale by the amax the previous
@@ -142,7 +133,7 @@ def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int):
     init = hist is None or hist.numel() != n
     if init:
         hist = sites[slot] = torch.zeros(n, device=t.device, dtype=torch.float32)
-    return C.fp8_quantize_both_delayed(t, hist, init)
+    return C.fp8_quantize_both_delayed(t, hist, init, colsum)
 
 
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
@@ -168,18 +159,18 @@ def _linear_fp8_bwd(ctx, dy):
     M, K = ctx.shape
     dyb = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
     dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
-    dx = dw = db = None
-    dzq, dztq, sdz = _quant_act(dz, w, 1)  # [M][N] for the data grad, [N][M] for the weight grad
+    dx = dw = None
+    want_db = b is not None and ctx.needs_input_grad[2]
+    db = grad_buffer(b) if want_db and _FP8_DELAYED else None  # column sums of dz from the quantisation pass
+    dzq, dztq, sdz = _quant_act(dz, w, 1, db)  # [M][N] for the data grad, [N][M] for the weight grad
     if ctx.needs_input_grad[0]:
         dx = C.gemm_fp8(dzq, wtq, sdz, sw, M, K, N, True)
     if ctx.needs_input_grad[1]:
         dw = grad_buffer(w)
         C.gemm_fp8_splitk_f32(dztq, xtq, sdz, sx, N, K, M, _splits(M, N, K), dw)
-    if b is not None and ctx.needs_input_grad[2]:
-        full = torch.empty(N, 8, device=dy.device, dtype=torch.float32)
-        C.gemm_splitk_f32(dz, _ones_col(M, dy.device), N, 8, M, N, 8, True, True, _splits(M, N, 8), full)
+    if want_db and db is None:
         db = grad_buffer(b)
-        db.copy_(full[:, 0])
+        C.colsum_f32(dz, db)
     dres = dyb if has_res and ctx.needs_input_grad[3] else None
     return dx, dw, db, dres, None, None
 
@@ -276,10 +267,8 @@ class PatchTokensF(torch.autograd.Function):
         M, K = rows.shape
         dw = grad_buffer(w)
         C.gemm_splitk_f32(demb, rows, D, K, M, D, K, True, True, _splits(M, D, K), dw)
-        full = torch.empty(D, 8, device=dtok.device, dtype=torch.float32)
-        C.gemm_splitk_f32(demb, _ones_col(M, dtok.device), D, 8, M, D, 8, True, True, _splits(M, D, 8), full)
         db = grad_buffer(b)
-        db.copy_(full[:, 0])
+        C.colsum_f32(demb.contiguous(), db)
         return None, dw, db, dcls, dpos, None
 
 

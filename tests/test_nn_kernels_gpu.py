@@ -343,6 +343,27 @@ def test_fp8_delayed_scaling():
     torch.testing.assert_close(s3[0], hist[0] / 448.0, rtol=1e-6, atol=0)
 
 
+def test_column_sums():
+    """Bias gradients: colsum_f32 and the column sums the delayed fp8 quantisation of dz emits."""
+    torch.manual_seed(2)
+    for r, c in [(1000, 72), (25216 // 8, 768), (64, 8)]:
+        x = torch.randn(r, c, device="cuda").bfloat16()
+        ref = x.double().sum(0)
+        out = torch.empty(c, device="cuda")
+        C().colsum_f32(x, out)
+        torch.testing.assert_close(out.double(), ref, atol=1e-3, rtol=1e-4)
+        out2 = torch.empty_like(out)
+        C().colsum_f32(x, out2)
+        assert torch.equal(out, out2)  # fixed summation order
+        if r % 16 == 0 and c % 16 == 0:
+            hist = torch.zeros(1 + C().fp8_delayed_slots(r, c), device="cuda")
+            cs = torch.full((c,), float("nan"), device="cuda")
+            q, qt, s = C().fp8_quantize_both_delayed(x, hist, True, cs)
+            torch.testing.assert_close(cs.double(), ref, atol=1e-3, rtol=1e-4)
+            q0, qt0, s0 = C().fp8_quantize_both(x)
+            assert torch.equal(q, q0) and torch.equal(s, s0)
+
+
 @pytest.mark.parametrize("tile", [128, 256])
 def test_fp8_quantize_and_gemm(tile):
     """References in float64: fp32 torch matmuls on this ROCm build are not full-precision.  Both fp8
