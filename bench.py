@@ -12,13 +12,25 @@ Weights: random init (torch.manual_seed(0), PyTorch default init - identical to 
 Scaling: weak (fixed per-rank batch), like the reference.
 Per-rank batch: 32768 images (the reference runs 100; `--batch-per-rank 100` reproduces that regime).
 The ConvNet is ~44 MFLOP/img, so a 100-image step is launch/latency-bound; 32768 fills 256 CUs and
-amortises the 455 KB gradient all-reduce (measured 1 GPU: 16384 -> 13.6M img/s, 32768 and 65536 ->
-14.1M img/s; activations ~1.5 GB of the 288 GB HBM3E).
+amortises the 455 KB gradient all-reduce (activations ~1.5 GB of the 288 GB HBM3E).
 
-Usage:
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-rank B]
+Launch (one process per GPU, RCCL over xGMI):
+  python bench.py --gpus N ...            N > 1 without WORLD_SIZE in the env: this process starts N
+                                          fresh ranks itself (ringdp.run; ref/mpspawn_dist.py:136-140)
+                                          and never touches the GPU
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
-      bench.py --gpus N --steps K --warmup W
+      bench.py --gpus N ...               the driver's form; ranks read RANK/LOCAL_RANK/WORLD_SIZE
+  python -m ringdp.run --nproc-per-node N bench.py --gpus N ...
+
+The gradient all-reduce runs at every N, including N=1 (a one-rank RCCL communicator, exactly what
+upstream DDP does), so every point of the scaling curve executes the same code path;
+``--no-force-comm`` skips it at N=1.  After the timed region (never inside it) the bench measures
+per-bucket device-timed collective durations over a few eager steps and the step time of a
+comm-free graph; their difference to the timed step is the exposed (non-overlapped) comm time.
+
+``--cpu`` runs the same flow on CPU ranks over the native host-ring ("gloo") backend and the ATen
+ConvNet: a plumbing rehearsal (BASELINE config #1), not a GPU measurement.
+
 Rank 0 prints one JSON line.
 """
 from __future__ import annotations
@@ -50,7 +62,7 @@ MODELS = {
 NUM_CLASSES = {"convnet": 10, "resnet18": 10, "resnet50": 1000, "vit_b_16": 1000}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -64,34 +76,69 @@ def parse():
     ap.add_argument("--comm-hook", type=str, default="allreduce", choices=["allreduce", "bf16_compress", "fp16_compress"])
     ap.add_argument("--no-graph", action="store_true", help="eager steps instead of one hipGraph per step")
     ap.add_argument("--pool", type=int, default=8, help="number of distinct synthetic batches cycled")
-    ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp8"],
-                    help="fp8: e4m3 linear-layer GEMMs on the block-scaled MFMA (vit_b_16)")
+    ap.add_argument("--dtype", type=str, default="bf16", choices=["bf16", "fp8", "fp32"],
+                    help="fp8: e4m3 linear-layer GEMMs on the block-scaled MFMA (vit_b_16); "
+                         "fp32: the ConvNet at the reference's precision (fp32 MFMA kernels)")
+    ap.add_argument("--no-force-comm", action="store_true",
+                    help="at world size 1 skip the bucket all-reduce (default: run it, the N>1 code path)")
+    ap.add_argument("--comm-stats-steps", type=int, default=20,
+                    help="after the timed region: eager steps with device-timed bucket collectives and "
+                         "comm-free graph replays for the exposed-comm estimate (0 = skip)")
+    ap.add_argument("--cpu", action="store_true",
+                    help="CPU ranks on the host-ring ('gloo') backend with the ATen ConvNet (plumbing only)")
     ap.add_argument("--local-rank", "--local_rank", type=int, default=None)
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def _self_launch(args) -> int:
+    """N ranks from one command: fresh interpreters via ringdp.run, before any GPU call here."""
+    from ringdp.run import launch_local
+
+    return launch_local(os.path.abspath(__file__), sys.argv[1:], args.gpus)
+
+
+def _store_agree(dist, key: str, ok: bool, rank: int, world: int) -> bool:
+    """Every rank publishes ``ok`` through the native store and reads everyone's.  Used where the
+    GPU communicator cannot be trusted (e.g. after a failed hipGraph capture)."""
+    st = dist.get_default_store()
+    st.set(f"bench/{key}/{rank}", b"1" if ok else b"0")
+    keys = [f"bench/{key}/{r}" for r in range(world)]
+    st.wait(keys)
+    return all(st.get(k) == b"1" for k in keys)
+
+
+def worker(args):
     import ringdp
     import ringdp.distributed as dist
     from ringdp import models
+    from ringdp._native import C
     from ringdp.nn import CrossEntropyLoss
     from ringdp.optim import SGD
     from ringdp.parallel import DistributedDataParallel as DDP
     from ringdp.utils.graph import StepGraph
 
+    launched = os.environ.get("WORLD_SIZE") is not None
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    rank_env = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", args.local_rank if args.local_rank is not None else 0))
-    torch.cuda.set_device(local_rank)
-    if world_env > 1 or "MASTER_ADDR" in os.environ:
-        dist.init_process_group(backend="nccl")
+    on_gpu = not args.cpu
+    if on_gpu:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        backend = "nccl"
     else:
-        dist.init_process_group(backend="nccl", store=dist.HashStore(), rank=0, world_size=1)
+        dev = torch.device("cpu")
+        backend = "gloo"
+        torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(world_env, 1)))
+    if launched:
+        dist.init_process_group(backend=backend)
+    else:
+        dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1)
     rank, world = dist.get_rank(), dist.get_world_size()
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but world size is {world}; reporting n_gpus={world}", file=sys.stderr)
-    dev = torch.device("cuda", local_rank)
+    force_comm = world == 1 and not args.no_force_comm
+    if force_comm:
+        os.environ["RINGDP_DDP_FORCE_COMM"] = "1"  # read by the reducer per bucket launch
     spec = MODELS[args.model]
     B = args.batch_per_rank or int(os.environ.get("RINGDP_BENCH_BATCH", spec["batch"]))
     lr = args.lr if args.lr is not None else spec["lr"]
@@ -107,26 +154,36 @@ def main():
         set_fp8(True)
     torch.manual_seed(0)
     if args.model == "convnet":
-        model = models.ConvNet().to(dev)
+        model = models.ConvNet(precision="fp32" if args.dtype == "fp32" else "bf16").to(dev)
     else:
+        if args.dtype == "fp32":
+            raise SystemExit("--dtype fp32 is implemented for --model convnet")
         model = getattr(models, args.model)(num_classes=NUM_CLASSES[args.model]).to(dev)
-    ddp = DDP(model, device_ids=[local_rank], output_device=local_rank, bucket_cap_mb=args.bucket_mb,
-              first_bucket_mb=args.first_bucket_mb)
+    ddp = DDP(model, device_ids=[local_rank] if on_gpu else None, output_device=local_rank if on_gpu else None,
+              bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
     if args.comm_hook != "allreduce":
         ddp._set_builtin_hook(args.comm_hook)
     crit = CrossEntropyLoss()
     opt = SGD(ddp.parameters(), lr=lr, momentum=spec["momentum"], nesterov=spec["nesterov"],
               weight_decay=spec["wd"])
 
-    if args.model == "convnet":
-        pool = [ringdp._C.synth_u8_images(B, 28, 28, 10, 1000 * rank + i, dev) for i in range(args.pool)]
+    ncls = NUM_CLASSES[args.model]
+    if args.model == "convnet" and on_gpu:
+        pool = [C.synth_u8_images(B, 28, 28, 10, 1000 * rank + i, dev) for i in range(args.pool)]
+    elif args.model == "convnet":
+        g = torch.Generator().manual_seed(1000 * rank)
+        pool = [(torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, generator=g),
+                 torch.randint(0, ncls, (B,), generator=g)) for _ in range(min(args.pool, 2))]
     else:
         g = torch.Generator(device=dev).manual_seed(1000 * rank)
-        ncls = NUM_CLASSES[args.model]
         pool = [(torch.randn((B,) + spec["shape"], device=dev, generator=g),
                  torch.randint(0, ncls, (B,), device=dev, generator=g)) for _ in range(min(args.pool, 4))]
     static_x = torch.empty_like(pool[0][0])
     static_y = torch.empty_like(pool[0][1])
+
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     def step_on(x, y):
         out = ddp(x)
@@ -139,7 +196,32 @@ def main():
     def static_step():
         return step_on(static_x, static_y)
 
-    use_graph = not args.no_graph
+    def capture():
+        """Capture one step into a hipGraph; all ranks agree on the outcome before going on (a
+        rank that fell back alone would issue a different collective sequence and hang its peers)."""
+        err = None
+        graph = None
+        try:
+            graph = StepGraph(static_step, warmup=2).capture()
+        except Exception as e:  # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+            sync()
+        ok = err is None
+        if world > 1:
+            ok = _store_agree(dist, f"capture{capture.n}", ok, rank, world)
+        capture.n += 1
+        if ok:
+            return graph
+        print(f"[bench] rank {rank}: hipGraph capture failed ({err or 'on another rank'})", file=sys.stderr, flush=True)
+        if world > 1:
+            # Captured-but-never-run collectives may have advanced the communicator's sequence on
+            # some ranks only; eager fallback could desynchronise them.  Fail loudly instead.
+            sys.stderr.flush()
+            os._exit(3)
+        return None
+    capture.n = 0
+
+    use_graph = on_gpu and not args.no_graph
     graph = None
     n_warm = max(args.warmup, 3)
     if use_graph:
@@ -149,55 +231,97 @@ def main():
             step_on(x, y)
         static_x.copy_(pool[0][0])
         static_y.copy_(pool[0][1])
-        try:
-            graph = StepGraph(static_step, warmup=2).capture()
-        except Exception as e:  # fall back to eager steps rather than report nothing
-            print(f"[bench] rank {rank}: hipGraph capture failed ({type(e).__name__}: {e}); running eager",
-                  file=sys.stderr, flush=True)
-            torch.cuda.synchronize()
-            use_graph, graph = False, None
-    if use_graph:
-        for i in range(n_warm):
-            x, y = pool[i % len(pool)]
-            static_x.copy_(x, non_blocking=True)
-            static_y.copy_(y, non_blocking=True)
-            graph.replay()
-    else:
-        for i in range(n_warm):
-            x, y = pool[i % len(pool)]
-            step_on(x, y)
+        graph = capture()
+        use_graph = graph is not None
 
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    loss = None
-    for i in range(args.steps):
-        x, y = pool[i % len(pool)]
-        if use_graph:
-            static_x.copy_(x, non_blocking=True)
-            static_y.copy_(y, non_blocking=True)
-            loss = graph.replay()
-        else:
-            loss = step_on(x, y)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def run_steps(n, g):
+        loss = None
+        for i in range(n):
+            x, y = pool[i % len(pool)]
+            if g is not None:
+                static_x.copy_(x, non_blocking=True)
+                static_y.copy_(y, non_blocking=True)
+                loss = g.replay()
+            else:
+                loss = step_on(x, y)
+        return loss
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed_max = float(t.item())
-    n_buckets = len(ddp.reducer.bucket_indices())
+    def timed(n, g):
+        sync()
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        loss = run_steps(n, g)
+        sync()
+        dist.barrier()
+        sync()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()), loss
+
+    run_steps(n_warm, graph)
+    elapsed_max, loss = timed(args.steps, graph)
     final_loss = float(loss.item()) if loss is not None else float("nan")
     ms_per_step = 1000.0 * elapsed_max / args.steps
     value = world * B * args.steps / elapsed_max
+    if rank == 0 and elapsed_max < 1.0:
+        print(f"[bench] note: the timed region is {elapsed_max * 1e3:.1f} ms ({args.steps} steps); "
+              "use more --steps for sampling-based observers", file=sys.stderr, flush=True)
+
+    # ------------------------------------------------------------------ comm observability
+    nat = ddp._native_pg
+    stats = ddp.reducer.stats()
+    comm_stats = {"bucket_bytes": [int(s.bytes) for s in stats]}
+    if args.comm_stats_steps > 0 and (world > 1 or force_comm):
+        S = args.comm_stats_steps
+        per_bucket = [[] for _ in stats]
+        if hasattr(nat, "set_timing"):
+            nat.set_timing(True)
+            for i in range(S):
+                x, y = pool[i % len(pool)]
+                step_on(x, y)
+                sync()
+                for b, d in enumerate(ddp.reducer.collect_comm_times()):
+                    if d >= 0:
+                        per_bucket[b].append(d)
+            nat.set_timing(False)
+            comm_stats["bucket_comm_us"] = [round(sum(v) / len(v), 1) if v else None for v in per_bucket]
+            comm_stats["bucket_comm_us_method"] = f"device events around each bucket collective on the comm stream, mean of {S} eager steps"
+        # step time without any gradient collective (same graph otherwise): exposed comm estimate
+        ddp.reducer.set_comm_hook(C.CommHook.NONE)
+        g2 = capture() if use_graph else None
+        run_steps(2, g2)
+        el_nc, _ = timed(S, g2)
+        ms_nc = 1000.0 * el_nc / S
+        comm_stats["step_ms_no_comm"] = round(ms_nc, 4)
+        comm_stats["exposed_comm_ms"] = round(ms_per_step - ms_nc, 4)
+        comm_stats["exposed_comm_method"] = (f"timed step minus the step time of the same {'graph' if use_graph else 'eager step'} "
+                                             f"captured with the bucket collectives disabled ({S} steps, max over ranks)")
+
+    n_buckets = len(ddp.reducer.bucket_indices())
+    sizes_kb = ",".join(f"{b / 1024:.0f}" for b in comm_stats["bucket_bytes"])
+    lib = "RCCL" if on_gpu else "host ring (gloo)"
+    if world > 1:
+        comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
+                f"cap {args.bucket_mb} MB" + (", side HIP stream overlapped with backward" if on_gpu else ""))
+    elif force_comm:
+        comm = (f"{lib} {args.comm_hook} (avg) over 1 rank, forced so N=1 runs the N>1 code path; "
+                f"{n_buckets} bucket(s) [{sizes_kb}] KB, cap {args.bucket_mb} MB")
+    else:
+        comm = "none (world_size 1, --no-force-comm)"
     if rank == 0:
         metric = METRIC if args.model == "convnet" else \
             f"images/sec (whole node) {args.model} synthetic DDP training at 1/2/4/8 MI355X"
-        data = ("synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)"
-                if args.model == "convnet" else
-                f"synthetic (on-device N(0,1) {spec['shape']} images + labels; random-init weights)")
+        if not on_gpu:
+            data = "synthetic (host uint8 MNIST-shaped images + labels; random-init weights; CPU plumbing run)"
+        elif args.model == "convnet":
+            data = "synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)"
+        else:
+            data = f"synthetic (on-device N(0,1) {spec['shape']} images + labels; random-init weights)"
+        dtype = {"bf16": "bf16", "fp32": "fp32", "fp8": "fp8 (e4m3 linear GEMMs, bf16 attention/norms)"}[args.dtype]
+        if not on_gpu:
+            dtype = "fp32 (CPU ATen)"
         res = {
             "metric": metric,
             "value": round(value, 1),
@@ -209,7 +333,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.dtype if args.dtype == "bf16" else "fp8 (e4m3 linear GEMMs, bf16 attention/norms)",
+            "dtype": dtype,
             "data": data,
             "config": {
                 "model": spec["desc"],
@@ -219,14 +343,25 @@ def main():
                 "image_shape": list(spec["shape"]),
                 "parallelism": f"dp{world}",
                 "optimizer": f"SGD lr={lr} momentum={spec['momentum']} nesterov={spec['nesterov']} wd={spec['wd']}",
-                "comm": f"RCCL all-reduce ({args.comm_hook}), {n_buckets} bucket(s), cap {args.bucket_mb} MB",
+                "comm": comm,
+                "comm_world_size": int(nat.size()),
+                "comm_backend": nat.backend_name(),
                 "hipgraph": use_graph,
                 "master_weights": "fp32",
+                "device": "cpu" if not on_gpu else torch.cuda.get_device_properties(dev).gcnArchName,
             },
+            "comm_stats": comm_stats,
             "final_loss": round(final_loss, 5),
         }
         print(json.dumps(res), flush=True)
     dist.destroy_process_group()
+
+
+def main(argv=None):
+    args = parse(argv)
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        sys.exit(_self_launch(args))
+    worker(args)
 
 
 if __name__ == "__main__":

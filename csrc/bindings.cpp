@@ -339,7 +339,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("rebuilt", &Reducer::rebuilt)
       .def("rebuild_buckets", &Reducer::rebuild_buckets)
       .def("iteration", &Reducer::iteration)
-      .def("stats", &Reducer::stats);
+      .def("stats", &Reducer::stats)
+      .def("collect_comm_times", &Reducer::collect_comm_times);
 
   m.def("compute_bucket_assignment_by_size",
         [](const std::vector<at::Tensor>& tensors, const std::vector<int64_t>& limits,

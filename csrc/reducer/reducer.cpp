@@ -233,6 +233,21 @@ std::vector<BucketStats> Reducer::stats() const {
   return out;
 }
 
+std::vector<double> Reducer::collect_comm_times() {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<double> out;
+  for (auto& b : buckets_) {
+    double d = b.work ? b.work->duration_us() : -1.0;
+    if (d >= 0 && b.st.last_comm_us != d) {
+      b.st.last_comm_us = d;
+      b.st.total_comm_us += d;
+      b.st.comm_samples += 1;
+    }
+    out.push_back(d);
+  }
+  return out;
+}
+
 void Reducer::rebuild_buckets(std::vector<std::vector<int64_t>> new_indices) {
   std::lock_guard<std::mutex> lk(mu_);
   RINGDP_CHECK(!expect_hooks_, "cannot rebuild buckets during backward");

@@ -80,6 +80,10 @@ class Reducer {
 
   int64_t iteration() const { return iteration_; }
   std::vector<BucketStats> stats() const;
+  // Device-measured duration of each bucket's last collective (-1 where unknown: no timing
+  // events, captured in a hipGraph, or not complete).  Call after synchronising the device;
+  // also folds the samples into stats().
+  std::vector<double> collect_comm_times();
 
   // Internal: invoked from the AccumulateGrad post hook.
   void autograd_hook(int64_t index);

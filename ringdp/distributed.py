@@ -258,15 +258,40 @@ def _rendezvous(init_method: str, rank: int, world_size: int, timeout: _dt.timed
     raise ValueError(f"ringdp: unsupported init_method {init_method!r} (env://, tcp://, file://)")
 
 
+def _reachable_ip(peer_host: str, peer_port: int) -> str:
+    """The local interface address peers use to reach this host: the source address the kernel
+    picks for a route to the master (no packet is sent).  Avoids resolving the container
+    hostname, which need not resolve."""
+    import socket
+
+    try:
+        with socket.socket(socket.AF_INET, socket.SOCK_DGRAM) as s:
+            s.connect((peer_host, peer_port))
+            return s.getsockname()[0]
+    except OSError:
+        return peer_host
+
+
 def _tcp_store(host: str, port: int, rank: int, world_size: int, tmo_ms: int, use_agent: bool):
     if use_agent and os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true":
-        # Started by torchrun: the elastic agent already serves a c10d store on MASTER_PORT.
-        # Rendezvous through it (bootstrap KV only) in the same per-attempt namespace c10d uses.
+        # Started by torchrun: the elastic agent owns MASTER_PORT with its own (c10d) store.  It is
+        # used for ONE exchange only: rank 0 starts ringdp's native TCPStore on an ephemeral port
+        # and publishes "<ip>:<port>" there; every rank then connects to the native store, which
+        # carries all further bootstrap traffic (RCCL unique ids, barriers, debug fingerprints).
         import torch.distributed as tdist
 
         attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
-        tstore = tdist.TCPStore(host, port, world_size, False, _dt.timedelta(milliseconds=tmo_ms))
-        return C.PrefixStore(f"/worker/attempt_{attempt}", C.PyStore(tstore, tmo_ms))
+        agent = tdist.TCPStore(host, port, world_size, False, _dt.timedelta(milliseconds=tmo_ms))
+        key = f"/ringdp/attempt_{attempt}/native_store"
+        if rank == 0:
+            st = C.TCPStore(host, 0, world_size, True, tmo_ms)
+            agent.set(key, f"{_reachable_ip(host, port)}:{st.port}")
+        else:
+            addr = agent.get(key).decode()
+            h, p = addr.rsplit(":", 1)
+            st = C.TCPStore(h, int(p), world_size, False, tmo_ms)
+        del agent
+        return st
     if use_agent and os.environ.get("RINGDP_USE_AGENT_STORE", "0") == "1":
         # Started by `python -m ringdp.launch`: the launcher on node 0 hosts the store on
         # MASTER_PORT; workers are clients, namespaced per restart attempt.

@@ -20,8 +20,15 @@ from ..ops.convnet import MNIST_MEAN, MNIST_STD, convnet_forward
 
 
 class ConvNet(nn.Module):
-    def __init__(self):
+    """``precision``: GPU compute precision - "bf16" (bf16 MFMA, fp32 accumulation and master
+    weights; the bench default) or "fp32" (the reference's precision, fp32 MFMA kernels).  The
+    CPU path is always fp32 ATen."""
+
+    def __init__(self, precision: str = "bf16"):
         super().__init__()
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"ConvNet: precision must be 'bf16' or 'fp32', got {precision!r}")
+        self.precision = precision
         self.relu = nn.ReLU()
         self.conv1 = nn.Conv2d(in_channels=1, out_channels=32, kernel_size=5, stride=1, padding=1)
         self.maxpool1 = nn.MaxPool2d(kernel_size=2, stride=2)
@@ -34,6 +41,10 @@ class ConvNet(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.is_cuda:
+            if self.precision == "fp32":
+                from ..ops.convnet_fp32 import convnet_forward_fp32
+
+                return convnet_forward_fp32(x, self.conv1, self.conv2, self.conv3, self.fc1)
             return convnet_forward(x, self.conv1, self.conv2, self.conv3, self.fc1)
         return self.reference_forward(x)
 

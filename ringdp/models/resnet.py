@@ -34,7 +34,14 @@ def _fused(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, residual=None):
     training = bn.training
     if training and bn.track_running_stats and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
-    momentum = bn.momentum if bn.momentum is not None else 0.1
+    if bn.momentum is not None:
+        momentum = bn.momentum
+    elif training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        # cumulative moving average (torch's exponential_average_factor for momentum=None);
+        # reads the counter on the host, as upstream does
+        momentum = 1.0 / float(bn.num_batches_tracked.item())
+    else:
+        momentum = 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
     return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, conv.stride[0], conv.padding[0],

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from .. import distributed as dist
+from .. import ops as _ops
 from .._native import C
 from . import comm_hooks as default_hooks
 from ..utils import tracing as _tracing
@@ -255,8 +256,15 @@ class DistributedDataParallel(nn.Module):
         self._comm_hook_name = name
 
     # ------------------------------------------------------------------ bucket rebuild (C5)
-    def _maybe_rebuild_buckets(self):
-        if not self._rebuild_enabled or self.reducer.rebuilt() or self.reducer.iteration() < 1:
+    def _will_rebuild(self) -> bool:
+        return self._rebuild_enabled and not self.reducer.rebuilt() and self.reducer.iteration() >= 1
+
+    def _maybe_rebuild_buckets(self, force: bool = False):
+        """``force``: a joined (shadowing) rank follows the active ranks' rebuild even if it never
+        ran a backward itself, so its buckets - and its zero-filled all-reduces - keep matching."""
+        if not force and not self._will_rebuild():
+            return
+        if not self._rebuild_enabled or self.reducer.rebuilt():
             return
         order = list(self.reducer.ready_order())
         g = self.process_group
@@ -288,10 +296,12 @@ class DistributedDataParallel(nn.Module):
         self._install_layout()
 
     # ------------------------------------------------------------------ forward
-    def _sync_buffers(self):
-        """C4: broadcast rank 0's buffers every forward (broadcast_buffers=True, U7 :2155-2221)."""
+    def _sync_buffers(self, src: Optional[int] = None):
+        """C4: broadcast the authoritative rank's buffers every forward (broadcast_buffers=True,
+        U7 :2155-2221): rank 0, or under join() the highest still-active rank (upstream's
+        _find_common_rank), so a rank that ran out of data never overwrites live BN statistics."""
         if self.process_group.size() > 1 and self._buffers_list:
-            self._broadcast_coalesced(self._buffers_list)
+            self._broadcast_coalesced(self._buffers_list, src=src)
 
     def _to_device(self, obj):
         if torch.is_tensor(obj):
@@ -306,13 +316,17 @@ class DistributedDataParallel(nn.Module):
         with torch.autograd.profiler.record_function("DistributedDataParallel.forward"), \
                 _tracing.range("ringdp.DDP.forward"):
             grad = torch.is_grad_enabled() and self.require_backward_grad_sync
+            buf_src = None
             if self._join_cfg is not None:
-                self._join_notify(grad)
-            if grad:
+                _, _, rebuild, buf_src = self._join_notify(grad)
+                if rebuild:
+                    self._maybe_rebuild_buckets(force=True)
+            elif grad:
                 self._maybe_rebuild_buckets()
+            if grad:
                 self.reducer.prepare_for_forward()
             if self.broadcast_buffers and self.require_forward_param_sync:
-                self._sync_buffers()
+                self._sync_buffers(buf_src)
             if self.device_ids is not None:
                 inputs = self._to_device(inputs)
                 kwargs = self._to_device(kwargs)
@@ -320,6 +334,7 @@ class DistributedDataParallel(nn.Module):
             if torch.is_grad_enabled():
                 self.reducer.set_require_sync(self.require_backward_grad_sync)
                 self.reducer.prepare_for_backward()
+                _ops.next_backward_epoch()
             self._iteration += 1
             return out
 
@@ -365,13 +380,29 @@ class DistributedDataParallel(nn.Module):
     def _join_device(self) -> torch.device:
         return self.device if self.device is not None else torch.device("cpu")
 
+    def _join_state(self, flag: torch.Tensor):
+        """Decode the per-iteration join all-reduce [n_active, n_sync, n_rebuild, active mask...]
+        -> (n_active, n_sync, rebuild?, authoritative global rank for buffers)."""
+        g = self.process_group
+        vals = flag.tolist()
+        active = [i for i in range(g.size()) if vals[3 + i] > 0]
+        src = g.ranks[max(active)] if active else g.ranks[0]
+        return int(vals[0]), int(vals[1]), vals[2] > 0, src
+
     def _join_notify(self, grad_sync: bool):
         g = self.process_group
-        flag = torch.tensor([1.0, 1.0 if grad_sync else 0.0], dtype=torch.float32, device=self._join_device())
+        flag = torch.zeros(3 + g.size(), dtype=torch.float32)
+        flag[0] = 1.0
+        flag[1] = 1.0 if grad_sync else 0.0
+        flag[2] = 1.0 if (grad_sync and self._will_rebuild()) else 0.0
+        flag[3 + g.rank()] = 1.0
+        flag = flag.to(self._join_device())
         dist.all_reduce(flag, group=g)
-        if self._join_cfg["throw"] and int(flag[0].item()) < g.size():
+        st = self._join_state(flag)
+        if self._join_cfg["throw"] and st[0] < g.size():
             raise RuntimeError(f"ringdp DDP.join: rank {g.rank()} detected that another rank exhausted its "
                                "inputs (throw_on_early_termination=True)")
+        return st
 
     def _join_shadow(self):
         g = self.process_group
@@ -379,18 +410,18 @@ class DistributedDataParallel(nn.Module):
         joined_at = self._iteration
         wire = {"bf16_compress": torch.bfloat16, "fp16_compress": torch.float16}.get(self._comm_hook_name)
         while True:
-            flag = torch.zeros(2, dtype=torch.float32, device=dev)
+            flag = torch.zeros(3 + g.size(), dtype=torch.float32, device=dev)
             dist.all_reduce(flag, group=g)
-            n_active, n_sync = int(flag[0].item()), int(flag[1].item())
+            n_active, n_sync, rebuild, buf_src = self._join_state(flag)
             if n_active == 0:
                 break
             if self._join_cfg["throw"]:
                 raise RuntimeError(f"ringdp DDP.join: rank {g.rank()} exhausted its inputs "
                                    "(throw_on_early_termination=True)")
-            if n_sync:
-                self._maybe_rebuild_buckets()
+            if rebuild:
+                self._maybe_rebuild_buckets(force=True)
             if self.broadcast_buffers and self.require_forward_param_sync:
-                self._sync_buffers()
+                self._sync_buffers(buf_src)
             if n_sync:
                 idx = self.reducer.bucket_indices()
                 for b, numel in enumerate(self.reducer.bucket_numels()):

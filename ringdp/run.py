@@ -236,5 +236,28 @@ def main(argv: Optional[List[str]] = None, legacy: bool = False) -> int:
     return run(args, legacy=legacy)
 
 
+def launch_local(script: str, script_args: List[str], nproc: int, master_addr: str = "127.0.0.1",
+                 master_port: Optional[int] = None, env: Optional[dict] = None) -> int:
+    """Programmatic single-node launch: ``nproc`` fresh interpreters running ``script`` with the
+    torchrun env contract; returns the group's exit code.  The calling process never touches the
+    GPU (it only forks/execs the workers), so a script can re-launch itself as N ranks
+    (``bench.py --gpus N``, ref/mpspawn_dist.py:136-140)."""
+    argv = ["--nproc-per-node", str(nproc), "--master-addr", master_addr,
+            "--master-port", str(master_port if master_port is not None else _free_port())]
+    saved = None
+    if env:
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return main(argv + [script] + list(script_args))
+    finally:
+        if saved:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+
 if __name__ == "__main__":
     sys.exit(main())

@@ -54,10 +54,12 @@ def load(path: str, model, optimizer=None, broadcast: bool = True, map_location=
         with torch.no_grad():
             for t in list(m.parameters()) + list(m.buffers()):
                 dist.broadcast(t.data, src=0)
-        if optimizer is not None:
-            box = [optimizer.state_dict() if _rank() == 0 else None, meta]
-            dist.broadcast_object_list(box, src=0)
-            if _rank() != 0:
-                optimizer.load_state_dict(box[0])
-                meta = box[1]
+        # meta (epoch, step, sampler epoch) always travels: ranks must agree on where they resume
+        # or their loops (and collective sequences) diverge; optimizer state only when given
+        box = [meta, optimizer.state_dict() if (optimizer is not None and _rank() == 0) else None]
+        dist.broadcast_object_list(box, src=0)
+        if _rank() != 0:
+            meta = box[0]
+            if optimizer is not None:
+                optimizer.load_state_dict(box[1])
     return meta

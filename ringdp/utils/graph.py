@@ -45,7 +45,10 @@ class StepGraph:
         drain_comms()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            self.output = self.step_fn()
+            out = self.step_fn()
+        # keep only the value: a live autograd graph would pin AccumulateGrad nodes created on the
+        # capture stream and make later eager steps on another stream synchronise against them
+        self.output = out.detach() if torch.is_tensor(out) else out
         torch.cuda.synchronize()
         return self
 

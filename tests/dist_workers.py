@@ -316,14 +316,18 @@ def checkpoint_resume_worker(rank, world, init_file, out_dir):
     step(m2, o2, 3)
     for a, b in zip(ref, m2.parameters()):
         assert torch.equal(a, b.detach()), (a - b).abs().max()
+    # model-only resume: every rank still gets rank 0's meta
+    m3, _ = make()
+    meta3 = checkpoint.load(ckpt, m3)
+    assert meta3 == {"epoch": 3, "step": 2}, (rank, meta3)
     dist.destroy_process_group()
 
 
 JOIN_BATCHES = (5, 3, 4, 2)
 
 
-def join_worker(rank, world, port, result_dir, hook):
-    """Uneven inputs under DDP.join(): rank r trains on JOIN_BATCHES[r] batches."""
+def join_worker(rank, world, port, result_dir, hook, batches=JOIN_BATCHES):
+    """Uneven inputs under DDP.join(): rank r trains on batches[r] batches."""
     dist = _init(rank, world, port)
     from ringdp.models import ConvNet
     from ringdp.optim import SGD
@@ -337,10 +341,10 @@ def join_worker(rank, world, port, result_dir, hook):
     if hook == "bf16":
         ddp.register_comm_hook(None, comm_hooks.bf16_compress_hook)
     opt = SGD(ddp.parameters(), lr=0.01, momentum=0.9)
-    steps = max(JOIN_BATCHES[:world])
+    steps = max(batches[:world])
     xs, ys = _convnet_batches(world, B, steps)
     with ddp.join():
-        for i in range(JOIN_BATCHES[rank]):
+        for i in range(batches[rank]):
             x = xs[i][rank * B:(rank + 1) * B]
             y = ys[i][rank * B:(rank + 1) * B]
             loss = torch.nn.functional.cross_entropy(ddp(x), y)

@@ -57,7 +57,7 @@ def test_ddp_equivalence(tmp_path, world, momentum, hook, bucket_mb, first_mb):
         assert len(res[0]["buckets"]) > 1
 
 
-def _reference_join(world, hook):
+def _reference_join(world, hook, batches=W.JOIN_BATCHES):
     """One process: iteration i averages the gradients of the ranks that still have data over the
     initial world size (the semantics of DDP.join(divide_by_initial_world_size=True))."""
     from ringdp.models import ConvNet
@@ -67,7 +67,7 @@ def _reference_join(world, hook):
     torch.manual_seed(5)
     model = ConvNet()
     opt = SGD(model.parameters(), lr=0.01, momentum=0.9)
-    n = W.JOIN_BATCHES[:world]
+    n = batches[:world]
     xs, ys = W._convnet_batches(world, B, max(n))
     for i in range(max(n)):
         loss = 0
@@ -81,12 +81,14 @@ def _reference_join(world, hook):
     return torch.cat([p.detach().reshape(-1) for p in model.parameters()])
 
 
-@pytest.mark.parametrize("world,hook", [(2, "allreduce"), (3, "allreduce"), (2, "bf16")])
-def test_join_uneven_inputs(tmp_path, world, hook):
-    spawn(W.join_worker, args=(world, free_port(), str(tmp_path), hook), nprocs=world)
+@pytest.mark.parametrize("world,hook,batches", [(2, "allreduce", W.JOIN_BATCHES), (3, "allreduce", W.JOIN_BATCHES),
+                                                (2, "bf16", W.JOIN_BATCHES),
+                                                (3, "allreduce", (0, 4, 2))])  # rank 0 joins before iteration 0
+def test_join_uneven_inputs(tmp_path, world, hook, batches):
+    spawn(W.join_worker, args=(world, free_port(), str(tmp_path), hook, batches), nprocs=world)
     res = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
     assert all(r["same"] for r in res), "final model sync from the last joiner failed"
-    ref = _reference_join(world, hook)
+    ref = _reference_join(world, hook, batches)
     err = float((res[0]["flat"] - ref).abs().max())
     assert err < (2e-2 if hook == "bf16" else 1e-4), err
 
