@@ -251,6 +251,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("recv", &ProcessGroup::recv, py::call_guard<py::gil_scoped_release>())
       .def("barrier", &ProcessGroup::barrier, py::call_guard<py::gil_scoped_release>())
       .def("split", &ProcessGroup::split, py::call_guard<py::gil_scoped_release>())
+      .def("coalesced",
+           [](ProcessGroup& pg, const std::vector<py::tuple>& items) {
+             // items: (kind, out, in_or_None, root, ReduceOp)
+             std::vector<CollOp> ops;
+             for (auto& it : items) {
+               CollOp c;
+               c.kind = it[0].cast<int>();
+               c.out = it[1].cast<at::Tensor>();
+               if (!it[2].is_none()) c.in = it[2].cast<at::Tensor>();
+               c.root = it[3].cast<int>();
+               c.op = it[4].cast<ReduceOp>();
+               ops.push_back(std::move(c));
+             }
+             py::gil_scoped_release nogil;
+             return pg.coalesced(ops);
+           })
       .def("shutdown", &ProcessGroup::shutdown, py::call_guard<py::gil_scoped_release>())
       .def("abort", &ProcessGroup::abort, py::call_guard<py::gil_scoped_release>());
 
@@ -280,6 +296,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("drain", &RcclPG::drain, py::call_guard<py::gil_scoped_release>())
       .def("error_message", &RcclPG::error_message)
       .def("set_timing", &RcclPG::set_timing)
+      .def("watch_stream",
+           [](RcclPG& pg, uint64_t stream) {
+             pg.watch_stream(reinterpret_cast<hipStream_t>(stream), OpType::GRAPH_REPLAY);
+           },
+           py::arg("stream"),
+           "watchdog-track the work queued so far on a raw hipStream_t (e.g. a graph replay)")
       .def("timing", &RcclPG::timing)
       .def("set_async_error_handling", &RcclPG::set_async_error_handling)
       .def("comm_stream_ptr",

@@ -39,6 +39,7 @@ const char* op_name(OpType t) {
     case OpType::RECV: return "recv";
     case OpType::BARRIER: return "barrier";
     case OpType::COALESCED: return "coalesced";
+    case OpType::GRAPH_REPLAY: return "graph_replay";
   }
   return "unknown";
 }

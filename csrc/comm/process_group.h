@@ -39,6 +39,7 @@ enum class OpType : int {
   RECV,
   BARRIER,
   COALESCED,
+  GRAPH_REPLAY,  // a captured step (hipGraph) that contains this group's collectives
 };
 
 const char* op_name(OpType t);
@@ -88,6 +89,34 @@ class HostWork : public Work {
   double duration_us_ = -1.0;
 };
 
+// Several Works completed together (the default coalesced() of host backends).
+class CompositeWork : public Work {
+ public:
+  CompositeWork(std::vector<std::shared_ptr<Work>> parts, uint64_t seq)
+      : Work(OpType::COALESCED, seq), parts_(std::move(parts)) {}
+  void wait(bool blocking = false) override {
+    for (auto& p : parts_) p->wait(blocking);
+  }
+  bool is_completed() override {
+    for (auto& p : parts_)
+      if (!p->is_completed()) return false;
+    return true;
+  }
+
+ private:
+  std::vector<std::shared_ptr<Work>> parts_;
+};
+
+// One collective of a coalesced batch (ringdp.distributed._coalescing_manager).
+struct CollOp {
+  enum Kind : int { ALLREDUCE = 0, BROADCAST = 1, ALLGATHER_INTO = 2, REDUCE_SCATTER = 3 };
+  int kind = ALLREDUCE;
+  at::Tensor out;  // in-place tensor for ALLREDUCE / BROADCAST
+  at::Tensor in;   // ALLGATHER_INTO / REDUCE_SCATTER input
+  int root = 0;
+  ReduceOp op = ReduceOp::SUM;
+};
+
 struct AllToAllSplits {
   std::vector<int64_t> output_split_sizes;
   std::vector<int64_t> input_split_sizes;
@@ -123,6 +152,33 @@ class ProcessGroup : public std::enable_shared_from_this<ProcessGroup> {
   virtual std::shared_ptr<Work> send(at::Tensor& tensor, int dst, int tag) = 0;
   virtual std::shared_ptr<Work> recv(at::Tensor& tensor, int src, int tag) = 0;
   virtual std::shared_ptr<Work> barrier() = 0;
+
+  // A batch of collectives issued as one unit.  GPU backends fuse it into one RCCL group (one
+  // launch, one completion event); the default issues them in order and waits for all.
+  virtual std::shared_ptr<Work> coalesced(std::vector<CollOp>& ops) {
+    std::vector<std::shared_ptr<Work>> parts;
+    for (auto& c : ops) {
+      switch (c.kind) {
+        case CollOp::ALLREDUCE: {
+          std::vector<at::Tensor> v{c.out};
+          parts.push_back(allreduce(v, c.op));
+          break;
+        }
+        case CollOp::BROADCAST: {
+          std::vector<at::Tensor> v{c.out};
+          parts.push_back(broadcast(v, c.root));
+          break;
+        }
+        case CollOp::ALLGATHER_INTO:
+          parts.push_back(allgather_into_tensor(c.out, c.in));
+          break;
+        case CollOp::REDUCE_SCATTER:
+          parts.push_back(reduce_scatter_tensor(c.out, c.in, c.op));
+          break;
+      }
+    }
+    return std::make_shared<CompositeWork>(std::move(parts), next_seq());
+  }
 
   // Collective creation of a sub-group.  Every member of this group must call it with the same
   // `ranks`; non-members receive nullptr.

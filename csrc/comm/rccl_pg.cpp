@@ -181,6 +181,16 @@ void RcclPG::drain() {
   inflight_.clear();
 }
 
+void RcclPG::watch_stream(hipStream_t stream, OpType what) {
+  if (stop_.load() || aborted_.load()) return;
+  DeviceScope ds(device_);
+  auto work = std::make_shared<RcclWork>(what, next_seq(), this, /*captured=*/false, /*timing=*/false);
+  RINGDP_HIP_CHECK(hipEventRecord(work->done_, stream));
+  work->deadline_us_ = now_us() + timeout_.count() * 1000;
+  std::lock_guard<std::mutex> wl(wd_mu_);
+  inflight_.push_back(std::move(work));
+}
+
 void RcclPG::abort() {
   if (comm_ && !aborted_.exchange(true)) {
     ncclCommAbort(comm_);
@@ -230,7 +240,9 @@ void RcclPG::watchdog_loop() {
                                " (seq ", w->seq(), ") did not complete within ",
                                timeout_.count(), " ms; aborting communicator");
         }
-        break;  // ops complete in order on the comm stream
+        // Entries are queued in issue order with deadlines in the same order: an incomplete
+        // head that is within its deadline means everything behind it is too.
+        break;
       }
     }
     if (failure.empty() && comm_) {
@@ -471,6 +483,50 @@ std::shared_ptr<Work> RcclPG::barrier() {
   std::vector<at::Tensor> v{t};
   auto w = allreduce(v, ReduceOp::SUM);
   return w;
+}
+
+std::shared_ptr<Work> RcclPG::coalesced(std::vector<CollOp>& ops) {
+  std::vector<at::Tensor> all;
+  for (auto& c : ops) {
+    check_tensor(c.out, "coalesced");
+    all.push_back(c.out);
+    if (c.kind == CollOp::ALLGATHER_INTO || c.kind == CollOp::REDUCE_SCATTER) {
+      check_tensor(c.in, "coalesced");
+      all.push_back(c.in);
+    }
+    if (c.kind == CollOp::ALLGATHER_INTO)
+      RINGDP_CHECK(c.out.numel() == c.in.numel() * size_, "coalesced all_gather_into_tensor: bad sizes");
+    if (c.kind == CollOp::REDUCE_SCATTER)
+      RINGDP_CHECK(c.in.numel() == c.out.numel() * size_, "coalesced reduce_scatter_tensor: bad sizes");
+    if (c.kind == CollOp::BROADCAST)
+      RINGDP_CHECK(c.root >= 0 && c.root < size_, "coalesced broadcast: invalid root ", c.root);
+  }
+  // One ncclGroupStart/End: RCCL fuses the batch into a single launch on the comm stream.
+  return launch(OpType::COALESCED, all, [&](hipStream_t s) {
+    RINGDP_NCCL_CHECK(ncclGroupStart());
+    for (auto& c : ops) {
+      auto dt = to_nccl_dtype(c.out.scalar_type());
+      switch (c.kind) {
+        case CollOp::ALLREDUCE:
+          RINGDP_NCCL_CHECK(ncclAllReduce(c.out.data_ptr(), c.out.data_ptr(), c.out.numel(), dt,
+                                          to_nccl_op(c.op), comm_, s));
+          break;
+        case CollOp::BROADCAST:
+          RINGDP_NCCL_CHECK(ncclBroadcast(c.out.data_ptr(), c.out.data_ptr(), c.out.numel(), dt,
+                                          c.root, comm_, s));
+          break;
+        case CollOp::ALLGATHER_INTO:
+          RINGDP_NCCL_CHECK(ncclAllGather(c.in.data_ptr(), c.out.data_ptr(), c.in.numel(), dt,
+                                          comm_, s));
+          break;
+        case CollOp::REDUCE_SCATTER:
+          RINGDP_NCCL_CHECK(ncclReduceScatter(c.in.data_ptr(), c.out.data_ptr(), c.out.numel(), dt,
+                                              to_nccl_op(c.op), comm_, s));
+          break;
+      }
+    }
+    RINGDP_NCCL_CHECK(ncclGroupEnd());
+  });
 }
 
 std::shared_ptr<ProcessGroup> RcclPG::split(const std::vector<int>& ranks, const std::string&) {

@@ -72,6 +72,7 @@ class RcclPG : public ProcessGroup {
   std::shared_ptr<Work> send(at::Tensor& tensor, int dst, int tag) override;
   std::shared_ptr<Work> recv(at::Tensor& tensor, int src, int tag) override;
   std::shared_ptr<Work> barrier() override;
+  std::shared_ptr<Work> coalesced(std::vector<CollOp>& ops) override;
   std::shared_ptr<ProcessGroup> split(const std::vector<int>& ranks,
                                       const std::string& tag) override;
   void shutdown() override;
@@ -80,6 +81,11 @@ class RcclPG : public ProcessGroup {
   // Host-blocks until every eagerly issued op has completed and clears the watchdog list, so
   // no event query can race a subsequent hipGraph capture.
   void drain();
+  // Puts the work queued so far on `stream` (e.g. a hipGraph replay whose captured collectives
+  // the per-op watchdog entries cannot see) under this group's watchdog: an event recorded on
+  // the stream must complete within the group timeout, else the communicator is aborted and the
+  // process exits non-zero like any other hung collective.
+  void watch_stream(hipStream_t stream, OpType what);
   bool aborted() const { return aborted_.load(); }
   std::string error_message() {
     std::lock_guard<std::mutex> lk(wd_mu_);

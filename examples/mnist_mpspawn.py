@@ -49,13 +49,13 @@ def train(gpu, args):
 
     if use_gpu:
         train_data, synthetic = mnist_or_synthetic(args.data)
-        sampler = DistributedSampler(train_data, num_replicas=args.world_size, rank=rank, shuffle=False)
+        sampler = DistributedSampler(train_data, num_replicas=args.world_size, rank=rank)  # shuffle=True, seed 0 (ref :77-81)
         loader = DeviceLoader(train_data, batch_size, torch.device("cuda", gpu), sampler=sampler,
                               out_dtype=torch.uint8)
     else:
         tf = T.Compose([T.ToTensor(), T.Normalize((0.1307,), (0.3081,))])
         train_data, synthetic = mnist_or_synthetic(args.data, transform=tf)
-        sampler = DistributedSampler(train_data, num_replicas=args.world_size, rank=rank, shuffle=False)
+        sampler = DistributedSampler(train_data, num_replicas=args.world_size, rank=rank)  # shuffle=True, seed 0 (ref :77-81)
         loader = DataLoader(train_data, batch_size=batch_size, shuffle=False, sampler=sampler)
     if synthetic:
         log(f"[note] MNIST not found under {args.data}: using synthetic 1x28x28 data of the same shape")

@@ -9,6 +9,11 @@ Everything is compiled in-tree so the built object travels with the repository s
 * link                     -> one shared object against torch's bundled HIP runtime + RCCL.
 
 Incremental: an object is rebuilt only when its source or any header under ``csrc/`` is newer.
+
+Sanitized host build (SURVEY.md §5 race/sanitizer row): ``--sanitize address`` compiles the host
+C++ runtime (stores, host ring, RCCL PG, reducer, bindings) with ``-fsanitize=address`` into
+``build/asan/`` (device code unchanged, no GPU sanitizer), linked by g++ against gcc's libasan.
+Load it with ``RINGDP_EXT_PATH=<that .so>`` and ``LD_PRELOAD=libasan.so`` (tools/asan_check.sh).
 Usage: ``python __graft_entry__.py build`` (the package import needs the built extension, so the
 driver is loaded by file path there).
 """
@@ -58,9 +63,9 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _obj_for(src: Path) -> Path:
+def _obj_for(src: Path, build_dir: Path = BUILD) -> Path:
     rel = src.relative_to(CSRC)
-    return BUILD / (str(rel).replace(os.sep, "__") + ".o")
+    return build_dir / (str(rel).replace(os.sep, "__") + ".o")
 
 
 def _hipcc() -> str:
@@ -72,7 +77,7 @@ def _cxx() -> str:
     return os.environ.get("RINGDP_CXX", shutil.which("g++") or "c++")
 
 
-def _compile_cmd(src: Path, obj: Path):
+def _compile_cmd(src: Path, obj: Path, sanitize: str | None = None):
     inc, _lib, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     common = [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-fPIC", "-std=c++17", f"-I{CSRC}"]
@@ -89,7 +94,8 @@ def _compile_cmd(src: Path, obj: Path):
         f"-DTORCH_EXTENSION_NAME={EXT_NAME}",
     ]
     incs = [f"-I{p}" for p in inc] + [f"-I{py_inc}", f"-I{ROCM / 'include'}"]
-    return [_cxx(), "-O2", "-g0", "-Wno-deprecated-declarations", *defs, *common, *incs,
+    opt = ["-O2", "-g0"] if not sanitize else ["-O1", "-g", f"-fsanitize={sanitize}", "-fno-omit-frame-pointer"]
+    return [_cxx(), *opt, "-Wno-deprecated-declarations", *defs, *common, *incs,
             "-c", str(src), "-o", str(obj)]
 
 
@@ -110,15 +116,26 @@ def _run(cmd):
     return r.stdout
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+def _link_cmd_sanitized(objs, out: Path, sanitize: str):
+    _inc, lib, _abi = _torch_paths()
+    libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+            "-lamdhip64", "-lrccl"]
+    return [_cxx(), "-shared", "-fPIC", f"-fsanitize={sanitize}", *map(str, objs), f"-L{lib}",
+            f"-L{ROCM / 'lib'}", *libs, f"-Wl,-rpath,{lib}", "-Wl,--no-as-needed", "-o", str(out)]
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
+          sanitize: str | None = None) -> Path:
     """Compile + link the extension; returns the path of the built shared object."""
-    BUILD.mkdir(parents=True, exist_ok=True)
+    bdir = BUILD if not sanitize else ROOT / "build" / f"native-{sanitize}"
+    bdir.mkdir(parents=True, exist_ok=True)
     hip, cpp = _sources()
     hdr_t = _headers_mtime()
     todo = []
     objs = []
     for src in hip + cpp:
-        obj = _obj_for(src)
+        # device code is never sanitized: reuse the regular objects
+        obj = _obj_for(src, BUILD if (sanitize and src.suffix == ".hip") else bdir)
         objs.append(obj)
         if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr_t):
             todo.append((src, obj))
@@ -127,16 +144,18 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if verbose:
             print(f"[ringdp build] compiling {len(todo)} file(s) with {jobs} job(s)", flush=True)
         with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-            futs = {ex.submit(_run, _compile_cmd(s, o)): s for s, o in todo}
+            futs = {ex.submit(_run, _compile_cmd(s, o, sanitize if s.suffix == ".cpp" else None)): s
+                    for s, o in todo}
             for f in cf.as_completed(futs):
                 f.result()
                 if verbose:
                     print(f"  built {futs[f].relative_to(ROOT)}", flush=True)
-    out = ext_path()
+    out = ext_path() if not sanitize else ROOT / "build" / sanitize / ext_path().name
+    out.parent.mkdir(parents=True, exist_ok=True)
     newest = max(o.stat().st_mtime for o in objs)
     if force or todo or not out.exists() or out.stat().st_mtime < newest:
         tmp = out.with_suffix(".tmp.so")
-        _run(_link_cmd(objs, tmp))
+        _run(_link_cmd(objs, tmp) if not sanitize else _link_cmd_sanitized(objs, tmp, sanitize))
         os.replace(tmp, out)
         if verbose:
             print(f"[ringdp build] linked {out.relative_to(ROOT)}", flush=True)
@@ -147,8 +166,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--sanitize", type=str, default=None, help="host-code sanitizer, e.g. 'address'")
     a = ap.parse_args(argv)
-    p = build(force=a.force, jobs=a.jobs, verbose=True)
+    p = build(force=a.force, jobs=a.jobs, verbose=True, sanitize=a.sanitize)
     print(p)
 
 

@@ -18,6 +18,17 @@ def load():
     global _C
     if _C is not None:
         return _C
+    alt = os.environ.get("RINGDP_EXT_PATH")
+    if alt:
+        # an alternative build of the same extension (e.g. the ASan host build, tools/asan_check.sh)
+        import importlib.util
+        import sys
+
+        spec = importlib.util.spec_from_file_location("ringdp._C", alt)
+        _C = importlib.util.module_from_spec(spec)
+        sys.modules["ringdp._C"] = _C
+        spec.loader.exec_module(_C)
+        return _C
     try:
         _C = importlib.import_module("ringdp._C")
     except ImportError as e:

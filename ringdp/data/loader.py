@@ -3,10 +3,15 @@
 ``DataLoader`` - the host loader the reference scripts use:
 ``DataLoader(dataset, batch_size=100, shuffle=False, pin_memory=True, sampler=DistributedSampler)``
 (ref/mpspawn_dist.py:88, ref/launch_dist.py:73-74) and ``num_workers=4`` for CIFAR
-(ref/example_mp.py:74-80).  Batches are produced in sampler order; ``num_workers`` > 0 assembles
-batches on a thread pool with a bounded prefetch window (the per-sample transforms are torch ops that
-release the GIL), and ``pin_memory`` pins every batch so ``.to(device, non_blocking=True)`` is a
-true async H2D copy.
+(ref/example_mp.py:74-80).  Batches are produced in sampler order.  ``num_workers`` > 0 starts that
+many worker *processes* (fork context by default, like torch on Linux): batch index lists go out
+round-robin on per-worker queues, collated batches come back through shared memory
+(torch.multiprocessing), a pin-memory thread in the main process pins them, and the iterator
+re-orders them so delivery follows the sampler exactly.  Each worker seeds torch's RNG with
+``base_seed + worker_id`` (random transforms differ per worker, reproducibly); a worker exception is
+re-raised in the main process with its traceback, a worker that dies is reported by pid.
+``worker_mode="thread"`` keeps the lighter thread-pool variant.  ``pin_memory`` pins every batch so
+``.to(device, non_blocking=True)`` is a true async H2D copy.
 
 ``DeviceLoader`` - the MI355X-first path (§2.4 U15): the whole uint8 dataset lives in HBM (MNIST is
 47 MB, CIFAR-10 150 MB against 288 GB), the epoch's sampler indices are one device tensor, and each
@@ -19,6 +24,9 @@ from __future__ import annotations
 import collections
 import concurrent.futures as cf
 import math
+import queue
+import threading
+import traceback
 from typing import Callable, Iterator, List, Optional, Sequence
 
 import torch
@@ -54,7 +62,12 @@ class DataLoader:
     def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False, sampler=None,
                  num_workers: int = 0, pin_memory: bool = False, drop_last: bool = False,
                  collate_fn: Optional[Callable] = None, prefetch_factor: int = 2,
-                 generator: Optional[torch.Generator] = None):
+                 generator: Optional[torch.Generator] = None, worker_init_fn: Optional[Callable] = None,
+                 multiprocessing_context=None, timeout: float = 0, worker_mode: str = "process"):
+        if worker_mode not in ("process", "thread"):
+            raise ValueError("worker_mode must be 'process' or 'thread'")
+        if timeout < 0:
+            raise ValueError("timeout option should be non-negative")
         if sampler is not None and shuffle:
             # same contract as torch: the sampler owns the order (ref/README.md:170)
             raise ValueError("sampler option is mutually exclusive with shuffle")
@@ -68,7 +81,13 @@ class DataLoader:
         self.pin_memory = bool(pin_memory) and torch.cuda.is_available()
         self.drop_last = drop_last
         self.collate_fn = collate_fn or default_collate
-        self.prefetch = max(1, prefetch_factor) * max(1, self.num_workers)
+        self.prefetch_factor = max(1, prefetch_factor)
+        self.prefetch = self.prefetch_factor * max(1, self.num_workers)
+        self.generator = generator
+        self.worker_init_fn = worker_init_fn
+        self.multiprocessing_context = multiprocessing_context
+        self.timeout = float(timeout)
+        self.worker_mode = worker_mode
 
     def __len__(self) -> int:
         n = len(self.sampler)
@@ -90,10 +109,18 @@ class DataLoader:
             batch = tuple(t.pin_memory() if isinstance(t, torch.Tensor) else t for t in batch)
         return batch
 
+    def _pin(self, batch):
+        if not self.pin_memory:
+            return batch
+        return tuple(t.pin_memory() if isinstance(t, torch.Tensor) else t for t in batch)
+
     def __iter__(self):
         if self.num_workers == 0:
             for idx in self._batches():
                 yield self._fetch(idx)
+            return
+        if self.worker_mode == "process":
+            yield from _MultiProcessIter(self)
             return
         with cf.ThreadPoolExecutor(self.num_workers, thread_name_prefix="ringdp-loader") as ex:
             pending: "collections.deque[cf.Future]" = collections.deque()
@@ -107,6 +134,152 @@ class DataLoader:
                 pending.append(ex.submit(self._fetch, idx))
             while pending:
                 yield pending.popleft().result()
+
+
+class _WorkerError:
+    def __init__(self, worker_id: int, exc: BaseException):
+        self.msg = (f"Caught {type(exc).__name__} in DataLoader worker process {worker_id}.\n"
+                    f"Original {traceback.format_exc()}")
+        self.exc_type = type(exc)
+
+
+def _worker_loop(dataset, collate_fn, index_q, result_q, base_seed: int, worker_id: int,
+                 num_workers: int, init_fn):
+    """Body of one DataLoader worker process (module level: picklable for spawn contexts)."""
+    torch.set_num_threads(1)
+    torch.manual_seed(base_seed + worker_id)
+    import random
+
+    random.seed(base_seed + worker_id)
+    try:
+        if init_fn is not None:
+            init_fn(worker_id)
+    except Exception as e:  # noqa: BLE001
+        result_q.put((-1, _WorkerError(worker_id, e)))
+        return
+    while True:
+        item = index_q.get()
+        if item is None:
+            break
+        bi, idx = item
+        try:
+            out = collate_fn([dataset[i] for i in idx])
+        except Exception as e:  # noqa: BLE001
+            out = _WorkerError(worker_id, e)
+        result_q.put((bi, out))
+
+
+class _MultiProcessIter:
+    """One epoch over worker processes: index lists round-robin out, results re-ordered in."""
+
+    _POLL_S = 1.0
+
+    def __init__(self, loader: DataLoader):
+        import torch.multiprocessing as tmp
+
+        self.loader = loader
+        ctx = loader.multiprocessing_context
+        if ctx is None or isinstance(ctx, str):
+            ctx = tmp.get_context(ctx or "fork")
+        W = loader.num_workers
+        base_seed = int(torch.empty((), dtype=torch.int64).random_(generator=loader.generator).item())
+        self.index_qs = [ctx.Queue() for _ in range(W)]
+        self.result_q = ctx.Queue()
+        self.workers = []
+        for wid in range(W):
+            w = ctx.Process(target=_worker_loop, args=(loader.dataset, loader.collate_fn, self.index_qs[wid],
+                                                       self.result_q, base_seed, wid, W, loader.worker_init_fn),
+                            daemon=True)
+            w.start()
+            self.workers.append(w)
+        # pin-memory thread: result queue -> (pinned) local queue
+        self.ready: "queue.Queue" = queue.Queue()
+        self.stop = threading.Event()
+        self.pin_thread = threading.Thread(target=self._pin_loop, daemon=True, name="ringdp-pin-memory")
+        self.pin_thread.start()
+        self.batches = loader._batches()
+        self.sent = 0
+        self.next = 0
+        self.buf = {}
+        self.done = False
+        for _ in range(loader.prefetch_factor * W):
+            self._put()
+
+    def _pin_loop(self):
+        while not self.stop.is_set():
+            try:
+                bi, data = self.result_q.get(timeout=0.1)
+            except queue.Empty:
+                continue
+            except (EOFError, OSError):
+                break
+            if not isinstance(data, _WorkerError):
+                try:
+                    data = self.loader._pin(data)
+                except Exception as e:  # noqa: BLE001
+                    data = _WorkerError(-1, e)
+            self.ready.put((bi, data))
+
+    def _put(self):
+        try:
+            idx = next(self.batches)
+        except StopIteration:
+            return
+        self.index_qs[self.sent % len(self.workers)].put((self.sent, idx))
+        self.sent += 1
+
+    def _shutdown(self):
+        if self.done:
+            return
+        self.done = True
+        for q in self.index_qs:
+            try:
+                q.put(None)
+            except Exception:  # noqa: BLE001
+                pass
+        for w in self.workers:
+            w.join(timeout=5)
+            if w.is_alive():
+                w.terminate()
+        self.stop.set()
+        self.pin_thread.join(timeout=5)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if self.next >= self.sent:
+            self._shutdown()
+            raise StopIteration
+        waited = 0.0
+        while self.next not in self.buf:
+            try:
+                bi, data = self.ready.get(timeout=self._POLL_S)
+            except queue.Empty:
+                waited += self._POLL_S
+                dead = [w for w in self.workers if not w.is_alive()]
+                if dead:
+                    self._shutdown()
+                    raise RuntimeError(f"DataLoader worker (pid(s) {', '.join(str(w.pid) for w in dead)}) "
+                                       f"exited unexpectedly (exit code {dead[0].exitcode})")
+                if self.loader.timeout and waited >= self.loader.timeout:
+                    self._shutdown()
+                    raise RuntimeError(f"DataLoader timed out after {self.loader.timeout} seconds")
+                continue
+            if isinstance(data, _WorkerError):
+                self._shutdown()
+                raise data.exc_type(data.msg) if data.exc_type is not KeyError else KeyError(data.msg)
+            self.buf[bi] = data
+        data = self.buf.pop(self.next)
+        self.next += 1
+        self._put()
+        return data
+
+    def __del__(self):
+        try:
+            self._shutdown()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 class DeviceLoader:

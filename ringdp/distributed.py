@@ -458,11 +458,21 @@ def new_group(ranks: Optional[Sequence[int]] = None, timeout: Optional[_dt.timed
     if len(set(ranks)) != len(ranks) or any(r < 0 or r >= world.size() for r in ranks):
         raise ValueError(f"ringdp.new_group: invalid ranks {ranks}")
     me = world.rank()
+    backends = Backend.normalize(backend) if backend is not None else dict(world._backends)
+    # RCCL sub-communicators come from ncclCommSplit of the world's communicator when that exists
+    # (every rank takes part in the split, non-members with NCCL_SPLIT_NOCOLOR), otherwise they are
+    # created lazily through the store on first use.
+    split = {}
+    if "rccl" in backends.values() and os.environ.get("RINGDP_COMM_SPLIT", "1") == "1":
+        for dev, parent in sorted(world._rccl.items()):
+            split[dev] = parent.split(ranks, name)
     if me not in ranks:
         return GroupMember.NON_GROUP_MEMBER
-    backends = Backend.normalize(backend) if backend is not None else dict(world._backends)
     pg = ProcessGroup(_world.store, ranks.index(me), len(ranks), backends, timeout or world._timeout,
                       ranks, name, _world.bind_hint)
+    for dev, child in split.items():
+        if child is not None:
+            pg._rccl[dev] = child
     _world.groups[name] = pg
     return pg
 
@@ -563,6 +573,8 @@ def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool
     if _not_member(group):
         return None
     g = _resolve(group)
+    if _coalesce(g, "all_reduce", tensor, op=op):
+        return None
     _pre(g, "all_reduce", [tensor], str(op))
     native, staged = g.native_for(tensor)
     ts, pairs = _stage([tensor], staged)
@@ -586,6 +598,8 @@ def broadcast(tensor: torch.Tensor, src: int = 0, group=None, async_op: bool = F
         return None
     g = _resolve(group)
     root = group_src if group_src is not None else g.local_rank_of(src)
+    if _coalesce(g, "broadcast", tensor, root=root):
+        return None
     _pre(g, "broadcast", [tensor], f"root={root}")
     native, staged = g.native_for(tensor)
     ts, pairs = _stage([tensor], staged)
@@ -611,6 +625,8 @@ def all_gather_into_tensor(output_tensor: torch.Tensor, input_tensor: torch.Tens
     if _not_member(group):
         return None
     g = _resolve(group)
+    if _coalesce(g, "all_gather_into_tensor", output_tensor, input_tensor):
+        return None
     _pre(g, "all_gather_into_tensor", [output_tensor, input_tensor])
     native, staged = g.native_for(input_tensor)
     (o, i), pairs = _stage([output_tensor, input_tensor], staged)
@@ -622,6 +638,8 @@ def reduce_scatter_tensor(output: torch.Tensor, input: torch.Tensor, op=ReduceOp
     if _not_member(group):
         return None
     g = _resolve(group)
+    if _coalesce(g, "reduce_scatter_tensor", output, input, op=op):
+        return None
     _pre(g, "reduce_scatter_tensor", [output, input], str(op))
     native, staged = g.native_for(input)
     (o, i), pairs = _stage([output, input], staged)
@@ -845,10 +863,75 @@ def scatter_object_list(scatter_object_output_list: List[Any], scatter_object_in
 
 
 # ----------------------------------------------------------------------------- misc helpers
+class _CoalescingManager:
+    """Collects the collectives issued inside ``_coalescing_manager`` and submits them as one
+    native batch (RCCL: a single ncclGroupStart/End, i.e. one fused launch and one completion
+    event).  Upstream: ``torch.distributed._coalescing_manager``."""
+
+    _KIND = {"all_reduce": 0, "broadcast": 1, "all_gather_into_tensor": 2, "reduce_scatter_tensor": 3}
+
+    def __init__(self, group: ProcessGroup):
+        self.group = group
+        self.ops = []
+        self.works = []
+
+    def append(self, kind: str, out: torch.Tensor, inp: Optional[torch.Tensor] = None, root: int = 0, op=None):
+        self.ops.append((self._KIND[kind], out, inp, root, _to_reduce_op(op if op is not None else ReduceOp.SUM)))
+
+    def flush(self):
+        if not self.ops:
+            return
+        native, staged = self.group.native_for(self.ops[0][1])
+        if staged:
+            # host backend with GPU tensors: issue one by one through the staging path
+            for kind, out, inp, root, op in self.ops:
+                if kind == 0:
+                    self.works.append(all_reduce(out, op, self.group, async_op=True))
+                elif kind == 1:
+                    self.works.append(broadcast(out, self.group.ranks[root], self.group, async_op=True))
+                elif kind == 2:
+                    self.works.append(all_gather_into_tensor(out, inp, self.group, async_op=True))
+                else:
+                    self.works.append(reduce_scatter_tensor(out, inp, op, self.group, async_op=True))
+        else:
+            self.works.append(native.coalesced(self.ops))
+        self.ops = []
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+
+_coalescing = threading.local()
+
+
+def _coalesce(g: ProcessGroup, kind: str, out, inp=None, root: int = 0, op=None) -> bool:
+    """Inside _coalescing_manager for group ``g``: record the op instead of issuing it."""
+    cm = getattr(_coalescing, "cm", None)
+    if cm is None or cm.group is not g:
+        return False
+    cm.append(kind, out, inp, root, op)
+    return True
+
+
 @contextmanager
 def _coalescing_manager(group=None, device=None, async_ops: bool = False):
-    """Compatibility shim: ops issued inside run eagerly (RCCL groups are formed per call)."""
-    yield None
+    """``with _coalescing_manager(group, async_ops=True) as cm: all_reduce(a); all_reduce(b)``
+    issues both as one RCCL group on exit; ``cm.wait()`` then fences the caller's stream
+    (``async_ops=False`` waits on exit)."""
+    g = _resolve(group)
+    if getattr(_coalescing, "cm", None) is not None:
+        raise RuntimeError("ringdp: _coalescing_manager cannot be nested")
+    cm = _CoalescingManager(g)
+    _coalescing.cm = cm
+    try:
+        yield cm
+    finally:
+        _coalescing.cm = None
+    cm.flush()
+    if not async_ops:
+        cm.wait()
 
 
 def get_default_store():

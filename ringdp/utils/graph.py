@@ -12,7 +12,8 @@ its graph-safe path (ringdp.optim.SGD flat path: no allocations, lr may be a dev
 """
 from __future__ import annotations
 
-from typing import Callable, Optional
+import os
+from typing import Callable, List, Optional
 
 import torch
 
@@ -27,12 +28,26 @@ def drain_comms():
             pg.drain()
 
 
+def _rccl_groups() -> List:
+    w = dist._world
+    return [pg for g in list(w.groups.values()) for pg in list(g._rccl.values())]
+
+
 class StepGraph:
+    """Capture/replay of one training step.
+
+    Watchdog: collectives inside a replay are invisible to the per-op RCCL watchdog (they were
+    issued once, at capture).  Each ``replay()`` therefore hands the replay's completion to every
+    RCCL group's watchdog (``RcclPG.watch_stream``): a replay that does not finish within the group
+    timeout - e.g. a peer died mid-step - aborts the communicator and exits non-zero, as a hung
+    eager collective does.  ``RINGDP_GRAPH_WATCHDOG=0`` turns this off."""
+
     def __init__(self, step_fn: Callable[[], Optional[torch.Tensor]], warmup: int = 3):
         self.step_fn = step_fn
         self.warmup = warmup
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.output = None
+        self._watch: List = []
 
     def capture(self):
         s = torch.cuda.Stream()
@@ -50,8 +65,15 @@ class StepGraph:
         # capture stream and make later eager steps on another stream synchronise against them
         self.output = out.detach() if torch.is_tensor(out) else out
         torch.cuda.synchronize()
+        if os.environ.get("RINGDP_GRAPH_WATCHDOG", "1") != "0":
+            dev = torch.cuda.current_device()
+            self._watch = [pg for pg in _rccl_groups() if pg.device == dev]
         return self
 
     def replay(self):
         self.graph.replay()
+        if self._watch:
+            s = torch.cuda.current_stream().cuda_stream
+            for pg in self._watch:
+                pg.watch_stream(s)
         return self.output

@@ -1,0 +1,226 @@
+"""Multi-rank workers shared by the multi-GPU tests (RCCL, one process per GPU) and their CPU
+rehearsal (host-ring "gloo", same code).  ``mode`` is "gpu" or "cpu".
+
+Reference: the reference trains DDP over NCCL with one process per GPU (ref/launch_dist.py:49-61,
+ref/example_mp.py:37-53); the checks mirror upstream's DDP tests:
+collective correctness, N ranks x B == 1 process x N*B, bit-identical replicas after every step,
+the same with the whole step in a hipGraph, deterministic bucket order under perturbed readiness.
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def _init(rank, world, port, mode, timeout_s=120):
+    import datetime
+
+    import ringdp.distributed as dist
+
+    if mode == "gpu":
+        torch.cuda.set_device(rank)
+        backend, dev = "nccl", torch.device("cuda", rank)
+    else:
+        torch.set_num_threads(1)
+        backend, dev = "gloo", torch.device("cpu")
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=timeout_s))
+    return dist, dev
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def collectives_worker(rank, world, port, result_dir, mode):
+    dist, dev = _init(rank, world, port, mode)
+    R = dist.ReduceOp
+    tri = world * (world + 1) // 2
+    for dt in (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int32, torch.int64):
+        for n in (1, 7, 4099, 1 << 20):
+            t = torch.full((n,), rank + 1, dtype=dt, device=dev)
+            dist.all_reduce(t)
+            assert torch.all(t == tri), (dt, n, t[:4])
+    for op, want in ((R.MAX, world - 1), (R.MIN, 0), (R.AVG, (world - 1) / 2)):
+        t = torch.full((33,), float(rank), device=dev)
+        dist.all_reduce(t, op=op)
+        assert torch.allclose(t, torch.full_like(t, want)), (op, t[:2])
+    t = torch.full((5,), float(rank + 1), device=dev)
+    dist.all_reduce(t, op=R.PRODUCT)
+    import math
+    assert torch.all(t == math.factorial(world))
+    # in-flight async ops complete in issue order and fence the caller's stream
+    ws = [dist.all_reduce(torch.full((1000,), float(i), device=dev), async_op=True) for i in range(8)]
+    for w in ws:
+        w.wait()
+    for root in range(world):
+        t = torch.full((1025,), float(rank), device=dev)
+        dist.broadcast(t, src=root)
+        assert torch.all(t == root)
+    outs = [torch.zeros(6, device=dev) for _ in range(world)]
+    dist.all_gather(outs, torch.full((6,), float(rank), device=dev))
+    assert all(torch.all(o == i) for i, o in enumerate(outs))
+    out = torch.zeros(world * 3, device=dev)
+    dist.all_gather_into_tensor(out, torch.full((3,), float(rank), device=dev))
+    assert torch.equal(out.cpu(), torch.arange(world).float().repeat_interleave(3))
+    inp = torch.arange(world * 4, dtype=torch.float32, device=dev)
+    out = torch.zeros(4, device=dev)
+    dist.reduce_scatter_tensor(out, inp)
+    assert torch.equal(out.cpu(), torch.arange(rank * 4, rank * 4 + 4).float() * world)
+    t = torch.ones(5, device=dev) * (rank + 1)
+    dist.reduce(t, dst=world - 1)
+    if rank == world - 1:
+        assert torch.all(t == tri)
+    inp = torch.arange(world, dtype=torch.float32, device=dev) + rank * world
+    out = torch.zeros(world, device=dev)
+    dist.all_to_all_single(out, inp)
+    assert torch.equal(out.cpu(), torch.tensor([float(r * world + rank) for r in range(world)]))
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    if world > 1:
+        buf = torch.zeros(10, device=dev)
+        if rank % 2 == 0:
+            dist.send(torch.full((10,), float(rank), device=dev), nxt)
+            dist.recv(buf, prv)
+        else:
+            dist.recv(buf, prv)
+            dist.send(torch.full((10,), float(rank), device=dev), nxt)
+        assert torch.all(buf == prv)
+    # sub-groups: evens, and a group of everyone but rank 0
+    even = dist.new_group([r for r in range(world) if r % 2 == 0])
+    if rank % 2 == 0:
+        t = torch.ones(3, device=dev)
+        dist.all_reduce(t, group=even)
+        assert torch.all(t == len(range(0, world, 2)))
+        assert dist.get_rank(even) == rank // 2
+    if world > 2:
+        rest = dist.new_group(list(range(1, world)))
+        if rank > 0:
+            t = torch.full((4,), float(rank), device=dev)
+            dist.broadcast(t, src=1, group=rest)
+            assert torch.all(t == 1)
+    # coalesced batch: one RCCL group (ncclGroupStart/End) on GPU, in-order issue on the host ring
+    a = torch.full((100,), float(rank + 1), device=dev)
+    b = torch.full((7,), float(rank), device=dev)
+    ag = torch.zeros(world * 2, device=dev)
+    rs = torch.zeros(3, device=dev)
+    with dist._coalescing_manager(async_ops=True) as cm:
+        dist.all_reduce(a)
+        dist.all_reduce(b, op=R.MAX)
+        dist.all_gather_into_tensor(ag, torch.full((2,), float(rank), device=dev))
+        dist.reduce_scatter_tensor(rs, torch.ones(world * 3, device=dev))
+        dist.broadcast(t := torch.full((5,), float(rank), device=dev), src=0)
+    cm.wait()
+    assert torch.all(a == tri) and torch.all(b == world - 1) and torch.all(t == 0)
+    assert torch.equal(ag.cpu(), torch.arange(world).float().repeat_interleave(2))
+    assert torch.all(rs == world)
+    objs = [None] * world
+    dist.all_gather_object(objs, {"rank": rank})
+    assert [o["rank"] for o in objs] == list(range(world))
+    dist.barrier()
+    _sync(dev)
+    with open(os.path.join(result_dir, f"r{rank}"), "w") as f:
+        f.write("ok")
+    dist.destroy_process_group()
+
+
+def _model(name, dev):
+    from ringdp import models
+
+    if name == "convnet":
+        return models.ConvNet().to(dev)
+    return models.resnet18(num_classes=10).to(dev)
+
+
+def _batches(name, world, B, steps, dev):
+    g = torch.Generator().manual_seed(11)
+    if name == "convnet":
+        xs = [torch.randint(0, 256, (world * B, 1, 28, 28), dtype=torch.uint8, generator=g) for _ in range(steps)]
+    else:
+        xs = [torch.randn(world * B, 3, 32, 32, generator=g) for _ in range(steps)]
+    ys = [torch.randint(0, 10, (world * B,), generator=g) for _ in range(steps)]
+    return [x.to(dev) for x in xs], [y.to(dev) for y in ys]
+
+
+def _flat(model):
+    return torch.cat([p.detach().float().reshape(-1) for p in model.parameters()])
+
+
+def ddp_train_worker(rank, world, port, result_dir, mode, name, graph, perturb):
+    """DDP training over `world` ranks; rank 0 then replays the same global batches in a single
+    process (per-rank chunks accumulated at 1/world, which is DDP's averaging also for BN models)
+    and stores both parameter vectors.  `perturb`: rank-dependent delays inside backward (bucket
+    launch order must not depend on readiness).  `graph`: steps 3.. are hipGraph replays."""
+    dist, dev = _init(rank, world, port, mode)
+    if mode == "gpu" and world == 1:
+        os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
+    from ringdp.nn import CrossEntropyLoss
+    from ringdp.optim import SGD
+    from ringdp.parallel import DistributedDataParallel as DDP
+    from ringdp.utils.graph import StepGraph
+
+    B, steps, lr = 8, 5, 0.05
+    torch.manual_seed(100 + rank)  # different init per rank: DDP must broadcast rank 0's
+    model = _model(name, dev)
+    ddp = DDP(model, device_ids=[rank] if mode == "gpu" else None, bucket_cap_mb=0.5 if name == "resnet18" else 0.1,
+              first_bucket_mb=0.05)
+    crit = CrossEntropyLoss()
+    opt = SGD(ddp.parameters(), lr=lr, momentum=0.9, nesterov=True, weight_decay=1e-4)
+    if perturb:
+        # stall the autograd thread at a rank-dependent parameter: readiness timing differs per rank
+        target = list(model.parameters())[(rank * 7) % len(list(model.parameters()))]
+        target.register_hook(lambda g: (time.sleep(0.02 * (rank + 1)), g)[1])
+    xs, ys = _batches(name, world, B, steps, dev)
+    sx = torch.empty_like(xs[0][:B])
+    sy = torch.empty_like(ys[0][:B])
+
+    def step(x, y):
+        loss = crit(ddp(x), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    g = None
+    same = []
+    for i in range(steps):
+        x, y = xs[i][rank * B:(rank + 1) * B], ys[i][rank * B:(rank + 1) * B]
+        if graph and i >= 2:
+            sx.copy_(x)
+            sy.copy_(y)
+            if g is None:  # capture records the step without running it
+                g = StepGraph(lambda: step(sx, sy), warmup=0).capture()
+            g.replay()
+        else:
+            step(x, y)
+        _sync(dev)
+        flat = _flat(model)
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        same.append(all(torch.equal(allp[0], a) for a in allp))
+    order = ddp.reducer.bucket_indices()
+    orders = [None] * world
+    dist.all_gather_object(orders, order)
+    res = {"same": same, "same_buckets": all(o == orders[0] for o in orders), "ddp": _flat(model).cpu(),
+           "n_buckets": len(order)}
+    if rank == 0:
+        torch.manual_seed(100)
+        ref = _model(name, dev)
+        ropt = SGD(ref.parameters(), lr=lr, momentum=0.9, nesterov=True, weight_decay=1e-4)
+        init = _flat(ref).cpu()
+        for i in range(steps):
+            ropt.zero_grad(set_to_none=True)
+            for r in range(world):
+                (crit(ref(xs[i][r * B:(r + 1) * B]), ys[i][r * B:(r + 1) * B]) / world).backward()
+            ropt.step()
+        _sync(dev)
+        res["ref"] = _flat(ref).cpu()
+        res["init"] = init
+    torch.save(res, os.path.join(result_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()

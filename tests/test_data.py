@@ -72,14 +72,14 @@ def test_transforms_semantics():
     assert torch.equal(T.RandomHorizontalFlip(p=0.0)(img), img)
 
 
-@pytest.mark.parametrize("workers", [0, 3])
-def test_dataloader_with_distributed_sampler(workers):
+@pytest.mark.parametrize("workers,mode", [(0, "process"), (3, "process"), (3, "thread")])
+def test_dataloader_with_distributed_sampler(workers, mode):
     ds = SyntheticImages(103, (28, 28), 10, seed=1, transform=T.ToTensor())
     seen = []
     for rank in range(2):
         s = DistributedSampler(ds, num_replicas=2, rank=rank, shuffle=True, seed=5)
         s.set_epoch(2)
-        dl = DataLoader(ds, batch_size=10, sampler=s, num_workers=workers)
+        dl = DataLoader(ds, batch_size=10, sampler=s, num_workers=workers, worker_mode=mode)
         order = list(iter(s))
         got = []
         for xb, yb in dl:
@@ -92,6 +92,45 @@ def test_dataloader_with_distributed_sampler(workers):
     with pytest.raises(ValueError):
         DataLoader(ds, batch_size=4, shuffle=True, sampler=DistributedSampler(ds, num_replicas=1, rank=0))
     assert len(DataLoader(ds, batch_size=10, drop_last=True)) == 10
+
+
+class _PidData:
+    """Each sample reports the pid of the process that produced it and a draw from torch's RNG."""
+
+    def __init__(self, n, fail_at=None):
+        self.n, self.fail_at = n, fail_at
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        if i == self.fail_at:
+            raise ValueError(f"bad sample {i}")
+        return torch.tensor([i, os.getpid()]), int(torch.randint(0, 1 << 30, ()))
+
+
+def test_dataloader_worker_processes():
+    ds = _PidData(40)
+    dl = DataLoader(ds, batch_size=4, num_workers=2, generator=torch.Generator().manual_seed(7))
+    ids, pids, draws = [], set(), []
+    for xb, rb in dl:
+        ids += xb[:, 0].tolist()
+        pids |= set(xb[:, 1].tolist())
+        draws.append(rb)
+    assert ids == list(range(40))                 # sampler order, whatever worker finished first
+    assert os.getpid() not in pids and len(pids) == 2  # produced in two separate processes
+    # reproducible per-worker seeding: the same generator seed gives the same random draws
+    dl2 = DataLoader(ds, batch_size=4, num_workers=2, generator=torch.Generator().manual_seed(7))
+    assert torch.equal(torch.cat(draws), torch.cat([r for _, r in dl2]))
+    # batch 0 (worker 0) and batch 1 (worker 1) drew from differently seeded streams
+    assert not torch.equal(draws[0], draws[1])
+
+
+def test_dataloader_worker_exception_propagates():
+    dl = DataLoader(_PidData(20, fail_at=13), batch_size=4, num_workers=2)
+    with pytest.raises(ValueError, match="bad sample 13"):
+        for _ in dl:
+            pass
 
 
 def _mix64(z):
