@@ -7,7 +7,9 @@ Set ``RINGDP_AUTOBUILD=1`` to compile it on first import instead.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 
 import torch  # noqa: F401  (loads libtorch / the bundled HIP runtime before our .so)
 
@@ -21,9 +23,6 @@ def load():
     alt = os.environ.get("RINGDP_EXT_PATH")
     if alt:
         # an alternative build of the same extension (e.g. the ASan host build, tools/asan_check.sh)
-        import importlib.util
-        import sys
-
         spec = importlib.util.spec_from_file_location("ringdp._C", alt)
         _C = importlib.util.module_from_spec(spec)
         sys.modules["ringdp._C"] = _C
