@@ -296,6 +296,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("drain", &RcclPG::drain, py::call_guard<py::gil_scoped_release>())
       .def("error_message", &RcclPG::error_message)
       .def("set_timing", &RcclPG::set_timing)
+      .def("p2p_max_bytes", &RcclPG::p2p_max_bytes)
+      .def("set_p2p_enabled", &RcclPG::set_p2p_enabled)
       .def("watch_stream",
            [](RcclPG& pg, uint64_t stream) {
              pg.watch_stream(reinterpret_cast<hipStream_t>(stream), OpType::GRAPH_REPLAY);
@@ -320,6 +322,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("FP16_COMPRESS", CommHook::FP16_COMPRESS)
       .value("PYTHON", CommHook::PYTHON)
       .value("NONE", CommHook::NONE);
+
+  // Standalone one-shot P2P all-reduce (tests; RcclPG owns one when enabled).  Ranks may share a
+  // GPU here - RCCL refuses that, IPC does not - which lets a one-GPU box run the multi-process path.
+  py::class_<P2PAllReduce, std::shared_ptr<P2PAllReduce>>(m, "P2PAllReduce")
+      .def(py::init([](std::shared_ptr<Store> store, int rank, int world, int device, int64_t max_bytes,
+                       int64_t timeout_ms) {
+             std::unique_ptr<P2PAllReduce> p;
+             {
+               py::gil_scoped_release nogil;
+               p = P2PAllReduce::create(store, rank, world, device, max_bytes, timeout_ms);
+             }
+             if (!p) throw RingdpError("[ringdp] P2P all-reduce setup failed on some rank");
+             return std::shared_ptr<P2PAllReduce>(std::move(p));
+           }),
+           py::arg("store"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("max_bytes"),
+           py::arg("timeout_ms"))
+      .def("eligible", &P2PAllReduce::eligible)
+      .def("run",
+           [](P2PAllReduce& p, at::Tensor t, bool average) {
+             RINGDP_CHECK(p.eligible(t), "P2PAllReduce.run: tensor not eligible (fp32/bf16, contiguous, 16-B multiple, <= max_bytes)");
+             p.run(t, average, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.get_device()).stream());
+           },
+           py::arg("tensor"), py::arg("average") = false)
+      .def("failed", &P2PAllReduce::failed)
+      .def_property_readonly("max_bytes", &P2PAllReduce::max_bytes);
 
   py::class_<BucketStats>(m, "BucketStats")
       .def_readonly("numel", &BucketStats::numel)

@@ -5,6 +5,7 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -133,6 +134,17 @@ RcclPG::RcclPG(std::shared_ptr<Store> store, int rank, int size, int device,
     std::memcpy(&uid, s.data(), sizeof(uid));
   }
   RINGDP_NCCL_CHECK(ncclCommInitRank(&comm_, size, uid, rank));
+  if (const char* e = std::getenv("RINGDP_P2P_ALLREDUCE_MAX_BYTES")) {
+    const int64_t max_bytes = std::atoll(e);
+    if (max_bytes > 0) {
+      // the kernel's own spin bound: the group timeout, capped so a dead peer ends it in minutes
+      const int64_t tmo = std::min<int64_t>(timeout_.count(), 300000);
+      p2p_ = P2PAllReduce::create(store, rank, size, device, max_bytes, tmo);
+      if (!p2p_ && rank == 0)
+        std::fprintf(stderr, "[ringdp] P2P all-reduce unavailable for this group (not one host, >8 ranks, "
+                             "or IPC setup failed); using RCCL for every size\n");
+    }
+  }
   init_common();
 }
 
@@ -168,6 +180,11 @@ void RcclPG::shutdown() {
     comm_ = nullptr;
   }
   inflight_.clear();
+  if (p2p_) {
+    DeviceScope ds(device_);
+    (void)hipStreamSynchronize(comm_stream_.stream());
+    p2p_.reset();
+  }
   if (ready_) {
     hipEventDestroy(ready_);
     ready_ = nullptr;
@@ -245,6 +262,10 @@ void RcclPG::watchdog_loop() {
         break;
       }
     }
+    if (failure.empty() && p2p_ && p2p_->failed()) {
+      failure = strcat_all("[ringdp] watchdog: rank ", rank_, " P2P all-reduce: a peer did not arrive "
+                           "within the timeout; aborting communicator");
+    }
     if (failure.empty() && comm_) {
       ncclResult_t async_err = ncclSuccess;
       if (ncclCommGetAsyncError(comm_, &async_err) == ncclSuccess && async_err != ncclSuccess &&
@@ -298,6 +319,13 @@ std::shared_ptr<Work> RcclPG::launch(OpType op, const std::vector<at::Tensor>& t
 
 std::shared_ptr<Work> RcclPG::allreduce(std::vector<at::Tensor>& tensors, ReduceOp op) {
   for (auto& t : tensors) check_tensor(t, "all_reduce");
+  if (p2p_ && p2p_on_ && tensors.size() == 1 && (op == ReduceOp::SUM || op == ReduceOp::AVG) &&
+      p2p_->eligible(tensors[0])) {
+    // small bucket on one xGMI node: one-shot read of every peer instead of 2(N-1) ring steps
+    return launch(OpType::ALLREDUCE, tensors, [&](hipStream_t s) {
+      p2p_->run(tensors[0], op == ReduceOp::AVG, s);
+    });
+  }
   auto red = to_nccl_op(op);
   return launch(OpType::ALLREDUCE, tensors, [&](hipStream_t s) {
     if (tensors.size() > 1) RINGDP_NCCL_CHECK(ncclGroupStart());

@@ -14,6 +14,7 @@
 #include <deque>
 #include <thread>
 
+#include "p2p_allreduce.h"
 #include "process_group.h"
 
 namespace ringdp {
@@ -94,6 +95,9 @@ class RcclPG : public ProcessGroup {
   void set_timing(bool on) { timing_ = on; }
   bool timing() const { return timing_; }
   void set_async_error_handling(bool on) { async_error_handling_ = on; }
+  // One-shot P2P all-reduce for small buckets (RINGDP_P2P_ALLREDUCE_MAX_BYTES > 0 at creation).
+  int64_t p2p_max_bytes() const { return p2p_ ? p2p_->max_bytes() : 0; }
+  void set_p2p_enabled(bool on) { p2p_on_ = on; }
   std::chrono::milliseconds timeout() const { return timeout_; }
 
  private:
@@ -105,6 +109,8 @@ class RcclPG : public ProcessGroup {
   void check_tensor(const at::Tensor& t, const char* what) const;
 
   ncclComm_t comm_ = nullptr;
+  std::unique_ptr<P2PAllReduce> p2p_;
+  bool p2p_on_ = true;
   int device_;
   std::chrono::milliseconds timeout_;
   // Normal priority by default: on gfx950 an eager step with its collectives on a high-priority

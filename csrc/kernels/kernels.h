@@ -40,6 +40,26 @@ void sgd_multi(const SgdTensor* table, const int64_t* chunks, int64_t nchunks, i
 // Deterministic split-K reduction: out[i] = sum_s slabs[s * n + i] (fixed order).
 void splitk_reduce(const float* slabs, int nslices, int64_t n, float* out, hipStream_t s);
 
+// ---------------------------------------------------------------- one-shot P2P all-reduce
+// (p2p.hip; host side csrc/comm/p2p_allreduce.cpp)
+constexpr int kP2PMaxRanks = 8;
+struct P2PArgs {
+  char* bufs[kP2PMaxRanks];       // staging buffer of every rank (IPC-mapped), 2 slots each
+  unsigned* flags[kP2PMaxRanks];  // flag block of every rank: [segment][source rank]
+  void* data;                     // in/out tensor (local)
+  unsigned* epochs;               // local per-segment epoch counters
+  int* error;                     // local: set when a peer did not arrive in time
+  int64_t nbytes;                 // multiple of 16
+  int64_t slot_bytes;             // bytes per staging slot
+  int seg_bytes;                  // bytes per workgroup segment (multiple of 16)
+  int world;
+  int rank;
+  int dtype;                      // 0 fp32, 1 bf16
+  float scale;                    // 1 (sum) or 1/world (average)
+  uint64_t timeout_ticks;         // wall_clock64 ticks (100 MHz)
+};
+void p2p_allreduce(const P2PArgs& a, hipStream_t s);
+
 // ---------------------------------------------------------------- cross entropy
 // logits [B, C] fp32; labels int64 [B]; writes lse [B], loss scalar (or per-row for
 // reduction none), denom (number of non-ignored rows) in ws.

@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""All-reduce latency / bandwidth sweep on ringdp's GPU process group (RCCL vs the one-shot P2P path).
+
+Sizes default to the DDP buckets that matter here: the ConvNet's two rebuilt
+buckets (77 KB, 377 KB) and its whole gradient (455 KB), then 1 / 4 / 25 MB.  For every size and
+dtype it times, per rank, a hipGraph of ``--reps`` back-to-back all-reduces (no launch overhead:
+what a captured training step sees) and reports the max over ranks as us/op plus algbw
+(S/t) and busbw (2(N-1)/N * S/t, the per-GPU ring traffic rate).
+
+  python tools/comm_bench.py --gpus 8                        # launches 8 ranks itself (ringdp.run)
+  python tools/comm_bench.py --gpus 8 --sweep                # + NCCL_ALGO / channel variants
+  python -m ringdp.run --nproc-per-node 8 tools/comm_bench.py
+
+The P2P rows exist when RINGDP_P2P_ALLREDUCE_MAX_BYTES is set (this tool sets 4 MiB unless told
+otherwise); the crossover between the two rows is the threshold to use for
+RINGDP_P2P_ALLREDUCE_MAX_BYTES in training.  Rank 0 prints one JSON line per measurement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+SWEEP = [
+    {},
+    {"NCCL_ALGO": "Ring"},
+    {"NCCL_ALGO": "Tree"},
+    {"NCCL_PROTO": "LL"},
+    {"NCCL_PROTO": "LL128"},
+    {"NCCL_MIN_NCHANNELS": "16"},
+    {"NCCL_MIN_NCHANNELS": "32"},
+]
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--sizes", type=str, default="77312,377408,454720,1048576,4194304,26214400",
+                    help="bytes, comma separated")
+    ap.add_argument("--dtypes", type=str, default="fp32,bf16")
+    ap.add_argument("--reps", type=int, default=20, help="all-reduces per graph")
+    ap.add_argument("--iters", type=int, default=20, help="timed graph replays")
+    ap.add_argument("--sweep", action="store_true", help="repeat under each RCCL env variant (parent mode)")
+    return ap.parse_args()
+
+
+def worker(args):
+    import torch
+
+    import ringdp.distributed as dist
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if os.environ.get("WORLD_SIZE"):
+        dist.init_process_group("nccl")
+    else:
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dev = torch.device("cuda", local)
+    probe = torch.zeros(1, device=dev)
+    dist.all_reduce(probe)
+    pg = dist._default().rccl(local)
+    impls = ["rccl"] + (["p2p"] if pg.p2p_max_bytes() > 0 else [])
+    variant = {k: os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS") if k in os.environ}
+    for dt_name in args.dtypes.split(","):
+        dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[dt_name]
+        es = torch.tensor([], dtype=dtype).element_size()
+        for nbytes in (int(s) for s in args.sizes.split(",")):
+            n = max(1, nbytes // es)
+            t = torch.ones(n, dtype=dtype, device=dev)
+            for impl in impls:
+                if impl == "p2p" and nbytes > pg.p2p_max_bytes():
+                    continue
+                pg.set_p2p_enabled(impl == "p2p")
+                for _ in range(3):
+                    dist.all_reduce(t, op=dist.ReduceOp.AVG)
+                torch.cuda.synchronize()
+                s = torch.cuda.Stream()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+                    for _ in range(args.reps):
+                        dist.all_reduce(t, op=dist.ReduceOp.AVG)
+                g.replay()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(args.iters):
+                    g.replay()
+                torch.cuda.synchronize()
+                el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+                dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                us = float(el.item()) * 1e6 / (args.iters * args.reps)
+                ok = bool(torch.all(t == 1).item())  # average of ones stays one
+                if rank == 0:
+                    algbw = nbytes / (us * 1e-6) / 1e9
+                    print(json.dumps({"impl": impl, "world": world, "dtype": dt_name, "bytes": nbytes,
+                                      "us_per_op": round(us, 2), "algbw_GBps": round(algbw, 2),
+                                      "busbw_GBps": round(algbw * 2 * (world - 1) / max(world, 1), 2),
+                                      "correct": ok, "rccl_env": variant}), flush=True)
+                del g
+    pg.set_p2p_enabled(True)
+    dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    os.environ.setdefault("RINGDP_P2P_ALLREDUCE_MAX_BYTES", str(4 << 20))
+    if os.environ.get("WORLD_SIZE") is None and (args.gpus > 1 or args.sweep):
+        from ringdp.run import launch_local
+
+        argv = [a for a in sys.argv[1:] if a != "--sweep"]
+        rc = 0
+        for env in (SWEEP if args.sweep else [{}]):
+            rc = launch_local(os.path.abspath(__file__), argv, args.gpus, env=env) or rc
+        sys.exit(rc)
+    worker(args)
+
+
+if __name__ == "__main__":
+    main()
