@@ -479,6 +479,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
   m.def("set_fp8_tile_mode", &ops::set_fp8_tile_mode,
         "fp8 GEMM kernel choice: 0 auto, 128 the generic 128x128 core, 256 the 256x256 DMA-pipelined kernel");
+  m.def("f32_conv_fwd", &ops::f32_conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
+        py::arg("mean") = 0.0, py::arg("std") = 1.0);
+  m.def("f32_conv_dgrad", &ops::f32_conv_dgrad);
+  m.def("f32_conv_wgrad", &ops::f32_conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("pad"), py::arg("mean"),
+        py::arg("std"), py::arg("dw"), py::arg("db"));
+  m.def("f32_pool_relu_fwd", &ops::f32_pool_relu_fwd);
+  m.def("f32_pool_relu_bwd", &ops::f32_pool_relu_bwd);
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);

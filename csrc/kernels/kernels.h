@@ -60,6 +60,28 @@ struct P2PArgs {
 };
 void p2p_allreduce(const P2PArgs& a, hipStream_t s);
 
+// ---------------------------------------------------------------- fp32 NCHW conv / pool (conv_f32.hip)
+// stride-1 conv, square kernel R, symmetric zero padding; fc layers are R=1 convs over 1x1 images
+struct ConvF32Geom {
+  int64_t B;
+  int C, H, W;     // input
+  int Kout, R, pad;
+  int OH, OW;      // output
+};
+// z = conv(x) + bias.  Input either fp32 `x` or raw uint8 `xu8` normalised on load ((v/255-mean)*inv_std).
+void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
+                  const float* w, const float* bias, float* z, hipStream_t s);
+void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, hipStream_t s);
+// split-K weight (+ bias, when db != nullptr) gradient; slab: slices * Kout * (C*R*R + 1) floats
+int conv_f32_wgrad_slices(const ConvF32Geom& g);
+void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const unsigned char* xu8, float mean,
+                    float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s);
+// a = relu(maxpool_k,st(z)) with a 1-byte argmax code (255: no gradient); backward is a gather
+void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,
+                       hipStream_t s);
+void pool_relu_f32_bwd(const float* da, const unsigned char* code, float* dz, int64_t BC, int H, int W, int k,
+                       int st, hipStream_t s);
+
 // ---------------------------------------------------------------- cross entropy
 // logits [B, C] fp32; labels int64 [B]; writes lse [B], loss scalar (or per-row for
 // reduction none), denom (number of non-ignored rows) in ws.

@@ -1,0 +1,130 @@
+// Tensor-level wrappers for the fp32 NCHW conv / pool kernels (csrc/kernels/conv_f32.hip): the
+// ConvNet at the reference's fp32 precision (ringdp/ops/convnet_fp32.py).
+#include <torch/extension.h>
+
+#include "../kernels/kernels.h"
+#include "util.h"
+
+namespace ringdp {
+namespace ops {
+
+namespace {
+
+kern::ConvF32Geom geom(const at::Tensor& x, const at::Tensor& w, int64_t pad) {
+  RINGDP_CHECK(x.dim() == 4 && w.dim() == 4, "conv_f32: expected 4-d input and weight");
+  RINGDP_CHECK(w.size(2) == w.size(3), "conv_f32: square kernels only");
+  RINGDP_CHECK(w.size(1) == x.size(1), "conv_f32: weight expects ", w.size(1), " input channels, input has ",
+               x.size(1));
+  kern::ConvF32Geom g;
+  g.B = x.size(0);
+  g.C = static_cast<int>(x.size(1));
+  g.H = static_cast<int>(x.size(2));
+  g.W = static_cast<int>(x.size(3));
+  g.Kout = static_cast<int>(w.size(0));
+  g.R = static_cast<int>(w.size(2));
+  g.pad = static_cast<int>(pad);
+  g.OH = g.H + 2 * g.pad - g.R + 1;
+  g.OW = g.W + 2 * g.pad - g.R + 1;
+  RINGDP_CHECK(g.OH > 0 && g.OW > 0, "conv_f32: empty output");
+  return g;
+}
+
+void check_input(const at::Tensor& x) {
+  util::gpu(x, "conv_f32 input");
+  RINGDP_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kByte,
+               "conv_f32 input: fp32 or raw uint8 pixels expected");
+}
+
+}  // namespace
+
+at::Tensor f32_conv_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                        int64_t pad, double mean, double std) {
+  check_input(x);
+  util::f32_gpu(w, "conv_f32 weight");
+  auto g = geom(x, w, pad);
+  const float* b = nullptr;
+  if (bias && bias->defined()) {
+    util::f32_gpu(*bias, "conv_f32 bias");
+    RINGDP_CHECK(bias->numel() == g.Kout, "conv_f32 bias: wrong size");
+    b = bias->data_ptr<float>();
+  }
+  auto z = at::empty({g.B, g.Kout, g.OH, g.OW}, w.options());
+  const bool u8 = x.scalar_type() == at::kByte;
+  kern::conv_f32_fwd(g, u8 ? nullptr : x.data_ptr<float>(), u8 ? x.data_ptr<uint8_t>() : nullptr,
+                     static_cast<float>(mean), static_cast<float>(1.0 / std), w.data_ptr<float>(), b,
+                     z.data_ptr<float>(), util::stream_of(w));
+  return z;
+}
+
+at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad) {
+  util::f32_gpu(dz, "conv_f32 dz");
+  util::f32_gpu(w, "conv_f32 weight");
+  kern::ConvF32Geom g;
+  g.B = dz.size(0);
+  g.Kout = static_cast<int>(w.size(0));
+  g.C = static_cast<int>(w.size(1));
+  g.R = static_cast<int>(w.size(2));
+  g.H = static_cast<int>(H);
+  g.W = static_cast<int>(W);
+  g.pad = static_cast<int>(pad);
+  g.OH = g.H + 2 * g.pad - g.R + 1;
+  g.OW = g.W + 2 * g.pad - g.R + 1;
+  RINGDP_CHECK(dz.dim() == 4 && dz.size(1) == g.Kout && dz.size(2) == g.OH && dz.size(3) == g.OW,
+               "conv_f32 dgrad: dz has shape ", dz.sizes());
+  auto dx = at::empty({g.B, g.C, g.H, g.W}, dz.options());
+  kern::conv_f32_dgrad(g, dz.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(), util::stream_of(dz));
+  return dx;
+}
+
+void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
+                    at::Tensor& dw, const c10::optional<at::Tensor>& db) {
+  check_input(x);
+  util::f32_gpu(dz, "conv_f32 dz");
+  util::f32_gpu(dw, "conv_f32 dw");
+  auto g = geom(x, dw, pad);
+  RINGDP_CHECK(dz.dim() == 4 && dz.size(0) == g.B && dz.size(1) == g.Kout && dz.size(2) == g.OH &&
+                   dz.size(3) == g.OW,
+               "conv_f32 wgrad: dz has shape ", dz.sizes());
+  float* dbp = nullptr;
+  if (db && db->defined()) {
+    util::f32_gpu(*db, "conv_f32 db");
+    RINGDP_CHECK(db->numel() == g.Kout, "conv_f32 db: wrong size");
+    dbp = db->data_ptr<float>();
+  }
+  const int slices = kern::conv_f32_wgrad_slices(g);
+  auto slab = at::empty({static_cast<int64_t>(slices) * g.Kout * (g.C * g.R * g.R + 1)}, dz.options());
+  const bool u8 = x.scalar_type() == at::kByte;
+  kern::conv_f32_wgrad(g, dz.data_ptr<float>(), u8 ? nullptr : x.data_ptr<float>(),
+                       u8 ? x.data_ptr<uint8_t>() : nullptr, static_cast<float>(mean),
+                       static_cast<float>(1.0 / std), slab.data_ptr<float>(), slices, dw.data_ptr<float>(), dbp,
+                       util::stream_of(dz));
+}
+
+std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_t k, int64_t stride) {
+  util::f32_gpu(z, "pool_relu_f32 input");
+  RINGDP_CHECK(z.dim() == 4, "pool_relu_f32: 4-d input expected");
+  const int64_t H = z.size(2), W = z.size(3);
+  const int64_t PH = (H - k) / stride + 1, PW = (W - k) / stride + 1;
+  RINGDP_CHECK(k >= 1 && k * k <= 254 && PH > 0 && PW > 0, "pool_relu_f32: bad window");
+  auto a = at::empty({z.size(0), z.size(1), PH, PW}, z.options());
+  auto code = at::empty({z.size(0), z.size(1), PH, PW}, z.options().dtype(at::kByte));
+  kern::pool_relu_f32_fwd(z.data_ptr<float>(), a.data_ptr<float>(), code.data_ptr<uint8_t>(),
+                          z.size(0) * z.size(1), static_cast<int>(H), static_cast<int>(W), static_cast<int>(k),
+                          static_cast<int>(stride), util::stream_of(z));
+  return {a, code};
+}
+
+at::Tensor f32_pool_relu_bwd(const at::Tensor& da, const at::Tensor& code, int64_t H, int64_t W, int64_t k,
+                             int64_t stride) {
+  util::f32_gpu(da, "pool_relu_f32 grad");
+  util::gpu(code, "pool_relu_f32 code");
+  RINGDP_CHECK(code.sizes() == da.sizes(), "pool_relu_f32 bwd: code/grad shape mismatch");
+  auto dz = at::empty({da.size(0), da.size(1), H, W}, da.options());
+  kern::pool_relu_f32_bwd(da.data_ptr<float>(), code.data_ptr<uint8_t>(), dz.data_ptr<float>(),
+                          da.size(0) * da.size(1), static_cast<int>(H), static_cast<int>(W), static_cast<int>(k),
+                          static_cast<int>(stride), util::stream_of(da));
+  return dz;
+}
+
+}  // namespace ops
+}  // namespace ringdp

@@ -82,5 +82,15 @@ std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t
                                                    int64_t num_classes, int64_t seed,
                                                    at::Device device);
 
+// fp32 NCHW conv / pool (conv_f32_ops.cpp)
+at::Tensor f32_conv_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
+                        int64_t pad, double mean, double std);
+at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad);
+void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
+                    at::Tensor& dw, const c10::optional<at::Tensor>& db);
+std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_t k, int64_t stride);
+at::Tensor f32_pool_relu_bwd(const at::Tensor& da, const at::Tensor& code, int64_t H, int64_t W, int64_t k,
+                             int64_t stride);
+
 }  // namespace ops
 }  // namespace ringdp
