@@ -75,6 +75,12 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
     const int j = r & 7, lane = (r >> 3) & 63, ks = (r >> 9) % KS, nt = (r >> 9) / KS;
     const int co = nt * 16 + (lane & 15), k = ks * 32 + 8 * (lane >> 4) + j;
     v = w[(co * CIN + k % CIN) * 9 + k / CIN];
+  } else if (e >= P3D_OFF && e < PFC_OFF) {
+    // conv3 dgrad, scatter form: A[row = ci][k = co] of tap t = W3[co][ci][t]; [ci tile][tap][kstep][lane][8]
+    const int r = e - P3D_OFF;
+    const int j = r & 7, lane = (r >> 3) & 63, ks = (r >> 9) % 36, nt = (r >> 9) / 36;
+    const int ci = nt * 16 + (lane & 15), tap = ks >> 2, co = (ks & 3) * 32 + 8 * (lane >> 4) + j;
+    v = w3[(co * 64 + ci) * 9 + tap];
   } else if (e < PFC_OFF) {  // dgrad fragments: B[k = tap'*COUT + co][n = ci] = W[co][ci][8 - tap']
     const bool l2 = e < P3D_OFF;
     const int r = e - (l2 ? P2D_OFF : P3D_OFF);
@@ -748,12 +754,16 @@ __device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int
   }
 }
 
-// dgrad GEMM per image, operands swapped so the output lands channel-contiguous:
-//   C[c = 64 input channels][m = 100 positions] = sum_k W3d[c][k] * Pimg[k][m],  K = 9 taps x 128.
-// 4 waves = 2 K-groups (18 of the 36 k-steps each) x 2 channel halves; a wave keeps the weight
-// fragments of its K-group and 2 channel tiles in VGPRs (144) for every image, covers all 7 position
-// tiles, and uses each image fragment it reads from LDS for 2 MFMAs.  The two K-group partials are
-// combined in a fixed order (deterministic).
+// dgrad per image in scatter form (the transpose of the forward conv, without its zero taps):
+//   Y[ci][(tap, p)] = sum_co W3[co][ci][tap] * dz3[p][co],   da2[p + off(tap)][ci] += Y[ci][(tap, p)]
+// over the 64 positions p of the 8x8 dz3 image, K = 128 output channels: 9 x 4 x 4 = 144 MFMAs per wave
+// (the full correlation over the 10x10 a2 image with the 3x3 flipped kernel needed 252: 900 (position,
+// tap) pairs of which only 576 are non-zero, padded to 7 m-tiles).  Operands are swapped so a lane's 4
+// results are 4 consecutive input channels of one position: wave w owns input channels 16w..16w+15,
+// so its col2im accumulation into the fp32 da2 image never meets another wave's.  Per tap, the 4
+// m-tiles (dz3 row pairs) hit disjoint da2 rows, so their read-add-writes are independent; consecutive
+// taps may hit the same da2 words from different lanes, so a compiler barrier keeps tap t+1's reads
+// behind tap t's writes (LDS executes one wave's instructions in order).  Fixed order: deterministic.
 __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ dz2, int B, int block, int nblocks) {
@@ -761,58 +771,49 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
   uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P);
   float* DA = reinterpret_cast<float*>(smem + C3D_P + C3D_AM);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int kg = wave >> 1, nh = wave & 1;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3D_OFF);
-  bf16x8 aw[2][18];
+  bf16x8 aw[36];  // [tap][kstep] weight fragments of this wave's 16 input channels
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int j = 0; j < 18; ++j) aw[t][j] = pk[((2 * nh + t) * 36 + 18 * kg + j) * 64 + lane];
-  int base[7];  // positions >= 100 read a clamped (valid) address; their outputs are dropped
-#pragma unroll
-  for (int mt = 0; mt < 7; ++mt) {
-    const int mm = min(mt * 16 + r16, 99);
-    base[mt] = (mm / 10) * C3_PY + (mm % 10) * C3_PX;
-  }
+  for (int j = 0; j < 36; ++j) aw[j] = pk[(wave * 36 + j) * 64 + lane];
+  // dz3 position p = 16 mt + r16 = (2 mt + (r16 >> 3), r16 & 7); its tap-(0,0) da2 target is p's (y, x)
+  const int pbase = ((r16 >> 3) + 2) * C3_PY + ((r16 & 7) + 2) * C3_PX + q8;
+  const int dbase = ((r16 >> 3) * 10 + (r16 & 7)) * C3_DARS + 16 * wave + c4;
   // the ring of the padded image stays zero; only the 8x8 interior is rewritten per image
   for (int c = tid; c < C3D_P / 16; c += 256) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
-  // the K-group is a template parameter, so every fragment address is a per-lane base plus an
-  // immediate offset (no hoisted address VGPRs)
-  auto mfma_phase = [&](auto kg_c) {
-    constexpr int KG = decltype(kg_c)::value;
-    f32x4 acc[7][2];
+  auto mfma_phase = [&]() {
+    for (int i = lane; i < 400; i += 64)  // this wave's 16-channel slice of da2
+      *reinterpret_cast<f32x4*>(DA + (i >> 2) * C3_DARS + 16 * wave + 4 * (i & 3)) = zero_f32x4();
+    // two m-tiles (4 dz3 rows) at a time keeps the B fragments at 32 VGPRs beside the 144 of weights
 #pragma unroll
-    for (int mt = 0; mt < 7; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 bfr[2][4];
 #pragma unroll
-    for (int j = 0; j < 18; ++j) {
-      const int ks = 18 * KG + j;
-      const int tapp = ks >> 2, c0 = (ks & 3) * 32;
-      const int shift = (tapp / 3) * C3_PY + (tapp % 3) * C3_PX;
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
-      for (int mt = 0; mt < 7; ++mt) {
-        const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(P + base[mt] + shift + c0 + q8);
-        acc[mt][0] = mfma16x16x32(aw[0][j], bfr, acc[mt][0]);
-        acc[mt][1] = mfma16x16x32(aw[1][j], bfr, acc[mt][1]);
+        for (int ks = 0; ks < 4; ++ks)
+          bfr[m][ks] = *reinterpret_cast<const bf16x8*>(P + pbase + 2 * (2 * half + m) * C3_PY + ks * 32);
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        f32x4 acc[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          acc[m] = zero_f32x4();
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) acc[m] = mfma16x16x32(aw[tap * 4 + ks], bfr[m][ks], acc[m]);
+        }
+        f32x4* d[2];
+        f32x4 old[2];
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          d[m] = reinterpret_cast<f32x4*>(DA + dbase + (20 * (2 * half + m) + (tap / 3) * 10 + tap % 3) * C3_DARS);
+          old[m] = *d[m];
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) *d[m] = old[m] + acc[m];
+        asm volatile("" ::: "memory");  // the next tap's reads stay behind these writes
       }
     }
-    // K-group 1 publishes, K-group 0 folds its partial in
-    auto publish = [&](bool add) {
-#pragma unroll
-      for (int mt = 0; mt < 7; ++mt) {
-        const int m = mt * 16 + r16;
-        if (m < 100) {
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            f32x4* d = reinterpret_cast<f32x4*>(DA + m * C3_DARS + (2 * nh + t) * 16 + c4);
-            *d = add ? acc[mt][t] + *d : acc[mt][t];
-          }
-        }
-      }
-    };
-    if (KG == 1) publish(false);
-    __syncthreads();
-    if (KG == 0) publish(true);
   };
   // pool2 + ReLU backward, one item per (output row y, channel quad), sliding along x: window (py, px)
   // covers outputs (py..py+1, px..px+1) and its one-hot code bit dy*2+dx names the one that receives
@@ -840,10 +841,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
     const int nb = b + nblocks;
     if (nb < B) pre.load(da3m, idx3, nb, tid);
     __syncthreads();
-    if (kg == 0)
-      mfma_phase(std::integral_constant<int, 0>{});
-    else
-      mfma_phase(std::integral_constant<int, 1>{});
+    mfma_phase();
     c_dma_wait();
     __syncthreads();
     if (tid < 176) {
@@ -1426,6 +1424,8 @@ static double split_frac(const char* env, double dflt) {
   return f > 0.05 && f < 0.95 ? f : dflt;
 }
 
+// dgrad and wgrad do the same MFMA work per image since the scatter-form dgrad (576 each per
+// workgroup image / image pair); measured best split 0.5-0.6 of the workgroup slots (B=32768).
 static void c3_split(int B, bool dgrad, int& nd, int& ws) {
   // 256-thread workgroups, two per CU; ws = image slices, each served by a pair of workgroups
   const int slots = 2 * num_cus();
@@ -1434,7 +1434,7 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
     ws = clampi(cdiv(B, 8), 1, slots / 2);
     return;
   }
-  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.70);
+  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.55);
   nd = clampi(B, 1, (int)(frac * slots));
   const int per = cdiv(B, nd);
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, (slots - nd) / 2));  // >= 2 images per slab
