@@ -602,7 +602,10 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ a
 //       da3m[b][w][co] = (a3 > 0) * sum_n dl[b][n] * Wfc[n][co*16 + w]     (bf16, Wfc from the pack)
 //     and the fc1 weight/bias gradient of this block's images as an fp32 slab.  The conv3 backward
 //     roles expand da3m to window-ordered rows (row 4w + argmax) in LDS.
-constexpr int FC_IMGS = 32;              // images per workgroup
+// images per workgroup: enough workgroups to fill the chip at small batches (B=100: 25 of 4 images,
+// was 4 of 32 and latency-bound at 21 us), fewer fp32 slabs at large ones (B=32768: 512 of 64 images,
+// halving the 84 MB of slab traffic)
+__host__ __device__ inline int fc_imgs(int B) { return B <= 1024 ? 4 : (B >= 32768 ? 64 : 32); }
 constexpr int FC_SLAB = 10 * 2048 + 10 + 128;  // dWfc + dbfc + db3 (the conv3 bias gradient is the sum of
                                                 // d(a3) over windows: no MFMA tile needed for it)
 
@@ -610,7 +613,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
                                                      const bf16* __restrict__ packed,
                                                      const float* __restrict__ dl,
                                                      bf16* __restrict__ da3m, float* __restrict__ slabs,
-                                                     int B) {
+                                                     int B, int imgs) {
   const int t = threadIdx.x;
   const int wd = t >> 4, co0 = (t & 15) * 8;  // this thread's 8 activations: window wd, channels co0..
   float wr[8][10];
@@ -632,7 +635,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
   float bacc = 0.f, dsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) dsum[j] = 0.f;
-  const int b0 = blockIdx.x * FC_IMGS, nimg = min(FC_IMGS, B - b0);
+  const int b0 = blockIdx.x * imgs, nimg = min(imgs, B - b0);
   for (int k0 = 0; k0 < nimg; k0 += 8) {
     bf16x8 av[8];
 #pragma unroll
@@ -1455,7 +1458,7 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
 
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 3 * num_cus()); }
 
-int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, FC_IMGS) * FC_SLAB; }
+int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, fc_imgs(B)) * FC_SLAB; }
 int64_t cn_conv3_slab_floats(int B, bool dgrad) {
   int nd, ws;
   c3_split(B, dgrad, nd, ws);
@@ -1474,9 +1477,9 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
   (void)wfc;  // the data gradient uses the packed bf16 copy, like every other dgrad
   int nd, ws;
   c3_split(B, dz2 != nullptr, nd, ws);
-  const int fs = cdiv(B, FC_IMGS);
+  const int fs = cdiv(B, fc_imgs(B));
   fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
-                                   static_cast<bf16*>(da3m), fc_slabs, B);
+                                   static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B));
   conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
                                            idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
                                            c3_slabs, ws, nd);
