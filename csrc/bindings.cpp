@@ -7,6 +7,7 @@
 #include "comm/fake_pg.h"
 #include "comm/host_ring.h"
 #include "comm/rccl_pg.h"
+#include "ops/blaslt.h"
 #include "ops/nn_ops.h"
 #include "ops/ops.h"
 #include "reducer/reducer.h"
@@ -477,6 +478,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("out_bf16") = true, py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("residual") = py::none(), py::arg("preact") = py::none());
   m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
+  m.def("set_gemm_backend", [](const std::string& b) {
+    RINGDP_CHECK(b == "ringdp" || b == "auto", "set_gemm_backend: 'ringdp' or 'auto'");
+    blaslt::set_enabled(b == "auto");
+  }, "'auto': plain dense GEMMs on hipBLASLt; 'ringdp': every GEMM on ringdp's MFMA kernels");
+  m.def("gemm_backend", [] { return std::string(blaslt::enabled() ? "auto" : "ringdp"); });
+  m.def("set_bf16_tile_mode", &ops::set_bf16_tile_mode, "0 auto, 128 / 256: force the bf16 GEMM tile kernel");
   m.def("set_fp8_tile_mode", &ops::set_fp8_tile_mode,
         "fp8 GEMM kernel choice: 0 auto, 128 the generic 128x128 core, 256 the 256x256 DMA-pipelined kernel");
   m.def("f32_conv_fwd", &ops::f32_conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),

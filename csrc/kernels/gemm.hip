@@ -633,8 +633,32 @@ __global__ __launch_bounds__(256) void reduce_parts_l2_kernel(const float* __res
 }  // namespace
 
 // ================================================================== launchers
+// 256x256 bf16 kernel (gemm_bf16_256.hip) for K-contiguous A and B: one workgroup per CU, so it pays
+// when the tile count fills whole rounds of the 256 CUs.  RINGDP_BF16_TILE=128 / 256 forces a path.
+static int g_bf16_tile = -1;
+static int bf16_tile_mode() {
+  if (g_bf16_tile < 0) {
+    const char* v = getenv("RINGDP_BF16_TILE");
+    g_bf16_tile = v ? atoi(v) : 0;
+  }
+  return g_bf16_tile;
+}
+void set_bf16_tile_mode(int mode) { g_bf16_tile = mode; }
+static bool bf16_use_256(int M, int N, int K, int batch, int splits) {
+  const int mode = bf16_tile_mode();
+  if (mode == 128) return false;
+  if (mode == 256) return true;
+  const int64_t tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch * std::max(1, splits);
+  const int64_t rounds = (tiles + 255) / 256;
+  const double fill = rounds > 0 ? (double)tiles / (256.0 * rounds) : 0.0;
+  return tiles >= 192 && fill >= 0.75 && K / std::max(1, splits) >= 512;
+}
+
 void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K, const GemmEpilogue& ep,
                int splits, hipStream_t s) {
+  if (!A.row_contig && !B.row_contig && bf16_use_256(M, N, K, batch, splits) &&
+      gemm_bf16_256(A, B, batch, M, N, K, ep, splits, s))
+    return;
   const DenseLoader da{static_cast<const bf16*>(A.p), A.ld, A.bstride, M, K};
   const DenseLoader db{static_cast<const bf16*>(B.p), B.ld, B.bstride, N, K};
   // aligned fast path: every k-tile of every split full, row-contiguous operands in whole 8-row vectors

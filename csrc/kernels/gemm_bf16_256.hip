@@ -1,0 +1,214 @@
+// 256x256-tile bf16 GEMM for K-contiguous operands (ViT linears forward, pointwise-conv forward):
+//   C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ),  A, B bf16 with K contiguous.
+//
+// The bf16 twin of gemm_fp8_256.hip (same pipeline, same byte geometry): one 512-thread workgroup
+// per CU (8 waves as 2 (M) x 4 (N), 128x64 outputs each, 32 accumulator tiles); operand tiles of
+// 256 rows x 64 k (128 B per row = two v_mfma_f32_16x16x32_bf16 k-steps) arrive by LDS-DMA
+// (global_load_lds_dwordx4 from inline asm) into two 64 KiB stages; each wave waits for its own
+// copies with a COUNTED vmcnt and a raw s_barrier publishes the stage, so the copy of tile k+2 stays
+// in flight across the barriers of tile k+1.  16-B chunk c of stage row r sits at c ^ (r & 7) (the
+// XOR swizzle is applied to the per-lane global source address, since the DMA image is lane-linear),
+// which keeps the fragment reads conflict-free.  MFMA issue is bracketed by s_setprio(1).
+//
+// The generic 128x128 core (gemm.hip) runs these shapes at 0.62-0.87 PF/s with two register-staged
+// workgroups per CU; this kernel trades occupancy for a deeper DMA pipeline and half the operand
+// re-reads per FLOP.
+#include <algorithm>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace ringdp {
+namespace kern {
+
+using namespace ringdp::dev;
+
+namespace {
+
+constexpr int TM = 256, TN = 256, TK = 128;  // TK in bytes (= 64 bf16 values, two k-steps of 32)
+constexpr int TKE = TK / 2;                  // k elements per tile
+constexpr int STAGE = (TM + TN) * TK;        // 64 KiB: A rows then B rows, 128 B each
+constexpr int DMA_PER_WAVE = (TM + TN) * TK / 1024 / 8;  // 8 wave-instructions of 1 KiB per stage
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// 16 B per lane global -> LDS at (wave-uniform base + lane * 16); M0 is set inside the asm.
+__device__ __forceinline__ void glds16(const void* gsrc, const void* lds_wave_base) {
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)((const __attribute__((address_space(3))) char*)(lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// A/B as bytes: lda / ldb / a_bs / b_bs / K / k_per_split in BYTES (2 per bf16 element)
+__global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                              int64_t a_bs, const uint8_t* __restrict__ B,
+                                                              int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
+                                                              int N, int K, int tiles_m, int tiles_n, int splits,
+                                                              int k_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int per_z = tiles_m * tiles_n;
+  const int zid = blockIdx.y;
+  const int t = xcd_remap(blockIdx.x, per_z);
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int b = zid / splits, split = zid - b * splits;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
+  const int nkt = max(0, (kend - kbeg) / TK);
+
+  // this lane's 8 DMA sources per stage: wave instruction i = 8*wave + j covers stage rows 8*i .. 8*i+7
+  // (A rows for i < 32, then B rows); lane -> row 8*i + (lane >> 3), physical chunk lane & 7 holding
+  // logical chunk (lane & 7) ^ (row & 7)
+  const uint8_t* src[DMA_PER_WAVE];
+#pragma unroll
+  for (int j = 0; j < DMA_PER_WAVE; ++j) {
+    const int i = DMA_PER_WAVE * wave + j;
+    const int r = 8 * (i & 31) + (lane >> 3);
+    const int lc = (lane & 7) ^ (r & 7);
+    if (i < 32) {
+      const int row = min(m0 + r, M - 1);  // rows past the edge re-read the last one; dropped on store
+      src[j] = A + (int64_t)b * a_bs + (int64_t)row * lda + kbeg + lc * 16;
+    } else {
+      const int row = min(n0 + r, N - 1);
+      src[j] = B + (int64_t)b * b_bs + (int64_t)row * ldb + kbeg + lc * 16;
+    }
+  }
+  auto issue = [&](int kt, int s) {
+    char* st = smem + s * STAGE + DMA_PER_WAVE * wave * 1024;
+#pragma unroll
+    for (int j = 0; j < DMA_PER_WAVE; ++j) glds16(src[j] + (int64_t)kt * TK, st + j * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero_f32x4();
+
+  // fragment byte offsets inside a stage: row R = tile row + (lane & 15) (R & 7 == lane & 7); k-step s
+  // reads logical chunk 4s + (lane >> 4) (8 bf16 = k 32s + 8*(lane>>4) .. +7)
+  const int sw0 = ((((lane >> 4)) ^ (lane & 7)) << 4), sw1 = (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
+  const int a_off = (wm * 128 + (lane & 15)) * TK;
+  const int b_off = TM * TK + (wn * 64 + (lane & 15)) * TK;
+
+  if (nkt > 0) issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int s = kt & 1;
+    if (kt + 1 < nkt)
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt has landed; kt + 1 may be in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // every wave's copies of tile kt are in LDS
+    const char* st = smem + s * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int sw = ks ? sw1 : sw0;
+      bf16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + b_off + j * 16 * TK + sw);
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh) {
+        bf16x8 fa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + a_off + (4 * mh + i) * 16 * TK + sw);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)  // C^T tile: lane ends with 4 consecutive n of one m
+            acc[4 * mh + i][j] = mfma16x16x32(fb[j], fa[i], acc[4 * mh + i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's fragment reads of stage s retired
+    raw_barrier();                   // every wave is done reading stage s
+    if (kt + 2 < nkt) issue(kt + 2, s);  // lands while tile kt + 1 computes
+  }
+
+  // ---------------- epilogue: lane holds C[m][n..n+3], m = m0 + wm*128 + 16i + (lane&15),
+  //                  n = n0 + wn*64 + 16j + 4*(lane>>4)
+  const int mrow = m0 + wm * 128 + (lane & 15);
+  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
+  const float dscale = 1.f;
+  if (ep.mode == GemmEpilogue::kSplitK) {
+    float* out = ep.partial + (int64_t)zid * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow + 16 * i;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = ncol + 16 * j;  // N % 4 == 0 (checked by the launcher)
+        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j] * dscale;
+      }
+    }
+    return;
+  }
+  const int64_t cb = (int64_t)b * ep.c_bstride;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow + 16 * i;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = ncol + 16 * j;
+      if (n >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] * dscale * ep.alpha;
+        if (ep.bias) v[e] += ep.bias[n + e];
+      }
+      const int64_t off = cb + (int64_t)m * ep.ldc + n;
+      if (ep.preact)
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      if (ep.residual) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.residual) + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
+      }
+      if (ep.out_bf16)
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      else
+        *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+  }
+}
+
+}  // namespace
+
+bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M, int N, int K,
+                   const GemmEpilogue& ep, int splits, hipStream_t s) {
+  // K-contiguous operands with 16-B aligned rows, whole 64-element k-tiles, whole 4-column runs, no
+  // statistics epilogue
+  if (A.row_contig || Bop.row_contig || K % TKE != 0 || N % 4 != 0 || M <= 0 || N <= 0 || ep.stats ||
+      A.ld % 8 != 0 || Bop.ld % 8 != 0 || (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0) ||
+      ep.scale_a || ep.scale_b)
+    return false;
+  const int tiles_m = (M + TM - 1) / TM, tiles_n = (N + TN - 1) / TN;
+  splits = std::max(1, splits);
+  int kps = (K + splits - 1) / splits;
+  kps = (kps + TKE - 1) / TKE * TKE;
+  splits = (K + kps - 1) / kps;
+  dim3 grid(tiles_m * tiles_n, batch * splits);
+  gemm_bf16_256_kernel<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
+                                            static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, ep, M,
+                                            N, K * 2, tiles_m, tiles_n, splits, kps * 2);
+  return true;
+}
+
+}  // namespace kern
+}  // namespace ringdp

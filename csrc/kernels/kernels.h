@@ -171,6 +171,11 @@ void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int
 void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes, const GemmEpilogue& ep,
               int splits, hipStream_t s);
 // the 256x256 e4m3 kernel behind gemm_fp8 (false = shape not supported, nothing launched)
+void set_bf16_tile_mode(int mode);  // 0 auto, 128 / 256 forced (A/B measurements)
+// 256x256 bf16 kernel for K-contiguous A and B (gemm_bf16_256.hip); false when the shape/layout is not
+// supported (the caller falls back to the 128x128 core).  K in elements.
+bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K,
+                   const GemmEpilogue& ep, int splits, hipStream_t s);
 bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes,
                   const GemmEpilogue& ep, int splits, hipStream_t s);
 // split-K count gemm_fp8 should be called with for an (M x N) fp32-partial GEMM (fills whole CU rounds)

@@ -2,6 +2,7 @@
 // (csrc/kernels/gemm.hip, nn.hip).  Activations are NHWC bf16; weights stay fp32 masters in
 // PyTorch layout and are packed to bf16 per forward.
 #include "nn_ops.h"
+#include "blaslt.h"
 
 #include "../kernels/kernels.h"
 #include "util.h"
@@ -91,6 +92,31 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, 
     e.preact = preact->data_ptr();
   }
   if (M == 0 || N == 0) return c;
+  {  // plain dense GEMM: hipBLASLt when the epilogue maps onto it (blaslt.cpp)
+    blaslt::Problem p;
+    p.A = a.data_ptr();
+    p.B = b.data_ptr();
+    p.C = c.data_ptr();
+    p.M = (int)M;
+    p.N = (int)N;
+    p.K = (int)K;
+    p.batch = (int)batch;
+    p.lda = lda;
+    p.ldb = ldb;
+    p.ldc = N;
+    p.a_bstride = a_bstride;
+    p.b_bstride = b_bstride;
+    p.c_bstride = M * N;
+    p.a_row = a_row;
+    p.b_row = b_row;
+    p.out_bf16 = out_bf16;
+    p.alpha = e.alpha;
+    p.bias = e.bias;
+    p.act = e.act;
+    p.preact = e.preact;
+    p.residual = e.residual;
+    if (blaslt::matmul(p, stream_of(a))) return c;
+  }
   kern::GemmOperand A{a.data_ptr(), lda, a_bstride, a_row};
   kern::GemmOperand B{b.data_ptr(), ldb, b_bstride, b_row};
   kern::gemm_bf16(A, B, (int)batch, (int)M, (int)N, (int)K, e, 1, stream_of(a));
@@ -106,6 +132,22 @@ at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, 
   RINGDP_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: leading dims must be multiples of 8");
   RINGDP_CHECK((a_row && b_row) || K % 8 == 0, "gemm: K must be a multiple of 8 for a K-contiguous operand");
   RINGDP_CHECK((!a_row || M % 8 == 0) && (!b_row || N % 8 == 0), "gemm: row-contiguous operand needs 8-multiple");
+  {  // fp32 weight gradient straight from hipBLASLt (it splits K internally when it pays)
+    blaslt::Problem p;
+    p.A = a.data_ptr();
+    p.B = b.data_ptr();
+    p.C = out.data_ptr();
+    p.M = (int)M;
+    p.N = (int)N;
+    p.K = (int)K;
+    p.lda = lda;
+    p.ldb = ldb;
+    p.ldc = N;
+    p.a_row = a_row;
+    p.b_row = b_row;
+    p.out_bf16 = false;
+    if (blaslt::matmul(p, stream_of(a))) return out;
+  }
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 64)));
   at::Tensor part = at::empty({splits, M, N}, out.options());
   kern::GemmEpilogue e{};
@@ -594,6 +636,7 @@ at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
 }
 
 void set_fp8_tile_mode(int64_t mode) { kern::set_fp8_tile_mode((int)mode); }
+void set_bf16_tile_mode(int64_t mode) { kern::set_bf16_tile_mode((int)mode); }
 
 void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a,
                          const at::Tensor& scale_b, int64_t M, int64_t N, int64_t K, int64_t splits, at::Tensor out) {

@@ -67,6 +67,7 @@ void colsum_f32(const at::Tensor& x, at::Tensor out);
 at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
                     int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,
                     const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& preact);
+void set_bf16_tile_mode(int64_t mode);
 void set_fp8_tile_mode(int64_t mode);
 void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a,
                          const at::Tensor& scale_b, int64_t M, int64_t N, int64_t K, int64_t splits, at::Tensor out);
