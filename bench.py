@@ -306,8 +306,10 @@ def worker(args):
         comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
                 f"cap {args.bucket_mb} MB" + (", side HIP stream overlapped with backward" if on_gpu else ""))
     elif force_comm:
-        comm = (f"{lib} {args.comm_hook} (avg) over 1 rank, forced so N=1 runs the N>1 code path; "
-                f"{n_buckets} bucket(s) [{sizes_kb}] KB, cap {args.bucket_mb} MB")
+        where = ("on the compute stream (a one-rank collective has nothing to overlap)"
+                 if getattr(nat, "same_stream", lambda: False)() else "on the side stream")
+        comm = (f"{lib} {args.comm_hook} (avg) over 1 rank, forced so N=1 runs the reducer + collective "
+                f"path of N>1, {where}; {n_buckets} bucket(s) [{sizes_kb}] KB, cap {args.bucket_mb} MB")
     else:
         comm = "none (world_size 1, --no-force-comm)"
     if rank == 0:

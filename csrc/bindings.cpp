@@ -298,6 +298,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("error_message", &RcclPG::error_message)
       .def("set_timing", &RcclPG::set_timing)
       .def("p2p_max_bytes", &RcclPG::p2p_max_bytes)
+      .def("same_stream", &RcclPG::same_stream)
       .def("set_p2p_enabled", &RcclPG::set_p2p_enabled)
       .def("watch_stream",
            [](RcclPG& pg, uint64_t stream) {

@@ -97,6 +97,7 @@ class RcclPG : public ProcessGroup {
   void set_async_error_handling(bool on) { async_error_handling_ = on; }
   // One-shot P2P all-reduce for small buckets (RINGDP_P2P_ALLREDUCE_MAX_BYTES > 0 at creation).
   int64_t p2p_max_bytes() const { return p2p_ ? p2p_->max_bytes() : 0; }
+  bool same_stream() const { return same_stream_; }
   void set_p2p_enabled(bool on) { p2p_on_ = on; }
   std::chrono::milliseconds timeout() const { return timeout_; }
 
@@ -119,6 +120,7 @@ class RcclPG : public ProcessGroup {
   HipStream comm_stream_;
   hipEvent_t ready_ = nullptr;
   bool timing_ = false;
+  bool same_stream_ = false;  // issue collectives on the caller's stream (see init_common)
   bool async_error_handling_ = true;
 
   std::mutex launch_mu_;

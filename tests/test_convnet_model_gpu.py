@@ -144,11 +144,14 @@ def test_hipgraph_step_matches_eager(world1):
         torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("hook", ["allreduce", "bf16"])
-def test_forced_comm_eager_and_graph(world1, monkeypatch, hook):
+@pytest.mark.parametrize("hook,stream", [("allreduce", "side"), ("bf16", "side"), ("allreduce", "same")])
+def test_forced_comm_eager_and_graph(world1, monkeypatch, hook, stream):
     """RINGDP_DDP_FORCE_COMM=1 runs the bucket all-reduces on the one-rank RCCL group: the side
-    stream, the event fork/join and RCCL inside hipGraph capture are exercised on one GPU, and the
-    result must match the no-communication run (AVG over one rank is the identity)."""
+    stream, the event fork/join and RCCL inside hipGraph capture are exercised on one GPU (the N>1
+    configuration, forced with RINGDP_COMM_SAME_STREAM=0), as is the compute-stream issue a one-rank
+    group uses by default; the result must match the no-communication run (AVG over one rank is the
+    identity)."""
+    monkeypatch.setenv("RINGDP_COMM_SAME_STREAM", "0" if stream == "side" else "1")
     from ringdp.models import ConvNet
     from ringdp.nn import CrossEntropyLoss
     from ringdp.optim import SGD
