@@ -23,6 +23,25 @@ inline int grid_for(int64_t work, int block, int cap = 4096) {
   return static_cast<int>(g);
 }
 
+// out[c][r] = in[r][c] for a bf16 [R][C] matrix, through a 64x64 LDS tile (+2 pad: conflict-free
+// column reads); 16-bit elements, 256 threads.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const unsigned short* __restrict__ in,
+                                                             unsigned short* __restrict__ out, int64_t R,
+                                                             int64_t C) {
+  __shared__ unsigned short tile[64][66];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? in[r * C + c] : (unsigned short)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) out[c * R + r] = tile[tx][i];
+  }
+}
+
 __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t n4 = n / 4;
@@ -348,6 +367,13 @@ void sgd_multi(const SgdTensor* table, const int64_t* chunks, int64_t nchunks, i
     sgd_multi_kernel<true><<<(unsigned)nchunks, 256, 0, s>>>(table, chunks, chunk_elems, a);
   else
     sgd_multi_kernel<false><<<(unsigned)nchunks, 256, 0, s>>>(table, chunks, chunk_elems, a);
+}
+
+void transpose_bf16(const void* in, void* out, int64_t R, int64_t C, hipStream_t s) {
+  if (R <= 0 || C <= 0) return;
+  dim3 grid((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64));
+  transpose_bf16_kernel<<<grid, 256, 0, s>>>(static_cast<const unsigned short*>(in), static_cast<unsigned short*>(out),
+                                            R, C);
 }
 
 void splitk_reduce(const float* slabs, int nslices, int64_t n, float* out, hipStream_t s) {

@@ -13,6 +13,8 @@ void cast_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s);
 void cast_bf16_to_f32(const void* src, float* dst, int64_t n, hipStream_t s);
 void cast_f32_to_f16(const float* src, void* dst, int64_t n, hipStream_t s);
 void cast_f16_to_f32(const void* src, float* dst, int64_t n, hipStream_t s);
+// out[c][r] = in[r][c], bf16 [R][C] -> [C][R]
+void transpose_bf16(const void* in, void* out, int64_t R, int64_t C, hipStream_t s);
 
 struct SgdArgs {
   float lr;

@@ -101,7 +101,8 @@ bool matmul(const Problem& p, hipStream_t stream) {
   else if (p.bias) epi = HIPBLASLT_EPILOGUE_BIAS;
 
   const Key key{p.M, p.N, p.K, p.batch, p.lda, p.ldb, p.ldc, p.a_row, p.b_row, p.out_bf16, (int)epi,
-                p.residual != nullptr, dev, p.a_bstride, p.b_bstride, p.c_bstride, 0};
+                p.residual != nullptr, dev, p.a_bstride, p.b_bstride, p.c_bstride, p.fp8 ? 1 : 0};
+  const hipDataType dtIn = p.fp8 ? HIP_R_8F_E4M3 : HIP_R_16BF;
   if (g_unsupported.count(key)) return false;
 
   hipblasLtMatmulDesc_t desc = nullptr;
@@ -120,6 +121,12 @@ bool matmul(const Problem& p, hipStream_t stream) {
     LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &opA, sizeof(opA)));
     LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &opB, sizeof(opB)));
     LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_EPILOGUE, &epi, sizeof(epi)));
+    if (p.fp8) {  // hipBLASLt "A" is our B
+      if (p.scale_b)
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_A_SCALE_POINTER, &p.scale_b, sizeof(void*)));
+      if (p.scale_a)
+        LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_B_SCALE_POINTER, &p.scale_a, sizeof(void*)));
+    }
     if (p.bias) {
       const hipDataType bt = HIP_R_32F;
       LT_CHECK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &p.bias, sizeof(void*)));
@@ -138,8 +145,8 @@ bool matmul(const Problem& p, hipStream_t stream) {
                                                  sizeof(abs)));
       }
     }
-    LT_CHECK(hipblasLtMatrixLayoutCreate(&la, HIP_R_16BF, a_rows, a_cols, p.ldb));
-    LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, HIP_R_16BF, b_rows, b_cols, p.lda));
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&la, dtIn, a_rows, a_cols, p.ldb));
+    LT_CHECK(hipblasLtMatrixLayoutCreate(&lb, dtIn, b_rows, b_cols, p.lda));
     LT_CHECK(hipblasLtMatrixLayoutCreate(&lc, dtD, p.N, p.M, p.ldc));
     LT_CHECK(hipblasLtMatrixLayoutCreate(&ld, dtD, p.N, p.M, p.ldc));
     if (p.batch > 1) {

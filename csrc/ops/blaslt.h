@@ -24,6 +24,11 @@ struct Problem {
   int act = 0;                 // 0 none, 2 GELU
   void* preact = nullptr;      // bf16 pre-activation (GELU aux)
   const void* residual = nullptr;
+  // fp8 (OCP e4m3) operands, both K-contiguous, with per-tensor dequantisation scales (device fp32):
+  // C = scale_a * scale_b * (A . B^T) ...
+  bool fp8 = false;
+  const float* scale_a = nullptr;
+  const float* scale_b = nullptr;
 };
 
 bool enabled();

@@ -630,6 +630,27 @@ at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
     bf16_gpu(*preact, "gemm preact");
     e.preact = preact->data_ptr();
   }
+  {  // hipBLASLt's e4m3 kernels when the epilogue maps (blaslt.cpp)
+    blaslt::Problem p;
+    p.A = a.data_ptr();
+    p.B = b.data_ptr();
+    p.C = c.data_ptr();
+    p.M = (int)M;
+    p.N = (int)N;
+    p.K = (int)K;
+    p.lda = K;
+    p.ldb = K;
+    p.ldc = N;
+    p.out_bf16 = out_bf16;
+    p.bias = e.bias;
+    p.act = e.act;
+    p.preact = e.preact;
+    p.residual = e.residual;
+    p.fp8 = true;
+    p.scale_a = e.scale_a;
+    p.scale_b = e.scale_b;
+    if (blaslt::matmul(p, stream_of(a))) return c;
+  }
   kern::GemmOperand A{a.data_ptr(), K, 0, false}, B{b.data_ptr(), K, 0, false};
   kern::gemm_fp8(A, B, 1, (int)M, (int)N, (int)K, e, 1, stream_of(a));
   return c;
@@ -644,6 +665,8 @@ void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Ten
   gpu(b, "fp8 B");
   f32_gpu(out, "fp8 gemm out");
   RINGDP_CHECK(K % 16 == 0 && out.numel() == M * N, "gemm_fp8_splitk_f32: bad shapes");
+  // (hipBLASLt measured 1.7x slower than ringdp's split-K 256x256 kernel on these long-K weight
+  // gradients: 72 vs 41 us at 768x768x25216, tools/blaslt_fp8_check.py - they stay here)
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 128)));
   splits = kern::gemm_fp8_pick_splits((int)M, (int)N, (int)K, (int)splits);
   at::Tensor part = at::empty({splits, M, N}, out.options());

@@ -472,5 +472,14 @@ std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t
   return {x, y};
 }
 
+at::Tensor transpose_bf16(const at::Tensor& x) {
+  check_cuda(x, "transpose_bf16");
+  check_dtype(x, at::kBFloat16, "transpose_bf16");
+  RINGDP_CHECK(x.dim() == 2, "transpose_bf16: 2-d input expected");
+  at::Tensor out = at::empty({x.size(1), x.size(0)}, x.options());
+  kern::transpose_bf16(x.data_ptr(), out.data_ptr(), x.size(0), x.size(1), cur_stream(x));
+  return out;
+}
+
 }  // namespace ops
 }  // namespace ringdp

@@ -92,5 +92,6 @@ std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_
 at::Tensor f32_pool_relu_bwd(const at::Tensor& da, const at::Tensor& code, int64_t H, int64_t W, int64_t k,
                              int64_t stride);
 
+at::Tensor transpose_bf16(const at::Tensor& x);
 }  // namespace ops
 }  // namespace ringdp

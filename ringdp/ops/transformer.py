@@ -90,8 +90,14 @@ class LinearF(torch.autograd.Function):
         dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
         dx = None
         if ctx.needs_input_grad[0]:
-            # dX[m][k] = sum_n dz[m][n] W[n][k]:  A = dz (K-contiguous over n), B = W^T (row-contiguous)
-            dx = C.gemm(dz, wb, M, K, N, N, K, False, True).view(M, K)
+            # dX[m][k] = sum_n dz[m][n] W[n][k].  With W^T materialised ([K][N], one small transpose of
+            # the weight per step) both operands are K-contiguous, which is the layout the plain-GEMM
+            # library path runs fastest (tools/blaslt_check.py); with RINGDP_GEMM_BACKEND=ringdp the
+            # row-contiguous form reads W directly.
+            if C.gemm_backend() == "auto":
+                dx = C.gemm(dz, C.transpose_bf16(wb), M, K, N, N, N, False, False).view(M, K)
+            else:
+                dx = C.gemm(dz, wb, M, K, N, N, K, False, True).view(M, K)
         dw = db = None
         if ctx.needs_input_grad[1]:
             # dW[n][k] = sum_m dz[m][n] x[m][k]:  A = dz^T, B = x^T (both row-contiguous), split over m
