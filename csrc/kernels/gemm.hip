@@ -633,7 +633,7 @@ __global__ __launch_bounds__(256) void reduce_parts_l2_kernel(const float* __res
 }  // namespace
 
 // ================================================================== launchers
-// 256x256 bf16 kernel (gemm_bf16_256.hip) for K-contiguous A and B: one workgroup per CU, so it pays
+// 256x256 bf16 kernel (gemm_bf16_256.hip), K- or row-contiguous A and B: one workgroup per CU, so it pays
 // when the tile count fills whole rounds of the 256 CUs.  RINGDP_BF16_TILE=128 / 256 forces a path.
 static int g_bf16_tile = -1;
 static int bf16_tile_mode() {
@@ -654,9 +654,30 @@ static bool bf16_use_256(int M, int N, int K, int batch, int splits) {
   return tiles >= 192 && fill >= 0.75 && K / std::max(1, splits) >= 512;
 }
 
+// Split count that fills whole rounds of the 256 CUs with 256x256 tiles (>= 4 k-tiles per split), for
+// the long-K weight gradients (K = tokens); `requested` (the 128-core choice) when none fills >= 75 %.
+int gemm_bf16_pick_splits(int M, int N, int K, int requested) {
+  if (requested <= 1 || bf16_tile_mode() == 128) return std::max(1, requested);
+  const int64_t tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  const int maxs = std::max(1, std::min(32, K / 256));
+  int best = 0;
+  double best_fill = 0.0;
+  for (int sp = 1; sp <= maxs; ++sp) {
+    const int64_t t = tiles * sp;
+    if (t < 192) continue;
+    const int64_t rounds = (t + 255) / 256;
+    const double f = (double)t / (256.0 * rounds) - 0.002 * sp;  // fewer fp32 partial planes on a tie
+    if (f > best_fill) {
+      best_fill = f;
+      best = sp;
+    }
+  }
+  return best > 0 && bf16_use_256(M, N, K, 1, best) ? best : requested;
+}
+
 void gemm_bf16(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K, const GemmEpilogue& ep,
                int splits, hipStream_t s) {
-  if (!A.row_contig && !B.row_contig && bf16_use_256(M, N, K, batch, splits) &&
+  if (bf16_use_256(M, N, K, batch, splits) &&
       gemm_bf16_256(A, B, batch, M, N, K, ep, splits, s))
     return;
   const DenseLoader da{static_cast<const bf16*>(A.p), A.ld, A.bstride, M, K};

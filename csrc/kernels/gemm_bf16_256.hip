@@ -1,5 +1,5 @@
-// 256x256-tile bf16 GEMM for K-contiguous operands (ViT linears forward, pointwise-conv forward):
-//   C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ),  A, B bf16 with K contiguous.
+// 256x256-tile bf16 GEMM (ViT linears forward, pointwise-conv forward, and the long-K weight gradients):
+//   C[m][n] = epilogue( sum_k A[m][k] * B[n][k] ),  A, B bf16 with K contiguous or row-contiguous.
 //
 // The bf16 twin of gemm_fp8_256.hip (same pipeline, same byte geometry): one 512-thread workgroup
 // per CU (8 waves as 2 (M) x 4 (N), 128x64 outputs each, 32 accumulator tiles); operand tiles of
@@ -45,7 +45,26 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// A/B as bytes: lda / ldb / a_bs / b_bs / K / k_per_split in BYTES (2 per bf16 element)
+// Row-contiguous operand X (element (r, k) at k * ld + r; weight gradients sum over the token index,
+// which is the ROW of both activations): its stage part is [64 k-rows][256 cols] (512 B rows, the same
+// 32 KiB), filled by DMA instructions of two k-rows each, and read back with ds_read_b64_tr_b16, which
+// hands lane i of a 16-lane group column i of a 4-row block: two reads give the 8 consecutive k of
+// the MFMA operand.  32-B unit u of k-row r sits at u ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2:
+// a 32-lane half of a transposed read touches rows 8g+4h+{0..3} and 8(g+1)+4h+{0..3}, whose eight
+// f values are distinct, so the half covers all 64 banks once (conflict-free).
+__device__ __forceinline__ int tr_swz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
+
+// fragment of the 16-row sub-tile `unit` (0..15) for k-step ks: row-contiguous image
+__device__ __forceinline__ bf16x8 frag_tr(const char* part, int unit, int ks, int tr_off, int f) {
+  const bf16x4 lo = lds_read_tr16(reinterpret_cast<const bf16*>(part + tr_off + (32 * ks) * 512 + ((unit ^ f) << 5)));
+  const bf16x4 hi =
+      lds_read_tr16(reinterpret_cast<const bf16*>(part + tr_off + (32 * ks + 4) * 512 + ((unit ^ f) << 5)));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// A/B as bytes: lda / ldb / a_bs / b_bs / K / k_per_split in BYTES (2 per bf16 element).  AROW / BROW:
+// the operand is row-contiguous (k-major); then M (resp. N) % 8 == 0 and its ld % 8 == 0.
+template <bool AROW, bool BROW>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __restrict__ A, int64_t lda,
                                                               int64_t a_bs, const uint8_t* __restrict__ B,
                                                               int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
@@ -63,27 +82,36 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
   const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
   const int nkt = max(0, (kend - kbeg) / TK);
 
-  // this lane's 8 DMA sources per stage: wave instruction i = 8*wave + j covers stage rows 8*i .. 8*i+7
-  // (A rows for i < 32, then B rows); lane -> row 8*i + (lane >> 3), physical chunk lane & 7 holding
-  // logical chunk (lane & 7) ^ (row & 7)
+  // this lane's 8 DMA sources per stage: wave instruction i = 8*wave + j (A part for i < 32, then B).
+  // K-contiguous part: rows 8*i .. 8*i+7, lane -> row 8*i + (lane >> 3), physical chunk lane & 7 holding
+  // logical chunk (lane & 7) ^ (row & 7).  Row-contiguous part: k-rows 2*i, 2*i+1, lane -> k-row
+  // 2*i + (lane >> 5), 16-B chunk lane & 31 of the 512-B row, in unit (chunk >> 1) ^ f(k-row).
   const uint8_t* src[DMA_PER_WAVE];
 #pragma unroll
   for (int j = 0; j < DMA_PER_WAVE; ++j) {
     const int i = DMA_PER_WAVE * wave + j;
-    const int r = 8 * (i & 31) + (lane >> 3);
-    const int lc = (lane & 7) ^ (r & 7);
-    if (i < 32) {
-      const int row = min(m0 + r, M - 1);  // rows past the edge re-read the last one; dropped on store
-      src[j] = A + (int64_t)b * a_bs + (int64_t)row * lda + kbeg + lc * 16;
+    const bool a_part = i < 32;
+    const bool row = a_part ? AROW : BROW;
+    const uint8_t* base = a_part ? A + (int64_t)b * a_bs : B + (int64_t)b * b_bs;
+    const int64_t ld = a_part ? lda : ldb;
+    const int lim = a_part ? M : N, r0 = a_part ? m0 : n0;
+    if (row) {
+      const int kr = 2 * (i & 31) + (lane >> 5), c = lane & 31;
+      const int col = min(r0 + (((c >> 1) ^ tr_swz(kr)) << 4) + 8 * (c & 1), lim - 8);  // past the edge: dropped
+      src[j] = base + (int64_t)(kbeg / 2 + kr) * ld + (int64_t)col * 2;
     } else {
-      const int row = min(n0 + r, N - 1);
-      src[j] = B + (int64_t)b * b_bs + (int64_t)row * ldb + kbeg + lc * 16;
+      const int r = 8 * (i & 31) + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      const int rr = min(r0 + r, lim - 1);  // rows past the edge re-read the last one; dropped on store
+      src[j] = base + (int64_t)rr * ld + kbeg + lc * 16;
     }
   }
+  // bytes one k-tile advances this wave's sources (wave-uniform: waves 0-3 copy A, 4-7 copy B)
+  const int64_t kstep = wave < 4 ? (AROW ? 64 * lda : TK) : (BROW ? 64 * ldb : TK);
   auto issue = [&](int kt, int s) {
     char* st = smem + s * STAGE + DMA_PER_WAVE * wave * 1024;
 #pragma unroll
-    for (int j = 0; j < DMA_PER_WAVE; ++j) glds16(src[j] + (int64_t)kt * TK, st + j * 1024);
+    for (int j = 0; j < DMA_PER_WAVE; ++j) glds16(src[j] + (int64_t)kt * kstep, st + j * 1024);
   };
 
   f32x4 acc[8][4];
@@ -97,6 +125,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
   const int sw0 = ((((lane >> 4)) ^ (lane & 7)) << 4), sw1 = (((4 + (lane >> 4)) ^ (lane & 7)) << 4);
   const int a_off = (wm * 128 + (lane & 15)) * TK;
   const int b_off = TM * TK + (wn * 64 + (lane & 15)) * TK;
+  // transposed reads: lane 4q+p of group g addresses k-row 8g + q (+32 ks, +4 for the upper half),
+  // columns 4p .. 4p+3 of the sub-tile's 32-B unit; f(k-row) depends only on q and g & 1
+  const int tr_g = lane >> 4, tr_q = (lane >> 2) & 3;
+  const int tr_off = (8 * tr_g + tr_q) * 512 + 8 * (lane & 3);
+  const int tr_f = tr_q | ((tr_g & 1) << 2);
 
   if (nkt > 0) issue(0, 0);
   if (nkt > 1) issue(1, 1);
@@ -113,12 +146,16 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
       const int sw = ks ? sw1 : sw0;
       bf16x8 fb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + b_off + j * 16 * TK + sw);
+      for (int j = 0; j < 4; ++j)
+        fb[j] = BROW ? frag_tr(st + TM * TK, wn * 4 + j, ks, tr_off, tr_f)
+                     : *reinterpret_cast<const bf16x8*>(st + b_off + j * 16 * TK + sw);
 #pragma unroll
       for (int mh = 0; mh < 2; ++mh) {
         bf16x8 fa[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(st + a_off + (4 * mh + i) * 16 * TK + sw);
+        for (int i = 0; i < 4; ++i)
+          fa[i] = AROW ? frag_tr(st, wm * 8 + 4 * mh + i, ks, tr_off, tr_f)
+                       : *reinterpret_cast<const bf16x8*>(st + a_off + (4 * mh + i) * 16 * TK + sw);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -192,11 +229,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
 
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s) {
-  // K-contiguous operands with 16-B aligned rows, whole 64-element k-tiles, whole 4-column runs, no
-  // statistics epilogue
-  if (A.row_contig || Bop.row_contig || K % TKE != 0 || N % 4 != 0 || M <= 0 || N <= 0 || ep.stats ||
-      A.ld % 8 != 0 || Bop.ld % 8 != 0 || (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0) ||
-      ep.scale_a || ep.scale_b)
+  // 16-B aligned rows, whole 64-element k-tiles (k-rows of a row-contiguous operand), whole 4-column
+  // runs, whole 8-column chunks of a row-contiguous operand, no statistics epilogue
+  if (K % TKE != 0 || N % 4 != 0 || M <= 0 || N <= 0 || ep.stats || A.ld % 8 != 0 || Bop.ld % 8 != 0 ||
+      (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0) || ep.scale_a || ep.scale_b ||
+      (A.row_contig && (M % 8 != 0 || A.bstride % 8 != 0)) || (Bop.row_contig && (N % 8 != 0 || Bop.bstride % 8 != 0)))
     return false;
   const int tiles_m = (M + TM - 1) / TM, tiles_n = (N + TN - 1) / TN;
   splits = std::max(1, splits);
@@ -204,9 +241,15 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   kps = (kps + TKE - 1) / TKE * TKE;
   splits = (K + kps - 1) / kps;
   dim3 grid(tiles_m * tiles_n, batch * splits);
-  gemm_bf16_256_kernel<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
-                                            static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, ep, M,
-                                            N, K * 2, tiles_m, tiles_n, splits, kps * 2);
+  auto go = [&](auto kern) {
+    kern<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
+                              static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, ep, M, N, K * 2,
+                              tiles_m, tiles_n, splits, kps * 2);
+  };
+  if (!A.row_contig && !Bop.row_contig) go(gemm_bf16_256_kernel<false, false>);
+  else if (A.row_contig && Bop.row_contig) go(gemm_bf16_256_kernel<true, true>);
+  else if (A.row_contig) go(gemm_bf16_256_kernel<true, false>);
+  else go(gemm_bf16_256_kernel<false, true>);
   return true;
 }
 

@@ -182,6 +182,7 @@ bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, 
                   const GemmEpilogue& ep, int splits, hipStream_t s);
 // split-K count gemm_fp8 should be called with for an (M x N) fp32-partial GEMM (fills whole CU rounds)
 int gemm_fp8_pick_splits(int M, int N, int Kbytes, int requested);
+int gemm_bf16_pick_splits(int M, int N, int K, int requested);
 void set_fp8_tile_mode(int mode);  // 0 auto, 128 / 256 force a kernel (tests, A/B runs)
 // per-tensor fp8 quantisation (fp8.hip): amax -> scale = amax / 448 -> e4m3, optionally transposed
 void fp8_amax(const void* x, int64_t n, float* amax, hipStream_t s);
@@ -256,6 +257,7 @@ bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp,
                  hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);
 void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s);
+void gelu_fwd(const void* x, int64_t n, void* y, hipStream_t s);  // n % 8 == 0
 void assemble_tokens(const void* patches, const float* cls, const float* pos, int B, int NP, int D, void* out,
                      hipStream_t s);
 void assemble_tokens_bwd(const void* dout, int B, int NP, int D, void* dpatches, float* dpos, float* dcls,

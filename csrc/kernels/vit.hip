@@ -353,6 +353,20 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
+// y = gelu_erf(x); the second half of a GEMM whose fused GELU-aux epilogue hipBLASLt has no algorithm for
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16* __restrict__ x, int64_t nvec, bf16* __restrict__ y) {
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
+    const bf16x8 z = reinterpret_cast<const bf16x8*>(x)[v];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float t = (float)z[j];
+      o[j] = (bf16)(0.5f * t * (1.f + erff(t * 0.70710678118654752f)));
+    }
+    reinterpret_cast<bf16x8*>(y)[v] = o;
+  }
+}
+
 // tokens [B][1+NP][D] = concat(cls, patches [B][NP][D]) + pos [1+NP][D]
 __global__ __launch_bounds__(256) void assemble_tokens_kernel(const bf16* __restrict__ patches,
                                                               const float* __restrict__ cls,
@@ -718,6 +732,10 @@ void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, fl
   else
     softmax_bwd_kernel<<<(int)((rows + 3) / 4), 256, 0, s>>>(static_cast<const bf16*>(p), dp, rows, T, Tp, scale,
                                                            static_cast<bf16*>(ds));
+}
+
+void gelu_fwd(const void* x, int64_t n, void* y, hipStream_t s) {
+  gelu_fwd_kernel<<<grid_for(n / 8), 256, 0, s>>>(static_cast<const bf16*>(x), n / 8, static_cast<bf16*>(y));
 }
 
 void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s) {

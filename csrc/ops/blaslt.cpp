@@ -16,6 +16,7 @@
 
 #include <hipblaslt/hipblaslt.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -23,6 +24,7 @@
 #include <tuple>
 
 #include "../common.h"
+#include "../kernels/kernels.h"
 
 namespace ringdp {
 namespace blaslt {
@@ -73,7 +75,27 @@ bool enabled() {
 }
 void set_enabled(bool on) { g_on = on ? 1 : 0; }
 
+static bool matmul_once(const Problem& p, hipStream_t stream);
+
 bool matmul(const Problem& p, hipStream_t stream) {
+  if (matmul_once(p, stream)) return true;
+  // hipBLASLt has no GELU-aux algorithm for some large shapes (ViT-B/16 fc1 forward, 25216x3072x768):
+  // bias epilogue into the pre-activation, then one GELU pass (2 bytes/elem in and out). Measured
+  // faster than ringdp's fused 256x256 kernel there (tools/gpu_vit.sh).
+  if (enabled() && p.act == 2 && p.preact && p.out_bf16 && !p.residual && p.ldc == p.N &&
+      (p.batch == 1 || p.c_bstride == (int64_t)p.M * p.N) && ((int64_t)p.M * p.N * p.batch) % 8 == 0) {
+    Problem q = p;
+    q.act = 0;
+    q.preact = nullptr;
+    q.C = p.preact;
+    if (!matmul_once(q, stream)) return false;
+    kern::gelu_fwd(p.preact, (int64_t)p.M * p.N * p.batch, p.C, stream);
+    return true;
+  }
+  return false;
+}
+
+static bool matmul_once(const Problem& p, hipStream_t stream) {
   if (!enabled()) return false;
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
   if (p.residual && p.act) return false;             // ringdp adds the residual after storing preact
@@ -172,6 +194,10 @@ bool matmul(const Problem& p, hipStream_t stream) {
       if (hipblasLtMatmulAlgoGetHeuristic(st.handle, desc, la, lb, lc, ld, pref, 1, &res, &n) !=
               HIPBLAS_STATUS_SUCCESS ||
           n < 1) {
+        if (std::getenv("RINGDP_BLASLT_DEBUG"))
+          std::fprintf(stderr, "[ringdp] hipBLASLt: no algorithm for M=%d N=%d K=%d batch=%d epilogue=%d fp8=%d "
+                               "residual=%d out_bf16=%d; using ringdp's kernel\n",
+                       p.M, p.N, p.K, p.batch, (int)epi, (int)p.fp8, p.residual != nullptr, (int)p.out_bf16);
         g_unsupported[key] = true;
         cleanup();
         return false;

@@ -149,6 +149,7 @@ at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, 
     if (blaslt::matmul(p, stream_of(a))) return out;
   }
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 64)));
+  splits = kern::gemm_bf16_pick_splits((int)M, (int)N, (int)K, (int)splits);
   at::Tensor part = at::empty({splits, M, N}, out.options());
   kern::GemmEpilogue e{};
   e.mode = kern::GemmEpilogue::kSplitK;
