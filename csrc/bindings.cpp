@@ -444,10 +444,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_splitk_f32", &ops::gemm_splitk_f32);
   m.def("pack_conv_weight", &ops::pack_conv_weight);
   m.def("conv2d_fwd", &ops::conv2d_fwd);
-  m.def("conv2d_dgrad", &ops::conv2d_dgrad);
+  m.def("conv2d_dgrad", &ops::conv2d_dgrad, py::arg("dz"), py::arg("w_crsk"), py::arg("H"), py::arg("W"),
+        py::arg("stride"), py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none());
   m.def("conv2d_wgrad", &ops::conv2d_wgrad);
   m.def("nchw_to_nhwc", &ops::nchw_to_nhwc);
-  m.def("bn_fwd_train", &ops::bn_fwd_train);
+  m.def("bn_fwd_train", &ops::bn_fwd_train, py::arg("z"), py::arg("sums"), py::arg("gamma"), py::arg("beta"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("eps"), py::arg("momentum"), py::arg("residual"),
+        py::arg("relu"), py::arg("num_batches_tracked") = py::none());
   m.def("bn_fwd_eval", &ops::bn_fwd_eval);
   m.def("bn_bwd", &ops::bn_bwd);
   m.def("maxpool2d_fwd", &ops::maxpool2d_fwd);

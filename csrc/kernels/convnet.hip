@@ -31,6 +31,9 @@
 #include <type_traits>
 #include <vector>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -368,7 +371,7 @@ constexpr int C2_XRS = 48;  // bf16 per LDS row of the a1 image (32 + 16 pad): 9
 __constant__ uint8_t c2f_tile_pos[128] = {0,3,6,1,8,17,12,9,18,13,10,11,4,7,2,5,14,23,20,15,28,31,26,29,32,27,22,25,24,21,16,19,34,37,40,35,42,51,46,43,44,41,36,45,38,33,30,39,48,57,54,49,62,65,60,55,58,61,56,59,52,47,50,53,68,71,66,63,76,77,74,69,78,75,70,79,72,67,64,73,82,85,80,83,88,91,94,89,92,95,90,93,86,81,84,87,96,105,100,97,102,111,108,103,112,109,104,107,106,101,98,99,116,119,114,117,255,255,255,255,255,255,118,255,120,115,110,113};
 constexpr int C2_CRS = 72;  // bf16 per LDS row of the output staging tile (64 + 8)
 
-__global__ __launch_bounds__(256, 2) void conv2_fwd_kernel(const bf16* __restrict__ a1,
+__global__ __launch_bounds__(256, 3) void conv2_fwd_kernel(const bf16* __restrict__ a1,
                                                            const bf16* __restrict__ packed,
                                                            const float* __restrict__ bias,
                                                            bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
@@ -1379,6 +1382,14 @@ int num_cus() {
 
 inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// workgroups per CU of a persistent forward kernel; RINGDP_CN_WPC_<name> overrides (A/B runs)
+int wpc(const char* name, int dflt) {
+  char key[64];
+  std::snprintf(key, sizeof(key), "RINGDP_CN_WPC_%s", name);
+  const char* v = std::getenv(key);
+  return v ? std::max(1, std::atoi(v)) : dflt;
+}
+
 }  // namespace
 
 // ================================================================== launchers
@@ -1391,7 +1402,7 @@ void cn_pack_weights(const float* w1, const float* w2, const float* w3, const fl
 
 void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
                   int B, float mean, float inv_std, float in_scale, hipStream_t s) {
-  const int grid = clampi(B, 1, 3 * num_cus());  // 48 KiB LDS: 3 workgroups per CU
+  const int grid = clampi(B, 1, wpc("C1F", 3) * num_cus());  // 51 KiB LDS: 3 workgroups per CU
   const bf16* pk = static_cast<const bf16*>(packed);
   if (u8)
     conv1_fwd_kernel<true><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
@@ -1401,14 +1412,14 @@ void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, v
 
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,
                   hipStream_t s) {
-  const int grid = clampi(B, 1, 2 * num_cus());
+  const int grid = clampi(B, 1, wpc("C2F", 3) * num_cus());  // 49 KiB LDS, 157 VGPRs: 3 per CU (303 -> 260 us)
   conv2_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a1), static_cast<const bf16*>(packed), b2,
                                         static_cast<bf16*>(a2), idx2, B);
 }
 
 void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s) {
-  const int grid = clampi(B, 1, 2 * num_cus());
+  const int grid = clampi(B, 1, wpc("C3F", 2) * num_cus());
   conv3_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a2), static_cast<const bf16*>(packed), b3,
                                         static_cast<bf16*>(a3), idx3, B);
   fc1_fwd_kernel<<<cdiv(B, 16 * FC1_G), 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), bfc,

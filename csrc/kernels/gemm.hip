@@ -260,6 +260,49 @@ struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 2>> {
   }
 };
 
+// Implicit-GEMM conv forward with C == 8 (the ResNet stem: RGB padded to 8 channels): one 16-B vector is
+// one whole filter tap, so a 64-wide k-tile holds 8 taps; the k-range R*S*8 is padded to whole k-tiles
+// (taps >= R*S read zeros, the packed weight rows carry a zero tail, ldw % 64 == 0).  The checked ConvFwdA
+// path ran the 7x7 stem at 30 TFLOP/s (two integer divisions and bounds checks per vector, no aligned B).
+struct ConvFwdA8 {
+  static constexpr bool kRow = false;
+  static constexpr int kKind = 4;
+  const bf16* x;
+  ConvGeom g;
+  int M, Kd;
+};
+template <class L>
+struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 4>> {
+  const bf16* base[4];
+  int h0[4], w0[4];
+  __device__ __forceinline__ void init(const L& ld, int, int tile_r0, int tid) {
+    const ConvGeom& g = ld.g;
+    const int pq = g.P * g.Q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = tile_r0 + (tid >> 3) + 32 * i;
+      if (m < ld.M) {
+        const int n = m / pq, rem = m - n * pq, p = rem / g.Q, q = rem - p * g.Q;
+        base[i] = ld.x + (int64_t)n * g.H * g.W * 8;
+        h0[i] = p * g.stride - g.pad;
+        w0[i] = q * g.stride - g.pad;
+      } else {
+        base[i] = ld.x;
+        h0[i] = -(1 << 20);
+        w0[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ bf16x8 get(const L& ld, int i, int k0, int tid) const {
+    const ConvGeom& g = ld.g;
+    const int t = (k0 >> 3) + (tid & 7);  // this vector's tap
+    const int r = t / g.S, sx = t - r * g.S;
+    const int h = h0[i] + r * g.dil, w = w0[i] + sx * g.dil;
+    if (t >= g.R * g.S || (unsigned)h >= (unsigned)g.H || (unsigned)w >= (unsigned)g.W) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(base[i] + ((int64_t)h * g.W + w) * 8);
+  }
+};
+
 // Transposed-conv gather of dY (data gradient) with K % 64 == 0: tap and output-channel base per k-tile.
 struct ConvDgradA64 {
   static constexpr bool kRow = false;
@@ -480,14 +523,26 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
       const int64_t off = cb + (int64_t)m * ep.ldc + n;
       const bool full = mok && n + 3 < N;
       if (ep.preact && mok) {
+        bf16* pa = static_cast<bf16*>(ep.preact) + off;
+        if (full) {
+          *reinterpret_cast<bf16x4*>(pa) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n + e < N) static_cast<bf16*>(ep.preact)[off + e] = (bf16)v[e];
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) pa[e] = (bf16)v[e];
+        }
       }
-      if (ep.residual && mok) {
+      if (ep.residual && mok) {  // one 8-byte load per lane (4 scalar 2-byte loads cost +30 % on ResNet dgrads)
+        const bf16* ra = static_cast<const bf16*>(ep.residual) + off;
+        if (full) {
+          const bf16x4 r = *reinterpret_cast<const bf16x4*>(ra);
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (n + e < N) v[e] += (float)static_cast<const bf16*>(ep.residual)[off + e];
+          for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) v[e] += (float)ra[e];
+        }
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -617,17 +672,26 @@ __global__ __launch_bounds__(256) void reduce_parts_l1_kernel(const float* __res
   }
 }
 
+// level 2: block = 64 channels, wave w sums groups w, w+4, .., the 4 wave totals combine in a fixed order
+// (one thread per channel serialised G dependent adds over a handful of workgroups: 7-10 us per call)
 __global__ __launch_bounds__(256) void reduce_parts_l2_kernel(const float* __restrict__ mid, int G, int N,
                                                               float* __restrict__ out0, float* __restrict__ out1) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= N) return;
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float a = 0.f, q = 0.f;
-  for (int g = 0; g < G; ++g) {
-    a += mid[(int64_t)g * 2 * N + c];
-    q += mid[(int64_t)g * 2 * N + N + c];
+  if (c < N)
+    for (int g = wave; g < G; g += 4) {
+      a += mid[(int64_t)g * 2 * N + c];
+      q += mid[(int64_t)g * 2 * N + N + c];
+    }
+  red[wave][0][lane] = a;
+  red[wave][1][lane] = q;
+  __syncthreads();
+  if (wave == 0 && c < N) {
+    out0[c] = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
+    out1[c] = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
   }
-  out0[c] = a;
-  out1[c] = q;
 }
 
 }  // namespace
@@ -771,10 +835,17 @@ static bool is_pointwise(const ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0 && g.P == g.H && g.Q == g.W;
 }
 
-void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {
+void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeom& g, const GemmEpilogue& ep,
+                   hipStream_t s) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   const ConvFwdA la{static_cast<const bf16*>(x), g, M, Kd};
-  const DenseLoader db{static_cast<const bf16*>(w_krsc), Kd, 0, g.K, Kd};
+  const DenseLoader db{static_cast<const bf16*>(w_krsc), ldw, 0, g.K, Kd};
+  const int Kpad = (Kd + BK - 1) / BK * BK;
+  if (Kd % BK != 0 && g.C == 8 && ldw % BK == 0 && ldw >= Kpad) {
+    const DenseLoader dbp{static_cast<const bf16*>(w_krsc), ldw, 0, g.K, Kpad};
+    launch(ConvFwdA8{static_cast<const bf16*>(x), g, M, Kpad}, DenseAligned<false>{dbp}, ep, 1, M, g.K, Kpad, 1, s);
+    return;
+  }
   if (Kd % BK == 0) {
     if (is_pointwise(g)) {  // 1x1 / stride 1 / pad 0: the im2col IS the NHWC activation matrix
       const DenseLoader da{static_cast<const bf16*>(x), g.C, 0, M, Kd};
@@ -853,11 +924,20 @@ int reduce_parts_scratch_floats(int nparts, int N) {
   return 2 * N * G;
 }
 
+int reduce_parts_groups(int nparts) { return std::min(PR_GROUPS, std::max(1, (nparts + 31) / 32)); }
+
+int reduce_parts_l1(const float* part, int nparts, int N, float* mid, hipStream_t s) {
+  const int G = reduce_parts_groups(nparts);
+  const int per = (nparts + G - 1) / G;
+  reduce_parts_l1_kernel<<<dim3((N + 63) / 64, G), 256, 0, s>>>(part, nparts, N, per, mid);
+  return G;
+}
+
 void reduce_parts(const float* part, int nparts, int N, float* scratch, float* out0, float* out1, hipStream_t s) {
   const int G = std::min(PR_GROUPS, std::max(1, (nparts + 31) / 32));
   const int per = (nparts + G - 1) / G;
   reduce_parts_l1_kernel<<<dim3((N + 63) / 64, G), 256, 0, s>>>(part, nparts, N, per, scratch);
-  reduce_parts_l2_kernel<<<(N + 255) / 256, 256, 0, s>>>(scratch, G, N, out0, out1);
+  reduce_parts_l2_kernel<<<(N + 63) / 64, 256, 0, s>>>(scratch, G, N, out0, out1);
 }
 
 int gemm_tiles_m(int M) { return (M + BM - 1) / BM; }

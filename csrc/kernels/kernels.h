@@ -199,7 +199,9 @@ int colsum_parts(int64_t rows);
 void colsum_bf16(const void* x, int64_t rows, int64_t cols, float* part, hipStream_t s);
 // out[c] = sum_s part[s][c] for many partial rows (n % 4 == 0), fixed order
 void rowsum_f32(const float* part, int S, int64_t n, float* out, hipStream_t s);
-void conv_fwd_bf16(const void* x, const void* w_krsc, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
+// w_krsc rows are ldw elements apart (>= R*S*C; a multiple of 64 enables the C = 8 stem path)
+void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeom& g, const GemmEpilogue& ep,
+                   hipStream_t s);
 void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,
                      hipStream_t s);
@@ -208,17 +210,22 @@ void splitk_sum(const float* part, int S, int64_t n, float* out, hipStream_t s);
 // out0[c] = sum_t part[t][0][c], out1[c] = sum_t part[t][1][c]  (two-level, fixed order)
 int reduce_parts_scratch_floats(int nparts, int N);
 void reduce_parts(const float* part, int nparts, int N, float* scratch, float* out0, float* out1, hipStream_t s);
+// first level only: part [nparts][2][N] -> mid [G][2][N]; returns G
+int reduce_parts_groups(int nparts);
+int reduce_parts_l1(const float* part, int nparts, int N, float* mid, hipStream_t s);
 int gemm_tiles_m(int M);
 
 // ---------------------------------------------------------------- NHWC network layers (nn.hip)
-void pack_conv_weight(const float* w_kcrs, int K, int C, int R, int S, int Cp, void* w_krsc, void* w_crsk,
+// w_krsc rows are ldk >= R*S*Cp elements (zero tail)
+void pack_conv_weight(const float* w_kcrs, int K, int C, int R, int S, int Cp, int ldk, void* w_krsc, void* w_crsk,
                       hipStream_t s);
 void nchw_to_nhwc_pad(const void* x, bool x_bf16, int N, int C, int H, int W, int Cp, void* y, hipStream_t s);
 // batch norm (training): sums = [sum(C), sumsq(C)] over M rows -> scale/shift (+ saved mean/invstd,
 // running-stat update), then y = act(z*scale + shift [+ res])
-void bn_prepare(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+// sums: G group partials [G][2][C] (reduce_parts_l1); num_batches_tracked (nullable) is incremented
+void bn_prepare(const float* sums, int G, int64_t M, int C, const float* gamma, const float* beta, float eps,
                 float momentum, float* running_mean, float* running_var, float* scale_shift, float* save,
-                hipStream_t s);
+                int64_t* num_batches_tracked, hipStream_t s);
 void bn_act_fwd(const void* z, const float* scale_shift, const void* res, bool relu, int64_t M, int C, void* y,
                 hipStream_t s);
 // backward part 1: g = dy * (y > 0 if relu); partial sums of g and g*zhat per channel -> part

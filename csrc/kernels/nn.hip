@@ -22,21 +22,24 @@ inline int grid_for(int64_t n, int per_block = 256, int cap = 4096) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((n + per_block - 1) / per_block, cap));
 }
 
+// KRSC rows are ldk >= R*S*Cp elements long (zero tail: the stem's k-range padded to whole 64-wide
+// k-tiles, see ConvFwdA8 in gemm.hip)
 __global__ __launch_bounds__(256) void pack_conv_weight_kernel(const float* __restrict__ w, int K, int C, int R,
-                                                               int S, int Cp, bf16* __restrict__ krsc,
+                                                               int S, int Cp, int ldk, bf16* __restrict__ krsc,
                                                                bf16* __restrict__ crsk) {
-  const int64_t total = (int64_t)K * R * S * Cp;
+  const int64_t total = (int64_t)K * ldk;
+  const int kd = R * S * Cp;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    // e indexes KRSC(padded): e = ((k*R + r)*S + s)*Cp + c
-    const int c = (int)(e % Cp);
-    int64_t t = e / Cp;
-    const int s = (int)(t % S);
-    t /= S;
-    const int r = (int)(t % R);
-    const int k = (int)(t / R);
-    const float v = c < C ? w[(((int64_t)k * C + c) * R + r) * S + s] : 0.f;
+    const int k = (int)(e / ldk), j = (int)(e - (int64_t)k * ldk);
+    if (j >= kd) {
+      krsc[e] = (bf16)0.f;
+      continue;
+    }
+    // j indexes RSC(padded): j = (r*S + s)*Cp + c
+    const int c = j % Cp, rs = j / Cp, sx = rs % S, r = rs / S;
+    const float v = c < C ? w[(((int64_t)k * C + c) * R + r) * S + sx] : 0.f;
     krsc[e] = (bf16)v;
-    crsk[(((int64_t)c * R + r) * S + s) * K + k] = (bf16)v;
+    crsk[(((int64_t)c * R + r) * S + sx) * K + k] = (bf16)v;
   }
 }
 
@@ -57,15 +60,35 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restric
   }
 }
 
-__global__ void bn_prepare_kernel(const float* __restrict__ sums, int64_t M, int C, const float* __restrict__ gamma,
-                                  const float* __restrict__ beta, float eps, float momentum,
-                                  float* __restrict__ running_mean, float* __restrict__ running_var,
-                                  float* __restrict__ ss, float* __restrict__ save) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// sums = G group partials [G][2][C] of the conv epilogue's per-tile statistics (first level of
+// reduce_parts); the second level is summed here in the same fixed order (one launch fewer per BN).
+// nbt: BatchNorm.num_batches_tracked, incremented on device (one launch fewer again).
+__global__ __launch_bounds__(256) void bn_prepare_kernel(const float* __restrict__ sums, int G, int64_t M, int C,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps, float momentum,
+                                                         float* __restrict__ running_mean,
+                                                         float* __restrict__ running_var, float* __restrict__ ss,
+                                                         float* __restrict__ save, int64_t* __restrict__ nbt) {
+  // block = 64 channels; wave w sums groups w, w+4, .. and the 4 wave totals combine in a fixed order
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  float a = 0.f, q = 0.f;
+  if (c < C)
+    for (int g = wave; g < G; g += 4) {
+      a += sums[(int64_t)g * 2 * C + c];
+      q += sums[(int64_t)g * 2 * C + C + c];
+    }
+  red[wave][0][lane] = a;
+  red[wave][1][lane] = q;
+  __syncthreads();
+  if (wave != 0 || c >= C) return;
+  const float s1 = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
+  const float s2 = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
   const double inv = 1.0 / (double)M;
-  const double mean = sums[c] * inv;
-  const double var = fmax(sums[C + c] * inv - mean * mean, 0.0);  // biased (normalisation)
+  const double mean = s1 * inv;
+  const double var = fmax(s2 * inv - mean * mean, 0.0);  // biased (normalisation)
   const float invstd = (float)(1.0 / sqrt(var + eps));
   const float sc = gamma[c] * invstd;
   ss[c] = sc;
@@ -417,9 +440,10 @@ __global__ __launch_bounds__(256) void add_bf16_kernel(const bf16* __restrict__ 
 
 }  // namespace
 
-void pack_conv_weight(const float* w, int K, int C, int R, int S, int Cp, void* krsc, void* crsk, hipStream_t s) {
-  const int64_t total = (int64_t)K * R * S * Cp;
-  pack_conv_weight_kernel<<<grid_for(total), 256, 0, s>>>(w, K, C, R, S, Cp, static_cast<bf16*>(krsc),
+void pack_conv_weight(const float* w, int K, int C, int R, int S, int Cp, int ldk, void* krsc, void* crsk,
+                      hipStream_t s) {
+  const int64_t total = (int64_t)K * ldk;
+  pack_conv_weight_kernel<<<grid_for(total), 256, 0, s>>>(w, K, C, R, S, Cp, ldk, static_cast<bf16*>(krsc),
                                                           static_cast<bf16*>(crsk));
 }
 
@@ -431,11 +455,11 @@ void nchw_to_nhwc_pad(const void* x, bool x_bf16, int N, int C, int H, int W, in
     nchw_to_nhwc_kernel<false><<<grid_for(total), 256, 0, s>>>(x, N, C, H, W, Cp, static_cast<bf16*>(y));
 }
 
-void bn_prepare(const float* sums, int64_t M, int C, const float* gamma, const float* beta, float eps,
+void bn_prepare(const float* sums, int G, int64_t M, int C, const float* gamma, const float* beta, float eps,
                 float momentum, float* running_mean, float* running_var, float* scale_shift, float* save,
-                hipStream_t s) {
-  bn_prepare_kernel<<<(C + 255) / 256, 256, 0, s>>>(sums, M, C, gamma, beta, eps, momentum, running_mean,
-                                                    running_var, scale_shift, save);
+                int64_t* num_batches_tracked, hipStream_t s) {
+  bn_prepare_kernel<<<(C + 63) / 64, 256, 0, s>>>(sums, G, M, C, gamma, beta, eps, momentum, running_mean,
+                                                    running_var, scale_shift, save, num_batches_tracked);
 }
 
 void bn_act_fwd(const void* z, const float* ss, const void* res, bool relu, int64_t M, int C, void* y,

@@ -170,8 +170,14 @@ std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t
   const int64_t K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
   RINGDP_CHECK(cpad >= C && cpad % 8 == 0, "conv weight: padded channels must be >= C and a multiple of 8");
   auto opt = w.options().dtype(at::kBFloat16);
-  at::Tensor krsc = at::empty({K, R, S, cpad}, opt), crsk = at::empty({cpad, R, S, K}, opt);
-  kern::pack_conv_weight(w.data_ptr<float>(), (int)K, (int)C, (int)R, (int)S, (int)cpad, krsc.data_ptr(),
+  // C = 8 (stem) with a ragged k-range: KRSC rows padded to whole 64-wide k-tiles with zeros (a strided
+  // [K, R, S, 8] view of [K, ldk] storage) for conv_fwd's aligned C = 8 path
+  const int64_t kd = R * S * cpad;
+  const int64_t ldk = (cpad == 8 && kd % 64 != 0) ? (kd + 63) / 64 * 64 : kd;
+  at::Tensor store = at::empty({K, ldk}, opt);
+  at::Tensor krsc = store.as_strided({K, R, S, cpad}, {ldk, S * cpad, cpad, 1});
+  at::Tensor crsk = at::empty({cpad, R, S, K}, opt);
+  kern::pack_conv_weight(w.data_ptr<float>(), (int)K, (int)C, (int)R, (int)S, (int)cpad, (int)ldk, store.data_ptr(),
                          crsk.data_ptr(), stream_of(w));
   return {krsc, crsk};
 }
@@ -179,9 +185,15 @@ std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t
 std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w_krsc, int64_t stride,
                                               int64_t pad, int64_t dil, bool want_stats) {
   bf16_gpu(x, "conv input");
-  bf16_gpu(w_krsc, "conv packed weight");
+  // rows may be padded (strided view, see pack_conv_weight): no contiguity check, the strides are
+  // checked below
+  RINGDP_CHECK(w_krsc.defined() && w_krsc.is_cuda(), "conv packed weight: expected a GPU tensor");
+  dtype(w_krsc, at::kBFloat16, "conv packed weight");
   const auto g = geom(x, w_krsc.size(0), w_krsc.size(1), w_krsc.size(2), stride, pad, dil);
   RINGDP_CHECK(w_krsc.size(3) == g.C, "conv: packed weight channels ", w_krsc.size(3), " != input channels ", g.C);
+  RINGDP_CHECK(w_krsc.stride(3) == 1 && w_krsc.stride(2) == g.C && w_krsc.stride(1) == g.S * g.C &&
+                   w_krsc.stride(0) >= (int64_t)g.R * g.S * g.C,
+               "conv: packed weight must be KRSC with contiguous rows");
   at::Tensor z = at::empty({g.N, g.P, g.Q, g.K}, x.options());
   at::Tensor sums;
   const int M = g.N * g.P * g.Q;
@@ -191,20 +203,18 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Ten
     const int tiles = kern::gemm_tiles_m(M);
     part = at::empty({tiles, 2, g.K}, x.options().dtype(at::kFloat));
     e.stats = part.data_ptr<float>();
-    sums = at::empty({2, g.K}, part.options());
   }
-  kern::conv_fwd_bf16(x.data_ptr(), w_krsc.data_ptr(), g, e, stream_of(x));
-  if (want_stats) {
+  kern::conv_fwd_bf16(x.data_ptr(), w_krsc.data_ptr(), w_krsc.stride(0), g, e, stream_of(x));
+  if (want_stats) {  // first level of the fixed-order reduction; bn_fwd_train's prepare sums the G groups
     const int tiles = kern::gemm_tiles_m(M);
-    at::Tensor scratch = at::empty({kern::reduce_parts_scratch_floats(tiles, g.K)}, part.options());
-    kern::reduce_parts(part.data_ptr<float>(), tiles, g.K, scratch.data_ptr<float>(), sums.data_ptr<float>(),
-                       sums.data_ptr<float>() + g.K, stream_of(x));
+    sums = at::empty({kern::reduce_parts_groups(tiles), 2, g.K}, part.options());
+    kern::reduce_parts_l1(part.data_ptr<float>(), tiles, g.K, sums.data_ptr<float>(), stream_of(x));
   }
   return {z, sums};
 }
 
 at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t H, int64_t W, int64_t stride,
-                        int64_t pad, int64_t dil) {
+                        int64_t pad, int64_t dil, const c10::optional<at::Tensor>& residual) {
   bf16_gpu(dz, "conv output grad");
   bf16_gpu(w_crsk, "conv packed weight (CRSK)");
   const int64_t Cp = w_crsk.size(0), R = w_crsk.size(1), S = w_crsk.size(2), K = w_crsk.size(3);
@@ -212,6 +222,13 @@ at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t 
   auto g = geom(dx, K, R, S, stride, pad, dil);
   RINGDP_CHECK(g.P == dz.size(1) && g.Q == dz.size(2) && dz.size(3) == K, "conv dgrad: output grad shape mismatch");
   auto e = make_epi(dx.data_ptr(), g.C, 0, true);
+  if (residual.has_value() && residual->defined()) {
+    // the input's other gradient (a residual/shortcut branch) summed in the epilogue instead of by
+    // autograd's separate add pass
+    bf16_gpu(*residual, "conv dgrad residual");
+    RINGDP_CHECK(residual->sizes() == dx.sizes(), "conv dgrad residual: shape mismatch");
+    e.residual = residual->data_ptr();
+  }
   kern::conv_dgrad_bf16(dz.data_ptr(), w_crsk.data_ptr(), g, e, stream_of(dz));
   return dx;
 }
@@ -252,11 +269,22 @@ std::tuple<at::Tensor, at::Tensor> bn_fwd_train(const at::Tensor& z, const at::T
                                                 const at::Tensor& beta, const c10::optional<at::Tensor>& running_mean,
                                                 const c10::optional<at::Tensor>& running_var, double eps,
                                                 double momentum, const c10::optional<at::Tensor>& residual,
-                                                bool relu) {
+                                                bool relu, const c10::optional<at::Tensor>& num_batches_tracked) {
   bf16_gpu(z, "bn input");
   const int64_t C = z.size(-1), M = z.numel() / C;
   RINGDP_CHECK(C % 8 == 0, "bn: channels must be a multiple of 8");
   f32_gpu(sums, "bn sums");
+  // [2, C] totals or [G, 2, C] group partials (conv2d_fwd's statistics)
+  RINGDP_CHECK((sums.dim() == 2 && sums.size(0) == 2 && sums.size(1) == C) ||
+                   (sums.dim() == 3 && sums.size(1) == 2 && sums.size(2) == C),
+               "bn sums: expected [2, C] or [G, 2, C]");
+  const int G = sums.dim() == 3 ? (int)sums.size(0) : 1;
+  int64_t* nbt = nullptr;
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    gpu(*num_batches_tracked, "bn num_batches_tracked");
+    dtype(*num_batches_tracked, at::kLong, "bn num_batches_tracked");
+    nbt = num_batches_tracked->data_ptr<int64_t>();
+  }
   f32_gpu(gamma, "bn weight");
   f32_gpu(beta, "bn bias");
   float* rm = nullptr;
@@ -275,8 +303,8 @@ std::tuple<at::Tensor, at::Tensor> bn_fwd_train(const at::Tensor& z, const at::T
   }
   at::Tensor ss = at::empty({2, C}, gamma.options());
   at::Tensor save = at::empty({2, C}, gamma.options());
-  kern::bn_prepare(sums.data_ptr<float>(), M, (int)C, gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
-                   (float)momentum, rm, rv, ss.data_ptr<float>(), save.data_ptr<float>(), stream_of(z));
+  kern::bn_prepare(sums.data_ptr<float>(), G, M, (int)C, gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
+                   (float)momentum, rm, rv, ss.data_ptr<float>(), save.data_ptr<float>(), nbt, stream_of(z));
   at::Tensor y = at::empty_like(z);
   kern::bn_act_fwd(z.data_ptr(), ss.data_ptr<float>(), res, relu, M, (int)C, y.data_ptr(), stream_of(z));
   return {y, save};

@@ -18,14 +18,14 @@ std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t
 std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w_krsc, int64_t stride,
                                               int64_t pad, int64_t dil, bool want_stats);
 at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t H, int64_t W, int64_t stride,
-                        int64_t pad, int64_t dil);
+                        int64_t pad, int64_t dil, const c10::optional<at::Tensor>& residual);
 void conv2d_wgrad(const at::Tensor& dz, const at::Tensor& x, at::Tensor dw, int64_t stride, int64_t pad, int64_t dil);
 at::Tensor nchw_to_nhwc(const at::Tensor& x, int64_t cpad);
 std::tuple<at::Tensor, at::Tensor> bn_fwd_train(const at::Tensor& z, const at::Tensor& sums, const at::Tensor& gamma,
                                                 const at::Tensor& beta, const c10::optional<at::Tensor>& running_mean,
                                                 const c10::optional<at::Tensor>& running_var, double eps,
                                                 double momentum, const c10::optional<at::Tensor>& residual,
-                                                bool relu);
+                                                bool relu, const c10::optional<at::Tensor>& num_batches_tracked);
 at::Tensor bn_fwd_eval(const at::Tensor& z, const at::Tensor& scale_shift, const c10::optional<at::Tensor>& residual,
                        bool relu);
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& z,

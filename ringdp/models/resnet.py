@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nhwc import AvgPoolLinear, ConvBNAct, MaxPoolNHWC, to_nhwc
+from ..ops.nhwc import AvgPoolLinear, ConvBNAct, ConvBNActFork, ConvBNActPair, MaxPoolNHWC, to_nhwc
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -30,22 +30,47 @@ def conv1x1(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
     return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
 
 
-def _fused(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, residual=None):
-    training = bn.training
-    if training and bn.track_running_stats and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+def _bn_args(bn: nn.BatchNorm2d):
+    """(momentum, num_batches_tracked to increment on device or None, running_mean, running_var)."""
+    count = bn.training and bn.track_running_stats and bn.num_batches_tracked is not None
+    nbt = None
     if bn.momentum is not None:
         momentum = bn.momentum
-    elif training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        nbt = bn.num_batches_tracked if count else None  # incremented by the BN kernel (no extra launch)
+    elif count:
         # cumulative moving average (torch's exponential_average_factor for momentum=None);
-        # reads the counter on the host, as upstream does
+        # reads the incremented counter on the host, as upstream does
+        bn.num_batches_tracked.add_(1)
         momentum = 1.0 / float(bn.num_batches_tracked.item())
     else:
         momentum = 0.0
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
+    return momentum, nbt, rm, rv
+
+
+def _fused(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, residual=None):
+    momentum, nbt, rm, rv = _bn_args(bn)
     return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, conv.stride[0], conv.padding[0],
-                           relu, training, momentum, bn.eps)
+                           relu, bn.training, momentum, bn.eps, nbt)
+
+
+def _fused_fork(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool):
+    """(conv+BN(+ReLU) of x, x as the identity shortcut) - the shortcut's gradient joins the conv's data
+    gradient in its GEMM epilogue."""
+    momentum, nbt, rm, rv = _bn_args(bn)
+    return ConvBNActFork.apply(x, conv.weight, bn.weight, bn.bias, rm, rv, conv.stride[0], conv.padding[0], relu,
+                               bn.training, momentum, bn.eps, nbt)
+
+
+def _fused_pair(x, conv1: nn.Conv2d, bn1: nn.BatchNorm2d, relu1: bool, conv2: nn.Conv2d, bn2: nn.BatchNorm2d,
+                relu2: bool):
+    """Two conv+BN branches of one input (first conv + projection shortcut)."""
+    m1, n1, rm1, rv1 = _bn_args(bn1)
+    m2, n2, rm2, rv2 = _bn_args(bn2)
+    return ConvBNActPair.apply(x, conv1.weight, bn1.weight, bn1.bias, rm1, rv1, n1, conv2.weight, bn2.weight, bn2.bias,
+                               rm2, rv2, n2, (conv1.stride[0], conv1.padding[0], relu1, m1),
+                               (conv2.stride[0], conv2.padding[0], relu2, m2), bn1.training, bn1.eps, bn2.eps)
 
 
 class BasicBlock(nn.Module):
@@ -68,8 +93,10 @@ class BasicBlock(nn.Module):
         return self.relu(out + identity)
 
     def forward_nhwc(self, x):
-        identity = x if self.downsample is None else _fused(x, self.downsample[0], self.downsample[1], False)
-        out = _fused(x, self.conv1, self.bn1, True)
+        if self.downsample is None:
+            out, identity = _fused_fork(x, self.conv1, self.bn1, True)
+        else:
+            out, identity = _fused_pair(x, self.conv1, self.bn1, True, self.downsample[0], self.downsample[1], False)
         return _fused(out, self.conv2, self.bn2, True, identity)
 
 
@@ -96,8 +123,10 @@ class Bottleneck(nn.Module):
         return self.relu(out + identity)
 
     def forward_nhwc(self, x):
-        identity = x if self.downsample is None else _fused(x, self.downsample[0], self.downsample[1], False)
-        out = _fused(x, self.conv1, self.bn1, True)
+        if self.downsample is None:
+            out, identity = _fused_fork(x, self.conv1, self.bn1, True)
+        else:
+            out, identity = _fused_pair(x, self.conv1, self.bn1, True, self.downsample[0], self.downsample[1], False)
         out = _fused(out, self.conv2, self.bn2, True)
         return _fused(out, self.conv3, self.bn3, True, identity)
 

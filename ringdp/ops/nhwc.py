@@ -32,43 +32,128 @@ def to_nhwc(x: torch.Tensor) -> torch.Tensor:
     return C.nchw_to_nhwc(x.contiguous(), _cpad(x.shape[1]))
 
 
+def _cba_forward(x, w, gamma, beta, residual, running_mean, running_var, stride, pad, relu, training, momentum, eps,
+                 num_batches_tracked):
+    """conv -> BN [-> + residual] [-> ReLU] forward; returns y and what the backward needs."""
+    krsc, crsk = C.pack_conv_weight(w, x.shape[-1])
+    if training:
+        z, sums = C.conv2d_fwd(x, krsc, stride, pad, 1, True)
+        y, save = C.bn_fwd_train(z, sums, gamma, beta, running_mean, running_var, eps, momentum, residual, relu,
+                                 num_batches_tracked)
+    else:
+        z, _ = C.conv2d_fwd(x, krsc, stride, pad, 1, False)
+        scale = gamma * torch.rsqrt(running_var + eps)
+        ss = torch.stack([scale, beta - running_mean * scale]).contiguous()
+        y = C.bn_fwd_eval(z, ss, residual, relu)
+        save = ss
+    return y, (z, y, save, crsk)
+
+
+def _cba_backward(saved, x, dy, w, gamma, beta, cfg, need_dx: bool, need_dw: bool, dx_residual=None):
+    """BN backward, then the data gradient (+ dx_residual, summed in the GEMM epilogue) and the weight
+    gradient.  Returns (dx, dw, dgamma, dbeta, g) with g = d(pre-activation) (the residual's gradient)."""
+    z, y, save, crsk = saved
+    stride, pad, relu, training = cfg
+    if not training:
+        raise RuntimeError("ConvBNAct: backward through eval-mode batch norm is not supported")
+    dgamma, dbeta = grad_buffer(gamma), grad_buffer(beta)
+    dz, g = C.bn_bwd(dy.contiguous(), y, z, save, gamma, relu, dgamma, dbeta)
+    dx = None
+    if need_dx:
+        res = dx_residual.contiguous() if dx_residual is not None else None
+        dx = C.conv2d_dgrad(dz, crsk, x.shape[1], x.shape[2], stride, pad, 1, res)
+    dw = None
+    if need_dw:
+        dw = grad_buffer(w)
+        C.conv2d_wgrad(dz, x, dw, stride, pad, 1)
+    return dx, dw, dgamma, dbeta, g
+
+
 class ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, stride: int, pad: int, relu: bool,
-                training: bool, momentum: float, eps: float):
-        krsc, crsk = C.pack_conv_weight(w, x.shape[-1])
-        if training:
-            z, sums = C.conv2d_fwd(x, krsc, stride, pad, 1, True)
-            y, save = C.bn_fwd_train(z, sums, gamma, beta, running_mean, running_var, eps, momentum, residual, relu)
-        else:
-            z, _ = C.conv2d_fwd(x, krsc, stride, pad, 1, False)
-            scale = gamma * torch.rsqrt(running_var + eps)
-            ss = torch.stack([scale, beta - running_mean * scale]).contiguous()
-            y = C.bn_fwd_eval(z, ss, residual, relu)
-            save = ss
-        ctx.save_for_backward(x, z, y, save, crsk)
+                training: bool, momentum: float, eps: float, num_batches_tracked=None):
+        y, saved = _cba_forward(x, w, gamma, beta, residual, running_mean, running_var, stride, pad, relu, training,
+                                momentum, eps, num_batches_tracked)
+        ctx.save_for_backward(x, *saved)
         ctx.params = (w, gamma, beta)
-        ctx.cfg = (stride, pad, relu, residual is not None, training)
+        ctx.cfg = (stride, pad, relu, training)
+        ctx.has_res = residual is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, z, y, save, crsk = ctx.saved_tensors
+        x, *saved = ctx.saved_tensors
         w, gamma, beta = ctx.params
-        stride, pad, relu, has_res, training = ctx.cfg
-        if not training:
-            raise RuntimeError("ConvBNAct: backward through eval-mode batch norm is not supported")
-        dgamma, dbeta = grad_buffer(gamma), grad_buffer(beta)
-        dz, g = C.bn_bwd(dy.contiguous(), y, z, save, gamma, relu, dgamma, dbeta)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = C.conv2d_dgrad(dz, crsk, x.shape[1], x.shape[2], stride, pad, 1)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            dw = grad_buffer(w)
-            C.conv2d_wgrad(dz, x, dw, stride, pad, 1)
-        dres = g if (has_res and ctx.needs_input_grad[4]) else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None
+        dx, dw, dgamma, dbeta, g = _cba_backward(saved, x, dy, w, gamma, beta, ctx.cfg, ctx.needs_input_grad[0],
+                                                 ctx.needs_input_grad[1])
+        dres = g if (ctx.has_res and ctx.needs_input_grad[4]) else None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+
+
+class ConvBNActFork(torch.autograd.Function):
+    """A block's first conv+BN(+ReLU) that also hands its input on as the block's identity shortcut:
+    ``y, identity = ConvBNActFork.apply(x, ...)``.  The shortcut's gradient then arrives in this
+    Function's backward and is summed into the conv's data gradient by the GEMM epilogue, instead of
+    autograd adding the two gradients of ``x`` in a separate elementwise pass (BasicBlock/Bottleneck
+    without downsample)."""
+
+    @staticmethod
+    def forward(ctx, x, w, gamma, beta, running_mean, running_var, stride: int, pad: int, relu: bool,
+                training: bool, momentum: float, eps: float, num_batches_tracked=None):
+        y, saved = _cba_forward(x, w, gamma, beta, None, running_mean, running_var, stride, pad, relu, training,
+                                momentum, eps, num_batches_tracked)
+        ctx.save_for_backward(x, *saved)
+        ctx.params = (w, gamma, beta)
+        ctx.cfg = (stride, pad, relu, training)
+        return y, x  # x returned unmodified: autograd makes it a view whose gradient comes back here
+
+    @staticmethod
+    def backward(ctx, dy, dident):
+        x, *saved = ctx.saved_tensors
+        w, gamma, beta = ctx.params
+        if dy is None:
+            dx = dident
+            dw = dgamma = dbeta = None
+        else:
+            dx, dw, dgamma, dbeta, _ = _cba_backward(saved, x, dy, w, gamma, beta, ctx.cfg, ctx.needs_input_grad[0],
+                                                     ctx.needs_input_grad[1], dx_residual=dident)
+            if dx is None:
+                dx = dident
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+
+
+class ConvBNActPair(torch.autograd.Function):
+    """Two conv+BN(+ReLU) branches reading the same input (a downsampling block's first conv and its
+    projection shortcut).  Backward: the second branch's data-gradient GEMM adds the first's in its
+    epilogue, so the two gradients of the input are never summed by a separate pass."""
+
+    @staticmethod
+    def forward(ctx, x, w1, gamma1, beta1, rm1, rv1, nbt1, w2, gamma2, beta2, rm2, rv2, nbt2, cfg1, cfg2,
+                training: bool, eps1: float, eps2: float):
+        (s1, p1, relu1, mom1), (s2, p2, relu2, mom2) = cfg1, cfg2
+        y1, saved1 = _cba_forward(x, w1, gamma1, beta1, None, rm1, rv1, s1, p1, relu1, training, mom1, eps1, nbt1)
+        y2, saved2 = _cba_forward(x, w2, gamma2, beta2, None, rm2, rv2, s2, p2, relu2, training, mom2, eps2, nbt2)
+        ctx.save_for_backward(x, *saved1, *saved2)
+        ctx.params = (w1, gamma1, beta1, w2, gamma2, beta2)
+        ctx.cfg = ((s1, p1, relu1, training), (s2, p2, relu2, training))
+        return y1, y2
+
+    @staticmethod
+    def backward(ctx, dy1, dy2):
+        x, *saved = ctx.saved_tensors
+        saved1, saved2 = saved[:4], saved[4:]
+        w1, gamma1, beta1, w2, gamma2, beta2 = ctx.params
+        need_dx = ctx.needs_input_grad[0]
+        r1 = r2 = (None,) * 5
+        if dy1 is not None:
+            r1 = _cba_backward(saved1, x, dy1, w1, gamma1, beta1, ctx.cfg[0], need_dx, ctx.needs_input_grad[1])
+        if dy2 is not None:
+            r2 = _cba_backward(saved2, x, dy2, w2, gamma2, beta2, ctx.cfg[1], need_dx, ctx.needs_input_grad[7],
+                               dx_residual=r1[0])
+        dx = r2[0] if r2[0] is not None else r1[0]
+        return (dx, r1[1], r1[2], r1[3], None, None, None, r2[1], r2[2], r2[3], None, None, None, None, None, None,
+                None, None)
 
 
 class MaxPoolNHWC(torch.autograd.Function):

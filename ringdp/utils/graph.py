@@ -59,8 +59,13 @@ class StepGraph:
         torch.cuda.synchronize()
         drain_comms()
         self.graph = torch.cuda.CUDAGraph()
+        dump = os.environ.get("RINGDP_GRAPH_DUMP")  # DOT file of the captured nodes (diagnostics)
+        if dump:
+            self.graph.enable_debug_mode()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             out = self.step_fn()
+        if dump:
+            self.graph.debug_dump(dump)
         # keep only the value: a live autograd graph would pin AccumulateGrad nodes created on the
         # capture stream and make later eager steps on another stream synchronise against them
         self.output = out.detach() if torch.is_tensor(out) else out

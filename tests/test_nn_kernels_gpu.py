@@ -99,6 +99,7 @@ def test_conv_fwd_dgrad_wgrad(case):
     ref = F.conv2d(xr, wr, stride=stride, padding=pad)
     assert rel(z.permute(0, 3, 1, 2), ref) < 1e-2
     zf = z.float().reshape(-1, K)
+    sums = sums.reshape(-1, 2, K).sum(0)  # [G, 2, K] group partials
     torch.testing.assert_close(sums[0], zf.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(sums[1], (zf * zf).sum(0), rtol=1e-3, atol=1e-1)
     dz = torch.randn_like(ref).bfloat16()
