@@ -185,11 +185,15 @@ def worker(args):
         if on_gpu:
             torch.cuda.synchronize()
 
+    # d(loss)/d(loss) = 1, allocated once: autograd would otherwise launch a fill kernel per step for the
+    # seed gradient (~5 us of a 118 us step at the reference batch)
+    seed_grad = torch.ones((), device=dev)
+
     def step_on(x, y):
         out = ddp(x)
         loss = crit(out, y)
         opt.zero_grad(set_to_none=True)
-        loss.backward()
+        loss.backward(seed_grad)
         opt.step()
         return loss
 

@@ -344,6 +344,122 @@ struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 3>> {
   }
 };
 
+// Stride-2 data gradient by input-pixel parity class (batch index b = 2*(h&1) + (w&1)): a class's input
+// pixels receive gradient only from the taps r = r0 + 2t (r0 = (ph + pad) & 1) and likewise s, so each
+// class is a dense GEMM over its own taps - 1/4 of the gather form's MFMA work, which multiplies zeros
+// for 3 of every 4 (pixel, tap) pairs.  K % 64 == 0 (a k-tile is inside one tap); rows of a class are
+// (n, i, j) with h = 2i + ph, w = 2j + pw, written back to dX through out_row().
+struct S2Class {
+  int r0, s0, nr, ns, dh, dw, Hc, Wc;
+};
+__device__ __forceinline__ S2Class s2_class(const ConvGeom& g, int b) {
+  S2Class c;
+  const int ph = b >> 1, pw = b & 1;
+  c.r0 = (ph + g.pad) & 1;
+  c.s0 = (pw + g.pad) & 1;
+  c.nr = max(0, (g.R - c.r0 + 1) / 2);
+  c.ns = max(0, (g.S - c.s0 + 1) / 2);
+  c.dh = (ph + g.pad - c.r0) / 2;
+  c.dw = (pw + g.pad - c.s0) / 2;
+  c.Hc = (g.H - ph + 1) / 2;
+  c.Wc = (g.W - pw + 1) / 2;
+  return c;
+}
+struct ConvDgradS2A {
+  static constexpr bool kRow = false;
+  static constexpr int kKind = 5;
+  const bf16* dy;
+  ConvGeom g;
+  __device__ __forceinline__ int kext(int b) const {
+    const S2Class c = s2_class(g, b);
+    return c.nr * c.ns * g.K;
+  }
+  __device__ __forceinline__ int mext(int b) const {
+    const S2Class c = s2_class(g, b);
+    return g.N * c.Hc * c.Wc;
+  }
+  __device__ __forceinline__ int64_t out_row(int b, int m) const {  // dX row (n, h, w) of class row m
+    const S2Class c = s2_class(g, b);
+    const int hw = c.Hc * c.Wc;
+    const int n = m / hw, rem = m - n * hw, i = rem / c.Wc, j = rem - i * c.Wc;
+    return ((int64_t)n * g.H + 2 * i + (b >> 1)) * g.W + 2 * j + (b & 1);
+  }
+};
+template <class L>
+struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 5>> {
+  const bf16* base[4];
+  int pi[4], qj[4];
+  int ns;
+  __device__ __forceinline__ void init(const L& ld, int b, int tile_r0, int tid) {
+    const ConvGeom& g = ld.g;
+    const S2Class c = s2_class(g, b);
+    ns = max(1, c.ns);
+    const int hw = c.Hc * c.Wc, mc = g.N * hw;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = tile_r0 + (tid >> 3) + 32 * i;
+      if (m < mc) {
+        const int n = m / hw, rem = m - n * hw, ii = rem / c.Wc, jj = rem - ii * c.Wc;
+        base[i] = ld.dy + (int64_t)n * g.P * g.Q * g.K + 8 * (tid & 7);
+        pi[i] = ii + c.dh;
+        qj[i] = jj + c.dw;
+      } else {
+        base[i] = ld.dy;
+        pi[i] = -(1 << 20);
+        qj[i] = 0;
+      }
+    }
+  }
+  __device__ __forceinline__ bf16x8 get(const L& ld, int i, int k0, int) const {
+    const ConvGeom& g = ld.g;
+    const int t = k0 / g.K, ko = k0 - t * g.K, tr = t / ns, ts = t - tr * ns;  // uniform
+    const int p = pi[i] - tr, q = qj[i] - ts;
+    if ((unsigned)p >= (unsigned)g.P || (unsigned)q >= (unsigned)g.Q) return zero_bf16x8();
+    return *reinterpret_cast<const bf16x8*>(base[i] + ((int64_t)p * g.Q + q) * g.K + ko);
+  }
+};
+// B of the parity-class dgrad: W as CRSK, row c, class k = (tr, ts, ko) -> tap (r0 + 2 tr, s0 + 2 ts)
+struct ConvDgradS2B {
+  static constexpr bool kRow = false;
+  static constexpr int kKind = 6;
+  const bf16* w_crsk;
+  ConvGeom g;
+};
+template <class L>
+struct StagerRows<L, std::enable_if_t<loader_kind<L>::value == 6>> {
+  const bf16* ptr[4];
+  int r0, s0, ns;
+  __device__ __forceinline__ void init(const L& ld, int b, int tile_r0, int tid) {
+    const ConvGeom& g = ld.g;
+    const S2Class c = s2_class(g, b);
+    r0 = c.r0;
+    s0 = c.s0;
+    ns = max(1, c.ns);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(tile_r0 + (tid >> 3) + 32 * i, g.C - 1);  // rows past C: dropped columns
+      ptr[i] = ld.w_crsk + (int64_t)r * g.R * g.S * g.K + 8 * (tid & 7);
+    }
+  }
+  __device__ __forceinline__ bf16x8 get(const L& ld, int i, int k0, int) const {
+    const ConvGeom& g = ld.g;
+    const int t = k0 / g.K, ko = k0 - t * g.K, tr = t / ns, ts = t - tr * ns;  // uniform
+    const int tap = (r0 + 2 * tr) * g.S + s0 + 2 * ts;
+    return *reinterpret_cast<const bf16x8*>(ptr[i] + (int64_t)tap * g.K + ko);
+  }
+};
+// per-batch reduction length / row count / output row (parity-class dgrad; identity otherwise)
+template <class L>
+__device__ __forceinline__ int k_extent(const L& l, int b, int K) {
+  if constexpr (loader_kind<L>::value == 5) return min(K, l.kext(b));
+  else return K;
+}
+template <class L>
+__device__ __forceinline__ int m_extent(const L& l, int b, int M) {
+  if constexpr (loader_kind<L>::value == 5) return min(M, l.mext(b));
+  else return M;
+}
+
 template <class L>
 struct Stager {
   StagerRows<L> rs;
@@ -409,8 +525,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
   const int tm = t / tiles_n, tn = t - tm * tiles_n;
   const int b = zid / splits, split = zid - b * splits;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
-  const int nkt = (kend - kbeg + BK - 1) / BK;
+  const int Kb = k_extent(la, b, K), Mb = m_extent(la, b, M);
+  const int kbeg = split * k_per_split, kend = min(Kb, kbeg + k_per_split);
+  const int nkt = max(0, (kend - kbeg + BK - 1) / BK);
 
   Stager<LA> sa;
   Stager<LB> sb;
@@ -510,7 +627,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = mrow + 16 * i;
-    const bool mok = m < M;
+    const bool mok = m < Mb;
+    int64_t row_off;
+    if constexpr (loader_kind<LA>::value == 5)
+      row_off = mok ? la.out_row(b, m) * ep.ldc : 0;
+    else
+      row_off = cb + (int64_t)m * ep.ldc;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = ncol + 16 * j;
@@ -520,7 +642,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
         v[e] = acc[i][j][e] * ep.alpha;
         if (ep.bias && n + e < N) v[e] += ep.bias[n + e];
       }
-      const int64_t off = cb + (int64_t)m * ep.ldc + n;
+      const int64_t off = row_off + n;
       const bool full = mok && n + 3 < N;
       if (ep.preact && mok) {
         bf16* pa = static_cast<bf16*>(ep.preact) + off;
@@ -860,8 +982,22 @@ void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeo
   launch(la, Dense<false>{db}, ep, 1, M, g.K, Kd, 1, s);
 }
 
+static int g_s2_dgrad = -1;  // RINGDP_S2_DGRAD=0: gather form for stride-2 data gradients (A/B runs)
 void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
+  if (g_s2_dgrad < 0) {
+    const char* v = getenv("RINGDP_S2_DGRAD");
+    g_s2_dgrad = v ? atoi(v) : 1;
+  }
+  if (g_s2_dgrad && g.stride == 2 && g.dil == 1 && g.K % BK == 0 && !ep.stats && ep.c_bstride == 0 &&
+      ep.mode != GemmEpilogue::kSplitK) {
+    // 4 parity classes as the batch; rows / k-range of the largest class (ph = pw = 0 for even pads)
+    const int Mc = g.N * ((g.H + 1) / 2) * ((g.W + 1) / 2);
+    const int Kc = ((g.R + 1) / 2) * ((g.S + 1) / 2) * g.K;
+    launch(ConvDgradS2A{static_cast<const bf16*>(dy), g}, ConvDgradS2B{static_cast<const bf16*>(w_crsk), g}, ep, 4,
+           Mc, g.C, Kc, 1, s);
+    return;
+  }
   const ConvDgradA la{static_cast<const bf16*>(dy), g, M, Kd};
   const DenseLoader db{static_cast<const bf16*>(w_crsk), Kd, 0, g.C, Kd};
   if (Kd % BK == 0) {

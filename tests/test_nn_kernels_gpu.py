@@ -107,6 +107,10 @@ def test_conv_fwd_dgrad_wgrad(case):
     dzh = dz.permute(0, 2, 3, 1).contiguous()
     dx = C().conv2d_dgrad(dzh, crsk, H, H, stride, pad, 1)
     assert rel(dx[..., :Cin].permute(0, 3, 1, 2), xr.grad) < 1e-2
+    # a second gradient of the input (shortcut branch) summed in the dgrad epilogue
+    res = torch.randn_like(dx)
+    dxr = C().conv2d_dgrad(dzh, crsk, H, H, stride, pad, 1, res)
+    assert rel(dxr.float(), dx.float() + res.float()) < 1e-2
     dw = torch.empty_like(w)
     C().conv2d_wgrad(dzh, xh, dw, stride, pad, 1)
     assert rel(dw, wr.grad) < 5e-3
