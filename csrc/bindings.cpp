@@ -443,6 +443,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("preact") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none());
   m.def("gemm_splitk_f32", &ops::gemm_splitk_f32);
   m.def("pack_conv_weight", &ops::pack_conv_weight);
+  m.def("pack_conv_weights", &ops::pack_conv_weights);
   m.def("conv2d_fwd", &ops::conv2d_fwd);
   m.def("conv2d_dgrad", &ops::conv2d_dgrad, py::arg("dz"), py::arg("w_crsk"), py::arg("H"), py::arg("W"),
         py::arg("stride"), py::arg("pad"), py::arg("dil"), py::arg("residual") = py::none());

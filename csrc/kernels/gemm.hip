@@ -756,8 +756,17 @@ __global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict
                                                          int perm_rs) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  float a = 0.f;
-  for (int s = 0; s < S; ++s) a += part[(int64_t)s * n + i];
+  // 4 interleaved partial sums keep 4 loads in flight; combined in a fixed order (deterministic)
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 4 <= S; s += 4) {
+    a0 += part[(int64_t)(s + 0) * n + i];
+    a1 += part[(int64_t)(s + 1) * n + i];
+    a2 += part[(int64_t)(s + 2) * n + i];
+    a3 += part[(int64_t)(s + 3) * n + i];
+  }
+  for (; s < S; ++s) a0 += part[(int64_t)s * n + i];
+  const float a = (a0 + a1) + (a2 + a3);
   if (perm_rs > 0) {  // i = ko*(RS*C) + rs*C + c  ->  ko*(C*RS) + c*RS + rs
     const int64_t per = (int64_t)perm_rs * perm_c;
     const int64_t ko = i / per, rem = i - ko * per, rs = rem / perm_c, c = rem - rs * perm_c;
@@ -813,6 +822,50 @@ __global__ __launch_bounds__(256) void reduce_parts_l2_kernel(const float* __res
   if (wave == 0 && c < N) {
     out0[c] = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
     out1[c] = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
+  }
+}
+
+// Split-K conv epilogue: out[r][c] = bf16(sum_s part[s][r][c] (+ residual)), plus (mid != null) the
+// per-channel sum / sum of squares of the stored values per row group g -> mid[g][2][N] (the layout
+// bn_prepare reads).  Block = 64 channels x one row group, wave w takes rows w, w+4, ..; fixed order.
+__global__ __launch_bounds__(256) void splitk_finish_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                            bf16* __restrict__ out, int64_t ldc,
+                                                            const bf16* __restrict__ residual,
+                                                            float* __restrict__ mid, int rows_per_group) {
+  __shared__ float red[4][2][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, g = blockIdx.y;
+  const int r0 = g * rows_per_group, r1 = min(M, r0 + rows_per_group);
+  float a = 0.f, q = 0.f;
+  if (c < N)
+    for (int r = r0 + wave; r < r1; r += 4) {
+      // 4 interleaved partial sums (independent loads in flight), combined in a fixed order
+      const float* pr = part + (int64_t)r * N + c;
+      const int64_t ps = (int64_t)M * N;
+      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+      int sp = 0;
+      for (; sp + 4 <= S; sp += 4) {
+        v0 += pr[(sp + 0) * ps];
+        v1 += pr[(sp + 1) * ps];
+        v2 += pr[(sp + 2) * ps];
+        v3 += pr[(sp + 3) * ps];
+      }
+      for (; sp < S; ++sp) v0 += pr[sp * ps];
+      float v = (v0 + v1) + (v2 + v3);
+      if (residual) v += (float)residual[(int64_t)r * ldc + c];
+      const bf16 o = (bf16)v;
+      out[(int64_t)r * ldc + c] = o;
+      const float f = (float)o;
+      a += f;
+      q += f * f;
+    }
+  if (!mid) return;
+  red[wave][0][lane] = a;
+  red[wave][1][lane] = q;
+  __syncthreads();
+  if (wave == 0 && c < N) {
+    mid[(int64_t)g * 2 * N + c] = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
+    mid[(int64_t)g * 2 * N + N + c] = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
   }
 }
 
@@ -957,8 +1010,35 @@ static bool is_pointwise(const ConvGeom& g) {
   return g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0 && g.P == g.H && g.Q == g.W;
 }
 
-void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeom& g, const GemmEpilogue& ep,
+// Split count for a conv GEMM with few output tiles (ResNet-18 CIFAR layers 2-4 run 8-32 tiles of 128x128
+// on 256 CUs with 18-72 serial k-tiles each): enough splits to give ~2 workgroups per CU, >= 4 k-tiles per
+// split.  Returns the count the launcher will actually use (its rounding of the k-range per split).
+int conv_gemm_splits(int M, int N, int K) {
+  const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  const int nkt = K / BK;
+  if (tiles >= 128 || nkt < 8) return 1;
+  int S = (int)std::min<int64_t>(nkt / 4, (512 + tiles - 1) / tiles);
+  S = std::max(1, std::min(S, 32));
+  int kps = (K + S - 1) / S;
+  kps = (kps + BK - 1) / BK * BK;
+  return (K + kps - 1) / kps;
+}
+
+int splitk_finish_groups(int M) {
+  const int rpg = std::max(16, (M + 127) / 128);
+  return (M + rpg - 1) / rpg;
+}
+
+void splitk_finish(const float* part, int S, int M, int N, void* out, int64_t ldc, const void* residual, float* mid,
                    hipStream_t s) {
+  const int rpg = std::max(16, (M + 127) / 128);
+  const int G = (M + rpg - 1) / rpg;
+  splitk_finish_kernel<<<dim3((N + 63) / 64, G), 256, 0, s>>>(part, S, M, N, static_cast<bf16*>(out), ldc,
+                                                              static_cast<const bf16*>(residual), mid, rpg);
+}
+
+void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeom& g, const GemmEpilogue& ep,
+                   hipStream_t s, int splits) {
   const int M = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
   const ConvFwdA la{static_cast<const bf16*>(x), g, M, Kd};
   const DenseLoader db{static_cast<const bf16*>(w_krsc), ldw, 0, g.K, Kd};
@@ -971,9 +1051,10 @@ void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeo
   if (Kd % BK == 0) {
     if (is_pointwise(g)) {  // 1x1 / stride 1 / pad 0: the im2col IS the NHWC activation matrix
       const DenseLoader da{static_cast<const bf16*>(x), g.C, 0, M, Kd};
-      launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
+      launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, splits, s);
     } else if (g.C % BK == 0) {
-      launch(ConvFwdA64{static_cast<const bf16*>(x), g, M, Kd}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
+      launch(ConvFwdA64{static_cast<const bf16*>(x), g, M, Kd}, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, splits,
+             s);
     } else {
       launch(la, DenseAligned<false>{db}, ep, 1, M, g.K, Kd, 1, s);
     }
@@ -983,7 +1064,8 @@ void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeo
 }
 
 static int g_s2_dgrad = -1;  // RINGDP_S2_DGRAD=0: gather form for stride-2 data gradients (A/B runs)
-void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s) {
+void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s,
+                     int splits) {
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   if (g_s2_dgrad < 0) {
     const char* v = getenv("RINGDP_S2_DGRAD");
@@ -1003,9 +1085,10 @@ void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, cons
   if (Kd % BK == 0) {
     if (is_pointwise(g)) {  // dX = dY W: dY is the dense [N*H*W][K] matrix
       const DenseLoader da{static_cast<const bf16*>(dy), g.K, 0, M, Kd};
-      launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
+      launch(DenseAligned<false>{da}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, splits, s);
     } else if (g.K % BK == 0) {
-      launch(ConvDgradA64{static_cast<const bf16*>(dy), g, M, Kd}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
+      launch(ConvDgradA64{static_cast<const bf16*>(dy), g, M, Kd}, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, splits,
+             s);
     } else {
       launch(la, DenseAligned<false>{db}, ep, 1, M, g.C, Kd, 1, s);
     }

@@ -200,9 +200,17 @@ void colsum_bf16(const void* x, int64_t rows, int64_t cols, float* part, hipStre
 // out[c] = sum_s part[s][c] for many partial rows (n % 4 == 0), fixed order
 void rowsum_f32(const float* part, int S, int64_t n, float* out, hipStream_t s);
 // w_krsc rows are ldw elements apart (>= R*S*C; a multiple of 64 enables the C = 8 stem path)
+// splits > 1 (aligned C % 64 / pointwise paths only): ep must be kSplitK with a [splits][M][N] partial;
+// finish with splitk_finish
 void conv_fwd_bf16(const void* x, const void* w_krsc, int64_t ldw, const ConvGeom& g, const GemmEpilogue& ep,
+                   hipStream_t s, int splits = 1);
+void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s,
+                     int splits = 1);
+int conv_gemm_splits(int M, int N, int K);
+int splitk_finish_groups(int M);
+// out (bf16, ldc) = sum of S fp32 partials [S][M][N] (+ residual); mid (nullable) = [groups][2][N] stats
+void splitk_finish(const float* part, int S, int M, int N, void* out, int64_t ldc, const void* residual, float* mid,
                    hipStream_t s);
-void conv_dgrad_bf16(const void* dy, const void* w_crsk, const ConvGeom& g, const GemmEpilogue& ep, hipStream_t s);
 void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int splits, float* partial, float* dw_kcrs,
                      hipStream_t s);
 int conv_wgrad_splits(const ConvGeom& g, int cus);
@@ -219,6 +227,21 @@ int gemm_tiles_m(int M);
 // w_krsc rows are ldk >= R*S*Cp elements (zero tail)
 void pack_conv_weight(const float* w_kcrs, int K, int C, int R, int S, int Cp, int ldk, void* w_krsc, void* w_crsk,
                       hipStream_t s);
+struct PackEntry {
+  const float* w;
+  void* krsc;  // bf16
+  void* crsk;  // bf16
+  int64_t start;       // first KRSC element of this weight in the launch's flat index space
+  int64_t start_tile;  // first 64x64 CRSK transpose tile
+  int K, C, R, S, Cp, ldk;
+};
+constexpr int kPackMax = 48;  // 48 x 64 B + header < the 4 KiB kernel-argument limit
+struct PackTable {
+  int n;
+  int64_t total, total_tiles;
+  PackEntry e[kPackMax];
+};
+void pack_conv_weights(const PackTable& t, hipStream_t s);
 void nchw_to_nhwc_pad(const void* x, bool x_bf16, int N, int C, int H, int W, int Cp, void* y, hipStream_t s);
 // batch norm (training): sums = [sum(C), sumsq(C)] over M rows -> scale/shift (+ saved mean/invstd,
 // running-stat update), then y = act(z*scale + shift [+ res])

@@ -43,6 +43,67 @@ __global__ __launch_bounds__(256) void pack_conv_weight_kernel(const float* __re
   }
 }
 
+// Many conv weights in one launch (a ResNet packs 21-53 of them per forward): the table travels as a
+// kernel argument; each thread finds its weight by a scan of the prefix offsets (uniform per wave
+// except at boundaries).
+__device__ __forceinline__ void pack_table_to_lds(const PackTable& t, PackEntry* se) {
+  // compile-time indices: indexing the by-value argument with a run-time index would copy it to
+  // scratch memory per thread
+#pragma unroll
+  for (int i = 0; i < kPackMax; ++i)
+    if (threadIdx.x == i && i < t.n) se[i] = t.e[i];
+  __syncthreads();
+}
+
+// KRSC rows (row-padded): element j of row k = w[k][c][r][s], j = (r*S + s)*Cp + c; the source row is
+// contiguous, so its strided gather stays in L1/L2
+__global__ __launch_bounds__(256) void pack_krsc_multi_kernel(PackTable t) {
+  __shared__ PackEntry se[kPackMax];
+  pack_table_to_lds(t, se);
+  for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < t.total; f += (int64_t)gridDim.x * 256) {
+    int i = 0;
+    while (i + 1 < t.n && f >= se[i + 1].start) ++i;
+    const PackEntry d = se[i];
+    const int64_t le = f - d.start;
+    const int k = (int)(le / d.ldk), j = (int)(le - (int64_t)k * d.ldk);
+    float v = 0.f;
+    if (j < d.R * d.S * d.Cp) {
+      const int c = j % d.Cp, rs = j / d.Cp;
+      if (c < d.C) v = d.w[((int64_t)k * d.C + c) * d.R * d.S + rs];
+    }
+    static_cast<bf16*>(d.krsc)[le] = (bf16)v;
+  }
+}
+
+// CRSK = the transpose of w viewed as [K][C*R*S] (same (c, r, s) order), plus zero rows for the padded
+// channels: 64x64 tiles through LDS, both sides coalesced.  blockIdx.x = a tile of some entry
+// (start_tile prefix over the entries).
+__global__ __launch_bounds__(256) void pack_crsk_multi_kernel(PackTable t) {
+  __shared__ PackEntry se[kPackMax];
+  __shared__ float tile[64][65];
+  pack_table_to_lds(t, se);
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < t.n && b >= se[i + 1].start_tile) ++i;
+  const PackEntry d = se[i];
+  const int crs_real = d.C * d.R * d.S, crs_all = d.Cp * d.R * d.S;
+  const int tiles_k = (d.K + 63) / 64;
+  const int tb = b - (int)d.start_tile;
+  const int crs0 = (tb / tiles_k) * 64, k0 = (tb % tiles_k) * 64;
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int kk = idx >> 6, cc = idx & 63;
+    const int k = k0 + kk, crs = crs0 + cc;
+    tile[kk][cc] = (k < d.K && crs < crs_real) ? d.w[(int64_t)k * crs_real + crs] : 0.f;
+  }
+  __syncthreads();
+  bf16* out = static_cast<bf16*>(d.crsk);
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int cc = idx >> 6, kk = idx & 63;
+    const int k = k0 + kk, crs = crs0 + cc;
+    if (k < d.K && crs < crs_all) out[(int64_t)crs * d.K + k] = (bf16)tile[kk][cc];
+  }
+}
+
 template <bool BF>
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restrict__ x, int N, int C, int H, int W,
                                                            int Cp, bf16* __restrict__ y) {
@@ -445,6 +506,12 @@ void pack_conv_weight(const float* w, int K, int C, int R, int S, int Cp, int ld
   const int64_t total = (int64_t)K * ldk;
   pack_conv_weight_kernel<<<grid_for(total), 256, 0, s>>>(w, K, C, R, S, Cp, ldk, static_cast<bf16*>(krsc),
                                                           static_cast<bf16*>(crsk));
+}
+
+void pack_conv_weights(const PackTable& t, hipStream_t s) {
+  if (t.total <= 0) return;
+  pack_krsc_multi_kernel<<<grid_for(t.total), 256, 0, s>>>(t);
+  pack_crsk_multi_kernel<<<(int)t.total_tiles, 256, 0, s>>>(t);
 }
 
 void nchw_to_nhwc_pad(const void* x, bool x_bf16, int N, int C, int H, int W, int Cp, void* y, hipStream_t s) {

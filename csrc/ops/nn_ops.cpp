@@ -164,6 +164,48 @@ at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, 
   return out;
 }
 
+std::vector<at::Tensor> pack_conv_weights(const std::vector<at::Tensor>& ws, const std::vector<int64_t>& cpads) {
+  RINGDP_CHECK(ws.size() == cpads.size(), "pack_conv_weights: one channel padding per weight");
+  std::vector<at::Tensor> out;
+  kern::PackTable t{};
+  auto flush = [&](hipStream_t st) {
+    kern::pack_conv_weights(t, st);
+    t = kern::PackTable{};
+  };
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const at::Tensor& w = ws[i];
+    const int64_t cpad = cpads[i];
+    f32_gpu(w, "conv weight");
+    RINGDP_CHECK(w.dim() == 4, "conv weight: expected [K, C, R, S]");
+    const int64_t K = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+    RINGDP_CHECK(cpad >= C && cpad % 8 == 0, "conv weight: padded channels must be >= C and a multiple of 8");
+    auto opt = w.options().dtype(at::kBFloat16);
+    const int64_t kd = R * S * cpad;
+    const int64_t ldk = (cpad == 8 && kd % 64 != 0) ? (kd + 63) / 64 * 64 : kd;  // as pack_conv_weight
+    at::Tensor store = at::empty({K, ldk}, opt);
+    at::Tensor crsk = at::empty({cpad, R, S, K}, opt);
+    out.push_back(store.as_strided({K, R, S, cpad}, {ldk, S * cpad, cpad, 1}));
+    out.push_back(crsk);
+    if (t.n == kern::kPackMax) flush(stream_of(w));
+    kern::PackEntry& e = t.e[t.n++];
+    e.w = w.data_ptr<float>();
+    e.krsc = store.data_ptr();
+    e.crsk = crsk.data_ptr();
+    e.start = t.total;
+    e.start_tile = t.total_tiles;
+    e.K = (int)K;
+    e.C = (int)C;
+    e.R = (int)R;
+    e.S = (int)S;
+    e.Cp = (int)cpad;
+    e.ldk = (int)ldk;
+    t.total += K * ldk;
+    t.total_tiles += ((cpad * R * S + 63) / 64) * ((K + 63) / 64);
+  }
+  if (t.n > 0) flush(stream_of(ws[0]));
+  return out;
+}
+
 std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t cpad) {
   f32_gpu(w, "conv weight");
   RINGDP_CHECK(w.dim() == 4, "conv weight: expected [K, C, R, S]");
@@ -197,7 +239,25 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Ten
   at::Tensor z = at::empty({g.N, g.P, g.Q, g.K}, x.options());
   at::Tensor sums;
   const int M = g.N * g.P * g.Q;
+  const int Kd = g.R * g.S * g.C;
   auto e = make_epi(z.data_ptr(), g.K, 0, true);
+  // few output tiles (small spatial maps): split the k-range, then one pass sums the partials, stores z
+  // and produces the statistics groups (aligned loaders only)
+  const bool pointwise = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+  const int splits = (Kd % 64 == 0 && (pointwise || g.C % 64 == 0)) ? kern::conv_gemm_splits(M, g.K, Kd) : 1;
+  if (splits > 1) {
+    at::Tensor part = at::empty({splits, M, g.K}, x.options().dtype(at::kFloat));
+    e.mode = kern::GemmEpilogue::kSplitK;
+    e.partial = part.data_ptr<float>();
+    kern::conv_fwd_bf16(x.data_ptr(), w_krsc.data_ptr(), w_krsc.stride(0), g, e, stream_of(x), splits);
+    float* mid = nullptr;
+    if (want_stats) {
+      sums = at::empty({kern::splitk_finish_groups(M), 2, g.K}, part.options());
+      mid = sums.data_ptr<float>();
+    }
+    kern::splitk_finish(part.data_ptr<float>(), splits, M, g.K, z.data_ptr(), g.K, nullptr, mid, stream_of(x));
+    return {z, sums};
+  }
   at::Tensor part;
   if (want_stats) {
     const int tiles = kern::gemm_tiles_m(M);
@@ -222,13 +282,28 @@ at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t 
   auto g = geom(dx, K, R, S, stride, pad, dil);
   RINGDP_CHECK(g.P == dz.size(1) && g.Q == dz.size(2) && dz.size(3) == K, "conv dgrad: output grad shape mismatch");
   auto e = make_epi(dx.data_ptr(), g.C, 0, true);
+  const void* res = nullptr;
   if (residual.has_value() && residual->defined()) {
     // the input's other gradient (a residual/shortcut branch) summed in the epilogue instead of by
     // autograd's separate add pass
     bf16_gpu(*residual, "conv dgrad residual");
     RINGDP_CHECK(residual->sizes() == dx.sizes(), "conv dgrad residual: shape mismatch");
-    e.residual = residual->data_ptr();
+    res = residual->data_ptr();
   }
+  const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
+  const bool pointwise = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
+  // stride 2 takes the parity-class path; few output tiles otherwise: split the k-range
+  const int splits = (g.stride != 2 && Kd % 64 == 0 && (pointwise || g.K % 64 == 0))
+                         ? kern::conv_gemm_splits(M, g.C, Kd) : 1;
+  if (splits > 1) {
+    at::Tensor part = at::empty({splits, M, g.C}, dz.options().dtype(at::kFloat));
+    e.mode = kern::GemmEpilogue::kSplitK;
+    e.partial = part.data_ptr<float>();
+    kern::conv_dgrad_bf16(dz.data_ptr(), w_crsk.data_ptr(), g, e, stream_of(dz), splits);
+    kern::splitk_finish(part.data_ptr<float>(), splits, M, g.C, dx.data_ptr(), g.C, res, nullptr, stream_of(dz));
+    return dx;
+  }
+  e.residual = res;
   kern::conv_dgrad_bf16(dz.data_ptr(), w_crsk.data_ptr(), g, e, stream_of(dz));
   return dx;
 }

@@ -15,6 +15,8 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, 
 at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, int64_t K, int64_t lda,
                            int64_t ldb, bool a_row, bool b_row, int64_t splits, const at::Tensor& out);
 std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t cpad);
+// several weights in one launch: returns [krsc0, crsk0, krsc1, crsk1, ...]
+std::vector<at::Tensor> pack_conv_weights(const std::vector<at::Tensor>& ws, const std::vector<int64_t>& cpads);
 std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w_krsc, int64_t stride,
                                               int64_t pad, int64_t dil, bool want_stats);
 at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t H, int64_t W, int64_t stride,

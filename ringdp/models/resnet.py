@@ -19,7 +19,12 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nhwc import AvgPoolLinear, ConvBNAct, ConvBNActFork, ConvBNActPair, MaxPoolNHWC, to_nhwc
+from ..ops.nhwc import (AvgPoolLinear, ConvBNAct, ConvBNActFork, ConvBNActPair, MaxPoolNHWC, pack_conv_weights,
+                        to_nhwc)
+
+# {id(conv): (krsc, crsk)} of the forward in progress (ResNet.forward_nhwc packs every conv weight in one
+# launch); empty outside it, so blocks called on their own pack per conv
+_PACKED: dict = {}
 
 
 def conv3x3(cin: int, cout: int, stride: int = 1) -> nn.Conv2d:
@@ -52,7 +57,7 @@ def _bn_args(bn: nn.BatchNorm2d):
 def _fused(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool, residual=None):
     momentum, nbt, rm, rv = _bn_args(bn)
     return ConvBNAct.apply(x, conv.weight, bn.weight, bn.bias, residual, rm, rv, conv.stride[0], conv.padding[0],
-                           relu, bn.training, momentum, bn.eps, nbt)
+                           relu, bn.training, momentum, bn.eps, nbt, _PACKED.get(id(conv)))
 
 
 def _fused_fork(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool):
@@ -60,7 +65,7 @@ def _fused_fork(x, conv: nn.Conv2d, bn: nn.BatchNorm2d, relu: bool):
     gradient in its GEMM epilogue."""
     momentum, nbt, rm, rv = _bn_args(bn)
     return ConvBNActFork.apply(x, conv.weight, bn.weight, bn.bias, rm, rv, conv.stride[0], conv.padding[0], relu,
-                               bn.training, momentum, bn.eps, nbt)
+                               bn.training, momentum, bn.eps, nbt, _PACKED.get(id(conv)))
 
 
 def _fused_pair(x, conv1: nn.Conv2d, bn1: nn.BatchNorm2d, relu1: bool, conv2: nn.Conv2d, bn2: nn.BatchNorm2d,
@@ -70,7 +75,8 @@ def _fused_pair(x, conv1: nn.Conv2d, bn1: nn.BatchNorm2d, relu1: bool, conv2: nn
     m2, n2, rm2, rv2 = _bn_args(bn2)
     return ConvBNActPair.apply(x, conv1.weight, bn1.weight, bn1.bias, rm1, rv1, n1, conv2.weight, bn2.weight, bn2.bias,
                                rm2, rv2, n2, (conv1.stride[0], conv1.padding[0], relu1, m1),
-                               (conv2.stride[0], conv2.padding[0], relu2, m2), bn1.training, bn1.eps, bn2.eps)
+                               (conv2.stride[0], conv2.padding[0], relu2, m2), bn1.training, bn1.eps, bn2.eps,
+                               _PACKED.get(id(conv1)), _PACKED.get(id(conv2)))
 
 
 class BasicBlock(nn.Module):
@@ -184,11 +190,15 @@ class ResNet(nn.Module):
     def forward_nhwc(self, x: torch.Tensor) -> torch.Tensor:
         """``x``: NCHW images (fp32/bf16), converted to NHWC bf16 + channel-padded on device."""
         h = to_nhwc(x)
-        h = _fused(h, self.conv1, self.bn1, True)
-        h = MaxPoolNHWC.apply(h, 3, 2, 1)
-        for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
-            for blk in layer:
-                h = blk.forward_nhwc(h)
+        _PACKED.update(pack_conv_weights(m for m in self.modules() if isinstance(m, nn.Conv2d)))
+        try:
+            h = _fused(h, self.conv1, self.bn1, True)
+            h = MaxPoolNHWC.apply(h, 3, 2, 1)
+            for layer in (self.layer1, self.layer2, self.layer3, self.layer4):
+                for blk in layer:
+                    h = blk.forward_nhwc(h)
+        finally:
+            _PACKED.clear()
         return AvgPoolLinear.apply(h, self.fc.weight, self.fc.bias)
 
 

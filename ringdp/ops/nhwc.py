@@ -27,15 +27,23 @@ def _cpad(c: int) -> int:
     return (c + 7) // 8 * 8
 
 
+def pack_conv_weights(convs) -> dict:
+    """bf16 KRSC/CRSK copies of many conv weights in one launch -> {id(conv): (krsc, crsk)}."""
+    convs = list(convs)
+    flat = C.pack_conv_weights([c.weight for c in convs], [_cpad(c.in_channels) for c in convs])
+    return {id(c): (flat[2 * i], flat[2 * i + 1]) for i, c in enumerate(convs)}
+
+
 def to_nhwc(x: torch.Tensor) -> torch.Tensor:
     """NCHW fp32/bf16 images -> NHWC bf16 with channels padded to a multiple of 8 (no gradient)."""
     return C.nchw_to_nhwc(x.contiguous(), _cpad(x.shape[1]))
 
 
 def _cba_forward(x, w, gamma, beta, residual, running_mean, running_var, stride, pad, relu, training, momentum, eps,
-                 num_batches_tracked):
-    """conv -> BN [-> + residual] [-> ReLU] forward; returns y and what the backward needs."""
-    krsc, crsk = C.pack_conv_weight(w, x.shape[-1])
+                 num_batches_tracked, packed=None):
+    """conv -> BN [-> + residual] [-> ReLU] forward; returns y and what the backward needs.  ``packed``:
+    (KRSC, CRSK) bf16 weights from a model-wide ``pack_conv_weights`` launch, else packed here."""
+    krsc, crsk = packed if packed is not None else C.pack_conv_weight(w, x.shape[-1])
     if training:
         z, sums = C.conv2d_fwd(x, krsc, stride, pad, 1, True)
         y, save = C.bn_fwd_train(z, sums, gamma, beta, running_mean, running_var, eps, momentum, residual, relu,
@@ -72,9 +80,9 @@ def _cba_backward(saved, x, dy, w, gamma, beta, cfg, need_dx: bool, need_dw: boo
 class ConvBNAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, residual, running_mean, running_var, stride: int, pad: int, relu: bool,
-                training: bool, momentum: float, eps: float, num_batches_tracked=None):
+                training: bool, momentum: float, eps: float, num_batches_tracked=None, packed=None):
         y, saved = _cba_forward(x, w, gamma, beta, residual, running_mean, running_var, stride, pad, relu, training,
-                                momentum, eps, num_batches_tracked)
+                                momentum, eps, num_batches_tracked, packed)
         ctx.save_for_backward(x, *saved)
         ctx.params = (w, gamma, beta)
         ctx.cfg = (stride, pad, relu, training)
@@ -88,7 +96,7 @@ class ConvBNAct(torch.autograd.Function):
         dx, dw, dgamma, dbeta, g = _cba_backward(saved, x, dy, w, gamma, beta, ctx.cfg, ctx.needs_input_grad[0],
                                                  ctx.needs_input_grad[1])
         dres = g if (ctx.has_res and ctx.needs_input_grad[4]) else None
-        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 
 
 class ConvBNActFork(torch.autograd.Function):
@@ -100,9 +108,9 @@ class ConvBNActFork(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, running_mean, running_var, stride: int, pad: int, relu: bool,
-                training: bool, momentum: float, eps: float, num_batches_tracked=None):
+                training: bool, momentum: float, eps: float, num_batches_tracked=None, packed=None):
         y, saved = _cba_forward(x, w, gamma, beta, None, running_mean, running_var, stride, pad, relu, training,
-                                momentum, eps, num_batches_tracked)
+                                momentum, eps, num_batches_tracked, packed)
         ctx.save_for_backward(x, *saved)
         ctx.params = (w, gamma, beta)
         ctx.cfg = (stride, pad, relu, training)
@@ -120,7 +128,7 @@ class ConvBNActFork(torch.autograd.Function):
                                                      ctx.needs_input_grad[1], dx_residual=dident)
             if dx is None:
                 dx = dident
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
 
 
 class ConvBNActPair(torch.autograd.Function):
@@ -130,10 +138,12 @@ class ConvBNActPair(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, gamma1, beta1, rm1, rv1, nbt1, w2, gamma2, beta2, rm2, rv2, nbt2, cfg1, cfg2,
-                training: bool, eps1: float, eps2: float):
+                training: bool, eps1: float, eps2: float, packed1=None, packed2=None):
         (s1, p1, relu1, mom1), (s2, p2, relu2, mom2) = cfg1, cfg2
-        y1, saved1 = _cba_forward(x, w1, gamma1, beta1, None, rm1, rv1, s1, p1, relu1, training, mom1, eps1, nbt1)
-        y2, saved2 = _cba_forward(x, w2, gamma2, beta2, None, rm2, rv2, s2, p2, relu2, training, mom2, eps2, nbt2)
+        y1, saved1 = _cba_forward(x, w1, gamma1, beta1, None, rm1, rv1, s1, p1, relu1, training, mom1, eps1, nbt1,
+                                  packed1)
+        y2, saved2 = _cba_forward(x, w2, gamma2, beta2, None, rm2, rv2, s2, p2, relu2, training, mom2, eps2, nbt2,
+                                  packed2)
         ctx.save_for_backward(x, *saved1, *saved2)
         ctx.params = (w1, gamma1, beta1, w2, gamma2, beta2)
         ctx.cfg = ((s1, p1, relu1, training), (s2, p2, relu2, training))
@@ -153,7 +163,7 @@ class ConvBNActPair(torch.autograd.Function):
                                dx_residual=r1[0])
         dx = r2[0] if r2[0] is not None else r1[0]
         return (dx, r1[1], r1[2], r1[3], None, None, None, r2[1], r2[2], r2[3], None, None, None, None, None, None,
-                None, None)
+                None, None, None, None)
 
 
 class MaxPoolNHWC(torch.autograd.Function):

@@ -477,3 +477,16 @@ def test_fused_attention_forward(T):
     assert (ds[:, :, T:] == 0).all() and (ds[:, T:, :] == 0).all()
     assert rel(ds.float(), dsr) < 1e-2
     assert rel(ds.float(), ds2.float()) < 1e-2
+
+
+def test_pack_conv_weights_multi_matches_single():
+    """One-launch packing of many conv weights == the per-weight pack (KRSC with padded rows, CRSK)."""
+    torch.manual_seed(3)
+    shapes = [(64, 3, 7, 7, 8), (64, 64, 3, 3, 64), (256, 64, 1, 1, 64), (512, 256, 3, 3, 256), (10, 5, 3, 3, 8)]
+    ws = [torch.randn(k, c, r, s, device="cuda") for k, c, r, s, _ in shapes]
+    flat = C().pack_conv_weights(ws, [cp for *_, cp in shapes])
+    for i, w in enumerate(ws):
+        krsc, crsk = C().pack_conv_weight(w, shapes[i][4])
+        assert torch.equal(flat[2 * i], krsc)
+        assert flat[2 * i].stride() == krsc.stride()
+        assert torch.equal(flat[2 * i + 1], crsk)
