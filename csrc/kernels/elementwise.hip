@@ -54,6 +54,24 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ src, bf16* __rest
     dst[i] = (bf16)src[i];
 }
 
+// Many fp32 -> bf16 casts in one launch (a model's weights per forward): the table is a kernel
+// argument copied to LDS with compile-time indices (run-time indexing of the argument goes to scratch);
+// 4-element vectors, every tensor's length a multiple of 4 (checked on the host).
+__global__ __launch_bounds__(256) void cast_multi_kernel(CastTable t) {
+  __shared__ CastEntry se[kCastMax];
+#pragma unroll
+  for (int i = 0; i < kCastMax; ++i)
+    if (threadIdx.x == i && i < t.n) se[i] = t.e[i];
+  __syncthreads();
+  int i = 0;  // v only grows, so the table scan resumes where the previous vector's ended
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < t.total4; v += (int64_t)gridDim.x * 256) {
+    while (i + 1 < t.n && v >= se[i + 1].start4) ++i;
+    const int64_t l = v - se[i].start4;
+    const float4 x = reinterpret_cast<const float4*>(se[i].src)[l];
+    reinterpret_cast<bf16x4*>(se[i].dst)[l] = bf16x4{(bf16)x.x, (bf16)x.y, (bf16)x.z, (bf16)x.w};
+  }
+}
+
 __global__ void cast_bf16_f32_kernel(const bf16* __restrict__ src, float* __restrict__ dst, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t n4 = n / 4;
@@ -337,6 +355,9 @@ __global__ void synth_u8_kernel(uint8_t* __restrict__ x, int64_t* __restrict__ l
 void cast_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   cast_f32_bf16_kernel<<<grid_for(n / 4 + 1, 256), 256, 0, s>>>(src, static_cast<bf16*>(dst), n);
+}
+void cast_f32_to_bf16_multi(const CastTable& t, hipStream_t s) {
+  if (t.total4 > 0) cast_multi_kernel<<<grid_for(t.total4, 256), 256, 0, s>>>(t);
 }
 void cast_bf16_to_f32(const void* src, float* dst, int64_t n, hipStream_t s) {
   if (n <= 0) return;

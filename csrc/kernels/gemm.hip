@@ -52,6 +52,9 @@ __device__ __forceinline__ int rsw(int kr, int col) {  // col: element column (m
 }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {  // d/dx of x * Phi(x) (erf form)
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
 
 // ------------------------------------------------------------------ loaders
 struct DenseLoader {  // element (b, r, k): K-contig p[b*bs + r*ld + k]; row-contig p[b*bs + k*ld + r]
@@ -644,7 +647,20 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
       }
       const int64_t off = row_off + n;
       const bool full = mok && n + 3 < N;
-      if (ep.preact && mok) {
+      if (ep.act == 3 && mok) {  // GELU backward: the incoming gradient times GELU'(pre-activation)
+        const bf16* pa = static_cast<const bf16*>(ep.preact) + off;
+        float z[4];
+        if (full) {
+          const bf16x4 r = *reinterpret_cast<const bf16x4*>(pa);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) z[e] = (float)r[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) z[e] = n + e < N ? (float)pa[e] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(z[e]);
+      } else if (ep.preact && mok) {
         bf16* pa = static_cast<bf16*>(ep.preact) + off;
         if (full) {
           *reinterpret_cast<bf16x4*>(pa) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};

@@ -205,7 +205,14 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
         if (ep.bias) v[e] += ep.bias[n + e];
       }
       const int64_t off = cb + (int64_t)m * ep.ldc + n;
-      if (ep.preact)
+      if (ep.act == 3) {  // GELU backward: times GELU'(pre-activation), preact read
+        const bf16x4 z = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.preact) + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = (float)z[e];
+          v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+        }
+      } else if (ep.preact)
         *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       if (ep.residual) {
         const bf16x4 r = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.residual) + off);

@@ -152,8 +152,9 @@ struct GemmEpilogue {
   bool out_bf16;
   float alpha;
   const float* bias;  // [N] or null
-  int act;            // 0 none, 1 relu, 2 gelu (erf)
-  void* preact;       // bf16 copy of the value before residual/activation (same layout as C) or null
+  int act;            // 0 none, 1 relu, 2 gelu (erf), 3 gelu backward: C *= GELU'(preact) (preact is an input)
+  void* preact;       // bf16 copy of the value before residual/activation (same layout as C) or null;
+                      // with act 3 it is read: the forward's pre-activation
   const void* residual;  // bf16, same layout as C, added before the activation
   float* stats;       // [b][tiles_m][2][N] per-channel sum / sumsq partials of the stored C, or null
   float* partial;     // split-K fp32 partials [b*splits][M][N]
@@ -227,6 +228,18 @@ int gemm_tiles_m(int M);
 // w_krsc rows are ldk >= R*S*Cp elements (zero tail)
 void pack_conv_weight(const float* w_kcrs, int K, int C, int R, int S, int Cp, int ldk, void* w_krsc, void* w_crsk,
                       hipStream_t s);
+struct CastEntry {
+  const float* src;
+  void* dst;       // bf16
+  int64_t start4;  // first 4-element vector of this tensor in the launch's index space
+};
+constexpr int kCastMax = 96;  // 96 x 24 B + header < the 4 KiB kernel-argument limit
+struct CastTable {
+  int n;
+  int64_t total4;
+  CastEntry e[kCastMax];
+};
+void cast_f32_to_bf16_multi(const CastTable& t, hipStream_t s);
 struct PackEntry {
   const float* w;
   void* krsc;  // bf16

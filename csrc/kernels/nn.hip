@@ -60,8 +60,8 @@ __device__ __forceinline__ void pack_table_to_lds(const PackTable& t, PackEntry*
 __global__ __launch_bounds__(256) void pack_krsc_multi_kernel(PackTable t) {
   __shared__ PackEntry se[kPackMax];
   pack_table_to_lds(t, se);
+  int i = 0;  // f only grows: the table scan resumes where it stopped
   for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < t.total; f += (int64_t)gridDim.x * 256) {
-    int i = 0;
     while (i + 1 < t.n && f >= se[i + 1].start) ++i;
     const PackEntry d = se[i];
     const int64_t le = f - d.start;

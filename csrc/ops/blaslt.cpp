@@ -92,6 +92,17 @@ bool matmul(const Problem& p, hipStream_t stream) {
     kern::gelu_fwd(p.preact, (int64_t)p.M * p.N * p.batch, p.C, stream);
     return true;
   }
+  // likewise no DGELU algorithm (same ViT shape): plain GEMM, then C *= GELU'(preact) in place - ringdp's
+  // own fused epilogue runs this short-K shape 1.7x slower than the pair
+  if (enabled() && p.act == 3 && p.preact && p.out_bf16 && !p.residual && !p.bias && p.ldc == p.N &&
+      (p.batch == 1 || p.c_bstride == (int64_t)p.M * p.N) && ((int64_t)p.M * p.N * p.batch) % 8 == 0) {
+    Problem q = p;
+    q.act = 0;
+    q.preact = nullptr;
+    if (!matmul_once(q, stream)) return false;
+    kern::gelu_bwd(p.C, p.preact, (int64_t)p.M * p.N * p.batch, p.C, stream);
+    return true;
+  }
   return false;
 }
 
@@ -100,7 +111,8 @@ static bool matmul_once(const Problem& p, hipStream_t stream) {
   if (p.M <= 0 || p.N <= 0 || p.K <= 0) return false;
   if (p.residual && p.act) return false;             // ringdp adds the residual after storing preact
   if (p.residual && !p.out_bf16) return false;       // C and D share a type
-  if (p.preact && p.act != 2) return false;
+  if (p.preact && p.act != 2 && p.act != 3) return false;
+  if (p.act == 3 && (!p.preact || p.bias || p.residual || !p.out_bf16)) return false;
   if (p.act == 1) return false;                      // ReLU layers are ringdp-fused (BN) anyway
   // Measured (tools/blaslt_check.py, ViT-B/16 shapes): the library wins on K-contiguous operands
   // (forward linears: 35-118 us vs 52-201 us with the bias epilogue) and loses on row-contiguous ones
@@ -120,6 +132,7 @@ static bool matmul_once(const Problem& p, hipStream_t stream) {
   hipblasLtEpilogue_t epi = HIPBLASLT_EPILOGUE_DEFAULT;
   if (p.act == 2) epi = p.preact ? (p.bias ? HIPBLASLT_EPILOGUE_GELU_AUX_BIAS : HIPBLASLT_EPILOGUE_GELU_AUX)
                                  : (p.bias ? HIPBLASLT_EPILOGUE_GELU_BIAS : HIPBLASLT_EPILOGUE_GELU);
+  else if (p.act == 3) epi = HIPBLASLT_EPILOGUE_DGELU;  // aux = the forward's pre-activation (input)
   else if (p.bias) epi = HIPBLASLT_EPILOGUE_BIAS;
 
   const Key key{p.M, p.N, p.K, p.batch, p.lda, p.ldb, p.ldc, p.a_row, p.b_row, p.out_bf16, (int)epi,

@@ -91,6 +91,8 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, 
     RINGDP_CHECK(preact->numel() >= batch * M * N, "gemm preact too small");
     e.preact = preact->data_ptr();
   }
+  // act 3: the GELU backward, C = (A B^T) * GELU'(preact) with preact an INPUT (the forward's pre-activation)
+  RINGDP_CHECK(act != 3 || (e.preact && !e.residual && !e.bias), "gemm act 3 (GELU backward) needs preact only");
   if (M == 0 || N == 0) return c;
   {  // plain dense GEMM: hipBLASLt when the epilogue maps onto it (blaslt.cpp)
     blaslt::Problem p;

@@ -85,6 +85,29 @@ kern::SgdArgs make_args(const SgdHyper& h, bool first, const c10::optional<at::T
 }  // namespace
 
 // ------------------------------------------------------------------ casts
+std::vector<at::Tensor> cast_bf16_multi(const std::vector<at::Tensor>& srcs) {
+  std::vector<at::Tensor> out;
+  kern::CastTable t{};
+  for (const at::Tensor& x : srcs) {
+    check_cuda(x, "cast_bf16_multi src");
+    RINGDP_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous(), "cast_bf16_multi: contiguous fp32 tensors");
+    RINGDP_CHECK(x.numel() % 4 == 0, "cast_bf16_multi: sizes must be multiples of 4");
+    at::Tensor y = at::empty(x.sizes(), x.options().dtype(at::kBFloat16));
+    out.push_back(y);
+    if (t.n == kern::kCastMax) {
+      kern::cast_f32_to_bf16_multi(t, cur_stream(x));
+      t = kern::CastTable{};
+    }
+    kern::CastEntry& e = t.e[t.n++];
+    e.src = x.data_ptr<float>();
+    e.dst = y.data_ptr();
+    e.start4 = t.total4;
+    t.total4 += x.numel() / 4;
+  }
+  if (t.n > 0) kern::cast_f32_to_bf16_multi(t, cur_stream(srcs[0]));
+  return out;
+}
+
 void cast_copy(at::Tensor dst, const at::Tensor& src) {
   RINGDP_CHECK(dst.numel() == src.numel(), "cast_copy: numel mismatch");
   if (!dst.is_cuda()) {

@@ -12,6 +12,8 @@ namespace ops {
 
 // dst = src converted (fp32 <-> bf16 / fp16).  GPU: ringdp cast kernel; CPU: ATen copy.
 void cast_copy(at::Tensor dst, const at::Tensor& src);
+// fp32 -> bf16 copies of many tensors in one launch
+std::vector<at::Tensor> cast_bf16_multi(const std::vector<at::Tensor>& srcs);
 
 struct SgdHyper {
   double lr = 0.01;

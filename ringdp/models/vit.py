@@ -18,7 +18,8 @@ from collections import OrderedDict
 import torch
 import torch.nn as nn
 
-from ..ops.transformer import AttentionF, ClassRowsF, LayerNormF, PatchTokensF, linear
+from ..ops.transformer import (AttentionF, ClassRowsF, LayerNormF, LayerNormFork, MLPF, PatchTokensF, cast_weights,
+                                clear_weights, fp8_enabled, linear)
 
 
 class MLPBlock(nn.Sequential):
@@ -49,13 +50,23 @@ class EncoderBlock(nn.Module):
 
     def forward_rows(self, x, B: int, T: int):  # ringdp path, x [B*T, D] bf16
         att = self.self_attention
-        h = LayerNormF.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+        if fp8_enabled():  # fp8 linears (LinearF's quantised path), autograd sums the residual gradients
+            h = LayerNormF.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+            qkv = _lin(h, att.in_proj_weight, att.in_proj_bias)
+            o = AttentionF.apply(qkv, B, T, self.num_heads)
+            x = linear(o, att.out_proj, residual=x)
+            h = LayerNormF.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
+            h = linear(h, self.mlp[0], act=2)
+            return linear(h, self.mlp[3], residual=x)
+        # bf16: the residual streams' gradients join in the LayerNorm backward kernels (LayerNormFork)
+        # and the GELU backward runs in fc2's data-gradient epilogue (MLPF)
+        h, x = LayerNormFork.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
         qkv = _lin(h, att.in_proj_weight, att.in_proj_bias)
         o = AttentionF.apply(qkv, B, T, self.num_heads)
         x = linear(o, att.out_proj, residual=x)
-        h = LayerNormF.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
-        h = linear(h, self.mlp[0], act=2)
-        return linear(h, self.mlp[3], residual=x)
+        h, x = LayerNormFork.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
+        fc1, fc2 = self.mlp[0], self.mlp[3]
+        return MLPF.apply(h, fc1.weight, fc1.bias, fc2.weight, fc2.bias, x)
 
 
 def _lin(x, w, b):
@@ -110,10 +121,19 @@ class VisionTransformer(nn.Module):
 
     def forward_rows(self, x: torch.Tensor) -> torch.Tensor:
         B, T = x.shape[0], self.seq_length
-        h = PatchTokensF.apply(x, self.conv_proj.weight, self.conv_proj.bias, self.class_token,
-                               self.encoder.pos_embedding, self.patch_size)
+        # every linear weight's bf16 copy in one launch (instead of one cast per linear)
+        ws = []
         for blk in self.encoder.layers:
-            h = blk.forward_rows(h, B, T)
+            att = blk.self_attention
+            ws += [att.in_proj_weight, att.out_proj.weight, blk.mlp[0].weight, blk.mlp[3].weight]
+        cast_weights(ws)
+        try:
+            h = PatchTokensF.apply(x, self.conv_proj.weight, self.conv_proj.bias, self.class_token,
+                                   self.encoder.pos_embedding, self.patch_size)
+            for blk in self.encoder.layers:
+                h = blk.forward_rows(h, B, T)
+        finally:
+            clear_weights()
         ln = self.encoder.ln
         h = LayerNormF.apply(h, ln.weight, ln.bias, ln.eps)
         cls = ClassRowsF.apply(h, B, T)

@@ -490,3 +490,30 @@ def test_pack_conv_weights_multi_matches_single():
         assert torch.equal(flat[2 * i], krsc)
         assert flat[2 * i].stride() == krsc.stride()
         assert torch.equal(flat[2 * i + 1], crsk)
+
+
+@pytest.mark.parametrize("backend", ["auto", "ringdp"])
+def test_gemm_gelu_backward_epilogue(backend):
+    """act 3: C = (A B^T) * GELU'(preact), preact read (hipBLASLt DGELU or ringdp's epilogue)."""
+    torch.manual_seed(4)
+    M, N, K = 320, 256, 192
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, K, device="cuda").bfloat16()
+    pre = torch.randn(M, N, device="cuda").bfloat16()
+    C().set_gemm_backend(backend)
+    try:
+        out = C().gemm(a, b, M, N, K, K, K, False, False, 1, 0, 0, True, None, 3, None, pre).view(M, N)
+    finally:
+        C().set_gemm_backend("auto")
+    x = pre.float()
+    gp = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+    ref = (a.float() @ b.float().t()) * gp
+    assert rel(out.float(), ref) < 1e-2
+
+
+def test_cast_bf16_multi():
+    torch.manual_seed(5)
+    xs = [torch.randn(n, device="cuda") for n in (4, 768 * 2304, 12, 3072 * 768, 400)] * 30  # > one launch table
+    ys = C().cast_bf16_multi(xs)
+    for x, y in zip(xs, ys):
+        assert y.dtype == torch.bfloat16 and torch.equal(y, x.bfloat16())
