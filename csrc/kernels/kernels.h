@@ -298,6 +298,10 @@ bool attn_fwd(const void* q, const void* k, const void* v, int BH, int T, int Tp
 // fused dP = dO V^T + softmax backward: dS = scale * P * (dP - rowsum(dP * P)) (bf16 [BH][Tp][Tp])
 bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp, int Dh, float scale, void* ds,
                  hipStream_t s);
+// fused attention backward (head dim 64, Tp <= 256): dQ, dK, dV straight into the dqkv rows [B*T][3*H*Dh];
+// dsum = [B*H][Tp] fp32 scratch
+bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* p, int B, int T, int H,
+              int Tp, int Dh, float scale, float* dsum, void* dqkv, hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);
 void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s);
 void gelu_fwd(const void* x, int64_t n, void* y, hipStream_t s);  // n % 8 == 0

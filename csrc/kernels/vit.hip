@@ -674,6 +674,183 @@ __global__ __launch_bounds__(256) void attn_bwd_ds_kernel(const bf16* __restrict
   }
 }
 
+// Fused attention backward, query side: dS (as attn_bwd_ds, in registers) and dQ = dS K in the same
+// pass - dQ^T = K^T dS^T with the dS registers as the MFMA B operand and K^T read from LDS with
+// ds_read_b64_tr_b16 (the forward's O^T = V^T P^T trick).  dQ rows go straight into the dqkv gradient
+// rows [B*T][3*H*Dh]; D = rowsum(dP * P) per query is stored for the key-side kernel.
+template <int NT>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ k,
+                                                          const bf16* __restrict__ v, const bf16* __restrict__ p,
+                                                          float scale, int T, int H, float* __restrict__ dsum,
+                                                          bf16* __restrict__ dqkv) {
+  constexpr int Tp = 16 * NT;
+  __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
+  __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t bh = blockIdx.x;
+  const int b = (int)(bh / H), h = (int)(bh % H);
+  const bf16* vb = v + bh * Tp * ATT_D;
+  const bf16* kb = k + bh * Tp * ATT_D;
+  for (int c = tid; c < Tp * 8; c += 256) {
+    const int r = c >> 3, d = (c & 7) * 8;
+    *reinterpret_cast<bf16x8*>(Vs + att_ksw(r, d)) = reinterpret_cast<const bf16x8*>(vb)[c];
+    *reinterpret_cast<bf16x8*>(Ks + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(kb)[c];
+  }
+  __syncthreads();
+  const int g = lane >> 4, qi = lane & 15;
+  const int q4 = qi >> 2, p4 = qi & 3;
+  const int64_t row3 = (int64_t)3 * H * ATT_D;
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int qrow = qt * 16 + qi;
+    const bf16* dp_ = dout + (bh * Tp + qrow) * ATT_D + 8 * g;
+    const bf16x8 of0 = *reinterpret_cast<const bf16x8*>(dp_);
+    const bf16x8 of1 = *reinterpret_cast<const bf16x8*>(dp_ + 32);
+    const bf16* prow = p + (bh * Tp + qrow) * Tp + 4 * g;
+    bf16x4 pv[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) pv[t] = *reinterpret_cast<const bf16x4*>(prow + 16 * t);
+    f32x4 dpt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int vr = 16 * t + qi;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Vs + att_ksw(vr, 8 * g));
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Vs + att_ksw(vr, 32 + 8 * g));
+      dpt[t] = mfma16x16x32(a1, of1, mfma16x16x32(a0, of0, zero_f32x4()));
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dot = fmaf(dpt[t][i], (float)pv[t][i], dot);
+    dot += __shfl_xor(dot, 16, 64);
+    dot += __shfl_xor(dot, 32, 64);
+    if (g == 0) dsum[bh * Tp + qrow] = dot;
+    bf16x4 dsb[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dsb[t][i] = (bf16)(scale * (float)pv[t][i] * (dpt[t][i] - dot));
+    // dQ^T[d][q] = sum over key pairs (t0, t1) of K^T (keys 16t + 4g + j) x dS^T
+    f32x4 qt4[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) qt4[dt] = zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < (NT + 1) / 2; ++ks) {
+      const int t0 = 2 * ks, t1 = 2 * ks + 1 < NT ? 2 * ks + 1 : t0;
+      const bf16x4 d1 = 2 * ks + 1 < NT ? dsb[2 * ks + 1] : bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      const bf16x8 bfr = bf16x8{dsb[t0][0], dsb[t0][1], dsb[t0][2], dsb[t0][3], d1[0], d1[1], d1[2], d1[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x4 lo = lds_read_tr16(Ks + att_vsw(16 * t0 + 4 * g + q4, 16 * dt + 4 * p4));
+        const bf16x4 hi = lds_read_tr16(Ks + att_vsw(16 * t1 + 4 * g + q4, 16 * dt + 4 * p4));
+        const bf16x8 afr = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        qt4[dt] = mfma16x16x32(afr, bfr, qt4[dt]);
+      }
+    }
+    if (qrow < T) {
+      bf16* drow = dqkv + ((int64_t)b * T + qrow) * row3 + h * ATT_D + 4 * g;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<bf16x4*>(drow + 16 * dt) =
+            bf16x4{(bf16)qt4[dt][0], (bf16)qt4[dt][1], (bf16)qt4[dt][2], (bf16)qt4[dt][3]};
+    }
+  }
+}
+
+// Fused attention backward, key side: each wave owns key tiles kt = wave, wave + 4, .. and walks all query
+// tiles in pairs, recomputing dP = dO V^T for its keys (rows = queries: lane (g, key) holds queries
+// 16qt + 4g + r), reading P and the stored D, forming dS = scale P (dP - D), and accumulating
+//   dV^T[d][key] += dO^T P     and     dK^T[d][key] += Q^T dS
+// with those registers as the MFMA B operand (reduction over the query pair, permuted like the forward's
+// key pairs) and dO^T / Q^T read from LDS with ds_read_b64_tr_b16.  dK, dV rows go straight into dqkv.
+template <int NT>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ q,
+                                                            const bf16* __restrict__ v, const bf16* __restrict__ p,
+                                                            const float* __restrict__ dsum, float scale, int T, int H,
+                                                            bf16* __restrict__ dqkv) {
+  constexpr int Tp = 16 * NT;
+  __shared__ __attribute__((aligned(16))) bf16 Qs[Tp * ATT_D];
+  __shared__ __attribute__((aligned(16))) bf16 Os[Tp * ATT_D];  // dO
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t bh = blockIdx.x;
+  const int b = (int)(bh / H), h = (int)(bh % H);
+  const bf16* qb = q + bh * Tp * ATT_D;
+  const bf16* ob = dout + bh * Tp * ATT_D;
+  for (int c = tid; c < Tp * 8; c += 256) {
+    const int r = c >> 3, d = (c & 7) * 8;
+    *reinterpret_cast<bf16x8*>(Qs + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(qb)[c];
+    *reinterpret_cast<bf16x8*>(Os + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(ob)[c];
+  }
+  __syncthreads();
+  const int g = lane >> 4, ki = lane & 15;
+  const int q4 = ki >> 2, p4 = ki & 3;
+  const int64_t row3 = (int64_t)3 * H * ATT_D;
+  const float* db = dsum + bh * Tp;
+  for (int kt = wave; kt < NT; kt += 4) {
+    const int key = kt * 16 + ki;
+    const bf16* vr = v + (bh * Tp + key) * ATT_D + 8 * g;
+    const bf16x8 vf0 = *reinterpret_cast<const bf16x8*>(vr);
+    const bf16x8 vf1 = *reinterpret_cast<const bf16x8*>(vr + 32);
+    const bf16* pcol = p + bh * Tp * Tp + key;
+    f32x4 dva[4], dka[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dva[dt] = dka[dt] = zero_f32x4();
+    for (int ks = 0; ks < (NT + 1) / 2; ++ks) {
+      const int qp[2] = {2 * ks, 2 * ks + 1 < NT ? 2 * ks + 1 : 2 * ks};
+      const bool has1 = 2 * ks + 1 < NT;
+      bf16x4 pb[2], sb[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // dP[q][key] for queries 16 qp + 4g + r: A = dO rows (from the LDS image), B = V rows (registers)
+        const int orow = 16 * qp[u] + ki;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Os + att_vsw(orow, 8 * g));
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Os + att_vsw(orow, 32 + 8 * g));
+        const f32x4 dp = mfma16x16x32(a1, vf1, mfma16x16x32(a0, vf0, zero_f32x4()));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qq = 16 * qp[u] + 4 * g + r;
+          const float pr = (u == 0 || has1) ? (float)pcol[(int64_t)qq * Tp] : 0.f;
+          pb[u][r] = (bf16)pr;
+          sb[u][r] = (bf16)(scale * pr * (dp[r] - db[qq]));
+        }
+      }
+      const bf16x8 pfr = bf16x8{pb[0][0], pb[0][1], pb[0][2], pb[0][3], pb[1][0], pb[1][1], pb[1][2], pb[1][3]};
+      const bf16x8 sfr = bf16x8{sb[0][0], sb[0][1], sb[0][2], sb[0][3], sb[1][0], sb[1][1], sb[1][2], sb[1][3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x4 olo = lds_read_tr16(Os + att_vsw(16 * qp[0] + 4 * g + q4, 16 * dt + 4 * p4));
+        const bf16x4 ohi = lds_read_tr16(Os + att_vsw(16 * qp[1] + 4 * g + q4, 16 * dt + 4 * p4));
+        dva[dt] = mfma16x16x32(bf16x8{olo[0], olo[1], olo[2], olo[3], ohi[0], ohi[1], ohi[2], ohi[3]}, pfr, dva[dt]);
+        const bf16x4 qlo = lds_read_tr16(Qs + att_vsw(16 * qp[0] + 4 * g + q4, 16 * dt + 4 * p4));
+        const bf16x4 qhi = lds_read_tr16(Qs + att_vsw(16 * qp[1] + 4 * g + q4, 16 * dt + 4 * p4));
+        dka[dt] = mfma16x16x32(bf16x8{qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]}, sfr, dka[dt]);
+      }
+    }
+    if (key < T) {
+      bf16* krow = dqkv + ((int64_t)b * T + key) * row3 + H * ATT_D + h * ATT_D + 4 * g;
+      bf16* vrow = krow + H * ATT_D;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        *reinterpret_cast<bf16x4*>(krow + 16 * dt) =
+            bf16x4{(bf16)dka[dt][0], (bf16)dka[dt][1], (bf16)dka[dt][2], (bf16)dka[dt][3]};
+        *reinterpret_cast<bf16x4*>(vrow + 16 * dt) =
+            bf16x4{(bf16)dva[dt][0], (bf16)dva[dt][1], (bf16)dva[dt][2], (bf16)dva[dt][3]};
+      }
+    }
+  }
+}
+
+template <int NT>
+void attn_bwd_launch(const void* dout, const void* q, const void* k, const void* v, const void* p, int BH, int T,
+                     int H, float scale, float* dsum, void* dqkv, hipStream_t s) {
+  attn_bwd_dq_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(dout), static_cast<const bf16*>(k),
+                                            static_cast<const bf16*>(v), static_cast<const bf16*>(p), scale, T, H,
+                                            dsum, static_cast<bf16*>(dqkv));
+  attn_bwd_dkdv_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(dout), static_cast<const bf16*>(q),
+                                              static_cast<const bf16*>(v), static_cast<const bf16*>(p), dsum, scale,
+                                              T, H, static_cast<bf16*>(dqkv));
+}
+
 template <int NT>
 void attn_bwd_ds_launch(const void* dout, const void* v, const void* p, int BH, float scale, void* ds,
                         hipStream_t s) {
@@ -715,6 +892,24 @@ bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp,
 #define RINGDP_ATT_CASE(n) \
   case n:                 \
     attn_bwd_ds_launch<n>(dout, v, p, BH, scale, ds, s); \
+    return true;
+    RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
+    RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)
+    RINGDP_ATT_CASE(11) RINGDP_ATT_CASE(12) RINGDP_ATT_CASE(13) RINGDP_ATT_CASE(14) RINGDP_ATT_CASE(15)
+    RINGDP_ATT_CASE(16)
+#undef RINGDP_ATT_CASE
+  }
+  return false;
+}
+
+bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* p, int B, int T, int H,
+              int Tp, int Dh, float scale, float* dsum, void* dqkv, hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
+  const int BH = B * H;
+  switch (Tp / 16) {
+#define RINGDP_ATT_CASE(n) \
+  case n:                 \
+    attn_bwd_launch<n>(dout, q, k, v, p, BH, T, H, scale, dsum, dqkv, s); \
     return true;
     RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
     RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)

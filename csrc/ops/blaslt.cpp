@@ -117,7 +117,12 @@ static bool matmul_once(const Problem& p, hipStream_t stream) {
   // Measured (tools/blaslt_check.py, ViT-B/16 shapes): the library wins on K-contiguous operands
   // (forward linears: 35-118 us vs 52-201 us with the bias epilogue) and loses on row-contiguous ones
   // (weight gradients 135-275 us vs 66-195 us): those stay on ringdp's kernels.
-  if (p.a_row || p.b_row) return false;
+  static const int row_ok = [] {
+    const char* v = std::getenv("RINGDP_BLASLT_ROW");
+    return v ? std::atoi(v) : 2;  // batched row-contiguous (attention-shaped): 75 vs 91-97 us, attn_gemm_ab.py
+  }();
+  // batched attention-shaped problems (RINGDP_BLASLT_ROW=2) or everything (=1): A/B runs
+  if ((p.a_row || p.b_row) && !(row_ok == 1 || (row_ok == 2 && p.batch > 1))) return false;
   int dev = 0;
   hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_mu);

@@ -590,6 +590,25 @@ at::Tensor attn_bwd_ds(const at::Tensor& dout, const at::Tensor& v, const at::Te
   return ds;
 }
 
+at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
+                    const at::Tensor& p, int64_t B, int64_t T, int64_t H, double scale) {
+  for (const at::Tensor* t : {&dout, &q, &k, &v}) {
+    bf16_gpu(*t, "attention operand");
+    RINGDP_CHECK(t->dim() == 3 && t->sizes() == q.sizes(), "attn_bwd: dO, Q, K, V must be [BH, Tp, Dh]");
+  }
+  bf16_gpu(p, "attention probs");
+  const int64_t BH = q.size(0), Tp = q.size(1), Dh = q.size(2);
+  RINGDP_CHECK(BH == B * H && p.dim() == 3 && p.size(0) == BH && p.size(1) == Tp && p.size(2) == Tp && T <= Tp,
+               "attn_bwd: shape mismatch");
+  at::Tensor dqkv = at::empty({B * T, 3 * H * Dh}, q.options());
+  at::Tensor dsum = at::empty({BH, Tp}, q.options().dtype(at::kFloat));
+  const bool ok = kern::attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), p.data_ptr(), (int)B,
+                                 (int)T, (int)H, (int)Tp, (int)Dh, (float)scale, dsum.data_ptr<float>(),
+                                 dqkv.data_ptr(), stream_of(q));
+  RINGDP_CHECK(ok, "attn_bwd: unsupported shape (needs head dim 64, Tp % 16 == 0, Tp <= 256)");
+  return dqkv;
+}
+
 at::Tensor softmax_bwd(const at::Tensor& p, const at::Tensor& dp, int64_t T, double scale) {
   bf16_gpu(p, "attention probs");
   f32_gpu(dp, "attention probs grad");

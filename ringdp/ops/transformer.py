@@ -19,6 +19,7 @@ from . import grad_buffer
 
 # RINGDP_ATTN_UNFUSED=1: attention forward as two GEMMs + a softmax pass (the path the fused kernel replaced)
 _ATTN_UNFUSED = os.environ.get("RINGDP_ATTN_UNFUSED", "0") == "1"
+_ATTN_BWD_GEMMS = os.environ.get("RINGDP_ATTN_BWD_GEMMS", "0") == "1"  # dS kernel + batched GEMMs (A/B runs)
 _FP8 = {"on": False}
 
 
@@ -322,6 +323,10 @@ class AttentionF(torch.autograd.Function):
         B, T, H, Tp, scale = ctx.cfg
         BH, _, Dh = q.shape
         do = C.rows_to_heads(dout.contiguous(), B, T, H, Tp)
+        if Dh == 64 and Tp <= 256 and not _ATTN_UNFUSED and not _ATTN_BWD_GEMMS:
+            # two fused kernels: query side (dS in registers, dQ) and key side (dK, dV), written
+            # straight into the qkv gradient rows
+            return C.attn_bwd(do, q, k, v, p, B, T, H, scale), None, None, None
         # dP = dO V^T (fp32) -> dS = scale * P * (dP - rowsum(dP * P))
         if Dh == 64 and Tp <= 256 and not _ATTN_UNFUSED:
             ds = C.attn_bwd_ds(do, v, p, scale)  # dP stays in registers

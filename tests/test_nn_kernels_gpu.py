@@ -517,3 +517,26 @@ def test_cast_bf16_multi():
     ys = C().cast_bf16_multi(xs)
     for x, y in zip(xs, ys):
         assert y.dtype == torch.bfloat16 and torch.equal(y, x.bfloat16())
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 197, 3), (3, 17, 2), (1, 64, 4)])
+def test_fused_attention_backward(B, T, H):
+    """attn_bwd (dQ kernel + dK/dV kernel, written into the dqkv rows) vs an fp32 PyTorch reference of
+    softmax attention with the same bf16 inputs and the forward's stored P."""
+    torch.manual_seed(B * 100 + T)
+    Dh, Tp = 64, (T + 15) // 16 * 16
+    qkv = (torch.randn(B * T, 3 * H * Dh, device="cuda") * 0.5).bfloat16()
+    q, k, v = C().qkv_split(qkv, B, T, H, Tp)
+    scale = Dh ** -0.5
+    p, o = C().attn_fwd(q, k, v, T, scale)
+    dout = (torch.randn(B * T, H * Dh, device="cuda") * 0.5).bfloat16()
+    do = C().rows_to_heads(dout, B, T, H, Tp)
+    dqkv = C().attn_bwd(do, q, k, v, p, B, T, H, scale)
+    # reference from the same bf16 q/k/v in fp32
+    qf, kf, vf = (t.float()[:, :T].requires_grad_() for t in (q, k, v))
+    att = torch.softmax((qf @ kf.transpose(1, 2)) * scale, dim=-1)
+    of = att @ vf
+    of.backward(do.float()[:, :T])
+    ref = torch.cat([g.view(B, H, T, Dh).permute(0, 2, 1, 3).reshape(B * T, H * Dh) for g in (qf.grad, kf.grad, vf.grad)],
+                    dim=1)
+    assert rel(dqkv.float(), ref) < 2e-2
