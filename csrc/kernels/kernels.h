@@ -302,6 +302,12 @@ bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp,
 // dsum = [B*H][Tp] fp32 scratch
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* p, int B, int T, int H,
               int Tp, int Dh, float scale, float* dsum, void* dqkv, hipStream_t s);
+// the same kernels reading the qkv projection rows [B*T][3*H*64] and writing the output rows [B*T][H*64]
+// (forward) / taking dO rows [B*T][H*64] (backward): no head-major split, merge or transposes
+bool attn_fwd_rows(const void* qkv, int B, int T, int H, int Tp, int Dh, float scale, void* p, void* out,
+                   hipStream_t s);
+bool attn_bwd_rows(const void* dout_rows, const void* qkv, const void* p, int B, int T, int H, int Tp, int Dh,
+                   float scale, float* dsum, void* dqkv, hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);
 void gelu_bwd(const void* dy, const void* pre, int64_t n, void* dx, hipStream_t s);
 void gelu_fwd(const void* x, int64_t n, void* y, hipStream_t s);  // n % 8 == 0

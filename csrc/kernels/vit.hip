@@ -527,34 +527,52 @@ namespace {
 // 2 x Tp^2 x 4 B per head of HBM traffic plus a softmax pass); P is still stored (bf16) for the backward.
 // Semantics match softmax_fwd + the P V GEMM: keys >= T get probability 0, padded query rows are 0.
 constexpr int ATT_D = 64;
+// Strided view of one attention operand: element (b, h, t, d) at base + b*sb + h*sh + t*st + d - either
+// head-major [B*H][Tp][64] (sb = Tp*64, sh = 0 with H = 1 per "batch" bh) or the token rows of the qkv
+// projection [B*T][3*H*64] (sb = T*st, sh = 64, st = 3*H*64), which the kernels then read directly
+// (no split/merge passes).  Rows t >= T read as zero.
+struct AttnIn {
+  const bf16* base;
+  int64_t sb, sh, st;
+  __device__ __forceinline__ const bf16* row(int bh, int H, int t) const {
+    return base + (int64_t)(bh / H) * sb + (int64_t)(bh % H) * sh + (int64_t)t * st;
+  }
+  __device__ __forceinline__ bf16x8 load8(int bh, int H, int t, int T, int d) const {
+    return t < T ? *reinterpret_cast<const bf16x8*>(row(bh, H, t) + d) : zero_bf16x8();
+  }
+};
+struct AttnOut {
+  bf16* base;
+  int64_t sb, sh, st;
+  int rows;  // rows t < rows are written (T for token rows, Tp for head-major)
+  __device__ __forceinline__ bf16* row(int bh, int H, int t) const {
+    return base + (int64_t)(bh / H) * sb + (int64_t)(bh % H) * sh + (int64_t)t * st;
+  }
+};
 __device__ __forceinline__ int att_ksw(int r, int d) { return r * ATT_D + ((((d >> 3) ^ (r & 7))) << 3) + (d & 7); }
 __device__ __forceinline__ int att_vsw(int r, int d) {
   return r * ATT_D + ((((d >> 4) ^ ((r >> 1) & 3))) << 4) + (d & 15);
 }
 
 template <int NT>  // key tiles of 16 (Tp = 16 * NT)
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ q, const bf16* __restrict__ k,
-                                                       const bf16* __restrict__ v, int T, float scale,
-                                                       bf16* __restrict__ p, bf16* __restrict__ o) {
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnIn q, AttnIn k, AttnIn v, int T, int H, float scale,
+                                                       bf16* __restrict__ p, AttnOut o) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t bh = blockIdx.x;
-  const bf16* kb = k + bh * Tp * ATT_D;
-  const bf16* vb = v + bh * Tp * ATT_D;
-  for (int c = tid; c < Tp * 8; c += 256) {  // 16-B chunks: row c >> 3, columns 8 (c & 7) ..
+  const int bh = blockIdx.x;
+  for (int c = tid; c < Tp * 8; c += 256) {  // 16-B chunks: row c >> 3, columns 8 (c & 7) ..; rows >= T zero
     const int r = c >> 3, d = (c & 7) * 8;
-    *reinterpret_cast<bf16x8*>(Ks + att_ksw(r, d)) = reinterpret_cast<const bf16x8*>(kb)[c];
-    *reinterpret_cast<bf16x8*>(Vs + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(vb)[c];
+    *reinterpret_cast<bf16x8*>(Ks + att_ksw(r, d)) = k.load8(bh, H, r, T, d);
+    *reinterpret_cast<bf16x8*>(Vs + att_vsw(r, d)) = v.load8(bh, H, r, T, d);
   }
   __syncthreads();
   const int g = lane >> 4, qi = lane & 15;
   for (int qt = wave; qt < NT; qt += 4) {
     const int qrow = qt * 16 + qi;
-    const bf16* qp = q + (bh * Tp + qrow) * ATT_D + 8 * g;
-    const bf16x8 qf0 = *reinterpret_cast<const bf16x8*>(qp);
-    const bf16x8 qf1 = *reinterpret_cast<const bf16x8*>(qp + 32);
+    const bf16x8 qf0 = q.load8(bh, H, qrow, T, 8 * g);
+    const bf16x8 qf1 = q.load8(bh, H, qrow, T, 32 + 8 * g);
     f32x4 st[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -588,7 +606,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
     sum += __shfl_xor(sum, 32, 64);
     const float inv = qrow < T ? 1.f / sum : 0.f;  // padded query rows: P = 0
     bf16x4 pb[NT];
-    bf16* prow = p + (bh * Tp + qrow) * Tp + 4 * g;
+    bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp + 4 * g;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       pb[t] = bf16x4{(bf16)(st[t][0] * inv), (bf16)(st[t][1] * inv), (bf16)(st[t][2] * inv), (bf16)(st[t][3] * inv)};
@@ -612,11 +630,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16* __restrict__ 
         ot[dt] = mfma16x16x32(afr, bfr, ot[dt]);
       }
     }
-    bf16* orow = o + (bh * Tp + qrow) * ATT_D + 4 * g;
+    if (qrow < o.rows) {
+      bf16* orow = o.row(bh, H, qrow) + 4 * g;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-      *reinterpret_cast<bf16x4*>(orow + 16 * dt) =
-          bf16x4{(bf16)ot[dt][0], (bf16)ot[dt][1], (bf16)ot[dt][2], (bf16)ot[dt][3]};
+      for (int dt = 0; dt < 4; ++dt)
+        *reinterpret_cast<bf16x4*>(orow + 16 * dt) =
+            bf16x4{(bf16)ot[dt][0], (bf16)ot[dt][1], (bf16)ot[dt][2], (bf16)ot[dt][3]};
+    }
   }
 }
 
@@ -679,33 +699,27 @@ __global__ __launch_bounds__(256) void attn_bwd_ds_kernel(const bf16* __restrict
 // ds_read_b64_tr_b16 (the forward's O^T = V^T P^T trick).  dQ rows go straight into the dqkv gradient
 // rows [B*T][3*H*Dh]; D = rowsum(dP * P) per query is stored for the key-side kernel.
 template <int NT>
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ k,
-                                                          const bf16* __restrict__ v, const bf16* __restrict__ p,
-                                                          float scale, int T, int H, float* __restrict__ dsum,
-                                                          bf16* __restrict__ dqkv) {
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k, AttnIn v,
+                                                          const bf16* __restrict__ p, float scale, int T, int H,
+                                                          float* __restrict__ dsum, AttnOut dq) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t bh = blockIdx.x;
-  const int b = (int)(bh / H), h = (int)(bh % H);
-  const bf16* vb = v + bh * Tp * ATT_D;
-  const bf16* kb = k + bh * Tp * ATT_D;
+  const int bh = blockIdx.x;
   for (int c = tid; c < Tp * 8; c += 256) {
     const int r = c >> 3, d = (c & 7) * 8;
-    *reinterpret_cast<bf16x8*>(Vs + att_ksw(r, d)) = reinterpret_cast<const bf16x8*>(vb)[c];
-    *reinterpret_cast<bf16x8*>(Ks + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(kb)[c];
+    *reinterpret_cast<bf16x8*>(Vs + att_ksw(r, d)) = v.load8(bh, H, r, T, d);
+    *reinterpret_cast<bf16x8*>(Ks + att_vsw(r, d)) = k.load8(bh, H, r, T, d);
   }
   __syncthreads();
   const int g = lane >> 4, qi = lane & 15;
   const int q4 = qi >> 2, p4 = qi & 3;
-  const int64_t row3 = (int64_t)3 * H * ATT_D;
   for (int qt = wave; qt < NT; qt += 4) {
     const int qrow = qt * 16 + qi;
-    const bf16* dp_ = dout + (bh * Tp + qrow) * ATT_D + 8 * g;
-    const bf16x8 of0 = *reinterpret_cast<const bf16x8*>(dp_);
-    const bf16x8 of1 = *reinterpret_cast<const bf16x8*>(dp_ + 32);
-    const bf16* prow = p + (bh * Tp + qrow) * Tp + 4 * g;
+    const bf16x8 of0 = dout.load8(bh, H, qrow, T, 8 * g);
+    const bf16x8 of1 = dout.load8(bh, H, qrow, T, 32 + 8 * g);
+    const bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp + 4 * g;
     bf16x4 pv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) pv[t] = *reinterpret_cast<const bf16x4*>(prow + 16 * t);
@@ -724,7 +738,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
       for (int i = 0; i < 4; ++i) dot = fmaf(dpt[t][i], (float)pv[t][i], dot);
     dot += __shfl_xor(dot, 16, 64);
     dot += __shfl_xor(dot, 32, 64);
-    if (g == 0) dsum[bh * Tp + qrow] = dot;
+    if (g == 0) dsum[(int64_t)bh * Tp + qrow] = dot;
     bf16x4 dsb[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -747,8 +761,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
         qt4[dt] = mfma16x16x32(afr, bfr, qt4[dt]);
       }
     }
-    if (qrow < T) {
-      bf16* drow = dqkv + ((int64_t)b * T + qrow) * row3 + h * ATT_D + 4 * g;
+    if (qrow < dq.rows) {
+      bf16* drow = dq.row(bh, H, qrow) + 4 * g;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         *reinterpret_cast<bf16x4*>(drow + 16 * dt) =
@@ -764,34 +778,28 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const bf16* __restrict
 // with those registers as the MFMA B operand (reduction over the query pair, permuted like the forward's
 // key pairs) and dO^T / Q^T read from LDS with ds_read_b64_tr_b16.  dK, dV rows go straight into dqkv.
 template <int NT>
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restrict__ dout, const bf16* __restrict__ q,
-                                                            const bf16* __restrict__ v, const bf16* __restrict__ p,
-                                                            const float* __restrict__ dsum, float scale, int T, int H,
-                                                            bf16* __restrict__ dqkv) {
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn q, AttnIn v,
+                                                            const bf16* __restrict__ p, const float* __restrict__ dsum,
+                                                            float scale, int T, int H, AttnOut dk, AttnOut dv) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Qs[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Os[Tp * ATT_D];  // dO
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t bh = blockIdx.x;
-  const int b = (int)(bh / H), h = (int)(bh % H);
-  const bf16* qb = q + bh * Tp * ATT_D;
-  const bf16* ob = dout + bh * Tp * ATT_D;
+  const int bh = blockIdx.x;
   for (int c = tid; c < Tp * 8; c += 256) {
     const int r = c >> 3, d = (c & 7) * 8;
-    *reinterpret_cast<bf16x8*>(Qs + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(qb)[c];
-    *reinterpret_cast<bf16x8*>(Os + att_vsw(r, d)) = reinterpret_cast<const bf16x8*>(ob)[c];
+    *reinterpret_cast<bf16x8*>(Qs + att_vsw(r, d)) = q.load8(bh, H, r, T, d);
+    *reinterpret_cast<bf16x8*>(Os + att_vsw(r, d)) = dout.load8(bh, H, r, T, d);
   }
   __syncthreads();
   const int g = lane >> 4, ki = lane & 15;
   const int q4 = ki >> 2, p4 = ki & 3;
-  const int64_t row3 = (int64_t)3 * H * ATT_D;
-  const float* db = dsum + bh * Tp;
+  const float* db = dsum + (int64_t)bh * Tp;
   for (int kt = wave; kt < NT; kt += 4) {
     const int key = kt * 16 + ki;
-    const bf16* vr = v + (bh * Tp + key) * ATT_D + 8 * g;
-    const bf16x8 vf0 = *reinterpret_cast<const bf16x8*>(vr);
-    const bf16x8 vf1 = *reinterpret_cast<const bf16x8*>(vr + 32);
-    const bf16* pcol = p + bh * Tp * Tp + key;
+    const bf16x8 vf0 = v.load8(bh, H, key, T, 8 * g);
+    const bf16x8 vf1 = v.load8(bh, H, key, T, 32 + 8 * g);
+    const bf16* pcol = p + (int64_t)bh * Tp * Tp + key;
     f32x4 dva[4], dka[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dva[dt] = dka[dt] = zero_f32x4();
@@ -805,13 +813,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
         const int orow = 16 * qp[u] + ki;
         const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Os + att_vsw(orow, 8 * g));
         const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Os + att_vsw(orow, 32 + 8 * g));
-        const f32x4 dp = mfma16x16x32(a1, vf1, mfma16x16x32(a0, vf0, zero_f32x4()));
+        const f32x4 dpv = mfma16x16x32(a1, vf1, mfma16x16x32(a0, vf0, zero_f32x4()));
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qq = 16 * qp[u] + 4 * g + r;
           const float pr = (u == 0 || has1) ? (float)pcol[(int64_t)qq * Tp] : 0.f;
           pb[u][r] = (bf16)pr;
-          sb[u][r] = (bf16)(scale * pr * (dp[r] - db[qq]));
+          sb[u][r] = (bf16)(scale * pr * (dpv[r] - db[qq]));
         }
       }
       const bf16x8 pfr = bf16x8{pb[0][0], pb[0][1], pb[0][2], pb[0][3], pb[1][0], pb[1][1], pb[1][2], pb[1][3]};
@@ -826,9 +834,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
         dka[dt] = mfma16x16x32(bf16x8{qlo[0], qlo[1], qlo[2], qlo[3], qhi[0], qhi[1], qhi[2], qhi[3]}, sfr, dka[dt]);
       }
     }
-    if (key < T) {
-      bf16* krow = dqkv + ((int64_t)b * T + key) * row3 + H * ATT_D + h * ATT_D + 4 * g;
-      bf16* vrow = krow + H * ATT_D;
+    if (key < dk.rows) {
+      bf16* krow = dk.row(bh, H, key) + 4 * g;
+      bf16* vrow = dv.row(bh, H, key) + 4 * g;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         *reinterpret_cast<bf16x4*>(krow + 16 * dt) =
@@ -841,14 +849,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const bf16* __restri
 }
 
 template <int NT>
-void attn_bwd_launch(const void* dout, const void* q, const void* k, const void* v, const void* p, int BH, int T,
-                     int H, float scale, float* dsum, void* dqkv, hipStream_t s) {
-  attn_bwd_dq_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(dout), static_cast<const bf16*>(k),
-                                            static_cast<const bf16*>(v), static_cast<const bf16*>(p), scale, T, H,
-                                            dsum, static_cast<bf16*>(dqkv));
-  attn_bwd_dkdv_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(dout), static_cast<const bf16*>(q),
-                                              static_cast<const bf16*>(v), static_cast<const bf16*>(p), dsum, scale,
-                                              T, H, static_cast<bf16*>(dqkv));
+void attn_bwd_launch(AttnIn dout, AttnIn q, AttnIn k, AttnIn v, const void* p, int BH, int T, int H, float scale,
+                     float* dsum, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s) {
+  attn_bwd_dq_kernel<NT><<<BH, 256, 0, s>>>(dout, k, v, static_cast<const bf16*>(p), scale, T, H, dsum, dq);
+  attn_bwd_dkdv_kernel<NT><<<BH, 256, 0, s>>>(dout, q, v, static_cast<const bf16*>(p), dsum, scale, T, H, dk, dv);
 }
 
 template <int NT>
@@ -859,29 +863,53 @@ void attn_bwd_ds_launch(const void* dout, const void* v, const void* p, int BH, 
 }
 
 template <int NT>
-void attn_fwd_launch(const void* q, const void* k, const void* v, int BH, int T, float scale, void* p, void* o,
+void attn_fwd_launch(AttnIn q, AttnIn k, AttnIn v, int BH, int T, int H, float scale, void* p, AttnOut o,
                      hipStream_t s) {
-  attn_fwd_kernel<NT><<<BH, 256, 0, s>>>(static_cast<const bf16*>(q), static_cast<const bf16*>(k),
-                                         static_cast<const bf16*>(v), T, scale, static_cast<bf16*>(p),
-                                         static_cast<bf16*>(o));
+  attn_fwd_kernel<NT><<<BH, 256, 0, s>>>(q, k, v, T, H, scale, static_cast<bf16*>(p), o);
 }
 
 }  // namespace
 
+// head-major [BH][Tp][64] views (H = 1: bh is the batch index) and token-row views of a [B*T][width]
+// matrix at column offset col0
+static AttnIn head_major(const void* base, int Tp) {
+  return AttnIn{static_cast<const bf16*>(base), (int64_t)Tp * ATT_D, 0, ATT_D};
+}
+static AttnOut head_major_out(void* base, int Tp) { return AttnOut{static_cast<bf16*>(base), (int64_t)Tp * ATT_D, 0, ATT_D, Tp}; }
+static AttnIn token_rows(const void* base, int T, int64_t width, int64_t col0) {
+  return AttnIn{static_cast<const bf16*>(base) + col0, (int64_t)T * width, ATT_D, width};
+}
+static AttnOut token_rows_out(void* base, int T, int64_t width, int64_t col0) {
+  return AttnOut{static_cast<bf16*>(base) + col0, (int64_t)T * width, ATT_D, width, T};
+}
+
+#define RINGDP_ATT_SWITCH(CALL)                                                                          \
+  switch (Tp / 16) {                                                                                     \
+    case 1: { constexpr int n = 1; CALL; return true; }   case 2: { constexpr int n = 2; CALL; return true; }   \
+    case 3: { constexpr int n = 3; CALL; return true; }   case 4: { constexpr int n = 4; CALL; return true; }   \
+    case 5: { constexpr int n = 5; CALL; return true; }   case 6: { constexpr int n = 6; CALL; return true; }   \
+    case 7: { constexpr int n = 7; CALL; return true; }   case 8: { constexpr int n = 8; CALL; return true; }   \
+    case 9: { constexpr int n = 9; CALL; return true; }   case 10: { constexpr int n = 10; CALL; return true; } \
+    case 11: { constexpr int n = 11; CALL; return true; } case 12: { constexpr int n = 12; CALL; return true; } \
+    case 13: { constexpr int n = 13; CALL; return true; } case 14: { constexpr int n = 14; CALL; return true; } \
+    case 15: { constexpr int n = 15; CALL; return true; } case 16: { constexpr int n = 16; CALL; return true; } \
+  }
+
 bool attn_fwd(const void* q, const void* k, const void* v, int BH, int T, int Tp, int Dh, float scale, void* p,
               void* o, hipStream_t s) {
   if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
-  switch (Tp / 16) {
-#define RINGDP_ATT_CASE(n) \
-  case n:                 \
-    attn_fwd_launch<n>(q, k, v, BH, T, scale, p, o, s); \
-    return true;
-    RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
-    RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)
-    RINGDP_ATT_CASE(11) RINGDP_ATT_CASE(12) RINGDP_ATT_CASE(13) RINGDP_ATT_CASE(14) RINGDP_ATT_CASE(15)
-    RINGDP_ATT_CASE(16)
-#undef RINGDP_ATT_CASE
-  }
+  RINGDP_ATT_SWITCH((attn_fwd_launch<n>(head_major(q, Tp), head_major(k, Tp), head_major(v, Tp), BH, T, 1, scale, p,
+                                        head_major_out(o, Tp), s)))
+  return false;
+}
+
+bool attn_fwd_rows(const void* qkv, int B, int T, int H, int Tp, int Dh, float scale, void* p, void* out,
+                   hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
+  const int64_t w3 = (int64_t)3 * H * ATT_D, w1 = (int64_t)H * ATT_D;
+  RINGDP_ATT_SWITCH((attn_fwd_launch<n>(token_rows(qkv, T, w3, 0), token_rows(qkv, T, w3, w1),
+                                        token_rows(qkv, T, w3, 2 * w1), B * H, T, H, scale, p,
+                                        token_rows_out(out, T, w1, 0), s)))
   return false;
 }
 
@@ -905,18 +933,24 @@ bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp,
 bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, const void* p, int B, int T, int H,
               int Tp, int Dh, float scale, float* dsum, void* dqkv, hipStream_t s) {
   if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
-  const int BH = B * H;
-  switch (Tp / 16) {
-#define RINGDP_ATT_CASE(n) \
-  case n:                 \
-    attn_bwd_launch<n>(dout, q, k, v, p, BH, T, H, scale, dsum, dqkv, s); \
-    return true;
-    RINGDP_ATT_CASE(1) RINGDP_ATT_CASE(2) RINGDP_ATT_CASE(3) RINGDP_ATT_CASE(4) RINGDP_ATT_CASE(5)
-    RINGDP_ATT_CASE(6) RINGDP_ATT_CASE(7) RINGDP_ATT_CASE(8) RINGDP_ATT_CASE(9) RINGDP_ATT_CASE(10)
-    RINGDP_ATT_CASE(11) RINGDP_ATT_CASE(12) RINGDP_ATT_CASE(13) RINGDP_ATT_CASE(14) RINGDP_ATT_CASE(15)
-    RINGDP_ATT_CASE(16)
-#undef RINGDP_ATT_CASE
-  }
+  // head-major operands of batch bh = b*H + h: element (bh, t) at bh*Tp*64 + t*64 = b*(H*Tp*64) + h*(Tp*64) + ..
+  const int64_t hm = (int64_t)Tp * ATT_D;
+  auto hmv = [&](const void* base) { return AttnIn{static_cast<const bf16*>(base), H * hm, hm, ATT_D}; };
+  const int64_t w3 = (int64_t)3 * H * ATT_D, w1 = (int64_t)H * ATT_D;
+  RINGDP_ATT_SWITCH((attn_bwd_launch<n>(hmv(dout), hmv(q), hmv(k), hmv(v), p, B * H, T, H, scale, dsum,
+                                        token_rows_out(dqkv, T, w3, 0), token_rows_out(dqkv, T, w3, w1),
+                                        token_rows_out(dqkv, T, w3, 2 * w1), s)))
+  return false;
+}
+
+bool attn_bwd_rows(const void* dout_rows, const void* qkv, const void* p, int B, int T, int H, int Tp, int Dh,
+                   float scale, float* dsum, void* dqkv, hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
+  const int64_t w3 = (int64_t)3 * H * ATT_D, w1 = (int64_t)H * ATT_D;
+  RINGDP_ATT_SWITCH((attn_bwd_launch<n>(token_rows(dout_rows, T, w1, 0), token_rows(qkv, T, w3, 0),
+                                        token_rows(qkv, T, w3, w1), token_rows(qkv, T, w3, 2 * w1), p, B * H, T, H,
+                                        scale, dsum, token_rows_out(dqkv, T, w3, 0), token_rows_out(dqkv, T, w3, w1),
+                                        token_rows_out(dqkv, T, w3, 2 * w1), s)))
   return false;
 }
 

@@ -301,6 +301,16 @@ class AttentionF(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, B: int, T: int, H: int):
         Tp = _tp(T)
+        Dh = qkv.shape[1] // (3 * H)
+        if Dh == 64 and Tp <= 256 and not _ATTN_UNFUSED and not _ATTN_BWD_GEMMS:
+            # fused kernels straight on the projection rows: no head-major split / merge passes
+            scale = 1.0 / math.sqrt(Dh)
+            p, out = C.attn_fwd_rows(qkv, B, T, H, scale)
+            ctx.save_for_backward(qkv, p)
+            ctx.cfg = (B, T, H, Tp, scale)
+            ctx.rows = True
+            return out
+        ctx.rows = False
         q, k, v = C.qkv_split(qkv, B, T, H, Tp)
         BH, _, Dh = q.shape
         scale = 1.0 / math.sqrt(Dh)
@@ -319,6 +329,10 @@ class AttentionF(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        if ctx.rows:
+            qkv, p = ctx.saved_tensors
+            B, T, H, Tp, scale = ctx.cfg
+            return C.attn_bwd_rows(dout.contiguous(), qkv, p, B, T, H, scale), None, None, None
         q, k, v, p = ctx.saved_tensors
         B, T, H, Tp, scale = ctx.cfg
         BH, _, Dh = q.shape

@@ -540,3 +540,22 @@ def test_fused_attention_backward(B, T, H):
     ref = torch.cat([g.view(B, H, T, Dh).permute(0, 2, 1, 3).reshape(B * T, H * Dh) for g in (qf.grad, kf.grad, vf.grad)],
                     dim=1)
     assert rel(dqkv.float(), ref) < 2e-2
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 197, 3), (3, 17, 2)])
+def test_attention_rows_layout_matches_head_major(B, T, H):
+    """attn_fwd_rows / attn_bwd_rows read the qkv projection rows directly: bitwise the same results as
+    the head-major kernels after qkv_split / heads_to_rows."""
+    torch.manual_seed(T)
+    Dh, Tp = 64, (T + 15) // 16 * 16
+    qkv = (torch.randn(B * T, 3 * H * Dh, device="cuda") * 0.5).bfloat16()
+    scale = Dh ** -0.5
+    q, k, v = C().qkv_split(qkv, B, T, H, Tp)
+    p, o = C().attn_fwd(q, k, v, T, scale)
+    p2, out2 = C().attn_fwd_rows(qkv, B, T, H, scale)
+    assert torch.equal(p, p2)
+    assert torch.equal(C().heads_to_rows(o, B, T), out2)
+    dout = (torch.randn(B * T, H * Dh, device="cuda") * 0.5).bfloat16()
+    d1 = C().attn_bwd(C().rows_to_heads(dout, B, T, H, Tp), q, k, v, p, B, T, H, scale)
+    d2 = C().attn_bwd_rows(dout, qkv, p2, B, T, H, scale)
+    assert torch.equal(d1, d2)
