@@ -413,6 +413,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def_readwrite("maximize", &ops::SgdHyper::maximize);
   m.def("cast_copy", &ops::cast_copy);
   m.def("cast_bf16_multi", &ops::cast_bf16_multi);
+  m.def("cast_bf16_t_multi", &ops::cast_bf16_t_multi);
   m.def("transpose_bf16", &ops::transpose_bf16);
   m.def("sgd_flat", &ops::sgd_flat, py::arg("param"), py::arg("grad"), py::arg("momentum_buf"),
         py::arg("hyper"), py::arg("first_step"), py::arg("lr_tensor") = py::none(),

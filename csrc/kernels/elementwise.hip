@@ -72,6 +72,43 @@ __global__ __launch_bounds__(256) void cast_multi_kernel(CastTable t) {
   }
 }
 
+// fp32 [R][C] -> bf16 [R][C] and its transpose bf16 [C][R], many matrices in one launch: block = one 64x64
+// tile of some matrix (start_tile prefix in the table), read once, both outputs written coalesced (the
+// transpose through LDS).  A linear layer's forward uses W, its data gradient W^T.
+__global__ __launch_bounds__(256) void cast_t_multi_kernel(CastTTable t) {
+  __shared__ CastTEntry se[kCastTMax];
+  __shared__ float tile[64][65];
+#pragma unroll
+  for (int i = 0; i < kCastTMax; ++i)
+    if (threadIdx.x == i && i < t.n) se[i] = t.e[i];
+  __syncthreads();
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < t.n && b >= se[i + 1].start_tile) ++i;
+  const CastTEntry d = se[i];
+  const int tiles_c = (d.C + 63) / 64;
+  const int tb = b - d.start_tile;
+  const int r0 = (tb / tiles_c) * 64, c0 = (tb % tiles_c) * 64;
+  bf16* w = static_cast<bf16*>(d.dst);
+  bf16* wt = static_cast<bf16*>(d.dst_t);
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int rr = idx >> 6, cc = idx & 63;
+    const int r = r0 + rr, c = c0 + cc;
+    float x = 0.f;
+    if (r < d.R && c < d.C) {
+      x = d.src[(int64_t)r * d.C + c];
+      w[(int64_t)r * d.C + c] = (bf16)x;
+    }
+    tile[rr][cc] = x;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+    const int cc = idx >> 6, rr = idx & 63;
+    const int r = r0 + rr, c = c0 + cc;
+    if (r < d.R && c < d.C) wt[(int64_t)c * d.R + r] = (bf16)tile[rr][cc];
+  }
+}
+
 __global__ void cast_bf16_f32_kernel(const bf16* __restrict__ src, float* __restrict__ dst, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t n4 = n / 4;
@@ -355,6 +392,9 @@ __global__ void synth_u8_kernel(uint8_t* __restrict__ x, int64_t* __restrict__ l
 void cast_f32_to_bf16(const float* src, void* dst, int64_t n, hipStream_t s) {
   if (n <= 0) return;
   cast_f32_bf16_kernel<<<grid_for(n / 4 + 1, 256), 256, 0, s>>>(src, static_cast<bf16*>(dst), n);
+}
+void cast_t_multi(const CastTTable& t, hipStream_t s) {
+  if (t.total_tiles > 0) cast_t_multi_kernel<<<t.total_tiles, 256, 0, s>>>(t);
 }
 void cast_f32_to_bf16_multi(const CastTable& t, hipStream_t s) {
   if (t.total4 > 0) cast_multi_kernel<<<grid_for(t.total4, 256), 256, 0, s>>>(t);

@@ -240,6 +240,20 @@ struct CastTable {
   CastEntry e[kCastMax];
 };
 void cast_f32_to_bf16_multi(const CastTable& t, hipStream_t s);
+struct CastTEntry {
+  const float* src;  // [R][C] fp32
+  void* dst;         // [R][C] bf16
+  void* dst_t;       // [C][R] bf16
+  int R, C;
+  int start_tile;    // first 64x64 tile of this matrix in the launch
+};
+constexpr int kCastTMax = 96;  // 96 x 40 B + header < the 4 KiB kernel-argument limit
+struct CastTTable {
+  int n;
+  int total_tiles;
+  CastTEntry e[kCastTMax];
+};
+void cast_t_multi(const CastTTable& t, hipStream_t s);
 struct PackEntry {
   const float* w;
   void* krsc;  // bf16

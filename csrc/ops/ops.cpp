@@ -108,6 +108,35 @@ std::vector<at::Tensor> cast_bf16_multi(const std::vector<at::Tensor>& srcs) {
   return out;
 }
 
+std::vector<at::Tensor> cast_bf16_t_multi(const std::vector<at::Tensor>& srcs) {
+  std::vector<at::Tensor> out;
+  kern::CastTTable t{};
+  for (const at::Tensor& x : srcs) {
+    check_cuda(x, "cast_bf16_t_multi src");
+    RINGDP_CHECK(x.scalar_type() == at::kFloat && x.is_contiguous() && x.dim() == 2,
+                 "cast_bf16_t_multi: contiguous fp32 matrices");
+    const int64_t R = x.size(0), Cc = x.size(1);
+    at::Tensor y = at::empty({R, Cc}, x.options().dtype(at::kBFloat16));
+    at::Tensor yt = at::empty({Cc, R}, x.options().dtype(at::kBFloat16));
+    out.push_back(y);
+    out.push_back(yt);
+    if (t.n == kern::kCastTMax) {
+      kern::cast_t_multi(t, cur_stream(x));
+      t = kern::CastTTable{};
+    }
+    kern::CastTEntry& e = t.e[t.n++];
+    e.src = x.data_ptr<float>();
+    e.dst = y.data_ptr();
+    e.dst_t = yt.data_ptr();
+    e.R = (int)R;
+    e.C = (int)Cc;
+    e.start_tile = t.total_tiles;
+    t.total_tiles += (int)(((R + 63) / 64) * ((Cc + 63) / 64));
+  }
+  if (t.n > 0) kern::cast_t_multi(t, cur_stream(srcs[0]));
+  return out;
+}
+
 void cast_copy(at::Tensor dst, const at::Tensor& src) {
   RINGDP_CHECK(dst.numel() == src.numel(), "cast_copy: numel mismatch");
   if (!dst.is_cuda()) {

@@ -14,6 +14,8 @@ namespace ops {
 void cast_copy(at::Tensor dst, const at::Tensor& src);
 // fp32 -> bf16 copies of many tensors in one launch
 std::vector<at::Tensor> cast_bf16_multi(const std::vector<at::Tensor>& srcs);
+// fp32 matrices -> [bf16 W, bf16 W^T] pairs in one launch
+std::vector<at::Tensor> cast_bf16_t_multi(const std::vector<at::Tensor>& srcs);
 
 struct SgdHyper {
   double lr = 0.01;

@@ -38,16 +38,30 @@ def fp8_enabled() -> bool:
 _BF16_WEIGHTS: dict = {}
 
 
+_BF16_WEIGHTS_T: dict = {}  # {id(bf16 copy): its transpose}, for the data-gradient GEMMs
+
+
 def cast_weights(ws) -> None:
-    """Cast many fp32 weights to bf16 in one launch for the forward in progress (see _bf16)."""
-    ws = [w for w in ws if w.is_cuda and w.dtype == torch.float32 and w.numel() % 4 == 0]
+    """Cast many fp32 [out, in] weights to bf16 AND bf16 transposed in one launch for the forward in
+    progress (see _bf16 / _bf16_t): the backward's data-gradient GEMMs take W^T K-contiguous."""
+    ws = [w for w in ws if w.is_cuda and w.dtype == torch.float32 and w.dim() == 2]
+    _BF16_WEIGHTS_T.clear()  # the previous step's backward has taken what it needed
     if ws:
-        for w, b in zip(ws, C.cast_bf16_multi([w.detach().contiguous() for w in ws])):
-            _BF16_WEIGHTS[id(w)] = b
+        flat = C.cast_bf16_t_multi([w.detach().contiguous() for w in ws])
+        for i, w in enumerate(ws):
+            _BF16_WEIGHTS[id(w)] = flat[2 * i]
+            # keyed by the bf16 copy, which the entry keeps alive (its id cannot be reused meanwhile)
+            _BF16_WEIGHTS_T[id(flat[2 * i])] = (flat[2 * i], flat[2 * i + 1])
 
 
 def clear_weights() -> None:
     _BF16_WEIGHTS.clear()
+
+
+def _bf16_t(wb: torch.Tensor) -> torch.Tensor:
+    """W^T of a bf16 weight copy: from the forward's cast launch when it made one, else a transpose."""
+    e = _BF16_WEIGHTS_T.pop(id(wb), None)
+    return e[1] if e is not None and e[0] is wb else C.transpose_bf16(wb)
 
 
 def _bf16(w: torch.Tensor) -> torch.Tensor:
@@ -116,7 +130,7 @@ class LinearF(torch.autograd.Function):
             # library path runs fastest (tools/blaslt_check.py); with RINGDP_GEMM_BACKEND=ringdp the
             # row-contiguous form reads W directly.
             if C.gemm_backend() == "auto":
-                dx = C.gemm(dz, C.transpose_bf16(wb), M, K, N, N, N, False, False).view(M, K)
+                dx = C.gemm(dz, _bf16_t(wb), M, K, N, N, N, False, False).view(M, K)
             else:
                 dx = C.gemm(dz, wb, M, K, N, N, K, False, True).view(M, K)
         dw = db = None
@@ -230,7 +244,7 @@ class MLPF(torch.autograd.Function):
         dy = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
         # d(fc1 output) = (dy W2) * GELU'(pre): the GELU backward rides in the GEMM epilogue (act 3)
         if C.gemm_backend() == "auto":
-            dz1 = C.gemm(dy, C.transpose_bf16(w2b), M, Hd, D, D, D, False, False, 1, 0, 0, True, None, 3, None,
+            dz1 = C.gemm(dy, _bf16_t(w2b), M, Hd, D, D, D, False, False, 1, 0, 0, True, None, 3, None,
                          pre).view(M, Hd)
         else:
             dz1 = C.gemm(dy, w2b, M, Hd, D, D, Hd, False, True, 1, 0, 0, True, None, 3, None, pre).view(M, Hd)
@@ -243,7 +257,7 @@ class MLPF(torch.autograd.Function):
         dh = None
         if ctx.needs_input_grad[0]:
             if C.gemm_backend() == "auto":
-                dh = C.gemm(dz1, C.transpose_bf16(w1b), M, D, Hd, Hd, Hd, False, False).view(M, D)
+                dh = C.gemm(dz1, _bf16_t(w1b), M, D, Hd, Hd, Hd, False, False).view(M, D)
             else:
                 dh = C.gemm(dz1, w1b, M, D, Hd, Hd, D, False, True).view(M, D)
         dres = dy if ctx.has_res else None

@@ -559,3 +559,12 @@ def test_attention_rows_layout_matches_head_major(B, T, H):
     d1 = C().attn_bwd(C().rows_to_heads(dout, B, T, H, Tp), q, k, v, p, B, T, H, scale)
     d2 = C().attn_bwd_rows(dout, qkv, p2, B, T, H, scale)
     assert torch.equal(d1, d2)
+
+
+def test_cast_bf16_t_multi():
+    torch.manual_seed(6)
+    xs = [torch.randn(r, c, device="cuda") for r, c in ((2304, 768), (10, 768), (3072, 768), (768, 3072), (70, 130))]
+    flat = C().cast_bf16_t_multi(xs)
+    for i, x in enumerate(xs):
+        assert torch.equal(flat[2 * i], x.bfloat16())
+        assert torch.equal(flat[2 * i + 1], x.t().contiguous().bfloat16())
