@@ -487,12 +487,21 @@ __device__ __forceinline__ void a2_glds(const bf16* __restrict__ a2, int b, bf16
   }
 }
 
-// staging buffer -> padded MFMA rows (C3_XRS): the padding keeps the 16 rows of a fragment read on
-// distinct banks, which a lane-linear DMA image cannot have
+// staging buffer -> padded MFMA rows (RS elements per row, C3_XRS by default): the padding keeps the 16
+// rows of a fragment read on distinct banks, which a lane-linear DMA image cannot have
+template <int RS = C3_XRS>
 __device__ __forceinline__ void a2_relayout(const bf16* R, bf16* X, int tid, int nthreads) {
   for (int c = tid; c < 800; c += nthreads)
-    *reinterpret_cast<bf16x8*>(X + (c >> 3) * C3_XRS + (c & 7) * 8) = reinterpret_cast<const bf16x8*>(R)[c];
+    *reinterpret_cast<bf16x8*>(X + (c >> 3) * RS + (c & 7) * 8) = reinterpret_cast<const bf16x8*>(R)[c];
 }
+
+// conv3 forward A-operand image: 160-B rows and this pool-window order of the m-tiles make every
+// ds_read_b128 fragment read conflict-free (modelled with the b128 lane groups of MI355X_MICROARCH.md:
+// 1.0 LDS cycles per read, was 2.0 with 144-B rows and the natural window order; the measured
+// SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS was 3.0).  Entry 4*mt + j = the pool window (row-major
+// in the 4x4 window grid) whose 4 positions are rows 4j..4j+3 of m-tile mt.
+constexpr int C3F_XRS = 80;
+__constant__ uint8_t c3f_win[16] = {1, 9, 13, 11, 10, 3, 15, 8, 7, 12, 0, 5, 4, 6, 2, 14};
 
 __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restrict__ a2,
                                                            const bf16* __restrict__ packed,
@@ -500,7 +509,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
                                                            bf16* __restrict__ a3,
                                                            uint8_t* __restrict__ idx3, int B) {
   __shared__ __attribute__((aligned(16))) bf16 R[100 * 64];
-  __shared__ __attribute__((aligned(16))) bf16 X[100 * C3_XRS];
+  __shared__ __attribute__((aligned(16))) bf16 X[100 * C3F_XRS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3F_OFF);
@@ -512,15 +521,18 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
   float bv[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) bv[t] = bias[32 * wave + 16 * t + r16];
-  int base[4];
+  int base[4], wcol[4];  // A row of this lane per m-tile; pool window of this lane's accumulators
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) base[mt] = win_pos(4 * (4 * mt + (r16 >> 2)) + (r16 & 3), 10);
+  for (int mt = 0; mt < 4; ++mt) {
+    base[mt] = win_pos(4 * c3f_win[4 * mt + (r16 >> 2)] + (r16 & 3), 10);
+    wcol[mt] = c3f_win[4 * mt + (lane >> 4)];
+  }
   int b = blockIdx.x;
   if (b < B) a2_glds(a2, b, R, wave, lane, 4);
   for (; b < B; b += gridDim.x) {
     c_dma_wait();
     __syncthreads();  // R has landed; the previous image's X reads are done
-    a2_relayout(R, X, tid, 256);
+    a2_relayout<C3F_XRS>(R, X, tid, 256);
     __syncthreads();  // X complete, R free
     const int nb = b + gridDim.x;
     if (nb < B) a2_glds(a2, nb, R, wave, lane, 4);  // lands while the MFMAs below run
@@ -533,7 +545,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
       const int shift = (tap / 3) * 10 + tap % 3;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(X + (base[mt] + shift) * C3_XRS + c0 + q8);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(X + (base[mt] + shift) * C3F_XRS + c0 + q8);
         acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
         acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
       }
@@ -542,7 +554,7 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int wc = 4 * mt + (lane >> 4), co = 32 * wave + 16 * t + r16;
+        const int wc = wcol[mt], co = 32 * wave + 16 * t + r16;
         int g;
         const bf16 pb = (bf16)pool4(acc[mt][t], bv[t], g);
         const int64_t o = ((int64_t)b * 16 + wc) * 128 + co;
