@@ -36,6 +36,7 @@ Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -108,6 +109,9 @@ def _store_agree(dist, key: str, ok: bool, rank: int, world: int) -> bool:
 
 
 def worker(args):
+    # RINGDP_BENCH_STACKS_S=N: dump every thread's Python stack after N seconds (hang diagnosis)
+    if os.environ.get("RINGDP_BENCH_STACKS_S"):
+        faulthandler.dump_traceback_later(float(os.environ["RINGDP_BENCH_STACKS_S"]), repeat=True, file=sys.stderr)
     import ringdp
     import ringdp.distributed as dist
     from ringdp import models
