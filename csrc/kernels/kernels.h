@@ -279,7 +279,7 @@ void bn_prepare(const float* sums, int G, int64_t M, int C, const float* gamma, 
 void bn_act_fwd(const void* z, const float* scale_shift, const void* res, bool relu, int64_t M, int C, void* y,
                 hipStream_t s);
 // backward part 1: g = dy * (y > 0 if relu); partial sums of g and g*zhat per channel -> part
-int bn_bwd_parts(int64_t M);
+int bn_bwd_parts(int64_t M, int C);
 void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
                    float* part, void* g_out, hipStream_t s);
 // part 2: dgamma/dbeta and dz = scale*(g - mean(g) - zhat*mean(g*zhat))/..., plus d(residual) = g

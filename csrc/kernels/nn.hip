@@ -234,12 +234,15 @@ __global__ __launch_bounds__(256) void bn_act_fwd_col_kernel(const bf16* __restr
 
 // dz = A*g + Bz*z + Cc per channel (A = gamma*invstd, Bz = -A*invstd*dgamma/M,
 // Cc = -A*dbeta/M - Bz*mean): the coefficients are formed once per thread in registers.
+// part != null (few partial rows, see kBnFewParts): every workgroup sums the [nparts][2][C] partials of
+// its channels itself in a fixed order and workgroup 0 stores dgamma / dbeta - two launches fewer than
+// the two-level reduction; otherwise dgamma / dbeta are inputs.
 __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
                                                                const float* __restrict__ save,
                                                                const float* __restrict__ gamma,
-                                                               const float* __restrict__ dgamma,
-                                                               const float* __restrict__ dbeta, int64_t M, int C,
-                                                               bf16* __restrict__ dz) {
+                                                               float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta, const float* __restrict__ part,
+                                                               int nparts, int64_t M, int C, bf16* __restrict__ dz) {
   const int cv = C >> 3, rpb = 256 / cv;
   const int col = threadIdx.x % cv, rsub = threadIdx.x / cv;
   const float invM = 1.f / (float)M;
@@ -247,8 +250,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __res
   load8(save + col * 8, mean);
   load8(save + C + col * 8, inv);
   load8(gamma + col * 8, ga);
-  load8(dgamma + col * 8, dg);
-  load8(dbeta + col * 8, db);
+  if (part) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg[j] = db[j] = 0.f;
+    for (int p = 0; p < nparts; ++p) {
+      float a[8], q[8];
+      load8(part + (int64_t)p * 2 * C + col * 8, a);      // sum of g
+      load8(part + (int64_t)p * 2 * C + C + col * 8, q);  // sum of g * zhat
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        db[j] += a[j];
+        dg[j] += q[j];
+      }
+    }
+    if (blockIdx.x == 0 && rsub == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        dbeta[col * 8 + j] = db[j];
+        dgamma[col * 8 + j] = dg[j];
+      }
+    }
+  } else {
+    load8(dgamma + col * 8, dg);
+    load8(dbeta + col * 8, db);
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     A[j] = ga[j] * inv[j];
@@ -281,7 +306,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __res
 
 // Rows are split over workgroups; each thread owns one 8-channel vector column (C/8 columns, C <= 2048)
 // and walks rows with a stride, accumulating in fp32; partials [part][2][C] (deterministic).
-inline int64_t bn_rows_per_part(int64_t M) { return std::max<int64_t>(64, (M + 1023) / 1024); }
+// Small tensors (ResNet-18 at CIFAR shape, layers 2-4: M*C <= 512K elements): at most kBnFewParts partial rows, which
+// the apply kernel sums itself (no separate two-level reduction launches).  Larger ones keep up to 1024
+// row slices so the reduction spreads over the whole chip (16 slices of a 50k x 1024 tensor took 7 ms per
+// ResNet-50 step more).
+constexpr int kBnFewParts = 32;
+inline int64_t bn_rows_per_part(int64_t M, int C) {
+  if (M * C <= (int64_t)1 << 19) return std::max<int64_t>(32, (M + kBnFewParts - 1) / kBnFewParts);
+  return std::max<int64_t>(64, (M + 1023) / 1024);
+}
 
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
                                                             const bf16* __restrict__ z, const float* __restrict__ save,
@@ -548,29 +581,32 @@ void bn_act_fwd(const void* z, const float* ss, const void* res, bool relu, int6
                                                    relu ? 1 : 0, nvec, C, static_cast<bf16*>(y));
 }
 
-int bn_bwd_parts(int64_t M) {
-  const int64_t rpp = bn_rows_per_part(M);
+int bn_bwd_parts(int64_t M, int C) {
+  const int64_t rpp = bn_rows_per_part(M, C);
   return (int)((M + rpp - 1) / rpp);
 }
 
 void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
                    float* part, void* g_out, hipStream_t s) {
-  bn_bwd_reduce_kernel<<<bn_bwd_parts(M), 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(y),
+  bn_bwd_reduce_kernel<<<bn_bwd_parts(M, C), 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(y),
                                                        static_cast<const bf16*>(z), save, relu ? 1 : 0, M, C,
-                                                       bn_rows_per_part(M), part, static_cast<bf16*>(g_out));
+                                                       bn_rows_per_part(M, C), part, static_cast<bf16*>(g_out));
 }
 
 void bn_bwd_apply(const float* part, int nparts, float* scratch, const void* g, const void* z, const float* save,
                   const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s) {
-  reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);  // part[p][0] = sum g, part[p][1] = sum g*zhat
   const int64_t nvec = M * C / 8;
   if (C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0) {
+    const bool few = nparts <= kBnFewParts;  // the apply kernel sums the partials itself
+    if (!few) reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);  // part[p][0] = sum g, [1] = sum g*zhat
     const int rpb = 256 / (C / 8);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((M + rpb * kBnUnroll - 1) / (rpb * kBnUnroll), 2048));
     bn_bwd_apply_col_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save, gamma,
-                                                 dgamma, dbeta, M, C, static_cast<bf16*>(dz));
+                                                 dgamma, dbeta, few ? part : nullptr, nparts, M, C,
+                                                 static_cast<bf16*>(dz));
     return;
   }
+  reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);
   bn_bwd_apply_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save,
                                                      gamma, dgamma, dbeta, M, C, nvec, static_cast<bf16*>(dz));
 }

@@ -269,8 +269,12 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Ten
   kern::conv_fwd_bf16(x.data_ptr(), w_krsc.data_ptr(), w_krsc.stride(0), g, e, stream_of(x));
   if (want_stats) {  // first level of the fixed-order reduction; bn_fwd_train's prepare sums the G groups
     const int tiles = kern::gemm_tiles_m(M);
-    sums = at::empty({kern::reduce_parts_groups(tiles), 2, g.K}, part.options());
-    kern::reduce_parts_l1(part.data_ptr<float>(), tiles, g.K, sums.data_ptr<float>(), stream_of(x));
+    if (tiles <= 64) {
+      sums = part;  // few tiles: the prepare kernel sums the per-tile partials directly (one launch fewer)
+    } else {
+      sums = at::empty({kern::reduce_parts_groups(tiles), 2, g.K}, part.options());
+      kern::reduce_parts_l1(part.data_ptr<float>(), tiles, g.K, sums.data_ptr<float>(), stream_of(x));
+    }
   }
   return {z, sums};
 }
@@ -412,7 +416,7 @@ std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor
   RINGDP_CHECK(C % 8 == 0 && C <= 2048, "bn backward: channels must be a multiple of 8 and <= 2048");
   f32_gpu(dgamma, "bn dweight");
   f32_gpu(dbeta, "bn dbias");
-  const int nparts = kern::bn_bwd_parts(M);
+  const int nparts = kern::bn_bwd_parts(M, (int)C);
   at::Tensor part = at::empty({nparts, 2, C}, gamma.options());
   at::Tensor g = at::empty_like(z);  // dL/d(pre-activation) = the residual branch's gradient
   kern::bn_bwd_reduce(dy.data_ptr(), relu ? y.data_ptr() : nullptr, z.data_ptr(), save.data_ptr<float>(), relu, M,
