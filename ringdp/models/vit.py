@@ -50,12 +50,12 @@ class EncoderBlock(nn.Module):
 
     def forward_rows(self, x, B: int, T: int):  # ringdp path, x [B*T, D] bf16
         att = self.self_attention
-        if fp8_enabled():  # fp8 linears (LinearF's quantised path), autograd sums the residual gradients
-            h = LayerNormF.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+        if fp8_enabled():  # fp8 linears (LinearF's quantised path); residual gradients join in the LN backward
+            h, x = LayerNormFork.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
             qkv = _lin(h, att.in_proj_weight, att.in_proj_bias)
             o = AttentionF.apply(qkv, B, T, self.num_heads)
             x = linear(o, att.out_proj, residual=x)
-            h = LayerNormF.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
+            h, x = LayerNormFork.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
             h = linear(h, self.mlp[0], act=2)
             return linear(h, self.mlp[3], residual=x)
         # bf16: the residual streams' gradients join in the LayerNorm backward kernels (LayerNormFork)

@@ -46,6 +46,10 @@ def cast_weights(ws) -> None:
     progress (see _bf16 / _bf16_t): the backward's data-gradient GEMMs take W^T K-contiguous."""
     ws = [w for w in ws if w.is_cuda and w.dtype == torch.float32 and w.dim() == 2]
     _BF16_WEIGHTS_T.clear()  # the previous step's backward has taken what it needed
+    if ws and _FP8["on"]:  # fp8 linears quantise W / W^T themselves: plain casts only
+        for w, b in zip(ws, C.cast_bf16_multi([w.detach().contiguous() for w in ws])):
+            _BF16_WEIGHTS[id(w)] = b
+        return
     if ws:
         flat = C.cast_bf16_t_multi([w.detach().contiguous() for w in ws])
         for i, w in enumerate(ws):
