@@ -79,10 +79,13 @@ __global__ __launch_bounds__(256) void quant_kernel(const bf16* __restrict__ x, 
 // next call's roll - no separate amax pass over x.
 // colsum != null: also this tile's 64 column sums of x (fp32, over its 64 rows; a fixed-order tree) to
 // colsum[blockIdx.y][cols] - the bias gradient of a linear layer rides on the quantisation of dz.
+// gpre (nullable): the tensor quantised is x * GELU'(gpre) - the GELU backward of an fp8 linear fused into
+// the quantisation of its output gradient (the bf16 dz never reaches memory)
 __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
                                                       const float* __restrict__ amax, uint8_t* __restrict__ out,
                                                       float* __restrict__ scale, uint8_t* __restrict__ out_rm,
-                                                      unsigned* __restrict__ amax_next, float* __restrict__ colsum) {
+                                                      unsigned* __restrict__ amax_next, float* __restrict__ colsum,
+                                                      const bf16* __restrict__ gpre) {
   __shared__ float tile[64][65];
   __shared__ float red[4];
   __shared__ float csum[4][64];
@@ -97,11 +100,19 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
   for (int pass = 0; pass < 2; ++pass) {
     const int r = (t >> 3) + 32 * pass, cv = t & 7;
     const int64_t gr = r0 + r, gc = c0 + cv * 8;
-    bf16x8 v = zero_bf16x8();
-    if (gr < rows && gc < cols) v = *reinterpret_cast<const bf16x8*>(x + gr * cols + gc);
+    bf16x8 v = zero_bf16x8(), pz = zero_bf16x8();
+    if (gr < rows && gc < cols) {
+      v = *reinterpret_cast<const bf16x8*>(x + gr * cols + gc);
+      if (gpre) pz = *reinterpret_cast<const bf16x8*>(gpre + gr * cols + gc);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float f = (float)v[j];
+      float f = (float)v[j];
+      if (gpre) {  // the bf16 dz the unfused path would have stored, then quantised
+        const float z = (float)pz[j];
+        f = (float)(bf16)(f * (0.5f * (1.f + erff(z * 0.70710678118654752f)) +
+                               z * 0.3989422804014327f * __expf(-0.5f * z * z)));
+      }
       bmax = fmaxf(bmax, fabsf(f));
       cs[j] += f;
       tile[r][cv * 8 + j] = fminf(fmaxf(f * inv, -lim), lim);
@@ -257,12 +268,12 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
   } else {
     dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
     quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, amax, static_cast<uint8_t*>(out),
-                                        scale, static_cast<uint8_t*>(out_rowmajor), nullptr, nullptr);
+                                        scale, static_cast<uint8_t*>(out_rowmajor), nullptr, nullptr, nullptr);
   }
 }
 
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
-                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part) {
+                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part, const void* gelu_pre) {
   dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows + 63) / 64));
   if (init)
     fp8_amax(x, rows * cols, hist, s);  // first use of the site: the exact amax of this tensor
@@ -270,7 +281,7 @@ void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist
     amax_roll_kernel<<<1, 1024, 0, s>>>(hist, (int)(grid.x * grid.y));
   quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, hist, static_cast<uint8_t*>(out_t),
                                       scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1),
-                                      colsum_part);
+                                      colsum_part, static_cast<const bf16*>(gelu_pre));
 }
 
 }  // namespace kern

@@ -193,7 +193,8 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
 // rolled from the tile maxima (or, init = first call of a site, measured exactly), then x is quantised
 // (q^T into out_t, q into out_rowmajor) while its tile maxima are written for the next call.
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
-                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part = nullptr);
+                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part = nullptr,
+                          const void* gelu_pre = nullptr);
 // column sums of a bf16 [rows][cols] matrix as colsum_parts(rows) fp32 partial rows (sum them with splitk_sum;
 // fp8_quantize_delayed's colsum_part has one partial row per 64-row tile instead)
 int colsum_parts(int64_t rows);

@@ -725,7 +725,8 @@ int64_t fp8_delayed_slots(int64_t rows, int64_t cols) { return ((rows + 63) / 64
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const at::Tensor& x, at::Tensor hist,
                                                                         bool init,
-                                                                        const c10::optional<at::Tensor>& colsum) {
+                                                                        const c10::optional<at::Tensor>& colsum,
+                                                                        const c10::optional<at::Tensor>& gelu_pre) {
   bf16_gpu(x, "fp8 quantize input");
   RINGDP_CHECK(x.dim() == 2 && x.size(0) % 16 == 0 && x.size(1) % 16 == 0,
                "fp8_quantize_both_delayed: expected a 2-D tensor with dims % 16 == 0");
@@ -741,8 +742,22 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const a
     RINGDP_CHECK(colsum->numel() == Cc && colsum->is_contiguous(), "fp8 quantize colsum: expected [cols] floats");
     part = at::empty({(R + 63) / 64, Cc}, x.options().dtype(at::kFloat));
   }
-  kern::fp8_quantize_delayed(x.data_ptr(), R, Cc, hist.data_ptr<float>(), init, qt.data_ptr(), scale.data_ptr<float>(),
-                             q.data_ptr(), stream_of(x), part.defined() ? part.data_ptr<float>() : nullptr);
+  // gelu_pre: quantise x * GELU'(gelu_pre) (an fp8 linear's GELU backward folded into the pass over its gradient)
+  const void* pre = nullptr;
+  at::Tensor src = x;
+  if (gelu_pre.has_value() && gelu_pre->defined()) {
+    bf16_gpu(*gelu_pre, "fp8 quantize gelu pre-activation");
+    RINGDP_CHECK(gelu_pre->sizes() == x.sizes() && gelu_pre->is_contiguous() && x.is_contiguous(),
+                 "fp8 quantize gelu pre-activation: expected a contiguous tensor of x's shape");
+    if (init) {  // the site's first amax is measured on the finished gradient: materialise it once
+      src = at::empty_like(x);
+      kern::gelu_bwd(x.data_ptr(), gelu_pre->data_ptr(), x.numel(), src.data_ptr(), stream_of(x));
+    } else {
+      pre = gelu_pre->data_ptr();
+    }
+  }
+  kern::fp8_quantize_delayed(src.data_ptr(), R, Cc, hist.data_ptr<float>(), init, qt.data_ptr(), scale.data_ptr<float>(),
+                             q.data_ptr(), stream_of(x), part.defined() ? part.data_ptr<float>() : nullptr, pre);
   if (part.defined())
     kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), Cc, colsum->data_ptr<float>(), stream_of(x));
   return {q, qt, scale};

@@ -162,14 +162,16 @@ class LinearF(torch.autograd.Function):
 _FP8_DELAYED = os.environ.get("RINGDP_FP8_DELAYED", "1") == "1"
 
 
-def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[torch.Tensor] = None):
+def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[torch.Tensor] = None,
+               gelu_pre: Optional[torch.Tensor] = None):
     """fp8 quantisation of an activation (slot 0: the linear's input x), output gradient (slot 1: dz) or
     the bf16 copy of the weight (slot 2) with per-site delayed scaling (TransformerEngine-style, history length 1), state kept on the weight:
     the first quantisation of a site measures its exact amax; later ones scale by the amax the previous
     step measured (values clamped to the e4m3 range) and record the current one inside the same pass,
-    which removes the separate amax pass over the tensor."""
+    which removes the separate amax pass over the tensor.  ``gelu_pre``: quantise ``t * GELU'(gelu_pre)``
+    instead (the GELU backward done inside the quantisation pass)."""
     if not _FP8_DELAYED:
-        return C.fp8_quantize_both(t)
+        return C.fp8_quantize_both(t if gelu_pre is None else C.gelu_bwd(t, gelu_pre))
     sites = getattr(w, "_ringdp_fp8", None)
     if sites is None:
         sites = w._ringdp_fp8 = [None, None, None]
@@ -178,7 +180,7 @@ def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[tor
     init = hist is None or hist.numel() != n
     if init:
         hist = sites[slot] = torch.zeros(n, device=t.device, dtype=torch.float32)
-    return C.fp8_quantize_both_delayed(t, hist, init, colsum)
+    return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre)
 
 
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
@@ -203,11 +205,13 @@ def _linear_fp8_bwd(ctx, dy):
     act, has_res, N = ctx.cfg
     M, K = ctx.shape
     dyb = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
-    dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
     dx = dw = None
     want_db = b is not None and ctx.needs_input_grad[2]
     db = grad_buffer(b) if want_db and _FP8_DELAYED else None  # column sums of dz from the quantisation pass
-    dzq, dztq, sdz = _quant_act(dz, w, 1, db)  # [M][N] for the data grad, [N][M] for the weight grad
+    # dz = dy * GELU'(pre) is formed inside the quantisation pass (delayed scaling) - never stored in bf16
+    fuse = act == 2 and _FP8_DELAYED
+    dz = dyb if act != 2 or fuse else C.gelu_bwd(dyb, pre)
+    dzq, dztq, sdz = _quant_act(dz, w, 1, db, pre if fuse else None)  # [M][N] data grad, [N][M] weight grad
     if ctx.needs_input_grad[0]:
         dx = C.gemm_fp8(dzq, wtq, sdz, sw, M, K, N, True)
     if ctx.needs_input_grad[1]:

@@ -348,6 +348,34 @@ def test_fp8_delayed_scaling():
     torch.testing.assert_close(s3[0], hist[0] / 448.0, rtol=1e-6, atol=0)
 
 
+def test_fp8_delayed_gelu_fused():
+    """fp8 linear backward: quantising dy * GELU'(pre) in one pass equals gelu_bwd followed by the
+    quantisation (same bf16 dz, same scale, same fp8 bytes, same column sums) - first call of the site
+    (materialised) and later ones (fused)."""
+    torch.manual_seed(3)
+    r, c = 320, 768
+    pre = (torch.randn(r, c, device="cuda") * 2).bfloat16()
+    h_ref = torch.zeros(1 + C().fp8_delayed_slots(r, c), device="cuda")
+    h_fus = torch.zeros_like(h_ref)
+    for step in range(3):
+        dy = (torch.randn(r, c, device="cuda") * (1 + step)).bfloat16()
+        dz = C().gelu_bwd(dy, pre)
+        ref32 = (dy.float() * _gelu_grad_ref(pre.float())).double()
+        torch.testing.assert_close(dz.double(), ref32, atol=1e-2, rtol=1e-2)
+        cs_ref = torch.empty(c, device="cuda")
+        cs_fus = torch.empty(c, device="cuda")
+        q0, qt0, s0 = C().fp8_quantize_both_delayed(dz, h_ref, step == 0, cs_ref)
+        q1, qt1, s1 = C().fp8_quantize_both_delayed(dy, h_fus, step == 0, cs_fus, pre)
+        assert torch.equal(s0, s1) and torch.equal(h_ref, h_fus)
+        assert torch.equal(q0, q1) and torch.equal(qt0, qt1)
+        torch.testing.assert_close(cs_fus, cs_ref, atol=1e-4, rtol=1e-5)
+
+
+def _gelu_grad_ref(x):
+    cdf = 0.5 * (1 + torch.erf(x / 2 ** 0.5))
+    return cdf + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+
+
 def test_column_sums():
     """Bias gradients: colsum_f32 and the column sums the delayed fp8 quantisation of dz emits."""
     torch.manual_seed(2)
