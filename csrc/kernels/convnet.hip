@@ -784,7 +784,7 @@ __device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int
 // behind tap t's writes (LDS executes one wave's instructions in order).  Fixed order: deterministic.
 __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
-                                 bf16* __restrict__ dz2, int B, int block, int nblocks) {
+                                 bf16* __restrict__ dz2, int b_first, int b_end, int b_step) {
   bf16* P = reinterpret_cast<bf16*>(smem);
   uint8_t* AM = reinterpret_cast<uint8_t*>(smem + C3D_P);
   float* DA = reinterpret_cast<float*>(smem + C3D_P + C3D_AM);
@@ -847,17 +847,17 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
     for (int j = 0; j < 4; ++j) g[j] = fmaf(d[j], (float)((m >> (8 * j)) & 0xffu), g[j]);
   };
   C3Pre pre;
-  int b = block;
-  if (b < B) pre.load(da3m, idx3, b, tid);
-  for (; b < B; b += nblocks) {
+  int b = b_first;
+  if (b < b_end) pre.load(da3m, idx3, b, tid);
+  for (; b < b_end; b += b_step) {
     __syncthreads();  // previous image fully consumed (P, DA, AM)
     c3_expand(pre, tid, [&](int r) {
       const int w = r >> 2, i = r & 3;
       return P + (2 * (w >> 2) + (i >> 1) + 2) * C3_PY + (2 * (w & 3) + (i & 1) + 2) * C3_PX;
     });
     codes_glds(idx2, b, AM, wave, lane);  // this image's codes land during the MFMA phase
-    const int nb = b + nblocks;
-    if (nb < B) pre.load(da3m, idx3, nb, tid);
+    const int nb = b + b_step;
+    if (nb < b_end) pre.load(da3m, idx3, nb, tid);
     __syncthreads();
     mfma_phase();
     c_dma_wait();
@@ -973,15 +973,23 @@ __global__ __launch_bounds__(256, 2) void conv3_bwd_kernel(const bf16* __restric
                                                            const bf16* __restrict__ packed,
                                                            bf16* __restrict__ dz2, int B,
                                                            float* __restrict__ slabs, int n_wgrad,
-                                                           int n_dgrad) {
+                                                           int n_dgrad, int b_dgrad) {
   __shared__ __attribute__((aligned(16))) char smem[C3B_LDS];
   const int blk = blockIdx.x;
-  if (blk < n_dgrad) {
-    conv3_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, B, blk, n_dgrad);
-  } else {
+  int b_first = blk, b_end = b_dgrad, b_step = n_dgrad;
+  if (blk >= n_dgrad) {
     const int w = blk - n_dgrad;
     conv3_wgrad_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w >> 1, w & 1);
+    // images [b_dgrad, B) of the data gradient go to the wgrad workgroups once their slice is done: a
+    // dgrad workgroup is slower per image than its wgrad neighbour (pool2 backward, barrier phases), so
+    // with one of each per CU the wgrad half would otherwise idle (static split: deterministic)
+    if (dz2 == nullptr || b_dgrad >= B) return;
+    __syncthreads();  // LDS changes role
+    b_first = b_dgrad + w;
+    b_end = B;
+    b_step = 2 * n_wgrad;
   }
+  conv3_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, b_first, b_end, b_step);  // one call site: inlined
 }
 
 __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
@@ -1460,10 +1468,23 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
     ws = clampi(cdiv(B, 8), 1, slots / 2);
     return;
   }
-  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.55);
+  static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.5);
   nd = clampi(B, 1, (int)(frac * slots));
   const int per = cdiv(B, nd);
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, (slots - nd) / 2));  // >= 2 images per slab
+}
+
+// Images [0, result) of the conv3 data gradient run on the dgrad workgroups, the rest on the wgrad
+// workgroups after their weight-gradient slice (RINGDP_C3_STEAL = that share; large batches only, where
+// each dgrad workgroup has many images).
+static int c3_dgrad_images(int B, int nd) {
+  static const double steal = [] {
+    const char* v = getenv("RINGDP_C3_STEAL");
+    const double f = v ? atof(v) : 0.1;
+    return f >= 0.0 && f < 0.9 ? f : 0.1;
+  }();
+  if (nd <= 0 || B < 32 * nd) return B;
+  return B - (int)(steal * B);
 }
 
 static void c2_split(int B, bool dgrad, int& nd, int& ws) {
@@ -1505,7 +1526,7 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
                                    static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B));
   conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
                                            idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
-                                           c3_slabs, ws, nd);
+                                           c3_slabs, ws, nd, c3_dgrad_images(B, nd));
   launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
                  seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
                  seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},
