@@ -108,6 +108,25 @@ def _store_agree(dist, key: str, ok: bool, rank: int, world: int) -> bool:
     return all(st.get(k) == b"1" for k in keys)
 
 
+def _pack_batch(x: torch.Tensor, y: torch.Tensor):
+    """(buffer, x view, y view): copies of x and y in one uint8 buffer (x bytes first, 8-aligned)."""
+    nx = x.numel() * x.element_size()
+    off = (nx + 7) // 8 * 8
+    buf = torch.empty(off + y.numel() * y.element_size(), dtype=torch.uint8, device=x.device)
+    xv = buf[:nx].view(x.dtype).view(x.shape)
+    yv = buf[off:].view(y.dtype).view(y.shape)
+    xv.copy_(x)
+    yv.copy_(y)
+    return buf, xv, yv
+
+
+def _phase(msg: str) -> None:
+    """One stderr line per bench phase (the JSON line stays the only stdout line): a run that stops
+    progressing names the phase it stopped in."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+
 def worker(args):
     # RINGDP_BENCH_STACKS_S=N: dump every thread's Python stack after N seconds (hang diagnosis)
     if os.environ.get("RINGDP_BENCH_STACKS_S"):
@@ -182,8 +201,10 @@ def worker(args):
         g = torch.Generator(device=dev).manual_seed(1000 * rank)
         pool = [(torch.randn((B,) + spec["shape"], device=dev, generator=g),
                  torch.randint(0, ncls, (B,), device=dev, generator=g)) for _ in range(min(args.pool, 4))]
-    static_x = torch.empty_like(pool[0][0])
-    static_y = torch.empty_like(pool[0][1])
+    # Each batch lives in one byte buffer (images, then labels), as a loader's staging buffer would:
+    # feeding the captured step is one device copy per step instead of two.
+    pool = [_pack_batch(x, y) for x, y in pool]
+    static_buf, static_x, static_y = _pack_batch(*pool[0][1:])
 
     def sync():
         if on_gpu:
@@ -229,26 +250,25 @@ def worker(args):
         return None
     capture.n = 0
 
+    _phase(f"model {args.model} dtype {args.dtype} B={B} world={world}: warmup + capture")
     use_graph = on_gpu and not args.no_graph
     graph = None
     n_warm = max(args.warmup, 3)
     if use_graph:
         # eager warmup (bucket rebuild happens at iteration 1), then capture
         for i in range(2):
-            x, y = pool[i % len(pool)]
+            _, x, y = pool[i % len(pool)]
             step_on(x, y)
-        static_x.copy_(pool[0][0])
-        static_y.copy_(pool[0][1])
+        static_buf.copy_(pool[0][0])
         graph = capture()
         use_graph = graph is not None
 
     def run_steps(n, g):
         loss = None
         for i in range(n):
-            x, y = pool[i % len(pool)]
+            buf, x, y = pool[i % len(pool)]
             if g is not None:
-                static_x.copy_(x, non_blocking=True)
-                static_y.copy_(y, non_blocking=True)
+                static_buf.copy_(buf, non_blocking=True)
                 loss = g.replay()
             else:
                 loss = step_on(x, y)
@@ -269,6 +289,7 @@ def worker(args):
         return float(t.item()), loss
 
     run_steps(n_warm, graph)
+    _phase(f"timed region: {args.steps} steps")
     elapsed_max, loss = timed(args.steps, graph)
     final_loss = float(loss.item()) if loss is not None else float("nan")
     ms_per_step = 1000.0 * elapsed_max / args.steps
@@ -281,13 +302,84 @@ def worker(args):
     nat = ddp._native_pg
     stats = ddp.reducer.stats()
     comm_stats = {"bucket_bytes": [int(s.bytes) for s in stats]}
+    def emit(comm_stats, text_only=False):
+        n_buckets = len(ddp.reducer.bucket_indices())
+        sizes_kb = ",".join(f"{b / 1024:.0f}" for b in comm_stats["bucket_bytes"])
+        lib = "RCCL" if on_gpu else "host ring (gloo)"
+        if world > 1:
+            comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
+                    f"cap {args.bucket_mb} MB" + (", side HIP stream overlapped with backward" if on_gpu else ""))
+        elif force_comm:
+            where = ("on the compute stream (a one-rank collective has nothing to overlap)"
+                     if getattr(nat, "same_stream", lambda: False)() else "on the side stream")
+            comm = (f"{lib} {args.comm_hook} (avg) over 1 rank, forced so N=1 runs the reducer + collective "
+                    f"path of N>1, {where}; {n_buckets} bucket(s) [{sizes_kb}] KB, cap {args.bucket_mb} MB")
+        else:
+            comm = "none (world_size 1, --no-force-comm)"
+        if rank == 0:
+            metric = METRIC if args.model == "convnet" else \
+                f"images/sec (whole node) {args.model} synthetic DDP training at 1/2/4/8 MI355X"
+            if not on_gpu:
+                data = "synthetic (host uint8 MNIST-shaped images + labels; random-init weights; CPU plumbing run)"
+            elif args.model == "convnet":
+                data = "synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)"
+            else:
+                data = f"synthetic (on-device N(0,1) {spec['shape']} images + labels; random-init weights)"
+            dtype = {"bf16": "bf16", "fp32": "fp32", "fp8": "fp8 (e4m3 linear GEMMs, bf16 attention/norms)"}[args.dtype]
+            if not on_gpu:
+                dtype = "fp32 (CPU ATen)"
+            res = {
+                "metric": metric,
+                "value": round(value, 1),
+                "unit": "images/sec",
+                "n_gpus": world,
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "ms_per_step": round(ms_per_step, 4),
+                "higher_is_better": True,
+                "scaling": "weak",
+                "vs_baseline": None,
+                "dtype": dtype,
+                "data": data,
+                "config": {
+                    "model": spec["desc"],
+                    "global_batch": B * world,
+                    "per_rank_batch": B,
+                    "seq_len": None,
+                    "image_shape": list(spec["shape"]),
+                    "parallelism": f"dp{world}",
+                    "optimizer": f"SGD lr={lr} momentum={spec['momentum']} nesterov={spec['nesterov']} wd={spec['wd']}",
+                    "comm": comm,
+                    "comm_world_size": int(nat.size()),
+                    "comm_backend": nat.backend_name(),
+                    "hipgraph": use_graph,
+                    "master_weights": "fp32",
+                    "device": "cpu" if not on_gpu else torch.cuda.get_device_properties(dev).gcnArchName,
+                },
+                "comm_stats": comm_stats,
+                "final_loss": round(final_loss, 5),
+            }
+            if text_only:
+                return json.dumps(res)
+            print(json.dumps(res), flush=True)
+
+    # The headline number is already measured: should the comm-statistics phase below stop making
+    # progress, a native timer writes the result line without those statistics and ends the rank
+    # (every rank arms one; only rank 0's carries the line).
+    guard_s = 90.0 + 40.0 * args.comm_stats_steps * ms_per_step / 1000.0
+    partial = dict(comm_stats, incomplete=f"comm-statistics phase exceeded {guard_s:.0f} s; statistics omitted")
+    line = emit(partial, text_only=True)
+    sys.stdout.flush()
+    if on_gpu:
+        C.exit_guard_arm(guard_s, line + "\n" if line else "")
     if args.comm_stats_steps > 0 and (world > 1 or force_comm):
         S = args.comm_stats_steps
         per_bucket = [[] for _ in stats]
+        _phase("comm stats: per-bucket timing")
         if hasattr(nat, "set_timing"):
             nat.set_timing(True)
             for i in range(S):
-                x, y = pool[i % len(pool)]
+                _, x, y = pool[i % len(pool)]
                 step_on(x, y)
                 sync()
                 for b, d in enumerate(ddp.reducer.collect_comm_times()):
@@ -297,9 +389,11 @@ def worker(args):
             comm_stats["bucket_comm_us"] = [round(sum(v) / len(v), 1) if v else None for v in per_bucket]
             comm_stats["bucket_comm_us_method"] = f"device events around each bucket collective on the comm stream, mean of {S} eager steps"
         # step time without any gradient collective (same graph otherwise): exposed comm estimate
+        _phase("comm stats: capture without collectives")
         hook = ddp.reducer.comm_hook()
         ddp.reducer.set_comm_hook(C.CommHook.NONE)
         g2 = capture() if use_graph else None
+        _phase("comm stats: interleaved with/without timings")
         ddp.reducer.set_comm_hook(hook)
         # interleave the two variants (with / without collectives) so clock drift cancels
         t_c, t_n = [], []
@@ -318,63 +412,9 @@ def worker(args):
         comm_stats["exposed_comm_method"] = (f"best of 3 interleaved {S}-step timings of the same {'graph' if use_graph else 'eager step'} "
                                              f"with and without the bucket collectives (max over ranks)")
 
-    n_buckets = len(ddp.reducer.bucket_indices())
-    sizes_kb = ",".join(f"{b / 1024:.0f}" for b in comm_stats["bucket_bytes"])
-    lib = "RCCL" if on_gpu else "host ring (gloo)"
-    if world > 1:
-        comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
-                f"cap {args.bucket_mb} MB" + (", side HIP stream overlapped with backward" if on_gpu else ""))
-    elif force_comm:
-        where = ("on the compute stream (a one-rank collective has nothing to overlap)"
-                 if getattr(nat, "same_stream", lambda: False)() else "on the side stream")
-        comm = (f"{lib} {args.comm_hook} (avg) over 1 rank, forced so N=1 runs the reducer + collective "
-                f"path of N>1, {where}; {n_buckets} bucket(s) [{sizes_kb}] KB, cap {args.bucket_mb} MB")
-    else:
-        comm = "none (world_size 1, --no-force-comm)"
-    if rank == 0:
-        metric = METRIC if args.model == "convnet" else \
-            f"images/sec (whole node) {args.model} synthetic DDP training at 1/2/4/8 MI355X"
-        if not on_gpu:
-            data = "synthetic (host uint8 MNIST-shaped images + labels; random-init weights; CPU plumbing run)"
-        elif args.model == "convnet":
-            data = "synthetic (on-device uint8 MNIST-shaped images + labels; random-init weights)"
-        else:
-            data = f"synthetic (on-device N(0,1) {spec['shape']} images + labels; random-init weights)"
-        dtype = {"bf16": "bf16", "fp32": "fp32", "fp8": "fp8 (e4m3 linear GEMMs, bf16 attention/norms)"}[args.dtype]
-        if not on_gpu:
-            dtype = "fp32 (CPU ATen)"
-        res = {
-            "metric": metric,
-            "value": round(value, 1),
-            "unit": "images/sec",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": dtype,
-            "data": data,
-            "config": {
-                "model": spec["desc"],
-                "global_batch": B * world,
-                "per_rank_batch": B,
-                "seq_len": None,
-                "image_shape": list(spec["shape"]),
-                "parallelism": f"dp{world}",
-                "optimizer": f"SGD lr={lr} momentum={spec['momentum']} nesterov={spec['nesterov']} wd={spec['wd']}",
-                "comm": comm,
-                "comm_world_size": int(nat.size()),
-                "comm_backend": nat.backend_name(),
-                "hipgraph": use_graph,
-                "master_weights": "fp32",
-                "device": "cpu" if not on_gpu else torch.cuda.get_device_properties(dev).gcnArchName,
-            },
-            "comm_stats": comm_stats,
-            "final_loss": round(final_loss, 5),
-        }
-        print(json.dumps(res), flush=True)
+    if on_gpu:
+        C.exit_guard_cancel()
+    emit(comm_stats)
     dist.destroy_process_group()
 
 

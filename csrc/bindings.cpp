@@ -14,6 +14,13 @@
 #include "store/store.h"
 #include "trace/trace.h"
 
+#include <unistd.h>
+
+#include <condition_variable>
+#include <cstdio>
+#include <mutex>
+#include <thread>
+
 namespace py = pybind11;
 using namespace ringdp;
 
@@ -284,6 +291,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("timeout_ms") = 1800000,
            py::arg("bind_hint") = "127.0.0.1");
 
+  py::class_<ReplayBeacon, std::shared_ptr<ReplayBeacon>>(m, "ReplayBeacon")
+      .def(py::init<int>(), py::arg("device"))
+      .def("mark", [](ReplayBeacon& b, uint64_t stream) { b.mark(reinterpret_cast<hipStream_t>(stream)); },
+           py::arg("stream"), "enqueue the completion marker (inside the capture, after the step)")
+      .def("issued", &ReplayBeacon::issued)
+      .def("issued_count", &ReplayBeacon::issued_count)
+      .def("completed", &ReplayBeacon::completed)
+      .def_property_readonly("device", &ReplayBeacon::device);
   py::class_<RcclPG, ProcessGroup, std::shared_ptr<RcclPG>>(m, "RcclPG")
       .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int device,
                        int64_t timeout_ms) {
@@ -300,16 +315,54 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("p2p_max_bytes", &RcclPG::p2p_max_bytes)
       .def("same_stream", &RcclPG::same_stream)
       .def("set_p2p_enabled", &RcclPG::set_p2p_enabled)
-      .def("watch_stream",
-           [](RcclPG& pg, uint64_t stream) {
-             pg.watch_stream(reinterpret_cast<hipStream_t>(stream), OpType::GRAPH_REPLAY);
-           },
-           py::arg("stream"),
-           "watchdog-track the work queued so far on a raw hipStream_t (e.g. a graph replay)")
+      .def("watch_beacon", &RcclPG::watch_beacon, py::arg("beacon"),
+           "watchdog-track the replays of a captured step through its ReplayBeacon")
       .def("timing", &RcclPG::timing)
       .def("set_async_error_handling", &RcclPG::set_async_error_handling)
       .def("comm_stream_ptr",
            [](RcclPG& pg) { return reinterpret_cast<uintptr_t>(pg.comm_stream()); });
+
+  // Exit guard (bench.py): a native thread that, unless cancelled within `seconds`, writes `text` to
+  // stdout and ends the process with status 0.  Native, so it fires even while the main thread is
+  // stuck inside a call that holds the GIL.
+  {
+    struct Guard {
+      std::mutex mu;
+      std::condition_variable cv;
+      bool cancelled = false;
+    };
+    static std::shared_ptr<Guard> guard;
+    m.def(
+        "exit_guard_arm",
+        [](double seconds, std::string text) {
+          auto g = std::make_shared<Guard>();
+          guard = g;
+          std::thread([g, seconds, text = std::move(text)] {
+            std::unique_lock<std::mutex> lk(g->mu);
+            if (g->cv.wait_for(lk, std::chrono::duration<double>(seconds), [&] { return g->cancelled; })) return;
+            if (!text.empty()) {
+              ssize_t off = 0;
+              while (off < (ssize_t)text.size()) {
+                const ssize_t n = ::write(1, text.data() + off, text.size() - off);
+                if (n <= 0) break;
+                off += n;
+              }
+            }
+            std::fflush(stderr);
+            std::_Exit(0);
+          }).detach();
+        },
+        py::arg("seconds"), py::arg("text"));
+    m.def("exit_guard_cancel", []() {
+      if (!guard) return;
+      {
+        std::lock_guard<std::mutex> lk(guard->mu);
+        guard->cancelled = true;
+      }
+      guard->cv.notify_all();
+      guard.reset();
+    });
+  }
 
   m.def("rccl_version", []() {
     int v = 0;

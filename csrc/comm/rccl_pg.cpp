@@ -1,6 +1,8 @@
 // RCCL process group implementation (see rccl_pg.h).
 #include "rccl_pg.h"
 
+#include "../kernels/kernels.h"
+
 #include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
@@ -116,6 +118,31 @@ double RcclWork::duration_us() {
   return static_cast<double>(ms) * 1000.0;
 }
 
+// ------------------------------------------------------------------ ReplayBeacon
+ReplayBeacon::ReplayBeacon(int device) : device_(device) {
+  DeviceScope ds(device_);
+  RINGDP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_), sizeof(*host_),
+                                 hipHostMallocCoherent | hipHostMallocMapped));
+  *host_ = 0;
+  RINGDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev_), sizeof(*dev_)));
+  RINGDP_HIP_CHECK(hipMemset(dev_, 0, sizeof(*dev_)));
+  RINGDP_HIP_CHECK(hipDeviceSynchronize());
+}
+
+ReplayBeacon::~ReplayBeacon() {
+  DeviceScope ds(device_);
+  (void)hipDeviceSynchronize();  // no replay may still write the counters
+  if (dev_) (void)hipFree(dev_);
+  if (host_) (void)hipHostFree(host_);
+}
+
+void ReplayBeacon::mark(hipStream_t stream) {
+  unsigned long long* hdev = nullptr;
+  RINGDP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), host_, 0));
+  kern::replay_beacon_mark(dev_, hdev, stream);
+  RINGDP_HIP_CHECK(hipGetLastError());
+}
+
 // ------------------------------------------------------------------ RcclPG
 RcclPG::RcclPG(std::shared_ptr<Store> store, int rank, int size, int device,
                std::chrono::milliseconds timeout)
@@ -206,14 +233,11 @@ void RcclPG::drain() {
   inflight_.clear();
 }
 
-void RcclPG::watch_stream(hipStream_t stream, OpType what) {
-  if (stop_.load() || aborted_.load()) return;
-  DeviceScope ds(device_);
-  auto work = std::make_shared<RcclWork>(what, next_seq(), this, /*captured=*/false, /*timing=*/false);
-  RINGDP_HIP_CHECK(hipEventRecord(work->done_, stream));
-  work->deadline_us_ = now_us() + timeout_.count() * 1000;
-  std::lock_guard<std::mutex> wl(wd_mu_);
-  inflight_.push_back(std::move(work));
+void RcclPG::watch_beacon(const std::shared_ptr<ReplayBeacon>& beacon) {
+  std::lock_guard<std::mutex> bl(beacon_mu_);
+  beacon->last_done_ = beacon->completed();
+  beacon->progress_us_ = now_us();
+  beacons_.push_back(beacon);
 }
 
 void RcclPG::abort() {
@@ -268,6 +292,29 @@ void RcclPG::watchdog_loop() {
         // Entries are queued in issue order with deadlines in the same order: an incomplete
         // head that is within its deadline means everything behind it is too.
         break;
+      }
+    }
+    if (failure.empty()) {
+      // captured steps: plain loads of the replay beacons (no HIP call on this thread)
+      std::lock_guard<std::mutex> bl(beacon_mu_);
+      const int64_t now = now_us();
+      for (auto it = beacons_.begin(); it != beacons_.end();) {
+        auto b = it->lock();
+        if (!b) {
+          it = beacons_.erase(it);
+          continue;
+        }
+        const uint64_t done = b->completed(), issued = b->issued_count();
+        if (done >= issued || done != b->last_done_) {
+          b->last_done_ = done;
+          b->progress_us_ = now;  // idle, or a replay finished since the last look
+        } else if (now - b->progress_us_ > timeout_.count() * 1000) {
+          failure = strcat_all("[ringdp] watchdog: rank ", rank_, " ", op_name(OpType::GRAPH_REPLAY), " ",
+                               done + 1, " of ", issued, " did not complete within ", timeout_.count(),
+                               " ms; aborting communicator");
+          break;
+        }
+        ++it;
       }
     }
     if (failure.empty() && p2p_ && p2p_->failed()) {

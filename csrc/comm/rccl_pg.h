@@ -23,6 +23,36 @@ using HipStream = c10::hip::HIPStreamMasqueradingAsCUDA;
 
 class RcclPG;
 
+// Completion beacon of a captured step (hipGraph).  The graph's last node (kern::replay_beacon_mark)
+// writes the number of finished replays into host-coherent memory; the host counts replays it
+// issued.  The watchdog compares the two with plain loads: watching a replay costs no HIP call on
+// either thread (an event created + recorded per replay and queried/destroyed by the watchdog thread
+// deadlocked inside the HIP runtime, ~1 in 3 ViT bench runs).
+class ReplayBeacon {
+ public:
+  explicit ReplayBeacon(int device);
+  ~ReplayBeacon();
+  ReplayBeacon(const ReplayBeacon&) = delete;
+  ReplayBeacon& operator=(const ReplayBeacon&) = delete;
+  // Enqueue the marker on `stream` (call while capturing, after the step).
+  void mark(hipStream_t stream);
+  // The host issued one more replay.
+  void issued() { issued_.fetch_add(1, std::memory_order_relaxed); }
+  uint64_t issued_count() const { return issued_.load(std::memory_order_relaxed); }
+  uint64_t completed() const { return __atomic_load_n(host_, __ATOMIC_ACQUIRE); }
+  int device() const { return device_; }
+
+  // watchdog bookkeeping (watchdog thread only)
+  uint64_t last_done_ = 0;
+  int64_t progress_us_ = 0;
+
+ private:
+  int device_;
+  unsigned long long* host_ = nullptr;  // hipHostMalloc'd, coherent + mapped
+  unsigned long long* dev_ = nullptr;   // device counter
+  std::atomic<uint64_t> issued_{0};
+};
+
 class RcclWork : public Work {
  public:
   RcclWork(OpType op, uint64_t seq, RcclPG* pg, bool captured, bool timing);
@@ -82,11 +112,11 @@ class RcclPG : public ProcessGroup {
   // Host-blocks until every eagerly issued op has completed and clears the watchdog list, so
   // no event query can race a subsequent hipGraph capture.
   void drain();
-  // Puts the work queued so far on `stream` (e.g. a hipGraph replay whose captured collectives
-  // the per-op watchdog entries cannot see) under this group's watchdog: an event recorded on
-  // the stream must complete within the group timeout, else the communicator is aborted and the
-  // process exits non-zero like any other hung collective.
-  void watch_stream(hipStream_t stream, OpType what);
+  // Puts the replays of a captured step (whose collectives the per-op watchdog entries cannot see)
+  // under this group's watchdog: while replays are outstanding, one must complete within the group
+  // timeout, else the communicator is aborted and the process exits non-zero like any other hung
+  // collective.
+  void watch_beacon(const std::shared_ptr<ReplayBeacon>& beacon);
   bool aborted() const { return aborted_.load(); }
   std::string error_message() {
     std::lock_guard<std::mutex> lk(wd_mu_);
@@ -127,6 +157,8 @@ class RcclPG : public ProcessGroup {
   std::mutex wd_mu_;
   std::condition_variable wd_cv_;
   std::deque<std::shared_ptr<RcclWork>> inflight_;
+  std::mutex beacon_mu_;
+  std::vector<std::weak_ptr<ReplayBeacon>> beacons_;
   std::thread watchdog_;
   std::atomic<bool> stop_{false};
   std::atomic<bool> aborted_{false};

@@ -462,6 +462,20 @@ void cross_entropy_bwd(const float* logits, const int64_t* labels, const float* 
                                                        dlogits);
 }
 
+// Replay beacon: the last node of a captured step bumps a device counter and stores the new value
+// (one vector store, system scope) into host-coherent memory, where the RCCL watchdog thread reads it
+// without any HIP call.
+__global__ void beacon_kernel(unsigned long long* __restrict__ dev_ctr, unsigned long long* host) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long v = __hip_atomic_load(dev_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1ull;  // vector load
+  __hip_atomic_store(dev_ctr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(host, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void replay_beacon_mark(unsigned long long* dev_ctr, unsigned long long* host, hipStream_t s) {
+  beacon_kernel<<<1, 64, 0, s>>>(dev_ctr, host);
+}
+
 void synth_u8_images(uint8_t* x, int64_t* labels, int B, int HW, int num_classes, uint64_t seed,
                      hipStream_t s) {
   const int64_t n = (int64_t)B * HW;

@@ -27,6 +27,8 @@ struct SgdArgs {
   const float* lr_ptr;    // optional device-resident lr (overrides `lr`; graph-capture friendly)
   const float* grad_scale_ptr;  // optional device scalar: grad *= 1/(*grad_scale_ptr)
 };
+// Graph-replay beacon (RcclPG watchdog): ++*dev_ctr, then the new value -> *host (host-coherent).
+void replay_beacon_mark(unsigned long long* dev_ctr, unsigned long long* host, hipStream_t s);
 // One kernel over a flat fp32 range (params / grads / momentum laid out identically).
 void sgd_flat(float* p, const float* g, float* m, int64_t n, const SgdArgs& a, hipStream_t s);
 // Multi-tensor: device table of {p, g, m, n} + chunk list {tensor, start}; one launch.

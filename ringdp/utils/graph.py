@@ -18,6 +18,9 @@ from typing import Callable, List, Optional
 import torch
 
 from .. import distributed as dist
+from .._native import C
+
+ReplayBeacon = getattr(C, "ReplayBeacon", None)
 
 
 def drain_comms():
@@ -37,17 +40,20 @@ class StepGraph:
     """Capture/replay of one training step.
 
     Watchdog: collectives inside a replay are invisible to the per-op RCCL watchdog (they were
-    issued once, at capture).  Each ``replay()`` therefore hands the replay's completion to every
-    RCCL group's watchdog (``RcclPG.watch_stream``): a replay that does not finish within the group
-    timeout - e.g. a peer died mid-step - aborts the communicator and exits non-zero, as a hung
-    eager collective does.  ``RINGDP_GRAPH_WATCHDOG=0`` turns this off."""
+    issued once, at capture).  The captured step therefore ends with a beacon node
+    (``ReplayBeacon``: a one-thread kernel that writes the count of finished replays into
+    host-coherent memory) and ``replay()`` counts issued replays; every RCCL group's watchdog
+    compares the two with plain loads (``RcclPG.watch_beacon``).  While replays are outstanding
+    and none finishes within the group timeout - e.g. a peer died mid-step - the communicator is
+    aborted and the process exits non-zero, as for a hung eager collective.  No HIP call is made
+    per replay on either thread.  ``RINGDP_GRAPH_WATCHDOG=0`` turns this off."""
 
     def __init__(self, step_fn: Callable[[], Optional[torch.Tensor]], warmup: int = 3):
         self.step_fn = step_fn
         self.warmup = warmup
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.output = None
-        self._watch: List = []
+        self._beacon = None
 
     def capture(self):
         s = torch.cuda.Stream()
@@ -62,23 +68,28 @@ class StepGraph:
         dump = os.environ.get("RINGDP_GRAPH_DUMP")  # DOT file of the captured nodes (diagnostics)
         if dump:
             self.graph.enable_debug_mode()
+        dev = torch.cuda.current_device()
+        watch = []
+        if os.environ.get("RINGDP_GRAPH_WATCHDOG", "1") != "0":
+            watch = [pg for pg in _rccl_groups() if pg.device == dev]
+        beacon = ReplayBeacon(dev) if watch else None
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             out = self.step_fn()
+            if beacon is not None:
+                beacon.mark(torch.cuda.current_stream().cuda_stream)
         if dump:
             self.graph.debug_dump(dump)
         # keep only the value: a live autograd graph would pin AccumulateGrad nodes created on the
         # capture stream and make later eager steps on another stream synchronise against them
         self.output = out.detach() if torch.is_tensor(out) else out
         torch.cuda.synchronize()
-        if os.environ.get("RINGDP_GRAPH_WATCHDOG", "1") != "0":
-            dev = torch.cuda.current_device()
-            self._watch = [pg for pg in _rccl_groups() if pg.device == dev]
+        for pg in watch:
+            pg.watch_beacon(beacon)
+        self._beacon = beacon
         return self
 
     def replay(self):
         self.graph.replay()
-        if self._watch:
-            s = torch.cuda.current_stream().cuda_stream
-            for pg in self._watch:
-                pg.watch_stream(s)
+        if self._beacon is not None:
+            self._beacon.issued()
         return self.output

@@ -1,5 +1,5 @@
 """One rank whose captured step stalls longer than the process-group timeout: the replay watchdog
-(ringdp.utils.graph.StepGraph -> RcclPG.watch_stream) must abort the communicator and end the
+(ringdp.utils.graph.StepGraph -> ReplayBeacon + RcclPG.watch_beacon) must abort the communicator and end the
 process non-zero.  The stall is a bounded spin kernel (torch.cuda._sleep) captured into the graph,
 so nothing on the GPU ever waits forever.  Run by tests/test_watchdog_gpu.py through ringdp.run."""
 import datetime
