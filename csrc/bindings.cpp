@@ -566,5 +566,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd);
   m.def("cn_conv2_bwd", &ops::cn_conv2_bwd);
   m.def("cn_conv1_wgrad", &ops::cn_conv1_wgrad);
+  m.def("cn_conv12_bwd", &ops::cn_conv12_bwd);
   m.def("synth_u8_images", &ops::synth_u8_images);
 }

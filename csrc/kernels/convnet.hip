@@ -1311,6 +1311,215 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict
   }
 }
 
+// ================================================================== F2 backward + F1 wgrad, fused
+// The conv2 data gradient of an image (da1, 13x13x32) has exactly one consumer: conv1's weight gradient.
+// The dgrad workgroups therefore keep da1 in LDS and run conv1 wgrad on it right away (the input image
+// and its pool1 codes arrive by register load / LDS-DMA while conv2 dgrad computes): da1 never goes to
+// HBM (2 x 354 MB per step at B=32768), and conv1 wgrad + its reduction are no longer launches of their
+// own.  Each dgrad workgroup leaves one conv1 slab (C1_WSLAB), reduced with conv2's slabs in one launch.
+// conv1 part: the 8 waves split K (rows oh = wave mod 8; dy = wave & 1 stays fixed per wave) and cover
+// all 2x2 output tiles, as conv1_wgrad_kernel does with 4 waves.
+constexpr int C12_O = 172 * C2_ORS * 2;             // 13760: da1 [169 + 3 zero windows][32 (+8 pad)] bf16
+constexpr int C12_XS = 5 * C1W_CS * 2;              // 15200: 5 shifted copies of the input image
+// P | O[2] | xs[2] | codes[2]: image i uses buffer set i & 1, so conv1 wgrad of image i-1 runs interleaved
+// with conv2 dgrad of image i (2 waves per SIMD: the MFMA stream of one hides the LDS/VALU of the other)
+constexpr int C12_OFF_O = C2D_P, C12_OFF_X = C12_OFF_O + 2 * C12_O, C12_OFF_C = C12_OFF_X + 2 * C12_XS;
+constexpr int C12_LDS = C12_OFF_C + 2 * C1I_IMG;    // 103632
+constexpr int C12B_LDS = C12_LDS > (C2W_D + C2W_X) ? C12_LDS : (C2W_D + C2W_X);
+static_assert(C2D_P % 16 == 0 && C12_O % 16 == 0 && C12_XS % 16 == 0, "16-B aligned LDS buffers");
+static_assert(8 * 4 * 64 * 4 * 4 <= C12_OFF_X, "conv1 cross-wave reduction fits in P + O");
+
+template <bool U8>
+__device__ void conv12_dgrad_role(char* smem, const void* __restrict__ xin, const uint8_t* __restrict__ idx1,
+                                  const bf16* __restrict__ dz2, const bf16* __restrict__ packed, int B, int block,
+                                  int nblocks, float mean, float inv_std, float in_scale,
+                                  float* __restrict__ slabs1) {
+  bf16* P = reinterpret_cast<bf16*>(smem);
+  auto Obuf = [&](int k) { return reinterpret_cast<bf16*>(smem + C12_OFF_O + k * C12_O); };
+  auto Xbuf = [&](int k) { return reinterpret_cast<bf16*>(smem + C12_OFF_X + k * C12_XS); };
+  auto Cbuf = [&](int k) { return reinterpret_cast<uint8_t*>(smem + C12_OFF_C + k * C1I_IMG); };
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // ---- conv2 dgrad operands (as conv2_dgrad_role)
+  const int nt = wave & 1, mg = wave >> 1;
+  const int r16 = lane & 15, q8 = (lane >> 4) * 8;
+  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P2D_OFF);
+  bf16x8 bw[18];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) bw[ks] = pk[(nt * 18 + ks) * 64 + lane];
+  int base[3];
+  int opos[3][4];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int mt = min(mg + 4 * k, 10);
+    const int mm = c2d_tile_pos[mt * 16 + r16] == 255 ? 0 : c2d_tile_pos[mt * 16 + r16];
+    base[k] = (mm / 13) * C2_PW + mm % 13;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) opos[k][i] = c2d_tile_pos[mt * 16 + (lane >> 4) * 4 + i];
+  }
+  // ---- conv1 wgrad operands (as conv1_wgrad_kernel)
+  const int i16 = lane & 15, g = lane >> 4, q = i16 >> 2, p = i16 & 3;
+  const int t1 = 16 + i16;
+  const int xoff0 = (i16 % 5) * C1W_CS + (i16 / 5) * C1W_RS + 8 * g;
+  const int xoff1 = t1 < 25 ? (t1 % 5) * C1W_CS + (t1 / 5) * C1W_RS + 8 * g : 0;
+  const uint32_t b1fill = t1 == 25 ? 0x3f803f80u : 0u;
+  const int dy = wave & 1;
+  f32x4 acc1[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) acc1[m][0] = acc1[m][1] = zero_f32x4();
+  // zero P (its ring stays zero), both O (windows 169..171 stay zero) and both copy sets (ring stays zero)
+  for (int c = tid; c < C12_OFF_C / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
+  // next image, staged in registers: dz2 rows, input pixels, pool1 code rows
+  bf16x8 pz[2];
+  uint4 pc = make_uint4(0, 0, 0, 0);
+  uint32_t xu = 0;
+  float4 xf = make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load = [&](int bb) {
+    const bf16x8* src = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
+    pz[0] = src[tid];
+    if (tid + 512 < 968) pz[1] = src[tid + 512];
+    if (tid < C1I_IMG / 16) pc = reinterpret_cast<const uint4*>(idx1 + (int64_t)bb * C1I_IMG)[tid];
+    c1_load<U8>(xin, bb, tid, xu, xf);
+  };
+  auto stage = [&](int k) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 512 * j;
+      if (c < 968) {
+        const int pos = c >> 3, cc = (c & 7) * 8;
+        *reinterpret_cast<bf16x8*>(P + ((pos / 11 + 2) * C2_PW + pos % 11 + 2) * C2_PRS + cc) = pz[j];
+      }
+    }
+    if (tid < C1I_IMG / 16) reinterpret_cast<uint4*>(Cbuf(k))[tid] = pc;
+    c1_store<U8, 5, C1W_RS, C1W_CS>(Xbuf(k), tid, xu, xf, mean, inv_std, in_scale);
+  };
+  // conv1 wgrad k-step j (rows oh = wave + 8j; j = 3 only for waves 0, 1) of the image in buffer set k
+  auto c1_step = [&](int j, int k) {
+    const int ks0 = wave + 8 * j;
+    const bool ok = ks0 < 26;  // wave-uniform
+    const int ks = ok ? ks0 : 0;
+    const int py = ks >> 1;
+    const bf16* O = Obuf(k);
+    const bf16* xs = Xbuf(k);
+    const uint8_t* CB = Cbuf(k);
+    bf16x8 A[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const uint2 d = __builtin_bit_cast(uint2, lds_read_tr16(O + (py * 13 + 4 * g + q) * C2_ORS + m * 16 + 4 * p));
+      const int co = m * 16 + i16;
+      const uint2 cu = *reinterpret_cast<const uint2*>(CB + py * 512 + (co >> 1) * 32 + 8 * g);
+      const int csh = 8 * (co & 1) + 2 * dy;
+      uint32_t pr[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t dv = e & 1 ? (e < 2 ? d.x : d.y) >> 16 : (e < 2 ? d.x : d.y) & 0xffffu;
+        const uint32_t sel = __builtin_amdgcn_ubfe(e < 2 ? cu.x : cu.y, 16 * (e & 1) + csh, 2);
+        pr[e] = ok ? dv * ((sel * 0x8001u) & 0x10001u) : 0u;
+      }
+      A[m] = __builtin_bit_cast(bf16x8, make_uint4(pr[0], pr[1], pr[2], pr[3]));
+    }
+    const bf16x8 B0 = *reinterpret_cast<const bf16x8*>(xs + xoff0 + ks * C1W_RS);
+    bf16x8 B1 = *reinterpret_cast<const bf16x8*>(xs + xoff1 + ks * C1W_RS);
+    if (t1 >= 25) B1 = __builtin_bit_cast(bf16x8, make_uint4(b1fill, b1fill, b1fill, b1fill));
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      acc1[m][0] = mfma16x16x32(A[m], B0, acc1[m][0]);
+      acc1[m][1] = mfma16x16x32(A[m], B1, acc1[m][1]);
+    }
+  };
+  // conv2 dgrad of the image staged in P -> O[k]; with C1 set, conv1 k-steps of buffer set k ^ 1 are
+  // issued between its k-steps (after dgrad k-steps 3, 7, 11, 15)
+  auto phase = [&](auto nk_c, auto c1_c, int k) {
+    constexpr int NK = decltype(nk_c)::value;
+    constexpr bool C1 = decltype(c1_c)::value;
+    f32x4 acc[NK];
+#pragma unroll
+    for (int m = 0; m < NK; ++m) acc[m] = zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int tapp = ks >> 1, c0 = (ks & 1) * 32;
+      const int shift = (tapp / 3) * C2_PW + tapp % 3;
+#pragma unroll
+      for (int m = 0; m < NK; ++m)
+        acc[m] = mfma16x16x32(*reinterpret_cast<const bf16x8*>(P + (base[m] + shift) * C2_PRS + c0 + q8), bw[ks],
+                              acc[m]);
+      if (C1 && (ks & 3) == 3 && ks < 16) c1_step(ks >> 2, k ^ 1);
+    }
+    bf16* O = Obuf(k);
+#pragma unroll
+    for (int m = 0; m < NK; ++m) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pos = opos[m][i];
+        if (pos < 169) O[pos * C2_ORS + nt * 16 + r16] = (bf16)acc[m][i];
+      }
+    }
+  };
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using T = std::true_type;
+  using Fa = std::false_type;
+  __syncthreads();  // zero fill done
+  int b = block, k = 0;
+  if (b < B) load(b);
+  for (int i = 0; b < B; ++i, b += nblocks, k ^= 1) {
+    __syncthreads();  // readers of P and of buffer set k (image i-2) are done
+    stage(k);
+    const int nb = b + nblocks;
+    if (nb < B) load(nb);
+    __syncthreads();  // image i staged; O[k ^ 1] (image i-1's da1) complete
+    if (i == 0) {
+      if (mg < 3) phase(I3{}, Fa{}, k);
+      else phase(I2{}, Fa{}, k);
+    } else {
+      if (mg < 3) phase(I3{}, T{}, k);
+      else phase(I2{}, T{}, k);
+    }
+  }
+  __syncthreads();
+  if (b != block) {  // at least one image: conv1 wgrad of the last one (buffer set k ^ 1)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c1_step(j, k ^ 1);
+  }
+  // combine the 8 K-groups in a fixed order (deterministic) and write this workgroup's conv1 slab
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);  // [wave][tile][lane][4]: 32 KiB over P + O
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+      *reinterpret_cast<f32x4*>(red + ((wave * 4 + m * 2 + n) * 64 + lane) * 4) = acc1[m][n];
+  __syncthreads();
+  if (tid >= 256) return;
+  const int tile = tid >> 6;
+  f32x4 sum = *reinterpret_cast<const f32x4*>(red + (tile * 64 + lane) * 4);
+#pragma unroll
+  for (int w = 1; w < 8; ++w) sum += *reinterpret_cast<const f32x4*>(red + ((w * 4 + tile) * 64 + lane) * 4);
+  float* slab = slabs1 + (int64_t)block * C1_WSLAB;
+  const int tap = (tile & 1) * 16 + i16;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = (tile >> 1) * 16 + g * 4 + r;
+    if (tap < 25) slab[co * 25 + tap] = sum[r];
+    if (tap == 25) slab[800 + co] = sum[r];
+  }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(512) void conv12_bwd_kernel(const void* __restrict__ xin,
+                                                         const uint8_t* __restrict__ idx1,
+                                                         const bf16* __restrict__ a1,
+                                                         const bf16* __restrict__ dz2,
+                                                         const bf16* __restrict__ packed, int B,
+                                                         float mean, float inv_std, float in_scale,
+                                                         float* __restrict__ slabs2, int nslices,
+                                                         float* __restrict__ slabs1, int n_dgrad) {
+  __shared__ __attribute__((aligned(16))) char smem[C12B_LDS];
+  if ((int)blockIdx.x < n_dgrad)
+    conv12_dgrad_role<U8>(smem, xin, idx1, dz2, packed, B, blockIdx.x, n_dgrad, mean, inv_std, in_scale, slabs1);
+  else
+    conv2_wgrad_role(smem, a1, dz2, slabs2, B, nslices, blockIdx.x - n_dgrad);
+}
+
 // ================================================================== fixed-order slab reductions
 struct ReduceSeg {
   const float* slabs;
@@ -1500,6 +1709,16 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));  // >= 2 images per slab
 }
 
+// fused conv2 backward + conv1 wgrad: the dgrad role also does conv1 wgrad (104 MFMAs per image on top
+// of conv2 dgrad's 396; conv2 wgrad: 304)
+static void c12_split(int B, int& nd, int& ws) {
+  const int cus = num_cus();
+  static const double frac = split_frac("RINGDP_C12_DGRAD_FRAC", 0.66);
+  nd = clampi(B, 1, (int)(frac * cus));
+  const int per = cdiv(B, nd);
+  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));
+}
+
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 3 * num_cus()); }
 
 int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, fc_imgs(B)) * FC_SLAB; }
@@ -1512,6 +1731,11 @@ int64_t cn_conv2_slab_floats(int B, bool dgrad) {
   int nd, ws;
   c2_split(B, dgrad, nd, ws);
   return (int64_t)ws * C2_WSLAB;
+}
+int64_t cn_conv12_slab_floats(int B) {
+  int nd, ws;
+  c12_split(B, nd, ws);
+  return (int64_t)ws * C2_WSLAB + (int64_t)nd * C1_WSLAB;
 }
 int64_t cn_conv1_slab_floats(int B) { return (int64_t)conv1_wslices(B) * C1_WSLAB; }
 
@@ -1541,6 +1765,27 @@ void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1
                                            static_cast<const bf16*>(packed), static_cast<bf16*>(da1), B, slabs,
                                            ws, nd);
   launch_reduce({seg(slabs, C2_WSLAB, 0, 288 * 64, ws, dw2, 1, 32, 64), seg(slabs, C2_WSLAB, 288 * 64, 64, ws, db2)},
+                s);
+}
+
+void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, const void* dz2,
+                   const void* packed, int B, float mean, float inv_std, float in_scale, float* slabs, float* dw2,
+                   float* db2, float* dw1, float* db1, hipStream_t s) {
+  int nd, ws;
+  c12_split(B, nd, ws);
+  float* slabs2 = slabs;
+  float* slabs1 = slabs + (int64_t)ws * C2_WSLAB;
+  const bf16* a1b = static_cast<const bf16*>(a1);
+  const bf16* dzb = static_cast<const bf16*>(dz2);
+  const bf16* pk = static_cast<const bf16*>(packed);
+  if (u8)
+    conv12_bwd_kernel<true><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
+                                                    slabs1, nd);
+  else
+    conv12_bwd_kernel<false><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
+                                                     slabs1, nd);
+  launch_reduce({seg(slabs2, C2_WSLAB, 0, 288 * 64, ws, dw2, 1, 32, 64), seg(slabs2, C2_WSLAB, 288 * 64, 64, ws, db2),
+                 seg(slabs1, C1_WSLAB, 0, 800, nd, dw1), seg(slabs1, C1_WSLAB, 800, 32, nd, db1)},
                 s);
 }
 

@@ -135,6 +135,12 @@ void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1
                   float* dw2, float* db2, hipStream_t s);
 // F1 backward (weights only: the input needs no gradient).  idx1 bytes carry argmax | relu<<2, laid
 // out [B][13 py][16 co/2][16 px][co&1] (px 13..15 zero).
+// conv2 backward (dgrad + wgrad) fused with conv1 wgrad: da1 stays in LDS; one reduction launch for
+// dW2/db2/dW1/db1.  slabs: cn_conv12_slab_floats(B) floats.
+int64_t cn_conv12_slab_floats(int B);
+void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, const void* dz2,
+                   const void* packed, int B, float mean, float inv_std, float in_scale, float* slabs, float* dw2,
+                   float* db2, float* dw1, float* db1, hipStream_t s);
 void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,
                     float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s);
 

@@ -444,6 +444,36 @@ at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::T
   return da1;
 }
 
+void cn_conv12_bwd(const at::Tensor& x, const at::Tensor& idx1, const at::Tensor& a1, const at::Tensor& dz2,
+                   const at::Tensor& packed, at::Tensor dw2, at::Tensor db2, at::Tensor dw1, at::Tensor db1,
+                   double mean, double std, double in_scale) {
+  int64_t B;
+  bool u8;
+  check_input(x, B, u8);
+  RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
+  check_act(idx1, {B, 13, 16, 16, 2}, at::kByte, "conv1 argmax");
+  check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
+  check_act(dz2, {B, 11, 11, 64}, at::kBFloat16, "conv2 output grad");
+  check_packed(packed);
+  check_f32_out(dw2, {64, 32, 3, 3}, "conv2 dw");
+  check_f32_out(db2, {64}, "conv2 db");
+  check_f32_out(dw1, {32, 1, 5, 5}, "conv1 dw");
+  check_f32_out(db1, {32}, "conv1 db");
+  if (B == 0) {
+    dw2.zero_();
+    db2.zero_();
+    dw1.zero_();
+    db1.zero_();
+    return;
+  }
+  const int bi = static_cast<int>(B);
+  at::Tensor slabs = at::empty({kern::cn_conv12_slab_floats(bi)}, dw2.options());
+  kern::cn_conv12_bwd(x.data_ptr(), u8, idx1.data_ptr<uint8_t>(), a1.data_ptr(), dz2.data_ptr(), packed.data_ptr(),
+                      bi, static_cast<float>(mean), static_cast<float>(1.0 / std), static_cast<float>(in_scale),
+                      slabs.data_ptr<float>(), dw2.data_ptr<float>(), db2.data_ptr<float>(), dw1.data_ptr<float>(),
+                      db1.data_ptr<float>(), cur_stream(x));
+}
+
 void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1, at::Tensor dw1,
                     at::Tensor db1, double mean, double std, double in_scale) {
   int64_t B;

@@ -73,6 +73,9 @@ at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const a
                            at::Tensor dwfc, at::Tensor dbfc);
 at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::Tensor& packed,
                         bool need_da1, at::Tensor dw2, at::Tensor db2);
+void cn_conv12_bwd(const at::Tensor& x, const at::Tensor& idx1, const at::Tensor& a1, const at::Tensor& dz2,
+                   const at::Tensor& packed, at::Tensor dw2, at::Tensor db2, at::Tensor dw1, at::Tensor db1,
+                   double mean, double std, double in_scale);
 void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1, at::Tensor dw1,
                     at::Tensor db1, double mean, double std, double in_scale);
 

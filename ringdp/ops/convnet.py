@@ -6,6 +6,9 @@ Forward is three fused blocks (reference layers ref/launch_dist.py:35-41):
 * ``_Conv2``  conv2 + bias + ReLU + overlapping pool2 -> a2 and one pool2 code byte per value
 * ``_Conv3FC``  conv3 + ReLU + pool3 + view + fc1 -> logits
 
+By default conv1 and conv2 form one node (``_Conv12``) whose backward is a single fused kernel: conv2's
+data gradient da1 stays in LDS and feeds conv1's weight gradient directly.
+
 conv2's pre-activation z2 is never materialised.  ``_Conv2`` returns a zero-stride placeholder
 for it (autograd's handle on "the gradient of conv2's output") next to the real activations;
 ``_Conv3FC``'s backward scatters d(a2) through the pool2 codes straight into dz2, so conv2's
@@ -18,10 +21,15 @@ backward kernels still run.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._native import C
 from . import grad_buffer
+
+# RINGDP_CN_FUSE12=0: conv1 / conv2 as separate autograd nodes with their own backward kernels (A/B)
+_FUSE12 = os.environ.get("RINGDP_CN_FUSE12", "1") != "0"
 
 MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
@@ -70,6 +78,44 @@ class _Conv2(torch.autograd.Function):
                 db if ctx.needs_input_grad[2] else None, None)
 
 
+class _Conv12(torch.autograd.Function):
+    """conv1 + pool1 and conv2 + pool2 as one autograd node: the backward is one fused kernel
+    (conv2 dgrad + wgrad, conv1 wgrad on the LDS-resident da1) and one reduction launch."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, packed, mean, std, in_scale):
+        a1, idx1 = C.cn_conv1_fwd(x, packed, b1, mean, std, in_scale)
+        a2, idx2 = C.cn_conv2_fwd(a1, packed, b2)
+        z2 = a2.new_empty((1, 1, 1, 1)).expand(a1.shape[0], 11, 11, 64)  # placeholder, never read
+        ctx.mark_non_differentiable(a2, idx2)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(x, idx1, a1, packed)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.norm = (mean, std, in_scale)
+        return z2, a2, idx2
+
+    @staticmethod
+    def backward(ctx, dz2, _da2, _didx2):
+        x, idx1, a1, packed = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        n = ctx.needs_input_grad
+        dz2 = dz2.contiguous()
+        if n[1] and n[2] and n[3] and n[4]:
+            dw1, db1, dw2, db2 = (grad_buffer(t) for t in (w1, b1, w2, b2))
+            C.cn_conv12_bwd(x, idx1, a1, dz2, packed, dw2, db2, dw1, db1, *ctx.norm)
+            return None, dw1, db1, dw2, db2, None, None, None, None
+        # partially frozen: the separate kernels
+        need_c1 = n[1] or n[2]
+        dw2, db2 = grad_buffer(w2), grad_buffer(b2)
+        da1 = C.cn_conv2_bwd(a1, dz2, packed, need_c1, dw2, db2)
+        dw1 = db1 = None
+        if need_c1:
+            dw1, db1 = grad_buffer(w1), grad_buffer(b1)
+            C.cn_conv1_wgrad(x, da1, idx1, dw1, db1, *ctx.norm)
+        return (None, dw1 if n[1] else None, db1 if n[2] else None, dw2 if n[3] else None,
+                db2 if n[4] else None, None, None, None, None)
+
+
 class _Conv3FC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z2, a2, idx2, w3, b3, wfc, bfc, packed):
@@ -108,6 +154,9 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         mean, std, scale = 0.0, 1.0, 1.0
     x = x.contiguous()
     packed = pack_weights(conv1, conv2, conv3, fc1)
-    a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
-    z2, a2, idx2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
+    if _FUSE12:
+        z2, a2, idx2 = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, packed, mean, std, scale)
+    else:
+        a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
+        z2, a2, idx2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
     return _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)

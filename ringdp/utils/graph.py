@@ -46,7 +46,8 @@ class StepGraph:
     compares the two with plain loads (``RcclPG.watch_beacon``).  While replays are outstanding
     and none finishes within the group timeout - e.g. a peer died mid-step - the communicator is
     aborted and the process exits non-zero, as for a hung eager collective.  No HIP call is made
-    per replay on either thread.  ``RINGDP_GRAPH_WATCHDOG=0`` turns this off."""
+    per replay on either thread.  ``RINGDP_GRAPH_WATCHDOG``: unset/``auto`` watches groups with more
+    than one rank, ``1`` every group, ``0`` none."""
 
     def __init__(self, step_fn: Callable[[], Optional[torch.Tensor]], warmup: int = 3):
         self.step_fn = step_fn
@@ -69,9 +70,12 @@ class StepGraph:
         if dump:
             self.graph.enable_debug_mode()
         dev = torch.cuda.current_device()
+        mode = os.environ.get("RINGDP_GRAPH_WATCHDOG", "auto")
         watch = []
-        if os.environ.get("RINGDP_GRAPH_WATCHDOG", "1") != "0":
-            watch = [pg for pg in _rccl_groups() if pg.device == dev]
+        if mode != "0":
+            # auto: groups with peers only (a one-rank group has no peer to die; its beacon node would
+            # only add a launch to the step)
+            watch = [pg for pg in _rccl_groups() if pg.device == dev and (mode == "1" or pg.size() > 1)]
         beacon = ReplayBeacon(dev) if watch else None
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             out = self.step_fn()

@@ -21,6 +21,7 @@ from ringdp.utils.graph import StepGraph  # noqa: E402
 def main():
     stall_cycles = int(sys.argv[1])
     os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
+    os.environ["RINGDP_GRAPH_WATCHDOG"] = "1"  # one rank: watched only when forced
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     dist.init_process_group("nccl", timeout=datetime.timedelta(milliseconds=int(os.environ["WD_TIMEOUT_MS"])))
     torch.manual_seed(0)

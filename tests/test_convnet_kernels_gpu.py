@@ -250,6 +250,49 @@ def test_conv1_wgrad(B, u8):
     assert rel_err(db, bq.grad) < 5e-3
 
 
+@pytest.mark.parametrize("B", [1, 7, 100, 513])
+@pytest.mark.parametrize("u8", [True, False])
+def test_conv12_backward_fused(B, u8):
+    """Fused conv2 backward + conv1 wgrad (da1 kept in LDS) against the fp32 PyTorch reference of both
+    layers, against the separate kernels, and bitwise run to run."""
+    torch.manual_seed(17 + B)
+    dev = torch.device("cuda")
+    ws = weights(dev, B + 6)
+    w1, b1, w2, b2 = ws[0], ws[1], ws[2], ws[3]
+    x, xn, norm = input_batch(B, u8, dev)
+    pk = packed(ws)
+    a1, idx1 = C().cn_conv1_fwd(x, pk, b1, *norm)
+    dz2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
+    outs = []
+    for _ in range(2):
+        g = [torch.empty_like(t) for t in (w2, b2, w1, b1)]
+        C().cn_conv12_bwd(x, idx1, a1, dz2, pk, *g, *norm)
+        outs.append(g)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    dw2, db2, dw1, db1 = outs[0]
+    # separate kernels
+    sw2, sb2, sw1, sb1 = (torch.empty_like(t) for t in (w2, b2, w1, b1))
+    da1 = C().cn_conv2_bwd(a1, dz2, pk, True, sw2, sb2)
+    C().cn_conv1_wgrad(x, da1, idx1, sw1, sb1, *norm)
+    for f, r in ((dw2, sw2), (db2, sb2), (dw1, sw1), (db1, sb1)):
+        assert rel_err(f, r) < 1e-4
+    # fp32 reference of both layers (conv2 on the kernel's a1, conv1 through the kernel's pool1 codes)
+    a1q = a1.permute(0, 3, 1, 2).float().requires_grad_()
+    w2q = bf(w2).requires_grad_()
+    b2q = b2.clone().requires_grad_()
+    F.conv2d(a1q, w2q, b2q).backward(dz2.float().permute(0, 3, 1, 2))
+    assert rel_err(dw2, w2q.grad) < 5e-3
+    assert rel_err(db2, b2q.grad) < 5e-3
+    da1_ref = bf(a1q.grad.permute(0, 2, 3, 1))
+    dconv = bf(unpool2x2(da1_ref, conv1_codes(idx1) & 3, a1, 26)).permute(0, 3, 1, 2)
+    w1q = w1.clone().requires_grad_()
+    b1q = b1.clone().requires_grad_()
+    F.conv2d(bf(xn), w1q, b1q, padding=1).backward(dconv)
+    assert rel_err(dw1, w1q.grad) < 1.5e-2
+    assert rel_err(db1, b1q.grad) < 1.5e-2
+
+
 def test_wgrad_deterministic():
     """Slab reductions and the dgrad K-group sums run in a fixed order: two identical backward calls
     are bitwise equal."""
