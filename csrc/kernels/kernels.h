@@ -288,6 +288,9 @@ void bn_prepare(const float* sums, int G, int64_t M, int C, const float* gamma, 
 void bn_act_fwd(const void* z, const float* scale_shift, const void* res, bool relu, int64_t M, int C, void* y,
                 hipStream_t s);
 // backward part 1: g = dy * (y > 0 if relu); partial sums of g and g*zhat per channel -> part
+// BN statistics of a stored bf16 z [M][C] (C % 8 == 0, C <= 2048): partials [bn_bwd_parts(M, C)][2][C]
+// (sum, sum of squares); returns the partial count.
+int bn_col_stats(const void* z, int64_t M, int C, float* part, hipStream_t s);
 int bn_bwd_parts(int64_t M, int C);
 void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
                    float* part, void* g_out, hipStream_t s);

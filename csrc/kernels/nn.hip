@@ -532,6 +532,57 @@ __global__ __launch_bounds__(256) void add_bf16_kernel(const bf16* __restrict__ 
   }
 }
 
+
+// Per-channel sum / sum of squares of a stored bf16 conv output z [M][C] (the BN statistics of a conv
+// whose GEMM ran on hipBLASLt, which has no statistics epilogue): partials [part][2][C] in the layout of
+// the GEMM epilogue's per-tile statistics, rows split over workgroups as in bn_bwd_reduce.
+__global__ __launch_bounds__(256) void bn_col_stats_kernel(const bf16* __restrict__ z, int64_t M, int C,
+                                                           int64_t rows_per_part, float* __restrict__ part) {
+  const int cv = C / 8;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_part;
+  const int64_t r1 = std::min<int64_t>(M, r0 + rows_per_part);
+  const int rows_in_flight = max(1, 256 / cv);
+  const int col = threadIdx.x % cv, rsub = threadIdx.x / cv;
+  __shared__ float red[2][256];
+  float sa[8], sq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sq[j] = 0.f;
+  if (rsub < rows_in_flight && col < cv) {
+    for (int64_t r = r0 + rsub; r < r1; r += kBnUnroll * rows_in_flight) {
+      bf16x8 zz[kBnUnroll];
+#pragma unroll
+      for (int u = 0; u < kBnUnroll; ++u) {
+        const int64_t rr = r + u * rows_in_flight;
+        zz[u] = rr < r1 ? reinterpret_cast<const bf16x8*>(z)[rr * cv + col] : zero_bf16x8();
+      }
+#pragma unroll
+      for (int u = 0; u < kBnUnroll; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = (float)zz[u][j];
+          sa[j] += v;
+          sq[j] += v * v;
+        }
+    }
+  }
+  __syncthreads();
+  for (int j = 0; j < 8; ++j) {
+    red[0][threadIdx.x] = sa[j];
+    red[1][threadIdx.x] = sq[j];
+    __syncthreads();
+    if (threadIdx.x < cv) {
+      float a = 0.f, q = 0.f;
+      for (int k = 0; k < rows_in_flight; ++k) {
+        a += red[0][k * cv + threadIdx.x];
+        q += red[1][k * cv + threadIdx.x];
+      }
+      part[((int64_t)blockIdx.x * 2) * C + threadIdx.x * 8 + j] = a;
+      part[((int64_t)blockIdx.x * 2 + 1) * C + threadIdx.x * 8 + j] = q;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 void pack_conv_weight(const float* w, int K, int C, int R, int S, int Cp, int ldk, void* krsc, void* crsk,
@@ -584,6 +635,12 @@ void bn_act_fwd(const void* z, const float* ss, const void* res, bool relu, int6
 int bn_bwd_parts(int64_t M, int C) {
   const int64_t rpp = bn_rows_per_part(M, C);
   return (int)((M + rpp - 1) / rpp);
+}
+
+int bn_col_stats(const void* z, int64_t M, int C, float* part, hipStream_t s) {
+  const int nparts = bn_bwd_parts(M, C);
+  bn_col_stats_kernel<<<nparts, 256, 0, s>>>(static_cast<const bf16*>(z), M, C, bn_rows_per_part(M, C), part);
+  return nparts;
 }
 
 void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,

@@ -122,7 +122,7 @@ static bool matmul_once(const Problem& p, hipStream_t stream) {
     return v ? std::atoi(v) : 2;  // batched row-contiguous (attention-shaped): 75 vs 91-97 us, attn_gemm_ab.py
   }();
   // batched attention-shaped problems (RINGDP_BLASLT_ROW=2) or everything (=1): A/B runs
-  if ((p.a_row || p.b_row) && !(row_ok == 1 || (row_ok == 2 && p.batch > 1))) return false;
+  if ((p.a_row || p.b_row) && !(p.allow_row || row_ok == 1 || (row_ok == 2 && p.batch > 1))) return false;
   int dev = 0;
   hipGetDevice(&dev);
   std::lock_guard<std::mutex> lk(g_mu);

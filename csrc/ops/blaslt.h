@@ -18,6 +18,7 @@ struct Problem {
   int64_t lda, ldb, ldc;
   int64_t a_bstride = 0, b_bstride = 0, c_bstride = 0;
   bool a_row = false, b_row = false;  // false: K-contiguous; true: row-contiguous
+  bool allow_row = false;             // row-contiguous operands at batch 1 (else only RINGDP_BLASLT_ROW=1)
   bool out_bf16 = true;
   float alpha = 1.f;
   const float* bias = nullptr;

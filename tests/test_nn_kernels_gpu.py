@@ -83,8 +83,14 @@ def _nhwc(x, cp):
     return out.bfloat16().contiguous()
 
 
-@pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_fwd_dgrad_wgrad(case):
+@pytest.mark.parametrize("case,pw", [(c, None) for c in CONV_CASES] +
+                         [((4, 64, 64, 256, 1, 1, 0), m) for m in ("", "fdw")] +
+                         [((2, 256, 64, 64, 1, 1, 0), m) for m in ("", "fdw")])
+def test_conv_fwd_dgrad_wgrad(case, pw, monkeypatch):
+    """pw: RINGDP_PW_BLASLT for the large pointwise cases (M >= 8192): "" = GEMM core, "fdw" = hipBLASLt
+    forward (+ BN statistics pass), data and weight gradient."""
+    if pw is not None:
+        monkeypatch.setenv("RINGDP_PW_BLASLT", pw)
     N, Cin, H, K, R, stride, pad = case
     torch.manual_seed(sum(case))
     dev = "cuda"
