@@ -241,10 +241,12 @@ __device__ __forceinline__ void c1_store(bf16* xc, int tid, uint32_t u, float4 f
   }
 }
 
-// conv1 pool/ReLU codes for the backward: [B][py 13][co/2 16][px 16][co&1] bytes (px 13..15 zero), each
-// 1 << argmax (dy*2+dx) if the pooled value is > 0, else 0 (the gradient's destination, one-hot).  Window rows per channel pair let conv1 wgrad read the
-// codes of 4 neighbouring windows of one channel as one 8-byte load.
-constexpr int C1I_IMG = 13 * 512;      // 6656 bytes per image
+// conv1 pool/ReLU codes for the backward: [B][py 13][co/2 16][px 16] bytes (px 13..15 zero), one nibble per
+// channel (low: even co, high: odd co), each 1 << argmax (dy*2+dx) if the pooled value is > 0, else 0 (the
+// gradient's destination, one-hot).  Window rows per channel pair let conv1 wgrad read the codes of 4
+// neighbouring windows of one channel as one 4-byte load.  (Nibbles, not bytes: conv1 forward is bound by
+// its HBM writes, 17.4 -> 14.1 KB per image.)
+constexpr int C1I_IMG = 13 * 256;      // 3328 bytes per image
 constexpr int C1A_IMG = 169 * 32;      // a1 elements per image
 
 // relu(max) + argmax of a 2x2 window (the 4 accumulator registers of a window-ordered m-tile, bias
@@ -283,7 +285,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
                                                         float mean, float inv_std, float in_scale) {
   __shared__ __attribute__((aligned(16))) bf16 xs[2][8 * C1F_CS];
   __shared__ __attribute__((aligned(16))) uint32_t ot[172 * 16];      // rows >= 169: dropped tiles
-  __shared__ __attribute__((aligned(16))) uint8_t ct[C1I_IMG + 512];  // + a dump row for them
+  __shared__ __attribute__((aligned(16))) uint8_t ct[C1I_IMG + 64];   // + a dump row for them
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, gq = lane >> 4;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P1_OFF);
@@ -303,7 +305,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
     const int oh = 2 * (w / 13) + (i >> 1), ow = 2 * (w % 13) + (i & 1);
     aoff[j] = (ow & 7) * C1F_CS + oh * XC_W + (ow & ~7) + gq * XC_W;
     const int wc = 4 * mt + gq;
-    coff[j] = wc < 169 ? (wc / 13) * 512 + r16 * 32 + (wc % 13) * 2 : C1I_IMG + 2 * lane;
+    coff[j] = wc < 169 ? (wc / 13) * 256 + r16 * 16 + wc % 13 : C1I_IMG + lane;
   }
   for (int i = tid; i < 2 * 8 * C1F_CS / 8; i += 256) reinterpret_cast<bf16x8*>(&xs[0][0])[i] = zero_bf16x8();
   for (int i = tid; i < C1I_IMG / 16; i += 256) reinterpret_cast<uint4*>(ct)[i] = make_uint4(0, 0, 0, 0);
@@ -327,7 +329,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
       const uint32_t v0 = pool4_key(c0, g0), v1 = pool4_key(c1, g1);
       const bf16x2v pv = __builtin_convertvector(f32x2v{__uint_as_float(v0), __uint_as_float(v1)}, bf16x2v);
       ot[(4 * (wave + 4 * j) + gq) * 16 + r16] = __builtin_bit_cast(uint32_t, pv);  // v_cvt_pk_bf16_f32
-      *reinterpret_cast<uint16_t*>(ct + coff[j]) = (uint16_t)(g0 | (g1 << 8));
+      ct[coff[j]] = (uint8_t)(g0 | (g1 << 4));
     };
     f32x4 p0 = zero_f32x4(), p1 = zero_f32x4();
 #pragma unroll
@@ -1197,7 +1199,7 @@ constexpr int C1W_XS = 0;                          // 5 shifted copies of the in
 constexpr int C1W_D = 5 * C1W_CS * 2;              // 15200: da1 image [169 (+3 zero) windows][32] bf16, x2
 constexpr int C1W_DSZ = 172 * 32 * 2;              // 11008
 constexpr int C1W_C = C1W_D + 2 * C1W_DSZ;         // 37216: code rows [13][16][16][2] bytes, x2
-constexpr int C1W_LDS = C1W_C + 2 * C1I_IMG;       // 50528 -> 3 workgroups per CU
+constexpr int C1W_LDS = C1W_C + 2 * C1I_IMG;       // 43872 -> 3 workgroups per CU
 
 template <bool U8>
 __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict__ xin,
@@ -1261,14 +1263,14 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const void* __restrict
         // (bit-cast the whole vector: __builtin_bit_cast of a single vector element miscompiles to element 0)
         const uint2 d = __builtin_bit_cast(uint2, lds_read_tr16(D + (py * 13 + 4 * g + q) * 32 + m * 16 + 4 * p));
         const int co = m * 16 + i16;
-        const uint2 cu = *reinterpret_cast<const uint2*>(CB + py * 512 + (co >> 1) * 32 + 8 * g);
-        const int csh = 8 * (co & 1) + 2 * dy;
+        const uint32_t cu = *reinterpret_cast<const uint32_t*>(CB + py * 256 + (co >> 1) * 16 + 4 * g);
+        const int csh = 4 * (co & 1) + 2 * dy;
         uint32_t pr[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const uint32_t dv = k & 1 ? (k < 2 ? d.x : d.y) >> 16 : (k < 2 ? d.x : d.y) & 0xffffu;
           // the two one-hot bits of window row dy: 1 -> dx = 0, 2 -> dx = 1, 0 -> no gradient
-          const uint32_t sel = __builtin_amdgcn_ubfe(k < 2 ? cu.x : cu.y, 16 * (k & 1) + csh, 2);
+          const uint32_t sel = __builtin_amdgcn_ubfe(cu, 8 * k + csh, 2);
           pr[k] = dv * ((sel * 0x8001u) & 0x10001u);  // dv, dv << 16 or 0
         }
         A[m] = __builtin_bit_cast(bf16x8, make_uint4(pr[0], pr[1], pr[2], pr[3]));
@@ -1324,7 +1326,7 @@ constexpr int C12_XS = 5 * C1W_CS * 2;              // 15200: 5 shifted copies o
 // P | O[2] | xs[2] | codes[2]: image i uses buffer set i & 1, so conv1 wgrad of image i-1 runs interleaved
 // with conv2 dgrad of image i (2 waves per SIMD: the MFMA stream of one hides the LDS/VALU of the other)
 constexpr int C12_OFF_O = C2D_P, C12_OFF_X = C12_OFF_O + 2 * C12_O, C12_OFF_C = C12_OFF_X + 2 * C12_XS;
-constexpr int C12_LDS = C12_OFF_C + 2 * C1I_IMG;    // 103632
+constexpr int C12_LDS = C12_OFF_C + 2 * C1I_IMG;    // 96976
 constexpr int C12B_LDS = C12_LDS > (C2W_D + C2W_X) ? C12_LDS : (C2W_D + C2W_X);
 static_assert(C2D_P % 16 == 0 && C12_O % 16 == 0 && C12_XS % 16 == 0, "16-B aligned LDS buffers");
 static_assert(8 * 4 * 64 * 4 * 4 <= C12_OFF_X, "conv1 cross-wave reduction fits in P + O");
@@ -1406,13 +1408,13 @@ __device__ void conv12_dgrad_role(char* smem, const void* __restrict__ xin, cons
     for (int m = 0; m < 2; ++m) {
       const uint2 d = __builtin_bit_cast(uint2, lds_read_tr16(O + (py * 13 + 4 * g + q) * C2_ORS + m * 16 + 4 * p));
       const int co = m * 16 + i16;
-      const uint2 cu = *reinterpret_cast<const uint2*>(CB + py * 512 + (co >> 1) * 32 + 8 * g);
-      const int csh = 8 * (co & 1) + 2 * dy;
+      const uint32_t cu = *reinterpret_cast<const uint32_t*>(CB + py * 256 + (co >> 1) * 16 + 4 * g);
+      const int csh = 4 * (co & 1) + 2 * dy;
       uint32_t pr[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const uint32_t dv = e & 1 ? (e < 2 ? d.x : d.y) >> 16 : (e < 2 ? d.x : d.y) & 0xffffu;
-        const uint32_t sel = __builtin_amdgcn_ubfe(e < 2 ? cu.x : cu.y, 16 * (e & 1) + csh, 2);
+        const uint32_t sel = __builtin_amdgcn_ubfe(cu, 8 * e + csh, 2);
         pr[e] = ok ? dv * ((sel * 0x8001u) & 0x10001u) : 0u;
       }
       A[m] = __builtin_bit_cast(bf16x8, make_uint4(pr[0], pr[1], pr[2], pr[3]));

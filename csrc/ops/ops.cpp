@@ -341,7 +341,7 @@ std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::T
   auto opt = x.options();
   at::Tensor a1 = at::empty({B, 13, 13, 32}, opt.dtype(at::kBFloat16));
   // pool1 codes in window rows per channel pair [B][py][co/2][px (13 + 3 zero)][co&1] (see convnet.hip F1)
-  at::Tensor idx = at::empty({B, 13, 16, 16, 2}, opt.dtype(at::kByte));
+  at::Tensor idx = at::empty({B, 13, 16, 16}, opt.dtype(at::kByte));
   if (B == 0) return {a1, idx};
   kern::cn_conv1_fwd(x.data_ptr(), u8, packed.data_ptr(), b1.data_ptr<float>(), a1.data_ptr(),
                      idx.data_ptr<uint8_t>(), static_cast<int>(B), static_cast<float>(mean),
@@ -451,7 +451,7 @@ void cn_conv12_bwd(const at::Tensor& x, const at::Tensor& idx1, const at::Tensor
   bool u8;
   check_input(x, B, u8);
   RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
-  check_act(idx1, {B, 13, 16, 16, 2}, at::kByte, "conv1 argmax");
+  check_act(idx1, {B, 13, 16, 16}, at::kByte, "conv1 argmax");
   check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "conv2 input");
   check_act(dz2, {B, 11, 11, 64}, at::kBFloat16, "conv2 output grad");
   check_packed(packed);
@@ -481,7 +481,7 @@ void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor
   check_input(x, B, u8);
   RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
   check_act(da1, {B, 13, 13, 32}, at::kBFloat16, "conv1 grad");
-  check_act(idx1, {B, 13, 16, 16, 2}, at::kByte, "conv1 argmax");
+  check_act(idx1, {B, 13, 16, 16}, at::kByte, "conv1 argmax");
   check_f32_out(dw1, {32, 1, 5, 5}, "conv1 dw");
   check_f32_out(db1, {32}, "conv1 db");
   if (B == 0) {

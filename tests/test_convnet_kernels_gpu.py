@@ -65,10 +65,12 @@ def unpool2x2(dout, idx, pooled, oh):
 
 
 def conv1_codes(idx):
-    """pool1 code rows [B,13 py,16 co/2,16 px,2 co&1] (px 13..15 zero) -> [B,13,13,32] (NHWC, like a1)."""
-    assert idx.dim() == 5 and idx.shape[1:] == (13, 16, 16, 2)
+    """pool1 code rows [B,13 py,16 co/2,16 px] bytes of two nibbles (low: even co, high: odd co; px 13..15
+    zero) -> [B,13,13,32] (NHWC, like a1)."""
+    assert idx.dim() == 4 and idx.shape[1:] == (13, 16, 16)
     assert not idx[:, :, :, 13:].any()
-    h = idx[:, :, :, :13].permute(0, 1, 3, 2, 4).reshape(idx.shape[0], 13, 13, 32)
+    nib = torch.stack([idx & 15, idx >> 4], -1)  # [B, 13, 16, 16, 2]
+    h = nib[:, :, :, :13].permute(0, 1, 3, 2, 4).reshape(idx.shape[0], 13, 13, 32)
     # one-hot destination (1 << argmax, 0 if the ReLU is off) -> argmax | 4 * relu
     assert torch.all((h == 0) | (h == 1) | (h == 2) | (h == 4) | (h == 8))
     arg = (h == 2).to(torch.uint8) + 2 * (h == 4).to(torch.uint8) + 3 * (h == 8).to(torch.uint8)
