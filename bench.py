@@ -288,7 +288,26 @@ def worker(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item()), loss
 
+    sync()
+    t_w = time.perf_counter()
     run_steps(n_warm, graph)
+    sync()
+    # Steady state: the W warmup steps of a short run (e.g. 5 x 2 ms) end before the GPU has left its
+    # idle clocks, and the first timed steps then run ~2.5 % slower.  Warmup therefore continues until
+    # RINGDP_BENCH_MIN_WARMUP_S of warm steps have run (0 disables); every rank runs the same count (MAX
+    # over ranks: the captured step holds collectives).  Reported as "warmup_steps_run".
+    min_warm_s = float(os.environ.get("RINGDP_BENCH_MIN_WARMUP_S", "0.5"))
+    warm_el = time.perf_counter() - t_w
+    extra = 0
+    if min_warm_s > 0 and warm_el < min_warm_s:
+        extra = min(5000, int((min_warm_s - warm_el) / max(warm_el / n_warm, 1e-6)) + 1)
+    if world > 1:
+        t_x = torch.tensor([extra], dtype=torch.int64, device=dev)
+        dist.all_reduce(t_x, op=dist.ReduceOp.MAX)
+        extra = int(t_x.item())
+    if extra:
+        run_steps(extra, graph)
+    n_warm += extra
     _phase(f"timed region: {args.steps} steps")
     elapsed_max, loss = timed(args.steps, graph)
     final_loss = float(loss.item()) if loss is not None else float("nan")
@@ -335,6 +354,7 @@ def worker(args):
                 "n_gpus": world,
                 "steps": args.steps,
                 "warmup": args.warmup,
+                "warmup_steps_run": n_warm,
                 "ms_per_step": round(ms_per_step, 4),
                 "higher_is_better": True,
                 "scaling": "weak",
