@@ -200,6 +200,9 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
 // delayed scaling: hist = {amax to scale by, per-64x64-tile |x|max of the last call...}; hist[0] is
 // rolled from the tile maxima (or, init = first call of a site, measured exactly), then x is quantised
 // (q^T into out_t, q into out_rowmajor) while its tile maxima are written for the next call.
+// tile counts of the quantise(+transpose) pass: per-tile amax slots and colsum partial rows
+int64_t fp8_quant_tiles(int64_t rows, int64_t cols);
+int64_t fp8_quant_row_tiles(int64_t rows);
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
                           float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part = nullptr,
                           const void* gelu_pre = nullptr);

@@ -606,11 +606,23 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnIn q, AttnIn k, AttnI
     sum += __shfl_xor(sum, 32, 64);
     const float inv = qrow < T ? 1.f / sum : 0.f;  // padded query rows: P = 0
     bf16x4 pb[NT];
-    bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp + 4 * g;
+    bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
+    for (int t = 0; t < NT; ++t)
       pb[t] = bf16x4{(bf16)(st[t][0] * inv), (bf16)(st[t][1] * inv), (bf16)(st[t][2] * inv), (bf16)(st[t][3] * inv)};
-      *reinterpret_cast<bf16x4*>(prow + 16 * t) = pb[t];
+    {  // tile pairs (t, t+1): lanes with g even store 8 keys of tile t, g odd 8 keys of tile t+1 (one xor-16
+       // exchange of 8 B): 16-B stores, 64 contiguous bytes of each of 16 rows per store instruction
+      const bool godd = g & 1;
+#pragma unroll
+      for (int t = 0; t + 1 < NT; t += 2) {
+        const uint2 sv = __builtin_bit_cast(uint2, godd ? pb[t] : pb[t + 1]);
+        const uint2 rv = make_uint2(__shfl_xor(sv.x, 16, 64), __shfl_xor(sv.y, 16, 64));
+        const bf16x4 rcv = __builtin_bit_cast(bf16x4, rv);
+        const bf16x4 lo = godd ? rcv : pb[t], hi = godd ? pb[t + 1] : rcv;
+        const int col = godd ? 16 * (t + 1) + 4 * (g - 1) : 16 * t + 4 * g;
+        *reinterpret_cast<bf16x8*>(prow + col) = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      if (NT & 1) *reinterpret_cast<bf16x4*>(prow + 16 * (NT - 1) + 4 * g) = pb[NT - 1];
     }
     // O^T[d][q] = sum over key pairs (t0, t1) of V^T (keys 16t + 4g + j) x P^T
     f32x4 ot[4];

@@ -792,7 +792,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both(const at::Tenso
   return {q, qt, scale};
 }
 
-int64_t fp8_delayed_slots(int64_t rows, int64_t cols) { return ((rows + 63) / 64) * ((cols + 63) / 64); }
+int64_t fp8_delayed_slots(int64_t rows, int64_t cols) { return kern::fp8_quant_tiles(rows, cols); }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const at::Tensor& x, at::Tensor hist,
                                                                         bool init,
@@ -811,7 +811,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const a
   if (colsum.has_value() && colsum->defined()) {  // column sums of x (a bias gradient) from the same pass
     f32_gpu(*colsum, "fp8 quantize colsum");
     RINGDP_CHECK(colsum->numel() == Cc && colsum->is_contiguous(), "fp8 quantize colsum: expected [cols] floats");
-    part = at::empty({(R + 63) / 64, Cc}, x.options().dtype(at::kFloat));
+    part = at::empty({kern::fp8_quant_row_tiles(R), Cc}, x.options().dtype(at::kFloat));
   }
   // gelu_pre: quantise x * GELU'(gelu_pre) (an fp8 linear's GELU backward folded into the pass over its gradient)
   const void* pre = nullptr;
