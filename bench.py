@@ -165,6 +165,10 @@ def worker(args):
     spec = MODELS[args.model]
     B = args.batch_per_rank or int(os.environ.get("RINGDP_BENCH_BATCH", spec["batch"]))
     lr = args.lr if args.lr is not None else spec["lr"]
+    if args.model == "convnet" and B <= 4096 and args.bucket_mb is None and args.first_bucket_mb is None:
+        # small per-rank batches: the conv2/conv1 backward is too short (~12 us at B=100) to hide the first
+        # bucket's collective behind, so one 455 KB bucket (one collective, one latency term) beats two
+        args.bucket_mb = args.first_bucket_mb = 1.0
     if args.bucket_mb is None:
         args.bucket_mb = spec.get("bucket_mb", 25.0)
     if args.first_bucket_mb is None:
