@@ -48,7 +48,9 @@ METRIC = "images/sec (whole node) MNIST ConvNet at 1/2/4/8 MI355X; DDP scaling e
 
 # Extra BASELINE.json configs (--model): the deeper families, synthetic data of the named shape.
 MODELS = {
-    "convnet": dict(batch=32768, shape=(1, 28, 28), lr=1e-4, momentum=0.0, nesterov=False, wd=0.0,
+    # per-rank batch: throughput plateau on one MI355X (B=32768 16.09M, 49152 16.15M, 65536 16.25M, 131072
+    # 16.22M img/s); 65536 also halves the exposed all-reduce share of the step at N > 1
+    "convnet": dict(batch=65536, shape=(1, 28, 28), lr=1e-4, momentum=0.0, nesterov=False, wd=0.0,
                     # 455 KB of fp32 grads in two buckets: [fc1 + conv3] is all-reduced while conv2/conv1
                     # backward still run; only the small [conv2 + conv1] bucket is exposed at the end.
                     bucket_mb=0.3, first_bucket_mb=0.3,
