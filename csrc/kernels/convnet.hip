@@ -1715,7 +1715,7 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
 // of conv2 dgrad's 396; conv2 wgrad: 304)
 static void c12_split(int B, int& nd, int& ws) {
   const int cus = num_cus();
-  static const double frac = split_frac("RINGDP_C12_DGRAD_FRAC", 0.66);
+  static const double frac = split_frac("RINGDP_C12_DGRAD_FRAC", 0.64);
   nd = clampi(B, 1, (int)(frac * cus));
   const int per = cdiv(B, nd);
   ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));
