@@ -135,14 +135,25 @@ __global__ __launch_bounds__(256) void bn_prepare_kernel(const float* __restrict
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
-  float a = 0.f, q = 0.f;
-  if (c < C)
-    for (int g = wave; g < G; g += 4) {
-      a += sums[(int64_t)g * 2 * C + c];
-      q += sums[(int64_t)g * 2 * C + C + c];
+  // 4 independent partial chains per wave (loads of 4 groups in flight): the serial chain over G/4 groups
+  // was latency-bound (10 us at G = 64 for a ResNet-18 layer-2 conv); combined in a fixed order
+  float a4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int g = wave;
+    for (; g + 12 < G; g += 16) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a4[u] += sums[(int64_t)(g + 4 * u) * 2 * C + c];
+        q4[u] += sums[(int64_t)(g + 4 * u) * 2 * C + C + c];
+      }
     }
-  red[wave][0][lane] = a;
-  red[wave][1][lane] = q;
+    for (; g < G; g += 4) {
+      a4[0] += sums[(int64_t)g * 2 * C + c];
+      q4[0] += sums[(int64_t)g * 2 * C + C + c];
+    }
+  }
+  red[wave][0][lane] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  red[wave][1][lane] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
   __syncthreads();
   if (wave != 0 || c >= C) return;
   const float s1 = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
@@ -253,15 +264,41 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __res
   if (part) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[j] = db[j] = 0.f;
-    for (int p = 0; p < nparts; ++p) {
+    // two partial rows per step with separate accumulators (independent loads in flight; the one-row
+    // serial chain took 12 us at 32 partials), combined in a fixed order
+    float db2[8], dg2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg2[j] = db2[j] = 0.f;
+    int p = 0;
+#pragma unroll 2
+    for (; p + 1 < nparts; p += 2) {
+      float a[8], q[8], a2[8], q2[8];
+      load8(part + (int64_t)p * 2 * C + col * 8, a);            // sum of g
+      load8(part + (int64_t)p * 2 * C + C + col * 8, q);        // sum of g * zhat
+      load8(part + (int64_t)(p + 1) * 2 * C + col * 8, a2);
+      load8(part + (int64_t)(p + 1) * 2 * C + C + col * 8, q2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        db[j] += a[j];
+        dg[j] += q[j];
+        db2[j] += a2[j];
+        dg2[j] += q2[j];
+      }
+    }
+    if (p < nparts) {
       float a[8], q[8];
-      load8(part + (int64_t)p * 2 * C + col * 8, a);      // sum of g
-      load8(part + (int64_t)p * 2 * C + C + col * 8, q);  // sum of g * zhat
+      load8(part + (int64_t)p * 2 * C + col * 8, a);
+      load8(part + (int64_t)p * 2 * C + C + col * 8, q);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         db[j] += a[j];
         dg[j] += q[j];
       }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      db[j] += db2[j];
+      dg[j] += dg2[j];
     }
     if (blockIdx.x == 0 && rsub == 0) {
 #pragma unroll
@@ -326,7 +363,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
   const int lanes_per_row = cv;
   const int rows_in_flight = max(1, 256 / lanes_per_row);
   const int col = threadIdx.x % lanes_per_row, rsub = threadIdx.x / lanes_per_row;
-  __shared__ float red[2][256];
+  __shared__ __attribute__((aligned(16))) float red[2][256][8];  // [statistic][thread][channel of its 8]
   float sg[8], sgz[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) sg[j] = sgz[j] = 0.f;
@@ -368,22 +405,21 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
       }
     }
   }
-  // combine the rows_in_flight partial rows for each column (fixed order)
-  __syncthreads();
+  // combine the rows_in_flight partial rows for each column (fixed order): every thread parks its 16 sums
+  // in LDS once, then each output (statistic, channel) is summed by its own thread - one barrier instead of
+  // 16, and no thread walks 8 channels x rows_in_flight serial LDS reads (the old tail was most of the
+  // kernel's time on small ResNet-18 layers)
+#pragma unroll
   for (int j = 0; j < 8; ++j) {
-    red[0][threadIdx.x] = sg[j];
-    red[1][threadIdx.x] = sgz[j];
-    __syncthreads();
-    if (threadIdx.x < lanes_per_row) {
-      float a = 0.f, q = 0.f;
-      for (int k = 0; k < rows_in_flight; ++k) {
-        a += red[0][k * lanes_per_row + threadIdx.x];
-        q += red[1][k * lanes_per_row + threadIdx.x];
-      }
-      part[((int64_t)blockIdx.x * 2) * C + threadIdx.x * 8 + j] = a;
-      part[((int64_t)blockIdx.x * 2 + 1) * C + threadIdx.x * 8 + j] = q;
-    }
-    __syncthreads();
+    red[0][threadIdx.x][j] = sg[j];
+    red[1][threadIdx.x][j] = sgz[j];
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < 2 * C; o += 256) {
+    const int st = o / C, c = o - st * C, cl = c >> 3, j = c & 7;
+    float a = 0.f;
+    for (int k = 0; k < rows_in_flight; ++k) a += red[st][k * lanes_per_row + cl][j];
+    part[((int64_t)blockIdx.x * 2 + st) * C + c] = a;
   }
 }
 
