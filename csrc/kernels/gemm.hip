@@ -772,17 +772,16 @@ __global__ __launch_bounds__(256) void splitk_sum_kernel(const float* __restrict
                                                          int perm_rs) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  // 4 interleaved partial sums keep 4 loads in flight; combined in a fixed order (deterministic)
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  // 8 interleaved partial sums keep 8 loads in flight (the sum is latency-bound: S/8 dependent rounds);
+  // combined in a fixed order (deterministic)
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   int s = 0;
-  for (; s + 4 <= S; s += 4) {
-    a0 += part[(int64_t)(s + 0) * n + i];
-    a1 += part[(int64_t)(s + 1) * n + i];
-    a2 += part[(int64_t)(s + 2) * n + i];
-    a3 += part[(int64_t)(s + 3) * n + i];
+  for (; s + 8 <= S; s += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += part[(int64_t)(s + u) * n + i];
   }
-  for (; s < S; ++s) a0 += part[(int64_t)s * n + i];
-  const float a = (a0 + a1) + (a2 + a3);
+  for (; s < S; ++s) acc[0] += part[(int64_t)s * n + i];
+  const float a = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   if (perm_rs > 0) {  // i = ko*(RS*C) + rs*C + c  ->  ko*(C*RS) + c*RS + rs
     const int64_t per = (int64_t)perm_rs * perm_c;
     const int64_t ko = i / per, rem = i - ko * per, rs = rem / perm_c, c = rem - rs * perm_c;
@@ -855,19 +854,17 @@ __global__ __launch_bounds__(256) void splitk_finish_kernel(const float* __restr
   float a = 0.f, q = 0.f;
   if (c < N)
     for (int r = r0 + wave; r < r1; r += 4) {
-      // 4 interleaved partial sums (independent loads in flight), combined in a fixed order
+      // 8 interleaved partial sums (independent loads in flight), combined in a fixed order
       const float* pr = part + (int64_t)r * N + c;
       const int64_t ps = (int64_t)M * N;
-      float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+      float vv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       int sp = 0;
-      for (; sp + 4 <= S; sp += 4) {
-        v0 += pr[(sp + 0) * ps];
-        v1 += pr[(sp + 1) * ps];
-        v2 += pr[(sp + 2) * ps];
-        v3 += pr[(sp + 3) * ps];
+      for (; sp + 8 <= S; sp += 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vv[u] += pr[(sp + u) * ps];
       }
-      for (; sp < S; ++sp) v0 += pr[sp * ps];
-      float v = (v0 + v1) + (v2 + v3);
+      for (; sp < S; ++sp) vv[0] += pr[sp * ps];
+      float v = ((vv[0] + vv[1]) + (vv[2] + vv[3])) + ((vv[4] + vv[5]) + (vv[6] + vv[7]));
       if (residual) v += (float)residual[(int64_t)r * ldc + c];
       const bf16 o = (bf16)v;
       out[(int64_t)r * ldc + c] = o;
