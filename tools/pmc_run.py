@@ -1,6 +1,6 @@
 """Run one ConvNet kernel group repeatedly for PMC collection under rocprofv3 --pmc.
 
-python tools/pmc_run.py <op> [B] [iters]   op: conv3_fc_bwd | conv2_bwd | conv3_fc_fwd | conv2_fwd | conv1_fwd | conv1_wgrad
+python tools/pmc_run.py <op> [B] [iters]   op: conv3_fc_bwd | conv12_bwd | conv2_bwd | conv3_fc_fwd | conv2_fwd | conv1_fwd | conv1_wgrad
 """
 import sys
 
@@ -47,6 +47,7 @@ def main():
         "conv2_bwd_w": lambda: C.cn_conv2_bwd(a1, dz2, pk, False, *g2),
         "conv2_bwd": lambda: C.cn_conv2_bwd(a1, dz2, pk, True, *g2),
         "conv1_wgrad": lambda: C.cn_conv1_wgrad(x, da1, i1, *g1, *norm),
+        "conv12_bwd": lambda: C.cn_conv12_bwd(x, i1, a1, dz2, pk, *g2, *g1, *norm),
     }
     for _ in range(iters):
         fns[op]()

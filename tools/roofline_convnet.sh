@@ -9,7 +9,7 @@ B=${1:-32768}
 OUT=$R/gpurun_out/roofline
 mkdir -p $OUT
 : > $OUT/summary.jsonl
-for op in conv1_fwd conv2_fwd conv3_fc_fwd conv3_fc_bwd conv2_bwd conv1_wgrad; do
+for op in ${OPS:-conv1_fwd conv2_fwd conv3_fc_fwd conv3_fc_bwd conv12_bwd}; do
   for pass in time fetch write lds; do
     case $pass in
       time)  args="--kernel-trace" ;;

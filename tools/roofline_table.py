@@ -21,6 +21,7 @@ OPS = {
     "conv3_fc_bwd": ("conv3_bwd_kernel|fc_bwd_kernel|slab_reduce_kernel", 18.88 + 0.08),
     "conv2_bwd": ("conv2_bwd_kernel|slab_reduce_kernel", 8.92),
     "conv1_wgrad": ("conv1_wgrad_kernel|slab_reduce_kernel", 1.08),
+    "conv12_bwd": ("conv12_bwd_kernel|slab_reduce_kernel", 8.92 + 1.08),
 }
 HBM_TBS = 8.0
 BF16_PF = 2.5
