@@ -622,7 +622,7 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ a
 // images per workgroup: enough workgroups to fill the chip at small batches (B=100: 25 of 4 images,
 // was 4 of 32 and latency-bound at 21 us), fewer fp32 slabs at large ones (B=32768: 512 of 64 images,
 // halving the 84 MB of slab traffic)
-__host__ __device__ inline int fc_imgs(int B) { return B <= 1024 ? 4 : (B >= 32768 ? 64 : 32); }
+__host__ __device__ inline int fc_imgs(int B) { return B <= 1024 ? 4 : (B >= 65536 ? 128 : (B >= 32768 ? 64 : 32)); }
 constexpr int FC_SLAB = 10 * 2048 + 10 + 128;  // dWfc + dbfc + db3 (the conv3 bias gradient is the sum of
                                                 // d(a3) over windows: no MFMA tile needed for it)
 
