@@ -10,9 +10,9 @@ Data: synthetic MNIST-shaped uint8 images + labels generated on the device (no d
 is possible offline); Normalize((0.1307,),(0.3081,)) is fused into the first conv kernel.
 Weights: random init (torch.manual_seed(0), PyTorch default init - identical to the reference).
 Scaling: weak (fixed per-rank batch), like the reference.
-Per-rank batch: 32768 images (the reference runs 100; `--batch-per-rank 100` reproduces that regime).
-The ConvNet is ~44 MFLOP/img, so a 100-image step is launch/latency-bound; 32768 fills 256 CUs and
-amortises the 455 KB gradient all-reduce (activations ~1.5 GB of the 288 GB HBM3E).
+Per-rank batch: 65536 images (the reference runs 100; `--batch-per-rank 100` reproduces that regime).
+The ConvNet is ~44 MFLOP/img, so a 100-image step is launch/latency-bound; 65536 fills 256 CUs and
+amortises the 455 KB gradient all-reduce (activations ~3 GB of the 288 GB HBM3E).
 
 Launch (one process per GPU, RCCL over xGMI):
   python bench.py --gpus N ...            N > 1 without WORLD_SIZE in the env: this process starts N
@@ -22,7 +22,11 @@ Launch (one process per GPU, RCCL over xGMI):
       bench.py --gpus N ...               the driver's form; ranks read RANK/LOCAL_RANK/WORLD_SIZE
   python -m ringdp.run --nproc-per-node N bench.py --gpus N ...
 
-The gradient all-reduce runs at every N, including N=1 (a one-rank RCCL communicator, exactly what
+Comm backend: RCCL (backend "nccl"); RINGDP_GPU_BACKEND=xgmi selects ringdp's own collective
+kernels over IPC-mapped peer memory instead (one node; ranks may then share a GPU, rank r using GPU
+r % device_count, as ref/launch_dist.py:47 binds devices).
+
+The gradient all-reduce runs at every N, including N=1 (a one-rank communicator, exactly what
 upstream DDP does), so every point of the scaling curve executes the same code path;
 ``--no-force-comm`` skips it at N=1.  After the timed region (never inside it) the bench measures
 per-bucket device-timed collective durations over a few eager steps and the step time of a
@@ -72,7 +76,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", type=str, default="convnet", choices=sorted(MODELS))
     ap.add_argument("--batch-per-rank", type=int, default=None,
-                    help="per-rank batch (default: 32768 for the ConvNet, RINGDP_BENCH_BATCH overrides)")
+                    help="per-rank batch (default: 65536 for the ConvNet, RINGDP_BENCH_BATCH overrides)")
     ap.add_argument("--lr", type=float, default=None)
     ap.add_argument("--bucket-mb", type=float, default=None, help="bucket cap (default: per model, else 25)")
     ap.add_argument("--first-bucket-mb", type=float, default=None)
@@ -147,8 +151,12 @@ def worker(args):
     local_rank = int(os.environ.get("LOCAL_RANK", args.local_rank if args.local_rank is not None else 0))
     on_gpu = not args.cpu
     if on_gpu:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # rank r on GPU r % device_count (device_count() does not initialise the GPU); more ranks than
+        # GPUs is only possible on the xgmi backend (RCCL refuses two ranks per GPU)
+        ndev = max(torch.cuda.device_count(), 1)
+        dev_index = local_rank % ndev
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
         backend = "nccl"
     else:
         dev = torch.device("cpu")
@@ -188,7 +196,7 @@ def worker(args):
         if args.dtype == "fp32":
             raise SystemExit("--dtype fp32 is implemented for --model convnet")
         model = getattr(models, args.model)(num_classes=NUM_CLASSES[args.model]).to(dev)
-    ddp = DDP(model, device_ids=[local_rank] if on_gpu else None, output_device=local_rank if on_gpu else None,
+    ddp = DDP(model, device_ids=[dev.index] if on_gpu else None, output_device=dev.index if on_gpu else None,
               bucket_cap_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb)
     if args.comm_hook != "allreduce":
         ddp._set_builtin_hook(args.comm_hook)
@@ -330,7 +338,8 @@ def worker(args):
     def emit(comm_stats, text_only=False):
         n_buckets = len(ddp.reducer.bucket_indices())
         sizes_kb = ",".join(f"{b / 1024:.0f}" for b in comm_stats["bucket_bytes"])
-        lib = "RCCL" if on_gpu else "host ring (gloo)"
+        lib = {"rccl": "RCCL", "xgmi": "ringdp xGMI kernels (IPC peer memory)"}.get(nat.backend_name(), nat.backend_name()) \
+            if on_gpu else "host ring (gloo)"
         if world > 1:
             comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
                     f"cap {args.bucket_mb} MB" + (", side HIP stream overlapped with backward" if on_gpu else ""))
@@ -385,6 +394,8 @@ def worker(args):
                 "comm_stats": comm_stats,
                 "final_loss": round(final_loss, 5),
             }
+            if on_gpu and world > torch.cuda.device_count():
+                res["config"]["ranks_per_gpu"] = world / torch.cuda.device_count()
             if text_only:
                 return json.dumps(res)
             print(json.dumps(res), flush=True)

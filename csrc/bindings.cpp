@@ -7,6 +7,7 @@
 #include "comm/fake_pg.h"
 #include "comm/host_ring.h"
 #include "comm/rccl_pg.h"
+#include "comm/xgmi_pg.h"
 #include "ops/blaslt.h"
 #include "ops/nn_ops.h"
 #include "ops/ops.h"
@@ -299,7 +300,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("issued_count", &ReplayBeacon::issued_count)
       .def("completed", &ReplayBeacon::completed)
       .def_property_readonly("device", &ReplayBeacon::device);
-  py::class_<RcclPG, ProcessGroup, std::shared_ptr<RcclPG>>(m, "RcclPG")
+  py::class_<GpuPG, ProcessGroup, std::shared_ptr<GpuPG>>(m, "GpuPG")
+      .def_property_readonly("device", &GpuPG::device)
+      .def("aborted", &GpuPG::aborted)
+      .def("drain", &GpuPG::drain, py::call_guard<py::gil_scoped_release>())
+      .def("error_message", &GpuPG::error_message)
+      .def("set_timing", &GpuPG::set_timing)
+      .def("timing", &GpuPG::timing)
+      .def("same_stream", &GpuPG::same_stream)
+      .def("watch_beacon", &GpuPG::watch_beacon, py::arg("beacon"),
+           "watchdog-track the replays of a captured step through its ReplayBeacon")
+      .def("join_into",
+           [](GpuPG& pg, uint64_t stream) { pg.join_into(reinterpret_cast<hipStream_t>(stream)); },
+           py::arg("stream"), "make `stream` wait for the last eager op of this group")
+      .def("set_async_error_handling", &GpuPG::set_async_error_handling)
+      .def("backend_failure", &GpuPG::backend_failure)
+      .def("comm_stream_ptr", [](GpuPG& pg) { return reinterpret_cast<uintptr_t>(pg.comm_stream()); });
+  py::class_<RcclPG, GpuPG, std::shared_ptr<RcclPG>>(m, "RcclPG")
       .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int device,
                        int64_t timeout_ms) {
              py::gil_scoped_release nogil;
@@ -307,24 +324,33 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            }),
            py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"),
            py::arg("timeout_ms") = 600000)
-      .def_property_readonly("device", &RcclPG::device)
-      .def("aborted", &RcclPG::aborted)
-      .def("drain", &RcclPG::drain, py::call_guard<py::gil_scoped_release>())
-      .def("error_message", &RcclPG::error_message)
-      .def("set_timing", &RcclPG::set_timing)
       .def("p2p_max_bytes", &RcclPG::p2p_max_bytes)
-      .def("same_stream", &RcclPG::same_stream)
       .def("set_p2p_enabled", &RcclPG::set_p2p_enabled)
-      .def("watch_beacon", &RcclPG::watch_beacon, py::arg("beacon"),
-           "watchdog-track the replays of a captured step through its ReplayBeacon")
-      .def("timing", &RcclPG::timing)
-      .def("set_async_error_handling", &RcclPG::set_async_error_handling)
-      .def("comm_stream_ptr",
-           [](RcclPG& pg) { return reinterpret_cast<uintptr_t>(pg.comm_stream()); });
+      .def("split_with_timeout", &RcclPG::split_with_timeout, py::arg("ranks"), py::arg("tag"),
+           py::arg("timeout_ms"), py::call_guard<py::gil_scoped_release>());
+  // Own-kernel collectives over IPC-mapped peer memory: one node, ranks may share a GPU.
+  py::class_<XgmiPG, GpuPG, std::shared_ptr<XgmiPG>>(m, "XgmiPG")
+      .def(py::init([](std::shared_ptr<Store> store, int rank, int size, int device,
+                       int64_t timeout_ms) {
+             py::gil_scoped_release nogil;
+             return std::make_shared<XgmiPG>(std::move(store), rank, size, device, ms(timeout_ms));
+           }),
+           py::arg("store"), py::arg("rank"), py::arg("size"), py::arg("device"),
+           py::arg("timeout_ms") = 600000)
+      .def("config", [](XgmiPG& pg) {
+        const auto& c = pg.config();
+        py::dict d;
+        d["nblocks"] = c.nblocks;
+        d["slot_bytes"] = c.slot_bytes;
+        d["p2p_slot_bytes"] = c.p2p_slot_bytes;
+        d["oneshot_max"] = c.oneshot_max;
+        return d;
+      });
 
   // Exit guard (bench.py): a native thread that, unless cancelled within `seconds`, writes `text` to
-  // stdout and ends the process with status 0.  Native, so it fires even while the main thread is
-  // stuck inside a call that holds the GIL.
+  // stdout and ends the process with status 3 (a hang is never reported as success; the launcher
+  // and CI see the failure).  Native, so it fires even while the main thread is stuck inside a call
+  // that holds the GIL.
   {
     struct Guard {
       std::mutex mu;
@@ -348,8 +374,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                 off += n;
               }
             }
+            static const char kMsg[] = "[ringdp] exit guard fired: a phase stopped making progress; exiting with status 3\n";
+            (void)!::write(2, kMsg, sizeof(kMsg) - 1);
             std::fflush(stderr);
-            std::_Exit(0);
+            std::_Exit(3);
           }).detach();
         },
         py::arg("seconds"), py::arg("text"));
@@ -377,31 +405,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .value("FP16_COMPRESS", CommHook::FP16_COMPRESS)
       .value("PYTHON", CommHook::PYTHON)
       .value("NONE", CommHook::NONE);
-
-  // Standalone one-shot P2P all-reduce (tests; RcclPG owns one when enabled).  Ranks may share a
-  // GPU here - RCCL refuses that, IPC does not - which lets a one-GPU box run the multi-process path.
-  py::class_<P2PAllReduce, std::shared_ptr<P2PAllReduce>>(m, "P2PAllReduce")
-      .def(py::init([](std::shared_ptr<Store> store, int rank, int world, int device, int64_t max_bytes,
-                       int64_t timeout_ms) {
-             std::unique_ptr<P2PAllReduce> p;
-             {
-               py::gil_scoped_release nogil;
-               p = P2PAllReduce::create(store, rank, world, device, max_bytes, timeout_ms);
-             }
-             if (!p) throw RingdpError("[ringdp] P2P all-reduce setup failed on some rank");
-             return std::shared_ptr<P2PAllReduce>(std::move(p));
-           }),
-           py::arg("store"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("max_bytes"),
-           py::arg("timeout_ms"))
-      .def("eligible", &P2PAllReduce::eligible)
-      .def("run",
-           [](P2PAllReduce& p, at::Tensor t, bool average) {
-             RINGDP_CHECK(p.eligible(t), "P2PAllReduce.run: tensor not eligible (fp32/bf16, contiguous, 16-B multiple, <= max_bytes)");
-             p.run(t, average, c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.get_device()).stream());
-           },
-           py::arg("tensor"), py::arg("average") = false)
-      .def("failed", &P2PAllReduce::failed)
-      .def_property_readonly("max_bytes", &P2PAllReduce::max_bytes);
 
   py::class_<BucketStats>(m, "BucketStats")
       .def_readonly("numel", &BucketStats::numel)

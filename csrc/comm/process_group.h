@@ -68,7 +68,7 @@ class Work {
   int64_t start_us_;
   std::vector<at::Tensor> outputs_;
   friend class HostRingPG;
-  friend class RcclPG;
+  friend class GpuPG;
   friend class FakePG;
 };
 

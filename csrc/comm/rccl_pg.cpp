@@ -1,9 +1,6 @@
 // RCCL process group implementation (see rccl_pg.h).
 #include "rccl_pg.h"
 
-#include "../kernels/kernels.h"
-
-#include <ATen/hip/impl/HIPCachingAllocatorMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -52,104 +49,24 @@ ncclRedOp_t to_nccl_op(ReduceOp op) {
   }
 }
 
-namespace {
-
-bool env_flag(const char* name, bool dflt) {
-  const char* v = std::getenv(name);
-  if (!v || !*v) return dflt;
-  return !(std::strcmp(v, "0") == 0 || std::strcmp(v, "false") == 0);
-}
-
-class DeviceScope {
- public:
-  explicit DeviceScope(int dev) {
-    hipGetDevice(&prev_);
-    if (prev_ != dev) hipSetDevice(dev);
+int to_xg_dtype(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return kern::XG_F32;
+    case at::kBFloat16: return kern::XG_BF16;
+    case at::kHalf: return kern::XG_F16;
+    case at::kDouble: return kern::XG_F64;
+    case at::kInt: return kern::XG_I32;
+    case at::kLong: return kern::XG_I64;
+    case at::kChar: return kern::XG_I8;
+    case at::kByte: return kern::XG_U8;
+    case at::kBool: return kern::XG_U8;
+    default: return -1;
   }
-  ~DeviceScope() { hipSetDevice(prev_); }
-
- private:
-  int prev_ = 0;
-};
-
-}  // namespace
-
-// ------------------------------------------------------------------ RcclWork
-RcclWork::RcclWork(OpType op, uint64_t seq, RcclPG* pg, bool captured, bool timing)
-    : Work(op, seq), captured_(captured), pg_(pg) {
-  RINGDP_HIP_CHECK(hipEventCreateWithFlags(&done_, timing ? hipEventDefault
-                                                           : hipEventDisableTiming));
-  if (timing) RINGDP_HIP_CHECK(hipEventCreateWithFlags(&start_, hipEventDefault));
-}
-
-RcclWork::~RcclWork() {
-  if (done_) hipEventDestroy(done_);
-  if (start_) hipEventDestroy(start_);
-}
-
-bool RcclWork::is_completed() {
-  if (captured_) return false;
-  return hipEventQuery(done_) == hipSuccess;
-}
-
-void RcclWork::wait(bool blocking) {
-  if (pg_->aborted())
-    throw RingdpError("[ringdp] RCCL communicator aborted: " + pg_->error_message());
-  HipStream cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(pg_->device());
-  RINGDP_HIP_CHECK(hipStreamWaitEvent(cur.stream(), done_, 0));
-  if (blocking && !captured_) {
-    auto deadline = now_us() + pg_->timeout().count() * 1000;
-    while (hipEventQuery(done_) == hipErrorNotReady) {
-      if (pg_->aborted())
-        throw RingdpError("[ringdp] RCCL communicator aborted: " + pg_->error_message());
-      if (now_us() > deadline)
-        throw TimeoutError(strcat_all("[ringdp] RCCL ", op_name(op_), " seq ", seq_,
-                                      " timed out after ", pg_->timeout().count(), " ms"));
-      std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-  }
-}
-
-double RcclWork::duration_us() {
-  if (!start_ || captured_) return -1.0;
-  if (hipEventQuery(done_) != hipSuccess) return -1.0;
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, start_, done_) != hipSuccess) return -1.0;
-  return static_cast<double>(ms) * 1000.0;
-}
-
-// ------------------------------------------------------------------ ReplayBeacon
-ReplayBeacon::ReplayBeacon(int device) : device_(device) {
-  DeviceScope ds(device_);
-  RINGDP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_), sizeof(*host_),
-                                 hipHostMallocCoherent | hipHostMallocMapped));
-  *host_ = 0;
-  RINGDP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&dev_), sizeof(*dev_)));
-  RINGDP_HIP_CHECK(hipMemset(dev_, 0, sizeof(*dev_)));
-  RINGDP_HIP_CHECK(hipDeviceSynchronize());
-}
-
-ReplayBeacon::~ReplayBeacon() {
-  DeviceScope ds(device_);
-  (void)hipDeviceSynchronize();  // no replay may still write the counters
-  if (dev_) (void)hipFree(dev_);
-  if (host_) (void)hipHostFree(host_);
-}
-
-void ReplayBeacon::mark(hipStream_t stream) {
-  unsigned long long* hdev = nullptr;
-  RINGDP_HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&hdev), host_, 0));
-  kern::replay_beacon_mark(dev_, hdev, stream);
-  RINGDP_HIP_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------------------ RcclPG
-RcclPG::RcclPG(std::shared_ptr<Store> store, int rank, int size, int device,
-               std::chrono::milliseconds timeout)
-    : ProcessGroup(rank, size),
-      device_(device),
-      timeout_(timeout),
-      comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(env_flag("RINGDP_COMM_HIGH_PRIORITY", false), device)) {
+RcclPG::RcclPG(std::shared_ptr<Store> store, int rank, int size, int device, std::chrono::milliseconds timeout)
+    : GpuPG(rank, size, device, timeout), store_(store) {
   DeviceScope ds(device_);
   ncclUniqueId uid;
   if (rank == 0) {
@@ -161,228 +78,83 @@ RcclPG::RcclPG(std::shared_ptr<Store> store, int rank, int size, int device,
     std::memcpy(&uid, s.data(), sizeof(uid));
   }
   RINGDP_NCCL_CHECK(ncclCommInitRank(&comm_, size, uid, rank));
-  if (const char* e = std::getenv("RINGDP_P2P_ALLREDUCE_MAX_BYTES")) {
-    const int64_t max_bytes = std::atoll(e);
-    if (max_bytes > 0) {
-      // the kernel's own spin bound: the group timeout, capped so a dead peer ends it in minutes
-      const int64_t tmo = std::min<int64_t>(timeout_.count(), 300000);
-      p2p_ = P2PAllReduce::create(store, rank, size, device, max_bytes, tmo);
-      if (!p2p_ && rank == 0)
-        std::fprintf(stderr, "[ringdp] P2P all-reduce unavailable for this group (not one host, >8 ranks, "
-                             "or IPC setup failed); using RCCL for every size\n");
-    }
-  }
-  init_common();
-}
-
-RcclPG::RcclPG(ncclComm_t comm, int rank, int size, int device, std::chrono::milliseconds timeout)
-    : ProcessGroup(rank, size),
-      comm_(comm),
-      device_(device),
-      timeout_(timeout),
-      comm_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(env_flag("RINGDP_COMM_HIGH_PRIORITY", false), device)) {
-  init_common();
-}
-
-void RcclPG::init_common() {
-  DeviceScope ds(device_);
+  setup_small_path(store);
   // Collectives of a one-rank group have nothing to overlap with, and a side-stream fork/join inside
   // a hipGraph is not free on ROCm 7 (ResNet-18 step: 3.52 ms forked vs 3.10 ms on the compute
   // stream, ConvNet unchanged): one-rank groups issue on the caller's stream.
-  // RINGDP_COMM_SAME_STREAM=1 / 0 forces either choice for any group size.
-  if (const char* v = std::getenv("RINGDP_COMM_SAME_STREAM"))
-    same_stream_ = std::strcmp(v, "1") == 0;
-  else
-    same_stream_ = size_ == 1;
-  RINGDP_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
-  timing_ = env_flag("RINGDP_COMM_TIMING", false);
-  async_error_handling_ = env_flag("RINGDP_ASYNC_ERROR_HANDLING", true);
-  watchdog_ = std::thread([this] { watchdog_loop(); });
+  init_common(size == 1);
+}
+
+RcclPG::RcclPG(ncclComm_t comm, std::shared_ptr<Store> store, int rank, int size, int device,
+               std::chrono::milliseconds timeout)
+    : GpuPG(rank, size, device, timeout), comm_(comm), store_(store) {
+  if (store) setup_small_path(store);
+  init_common(size == 1);
+}
+
+void RcclPG::setup_small_path(const std::shared_ptr<Store>& store) {
+  const char* e = std::getenv("RINGDP_P2P_ALLREDUCE_MAX_BYTES");
+  const int64_t max_bytes = e ? std::atoll(e) : 0;
+  if (max_bytes <= 0) return;
+  XgmiConfig cfg = XgmiConfig::from_env();
+  // one-shot only: the slot must hold the largest routed message
+  cfg.slot_bytes = std::max(cfg.slot_bytes, (max_bytes + 15) / 16 * 16);
+  cfg.oneshot_max = cfg.slot_bytes;
+  cfg.p2p_slot_bytes = 16;
+  auto sub = std::make_shared<PrefixStore>("xgmi_small", store);
+  std::string why;
+  xg_ = XgmiEngine::create(sub, rank_, size_, device_, cfg, timeout_.count(), &why);
+  p2p_max_bytes_ = max_bytes;
+  if (!xg_ && rank_ == 0)
+    std::fprintf(stderr, "[ringdp] xGMI small-message all-reduce unavailable for this group (%s); "
+                         "using RCCL for every size\n", why.c_str());
 }
 
 RcclPG::~RcclPG() { shutdown(); }
 
 void RcclPG::shutdown() {
-  if (stop_.exchange(true)) return;
-  wd_cv_.notify_all();
-  if (watchdog_.joinable()) watchdog_.join();
+  stop_common();
   if (comm_) {
     DeviceScope ds(device_);
-    if (!aborted_.load()) {
-      (void)hipStreamSynchronize(comm_stream_.stream());
-      ncclCommDestroy(comm_);
-    }
+    if (!aborted_.load()) ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
-  inflight_.clear();
-  if (p2p_) {
-    DeviceScope ds(device_);
-    (void)hipStreamSynchronize(comm_stream_.stream());
-    p2p_.reset();
-  }
-  if (ready_) {
-    hipEventDestroy(ready_);
-    ready_ = nullptr;
-  }
+  xg_.reset();
 }
 
-void RcclPG::drain() {
-  std::lock_guard<std::mutex> lk(wd_mu_);
-  DeviceScope ds(device_);
-  for (auto& w : inflight_) (void)hipEventSynchronize(w->done_);
-  inflight_.clear();
+void RcclPG::abort_backend() {
+  if (comm_) ncclCommAbort(comm_);
 }
 
-void RcclPG::watch_beacon(const std::shared_ptr<ReplayBeacon>& beacon) {
-  std::lock_guard<std::mutex> bl(beacon_mu_);
-  beacon->last_done_ = beacon->completed();
-  beacon->progress_us_ = now_us();
-  beacons_.push_back(beacon);
+std::string RcclPG::backend_failure() {
+  if (xg_ && xg_->failed()) return "xGMI small-message all-reduce: a peer did not arrive within the timeout";
+  return "";
 }
 
-void RcclPG::abort() {
-  if (comm_ && !aborted_.exchange(true)) {
-    ncclCommAbort(comm_);
-  }
-  aborted_.store(true);
-}
-
-void RcclPG::fail(const std::string& msg) {
-  {
-    std::lock_guard<std::mutex> lk(wd_mu_);
-    error_ = msg;
-  }
-  std::fprintf(stderr, "%s\n", msg.c_str());
-  std::fflush(stderr);
-  if (comm_ && !aborted_.exchange(true)) ncclCommAbort(comm_);
-  if (async_error_handling_) {
-    std::fprintf(stderr,
-                 "[ringdp] rank %d: tearing the process down after a communicator failure "
-                 "(set RINGDP_ASYNC_ERROR_HANDLING=0 to raise instead)\n",
-                 rank_);
-    std::fflush(stderr);
-    std::_Exit(1);
-  }
-}
-
-void RcclPG::watchdog_loop() {
-  hipSetDevice(device_);
-  while (!stop_.load()) {
-    {
-      std::unique_lock<std::mutex> lk(wd_mu_);
-      wd_cv_.wait_for(lk, std::chrono::milliseconds(50), [&] { return stop_.load(); });
-    }
-    if (stop_.load() || aborted_.load()) break;
-    std::string failure;
-    {
-      std::lock_guard<std::mutex> lk(wd_mu_);
-      int64_t now = now_us();
-      while (!inflight_.empty()) {
-        auto& w = inflight_.front();
-        hipError_t q = hipEventQuery(w->done_);
-        if (q == hipSuccess) {
-          inflight_.pop_front();
-          continue;
-        }
-        if (now > w->deadline_us_) {
-          failure = strcat_all("[ringdp] watchdog: rank ", rank_, " RCCL ", op_name(w->op()),
-                               " (seq ", w->seq(), ") did not complete within ",
-                               timeout_.count(), " ms; aborting communicator");
-        }
-        // Entries are queued in issue order with deadlines in the same order: an incomplete
-        // head that is within its deadline means everything behind it is too.
-        break;
-      }
-    }
-    if (failure.empty()) {
-      // captured steps: plain loads of the replay beacons (no HIP call on this thread)
-      std::lock_guard<std::mutex> bl(beacon_mu_);
-      const int64_t now = now_us();
-      for (auto it = beacons_.begin(); it != beacons_.end();) {
-        auto b = it->lock();
-        if (!b) {
-          it = beacons_.erase(it);
-          continue;
-        }
-        const uint64_t done = b->completed(), issued = b->issued_count();
-        if (done >= issued || done != b->last_done_) {
-          b->last_done_ = done;
-          b->progress_us_ = now;  // idle, or a replay finished since the last look
-        } else if (now - b->progress_us_ > timeout_.count() * 1000) {
-          failure = strcat_all("[ringdp] watchdog: rank ", rank_, " ", op_name(OpType::GRAPH_REPLAY), " ",
-                               done + 1, " of ", issued, " did not complete within ", timeout_.count(),
-                               " ms; aborting communicator");
-          break;
-        }
-        ++it;
-      }
-    }
-    if (failure.empty() && p2p_ && p2p_->failed()) {
-      failure = strcat_all("[ringdp] watchdog: rank ", rank_, " P2P all-reduce: a peer did not arrive "
-                           "within the timeout; aborting communicator");
-    }
-    if (failure.empty() && comm_) {
-      ncclResult_t async_err = ncclSuccess;
-      if (ncclCommGetAsyncError(comm_, &async_err) == ncclSuccess && async_err != ncclSuccess &&
-          async_err != ncclInProgress) {
-        failure = strcat_all("[ringdp] watchdog: rank ", rank_, " RCCL async error: ",
-                             ncclGetErrorString(async_err));
-      }
-    }
-    if (!failure.empty()) fail(failure);
-  }
-}
-
-void RcclPG::check_tensor(const at::Tensor& t, const char* what) const {
-  RINGDP_CHECK(t.is_cuda(), what, ": rccl backend expects GPU tensors, got ", t.device());
-  RINGDP_CHECK(t.get_device() == device_, what, ": tensor on device ", t.get_device(),
-               " but process group is bound to device ", device_);
-  RINGDP_CHECK(t.is_contiguous(), what, ": tensor must be contiguous");
-}
-
-template <typename Fn>
-std::shared_ptr<Work> RcclPG::launch(OpType op, const std::vector<at::Tensor>& tensors, Fn&& body) {
-  RINGDP_CHECK(!aborted_.load(), "RCCL communicator was aborted: ", error_message());
-  RINGDP_CHECK(comm_ != nullptr, "process group has been shut down");
-  std::lock_guard<std::mutex> lk(launch_mu_);
-  DeviceScope ds(device_);
-  HipStream cur = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_);
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  RINGDP_HIP_CHECK(hipStreamIsCapturing(cur.stream(), &cap));
-  const bool captured = cap == hipStreamCaptureStatusActive;
-  auto work = std::make_shared<RcclWork>(op, next_seq(), this, captured, timing_ && !captured);
-  const bool same_stream = same_stream_;
-  hipStream_t cs = same_stream ? cur.stream() : comm_stream_.stream();
-  // Fence: the comm stream waits for everything queued so far on the producer stream.
-  if (!same_stream) {
-    RINGDP_HIP_CHECK(hipEventRecord(ready_, cur.stream()));
-    RINGDP_HIP_CHECK(hipStreamWaitEvent(cs, ready_, 0));
-  }
-  if (work->start_) RINGDP_HIP_CHECK(hipEventRecord(work->start_, cs));
-  for (auto& t : tensors) {
-    if (!same_stream && t.defined() && t.is_cuda() && t.numel() > 0)
-      c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(
-          t.storage().data_ptr(), comm_stream_);
-  }
-  body(cs);
-  RINGDP_HIP_CHECK(hipEventRecord(work->done_, cs));
-  work->outputs_ = tensors;
-  if (!captured) {
-    work->deadline_us_ = now_us() + timeout_.count() * 1000;
-    std::lock_guard<std::mutex> wl(wd_mu_);
-    inflight_.push_back(work);
-  }
-  return work;
+std::string RcclPG::poll_async_error() {
+  std::string f = backend_failure();
+  if (!f.empty() || !comm_) return f;
+  ncclResult_t async_err = ncclSuccess;
+  if (ncclCommGetAsyncError(comm_, &async_err) == ncclSuccess && async_err != ncclSuccess &&
+      async_err != ncclInProgress)
+    return strcat_all("RCCL async error: ", ncclGetErrorString(async_err));
+  return "";
 }
 
 std::shared_ptr<Work> RcclPG::allreduce(std::vector<at::Tensor>& tensors, ReduceOp op) {
   for (auto& t : tensors) check_tensor(t, "all_reduce");
-  if (p2p_ && p2p_on_ && tensors.size() == 1 && (op == ReduceOp::SUM || op == ReduceOp::AVG) &&
-      p2p_->eligible(tensors[0])) {
-    // small bucket on one xGMI node: one-shot read of every peer instead of 2(N-1) ring steps
-    return launch(OpType::ALLREDUCE, tensors, [&](hipStream_t s) {
-      p2p_->run(tensors[0], op == ReduceOp::AVG, s);
-    });
+  RINGDP_CHECK(comm_ != nullptr, "process group has been shut down");
+  if (xg_ && p2p_on_ && tensors.size() == 1 && (op == ReduceOp::SUM || op == ReduceOp::AVG)) {
+    at::Tensor& t = tensors[0];
+    const int64_t nb = t.numel() * static_cast<int64_t>(t.element_size());
+    const int dt = to_xg_dtype(t.scalar_type());
+    if (dt >= 0 && t.scalar_type() != at::kBool && nb > 0 && nb <= p2p_max_bytes_ &&
+        reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0) {
+      // small bucket on one xGMI node: one push to every peer + one handshake instead of 2(N-1) ring steps
+      return launch(OpType::ALLREDUCE, tensors, [&](hipStream_t s) {
+        xg_->allreduce(t.data_ptr(), t.data_ptr(), nb, dt, kern::XG_SUM, op == ReduceOp::AVG, s);
+      });
+    }
   }
   auto red = to_nccl_op(op);
   return launch(OpType::ALLREDUCE, tensors, [&](hipStream_t s) {
@@ -615,7 +387,12 @@ std::shared_ptr<Work> RcclPG::coalesced(std::vector<CollOp>& ops) {
   });
 }
 
-std::shared_ptr<ProcessGroup> RcclPG::split(const std::vector<int>& ranks, const std::string&) {
+std::shared_ptr<ProcessGroup> RcclPG::split(const std::vector<int>& ranks, const std::string& tag) {
+  return split_with_timeout(ranks, tag, 0);
+}
+
+std::shared_ptr<ProcessGroup> RcclPG::split_with_timeout(const std::vector<int>& ranks, const std::string& tag,
+                                                         int64_t timeout_ms) {
   int new_rank = -1;
   for (size_t i = 0; i < ranks.size(); ++i)
     if (ranks[i] == rank_) new_rank = static_cast<int>(i);
@@ -625,7 +402,11 @@ std::shared_ptr<ProcessGroup> RcclPG::split(const std::vector<int>& ranks, const
   RINGDP_NCCL_CHECK(ncclCommSplit(comm_, new_rank >= 0 ? 0 : NCCL_SPLIT_NOCOLOR,
                                   new_rank >= 0 ? new_rank : rank_, &nc, nullptr));
   if (new_rank < 0) return nullptr;
-  return std::make_shared<RcclPG>(nc, new_rank, static_cast<int>(ranks.size()), device_, timeout_);
+  // the child's own timeout and (when enabled) its own xGMI small-message path, through a store
+  // namespace of its own
+  auto child_store = store_ ? std::make_shared<PrefixStore>("split/" + tag, store_) : nullptr;
+  const auto tmo = timeout_ms > 0 ? std::chrono::milliseconds(timeout_ms) : timeout_;
+  return std::make_shared<RcclPG>(nc, child_store, new_rank, static_cast<int>(ranks.size()), device_, tmo);
 }
 
 }  // namespace ringdp

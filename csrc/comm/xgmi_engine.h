@@ -1,0 +1,80 @@
+// xGMI collective engine: IPC-mapped symmetric staging memory + the kernels of csrc/kernels/xgmi.hip.
+//
+// Owned by an XgmiPG (every collective) or by an RcclPG (small all-reduces, when
+// RINGDP_P2P_ALLREDUCE_MAX_BYTES > 0).  Creation is collective over the group: every rank allocates an
+// uncached staging buffer and a flag block on its GPU, exports both by IPC handle through the store,
+// maps every peer's, and all ranks agree through the store that every one of them succeeded.  Ranks
+// may share a GPU (IPC within one device).  Every op is stream-ordered on the stream it is given,
+// hipGraph-capturable (epochs live in device memory), and issues exactly `nblocks` workgroups.
+//
+// Staging layout (each rank, one allocation):
+//   region A  [2 parities][world][slot]   one-shot / reduce-scatter / all-gather / broadcast inbound
+//   region B  [2 parities][world][slot]   two-shot all-gather inbound
+//   region P  [16 sources][2 parities][p2p_slot]   send/recv
+// Messages larger than a slot are cut into pieces, each one op (one epoch).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../kernels/kernels.h"
+#include "../store/store.h"
+
+namespace ringdp {
+
+struct XgmiConfig {
+  int nblocks = 64;                  // RINGDP_XGMI_BLOCKS
+  int64_t slot_bytes = 4 << 20;      // RINGDP_XGMI_SLOT_MB
+  int64_t p2p_slot_bytes = 1 << 20;  // RINGDP_XGMI_P2P_SLOT_MB
+  int64_t oneshot_max = 512 << 10;   // RINGDP_XGMI_ONESHOT_KB: all-reduces up to this size are one-shot
+  static XgmiConfig from_env();
+};
+
+class XgmiEngine {
+ public:
+  // nullptr on every rank when the path cannot be used (ranks on different hosts, more than 16
+  // ranks, an allocation or IPC failure on any rank); `why` says which.
+  static std::unique_ptr<XgmiEngine> create(const std::shared_ptr<Store>& store, int rank, int world,
+                                            int device, const XgmiConfig& cfg, int64_t timeout_ms,
+                                            std::string* why = nullptr);
+  ~XgmiEngine();
+
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  const XgmiConfig& config() const { return cfg_; }
+
+  // dtype: kern::XgDtype; red: kern::XgRed.  Pointers 16-B aligned, sizes in bytes.
+  // In place (in == out allowed).
+  void allreduce(const void* in, void* out, int64_t nbytes, int dtype, int red, bool average,
+                 hipStream_t s);
+  // in: world blocks of block_bytes (multiple of 16), out: block_bytes.
+  void reduce_scatter(const void* in, void* out, int64_t block_bytes, int dtype, int red, bool average,
+                      hipStream_t s);
+  // in: block_bytes, out: world blocks of block_bytes (multiple of 16).
+  void allgather(const void* in, void* out, int64_t block_bytes, hipStream_t s);
+  void broadcast(const void* in, void* out, int64_t nbytes, int root, hipStream_t s);
+  void send(const void* in, int64_t nbytes, int dst, hipStream_t s);
+  void recv(void* out, int64_t nbytes, int src, hipStream_t s);
+  void barrier(hipStream_t s);
+
+  // Host-side check of the kernels' timeout word (true: some peer did not arrive in time).
+  bool failed() const;
+
+ private:
+  XgmiEngine() = default;
+  void launch(kern::XgArgs& a, hipStream_t s);
+
+  int rank_ = 0, world_ = 1, device_ = 0;
+  XgmiConfig cfg_;
+  char* stage_ = nullptr;
+  unsigned* flags_ = nullptr;
+  unsigned* epochs_ = nullptr;
+  int* error_ = nullptr;  // hipHostMalloc'd, mapped
+  std::vector<void*> opened_;
+  kern::XgArgs base_{};
+};
+
+}  // namespace ringdp

@@ -44,25 +44,50 @@ void sgd_multi(const SgdTensor* table, const int64_t* chunks, int64_t nchunks, i
 // Deterministic split-K reduction: out[i] = sum_s slabs[s * n + i] (fixed order).
 void splitk_reduce(const float* slabs, int nslices, int64_t n, float* out, hipStream_t s);
 
-// ---------------------------------------------------------------- one-shot P2P all-reduce
-// (p2p.hip; host side csrc/comm/p2p_allreduce.cpp)
-constexpr int kP2PMaxRanks = 8;
-struct P2PArgs {
-  char* bufs[kP2PMaxRanks];       // staging buffer of every rank (IPC-mapped), 2 slots each
-  unsigned* flags[kP2PMaxRanks];  // flag block of every rank: [segment][source rank]
-  void* data;                     // in/out tensor (local)
-  unsigned* epochs;               // local per-segment epoch counters
-  int* error;                     // local: set when a peer did not arrive in time
-  int64_t nbytes;                 // multiple of 16
-  int64_t slot_bytes;             // bytes per staging slot
-  int seg_bytes;                  // bytes per workgroup segment (multiple of 16)
+// ---------------------------------------------------------------- xGMI collectives (xgmi.hip)
+// Collectives over IPC-mapped peer staging memory; host side csrc/comm/xgmi_engine.cpp.
+constexpr int kXgMaxRanks = 16;
+constexpr int kXgThreads = 256;
+constexpr int kXgSeg = kXgThreads * 16;  // bytes one workgroup moves per pass
+enum XgKind : int {
+  XG_BARRIER = 0,
+  XG_ONESHOT = 1,         // all-reduce: push everything to everyone, local rank-order reduce
+  XG_TWOSHOT = 2,         // all-reduce: reduce-scatter by push + all-gather by push
+  XG_REDUCE_SCATTER = 3,
+  XG_ALLGATHER = 4,
+  XG_BROADCAST = 5,
+  XG_SEND = 6,
+  XG_RECV = 7,
+};
+enum XgDtype : int { XG_F32 = 0, XG_BF16, XG_F16, XG_F64, XG_I32, XG_I64, XG_I8, XG_U8 };
+enum XgRed : int { XG_SUM = 0, XG_PROD, XG_MIN, XG_MAX };
+struct XgArgs {
+  char* stage[kXgMaxRanks];      // staging buffer of every rank (IPC-mapped; [rank] = mine)
+  unsigned* flags[kXgMaxRanks];  // flag block of every rank (IPC-mapped)
+  unsigned* epochs;              // local: [G] collective, [16][G] send per peer, [16][G] recv per peer
+  int* error;                    // device address of a host-mapped word: set when a peer never arrived
+  uint64_t timeout_ticks;        // wall_clock64 ticks (100 MHz)
   int world;
   int rank;
-  int dtype;                      // 0 fp32, 1 bf16
-  float scale;                    // 1 (sum) or 1/world (average)
-  uint64_t timeout_ticks;         // wall_clock64 ticks (100 MHz)
+  int nblocks;                   // G: fixed for the group (segment ownership must not change)
+  int64_t slot;                  // bytes per (parity, source) slot of regions A and B
+  int64_t p2p_slot;              // bytes per (source, parity) slot of the send/recv region
+  int64_t off_a, off_b, off_p2p; // region offsets inside every staging buffer
+  // the op
+  int kind;
+  int dtype;
+  int red;
+  int average;                   // divide by world (float: * scale)
+  float scale;
+  int root;                      // broadcast
+  int peer;                      // send: destination, recv: source
+  const char* in;
+  char* out;
+  int64_t nbytes;                // oneshot/twoshot/broadcast/send/recv: message; RS/AG: per-rank block
+  int64_t chunk;                 // twoshot: per-rank chunk (multiple of 16)
+  int64_t stride;                // RS: input block stride, AG: output block stride (bytes)
 };
-void p2p_allreduce(const P2PArgs& a, hipStream_t s);
+void xgmi_collective(const XgArgs& a, hipStream_t s);
 
 // ---------------------------------------------------------------- fp32 NCHW conv / pool (conv_f32.hip)
 // stride-1 conv, square kernel R, symmetric zero padding; fc layers are R=1 convs over 1x1 images

@@ -11,7 +11,9 @@ API parity target: ``torch.distributed`` as exercised by the reference
 * ``get_rank/get_world_size/new_group/barrier/all_reduce/broadcast/all_gather/...`` with global
   ranks in src/dst arguments, ``async_op`` returning a Work whose ``wait()`` fences the caller's
   stream (GPU) or blocks (CPU).
-* backends: ``"nccl"``/``"rccl"`` -> RCCL over xGMI (GPU tensors), ``"gloo"``/``"host"`` -> the
+* backends: ``"nccl"``/``"rccl"`` -> RCCL over xGMI (GPU tensors), ``"xgmi"`` -> ringdp's own
+  collective kernels over IPC-mapped peer memory (GPU tensors, ranks on one node, which may share a
+  GPU; ``RINGDP_GPU_BACKEND=xgmi`` makes ``"nccl"`` select it), ``"gloo"``/``"host"`` -> the
   native host ring (CPU tensors; GPU tensors are staged through host memory),
   ``None``/``"cpu:gloo,cuda:nccl"`` -> both, dispatched on the tensor's device.
 
@@ -48,12 +50,23 @@ default_pg_timeout = _dt.timedelta(minutes=30)
 default_pg_nccl_timeout = _dt.timedelta(minutes=10)
 
 _GPU_BACKENDS = ("nccl", "rccl")
+_GPU_KINDS = ("rccl", "xgmi")  # native GPU process-group kinds
+
+
+def _gpu_kind_for_nccl() -> str:
+    """What "nccl"/"rccl" maps to: RCCL, unless RINGDP_GPU_BACKEND=xgmi selects ringdp's own
+    collective kernels over IPC-mapped peer memory (one node; ranks may share a GPU)."""
+    v = os.environ.get("RINGDP_GPU_BACKEND", "rccl").strip().lower()
+    if v not in _GPU_KINDS:
+        raise ValueError(f"ringdp: RINGDP_GPU_BACKEND must be 'rccl' or 'xgmi', got {v!r}")
+    return v
 _CPU_BACKENDS = ("gloo", "host", "host_ring", "cpu")
 
 
 class Backend:
     NCCL = "nccl"
     RCCL = "rccl"
+    XGMI = "xgmi"  # ringdp's own collective kernels over IPC-mapped peer memory (one node)
     GLOO = "gloo"
     HOST = "host"
     FAKE = "fake"  # collectives are no-ops (upstream fake_pg.py): single-process tests as rank r of N
@@ -62,21 +75,25 @@ class Backend:
     def normalize(backend: Optional[str]) -> Dict[str, str]:
         """Returns {device_type: native backend} for a user backend string."""
         if backend is None or backend == "undefined":
-            return {"cpu": "host", "cuda": "rccl"}
+            return {"cpu": "host", "cuda": _gpu_kind_for_nccl()}
         b = str(backend).lower()
         if ":" in b:
             out = {}
             for part in b.split(","):
                 dev, name = part.split(":")
-                out[dev.strip()] = "rccl" if name.strip() in _GPU_BACKENDS else "host"
+                name = name.strip()
+                out[dev.strip()] = (_gpu_kind_for_nccl() if name in _GPU_BACKENDS else
+                                    "xgmi" if name == "xgmi" else "host")
             return out
         if b in _GPU_BACKENDS:
-            return {"cuda": "rccl"}
+            return {"cuda": _gpu_kind_for_nccl()}
+        if b in ("xgmi", "ipc"):
+            return {"cuda": "xgmi"}
         if b in _CPU_BACKENDS:
             return {"cpu": "host", "cuda": "host"}
         if b == "fake":
             return {"cpu": "fake", "cuda": "fake"}
-        raise ValueError(f"ringdp: unknown backend {backend!r} (use 'nccl', 'rccl', 'gloo', 'host', 'fake')")
+        raise ValueError(f"ringdp: unknown backend {backend!r} (use 'nccl', 'rccl', 'xgmi', 'gloo', 'host', 'fake')")
 
 
 def _to_reduce_op(op) -> "C.ReduceOp":
@@ -116,7 +133,7 @@ class ProcessGroup:
         self._bind_hint = bind_hint
         self._host = None
         self._fake = None
-        self._rccl: Dict[int, Any] = {}
+        self._gpu: Dict[int, Any] = {}  # device -> native GPU process group (RcclPG / XgmiPG)
         self._lock = threading.Lock()
         self._coll_count = 0
 
@@ -154,16 +171,24 @@ class ProcessGroup:
                 self._host = C.HostRingPG(sub, self._rank, self._size, self.timeout_ms, self._bind_hint)
             return self._host
 
-    def rccl(self, device: int):
+    def gpu(self, device: int):
+        """The native GPU process group of this group on ``device`` (created on first use; collective
+        over the group's members)."""
         with self._lock:
-            pg = self._rccl.get(device)
+            pg = self._gpu.get(device)
             if pg is None:
+                kind = self._backends.get("cuda", "rccl")
+                if kind not in _GPU_KINDS:
+                    kind = "rccl"
                 if not torch.cuda.is_available():
-                    raise RuntimeError("ringdp: the rccl backend needs a GPU (torch.cuda.is_available() is False)")
-                sub = C.PrefixStore(f"{self.group_name}/rccl/{device}", self._store)
-                pg = C.RcclPG(sub, self._rank, self._size, device, self.timeout_ms)
-                self._rccl[device] = pg
+                    raise RuntimeError(f"ringdp: the {kind} backend needs a GPU (torch.cuda.is_available() is False)")
+                sub = C.PrefixStore(f"{self.group_name}/{kind}/{device}", self._store)
+                cls = C.RcclPG if kind == "rccl" else C.XgmiPG
+                pg = cls(sub, self._rank, self._size, device, self.timeout_ms)
+                self._gpu[device] = pg
             return pg
+
+    rccl = gpu  # older name
 
     def native_for(self, tensor: torch.Tensor):
         """(native process group, staged-through-host?) for a tensor."""
@@ -178,8 +203,8 @@ class ProcessGroup:
                 if self._fake is None:
                     self._fake = C.FakePG(self._rank, self._size)
             return self._fake, False
-        if kind == "rccl":
-            return self.rccl(tensor.device.index if tensor.device.index is not None else torch.cuda.current_device()), False
+        if kind in _GPU_KINDS:
+            return self.gpu(tensor.device.index if tensor.device.index is not None else torch.cuda.current_device()), False
         return self.host(), tensor.is_cuda
 
     def local_rank_of(self, global_rank: int) -> int:
@@ -191,9 +216,9 @@ class ProcessGroup:
     def shutdown(self):
         with self._lock:
             self._fake = None
-            for pg in self._rccl.values():
+            for pg in self._gpu.values():
                 pg.shutdown()
-            self._rccl.clear()
+            self._gpu.clear()
             if self._host is not None:
                 self._host.shutdown()
                 self._host = None
@@ -339,7 +364,7 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
         raise ValueError("trying to initialize the default process group twice!")
     backends = Backend.normalize(backend)
     if timeout is None:
-        timeout = default_pg_nccl_timeout if set(backends.values()) == {"rccl"} else default_pg_timeout
+        timeout = default_pg_nccl_timeout if set(backends.values()) <= set(_GPU_KINDS) else default_pg_timeout
     if set(backends.values()) == {"fake"} and store is None and init_method is None:
         # upstream: init_process_group("fake") short-circuits the rendezvous
         if rank < 0 or world_size <= 0:
@@ -428,6 +453,8 @@ def get_backend(group: Optional[ProcessGroup] = None) -> str:
     kinds = set(g._backends.values())
     if kinds == {"rccl"}:
         return "nccl"
+    if kinds == {"xgmi"}:
+        return "xgmi"
     if kinds == {"host"}:
         return "gloo"
     if kinds == {"fake"}:
@@ -463,16 +490,18 @@ def new_group(ranks: Optional[Sequence[int]] = None, timeout: Optional[_dt.timed
     # (every rank takes part in the split, non-members with NCCL_SPLIT_NOCOLOR), otherwise they are
     # created lazily through the store on first use.
     split = {}
-    if "rccl" in backends.values() and os.environ.get("RINGDP_COMM_SPLIT", "1") == "1":
-        for dev, parent in sorted(world._rccl.items()):
-            split[dev] = parent.split(ranks, name)
+    if backends.get("cuda") == "rccl" and os.environ.get("RINGDP_COMM_SPLIT", "1") == "1":
+        for dev, parent in sorted(world._gpu.items()):
+            if isinstance(parent, C.RcclPG):
+                tmo_ms = int(timeout.total_seconds() * 1000) if timeout is not None else 0
+                split[dev] = parent.split_with_timeout(ranks, name, tmo_ms)
     if me not in ranks:
         return GroupMember.NON_GROUP_MEMBER
     pg = ProcessGroup(_world.store, ranks.index(me), len(ranks), backends, timeout or world._timeout,
                       ranks, name, _world.bind_hint)
     for dev, child in split.items():
         if child is not None:
-            pg._rccl[dev] = child
+            pg._gpu[dev] = child
     _world.groups[name] = pg
     return pg
 
@@ -763,10 +792,10 @@ def barrier(group=None, async_op: bool = False, device_ids=None):
         return None
     g = _resolve(group)
     _pre(g, "barrier", [])
-    use_gpu = "rccl" in g._backends.values() and "host" not in g._backends.values() and torch.cuda.is_available()
+    use_gpu = g._backends.get("cuda") in _GPU_KINDS and "host" not in g._backends.values() and torch.cuda.is_available()
     if use_gpu:
         dev = device_ids[0] if device_ids else torch.cuda.current_device()
-        w = g.rccl(dev).barrier()
+        w = g.gpu(dev).barrier()
     else:
         w = g.host().barrier()
     if async_op:
@@ -945,4 +974,4 @@ def native_group(group=None, device: Optional[int] = None):
         return g.host()
     if device is None:
         return g.host()
-    return g.rccl(device)
+    return g.gpu(device)

@@ -1,10 +1,10 @@
 """hipGraph capture of a whole training step (MI355X-first replacement for a tracing compiler).
 
 A ringdp training step at the reference's shapes is launch-bound: forward,
-backward, the RCCL bucket all-reduces on the side stream and the fused optimizer are a few dozen
-small launches.  ``StepGraph`` warms the step up on a side stream, drains every RCCL watchdog
-queue, then captures one step (including the cross-stream event fork/join of the reducer and
-the RCCL kernels) into a hipGraph that ``replay()`` launches with a single call.
+backward, the bucket all-reduces (RCCL or ringdp's xGMI kernels) on the side stream and the fused
+optimizer are a few dozen small launches.  ``StepGraph`` warms the step up on a side stream, drains
+every GPU watchdog queue, then captures one step (including the cross-stream event fork/join of the
+reducer and the collective kernels) into a hipGraph that ``replay()`` launches with a single call.
 
 Requirements: inputs the step reads must live in static tensors (copy each new batch into
 them), DDP bucket rebuild must have happened (warmup >= 2 steps), and the optimizer must use
@@ -23,27 +23,26 @@ from .._native import C
 ReplayBeacon = getattr(C, "ReplayBeacon", None)
 
 
+def _gpu_groups() -> List:
+    """Every native GPU process group (RCCL or xGMI) of every group."""
+    w = dist._world
+    return [pg for g in list(w.groups.values()) for pg in list(g._gpu.values())]
+
+
 def drain_comms():
-    """Block until every in-flight RCCL op of every group has completed."""
-    w = dist._world
-    for g in list(w.groups.values()):
-        for pg in list(g._rccl.values()):
-            pg.drain()
-
-
-def _rccl_groups() -> List:
-    w = dist._world
-    return [pg for g in list(w.groups.values()) for pg in list(g._rccl.values())]
+    """Block until every in-flight GPU collective of every group has completed."""
+    for pg in _gpu_groups():
+        pg.drain()
 
 
 class StepGraph:
     """Capture/replay of one training step.
 
-    Watchdog: collectives inside a replay are invisible to the per-op RCCL watchdog (they were
+    Watchdog: collectives inside a replay are invisible to the per-op watchdog (they were
     issued once, at capture).  The captured step therefore ends with a beacon node
     (``ReplayBeacon``: a one-thread kernel that writes the count of finished replays into
-    host-coherent memory) and ``replay()`` counts issued replays; every RCCL group's watchdog
-    compares the two with plain loads (``RcclPG.watch_beacon``).  While replays are outstanding
+    host-coherent memory) and ``replay()`` counts issued replays; every GPU group's watchdog
+    compares the two with plain loads (``GpuPG.watch_beacon``).  While replays are outstanding
     and none finishes within the group timeout - e.g. a peer died mid-step - the communicator is
     aborted and the process exits non-zero, as for a hung eager collective.  No HIP call is made
     per replay on either thread.  ``RINGDP_GRAPH_WATCHDOG``: unset/``auto`` watches groups with more
@@ -55,6 +54,7 @@ class StepGraph:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.output = None
         self._beacon = None
+        self._groups: List = []
 
     def capture(self):
         s = torch.cuda.Stream()
@@ -75,7 +75,7 @@ class StepGraph:
         if mode != "0":
             # auto: groups with peers only (a one-rank group has no peer to die; its beacon node would
             # only add a launch to the step)
-            watch = [pg for pg in _rccl_groups() if pg.device == dev and (mode == "1" or pg.size() > 1)]
+            watch = [pg for pg in _gpu_groups() if pg.device == dev and (mode == "1" or pg.size() > 1)]
         beacon = ReplayBeacon(dev) if watch else None
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             out = self.step_fn()
@@ -90,9 +90,17 @@ class StepGraph:
         for pg in watch:
             pg.watch_beacon(beacon)
         self._beacon = beacon
+        self._groups = [pg for pg in _gpu_groups() if pg.device == dev]
         return self
 
     def replay(self):
+        # an eager collective still running on a group's comm stream must finish before the replay's
+        # own collectives of that group start (xGMI kernels reuse slots in issue order); join_into
+        # makes no HIP call unless an eager op was issued since the last join
+        if self._groups:
+            stream = torch.cuda.current_stream().cuda_stream
+            for pg in self._groups:
+                pg.join_into(stream)
         self.graph.replay()
         if self._beacon is not None:
             self._beacon.issued()

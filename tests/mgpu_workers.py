@@ -1,5 +1,6 @@
-"""Multi-rank workers shared by the multi-GPU tests (RCCL, one process per GPU) and their CPU
-rehearsal (host-ring "gloo", same code).  ``mode`` is "gpu" or "cpu".
+"""Multi-rank workers shared by the multi-GPU tests (RCCL, one process per GPU; the xGMI backend,
+ranks possibly sharing a GPU) and their CPU rehearsal (host-ring "gloo", same code).  ``mode`` is
+"gpu", "xgmi" or "cpu".
 
 Reference: the reference trains DDP over NCCL with one process per GPU (ref/launch_dist.py:49-61,
 ref/example_mp.py:37-53); the checks mirror upstream's DDP tests:
@@ -18,6 +19,9 @@ import torch  # noqa: E402
 
 
 def _init(rank, world, port, mode, timeout_s=120):
+    """mode "gpu": RCCL, one GPU per rank; "xgmi": ringdp's own collective kernels over IPC-mapped
+    peer memory, ranks spread over the visible GPUs (several ranks share one GPU on a one-GPU box,
+    which RCCL refuses); "cpu": the host ring."""
     import datetime
 
     import ringdp.distributed as dist
@@ -25,6 +29,10 @@ def _init(rank, world, port, mode, timeout_s=120):
     if mode == "gpu":
         torch.cuda.set_device(rank)
         backend, dev = "nccl", torch.device("cuda", rank)
+    elif mode == "xgmi":
+        d = rank % torch.cuda.device_count()
+        torch.cuda.set_device(d)
+        backend, dev = "xgmi", torch.device("cuda", d)
     else:
         torch.set_num_threads(1)
         backend, dev = "gloo", torch.device("cpu")
@@ -157,7 +165,7 @@ def ddp_train_worker(rank, world, port, result_dir, mode, name, graph, perturb):
     and stores both parameter vectors.  `perturb`: rank-dependent delays inside backward (bucket
     launch order must not depend on readiness).  `graph`: steps 3.. are hipGraph replays."""
     dist, dev = _init(rank, world, port, mode)
-    if mode == "gpu" and world == 1:
+    if mode != "cpu" and world == 1:
         os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
     from ringdp.nn import CrossEntropyLoss
     from ringdp.optim import SGD
@@ -167,7 +175,8 @@ def ddp_train_worker(rank, world, port, result_dir, mode, name, graph, perturb):
     B, steps, lr = 8, 5, 0.05
     torch.manual_seed(100 + rank)  # different init per rank: DDP must broadcast rank 0's
     model = _model(name, dev)
-    ddp = DDP(model, device_ids=[rank] if mode == "gpu" else None, bucket_cap_mb=0.5 if name == "resnet18" else 0.1,
+    ddp = DDP(model, device_ids=[dev.index] if dev.type == "cuda" else None,
+              bucket_cap_mb=0.5 if name == "resnet18" else 0.1,
               first_bucket_mb=0.05)
     crit = CrossEntropyLoss()
     opt = SGD(ddp.parameters(), lr=lr, momentum=0.9, nesterov=True, weight_decay=1e-4)

@@ -1,0 +1,187 @@
+"""The "xgmi" backend: ringdp's own collective kernels over IPC-mapped peer memory
+(csrc/kernels/xgmi.hip, csrc/comm/xgmi_pg.cpp) - multi-process on whatever GPUs exist.
+
+Ranks share a GPU when there are fewer GPUs than ranks: the IPC-mapped staging buffers and the
+cross-process flag protocol are the same code as on an 8-GPU xGMI node, so a one-GPU box runs the
+real multi-process path (RCCL itself refuses two ranks per GPU).  This is where ringdp's DDP runs
+with several GPU ranks on a one-GPU box:
+
+* kernel exactness: every all-reduce equals the fp32 rank-order reference bit for bit (one-shot,
+  two-shot, multi-piece, ragged tails, fp32/bf16/fp16/fp64/int, sum/avg/min/max), reduce-scatter,
+  all-gather, broadcast, send/recv, back-to-back ops without host syncs, hipGraph replays;
+* the full collective suite and DDP equivalence (ConvNet, ResNet-18; eager and hipGraph; bitwise
+  replicas after every step; bucket order under perturbed readiness) at ws 2 and 4;
+* failure: a peer that never arrives ends the op with an error (never unreduced data), and a rank
+  killed mid-replay makes the survivor exit non-zero through its watchdog; the launcher reports it;
+* the bench contract at --gpus 2 on the xgmi backend;
+* RcclPG's small-message path (RINGDP_P2P_ALLREDUCE_MAX_BYTES) on the same kernels."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+import torch
+
+import mgpu_workers as MW
+import xgmi_workers as W
+from conftest import ROOT, free_port
+from ringdp.multiprocessing import spawn
+
+pytestmark = pytest.mark.gpu
+
+FAULT = os.path.join(ROOT, "tests", "scripts", "xgmi_fault_script.py")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_kernels_exact(tmp_path, world):
+    spawn(W.exact_worker, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    counts = [int((tmp_path / f"r{r}").read_text()) for r in range(world)]
+    assert len(set(counts)) == 1 and counts[0] > 80, counts
+
+
+def test_xgmi_missing_peer_raises(tmp_path):
+    spawn(W.timeout_worker, args=(2, free_port(), str(tmp_path)), nprocs=2)
+    r0 = (tmp_path / "r0").read_text()
+    assert r0.startswith("raised"), r0
+    assert float(r0.split("dt=")[1].split()[0]) < 15, r0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_collectives(tmp_path, world):
+    spawn(MW.collectives_worker, args=(world, free_port(), str(tmp_path), "xgmi"), nprocs=world)
+    assert sorted(os.listdir(tmp_path)) == [f"r{r}" for r in range(world)]
+
+
+def _check_train(tmp_path, world, rel):
+    res = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
+    assert all(all(r["same"]) for r in res), [r["same"] for r in res]  # bitwise replicas, every step
+    assert all(r["same_buckets"] for r in res)
+    r0 = res[0]
+    upd = float((r0["ref"] - r0["init"]).abs().max())
+    err = float((r0["ddp"] - r0["ref"]).abs().max())
+    assert upd > 0
+    assert err <= rel * upd + 1e-7, (err, upd)
+    return r0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("name,graph", [("convnet", False), ("convnet", True), ("resnet18", False), ("resnet18", True)])
+def test_xgmi_ddp_equivalence(tmp_path, world, name, graph):
+    spawn(MW.ddp_train_worker, args=(world, free_port(), str(tmp_path), "xgmi", name, graph, False), nprocs=world)
+    # the same bf16 kernels on the same per-rank chunks; only the fp32 averaging order differs
+    _check_train(tmp_path, world, rel=1e-3)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_bucket_order_under_perturbed_readiness(tmp_path, world):
+    spawn(MW.ddp_train_worker, args=(world, free_port(), str(tmp_path), "xgmi", "convnet", True, True), nprocs=world)
+    r0 = _check_train(tmp_path, world, rel=1e-3)
+    assert r0["n_buckets"] > 1
+
+
+def _fault_env(port, rank, world=2):
+    return dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FAULT_TIMEOUT_MS="4000", FAULT_AT="3",
+                PYTHONPATH=ROOT)
+
+
+def test_xgmi_rank_killed_mid_replay_survivor_exits_nonzero():
+    """No launcher in between: the survivor itself must notice (kernel timeout word / replay beacon)
+    and end non-zero within the group timeout plus slack, with the watchdog's message."""
+    port = free_port()
+    procs = [subprocess.Popen([sys.executable, FAULT], cwd=ROOT, env=_fault_env(port, r), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    t0 = time.time()
+    try:
+        out1, err1 = procs[1].communicate(timeout=240)
+        t_dead = time.time()
+        out0, err0 = procs[0].communicate(timeout=120)
+        dt = time.time() - t_dead
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert procs[1].returncode == 17, err1[-2000:]
+    assert procs[0].returncode not in (0, None), (out0, err0[-3000:])
+    assert "SURVIVED" not in out0
+    assert "watchdog" in err0, err0[-3000:]
+    assert dt < 60, dt
+    del t0
+
+
+def test_xgmi_rank_killed_launcher_reports():
+    r = subprocess.run([sys.executable, "-m", "ringdp.run", "--standalone", "--nproc-per-node", "2", FAULT],
+                       cwd=ROOT, env=dict(os.environ, FAULT_TIMEOUT_MS="4000", FAULT_AT="3", PYTHONPATH=ROOT),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 17, (r.returncode, r.stderr[-3000:])
+    assert "failed with exit code" in r.stderr, r.stderr[-3000:]
+    assert "SURVIVED" not in r.stdout
+
+
+def test_bench_contract_two_ranks_xgmi():
+    """bench.py --gpus 2 starts two ranks itself (sharing the GPU on a one-GPU box) on the xgmi
+    backend and prints exactly one JSON line with the contract fields."""
+    env = dict(os.environ, RINGDP_GPU_BACKEND="xgmi", PYTHONPATH=ROOT, RINGDP_BENCH_MIN_WARMUP_S="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "6", "--warmup", "2",
+                        "--batch-per-rank", "1024", "--comm-stats-steps", "3"],
+                       cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 6 and d["warmup"] == 2
+    assert d["config"]["comm_backend"] == "xgmi" and d["config"]["comm_world_size"] == 2
+    assert d["config"]["parallelism"] == "dp2" and d["value"] > 0
+    assert d["comm_stats"]["bucket_comm_us"][0] > 0
+
+
+def test_rccl_pg_routes_small_buckets_to_xgmi():
+    """World size 1 through the real RcclPG: the xGMI small-message path is set up, serves eligible
+    all-reduces and DDP buckets (also inside a hipGraph), and RCCL still serves the rest."""
+    code = r'''
+import os, torch
+import ringdp.distributed as dist
+from ringdp.models import ConvNet
+from ringdp.nn import CrossEntropyLoss
+from ringdp.optim import SGD
+from ringdp.parallel import DistributedDataParallel as DDP
+from ringdp.utils.graph import StepGraph
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+t = torch.arange(4096, dtype=torch.float32, device="cuda")
+dist.all_reduce(t, op=dist.ReduceOp.AVG)
+pg = dist._default().gpu(0)
+assert pg.backend_name() == "rccl"
+assert pg.p2p_max_bytes() == 1 << 20, pg.p2p_max_bytes()
+assert torch.equal(t.cpu(), torch.arange(4096, dtype=torch.float32))
+big = torch.ones(1 << 19, device="cuda")  # 2 MB > threshold: RCCL
+dist.all_reduce(big)
+assert torch.all(big == 1)
+os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
+torch.manual_seed(0)
+m = ConvNet().cuda()
+ref = ConvNet().cuda(); ref.load_state_dict(m.state_dict())
+ddp = DDP(m, device_ids=[0], bucket_cap_mb=0.3, first_bucket_mb=0.3)
+opt = SGD(ddp.parameters(), lr=0.05); ropt = SGD(ref.parameters(), lr=0.05)
+crit = CrossEntropyLoss()
+x = torch.randint(0, 256, (256, 1, 28, 28), dtype=torch.uint8, device="cuda"); y = torch.randint(0, 10, (256,), device="cuda")
+def step():
+    l = crit(ddp(x), y); opt.zero_grad(set_to_none=True); l.backward(); opt.step(); return l
+for _ in range(2):
+    step()
+g = StepGraph(step, warmup=1).capture()
+for _ in range(3):
+    g.replay()
+for _ in range(6):
+    l = crit(ref(x), y); ropt.zero_grad(set_to_none=True); l.backward(); ropt.step()
+torch.cuda.synchronize()
+for a, b in zip(m.parameters(), ref.parameters()):
+    assert torch.equal(a, b), (a - b).abs().max()
+print("P2P_OK")
+'''
+    env = dict(os.environ, RINGDP_P2P_ALLREDUCE_MAX_BYTES=str(1 << 20), PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, timeout=180)
+    assert r.returncode == 0 and "P2P_OK" in r.stdout, r.stderr[-3000:]
