@@ -105,6 +105,7 @@ void GpuPG::init_common(bool same_stream_default) {
     same_stream_ = same_stream_default;
   RINGDP_HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   RINGDP_HIP_CHECK(hipEventCreateWithFlags(&last_, hipEventDisableTiming));
+  RINGDP_HIP_CHECK(hipEventCreateWithFlags(&last_aux_, hipEventDisableTiming));
   timing_ = env_flag("RINGDP_COMM_TIMING", false);
   async_error_handling_ = env_flag("RINGDP_ASYNC_ERROR_HANDLING", true);
   watchdog_ = std::thread([this] { watchdog_loop(); });
@@ -126,7 +127,8 @@ void GpuPG::stop_common() {
     inflight_.clear();
     if (ready_) hipEventDestroy(ready_);
     if (last_) hipEventDestroy(last_);
-    ready_ = last_ = nullptr;
+    if (last_aux_) hipEventDestroy(last_aux_);
+    ready_ = last_ = last_aux_ = nullptr;
   }
 }
 
@@ -148,9 +150,9 @@ void GpuPG::watch_beacon(const std::shared_ptr<ReplayBeacon>& beacon) {
 
 void GpuPG::join_into(hipStream_t stream) {
   std::lock_guard<std::mutex> lk(launch_mu_);
-  if (!eager_since_join_ || !last_) return;
-  RINGDP_HIP_CHECK(hipStreamWaitEvent(stream, last_, 0));
-  eager_since_join_ = false;
+  if (eager_since_join_ && last_) RINGDP_HIP_CHECK(hipStreamWaitEvent(stream, last_, 0));
+  if (eager_aux_since_join_ && last_aux_) RINGDP_HIP_CHECK(hipStreamWaitEvent(stream, last_aux_, 0));
+  eager_since_join_ = eager_aux_since_join_ = false;
 }
 
 void GpuPG::abort() {

@@ -14,6 +14,7 @@
 
 #include <deque>
 #include <thread>
+#include <type_traits>
 
 #include "process_group.h"
 
@@ -128,7 +129,9 @@ class GpuPG : public ProcessGroup {
   HipStream comm_stream_;
   hipEvent_t ready_ = nullptr;
   hipEvent_t last_ = nullptr;      // recorded after every eager op on the comm stream (join_into)
+  hipEvent_t last_aux_ = nullptr;  // ... and after eager ops that complete on an auxiliary stream
   bool eager_since_join_ = false;
+  bool eager_aux_since_join_ = false;
   bool timing_ = false;
   bool same_stream_ = false;  // issue collectives on the caller's stream (see init_common)
   bool async_error_handling_ = true;
@@ -185,13 +188,22 @@ std::shared_ptr<Work> GpuPG::launch(OpType op, const std::vector<at::Tensor>& te
       c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(
           t.storage().data_ptr(), comm_stream_);
   }
-  body(cs);
-  RINGDP_HIP_CHECK(hipEventRecord(work->done_, cs));
+  // The body may finish the op on another stream (the xGMI sends): it then returns that stream, and
+  // the op's completion event is recorded there instead of on the comm stream.
+  hipStream_t done_stream = cs;
+  if constexpr (std::is_void_v<decltype(body(cs))>) {
+    body(cs);
+  } else {
+    hipStream_t r = body(cs);
+    if (r) done_stream = r;
+  }
+  RINGDP_HIP_CHECK(hipEventRecord(work->done_, done_stream));
   work->outputs_ = tensors;
   if (!captured) {
     if (!same_stream) {
-      RINGDP_HIP_CHECK(hipEventRecord(last_, cs));
-      eager_since_join_ = true;
+      RINGDP_HIP_CHECK(hipEventRecord(done_stream == cs ? last_ : last_aux_, done_stream));
+      if (done_stream == cs) eager_since_join_ = true;
+      else eager_aux_since_join_ = true;
     }
     work->deadline_us_ = now_us() + timeout_.count() * 1000;
     std::lock_guard<std::mutex> wl(wd_mu_);

@@ -41,8 +41,12 @@ int xg_dtype(const at::Tensor& t) {
 }  // namespace
 
 XgmiPG::XgmiPG(std::shared_ptr<Store> store, int rank, int size, int device, std::chrono::milliseconds timeout)
-    : GpuPG(rank, size, device, timeout), store_(store) {
+    : GpuPG(rank, size, device, timeout),
+      store_(store),
+      send_stream_(c10::hip::getStreamFromPoolMasqueradingAsCUDA(false, device)) {
   DeviceScope ds(device_);
+  RINGDP_HIP_CHECK(hipEventCreateWithFlags(&send_fence_, hipEventDisableTiming));
+  RINGDP_HIP_CHECK(hipEventCreateWithFlags(&send_done_, hipEventDisableTiming));
   std::string why;
   eng_ = XgmiEngine::create(std::make_shared<PrefixStore>("xgmi", store), rank, size, device,
                             XgmiConfig::from_env(), timeout.count(), &why);
@@ -56,7 +60,23 @@ XgmiPG::~XgmiPG() { shutdown(); }
 
 void XgmiPG::shutdown() {
   stop_common();
+  DeviceScope ds(device_);
+  if (!aborted_.load()) (void)hipStreamSynchronize(send_stream_.stream());
   eng_.reset();
+  if (send_fence_) hipEventDestroy(send_fence_);
+  if (send_done_) hipEventDestroy(send_done_);
+  send_fence_ = send_done_ = nullptr;
+}
+
+hipStream_t XgmiPG::send_on(hipStream_t cs) {
+  RINGDP_HIP_CHECK(hipEventRecord(send_fence_, cs));
+  RINGDP_HIP_CHECK(hipStreamWaitEvent(send_stream_.stream(), send_fence_, 0));
+  return send_stream_.stream();
+}
+
+void XgmiPG::join_sends(hipStream_t cs) {
+  RINGDP_HIP_CHECK(hipEventRecord(send_done_, send_stream_.stream()));
+  RINGDP_HIP_CHECK(hipStreamWaitEvent(cs, send_done_, 0));
 }
 
 std::string XgmiPG::backend_failure() {
@@ -255,7 +275,8 @@ std::shared_ptr<Work> XgmiPG::scatter(at::Tensor& output, std::vector<at::Tensor
         if (r == root) continue;
         at::Tensor tin = scratch(round16(M));
         d2d(tin.data_ptr(), inputs[r].data_ptr(), M, s);
-        eng_->send(tin.data_ptr(), M, r, s);
+        eng_->send(tin.data_ptr(), M, r, send_on(s));
+        join_sends(s);  // the scratch copy lives on s: keep it until the send has read it
       }
       d2d(output.data_ptr(), inputs[root].data_ptr(), M, s);
     } else {
@@ -289,31 +310,45 @@ std::shared_ptr<Work> XgmiPG::alltoall_base(at::Tensor& output, const at::Tensor
     char* in = static_cast<char*>(input.data_ptr());
     char* out = static_cast<char*>(output.data_ptr());
     d2d(out + roff[rank_], in + soff[rank_], sbytes[rank_], s);
-    // step k: send to rank+k, receive from rank-k (sends never wait on their receiver's progress,
-    // except for slot reuse two messages back, so the pairing cannot deadlock)
+    // step k: send to rank+k (send stream), receive from rank-k (comm stream): a send waits only for
+    // its receiver to have read the slot it refills, which no send of the receiver can hold up
+    std::vector<at::Tensor> keep;
     for (int k = 1; k < n; ++k) {
       const int dst = (rank_ + k) % n, src = (rank_ - k + n) % n;
       at::Tensor tin = scratch(round16(sbytes[dst])), tout = scratch(round16(rbytes[src]));
       d2d(tin.data_ptr(), in + soff[dst], sbytes[dst], s);
-      eng_->send(tin.data_ptr(), sbytes[dst], dst, s);
+      eng_->send(tin.data_ptr(), sbytes[dst], dst, send_on(s));
       eng_->recv(tout.data_ptr(), rbytes[src], src, s);
       d2d(out + roff[src], tout.data_ptr(), rbytes[src], s);
+      keep.push_back(tin);
     }
+    join_sends(s);  // scratch inputs of the sends stay allocated (stream-ordered on s) until here
   });
 }
 
 std::shared_ptr<Work> XgmiPG::send(at::Tensor& tensor, int dst, int /*tag*/) {
   check_tensor(tensor, "send");
   RINGDP_CHECK(dst >= 0 && dst < size_ && dst != rank_, "send: invalid peer ", dst);
-  return launch(OpType::SEND, {tensor}, [&](hipStream_t s) {
+  return launch(OpType::SEND, {tensor}, [&](hipStream_t s) -> hipStream_t {
     const int64_t nb = tensor.numel() * static_cast<int64_t>(tensor.element_size());
-    if (aligned16(tensor.data_ptr())) {
+    if (same_stream_) {  // one stream by request: the caller orders sends and receives
       eng_->send(tensor.data_ptr(), nb, dst, s);
+      return s;
+    }
+    if (aligned16(tensor.data_ptr())) {
+      eng_->send(tensor.data_ptr(), nb, dst, send_on(s));
     } else {
       at::Tensor tin = scratch(round16(nb));
       d2d(tin.data_ptr(), tensor.data_ptr(), nb, s);
-      eng_->send(tin.data_ptr(), nb, dst, s);
+      eng_->send(tin.data_ptr(), nb, dst, send_on(s));
+      join_sends(s);  // the scratch copy lives on s
+      return s;
     }
+    // the op completes on the send stream; the tensor is kept alive by the Work, and the caching
+    // allocator learns about the second stream here
+    c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(tensor.storage().data_ptr(),
+                                                                                    send_stream_);
+    return send_stream_.stream();
   });
 }
 

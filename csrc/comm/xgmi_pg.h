@@ -46,8 +46,17 @@ class XgmiPG : public GpuPG {
   void allreduce_one(at::Tensor& t, ReduceOp op, hipStream_t s);
   at::Tensor scratch(int64_t nbytes);  // uint8, allocated on the comm stream
 
+  // Sends run on a stream of their own: a send waits (on the device) only for its receiver to have
+  // read the slot it refills, so with sends and receives on one in-order stream a send-then-recv
+  // exchange of multi-slot messages would deadlock; receives and collectives stay on the comm stream.
+  hipStream_t send_on(hipStream_t cs);   // fences the send stream after `cs`, returns it
+  void join_sends(hipStream_t cs);       // `cs` waits for every send issued so far
+
   std::shared_ptr<Store> store_;
   std::unique_ptr<XgmiEngine> eng_;
+  HipStream send_stream_;
+  hipEvent_t send_fence_ = nullptr;
+  hipEvent_t send_done_ = nullptr;
 };
 
 }  // namespace ringdp

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""All-reduce latency / bandwidth sweep on ringdp's GPU process group (RCCL vs the one-shot P2P path).
+"""All-reduce latency / bandwidth sweep on ringdp's GPU process groups: RCCL, RCCL with its small
+all-reduces on the xGMI one-shot kernel, and the "xgmi" backend (ringdp's own kernels for every size).
 
 Sizes default to the DDP buckets that matter here: the ConvNet's two rebuilt
 buckets (77 KB, 377 KB) and its whole gradient (455 KB), then 1 / 4 / 25 MB.  For every size and
@@ -11,9 +12,11 @@ what a captured training step sees) and reports the max over ranks as us/op plus
   python tools/comm_bench.py --gpus 8 --sweep                # + NCCL_ALGO / channel variants
   python -m ringdp.run --nproc-per-node 8 tools/comm_bench.py
 
-The P2P rows exist when RINGDP_P2P_ALLREDUCE_MAX_BYTES is set (this tool sets 4 MiB unless told
-otherwise); the crossover between the two rows is the threshold to use for
-RINGDP_P2P_ALLREDUCE_MAX_BYTES in training.  Rank 0 prints one JSON line per measurement.
+The "rccl+xgmi_small" rows exist when RINGDP_P2P_ALLREDUCE_MAX_BYTES is set (this tool sets 4 MiB
+unless told otherwise); the crossover between them and the "rccl" rows is the threshold to use for
+RINGDP_P2P_ALLREDUCE_MAX_BYTES in training.  ``--backend xgmi``: every all-reduce on the xgmi backend
+(ranks may share a GPU: rank r uses GPU r % device_count, so a one-GPU box runs --gpus 2/4, which RCCL
+refuses).  Rank 0 prints one JSON line per measurement.
 """
 from __future__ import annotations
 
@@ -47,6 +50,8 @@ def parse():
     ap.add_argument("--reps", type=int, default=20, help="all-reduces per graph")
     ap.add_argument("--iters", type=int, default=20, help="timed graph replays")
     ap.add_argument("--sweep", action="store_true", help="repeat under each RCCL env variant (parent mode)")
+    ap.add_argument("--backend", type=str, default=None, choices=["rccl", "xgmi"],
+                    help="GPU backend (default: RINGDP_GPU_BACKEND, else rccl)")
     return ap.parse_args()
 
 
@@ -55,7 +60,7 @@ def worker(args):
 
     import ringdp.distributed as dist
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if os.environ.get("WORLD_SIZE"):
         dist.init_process_group("nccl")
@@ -65,8 +70,11 @@ def worker(args):
     dev = torch.device("cuda", local)
     probe = torch.zeros(1, device=dev)
     dist.all_reduce(probe)
-    pg = dist._default().rccl(local)
-    impls = ["rccl"] + (["p2p"] if pg.p2p_max_bytes() > 0 else [])
+    pg = dist._default().gpu(local)
+    if pg.backend_name() == "xgmi":
+        impls = ["xgmi"]
+    else:
+        impls = ["rccl"] + (["rccl+xgmi_small"] if pg.p2p_max_bytes() > 0 else [])
     variant = {k: os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS") if k in os.environ}
     for dt_name in args.dtypes.split(","):
         dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[dt_name]
@@ -75,9 +83,10 @@ def worker(args):
             n = max(1, nbytes // es)
             t = torch.ones(n, dtype=dtype, device=dev)
             for impl in impls:
-                if impl == "p2p" and nbytes > pg.p2p_max_bytes():
+                if impl == "rccl+xgmi_small" and nbytes > pg.p2p_max_bytes():
                     continue
-                pg.set_p2p_enabled(impl == "p2p")
+                if impl != "xgmi":
+                    pg.set_p2p_enabled(impl == "rccl+xgmi_small")
                 for _ in range(3):
                     dist.all_reduce(t, op=dist.ReduceOp.AVG)
                 torch.cuda.synchronize()
@@ -104,13 +113,16 @@ def worker(args):
                                       "busbw_GBps": round(algbw * 2 * (world - 1) / max(world, 1), 2),
                                       "correct": ok, "rccl_env": variant}), flush=True)
                 del g
-    pg.set_p2p_enabled(True)
+    if pg.backend_name() != "xgmi":
+        pg.set_p2p_enabled(True)
     dist.destroy_process_group()
 
 
 def main():
     args = parse()
     os.environ.setdefault("RINGDP_P2P_ALLREDUCE_MAX_BYTES", str(4 << 20))
+    if args.backend:
+        os.environ["RINGDP_GPU_BACKEND"] = args.backend
     if os.environ.get("WORLD_SIZE") is None and (args.gpus > 1 or args.sweep):
         from ringdp.run import launch_local
 
