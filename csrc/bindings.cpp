@@ -553,6 +553,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   }, "'auto': plain dense GEMMs on hipBLASLt; 'ringdp': every GEMM on ringdp's MFMA kernels");
   m.def("gemm_backend", [] { return std::string(blaslt::enabled() ? "auto" : "ringdp"); });
   m.def("set_bf16_tile_mode", &ops::set_bf16_tile_mode, "0 auto, 128 / 256: force the bf16 GEMM tile kernel");
+  m.def("set_gemm256_phased", &kern::set_gemm256_phased, "K-contiguous 256x256 GEMM: 1 phased pipeline, 0 older kernel");
   m.def("set_fp8_tile_mode", &ops::set_fp8_tile_mode,
         "fp8 GEMM kernel choice: 0 auto, 128 the generic 128x128 core, 256 the 256x256 DMA-pipelined kernel");
   m.def("f32_conv_fwd", &ops::f32_conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),

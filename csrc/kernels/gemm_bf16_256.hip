@@ -232,7 +232,222 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// K-contiguous A and B: the phased pipeline.  Each 64-k tile is computed in 4 phases, one per
+// (64-row x 32-col) quadrant of the wave's 128 x 64 outputs, in the order q00 q01 q11 q10.  The tile's
+// operands live in four 16 KiB half-tiles, grouped by the phase that first reads them:
+//   A-lo = tile rows {0-63, 128-191}     (quadrant row 0 of both wave rows: read in phase 0)
+//   B-lo = tile cols {0-31, 64-95, ...}  (quadrant col 0 of the four wave columns: phase 0)
+//   B-hi = the other 128 cols            (phase 1)
+//   A-hi = tile rows {64-127, 192-255}   (phase 2)
+// Phase p of tile t issues the half-tile of tile t+1 that phase p needs (2 LDS-DMA instructions per
+// wave), so every half-tile is in flight for 3-4 phases of MFMA work before it is read; one counted
+// vmcnt + one raw barrier per phase retire exactly the half-tile the next phase reads (never
+// vmcnt(0) in the loop), and each buffer region is refilled >= 3 phases after its last read.
+// Fragments are read once per tile: A of a quadrant row in phases 0 and 2, B-lo in phase 0 (kept in
+// registers for phase 3), B-hi in phase 1.
+constexpr int HT = 128 * TK;   // 16 KiB half-tile
+constexpr int PBUF = 4 * HT;   // one k-tile: [A-lo | B-lo | B-hi | A-hi]
+
+// tile row (A) / col (B) of slot row j of half-tile kind h (0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi)
+__device__ __forceinline__ int half_row(int h, int j) {
+  switch (h) {
+    case 0: return j < 64 ? j : j + 64;
+    case 3: return j < 64 ? j + 64 : j + 128;
+    case 1: return (j >> 5) * 64 + (j & 31);
+    default: return (j >> 5) * 64 + 32 + (j & 31);
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                               int64_t a_bs, const uint8_t* __restrict__ B,
+                                                               int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
+                                                               int N, int K, int tiles_m, int tiles_n, int splits,
+                                                               int k_per_split) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PBUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int per_z = tiles_m * tiles_n;
+  const int zid = blockIdx.y;
+  const int t = xcd_remap(blockIdx.x, per_z);
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int b = zid / splits, split = zid - b * splits;
+  const int m0 = tm * TM, n0 = tn * TN;
+  const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
+  const int nkt = max(0, (kend - kbeg) / TK);
+
+  // this lane's DMA source for instruction i (0, 1) of half-tile kind h: slot row 16*wave + 8i + lane/8,
+  // physical 16-B chunk lane & 7 holding logical chunk (lane & 7) ^ (slot row & 7)
+  const uint8_t* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const bool is_a = h == 0 || h == 3;
+    const uint8_t* base = is_a ? A + (int64_t)b * a_bs : B + (int64_t)b * b_bs;
+    const int64_t ld = is_a ? lda : ldb;
+    const int lim = is_a ? M : N, r0 = is_a ? m0 : n0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = 16 * wave + 8 * i + (lane >> 3);
+      const int lc = (lane & 7) ^ (j & 7);
+      const int rr = min(r0 + half_row(h, j), lim - 1);  // past the edge: re-read the last row, dropped on store
+      src[h][i] = base + (int64_t)rr * ld + kbeg + lc * 16;
+    }
+  }
+  auto issue = [&](int h, int kt) {
+    char* dst = smem + (kt & 1) * PBUF + h * HT + 2 * wave * 1024;
+    glds16(src[h][0] + (int64_t)kt * TK, dst);
+    glds16(src[h][1] + (int64_t)kt * TK, dst + 1024);
+  };
+
+  f32x4 acc[8][4];  // [qm*4 + mt][qn*2 + nt]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero_f32x4();
+
+  // fragment offsets: slot row = (wr*64 | wc*32) + 16*tile + (lane & 15) == lane (mod 8), so the swizzled
+  // chunk of k-step s is (4s + lane/16) ^ (lane & 7)
+  const int sw0 = (((lane >> 4)) ^ (lane & 7)) << 4, sw1 = ((4 + (lane >> 4)) ^ (lane & 7)) << 4;
+  const int a_row = (wr * 64 + (lane & 15)) * TK;
+  const int b_row = (wc * 32 + (lane & 15)) * TK;
+
+  if (nkt > 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue(h, 0);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-lo, B-lo of tile 0
+    raw_barrier();
+  }
+  bf16x8 fa[4][2], fbl[2][2], fbh[2][2];
+  for (int kt = 0; kt < nkt; ++kt) {
+    const char* st = smem + (kt & 1) * PBUF;
+    const bool next = kt + 1 < nkt;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      // fragments this phase reads first
+      if (p == 0 || p == 2) {
+        const char* ap = st + (p == 0 ? 0 : 3 * HT) + a_row;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          fa[mt][0] = *reinterpret_cast<const bf16x8*>(ap + mt * 16 * TK + sw0);
+          fa[mt][1] = *reinterpret_cast<const bf16x8*>(ap + mt * 16 * TK + sw1);
+        }
+      }
+      if (p == 0 || p == 1) {
+        const char* bp = st + (p == 0 ? HT : 2 * HT) + b_row;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const bf16x8 x0 = *reinterpret_cast<const bf16x8*>(bp + nt * 16 * TK + sw0);
+          const bf16x8 x1 = *reinterpret_cast<const bf16x8*>(bp + nt * 16 * TK + sw1);
+          if (p == 0) {
+            fbl[nt][0] = x0;
+            fbl[nt][1] = x1;
+          } else {
+            fbh[nt][0] = x0;
+            fbh[nt][1] = x1;
+          }
+        }
+      }
+      // next tile's half-tile for this phase: [A-lo, B-lo, B-hi, A-hi][p]
+      if (next) issue(p, kt + 1);
+      const int qm = (p == 2 || p == 3) ? 1 : 0;
+      const bool qn1 = p == 1 || p == 2;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)  // C^T tile: lane ends with 4 consecutive n of one m
+            acc[qm * 4 + mt][(qn1 ? 2 : 0) + nt] =
+                mfma16x16x32(qn1 ? fbh[nt][ks] : fbl[nt][ks], fa[mt][ks], acc[qm * 4 + mt][(qn1 ? 2 : 0) + nt]);
+      __builtin_amdgcn_s_setprio(0);
+      // retire the half-tile the next phase reads first (one phase ahead of the read)
+      if (p == 0) {
+        if (next) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // B-hi(t)
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else if (p == 1) {
+        if (next) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-hi(t)
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (p == 3) {
+        if (next) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-lo(t+1), B-lo(t+1)
+      }
+      raw_barrier();
+    }
+  }
+
+  // ---------------- epilogue: acc[qm*4+mt][qn*2+nt] holds C[m][n..n+3],
+  //   m = m0 + wr*128 + qm*64 + 16 mt + (lane & 15),  n = n0 + wc*64 + qn*32 + 16 nt + 4 (lane >> 4)
+  const int mrow = m0 + wr * 128 + (lane & 15);
+  const int ncol = n0 + wc * 64 + 4 * (lane >> 4);
+  if (ep.mode == GemmEpilogue::kSplitK) {
+    float* out = ep.partial + (int64_t)zid * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mrow + (i >> 2) * 64 + 16 * (i & 3);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = ncol + (j >> 1) * 32 + 16 * (j & 1);
+        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j];
+      }
+    }
+    return;
+  }
+  const int64_t cb = (int64_t)b * ep.c_bstride;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = mrow + (i >> 2) * 64 + 16 * (i & 3);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = ncol + (j >> 1) * 32 + 16 * (j & 1);
+      if (n >= N) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] * ep.alpha;
+        if (ep.bias) v[e] += ep.bias[n + e];
+      }
+      const int64_t off = cb + (int64_t)m * ep.ldc + n;
+      if (ep.act == 3) {  // GELU backward: times GELU'(pre-activation), preact read
+        const bf16x4 z = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.preact) + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = (float)z[e];
+          v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+        }
+      } else if (ep.preact)
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      if (ep.residual) {
+        const bf16x4 r = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.residual) + off);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
+      }
+      if (ep.out_bf16)
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      else
+        *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+  }
+}
+
+int g_phased = -1;
+int phased_mode() {
+  if (g_phased < 0) {
+    const char* v = getenv("RINGDP_GEMM256_PHASED");  // 0: the single-stage-wait pipeline (A/B)
+    g_phased = (v && v[0] == '0') ? 0 : 1;
+  }
+  return g_phased;
+}
+
 }  // namespace
+
+void set_gemm256_phased(int on) { g_phased = on ? 1 : 0; }
 
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s) {
@@ -253,7 +468,10 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
                               static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, ep, M, N, K * 2,
                               tiles_m, tiles_n, splits, kps * 2);
   };
-  if (!A.row_contig && !Bop.row_contig) go(gemm_bf16_256_kernel<false, false>);
+  if (!A.row_contig && !Bop.row_contig) {
+    if (phased_mode()) go(gemm_bf16_256p_kernel);
+    else go(gemm_bf16_256_kernel<false, false>);
+  }
   else if (A.row_contig && Bop.row_contig) go(gemm_bf16_256_kernel<true, true>);
   else if (A.row_contig) go(gemm_bf16_256_kernel<true, false>);
   else go(gemm_bf16_256_kernel<false, true>);

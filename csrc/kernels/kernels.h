@@ -212,6 +212,7 @@ void set_bf16_tile_mode(int mode);  // 0 auto, 128 / 256 forced (A/B measurement
 // supported (the caller falls back to the 128x128 core).  K in elements.
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s);
+void set_gemm256_phased(int on);  // A/B: 1 phased pipeline (default), 0 the single-stage-wait kernel
 bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes,
                   const GemmEpilogue& ep, int splits, hipStream_t s);
 // split-K count gemm_fp8 should be called with for an (M x N) fp32-partial GEMM (fills whole CU rounds)
