@@ -8,7 +8,6 @@
 #include "comm/host_ring.h"
 #include "comm/rccl_pg.h"
 #include "comm/xgmi_pg.h"
-#include "ops/blaslt.h"
 #include "ops/nn_ops.h"
 #include "ops/ops.h"
 #include "reducer/reducer.h"
@@ -547,11 +546,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("N"), py::arg("K"), py::arg("out_bf16") = true, py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("residual") = py::none(), py::arg("preact") = py::none());
   m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
-  m.def("set_gemm_backend", [](const std::string& b) {
-    RINGDP_CHECK(b == "ringdp" || b == "auto", "set_gemm_backend: 'ringdp' or 'auto'");
-    blaslt::set_enabled(b == "auto");
-  }, "'auto': plain dense GEMMs on hipBLASLt; 'ringdp': every GEMM on ringdp's MFMA kernels");
-  m.def("gemm_backend", [] { return std::string(blaslt::enabled() ? "auto" : "ringdp"); });
   m.def("set_bf16_tile_mode", &ops::set_bf16_tile_mode, "0 auto, 128 / 256: force the bf16 GEMM tile kernel");
   m.def("set_gemm256_phased", &kern::set_gemm256_phased, "K-contiguous 256x256 GEMM: 1 phased pipeline, 0 older kernel");
   m.def("set_fp8_tile_mode", &ops::set_fp8_tile_mode,

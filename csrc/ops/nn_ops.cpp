@@ -6,7 +6,6 @@
 #include <cstdlib>
 #include <cstring>
 
-#include "blaslt.h"
 
 #include "../kernels/kernels.h"
 #include "util.h"
@@ -98,31 +97,6 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, 
   // act 3: the GELU backward, C = (A B^T) * GELU'(preact) with preact an INPUT (the forward's pre-activation)
   RINGDP_CHECK(act != 3 || (e.preact && !e.residual && !e.bias), "gemm act 3 (GELU backward) needs preact only");
   if (M == 0 || N == 0) return c;
-  {  // plain dense GEMM: hipBLASLt when the epilogue maps onto it (blaslt.cpp)
-    blaslt::Problem p;
-    p.A = a.data_ptr();
-    p.B = b.data_ptr();
-    p.C = c.data_ptr();
-    p.M = (int)M;
-    p.N = (int)N;
-    p.K = (int)K;
-    p.batch = (int)batch;
-    p.lda = lda;
-    p.ldb = ldb;
-    p.ldc = N;
-    p.a_bstride = a_bstride;
-    p.b_bstride = b_bstride;
-    p.c_bstride = M * N;
-    p.a_row = a_row;
-    p.b_row = b_row;
-    p.out_bf16 = out_bf16;
-    p.alpha = e.alpha;
-    p.bias = e.bias;
-    p.act = e.act;
-    p.preact = e.preact;
-    p.residual = e.residual;
-    if (blaslt::matmul(p, stream_of(a))) return c;
-  }
   kern::GemmOperand A{a.data_ptr(), lda, a_bstride, a_row};
   kern::GemmOperand B{b.data_ptr(), ldb, b_bstride, b_row};
   kern::gemm_bf16(A, B, (int)batch, (int)M, (int)N, (int)K, e, 1, stream_of(a));
@@ -138,22 +112,6 @@ at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, 
   RINGDP_CHECK(lda % 8 == 0 && ldb % 8 == 0, "gemm: leading dims must be multiples of 8");
   RINGDP_CHECK((a_row && b_row) || K % 8 == 0, "gemm: K must be a multiple of 8 for a K-contiguous operand");
   RINGDP_CHECK((!a_row || M % 8 == 0) && (!b_row || N % 8 == 0), "gemm: row-contiguous operand needs 8-multiple");
-  {  // fp32 weight gradient straight from hipBLASLt (it splits K internally when it pays)
-    blaslt::Problem p;
-    p.A = a.data_ptr();
-    p.B = b.data_ptr();
-    p.C = out.data_ptr();
-    p.M = (int)M;
-    p.N = (int)N;
-    p.K = (int)K;
-    p.lda = lda;
-    p.ldb = ldb;
-    p.ldc = N;
-    p.a_row = a_row;
-    p.b_row = b_row;
-    p.out_bf16 = false;
-    if (blaslt::matmul(p, stream_of(a))) return out;
-  }
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 64)));
   splits = kern::gemm_bf16_pick_splits((int)M, (int)N, (int)K, (int)splits);
   at::Tensor part = at::empty({splits, M, N}, out.options());
@@ -230,16 +188,6 @@ std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t
   return {krsc, crsk};
 }
 
-// Pointwise (1x1, stride 1, no padding) convs are plain GEMMs over the NHWC activation matrix; for the large
-// ones hipBLASLt beats the GEMM core (ResNet-50 B=256: 131 vs 241 us for 64->256 at 56x56, tools/pw_bench.py),
-// so they go there and the BN statistics come from one read of z instead of the GEMM epilogue.
-// RINGDP_PW_BLASLT: letters f (forward), d (data gradient), w (weight gradient); default "fd"; "" = none.
-bool pw_blaslt(char which, int64_t M) {
-  if (M < 8192 || !blaslt::enabled()) return false;
-  const char* v = std::getenv("RINGDP_PW_BLASLT");  // read per call: tests switch it in-process
-  return std::strchr(v ? v : "fd", which) != nullptr;
-}
-
 std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Tensor& w_krsc, int64_t stride,
                                               int64_t pad, int64_t dil, bool want_stats) {
   bf16_gpu(x, "conv input");
@@ -260,31 +208,6 @@ std::tuple<at::Tensor, at::Tensor> conv2d_fwd(const at::Tensor& x, const at::Ten
   // few output tiles (small spatial maps): split the k-range, then one pass sums the partials, stores z
   // and produces the statistics groups (aligned loaders only)
   const bool pointwise = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
-  if (pointwise && pw_blaslt('f', M) && g.K % 8 == 0 && g.K <= 2048) {
-    blaslt::Problem p;
-    p.A = x.data_ptr();
-    p.B = w_krsc.data_ptr();
-    p.C = z.data_ptr();
-    p.M = M;
-    p.N = g.K;
-    p.K = g.C;
-    p.lda = g.C;
-    p.ldb = w_krsc.stride(0);
-    p.ldc = g.K;
-    if (blaslt::matmul(p, stream_of(x))) {
-      if (want_stats) {
-        at::Tensor part = at::empty({kern::bn_bwd_parts(M, g.K), 2, g.K}, x.options().dtype(at::kFloat));
-        const int np = kern::bn_col_stats(z.data_ptr(), M, g.K, part.data_ptr<float>(), stream_of(x));
-        if (np <= 64) {
-          sums = part;
-        } else {
-          sums = at::empty({kern::reduce_parts_groups(np), 2, g.K}, part.options());
-          kern::reduce_parts_l1(part.data_ptr<float>(), np, g.K, sums.data_ptr<float>(), stream_of(x));
-        }
-      }
-      return {z, sums};
-    }
-  }
   const int splits = (Kd % 64 == 0 && (pointwise || g.C % 64 == 0)) ? kern::conv_gemm_splits(M, g.K, Kd) : 1;
   if (splits > 1) {
     at::Tensor part = at::empty({splits, M, g.K}, x.options().dtype(at::kFloat));
@@ -337,20 +260,6 @@ at::Tensor conv2d_dgrad(const at::Tensor& dz, const at::Tensor& w_crsk, int64_t 
   }
   const int M = g.N * g.H * g.W, Kd = g.R * g.S * g.K;
   const bool pointwise = g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0;
-  if (pointwise && pw_blaslt('d', M)) {
-    blaslt::Problem p;  // dX[M][C] = dZ[M][K] . W^T, W as CRSK = [C][K] (K-contiguous rows)
-    p.A = dz.data_ptr();
-    p.B = w_crsk.data_ptr();
-    p.C = dx.data_ptr();
-    p.M = M;
-    p.N = g.C;
-    p.K = g.K;
-    p.lda = g.K;
-    p.ldb = w_crsk.stride(0);
-    p.ldc = g.C;
-    p.residual = res;
-    if (blaslt::matmul(p, stream_of(dz))) return dx;
-  }
   // stride 2 takes the parity-class path; few output tiles otherwise: split the k-range
   const int splits = (g.stride != 2 && Kd % 64 == 0 && (pointwise || g.K % 64 == 0))
                          ? kern::conv_gemm_splits(M, g.C, Kd) : 1;
@@ -377,24 +286,6 @@ void conv2d_wgrad(const at::Tensor& dz, const at::Tensor& x, at::Tensor dw, int6
   auto g = geom(x, K, R, S, stride, pad, dil);
   RINGDP_CHECK(dz.size(0) == g.N && dz.size(1) == g.P && dz.size(2) == g.Q && dz.size(3) == K,
                "conv wgrad: output grad shape mismatch");
-  const int64_t Mrows = (int64_t)g.N * g.P * g.Q;
-  if (g.R == 1 && g.S == 1 && g.stride == 1 && g.pad == 0 && C == g.C && dw.is_contiguous() &&
-      pw_blaslt('w', Mrows)) {
-    blaslt::Problem p;  // dW[K][C] = dZ^T . X, both row-contiguous over the M positions
-    p.A = dz.data_ptr();
-    p.B = x.data_ptr();
-    p.C = dw.data_ptr();
-    p.M = (int)K;
-    p.N = (int)C;
-    p.K = (int)Mrows;
-    p.lda = K;
-    p.ldb = g.C;
-    p.ldc = C;
-    p.a_row = p.b_row = true;
-    p.allow_row = true;
-    p.out_bf16 = false;
-    if (blaslt::matmul(p, stream_of(x))) return;
-  }
   // the GEMM runs over the padded channels; drop the padding when C < Cp
   at::Tensor target = dw;
   if (C != g.C) target = at::empty({K, (int64_t)g.C, R, S}, dw.options());
@@ -874,27 +765,6 @@ at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
     bf16_gpu(*preact, "gemm preact");
     e.preact = preact->data_ptr();
   }
-  {  // hipBLASLt's e4m3 kernels when the epilogue maps (blaslt.cpp)
-    blaslt::Problem p;
-    p.A = a.data_ptr();
-    p.B = b.data_ptr();
-    p.C = c.data_ptr();
-    p.M = (int)M;
-    p.N = (int)N;
-    p.K = (int)K;
-    p.lda = K;
-    p.ldb = K;
-    p.ldc = N;
-    p.out_bf16 = out_bf16;
-    p.bias = e.bias;
-    p.act = e.act;
-    p.preact = e.preact;
-    p.residual = e.residual;
-    p.fp8 = true;
-    p.scale_a = e.scale_a;
-    p.scale_b = e.scale_b;
-    if (blaslt::matmul(p, stream_of(a))) return c;
-  }
   kern::GemmOperand A{a.data_ptr(), K, 0, false}, B{b.data_ptr(), K, 0, false};
   kern::gemm_fp8(A, B, 1, (int)M, (int)N, (int)K, e, 1, stream_of(a));
   return c;
@@ -909,8 +779,6 @@ void gemm_fp8_splitk_f32(const at::Tensor& a, const at::Tensor& b, const at::Ten
   gpu(b, "fp8 B");
   f32_gpu(out, "fp8 gemm out");
   RINGDP_CHECK(K % 16 == 0 && out.numel() == M * N, "gemm_fp8_splitk_f32: bad shapes");
-  // (hipBLASLt measured 1.7x slower than ringdp's split-K 256x256 kernel on these long-K weight
-  // gradients: 72 vs 41 us at 768x768x25216, tools/blaslt_fp8_check.py - they stay here)
   splits = std::max<int64_t>(1, std::min<int64_t>(splits, std::max<int64_t>(1, K / 128)));
   splits = kern::gemm_fp8_pick_splits((int)M, (int)N, (int)K, (int)splits);
   at::Tensor part = at::empty({splits, M, N}, out.options());

@@ -102,7 +102,7 @@ def _compile_cmd(src: Path, obj: Path, sanitize: str | None = None):
 def _link_cmd(objs, out: Path):
     _inc, lib, _abi = _torch_paths()
     libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-            "-lamdhip64", "-lrccl", "-lhipblaslt"]  # hipBLASLt: torch's bundled copy (same one torch loads)
+            "-lamdhip64", "-lrccl"]
     return [
         _hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-fno-gpu-rdc", *map(str, objs),
         f"-L{lib}", *libs, f"-Wl,-rpath,{lib}", "-Wl,--no-as-needed", "-o", str(out),
@@ -119,7 +119,7 @@ def _run(cmd):
 def _link_cmd_sanitized(objs, out: Path, sanitize: str):
     _inc, lib, _abi = _torch_paths()
     libs = ["-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-            "-lamdhip64", "-lrccl", "-lhipblaslt"]
+            "-lamdhip64", "-lrccl"]
     return [_cxx(), "-shared", "-fPIC", f"-fsanitize={sanitize}", *map(str, objs), f"-L{lib}",
             f"-L{ROCM / 'lib'}", *libs, f"-Wl,-rpath,{lib}", "-Wl,--no-as-needed", "-o", str(out)]
 

@@ -40,6 +40,9 @@ _BF16_WEIGHTS: dict = {}
 
 _BF16_WEIGHTS_T: dict = {}  # {id(bf16 copy): its transpose}, for the data-gradient GEMMs
 
+# data-gradient GEMMs on W^T (K-contiguous, the phased 256x256 kernel) instead of row-contiguous W
+_DGRAD_WT = os.environ.get("RINGDP_DGRAD_WT", "1") == "1"
+
 
 def cast_weights(ws) -> None:
     """Cast many fp32 [out, in] weights to bf16 AND bf16 transposed in one launch for the forward in
@@ -129,11 +132,9 @@ class LinearF(torch.autograd.Function):
         dz = C.gelu_bwd(dyb, pre) if act == 2 else dyb
         dx = None
         if ctx.needs_input_grad[0]:
-            # dX[m][k] = sum_n dz[m][n] W[n][k].  With W^T materialised ([K][N], one small transpose of
-            # the weight per step) both operands are K-contiguous, which is the layout the plain-GEMM
-            # library path runs fastest (tools/blaslt_check.py); with RINGDP_GEMM_BACKEND=ringdp the
-            # row-contiguous form reads W directly.
-            if C.gemm_backend() == "auto":
+            # dX[m][k] = sum_n dz[m][n] W[n][k]: W^T K-contiguous (from the forward's cast launch) for the
+            # phased 256x256 kernel, or W read row-contiguously (RINGDP_DGRAD_WT=0)
+            if _DGRAD_WT:
                 dx = C.gemm(dz, _bf16_t(wb), M, K, N, N, N, False, False).view(M, K)
             else:
                 dx = C.gemm(dz, wb, M, K, N, N, K, False, True).view(M, K)
@@ -226,8 +227,8 @@ def _linear_fp8_bwd(ctx, dy):
 
 class MLPF(torch.autograd.Function):
     """The transformer MLP ``y = fc2(GELU(fc1(h))) + residual`` as one Function (bf16 path), so that
-    the backward runs the GELU derivative inside fc2's data-gradient GEMM epilogue (hipBLASLt DGELU, or
-    ringdp's act-3 epilogue) instead of a separate pass over the [tokens, 3072] gradient
+    the backward runs the GELU derivative inside fc2's data-gradient GEMM epilogue (ringdp's act-3
+    epilogue) instead of a separate pass over the [tokens, 3072] gradient
     (gelu_bwd: 79 us per ViT-B/16 block)."""
 
     @staticmethod
@@ -251,7 +252,7 @@ class MLPF(torch.autograd.Function):
         Hd = w1b.shape[0]
         dy = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
         # d(fc1 output) = (dy W2) * GELU'(pre): the GELU backward rides in the GEMM epilogue (act 3)
-        if C.gemm_backend() == "auto":
+        if _DGRAD_WT:
             dz1 = C.gemm(dy, _bf16_t(w2b), M, Hd, D, D, D, False, False, 1, 0, 0, True, None, 3, None,
                          pre).view(M, Hd)
         else:
@@ -264,7 +265,7 @@ class MLPF(torch.autograd.Function):
         C.colsum_f32(dz1, db1)
         dh = None
         if ctx.needs_input_grad[0]:
-            if C.gemm_backend() == "auto":
+            if _DGRAD_WT:
                 dh = C.gemm(dz1, _bf16_t(w1b), M, D, Hd, Hd, Hd, False, False).view(M, D)
             else:
                 dh = C.gemm(dz1, w1b, M, D, Hd, Hd, D, False, True).view(M, D)

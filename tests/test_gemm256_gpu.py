@@ -12,10 +12,9 @@ def C():
 
     c = ringdp._C
     c.set_bf16_tile_mode(256)
-    c.set_gemm_backend("ringdp")
     yield c
     c.set_bf16_tile_mode(0)
-    c.set_gemm_backend("auto")
+    c.set_gemm256_phased(1)
 
 
 def _operand(rows, K, row, batch, g):
@@ -25,9 +24,11 @@ def _operand(rows, K, row, batch, g):
     return x.float(), store.cuda()
 
 
+@pytest.mark.parametrize("phased", [1, 0])
 @pytest.mark.parametrize("a_row,b_row", [(False, False), (True, True), (True, False), (False, True)])
-@pytest.mark.parametrize("M,N,K,batch", [(520, 264, 640, 2), (256, 512, 128, 1), (8, 8, 64, 3)])
-def test_gemm256_layouts(C, a_row, b_row, M, N, K, batch):
+@pytest.mark.parametrize("M,N,K,batch", [(520, 264, 640, 2), (256, 512, 128, 1), (8, 8, 64, 3), (300, 700, 64, 1)])
+def test_gemm256_layouts(C, a_row, b_row, M, N, K, batch, phased):
+    C.set_gemm256_phased(phased)  # K-contiguous operands: the phased pipeline or the older kernel
     g = torch.Generator().manual_seed(M + N + K)
     a, ad = _operand(M, K, a_row, batch, g)
     b, bd = _operand(N, K, b_row, batch, g)

@@ -83,14 +83,10 @@ def _nhwc(x, cp):
     return out.bfloat16().contiguous()
 
 
-@pytest.mark.parametrize("case,pw", [(c, None) for c in CONV_CASES] +
-                         [((4, 64, 64, 256, 1, 1, 0), m) for m in ("", "fdw")] +
-                         [((2, 256, 64, 64, 1, 1, 0), m) for m in ("", "fdw")])
-def test_conv_fwd_dgrad_wgrad(case, pw, monkeypatch):
-    """pw: RINGDP_PW_BLASLT for the large pointwise cases (M >= 8192): "" = GEMM core, "fdw" = hipBLASLt
-    forward (+ BN statistics pass), data and weight gradient."""
-    if pw is not None:
-        monkeypatch.setenv("RINGDP_PW_BLASLT", pw)
+@pytest.mark.parametrize("case", CONV_CASES + [(4, 64, 64, 256, 1, 1, 0), (2, 256, 64, 64, 1, 1, 0)])
+def test_conv_fwd_dgrad_wgrad(case):
+    """Implicit-GEMM conv forward (+ BN statistics), data and weight gradient; the last two cases are
+    large pointwise convs (M >= 8192 rows), plain GEMMs on the same kernels."""
     N, Cin, H, K, R, stride, pad = case
     torch.manual_seed(sum(case))
     dev = "cuda"
@@ -526,19 +522,19 @@ def test_pack_conv_weights_multi_matches_single():
         assert torch.equal(flat[2 * i + 1], crsk)
 
 
-@pytest.mark.parametrize("backend", ["auto", "ringdp"])
-def test_gemm_gelu_backward_epilogue(backend):
-    """act 3: C = (A B^T) * GELU'(preact), preact read (hipBLASLt DGELU or ringdp's epilogue)."""
+@pytest.mark.parametrize("tile", [128, 256])
+def test_gemm_gelu_backward_epilogue(tile):
+    """act 3: C = (A B^T) * GELU'(preact), preact read (ringdp's GEMM epilogue, both tile kernels)."""
     torch.manual_seed(4)
     M, N, K = 320, 256, 192
     a = torch.randn(M, K, device="cuda").bfloat16()
     b = torch.randn(N, K, device="cuda").bfloat16()
     pre = torch.randn(M, N, device="cuda").bfloat16()
-    C().set_gemm_backend(backend)
+    C().set_bf16_tile_mode(tile)
     try:
         out = C().gemm(a, b, M, N, K, K, K, False, False, 1, 0, 0, True, None, 3, None, pre).view(M, N)
     finally:
-        C().set_gemm_backend("auto")
+        C().set_bf16_tile_mode(0)
     x = pre.float()
     gp = 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
     ref = (a.float() @ b.float().t()) * gp

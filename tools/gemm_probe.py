@@ -31,7 +31,6 @@ def timeit(fn, iters=20, warm=3):
 
 def main():
     torch.manual_seed(0)
-    C.set_gemm_backend("ringdp")
     C.set_bf16_tile_mode(256)
     for M, N, K, note in SHAPES:
         A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
