@@ -627,31 +627,51 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
 #pragma unroll
     for (int e = 0; e < 4; ++e) ssum[j][e] = ssq[j][e] = 0.f;
   const int64_t cb = (int64_t)b * ep.c_bstride;
+  // Every load of the epilogue is issued before the first use (bias, and the residual or GELU-backward
+  // pre-activation of every full tile): a load-wait-store chain per tile is one memory round trip per
+  // tile, 16 in a row.
+  int64_t row_offs[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mrow + 16 * i;
+    if constexpr (loader_kind<LA>::value == 5)
+      row_offs[i] = m < Mb ? la.out_row(b, m) * ep.ldc : 0;
+    else
+      row_offs[i] = cb + (int64_t)m * ep.ldc;
+  }
+  float bias[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[j][e] = (ep.bias && ncol + 16 * j + e < N) ? ep.bias[ncol + 16 * j + e] : 0.f;
+  const bf16* side = static_cast<const bf16*>(ep.residual ? ep.residual : (ep.act == 3 ? ep.preact : nullptr));
+  bf16x4 sv[4][4];
+  if (side) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (mrow + 16 * i < Mb && ncol + 16 * j + 3 < N)
+          sv[i][j] = *reinterpret_cast<const bf16x4*>(side + row_offs[i] + ncol + 16 * j);
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = mrow + 16 * i;
     const bool mok = m < Mb;
-    int64_t row_off;
-    if constexpr (loader_kind<LA>::value == 5)
-      row_off = mok ? la.out_row(b, m) * ep.ldc : 0;
-    else
-      row_off = cb + (int64_t)m * ep.ldc;
+    const int64_t row_off = row_offs[i];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = ncol + 16 * j;
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] * ep.alpha;
-        if (ep.bias && n + e < N) v[e] += ep.bias[n + e];
-      }
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * ep.alpha + bias[j][e];
       const int64_t off = row_off + n;
       const bool full = mok && n + 3 < N;
       if (ep.act == 3 && mok) {  // GELU backward: the incoming gradient times GELU'(pre-activation)
         const bf16* pa = static_cast<const bf16*>(ep.preact) + off;
         float z[4];
         if (full) {
-          const bf16x4 r = *reinterpret_cast<const bf16x4*>(pa);
+          const bf16x4 r = sv[i][j];
 #pragma unroll
           for (int e = 0; e < 4; ++e) z[e] = (float)r[e];
         } else {
@@ -673,7 +693,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
       if (ep.residual && mok) {  // one 8-byte load per lane (4 scalar 2-byte loads cost +30 % on ResNet dgrads)
         const bf16* ra = static_cast<const bf16*>(ep.residual) + off;
         if (full) {
-          const bf16x4 r = *reinterpret_cast<const bf16x4*>(ra);
+          const bf16x4 r = sv[i][j];
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
         } else {

@@ -16,6 +16,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "gemm256_epilogue.h"
 #include "kernels.h"
 
 namespace ringdp {
@@ -30,7 +31,6 @@ constexpr int TKE = TK / 2;                  // k elements per tile
 constexpr int STAGE = (TM + TN) * TK;        // 64 KiB: A rows then B rows, 128 B each
 constexpr int DMA_PER_WAVE = (TM + TN) * TK / 1024 / 8;  // 8 wave-instructions of 1 KiB per stage
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 
 // 16 B per lane global -> LDS at (wave-uniform base + lane * 16); M0 is set inside the asm.
 __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_wave_base) {
@@ -172,64 +172,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
 
   // ---------------- epilogue: lane holds C[m][n..n+3], m = m0 + wm*128 + 16i + (lane&15),
   //                  n = n0 + wn*64 + 16j + 4*(lane>>4)
-  const int mrow = m0 + wm * 128 + (lane & 15);
-  const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
-  const float dscale = 1.f;
-  if (ep.mode == GemmEpilogue::kSplitK) {
-    float* out = ep.partial + (int64_t)zid * M * N;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mrow + 16 * i;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = ncol + 16 * j;  // N % 4 == 0 (checked by the launcher)
-        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j] * dscale;
-      }
-    }
-    return;
-  }
-  const int64_t cb = (int64_t)b * ep.c_bstride;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mrow + 16 * i;
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = ncol + 16 * j;
-      if (n >= N) continue;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] * dscale * ep.alpha;
-        if (ep.bias) v[e] += ep.bias[n + e];
-      }
-      const int64_t off = cb + (int64_t)m * ep.ldc + n;
-      if (ep.act == 3) {  // GELU backward: times GELU'(pre-activation), preact read
-        const bf16x4 z = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.preact) + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = (float)z[e];
-          v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-        }
-      } else if (ep.preact)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      if (ep.residual) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.residual) + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
-      }
-      if (ep.out_bf16)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      else
-        *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
-    }
-  }
+  gemm256_store<false>(acc, ep, M, N, zid, b, m0 + wm * 128 + (lane & 15), n0 + wn * 64 + 4 * (lane >> 4), 1.f);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -377,63 +320,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* _
 
   // ---------------- epilogue: acc[qm*4+mt][qn*2+nt] holds C[m][n..n+3],
   //   m = m0 + wr*128 + qm*64 + 16 mt + (lane & 15),  n = n0 + wc*64 + qn*32 + 16 nt + 4 (lane >> 4)
-  const int mrow = m0 + wr * 128 + (lane & 15);
-  const int ncol = n0 + wc * 64 + 4 * (lane >> 4);
-  if (ep.mode == GemmEpilogue::kSplitK) {
-    float* out = ep.partial + (int64_t)zid * M * N;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mrow + (i >> 2) * 64 + 16 * (i & 3);
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = ncol + (j >> 1) * 32 + 16 * (j & 1);
-        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j];
-      }
-    }
-    return;
-  }
-  const int64_t cb = (int64_t)b * ep.c_bstride;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mrow + (i >> 2) * 64 + 16 * (i & 3);
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = ncol + (j >> 1) * 32 + 16 * (j & 1);
-      if (n >= N) continue;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] * ep.alpha;
-        if (ep.bias) v[e] += ep.bias[n + e];
-      }
-      const int64_t off = cb + (int64_t)m * ep.ldc + n;
-      if (ep.act == 3) {  // GELU backward: times GELU'(pre-activation), preact read
-        const bf16x4 z = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.preact) + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = (float)z[e];
-          v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-        }
-      } else if (ep.preact)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      if (ep.residual) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.residual) + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
-      }
-      if (ep.out_bf16)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      else
-        *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
-    }
-  }
+  gemm256_store<true>(acc, ep, M, N, zid, b, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + 4 * (lane >> 4), 1.f);
 }
 
 int g_phased = -1;
@@ -455,6 +342,7 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   // runs, whole 8-column chunks of a row-contiguous operand, no statistics epilogue
   if (K % TKE != 0 || N % 4 != 0 || M <= 0 || N <= 0 || ep.stats || A.ld % 8 != 0 || Bop.ld % 8 != 0 ||
       (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0) || ep.scale_a || ep.scale_b ||
+      reinterpret_cast<uintptr_t>(ep.bias) % 16 != 0 ||
       (A.row_contig && (M % 8 != 0 || A.bstride % 8 != 0)) || (Bop.row_contig && (N % 8 != 0 || Bop.bstride % 8 != 0)))
     return false;
   const int tiles_m = (M + TM - 1) / TM, tiles_n = (N + TN - 1) / TN;

@@ -17,6 +17,7 @@
 #include <algorithm>
 
 #include "device_common.h"
+#include "gemm256_epilogue.h"
 #include "kernels.h"
 
 namespace ringdp {
@@ -147,54 +148,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(const uint8_t* __r
   const int mrow = m0 + wm * 128 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
   const float dscale = (ep.scale_a ? ep.scale_a[0] : 1.f) * (ep.scale_b ? ep.scale_b[0] : 1.f);
-  if (ep.mode == GemmEpilogue::kSplitK) {
-    float* out = ep.partial + (int64_t)zid * M * N;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mrow + 16 * i;
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = ncol + 16 * j;  // N % 4 == 0 (checked by the launcher)
-        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j] * dscale;
-      }
-    }
-    return;
-  }
-  const int64_t cb = (int64_t)b * ep.c_bstride;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int m = mrow + 16 * i;
-    if (m >= M) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = ncol + 16 * j;
-      if (n >= N) continue;
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] * dscale * ep.alpha;
-        if (ep.bias) v[e] += ep.bias[n + e];
-      }
-      const int64_t off = cb + (int64_t)m * ep.ldc + n;
-      if (ep.preact)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      if (ep.residual) {
-        const bf16x4 r = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(ep.residual) + off);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
-      }
-      if (ep.out_bf16)
-        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      else
-        *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
-    }
-  }
+  gemm256_store<false>(acc, ep, M, N, zid, b, mrow, ncol, dscale);
 }
 
 }  // namespace
@@ -204,7 +158,8 @@ bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M
   // K-contiguous operands with 16-B aligned rows, whole 128-byte k-steps, whole 4-column runs, no
   // statistics epilogue (BN layers never run in fp8)
   if (A.row_contig || Bop.row_contig || Kbytes % TK != 0 || N % 4 != 0 || M <= 0 || N <= 0 || ep.stats ||
-      A.ld % 16 != 0 || Bop.ld % 16 != 0 || (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0))
+      A.ld % 16 != 0 || Bop.ld % 16 != 0 || (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0) ||
+      reinterpret_cast<uintptr_t>(ep.bias) % 16 != 0)
     return false;
   const int tiles_m = (M + TM - 1) / TM, tiles_n = (N + TN - 1) / TN;
   splits = std::max(1, splits);
