@@ -716,7 +716,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
 //   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a workgroup pair per
 //          image slice (one half of the 576 n columns each).  db3 comes from fc1's backward.
 // Padded d(conv3) image (12x12 positions, 8x8 interior, ring of 2 zeros) in LDS: position (Y, X) at
-// Y*C3_PY + X*C3_PX bf16.  These strides (tools/lds_bank_model_conv3.py: 288-B positions, 3648-B rows)
+// Y*C3_PY + X*C3_PX bf16.  These strides (tools/scratch/lds_bank_model_conv3.py: 288-B positions, 3648-B rows)
 // make every B-fragment read of the dgrad GEMM conflict-free (4 LDS cycles per ds_read_b128, was 7.7
 // with 136-element rows) while each read stays a per-lane base plus an immediate tap offset.
 constexpr int C3_PX = 144;   // bf16 per position (128 + 16)
