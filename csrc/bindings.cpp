@@ -548,6 +548,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
   m.def("set_bf16_tile_mode", &ops::set_bf16_tile_mode, "0 auto, 128 / 256: force the bf16 GEMM tile kernel");
   m.def("set_gemm256_phased", &kern::set_gemm256_phased, "K-contiguous 256x256 GEMM: 1 phased pipeline, 0 older kernel");
+  m.def("set_gemm_wide_store", &kern::set_gemm_wide_store, "256x256 GEMM epilogue: 1 16-B bf16 stores, 0 8-B stores");
   m.def("set_fp8_tile_mode", &ops::set_fp8_tile_mode,
         "fp8 GEMM kernel choice: 0 auto, 128 the generic 128x128 core, 256 the 256x256 DMA-pipelined kernel");
   m.def("f32_conv_fwd", &ops::f32_conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),

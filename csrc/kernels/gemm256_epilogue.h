@@ -12,11 +12,19 @@
 namespace ringdp {
 namespace kern {
 
+
+// 16-B output stores need whole 8-column runs, 16-B aligned rows and base
+__device__ __forceinline__ bool wide_ok(const GemmEpilogue& ep, int N) {
+  return N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 && (ep.c_bstride % 8) == 0;
+}
+
 // QUAD: the phased kernel's tile order (acc[qm*4 + mt][qn*2 + nt], quadrants of 64 rows x 32 cols);
 // otherwise acc[i][j] covers rows mrow + 16 i, columns ncol + 16 j.
+// lds_wave: this wave's 16 KiB of the kernel's LDS (free once the main loop's last barrier has passed):
+// store mode 2 writes the wave's 128 x 64 bf16 tile there and stores it back as whole 128-B rows.
 template <bool QUAD>
 __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep, int M, int N,
-                                              int zid, int bidx, int mrow, int ncol, float scale) {
+                                              int zid, int bidx, int mrow, int ncol, float scale, char* lds_wave) {
   using namespace ringdp::dev;
   auto mof = [&](int i) { return QUAD ? mrow + (i >> 2) * 64 + 16 * (i & 3) : mrow + 16 * i; };
   auto nof = [&](int j) { return QUAD ? ncol + (j >> 1) * 32 + 16 * (j & 1) : ncol + 16 * j; };
@@ -54,6 +62,128 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
       }
   }
   // ---- compute + stores
+  // bf16 output with whole 8-column runs: lanes l and l ^ 16 (same row, adjacent 4-column groups)
+  // exchange one of their two vertically adjacent tiles, so each stores 8 consecutive bf16 (16 B)
+  // instead of 4 (8 B): half the store instructions of a store-issue-bound epilogue (guide T21).
+  if (ep.out_bf16 && ep.store_mode == 3) {  // probe: compute but never store
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
+  if (ep.out_bf16 && ep.store_mode == 2 && wide_ok(ep, N)) {
+    // final values -> bf16 -> LDS image [128 rows][64 cols] (128-B rows, 16-B chunk c of row r at c ^ (r & 7)),
+    // then 8 lanes per row store whole 128-B rows
+    const int lane = threadIdx.x & 63;
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = mof(i), n = nof(j);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * scale * ep.alpha + bias[j][e];
+        const int64_t off = cb + (int64_t)m * ep.ldc + n;
+        if (ep.act == 3) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = (float)sv[i][j][e];
+            v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+          }
+        } else if (ep.preact && m < M && n < N) {
+          *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        }
+        if (ep.residual) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)sv[i][j][e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+          else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+        }
+        const int r = (QUAD ? (i >> 2) * 64 + 16 * (i & 3) : 16 * i) + fr;    // row in the wave tile
+        const int c = QUAD ? (j >> 1) * 32 + 16 * (j & 1) + 4 * fq : 16 * j + 4 * fq;  // column
+        *reinterpret_cast<bf16x4*>(lds_wave + r * 128 + ((((c >> 3) ^ (r & 7)) << 4) | ((c & 7) << 1))) =
+            bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      }
+    }
+    // each wave reads back only what it wrote (LDS executes one wave's operations in order)
+    const int m_base = mrow - fr, n_base = ncol - 4 * fq;  // the wave tile's first row / column
+    // Row order rotated per wave tile: in lockstep, every wave of every block would write the same row
+    // offset at the same moment, i.e. addresses a multiple of 128 rows apart - on a few memory channels.
+    const int rot = ep.store_rot ? (((m_base >> 7) * 5 + (n_base >> 6) * 3) & 15) : 0;
+#pragma unroll
+    for (int k0 = 0; k0 < 16; ++k0) {
+      const int k = (k0 + rot) & 15;
+      const int r = 8 * k + (lane >> 3), ch = lane & 7;
+      const uint4 w = *reinterpret_cast<const uint4*>(lds_wave + r * 128 + ((ch ^ (r & 7)) << 4));
+      const int m = m_base + r, n = n_base + 8 * ch;
+      if (m < M && n < N)
+        *reinterpret_cast<uint4*>(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + n) = w;
+    }
+    return;
+  }
+  const bool wide = ep.out_bf16 && ep.store_mode == 1 && wide_ok(ep, N);
+  if (wide) {
+    const int lane = threadIdx.x & 63;
+    const bool upper = (lane >> 4) & 1;  // odd 4-column group: keeps the lower tile of the pair
+#pragma unroll
+    for (int i2 = 0; i2 < 8; i2 += 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nof(j);
+        unsigned pk[2][2];  // [tile of the pair][2 x packed bf16 pair]
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int i = i2 + t;
+          const int m = mof(i);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * scale * ep.alpha + bias[j][e];
+          const int64_t off = cb + (int64_t)m * ep.ldc + n;
+          if (ep.act == 3) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x = (float)sv[i][j][e];
+              v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+            }
+          } else if (ep.preact && m < M && n < N) {
+            *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) =
+                bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          }
+          if (ep.residual) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)sv[i][j][e];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+            else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+          }
+          const bf16x4 q = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          const unsigned* qu = reinterpret_cast<const unsigned*>(&q);
+          pk[t][0] = qu[0];
+          pk[t][1] = qu[1];
+        }
+        // the lower lane sends its upper tile, the upper lane its lower tile
+        const unsigned s0 = upper ? pk[0][0] : pk[1][0], s1 = upper ? pk[0][1] : pk[1][1];
+        const unsigned r0 = __shfl_xor(s0, 16, 64), r1 = __shfl_xor(s1, 16, 64);
+        const int i = upper ? i2 + 1 : i2;
+        const int m = mof(i);
+        const int nc = upper ? n - 4 : n;  // first of the 8 columns this lane stores
+        if (m < M && nc < N) {
+          uint4 w;
+          if (upper) w = make_uint4(r0, r1, pk[1][0], pk[1][1]);
+          else w = make_uint4(pk[0][0], pk[0][1], r0, r1);
+          *reinterpret_cast<uint4*>(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + nc) = w;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int m = mof(i);

@@ -172,7 +172,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
 
   // ---------------- epilogue: lane holds C[m][n..n+3], m = m0 + wm*128 + 16i + (lane&15),
   //                  n = n0 + wn*64 + 16j + 4*(lane>>4)
-  gemm256_store<false>(acc, ep, M, N, zid, b, m0 + wm * 128 + (lane & 15), n0 + wn * 64 + 4 * (lane >> 4), 1.f);
+  gemm256_store<false>(acc, ep, M, N, zid, b, m0 + wm * 128 + (lane & 15), n0 + wn * 64 + 4 * (lane >> 4), 1.f,
+                       smem + wave * 16384);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -320,7 +321,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* _
 
   // ---------------- epilogue: acc[qm*4+mt][qn*2+nt] holds C[m][n..n+3],
   //   m = m0 + wr*128 + qm*64 + 16 mt + (lane & 15),  n = n0 + wc*64 + qn*32 + 16 nt + 4 (lane >> 4)
-  gemm256_store<true>(acc, ep, M, N, zid, b, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + 4 * (lane >> 4), 1.f);
+  gemm256_store<true>(acc, ep, M, N, zid, b, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + 4 * (lane >> 4), 1.f,
+                      smem + wave * 16384);
 }
 
 int g_phased = -1;
@@ -335,6 +337,16 @@ int phased_mode() {
 }  // namespace
 
 void set_gemm256_phased(int on) { g_phased = on ? 1 : 0; }
+
+static int g_wide = -1;
+int gemm_wide_store_mode() {
+  if (g_wide < 0) {
+    const char* v = getenv("RINGDP_GEMM_WIDE_STORE");
+    g_wide = v && *v ? atoi(v) : 2;
+  }
+  return g_wide;
+}
+void set_gemm_wide_store(int mode) { g_wide = mode; }
 
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s) {
@@ -351,9 +363,12 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   kps = (kps + TKE - 1) / TKE * TKE;
   splits = (K + kps - 1) / kps;
   dim3 grid(tiles_m * tiles_n, batch * splits);
+  GemmEpilogue e2 = ep;
+  e2.store_mode = gemm_wide_store_mode() % 10;
+  e2.store_rot = gemm_wide_store_mode() < 10;
   auto go = [&](auto kern) {
     kern<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
-                              static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, ep, M, N, K * 2,
+                              static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M, N, K * 2,
                               tiles_m, tiles_n, splits, kps * 2);
   };
   if (!A.row_contig && !Bop.row_contig) {

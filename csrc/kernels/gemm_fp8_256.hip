@@ -148,7 +148,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(const uint8_t* __r
   const int mrow = m0 + wm * 128 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
   const float dscale = (ep.scale_a ? ep.scale_a[0] : 1.f) * (ep.scale_b ? ep.scale_b[0] : 1.f);
-  gemm256_store<false>(acc, ep, M, N, zid, b, mrow, ncol, dscale);
+  gemm256_store<false>(acc, ep, M, N, zid, b, mrow, ncol, dscale, smem + wave * 16384);
 }
 
 }  // namespace
@@ -167,8 +167,11 @@ bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M
   kps = (kps + TK - 1) / TK * TK;
   splits = (Kbytes + kps - 1) / kps;
   dim3 grid(tiles_m * tiles_n, batch * splits);
+  GemmEpilogue e2 = ep;
+  e2.store_mode = gemm_wide_store_mode() % 10;
+  e2.store_rot = gemm_wide_store_mode() < 10;
   gemm_fp8_256_kernel<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld, A.bstride,
-                                           static_cast<const uint8_t*>(Bop.p), Bop.ld, Bop.bstride, ep, M, N, Kbytes,
+                                           static_cast<const uint8_t*>(Bop.p), Bop.ld, Bop.bstride, e2, M, N, Kbytes,
                                            tiles_m, tiles_n, splits, kps);
   return true;
 }
