@@ -560,6 +560,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_pool_relu_bwd", &ops::f32_pool_relu_bwd);
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
+  m.def("cn_conv1_fwd_pack", &ops::cn_conv1_fwd_pack);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);
   m.def("cn_conv3_fc_fwd", &ops::cn_conv3_fc_fwd);
   m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd);

@@ -57,13 +57,19 @@ constexpr int PFC_OFF = P3D_OFF + P3D_N, PFC_N = 16 * 128 * 10; // fc1 [window][
 constexpr int PFF_OFF = PFC_OFF + PFC_N, PFF_N = 64 * 64 * 8;    // fc1 fwd B fragments, k = w*128 + co
 constexpr int PACK_TOTAL = PFF_OFF + PFF_N;
 
-__global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ w1,
-                                                           const float* __restrict__ w2,
-                                                           const float* __restrict__ w3,
-                                                           const float* __restrict__ wfc,
-                                                           bf16* __restrict__ out) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= PACK_TOTAL) return;
+struct PackSrc {
+  const float* w1;
+  const float* w2;
+  const float* w3;
+  const float* wfc;
+};
+
+// fp32 master weight of packed element e
+__device__ __forceinline__ float pack_value(int e, const PackSrc& ws) {
+  const float* __restrict__ w1 = ws.w1;
+  const float* __restrict__ w2 = ws.w2;
+  const float* __restrict__ w3 = ws.w3;
+  const float* __restrict__ wfc = ws.wfc;
   float v = 0.f;
   if (e < P2F_OFF) {  // [nt][ks][lane][8]: k = ks*32 + 8*(lane>>4) + j -> kh = ks*4 + (lane>>4), kw = j
     // n-tile nt, column c = channel 2c + nt: a lane's two accumulator tiles are a channel pair
@@ -102,7 +108,22 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
     const int n = lane & 15, k = ks * 32 + 8 * (lane >> 4) + j;
     v = n < 10 ? wfc[n * 2048 + (k & 127) * 16 + (k >> 7)] : 0.f;
   }
-  out[e] = (bf16)v;
+  return v;
+}
+
+// packs elements [first, PACK_TOTAL) with `nblocks` workgroups (this one is `blk`), 4 per thread
+__device__ __forceinline__ void pack_range(const PackSrc& ws, bf16* __restrict__ out, int first, int blk, int nblocks) {
+  for (int e0 = first + 4 * (blk * 256 + (int)threadIdx.x); e0 < PACK_TOTAL; e0 += 4 * 256 * nblocks) {
+    bf16x4 q;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = (bf16)pack_value(e0 + j, ws);  // PACK_TOTAL % 4 == 0
+    *reinterpret_cast<bf16x4*>(out + e0) = q;
+  }
+}
+static_assert(PACK_TOTAL % 4 == 0 && P2F_OFF % 4 == 0, "packed regions in whole 8-B runs");
+
+__global__ __launch_bounds__(256) void pack_weights_kernel(PackSrc ws, bf16* __restrict__ out) {
+  pack_range(ws, out, 0, blockIdx.x, gridDim.x);
 }
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -276,13 +297,22 @@ constexpr int C1F_MT = 11;  // m-tiles per wave (wave 3: 10)
 constexpr int C1F_CS = 1048;
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
-template <bool U8>
+// PACK: this launch also packs every layer's weights (cn_pack_weights) for the kernels after it: workgroups
+// >= conv_blocks do only that, and the conv1 workgroups build their own fragments from the fp32 masters
+// (one launch per step fewer; at the reference batch every launch is ~5 us of a ~100 us step).
+template <bool U8, bool PACK>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__ xin,
                                                         const bf16* __restrict__ packed,
                                                         const float* __restrict__ bias,
                                                         bf16* __restrict__ a1,
                                                         uint8_t* __restrict__ idx1, int B,
-                                                        float mean, float inv_std, float in_scale) {
+                                                        float mean, float inv_std, float in_scale,
+                                                        PackSrc ws, bf16* __restrict__ pack_out,
+                                                        int conv_blocks) {
+  if (PACK && (int)blockIdx.x >= conv_blocks) {
+    pack_range(ws, pack_out, 0, blockIdx.x - conv_blocks, gridDim.x - conv_blocks);
+    return;
+  }
   __shared__ __attribute__((aligned(16))) bf16 xs[2][8 * C1F_CS];
   __shared__ __attribute__((aligned(16))) uint32_t ot[172 * 16];      // rows >= 169: dropped tiles
   __shared__ __attribute__((aligned(16))) uint8_t ct[C1I_IMG + 64];   // + a dump row for them
@@ -293,7 +323,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) bw[nt][ks] = pk[(nt * 2 + ks) * 64 + lane];
+    for (int ks = 0; ks < 2; ++ks) {
+      if (PACK) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bw[nt][ks][j] = (bf16)pack_value(P1_OFF + ((nt * 2 + ks) * 64 + lane) * 8 + j, ws);
+      } else {
+        bw[nt][ks] = pk[(nt * 2 + ks) * 64 + lane];
+      }
+    }
   const float bias0 = bias[2 * r16], bias1 = bias[2 * r16 + 1];
   const f32x4 bias0v = {bias0, bias0, bias0, bias0}, bias1v = {bias1, bias1, bias1, bias1};
   // per m-tile: A-row offset inside a copy buffer (elements; kh row added per k-step) and code offset
@@ -319,8 +356,9 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const void* __restrict__
   }
   __syncthreads();
   int cur = 0;
-  for (; b < B; b += gridDim.x) {
-    const int nb = b + gridDim.x;
+  const int nblk = PACK ? conv_blocks : (int)gridDim.x;
+  for (; b < B; b += nblk) {
+    const int nb = b + nblk;
     if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
     const bf16* x = xs[cur];
     // software-pipelined: the MFMAs of tile j are issued before the epilogue of tile j-1
@@ -505,14 +543,29 @@ __device__ __forceinline__ void a2_relayout(const bf16* R, bf16* X, int tid, int
 constexpr int C3F_XRS = 80;
 __constant__ uint8_t c3f_win[16] = {1, 9, 13, 11, 10, 3, 15, 8, 7, 12, 0, 5, 4, 6, 2, 14};
 
+// FC (small batches): fc1 runs in this launch too.  Each lane multiplies its 8 pooled values by their
+// 10 fc1 weights (the [window][co][n] pack, staged in LDS once per workgroup) and the 256 lanes' partial
+// logits are summed through LDS in a fixed order.  At B <= a few thousand the separate fc1 launch (and
+// its ~1.5 us kernel boundary) cost more than this; at large B the MFMA fc1 pass over a3 is cheaper.
+constexpr int C3F_FCW = 16 * 128 * 10;  // bf16 fc1 weights in LDS
+template <bool FC>
 __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restrict__ a2,
                                                            const bf16* __restrict__ packed,
                                                            const float* __restrict__ bias,
                                                            bf16* __restrict__ a3,
-                                                           uint8_t* __restrict__ idx3, int B) {
+                                                           uint8_t* __restrict__ idx3, int B,
+                                                           const float* __restrict__ bfc,
+                                                           float* __restrict__ logits) {
   __shared__ __attribute__((aligned(16))) bf16 R[100 * 64];
   __shared__ __attribute__((aligned(16))) bf16 X[100 * C3F_XRS];
+  __shared__ __attribute__((aligned(16))) char fcs[FC ? C3F_FCW * 2 + 10 * 256 * 4 : 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  bf16* fw = reinterpret_cast<bf16*>(fcs);                      // [window][co][n]
+  float* fred = reinterpret_cast<float*>(fcs + C3F_FCW * 2);    // [n][256 lanes]
+  if (FC) {
+    const uint4* src = reinterpret_cast<const uint4*>(packed + PFC_OFF);
+    for (int c = tid; c < C3F_FCW / 8; c += 256) reinterpret_cast<uint4*>(fw)[c] = src[c];
+  }
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
   const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3F_OFF);
   bf16x8 bw[2][18];
@@ -552,6 +605,9 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
         acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
       }
     }
+    float part[10];
+#pragma unroll
+    for (int n = 0; n < 10; ++n) part[n] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -562,7 +618,33 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
         const int64_t o = ((int64_t)b * 16 + wc) * 128 + co;
         a3[o] = pb;
         idx3[o] = (uint8_t)g;
+        if (FC) {
+          const float pv = (float)pb;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(fw + (wc * 128 + co) * 10);  // 4-B aligned
+#pragma unroll
+          for (int h = 0; h < 5; ++h) {
+            const uint32_t u = wp[h];
+            part[2 * h] = fmaf(pv, __uint_as_float(u << 16), part[2 * h]);
+            part[2 * h + 1] = fmaf(pv, __uint_as_float(u & 0xffff0000u), part[2 * h + 1]);
+          }
+        }
       }
+    if (FC) {
+#pragma unroll
+      for (int n = 0; n < 10; ++n) fred[n * 256 + tid] = part[n];
+      __syncthreads();
+      // 160 threads: logit n = t >> 4 sums lanes c + 16 i (i < 16), then 16 lanes combine by shuffles
+      if (tid < 160) {
+        const int n = tid >> 4, c = tid & 15;
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v += fred[n * 256 + c + 16 * i];
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (c == 0) logits[(int64_t)b * 10 + n] = v + bfc[n];
+      }
+      // the next image's top barrier orders these reads before fred is rewritten
+    }
   }
 }
 
@@ -1613,6 +1695,15 @@ int num_cus() {
 
 inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// largest batch whose fc1 runs inside the conv3 forward launch (RINGDP_CN_FC_FUSED_MAX overrides)
+int fc_fused_max_batch() {
+  static const int v = [] {
+    const char* e = std::getenv("RINGDP_CN_FC_FUSED_MAX");
+    return e ? std::atoi(e) : 4096;
+  }();
+  return v;
+}
+
 // workgroups per CU of a persistent forward kernel; RINGDP_CN_WPC_<name> overrides (A/B runs)
 int wpc(const char* name, int dflt) {
   char key[64];
@@ -1628,17 +1719,31 @@ int64_t cn_packed_elems() { return PACK_TOTAL; }
 
 void cn_pack_weights(const float* w1, const float* w2, const float* w3, const float* wfc, void* out,
                      hipStream_t s) {
-  pack_weights_kernel<<<cdiv(PACK_TOTAL, 256), 256, 0, s>>>(w1, w2, w3, wfc, static_cast<bf16*>(out));
+  pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(PackSrc{w1, w2, w3, wfc}, static_cast<bf16*>(out));
 }
 
 void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
-                  int B, float mean, float inv_std, float in_scale, hipStream_t s) {
+                  int B, float mean, float inv_std, float in_scale, hipStream_t s, const float* const* pack_w,
+                  void* pack_out) {
   const int grid = clampi(B, 1, wpc("C1F", 3) * num_cus());  // 51 KiB LDS: 3 workgroups per CU
   const bf16* pk = static_cast<const bf16*>(packed);
+  bf16* a1b = static_cast<bf16*>(a1);
+  if (pack_w) {
+    // + the pack workgroups (4 elements per thread): PACK_TOTAL / 1024 of them
+    const PackSrc ws{pack_w[0], pack_w[1], pack_w[2], pack_w[3]};
+    const int g = grid + cdiv(PACK_TOTAL, 1024);
+    bf16* po = static_cast<bf16*>(pack_out);
+    if (u8)
+      conv1_fwd_kernel<true, true><<<g, 256, 0, s>>>(x, pk, b1, a1b, idx1, B, mean, inv_std, in_scale, ws, po, grid);
+    else
+      conv1_fwd_kernel<false, true><<<g, 256, 0, s>>>(x, pk, b1, a1b, idx1, B, mean, inv_std, in_scale, ws, po, grid);
+    return;
+  }
+  const PackSrc none{nullptr, nullptr, nullptr, nullptr};
   if (u8)
-    conv1_fwd_kernel<true><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
+    conv1_fwd_kernel<true, false><<<grid, 256, 0, s>>>(x, pk, b1, a1b, idx1, B, mean, inv_std, in_scale, none, nullptr, grid);
   else
-    conv1_fwd_kernel<false><<<grid, 256, 0, s>>>(x, pk, b1, static_cast<bf16*>(a1), idx1, B, mean, inv_std, in_scale);
+    conv1_fwd_kernel<false, false><<<grid, 256, 0, s>>>(x, pk, b1, a1b, idx1, B, mean, inv_std, in_scale, none, nullptr, grid);
 }
 
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,
@@ -1651,10 +1756,14 @@ void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2,
 void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s) {
   const int grid = clampi(B, 1, wpc("C3F", 2) * num_cus());
-  conv3_fwd_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(a2), static_cast<const bf16*>(packed), b3,
-                                        static_cast<bf16*>(a3), idx3, B);
-  fc1_fwd_kernel<<<cdiv(B, 16 * FC1_G), 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), bfc,
-                                             logits, B);
+  const bf16* a2b = static_cast<const bf16*>(a2);
+  const bf16* pk = static_cast<const bf16*>(packed);
+  if (B <= fc_fused_max_batch()) {
+    conv3_fwd_kernel<true><<<grid, 256, 0, s>>>(a2b, pk, b3, static_cast<bf16*>(a3), idx3, B, bfc, logits);
+    return;
+  }
+  conv3_fwd_kernel<false><<<grid, 256, 0, s>>>(a2b, pk, b3, static_cast<bf16*>(a3), idx3, B, nullptr, nullptr);
+  fc1_fwd_kernel<<<cdiv(B, 16 * FC1_G), 256, 0, s>>>(static_cast<const bf16*>(a3), pk, bfc, logits, B);
 }
 
 // Work split of the role-fused backward launches.  All blocks of a launch are co-resident (one

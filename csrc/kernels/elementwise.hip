@@ -306,6 +306,14 @@ __global__ __launch_bounds__(256) void ce_fwd_kernel(const float* __restrict__ l
     }
     __syncthreads();
   }
+  if (nparts == 1) {  // one block (B <= 256 rows for small C): no cross-block hand-off, no fences
+    if (tid == 0) {
+      const float denom = reduction == 1 ? s_cnt[0] : 1.f;
+      partials[2 * nparts] = denom;
+      loss[0] = reduction == 1 ? s_sum[0] / denom : s_sum[0];
+    }
+    return;
+  }
   if (tid == 0) {
     partials[2 * blockIdx.x] = s_sum[0];
     partials[2 * blockIdx.x + 1] = s_cnt[0];

@@ -135,8 +135,11 @@ int64_t cn_packed_elems();
 void cn_pack_weights(const float* w1, const float* w2, const float* w3, const float* wfc, void* out,
                      hipStream_t s);
 // F1: conv1 + ReLU + pool1 (x u8 or fp32 [B,28,28]; normalisation fused).
+// pack_w = {w1, w2, w3, wfc}: the same launch also packs every layer's weights into pack_out (then
+// `packed` is not read: conv1 builds its fragments from w1).
 void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, void* a1, uint8_t* idx1,
-                  int B, float mean, float inv_std, float in_scale, hipStream_t s);
+                  int B, float mean, float inv_std, float in_scale, hipStream_t s,
+                  const float* const* pack_w = nullptr, void* pack_out = nullptr);
 // F2: conv2 + bias + ReLU + pool2 (2x2/s1) -> a2 [B,10,10,64] + pool2 codes idx2 [B,10,10,64]
 // (0..3 = first-max position in the window, bit 2 = pooled value 0 / no gradient).
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,

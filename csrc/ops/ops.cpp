@@ -349,6 +349,34 @@ std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::T
   return {a1, idx};
 }
 
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv1_fwd_pack(const at::Tensor& x, const at::Tensor& w1,
+                                                                 const at::Tensor& w2, const at::Tensor& w3,
+                                                                 const at::Tensor& wfc, const at::Tensor& b1,
+                                                                 double mean, double std, double in_scale) {
+  int64_t B;
+  bool u8;
+  check_input(x, B, u8);
+  RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
+  check_f32_out(w1, {32, 1, 5, 5}, "conv1 weight");
+  check_f32_out(w2, {64, 32, 3, 3}, "conv2 weight");
+  check_f32_out(w3, {128, 64, 3, 3}, "conv3 weight");
+  check_f32_out(wfc, {10, 2048}, "fc1 weight");
+  check_f32_out(b1, {32}, "conv1 bias");
+  auto opt = x.options();
+  at::Tensor packed = at::empty({kern::cn_packed_elems()}, w1.options().dtype(at::kBFloat16));
+  at::Tensor a1 = at::empty({B, 13, 13, 32}, opt.dtype(at::kBFloat16));
+  at::Tensor idx = at::empty({B, 13, 16, 16}, opt.dtype(at::kByte));
+  const float* pw[4] = {w1.data_ptr<float>(), w2.data_ptr<float>(), w3.data_ptr<float>(), wfc.data_ptr<float>()};
+  if (B == 0) {
+    kern::cn_pack_weights(pw[0], pw[1], pw[2], pw[3], packed.data_ptr(), cur_stream(w1));
+    return {a1, idx, packed};
+  }
+  kern::cn_conv1_fwd(x.data_ptr(), u8, nullptr, b1.data_ptr<float>(), a1.data_ptr(), idx.data_ptr<uint8_t>(),
+                     static_cast<int>(B), static_cast<float>(mean), static_cast<float>(1.0 / std),
+                     static_cast<float>(in_scale), cur_stream(x), pw, packed.data_ptr());
+  return {a1, idx, packed};
+}
+
 std::tuple<at::Tensor, at::Tensor> cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed,
                                                 const at::Tensor& b2) {
   const int64_t B = a1.size(0);

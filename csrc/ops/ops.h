@@ -63,6 +63,11 @@ std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::T
                                                 double in_scale);
 std::tuple<at::Tensor, at::Tensor> cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed,
                                                 const at::Tensor& b2);
+// conv1 forward that also packs every layer's weights in the same launch: (a1, idx1, packed)
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv1_fwd_pack(const at::Tensor& x, const at::Tensor& w1,
+                                                                 const at::Tensor& w2, const at::Tensor& w3,
+                                                                 const at::Tensor& wfc, const at::Tensor& b1,
+                                                                 double mean, double std, double in_scale);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor& a2,
                                                                const at::Tensor& packed,
                                                                const at::Tensor& b3,

@@ -15,7 +15,7 @@ for it (autograd's handle on "the gradient of conv2's output") next to the real 
 backward is a plain linear-layer backward and pool2/ReLU backward costs no extra pass over
 memory.  Weights are packed
 once per forward into bf16 MFMA fragments (``C.cn_pack_weights``); the fp32 masters stay the
-parameters.  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
+parameters (packed inside conv1's launch on the default path).  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
 ``_Conv3FC.backward`` - so ringdp's reducer starts the first bucket all-reduce while conv2/conv1
 backward kernels still run.
 """
@@ -83,19 +83,21 @@ class _Conv12(torch.autograd.Function):
     (conv2 dgrad + wgrad, conv1 wgrad on the LDS-resident da1) and one reduction launch."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, packed, mean, std, in_scale):
-        a1, idx1 = C.cn_conv1_fwd(x, packed, b1, mean, std, in_scale)
+    def forward(ctx, x, w1, b1, w2, b2, w3, wfc, mean, std, in_scale):
+        # conv1's launch also packs every layer's bf16 MFMA fragments (w3 / wfc arrive detached: this
+        # node only reads them for the packing)
+        a1, idx1, packed = C.cn_conv1_fwd_pack(x, w1, w2, w3, wfc, b1, mean, std, in_scale)
         a2, idx2 = C.cn_conv2_fwd(a1, packed, b2)
         z2 = a2.new_empty((1, 1, 1, 1)).expand(a1.shape[0], 11, 11, 64)  # placeholder, never read
-        ctx.mark_non_differentiable(a2, idx2)
+        ctx.mark_non_differentiable(a2, idx2, packed)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(x, idx1, a1, packed)
         ctx.params = (w1, b1, w2, b2)
         ctx.norm = (mean, std, in_scale)
-        return z2, a2, idx2
+        return z2, a2, idx2, packed
 
     @staticmethod
-    def backward(ctx, dz2, _da2, _didx2):
+    def backward(ctx, dz2, _da2, _didx2, _dpacked):
         x, idx1, a1, packed = ctx.saved_tensors
         w1, b1, w2, b2 = ctx.params
         n = ctx.needs_input_grad
@@ -103,7 +105,7 @@ class _Conv12(torch.autograd.Function):
         if n[1] and n[2] and n[3] and n[4]:
             dw1, db1, dw2, db2 = (grad_buffer(t) for t in (w1, b1, w2, b2))
             C.cn_conv12_bwd(x, idx1, a1, dz2, packed, dw2, db2, dw1, db1, *ctx.norm)
-            return None, dw1, db1, dw2, db2, None, None, None, None
+            return None, dw1, db1, dw2, db2, None, None, None, None, None
         # partially frozen: the separate kernels
         need_c1 = n[1] or n[2]
         dw2, db2 = grad_buffer(w2), grad_buffer(b2)
@@ -113,7 +115,7 @@ class _Conv12(torch.autograd.Function):
             dw1, db1 = grad_buffer(w1), grad_buffer(b1)
             C.cn_conv1_wgrad(x, da1, idx1, dw1, db1, *ctx.norm)
         return (None, dw1 if n[1] else None, db1 if n[2] else None, dw2 if n[3] else None,
-                db2 if n[4] else None, None, None, None, None)
+                db2 if n[4] else None, None, None, None, None, None)
 
 
 class _Conv3FC(torch.autograd.Function):
@@ -153,10 +155,11 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         x = x.float()
         mean, std, scale = 0.0, 1.0, 1.0
     x = x.contiguous()
-    packed = pack_weights(conv1, conv2, conv3, fc1)
     if _FUSE12:
-        z2, a2, idx2 = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias, packed, mean, std, scale)
+        z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
+                                             conv3.weight.detach(), fc1.weight.detach(), mean, std, scale)
     else:
+        packed = pack_weights(conv1, conv2, conv3, fc1)
         a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
         z2, a2, idx2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
     return _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)
