@@ -196,7 +196,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
 __device__ __forceinline__ void glds16_async(const void* gsrc, void* lds_wave_base) {
   const unsigned base = __builtin_amdgcn_readfirstlane(
       (unsigned)(size_t)((__attribute__((address_space(3))) char*)(lds_wave_base)));
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
 }
 __device__ __forceinline__ void c_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

@@ -13,6 +13,22 @@ namespace ringdp {
 namespace kern {
 
 
+typedef unsigned int gemm_u32x4 __attribute__((ext_vector_type(4)));
+
+// One 16-B output store in the cache flavour ep.store_cache: 0 plain (the line stays in the XCD's L2),
+// 1 nontemporal (`nt`), 2 write-through `sc1` (the line leaves L2: the output does not evict the operand
+// panels the next tiles read).  Asm stores end with s_nop 1 (their data VGPRs are read after issue).
+__device__ __forceinline__ void gemm_st16(void* p, uint4 v, int flavour) {
+  const gemm_u32x4 w = {v.x, v.y, v.z, v.w};
+  if (flavour == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  } else if (flavour == 1) {
+    __builtin_nontemporal_store(w, reinterpret_cast<gemm_u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+
 // 16-B output stores need whole 8-column runs, 16-B aligned rows and base
 __device__ __forceinline__ bool wide_ok(const GemmEpilogue& ep, int N) {
   return N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 && (ep.c_bstride % 8) == 0;
@@ -121,8 +137,7 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
       const int r = 8 * k + (lane >> 3), ch = lane & 7;
       const uint4 w = *reinterpret_cast<const uint4*>(lds_wave + r * 128 + ((ch ^ (r & 7)) << 4));
       const int m = m_base + r, n = n_base + 8 * ch;
-      if (m < M && n < N)
-        *reinterpret_cast<uint4*>(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + n) = w;
+      if (m < M && n < N) gemm_st16(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + n, w, ep.store_cache);
     }
     return;
   }
@@ -218,6 +233,139 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
         *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       else
         *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Epilogue of the persistent kernels (gemm_bf16_256q): no LDS (the next tile's first k-tile is already
+// landing there) and an EXACT number of store instructions per lane, gemm256_q_stores(ep): stores past the
+// M / N edge go to ep.sink instead of being skipped, so the kernel can count them in its vmcnt waits.
+// bf16 outputs need wide_ok (checked by the launcher).
+__device__ __forceinline__ int gemm256_q_stores(const GemmEpilogue& ep) {
+  if (ep.mode == GemmEpilogue::kSplitK || !ep.out_bf16) return 32;
+  return (ep.preact && ep.act != 3) ? 48 : 16;
+}
+
+__device__ __forceinline__ float gemm_gelu_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+template <bool QUAD>
+__device__ __forceinline__ void gemm256_store_q(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep, int M, int N,
+                                                int zid, int bidx, int mrow, int ncol, float scale) {
+  using namespace ringdp::dev;
+  auto mof = [&](int i) { return QUAD ? mrow + (i >> 2) * 64 + 16 * (i & 3) : mrow + 16 * i; };
+  auto nof = [&](int j) { return QUAD ? ncol + (j >> 1) * 32 + 16 * (j & 1) : ncol + 16 * j; };
+  char* sink = static_cast<char*>(ep.sink);
+  if (ep.mode == GemmEpilogue::kSplitK || !ep.out_bf16) {
+    float* out = ep.mode == GemmEpilogue::kSplitK ? ep.partial + (int64_t)zid * M * N
+                                                   : static_cast<float*>(ep.C) + (int64_t)bidx * ep.c_bstride;
+    const int64_t ld = ep.mode == GemmEpilogue::kSplitK ? N : ep.ldc;
+    const bool plain = ep.mode == GemmEpilogue::kSplitK;
+    f32x4 bias[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nof(j);
+      bias[j] = (!plain && ep.bias && n < N) ? *reinterpret_cast<const f32x4*>(ep.bias + n) : zero_f32x4();
+    }
+    const bf16* res = plain ? nullptr : static_cast<const bf16*>(ep.residual);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mof(i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nof(j);
+        const bool ok = m < M && n < N;
+        f32x4 v = acc[i][j] * scale;
+        if (!plain) {
+          v = v * ep.alpha + bias[j];
+          if (res && ok) {
+            const bf16x4 r = *reinterpret_cast<const bf16x4*>(res + (int64_t)bidx * ep.c_bstride + (int64_t)m * ep.ldc + n);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+            else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+          }
+        }
+        void* dst = ok ? static_cast<void*>(out + (int64_t)m * ld + n) : static_cast<void*>(sink);
+        gemm_st16(dst, __builtin_bit_cast(uint4, v), ep.store_cache);
+      }
+    }
+    return;
+  }
+  const int64_t cb = (int64_t)bidx * ep.c_bstride;
+  f32x4 bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = nof(j);
+    bias[j] = (ep.bias && n < N) ? *reinterpret_cast<const f32x4*>(ep.bias + n) : zero_f32x4();
+  }
+  const bf16* side = static_cast<const bf16*>(ep.residual ? ep.residual : (ep.act == 3 ? ep.preact : nullptr));
+  bf16x4 sv[8][4];
+  if (side) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = min(mof(i), M - 1), n = min(nof(j), N - 4);
+        sv[i][j] = *reinterpret_cast<const bf16x4*>(side + cb + (int64_t)m * ep.ldc + n);
+      }
+  }
+  const bool store_pre = ep.preact && ep.act != 3;
+  const int lane = threadIdx.x & 63;
+  const bool upper = (lane >> 4) & 1;  // odd 4-column group: keeps the lower tile of the pair
+#pragma unroll
+  for (int i2 = 0; i2 < 8; i2 += 2) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nof(j);
+      unsigned pk[2][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int i = i2 + t;
+        const int m = mof(i);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * scale * ep.alpha + bias[j][e];
+        if (ep.act == 3) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= gemm_gelu_grad((float)sv[i][j][e]);
+        } else if (store_pre) {
+          const bool ok = m < M && n < N;
+          bf16x4* pd = ok ? reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + cb + (int64_t)m * ep.ldc + n)
+                          : reinterpret_cast<bf16x4*>(sink);
+          *pd = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        }
+        if (ep.residual) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)sv[i][j][e];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
+          else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+        }
+        const bf16x4 q = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        const unsigned* qu = reinterpret_cast<const unsigned*>(&q);
+        pk[t][0] = qu[0];
+        pk[t][1] = qu[1];
+      }
+      const unsigned s0 = upper ? pk[0][0] : pk[1][0], s1 = upper ? pk[0][1] : pk[1][1];
+      const unsigned r0 = __shfl_xor(s0, 16, 64), r1 = __shfl_xor(s1, 16, 64);
+      const int i = upper ? i2 + 1 : i2;
+      const int m = mof(i);
+      const int nc = upper ? n - 4 : n;  // first of the 8 columns this lane stores
+      uint4 w;
+      if (upper) w = make_uint4(r0, r1, pk[1][0], pk[1][1]);
+      else w = make_uint4(pk[0][0], pk[0][1], r0, r1);
+      const bool ok = m < M && nc < N;
+      uint4* dst = ok ? reinterpret_cast<uint4*>(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + nc)
+                      : reinterpret_cast<uint4*>(sink);
+      gemm_st16(dst, w, ep.store_cache);
     }
   }
 }

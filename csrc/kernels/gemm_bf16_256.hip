@@ -36,7 +36,20 @@ constexpr int DMA_PER_WAVE = (TM + TN) * TK / 1024 / 8;  // 8 wave-instructions 
 __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_wave_base) {
   const unsigned base = __builtin_amdgcn_readfirstlane(
       (unsigned)(size_t)((const __attribute__((address_space(3))) char*)(lds_wave_base)));
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
+}
+
+// the same copy from a wave-uniform 64-bit base (SGPRs) plus a per-lane 32-bit byte offset
+__device__ __forceinline__ void glds16s(uint32_t voff, const void* sbase, const void* lds_wave_base) {
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)((const __attribute__((address_space(3))) char*)(lds_wave_base)));
+  const uint64_t sb = (uint64_t)(uintptr_t)sbase;
+  // (readfirstlane returns int: go through uint32_t, or a low half >= 2^31 would sign-extend into the high one)
+  const uint64_t sbu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(sb >> 32)) << 32) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)sb);
+  // s_nop 4: the base SGPRs were just written by v_readfirstlane (VALU SGPR write -> VMEM base read);
+  // s_nop 0: SALU M0 write -> LDS-DMA M0 read
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(base), "v"(voff), "s"(sbu) : "memory");
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -325,6 +338,233 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* _
                       smem + wave * 16384);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The phased pipeline as a PERSISTENT kernel: one workgroup per CU walks tiles w = blockIdx.x,
+// blockIdx.x + gridDim.x, ... (XCD-remapped over the whole work list).  The last k-tile of a tile issues
+// the half-tiles of the NEXT tile's first k-tile (same phase / buffer rules as any k-tile), so the next
+// tile's operands land while this tile's epilogue runs; the epilogue uses no LDS and issues an exact
+// number of stores (gemm256_store_q), which the first k-tile of the next tile adds to its two counted
+// waits.  What this removes per tile: the cold prologue (a full DMA latency with no MFMA work) and the
+// workgroup launch; the stores drain during the next tile's first phases.
+// Counted waits (DMA instructions younger than the half-tile retired; e = the epilogue's stores):
+//   steady k-tile              p0 B-hi: 4        p1 A-hi: 4        p3 next A-lo/B-lo: 4
+//   last k-tile, no next tile  p0: 2             p1: 0
+//   first k-tile, early issue  p0: 10 + e        p1: 8 + e         p3: 4 + e   (k-tile 1 issued before e)
+//   second k-tile after early / first k-tile otherwise: p0 4 + e (2 + e), p1 4 + e (0), p3 4
+__global__ __launch_bounds__(512, 1) void gemm_bf16_256q_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                               int64_t a_bs, const uint8_t* __restrict__ B,
+                                                               int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
+                                                               int N, int K, int tiles_m, int tiles_n, int splits,
+                                                               int k_per_split, int total) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * PBUF];
+  // wave index in an SGPR (readfirstlane): the per-wave terms of the DMA offsets and LDS addresses then cost
+  // no VGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int per_z = tiles_m * tiles_n;
+  const int nstores = gemm256_q_stores(ep);
+
+  // per-lane 32-bit byte offsets of the 8 DMA sources (kind h, instruction i) from the tile's A / B base,
+  // which live in SGPRs (global_load_lds_dwordx4 v_off, s[base]): 8 VGPRs instead of 16 for 64-bit pointers
+  uint32_t off[4][2];
+  const uint8_t* abase = A;
+  const uint8_t* bbase = B;
+  int m0 = 0, n0 = 0, zid = 0, bb = 0, nkt = 0;
+  // work item -> tile coordinates, operand bases and this lane's DMA offsets (see gemm_bf16_256p_kernel)
+  auto setup = [&](int w, int& tm0, int& tn0, int& z, int& b, int& nk) {
+    const int t = xcd_remap(w, total);
+    z = t / per_z;
+    const int tt = t - z * per_z;
+    const int tm = tt / tiles_n, tn = tt - tm * tiles_n;
+    b = z / splits;
+    const int split = z - b * splits;
+    tm0 = tm * TM;
+    tn0 = tn * TN;
+    const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
+    nk = max(0, (kend - kbeg) / TK);
+    abase = A + (int64_t)b * a_bs + kbeg;
+    bbase = B + (int64_t)b * b_bs + kbeg;
+    // the lane index through an opaque move: the per-lane row terms below are then recomputed here (a few
+    // VALU ops per tile) instead of being hoisted out of the tile loop into registers the main loop needs
+    int ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const bool is_a = h == 0 || h == 3;
+      const int ld = is_a ? (int)lda : (int)ldb;
+      const int lim = is_a ? M : N, r0 = is_a ? tm0 : tn0;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int j = 16 * wave + 8 * i + (ln >> 3);
+        const int lc = (ln & 7) ^ (j & 7);
+        const int rr = min(r0 + half_row(h, j), lim - 1);
+        off[h][i] = (uint32_t)rr * (uint32_t)ld + (uint32_t)(lc * 16);
+      }
+    }
+  };
+  // half-tile h of k-tile kt (of the tile the offsets describe) into buffer `buf`
+  auto issue = [&](int h, int kt, int buf) {
+    const uint8_t* base = (h == 0 || h == 3) ? abase : bbase;
+    char* dst = smem + buf * PBUF + h * HT + 2 * wave * 1024;
+    glds16s(off[h][0] + (uint32_t)(kt * TK), base, dst);
+    glds16s(off[h][1] + (uint32_t)(kt * TK), base, dst + 1024);
+  };
+  auto wait_vm = [&](int n) {  // s_waitcnt needs an immediate; n is even here (2 DMAs per half-tile)
+    switch (n) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+      case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+      case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+      case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+      case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+      case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+      case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+      case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+      case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
+      case 24: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+      case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+      case 28: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+      case 30: asm volatile("s_waitcnt vmcnt(30)" ::: "memory"); break;
+      case 32: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
+      case 34: asm volatile("s_waitcnt vmcnt(34)" ::: "memory"); break;
+      case 36: asm volatile("s_waitcnt vmcnt(36)" ::: "memory"); break;
+      case 38: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
+      case 40: asm volatile("s_waitcnt vmcnt(40)" ::: "memory"); break;
+      case 42: asm volatile("s_waitcnt vmcnt(42)" ::: "memory"); break;
+      case 44: asm volatile("s_waitcnt vmcnt(44)" ::: "memory"); break;
+      case 46: asm volatile("s_waitcnt vmcnt(46)" ::: "memory"); break;
+      case 48: asm volatile("s_waitcnt vmcnt(48)" ::: "memory"); break;
+      case 50: asm volatile("s_waitcnt vmcnt(50)" ::: "memory"); break;
+      case 52: asm volatile("s_waitcnt vmcnt(52)" ::: "memory"); break;
+      case 54: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
+      case 56: asm volatile("s_waitcnt vmcnt(56)" ::: "memory"); break;
+      case 58: asm volatile("s_waitcnt vmcnt(58)" ::: "memory"); break;
+      case 60: asm volatile("s_waitcnt vmcnt(60)" ::: "memory"); break;
+      case 62: asm volatile("s_waitcnt vmcnt(62)" ::: "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+  };
+
+  const int sw0 = (((lane >> 4)) ^ (lane & 7)) << 4, sw1 = ((4 + (lane >> 4)) ^ (lane & 7)) << 4;
+  const int a_row = (wr * 64 + (lane & 15)) * TK;
+  const int b_row = (wc * 32 + (lane & 15)) * TK;
+
+  int w = blockIdx.x;
+  if (w >= total) return;
+  setup(w, m0, n0, zid, bb, nkt);
+  int g = 0;  // running k-tile count of this workgroup: k-tile g lives in buffer g & 1
+  if (nkt > 0) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) issue(h, 0, 0);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-lo, B-lo of the first k-tile
+    raw_barrier();
+  }
+  int extra = 0;       // stores of the previous tile's epilogue still counted in vmcnt
+  bool early = false;  // this tile's k-tile 1 was issued before the previous tile's epilogue
+  bf16x8 fa[4][2], fb[2][2];
+  for (;;) {
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = zero_f32x4();
+    const int wn = w + gridDim.x;
+    const bool has_next = wn < total;
+    int nm0 = 0, nn0 = 0, nz = 0, nb = 0, nnkt = 0;
+    for (int kt = 0; kt < nkt; ++kt, ++g) {
+      const char* st = smem + (g & 1) * PBUF;
+      const bool last = kt + 1 == nkt;
+      if (last && has_next) {
+        // the sources of this tile are no longer needed: switch to the next tile's (k-tile 0 of it is
+        // issued by the phases below); an empty next tile (nnkt == 0) gets nothing issued
+        setup(wn, nm0, nn0, nz, nb, nnkt);
+      }
+      const bool next = !last || (has_next && nnkt > 0);
+      const int nkt_issue = last ? 0 : kt + 1;
+      // counted waits, in DMA instructions younger than the half-tile each one retires (see the table in
+      // the comment above the kernel); `e` = the previous epilogue's stores when they are among them
+      const bool skip = early && kt == 0;  // k-tile 1 is already in flight
+      const int e = (kt == 0 || (early && kt == 1)) ? extra : 0;
+      const int w0 = skip ? 10 + e : (next ? 4 + e : 2 + e);
+      const int w1 = skip ? 8 + e : (next ? 4 + e : 0);
+      const int w3 = skip ? 4 + e : 4;
+      const bool do3 = skip || next;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        if (p == 0 || p == 2) {
+          const char* ap = st + (p == 0 ? 0 : 3 * HT) + a_row;
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            fa[mt][0] = *reinterpret_cast<const bf16x8*>(ap + mt * 16 * TK + sw0);
+            fa[mt][1] = *reinterpret_cast<const bf16x8*>(ap + mt * 16 * TK + sw1);
+          }
+        }
+        if (p != 2) {  // B-lo in phases 0 and 3 (re-read: 16 VGPRs fewer than keeping it), B-hi in phase 1
+          const char* bp = st + (p == 1 ? 2 * HT : HT) + b_row;
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt) {
+            fb[nt][0] = *reinterpret_cast<const bf16x8*>(bp + nt * 16 * TK + sw0);
+            fb[nt][1] = *reinterpret_cast<const bf16x8*>(bp + nt * 16 * TK + sw1);
+          }
+        }
+        if (next && !skip) issue(p, nkt_issue, (g + 1) & 1);
+        const int qm = (p == 2 || p == 3) ? 1 : 0;
+        const bool qn1 = p == 1 || p == 2;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt)
+              acc[qm * 4 + mt][(qn1 ? 2 : 0) + nt] = mfma16x16x32(fb[nt][ks], fa[mt][ks], acc[qm * 4 + mt][(qn1 ? 2 : 0) + nt]);
+        __builtin_amdgcn_s_setprio(0);
+        // retire the half-tile the next phase reads first; in the first k-tile of a tile the previous
+        // epilogue's `e` stores sit between the waited-for copies and the newest ones
+        if (p == 0) {
+          wait_vm(w0);  // B-hi of this k-tile
+        } else if (p == 1) {
+          wait_vm(w1);  // A-hi of this k-tile
+        } else if (p == 3) {
+          if (do3) wait_vm(w3);  // A-lo, B-lo of the next k-tile
+        }
+        raw_barrier();
+      }
+    }
+    bool cold = false;  // an empty tile (no k-tiles) issued nothing for the next one: start it cold
+    if (has_next && nkt == 0) {
+      setup(wn, nm0, nn0, nz, nb, nnkt);
+      cold = true;
+    }
+    // the next tile's k-tile 1 goes into the buffer the last k-tile just finished with, BEFORE the epilogue:
+    // the first waits of the next tile then retire copies that are all older than this epilogue's stores
+    // and the stores get ~7 phases to drain before any wait covers them
+    const bool early_next = has_next && nnkt >= 2 && !cold;
+    if (early_next) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) issue(h, 1, (g + 1) & 1);
+    }
+    gemm256_store_q<true>(acc, ep, M, N, zid, bb, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + 4 * (lane >> 4), 1.f);
+    if (!has_next) break;
+    early = early_next;
+    if (cold && nnkt > 0) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) issue(h, 0, g & 1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // A-lo, B-lo of its first k-tile (and every store)
+      raw_barrier();
+    }
+    w = wn;
+    m0 = nm0;
+    n0 = nn0;
+    zid = nz;
+    bb = nb;
+    nkt = nnkt;
+    extra = cold ? 0 : nstores;
+  }
+}
+
 int g_phased = -1;
 int phased_mode() {
   if (g_phased < 0) {
@@ -338,6 +578,44 @@ int phased_mode() {
 
 void set_gemm256_phased(int on) { g_phased = on ? 1 : 0; }
 
+// persistent phased kernel (gemm_bf16_256q), off by default: RINGDP_GEMM256_PERSIST=1 selects it.
+// Measured (tools/gemm_epi_probe.py, profiles/r03/gemm_epilogue.md): 10-20 % SLOWER than one workgroup per
+// tile on every shape tried - the output stores of a tile drain slowly under load, and the in-order vmcnt
+// makes the next tile's first DMA wait behind them; with one workgroup per CU the drain is just as exposed
+// at the workgroup's end, so neither form overlaps it.
+static int g_persist = -1;
+static int persist_mode() {
+  if (g_persist < 0) {
+    const char* v = getenv("RINGDP_GEMM256_PERSIST");
+    g_persist = (v && v[0] == '1') ? 1 : 0;
+  }
+  return g_persist;
+}
+void set_gemm256_persist(int on) { g_persist = on ? 1 : 0; }
+
+// 256 B of device memory per device that the persistent epilogue's edge stores land in (never read)
+static void* store_sink() {
+  static void* sinks[64] = {};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!sinks[dev]) {
+    if (hipMalloc(&sinks[dev], 256) != hipSuccess) sinks[dev] = nullptr;
+  }
+  return sinks[dev];
+}
+
+static int cu_count() {
+  static int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, dev) == hipSuccess) n = p.multiProcessorCount;
+    }
+    return n;
+  }();
+  return cus;
+}
+
 static int g_wide = -1;
 int gemm_wide_store_mode() {
   if (g_wide < 0) {
@@ -347,6 +625,15 @@ int gemm_wide_store_mode() {
   return g_wide;
 }
 void set_gemm_wide_store(int mode) { g_wide = mode; }
+static int g_store_cache = -1;
+int gemm_store_cache() {
+  if (g_store_cache < 0) {
+    const char* v = getenv("RINGDP_GEMM_STORE_CACHE");
+    g_store_cache = v && *v ? atoi(v) : 0;
+  }
+  return g_store_cache;
+}
+void set_gemm_store_cache(int flavour) { g_store_cache = flavour; }
 
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s) {
@@ -366,11 +653,28 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   GemmEpilogue e2 = ep;
   e2.store_mode = gemm_wide_store_mode() % 10;
   e2.store_rot = gemm_wide_store_mode() < 10;
+  e2.store_cache = gemm_store_cache();
   auto go = [&](auto kern) {
     kern<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
                               static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M, N, K * 2,
                               tiles_m, tiles_n, splits, kps * 2);
   };
+  const bool wide_bf16 = N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 &&
+                         ep.c_bstride % 8 == 0;
+  const bool off32 = (int64_t)M * A.ld * 2 + (int64_t)K * 2 < (1ll << 32) &&
+                     (int64_t)N * Bop.ld * 2 + (int64_t)K * 2 < (1ll << 32);
+  if (!A.row_contig && !Bop.row_contig && phased_mode() && persist_mode() && off32 &&
+      (ep.mode == GemmEpilogue::kSplitK || !ep.out_bf16 || wide_bf16)) {
+    e2.sink = store_sink();
+    if (e2.sink) {
+      const int total = tiles_m * tiles_n * batch * splits;
+      const int g = std::min(total, cu_count());
+      gemm_bf16_256q_kernel<<<g, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
+                                             static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M,
+                                             N, K * 2, tiles_m, tiles_n, splits, kps * 2, total);
+      return true;
+    }
+  }
   if (!A.row_contig && !Bop.row_contig) {
     if (phased_mode()) go(gemm_bf16_256p_kernel);
     else go(gemm_bf16_256_kernel<false, false>);

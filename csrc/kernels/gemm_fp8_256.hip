@@ -39,7 +39,7 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + er
 __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_wave_base) {
   const unsigned base = __builtin_amdgcn_readfirstlane(
       (unsigned)(size_t)((const __attribute__((address_space(3))) char*)(lds_wave_base)));
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(base), "v"(gsrc) : "memory");
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -170,6 +170,7 @@ bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M
   GemmEpilogue e2 = ep;
   e2.store_mode = gemm_wide_store_mode() % 10;
   e2.store_rot = gemm_wide_store_mode() < 10;
+  e2.store_cache = gemm_store_cache();
   gemm_fp8_256_kernel<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld, A.bstride,
                                            static_cast<const uint8_t*>(Bop.p), Bop.ld, Bop.bstride, e2, M, N, Kbytes,
                                            tiles_m, tiles_n, splits, kps);

@@ -199,6 +199,9 @@ struct GemmEpilogue {
   int store_mode;     // set by the 256x256 launchers (bf16 output): 0 8-B stores, 1 16-B stores after a lane
                       // exchange, 2 staged through LDS into whole 128-B rows, 3 discard (probe only)
   bool store_rot;     // mode 2: rotate the row order per wave tile (spreads concurrent rows over channels)
+  int store_cache;    // 256x256 kernels' 16-B output stores: 0 plain, 1 nontemporal, 2 write-through sc1
+  void* sink;         // persistent 256x256 kernels: >= 16 B target of the stores past the M / N edge (set by
+                      // the launcher)
 };
 struct ConvGeom {
   int N, H, W, C;   // input NHWC (C padded to a multiple of 8)
@@ -218,9 +221,12 @@ void set_bf16_tile_mode(int mode);  // 0 auto, 128 / 256 forced (A/B measurement
 // supported (the caller falls back to the 128x128 core).  K in elements.
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s);
+void set_gemm256_persist(int on);  // A/B: 1 persistent phased kernel (default), 0 one workgroup per tile
 void set_gemm256_phased(int on);  // A/B: 1 phased pipeline (default), 0 the single-stage-wait kernel
-void set_gemm_wide_store(int mode);  // A/B: epilogue store mode of the 256x256 kernels (GemmEpilogue::store_mode)
+void set_gemm_wide_store(int mode);
+void set_gemm_store_cache(int flavour);  // A/B: GemmEpilogue::store_cache of the 256x256 kernels  // A/B: epilogue store mode of the 256x256 kernels (GemmEpilogue::store_mode)
 int gemm_wide_store_mode();         // RINGDP_GEMM_WIDE_STORE (default 2)
+int gemm_store_cache();             // RINGDP_GEMM_STORE_CACHE (default 0)
 bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes,
                   const GemmEpilogue& ep, int splits, hipStream_t s);
 // split-K count gemm_fp8 should be called with for an (M x N) fp32-partial GEMM (fills whole CU rounds)

@@ -53,3 +53,66 @@ def test_gemm256_wgrad_splitk(C, M, N):
     ref = dz.float().t() @ x.float()
     err = (out.cpu() - ref).abs().max() / ref.abs().max()
     assert err < 1e-4, float(err)
+
+
+def _gelu_grad(x):
+    return 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * 0.3989422804014327 * torch.exp(-0.5 * x * x)
+
+
+@pytest.mark.parametrize("persist", [1, 0])
+@pytest.mark.parametrize("epi", ["bf16_bias", "gelu_preact", "residual", "gelu_bwd", "f32_plain"])
+@pytest.mark.parametrize("M,N,K,batch", [(4200, 4104, 128, 1), (1000, 776, 192, 3), (264, 256, 64, 1)])
+def test_gemm256_persistent_epilogues(C, persist, epi, M, N, K, batch):
+    """The persistent phased kernel (several tiles per workgroup once tiles > CUs, next tile's first k-tile
+    landing during the epilogue, exact-count edge stores into a sink) against fp32 references, for every
+    epilogue kind it serves; persist=0 is the one-workgroup-per-tile kernel on the same inputs."""
+    C.set_gemm256_persist(persist)
+    try:
+        g = torch.Generator().manual_seed(M * 3 + N + K + batch)
+        a, ad = _operand(M, K, False, batch, g)
+        b, bd = _operand(N, K, False, batch, g)
+        ref = torch.bmm(a, b.transpose(1, 2))
+        bias = torch.randn(N, generator=g)
+        side = (torch.randn(batch, M, N, generator=g)).bfloat16()
+        if epi == "f32_plain":
+            out = C.gemm(ad, bd, M, N, K, K, K, False, False, batch, M * K, N * K, False)
+            want = ref
+        elif epi == "bf16_bias":
+            out = C.gemm(ad, bd, M, N, K, K, K, False, False, batch, M * K, N * K, True, bias.cuda())
+            want = ref + bias
+        elif epi == "gelu_preact":
+            pre = torch.empty(batch * M * N, device="cuda", dtype=torch.bfloat16)
+            out = C.gemm(ad, bd, M, N, K, K, K, False, False, batch, M * K, N * K, True, bias.cuda(), 2, None, pre)
+            z = ref + bias
+            want = torch.nn.functional.gelu(z)
+            perr = (pre.cpu().float().view(batch, M, N) - z).abs().max() / z.abs().max()
+            assert perr < 8e-3, float(perr)
+        elif epi == "residual":
+            out = C.gemm(ad, bd, M, N, K, K, K, False, False, batch, M * K, N * K, True, bias.cuda(), 0, side.cuda())
+            want = ref + bias + side.float()
+        else:  # GELU backward: C = (A B^T) * GELU'(preact)
+            out = C.gemm(ad, bd, M, N, K, K, K, False, False, batch, M * K, N * K, True, None, 3, None, side.cuda())
+            want = ref * _gelu_grad(side.float())
+        got = out.cpu().float().view(batch, M, N)
+        err = (got - want).abs().max() / want.abs().max()
+        assert err < (2e-3 if epi == "f32_plain" else 8e-3), float(err)
+    finally:
+        C.set_gemm256_persist(0)
+
+
+@pytest.mark.parametrize("persist", [1, 0])
+def test_gemm256_persistent_splitk(C, persist):
+    """K-contiguous split-K through the persistent kernel (work items = tiles x splits)."""
+    C.set_gemm256_persist(persist)
+    try:
+        M, N, K = 1032, 1288, 4096
+        g = torch.Generator().manual_seed(11)
+        a = (torch.randn(M, K, generator=g) * 0.5).bfloat16()
+        b = (torch.randn(N, K, generator=g) * 0.5).bfloat16()
+        out = torch.empty(M, N, device="cuda")
+        C.gemm_splitk_f32(a.cuda(), b.cuda(), M, N, K, K, K, False, False, 8, out)
+        ref = a.float() @ b.float().t()
+        err = (out.cpu() - ref).abs().max() / ref.abs().max()
+        assert err < 1e-4, float(err)
+    finally:
+        C.set_gemm256_persist(0)
