@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "device_common.h"
+#include "gemm256_epilogue.h"
 #include "kernels.h"
 
 namespace ringdp {
@@ -51,10 +52,9 @@ __device__ __forceinline__ int rsw(int kr, int col) {  // col: element column (m
   return kr * RROW + (((col >> 4) ^ f) << 4) + (col & 15);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {  // d/dx of x * Phi(x) (erf form)
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-}
+// GELU (erf form) and its derivative on the branch-free erf of gemm256_epilogue.h
+__device__ __forceinline__ float gelu_erf(float x) { return gemm_gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return gemm_gelu_grad(x); }  // d/dx of x * Phi(x)
 
 // ------------------------------------------------------------------ loaders
 struct DenseLoader {  // element (b, r, k): K-contig p[b*bs + r*ld + k]; row-contig p[b*bs + k*ld + r]
@@ -621,6 +621,14 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
     }
     return;
   }
+  // epilogue kind as wave-uniform values (scalar branches: a branch on a VGPR copy of a kernel argument
+  // would exec-mask every path of every element, the GELU included)
+  const int act = __builtin_amdgcn_readfirstlane(ep.act);
+  const bool has_bias = __builtin_amdgcn_readfirstlane(ep.bias != nullptr ? 1 : 0) != 0;
+  const bool has_res = __builtin_amdgcn_readfirstlane(ep.residual != nullptr ? 1 : 0) != 0;
+  const bool has_pre = __builtin_amdgcn_readfirstlane(ep.preact != nullptr ? 1 : 0) != 0;
+  const bool has_stats = __builtin_amdgcn_readfirstlane(ep.stats != nullptr ? 1 : 0) != 0;
+  const bool out_bf16 = __builtin_amdgcn_readfirstlane(ep.out_bf16 ? 1 : 0) != 0;
   float ssum[4][4], ssq[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -643,8 +651,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias[j][e] = (ep.bias && ncol + 16 * j + e < N) ? ep.bias[ncol + 16 * j + e] : 0.f;
-  const bf16* side = static_cast<const bf16*>(ep.residual ? ep.residual : (ep.act == 3 ? ep.preact : nullptr));
+    for (int e = 0; e < 4; ++e) bias[j][e] = (has_bias && ncol + 16 * j + e < N) ? ep.bias[ncol + 16 * j + e] : 0.f;
+  const bf16* side = static_cast<const bf16*>(has_res ? ep.residual : (act == 3 ? ep.preact : nullptr));
   bf16x4 sv[4][4];
   if (side) {
 #pragma unroll
@@ -667,7 +675,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * ep.alpha + bias[j][e];
       const int64_t off = row_off + n;
       const bool full = mok && n + 3 < N;
-      if (ep.act == 3 && mok) {  // GELU backward: the incoming gradient times GELU'(pre-activation)
+      if (act == 3 && mok) {  // GELU backward: the incoming gradient times GELU'(pre-activation)
         const bf16* pa = static_cast<const bf16*>(ep.preact) + off;
         float z[4];
         if (full) {
@@ -680,7 +688,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] *= gelu_grad(z[e]);
-      } else if (ep.preact && mok) {
+      } else if (has_pre && mok) {
         bf16* pa = static_cast<bf16*>(ep.preact) + off;
         if (full) {
           *reinterpret_cast<bf16x4*>(pa) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
@@ -690,7 +698,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
             if (n + e < N) pa[e] = (bf16)v[e];
         }
       }
-      if (ep.residual && mok) {  // one 8-byte load per lane (4 scalar 2-byte loads cost +30 % on ResNet dgrads)
+      if (has_res && mok) {  // one 8-byte load per lane (4 scalar 2-byte loads cost +30 % on ResNet dgrads)
         const bf16* ra = static_cast<const bf16*>(ep.residual) + off;
         if (full) {
           const bf16x4 r = sv[i][j];
@@ -704,11 +712,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-        else if (ep.act == 2) v[e] = gelu_erf(v[e]);
+        if (act == 1) v[e] = fmaxf(v[e], 0.f);
+        else if (act == 2) v[e] = gelu_erf(v[e]);
       }
       if (mok) {
-        if (ep.out_bf16) {
+        if (out_bf16) {
           bf16* c = static_cast<bf16*>(ep.C) + off;
           if (full) {
             *reinterpret_cast<bf16x4*>(c) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
@@ -730,7 +738,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
               if (n + e < N) c[e] = v[e];
           }
         }
-        if (ep.stats) {
+        if (has_stats) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             ssum[j][e] += v[e];
@@ -740,7 +748,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(LA la, LB lb, GemmEpilogue
       }
     }
   }
-  if (!ep.stats) return;
+  if (!has_stats) return;
   // per-channel partials of this block's 128 rows: reduce over the 16 m-lanes, then the 2 m-waves
 #pragma unroll
   for (int j = 0; j < 4; ++j)

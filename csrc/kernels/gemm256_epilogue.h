@@ -34,64 +34,107 @@ __device__ __forceinline__ bool wide_ok(const GemmEpilogue& ep, int N) {
   return N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 && (ep.c_bstride % 8) == 0;
 }
 
+// erf to ~3e-7 absolute without branches (Abramowitz-Stegun 7.1.26 + hardware rcp / exp): ocml's erff
+// takes two divergent polynomial paths on |x| < 1, which exec-masks both in every wave of an epilogue.
+__device__ __forceinline__ float gemm_erf(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  return copysignf(1.f - p * t * __expf(-ax * ax), x);
+}
+__device__ __forceinline__ float gemm_gelu(float x) { return 0.5f * x * (1.f + gemm_erf(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gemm_gelu_grad(float x) {
+  return 0.5f * (1.f + gemm_erf(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Epilogue flags as wave-uniform values: read through readfirstlane, so every branch on them is a scalar
+// branch (kernel-argument structs can end up in VGPRs, and a branch on a VGPR value is exec-masked:
+// every wave then runs every path of every element, the GELU's erf included).
+struct EpiFlags {
+  int act, mode;
+  bool bias, res, pre, st_pre;
+};
+__device__ __forceinline__ EpiFlags epi_flags(const GemmEpilogue& ep) {
+  EpiFlags f;
+  f.act = __builtin_amdgcn_readfirstlane(ep.act);
+  f.mode = __builtin_amdgcn_readfirstlane(ep.store_mode);
+  f.bias = __builtin_amdgcn_readfirstlane(ep.bias != nullptr ? 1 : 0) != 0;
+  f.res = __builtin_amdgcn_readfirstlane(ep.residual != nullptr ? 1 : 0) != 0;
+  f.pre = __builtin_amdgcn_readfirstlane(ep.preact != nullptr ? 1 : 0) != 0;
+  f.st_pre = f.pre && f.act != 3;
+  return f;
+}
+
+// value of one accumulator quad after scale, bias, [GELU backward], [pre-activation copy], residual, activation
+template <int ACT>
+__device__ __forceinline__ void epi_values(const dev::f32x4& a, float sa, const dev::f32x4& bias, const dev::bf16x4& side,
+                                           bool has_res, float (&v)[4]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = fmaf(a[e], sa, bias[e]);
+    if (ACT == 3) v[e] *= gemm_gelu_grad((float)side[e]);
+  }
+}
+template <int ACT>
+__device__ __forceinline__ void epi_finish(float (&v)[4], const dev::bf16x4& side, bool has_res) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (has_res) v[e] += (float)side[e];
+    if (ACT == 1) v[e] = fmaxf(v[e], 0.f);
+    else if (ACT == 2) v[e] = gemm_gelu(v[e]);
+  }
+}
+
 // QUAD: the phased kernel's tile order (acc[qm*4 + mt][qn*2 + nt], quadrants of 64 rows x 32 cols);
 // otherwise acc[i][j] covers rows mrow + 16 i, columns ncol + 16 j.
 // lds_wave: this wave's 16 KiB of the kernel's LDS (free once the main loop's last barrier has passed):
 // store mode 2 writes the wave's 128 x 64 bf16 tile there and stores it back as whole 128-B rows.
-template <bool QUAD>
-__device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep, int M, int N,
-                                              int zid, int bidx, int mrow, int ncol, float scale, char* lds_wave) {
+template <bool QUAD, int ACT>
+__device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep,
+                                                   const EpiFlags& fl, int M, int N, int bidx, int mrow, int ncol,
+                                                   float scale, char* lds_wave) {
   using namespace ringdp::dev;
   auto mof = [&](int i) { return QUAD ? mrow + (i >> 2) * 64 + 16 * (i & 3) : mrow + 16 * i; };
   auto nof = [&](int j) { return QUAD ? ncol + (j >> 1) * 32 + 16 * (j & 1) : ncol + 16 * j; };
-  if (ep.mode == GemmEpilogue::kSplitK) {
-    float* out = ep.partial + (int64_t)zid * M * N;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int m = mof(i);
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = nof(j);  // N % 4 == 0 (checked by the launchers)
-        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j] * scale;
-      }
-    }
-    return;
-  }
   const int64_t cb = (int64_t)bidx * ep.c_bstride;
+  const float sa = scale * ep.alpha;
   // ---- all loads first
   f32x4 bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = nof(j);
-    bias[j] = (ep.bias && n < N) ? *reinterpret_cast<const f32x4*>(ep.bias + n) : zero_f32x4();
+    bias[j] = (fl.bias && n < N) ? *reinterpret_cast<const f32x4*>(ep.bias + n) : zero_f32x4();
   }
-  const bf16* side = static_cast<const bf16*>(ep.residual ? ep.residual : (ep.act == 3 ? ep.preact : nullptr));
+  const bool has_side = fl.res || ACT == 3;
+  const bf16* side = static_cast<const bf16*>(fl.res ? ep.residual : ep.preact);
   bf16x4 sv[8][4];
-  if (side) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sv[i][j] = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+  if (has_side) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int m = mof(i), n = nof(j);
-        if (m < M && n < N) sv[i][j] = *reinterpret_cast<const bf16x4*>(side + cb + (int64_t)m * ep.ldc + n);
+        const int m = min(mof(i), M - 1), n = min(nof(j), N - 4);
+        sv[i][j] = *reinterpret_cast<const bf16x4*>(side + cb + (int64_t)m * ep.ldc + n);
       }
   }
-  // ---- compute + stores
-  // bf16 output with whole 8-column runs: lanes l and l ^ 16 (same row, adjacent 4-column groups)
-  // exchange one of their two vertically adjacent tiles, so each stores 8 consecutive bf16 (16 B)
-  // instead of 4 (8 B): half the store instructions of a store-issue-bound epilogue (guide T21).
-  if (ep.out_bf16 && ep.store_mode == 3) {  // probe: compute but never store
+  if (ep.out_bf16 && fl.mode == 3) {  // probe: compute but never store
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  if (ep.out_bf16 && ep.store_mode == 2 && wide_ok(ep, N)) {
+  const int lane = threadIdx.x & 63;
+  if (ep.out_bf16 && (fl.mode == 2 || fl.mode == 4) && wide_ok(ep, N)) {
     // final values -> bf16 -> LDS image [128 rows][64 cols] (128-B rows, 16-B chunk c of row r at c ^ (r & 7)),
     // then 8 lanes per row store whole 128-B rows
-    const int lane = threadIdx.x & 63;
     const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -99,27 +142,11 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
       for (int j = 0; j < 4; ++j) {
         const int m = mof(i), n = nof(j);
         float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * scale * ep.alpha + bias[j][e];
-        const int64_t off = cb + (int64_t)m * ep.ldc + n;
-        if (ep.act == 3) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x = (float)sv[i][j][e];
-            v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-          }
-        } else if (ep.preact && m < M && n < N) {
-          *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        }
-        if (ep.residual) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)sv[i][j][e];
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-          else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
-        }
+        epi_values<ACT>(acc[i][j], sa, bias[j], sv[i][j], fl.res, v);
+        if (fl.st_pre && m < M && n < N)
+          *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + cb + (int64_t)m * ep.ldc + n) =
+              bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        epi_finish<ACT>(v, sv[i][j], fl.res);
         const int r = (QUAD ? (i >> 2) * 64 + 16 * (i & 3) : 16 * i) + fr;    // row in the wave tile
         const int c = QUAD ? (j >> 1) * 32 + 16 * (j & 1) + 4 * fq : 16 * j + 4 * fq;  // column
         *reinterpret_cast<bf16x4*>(lds_wave + r * 128 + ((((c >> 3) ^ (r & 7)) << 4) | ((c & 7) << 1))) =
@@ -131,19 +158,24 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
     // Row order rotated per wave tile: in lockstep, every wave of every block would write the same row
     // offset at the same moment, i.e. addresses a multiple of 128 rows apart - on a few memory channels.
     const int rot = ep.store_rot ? (((m_base >> 7) * 5 + (n_base >> 6) * 3) & 15) : 0;
+    bf16* cbase = static_cast<bf16*>(ep.C) + cb;
 #pragma unroll
     for (int k0 = 0; k0 < 16; ++k0) {
       const int k = (k0 + rot) & 15;
       const int r = 8 * k + (lane >> 3), ch = lane & 7;
       const uint4 w = *reinterpret_cast<const uint4*>(lds_wave + r * 128 + ((ch ^ (r & 7)) << 4));
       const int m = m_base + r, n = n_base + 8 * ch;
-      if (m < M && n < N) gemm_st16(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + n, w, ep.store_cache);
+      if (m < M && n < N) {
+        // probe mode 4: the whole epilogue, but every store goes to one 16-B sink (no HBM write traffic)
+        void* dst = fl.mode == 4 ? ep.sink : static_cast<void*>(cbase + (int64_t)m * ep.ldc + n);
+        gemm_st16(dst, w, ep.store_cache);
+      }
     }
     return;
   }
-  const bool wide = ep.out_bf16 && ep.store_mode == 1 && wide_ok(ep, N);
-  if (wide) {
-    const int lane = threadIdx.x & 63;
+  if (ep.out_bf16 && fl.mode == 1 && wide_ok(ep, N)) {
+    // lanes l and l ^ 16 (same row, adjacent 4-column groups) exchange one of their two vertically adjacent
+    // tiles, so each stores 8 consecutive bf16 (16 B) instead of 4 (8 B)
     const bool upper = (lane >> 4) & 1;  // odd 4-column group: keeps the lower tile of the pair
 #pragma unroll
     for (int i2 = 0; i2 < 8; i2 += 2) {
@@ -156,28 +188,11 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
           const int i = i2 + t;
           const int m = mof(i);
           float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * scale * ep.alpha + bias[j][e];
-          const int64_t off = cb + (int64_t)m * ep.ldc + n;
-          if (ep.act == 3) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float x = (float)sv[i][j][e];
-              v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-            }
-          } else if (ep.preact && m < M && n < N) {
-            *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) =
+          epi_values<ACT>(acc[i][j], sa, bias[j], sv[i][j], fl.res, v);
+          if (fl.st_pre && m < M && n < N)
+            *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + cb + (int64_t)m * ep.ldc + n) =
                 bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-          }
-          if (ep.residual) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)sv[i][j][e];
-          }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-            else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
-          }
+          epi_finish<ACT>(v, sv[i][j], fl.res);
           const bf16x4 q = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
           const unsigned* qu = reinterpret_cast<const unsigned*>(&q);
           pk[t][0] = qu[0];
@@ -193,7 +208,7 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
           uint4 w;
           if (upper) w = make_uint4(r0, r1, pk[1][0], pk[1][1]);
           else w = make_uint4(pk[0][0], pk[0][1], r0, r1);
-          *reinterpret_cast<uint4*>(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + nc) = w;
+          gemm_st16(static_cast<bf16*>(ep.C) + cb + (int64_t)m * ep.ldc + nc, w, ep.store_cache);
         }
       }
     }
@@ -208,32 +223,46 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
       const int n = nof(j);
       if (n >= N) continue;
       float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * scale * ep.alpha + bias[j][e];
+      epi_values<ACT>(acc[i][j], sa, bias[j], sv[i][j], fl.res, v);
       const int64_t off = cb + (int64_t)m * ep.ldc + n;
-      if (ep.act == 3) {  // GELU backward: times GELU'(pre-activation)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float x = (float)sv[i][j][e];
-          v[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-        }
-      } else if (ep.preact) {
+      if (fl.st_pre)
         *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      }
-      if (ep.residual) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += (float)sv[i][j][e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-        else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
-      }
+      epi_finish<ACT>(v, sv[i][j], fl.res);
       if (ep.out_bf16)
         *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.C) + off) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       else
         *reinterpret_cast<f32x4*>(static_cast<float*>(ep.C) + off) = f32x4{v[0], v[1], v[2], v[3]};
     }
+  }
+}
+
+template <bool QUAD>
+__device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep, int M, int N,
+                                              int zid, int bidx, int mrow, int ncol, float scale, char* lds_wave) {
+  using namespace ringdp::dev;
+  if (__builtin_amdgcn_readfirstlane(ep.mode) == GemmEpilogue::kSplitK) {
+    auto mof = [&](int i) { return QUAD ? mrow + (i >> 2) * 64 + 16 * (i & 3) : mrow + 16 * i; };
+    auto nof = [&](int j) { return QUAD ? ncol + (j >> 1) * 32 + 16 * (j & 1) : ncol + 16 * j; };
+    float* out = ep.partial + (int64_t)zid * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mof(i);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nof(j);  // N % 4 == 0 (checked by the launchers)
+        if (n < N) *reinterpret_cast<f32x4*>(out + (int64_t)m * N + n) = acc[i][j] * scale;
+      }
+    }
+    return;
+  }
+  const EpiFlags fl = epi_flags(ep);
+  // one specialised body per activation: the per-element code holds no branch on the epilogue kind
+  switch (fl.act) {
+    case 1: gemm256_store_impl<QUAD, 1>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 2: gemm256_store_impl<QUAD, 2>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 3: gemm256_store_impl<QUAD, 3>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    default: gemm256_store_impl<QUAD, 0>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
   }
 }
 
@@ -245,10 +274,6 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
 __device__ __forceinline__ int gemm256_q_stores(const GemmEpilogue& ep) {
   if (ep.mode == GemmEpilogue::kSplitK || !ep.out_bf16) return 32;
   return (ep.preact && ep.act != 3) ? 48 : 16;
-}
-
-__device__ __forceinline__ float gemm_gelu_grad(float x) {
-  return 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
 }
 
 template <bool QUAD>
@@ -288,7 +313,7 @@ __device__ __forceinline__ void gemm256_store_q(const dev::f32x4 (&acc)[8][4], c
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-            else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+            else if (ep.act == 2) v[e] = gemm_gelu(v[e]);
           }
         }
         void* dst = ok ? static_cast<void*>(out + (int64_t)m * ld + n) : static_cast<void*>(sink);
@@ -347,7 +372,7 @@ __device__ __forceinline__ void gemm256_store_q(const dev::f32x4 (&acc)[8][4], c
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (ep.act == 1) v[e] = fmaxf(v[e], 0.f);
-          else if (ep.act == 2) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+          else if (ep.act == 2) v[e] = gemm_gelu(v[e]);
         }
         const bf16x4 q = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         const unsigned* qu = reinterpret_cast<const unsigned*>(&q);

@@ -654,6 +654,7 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   e2.store_mode = gemm_wide_store_mode() % 10;
   e2.store_rot = gemm_wide_store_mode() < 10;
   e2.store_cache = gemm_store_cache();
+  e2.sink = store_sink();
   auto go = [&](auto kern) {
     kern<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
                               static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M, N, K * 2,

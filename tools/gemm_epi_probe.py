@@ -40,10 +40,14 @@ def main():
         C.set_gemm256_persist(0)
         C.set_gemm_wide_store(3)
         res["compute_only"] = round(timeit(plain), 1)
+        C.set_gemm_wide_store(4)
+        res["epilogue_to_sink"] = round(timeit(plain), 1)
+        if K == 768 and N == 3072:
+            res["gelu_to_sink"] = round(timeit(gelu), 1)
         C.set_gemm_wide_store(2)
-        for persist in (0, 1):
+        for persist in (0,):
             C.set_gemm256_persist(persist)
-            for fl in (0, 1, 2):
+            for fl in (0,):
                 C.set_gemm_store_cache(fl)
                 res[f"p{persist}_c{fl}"] = round(timeit(plain), 1)
                 if K == 768 and N == 3072:

@@ -22,9 +22,18 @@
     }                                                                                          \
   } while (0)
 
+template <bool BIGLDS>
 __global__ __launch_bounds__(512) void store_tiles(uint4* __restrict__ C, int M, int N, int tiles_n, int ntiles,
-                                                   int mode, int persistent) {
+                                                   int mode, int persistent, int spin) {
+  // BIGLDS: 128 KiB of LDS per workgroup (one per CU, as the 256x256 GEMM), touched so it is kept
+  __shared__ uint4 pad[BIGLDS ? 8192 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (BIGLDS) pad[tid] = make_uint4(tid, 0, 0, 0);
+  if (spin) {  // stand-in for a tile's compute: `spin` x ~1000 cycles of dependent VALU
+    float x = (float)tid;
+    for (int i = 0; i < spin * 250; ++i) x = x * 0.999f + 0.5f;
+    if (x == 12345.f) C[0] = make_uint4(1, 1, 1, 1);
+  }
   const int wr = wave >> 2, wc = wave & 3;
   const uint4 v = make_uint4(tid, blockIdx.x, 1, 2);
   const int step = persistent ? gridDim.x : ntiles;
@@ -53,7 +62,7 @@ __global__ __launch_bounds__(512) void store_tiles(uint4* __restrict__ C, int M,
           const int c = n0 + wc * 64 + 32 * j + 8 * (lane >> 4);
           if (r < M && c < N) C[((size_t)r * N + c) / 8] = v;
         }
-    } else {
+    } else if (mode == 5) {
       const size_t base = (size_t)t * 256 * 256 / 8;  // 8 KiB-contiguous chunks of the matrix
       for (int k = 0; k < 16; ++k) {
         const size_t i = base + (size_t)k * 512 + tid;
@@ -71,21 +80,29 @@ int main() {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  const char* names[] = {"rows8", "rows8rot", "full2", "full2rot", "lane16", "fill"};
-  for (int persistent = 0; persistent < 2; ++persistent)
-    for (int mode = 0; mode < 6; ++mode) {
-      const int grid = persistent ? 256 : ntiles;
-      for (int i = 0; i < 3; ++i) store_tiles<<<grid, 512>>>(C, M, N, tiles_n, ntiles, mode, persistent);
+  for (int cfg = 0; cfg < 8; ++cfg) {
+    // cfg: bit 0 big LDS (1 WG per CU), bit 1 spin (~20 us of "compute" per tile), bit 2 skip stores
+    const bool big = cfg & 1;
+    const int spin = (cfg & 2) ? 40 : 0;
+    const int mode = (cfg & 4) ? 6 : 2;
+    const int persistent = 0;
+    {
+      const int grid = ntiles;
+      auto launch = [&]() {
+        if (big) store_tiles<true><<<grid, 512>>>(C, M, N, tiles_n, ntiles, mode, persistent, spin);
+        else store_tiles<false><<<grid, 512>>>(C, M, N, tiles_n, ntiles, mode, persistent, spin);
+      };
+      for (int i = 0; i < 3; ++i) launch();
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(a));
-      for (int i = 0; i < 20; ++i) store_tiles<<<grid, 512>>>(C, M, N, tiles_n, ntiles, mode, persistent);
+      for (int i = 0; i < 20; ++i) launch();
       CK(hipEventRecord(b));
       CK(hipEventSynchronize(b));
       float ms;
       CK(hipEventElapsedTime(&ms, a, b));
       const double us = ms * 1000.0 / 20;
-      std::printf("{\"pattern\": \"%s\", \"persistent\": %d, \"us\": %.1f, \"TBps\": %.2f}\n", names[mode], persistent,
-                  us, (double)M * N * 2 / us / 1e6);
+      std::printf("{\"big_lds\": %d, \"spin\": %d, \"stores\": %d, \"us\": %.1f}\n", (int)big, spin, mode != 6, us);
     }
+  }
   return 0;
 }
