@@ -1004,8 +1004,8 @@ static double fp8_256_fill(int64_t tiles) {
 }
 // Measured (tools/gemm_bench.py --vit-fp8, ViT-B/16 shapes): the 256 kernel wins on the long-K split-K
 // weight gradients (K = 25216 tokens: 74-86 us vs 95-118 us at >= 27 output tiles) and on K >= 4096
-// (8192^3: 1.95 vs 1.67 PF/s), and loses on short-K single-pass GEMMs (K = 768 / 3072 over 25216 rows:
-// 6-24 k-steps per tile do not amortise its one-workgroup-per-CU prologue and epilogue).
+// (8192^3: 1.95 vs 1.67 PF/s).  It lost on short-K single-pass GEMMs only while its epilogue branched on
+// VGPR copies of the epilogue flags; since those are scalar it wins there too at >= 75 % round fill.
 static bool fp8_use_256(int M, int N, int Kbytes, int batch, int splits) {
   const int mode = fp8_tile_mode();
   if (mode == 128) return false;
@@ -1013,7 +1013,9 @@ static bool fp8_use_256(int M, int N, int Kbytes, int batch, int splits) {
   const int64_t out_tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
   const int64_t tiles = out_tiles * std::max(1, splits);
   if (tiles < 192 || fp8_256_fill(tiles) < 0.75) return false;
-  return splits > 1 ? out_tiles >= 16 : Kbytes >= 4096;
+  // (single-pass GEMMs of any K: with the scalar-branch epilogue the 256 kernel wins at >= 75 % round fill,
+  // e.g. 25216 x 3072 x 768 104 vs 126 us, x 2304 87 vs 98 us; profiles/r03/gemm_tiles.jsonl)
+  return splits > 1 ? out_tiles >= 16 : true;
 }
 
 int gemm_fp8_pick_splits(int M, int N, int Kbytes, int requested) {

@@ -209,3 +209,87 @@ def test_forced_comm_eager_and_graph(world1, monkeypatch, hook, stream):
         else:  # gradients went over the wire in bf16
             assert torch.isfinite(pb).all()
             torch.testing.assert_close(pa, pb, rtol=2e-2, atol=2e-3)
+
+
+def _rb(t):
+    """bf16 rounding in the forward, identity in the backward (straight-through)."""
+    return t + (t.bfloat16().float() - t).detach()
+
+
+def _bf16_oracle_forward(m, x):
+    """The reference forward with ringdp's bf16 storage points emulated: weights and the input image rounded
+    to bf16, conv2's pre-activation rounded before its pool, and each pooled activation (a1, a2, a3: bf16
+    in HBM) rounded after its pool; fp32 math."""
+    x = (x.float() / 255.0 - 0.1307) / 0.3081
+    w1, w2, w3, wf = (_rb(p) for p in (m.conv1.weight, m.conv2.weight, m.conv3.weight, m.fc1.weight))
+    a = _rb(F.max_pool2d(F.relu(F.conv2d(_rb(x), w1, m.conv1.bias, padding=1)), 2, 2))
+    # conv2's pre-activation is staged as bf16 before the overlapping pool (csrc/kernels/convnet.hip F2), so
+    # its argmax ties are broken on bf16 values: round before the pool too
+    a = _rb(F.max_pool2d(F.relu(_rb(F.conv2d(a, w2, m.conv2.bias))), 2, 1))
+    a = _rb(F.max_pool2d(F.relu(F.conv2d(a, w3, m.conv3.bias)), 2, 2))
+    return F.linear(a.reshape(-1, 2048), wf, m.fc1.bias)
+
+
+@pytest.mark.parametrize("B", [100, 4096])
+def test_convnet_grads_vs_bf16_oracle(B):
+    """One-step parity per parameter (||g - g_ref|| / ||g_ref|| <= 2e-2) against the bf16-storage
+    oracle: what remains is the bf16 rounding of the backward's intermediate gradients (dz2, d(a3)) and
+    fp32 summation order."""
+    from ringdp.models import ConvNet
+
+    torch.manual_seed(0)
+    m = ConvNet().cuda()
+    g = torch.Generator(device="cuda").manual_seed(B)
+    x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    out = m(x)
+    ref = _bf16_oracle_forward(m, x)
+    ferr = float((out - ref).abs().max() / ref.abs().max())
+    assert ferr < 1e-2, ferr
+    F.cross_entropy(out, y).backward()
+    mine = {n: p.grad.clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    F.cross_entropy(_bf16_oracle_forward(m, x), y).backward()
+    l2, worst = {}, {}
+    for n, p in m.named_parameters():
+        l2[n] = float((mine[n] - p.grad).norm() / p.grad.norm())
+        worst[n] = float((mine[n] - p.grad).abs().max() / p.grad.abs().max())
+    print("l2", {k: f"{v:.1e}" for k, v in l2.items()}, "max", {k: f"{v:.1e}" for k, v in worst.items()})
+    # relative L2 per parameter: the gate.  The max-abs ratio is looser: a pooling argmax that flips on a
+    # near-tie (fp32 summation order) routes one element's gradient to a neighbour, which moves single
+    # conv1/conv2 weight-gradient entries by a few percent of the largest
+    assert max(l2.values()) < 2e-2, l2
+    assert max(worst.values()) < 1e-1, worst
+
+
+def test_convnet_bf16_trajectory_b4096():
+    """200 SGD steps at B=4096 (the fc1-in-conv3 launch, the one-bucket regime) track the ATen fp32 loss."""
+    from ringdp.models import ConvNet
+    from ringdp.optim import SGD
+
+    g = torch.Generator(device="cuda").manual_seed(9)
+    xs = [torch.randint(0, 256, (4096, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g) for _ in range(4)]
+    proj = torch.randn(784, 10, device="cuda", generator=g)
+    ys = [(x.float().view(4096, -1) @ proj).argmax(1) for x in xs]
+
+    def traj(model, fwd):
+        opt = SGD(model.parameters(), lr=0.01)
+        out = []
+        for i in range(200):
+            loss = F.cross_entropy(fwd(xs[i % 4]), ys[i % 4])
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+            out.append(float(loss))
+        return torch.tensor(out)
+
+    torch.manual_seed(3)
+    ref = ConvNet().cuda()
+    torch.manual_seed(3)
+    m16 = ConvNet().cuda()
+    l_ref = traj(ref, ref.reference_forward)
+    l_16 = traj(m16, m16)
+    assert l_ref[-20:].mean() < l_ref[:4].mean() - 0.3, l_ref
+    d = float((l_16 - l_ref).abs().max())
+    print(f"B=4096 max |loss - aten fp32| over 200 steps: {d:.2e}")
+    assert d < 5e-3, d
