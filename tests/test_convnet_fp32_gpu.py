@@ -46,6 +46,44 @@ def test_conv_f32_kernels(B, Cin, H, K, R, pad):
     _close(db, br.grad.float(), rtol=2e-5)
 
 
+def _conv_roundtrip(B, Cin, H, K, R, pad, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+    w = torch.randn(K, Cin, R, R, device=DEV, generator=g) * 0.1
+    b = torch.randn(K, device=DEV, generator=g)
+    z = C.f32_conv_fwd(x, w, b, pad)
+    dz = torch.randn_like(z)
+    dx = C.f32_conv_dgrad(dz, w, H, H, pad)
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    C.f32_conv_wgrad(dz, x, pad, 0.0, 1.0, dw, db)
+    xr, wr, br = (t.double().requires_grad_() for t in (x, w, b))
+    ref = F.conv2d(xr, wr, br, padding=pad)
+    ref.backward(dz.double())
+    return (z, dx, dw, db), (ref.detach().float(), xr.grad.float(), wr.grad.float(), br.grad.float())
+
+
+@pytest.mark.parametrize("B,Cin,H,K,R,pad", [(40, 32, 13, 64, 3, 0), (33, 64, 10, 128, 3, 0), (70, 1, 28, 32, 5, 1),
+                                             (300, 2048, 1, 10, 1, 0)])
+def test_conv_f32_many_tiles_and_slices(B, Cin, H, K, R, pad):
+    """Batches that give ragged m tiles, several split-K weight-gradient slices and the 128x32 / 32x128
+    tile layouts."""
+    got, ref = _conv_roundtrip(B, Cin, H, K, R, pad, B + K)
+    for a, r, tol in zip(got, ref, (1e-5, 1e-5, 3e-5, 3e-5)):
+        _close(a, r, rtol=tol)
+
+
+def test_conv_f32_batch_chunks(monkeypatch):
+    """The host launchers split the batch so every index stays 32-bit; a lowered limit runs that path
+    (conv2 shape: 7744 output elements per image, limit 3 images -> chunks of 3, 3, 2)."""
+    monkeypatch.setenv("RINGDP_F32_CHUNK_LIMIT", str(3 * 7744))
+    got, ref = _conv_roundtrip(8, 32, 13, 64, 3, 0, 5)
+    for a, r in zip(got, ref):
+        _close(a, r, rtol=3e-5)
+    z = torch.randn(8, 64, 11, 11, device=DEV)
+    a, code = C.f32_pool_relu_fwd(z, 2, 1)
+    assert torch.equal(a, F.max_pool2d(F.relu(z), 2, 1))
+
+
 def test_conv_f32_uint8_input_fuses_normalize():
     g = torch.Generator(device=DEV).manual_seed(3)
     xu8 = torch.randint(0, 256, (6, 1, 28, 28), dtype=torch.uint8, device=DEV, generator=g)
@@ -61,7 +99,7 @@ def test_conv_f32_uint8_input_fuses_normalize():
     _close(dw, wr.grad.float(), rtol=2e-5, atol=1e-3)
 
 
-@pytest.mark.parametrize("H,k,st", [(26, 2, 2), (11, 2, 1), (8, 2, 2)])
+@pytest.mark.parametrize("H,k,st", [(26, 2, 2), (11, 2, 1), (8, 2, 2), (9, 2, 2), (10, 3, 2)])
 def test_pool_relu_f32(H, k, st):
     g = torch.Generator(device=DEV).manual_seed(H)
     z = torch.randn(4, 16, H, H, device=DEV, generator=g)
