@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "device_common.h"
 #include "kernels.h"
@@ -38,7 +39,10 @@ namespace {
 
 using dev::f32x4;
 
-constexpr int BK = 16, TPB = 256;
+#ifndef RINGDP_F32_BK
+#define RINGDP_F32_BK 16
+#endif
+constexpr int BK = RINGDP_F32_BK, TPB = 256;
 
 // n / d for 0 <= n < 2^31 without a divide: q = (mulhi(n, mul) + n) >> shift.
 struct FastDiv {
@@ -60,47 +64,78 @@ __device__ __forceinline__ int unpack_dy(int v) { return static_cast<int>(static
 __device__ __forceinline__ int unpack_dx(int v) { return v >> 16; }
 constexpr int kOut = -0x2000;  // added to a coordinate <= 1024 it can never land in [0, H)
 
-__device__ __forceinline__ float ld_x(const float* x, const unsigned char* xu8, float mean, float inv_std, int off) {
-  if (xu8) return (static_cast<float>(xu8[off]) * (1.0f / 255.0f) - mean) * inv_std;
-  return x[off];
-}
-
 // ---------------------------------------------------------------- operand loaders
 // GEMM C[M][N] = sum_k A(m, k) * B(k, n).  kMC: the operand's thread-fixed index is contiguous in
 // memory (lanes walk m), with a per-workgroup k table; otherwise lanes walk k.
+// A loader resolves an element to a Ref: an element offset into its source and a valid flag.  The
+// kernel reads every element with a raw buffer load (SGPR resource + 32-bit VGPR offset): invalid
+// elements (zero padding, past an edge) get an offset beyond the resource's range and the hardware
+// returns 0, so the loads are branch-free, their count is static and they need no 64-bit address
+// arithmetic.  u8 pixels are normalised at the stash, where their padding (0 AFTER normalisation)
+// needs the valid flag.
+constexpr int kBadOff = 0x20000000;  // x 4 bytes = 2^31: past every source (chunks stay < 2^31 bytes)
+struct Ref {
+  int off, ok;
+};
+__device__ __forceinline__ Ref ref_if(bool ok, int off) { return Ref{ok ? off : kBadOff, ok ? 1 : 0}; }
+__device__ __forceinline__ bool in2(int y, int x, int H, int W) {
+  return static_cast<unsigned>(y) < static_cast<unsigned>(H) && static_cast<unsigned>(x) < static_cast<unsigned>(W);
+}
 
+template <bool U8>
+struct Src {  // fp32 tensor, or raw uint8 pixels normalised as (v / 255 - mean) * inv_std
+  typedef typename std::conditional<U8, unsigned char, float>::type T;
+  static constexpr bool kU8 = U8;
+  const T* p;
+  int bytes;  // buffer-resource range
+  float mean, inv_std;
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(p), 0, bytes, 0x00020000);
+  }
+  __device__ __forceinline__ T load(__amdgpu_buffer_rsrc_t r, int off) const {
+    if constexpr (U8) return __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+    else return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off * 4, 0, 0));
+  }
+  __device__ __forceinline__ float cvt(T v) const {
+    if constexpr (U8) return (static_cast<float>(v) * (1.0f / 255.0f) - mean) * inv_std;
+    else return v;
+  }
+};
+
+// PAD = false (a valid conv over an fp32 input): every (m, k) is in bounds, so rows past M and
+// k past K are clamped onto real elements instead of checked - the rows are never stored and the
+// weights past K are zero.
+template <bool U8, bool PAD>
 struct FwdA {  // A(m = (b, oy, ox), k = (c, ky, kx)) = x[b, c, oy + ky - pad, ox + kx - pad]
   static constexpr bool kMC = true;
-  const float* x;
-  const unsigned char* xu8;
-  float mean, inv_std;
+  Src<U8> src;
   int C, H, W, R, pad, OW, K, M;
   FastDiv ohw, ow;
   struct O {
     int base, y, x;
   };
   __device__ O outer(int m) const {
-    if (m >= M) return O{0, kOut, kOut};
+    if constexpr (!PAD) m = min(m, M - 1);
+    else if (m >= M) return O{0, kOut, kOut};
     const int b = fdiv(m, ohw), r = m - b * static_cast<int>(ohw.d);
     const int oy = fdiv(r, ow), ox = r - oy * OW;
     return O{b * C * H * W + (oy - pad) * W + (ox - pad), oy - pad, ox - pad};
   }
   __device__ int2 ktab(int k) const {  // (offset, dy|dx)
-    if (k >= K) return int2{0, pack_dyx(kOut, kOut)};
+    if constexpr (!PAD) k = min(k, K - 1);
+    else if (k >= K) return int2{0, pack_dyx(kOut, kOut)};
     const int rr = R * R, c = k / rr, t = k - c * rr, ky = t / R, kx = t - ky * R;
     return int2{c * H * W + ky * W + kx, pack_dyx(ky, kx)};
   }
-  __device__ float load(const O& o, int2 kt) const {
-    const int iy = o.y + unpack_dy(kt.y), ix = o.x + unpack_dx(kt.y);
-    if (static_cast<unsigned>(iy) >= static_cast<unsigned>(H) || static_cast<unsigned>(ix) >= static_cast<unsigned>(W))
-      return 0.f;  // zero padding after Normalize
-    return ld_x(x, xu8, mean, inv_std, o.base + kt.x);
+  __device__ Ref ref(const O& o, int2 kt) const {  // zero padding after Normalize
+    if constexpr (!PAD) return Ref{o.base + kt.x, 1};
+    else return ref_if(in2(o.y + unpack_dy(kt.y), o.x + unpack_dx(kt.y), H, W), o.base + kt.x);
   }
 };
 
 struct DgradA {  // A(m = (b, iy, ix), k = (n, ky, kx)) = dz[b, n, iy + pad - ky, ix + pad - kx]
   static constexpr bool kMC = true;
-  const float* dz;
+  Src<false> src;
   int Kout, W, R, OH, OW, pad, K, M;
   FastDiv hw, w;
   struct O {
@@ -117,28 +152,25 @@ struct DgradA {  // A(m = (b, iy, ix), k = (n, ky, kx)) = dz[b, n, iy + pad - ky
     const int rr = R * R, n = k / rr, t = k - n * rr, ky = t / R, kx = t - ky * R;
     return int2{n * OH * OW - ky * OW - kx, pack_dyx(-ky, -kx)};
   }
-  __device__ float load(const O& o, int2 kt) const {
-    const int oy = o.y + unpack_dy(kt.y), ox = o.x + unpack_dx(kt.y);
-    if (static_cast<unsigned>(oy) >= static_cast<unsigned>(OH) || static_cast<unsigned>(ox) >= static_cast<unsigned>(OW))
-      return 0.f;
-    return dz[o.base + kt.x];
+  __device__ Ref ref(const O& o, int2 kt) const {
+    return ref_if(in2(o.y + unpack_dy(kt.y), o.x + unpack_dx(kt.y), OH, OW), o.base + kt.x);
   }
 };
 
 struct WeightB {  // B(k = (c, ky, kx), n) = w[n][c][ky][kx]; lanes walk k
   static constexpr bool kMC = false;
-  const float* w;
+  Src<false> src;
   int K, N;
   typedef int O;
   typedef int KS;
   __device__ O outer(int n) const { return n < N ? n * K : -1; }
   __device__ KS kstate(int k, int kend) const { return k < kend ? k : -1; }
-  __device__ float load(O o, KS k) const { return (o >= 0 && k >= 0) ? w[o + k] : 0.f; }
+  __device__ Ref ref(O o, KS k) const { return ref_if((o | k) >= 0, o + k); }
 };
 
 struct DgradB {  // B(k = (n, ky, kx), c) = w[n][c][ky][kx]; lanes walk k
   static constexpr bool kMC = false;
-  const float* w;
+  Src<false> src;
   int C, rr, K;
   FastDiv frr;
   typedef int O;
@@ -149,12 +181,12 @@ struct DgradB {  // B(k = (n, ky, kx), c) = w[n][c][ky][kx]; lanes walk k
     const int n = fdiv(k, frr);
     return n * C * rr + (k - n * rr);
   }
-  __device__ float load(O o, KS k) const { return (o >= 0 && k >= 0) ? w[o + k] : 0.f; }
+  __device__ Ref ref(O o, KS k) const { return ref_if((o | k) >= 0, o + k); }
 };
 
 struct WgradA {  // A(m = n, k = (b, r)) = dz[b, n, r]     (k runs over batch x output pixels)
   static constexpr bool kMC = false;
-  const float* dz;
+  Src<false> src;
   int Kout, ohwi;
   FastDiv ohw;
   typedef int O;
@@ -165,42 +197,39 @@ struct WgradA {  // A(m = n, k = (b, r)) = dz[b, n, r]     (k runs over batch x 
     const int b = fdiv(k, ohw);
     return b * Kout * ohwi + (k - b * ohwi);
   }
-  __device__ float load(O o, KS k) const { return (o >= 0 && k >= 0) ? dz[o + k] : 0.f; }
+  __device__ Ref ref(O o, KS k) const { return ref_if((o | k) >= 0, o + k); }
 };
 
-struct WgradB {  // B(k = (b, oy, ox), j = (c, ky, kx)) = x[b, c, oy + ky - pad, ox + kx - pad];
-                 // column j == Nw is all ones: the bias gradient comes out as one more GEMM column
+// PAD = false: as FwdA - columns past Nw and k past the slice are clamped onto real elements (the
+// columns are never stored, A is zero past the slice).
+template <bool U8, bool PAD>
+struct WgradB {  // B(k = (b, oy, ox), j = (c, ky, kx)) = x[b, c, oy + ky - pad, ox + kx - pad]
   static constexpr bool kMC = false;
-  const float* x;
-  const unsigned char* xu8;
-  float mean, inv_std;
+  Src<U8> src;
   int C, H, W, R, pad, OW, Nw;
   FastDiv ohw, ow;
   struct O {
-    int off, dyx, kind;  // kind 0: pixel, 1: ones (bias column), 2: zero (past the last column)
+    int off, dyx;  // dyx never in bounds past the last column
   };
   struct KS {
     int base, y, x;  // y = oy - pad, x = ox - pad; y = kOut when k is past the slice
   };
   __device__ O outer(int j) const {
-    if (j > Nw) return O{0, 0, 2};
-    if (j == Nw) return O{0, 0, 1};
+    if constexpr (!PAD) j = min(j, Nw - 1);
+    else if (j >= Nw) return O{0, pack_dyx(kOut, kOut)};
     const int rr = R * R, c = j / rr, t = j - c * rr, ky = t / R, kx = t - ky * R;
-    return O{c * H * W + ky * W + kx, pack_dyx(ky, kx), 0};
+    return O{c * H * W + ky * W + kx, pack_dyx(ky, kx)};
   }
   __device__ KS kstate(int k, int kend) const {
-    if (k >= kend) return KS{0, kOut, kOut};
+    if constexpr (!PAD) k = min(k, kend - 1);
+    else if (k >= kend) return KS{0, kOut, kOut};
     const int b = fdiv(k, ohw), r = k - b * static_cast<int>(ohw.d);
     const int oy = fdiv(r, ow), ox = r - oy * OW;
     return KS{b * C * H * W + (oy - pad) * W + (ox - pad), oy - pad, ox - pad};
   }
-  __device__ float load(const O& o, const KS& k) const {
-    if (o.kind == 2) return 0.f;
-    if (o.kind == 1) return k.y == kOut ? 0.f : 1.f;
-    const int iy = k.y + unpack_dy(o.dyx), ix = k.x + unpack_dx(o.dyx);
-    if (static_cast<unsigned>(iy) >= static_cast<unsigned>(H) || static_cast<unsigned>(ix) >= static_cast<unsigned>(W))
-      return 0.f;
-    return ld_x(x, xu8, mean, inv_std, k.base + o.off);
+  __device__ Ref ref(const O& o, const KS& k) const {
+    if constexpr (!PAD) return Ref{k.base + o.off, 1};
+    return ref_if(in2(k.y + unpack_dy(o.dyx), k.x + unpack_dx(o.dyx), H, W), k.base + o.off);
   }
 };
 
@@ -227,16 +256,20 @@ struct SlabOut {  // split-K slice z: slab[z][m][n]
 };
 
 // ---------------------------------------------------------------- the GEMM core
-// grid: x = m tiles, y = n tiles, z = k slices (each covers k_per_slice of K).  WM x WN waves of
-// 32x32; with WM * WN < 4 the remaining waves split each k-tile's MFMA steps between them and the
-// partial accumulators are summed in a fixed wave order at the end (the 32x32 tile of the small
-// conv1 weight gradient).  ktab_n > 0: the A operand's k table (K rounded up to 16) in dynamic LDS.
-template <int WM, int WN, class LA, class LB, class Epi>
-__global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int k_per_slice, int ktab_n, LA la,
-                                                       LB lb, Epi epi) {
-  constexpr int BM = 32 * WM, BN = 32 * WN, KSPLIT = 4 / (WM * WN);
+// grid: x = m tiles, y = n tiles, z = k slices (each covers k_per_slice of K).  WM x WN waves, each
+// owning a (16 TM) x (16 TN) block of the output (TM x TN MFMA tiles).  On gfx950 the f32 MFMA runs
+// at the f32 VALU rate and the loaders' VALU work competes with it (PMC: MFMA busy 48 % with 5.7
+// VALU instructions per MFMA on 32x32 wave blocks), so the wave blocks are as large as the GEMM's
+// narrow side allows: elements gathered per MFMA per lane = 16 / BN (A) + 16 / BM (B).
+// With WM * WN < 4 the remaining waves split each k-tile's MFMA steps between them and the partial
+// accumulators are summed in a fixed wave order at the end (the 32x32 tile of conv1's weight
+// gradient).  ktab_n > 0: the A operand's k table (K rounded up to BK) in dynamic LDS.
+template <int WM, int WN, int TM, int TN, class LA, class LB, class Epi>
+__global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int k_per_slice, int ktab_n, int bias_col,
+                                                       LA la, LB lb, Epi epi) {
+  constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN, KSPLIT = 4 / (WM * WN);
   static_assert(KSPLIT * WM * WN == 4 && BK / 4 >= KSPLIT, "4 waves");
-  constexpr int LDA = BM + 16, LDB = BN + 16;  // row stride: 16 banks apart, conflict-free reads
+  constexpr int LDA = BM + 16, LDB = BN + 16;  // row stride = 16 banks mod 64: conflict-free MFMA reads
   constexpr int EA = BM * BK / TPB, EB = BN * BK / TPB;
   __shared__ float As[2][BK][LDA];
   __shared__ float Bs[2][BK][LDB];
@@ -244,7 +277,7 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN);
-  const int wm = (wmn / WN) * 32, wn = (wmn % WN) * 32;
+  const int wm = (wmn / WN) * 16 * TM, wn = (wmn % WN) * 16 * TN;
   const int m0 = static_cast<int>(blockIdx.x) * BM;
   const int n0 = static_cast<int>(blockIdx.y) * BN;
   const int kbeg = static_cast<int>(blockIdx.z) * k_per_slice;
@@ -268,48 +301,90 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
     for (int i = 0; i < EB; ++i) ob[i] = lb.outer(n0 + tid / BK + (TPB / BK) * i);
   if constexpr (LA::kMC) __syncthreads();  // k table visible
 
-  float ra[EA], rb[EB];
+  // the next k-tile's raw elements (loaded branch-free while the current tile is multiplied); u8
+  // sources also keep a valid bit per element, applied when the tile is stashed
+  const auto rsa = la.src.rsrc();
+  const auto rsb = lb.src.rsrc();
+  constexpr bool UA = decltype(la.src)::kU8, UB = decltype(lb.src)::kU8;
+  typename decltype(la.src)::T ra[EA];
+  typename decltype(lb.src)::T rb[EB];
+  uint32_t va = 0, vb = 0;
+  static_assert(EA <= 32 && EB <= 32, "valid bits");
   auto fetch = [&](int k0) {
-    if constexpr (LA::kMC) {
-#pragma unroll
-      for (int i = 0; i < EA; ++i) {
-        const int k = k0 + tid / BM + (TPB / BM) * i;
-        ra[i] = la.load(oa[0], ktab[k]);
-      }
-    } else {
-      const auto ks = la.kstate(k0 + tid % BK, kend);
-#pragma unroll
-      for (int i = 0; i < EA; ++i) ra[i] = la.load(oa[i], ks);
-    }
-    if constexpr (LB::kMC) {
-#pragma unroll
-      for (int i = 0; i < EB; ++i) rb[i] = lb.load(ob[0], ktab[k0 + tid / BN + (TPB / BN) * i]);
-    } else {
-      const auto ks = lb.kstate(k0 + tid % BK, kend);
-#pragma unroll
-      for (int i = 0; i < EB; ++i) rb[i] = lb.load(ob[i], ks);
-    }
-  };
-  auto stash = [&](int buf) {
+    va = 0;
+    vb = 0;
 #pragma unroll
     for (int i = 0; i < EA; ++i) {
-      if constexpr (LA::kMC) As[buf][tid / BM + (TPB / BM) * i][tid % BM] = ra[i];
-      else As[buf][tid % BK][tid / BK + (TPB / BK) * i] = ra[i];
+      Ref r;
+      if constexpr (LA::kMC) r = la.ref(oa[0], ktab[k0 + tid / BM + (TPB / BM) * i]);
+      else r = la.ref(oa[i], la.kstate(k0 + tid % BK, kend));
+      ra[i] = la.src.load(rsa, r.off);
+      if constexpr (UA) va |= static_cast<uint32_t>(r.ok) << i;
     }
 #pragma unroll
     for (int i = 0; i < EB; ++i) {
-      if constexpr (LB::kMC) Bs[buf][tid / BN + (TPB / BN) * i][tid % BN] = rb[i];
-      else Bs[buf][tid % BK][tid / BK + (TPB / BK) * i] = rb[i];
+      Ref r;
+      if constexpr (LB::kMC) r = lb.ref(ob[0], ktab[k0 + tid / BN + (TPB / BN) * i]);
+      else r = lb.ref(ob[i], lb.kstate(k0 + tid % BK, kend));
+      rb[i] = lb.src.load(rsb, r.off);
+      if constexpr (UB) vb |= static_cast<uint32_t>(r.ok) << i;
+    }
+  };
+  // bias gradient (weight-gradient GEMMs, bias_col >= 0): row sums of A, accumulated by the n-tile 0
+  // workgroups as they stash A (a k-contiguous dz tile) and reduced over the 16 k lanes at the end
+  const bool bias_rows = !LA::kMC && bias_col >= 0 && blockIdx.y == 0;
+  float bsum[LA::kMC ? 1 : EA];
+#pragma unroll
+  for (int i = 0; i < (LA::kMC ? 1 : EA); ++i) bsum[i] = 0.f;
+  auto stash = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < EA; ++i) {
+      float v;
+      if constexpr (UA) v = ((va >> i) & 1) ? la.src.cvt(ra[i]) : 0.f;
+      else v = ra[i];
+      if constexpr (!LA::kMC) {
+        if (bias_rows) bsum[i] += v;
+      }
+      if constexpr (LA::kMC) As[buf][tid / BM + (TPB / BM) * i][tid % BM] = v;
+      else As[buf][tid % BK][tid / BK + (TPB / BK) * i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < EB; ++i) {
+      float v;
+      if constexpr (UB) v = ((vb >> i) & 1) ? lb.src.cvt(rb[i]) : 0.f;
+      else v = rb[i];
+      if constexpr (LB::kMC) Bs[buf][tid / BN + (TPB / BN) * i][tid % BN] = v;
+      else Bs[buf][tid % BK][tid / BK + (TPB / BK) * i] = v;
     }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = dev::zero_f32x4();
+    for (int j = 0; j < TN; ++j) acc[i][j] = dev::zero_f32x4();
 
   const int lr = lane & 15, lk = lane >> 4;
+  // this wave's k steps of a tile: all of them, or with KSPLIT waves per block every KSPLIT-th one
+  // (wave-uniform start)
+  constexpr int NKK = BK / 4 / KSPLIT;
+  const int kk0 = 4 * __builtin_amdgcn_readfirstlane(wk);
+  auto mfma_tile = [&](int buf) {
+#pragma unroll
+    for (int t = 0; t < NKK; ++t) {
+      const int kk = (KSPLIT == 1 ? 4 * t : kk0 + 4 * KSPLIT * t) + lk;
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[buf][kk][wm + 16 * i + lr];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[buf][kk][wn + 16 * j + lr];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)  // B as the row operand: D[n][m], lane l holds n = 4 (l >> 4) + r, m = l & 15
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b[j], a[i], acc[i][j], 0, 0, 0);
+    }
+  };
   if (kbeg < kend) {
     fetch(kbeg);
     stash(0);
@@ -319,39 +394,43 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
   for (int k0 = kbeg; k0 < kend; k0 += BK) {
     const bool more = k0 + BK < kend;
     if (more) fetch(k0 + BK);  // next tile in flight during the MFMAs
-#pragma unroll
-    for (int kk = 4 * wk; kk < BK; kk += 4 * KSPLIT) {
-      const float a0 = As[buf][kk + lk][wm + lr], a1 = As[buf][kk + lk][wm + 16 + lr];
-      const float b0 = Bs[buf][kk + lk][wn + lr], b1 = Bs[buf][kk + lk][wn + 16 + lr];
-      // B as the row operand: D[n][m], lane l holds n = 4 (l >> 4) + r, m = l & 15
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(b0, a0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(b1, a0, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(b0, a1, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(b1, a1, acc[1][1], 0, 0, 0);
-    }
+    mfma_tile(buf);
     if (more) stash(buf ^ 1);  // the other buffer's last readers passed the previous barrier
     __syncthreads();
     buf ^= 1;
   }
+  if constexpr (!LA::kMC) {
+    if (bias_rows) {
+      static_assert(BK == 16, "bias rows: one 16-lane group per A row");
+#pragma unroll
+      for (int i = 0; i < EA; ++i) {
+        float v = bsum[i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+        const int m = m0 + tid / BK + (TPB / BK) * i;
+        if ((tid % BK) == 0 && m < M) epi.store(epi.row(m), bias_col, v);
+      }
+    }
+  }
   if constexpr (KSPLIT > 1) {
-    __shared__ f32x4 red[KSPLIT > 1 ? (KSPLIT - 1) * 4 * 64 : 1];
+    __shared__ f32x4 red[KSPLIT > 1 ? (KSPLIT - 1) * TM * TN * 64 : 1];
     if (wk > 0)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) red[((wk - 1) * 4 + q) * 64 + lane] = acc[q >> 1][q & 1];
+      for (int q = 0; q < TM * TN; ++q) red[((wk - 1) * TM * TN + q) * 64 + lane] = acc[q / TN][q % TN];
     __syncthreads();
     if (wk > 0) return;
 #pragma unroll
     for (int w = 0; w < KSPLIT - 1; ++w)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] += red[(w * 4 + q) * 64 + lane];
+      for (int q = 0; q < TM * TN; ++q) acc[q / TN][q % TN] += red[(w * TM * TN + q) * 64 + lane];
   }
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm + i * 16 + lr;
     if (m >= M) continue;
     const int rowoff = epi.row(m);
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn + j * 16 + 4 * lk + r;
@@ -360,34 +439,42 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
   }
 }
 
-// wave layout by GEMM shape: 64x64 by default, 128x32 for N <= 32, 32x128 for M <= 32, 32x32 with
-// the k-tile split over the 4 waves when both are
-int pick_layout(int M, int N) {
-  if (M <= 32 && N <= 32) return 11;
-  if (N <= 32 && M > 32) return 41;
-  if (M <= 32 && N > 32) return 14;
-  return 22;
+// Workgroup tile layouts (WM, WN waves of TM x TN MFMA tiles), chosen per GEMM by its narrow side.
+enum Layout { L32x32K4, L256x32, L128x64, L64x128, L32x128 };
+
+constexpr int layout_bm(Layout l) { return l == L256x32 ? 256 : l == L128x64 ? 128 : l == L64x128 ? 64 : 32; }
+constexpr int layout_bn(Layout l) { return l == L256x32 ? 32 : l == L128x64 ? 64 : l == L32x32K4 ? 32 : 128; }
+
+// Forward / data-gradient GEMMs: m = pixels (huge), n = channels.  Weight gradients: m = output
+// channels, n = input channels x taps (+ bias column), k = batch x pixels.
+Layout pick_layout(int M, int N) {
+  if (M <= 32 && N <= 32) return L32x32K4;
+  if (M <= 32) return L32x128;
+  if (N <= 32) return L256x32;
+  if (N <= 64 || M >= 128) return L128x64;
+  return L64x128;
 }
 
-template <int WM, int WN, class LA, class LB, class Epi>
-void launch_layout(int M, int N, int K, int per, int slices, const LA& la, const LB& lb, const Epi& epi,
-                   hipStream_t s) {
-  constexpr int BM = 32 * WM, BN = 32 * WN;
+template <int WM, int WN, int TM, int TN, class LA, class LB, class Epi>
+void launch_layout(int M, int N, int K, int per, int slices, int bias_col, const LA& la, const LB& lb,
+                   const Epi& epi, hipStream_t s) {
+  constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
   dim3 grid(static_cast<unsigned>((M + BM - 1) / BM), static_cast<unsigned>((N + BN - 1) / BN),
             static_cast<unsigned>(slices));
   const int ktab_n = LA::kMC ? (K + BK - 1) / BK * BK : 0;
-  hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, LA, LB, Epi>), grid, dim3(TPB), ktab_n * sizeof(int2), s, M, N, K,
-                     per, ktab_n, la, lb, epi);
+  hipLaunchKernelGGL((gemm_f32_kernel<WM, WN, TM, TN, LA, LB, Epi>), grid, dim3(TPB), ktab_n * sizeof(int2), s, M,
+                     N, K, per, ktab_n, bias_col, la, lb, epi);
 }
 
 template <class LA, class LB, class Epi>
-void launch_gemm(int M, int N, int K, int per, int slices, const LA& la, const LB& lb, const Epi& epi,
-                 hipStream_t s) {
+void launch_gemm(int M, int N, int K, int per, int slices, int bias_col, const LA& la, const LB& lb,
+                 const Epi& epi, hipStream_t s) {
   switch (pick_layout(M, N)) {
-    case 41: launch_layout<4, 1>(M, N, K, per, slices, la, lb, epi, s); break;
-    case 14: launch_layout<1, 4>(M, N, K, per, slices, la, lb, epi, s); break;
-    case 11: launch_layout<1, 1>(M, N, K, per, slices, la, lb, epi, s); break;
-    default: launch_layout<2, 2>(M, N, K, per, slices, la, lb, epi, s); break;
+    case L32x32K4: launch_layout<1, 1, 2, 2>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
+    case L256x32: launch_layout<4, 1, 4, 2>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
+    case L128x64: launch_layout<4, 1, 2, 4>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
+    case L64x128: launch_layout<2, 2, 2, 4>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
+    case L32x128: launch_layout<1, 4, 2, 2>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
   }
 }
 
@@ -413,6 +500,46 @@ __global__ __launch_bounds__(256) void pool_relu_fwd_kernel(const float* __restr
     a[i] = live ? best : 0.f;
     code[i] = live ? static_cast<unsigned char>(arg) : 255;
   }
+}
+
+// 2x2/s2 windows with an even input width: two 8-B row loads per window.
+__global__ __launch_bounds__(256) void pool2s2_fwd_kernel(const float* __restrict__ z, float* __restrict__ a,
+                                                          unsigned char* __restrict__ code, int total, int H,
+                                                          int W, FastDiv fphw, FastDiv fpw) {
+  const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= total) return;
+  const int bc = fdiv(i, fphw), r = i - bc * static_cast<int>(fphw.d);
+  const int py = fdiv(r, fpw), px = r - py * static_cast<int>(fpw.d);
+  const float* zp = z + bc * H * W + (2 * py) * W + 2 * px;
+  const float2 t = *reinterpret_cast<const float2*>(zp), b = *reinterpret_cast<const float2*>(zp + W);
+  float best = t.x;
+  int arg = 0;
+  if (t.y > best) { best = t.y; arg = 1; }
+  if (b.x > best) { best = b.x; arg = 2; }
+  if (b.y > best) { best = b.y; arg = 3; }
+  const bool live = best > 0.f;
+  a[i] = live ? best : 0.f;
+  code[i] = live ? static_cast<unsigned char>(arg) : 255;
+}
+
+// 2x2/s1 windows: the four loads issued together.
+__global__ __launch_bounds__(256) void pool2s1_fwd_kernel(const float* __restrict__ z, float* __restrict__ a,
+                                                          unsigned char* __restrict__ code, int total, int H,
+                                                          int W, FastDiv fphw, FastDiv fpw) {
+  const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= total) return;
+  const int bc = fdiv(i, fphw), r = i - bc * static_cast<int>(fphw.d);
+  const int py = fdiv(r, fpw), px = r - py * static_cast<int>(fpw.d);
+  const float* zp = z + bc * H * W + py * W + px;
+  const float v0 = zp[0], v1 = zp[1], v2 = zp[W], v3 = zp[W + 1];
+  float best = v0;
+  int arg = 0;
+  if (v1 > best) { best = v1; arg = 1; }
+  if (v2 > best) { best = v2; arg = 2; }
+  if (v3 > best) { best = v3; arg = 3; }
+  const bool live = best > 0.f;
+  a[i] = live ? best : 0.f;
+  code[i] = live ? static_cast<unsigned char>(arg) : 255;
 }
 
 // dz[bc, y, x] = sum over windows (py, px) covering (y, x) whose code points at (y, x) of da[bc, py, px]
@@ -485,22 +612,44 @@ __global__ __launch_bounds__(256) void pool2s1_bwd_kernel(const float* __restric
     const int bc = fdiv(i, fhw), r = i - bc * static_cast<int>(fhw.d);
     const int y = fdiv(r, fw), x = r - y * static_cast<int>(fw.d);
     const int base = bc * PH * PW;
+    // all 8 loads issued together (clamped in-plane addresses), then masked: one memory round trip
+    int o[4];
+    bool in[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int py = y - (q >> 1), px = x - (q & 1);
+      in[q] = static_cast<unsigned>(py) < static_cast<unsigned>(PH) && static_cast<unsigned>(px) < static_cast<unsigned>(PW);
+      o[q] = base + min(max(py, 0), PH - 1) * PW + min(max(px, 0), PW - 1);
+    }
+    int c[4];
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      c[q] = code[o[q]];
+      v[q] = da[o[q]];
+    }
     float g = 0.f;
 #pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const int py = y - dy, px = x - dx;
-        if (static_cast<unsigned>(py) < static_cast<unsigned>(PH) && static_cast<unsigned>(px) < static_cast<unsigned>(PW)) {
-          const int o = base + py * PW + px;
-          if (code[o] == dy * 2 + dx) g += da[o];
-        }
-      }
+    for (int q = 0; q < 4; ++q)
+      if (in[q] && c[q] == q) g += v[q];
     dz[i] = g;
   }
 }
 
-// Fixed-order sum of the split-K slabs [slices][Kout][Nw + has_bias] into dw [Kout][Nw] and db [Kout].
+// Fixed-order sums of the split-K slabs [slices][Kout][Nw + has_bias]: stage 1 sums groups of
+// kSlabGroup consecutive slices into part[group] (grid.y = groups), stage 2 sums the groups into
+// dw [Kout][Nw] and db [Kout].  Two stages keep each thread's serial chain short.
+constexpr int kSlabGroup = 32;
+__global__ __launch_bounds__(256) void slab_group_kernel(const float* __restrict__ slab, int slices, int total,
+                                                         float* __restrict__ part) {
+  const int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= total) return;
+  const int z0 = static_cast<int>(blockIdx.y) * kSlabGroup, z1 = min(z0 + kSlabGroup, slices);
+  float acc = 0.f;
+  for (int z = z0; z < z1; ++z) acc += slab[static_cast<int64_t>(z) * total + i];
+  part[static_cast<int64_t>(blockIdx.y) * total + i] = acc;
+}
+
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, int slices, int Kout,
                                                            int Nw, int ncol, float* __restrict__ dw,
                                                            float* __restrict__ db) {
@@ -520,12 +669,17 @@ int grid_1d(int64_t n) {
   return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
 }
 
-// Largest batch chunk whose per-chunk element counts (each listed per-image size) stay < 2^31
+// One element per thread for the pool kernels: their per-element loads are dependent (code, then
+// gradient), so a grid-stride loop over a capped grid runs at one load round trip per iteration.
+int grid_elems(int64_t n) { return static_cast<int>(std::max<int64_t>(1, (n + 255) / 256)); }
+
+// Largest batch chunk whose per-chunk element counts (each listed per-image size) stay < 2^29, so
+// every fp32 operand chunk is < 2^31 bytes: 32-bit buffer offsets, and kBadOff is out of range
 // (RINGDP_F32_CHUNK_LIMIT lowers the bound: the tests run the chunked path at small batches).
 int64_t batch_chunk(int64_t B, std::initializer_list<int64_t> per_image) {
   int64_t worst = 1;
   for (int64_t v : per_image) worst = std::max(worst, v);
-  int64_t limit = (int64_t{1} << 31) - 1;
+  int64_t limit = (int64_t{1} << 29) - 1;
   if (const char* e = std::getenv("RINGDP_F32_CHUNK_LIMIT")) limit = std::max<int64_t>(1, std::min<int64_t>(limit, std::atoll(e)));
   const int64_t cap = limit / worst;
   return std::max<int64_t>(1, std::min(B, cap));
@@ -533,8 +687,8 @@ int64_t batch_chunk(int64_t B, std::initializer_list<int64_t> per_image) {
 
 int wgrad_slices(int M, int N, int64_t K) {
   // enough slices to put >= ~2048 workgroups on the 256 CUs, each slice >= 1024 deep
-  const int l = pick_layout(M, N);
-  const int bm = 32 * (l / 10), bn = 32 * (l % 10);
+  const Layout l = pick_layout(M, N);
+  const int bm = layout_bm(l), bn = layout_bn(l);
   const int64_t tiles = static_cast<int64_t>((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   int64_t s = (2048 + tiles - 1) / tiles;
   const int64_t cap = (K + 1023) / 1024;
@@ -551,8 +705,9 @@ int64_t wgrad_chunk(const ConvF32Geom& g) {
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
   const int64_t chunk = wgrad_chunk(g);
   const int64_t nchunks = (g.B + chunk - 1) / chunk;
-  return static_cast<int>(nchunks) *
-         wgrad_slices(g.Kout, g.C * g.R * g.R + 1, chunk * static_cast<int64_t>(g.OH) * g.OW);
+  const int slices = static_cast<int>(nchunks) *
+                     wgrad_slices(g.Kout, g.C * g.R * g.R, chunk * static_cast<int64_t>(g.OH) * g.OW);
+  return slices + (slices + kSlabGroup - 1) / kSlabGroup;  // + room for the stage-1 group sums
 }
 
 void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
@@ -563,11 +718,22 @@ void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8
   for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {
     const int nb = static_cast<int>(std::min(chunk, g.B - b0));
     const int M = nb * g.OH * g.OW;
-    FwdA la{x ? x + b0 * xin : nullptr, xu8 ? xu8 + b0 * xin : nullptr, mean, inv_std, g.C, g.H, g.W, g.R, g.pad,
-            g.OW, K, M, make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
-    WeightB lb{w, K, g.Kout};
+    const int xbytes = static_cast<int>(nb * xin);
+    WeightB lb{{w, K * g.Kout * 4, 0.f, 1.f}, K, g.Kout};
     NCHWOut epi{z + b0 * zout, bias, g.Kout, M, make_fdiv(g.OH * g.OW)};
-    launch_gemm(M, g.Kout, K, K, 1, la, lb, epi, s);
+    if (xu8) {
+      FwdA<true, true> la{{xu8 + b0 * xin, xbytes, mean, inv_std}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                          make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
+      launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    } else if (g.pad) {
+      FwdA<false, true> la{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                           make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
+      launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    } else {
+      FwdA<false, false> la{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                            make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
+      launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    }
   }
 }
 
@@ -578,10 +744,11 @@ void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float
   for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {
     const int nb = static_cast<int>(std::min(chunk, g.B - b0));
     const int M = nb * g.H * g.W;
-    DgradA la{dz + b0 * zin, g.Kout, g.W, g.R, g.OH, g.OW, g.pad, K, M, make_fdiv(g.H * g.W), make_fdiv(g.W)};
-    DgradB lb{w, g.C, g.R * g.R, K, make_fdiv(g.R * g.R)};
+    DgradA la{{dz + b0 * zin, static_cast<int>(nb * zin * 4), 0.f, 1.f}, g.Kout, g.W, g.R, g.OH, g.OW, g.pad, K,
+              M, make_fdiv(g.H * g.W), make_fdiv(g.W)};
+    DgradB lb{{w, K * g.C * 4, 0.f, 1.f}, g.C, g.R * g.R, K, make_fdiv(g.R * g.R)};
     NCHWOut epi{dx + b0 * xout, nullptr, g.C, M, make_fdiv(g.H * g.W)};
-    launch_gemm(M, g.C, K, K, 1, la, lb, epi, s);
+    launch_gemm(M, g.C, K, K, 1, -1, la, lb, epi, s);
   }
 }
 
@@ -596,20 +763,43 @@ void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const
   for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {
     const int nb = static_cast<int>(std::min(chunk, g.B - b0));
     const int K = nb * ohw;
-    const int sl = wgrad_slices(g.Kout, Nw + 1, static_cast<int64_t>(chunk) * ohw);
+    const int sl = wgrad_slices(g.Kout, Nw, static_cast<int64_t>(chunk) * ohw);
     int per = (K + sl - 1) / sl;
     per = (per + BK - 1) / BK * BK;
     const int used_sl = (K + per - 1) / per;
-    WgradA la{dz + b0 * zin, g.Kout, ohw, make_fdiv(ohw)};
-    WgradB lb{x ? x + b0 * xin : nullptr, xu8 ? xu8 + b0 * xin : nullptr, mean, inv_std, g.C, g.H, g.W, g.R,
-              g.pad, g.OW, Nw, make_fdiv(ohw), make_fdiv(g.OW)};
+    // GEMM columns = the Nw weights; the bias column (ncol - 1) comes from the dz row sums
+    WgradA la{{dz + b0 * zin, static_cast<int>(nb * zin * 4), 0.f, 1.f}, g.Kout, ohw, make_fdiv(ohw)};
     SlabOut epi{slab + static_cast<int64_t>(used) * g.Kout * ncol, ncol, g.Kout};
-    launch_gemm(g.Kout, ncol, K, per, used_sl, la, lb, epi, s);
+    const int bias_col = db ? Nw : -1;
+    const int xbytes = static_cast<int>(nb * xin);
+    if (xu8) {
+      WgradB<true, true> lb{{xu8 + b0 * xin, xbytes, mean, inv_std}, g.C, g.H, g.W, g.R, g.pad, g.OW, Nw,
+                            make_fdiv(ohw), make_fdiv(g.OW)};
+      launch_gemm(g.Kout, Nw, K, per, used_sl, bias_col, la, lb, epi, s);
+    } else if (g.pad) {
+      WgradB<false, true> lb{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, Nw,
+                             make_fdiv(ohw), make_fdiv(g.OW)};
+      launch_gemm(g.Kout, Nw, K, per, used_sl, bias_col, la, lb, epi, s);
+    } else {
+      WgradB<false, false> lb{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, Nw,
+                              make_fdiv(ohw), make_fdiv(g.OW)};
+      launch_gemm(g.Kout, Nw, K, per, used_sl, bias_col, la, lb, epi, s);
+    }
     used += used_sl;
   }
-  (void)slices;  // the slab holds conv_f32_wgrad_slices(g) >= used slices
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_1d(static_cast<int64_t>(g.Kout) * ncol)), dim3(256), 0, s,
-                     slab, used, g.Kout, Nw, ncol, dw, db);
+  // the slab holds conv_f32_wgrad_slices(g) = (slices of all chunks) + their group count >= used + groups
+  (void)slices;
+  const int total = g.Kout * ncol;
+  const float* src = slab;
+  int nsum = used;
+  if (used > kSlabGroup) {
+    float* part = slab + static_cast<int64_t>(used) * total;
+    nsum = (used + kSlabGroup - 1) / kSlabGroup;
+    hipLaunchKernelGGL(slab_group_kernel, dim3((total + 255) / 256, nsum), dim3(256), 0, s, slab, used, total, part);
+    src = part;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_1d(total)), dim3(256), 0, s, src, nsum, g.Kout, Nw, ncol, dw,
+                     db);
 }
 
 void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,
@@ -619,7 +809,17 @@ void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC
   for (int64_t c0 = 0; c0 < BC; c0 += chunk) {
     const int64_t nbc = std::min(chunk, BC - c0);
     const int total = static_cast<int>(nbc * PH * PW);
-    hipLaunchKernelGGL(pool_relu_fwd_kernel, dim3(grid_1d(total)), dim3(256), 0, s, z + c0 * H * W,
+    if (k == 2 && st == 2 && (W & 1) == 0) {
+      hipLaunchKernelGGL(pool2s2_fwd_kernel, dim3(grid_elems(total)), dim3(256), 0, s, z + c0 * H * W,
+                         a + c0 * PH * PW, code + c0 * PH * PW, total, H, W, make_fdiv(PH * PW), make_fdiv(PW));
+      continue;
+    }
+    if (k == 2 && st == 1) {
+      hipLaunchKernelGGL(pool2s1_fwd_kernel, dim3(grid_elems(total)), dim3(256), 0, s, z + c0 * H * W,
+                         a + c0 * PH * PW, code + c0 * PH * PW, total, H, W, make_fdiv(PH * PW), make_fdiv(PW));
+      continue;
+    }
+    hipLaunchKernelGGL(pool_relu_fwd_kernel, dim3(grid_elems(total)), dim3(256), 0, s, z + c0 * H * W,
                        a + c0 * PH * PW, code + c0 * PH * PW, total, H, W, make_fdiv(PH * PW), make_fdiv(PW), k, st);
   }
 }
@@ -633,16 +833,16 @@ void pool_relu_f32_bwd(const float* da, const unsigned char* code, float* dz, in
     const int total = static_cast<int>(nbc * H * W);
     if (k == 2 && st == 2) {
       const int wins = static_cast<int>(nbc * PH * PW);
-      hipLaunchKernelGGL(pool2s2_bwd_kernel, dim3(grid_1d(wins)), dim3(256), 0, s, da + c0 * PH * PW,
+      hipLaunchKernelGGL(pool2s2_bwd_kernel, dim3(grid_elems(wins)), dim3(256), 0, s, da + c0 * PH * PW,
                          code + c0 * PH * PW, dz + c0 * H * W, wins, make_fdiv(PH * PW), make_fdiv(PW), H, W);
       continue;
     }
     if (k == 2 && st == 1) {
-      hipLaunchKernelGGL(pool2s1_bwd_kernel, dim3(grid_1d(total)), dim3(256), 0, s, da + c0 * PH * PW,
+      hipLaunchKernelGGL(pool2s1_bwd_kernel, dim3(grid_elems(total)), dim3(256), 0, s, da + c0 * PH * PW,
                          code + c0 * PH * PW, dz + c0 * H * W, total, make_fdiv(H * W), make_fdiv(W), PH, PW);
       continue;
     }
-    hipLaunchKernelGGL(pool_relu_bwd_kernel, dim3(grid_1d(total)), dim3(256), 0, s, da + c0 * PH * PW,
+    hipLaunchKernelGGL(pool_relu_bwd_kernel, dim3(grid_elems(total)), dim3(256), 0, s, da + c0 * PH * PW,
                        code + c0 * PH * PW, dz + c0 * H * W, total, make_fdiv(H * W), make_fdiv(W), PH, PW, k, st);
   }
 }
