@@ -555,6 +555,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fp8 GEMM kernel choice: 0 auto, 128 the generic 128x128 core, 256 the 256x256 DMA-pipelined kernel");
   m.def("f32_conv_fwd", &ops::f32_conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
         py::arg("mean") = 0.0, py::arg("std") = 1.0);
+  m.def("f32_conv_pool_fwd", &ops::f32_conv_pool_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
+        py::arg("mean") = 0.0, py::arg("std") = 1.0,
+        "conv + bias + ReLU + 2x2/s2 max-pool in one launch: (pooled activation, 1-byte argmax code)");
+  m.def("f32_conv1_pool_fwd", &ops::f32_conv1_pool_fwd, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("mean"),
+        py::arg("std"), "ConvNet conv1 + ReLU + pool1 at fp32, one wave per image: (a1, code1)");
+  m.def("f32_conv1_wgrad", &ops::f32_conv1_wgrad, py::arg("x"), py::arg("da1"), py::arg("code1"), py::arg("mean"),
+        py::arg("std"), py::arg("dw1"), py::arg("db1"),
+        "ConvNet conv1 weight + bias gradient at fp32 from the pooled gradient (pool backward folded in)");
   m.def("f32_conv_dgrad", &ops::f32_conv_dgrad);
   m.def("f32_conv_wgrad", &ops::f32_conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("pad"), py::arg("mean"),
         py::arg("std"), py::arg("dw"), py::arg("db"));

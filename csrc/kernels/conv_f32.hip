@@ -105,7 +105,10 @@ struct Src {  // fp32 tensor, or raw uint8 pixels normalised as (v / 255 - mean)
 // PAD = false (a valid conv over an fp32 input): every (m, k) is in bounds, so rows past M and
 // k past K are clamped onto real elements instead of checked - the rows are never stored and the
 // weights past K are zero.
-template <bool U8, bool PAD>
+// WIN: window-major output pixels, m = (b, py, px, wy, wx) with (oy, ox) = (2 py + wy, 2 px + wx), so
+// the 4 pixels of a 2x2/s2 pooling window are 4 consecutive m (the PoolOut epilogue); `ow` then
+// divides by the pooled width.
+template <bool U8, bool PAD, bool WIN = false>
 struct FwdA {  // A(m = (b, oy, ox), k = (c, ky, kx)) = x[b, c, oy + ky - pad, ox + kx - pad]
   static constexpr bool kMC = true;
   Src<U8> src;
@@ -118,7 +121,15 @@ struct FwdA {  // A(m = (b, oy, ox), k = (c, ky, kx)) = x[b, c, oy + ky - pad, o
     if constexpr (!PAD) m = min(m, M - 1);
     else if (m >= M) return O{0, kOut, kOut};
     const int b = fdiv(m, ohw), r = m - b * static_cast<int>(ohw.d);
-    const int oy = fdiv(r, ow), ox = r - oy * OW;
+    int oy, ox;
+    if constexpr (WIN) {
+      const int w = r >> 2, py = fdiv(w, ow);
+      oy = 2 * py + ((r >> 1) & 1);
+      ox = 2 * (w - py * static_cast<int>(ow.d)) + (r & 1);
+    } else {
+      oy = fdiv(r, ow);
+      ox = r - oy * OW;
+    }
     return O{b * C * H * W + (oy - pad) * W + (ox - pad), oy - pad, ox - pad};
   }
   __device__ int2 ktab(int k) const {  // (offset, dy|dx)
@@ -235,6 +246,7 @@ struct WgradB {  // B(k = (b, oy, ox), j = (c, ky, kx)) = x[b, c, oy + ky - pad,
 
 // ---------------------------------------------------------------- epilogues
 struct NCHWOut {  // C[m = (b, p)][n] (+ bias[n]) -> out[b, n, p]
+  static constexpr bool kPool = false;
   float* out;
   const float* bias;
   int N, M;
@@ -249,10 +261,28 @@ struct NCHWOut {  // C[m = (b, p)][n] (+ bias[n]) -> out[b, n, p]
 };
 
 struct SlabOut {  // split-K slice z: slab[z][m][n]
+  static constexpr bool kPool = false;
   float* slab;
   int N, M;
   __device__ int row(int m) const { return static_cast<int>(blockIdx.z) * M * N + m * N; }
   __device__ void store(int rowoff, int n, float v) const { slab[rowoff + n] = v; }
+};
+
+// Fused ReLU + 2x2/s2 max-pool over window-major m (FwdA<.., WIN>): the 4 pixels of a window are
+// the 4 lanes 4q..4q+3 of a 16-lane MFMA row group, reduced with two lane exchanges.
+// a[b, n, w] = relu(max_t (C[m][n] + bias[n])), code[b, n, w] = first argmax t (255: not live); the
+// pre-activation is never written.
+struct PoolOut {
+  static constexpr bool kPool = true;
+  float* a;
+  unsigned char* code;
+  const float* bias;
+  int N, M, phw;  // phw = pooled pixels per plane
+  FastDiv hw;     // conv output pixels per plane
+  __device__ int row(int m) const {  // offset of a[b, 0, w]
+    const int b = fdiv(m, hw);
+    return b * N * phw + ((m - b * static_cast<int>(hw.d)) >> 2);
+  }
 };
 
 // ---------------------------------------------------------------- the GEMM core
@@ -424,18 +454,50 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
 #pragma unroll
       for (int q = 0; q < TM * TN; ++q) acc[q / TN][q % TN] += red[(w * TM * TN + q) * 64 + lane];
   }
+  if constexpr (Epi::kPool) {
+    const int tap = lr & 3;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm + i * 16 + lr;
-    if (m >= M) continue;
-    const int rowoff = epi.row(m);
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 16 + lr;  // M is a multiple of 4: a window is all in or all out
+      const int rowoff = epi.row(min(m, M - 1));
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn + j * 16 + 4 * lk + r;
-        if (n < N) epi.store(rowoff, n, acc[i][j][r]);
-      }
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wn + j * 16 + 4 * lk + r;
+          // bias before the max, exactly as conv-then-pool (argmax ties included)
+          float best = acc[i][j][r] + (epi.bias && n < N ? epi.bias[n] : 0.f);
+          int bt = tap;
+#pragma unroll
+          for (int o = 1; o <= 2; o <<= 1) {  // first maximum in window order wins, as max_pool2d
+            const float ov = __shfl_xor(best, o, 64);
+            const int ot = __shfl_xor(bt, o, 64);
+            if (ov > best || (ov == best && ot < bt)) {
+              best = ov;
+              bt = ot;
+            }
+          }
+          if (tap == 0 && m < M && n < N) {
+            const bool live = best > 0.f;
+            epi.a[rowoff + n * epi.phw] = live ? best : 0.f;
+            epi.code[rowoff + n * epi.phw] = live ? static_cast<unsigned char>(bt) : 255;
+          }
+        }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm + i * 16 + lr;
+      if (m >= M) continue;
+      const int rowoff = epi.row(m);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = n0 + wn + j * 16 + 4 * lk + r;
+          if (n < N) epi.store(rowoff, n, acc[i][j][r]);
+        }
+    }
   }
 }
 
@@ -737,6 +799,35 @@ void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8
   }
 }
 
+void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
+                       const float* w, const float* bias, float* a, unsigned char* code, hipStream_t s) {
+  const int K = g.C * g.R * g.R;
+  const int phw = (g.OH / 2) * (g.OW / 2);
+  const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, aout = static_cast<int64_t>(g.Kout) * phw;
+  const int64_t chunk = batch_chunk(g.B, {xin, static_cast<int64_t>(g.Kout) * g.OH * g.OW});
+  for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {
+    const int nb = static_cast<int>(std::min(chunk, g.B - b0));
+    const int M = nb * g.OH * g.OW;
+    const int xbytes = static_cast<int>(nb * xin);
+    WeightB lb{{w, K * g.Kout * 4, 0.f, 1.f}, K, g.Kout};
+    PoolOut epi{a + b0 * aout, code + b0 * aout, bias, g.Kout, M, phw, make_fdiv(g.OH * g.OW)};
+    const FastDiv fpw = make_fdiv(g.OW / 2);
+    if (xu8) {
+      FwdA<true, true, true> la{{xu8 + b0 * xin, xbytes, mean, inv_std}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                                make_fdiv(g.OH * g.OW), fpw};
+      launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    } else if (g.pad) {
+      FwdA<false, true, true> la{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                                 make_fdiv(g.OH * g.OW), fpw};
+      launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    } else {
+      FwdA<false, false, true> la{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                                  make_fdiv(g.OH * g.OW), fpw};
+      launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    }
+  }
+}
+
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, hipStream_t s) {
   const int K = g.Kout * g.R * g.R;
   const int64_t zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW, xout = static_cast<int64_t>(g.C) * g.H * g.W;
@@ -789,17 +880,23 @@ void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const
   }
   // the slab holds conv_f32_wgrad_slices(g) = (slices of all chunks) + their group count >= used + groups
   (void)slices;
-  const int total = g.Kout * ncol;
+  f32_slab_reduce(slab, used, g.Kout, Nw, ncol, dw, db, s);
+}
+
+int f32_slab_capacity(int slices) { return slices + (slices + kSlabGroup - 1) / kSlabGroup; }
+
+void f32_slab_reduce(float* slab, int slices, int Kout, int Nw, int ncol, float* dw, float* db, hipStream_t s) {
+  const int total = Kout * ncol;
   const float* src = slab;
-  int nsum = used;
-  if (used > kSlabGroup) {
-    float* part = slab + static_cast<int64_t>(used) * total;
-    nsum = (used + kSlabGroup - 1) / kSlabGroup;
-    hipLaunchKernelGGL(slab_group_kernel, dim3((total + 255) / 256, nsum), dim3(256), 0, s, slab, used, total, part);
+  int nsum = slices;
+  if (slices > kSlabGroup) {
+    float* part = slab + static_cast<int64_t>(slices) * total;
+    nsum = (slices + kSlabGroup - 1) / kSlabGroup;
+    hipLaunchKernelGGL(slab_group_kernel, dim3((total + 255) / 256, nsum), dim3(256), 0, s, slab, slices, total,
+                       part);
     src = part;
   }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_1d(total)), dim3(256), 0, s, src, nsum, g.Kout, Nw, ncol, dw,
-                     db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_1d(total)), dim3(256), 0, s, src, nsum, Kout, Nw, ncol, dw, db);
 }
 
 void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,

@@ -100,11 +100,28 @@ struct ConvF32Geom {
 // z = conv(x) + bias.  Input either fp32 `x` or raw uint8 `xu8` normalised on load ((v/255-mean)*inv_std).
 void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
                   const float* w, const float* bias, float* z, hipStream_t s);
+// Fused conv + bias + ReLU + 2x2/s2 max-pool (OH, OW even): a = relu(maxpool(conv(x) + bias)) with
+// the 1-byte argmax code of pool_relu_f32_fwd; the conv output is never written.
+void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
+                       const float* w, const float* bias, float* a, unsigned char* code, hipStream_t s);
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, hipStream_t s);
 // split-K weight (+ bias, when db != nullptr) gradient; slab: slices * Kout * (C*R*R + 1) floats
 int conv_f32_wgrad_slices(const ConvF32Geom& g);
 void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const unsigned char* xu8, float mean,
                     float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s);
+// Fixed-order sum of split-K slabs [slices][Kout][ncol] into dw [Kout][Nw] and (column Nw) db;
+// the slab must hold f32_slab_capacity(slices) slices (room for the stage-1 group sums).
+int f32_slab_capacity(int slices);
+void f32_slab_reduce(float* slab, int slices, int Kout, int Nw, int ncol, float* dw, float* db, hipStream_t s);
+// The ConvNet's conv1 (1->32, 5x5, pad 1, 28x28) + bias + ReLU + 2x2/s2 max-pool at fp32
+// (conv1_f32.hip): a1 [B][32][13][13] and its argmax code; and its weight + bias gradient from the
+// pooled gradient da1 and the code (the pool backward is folded in): per-workgroup partials in slab
+// [conv1_f32_wgrad_blocks(B)][32][26] (capacity f32_slab_capacity of that), reduced into dw1, db1.
+int conv1_f32_wgrad_blocks(int64_t B);
+void conv1_pool_f32_fwd(const float* x, const unsigned char* xu8, int64_t B, float mean, float inv_std,
+                        const float* w1, const float* b1, float* a1, unsigned char* code1, hipStream_t s);
+void conv1_wgrad_f32(const float* x, const unsigned char* xu8, int64_t B, float mean, float inv_std, const float* da1,
+                     const unsigned char* code1, float* slab, hipStream_t s);
 // a = relu(maxpool_k,st(z)) with a 1-byte argmax code (255: no gradient); backward is a gather
 void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,
                        hipStream_t s);

@@ -56,6 +56,75 @@ at::Tensor f32_conv_fwd(const at::Tensor& x, const at::Tensor& w, const c10::opt
   return z;
 }
 
+std::tuple<at::Tensor, at::Tensor> f32_conv_pool_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                     const c10::optional<at::Tensor>& bias, int64_t pad, double mean,
+                                                     double std) {
+  check_input(x);
+  util::f32_gpu(w, "conv_f32 weight");
+  auto g = geom(x, w, pad);
+  RINGDP_CHECK(g.OH % 2 == 0 && g.OW % 2 == 0, "conv_f32 + pool: the conv output must have even height and width");
+  const float* b = nullptr;
+  if (bias && bias->defined()) {
+    util::f32_gpu(*bias, "conv_f32 bias");
+    RINGDP_CHECK(bias->numel() == g.Kout, "conv_f32 bias: wrong size");
+    b = bias->data_ptr<float>();
+  }
+  auto a = at::empty({g.B, g.Kout, g.OH / 2, g.OW / 2}, w.options());
+  auto code = at::empty({g.B, g.Kout, g.OH / 2, g.OW / 2}, w.options().dtype(at::kByte));
+  const bool u8 = x.scalar_type() == at::kByte;
+  kern::conv_f32_fwd_pool(g, u8 ? nullptr : x.data_ptr<float>(), u8 ? x.data_ptr<uint8_t>() : nullptr,
+                          static_cast<float>(mean), static_cast<float>(1.0 / std), w.data_ptr<float>(), b,
+                          a.data_ptr<float>(), code.data_ptr<uint8_t>(), util::stream_of(w));
+  return {a, code};
+}
+
+namespace {
+void check_conv1(const at::Tensor& x, const at::Tensor& w1) {
+  check_input(x);
+  util::f32_gpu(w1, "conv1 weight");
+  RINGDP_CHECK(x.dim() == 4 && x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28,
+               "f32 conv1: [B, 1, 28, 28] input expected, got ", x.sizes());
+  RINGDP_CHECK(w1.sizes() == at::IntArrayRef({32, 1, 5, 5}), "f32 conv1: [32, 1, 5, 5] weight expected");
+  RINGDP_CHECK(x.size(0) * 32 * 169 < (int64_t{1} << 31), "f32 conv1: batch too large for 32-bit offsets");
+}
+}  // namespace
+
+std::tuple<at::Tensor, at::Tensor> f32_conv1_pool_fwd(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1,
+                                                      double mean, double std) {
+  check_conv1(x, w1);
+  util::f32_gpu(b1, "conv1 bias");
+  const int64_t B = x.size(0);
+  auto a1 = at::empty({B, 32, 13, 13}, w1.options());
+  auto code1 = at::empty({B, 32, 13, 13}, w1.options().dtype(at::kByte));
+  const bool u8 = x.scalar_type() == at::kByte;
+  auto xc = x.contiguous();
+  kern::conv1_pool_f32_fwd(u8 ? nullptr : xc.data_ptr<float>(), u8 ? xc.data_ptr<uint8_t>() : nullptr, B,
+                           static_cast<float>(mean), static_cast<float>(1.0 / std), w1.data_ptr<float>(),
+                           b1.data_ptr<float>(), a1.data_ptr<float>(), code1.data_ptr<uint8_t>(), util::stream_of(w1));
+  return {a1, code1};
+}
+
+void f32_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& code1, double mean, double std,
+                     at::Tensor& dw1, at::Tensor& db1) {
+  check_conv1(x, dw1);
+  util::f32_gpu(da1, "conv1 pooled grad");
+  util::f32_gpu(db1, "conv1 db");
+  const int64_t B = x.size(0);
+  RINGDP_CHECK(da1.sizes() == at::IntArrayRef({B, 32, 13, 13}) && code1.sizes() == da1.sizes() &&
+                   code1.scalar_type() == at::kByte,
+               "f32 conv1 wgrad: pooled grad / code must be [B, 32, 13, 13]");
+  const int blocks = kern::conv1_f32_wgrad_blocks(B);
+  auto slab = at::empty({static_cast<int64_t>(kern::f32_slab_capacity(blocks)) * 32 * 26}, da1.options());
+  const bool u8 = x.scalar_type() == at::kByte;
+  auto xc = x.contiguous();
+  auto dac = da1.contiguous();
+  auto st = util::stream_of(da1);
+  kern::conv1_wgrad_f32(u8 ? nullptr : xc.data_ptr<float>(), u8 ? xc.data_ptr<uint8_t>() : nullptr, B,
+                        static_cast<float>(mean), static_cast<float>(1.0 / std), dac.data_ptr<float>(),
+                        code1.data_ptr<uint8_t>(), slab.data_ptr<float>(), st);
+  kern::f32_slab_reduce(slab.data_ptr<float>(), blocks, 32, 25, 26, dw1.data_ptr<float>(), db1.data_ptr<float>(), st);
+}
+
 at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad) {
   util::f32_gpu(dz, "conv_f32 dz");
   util::f32_gpu(w, "conv_f32 weight");

@@ -97,6 +97,13 @@ std::tuple<at::Tensor, at::Tensor> synth_u8_images(int64_t B, int64_t H, int64_t
 // fp32 NCHW conv / pool (conv_f32_ops.cpp)
 at::Tensor f32_conv_fwd(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias,
                         int64_t pad, double mean, double std);
+std::tuple<at::Tensor, at::Tensor> f32_conv_pool_fwd(const at::Tensor& x, const at::Tensor& w,
+                                                     const c10::optional<at::Tensor>& bias, int64_t pad, double mean,
+                                                     double std);
+std::tuple<at::Tensor, at::Tensor> f32_conv1_pool_fwd(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1,
+                                                      double mean, double std);
+void f32_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& code1, double mean, double std,
+                     at::Tensor& dw1, at::Tensor& db1);
 at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad);
 void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
                     at::Tensor& dw, const c10::optional<at::Tensor>& db);

@@ -84,6 +84,59 @@ def test_conv_f32_batch_chunks(monkeypatch):
     assert torch.equal(a, F.max_pool2d(F.relu(z), 2, 1))
 
 
+@pytest.mark.parametrize("B,Cin,H,K,R,pad,u8", [(5, 1, 28, 32, 5, 1, True), (9, 64, 10, 128, 3, 0, False),
+                                                (3, 3, 8, 8, 3, 1, False)])
+def test_conv_f32_pool_fused(B, Cin, H, K, R, pad, u8):
+    """conv + bias + ReLU + 2x2/s2 max-pool in one launch == conv kernel then the pool kernel (bit-exact:
+    same products in the same order), and == ATen."""
+    g = torch.Generator(device=DEV).manual_seed(B * 7 + K)
+    if u8:
+        x = torch.randint(0, 256, (B, Cin, H, H), dtype=torch.uint8, device=DEV, generator=g)
+        mean, std = 0.1307, 0.3081
+        xf = (x.float() / 255.0 - mean) / std
+    else:
+        x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+        mean, std = 0.0, 1.0
+        xf = x
+    w = torch.randn(K, Cin, R, R, device=DEV, generator=g) * 0.2
+    b = torch.randn(K, device=DEV, generator=g) * 0.1
+    a, code = C.f32_conv_pool_fwd(x, w, b, pad, mean, std)
+    z = C.f32_conv_fwd(x, w, b, pad, mean, std)
+    a2, code2 = C.f32_pool_relu_fwd(z, 2, 2)
+    assert torch.equal(a, a2)
+    assert torch.equal(code, code2)
+    ref = F.max_pool2d(F.relu(F.conv2d(xf.double(), w.double(), b.double(), padding=pad)), 2, 2).float()
+    _close(a, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("u8", [True, False])
+@pytest.mark.parametrize("B", [1, 7, 37])
+def test_conv1_f32_dedicated(B, u8):
+    """conv1 + ReLU + pool1 (one wave per image) == the generic conv+pool kernels bit-exactly, and its
+    weight/bias gradient from the pooled gradient == pool backward + generic wgrad (fp32 rounding)."""
+    g = torch.Generator(device=DEV).manual_seed(B + 11 * u8)
+    if u8:
+        x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device=DEV, generator=g)
+        mean, std = 0.1307, 0.3081
+    else:
+        x = torch.randn(B, 1, 28, 28, device=DEV, generator=g)
+        mean, std = 0.0, 1.0
+    w = torch.randn(32, 1, 5, 5, device=DEV, generator=g) * 0.2
+    b = torch.randn(32, device=DEV, generator=g) * 0.1
+    a, code = C.f32_conv1_pool_fwd(x, w, b, mean, std)
+    a_ref, code_ref = C.f32_conv_pool_fwd(x, w, b, 1, mean, std)
+    _close(a, a_ref, rtol=1e-6, atol=1e-6)
+    assert float((code != code_ref).float().mean()) < 1e-3  # ties only
+    da = torch.randn(B, 32, 13, 13, device=DEV, generator=g)
+    dw, db = torch.empty_like(w), torch.empty_like(b)
+    C.f32_conv1_wgrad(x, da, code, mean, std, dw, db)
+    dz = C.f32_pool_relu_bwd(da, code, 26, 26, 2, 2)
+    dw_ref, db_ref = torch.empty_like(w), torch.empty_like(b)
+    C.f32_conv_wgrad(dz, x, 1, mean, std, dw_ref, db_ref)
+    _close(dw, dw_ref, rtol=2e-5, atol=1e-5)
+    _close(db, db_ref, rtol=2e-5, atol=1e-5)
+
+
 def test_conv_f32_uint8_input_fuses_normalize():
     g = torch.Generator(device=DEV).manual_seed(3)
     xu8 = torch.randint(0, 256, (6, 1, 28, 28), dtype=torch.uint8, device=DEV, generator=g)

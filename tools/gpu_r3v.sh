@@ -1,6 +1,6 @@
 # r3v: fp32 ConvNet kernels rework - numerics tests, bench, kernel table
 set -o pipefail
-O=gpurun_out/r3v; mkdir -p $O
+O=gpurun_out/${RUN:-r3v}; mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -q -s --timeout 200 --timeout-method thread tests/test_convnet_fp32_gpu.py > $O/tests.log 2>&1; rc=$?; grep -E "passed|failed|max \|loss" $O/tests.log | tail -4; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --dtype fp32 --steps 10 --warmup 3 --comm-stats-steps 0 > $O/b_f32.json 2>$O/b_f32.err || exit $?; grep -o '"value": [0-9.]*' $O/b_f32.json
 cd /tmp; cd - >/dev/null; export TMPDIR=/tmp
