@@ -556,8 +556,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_conv_fwd", &ops::f32_conv_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
         py::arg("mean") = 0.0, py::arg("std") = 1.0);
   m.def("f32_conv_pool_fwd", &ops::f32_conv_pool_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("pad"),
-        py::arg("mean") = 0.0, py::arg("std") = 1.0,
-        "conv + bias + ReLU + 2x2/s2 max-pool in one launch: (pooled activation, 1-byte argmax code)");
+        py::arg("mean") = 0.0, py::arg("std") = 1.0, py::arg("stride") = 2,
+        "conv + bias + ReLU + 2x2 max-pool (stride 2 or 1) in one launch: (pooled activation, 1-byte argmax code)");
   m.def("f32_conv1_pool_fwd", &ops::f32_conv1_pool_fwd, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("mean"),
         py::arg("std"), "ConvNet conv1 + ReLU + pool1 at fp32, one wave per image: (a1, code1)");
   m.def("f32_conv1_wgrad", &ops::f32_conv1_wgrad, py::arg("x"), py::arg("da1"), py::arg("code1"), py::arg("mean"),

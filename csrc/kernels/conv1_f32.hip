@@ -31,15 +31,35 @@ constexpr int LDS_IMG = PADW * PADW + 4;
 constexpr int WAVES = 4;
 
 // Normalised image b into the wave's LDS copy (interior only: the zero border is written once).
+// All 13 loads of a lane are issued before the first store: one memory round trip per image.
 template <bool U8>
 __device__ __forceinline__ void stage_image(float* im, const void* x, int b, float mean, float inv_std, int lane) {
-  for (int i = lane; i < IMG * IMG; i += 64) {
-    const int y = i / IMG, xx = i - y * IMG;
-    float v;
-    if constexpr (U8) v = (static_cast<float>(static_cast<const unsigned char*>(x)[b * IMG * IMG + i]) * (1.0f / 255.0f) - mean) * inv_std;
-    else v = static_cast<const float*>(x)[b * IMG * IMG + i];
-    im[(y + 1) * PADW + xx + 1] = v;
+  constexpr int PER = (IMG * IMG + 63) / 64;
+  float v[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = min(lane + 64 * q, IMG * IMG - 1);
+    if constexpr (U8) v[q] = static_cast<float>(static_cast<const unsigned char*>(x)[b * IMG * IMG + i]);
+    else v[q] = static_cast<const float*>(x)[b * IMG * IMG + i];
   }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = lane + 64 * q;
+    if (i < IMG * IMG) {
+      const int y = i / IMG, xx = i - y * IMG;
+      im[(y + 1) * PADW + xx + 1] = U8 ? (v[q] * (1.0f / 255.0f) - mean) * inv_std : v[q];
+    }
+  }
+}
+
+// lane exchange inside a quad (DPP, full-rate VALU, no LDS round trip): xor 1 / xor 2
+template <int X>
+__device__ __forceinline__ int quad_xor(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, X == 1 ? 0xB1 : 0x4E, 0xF, 0xF, false);
+}
+template <int X>
+__device__ __forceinline__ float quad_xor(float v) {
+  return __builtin_bit_cast(float, quad_xor<X>(__builtin_bit_cast(int, v)));
 }
 
 // padded-image offset of window-major output pixel m (m < 676): window m >> 2 = (py, px), tap-in-
@@ -102,10 +122,17 @@ __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restr
         for (int r = 0; r < 4; ++r) {
           float best = acc[j][r] + bias[j][r];
           int bt = tap;
-#pragma unroll
-          for (int o = 1; o <= 2; o <<= 1) {  // first maximum in window order wins, as max_pool2d
-            const float ov = __shfl_xor(best, o, 64);
-            const int ot = __shfl_xor(bt, o, 64);
+          {  // first maximum in window order wins, as max_pool2d
+            const float ov = quad_xor<1>(best);
+            const int ot = quad_xor<1>(bt);
+            if (ov > best || (ov == best && ot < bt)) {
+              best = ov;
+              bt = ot;
+            }
+          }
+          {
+            const float ov = quad_xor<2>(best);
+            const int ot = quad_xor<2>(bt);
             if (ov > best || (ov == best && ot < bt)) {
               best = ov;
               bt = ot;
@@ -160,29 +187,33 @@ __global__ __launch_bounds__(256) void conv1_wgrad_f32_kernel(const void* __rest
     if (b >= B) continue;
     const float* db = da1 + static_cast<int64_t>(b) * C1 * NWIN;
     const unsigned char* cbp = code1 + static_cast<int64_t>(b) * C1 * NWIN;
-    int py = 0, px = 0;
-    for (int s = 0; s < NWIN; ++s) {
-      // A operand (row = n = 16 jn + lr): dz1[n][p] = da1[n][s] where the code points at tap lk
-      float av[2];
+    // one pooled row (13 windows) at a time: its 52 gradient / code loads are issued together
+    for (int py = 0; py < PW1; ++py) {
+      float dv[PW1][2];
+      int cv[PW1][2];
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn) {
-        const int o = (16 * jn + lr) * NWIN + s;
-        const int c = cbp[o];
-        const float d = db[o];
-        av[jn] = c == lk ? d : 0.f;
-      }
-      const int pb = 2 * py * PADW + 2 * px + woff;
-      float bv[2];
+      for (int px = 0; px < PW1; ++px)
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) bv[jt] = im[pb + tapoff[jt]] * tapmul[jt] + tapone[jt];
+        for (int jn = 0; jn < 2; ++jn) {
+          const int o = (16 * jn + lr) * NWIN + py * PW1 + px;
+          cv[px][jn] = cbp[o];
+          dv[px][jn] = db[o];
+        }
 #pragma unroll
-      for (int jn = 0; jn < 2; ++jn)
+      for (int px = 0; px < PW1; ++px) {
+        // A operand (row = n = 16 jn + lr): dz1[n][p] = da1[n][window] where the code points at tap lk
+        float av[2];
 #pragma unroll
-        for (int jt = 0; jt < 2; ++jt)
-          acc[jn][jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[jn], bv[jt], acc[jn][jt], 0, 0, 0);
-      if (++px == PW1) {
-        px = 0;
-        ++py;
+        for (int jn = 0; jn < 2; ++jn) av[jn] = cv[px][jn] == lk ? dv[px][jn] : 0.f;
+        const int pb = 2 * py * PADW + 2 * px + woff;
+        float bv[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) bv[jt] = im[pb + tapoff[jt]] * tapmul[jt] + tapone[jt];
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt)
+            acc[jn][jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[jn], bv[jt], acc[jn][jt], 0, 0, 0);
       }
     }
   }

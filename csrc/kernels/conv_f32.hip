@@ -108,7 +108,9 @@ struct Src {  // fp32 tensor, or raw uint8 pixels normalised as (v / 255 - mean)
 // WIN: window-major output pixels, m = (b, py, px, wy, wx) with (oy, ox) = (2 py + wy, 2 px + wx), so
 // the 4 pixels of a 2x2/s2 pooling window are 4 consecutive m (the PoolOut epilogue); `ow` then
 // divides by the pooled width.
-template <bool U8, bool PAD, bool WIN = false>
+// MODE 2: one image per 128-row m tile, m = (b, p < 128), p >= OH*OW clamped onto the last pixel
+// (those rows are never stored) - the PoolS1Out epilogue pools a whole image from LDS.
+template <bool U8, bool PAD, int MODE = 0>
 struct FwdA {  // A(m = (b, oy, ox), k = (c, ky, kx)) = x[b, c, oy + ky - pad, ox + kx - pad]
   static constexpr bool kMC = true;
   Src<U8> src;
@@ -120,9 +122,16 @@ struct FwdA {  // A(m = (b, oy, ox), k = (c, ky, kx)) = x[b, c, oy + ky - pad, o
   __device__ O outer(int m) const {
     if constexpr (!PAD) m = min(m, M - 1);
     else if (m >= M) return O{0, kOut, kOut};
-    const int b = fdiv(m, ohw), r = m - b * static_cast<int>(ohw.d);
+    int b, r;
+    if constexpr (MODE == 2) {
+      b = m >> 7;
+      r = min(m & 127, static_cast<int>(ohw.d) - 1);
+    } else {
+      b = fdiv(m, ohw);
+      r = m - b * static_cast<int>(ohw.d);
+    }
     int oy, ox;
-    if constexpr (WIN) {
+    if constexpr (MODE == 1) {
       const int w = r >> 2, py = fdiv(w, ow);
       oy = 2 * py + ((r >> 1) & 1);
       ox = 2 * (w - py * static_cast<int>(ow.d)) + (r & 1);
@@ -246,7 +255,7 @@ struct WgradB {  // B(k = (b, oy, ox), j = (c, ky, kx)) = x[b, c, oy + ky - pad,
 
 // ---------------------------------------------------------------- epilogues
 struct NCHWOut {  // C[m = (b, p)][n] (+ bias[n]) -> out[b, n, p]
-  static constexpr bool kPool = false;
+  static constexpr bool kPool = false, kPoolS1 = false;
   float* out;
   const float* bias;
   int N, M;
@@ -261,7 +270,7 @@ struct NCHWOut {  // C[m = (b, p)][n] (+ bias[n]) -> out[b, n, p]
 };
 
 struct SlabOut {  // split-K slice z: slab[z][m][n]
-  static constexpr bool kPool = false;
+  static constexpr bool kPool = false, kPoolS1 = false;
   float* slab;
   int N, M;
   __device__ int row(int m) const { return static_cast<int>(blockIdx.z) * M * N + m * N; }
@@ -273,7 +282,7 @@ struct SlabOut {  // split-K slice z: slab[z][m][n]
 // a[b, n, w] = relu(max_t (C[m][n] + bias[n])), code[b, n, w] = first argmax t (255: not live); the
 // pre-activation is never written.
 struct PoolOut {
-  static constexpr bool kPool = true;
+  static constexpr bool kPool = true, kPoolS1 = false;
   float* a;
   unsigned char* code;
   const float* bias;
@@ -284,6 +293,28 @@ struct PoolOut {
     return b * N * phw + ((m - b * static_cast<int>(hw.d)) >> 2);
   }
 };
+
+// Fused ReLU + 2x2/s1 (overlapping) max-pool over one image per 128-row tile (FwdA<.., 2>): the tile's
+// C + bias goes to LDS and the workgroup pools the whole image from there.
+struct PoolS1Out {
+  static constexpr bool kPool = false, kPoolS1 = true;
+  float* a;
+  unsigned char* code;
+  const float* bias;
+  int N, OW, PW, phw;  // conv output width, pooled width, pooled pixels per plane
+  FastDiv fphw, fpw;
+};
+
+template <int CTL>
+__device__ __forceinline__ void pool_quad_step(float& best, int& bt) {
+  const float ov = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, best), CTL, 0xF,
+                                                                         0xF, false));
+  const int ot = __builtin_amdgcn_update_dpp(0, bt, CTL, 0xF, 0xF, false);
+  if (ov > best || (ov == best && ot < bt)) {
+    best = ov;
+    bt = ot;
+  }
+}
 
 // ---------------------------------------------------------------- the GEMM core
 // grid: x = m tiles, y = n tiles, z = k slices (each covers k_per_slice of K).  WM x WN waves, each
@@ -301,8 +332,11 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
   static_assert(KSPLIT * WM * WN == 4 && BK / 4 >= KSPLIT, "4 waves");
   constexpr int LDA = BM + 16, LDB = BN + 16;  // row stride = 16 banks mod 64: conflict-free MFMA reads
   constexpr int EA = BM * BK / TPB, EB = BN * BK / TPB;
-  __shared__ float As[2][BK][LDA];
-  __shared__ float Bs[2][BK][LDB];
+  constexpr int LDT = BM + 4;  // PoolS1Out staging row stride
+  constexpr int SM_AB = 2 * BK * (LDA + LDB), SM = (Epi::kPoolS1 && BN * LDT > SM_AB) ? BN * LDT : SM_AB;
+  __shared__ float smem[SM];
+  auto As = reinterpret_cast<float(*)[BK][LDA]>(smem);
+  auto Bs = reinterpret_cast<float(*)[BK][LDB]>(smem + 2 * BK * LDA);
   extern __shared__ int2 ktab[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -454,7 +488,37 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
 #pragma unroll
       for (int q = 0; q < TM * TN; ++q) acc[q / TN][q % TN] += red[(w * TM * TN + q) * 64 + lane];
   }
-  if constexpr (Epi::kPool) {
+  if constexpr (Epi::kPoolS1) {
+    static_assert(BM == 128, "one image per 128-row tile");
+    float* T = smem;  // [BN][LDT]; the k-loop ended with a barrier, As / Bs are dead
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int nl = wn + j * 16 + 4 * lk + r, n = n0 + nl;
+          T[nl * LDT + wm + i * 16 + lr] = acc[i][j][r] + (epi.bias && n < N ? epi.bias[n] : 0.f);
+        }
+    __syncthreads();
+    const int b = m0 >> 7;
+    for (int idx = tid; idx < BN * epi.phw; idx += TPB) {
+      const int nl = fdiv(idx, epi.fphw), q = idx - nl * epi.phw;
+      if (n0 + nl >= N) break;
+      const int py = fdiv(q, epi.fpw), px = q - py * epi.PW;
+      const float* t = T + nl * LDT + py * epi.OW + px;
+      const float v[4] = {t[0], t[1], t[epi.OW], t[epi.OW + 1]};
+      float best = v[0];
+      int bt = 0;
+#pragma unroll
+      for (int u = 1; u < 4; ++u)
+        if (v[u] > best) { best = v[u]; bt = u; }
+      const bool live = best > 0.f;
+      const int64_t o = (static_cast<int64_t>(b) * N + n0 + nl) * epi.phw + q;
+      epi.a[o] = live ? best : 0.f;
+      epi.code[o] = live ? static_cast<unsigned char>(bt) : 255;
+    }
+  } else if constexpr (Epi::kPool) {
     const int tap = lr & 3;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -468,15 +532,9 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(int M, int N, int K, int 
           // bias before the max, exactly as conv-then-pool (argmax ties included)
           float best = acc[i][j][r] + (epi.bias && n < N ? epi.bias[n] : 0.f);
           int bt = tap;
-#pragma unroll
-          for (int o = 1; o <= 2; o <<= 1) {  // first maximum in window order wins, as max_pool2d
-            const float ov = __shfl_xor(best, o, 64);
-            const int ot = __shfl_xor(bt, o, 64);
-            if (ov > best || (ov == best && ot < bt)) {
-              best = ov;
-              bt = ot;
-            }
-          }
+          // first maximum in window order wins, as max_pool2d; quad lane exchanges by DPP
+          pool_quad_step<0xB1>(best, bt);  // xor 1: quad_perm [1,0,3,2]
+          pool_quad_step<0x4E>(best, bt);  // xor 2: quad_perm [2,3,0,1]
           if (tap == 0 && m < M && n < N) {
             const bool live = best > 0.f;
             epi.a[rowoff + n * epi.phw] = live ? best : 0.f;
@@ -824,6 +882,29 @@ void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char
       FwdA<false, false, true> la{{x + b0 * xin, xbytes * 4, 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
                                   make_fdiv(g.OH * g.OW), fpw};
       launch_gemm(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    }
+  }
+}
+
+void conv_f32_fwd_pool_s1(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* a,
+                          unsigned char* code, hipStream_t s) {
+  const int K = g.C * g.R * g.R;
+  const int PH = g.OH - 1, PW = g.OW - 1, phw = PH * PW;
+  const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, aout = static_cast<int64_t>(g.Kout) * phw;
+  const int64_t chunk = batch_chunk(g.B, {xin, int64_t{128} * g.Kout});
+  for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {
+    const int nb = static_cast<int>(std::min(chunk, g.B - b0));
+    const int M = nb * 128;
+    WeightB lb{{w, K * g.Kout * 4, 0.f, 1.f}, K, g.Kout};
+    PoolS1Out epi{a + b0 * aout, code + b0 * aout, bias, g.Kout, g.OW, PW, phw, make_fdiv(phw), make_fdiv(PW)};
+    if (g.pad) {
+      FwdA<false, true, 2> la{{x + b0 * xin, static_cast<int>(nb * xin * 4), 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad,
+                              g.OW, K, M, make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
+      launch_layout<4, 1, 2, 4>(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
+    } else {
+      FwdA<false, false, 2> la{{x + b0 * xin, static_cast<int>(nb * xin * 4), 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad,
+                               g.OW, K, M, make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
+      launch_layout<4, 1, 2, 4>(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
     }
   }
 }

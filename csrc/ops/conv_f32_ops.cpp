@@ -58,17 +58,28 @@ at::Tensor f32_conv_fwd(const at::Tensor& x, const at::Tensor& w, const c10::opt
 
 std::tuple<at::Tensor, at::Tensor> f32_conv_pool_fwd(const at::Tensor& x, const at::Tensor& w,
                                                      const c10::optional<at::Tensor>& bias, int64_t pad, double mean,
-                                                     double std) {
+                                                     double std, int64_t stride) {
   check_input(x);
   util::f32_gpu(w, "conv_f32 weight");
   auto g = geom(x, w, pad);
-  RINGDP_CHECK(g.OH % 2 == 0 && g.OW % 2 == 0, "conv_f32 + pool: the conv output must have even height and width");
+  RINGDP_CHECK(stride == 1 || (g.OH % 2 == 0 && g.OW % 2 == 0),
+               "conv_f32 + 2x2/s2 pool: the conv output must have even height and width");
   const float* b = nullptr;
   if (bias && bias->defined()) {
     util::f32_gpu(*bias, "conv_f32 bias");
     RINGDP_CHECK(bias->numel() == g.Kout, "conv_f32 bias: wrong size");
     b = bias->data_ptr<float>();
   }
+  if (stride == 1) {
+    RINGDP_CHECK(x.scalar_type() == at::kFloat && g.OH * g.OW <= 128,
+                 "conv_f32 + 2x2/s1 pool: fp32 input and at most 128 output pixels per image");
+    auto a = at::empty({g.B, g.Kout, g.OH - 1, g.OW - 1}, w.options());
+    auto code = at::empty({g.B, g.Kout, g.OH - 1, g.OW - 1}, w.options().dtype(at::kByte));
+    kern::conv_f32_fwd_pool_s1(g, x.data_ptr<float>(), w.data_ptr<float>(), b, a.data_ptr<float>(),
+                               code.data_ptr<uint8_t>(), util::stream_of(w));
+    return {a, code};
+  }
+  RINGDP_CHECK(stride == 2, "conv_f32 + pool: 2x2 windows with stride 1 or 2");
   auto a = at::empty({g.B, g.Kout, g.OH / 2, g.OW / 2}, w.options());
   auto code = at::empty({g.B, g.Kout, g.OH / 2, g.OW / 2}, w.options().dtype(at::kByte));
   const bool u8 = x.scalar_type() == at::kByte;

@@ -99,7 +99,7 @@ at::Tensor f32_conv_fwd(const at::Tensor& x, const at::Tensor& w, const c10::opt
                         int64_t pad, double mean, double std);
 std::tuple<at::Tensor, at::Tensor> f32_conv_pool_fwd(const at::Tensor& x, const at::Tensor& w,
                                                      const c10::optional<at::Tensor>& bias, int64_t pad, double mean,
-                                                     double std);
+                                                     double std, int64_t stride);
 std::tuple<at::Tensor, at::Tensor> f32_conv1_pool_fwd(const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1,
                                                       double mean, double std);
 void f32_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& code1, double mean, double std,

@@ -3,8 +3,9 @@
 Layer-by-layer autograd Functions over the exact-f32 MFMA kernels of csrc/kernels/conv_f32.hip:
 conv (implicit GEMM; fc1 runs as a 1x1 conv over the flattened 2048-vector), and ReLU fused into
 max-pool with a 1-byte argmax code (backward is a gather, deterministic also for the overlapping
-2x2/s1 pool2).  conv1 and conv3 run ReLU + their 2x2/s2 pool inside the conv launch (window-major
-output pixels, the pre-activation never reaches memory).  ToTensor+Normalize of uint8 pixels is fused into conv1's operand loads.  Weight and
+2x2/s1 pool2).  Every conv runs ReLU + its pool inside the conv launch (conv1: a dedicated one-wave-
+per-image kernel; conv2: one image per tile, pooled from LDS; conv3: window-major output pixels), so
+no pre-activation reaches memory.  ToTensor+Normalize of uint8 pixels is fused into conv1's operand loads.  Weight and
 bias gradients come out of one split-K GEMM (bias = an extra column of ones) and land directly in
 the DDP bucket slots (``grad_buffer``).  ``ConvNet(precision="bf16")`` (ringdp/ops/convnet.py) is
 the fused bf16 fast path; this module is what ``ConvNet(precision="fp32")`` and
@@ -57,11 +58,11 @@ class _ConvPoolF32(torch.autograd.Function):
     written); backward = the pool gather into dz, then the conv's data / weight gradients."""
 
     @staticmethod
-    def forward(ctx, x, w, b, pad, mean, std):
-        a, code = C.f32_conv_pool_fwd(x, w, b, pad, mean, std)
+    def forward(ctx, x, w, b, pad, mean, std, stride=2):
+        a, code = C.f32_conv_pool_fwd(x, w, b, pad, mean, std, stride)
         ctx.save_for_backward(x, code)
         ctx.params = (w, b)
-        ctx.cfg = (pad, mean, std)
+        ctx.cfg = (pad, mean, std, stride)
         ctx.mark_non_differentiable(code)
         return a
 
@@ -69,15 +70,15 @@ class _ConvPoolF32(torch.autograd.Function):
     def backward(ctx, da):
         x, code = ctx.saved_tensors
         w, b = ctx.params
-        pad, mean, std = ctx.cfg
-        OH, OW = 2 * code.shape[2], 2 * code.shape[3]
-        dz = C.f32_pool_relu_bwd(da.contiguous(), code, OH, OW, 2, 2)
+        pad, mean, std, stride = ctx.cfg
+        OH, OW = stride * (code.shape[2] - 1) + 2, stride * (code.shape[3] - 1) + 2
+        dz = C.f32_pool_relu_bwd(da.contiguous(), code, OH, OW, 2, stride)
         dx = C.f32_conv_dgrad(dz, w, x.shape[2], x.shape[3], pad) if ctx.needs_input_grad[0] else None
         dw = grad_buffer(w)
         db = grad_buffer(b) if b is not None else None
         C.f32_conv_wgrad(dz, x, pad, mean, std, dw, db)
         return (dx, dw if ctx.needs_input_grad[1] else None,
-                db if (b is not None and ctx.needs_input_grad[2]) else None, None, None, None)
+                db if (b is not None and ctx.needs_input_grad[2]) else None, None, None, None, None)
 
 
 class _Conv1PoolF32(torch.autograd.Function):
@@ -132,6 +133,6 @@ def convnet_forward_fp32(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Ten
         a = _Conv1PoolF32.apply(x, conv1.weight, conv1.bias, mean, std)
     else:
         a = _ConvPoolF32.apply(x, conv1.weight, conv1.bias, 1, mean, std)
-    a = _PoolReLUF32.apply(_ConvF32.apply(a, conv2.weight, conv2.bias, 0, 0.0, 1.0), 2, 1)
+    a = _ConvPoolF32.apply(a, conv2.weight, conv2.bias, 0, 0.0, 1.0, 1)
     a = _ConvPoolF32.apply(a, conv3.weight, conv3.bias, 0, 0.0, 1.0)
     return _ConvF32.apply(a.reshape(a.shape[0], -1), fc1.weight, fc1.bias, 0, 0.0, 1.0)

@@ -84,9 +84,10 @@ def test_conv_f32_batch_chunks(monkeypatch):
     assert torch.equal(a, F.max_pool2d(F.relu(z), 2, 1))
 
 
-@pytest.mark.parametrize("B,Cin,H,K,R,pad,u8", [(5, 1, 28, 32, 5, 1, True), (9, 64, 10, 128, 3, 0, False),
-                                                (3, 3, 8, 8, 3, 1, False)])
-def test_conv_f32_pool_fused(B, Cin, H, K, R, pad, u8):
+@pytest.mark.parametrize("B,Cin,H,K,R,pad,u8,st", [(5, 1, 28, 32, 5, 1, True, 2), (9, 64, 10, 128, 3, 0, False, 2),
+                                                   (3, 3, 8, 8, 3, 1, False, 2), (7, 32, 13, 64, 3, 0, False, 1),
+                                                   (4, 5, 9, 80, 3, 1, False, 1)])
+def test_conv_f32_pool_fused(B, Cin, H, K, R, pad, u8, st):
     """conv + bias + ReLU + 2x2/s2 max-pool in one launch == conv kernel then the pool kernel (bit-exact:
     same products in the same order), and == ATen."""
     g = torch.Generator(device=DEV).manual_seed(B * 7 + K)
@@ -100,12 +101,12 @@ def test_conv_f32_pool_fused(B, Cin, H, K, R, pad, u8):
         xf = x
     w = torch.randn(K, Cin, R, R, device=DEV, generator=g) * 0.2
     b = torch.randn(K, device=DEV, generator=g) * 0.1
-    a, code = C.f32_conv_pool_fwd(x, w, b, pad, mean, std)
+    a, code = C.f32_conv_pool_fwd(x, w, b, pad, mean, std, st)
     z = C.f32_conv_fwd(x, w, b, pad, mean, std)
-    a2, code2 = C.f32_pool_relu_fwd(z, 2, 2)
+    a2, code2 = C.f32_pool_relu_fwd(z, 2, st)
     assert torch.equal(a, a2)
     assert torch.equal(code, code2)
-    ref = F.max_pool2d(F.relu(F.conv2d(xf.double(), w.double(), b.double(), padding=pad)), 2, 2).float()
+    ref = F.max_pool2d(F.relu(F.conv2d(xf.double(), w.double(), b.double(), padding=pad)), 2, st).float()
     _close(a, ref, rtol=1e-5, atol=1e-5)
 
 
