@@ -924,6 +924,17 @@ static int bf16_tile_mode() {
   return g_bf16_tile;
 }
 void set_bf16_tile_mode(int mode) { g_bf16_tile = mode; }
+// Minimum round fill for the 256x256 kernel (RINGDP_BF16_256_FILL).  ViT-B/16's N = 768 GEMMs (297 tiles:
+// 2 rounds at 58 %) measured faster there than on the 128 core in 4 of 5 shapes (-1.5 % step,
+// profiles/r03/gemm_routing.md).
+static double bf16_256_fill() {
+  static double f = -1.0;
+  if (f < 0) {
+    const char* v = getenv("RINGDP_BF16_256_FILL");
+    f = v ? atof(v) : 0.55;
+  }
+  return f;
+}
 static bool bf16_use_256(int M, int N, int K, int batch, int splits) {
   const int mode = bf16_tile_mode();
   if (mode == 128) return false;
@@ -931,7 +942,7 @@ static bool bf16_use_256(int M, int N, int K, int batch, int splits) {
   const int64_t tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch * std::max(1, splits);
   const int64_t rounds = (tiles + 255) / 256;
   const double fill = rounds > 0 ? (double)tiles / (256.0 * rounds) : 0.0;
-  return tiles >= 192 && fill >= 0.75 && K / std::max(1, splits) >= 512;
+  return tiles >= 192 && fill >= bf16_256_fill() && K / std::max(1, splits) >= 512;
 }
 
 // Split count that fills whole rounds of the 256 CUs with 256x256 tiles (>= 4 k-tiles per split), for
