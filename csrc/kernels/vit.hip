@@ -735,27 +735,32 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k,
     bf16x4 pv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) pv[t] = *reinterpret_cast<const bf16x4*>(prow + 16 * t);
-    f32x4 dpt[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
+    // dP = dO V^T tile by tile, recomputed in the second pass instead of held: the NT x 4 fp32 dP
+    // registers had pushed the kernel to 232 VGPRs (one wave per SIMD)
+    auto dp_tile = [&](int t) {
       const int vr = 16 * t + qi;
       const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Vs + att_ksw(vr, 8 * g));
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Vs + att_ksw(vr, 32 + 8 * g));
-      dpt[t] = mfma16x16x32(a1, of1, mfma16x16x32(a0, of0, zero_f32x4()));
-    }
+      return mfma16x16x32(a1, of1, mfma16x16x32(a0, of0, zero_f32x4()));
+    };
     float dot = 0.f;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 dpt = dp_tile(t);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dot = fmaf(dpt[t][i], (float)pv[t][i], dot);
+      for (int i = 0; i < 4; ++i) dot = fmaf(dpt[i], (float)pv[t][i], dot);
+    }
     dot += __shfl_xor(dot, 16, 64);
     dot += __shfl_xor(dot, 32, 64);
     if (g == 0) dsum[(int64_t)bh * Tp + qrow] = dot;
-    bf16x4 dsb[NT];
+    asm volatile("" ::: "memory");  // pass 2 re-reads V from LDS: no CSE of the pass-1 dP registers
+    auto ds_tile = [&](int t) {
+      const f32x4 dpt = dp_tile(t);
+      bf16x4 r;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) dsb[t][i] = (bf16)(scale * (float)pv[t][i] * (dpt[t][i] - dot));
+      for (int i = 0; i < 4; ++i) r[i] = (bf16)(scale * (float)pv[t][i] * (dpt[i] - dot));
+      return r;
+    };
     // dQ^T[d][q] = sum over key pairs (t0, t1) of K^T (keys 16t + 4g + j) x dS^T
     f32x4 qt4[4];
 #pragma unroll
@@ -763,8 +768,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k,
 #pragma unroll
     for (int ks = 0; ks < (NT + 1) / 2; ++ks) {
       const int t0 = 2 * ks, t1 = 2 * ks + 1 < NT ? 2 * ks + 1 : t0;
-      const bf16x4 d1 = 2 * ks + 1 < NT ? dsb[2 * ks + 1] : bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
-      const bf16x8 bfr = bf16x8{dsb[t0][0], dsb[t0][1], dsb[t0][2], dsb[t0][3], d1[0], d1[1], d1[2], d1[3]};
+      const bf16x4 d0 = ds_tile(t0);
+      const bf16x4 d1 = 2 * ks + 1 < NT ? ds_tile(2 * ks + 1) : bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      const bf16x8 bfr = bf16x8{d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const bf16x4 lo = lds_read_tr16(Ks + att_vsw(16 * t0 + 4 * g + q4, 16 * dt + 4 * p4));
