@@ -119,6 +119,10 @@ void RcclPG::shutdown() {
     if (!aborted_.load()) ncclCommDestroy(comm_);
     comm_ = nullptr;
   }
+  if (xg_) {
+    if (aborted_.load() || xg_->failed()) xg_->mark_unsafe();
+    else (void)xg_->quiesce(std::min<int64_t>(timeout_.count(), 60000));
+  }
   xg_.reset();
 }
 

@@ -8,6 +8,9 @@
 #include <fstream>
 #include <unistd.h>
 
+#include <chrono>
+#include <thread>
+
 #include "../common.h"
 
 namespace ringdp {
@@ -141,8 +144,9 @@ std::unique_ptr<XgmiEngine> XgmiEngine::create(const std::shared_ptr<Store>& sto
   hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_err), p->error_, 0);
   a.epochs = p->epochs_;
   a.error = dev_err;
-  // the kernels' own spin bound: the group timeout, capped so a dead peer ends a kernel in minutes
-  a.timeout_ticks = static_cast<uint64_t>(std::min<int64_t>(std::max<int64_t>(timeout_ms, 1), 300000)) * 100000ull;
+  // the kernels' own spin bound is the group timeout itself (s_memrealtime: 100 MHz ticks), uncapped,
+  // so a slow but healthy peer (evaluation, checkpointing) gets the same grace as under c10d
+  a.timeout_ticks = static_cast<uint64_t>(std::max<int64_t>(timeout_ms, 1)) * 100000ull;
   a.world = world;
   a.rank = rank;
   a.nblocks = G;
@@ -152,7 +156,29 @@ std::unique_ptr<XgmiEngine> XgmiEngine::create(const std::shared_ptr<Store>& sto
   a.off_b = off_b;
   a.off_p2p = off_p2p;
   a.scale = 1.0f / static_cast<float>(world);
+  p->store_ = store;
   return p;
+}
+
+bool XgmiEngine::quiesce(int64_t timeout_ms) {
+  if (quiesced_) return !leak_exported_;
+  quiesced_ = true;
+  if (world_ == 1) return true;
+  try {
+    store_->add("xgmi/fin", 1);
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(std::max<int64_t>(timeout_ms, 1));
+    while (store_->add("xgmi/fin", 0) < world_) {
+      if (std::chrono::steady_clock::now() > deadline) {
+        leak_exported_ = true;
+        return false;
+      }
+      std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    return true;
+  } catch (const std::exception&) {
+    leak_exported_ = true;
+    return false;
+  }
 }
 
 XgmiEngine::~XgmiEngine() {
@@ -160,8 +186,10 @@ XgmiEngine::~XgmiEngine() {
   hipGetDevice(&prev);
   hipSetDevice(device_);
   for (void* q : opened_) hipIpcCloseMemHandle(q);
-  if (stage_) hipFree(stage_);
-  if (flags_) hipFree(flags_);
+  // memory that peers map: freed only after a group-wide quiesce (a peer kernel could still push)
+  const bool free_exported = world_ == 1 || (quiesced_ && !leak_exported_);
+  if (stage_ && free_exported) hipFree(stage_);
+  if (flags_ && free_exported) hipFree(flags_);
   if (epochs_) hipFree(epochs_);
   if (error_) hipHostFree(error_);
   hipSetDevice(prev);

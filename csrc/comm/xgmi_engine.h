@@ -63,6 +63,15 @@ class XgmiEngine {
   // Host-side check of the kernels' timeout word (true: some peer did not arrive in time).
   bool failed() const;
 
+  // Group-wide quiesce before teardown: every rank has drained its streams and arrived through the
+  // store, so no peer kernel can still be writing into this rank's exported staging / flag memory.
+  // Call it (collectively) before destroying the engine of a healthy group.  On failure (a peer never
+  // arrives within `timeout_ms`, or the store is gone) the exported buffers are leaked rather than
+  // freed under a possibly live writer.
+  bool quiesce(int64_t timeout_ms);
+  // Aborted groups skip the quiesce: peers are dead or desynchronised; leak the exported memory.
+  void mark_unsafe() { leak_exported_ = true; }
+
  private:
   XgmiEngine() = default;
   void launch(kern::XgArgs& a, hipStream_t s);
@@ -75,6 +84,8 @@ class XgmiEngine {
   int* error_ = nullptr;  // hipHostMalloc'd, mapped
   std::vector<void*> opened_;
   kern::XgArgs base_{};
+  std::shared_ptr<Store> store_;
+  bool quiesced_ = false, leak_exported_ = false;
 };
 
 }  // namespace ringdp

@@ -62,6 +62,11 @@ void XgmiPG::shutdown() {
   stop_common();
   DeviceScope ds(device_);
   if (!aborted_.load()) (void)hipStreamSynchronize(send_stream_.stream());
+  if (eng_) {
+    // every rank's streams are drained: meet through the store before freeing memory peers map
+    if (aborted_.load() || eng_->failed()) eng_->mark_unsafe();
+    else (void)eng_->quiesce(std::min<int64_t>(timeout_.count(), 60000));
+  }
   eng_.reset();
   if (send_fence_) hipEventDestroy(send_fence_);
   if (send_done_) hipEventDestroy(send_done_);
@@ -271,14 +276,16 @@ std::shared_ptr<Work> XgmiPG::scatter(at::Tensor& output, std::vector<at::Tensor
   return launch(OpType::SCATTER, all, [&](hipStream_t s) {
     const int64_t M = output.numel() * static_cast<int64_t>(output.element_size());
     if (rank_ == root) {
+      std::vector<at::Tensor> keep;
       for (int r = 0; r < size_; ++r) {
         if (r == root) continue;
         at::Tensor tin = scratch(round16(M));
         d2d(tin.data_ptr(), inputs[r].data_ptr(), M, s);
         eng_->send(tin.data_ptr(), M, r, send_on(s));
-        join_sends(s);  // the scratch copy lives on s: keep it until the send has read it
+        keep.push_back(tin);
       }
       d2d(output.data_ptr(), inputs[root].data_ptr(), M, s);
+      join_sends(s);  // the scratch copies live on s: keep them until the sends have read them
     } else {
       at::Tensor tout = scratch(round16(M));
       eng_->recv(tout.data_ptr(), M, root, s);
@@ -335,14 +342,18 @@ std::shared_ptr<Work> XgmiPG::send(at::Tensor& tensor, int dst, int /*tag*/) {
       eng_->send(tensor.data_ptr(), nb, dst, s);
       return s;
     }
+    hipStream_t ss = send_on(s);
     if (aligned16(tensor.data_ptr())) {
-      eng_->send(tensor.data_ptr(), nb, dst, send_on(s));
+      eng_->send(tensor.data_ptr(), nb, dst, ss);
     } else {
+      // stage through an aligned copy made ON the send stream, so the comm stream never waits for a
+      // send (a send blocks until its receiver drains the P2P slots; a comm stream held behind it would
+      // keep this rank's own recv from running: two ranks exchanging > 2 slots would deadlock)
       at::Tensor tin = scratch(round16(nb));
-      d2d(tin.data_ptr(), tensor.data_ptr(), nb, s);
-      eng_->send(tin.data_ptr(), nb, dst, send_on(s));
-      join_sends(s);  // the scratch copy lives on s
-      return s;
+      d2d(tin.data_ptr(), tensor.data_ptr(), nb, ss);
+      eng_->send(tin.data_ptr(), nb, dst, ss);
+      c10::hip::HIPCachingAllocatorMasqueradingAsCUDA::recordStreamMasqueradingAsCUDA(tin.storage().data_ptr(),
+                                                                                      send_stream_);
     }
     // the op completes on the send stream; the tensor is kept alive by the Work, and the caching
     // allocator learns about the second stream here

@@ -136,6 +136,8 @@ class ProcessGroup:
         self._gpu: Dict[int, Any] = {}  # device -> native GPU process group (RcclPG / XgmiPG)
         self._lock = threading.Lock()
         self._coll_count = 0
+        self.requested_backend: Optional[str] = None  # the user's backend string (get_backend)
+        self._kind_agreed = False
 
     # -- introspection
     def rank(self) -> int:
@@ -182,6 +184,7 @@ class ProcessGroup:
                     kind = "rccl"
                 if not torch.cuda.is_available():
                     raise RuntimeError(f"ringdp: the {kind} backend needs a GPU (torch.cuda.is_available() is False)")
+                self._agree_gpu_kind(kind)
                 sub = C.PrefixStore(f"{self.group_name}/{kind}/{device}", self._store)
                 cls = C.RcclPG if kind == "rccl" else C.XgmiPG
                 pg = cls(sub, self._rank, self._size, device, self.timeout_ms)
@@ -189,6 +192,19 @@ class ProcessGroup:
             return pg
 
     rccl = gpu  # older name
+
+    def _agree_gpu_kind(self, kind: str) -> None:
+        """Every member publishes the GPU backend it resolved (RINGDP_GPU_BACKEND is read per
+        process); a mismatch raises here instead of leaving ranks waiting on different store keys."""
+        if self._kind_agreed or self._size == 1:
+            return
+        self._store.set(f"{self.group_name}/gpukind/{self._rank}", kind)
+        kinds = {r: self._store.get(f"{self.group_name}/gpukind/{r}").decode() for r in range(self._size)}
+        if len(set(kinds.values())) != 1:
+            raise RuntimeError(
+                f"ringdp: ranks of group {self.group_name} resolved different GPU backends {kinds} "
+                "(set RINGDP_GPU_BACKEND identically on every rank)")
+        self._kind_agreed = True
 
     def native_for(self, tensor: torch.Tensor):
         """(native process group, staged-through-host?) for a tensor."""
@@ -389,6 +405,7 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     root = C.PrefixStore("ringdp", store)
     name = group_name or "default_pg"
     pg = ProcessGroup(root, rank, world_size, backends, timeout, list(range(world_size)), name, bind_hint)
+    pg.requested_backend = backend if isinstance(backend, str) else None
     _world.default_pg = pg
     _world.groups = {name: pg}
     _world.group_count = 0
@@ -450,6 +467,9 @@ def get_world_size(group: Optional[ProcessGroup] = None) -> int:
 
 def get_backend(group: Optional[ProcessGroup] = None) -> str:
     g = _resolve(group)
+    req = g.requested_backend
+    if isinstance(req, str) and req and Backend.normalize(req) == g._backends:
+        return req.lower()  # upstream returns the name the user asked for ("nccl", even when xgmi serves it)
     kinds = set(g._backends.values())
     if kinds == {"rccl"}:
         return "nccl"
@@ -499,6 +519,7 @@ def new_group(ranks: Optional[Sequence[int]] = None, timeout: Optional[_dt.timed
         return GroupMember.NON_GROUP_MEMBER
     pg = ProcessGroup(_world.store, ranks.index(me), len(ranks), backends, timeout or world._timeout,
                       ranks, name, _world.bind_hint)
+    pg.requested_backend = backend if isinstance(backend, str) else world.requested_backend
     for dev, child in split.items():
         if child is not None:
             pg._gpu[dev] = child

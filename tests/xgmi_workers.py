@@ -130,6 +130,19 @@ def exact_worker(rank, world, port, result_dir):
             w2.wait(True)
             assert torch.all(buf == prv), n
             checks += 1
+        # unaligned (t[1:] views) messages larger than two P2P slots, two sends posted before their
+        # recvs: the scratch staging of an unaligned send must not hold the comm stream
+        n = 3 * (1 << 20) // 4
+        srcs = [torch.arange(n + 1, device="cuda", dtype=torch.float32) + 1000.0 * rank + 0.5 * j for j in range(2)]
+        dsts = [torch.zeros(n + 1, device="cuda") for _ in range(2)]
+        ws = [pg.send(srcs[j][1:], nxt, 0) for j in range(2)]
+        ws += [pg.recv(dsts[j][1:], prv, 0) for j in range(2)]
+        for w in ws:
+            w.wait(True)
+        for j in range(2):
+            exp = torch.arange(n + 1, dtype=torch.float32)[1:] + 1000.0 * prv + 0.5 * j
+            assert torch.equal(dsts[j][1:].cpu(), exp), j
+            checks += 1
     # hipGraph: capture once (one-shot + two-shot), replay with fresh inputs copied into the captured tensors
     small = torch.zeros(94352 // 8, device="cuda")  # one-shot
     big = torch.zeros(300000, device="cuda")         # two-shot
