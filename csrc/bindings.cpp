@@ -574,6 +574,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);
   m.def("cn_conv3_fc_fwd", &ops::cn_conv3_fc_fwd);
   m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd);
+  m.def("cn_set_variant", [](const std::string& name, int value) {
+    RINGDP_CHECK(kern::cn_set_variant(name.c_str(), value), "cn_set_variant: unknown variant ", name, "=", value);
+  });
+  m.def("cn_get_variant", [](const std::string& name) { return kern::cn_get_variant(name.c_str()); });
+  m.def("cn_debug_stamps", []() {
+    at::Tensor t = at::zeros({4, 16, 16}, at::TensorOptions().dtype(at::kLong));
+    return kern::cn_debug_stamps(t.data_ptr()) ? t : at::Tensor();
+  });
   m.def("cn_conv2_bwd", &ops::cn_conv2_bwd);
   m.def("cn_conv1_wgrad", &ops::cn_conv1_wgrad);
   m.def("cn_conv12_bwd", &ops::cn_conv12_bwd);

@@ -168,6 +168,10 @@ void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2,
 void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s);
 
+// Run-time kernel variant knobs (A/B tests): returns false for an unknown name / value.
+bool cn_set_variant(const char* name, int value);
+int cn_get_variant(const char* name);
+bool cn_debug_stamps(void* host_out);  // 4*16*16 u64; false unless built with -DRINGDP_C3V_STAMP
 // Workspace sizes (floats) of the backward weight-gradient slabs.
 int64_t cn_fc_slab_floats(int B, bool dgrad);
 int64_t cn_conv3_slab_floats(int B, bool dgrad);

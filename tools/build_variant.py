@@ -12,7 +12,7 @@ spec.loader.exec_module(b)
 
 name, src, defs = sys.argv[1], (ROOT / sys.argv[2]).resolve(), sys.argv[3:]
 b.build(verbose=False)
-out_dir = ROOT / "variants"
+out_dir = ROOT / __import__("os").environ.get("RINGDP_VARIANT_DIR", "variants")
 out_dir.mkdir(exist_ok=True)
 obj = out_dir / f"{name}.{src.stem}.o"
 cmd = b._compile_cmd(src, obj)

@@ -12,10 +12,7 @@ import ringdp  # noqa: E402
 C = ringdp._C
 
 
-def main():
-    op = sys.argv[1]
-    B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
-    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+def build_ops(B):
     dev = torch.device("cuda")
     torch.manual_seed(0)
     x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device=dev)
@@ -49,6 +46,14 @@ def main():
         "conv1_wgrad": lambda: C.cn_conv1_wgrad(x, da1, i1, *g1, *norm),
         "conv12_bwd": lambda: C.cn_conv12_bwd(x, i1, a1, dz2, pk, *g2, *g1, *norm),
     }
+    return fns
+
+
+def main():
+    op = sys.argv[1]
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
+    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    fns = build_ops(B)
     for _ in range(iters):
         fns[op]()
     torch.cuda.synchronize()
