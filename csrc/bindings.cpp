@@ -573,7 +573,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cn_conv1_fwd_pack", &ops::cn_conv1_fwd_pack);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);
   m.def("cn_conv3_fc_fwd", &ops::cn_conv3_fc_fwd);
-  m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd);
+  m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd, py::arg("a2"), py::arg("idx2"), py::arg("a3"), py::arg("idx3"),
+        py::arg("wfc"), py::arg("dlogits"), py::arg("packed"), py::arg("need_dz2"), py::arg("dw3"), py::arg("db3"),
+        py::arg("dwfc"), py::arg("dbfc"), py::arg("defer_reduce") = false);
+  m.def("cn_conv3_fc_ce_bwd", &ops::cn_conv3_fc_ce_bwd);
+  m.def("cn_flush_reduce", &ops::cn_flush_reduce);
+  m.def("cn_reduce_pending", &ops::cn_reduce_pending);
+  m.def("cn_merged_reductions", &ops::cn_merged_reductions);
   m.def("cn_set_variant", [](const std::string& name, int value) {
     RINGDP_CHECK(kern::cn_set_variant(name.c_str(), value), "cn_set_variant: unknown variant ", name, "=", value);
   });

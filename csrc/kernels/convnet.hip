@@ -709,11 +709,15 @@ __host__ __device__ inline int fc_imgs(int B) { return B <= 1024 ? 4 : (B >= 655
 constexpr int FC_SLAB = 10 * 2048 + 10 + 128;  // dWfc + dbfc + db3 (the conv3 bias gradient is the sum of
                                                 // d(a3) over windows: no MFMA tile needed for it)
 
+// kCE: the logits gradient is formed here from the cross-entropy forward's logits / log-sum-exp
+// (same expression as ce_bwd_kernel, elementwise.hip) - 80 threads per group of 8 images into LDS -
+// instead of read from a [B,10] tensor: the separate ce_bwd launch disappears.
+template <bool kCE>
 __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3,
                                                      const bf16* __restrict__ packed,
                                                      const float* __restrict__ dl,
                                                      bf16* __restrict__ da3m, float* __restrict__ slabs,
-                                                     int B, int imgs) {
+                                                     int B, int imgs, CeFuse ce) {
   const int t = threadIdx.x;
   const int wd = t >> 4, co0 = (t & 15) * 8;  // this thread's 8 activations: window wd, channels co0..
   float wr[8][10];
@@ -736,7 +740,28 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
 #pragma unroll
   for (int j = 0; j < 8; ++j) dsum[j] = 0.f;
   const int b0 = blockIdx.x * imgs, nimg = min(imgs, B - b0);
+  __shared__ float gl[8][10];
+  float ce_scale = 0.f;
+  if constexpr (kCE) ce_scale = ce.reduction == 0 ? 1.f : ce.grad_out[0] / ce.denom[0];
   for (int k0 = 0; k0 < nimg; k0 += 8) {
+    if constexpr (kCE) {
+      if (k0) __syncthreads();  // the previous group's reads of gl are done
+      if (t < 80) {
+        const int k = t / 10, n = t - 10 * k;
+        float g = 0.f;
+        if (k0 + k < nimg) {
+          const int b = b0 + k0 + k;
+          const int64_t y = ce.labels[b];
+          if (y != ce.ignore_index) {
+            const float p = __expf(ce.logits[(int64_t)b * 10 + n] - ce.lse[b]);
+            const float q = (n == y ? (1.f - ce.eps) : 0.f) + ce.eps / 10.f;
+            g = (p - q) * (ce.reduction == 0 ? ce.grad_out[b] : ce_scale);
+          }
+        }
+        gl[k][n] = g;
+      }
+      __syncthreads();
+    }
     bf16x8 av[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -747,7 +772,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
         const int b = b0 + k0 + k;
         float g[10];
 #pragma unroll
-        for (int n = 0; n < 10; ++n) g[n] = dl[(int64_t)b * 10 + n];
+        for (int n = 0; n < 10; ++n) g[n] = kCE ? gl[k][n] : dl[(int64_t)b * 10 + n];
         bf16x8 v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -763,7 +788,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
           v[j] = (bf16)m;
         }
         *reinterpret_cast<bf16x8*>(da3m + (int64_t)b * 2048 + wd * 128 + co0) = v;
-        if (t < 10) bacc += dl[(int64_t)b * 10 + t];
+        if (t < 10) bacc += kCE ? gl[k][t] : dl[(int64_t)b * 10 + t];
       }
     }
   }
@@ -2025,20 +2050,10 @@ __global__ __launch_bounds__(512) void conv12_bwd_kernel(const void* __restrict_
 }
 
 // ================================================================== fixed-order slab reductions
-struct ReduceSeg {
-  const float* slabs;
-  int64_t stride;  // floats between consecutive slices
-  int64_t off;     // first float of this segment inside a slice
-  int64_t n;       // outputs
-  int nslices;
-  float* out;
-  int mode;  // 0: out[i] = sum; 1: conv transpose dWt[n = tap*cin + ci][co] -> W[co][ci][tap];
-             // 2: fc1 slab in fc_bwd thread order (n*8 + j)*256 + t -> dWfc[n][co*16 + w]
-  int cin, cout;
-  int blocks;
-};
+// ReduceSeg: kernels.h
+constexpr int kMaxRedSegs = 8;
 struct ReduceSegs {
-  ReduceSeg seg[4];
+  ReduceSeg seg[kMaxRedSegs];
   int count;
 };
 
@@ -2091,6 +2106,12 @@ ReduceSeg seg(const float* slabs, int64_t stride, int64_t off, int64_t n, int ns
 }
 
 void launch_reduce(const std::vector<ReduceSeg>& v, hipStream_t s) {
+  if (v.empty()) return;
+  if (v.size() > (size_t)kMaxRedSegs) {  // more than one launch holds: split
+    launch_reduce(std::vector<ReduceSeg>(v.begin(), v.begin() + kMaxRedSegs), s);
+    launch_reduce(std::vector<ReduceSeg>(v.begin() + kMaxRedSegs, v.end()), s);
+    return;
+  }
   ReduceSegs segs{};
   int total = 0;
   segs.count = (int)v.size();
@@ -2198,6 +2219,13 @@ static double split_frac(const char* env, double dflt) {
   return f > 0.05 && f < 0.95 ? f : dflt;
 }
 
+// fewest images per weight-gradient slab (small batches: more slabs = more reduction traffic)
+static int min_slab_images(const char* env, int dflt) {
+  const char* v = getenv(env);
+  const int n = v ? atoi(v) : dflt;
+  return n >= 1 && n <= 64 ? n : dflt;
+}
+
 // dgrad and wgrad do the same MFMA work per image since the scatter-form dgrad (576 each per
 // workgroup image / image pair); measured best split 0.5-0.6 of the workgroup slots (B=32768).
 static void c3_split(int B, bool dgrad, int& nd, int& ws) {
@@ -2209,9 +2237,10 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
     return;
   }
   static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.5);
+  static const int wmin = min_slab_images("RINGDP_C3_WMIN", 2);
   nd = clampi(B, 1, (int)(frac * slots));
   const int per = cdiv(B, nd);
-  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, (slots - nd) / 2));  // >= 2 images per slab
+  ws = clampi(cdiv(B, std::max(per, wmin)), 1, std::max(1, (slots - nd) / 2));  // >= wmin images per slab
 }
 
 // Images [0, result) of the conv3 data gradient run on the dgrad workgroups, the rest on the wgrad
@@ -2245,9 +2274,10 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
 static void c12_split(int B, int& nd, int& ws) {
   const int cus = num_cus();
   static const double frac = split_frac("RINGDP_C12_DGRAD_FRAC", 0.64);
+  static const int wmin = min_slab_images("RINGDP_C12_WMIN", 2);
   nd = clampi(B, 1, (int)(frac * cus));
   const int per = cdiv(B, nd);
-  ws = clampi(cdiv(B, std::max(per, 2)), 1, std::max(1, cus - nd));
+  ws = clampi(cdiv(B, std::max(per, wmin)), 1, std::max(1, cus - nd));
 }
 
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 3 * num_cus()); }
@@ -2300,13 +2330,18 @@ int64_t cn_conv1_slab_floats(int B) { return (int64_t)conv1_wslices(B) * C1_WSLA
 
 void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const uint8_t* idx3, const float* wfc,
                      const float* dl, const void* packed, void* da3m, void* dz2, int B, float* fc_slabs,
-                     float* c3_slabs, float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s) {
+                     float* c3_slabs, float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s,
+                     const CeFuse* ce, ReduceList* defer) {
   (void)wfc;  // the data gradient uses the packed bf16 copy, like every other dgrad
   int nd, ws;
   c3_split(B, dz2 != nullptr, nd, ws);
   const int fs = cdiv(B, fc_imgs(B));
-  fc_bwd_kernel<<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
-                                   static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B));
+  if (ce)
+    fc_bwd_kernel<true><<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), nullptr,
+                                           static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), *ce);
+  else
+    fc_bwd_kernel<false><<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
+                                            static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), CeFuse{});
   if (c3_bwd_version() == 1)
     conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
                                                idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
@@ -2315,11 +2350,16 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
     conv3_bwd2_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
                                                 idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
                                                 c3_slabs, ws, nd, c3_dgrad_images(B, nd));
-  launch_reduce({seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
-                 seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
-                 seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)},
-                s);
+  ReduceList r{seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
+               seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
+               seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)};
+  if (defer)
+    defer->insert(defer->end(), r.begin(), r.end());
+  else
+    launch_reduce(r, s);
 }
+
+void cn_launch_reduce(const ReduceList& segs, hipStream_t s) { launch_reduce(segs, s); }
 
 void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1, int B, float* slabs,
                   float* dw2, float* db2, hipStream_t s) {
@@ -2334,7 +2374,7 @@ void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1
 
 void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, const void* dz2,
                    const void* packed, int B, float mean, float inv_std, float in_scale, float* slabs, float* dw2,
-                   float* db2, float* dw1, float* db1, hipStream_t s) {
+                   float* db2, float* dw1, float* db1, hipStream_t s, const ReduceList* extra) {
   int nd, ws;
   c12_split(B, nd, ws);
   float* slabs2 = slabs;
@@ -2348,9 +2388,12 @@ void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, 
   else
     conv12_bwd_kernel<false><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
                                                      slabs1, nd);
-  launch_reduce({seg(slabs2, C2_WSLAB, 0, 288 * 64, ws, dw2, 1, 32, 64), seg(slabs2, C2_WSLAB, 288 * 64, 64, ws, db2),
-                 seg(slabs1, C1_WSLAB, 0, 800, nd, dw1), seg(slabs1, C1_WSLAB, 800, 32, nd, db1)},
-                s);
+  ReduceList r = extra ? *extra : ReduceList{};  // a deferred conv3 / fc1 reduction rides along
+  for (const ReduceSeg& g : {seg(slabs2, C2_WSLAB, 0, 288 * 64, ws, dw2, 1, 32, 64),
+                             seg(slabs2, C2_WSLAB, 288 * 64, 64, ws, db2), seg(slabs1, C1_WSLAB, 0, 800, nd, dw1),
+                             seg(slabs1, C1_WSLAB, 800, 32, nd, db1)})
+    r.push_back(g);
+  launch_reduce(r, s);
 }
 
 void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace ringdp {
 namespace kern {
 
@@ -177,11 +179,43 @@ int64_t cn_fc_slab_floats(int B, bool dgrad);
 int64_t cn_conv3_slab_floats(int B, bool dgrad);
 int64_t cn_conv2_slab_floats(int B, bool dgrad);
 int64_t cn_conv1_slab_floats(int B);
+// One output range of the fixed-order slab reduction (sum over slices, optional layout transform).
+struct ReduceSeg {
+  const float* slabs;
+  int64_t stride;  // floats between consecutive slices
+  int64_t off;     // first float of this segment inside a slice
+  int64_t n;       // outputs
+  int nslices;
+  float* out;
+  int mode;  // 0: out[i] = sum; 1: conv transpose dWt[n = tap*cin + ci][co] -> W[co][ci][tap];
+             // 2: fc1 slab in fc_bwd thread order (n*8 + j)*256 + t -> dWfc[n][co*16 + w]
+  int cin, cout;
+  int blocks;
+};
+using ReduceList = std::vector<ReduceSeg>;
+void cn_launch_reduce(const ReduceList& segs, hipStream_t s);  // one launch, at most 8 segments
+
+// Cross entropy fused into the fc1 backward: the kernel forms dlogits itself from the forward's
+// logits / log-sum-exp (ce_fwd_kernel) instead of reading a materialised [B,10] gradient.
+struct CeFuse {
+  const float* logits;
+  const int64_t* labels;
+  const float* lse;
+  const float* grad_out;  // scalar (mean / sum) or [B] (none)
+  const float* denom;     // ce_fwd's valid-row count (mean) - device scalar
+  int ignore_index;
+  float eps;
+  int reduction;  // 0 none, 1 mean, 2 sum
+};
+
 // F3 backward: da3m is a [B,16,128] bf16 workspace; dz2 [B,11,11,64] (the gradient of conv2's
-// pre-activation, through pool2 + ReLU) may be null (skip the data gradient).
+// pre-activation, through pool2 + ReLU) may be null (skip the data gradient).  Either dl ([B,10]
+// fp32 logits gradient) or ce (fused cross entropy) is given.  defer != null: the weight-gradient
+// reduction is appended to *defer instead of launched (the caller folds it into a later launch).
 void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const uint8_t* idx3, const float* wfc,
                      const float* dl, const void* packed, void* da3m, void* dz2, int B, float* fc_slabs,
-                     float* c3_slabs, float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s);
+                     float* c3_slabs, float* dw3, float* db3, float* dwfc, float* dbfc, hipStream_t s,
+                     const CeFuse* ce = nullptr, ReduceList* defer = nullptr);
 // F2 backward: da1 may be null.
 void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1, int B, float* slabs,
                   float* dw2, float* db2, hipStream_t s);
@@ -192,7 +226,7 @@ void cn_conv2_bwd(const void* a1, const void* dz2, const void* packed, void* da1
 int64_t cn_conv12_slab_floats(int B);
 void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, const void* dz2,
                    const void* packed, int B, float mean, float inv_std, float in_scale, float* slabs, float* dw2,
-                   float* db2, float* dw1, float* db1, hipStream_t s);
+                   float* db2, float* dw1, float* db1, hipStream_t s, const ReduceList* extra = nullptr);
 void cn_conv1_wgrad(const void* x, bool u8, const void* da1, const uint8_t* idx1, int B, float mean,
                     float inv_std, float in_scale, float* slabs, float* dw1, float* db1, hipStream_t s);
 

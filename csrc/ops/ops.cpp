@@ -4,6 +4,7 @@
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -410,10 +411,40 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor&
   return {logits, a3, idx3};
 }
 
-at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
-                           const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& dlogits,
-                           const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
-                           at::Tensor dwfc, at::Tensor dbfc) {
+namespace {
+// A conv3 / fc1 weight-gradient reduction held back to ride along with the next conv12 backward's
+// reduction launch (one launch instead of two).  Keyed by device; `keep` holds the slab tensors
+// until the launch is queued (the caching allocator is stream-ordered, so releasing them right
+// after the launch is safe).
+struct PendingReduce {
+  kern::ReduceList segs;
+  std::vector<at::Tensor> keep;
+  hipStream_t stream = nullptr;
+};
+std::mutex g_pend_mu;
+std::map<int, PendingReduce> g_pend;
+std::atomic<int64_t> g_merged{0};  // deferrals folded into a conv12 reduction launch (tests)
+
+PendingReduce take_pending(int dev) {
+  std::lock_guard<std::mutex> lk(g_pend_mu);
+  PendingReduce p;
+  auto it = g_pend.find(dev);
+  if (it != g_pend.end()) {
+    p = std::move(it->second);
+    g_pend.erase(it);
+  }
+  return p;
+}
+
+void flush_pending(int dev) {
+  PendingReduce p = take_pending(dev);
+  if (!p.segs.empty()) kern::cn_launch_reduce(p.segs, p.stream);
+}
+
+at::Tensor conv3_fc_bwd_impl(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
+                             const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor* dlogits,
+                             const kern::CeFuse* ce, const at::Tensor& packed, bool need_dz2, at::Tensor dw3,
+                             at::Tensor db3, at::Tensor dwfc, at::Tensor dbfc, bool defer) {
   const int64_t B = a2.size(0);
   check_act(a2, {B, 10, 10, 64}, at::kBFloat16, "pooled conv2 activation a2");
   check_act(idx2, {B, 10, 10, 64}, at::kByte, "pool2 codes");
@@ -425,11 +456,16 @@ at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const a
   check_f32_out(db3, {128}, "conv3 db");
   check_f32_out(dwfc, {10, 2048}, "fc1 dw");
   check_f32_out(dbfc, {10}, "fc1 db");
-  check_cuda(dlogits, "logits grad");
-  at::Tensor dl = dlogits.to(at::kFloat).contiguous();
-  check_shape(dl, {B, 10}, "logits grad");
+  at::Tensor dl;
+  if (dlogits) {
+    check_cuda(*dlogits, "logits grad");
+    dl = dlogits->to(at::kFloat).contiguous();
+    check_shape(dl, {B, 10}, "logits grad");
+  }
   at::Tensor dz2;
   if (need_dz2) dz2 = at::empty({B, 11, 11, 64}, a2.options());
+  const int dev = a2.get_device();
+  flush_pending(dev);  // a stale deferral (its conv12 backward never ran) goes out first
   if (B == 0) {
     dw3.zero_();
     db3.zero_();
@@ -441,12 +477,67 @@ at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const a
   at::Tensor da3m = at::empty({B, 16, 128}, a2.options());
   at::Tensor fs = at::empty({kern::cn_fc_slab_floats(bi, need_dz2)}, dw3.options());
   at::Tensor cs = at::empty({kern::cn_conv3_slab_floats(bi, need_dz2)}, dw3.options());
+  const hipStream_t st = cur_stream(a2);
+  kern::ReduceList held;
   kern::cn_conv3_fc_bwd(a2.data_ptr(), idx2.data_ptr<uint8_t>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
-                        wfc.data_ptr<float>(), dl.data_ptr<float>(), packed.data_ptr(), da3m.data_ptr(),
-                        need_dz2 ? dz2.data_ptr() : nullptr, bi, fs.data_ptr<float>(),
-                        cs.data_ptr<float>(), dw3.data_ptr<float>(), db3.data_ptr<float>(),
-                        dwfc.data_ptr<float>(), dbfc.data_ptr<float>(), cur_stream(a2));
+                        wfc.data_ptr<float>(), dl.defined() ? dl.data_ptr<float>() : nullptr, packed.data_ptr(),
+                        da3m.data_ptr(), need_dz2 ? dz2.data_ptr() : nullptr, bi, fs.data_ptr<float>(),
+                        cs.data_ptr<float>(), dw3.data_ptr<float>(), db3.data_ptr<float>(), dwfc.data_ptr<float>(),
+                        dbfc.data_ptr<float>(), st, ce, defer ? &held : nullptr);
+  if (defer) {
+    std::lock_guard<std::mutex> lk(g_pend_mu);
+    PendingReduce& p = g_pend[dev];
+    p.segs = std::move(held);
+    p.keep = {fs, cs};
+    p.stream = st;
+  }
   return dz2;
+}
+}  // namespace
+
+at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
+                           const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& dlogits,
+                           const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
+                           at::Tensor dwfc, at::Tensor dbfc, bool defer_reduce) {
+  return conv3_fc_bwd_impl(a2, idx2, a3, idx3, wfc, &dlogits, nullptr, packed, need_dz2, dw3, db3, dwfc, dbfc,
+                           defer_reduce);
+}
+
+at::Tensor cn_conv3_fc_ce_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
+                              const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& logits,
+                              const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& ws,
+                              const at::Tensor& grad_out, int64_t ignore_index, double smoothing, int64_t reduction,
+                              const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
+                              at::Tensor dwfc, at::Tensor dbfc, bool defer_reduce) {
+  const int64_t B = a2.size(0);
+  check_cuda(logits, "cross_entropy logits");
+  check_dtype(logits, at::kFloat, "cross_entropy logits");
+  check_shape(logits, {B, 10}, "cross_entropy logits");
+  check_cuda(labels, "cross_entropy labels");
+  check_dtype(labels, at::kLong, "cross_entropy labels");
+  check_shape(labels, {B}, "cross_entropy labels");
+  check_cuda(lse, "cross_entropy lse");
+  check_cuda(grad_out, "cross_entropy grad_out");
+  RINGDP_CHECK(reduction >= 0 && reduction <= 2, "cross_entropy: bad reduction ", reduction);
+  at::Tensor g = grad_out.to(at::kFloat).contiguous();
+  RINGDP_CHECK(g.numel() == (reduction == 0 ? B : 1), "cross_entropy grad_out: expected ",
+               reduction == 0 ? B : 1, " elements, got ", g.numel());
+  const int nparts = static_cast<int>((ws.numel() - 4) / 2);
+  const kern::CeFuse ce{logits.data_ptr<float>(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                        g.data_ptr<float>(), ws.data_ptr<float>() + 2 * nparts, static_cast<int>(ignore_index),
+                        static_cast<float>(smoothing), static_cast<int>(reduction)};
+  return conv3_fc_bwd_impl(a2, idx2, a3, idx3, wfc, nullptr, &ce, packed, need_dz2, dw3, db3, dwfc, dbfc,
+                           defer_reduce);
+}
+
+void cn_flush_reduce(int64_t device) { flush_pending(static_cast<int>(device)); }
+
+int64_t cn_merged_reductions() { return g_merged.load(); }
+
+bool cn_reduce_pending(int64_t device) {
+  std::lock_guard<std::mutex> lk(g_pend_mu);
+  auto it = g_pend.find(static_cast<int>(device));
+  return it != g_pend.end() && !it->second.segs.empty();
 }
 
 at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::Tensor& packed,
@@ -496,10 +587,17 @@ void cn_conv12_bwd(const at::Tensor& x, const at::Tensor& idx1, const at::Tensor
   }
   const int bi = static_cast<int>(B);
   at::Tensor slabs = at::empty({kern::cn_conv12_slab_floats(bi)}, dw2.options());
+  const hipStream_t st = cur_stream(x);
+  PendingReduce pend = take_pending(x.get_device());
+  if (!pend.segs.empty() && pend.stream != st) {  // deferred on another stream: it goes out there
+    kern::cn_launch_reduce(pend.segs, pend.stream);
+    pend.segs.clear();
+  }
+  if (!pend.segs.empty()) ++g_merged;
   kern::cn_conv12_bwd(x.data_ptr(), u8, idx1.data_ptr<uint8_t>(), a1.data_ptr(), dz2.data_ptr(), packed.data_ptr(),
                       bi, static_cast<float>(mean), static_cast<float>(1.0 / std), static_cast<float>(in_scale),
                       slabs.data_ptr<float>(), dw2.data_ptr<float>(), db2.data_ptr<float>(), dw1.data_ptr<float>(),
-                      db1.data_ptr<float>(), cur_stream(x));
+                      db1.data_ptr<float>(), st, pend.segs.empty() ? nullptr : &pend.segs);
 }
 
 void cn_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& idx1, at::Tensor dw1,

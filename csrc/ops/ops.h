@@ -75,7 +75,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv3_fc_fwd(const at::Tensor&
 at::Tensor cn_conv3_fc_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
                            const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& dlogits,
                            const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
-                           at::Tensor dwfc, at::Tensor dbfc);
+                           at::Tensor dwfc, at::Tensor dbfc, bool defer_reduce);
+// Same with the cross entropy backward fused into the fc1 backward (logits / lse / ws from
+// cross_entropy_fwd).  defer_reduce: the weight-gradient reduction is held back and launched
+// together with the next cn_conv12_bwd's on this device (or by cn_flush_reduce).
+at::Tensor cn_conv3_fc_ce_bwd(const at::Tensor& a2, const at::Tensor& idx2, const at::Tensor& a3,
+                              const at::Tensor& idx3, const at::Tensor& wfc, const at::Tensor& logits,
+                              const at::Tensor& labels, const at::Tensor& lse, const at::Tensor& ws,
+                              const at::Tensor& grad_out, int64_t ignore_index, double smoothing, int64_t reduction,
+                              const at::Tensor& packed, bool need_dz2, at::Tensor dw3, at::Tensor db3,
+                              at::Tensor dwfc, at::Tensor dbfc, bool defer_reduce);
+void cn_flush_reduce(int64_t device);
+bool cn_reduce_pending(int64_t device);
+int64_t cn_merged_reductions();
 at::Tensor cn_conv2_bwd(const at::Tensor& a1, const at::Tensor& dz2, const at::Tensor& packed,
                         bool need_da1, at::Tensor dw2, at::Tensor db2);
 void cn_conv12_bwd(const at::Tensor& x, const at::Tensor& idx1, const at::Tensor& a1, const at::Tensor& dz2,

@@ -183,7 +183,7 @@ class ResNet(nn.Module):
 
     def reference_forward(self, x: torch.Tensor) -> torch.Tensor:
         """ATen NCHW forward (CPU path and numerics oracle)."""
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x.float()))))
+        x = self.maxpool(self.relu(self.bn1(self.conv1(x.to(self.conv1.weight.dtype)))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 

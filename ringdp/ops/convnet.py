@@ -30,6 +30,31 @@ from . import grad_buffer
 
 # RINGDP_CN_FUSE12=0: conv1 / conv2 as separate autograd nodes with their own backward kernels (A/B)
 _FUSE12 = os.environ.get("RINGDP_CN_FUSE12", "1") != "0"
+# RINGDP_CN_DEFER_REDUCE=0: conv3 / fc1 weight-gradient reduction in its own launch (A/B)
+_DEFER = os.environ.get("RINGDP_CN_DEFER_REDUCE", "1") != "0"
+# RINGDP_CN_HEAD_CE=0: ringdp's cross entropy on the ConvNet logits stays a separate node (A/B)
+_HEAD_CE = os.environ.get("RINGDP_CN_HEAD_CE", "1") != "0"
+
+
+def _defer_reduce(params, grads, need_in: bool) -> bool:
+    """May the conv3 / fc1 weight-gradient reduction wait for conv12's backward (one reduction
+    launch for the whole backward instead of two)?
+
+    Only when nothing reads those gradients before then: every one of them is written straight
+    into its DDP bucket slot (AccumulateGrad adopts the slot, no accumulation kernel reads it),
+    the slots belong to the bucket that is all-reduced last (the reducer launches buckets in
+    order, after conv12's parameters are ready), and conv12's backward follows (the conv3 input
+    needs a gradient).  An end-of-backward callback flushes a deferral that nothing consumed
+    (e.g. ``torch.autograd.grad`` restricted to the head parameters)."""
+    if not (_DEFER and need_in):
+        return False
+    for p, g in zip(params, grads):
+        slot = getattr(p, "_ringdp_grad_slot", None)
+        if slot is None or not getattr(p, "_ringdp_last_bucket", False) or g.data_ptr() != slot.data_ptr():
+            return False
+    dev = grads[0].get_device()
+    torch.autograd.Variable._execution_engine.queue_callback(lambda: C.cn_flush_reduce(dev))
+    return True
 
 MNIST_MEAN = 0.1307
 MNIST_STD = 0.3081
@@ -71,6 +96,7 @@ class _Conv2(torch.autograd.Function):
     def backward(ctx, dz2, _da2, _didx2):
         a1, packed = ctx.saved_tensors
         w, b = ctx.params
+        C.cn_flush_reduce(a1.get_device())
         dw, db = grad_buffer(w), grad_buffer(b)
         need_in = ctx.needs_input_grad[0]
         da1 = C.cn_conv2_bwd(a1, dz2.contiguous(), packed, need_in, dw, db)
@@ -104,9 +130,11 @@ class _Conv12(torch.autograd.Function):
         dz2 = dz2.contiguous()
         if n[1] and n[2] and n[3] and n[4]:
             dw1, db1, dw2, db2 = (grad_buffer(t) for t in (w1, b1, w2, b2))
+            # also launches a reduction _Conv3FC / _HeadCE deferred into this one
             C.cn_conv12_bwd(x, idx1, a1, dz2, packed, dw2, db2, dw1, db1, *ctx.norm)
             return None, dw1, db1, dw2, db2, None, None, None, None, None
         # partially frozen: the separate kernels
+        C.cn_flush_reduce(x.get_device())
         need_c1 = n[1] or n[2]
         dw2, db2 = grad_buffer(w2), grad_buffer(b2)
         da1 = C.cn_conv2_bwd(a1, dz2, packed, need_c1, dw2, db2)
@@ -122,21 +150,73 @@ class _Conv3FC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z2, a2, idx2, w3, b3, wfc, bfc, packed):
         logits, a3, idx3 = C.cn_conv3_fc_fwd(a2, packed, b3, bfc)
+        ctx.mark_non_differentiable(a3, idx3)
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(a2, idx2, a3, idx3, wfc, packed)
         ctx.params = (w3, b3, wfc, bfc)
-        return logits
+        return logits, a3, idx3
 
     @staticmethod
-    def backward(ctx, dlogits):
+    def backward(ctx, dlogits, _da3, _didx3):
         a2, idx2, a3, idx3, wfc_saved, packed = ctx.saved_tensors
         w3, b3, wfc, bfc = ctx.params
-        dw3, db3, dwfc, dbfc = (grad_buffer(p) for p in (w3, b3, wfc, bfc))
-        need_in = ctx.needs_input_grad[0]
-        dz2 = C.cn_conv3_fc_bwd(a2, idx2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
-                                dw3, db3, dwfc, dbfc)
         n = ctx.needs_input_grad
+        if dlogits is None:
+            return (None,) * 8
+        grads = [grad_buffer(p) for p in (w3, b3, wfc, bfc)]
+        need_in = n[0]
+        defer = _defer_reduce((w3, b3, wfc, bfc), grads, need_in)
+        dz2 = C.cn_conv3_fc_bwd(a2, idx2, a3, idx3, wfc_saved, dlogits.contiguous(), packed, need_in,
+                                *grads, defer_reduce=defer)
+        dw3, db3, dwfc, dbfc = grads
         return (dz2 if need_in else None, None, None, dw3 if n[3] else None, db3 if n[4] else None,
                 dwfc if n[5] else None, dbfc if n[6] else None, None)
+
+
+class _HeadCE(torch.autograd.Function):
+    """Cross entropy straight on the ConvNet head: ``loss = CE(fc1(pool3(relu(conv3(a2)))), y)`` as
+    one node whose backward forms d(logits) inside the fc1 backward kernel (no ce_bwd launch, no
+    [B,10] gradient tensor).  The forward reuses the logits ``_Conv3FC`` already computed; that
+    node stays in the graph for any other use of the logits, so gradients through other paths are
+    unchanged (the engine sums them)."""
+
+    @staticmethod
+    def forward(ctx, z2, w3, b3, wfc, bfc, logits, target, head, ignore_index, eps, reduction):
+        loss, lse, ws = C.cross_entropy_fwd(logits, target, ignore_index, eps, reduction)
+        ctx.save_for_backward(logits, target, lse, ws)
+        ctx.head = head
+        ctx.params = (w3, b3, wfc, bfc)
+        ctx.cfg = (ignore_index, eps, reduction)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, target, lse, ws = ctx.saved_tensors
+        a2, idx2, a3, idx3, packed = ctx.head
+        w3, b3, wfc, bfc = ctx.params
+        n = ctx.needs_input_grad
+        grads = [grad_buffer(p) for p in (w3, b3, wfc, bfc)]
+        need_in = n[0]
+        defer = _defer_reduce((w3, b3, wfc, bfc), grads, need_in)
+        dz2 = C.cn_conv3_fc_ce_bwd(a2, idx2, a3, idx3, wfc.detach(), logits, target, lse, ws,
+                                   grad_out.contiguous(), *ctx.cfg, packed, need_in, *grads, defer)
+        dw3, db3, dwfc, dbfc = grads
+        return (dz2 if need_in else None, dw3 if n[1] else None, db3 if n[2] else None,
+                dwfc if n[3] else None, dbfc if n[4] else None) + (None,) * 6
+
+
+def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int, eps: float,
+                       reduction: int):
+    """Fused head + cross entropy when ``logits`` is a ConvNet head output (see ``_HeadCE``), else
+    None.  Called by ringdp.ops.loss.cross_entropy."""
+    head = getattr(logits, "_ringdp_head", None)
+    if head is None or not _HEAD_CE or not torch.is_grad_enabled() or not logits.requires_grad:
+        return None
+    if target.dim() != 1 or target.shape[0] != logits.shape[0] or not target.is_cuda:
+        return None
+    z2, a2, idx2, w3, b3, wfc, bfc, packed, a3, idx3 = head
+    return _HeadCE.apply(z2, w3, b3, wfc, bfc, logits.detach(), target.long().contiguous(),
+                         (a2, idx2, a3, idx3, packed), ignore_index, eps, reduction)
 
 
 def pack_weights(conv1, conv2, conv3, fc1) -> torch.Tensor:
@@ -162,4 +242,8 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         packed = pack_weights(conv1, conv2, conv3, fc1)
         a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
         z2, a2, idx2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
-    return _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)
+    logits, a3, idx3 = _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)
+    if logits.requires_grad:
+        # what ringdp's cross entropy needs to fuse itself into the head (head_cross_entropy)
+        logits._ringdp_head = (z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed, a3, idx3)
+    return logits

@@ -230,6 +230,12 @@ class DistributedDataParallel(nn.Module):
         flat_by_dtype = {f.dtype: f for f in flats}
         for p, s in zip(self._params, slots):
             p._ringdp_grad_slot = s
+        # parameters of the bucket launched last: an op may hold back their final reduction
+        # until a later op of the same backward (ringdp/ops/convnet.py deferred reduction)
+        buckets = [list(b) for b in self.reducer.bucket_indices()]
+        last = set(buckets[-1]) if buckets else set()
+        for i, p in enumerate(self._params):
+            p._ringdp_last_bucket = i in last
         if not self._flatten:
             return
         self._flat_params = {}

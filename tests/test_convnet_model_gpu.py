@@ -293,3 +293,54 @@ def test_convnet_bf16_trajectory_b4096():
     d = float((l_16 - l_ref).abs().max())
     print(f"B=4096 max |loss - aten fp32| over 200 steps: {d:.2e}")
     assert d < 5e-3, d
+
+
+@pytest.mark.parametrize("B,bucket_mb", [(100, None), (4096, None), (100, 0.05)])
+def test_head_ce_fusion_and_deferred_reduce(world1, B, bucket_mb):
+    """The cross entropy fused into the fc1 backward (no ce_bwd launch) and the conv3 / fc1
+    weight-gradient reduction folded into conv12's reduction launch give bit-identical losses and
+    gradients to the separate kernels, plain and under DDP; with small buckets (conv3 / fc1 in the
+    first bucket, all-reduced before conv12's backward) the reduction must not be deferred."""
+    import ringdp.ops.convnet as cn
+    from ringdp._native import C
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+    from ringdp.parallel import DistributedDataParallel as DDP
+
+    crit = CrossEntropyLoss()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g)
+    y = torch.randint(0, 10, (B,), device="cuda", generator=g)
+
+    def run(head_ce, defer, ddp):
+        cn._HEAD_CE, cn._DEFER = head_ce, defer
+        torch.manual_seed(0)
+        m = ConvNet().cuda()
+        kw = {} if bucket_mb is None else {"bucket_cap_mb": bucket_mb, "first_bucket_mb": bucket_mb}
+        mod = DDP(m, device_ids=[0], **kw) if ddp else m
+        merged0 = C.cn_merged_reductions()
+        for _ in range(3):  # the DDP bucket rebuild happens after iteration 0
+            for p in m.parameters():
+                p.grad = None
+            loss = crit(mod(x), y)
+            loss.backward()
+        torch.cuda.synchronize()
+        assert not C.cn_reduce_pending(0)
+        return loss.detach(), [p.grad.clone() for p in m.parameters()], C.cn_merged_reductions() - merged0
+
+    try:
+        l0, g0, n0 = run(False, False, False)
+        assert n0 == 0
+        for cfg in [(True, False, False), (True, True, True), (False, True, True), (True, True, False)]:
+            l1, g1, n1 = run(*cfg)
+            assert torch.equal(l1, l0), cfg
+            for a, b in zip(g1, g0):
+                assert torch.equal(a, b), cfg
+            if cfg[1] and cfg[2]:  # deferral only under DDP, and only into the last bucket: with small
+                # buckets conv3 / fc1 sit in the first one once the buckets follow the ready order
+                # (iteration 0's registration-order buckets may still allow it)
+                assert (n1 <= 1) if bucket_mb is not None else (n1 >= 2), (cfg, n1)
+            else:
+                assert n1 == 0, (cfg, n1)
+    finally:
+        cn._HEAD_CE, cn._DEFER = True, True

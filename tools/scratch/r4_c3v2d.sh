@@ -10,4 +10,6 @@ for r in 1 2; do
   RINGDP_C3_BWD=2 timeout -k 10 120 python tools/op_time.py conv3_fc_bwd_w 65536 15 >> $O/times.jsonl 2>>$O/t.err || exit 1
 done
 cat $O/times.jsonl
+
+timeout -k 10 300 python -u -m pytest tests/test_model_parity_gpu.py -x -q -s --timeout 120 --timeout-method thread -p no:cacheprovider > $O/parity.log 2>&1; tail -12 $O/parity.log
 echo ALLDONE
