@@ -571,6 +571,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cn_pack_weights", &ops::cn_pack_weights);
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv1_fwd_pack", &ops::cn_conv1_fwd_pack);
+  m.def("cn_forward_buffers", &ops::cn_forward_buffers);
+  m.def("cn_forward_fused", &ops::cn_forward_fused);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);
   m.def("cn_conv3_fc_fwd", &ops::cn_conv3_fc_fwd);
   m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd, py::arg("a2"), py::arg("idx2"), py::arg("a3"), py::arg("idx3"),
@@ -580,14 +582,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cn_flush_reduce", &ops::cn_flush_reduce);
   m.def("cn_reduce_pending", &ops::cn_reduce_pending);
   m.def("cn_merged_reductions", &ops::cn_merged_reductions);
-  m.def("cn_set_variant", [](const std::string& name, int value) {
-    RINGDP_CHECK(kern::cn_set_variant(name.c_str(), value), "cn_set_variant: unknown variant ", name, "=", value);
-  });
-  m.def("cn_get_variant", [](const std::string& name) { return kern::cn_get_variant(name.c_str()); });
-  m.def("cn_debug_stamps", []() {
-    at::Tensor t = at::zeros({4, 16, 16}, at::TensorOptions().dtype(at::kLong));
-    return kern::cn_debug_stamps(t.data_ptr()) ? t : at::Tensor();
-  });
   m.def("cn_conv2_bwd", &ops::cn_conv2_bwd);
   m.def("cn_conv1_wgrad", &ops::cn_conv1_wgrad);
   m.def("cn_conv12_bwd", &ops::cn_conv12_bwd);

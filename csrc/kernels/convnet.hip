@@ -33,7 +33,6 @@
 
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
 
 #include "device_common.h"
 #include "kernels.h"
@@ -697,6 +696,348 @@ __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ a
   }
 }
 
+// ================================================================== F1+F2+F3: fused forward
+// The whole forward of one image in one 512-thread workgroup, a1 / a2 never re-read from HBM (the
+// three separate launches move 64 KB per image, this one 40 KB: the forward is HBM- as much as
+// MFMA-bound).  Waves 0-3 are the PRODUCER (conv1 + pool1, conv2 + pool2 of image s), waves 4-7 the
+// CONSUMER (conv3 + pool3 + fc1 of image s-1, one step behind).  A step is three barrier-separated
+// phases, the same barriers for both halves:
+//   phase 1  producer: conv1 MFMAs on the staged input -> pooled a1 straight into conv2's operand
+//                      rows (X2) + codes (CT)               consumer: conv3 k-steps 0-8 of image s-1
+//   phase 2  producer: next input -> XS; a1 / idx1 -> HBM; conv2 MFMAs -> Cs
+//                                                           consumer: conv3 k-steps 9-17
+//   phase 3  producer: pool2 of Cs -> a2 / idx2 (HBM) and conv3's operand rows X3
+//                                                           consumer: pool3 -> a3 / idx3, fc1 partials
+// Each LDS buffer has one writer phase and its readers in other phases, so every buffer is single.
+// The layouts are the separate kernels' (conv1_fwd_kernel / conv2_fwd_kernel / conv3_fwd_kernel<true>).
+// PACK: weight fragments built from the fp32 masters (pack_value) by each workgroup, and the extra
+// workgroups >= conv_blocks write the packed buffer for the backward.
+constexpr int FF_XS = 8 * C1F_CS * 2;      // 16768: conv1 input, 8 shifted copies
+constexpr int FF_X2 = 172 * C2_XRS * 2;    // 16512: a1 in conv2 operand rows (+3 dump rows)
+constexpr int FF_CT = C1I_IMG + 64;        // 3392: conv1 codes (+ dump row)
+constexpr int FF_CS = 121 * C2_CRS * 2;    // 17424: conv2 output tile
+constexpr int FF_X3 = 100 * C3F_XRS * 2;   // 16000: a2 in conv3 operand rows
+constexpr int FF_FW = C3F_FCW * 2;         // 40960: fc1 weights [window][co][n]
+constexpr int FF_FR = 10 * 256 * 4;        // 10240: fc1 partial logits [n][256]
+constexpr int FF_OFF_X2 = FF_XS, FF_OFF_CT = FF_OFF_X2 + FF_X2, FF_OFF_CS = FF_OFF_CT + FF_CT,
+              FF_OFF_X3 = FF_OFF_CS + FF_CS, FF_OFF_FW = FF_OFF_X3 + FF_X3, FF_OFF_FR = FF_OFF_FW + FF_FW;
+constexpr int FF_LDS = FF_OFF_FR + FF_FR;  // 121296
+static_assert(FF_OFF_X2 % 16 == 0 && FF_OFF_CT % 16 == 0 && FF_OFF_CS % 16 == 0 && FF_OFF_X3 % 16 == 0 &&
+                  FF_OFF_FW % 16 == 0 && FF_LDS <= 160 * 1024,
+              "fused forward LDS");
+
+template <bool PACK>
+__device__ __forceinline__ bf16x8 ff_frag(const bf16* __restrict__ packed, const PackSrc& ws, int off, int lane) {
+  bf16x8 v;
+  if (PACK) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)pack_value(off + lane * 8 + j, ws);
+  } else {
+    v = reinterpret_cast<const bf16x8*>(packed + off)[lane];
+  }
+  return v;
+}
+
+template <bool U8, bool PACK>
+__device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16* __restrict__ packed,
+                            const PackSrc& ws, const float* __restrict__ b1, const float* __restrict__ b2,
+                            bf16* __restrict__ a1, uint8_t* __restrict__ idx1, bf16* __restrict__ a2,
+                            uint8_t* __restrict__ idx2, int B, int b0, int bstep, int nsteps, float mean,
+                            float inv_std, float in_scale) {
+  bf16* XS = reinterpret_cast<bf16*>(smem);
+  bf16* X2 = reinterpret_cast<bf16*>(smem + FF_OFF_X2);
+  uint32_t* X2u = reinterpret_cast<uint32_t*>(X2);
+  uint8_t* CT = reinterpret_cast<uint8_t*>(smem + FF_OFF_CT);
+  bf16* Cs = reinterpret_cast<bf16*>(smem + FF_OFF_CS);
+  bf16* X3 = reinterpret_cast<bf16*>(smem + FF_OFF_X3);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;  // tid < 256
+  const int r16 = lane & 15, gq = lane >> 4;
+  // ---- conv1 setup (conv1_fwd_kernel)
+  bf16x8 bw1[2][2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) bw1[nt][ks] = ff_frag<PACK>(packed, ws, P1_OFF + (nt * 2 + ks) * 512, lane);
+  const float c1b0 = b1[2 * r16], c1b1 = b1[2 * r16 + 1];
+  const f32x4 bias0v = {c1b0, c1b0, c1b0, c1b0}, bias1v = {c1b1, c1b1, c1b1, c1b1};
+  int aoff[C1F_MT], coff[C1F_MT];
+#pragma unroll
+  for (int j = 0; j < C1F_MT; ++j) {
+    const int mt = wave + 4 * j;
+    const int w = min(4 * mt + (r16 >> 2), 168), i = r16 & 3;
+    const int oh = 2 * (w / 13) + (i >> 1), ow = 2 * (w % 13) + (i & 1);
+    aoff[j] = (ow & 7) * C1F_CS + oh * XC_W + (ow & ~7) + gq * XC_W;
+    const int wc = 4 * mt + gq;
+    coff[j] = wc < 169 ? (wc / 13) * 256 + r16 * 16 + wc % 13 : C1I_IMG + lane;
+  }
+  // ---- conv2 setup (conv2_fwd_kernel)
+  const int wm = wave >> 1, wn = wave & 1, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
+  bf16x8 bw2[2][9];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 9; ++ks) bw2[t][ks] = ff_frag<PACK>(packed, ws, P2F_OFF + ((2 * wn + t) * 9 + ks) * 512, lane);
+  f32x4 bv2[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv2[t][i] = b2[(2 * wn + t) * 16 + c4 + i];
+  int base2[4], opos2[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    opos2[mt] = c2f_tile_pos[(4 * wm + mt) * 16 + r16];
+    const int mm = opos2[mt] == 255 ? 0 : opos2[mt];
+    base2[mt] = (mm / 11) * 13 + mm % 11;
+  }
+  // zero ring of the input copies and the never-written code columns (px 13..15), once
+  for (int i = tid; i < FF_XS / 16; i += 256) reinterpret_cast<bf16x8*>(XS)[i] = zero_bf16x8();
+  for (int i = tid; i < C1I_IMG / 16; i += 256) reinterpret_cast<uint4*>(CT)[i] = make_uint4(0, 0, 0, 0);
+  __syncthreads();  // [S0a] zeroing before the first input store
+  uint32_t pu = 0;
+  float4 pf = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (b0 < B) {
+    c1_load<U8>(xin, b0, tid, pu, pf);
+    c1_store<U8, 8, XC_W, C1F_CS>(XS, tid, pu, pf, mean, inv_std, in_scale);
+  }
+  __syncthreads();  // [S0b] first input staged
+  for (int s = 0; s < nsteps; ++s) {
+    const int b = b0 + s * bstep;
+    const bool live = b < B;
+    const int nb = b + bstep;
+    // ---------------- phase 1: conv1 -> X2 / CT
+    if (live) {
+      if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
+      auto epilogue = [&](int j, const f32x4& c0, const f32x4& c1) {
+        uint32_t g0, g1;
+        const uint32_t v0 = pool4_key(c0, g0), v1 = pool4_key(c1, g1);
+        const bf16x2v pv = __builtin_convertvector(f32x2v{__uint_as_float(v0), __uint_as_float(v1)}, bf16x2v);
+        X2u[(4 * (wave + 4 * j) + gq) * (C2_XRS / 2) + r16] = __builtin_bit_cast(uint32_t, pv);
+        CT[coff[j]] = (uint8_t)(g0 | (g1 << 4));
+      };
+      f32x4 p0 = zero_f32x4(), p1 = zero_f32x4();
+#pragma unroll
+      for (int j = 0; j < C1F_MT; ++j) {
+        f32x4 c0 = bias0v, c1 = bias1v;
+        const bool lv = j < C1F_MT - 1 || wave < 3;
+        if (lv) {
+          const bf16* xr = XS + aoff[j];
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(xr);
+          const bf16x8 a1v = *reinterpret_cast<const bf16x8*>(xr + (4 - gq) * XC_W);
+          c0 = mfma16x16x32(a0, bw1[0][0], c0);
+          c1 = mfma16x16x32(a0, bw1[1][0], c1);
+          c0 = mfma16x16x32(a1v, bw1[0][1], c0);
+          c1 = mfma16x16x32(a1v, bw1[1][1], c1);
+        }
+        if (j > 0) epilogue(j - 1, p0, p1);
+        if (lv && j == C1F_MT - 1) epilogue(j, c0, c1);
+        p0 = c0;
+        p1 = c1;
+      }
+    }
+    __syncthreads();  // [S1] X2 / CT complete, XS free
+    // ---------------- phase 2: next input; a1 / idx1 out; conv2 -> Cs
+    f32x4 acc[4][2];
+    if (live) {
+      if (nb < B) c1_store<U8, 8, XC_W, C1F_CS>(XS, tid, pu, pf, mean, inv_std, in_scale);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
+#pragma unroll
+      for (int ks = 0; ks < 9; ++ks) {
+        const int shift = (ks / 3) * 13 + ks % 3;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(X2 + (base2[mt] + shift) * C2_XRS + q8);
+          acc[mt][0] = mfma16x16x32(bw2[0][ks], a, acc[mt][0]);
+          acc[mt][1] = mfma16x16x32(bw2[1][ks], a, acc[mt][1]);
+        }
+      }
+      // a1 / idx1 to HBM while the MFMAs drain
+      uint4* og = reinterpret_cast<uint4*>(a1 + (int64_t)b * C1A_IMG);
+      for (int c = tid; c < C1A_IMG / 8; c += 256)
+        og[c] = *reinterpret_cast<const uint4*>(X2 + (c >> 2) * C2_XRS + (c & 3) * 8);
+      const uint4* cs = reinterpret_cast<const uint4*>(CT);
+      uint4* cg = reinterpret_cast<uint4*>(idx1 + (int64_t)b * C1I_IMG);
+      for (int c = tid; c < C1I_IMG / 16; c += 256) cg[c] = cs[c];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = opos2[mt];
+        if (m < 121) {
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            const f32x4 v = acc[mt][t] + bv2[t];
+            *reinterpret_cast<bf16x4*>(Cs + m * C2_CRS + (2 * wn + t) * 16 + c4) =
+                bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          }
+        }
+      }
+    }
+    __syncthreads();  // [S2] Cs complete; the consumer is done reading X3
+    // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3
+    if (live) {
+      bf16x8* da = reinterpret_cast<bf16x8*>(a2 + (int64_t)b * 6400);
+      uint2* di = reinterpret_cast<uint2*>(idx2 + (int64_t)b * 6400);
+      for (int it = tid; it < 800; it += 256) {
+        const int p = it >> 3, c = (it & 7) * 8;
+        bf16x8 v;
+        uint2 code;
+        pool2_code8(Cs + ((p / 10) * 11 + p % 10) * C2_CRS + c, C2_CRS, 11, v, code);
+        da[it] = v;
+        di[it] = code;
+        *reinterpret_cast<bf16x8*>(X3 + p * C3F_XRS + c) = v;
+      }
+    }
+    __syncthreads();  // [S3] X3 complete; Cs, X2, CT free
+  }
+}
+
+template <bool PACK>
+__device__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const PackSrc& ws,
+                            const float* __restrict__ b3, const float* __restrict__ bfc, bf16* __restrict__ a3,
+                            uint8_t* __restrict__ idx3, float* __restrict__ logits, int B, int b0, int bstep,
+                            int nsteps) {
+  const bf16* X3 = reinterpret_cast<const bf16*>(smem + FF_OFF_X3);
+  bf16* fw = reinterpret_cast<bf16*>(smem + FF_OFF_FW);
+  float* fred = reinterpret_cast<float*>(smem + FF_OFF_FR);
+  const int tid = threadIdx.x - 256, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, q8 = (lane >> 4) * 8;
+  if (PACK) {
+    for (int c = tid; c < C3F_FCW / 8; c += 256) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)pack_value(PFC_OFF + c * 8 + j, ws);
+      reinterpret_cast<bf16x8*>(fw)[c] = v;
+    }
+  } else {
+    const uint4* src = reinterpret_cast<const uint4*>(packed + PFC_OFF);
+    for (int c = tid; c < C3F_FCW / 8; c += 256) reinterpret_cast<uint4*>(fw)[c] = src[c];
+  }
+  bf16x8 bw[2][18];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) bw[t][ks] = ff_frag<PACK>(packed, ws, P3F_OFF + ((2 * wave + t) * 18 + ks) * 512, lane);
+  float bv[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) bv[t] = b3[32 * wave + 16 * t + r16];
+  const float bn = tid < 160 ? bfc[tid >> 4] : 0.f;
+  int base[4], wcol[4];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+    base[mt] = win_pos(4 * c3f_win[4 * mt + (r16 >> 2)] + (r16 & 3), 10);
+    wcol[mt] = c3f_win[4 * mt + (lane >> 4)];
+  }
+  __syncthreads();  // [S0a]
+  __syncthreads();  // [S0b]  (fw is complete past these)
+  auto fc_reduce = [&](int bb) {  // after a barrier that follows the fred writes of image bb
+    if (tid < 160) {
+      const int n = tid >> 4, c = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) v += fred[n * 256 + c + 16 * i];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (c == 0) logits[(int64_t)bb * 10 + n] = v + bn;
+    }
+  };
+  f32x4 acc[4][2];
+  for (int s = 0; s < nsteps; ++s) {
+    const int b = b0 + (s - 1) * bstep;  // image of this step (one behind the producer)
+    const bool live = s >= 1 && b < B;
+    const int bp = b - bstep;            // image whose fc1 partials sit in fred
+    // ---------------- phase 1: fc1 reduction of the previous image; k-steps 0-8
+    if (s >= 2 && bp < B) fc_reduce(bp);
+    if (live) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
+#pragma unroll
+      for (int ks = 0; ks < 9; ++ks) {
+        const int tap = ks >> 1, c0 = (ks & 1) * 32;
+        const int shift = (tap / 3) * 10 + tap % 3;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(X3 + (base[mt] + shift) * C3F_XRS + c0 + q8);
+          acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
+          acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
+        }
+      }
+    }
+    __syncthreads();  // [S1]
+    // ---------------- phase 2: k-steps 9-17
+    if (live) {
+#pragma unroll
+      for (int ks = 9; ks < 18; ++ks) {
+        const int tap = ks >> 1, c0 = (ks & 1) * 32;
+        const int shift = (tap / 3) * 10 + tap % 3;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(X3 + (base[mt] + shift) * C3F_XRS + c0 + q8);
+          acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
+          acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
+        }
+      }
+    }
+    __syncthreads();  // [S2]
+    // ---------------- phase 3: pool3 + ReLU -> a3 / idx3, fc1 partials -> fred
+    if (live) {
+      float part[10];
+#pragma unroll
+      for (int n = 0; n < 10; ++n) part[n] = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int wc = wcol[mt], co = 32 * wave + 16 * t + r16;
+          int g;
+          const bf16 pb = (bf16)pool4(acc[mt][t], bv[t], g);
+          const int64_t o = ((int64_t)b * 16 + wc) * 128 + co;
+          a3[o] = pb;
+          idx3[o] = (uint8_t)g;
+          const float pv = (float)pb;
+          const uint32_t* wp = reinterpret_cast<const uint32_t*>(fw + (wc * 128 + co) * 10);
+#pragma unroll
+          for (int h = 0; h < 5; ++h) {
+            const uint32_t u = wp[h];
+            part[2 * h] = fmaf(pv, __uint_as_float(u << 16), part[2 * h]);
+            part[2 * h + 1] = fmaf(pv, __uint_as_float(u & 0xffff0000u), part[2 * h + 1]);
+          }
+        }
+#pragma unroll
+      for (int n = 0; n < 10; ++n) fred[n * 256 + tid] = part[n];
+    }
+    __syncthreads();  // [S3]
+  }
+  const int bl = b0 + (nsteps - 2) * bstep;  // the last image's partials
+  if (nsteps >= 2 && bl < B) fc_reduce(bl);
+}
+
+template <bool U8, bool PACK>
+__global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restrict__ xin,
+                                                          const bf16* __restrict__ packed, PackSrc ws,
+                                                          bf16* __restrict__ pack_out, int conv_blocks,
+                                                          const float* __restrict__ b1, const float* __restrict__ b2,
+                                                          const float* __restrict__ b3, const float* __restrict__ bfc,
+                                                          bf16* __restrict__ a1, uint8_t* __restrict__ idx1,
+                                                          bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
+                                                          bf16* __restrict__ a3, uint8_t* __restrict__ idx3,
+                                                          float* __restrict__ logits, int B, float mean,
+                                                          float inv_std, float in_scale, int ablate) {
+  if (PACK && (int)blockIdx.x >= conv_blocks) {
+    if (threadIdx.x < 256) pack_range(ws, pack_out, 0, blockIdx.x - conv_blocks, gridDim.x - conv_blocks);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) char ff_smem[FF_LDS];
+  const int b0 = blockIdx.x, bstep = conv_blocks;
+  const int nimg = b0 < B ? (B - b0 + bstep - 1) / bstep : 0;
+  const int nsteps = nimg + 1;  // the consumer trails by one step
+  // wave-uniform role split (an SGPR condition: the two roles are separate code paths, not one
+  // exec-masked sequence whose live ranges the register allocator would have to overlap)
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4)
+    ff_producer<U8, PACK>(ff_smem, xin, packed, ws, b1, b2, a1, idx1, a2, idx2, (ablate & 1) ? 0 : B, b0, bstep,
+                          nsteps, mean, inv_std, in_scale);
+  else
+    ff_consumer<PACK>(ff_smem, packed, ws, b3, bfc, a3, idx3, logits, (ablate & 2) ? 0 : B, b0, bstep, nsteps);
+}
+
 // ================================================================== F3 backward
 // (1) fc1 backward, one pass over a3: compact data gradient
 //       da3m[b][w][co] = (a3 > 0) * sum_n dl[b][n] * Wfc[n][co*16 + w]     (bf16, Wfc from the pack)
@@ -867,11 +1208,7 @@ __device__ __forceinline__ void c3_expand(const C3Pre& p, int tid, RowPtr row_pt
       bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-#if defined(RINGDP_ABL_EXPAND)
-        v[j] = p.da[j];  // ablation: no selects (wrong values; timing only)
-#else
         v[j] = byte_of(p.id, j) == i ? p.da[j] : (bf16)0.f;
-#endif
       }
       *reinterpret_cast<bf16x8*>(row_ptr(4 * w + i) + cc) = v;
     }
@@ -945,11 +1282,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
         }
 #pragma unroll
         for (int m = 0; m < 2; ++m) {
-#if defined(RINGDP_ABL_COL2IM)
-          *d[m] = acc[m];  // ablation: no read-add (wrong values; timing only)
-#else
           *d[m] = old[m] + acc[m];
-#endif
         }
         asm volatile("" ::: "memory");  // the next tap's reads stay behind these writes
       }
@@ -1003,15 +1336,10 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
           eb = dB[x * (C3_DARS / 4)];
         }
         f32x4 g = zero_f32x4();
-#if defined(RINGDP_ABL_POOL2)
-        g = ea + eb;  // ablation: no code masks (wrong values; timing only)
-        (void)pa; (void)pb; (void)qa; (void)qb; (void)na; (void)nb2;
-#else
         if (x < 10) masked_add(g, na, sA, ea);
         if (x > 0) masked_add(g, pa, sA + 1, qa);
         if (x < 10) masked_add(g, nb2, sB, eb);
         if (x > 0) masked_add(g, pb, sB + 1, qb);
-#endif
         dst[x * 16] = bf16x4{(bf16)g[0], (bf16)g[1], (bf16)g[2], (bf16)g[3]};
         pa = na;
         pb = nb2;
@@ -1117,408 +1445,6 @@ __global__ __launch_bounds__(256, 2) void conv3_bwd_kernel(const bf16* __restric
     b_step = 2 * n_wgrad;
   }
   conv3_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, b_first, b_end, b_step);  // one call site: inlined
-}
-
-// ================================================================== F3 backward, v2 (software-pipelined)
-// Same math and roles as conv3_bwd_kernel; restructured from the round-4 measurements
-// (profiles/r04/README.md): the v1 dgrad role spent ~14k cycles per image on 576 MFMAs because its
-// phases (expand | MFMA + col2im | pool2 backward) were barrier-separated, so the MFMA pipe idled during
-// the VALU-heavy pool2 phase.  v2:
-//   * dgrad: the pool2 + ReLU backward of image i-1 is interleaved, one x-step per tap group, into the
-//     MFMA stream of image i (double-buffered fp32 da2 image and pool2 codes); col2im accumulates with
-//     LDS float atomics (ds_add_f32: no read, no VALU add, fixed order per wave -> deterministic); the
-//     operand image holds only the 8x8 dz3 positions (the scatter form never reads a zero ring);
-//   * wgrad: the workgroup pair of an image slice splits the OUTPUT CHANNELS (co halves), so each expands
-//     only its 64 channels; operands double-buffered, one barrier per image, next image's a2 / compact
-//     gradient staged through registers while the MFMAs run;
-//   * expansion (compact d(a3) + pool3 argmax -> window-ordered rows): per channel pair one v_perm, two
-//     packed 16-bit shifts and one v_bitop3 per row (argmax bit planes as halfword sign masks).
-// LDS layouts (tools/lds_model_c3v2.py): P rows XOR-swizzled by position (conflict-free B reads), da2
-// 16-B chunks XOR-swizzled by (x + 8*(y&1)), D 32-B blocks XOR-swizzled by row bits 1,3, X rows of 80.
-typedef short s16x2v __attribute__((ext_vector_type(2)));
-typedef unsigned char u8x4 __attribute__((ext_vector_type(4)));
-
-// masked rows of one channel pair: d = bf16 pair (ch 2k lo, ch 2k+1 hi), t = their argmax (0..3) in bits
-// 0-1 and 16-17.  row i keeps a channel iff its argmax == i.
-__device__ __forceinline__ void c3v_rows(uint32_t d, uint32_t t, uint32_t& r0, uint32_t& r1, uint32_t& r2,
-                                         uint32_t& r3) {
-  const s16x2v ts = __builtin_bit_cast(s16x2v, t);
-  const uint32_t a0 = __builtin_bit_cast(uint32_t, (s16x2v)(ts << 15) >> 15);  // halfword = -(argmax bit 0)
-  const uint32_t a1 = __builtin_bit_cast(uint32_t, (s16x2v)(ts << 14) >> 15);  // halfword = -(argmax bit 1)
-  // v_bitop3 truth-table index = (S0 << 2) | (S1 << 1) | S2 with S0 = d, S1 = a0, S2 = a1
-  r0 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x10);  // d & ~a0 & ~a1
-  r1 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x40);  // d &  a0 & ~a1
-  r2 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x20);  // d & ~a0 &  a1
-  r3 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x80);  // d &  a0 &  a1
-}
-// the argmax bytes of channels (2k, 2k+1) of a 4-channel dword -> bits 0-1 / 16-17
-__device__ __forceinline__ uint32_t c3v_pair_t(uint32_t id4, int k) {
-  return __builtin_amdgcn_perm(id4, id4, k ? 0x0c030c02u : 0x0c010c00u);
-}
-
-constexpr int C3V_P = 64 * 256;                  // dz3 operand image: [64 positions][128 co] bf16
-constexpr int C3V_DA = 100 * 256;                // da2 fp32 [100][64], one buffer
-constexpr int C3V_AM = 6400;                     // pool2 codes of one image
-constexpr int C3V_OFF_DA = C3V_P, C3V_OFF_AM = C3V_P + 2 * C3V_DA;
-constexpr int C3V_DLDS = C3V_OFF_AM + 2 * C3V_AM;  // 80384
-constexpr int C3V_XRS = 80;                      // a2 rows (bf16) of the wgrad B image: conflict-free tr16 reads
-constexpr int C3V_X = 100 * C3V_XRS * 2;         // 16000
-constexpr int C3V_D = 64 * 128;                  // 8192: [64 window-ordered rows][64 co] bf16
-constexpr int C3V_WLDS = 2 * (C3V_X + C3V_D);    // 48384
-constexpr int C3V_LDS = C3V_DLDS > C3V_WLDS ? C3V_DLDS : C3V_WLDS;
-static_assert(2 * C3V_LDS <= 160 * 1024, "two conv3 backward v2 workgroups per CU");
-
-__device__ __forceinline__ int c3v_p_off(int pos, int chunk) { return pos * 256 + ((chunk ^ (pos & 15)) << 4); }
-__device__ __forceinline__ int c3v_da_off(int y, int x, int c16) {
-  return (y * 10 + x) * 256 + ((c16 ^ ((x + 8 * (y & 1)) & 15)) << 4);
-}
-__device__ __forceinline__ int c3v_d_off(int r, int byte) {  // byte offset inside a 128-B row
-  const int g = ((r >> 1) & 1) | ((r >> 2) & 2);
-  return r * 128 + ((((byte >> 5) ^ g)) << 5) + (byte & 31);
-}
-
-#if defined(RINGDP_C3V_STAMP)
-// diagnostic build only: s_memtime stamps of WG 0's waves, [wave][image][slot]
-__device__ unsigned long long g_c3v_stamp[4][16][16];
-#define C3V_STAMP(img, slot)                                                                         \
-  do {                                                                                               \
-    if (blockIdx.x == 0 && (img) < 16) {                                                             \
-      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                    \
-      if ((threadIdx.x & 63) == 0) g_c3v_stamp[threadIdx.x >> 6][(img)][(slot)] = t_;                \
-    }                                                                                                \
-  } while (0)
-#else
-#define C3V_STAMP(img, slot) \
-  do {                       \
-  } while (0)
-#endif
-
-__device__ void c3v_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
-                               const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
-                               bf16* __restrict__ dz2, int b_first, int b_end, int b_step) {
-  char* P = smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3D_OFF);
-  bf16x8 aw[36];  // [tap][kstep] weight fragments of this wave's 16 input channels
-#pragma unroll
-  for (int j = 0; j < 36; ++j) aw[j] = pk[(wave * 36 + j) * 64 + lane];
-  uint4 pda = make_uint4(0, 0, 0, 0);
-  uint2 pid = make_uint2(0, 0);
-  auto load_pre = [&](int bb) {
-    pda = reinterpret_cast<const uint4*>(da3m + (int64_t)bb * 2048)[tid];
-    pid = reinterpret_cast<const uint2*>(idx3 + (int64_t)bb * 2048)[tid];
-  };
-  // expansion item: window w = tid >> 4, channels 8*(tid & 15) .. +7 -> its 4 positions in P
-  auto expand = [&]() {
-    const int ew = tid >> 4, ec8 = tid & 15;
-    uint32_t rr[4][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t d = k == 0 ? pda.x : k == 1 ? pda.y : k == 2 ? pda.z : pda.w;
-      const uint32_t t = c3v_pair_t(k < 2 ? pid.x : pid.y, k & 1);
-      c3v_rows(d, t, rr[0][k], rr[1][k], rr[2][k], rr[3][k]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int pos = (2 * (ew >> 2) + (i >> 1)) * 8 + 2 * (ew & 3) + (i & 1);
-      *reinterpret_cast<uint4*>(P + c3v_p_off(pos, ec8)) = make_uint4(rr[i][0], rr[i][1], rr[i][2], rr[i][3]);
-    }
-  };
-  auto masked_add = [](f32x4& g, uint32_t cw, int sh, const f32x4& d) {
-    const u8x4 mb = __builtin_bit_cast(u8x4, (cw >> sh) & 0x01010101u);  // v_cvt_f32_ubyte{0..3}
-#pragma unroll
-    for (int j = 0; j < 4; ++j) g[j] = fmaf(d[j], (float)mb[j], g[j]);
-  };
-  // MFMA + col2im of the image in P into DA; with POOL the pool2 + ReLU backward x-steps of the previous
-  // image (gather over the 4 windows covering each z2 position, masked by the one-hot code bits) run
-  // between the tap groups.  Every lane-dependent address is derived inside the phase from an opaque copy
-  // of the lane id, and each pool2 step re-derives its own from an opaque base (asm barriers): otherwise
-  // the compiler hoists ~60 swizzled addresses out of the image loop and spills.
-  int kimg = 0;
-  (void)kimg;
-  auto phase = [&](auto pool_c, char* DA, const char* DAp, const uint8_t* AMp, bf16* dstp) {
-    constexpr bool POOL = decltype(pool_c)::value;
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int r16 = ln & 15, g4 = ln >> 4;
-    const int px0 = r16 & 7, py0 = r16 >> 3;
-    const int c16 = 4 * wave + g4;  // this lane's 16-B chunk of a da2 row (4 input channels)
-    // col2im target (y, x) = (2 mt + py0 + ty, px0 + tx); chunk' = c16 ^ x ^ 8 (y & 1) (x <= 9), and the
-    // row base is a multiple of 256 B, so  addr = (KS[tx] ^ 128 (ty & 1)) + const(mt, ty, tx)
-    int KS[3];
-#pragma unroll
-    for (int tx = 0; tx < 3; ++tx) KS[tx] = (py0 * 10 + px0) * 256 + ((c16 ^ (px0 + tx) ^ (8 * py0)) << 4);
-    // pool2 item: z2 row y = wave + 4 g4 (waves 0-2: rows w, w+4, w+8; wave 3: rows 3, 7), channel quad r16
-    const int py2 = wave + 4 * g4;
-    const bool pact = py2 <= 10;
-    const int rowA = min(py2, 9), rowB = min(max(py2 - 1, 0), 9);  // idle lanes read valid addresses
-    const int sA = py2 <= 9 ? 0 : 4, sB = py2 >= 1 ? 2 : 4;        // shift 4: a bit that is never set
-    const int BA = rowA * 2560 + ((r16 ^ (8 * (rowA & 1))) << 4), BB = rowB * 2560 + ((r16 ^ (8 * (rowB & 1))) << 4);
-    const int CA = rowA * 640 + 4 * r16, CB = rowB * 640 + 4 * r16;
-    // zero the da2 positions the first (plain-store) taps of m-tiles 0 and 2 do not cover: rows 2,3,6,7,8,9
-    // and x = 8,9 of rows 0,1,4,5 (68 positions x this wave's 4 chunks)
-#pragma unroll
-    for (int it = 0; it < 5; ++it) {
-      const int i = ln + 64 * it;
-      if (i < 68 * 4) {
-        const int q = i >> 2, c = 4 * wave + (i & 3);
-        const int qd = (q * 205) >> 11;  // q / 10 for q < 68
-        const int yz = qd < 2 ? qd + 2 : (qd < 4 ? qd + 4 : 8 + (qd - 4));
-        const int y = q < 60 ? yz : ((q - 60) >> 1) + ((q - 60) >= 4 ? 2 : 0);
-        const int x = q < 60 ? q - 10 * qd : 8 + ((q - 60) & 1);
-        *reinterpret_cast<f32x4*>(DA + c3v_da_off(y, x, c)) = zero_f32x4();
-      }
-    }
-    // pool2 over window columns s = 0..10: the windows of column s add to z2 column s (code bits dx = 0)
-    // and carry into column s+1 (dx = 1).  A step's LDS reads are issued before the MFMAs of its tap group
-    // and consumed after them (their latency hides under the MFMAs, their registers live one group only).
-    uint32_t nna = 0, nnb = 0;
-    f32x4 nea = zero_f32x4(), neb = zero_f32x4(), carry = zero_f32x4();
-    auto p2_issue = [&](int x) {
-      if (x > 9) return;
-      int ba = BA, bb = BB;
-      asm volatile("" : "+v"(ba), "+v"(bb));
-      nna = *reinterpret_cast<const uint32_t*>(AMp + CA + x * 64);
-      nnb = *reinterpret_cast<const uint32_t*>(AMp + CB + x * 64);
-      nea = *reinterpret_cast<const f32x4*>(DAp + ((ba ^ (x << 4)) + x * 256));
-      neb = *reinterpret_cast<const f32x4*>(DAp + ((bb ^ (x << 4)) + x * 256));
-    };
-    auto p2_finish = [&](int x) {
-      f32x4 out = carry;
-      if (x <= 9) {
-        masked_add(out, nna, sA, nea);
-        masked_add(out, nnb, sB, neb);
-        carry = zero_f32x4();
-        masked_add(carry, nna, sA + 1, nea);
-        masked_add(carry, nnb, sB + 1, neb);
-      }
-      if (pact)
-        *reinterpret_cast<bf16x4*>(dstp + (py2 * 11 + x) * 64 + 4 * r16) =
-            bf16x4{(bf16)out[0], (bf16)out[1], (bf16)out[2], (bf16)out[3]};
-    };
-    // m-tiles (two dz3 rows each) in two passes of a far-apart pair, (0, 2) then (1, 3), alternating tap by
-    // tap: consecutive groups then write disjoint da2 rows, so each group's col2im read is issued one group
-    // early (before the previous group's MFMAs) and its LDS latency hides under them.  Within a pass the
-    // pair's 8 B fragments stay live across the 9 taps.
-    int step = 0;
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      bf16x8 bfr[2][4];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          bfr[u][ks] = *reinterpret_cast<const bf16x8*>(P + c3v_p_off(16 * (pass + 2 * u) + r16, 4 * ks + g4));
-      auto target = [&](int u, int tap) {
-        const int mt = pass + 2 * u, ty = tap / 3, tx = tap % 3;
-        return reinterpret_cast<f32x4*>(DA + ((KS[tx] ^ (128 * (ty & 1))) + (2 * mt + ty) * 2560 + tx * 256));
-      };
-      // first writers: taps 0 of m-tiles 0 and 2 (rows 0,1 / 4,5, x 0-7); everything else read-add-writes
-      f32x4 nold = pass == 0 ? zero_f32x4() : *target(0, 0);
-#pragma unroll
-      for (int g = 0; g < 18; ++g) {
-        const int u = g & 1, tap = g >> 1;
-        f32x4* dv = target(u, tap);
-        const f32x4 old = nold;
-        if (g + 1 < 18) {
-          const int u1 = (g + 1) & 1, t1 = (g + 1) >> 1;
-          nold = (pass == 0 && t1 == 0) ? zero_f32x4() : *target(u1, t1);
-        }
-        const bool p2 = POOL && step % 3 == 0 && step / 3 < 11;
-        if (p2) p2_issue(step / 3);
-        __builtin_amdgcn_sched_barrier(0);
-        f32x4 acc = zero_f32x4();
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) acc = mfma16x16x32(aw[tap * 4 + ks], bfr[u][ks], acc);
-        __builtin_amdgcn_sched_barrier(0);
-        if (p2) p2_finish(step / 3);
-        *dv = old + acc;
-        asm volatile("" ::: "memory");  // LDS program order: the pair's next read stays behind this write
-        ++step;
-        if (g == 17) C3V_STAMP(kimg, 5 + 2 * pass);
-      }
-    }
-  };
-  int b = b_first, k = 0, prev = -1;
-  if (b < b_end) load_pre(b);
-  for (; b < b_end; b += b_step, ++k) {
-    const int s = k & 1;
-    kimg = k;
-    C3V_STAMP(kimg, 0);
-    __syncthreads();  // [A] P, DA[s], AM[s] free (MFMA / pool2 of earlier images done)
-    C3V_STAMP(kimg, 1);
-    c_dma_wait();     // this image's compact gradient (registers) and the previous image's codes (AM[s^1])
-    C3V_STAMP(kimg, 2);
-    expand();
-    C3V_STAMP(kimg, 9);
-    codes_glds(idx2, b, reinterpret_cast<uint8_t*>(smem + C3V_OFF_AM + s * C3V_AM), wave, lane);
-    C3V_STAMP(kimg, 10);
-    if (b + b_step < b_end) load_pre(b + b_step);
-    C3V_STAMP(kimg, 3);
-    __syncthreads();  // [B] P complete; DA[s^1] / AM[s^1] of the previous image complete
-    C3V_STAMP(kimg, 4);
-    char* DA = smem + C3V_OFF_DA + s * C3V_DA;
-    if (prev >= 0)
-      phase(std::true_type{}, DA, smem + C3V_OFF_DA + (s ^ 1) * C3V_DA,
-            reinterpret_cast<const uint8_t*>(smem + C3V_OFF_AM + (s ^ 1) * C3V_AM), dz2 + (int64_t)prev * 121 * 64);
-    else
-      phase(std::false_type{}, DA, nullptr, nullptr, nullptr);
-    prev = b;
-  }
-  if (prev >= 0) {  // the last image's pool2 backward
-    const int s = (k - 1) & 1;
-    c_dma_wait();
-    __syncthreads();
-    // (the phase without MFMA work: pool2 steps only; DA argument unused)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int r16 = ln & 15, g4 = ln >> 4;
-    const int py2 = wave + 4 * g4;
-    const bool pact = py2 <= 10;
-    const int rowA = min(py2, 9), rowB = min(max(py2 - 1, 0), 9);
-    const int sA = py2 <= 9 ? 0 : 4, sB = py2 >= 1 ? 2 : 4;
-    const char* DAp = smem + C3V_OFF_DA + s * C3V_DA;
-    const uint8_t* AMp = reinterpret_cast<const uint8_t*>(smem + C3V_OFF_AM + s * C3V_AM);
-    bf16* dstp = dz2 + (int64_t)prev * 121 * 64;
-#pragma unroll
-    for (int x = 0; x < 11; ++x) {
-      f32x4 g = zero_f32x4();
-#pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        const int wx = x - dx;
-        if (wx < 0 || wx > 9) continue;
-        masked_add(g, *reinterpret_cast<const uint32_t*>(AMp + rowA * 640 + wx * 64 + 4 * r16), sA + dx,
-                   *reinterpret_cast<const f32x4*>(DAp + c3v_da_off(rowA, wx, r16)));
-        masked_add(g, *reinterpret_cast<const uint32_t*>(AMp + rowB * 640 + wx * 64 + 4 * r16), sB + dx,
-                   *reinterpret_cast<const f32x4*>(DAp + c3v_da_off(rowB, wx, r16)));
-      }
-      if (pact)
-        *reinterpret_cast<bf16x4*>(dstp + (py2 * 11 + x) * 64 + 4 * r16) = bf16x4{(bf16)g[0], (bf16)g[1], (bf16)g[2], (bf16)g[3]};
-    }
-  }
-}
-
-// wgrad v2: the workgroup pair (h = 0, 1) of an image slice covers output channels 64h .. 64h+63 (4
-// m-tiles) x all 36 n-tiles of dW3t [576][128]; wave w owns n-tiles 9w .. 9w+8.
-__device__ void c3v_wgrad_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
-                               const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B, int nslices,
-                               int slice, int h) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
-  auto Xb = [&](int s) { return reinterpret_cast<bf16*>(smem + s * (C3V_X + C3V_D)); };
-  auto Db = [&](int s) { return smem + s * (C3V_X + C3V_D) + C3V_X; };
-  f32x4 acc[4][9];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 9; ++j) acc[i][j] = zero_f32x4();
-  const int per = cdiv(B, nslices);
-  const int b_lo = slice * per, b_hi = min(B, b_lo + per);
-  // staged next image (registers): a2 chunks t + 256 k, this thread's 4 channels of compact d(a3) + argmax
-  // (named registers, not an array: a lambda-captured array with guarded element loads went to scratch)
-  uint4 xr0 = make_uint4(0, 0, 0, 0), xr1 = xr0, xr2 = xr0, xr3 = xr0;
-  uint2 dr = make_uint2(0, 0);
-  uint32_t ir = 0;
-  const int ew = tid >> 4, ec4 = tid & 15;
-  const bool x3 = tid < 800 - 768;  // the 4th a2 chunk: threads 0..31
-  auto load = [&](int bb) {
-    const uint4* src = reinterpret_cast<const uint4*>(a2 + (int64_t)bb * 6400) + tid;
-    xr0 = src[0];
-    xr1 = src[256];
-    xr2 = src[512];
-    if (x3) xr3 = src[768];
-    dr = *reinterpret_cast<const uint2*>(da3m + (int64_t)bb * 2048 + ew * 128 + 64 * h + 4 * ec4);
-    ir = *reinterpret_cast<const uint32_t*>(idx3 + (int64_t)bb * 2048 + ew * 128 + 64 * h + 4 * ec4);
-  };
-  auto stage = [&](int s) {
-    bf16* X = Xb(s);
-    *reinterpret_cast<uint4*>(X + (tid >> 3) * C3V_XRS + (tid & 7) * 8) = xr0;
-    *reinterpret_cast<uint4*>(X + ((tid + 256) >> 3) * C3V_XRS + (tid & 7) * 8) = xr1;
-    *reinterpret_cast<uint4*>(X + ((tid + 512) >> 3) * C3V_XRS + (tid & 7) * 8) = xr2;
-    if (x3) *reinterpret_cast<uint4*>(X + ((tid + 768) >> 3) * C3V_XRS + (tid & 7) * 8) = xr3;
-    uint32_t r[4][2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) c3v_rows(k ? dr.y : dr.x, c3v_pair_t(ir, k), r[0][k], r[1][k], r[2][k], r[3][k]);
-    char* D = Db(s);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<uint2*>(D + c3v_d_off(4 * ew + i, 8 * ec4)) = make_uint2(r[i][0], r[i][1]);
-  };
-  if (b_lo < b_hi) {
-    load(b_lo);
-    c_dma_wait();
-    stage(0);
-    if (b_lo + 1 < b_hi) load(b_lo + 1);
-  }
-  for (int b = b_lo, s = 0; b < b_hi; ++b, s ^= 1) {
-    __syncthreads();  // buffers s complete; buffers s^1 free (MFMAs of image b-1 done)
-    if (b + 1 < b_hi) {
-      c_dma_wait();
-      stage(s ^ 1);
-      if (b + 2 < b_hi) load(b + 2);
-    }
-    const bf16* X = Xb(s);
-    const char* D = Db(s);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int kb = ks * 32 + grp * 8;
-      bf16x8 af[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bf16x4 lo = lds_read_tr16(reinterpret_cast<const bf16*>(D + c3v_d_off(kb + q, 32 * i + 8 * p)));
-        const bf16x4 hi = lds_read_tr16(reinterpret_cast<const bf16*>(D + c3v_d_off(kb + 4 + q, 32 * i + 8 * p)));
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      const int x0 = win_pos(kb + q, 10), x1 = win_pos(kb + 4 + q, 10);
-#pragma unroll
-      for (int j = 0; j < 9; ++j) {
-        const int n0 = (9 * wave + j) * 16;  // n = tap*64 + ci
-        const int tap = n0 >> 6, c0 = n0 & 63;
-        const int shift = (tap / 3) * 10 + tap % 3;
-        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3V_XRS + c0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C3V_XRS + c0 + 4 * p);
-        const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i][j] = mfma16x16x32(af[i], bf, acc[i][j]);
-      }
-    }
-  }
-  float* slab = slabs + (int64_t)slice * C3_WSLAB;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = 64 * h + i * 16 + grp * 4;
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int n = (9 * wave + j) * 16 + g16;
-      *reinterpret_cast<f32x4*>(slab + (int64_t)n * 128 + co) = acc[i][j];
-    }
-  }
-}
-
-__global__ __launch_bounds__(256, 2) void conv3_bwd2_kernel(const bf16* __restrict__ a2,
-                                                            const uint8_t* __restrict__ idx2,
-                                                            const bf16* __restrict__ da3m,
-                                                            const uint8_t* __restrict__ idx3,
-                                                            const bf16* __restrict__ packed,
-                                                            bf16* __restrict__ dz2, int B,
-                                                            float* __restrict__ slabs, int n_wgrad,
-                                                            int n_dgrad, int b_dgrad) {
-  __shared__ __attribute__((aligned(16))) char smem[C3V_LDS];
-  const int blk = blockIdx.x;
-  int b_first = blk, b_end = b_dgrad, b_step = n_dgrad;
-  if (blk >= n_dgrad) {
-    const int w = blk - n_dgrad;
-#if defined(RINGDP_C3V_ABL_NOWG)
-    return;  // ablation: the dgrad role alone (timing only)
-#endif
-    c3v_wgrad_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w >> 1, w & 1);
-    if (dz2 == nullptr || b_dgrad >= B) return;
-    __syncthreads();  // LDS changes role
-    b_first = b_dgrad + w;
-    b_end = B;
-    b_step = 2 * n_wgrad;
-  }
-  c3v_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, b_first, b_end, b_step);
 }
 
 __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
@@ -2187,6 +2113,35 @@ void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, v
     conv1_fwd_kernel<false, false><<<grid, 256, 0, s>>>(x, pk, b1, a1b, idx1, B, mean, inv_std, in_scale, none, nullptr, grid);
 }
 
+void cn_forward_fused(const void* x, bool u8, const float* const* w, const float* b1, const float* b2,
+                      const float* b3, const float* bfc, void* packed, void* a1, uint8_t* idx1, void* a2,
+                      uint8_t* idx2, void* a3, uint8_t* idx3, float* logits, int B, float mean, float inv_std,
+                      float in_scale, hipStream_t s) {
+  const int conv = clampi(B, 1, wpc("FF", 1) * num_cus());  // 121 KiB LDS: one 512-thread workgroup per CU
+  const PackSrc ws{w[0], w[1], w[2], w[3]};
+  bf16* pk = static_cast<bf16*>(packed);
+  bf16 *a1b = static_cast<bf16*>(a1), *a2b = static_cast<bf16*>(a2), *a3b = static_cast<bf16*>(a3);
+  static const int ablate = [] { const char* v = getenv("RINGDP_FF_ABLATE"); return v ? atoi(v) : 0; }();
+  static const bool inpack = [] { const char* v = getenv("RINGDP_FF_INPACK"); return v && atoi(v) != 0; }();
+  if (inpack) {  // fragments from the fp32 masters in every workgroup + pack workgroups in this launch
+    const int grid = conv + cdiv(PACK_TOTAL, 1024);
+    if (u8)
+      fused_fwd_kernel<true, true><<<grid, 512, 0, s>>>(x, nullptr, ws, pk, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
+                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+    else
+      fused_fwd_kernel<false, true><<<grid, 512, 0, s>>>(x, nullptr, ws, pk, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
+                                                         idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+    return;
+  }
+  pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(ws, pk);
+  if (u8)
+    fused_fwd_kernel<true, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
+                                                       idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+  else
+    fused_fwd_kernel<false, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
+                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+}
+
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,
                   hipStream_t s) {
   const int grid = clampi(B, 1, wpc("C2F", 3) * num_cus());  // 49 KiB LDS, 157 VGPRs: 3 per CU (303 -> 260 us)
@@ -2282,34 +2237,6 @@ static void c12_split(int B, int& nd, int& ws) {
 
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 3 * num_cus()); }
 
-// Kernel variants selectable at run time (A/B tests and measurements): "c3_bwd" 1 = the round-3 conv3
-// backward (default), 2 = the software-pipelined v2 (in development; env RINGDP_C3_BWD).
-static int g_c3_bwd = -1;
-static int c3_bwd_version() {
-  if (g_c3_bwd < 0) {
-    const char* v = getenv("RINGDP_C3_BWD");
-    g_c3_bwd = v ? atoi(v) : 1;
-  }
-  return g_c3_bwd;
-}
-bool cn_set_variant(const char* name, int value) {
-  if (std::strcmp(name, "c3_bwd") == 0 && (value == 1 || value == 2)) {
-    g_c3_bwd = value;
-    return true;
-  }
-  return false;
-}
-// diagnostic builds (-DRINGDP_C3V_STAMP): copy WG 0's stamps [4 waves][16 images][16 slots] (u64)
-bool cn_debug_stamps(void* host_out) {
-#if defined(RINGDP_C3V_STAMP)
-  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_c3v_stamp), sizeof(g_c3v_stamp)) == hipSuccess;
-#else
-  (void)host_out;
-  return false;
-#endif
-}
-int cn_get_variant(const char* name) { return std::strcmp(name, "c3_bwd") == 0 ? c3_bwd_version() : -1; }
-
 int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, fc_imgs(B)) * FC_SLAB; }
 int64_t cn_conv3_slab_floats(int B, bool dgrad) {
   int nd, ws;
@@ -2342,14 +2269,9 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
   else
     fc_bwd_kernel<false><<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
                                             static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), CeFuse{});
-  if (c3_bwd_version() == 1)
-    conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
-                                               idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
-                                               c3_slabs, ws, nd, c3_dgrad_images(B, nd));
-  else
-    conv3_bwd2_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
-                                                idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
-                                                c3_slabs, ws, nd, c3_dgrad_images(B, nd));
+  conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
+                                             idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
+                                             c3_slabs, ws, nd, c3_dgrad_images(B, nd));
   ReduceList r{seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
                seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
                seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)};

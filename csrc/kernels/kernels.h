@@ -170,10 +170,13 @@ void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2,
 void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const float* bfc, float* logits,
                      void* a3, uint8_t* idx3, int B, hipStream_t s);
 
-// Run-time kernel variant knobs (A/B tests): returns false for an unknown name / value.
-bool cn_set_variant(const char* name, int value);
-int cn_get_variant(const char* name);
-bool cn_debug_stamps(void* host_out);  // 4*16*16 u64; false unless built with -DRINGDP_C3V_STAMP
+// F1+F2+F3 in one launch (conv1 -> conv2 -> conv3 + fc1 per image, a1 / a2 kept in LDS between the
+// layers; also packs the bf16 weight fragments into `packed` for the backward).  w = {w1, w2, w3, wfc}.
+void cn_forward_fused(const void* x, bool u8, const float* const* w, const float* b1, const float* b2,
+                      const float* b3, const float* bfc, void* packed, void* a1, uint8_t* idx1, void* a2,
+                      uint8_t* idx2, void* a3, uint8_t* idx3, float* logits, int B, float mean, float inv_std,
+                      float in_scale, hipStream_t s);
+
 // Workspace sizes (floats) of the backward weight-gradient slabs.
 int64_t cn_fc_slab_floats(int B, bool dgrad);
 int64_t cn_conv3_slab_floats(int B, bool dgrad);

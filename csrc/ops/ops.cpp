@@ -378,6 +378,53 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv1_fwd_pack(const at::Tenso
   return {a1, idx, packed};
 }
 
+std::vector<at::Tensor> cn_forward_buffers(const at::Tensor& x) {
+  int64_t B;
+  bool u8;
+  check_input(x, B, u8);
+  auto bf = x.options().dtype(at::kBFloat16), u = x.options().dtype(at::kByte);
+  return {at::empty({B, 13, 13, 32}, bf), at::empty({B, 13, 16, 16}, u), at::empty({B, 10, 10, 64}, bf),
+          at::empty({B, 10, 10, 64}, u), at::empty({kern::cn_packed_elems()}, bf)};
+}
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_forward_fused(
+    const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
+    const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& wfc, const at::Tensor& bfc, double mean, double std,
+    double in_scale, at::Tensor a1, at::Tensor idx1, at::Tensor a2, at::Tensor idx2, at::Tensor packed) {
+  int64_t B;
+  bool u8;
+  check_input(x, B, u8);
+  RINGDP_CHECK(x.is_contiguous(), "convnet input must be contiguous");
+  check_f32_out(w1, {32, 1, 5, 5}, "conv1 weight");
+  check_f32_out(w2, {64, 32, 3, 3}, "conv2 weight");
+  check_f32_out(w3, {128, 64, 3, 3}, "conv3 weight");
+  check_f32_out(wfc, {10, 2048}, "fc1 weight");
+  check_f32_out(b1, {32}, "conv1 bias");
+  check_f32_out(b2, {64}, "conv2 bias");
+  check_f32_out(b3, {128}, "conv3 bias");
+  check_f32_out(bfc, {10}, "fc1 bias");
+  check_act(a1, {B, 13, 13, 32}, at::kBFloat16, "a1 buffer");
+  check_act(idx1, {B, 13, 16, 16}, at::kByte, "conv1 code buffer");
+  check_act(a2, {B, 10, 10, 64}, at::kBFloat16, "a2 buffer");
+  check_act(idx2, {B, 10, 10, 64}, at::kByte, "pool2 code buffer");
+  check_packed(packed);
+  auto opt = x.options();
+  at::Tensor logits = at::empty({B, 10}, opt.dtype(at::kFloat));
+  at::Tensor a3 = at::empty({B, 16, 128}, opt.dtype(at::kBFloat16));
+  at::Tensor idx3 = at::empty({B, 16, 128}, opt.dtype(at::kByte));
+  const float* pw[4] = {w1.data_ptr<float>(), w2.data_ptr<float>(), w3.data_ptr<float>(), wfc.data_ptr<float>()};
+  if (B == 0) {
+    kern::cn_pack_weights(pw[0], pw[1], pw[2], pw[3], packed.data_ptr(), cur_stream(x));
+    return {logits, a3, idx3};
+  }
+  kern::cn_forward_fused(x.data_ptr(), u8, pw, b1.data_ptr<float>(), b2.data_ptr<float>(), b3.data_ptr<float>(),
+                         bfc.data_ptr<float>(), packed.data_ptr(), a1.data_ptr(), idx1.data_ptr<uint8_t>(),
+                         a2.data_ptr(), idx2.data_ptr<uint8_t>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
+                         logits.data_ptr<float>(), static_cast<int>(B), static_cast<float>(mean),
+                         static_cast<float>(1.0 / std), static_cast<float>(in_scale), cur_stream(x));
+  return {logits, a3, idx3};
+}
+
 std::tuple<at::Tensor, at::Tensor> cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed,
                                                 const at::Tensor& b2) {
   const int64_t B = a1.size(0);

@@ -64,6 +64,13 @@ std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::T
 std::tuple<at::Tensor, at::Tensor> cn_conv2_fwd(const at::Tensor& a1, const at::Tensor& packed,
                                                 const at::Tensor& b2);
 // conv1 forward that also packs every layer's weights in the same launch: (a1, idx1, packed)
+// Whole ConvNet forward in one launch: writes a1 / idx1 / a2 / idx2 / packed (cn_forward_buffers) and
+// returns logits, a3, idx3.
+std::vector<at::Tensor> cn_forward_buffers(const at::Tensor& x);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_forward_fused(
+    const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
+    const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& wfc, const at::Tensor& bfc, double mean, double std,
+    double in_scale, at::Tensor a1, at::Tensor idx1, at::Tensor a2, at::Tensor idx2, at::Tensor packed);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv1_fwd_pack(const at::Tensor& x, const at::Tensor& w1,
                                                                  const at::Tensor& w2, const at::Tensor& w3,
                                                                  const at::Tensor& wfc, const at::Tensor& b1,

@@ -30,6 +30,8 @@ from . import grad_buffer
 
 # RINGDP_CN_FUSE12=0: conv1 / conv2 as separate autograd nodes with their own backward kernels (A/B)
 _FUSE12 = os.environ.get("RINGDP_CN_FUSE12", "1") != "0"
+# RINGDP_CN_FUSED_FWD=1: the whole forward in one launch (cn_forward_fused; A/B against the three-launch path)
+_FUSED_FWD = os.environ.get("RINGDP_CN_FUSED_FWD", "0") == "1"
 # RINGDP_CN_DEFER_REDUCE=0: conv3 / fc1 weight-gradient reduction in its own launch (A/B)
 _DEFER = os.environ.get("RINGDP_CN_DEFER_REDUCE", "1") != "0"
 # RINGDP_CN_HEAD_CE=0: ringdp's cross entropy on the ConvNet logits stays a separate node (A/B)
@@ -109,11 +111,16 @@ class _Conv12(torch.autograd.Function):
     (conv2 dgrad + wgrad, conv1 wgrad on the LDS-resident da1) and one reduction launch."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, w3, wfc, mean, std, in_scale):
-        # conv1's launch also packs every layer's bf16 MFMA fragments (w3 / wfc arrive detached: this
-        # node only reads them for the packing)
-        a1, idx1, packed = C.cn_conv1_fwd_pack(x, w1, w2, w3, wfc, b1, mean, std, in_scale)
-        a2, idx2 = C.cn_conv2_fwd(a1, packed, b2)
+    def forward(ctx, x, w1, b1, w2, b2, w3, wfc, mean, std, in_scale, bufs=None):
+        if bufs is not None:
+            # fused forward: _Conv3FC's launch (cn_forward_fused) fills these buffers, stream-ordered
+            # before any backward kernel reads them
+            a1, idx1, a2, idx2, packed = bufs
+        else:
+            # conv1's launch also packs every layer's bf16 MFMA fragments (w3 / wfc arrive detached:
+            # this node only reads them for the packing)
+            a1, idx1, packed = C.cn_conv1_fwd_pack(x, w1, w2, w3, wfc, b1, mean, std, in_scale)
+            a2, idx2 = C.cn_conv2_fwd(a1, packed, b2)
         z2 = a2.new_empty((1, 1, 1, 1)).expand(a1.shape[0], 11, 11, 64)  # placeholder, never read
         ctx.mark_non_differentiable(a2, idx2, packed)
         ctx.set_materialize_grads(False)
@@ -132,7 +139,7 @@ class _Conv12(torch.autograd.Function):
             dw1, db1, dw2, db2 = (grad_buffer(t) for t in (w1, b1, w2, b2))
             # also launches a reduction _Conv3FC / _HeadCE deferred into this one
             C.cn_conv12_bwd(x, idx1, a1, dz2, packed, dw2, db2, dw1, db1, *ctx.norm)
-            return None, dw1, db1, dw2, db2, None, None, None, None, None
+            return None, dw1, db1, dw2, db2, None, None, None, None, None, None
         # partially frozen: the separate kernels
         C.cn_flush_reduce(x.get_device())
         need_c1 = n[1] or n[2]
@@ -143,13 +150,18 @@ class _Conv12(torch.autograd.Function):
             dw1, db1 = grad_buffer(w1), grad_buffer(b1)
             C.cn_conv1_wgrad(x, da1, idx1, dw1, db1, *ctx.norm)
         return (None, dw1 if n[1] else None, db1 if n[2] else None, dw2 if n[3] else None,
-                db2 if n[4] else None, None, None, None, None, None)
+                db2 if n[4] else None, None, None, None, None, None, None)
 
 
 class _Conv3FC(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z2, a2, idx2, w3, b3, wfc, bfc, packed):
-        logits, a3, idx3 = C.cn_conv3_fc_fwd(a2, packed, b3, bfc)
+    def forward(ctx, z2, a2, idx2, w3, b3, wfc, bfc, packed, fused=None):
+        if fused is not None:  # (x, w1, b1, w2, b2, mean, std, in_scale, a1, idx1): the whole forward here
+            x, w1, b1, w2, b2, mean, std, in_scale, a1, idx1 = fused
+            logits, a3, idx3 = C.cn_forward_fused(x, w1, b1, w2, b2, w3, b3, wfc, bfc, mean, std, in_scale,
+                                                  a1, idx1, a2, idx2, packed)
+        else:
+            logits, a3, idx3 = C.cn_conv3_fc_fwd(a2, packed, b3, bfc)
         ctx.mark_non_differentiable(a3, idx3)
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(a2, idx2, a3, idx3, wfc, packed)
@@ -162,7 +174,7 @@ class _Conv3FC(torch.autograd.Function):
         w3, b3, wfc, bfc = ctx.params
         n = ctx.needs_input_grad
         if dlogits is None:
-            return (None,) * 8
+            return (None,) * 9
         grads = [grad_buffer(p) for p in (w3, b3, wfc, bfc)]
         need_in = n[0]
         defer = _defer_reduce((w3, b3, wfc, bfc), grads, need_in)
@@ -170,7 +182,7 @@ class _Conv3FC(torch.autograd.Function):
                                 *grads, defer_reduce=defer)
         dw3, db3, dwfc, dbfc = grads
         return (dz2 if need_in else None, None, None, dw3 if n[3] else None, db3 if n[4] else None,
-                dwfc if n[5] else None, dbfc if n[6] else None, None)
+                dwfc if n[5] else None, dbfc if n[6] else None, None, None)
 
 
 class _HeadCE(torch.autograd.Function):
@@ -235,14 +247,22 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         x = x.float()
         mean, std, scale = 0.0, 1.0, 1.0
     x = x.contiguous()
-    if _FUSE12:
+    fused = None
+    if _FUSE12 and _FUSED_FWD:
+        bufs = C.cn_forward_buffers(x)
+        z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
+                                             conv3.weight.detach(), fc1.weight.detach(), mean, std, scale, bufs)
+        fused = (x, conv1.weight.detach(), conv1.bias.detach(), conv2.weight.detach(), conv2.bias.detach(),
+                 mean, std, scale, bufs[0], bufs[1])
+    elif _FUSE12:
         z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
                                              conv3.weight.detach(), fc1.weight.detach(), mean, std, scale)
     else:
         packed = pack_weights(conv1, conv2, conv3, fc1)
         a1 = _Conv1.apply(x, conv1.weight, conv1.bias, packed, mean, std, scale)
         z2, a2, idx2 = _Conv2.apply(a1, conv2.weight, conv2.bias, packed)
-    logits, a3, idx3 = _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed)
+    logits, a3, idx3 = _Conv3FC.apply(z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed,
+                                      fused)
     if logits.requires_grad:
         # what ringdp's cross entropy needs to fuse itself into the head (head_cross_entropy)
         logits._ringdp_head = (z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed, a3, idx3)

@@ -295,38 +295,6 @@ def test_conv12_backward_fused(B, u8):
     assert rel_err(db1, b1q.grad) < 1.5e-2
 
 
-@pytest.mark.parametrize("B", [1, 3, 64, 257, 3000, 9000])
-def test_conv3_backward_v2_matches_v1(B):
-    """The software-pipelined conv3 backward (v2, default) against the round-3 kernel (v1): the weight
-    gradients accumulate the same MFMA products in the same order (bitwise equal); the data gradient's
-    col2im adds taps in a different order (fp32 rounding only).  B=9000 exercises the stolen dgrad images
-    on the wgrad workgroups, B >= 3000 the multi-image software pipeline."""
-    torch.manual_seed(29 + B)
-    dev = torch.device("cuda")
-    ws = weights(dev, B + 8)
-    w3, b3, wf, bfc = ws[4], ws[5], ws[6], ws[7]
-    a2, idx2 = pool2_ref(torch.randn(B, 11, 11, 64, device=dev).bfloat16())
-    pk = packed(ws)
-    logits, a3, idx3 = C().cn_conv3_fc_fwd(a2, pk, b3, bfc)
-    dl = torch.randn(B, 10, device=dev)
-    outs = {}
-    old = C().cn_get_variant("c3_bwd")
-    try:
-        for v in (1, 2):
-            C().cn_set_variant("c3_bwd", v)
-            g = [torch.empty_like(t) for t in (w3, b3, wf, bfc)]
-            dz2 = C().cn_conv3_fc_bwd(a2, idx2, a3, idx3, wf, dl, pk, True, *g)
-            outs[v] = g + [dz2]
-    finally:
-        C().cn_set_variant("c3_bwd", old)
-    for a, b in zip(outs[1][:4], outs[2][:4]):
-        assert torch.equal(a, b)
-    d1, d2 = outs[1][4].float(), outs[2][4].float()
-    assert rel_err(d2, d1) < 1e-2
-    # fp32 reordering: at most a last-bit bf16 difference on a small fraction of the elements
-    assert float((d1 != d2).float().mean()) < 0.02
-
-
 def test_wgrad_deterministic():
     """Slab reductions and the dgrad K-group sums run in a fixed order: two identical backward calls
     are bitwise equal."""
@@ -432,3 +400,32 @@ def test_synth_images_deterministic():
     b = C().synth_u8_images(64, 28, 28, 10, 5, dev)
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     assert a[0].shape == (64, 1, 28, 28) and int(a[1].max()) < 10
+
+
+@pytest.mark.parametrize("B,u8", [(1, True), (100, True), (300, False), (1031, True), (5000, True)])
+def test_fused_forward_matches_separate_kernels(B, u8):
+    """cn_forward_fused (conv1 -> conv2 -> conv3 + fc1 in one launch, a1 / a2 handed over in LDS) writes
+    the same a1 / idx1 / a2 / idx2 / a3 / idx3 / packed bytes as the three-launch path, and the same
+    logits (bit-identical where the separate path also runs fc1 inside conv3's launch, B <= 4096)."""
+    torch.manual_seed(B)
+    ws = weights("cuda", seed=B)
+    w1, b1, w2, b2, w3, b3, wf, bfc = ws
+    if u8:
+        x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device="cuda")
+        norm = NORM_U8
+    else:
+        x = torch.randn(B, 1, 28, 28, device="cuda")
+        norm = NORM_F32
+    a1, i1, pk = C().cn_conv1_fwd_pack(x, w1, w2, w3, wf, b1, *norm)
+    a2, i2 = C().cn_conv2_fwd(a1, pk, b2)
+    lg, a3, i3 = C().cn_conv3_fc_fwd(a2, pk, b3, bfc)
+    bufs = C().cn_forward_buffers(x)
+    lg_f, a3_f, i3_f = C().cn_forward_fused(x, w1, b1, w2, b2, w3, b3, wf, bfc, *norm, *bufs)
+    torch.cuda.synchronize()
+    for name, want, got in (("a1", a1, bufs[0]), ("idx1", i1, bufs[1]), ("a2", a2, bufs[2]), ("idx2", i2, bufs[3]),
+                            ("packed", pk, bufs[4]), ("a3", a3, a3_f), ("idx3", i3, i3_f)):
+        assert torch.equal(want, got), name
+    if B <= 4096:
+        assert torch.equal(lg, lg_f)
+    else:
+        torch.testing.assert_close(lg_f, lg, rtol=1e-4, atol=1e-4)

@@ -30,7 +30,7 @@ def main():
         ts.append(a.elapsed_time(b) * 1000.0)
     ts.sort()
     print(json.dumps({"op": op, "B": B, "us_median": round(ts[len(ts) // 2], 1), "us_min": round(ts[0], 1),
-                      "ext": os.environ.get("RINGDP_EXT_PATH", "in-tree"), "c3_bwd": os.environ.get("RINGDP_C3_BWD", "")}))
+                      "ext": os.environ.get("RINGDP_EXT_PATH", "in-tree")}))
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 """Run one ConvNet kernel group repeatedly for PMC collection under rocprofv3 --pmc.
 
-python tools/pmc_run.py <op> [B] [iters]   op: conv3_fc_bwd | conv12_bwd | conv2_bwd | conv3_fc_fwd | conv2_fwd | conv1_fwd | conv1_wgrad
+python tools/pmc_run.py <op> [B] [iters]   op: fwd_fused | fwd_sep | conv3_fc_bwd | conv12_bwd | conv2_bwd | conv3_fc_fwd | conv2_fwd | conv1_fwd | conv1_wgrad
 """
 import sys
 
@@ -35,11 +35,25 @@ def build_ops(B):
     g3 = [torch.empty_like(t) for t in (w3, b3, wf, bfc)]
     g2 = [torch.empty_like(t) for t in (w2, b2)]
     g1 = [torch.empty_like(t) for t in (w1, b1)]
+    bufs = C.cn_forward_buffers(x)
+    labels = torch.randint(0, 10, (B,), device=dev)
+    loss, lse, cews = C.cross_entropy_fwd(logits, labels, -100, 0.0, 1)
+    one = torch.ones((), device=dev)
+
+    def fwd_sep():
+        a1_, i1_, pk_ = C.cn_conv1_fwd_pack(x, w1, w2, w3, wf, b1, *norm)
+        a2_, i2_ = C.cn_conv2_fwd(a1_, pk_, b2)
+        return C.cn_conv3_fc_fwd(a2_, pk_, b3, bfc)
+
     fns = {
+        "fwd_fused": lambda: C.cn_forward_fused(x, w1, b1, w2, b2, w3, b3, wf, bfc, *norm, *bufs),
+        "fwd_sep": fwd_sep,
         "conv1_fwd": lambda: C.cn_conv1_fwd(x, pk, b1, *norm),
         "conv2_fwd": lambda: C.cn_conv2_fwd(a1, pk, b2),
         "conv3_fc_fwd": lambda: C.cn_conv3_fc_fwd(a2, pk, b3, bfc),
         "conv3_fc_bwd": lambda: C.cn_conv3_fc_bwd(a2, i2, a3, i3, wf, dl, pk, True, *g3),
+        "conv3_fc_ce_bwd": lambda: C.cn_conv3_fc_ce_bwd(a2, i2, a3, i3, wf, logits, labels, lse, cews, one, -100,
+                                                        0.0, 1, pk, True, *g3, False),
         "conv3_fc_bwd_w": lambda: C.cn_conv3_fc_bwd(a2, i2, a3, i3, wf, dl, pk, False, *g3),
         "conv2_bwd_w": lambda: C.cn_conv2_bwd(a1, dz2, pk, False, *g2),
         "conv2_bwd": lambda: C.cn_conv2_bwd(a1, dz2, pk, True, *g2),
