@@ -88,6 +88,10 @@ def parse(argv=None):
                          "fp32: the ConvNet at the reference's precision (fp32 MFMA kernels)")
     ap.add_argument("--no-force-comm", action="store_true",
                     help="at world size 1 skip the bucket all-reduce (default: run it, the N>1 code path)")
+    ap.add_argument("--comm-stream", type=str, default="auto", choices=["auto", "side", "same"],
+                    help="N>1 bucket collectives inside the captured step: side HIP stream (overlaps backward; "
+                         "any second stream costs the graph its batched launch), the compute stream, or auto: "
+                         "both are captured during warmup and the faster one (max over ranks) is timed")
     ap.add_argument("--comm-stats-steps", type=int, default=20,
                     help="after the timed region: eager steps with device-timed bucket collectives and "
                          "comm-free graph replays for the exposed-comm estimate (0 = skip)")
@@ -277,6 +281,40 @@ def worker(args):
         graph = capture()
         use_graph = graph is not None
 
+    comm_stream_note = None
+    nat_pg = getattr(ddp, "_native_pg", None)
+    if use_graph and world > 1 and hasattr(nat_pg, "set_same_stream") and \
+            os.environ.get("RINGDP_COMM_SAME_STREAM") is None and args.comm_stream != "side":
+        # Placement of the bucket collectives in the captured step (a side stream forks
+        # the graph, and a forked graph loses HIP's batched packet launch: +1.2-2 us per kernel).
+        def time_graph(g, n=20):
+            sync()
+            dist.barrier()
+            sync()
+            t0 = time.perf_counter()
+            for i in range(n):
+                static_buf.copy_(pool[i % len(pool)][0], non_blocking=True)
+                g.replay()
+            sync()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item()) / n
+        t_side = time_graph(graph) if args.comm_stream == "auto" else None
+        nat_pg.set_same_stream(True)
+        g_same = capture()
+        if g_same is None:
+            nat_pg.set_same_stream(False)
+        else:
+            t_same = time_graph(g_same)
+            if t_side is not None and t_side < t_same:
+                nat_pg.set_same_stream(False)
+                del g_same
+            else:
+                graph = g_same
+            comm_stream_note = ("compute stream" if nat_pg.same_stream() else "side stream") + (
+                f" (autotuned: side {t_side * 1e3:.3f} ms, same {t_same * 1e3:.3f} ms per step)"
+                if t_side is not None else " (--comm-stream same)")
+
     def run_steps(n, g):
         loss = None
         for i in range(n):
@@ -341,8 +379,13 @@ def worker(args):
         lib = {"rccl": "RCCL", "xgmi": "ringdp xGMI kernels (IPC peer memory)"}.get(nat.backend_name(), nat.backend_name()) \
             if on_gpu else "host ring (gloo)"
         if world > 1:
+            where = ""
+            if on_gpu:
+                where = (f", collectives on the {comm_stream_note}" if comm_stream_note else
+                         (", compute stream" if getattr(nat, "same_stream", lambda: False)()
+                          else ", side HIP stream overlapped with backward"))
             comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
-                    f"cap {args.bucket_mb} MB" + (", side HIP stream overlapped with backward" if on_gpu else ""))
+                    f"cap {args.bucket_mb} MB" + where)
         elif force_comm:
             where = ("on the compute stream (a one-rank collective has nothing to overlap)"
                      if getattr(nat, "same_stream", lambda: False)() else "on the side stream")

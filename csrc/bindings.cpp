@@ -307,6 +307,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("set_timing", &GpuPG::set_timing)
       .def("timing", &GpuPG::timing)
       .def("same_stream", &GpuPG::same_stream)
+      .def("set_same_stream", &GpuPG::set_same_stream, py::call_guard<py::gil_scoped_release>())
       .def("watch_beacon", &GpuPG::watch_beacon, py::arg("beacon"),
            "watchdog-track the replays of a captured step through its ReplayBeacon")
       .def("join_into",

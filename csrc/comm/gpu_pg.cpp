@@ -111,6 +111,14 @@ void GpuPG::init_common(bool same_stream_default) {
   watchdog_ = std::thread([this] { watchdog_loop(); });
 }
 
+void GpuPG::set_same_stream(bool v) {
+  std::lock_guard<std::mutex> lk(launch_mu_);
+  if (v == same_stream_) return;
+  DeviceScope ds(device_);
+  RINGDP_HIP_CHECK(hipDeviceSynchronize());
+  same_stream_ = v;
+}
+
 void GpuPG::stop_common() {
   if (stopped_.exchange(true)) return;
   stop_.store(true);

@@ -80,6 +80,9 @@ class GpuPG : public ProcessGroup {
   hipStream_t comm_stream() const { return comm_stream_.stream(); }
   std::chrono::milliseconds timeout() const { return timeout_; }
   bool same_stream() const { return same_stream_; }
+  // Switch between the caller's stream and the side stream for later ops (drains the device first:
+  // nothing issued under the old placement is still in flight).  For A/B placement tuning.
+  void set_same_stream(bool v);
 
   // Host-blocks until every eagerly issued op has completed and clears the watchdog list, so
   // no event query can race a subsequent hipGraph capture.

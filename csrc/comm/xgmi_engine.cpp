@@ -144,6 +144,20 @@ std::unique_ptr<XgmiEngine> XgmiEngine::create(const std::shared_ptr<Store>& sto
   hipHostGetDevicePointer(reinterpret_cast<void**>(&dev_err), p->error_, 0);
   a.epochs = p->epochs_;
   a.error = dev_err;
+  // the per-rank pointers as a device-memory table: the kernels index it by peer (a kernel-argument
+  // array indexed by a run-time value is copied to scratch first in every thread)
+  {
+    void* tab[2 * kern::kXgMaxRanks];
+    for (int r = 0; r < kern::kXgMaxRanks; ++r) {
+      tab[r] = a.stage[r];
+      tab[kern::kXgMaxRanks + r] = a.flags[r];
+    }
+    if (hipMalloc(reinterpret_cast<void**>(&p->ptr_tab_), sizeof(tab)) != hipSuccess ||
+        hipMemcpy(p->ptr_tab_, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
+      return say("pointer table allocation failed");
+    a.stage_tab = reinterpret_cast<char* const*>(p->ptr_tab_);
+    a.flag_tab = reinterpret_cast<unsigned* const*>(p->ptr_tab_ + kern::kXgMaxRanks);
+  }
   // the kernels' own spin bound is the group timeout itself (s_memrealtime: 100 MHz ticks), uncapped,
   // so a slow but healthy peer (evaluation, checkpointing) gets the same grace as under c10d
   a.timeout_ticks = static_cast<uint64_t>(std::max<int64_t>(timeout_ms, 1)) * 100000ull;
@@ -191,6 +205,7 @@ XgmiEngine::~XgmiEngine() {
   if (stage_ && free_exported) hipFree(stage_);
   if (flags_ && free_exported) hipFree(flags_);
   if (epochs_) hipFree(epochs_);
+  if (ptr_tab_) hipFree(ptr_tab_);
   if (error_) hipHostFree(error_);
   hipSetDevice(prev);
 }

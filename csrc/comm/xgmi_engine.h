@@ -81,6 +81,7 @@ class XgmiEngine {
   char* stage_ = nullptr;
   unsigned* flags_ = nullptr;
   unsigned* epochs_ = nullptr;
+  void** ptr_tab_ = nullptr;  // device copy of the stage / flag pointer tables (XgArgs::stage_tab)
   int* error_ = nullptr;  // hipHostMalloc'd, mapped
   std::vector<void*> opened_;
   kern::XgArgs base_{};

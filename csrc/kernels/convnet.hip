@@ -716,12 +716,13 @@ constexpr int FF_XS = 8 * C1F_CS * 2;      // 16768: conv1 input, 8 shifted copi
 constexpr int FF_X2 = 172 * C2_XRS * 2;    // 16512: a1 in conv2 operand rows (+3 dump rows)
 constexpr int FF_CT = C1I_IMG + 64;        // 3392: conv1 codes (+ dump row)
 constexpr int FF_CS = 121 * C2_CRS * 2;    // 17424: conv2 output tile
-constexpr int FF_X3 = 100 * C3F_XRS * 2;   // 16000: a2 in conv3 operand rows
+constexpr int FF_X3H = 100 * C3F_XRS;      // bf16 per a2 image in conv3 operand rows (16000 B)
+constexpr int FF_X3 = 2 * FF_X3H * 2;      // double-buffered: the consumer reads image s-1 while image s lands
 constexpr int FF_FW = C3F_FCW * 2;         // 40960: fc1 weights [window][co][n]
 constexpr int FF_FR = 10 * 256 * 4;        // 10240: fc1 partial logits [n][256]
 constexpr int FF_OFF_X2 = FF_XS, FF_OFF_CT = FF_OFF_X2 + FF_X2, FF_OFF_CS = FF_OFF_CT + FF_CT,
               FF_OFF_X3 = FF_OFF_CS + FF_CS, FF_OFF_FW = FF_OFF_X3 + FF_X3, FF_OFF_FR = FF_OFF_FW + FF_FW;
-constexpr int FF_LDS = FF_OFF_FR + FF_FR;  // 121296
+constexpr int FF_LDS = FF_OFF_FR + FF_FR;  // 137296
 static_assert(FF_OFF_X2 % 16 == 0 && FF_OFF_CT % 16 == 0 && FF_OFF_CS % 16 == 0 && FF_OFF_X3 % 16 == 0 &&
                   FF_OFF_FW % 16 == 0 && FF_LDS <= 160 * 1024,
               "fused forward LDS");
@@ -738,12 +739,28 @@ __device__ __forceinline__ bf16x8 ff_frag(const bf16* __restrict__ packed, const
   return v;
 }
 
+// In-launch weight packing (PACK): workgroups >= conv_blocks write the packed fragments and count
+// themselves done in sync[0]; a conv wave waits for all of them before its first fragment read (lane 0
+// polls with an agent-scope acquire, s_sleep between polls, bounded: the pack workgroups depend on
+// nothing, so they finish).  The last conv workgroup to finish resets both words for the next launch
+// (graph-replay safe: the counters live in a persistent pool, ops.cpp next_counter).
+__device__ __forceinline__ void ff_wait_packed(unsigned* sync, int npack) {
+  if ((threadIdx.x & 63) == 0) {
+    for (int it = 0; it < (1 << 24); ++it) {
+      if (__hip_atomic_load(sync, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)npack) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 template <bool U8, bool PACK>
-__device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16* __restrict__ packed,
+__device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16* __restrict__ packed,
                             const PackSrc& ws, const float* __restrict__ b1, const float* __restrict__ b2,
                             bf16* __restrict__ a1, uint8_t* __restrict__ idx1, bf16* __restrict__ a2,
                             uint8_t* __restrict__ idx2, int B, int b0, int bstep, int nsteps, float mean,
-                            float inv_std, float in_scale) {
+                            float inv_std, float in_scale, unsigned* sync, int npack) {
   bf16* XS = reinterpret_cast<bf16*>(smem);
   bf16* X2 = reinterpret_cast<bf16*>(smem + FF_OFF_X2);
   uint32_t* X2u = reinterpret_cast<uint32_t*>(X2);
@@ -758,6 +775,7 @@ __device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) bw1[nt][ks] = ff_frag<PACK>(packed, ws, P1_OFF + (nt * 2 + ks) * 512, lane);
+  if (PACK) ff_wait_packed(sync, npack);  // conv1's 32 values per lane came from the masters directly
   const float c1b0 = b1[2 * r16], c1b1 = b1[2 * r16 + 1];
   const f32x4 bias0v = {c1b0, c1b0, c1b0, c1b0}, bias1v = {c1b1, c1b1, c1b1, c1b1};
   int aoff[C1F_MT], coff[C1F_MT];
@@ -776,7 +794,7 @@ __device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int ks = 0; ks < 9; ++ks) bw2[t][ks] = ff_frag<PACK>(packed, ws, P2F_OFF + ((2 * wn + t) * 9 + ks) * 512, lane);
+    for (int ks = 0; ks < 9; ++ks) bw2[t][ks] = ff_frag<false>(packed, ws, P2F_OFF + ((2 * wn + t) * 9 + ks) * 512, lane);
   f32x4 bv2[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -871,7 +889,7 @@ __device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16
         }
       }
     }
-    __syncthreads();  // [S2] Cs complete; the consumer is done reading X3
+    __syncthreads();  // [S2] Cs complete
     // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3
     if (live) {
       bf16x8* da = reinterpret_cast<bf16x8*>(a2 + (int64_t)b * 6400);
@@ -883,7 +901,7 @@ __device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16
         pool2_code8(Cs + ((p / 10) * 11 + p % 10) * C2_CRS + c, C2_CRS, 11, v, code);
         da[it] = v;
         di[it] = code;
-        *reinterpret_cast<bf16x8*>(X3 + p * C3F_XRS + c) = v;
+        *reinterpret_cast<bf16x8*>(X3 + (s & 1) * FF_X3H + p * C3F_XRS + c) = v;
       }
     }
     __syncthreads();  // [S3] X3 complete; Cs, X2, CT free
@@ -891,23 +909,17 @@ __device__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16
 }
 
 template <bool PACK>
-__device__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const PackSrc& ws,
+__device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const PackSrc& ws,
                             const float* __restrict__ b3, const float* __restrict__ bfc, bf16* __restrict__ a3,
                             uint8_t* __restrict__ idx3, float* __restrict__ logits, int B, int b0, int bstep,
-                            int nsteps) {
+                            int nsteps, unsigned* sync, int npack) {
   const bf16* X3 = reinterpret_cast<const bf16*>(smem + FF_OFF_X3);
   bf16* fw = reinterpret_cast<bf16*>(smem + FF_OFF_FW);
   float* fred = reinterpret_cast<float*>(smem + FF_OFF_FR);
   const int tid = threadIdx.x - 256, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
-  if (PACK) {
-    for (int c = tid; c < C3F_FCW / 8; c += 256) {
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)pack_value(PFC_OFF + c * 8 + j, ws);
-      reinterpret_cast<bf16x8*>(fw)[c] = v;
-    }
-  } else {
+  if (PACK) ff_wait_packed(sync, npack);
+  {
     const uint4* src = reinterpret_cast<const uint4*>(packed + PFC_OFF);
     for (int c = tid; c < C3F_FCW / 8; c += 256) reinterpret_cast<uint4*>(fw)[c] = src[c];
   }
@@ -915,7 +927,7 @@ __device__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const P
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
-    for (int ks = 0; ks < 18; ++ks) bw[t][ks] = ff_frag<PACK>(packed, ws, P3F_OFF + ((2 * wave + t) * 18 + ks) * 512, lane);
+    for (int ks = 0; ks < 18; ++ks) bw[t][ks] = ff_frag<false>(packed, ws, P3F_OFF + ((2 * wave + t) * 18 + ks) * 512, lane);
   float bv[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) bv[t] = b3[32 * wave + 16 * t + r16];
@@ -940,45 +952,29 @@ __device__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const P
     }
   };
   f32x4 acc[4][2];
+  // conv3 k-steps [k0, k1) of the image in buffer xb
+  auto mfma_ks = [&](const bf16* xb, auto k0c, auto k1c) {
+#pragma unroll
+    for (int ks = decltype(k0c)::value; ks < decltype(k1c)::value; ++ks) {
+      const int tap = ks >> 1, c0 = (ks & 1) * 32;
+      const int shift = (tap / 3) * 10 + tap % 3;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(xb + (base[mt] + shift) * C3F_XRS + c0 + q8);
+        acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
+        acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
+      }
+    }
+  };
+  // Step s: pool3 / fc1-partials epilogue of image s-2 and the first 4 k-steps of image s-1 (phase 1,
+  // beside the producer's MFMA-light conv1), fc1 reduction of s-2 + k-steps 4-10 (phase 2), k-steps
+  // 11-17 (phase 3, beside the producer's VALU-only pool2): the MFMA pipe has work in every phase.
   for (int s = 0; s < nsteps; ++s) {
-    const int b = b0 + (s - 1) * bstep;  // image of this step (one behind the producer)
-    const bool live = s >= 1 && b < B;
-    const int bp = b - bstep;            // image whose fc1 partials sit in fred
-    // ---------------- phase 1: fc1 reduction of the previous image; k-steps 0-8
-    if (s >= 2 && bp < B) fc_reduce(bp);
-    if (live) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
-#pragma unroll
-      for (int ks = 0; ks < 9; ++ks) {
-        const int tap = ks >> 1, c0 = (ks & 1) * 32;
-        const int shift = (tap / 3) * 10 + tap % 3;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(X3 + (base[mt] + shift) * C3F_XRS + c0 + q8);
-          acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
-          acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
-        }
-      }
-    }
-    __syncthreads();  // [S1]
-    // ---------------- phase 2: k-steps 9-17
-    if (live) {
-#pragma unroll
-      for (int ks = 9; ks < 18; ++ks) {
-        const int tap = ks >> 1, c0 = (ks & 1) * 32;
-        const int shift = (tap / 3) * 10 + tap % 3;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(X3 + (base[mt] + shift) * C3F_XRS + c0 + q8);
-          acc[mt][0] = mfma16x16x32(a, bw[0][ks], acc[mt][0]);
-          acc[mt][1] = mfma16x16x32(a, bw[1][ks], acc[mt][1]);
-        }
-      }
-    }
-    __syncthreads();  // [S2]
-    // ---------------- phase 3: pool3 + ReLU -> a3 / idx3, fc1 partials -> fred
-    if (live) {
+    const int bm = b0 + (s - 1) * bstep, be = bm - bstep;
+    const bool live_m = s >= 1 && bm < B, live_e = s >= 2 && be < B;
+    const bf16* xb = X3 + ((s - 1) & 1) * FF_X3H;
+    // ---------------- phase 1
+    if (live_e) {
       float part[10];
 #pragma unroll
       for (int n = 0; n < 10; ++n) part[n] = 0.f;
@@ -989,7 +985,7 @@ __device__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const P
           const int wc = wcol[mt], co = 32 * wave + 16 * t + r16;
           int g;
           const bf16 pb = (bf16)pool4(acc[mt][t], bv[t], g);
-          const int64_t o = ((int64_t)b * 16 + wc) * 128 + co;
+          const int64_t o = ((int64_t)be * 16 + wc) * 128 + co;
           a3[o] = pb;
           idx3[o] = (uint8_t)g;
           const float pv = (float)pb;
@@ -1004,10 +1000,20 @@ __device__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const P
 #pragma unroll
       for (int n = 0; n < 10; ++n) fred[n * 256 + tid] = part[n];
     }
+    if (live_m) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
+      mfma_ks(xb, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+    }
+    __syncthreads();  // [S1]
+    // ---------------- phase 2
+    if (live_e) fc_reduce(be);
+    if (live_m) mfma_ks(xb, std::integral_constant<int, 4>{}, std::integral_constant<int, 11>{});
+    __syncthreads();  // [S2]
+    // ---------------- phase 3
+    if (live_m) mfma_ks(xb, std::integral_constant<int, 11>{}, std::integral_constant<int, 18>{});
     __syncthreads();  // [S3]
   }
-  const int bl = b0 + (nsteps - 2) * bstep;  // the last image's partials
-  if (nsteps >= 2 && bl < B) fc_reduce(bl);
 }
 
 template <bool U8, bool PACK>
@@ -1020,22 +1026,38 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
                                                           bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
                                                           bf16* __restrict__ a3, uint8_t* __restrict__ idx3,
                                                           float* __restrict__ logits, int B, float mean,
-                                                          float inv_std, float in_scale, int ablate) {
+                                                          float inv_std, float in_scale, int ablate,
+                                                          unsigned* sync) {
+  const int npack = (int)gridDim.x - conv_blocks;
   if (PACK && (int)blockIdx.x >= conv_blocks) {
-    if (threadIdx.x < 256) pack_range(ws, pack_out, 0, blockIdx.x - conv_blocks, gridDim.x - conv_blocks);
+    if (threadIdx.x < 256) pack_range(ws, pack_out, 0, blockIdx.x - conv_blocks, npack);
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   __shared__ __attribute__((aligned(16))) char ff_smem[FF_LDS];
   const int b0 = blockIdx.x, bstep = conv_blocks;
   const int nimg = b0 < B ? (B - b0 + bstep - 1) / bstep : 0;
-  const int nsteps = nimg + 1;  // the consumer trails by one step
+  const int nsteps = nimg + 2;  // the consumer's MFMAs trail by one step, its epilogue by two
   // wave-uniform role split (an SGPR condition: the two roles are separate code paths, not one
   // exec-masked sequence whose live ranges the register allocator would have to overlap)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4)
-    ff_producer<U8, PACK>(ff_smem, xin, packed, ws, b1, b2, a1, idx1, a2, idx2, (ablate & 1) ? 0 : B, b0, bstep,
-                          nsteps, mean, inv_std, in_scale);
+    ff_producer<U8, PACK>(ff_smem, xin, PACK ? pack_out : packed, ws, b1, b2, a1, idx1, a2, idx2,
+                          (ablate & 1) ? 0 : B, b0, bstep, nsteps, mean, inv_std, in_scale, sync, npack);
   else
-    ff_consumer<PACK>(ff_smem, packed, ws, b3, bfc, a3, idx3, logits, (ablate & 2) ? 0 : B, b0, bstep, nsteps);
+    ff_consumer<PACK>(ff_smem, PACK ? pack_out : packed, ws, b3, bfc, a3, idx3, logits, (ablate & 2) ? 0 : B, b0,
+                      bstep, nsteps, sync, npack);
+  if (PACK) {  // the last conv workgroup out re-arms the counters
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(sync + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == (unsigned)conv_blocks - 1) {
+        __hip_atomic_store(sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
 }
 
 // ================================================================== F3 backward
@@ -1235,7 +1257,7 @@ __device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int
 // m-tiles (dz3 row pairs) hit disjoint da2 rows, so their read-add-writes are independent; consecutive
 // taps may hit the same da2 words from different lanes, so a compiler barrier keeps tap t+1's reads
 // behind tap t's writes (LDS executes one wave's instructions in order).  Fixed order: deterministic.
-__device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
+__device__ __forceinline__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ dz2, int b_first, int b_end, int b_step) {
   bf16* P = reinterpret_cast<bf16*>(smem);
@@ -1352,7 +1374,7 @@ __device__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, cons
 
 // wgrad: workgroup half h of an image slice covers n-tiles 18h..18h+17 of dW3t [576][128];
 // wave (wm, wn) owns m-tiles (co) 4wm..4wm+3 x n-tiles 18h + 9wn .. +8.
-__device__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
+__device__ __forceinline__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
                                  const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
                                  int nslices, int slice, int h) {
   bf16* D = reinterpret_cast<bf16*>(smem);
@@ -1472,7 +1494,7 @@ constexpr int C2W_X = 169 * C2_XRS * 2;            // 13520
 constexpr int C2B_LDS = (C2D_P + 2 * C2D_O) > (C2W_D + C2W_X) ? (C2D_P + 2 * C2D_O) : (C2W_D + C2W_X);
 constexpr int C2_WSLAB = 288 * 64 + 64;
 
-__device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ dz2, const bf16* __restrict__ packed,
+__device__ __forceinline__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ dz2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ da1, int B, int block, int nblocks) {
   bf16* P = reinterpret_cast<bf16*>(smem);
   bf16* O = reinterpret_cast<bf16*>(smem + C2D_P);
@@ -1556,7 +1578,7 @@ __device__ void conv2_dgrad_role(char* smem, const bf16* __restrict__ dz2, const
   if (prev >= 0) copy_out(prev, O + (cur ^ 1) * 169 * C2_ORS);
 }
 
-__device__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ dz2,
+__device__ __forceinline__ void conv2_wgrad_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ dz2,
                                  float* __restrict__ slabs, int B, int nslices, int slice) {
   bf16* D = reinterpret_cast<bf16*>(smem);
   bf16* X = reinterpret_cast<bf16*>(smem + C2W_D);
@@ -1785,7 +1807,7 @@ static_assert(C2D_P % 16 == 0 && C12_O % 16 == 0 && C12_XS % 16 == 0, "16-B alig
 static_assert(8 * 4 * 64 * 4 * 4 <= C12_OFF_X, "conv1 cross-wave reduction fits in P + O");
 
 template <bool U8>
-__device__ void conv12_dgrad_role(char* smem, const void* __restrict__ xin, const uint8_t* __restrict__ idx1,
+__device__ __forceinline__ void conv12_dgrad_role(char* smem, const void* __restrict__ xin, const uint8_t* __restrict__ idx1,
                                   const bf16* __restrict__ dz2, const bf16* __restrict__ packed, int B, int block,
                                   int nblocks, float mean, float inv_std, float in_scale,
                                   float* __restrict__ slabs1) {
@@ -2116,30 +2138,37 @@ void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, v
 void cn_forward_fused(const void* x, bool u8, const float* const* w, const float* b1, const float* b2,
                       const float* b3, const float* bfc, void* packed, void* a1, uint8_t* idx1, void* a2,
                       uint8_t* idx2, void* a3, uint8_t* idx3, float* logits, int B, float mean, float inv_std,
-                      float in_scale, hipStream_t s) {
+                      float in_scale, unsigned* sync, hipStream_t s) {
   const int conv = clampi(B, 1, wpc("FF", 1) * num_cus());  // 121 KiB LDS: one 512-thread workgroup per CU
   const PackSrc ws{w[0], w[1], w[2], w[3]};
   bf16* pk = static_cast<bf16*>(packed);
   bf16 *a1b = static_cast<bf16*>(a1), *a2b = static_cast<bf16*>(a2), *a3b = static_cast<bf16*>(a3);
   static const int ablate = [] { const char* v = getenv("RINGDP_FF_ABLATE"); return v ? atoi(v) : 0; }();
-  static const bool inpack = [] { const char* v = getenv("RINGDP_FF_INPACK"); return v && atoi(v) != 0; }();
-  if (inpack) {  // fragments from the fp32 masters in every workgroup + pack workgroups in this launch
+  static const bool inpack = [] { const char* v = getenv("RINGDP_FF_INPACK"); return !v || atoi(v) != 0; }();
+  // Pack workgroups in this launch, the conv workgroups waiting for them, only while whole CUs stay
+  // free for the pack workgroups: a conv workgroup takes a CU's entire register file (2 x 256 VGPRs per
+  // SIMD), so with a conv workgroup on every CU the pack workgroups could never start.
+  if (inpack && sync && conv <= num_cus() - 32) {
     const int grid = conv + cdiv(PACK_TOTAL, 1024);
     if (u8)
       fused_fwd_kernel<true, true><<<grid, 512, 0, s>>>(x, nullptr, ws, pk, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
-                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
+                                                        sync);
     else
       fused_fwd_kernel<false, true><<<grid, 512, 0, s>>>(x, nullptr, ws, pk, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
-                                                         idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+                                                         idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
+                                                         sync);
     return;
   }
   pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(ws, pk);
   if (u8)
     fused_fwd_kernel<true, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
-                                                       idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+                                                       idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
+                                                       nullptr);
   else
     fused_fwd_kernel<false, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
-                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate);
+                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
+                                                        nullptr);
 }
 
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,

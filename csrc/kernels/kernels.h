@@ -66,6 +66,8 @@ enum XgRed : int { XG_SUM = 0, XG_PROD, XG_MIN, XG_MAX };
 struct XgArgs {
   char* stage[kXgMaxRanks];      // staging buffer of every rank (IPC-mapped; [rank] = mine)
   unsigned* flags[kXgMaxRanks];  // flag block of every rank (IPC-mapped)
+  char* const* stage_tab;        // the same two tables in device memory (what the kernels index)
+  unsigned* const* flag_tab;
   unsigned* epochs;              // local: [G] collective, [16][G] send per peer, [16][G] recv per peer
   int* error;                    // device address of a host-mapped word: set when a peer never arrived
   uint64_t timeout_ticks;        // wall_clock64 ticks (100 MHz)
@@ -175,7 +177,7 @@ void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const 
 void cn_forward_fused(const void* x, bool u8, const float* const* w, const float* b1, const float* b2,
                       const float* b3, const float* bfc, void* packed, void* a1, uint8_t* idx1, void* a2,
                       uint8_t* idx2, void* a3, uint8_t* idx3, float* logits, int B, float mean, float inv_std,
-                      float in_scale, hipStream_t s);
+                      float in_scale, unsigned* sync, hipStream_t s);  // sync: 2 zeroed words, self re-arming
 
 // Workspace sizes (floats) of the backward weight-gradient slabs.
 int64_t cn_fc_slab_floats(int B, bool dgrad);

@@ -52,15 +52,19 @@ __device__ __forceinline__ void st_flag(unsigned* f, unsigned v) {
 __device__ __forceinline__ uint4 ld16(const char* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ void st16(char* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 // the first n (< 16) bytes at p, zero-filled (a message's tail vector)
+// (byte loops fully unrolled over register words: an addressable local would live in scratch)
 __device__ __forceinline__ uint4 ld_part(const char* p, int n) {
-  uint4 v = make_uint4(0u, 0u, 0u, 0u);
-  char* d = reinterpret_cast<char*>(&v);
-  for (int i = 0; i < n; ++i) d[i] = p[i];
-  return v;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < n) w[i >> 2] |= static_cast<uint32_t>(static_cast<uint8_t>(p[i])) << (8 * (i & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
 }
 __device__ __forceinline__ void st_part(char* p, uint4 v, int n) {
-  const char* s = reinterpret_cast<const char*>(&v);
-  for (int i = 0; i < n; ++i) p[i] = s[i];
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < n) p[i] = static_cast<char>(w[i >> 2] >> (8 * (i & 3)));
 }
 __device__ __forceinline__ uint4 ld_n(const char* p, int n) { return n == 16 ? ld16(p) : ld_part(p, n); }
 __device__ __forceinline__ void st_n(char* p, uint4 v, int n) {
@@ -177,24 +181,24 @@ struct VecAcc {
 
 // ---------------------------------------------------------------- staging / flag addressing
 __device__ __forceinline__ char* reg_a(const XgArgs& a, int owner, int par, int src) {
-  return a.stage[owner] + a.off_a + (static_cast<int64_t>(par) * a.world + src) * a.slot;
+  return a.stage_tab[owner] + a.off_a + (static_cast<int64_t>(par) * a.world + src) * a.slot;
 }
 __device__ __forceinline__ char* reg_b(const XgArgs& a, int owner, int par, int src) {
-  return a.stage[owner] + a.off_b + (static_cast<int64_t>(par) * a.world + src) * a.slot;
+  return a.stage_tab[owner] + a.off_b + (static_cast<int64_t>(par) * a.world + src) * a.slot;
 }
 __device__ __forceinline__ char* reg_p(const XgArgs& a, int owner, int src, int par) {
-  return a.stage[owner] + a.off_p2p + (static_cast<int64_t>(src) * 2 + par) * a.p2p_slot;
+  return a.stage_tab[owner] + a.off_p2p + (static_cast<int64_t>(src) * 2 + par) * a.p2p_slot;
 }
 // collective handshake words on `owner`: [channel][block][source rank]
 __device__ __forceinline__ unsigned* flag_c(const XgArgs& a, int owner, int ch, int b, int src) {
-  return a.flags[owner] + (static_cast<int64_t>(ch) * a.nblocks + b) * kXgMaxRanks + src;
+  return a.flag_tab[owner] + (static_cast<int64_t>(ch) * a.nblocks + b) * kXgMaxRanks + src;
 }
 // send/recv: data-ready words on the receiver [src][block], ack words on the sender [dst][block]
 __device__ __forceinline__ unsigned* flag_pd(const XgArgs& a, int owner, int src, int b) {
-  return a.flags[owner] + 2 * a.nblocks * kXgMaxRanks + src * a.nblocks + b;
+  return a.flag_tab[owner] + 2 * a.nblocks * kXgMaxRanks + src * a.nblocks + b;
 }
 __device__ __forceinline__ unsigned* flag_pa(const XgArgs& a, int owner, int dst, int b) {
-  return a.flags[owner] + 3 * a.nblocks * kXgMaxRanks + dst * a.nblocks + b;
+  return a.flag_tab[owner] + 3 * a.nblocks * kXgMaxRanks + dst * a.nblocks + b;
 }
 
 // Bounded relaxed poll until (int)(*f - e) >= 0.  false: timed out.
@@ -209,7 +213,7 @@ __device__ __forceinline__ bool poll_ge(const unsigned* f, unsigned e, uint64_t 
 
 // All of this workgroup's stores are published to every peer (flag word [b][me] := e on each peer),
 // then the workgroup waits until every peer has published epoch e to us.  Called by all threads.
-__device__ bool exchange(const XgArgs& a, int ch, int b, unsigned e, int* s_fail) {
+__device__ __forceinline__ bool exchange(const XgArgs& a, int ch, int b, unsigned e, int* s_fail) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains
   __syncthreads();
   const int tid = threadIdx.x;
@@ -235,25 +239,56 @@ __device__ __forceinline__ int vec_bytes(int64_t o, int64_t len) {
   return static_cast<int>(len - o < 16 ? len - o : 16);
 }
 
+// The same ownership, kU vectors per iteration (offsets o0 + u * G * 4 KiB): the loads of all kU are
+// issued before any dependent store / add, so a thread has kU memory round trips in flight instead
+// of one (a 26 MB two-shot is ~100 owned vectors per thread).
+constexpr int kU = 4;
+#define XG_FOR_OWNED_U(o0, len)                                                                    \
+  for (int64_t o0 = static_cast<int64_t>(b) * kSeg + 16 * tid; o0 < (len);                        \
+       o0 += static_cast<int64_t>(kU) * a.nblocks * kSeg)
+#define XG_UOFF(o0, u) ((o0) + static_cast<int64_t>(u) * a.nblocks * kSeg)
+
 template <typename T, int RED>
-__device__ void run_oneshot(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
+__device__ __forceinline__ void run_oneshot(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
   const int tid = threadIdx.x, me = a.rank, W = a.world;
   const int64_t S = a.nbytes;
-  XG_FOR_OWNED(o, S) {
-    const uint4 v = ld_n(a.in + o, vec_bytes(o, S));
-    for (int p = 0; p < W; ++p)
-      if (p != me) st16(reg_a(a, p, par, me) + o, v);
+  XG_FOR_OWNED_U(o0, S) {
+    uint4 v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t o = XG_UOFF(o0, u);
+      if (o < S) v[u] = ld_n(a.in + o, vec_bytes(o, S));
+    }
+    for (int p = 0; p < W; ++p) {
+      if (p == me) continue;
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < S) st16(reg_a(a, p, par, me) + o, v[u]);
+      }
+    }
   }
   if (!exchange(a, 0, b, e, s_fail)) return;
-  XG_FOR_OWNED(o, S) {
-    const int n = vec_bytes(o, S);
-    VecAcc<T, RED> acc;
+  XG_FOR_OWNED_U(o0, S) {
+    VecAcc<T, RED> acc[kU];
     for (int r = 0; r < W; ++r) {
-      const uint4 v = r == me ? ld_n(a.in + o, n) : ld16(reg_a(a, me, par, r) + o);
-      if (r == 0) acc.set(v);
-      else acc.add(v);
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < S) v[u] = r == me ? ld_n(a.in + o, vec_bytes(o, S)) : ld16(reg_a(a, me, par, r) + o);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (r == 0) acc[u].set(v[u]);
+        else acc[u].add(v[u]);
+      }
     }
-    st_n(a.out + o, acc.get(a), n);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t o = XG_UOFF(o0, u);
+      if (o < S) st_n(a.out + o, acc[u].get(a), vec_bytes(o, S));
+    }
   }
 }
 
@@ -264,47 +299,79 @@ __device__ __forceinline__ int64_t chunk_len(const XgArgs& a, int j) {
 }
 
 template <typename T, int RED>
-__device__ void run_twoshot(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
+__device__ __forceinline__ void run_twoshot(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
   const int tid = threadIdx.x, me = a.rank, W = a.world;
   const int64_t C = a.chunk;
   // 1. reduce-scatter: my copy of chunk p goes to rank p
-  XG_FOR_OWNED(o, C) {
+  XG_FOR_OWNED_U(o0, C) {
     for (int p = 0; p < W; ++p) {
       if (p == me) continue;
       const int64_t L = chunk_len(a, p);
-      if (o < L) st16(reg_a(a, p, par, me) + o, ld_n(a.in + p * C + o, vec_bytes(o, L)));
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < L) v[u] = ld_n(a.in + p * C + o, vec_bytes(o, L));
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < L) st16(reg_a(a, p, par, me) + o, v[u]);
+      }
     }
   }
   if (!exchange(a, 0, b, e, s_fail)) return;
   // 2. my chunk: rank-order sum, written locally and pushed to every peer
   const int64_t Lme = chunk_len(a, me);
-  XG_FOR_OWNED(o, Lme) {
-    const int n = vec_bytes(o, Lme);
-    VecAcc<T, RED> acc;
+  XG_FOR_OWNED_U(o0, Lme) {
+    VecAcc<T, RED> acc[kU];
     for (int r = 0; r < W; ++r) {
-      const uint4 v = r == me ? ld_n(a.in + me * C + o, n) : ld16(reg_a(a, me, par, r) + o);
-      if (r == 0) acc.set(v);
-      else acc.add(v);
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < Lme) v[u] = r == me ? ld_n(a.in + me * C + o, vec_bytes(o, Lme)) : ld16(reg_a(a, me, par, r) + o);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (r == 0) acc[u].set(v[u]);
+        else acc[u].add(v[u]);
+      }
     }
-    const uint4 res = acc.get(a);
-    st_n(a.out + me * C + o, res, n);
-    for (int p = 0; p < W; ++p)
-      if (p != me) st16(reg_b(a, p, par, me) + o, res);
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t o = XG_UOFF(o0, u);
+      if (o >= Lme) continue;
+      const uint4 res = acc[u].get(a);
+      st_n(a.out + me * C + o, res, vec_bytes(o, Lme));
+      for (int p = 0; p < W; ++p)
+        if (p != me) st16(reg_b(a, p, par, me) + o, res);
+    }
   }
   if (!exchange(a, 1, b, e, s_fail)) return;
   // 3. all-gather: every other chunk from the rank that reduced it
-  XG_FOR_OWNED(o, C) {
+  XG_FOR_OWNED_U(o0, C) {
     for (int r = 0; r < W; ++r) {
       if (r == me) continue;
       const int64_t L = chunk_len(a, r);
-      if (o < L) st_n(a.out + r * C + o, ld16(reg_b(a, me, par, r) + o), vec_bytes(o, L));
+      uint4 v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < L) v[u] = ld16(reg_b(a, me, par, r) + o);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int64_t o = XG_UOFF(o0, u);
+        if (o < L) st_n(a.out + r * C + o, v[u], vec_bytes(o, L));
+      }
     }
   }
 }
 
 // in: W blocks of M bytes at stride a.stride; out: my M bytes.
 template <typename T, int RED>
-__device__ void run_reduce_scatter(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
+__device__ __forceinline__ void run_reduce_scatter(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
   const int tid = threadIdx.x, me = a.rank, W = a.world;
   const int64_t M = a.nbytes;
   XG_FOR_OWNED(o, M) {
@@ -325,7 +392,7 @@ __device__ void run_reduce_scatter(const XgArgs& a, int b, unsigned e, int par, 
 }
 
 // in: my M bytes; out: W blocks of M bytes at stride a.stride.
-__device__ void run_allgather(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
+__device__ __forceinline__ void run_allgather(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
   const int tid = threadIdx.x, me = a.rank, W = a.world;
   const int64_t M = a.nbytes;
   XG_FOR_OWNED(o, M) {
@@ -343,7 +410,7 @@ __device__ void run_allgather(const XgArgs& a, int b, unsigned e, int par, int* 
   }
 }
 
-__device__ void run_broadcast(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
+__device__ __forceinline__ void run_broadcast(const XgArgs& a, int b, unsigned e, int par, int* s_fail) {
   const int tid = threadIdx.x, me = a.rank, W = a.world, root = a.root;
   const int64_t S = a.nbytes;
   if (me == root) {
@@ -361,7 +428,7 @@ __device__ void run_broadcast(const XgArgs& a, int b, unsigned e, int par, int* 
   }
 }
 
-__device__ void run_send(const XgArgs& a, int b, int* s_fail, unsigned* ep) {
+__device__ __forceinline__ void run_send(const XgArgs& a, int b, int* s_fail, unsigned* ep) {
   const int tid = threadIdx.x, me = a.rank, dst = a.peer;
   const unsigned e = *ep + 1u;
   const int par = e & 1;
@@ -383,7 +450,7 @@ __device__ void run_send(const XgArgs& a, int b, int* s_fail, unsigned* ep) {
   if (tid == 0) *ep = e;
 }
 
-__device__ void run_recv(const XgArgs& a, int b, int* s_fail, unsigned* ep) {
+__device__ __forceinline__ void run_recv(const XgArgs& a, int b, int* s_fail, unsigned* ep) {
   const int tid = threadIdx.x, me = a.rank, src = a.peer;
   const unsigned e = *ep + 1u;
   const int par = e & 1;

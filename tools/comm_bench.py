@@ -95,9 +95,11 @@ def worker(args):
                 with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
                     for _ in range(args.reps):
                         dist.all_reduce(t, op=dist.ReduceOp.AVG)
-                g.replay()
+                for _ in range(3):  # warm replays: the first ones pay graph upload / first-touch costs
+                    g.replay()
                 torch.cuda.synchronize()
                 dist.barrier()
+                torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for _ in range(args.iters):
                     g.replay()

@@ -16,3 +16,10 @@ for op in conv3_fc_bwd conv3_fc_ce_bwd; do
 done
 cat $O/times.jsonl
 echo ALLDONE
+# xgmi engine: exactness tests, then the all-reduce sweep at ws 2 (ranks share the GPU), blocks 64 / 256
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_xgmi_gpu.py -k "exact" > $O/xgmi_tests.log 2>&1; rc=$?; tail -2 $O/xgmi_tests.log; [ $rc -eq 0 ] || exit 1
+for nb in 64 256; do
+  RINGDP_XGMI_BLOCKS=$nb timeout -k 10 300 python tools/comm_bench.py --gpus 2 --backend xgmi --dtypes fp32 > $O/comm_xgmi_ws2_b$nb.jsonl 2>$O/comm.err || { tail -5 $O/comm.err; exit 1; }
+  echo "blocks $nb"; grep '"impl"' $O/comm_xgmi_ws2_b$nb.jsonl
+done
+echo ALLDONE2
