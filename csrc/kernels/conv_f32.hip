@@ -820,6 +820,40 @@ int64_t wgrad_chunk(const ConvF32Geom& g) {
   return batch_chunk(g.B, {static_cast<int64_t>(g.C) * g.H * g.W, static_cast<int64_t>(g.Kout) * g.OH * g.OW});
 }
 
+// Linear layer with few outputs (the ConvNet's fc1: N = 10, K = 2048) at small batches: the GEMM core's
+// single 128-row tile ran K serially in one workgroup (163 us at B=100).  One wave per input row: lane l
+// accumulates k = l, l+64, ... for every output, then a fixed butterfly sums the lanes (deterministic).
+template <int N>
+__global__ __launch_bounds__(256) void linear_skinny_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                              const float* __restrict__ bias, float* __restrict__ z,
+                                                              int M, int K) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (int64_t)row * K;
+  float acc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float v = xr[k];
+#pragma unroll
+    for (int n = 0; n < N; ++n) acc[n] = fmaf(v, w[(int64_t)n * K + k], acc[n]);
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float v = acc[n];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    acc[n] = v;
+  }
+  if (lane < N) {
+    float v = 0.f;
+#pragma unroll
+    for (int n = 0; n < N; ++n) v = lane == n ? acc[n] : v;
+    z[(int64_t)row * N + lane] = v + (bias ? bias[lane] : 0.f);
+  }
+}
+
 }  // namespace
 
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
@@ -833,6 +867,11 @@ int conv_f32_wgrad_slices(const ConvF32Geom& g) {
 void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
                   const float* w, const float* bias, float* z, hipStream_t s) {
   const int K = g.C * g.R * g.R;
+  if (!xu8 && g.R == 1 && g.H == 1 && g.W == 1 && g.Kout == 10 && g.B <= 8192) {  // fc1 at small batches
+    linear_skinny_f32_kernel<10><<<static_cast<unsigned>((g.B + 3) / 4), 256, 0, s>>>(x, w, bias, z,
+                                                                                     static_cast<int>(g.B), K);
+    return;
+  }
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zout = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
   const int64_t chunk = batch_chunk(g.B, {xin, zout});
   for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {

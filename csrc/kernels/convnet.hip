@@ -2144,7 +2144,10 @@ void cn_forward_fused(const void* x, bool u8, const float* const* w, const float
   bf16* pk = static_cast<bf16*>(packed);
   bf16 *a1b = static_cast<bf16*>(a1), *a2b = static_cast<bf16*>(a2), *a3b = static_cast<bf16*>(a3);
   static const int ablate = [] { const char* v = getenv("RINGDP_FF_ABLATE"); return v ? atoi(v) : 0; }();
-  static const bool inpack = [] { const char* v = getenv("RINGDP_FF_INPACK"); return !v || atoi(v) != 0; }();
+  // In-launch packing (RINGDP_FF_INPACK=1) is correct but slow on MI355X: the pack workgroups' agent-scope
+  // release has to write their XCD's L2 back before the other XCDs may read the fragments (measured
+  // B=100: 114 us against 23 us with the separate pack launch), so it is off by default.
+  static const bool inpack = [] { const char* v = getenv("RINGDP_FF_INPACK"); return v && atoi(v) != 0; }();
   // Pack workgroups in this launch, the conv workgroups waiting for them, only while whole CUs stay
   // free for the pack workgroups: a conv workgroup takes a CU's entire register file (2 x 256 VGPRs per
   // SIMD), so with a conv workgroup on every CU the pack workgroups could never start.

@@ -30,8 +30,9 @@ from . import grad_buffer
 
 # RINGDP_CN_FUSE12=0: conv1 / conv2 as separate autograd nodes with their own backward kernels (A/B)
 _FUSE12 = os.environ.get("RINGDP_CN_FUSE12", "1") != "0"
-# RINGDP_CN_FUSED_FWD=1: the whole forward in one launch (cn_forward_fused; A/B against the three-launch path)
-_FUSED_FWD = os.environ.get("RINGDP_CN_FUSED_FWD", "0") == "1"
+# RINGDP_CN_FUSED_FWD=0: the three-launch forward (conv1+pack / conv2 / conv3+fc1) instead of the
+# whole-forward kernel (weight pack + cn_forward_fused; B=65536: forward 1469 -> 1390 us, B=100: 28 -> 23 us)
+_FUSED_FWD = os.environ.get("RINGDP_CN_FUSED_FWD", "1") != "0"
 # RINGDP_CN_DEFER_REDUCE=0: conv3 / fc1 weight-gradient reduction in its own launch (A/B)
 _DEFER = os.environ.get("RINGDP_CN_DEFER_REDUCE", "1") != "0"
 # RINGDP_CN_HEAD_CE=0: ringdp's cross entropy on the ConvNet logits stays a separate node (A/B)

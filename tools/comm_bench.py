@@ -76,6 +76,23 @@ def worker(args):
     else:
         impls = ["rccl"] + (["rccl+xgmi_small"] if pg.p2p_max_bytes() > 0 else [])
     variant = {k: os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS") if k in os.environ}
+    # The first timed measurement of a process ran several times slower whatever its size (ranks sharing
+    # a GPU settle their queues / clocks): one untimed pass of the first size goes before the sweep.
+    first = max(1, int(args.sizes.split(",")[0]) // 4)
+    w = torch.ones(first, dtype=torch.float32, device=dev)
+    for _ in range(50):
+        dist.all_reduce(w, op=dist.ReduceOp.AVG)
+    torch.cuda.synchronize()
+    s0 = torch.cuda.Stream()
+    g0 = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s0), torch.cuda.graph(g0, stream=s0):
+        for _ in range(args.reps):
+            dist.all_reduce(w, op=dist.ReduceOp.AVG)
+    for _ in range(args.iters):
+        g0.replay()
+    torch.cuda.synchronize()
+    dist.barrier()
+    del g0
     for dt_name in args.dtypes.split(","):
         dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[dt_name]
         es = torch.tensor([], dtype=dtype).element_size()
