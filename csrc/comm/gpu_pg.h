@@ -83,6 +83,10 @@ class GpuPG : public ProcessGroup {
   // Switch between the caller's stream and the side stream for later ops (drains the device first:
   // nothing issued under the old placement is still in flight).  For A/B placement tuning.
   void set_same_stream(bool v);
+  // the stream the next op will be issued on (the caller's in same-stream mode, else the comm stream)
+  c10::hip::HIPStreamMasqueradingAsCUDA op_stream() const {
+    return same_stream_ ? c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_) : comm_stream_;
+  }
 
   // Host-blocks until every eagerly issued op has completed and clears the watchdog list, so
   // no event query can race a subsequent hipGraph capture.

@@ -193,10 +193,12 @@ std::shared_ptr<Work> RcclPG::allgather(std::vector<at::Tensor>& outputs, const 
   for (auto& o : outputs) {
     RINGDP_CHECK(o.is_cuda() && o.numel() == input.numel(), "all_gather: bad output tensor");
   }
-  // Gather into a flat staging buffer allocated on the comm stream, then scatter-copy out.
+  // Gather into a flat staging buffer, then scatter-copy out - both on the stream the op is issued on
+  // (the comm stream, or the caller's in same-stream mode: copying on the comm stream there raced the
+  // gather on the caller's stream and read a stale buffer).
   at::Tensor flat;
   {
-    c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
+    c10::hip::HIPStreamGuardMasqueradingAsCUDA g(op_stream());
     flat = at::empty({size_ * input.numel()}, input.options());
   }
   std::vector<at::Tensor> all = outputs;
@@ -205,7 +207,7 @@ std::shared_ptr<Work> RcclPG::allgather(std::vector<at::Tensor>& outputs, const 
   return launch(OpType::ALLGATHER, all, [&](hipStream_t s) {
     RINGDP_NCCL_CHECK(ncclAllGather(input.data_ptr(), flat.data_ptr(), input.numel(),
                                     to_nccl_dtype(input.scalar_type()), comm_, s));
-    c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
+    c10::hip::HIPStreamGuardMasqueradingAsCUDA g(c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, device_));
     for (int i = 0; i < size_; ++i)
       outputs[i].copy_(flat.narrow(0, i * input.numel(), input.numel()).view(outputs[i].sizes()),
                        /*non_blocking=*/true);
@@ -264,7 +266,7 @@ std::shared_ptr<Work> RcclPG::gather(std::vector<at::Tensor>& outputs, const at:
     }
     RINGDP_NCCL_CHECK(ncclGroupEnd());
     if (rank_ == root) {
-      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, device_));
       outputs[root].copy_(input, true);
     }
   });
@@ -289,7 +291,7 @@ std::shared_ptr<Work> RcclPG::scatter(at::Tensor& output, std::vector<at::Tensor
     }
     RINGDP_NCCL_CHECK(ncclGroupEnd());
     if (rank_ == root) {
-      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
+      c10::hip::HIPStreamGuardMasqueradingAsCUDA g(c10::hip::getStreamFromExternalMasqueradingAsCUDA(s, device_));
       output.copy_(inputs[root], true);
     }
   });

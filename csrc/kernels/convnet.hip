@@ -755,12 +755,32 @@ __device__ __forceinline__ void ff_wait_packed(unsigned* sync, int npack) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
 
+// pool2 + ReLU of items [lo, hi) (item = position p, 8-channel chunk) of the staged conv2 tile -> a2 /
+// idx2 in HBM and the conv3 operand rows of buffer X3b.  Phase 3 splits the items between the producer
+// and the consumer (the producer is the long pole: 1103 vs 808 us alone at B=65536).
+// items [0, p2split) are the producer's (kernel argument; RINGDP_FF_P2, default 560 of 800: measured
+// 400 / 480 / 560 / 800 -> 1402 / 1387 / 1342 / 1363 us at B=65536)
+__device__ __forceinline__ void ff_pool2(const bf16* Cs, bf16* X3b, bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
+                                         int b, int t, int lo, int hi) {
+  bf16x8* da = reinterpret_cast<bf16x8*>(a2 + (int64_t)b * 6400);
+  uint2* di = reinterpret_cast<uint2*>(idx2 + (int64_t)b * 6400);
+  for (int it = lo + t; it < hi; it += 256) {
+    const int p = it >> 3, c = (it & 7) * 8;
+    bf16x8 v;
+    uint2 code;
+    pool2_code8(Cs + ((p / 10) * 11 + p % 10) * C2_CRS + c, C2_CRS, 11, v, code);
+    da[it] = v;
+    di[it] = code;
+    *reinterpret_cast<bf16x8*>(X3b + p * C3F_XRS + c) = v;
+  }
+}
+
 template <bool U8, bool PACK>
 __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16* __restrict__ packed,
                             const PackSrc& ws, const float* __restrict__ b1, const float* __restrict__ b2,
                             bf16* __restrict__ a1, uint8_t* __restrict__ idx1, bf16* __restrict__ a2,
                             uint8_t* __restrict__ idx2, int B, int b0, int bstep, int nsteps, float mean,
-                            float inv_std, float in_scale, unsigned* sync, int npack) {
+                            float inv_std, float in_scale, unsigned* sync, int npack, int p2split) {
   bf16* XS = reinterpret_cast<bf16*>(smem);
   bf16* X2 = reinterpret_cast<bf16*>(smem + FF_OFF_X2);
   uint32_t* X2u = reinterpret_cast<uint32_t*>(X2);
@@ -890,20 +910,8 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
       }
     }
     __syncthreads();  // [S2] Cs complete
-    // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3
-    if (live) {
-      bf16x8* da = reinterpret_cast<bf16x8*>(a2 + (int64_t)b * 6400);
-      uint2* di = reinterpret_cast<uint2*>(idx2 + (int64_t)b * 6400);
-      for (int it = tid; it < 800; it += 256) {
-        const int p = it >> 3, c = (it & 7) * 8;
-        bf16x8 v;
-        uint2 code;
-        pool2_code8(Cs + ((p / 10) * 11 + p % 10) * C2_CRS + c, C2_CRS, 11, v, code);
-        da[it] = v;
-        di[it] = code;
-        *reinterpret_cast<bf16x8*>(X3 + (s & 1) * FF_X3H + p * C3F_XRS + c) = v;
-      }
-    }
+    // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3 (items [0, FF_P2_PROD); the consumer pools the rest)
+    if (live) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, b, tid, 0, p2split);
     __syncthreads();  // [S3] X3 complete; Cs, X2, CT free
   }
 }
@@ -911,9 +919,11 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
 template <bool PACK>
 __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const PackSrc& ws,
                             const float* __restrict__ b3, const float* __restrict__ bfc, bf16* __restrict__ a3,
-                            uint8_t* __restrict__ idx3, float* __restrict__ logits, int B, int b0, int bstep,
-                            int nsteps, unsigned* sync, int npack) {
-  const bf16* X3 = reinterpret_cast<const bf16*>(smem + FF_OFF_X3);
+                            uint8_t* __restrict__ idx3, float* __restrict__ logits, bf16* __restrict__ a2,
+                            uint8_t* __restrict__ idx2, int Bp, int B, int b0, int bstep, int nsteps,
+                            unsigned* sync, int npack, int p2split) {
+  bf16* X3 = reinterpret_cast<bf16*>(smem + FF_OFF_X3);
+  const bf16* Cs = reinterpret_cast<const bf16*>(smem + FF_OFF_CS);
   bf16* fw = reinterpret_cast<bf16*>(smem + FF_OFF_FW);
   float* fred = reinterpret_cast<float*>(smem + FF_OFF_FR);
   const int tid = threadIdx.x - 256, lane = tid & 63, wave = tid >> 6;
@@ -1010,7 +1020,11 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     if (live_e) fc_reduce(be);
     if (live_m) mfma_ks(xb, std::integral_constant<int, 4>{}, std::integral_constant<int, 11>{});
     __syncthreads();  // [S2]
-    // ---------------- phase 3
+    // ---------------- phase 3: the rest of the producer's pool2 (image s), k-steps 11-17
+    {
+      const int bpr = b0 + s * bstep;
+      if (bpr < Bp) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, bpr, tid, p2split, 800);
+    }
     if (live_m) mfma_ks(xb, std::integral_constant<int, 11>{}, std::integral_constant<int, 18>{});
     __syncthreads();  // [S3]
   }
@@ -1027,7 +1041,7 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
                                                           bf16* __restrict__ a3, uint8_t* __restrict__ idx3,
                                                           float* __restrict__ logits, int B, float mean,
                                                           float inv_std, float in_scale, int ablate,
-                                                          unsigned* sync) {
+                                                          unsigned* sync, int p2split) {
   const int npack = (int)gridDim.x - conv_blocks;
   if (PACK && (int)blockIdx.x >= conv_blocks) {
     if (threadIdx.x < 256) pack_range(ws, pack_out, 0, blockIdx.x - conv_blocks, npack);
@@ -1044,10 +1058,10 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
   // exec-masked sequence whose live ranges the register allocator would have to overlap)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4)
     ff_producer<U8, PACK>(ff_smem, xin, PACK ? pack_out : packed, ws, b1, b2, a1, idx1, a2, idx2,
-                          (ablate & 1) ? 0 : B, b0, bstep, nsteps, mean, inv_std, in_scale, sync, npack);
+                          (ablate & 1) ? 0 : B, b0, bstep, nsteps, mean, inv_std, in_scale, sync, npack, p2split);
   else
-    ff_consumer<PACK>(ff_smem, PACK ? pack_out : packed, ws, b3, bfc, a3, idx3, logits, (ablate & 2) ? 0 : B, b0,
-                      bstep, nsteps, sync, npack);
+    ff_consumer<PACK>(ff_smem, PACK ? pack_out : packed, ws, b3, bfc, a3, idx3, logits, a2, idx2,
+                      (ablate & 1) ? 0 : B, (ablate & 2) ? 0 : B, b0, bstep, nsteps, sync, npack, p2split);
   if (PACK) {  // the last conv workgroup out re-arms the counters
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -2005,38 +2019,12 @@ struct ReduceSegs {
   int count;
 };
 
-// Each workgroup owns 64 outputs of one segment and sums its slices with 16 waves (lane = output,
-// coalesced rows), combined in a fixed order.  16 (not 4) waves: the conv1 / fc1 segments have few
-// outputs (13-20 workgroups) and hundreds of slices, so the per-wave slice chains were the whole cost.
+// Each workgroup owns 64 x vec outputs of one segment (vec = 4: one 16-B load per slice per lane) and sums
+// its slices with 16 waves (coalesced rows), combined in a fixed order.  16 (not 4) waves: the conv1 / fc1
+// segments have few outputs (13-20 workgroups) and hundreds of slices, so the per-wave slice chains were
+// the whole cost; 4 outputs per lane cut the B=100 merged reduction's wave count 4x (it was latency rounds).
 constexpr int kRedWaves = 16;
-__global__ __launch_bounds__(1024) void slab_reduce_kernel(ReduceSegs segs) {
-  __shared__ float part[kRedWaves][64];
-  int blk = blockIdx.x, sidx = 0;
-  while (sidx < segs.count - 1 && blk >= segs.seg[sidx].blocks) {
-    blk -= segs.seg[sidx].blocks;
-    ++sidx;
-  }
-  const ReduceSeg& sg = segs.seg[sidx];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blk * 64 + lane;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  if (i < sg.n) {
-    const float* pp = sg.slabs + sg.off + i;
-    int s = wave;
-    for (; s + 3 * kRedWaves < sg.nslices; s += 4 * kRedWaves) {
-      a0 += pp[(int64_t)s * sg.stride];
-      a1 += pp[(int64_t)(s + kRedWaves) * sg.stride];
-      a2 += pp[(int64_t)(s + 2 * kRedWaves) * sg.stride];
-      a3 += pp[(int64_t)(s + 3 * kRedWaves) * sg.stride];
-    }
-    for (; s < sg.nslices; s += kRedWaves) a0 += pp[(int64_t)s * sg.stride];
-  }
-  part[wave][lane] = (a0 + a1) + (a2 + a3);
-  __syncthreads();
-  if (wave != 0 || i >= sg.n) return;
-  float v = 0.f;
-#pragma unroll
-  for (int w = 0; w < kRedWaves; ++w) v += part[w][lane];
+__device__ __forceinline__ void red_store(const ReduceSeg& sg, int64_t i, float v) {
   if (sg.mode == 0) {
     sg.out[i] = v;
   } else if (sg.mode == 2) {
@@ -2048,9 +2036,52 @@ __global__ __launch_bounds__(1024) void slab_reduce_kernel(ReduceSegs segs) {
   }
 }
 
+__global__ __launch_bounds__(1024) void slab_reduce_kernel(ReduceSegs segs) {
+  __shared__ f32x4 part[kRedWaves][64];
+  int blk = blockIdx.x, sidx = 0;
+  while (sidx < segs.count - 1 && blk >= segs.seg[sidx].blocks) {
+    blk -= segs.seg[sidx].blocks;
+    ++sidx;
+  }
+  const ReduceSeg& sg = segs.seg[sidx];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int V = sg.vec;
+  const int64_t i0 = ((int64_t)blk * 64 + lane) * V;
+  f32x4 a0 = zero_f32x4(), a1 = zero_f32x4(), a2 = zero_f32x4(), a3 = zero_f32x4();
+  if (i0 < sg.n) {
+    const float* pp = sg.slabs + sg.off + i0;
+    int s = wave;
+    if (V == 4) {
+      for (; s + 3 * kRedWaves < sg.nslices; s += 4 * kRedWaves) {
+        a0 += *reinterpret_cast<const f32x4*>(pp + (int64_t)s * sg.stride);
+        a1 += *reinterpret_cast<const f32x4*>(pp + (int64_t)(s + kRedWaves) * sg.stride);
+        a2 += *reinterpret_cast<const f32x4*>(pp + (int64_t)(s + 2 * kRedWaves) * sg.stride);
+        a3 += *reinterpret_cast<const f32x4*>(pp + (int64_t)(s + 3 * kRedWaves) * sg.stride);
+      }
+      for (; s < sg.nslices; s += kRedWaves) a0 += *reinterpret_cast<const f32x4*>(pp + (int64_t)s * sg.stride);
+    } else {
+      for (; s + 3 * kRedWaves < sg.nslices; s += 4 * kRedWaves) {
+        a0[0] += pp[(int64_t)s * sg.stride];
+        a1[0] += pp[(int64_t)(s + kRedWaves) * sg.stride];
+        a2[0] += pp[(int64_t)(s + 2 * kRedWaves) * sg.stride];
+        a3[0] += pp[(int64_t)(s + 3 * kRedWaves) * sg.stride];
+      }
+      for (; s < sg.nslices; s += kRedWaves) a0[0] += pp[(int64_t)s * sg.stride];
+    }
+  }
+  part[wave][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wave != 0 || i0 >= sg.n) return;
+  f32x4 v = zero_f32x4();
+#pragma unroll
+  for (int w = 0; w < kRedWaves; ++w) v += part[w][lane];
+  for (int k = 0; k < V; ++k) red_store(sg, i0 + k, v[k]);
+}
+
 ReduceSeg seg(const float* slabs, int64_t stride, int64_t off, int64_t n, int nslices, float* out,
               int mode = 0, int cin = 0, int cout = 0) {
-  return ReduceSeg{slabs, stride, off, n, nslices, out, mode, cin, cout, (int)((n + 63) / 64)};
+  const int vec = ((off | stride | n) & 3) == 0 ? 4 : 1;
+  return ReduceSeg{slabs, stride, off, n, nslices, out, mode, cin, cout, (int)((n + 64 * vec - 1) / (64 * vec)), vec};
 }
 
 void launch_reduce(const std::vector<ReduceSeg>& v, hipStream_t s) {
@@ -2144,6 +2175,8 @@ void cn_forward_fused(const void* x, bool u8, const float* const* w, const float
   bf16* pk = static_cast<bf16*>(packed);
   bf16 *a1b = static_cast<bf16*>(a1), *a2b = static_cast<bf16*>(a2), *a3b = static_cast<bf16*>(a3);
   static const int ablate = [] { const char* v = getenv("RINGDP_FF_ABLATE"); return v ? atoi(v) : 0; }();
+  static const int p2split = [] { const char* v = getenv("RINGDP_FF_P2"); const int n = v ? atoi(v) : 560;
+                                  return n >= 0 && n <= 800 ? n : 560; }();
   // In-launch packing (RINGDP_FF_INPACK=1) is correct but slow on MI355X: the pack workgroups' agent-scope
   // release has to write their XCD's L2 back before the other XCDs may read the fragments (measured
   // B=100: 114 us against 23 us with the separate pack launch), so it is off by default.
@@ -2156,22 +2189,22 @@ void cn_forward_fused(const void* x, bool u8, const float* const* w, const float
     if (u8)
       fused_fwd_kernel<true, true><<<grid, 512, 0, s>>>(x, nullptr, ws, pk, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
                                                         idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
-                                                        sync);
+                                                        sync, p2split);
     else
       fused_fwd_kernel<false, true><<<grid, 512, 0, s>>>(x, nullptr, ws, pk, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
                                                          idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
-                                                         sync);
+                                                         sync, p2split);
     return;
   }
   pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(ws, pk);
   if (u8)
     fused_fwd_kernel<true, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
-                                                       nullptr);
+                                                       nullptr, p2split);
   else
     fused_fwd_kernel<false, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
                                                         idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
-                                                        nullptr);
+                                                        nullptr, p2split);
 }
 
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,

@@ -196,6 +196,7 @@ struct ReduceSeg {
              // 2: fc1 slab in fc_bwd thread order (n*8 + j)*256 + t -> dWfc[n][co*16 + w]
   int cin, cout;
   int blocks;
+  int vec;  // outputs per thread: 4 when off, stride and n are multiples of 4 floats (16-B loads), else 1
 };
 using ReduceList = std::vector<ReduceSeg>;
 void cn_launch_reduce(const ReduceList& segs, hipStream_t s);  // one launch, at most 8 segments
