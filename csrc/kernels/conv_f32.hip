@@ -567,12 +567,29 @@ constexpr int layout_bn(Layout l) { return l == L256x32 ? 32 : l == L128x64 ? 64
 
 // Forward / data-gradient GEMMs: m = pixels (huge), n = channels.  Weight gradients: m = output
 // channels, n = input channels x taps (+ bias column), k = batch x pixels.
-Layout pick_layout(int M, int N) {
+int f32_num_cus() {
+  static const int n = [] {
+    int dev = 0, v = 256;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+Layout pick_layout(int M, int N, int slices) {
   if (M <= 32 && N <= 32) return L32x32K4;
   if (M <= 32) return L32x128;
-  if (N <= 32) return L256x32;
-  if (N <= 64 || M >= 128) return L128x64;
-  return L64x128;
+  Layout l = L64x128;
+  if (N <= 32) l = L256x32;
+  else if (N <= 64 || M >= 128) l = L128x64;
+  // Small batches (the reference's 100 images per rank): the big tiles leave most CUs idle with one
+  // long K loop each (conv3's data gradient at B=100: 79 workgroups, 97 us); 32x32 tiles with the
+  // k-range split over the 4 waves fill the chip instead.
+  const int bm = l == L256x32 ? 256 : (l == L128x64 ? 128 : 64), bn = l == L256x32 ? 32 : (l == L128x64 ? 64 : 128);
+  const long blocks = (long)((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+  if (blocks * slices < f32_num_cus()) return L32x32K4;
+  return l;
 }
 
 template <int WM, int WN, int TM, int TN, class LA, class LB, class Epi>
@@ -589,7 +606,7 @@ void launch_layout(int M, int N, int K, int per, int slices, int bias_col, const
 template <class LA, class LB, class Epi>
 void launch_gemm(int M, int N, int K, int per, int slices, int bias_col, const LA& la, const LB& lb,
                  const Epi& epi, hipStream_t s) {
-  switch (pick_layout(M, N)) {
+  switch (pick_layout(M, N, slices)) {
     case L32x32K4: launch_layout<1, 1, 2, 2>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
     case L256x32: launch_layout<4, 1, 4, 2>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
     case L128x64: launch_layout<4, 1, 2, 4>(M, N, K, per, slices, bias_col, la, lb, epi, s); break;
@@ -807,7 +824,7 @@ int64_t batch_chunk(int64_t B, std::initializer_list<int64_t> per_image) {
 
 int wgrad_slices(int M, int N, int64_t K) {
   // enough slices to put >= ~2048 workgroups on the 256 CUs, each slice >= 1024 deep
-  const Layout l = pick_layout(M, N);
+  const Layout l = pick_layout(M, N, 1 << 20);  // the big-tile layout (the launch may still pick 32x32)
   const int bm = layout_bm(l), bn = layout_bn(l);
   const int64_t tiles = static_cast<int64_t>((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   int64_t s = (2048 + tiles - 1) / tiles;

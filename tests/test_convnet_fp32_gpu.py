@@ -88,8 +88,10 @@ def test_conv_f32_batch_chunks(monkeypatch):
                                                    (3, 3, 8, 8, 3, 1, False, 2), (7, 32, 13, 64, 3, 0, False, 1),
                                                    (4, 5, 9, 80, 3, 1, False, 1)])
 def test_conv_f32_pool_fused(B, Cin, H, K, R, pad, u8, st):
-    """conv + bias + ReLU + 2x2/s2 max-pool in one launch == conv kernel then the pool kernel (bit-exact:
-    same products in the same order), and == ATen."""
+    """conv + bias + ReLU + 2x2/s2 max-pool in one launch == conv kernel then the pool kernel, and == ATen.
+    Bit-exact where both launches use the same tile layout; at small batches the plain conv may take the
+    32x32 tiles with the k-range split over 4 waves (another fp32 summation order): then equal to a few
+    ulp, and the argmax codes equal except at near-ties."""
     g = torch.Generator(device=DEV).manual_seed(B * 7 + K)
     if u8:
         x = torch.randint(0, 256, (B, Cin, H, H), dtype=torch.uint8, device=DEV, generator=g)
@@ -104,8 +106,11 @@ def test_conv_f32_pool_fused(B, Cin, H, K, R, pad, u8, st):
     a, code = C.f32_conv_pool_fwd(x, w, b, pad, mean, std, st)
     z = C.f32_conv_fwd(x, w, b, pad, mean, std)
     a2, code2 = C.f32_pool_relu_fwd(z, 2, st)
-    assert torch.equal(a, a2)
-    assert torch.equal(code, code2)
+    if not torch.equal(a, a2):
+        torch.testing.assert_close(a, a2, rtol=4e-6, atol=4e-6)
+        assert float((code == code2).float().mean()) > 0.995
+    else:
+        assert torch.equal(code, code2)
     ref = F.max_pool2d(F.relu(F.conv2d(xf.double(), w.double(), b.double(), padding=pad)), 2, st).float()
     _close(a, ref, rtol=1e-5, atol=1e-5)
 
