@@ -69,6 +69,10 @@ __device__ __forceinline__ int pix_base(int m) {
   return (2 * py + (t >> 1)) * PADW + 2 * px + (t & 1);
 }
 
+// Small batches: one image per workgroup (its 4 waves split the image) instead of one per wave, so a
+// B=100 step runs 100 workgroups x 4 waves, not 25 x 4 waves each walking a whole image (71 us).
+__host__ __device__ inline bool split_mode(int64_t B) { return B < 2048; }
+
 template <bool U8>
 __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restrict__ x, const float* __restrict__ w1,
                                                              const float* __restrict__ b1, float* __restrict__ a1,
@@ -95,16 +99,19 @@ __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restr
     for (int r = 0; r < 4; ++r) bias[j][r] = b1[16 * j + 4 * lk + r];
   const int tap = lr & 3;
 
-  const int rounds = (B + WAVES * gridDim.x - 1) / (WAVES * gridDim.x);
+  // small batches (split_mode): the 4 waves share one image per round, each taking every 4th pixel group
+  const bool split = split_mode(B);
+  const int ipr = split ? 1 : WAVES;  // images per workgroup round
+  const int rounds = (B + ipr * gridDim.x - 1) / (ipr * gridDim.x);
   for (int round = 0; round < rounds; ++round) {
-    const int b = (round * gridDim.x + blockIdx.x) * WAVES + wave;
+    const int b = split ? round * gridDim.x + blockIdx.x : (round * gridDim.x + blockIdx.x) * WAVES + wave;
     __syncthreads();  // the previous image's reads are done (uniform trip count: every wave gets here)
     if (b < B) stage_image<U8>(im, x, b, mean, inv_std, lane);
     __syncthreads();
     if (b >= B) continue;
     float* ab = a1 + static_cast<int64_t>(b) * C1 * NWIN;
     unsigned char* cb = code1 + static_cast<int64_t>(b) * C1 * NWIN;
-    for (int g = 0; g < (4 * NWIN + 15) / 16; ++g) {
+    for (int g = split ? wave : 0; g < (4 * NWIN + 15) / 16; g += split ? WAVES : 1) {
       const int m = 16 * g + lr;
       const int base = m < 4 * NWIN ? pix_base(m) : 0;
       f32x4 acc[2] = {dev::zero_f32x4(), dev::zero_f32x4()};
@@ -178,9 +185,11 @@ __global__ __launch_bounds__(256) void conv1_wgrad_f32_kernel(const void* __rest
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = dev::zero_f32x4();
 
-  const int rounds = (B + WAVES * gridDim.x - 1) / (WAVES * gridDim.x);
+  const bool split = split_mode(B);
+  const int ipr = split ? 1 : WAVES;
+  const int rounds = (B + ipr * gridDim.x - 1) / (ipr * gridDim.x);
   for (int round = 0; round < rounds; ++round) {
-    const int b = (round * gridDim.x + blockIdx.x) * WAVES + wave;
+    const int b = split ? round * gridDim.x + blockIdx.x : (round * gridDim.x + blockIdx.x) * WAVES + wave;
     __syncthreads();
     if (b < B) stage_image<U8>(im, x, b, mean, inv_std, lane);
     __syncthreads();
@@ -188,7 +197,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_f32_kernel(const void* __rest
     const float* db = da1 + static_cast<int64_t>(b) * C1 * NWIN;
     const unsigned char* cbp = code1 + static_cast<int64_t>(b) * C1 * NWIN;
     // one pooled row (13 windows) at a time: its 52 gradient / code loads are issued together
-    for (int py = 0; py < PW1; ++py) {
+    for (int py = split ? wave : 0; py < PW1; py += split ? WAVES : 1) {
       float dv[PW1][2];
       int cv[PW1][2];
 #pragma unroll
@@ -240,8 +249,8 @@ __global__ __launch_bounds__(256) void conv1_wgrad_f32_kernel(const void* __rest
 }
 
 int conv1_blocks(int64_t B) {
-  // 4 images per workgroup round; ~4 workgroups per CU, at least a few rounds each
-  const int64_t want = (B + WAVES - 1) / WAVES;
+  // 4 images per workgroup round (1 in split mode); ~4 workgroups per CU, at least a few rounds each
+  const int64_t want = split_mode(B) ? B : (B + WAVES - 1) / WAVES;
   return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(want, 1024)));
 }
 

@@ -1089,12 +1089,13 @@ constexpr int FC_SLAB = 10 * 2048 + 10 + 128;  // dWfc + dbfc + db3 (the conv3 b
 // kCE: the logits gradient is formed here from the cross-entropy forward's logits / log-sum-exp
 // (same expression as ce_bwd_kernel, elementwise.hip) - 80 threads per group of 8 images into LDS -
 // instead of read from a [B,10] tensor: the separate ce_bwd launch disappears.
+// The body runs as its own launch (fc_bwd_kernel) or as the first workgroups of the conv3 backward launch at
+// small batches (conv3_bwd_kernel<true>, blk = that workgroup's fc index; da3m == nullptr: the conv3
+// roles form their own compact gradient, C3Pre::load).
 template <bool kCE>
-__global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3,
-                                                     const bf16* __restrict__ packed,
-                                                     const float* __restrict__ dl,
-                                                     bf16* __restrict__ da3m, float* __restrict__ slabs,
-                                                     int B, int imgs, CeFuse ce) {
+__device__ __forceinline__ void fc_bwd_body(const bf16* __restrict__ a3, const bf16* __restrict__ packed,
+                                            const float* __restrict__ dl, bf16* __restrict__ da3m,
+                                            float* __restrict__ slabs, int B, int imgs, const CeFuse& ce, int blk) {
   const int t = threadIdx.x;
   const int wd = t >> 4, co0 = (t & 15) * 8;  // this thread's 8 activations: window wd, channels co0..
   float wr[8][10];
@@ -1116,29 +1117,25 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
   float bacc = 0.f, dsum[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) dsum[j] = 0.f;
-  const int b0 = blockIdx.x * imgs, nimg = min(imgs, B - b0);
-  __shared__ float gl[8][10];
-  float ce_scale = 0.f;
-  if constexpr (kCE) ce_scale = ce.reduction == 0 ? 1.f : ce.grad_out[0] / ce.denom[0];
-  for (int k0 = 0; k0 < nimg; k0 += 8) {
-    if constexpr (kCE) {
-      if (k0) __syncthreads();  // the previous group's reads of gl are done
-      if (t < 80) {
-        const int k = t / 10, n = t - 10 * k;
-        float g = 0.f;
-        if (k0 + k < nimg) {
-          const int b = b0 + k0 + k;
-          const int64_t y = ce.labels[b];
-          if (y != ce.ignore_index) {
-            const float p = __expf(ce.logits[(int64_t)b * 10 + n] - ce.lse[b]);
-            const float q = (n == y ? (1.f - ce.eps) : 0.f) + ce.eps / 10.f;
-            g = (p - q) * (ce.reduction == 0 ? ce.grad_out[b] : ce_scale);
-          }
-        }
-        gl[k][n] = g;
+  const int b0 = blk * imgs, nimg = min(imgs, B - b0);
+  // kCE: the logits gradient of all this block's images (<= 128 x 10) formed once into LDS, one barrier
+  __shared__ float gl[128 * 10];
+  if constexpr (kCE) {
+    const float ce_scale = ce.reduction == 0 ? 1.f : ce.grad_out[0] / ce.denom[0];
+    for (int e = t; e < nimg * 10; e += 256) {
+      const int k = e / 10, n = e - 10 * k, b = b0 + k;
+      float g = 0.f;
+      const int64_t y = ce.labels[b];
+      if (y != ce.ignore_index) {
+        const float p = __expf(ce.logits[(int64_t)b * 10 + n] - ce.lse[b]);
+        const float q = (n == y ? (1.f - ce.eps) : 0.f) + ce.eps / 10.f;
+        g = (p - q) * (ce.reduction == 0 ? ce.grad_out[b] : ce_scale);
       }
-      __syncthreads();
+      gl[e] = g;
     }
+    __syncthreads();
+  }
+  for (int k0 = 0; k0 < nimg; k0 += 8) {
     bf16x8 av[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -1149,7 +1146,7 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
         const int b = b0 + k0 + k;
         float g[10];
 #pragma unroll
-        for (int n = 0; n < 10; ++n) g[n] = kCE ? gl[k][n] : dl[(int64_t)b * 10 + n];
+        for (int n = 0; n < 10; ++n) g[n] = kCE ? gl[(k0 + k) * 10 + n] : dl[(int64_t)b * 10 + n];
         bf16x8 v;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -1164,14 +1161,14 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
           dsum[j] += m;
           v[j] = (bf16)m;
         }
-        *reinterpret_cast<bf16x8*>(da3m + (int64_t)b * 2048 + wd * 128 + co0) = v;
-        if (t < 10) bacc += kCE ? gl[k][t] : dl[(int64_t)b * 10 + t];
+        if (da3m) *reinterpret_cast<bf16x8*>(da3m + (int64_t)b * 2048 + wd * 128 + co0) = v;
+        if (t < 10) bacc += kCE ? gl[(k0 + k) * 10 + t] : dl[(int64_t)b * 10 + t];
       }
     }
   }
   // slab in thread order (coalesced): element (n*8 + j)*256 + t; the reduction (mode 2) maps it back
   // to dWfc[n][co*16 + w]
-  float* slab = slabs + (int64_t)blockIdx.x * FC_SLAB;
+  float* slab = slabs + (int64_t)blk * FC_SLAB;
 #pragma unroll
   for (int n = 0; n < 10; ++n)
 #pragma unroll
@@ -1192,6 +1189,13 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
   }
   __syncthreads();
   if (t < 128) slab[20490 + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+}
+
+template <bool kCE>
+__global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3, const bf16* __restrict__ packed,
+                                                     const float* __restrict__ dl, bf16* __restrict__ da3m,
+                                                     float* __restrict__ slabs, int B, int imgs, CeFuse ce) {
+  fc_bwd_body<kCE>(a3, packed, dl, da3m, slabs, B, imgs, ce, blockIdx.x);
 }
 
 // (2) conv3 backward, two roles in one launch of 256-thread workgroups, two per CU (a CU usually
@@ -1222,14 +1226,61 @@ constexpr int C3_WSLAB = 576 * 128;  // dW3t
 
 // The compact F3-backward input of one image, held in registers while the previous image is
 // computed on: d(a3) chunk + its pool3 argmax bytes (threads < 256).
+// Where the conv3 backward roles get an image's compact d(a3): the fc1 backward launch's da3m, or (small
+// batches, fc1 backward inside this launch) computed in place from a3, the logits gradient and the packed
+// fc1 weights - the same expression and order as fc_bwd_body, so the values are bit-identical.
+struct C3Src {
+  const bf16* da3m;  // null: compute
+  const bf16* a3;
+  const bf16* packed;
+  const float* dl;   // logits gradient, or null with ce
+  CeFuse ce;
+};
+
 struct C3Pre {
   bf16x8 da;
   uint2 id;
-  __device__ __forceinline__ void load(const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3, int b,
-                                       int tid) {
+  template <bool kFC>
+  __device__ __forceinline__ void load(const C3Src& src, const uint8_t* __restrict__ idx3, int b, int tid) {
     if (tid < 256) {
-      da = reinterpret_cast<const bf16x8*>(da3m + (int64_t)b * 2048)[tid];
       id = reinterpret_cast<const uint2*>(idx3 + (int64_t)b * 2048)[tid];
+      if (!kFC) {
+        da = reinterpret_cast<const bf16x8*>(src.da3m + (int64_t)b * 2048)[tid];
+        return;
+      }
+      const int wd = tid >> 4, co0 = (tid & 15) * 8;
+      const bf16x8 av = reinterpret_cast<const bf16x8*>(src.a3 + (int64_t)b * 2048)[tid];
+      float g[10];
+      if (src.dl) {
+#pragma unroll
+        for (int n = 0; n < 10; ++n) g[n] = src.dl[(int64_t)b * 10 + n];
+      } else {
+        const CeFuse& ce = src.ce;
+        const int64_t y = ce.labels[b];
+        const float sc = ce.reduction == 0 ? ce.grad_out[b] : ce.grad_out[0] / ce.denom[0];
+        const float lse = ce.lse[b];
+#pragma unroll
+        for (int n = 0; n < 10; ++n) {
+          float gv = 0.f;
+          if (y != ce.ignore_index) {
+            const float p = __expf(ce.logits[(int64_t)b * 10 + n] - lse);
+            const float q = (n == y ? (1.f - ce.eps) : 0.f) + ce.eps / 10.f;
+            gv = (p - q) * sc;
+          }
+          g[n] = gv;
+        }
+      }
+      const bf16x8* wsrc = reinterpret_cast<const bf16x8*>(src.packed + PFC_OFF + (wd * 128 + co0) * 10);
+      bf16x8 wv[10];
+#pragma unroll
+      for (int h = 0; h < 10; ++h) wv[h] = wsrc[h];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int n = 0; n < 10; ++n) s = fmaf(g[n], (float)wv[(10 * j + n) / 8][(10 * j + n) % 8], s);
+        da[j] = (bf16)((float)av[j] > 0.f ? s : 0.f);
+      }
     }
   }
 };
@@ -1271,7 +1322,8 @@ __device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int
 // m-tiles (dz3 row pairs) hit disjoint da2 rows, so their read-add-writes are independent; consecutive
 // taps may hit the same da2 words from different lanes, so a compiler barrier keeps tap t+1's reads
 // behind tap t's writes (LDS executes one wave's instructions in order).  Fixed order: deterministic.
-__device__ __forceinline__ void conv3_dgrad_role(char* smem, const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
+template <bool kFC>
+__device__ __forceinline__ void conv3_dgrad_role(char* smem, const C3Src& src, const uint8_t* __restrict__ idx3,
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
                                  bf16* __restrict__ dz2, int b_first, int b_end, int b_step) {
   bf16* P = reinterpret_cast<bf16*>(smem);
@@ -1339,7 +1391,7 @@ __device__ __forceinline__ void conv3_dgrad_role(char* smem, const bf16* __restr
   };
   C3Pre pre;
   int b = b_first;
-  if (b < b_end) pre.load(da3m, idx3, b, tid);
+  if (b < b_end) pre.template load<kFC>(src, idx3, b, tid);
   for (; b < b_end; b += b_step) {
     __syncthreads();  // previous image fully consumed (P, DA, AM)
     c3_expand(pre, tid, [&](int r) {
@@ -1348,7 +1400,7 @@ __device__ __forceinline__ void conv3_dgrad_role(char* smem, const bf16* __restr
     });
     codes_glds(idx2, b, AM, wave, lane);  // this image's codes land during the MFMA phase
     const int nb = b + b_step;
-    if (nb < b_end) pre.load(da3m, idx3, nb, tid);
+    if (nb < b_end) pre.template load<kFC>(src, idx3, nb, tid);
     __syncthreads();
     mfma_phase();
     c_dma_wait();
@@ -1388,7 +1440,8 @@ __device__ __forceinline__ void conv3_dgrad_role(char* smem, const bf16* __restr
 
 // wgrad: workgroup half h of an image slice covers n-tiles 18h..18h+17 of dW3t [576][128];
 // wave (wm, wn) owns m-tiles (co) 4wm..4wm+3 x n-tiles 18h + 9wn .. +8.
-__device__ __forceinline__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
+template <bool kFC>
+__device__ __forceinline__ void conv3_wgrad_role(char* smem, const bf16* __restrict__ a2, const C3Src& src,
                                  const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
                                  int nslices, int slice, int h) {
   bf16* D = reinterpret_cast<bf16*>(smem);
@@ -1407,7 +1460,7 @@ __device__ __forceinline__ void conv3_wgrad_role(char* smem, const bf16* __restr
   const int b_lo = slice * per, b_hi = min(B, b_lo + per);
   C3Pre pre;
   if (b_lo < b_hi) {
-    pre.load(da3m, idx3, b_lo, tid);
+    pre.template load<kFC>(src, idx3, b_lo, tid);
     a2_glds(a2, b_lo, R, wave, lane, 4);
   }
   for (int b = b_lo; b < b_hi; ++b) {
@@ -1417,7 +1470,7 @@ __device__ __forceinline__ void conv3_wgrad_role(char* smem, const bf16* __restr
     a2_relayout(R, X, tid, 256);
     __syncthreads();  // D, X complete; R free
     if (b + 1 < b_hi) {  // lands during the MFMAs
-      pre.load(da3m, idx3, b + 1, tid);
+      pre.template load<kFC>(src, idx3, b + 1, tid);
       a2_glds(a2, b + 1, R, wave, lane, 4);
     }
 #pragma unroll
@@ -1457,20 +1510,34 @@ __device__ __forceinline__ void conv3_wgrad_role(char* smem, const bf16* __restr
   }
 }
 
-__global__ __launch_bounds__(256, 2) void conv3_bwd_kernel(const bf16* __restrict__ a2,
-                                                           const uint8_t* __restrict__ idx2,
-                                                           const bf16* __restrict__ da3m,
-                                                           const uint8_t* __restrict__ idx3,
-                                                           const bf16* __restrict__ packed,
-                                                           bf16* __restrict__ dz2, int B,
-                                                           float* __restrict__ slabs, int n_wgrad,
-                                                           int n_dgrad, int b_dgrad) {
+// kFC (small batches): workgroups [0, n_fc) run the fc1 backward (weight / bias gradient slabs only) and the
+// conv3 roles form each image's compact gradient themselves (C3Src without da3m): the fc1 backward launch
+// disappears.  One workgroup per CU then (the compact-gradient load holds the fc1 weights in registers).
+template <bool kFC>
+__global__ __launch_bounds__(256, kFC ? 1 : 2) void conv3_bwd_kernel(const bf16* __restrict__ a2,
+                                                                     const uint8_t* __restrict__ idx2, C3Src src,
+                                                                     const uint8_t* __restrict__ idx3,
+                                                                     const bf16* __restrict__ packed,
+                                                                     bf16* __restrict__ dz2, int B,
+                                                                     float* __restrict__ slabs, int n_wgrad,
+                                                                     int n_dgrad, int b_dgrad, int n_fc,
+                                                                     float* __restrict__ fc_slabs, int fc_n_imgs) {
   __shared__ __attribute__((aligned(16))) char smem[C3B_LDS];
-  const int blk = blockIdx.x;
+  int blk = blockIdx.x;
+  if (kFC) {
+    if (blk < n_fc) {
+      if (src.dl)
+        fc_bwd_body<false>(src.a3, packed, src.dl, nullptr, fc_slabs, B, fc_n_imgs, src.ce, blk);
+      else
+        fc_bwd_body<true>(src.a3, packed, nullptr, nullptr, fc_slabs, B, fc_n_imgs, src.ce, blk);
+      return;
+    }
+    blk -= n_fc;
+  }
   int b_first = blk, b_end = b_dgrad, b_step = n_dgrad;
   if (blk >= n_dgrad) {
     const int w = blk - n_dgrad;
-    conv3_wgrad_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w >> 1, w & 1);
+    conv3_wgrad_role<kFC>(smem, a2, src, idx3, slabs, B, n_wgrad, w >> 1, w & 1);
     // images [b_dgrad, B) of the data gradient go to the wgrad workgroups once their slice is done: a
     // dgrad workgroup is slower per image than its wgrad neighbour (pool2 backward, barrier phases), so
     // with one of each per CU the wgrad half would otherwise idle (static split: deterministic)
@@ -1480,7 +1547,7 @@ __global__ __launch_bounds__(256, 2) void conv3_bwd_kernel(const bf16* __restric
     b_end = B;
     b_step = 2 * n_wgrad;
   }
-  conv3_dgrad_role(smem, da3m, idx3, idx2, packed, dz2, b_first, b_end, b_step);  // one call site: inlined
+  conv3_dgrad_role<kFC>(smem, src, idx3, idx2, packed, dz2, b_first, b_end, b_step);  // one call site: inlined
 }
 
 __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
@@ -2115,6 +2182,15 @@ int num_cus() {
 
 inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// largest batch whose fc1 backward runs inside the conv3 backward launch (RINGDP_CN_FC_IN_C3_MAX overrides)
+int fc_in_c3_max_batch() {
+  static const int v = [] {
+    const char* e = std::getenv("RINGDP_CN_FC_IN_C3_MAX");
+    return e ? std::atoi(e) : 2048;
+  }();
+  return v;
+}
+
 // largest batch whose fc1 runs inside the conv3 forward launch (RINGDP_CN_FC_FUSED_MAX overrides)
 int fc_fused_max_batch() {
   static const int v = [] {
@@ -2328,15 +2404,24 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
   int nd, ws;
   c3_split(B, dz2 != nullptr, nd, ws);
   const int fs = cdiv(B, fc_imgs(B));
-  if (ce)
-    fc_bwd_kernel<true><<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), nullptr,
-                                           static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), *ce);
-  else
-    fc_bwd_kernel<false><<<fs, 256, 0, s>>>(static_cast<const bf16*>(a3), static_cast<const bf16*>(packed), dl,
-                                            static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), CeFuse{});
-  conv3_bwd_kernel<<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m),
-                                             idx3, static_cast<const bf16*>(packed), static_cast<bf16*>(dz2), B,
-                                             c3_slabs, ws, nd, c3_dgrad_images(B, nd));
+  const bf16* a3b = static_cast<const bf16*>(a3);
+  const bf16* pk = static_cast<const bf16*>(packed);
+  const CeFuse cef = ce ? *ce : CeFuse{};
+  if (B <= fc_in_c3_max_batch()) {  // fc1 backward inside the conv3 backward launch
+    const C3Src src{nullptr, a3b, pk, ce ? nullptr : dl, cef};
+    conv3_bwd_kernel<true><<<fs + nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
+                                                             static_cast<bf16*>(dz2), B, c3_slabs, ws, nd,
+                                                             c3_dgrad_images(B, nd), fs, fc_slabs, fc_imgs(B));
+  } else {
+    if (ce)
+      fc_bwd_kernel<true><<<fs, 256, 0, s>>>(a3b, pk, nullptr, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), cef);
+    else
+      fc_bwd_kernel<false><<<fs, 256, 0, s>>>(a3b, pk, dl, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), cef);
+    const C3Src src{static_cast<const bf16*>(da3m), a3b, pk, dl, cef};
+    conv3_bwd_kernel<false><<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
+                                                         static_cast<bf16*>(dz2), B, c3_slabs, ws, nd,
+                                                         c3_dgrad_images(B, nd), 0, nullptr, 0);
+  }
   ReduceList r{seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
                seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),
                seg(fc_slabs, FC_SLAB, 20480, 10, fs, dbfc)};

@@ -429,3 +429,31 @@ def test_fused_forward_matches_separate_kernels(B, u8):
         assert torch.equal(lg, lg_f)
     else:
         torch.testing.assert_close(lg_f, lg, rtol=1e-4, atol=1e-4)
+
+
+def test_fc_backward_inside_conv3_launch_matches_separate():
+    """B <= 2048: the fc1 backward runs as the first workgroups of the conv3 backward launch and the conv3
+    roles form the compact gradient themselves; B = 2049 takes the separate fc1 launch.  With a zero
+    logits gradient for the extra image, dz2 of the shared 2048 images is bit-identical and the weight
+    gradients agree to summation order."""
+    torch.manual_seed(11)
+    dev = torch.device("cuda")
+    ws = weights(dev, 13)
+    w3, b3, wf, bfc = ws[4], ws[5], ws[6], ws[7]
+    pk = packed(ws)
+    B = 2049
+    z2 = torch.randn(B, 11, 11, 64, device=dev).bfloat16()
+    a2, idx2 = pool2_ref(z2)
+    logits, a3, idx3 = C().cn_conv3_fc_fwd(a2, pk, b3, bfc)
+    dl = torch.randn(B, 10, device=dev)
+    dl[-1] = 0
+    outs = []
+    for n in (B - 1, B):
+        g = [torch.empty_like(t) for t in (w3, b3, wf, bfc)]
+        dz2 = C().cn_conv3_fc_bwd(a2[:n].contiguous(), idx2[:n].contiguous(), a3[:n].contiguous(),
+                                  idx3[:n].contiguous(), wf, dl[:n].contiguous(), pk, True, *g)
+        outs.append((dz2, g))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0][: B - 1])
+    for a, b in zip(outs[0][1], outs[1][1]):  # other slab partitions: other fp32 summation orders
+        assert float((a - b).norm() / b.norm()) < 1e-5
