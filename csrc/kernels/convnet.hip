@@ -1083,8 +1083,9 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
 // was 4 of 32 and latency-bound at 21 us), fewer fp32 slabs at large ones (B=32768: 512 of 64 images,
 // halving the 84 MB of slab traffic)
 __host__ __device__ inline int fc_imgs(int B) { return B <= 1024 ? 4 : (B >= 65536 ? 128 : (B >= 32768 ? 64 : 32)); }
-constexpr int FC_SLAB = 10 * 2048 + 10 + 128;  // dWfc + dbfc + db3 (the conv3 bias gradient is the sum of
-                                                // d(a3) over windows: no MFMA tile needed for it)
+constexpr int FC_SLAB = 10 * 2048 + 10 + 128 + 2;  // dWfc + dbfc + db3 (the conv3 bias gradient is the sum
+                                                    // of d(a3) over windows: no MFMA tile needed for it),
+                                                    // padded to a 16-B multiple (vector slab reduction)
 
 // kCE: the logits gradient is formed here from the cross-entropy forward's logits / log-sum-exp
 // (same expression as ce_bwd_kernel, elementwise.hip) - 80 threads per group of 8 images into LDS -
@@ -2087,10 +2088,10 @@ struct ReduceSegs {
 };
 
 // Each workgroup owns 64 x vec outputs of one segment (vec = 4: one 16-B load per slice per lane) and sums
-// its slices with 16 waves (coalesced rows), combined in a fixed order.  16 (not 4) waves: the conv1 / fc1
-// segments have few outputs (13-20 workgroups) and hundreds of slices, so the per-wave slice chains were
-// the whole cost; 4 outputs per lane cut the B=100 merged reduction's wave count 4x (it was latency rounds).
-constexpr int kRedWaves = 16;
+// its slices with 8 waves (coalesced rows, 4 loads in flight per wave), combined in a fixed order.  Several
+// waves per output group because the conv1 / fc1 segments have few outputs and hundreds of slices; 4
+// outputs per lane and 8 (was 16) waves cut the B=100 merged reduction's wave count 8x.
+constexpr int kRedWaves = 8;
 __device__ __forceinline__ void red_store(const ReduceSeg& sg, int64_t i, float v) {
   if (sg.mode == 0) {
     sg.out[i] = v;
@@ -2103,7 +2104,7 @@ __device__ __forceinline__ void red_store(const ReduceSeg& sg, int64_t i, float 
   }
 }
 
-__global__ __launch_bounds__(1024) void slab_reduce_kernel(ReduceSegs segs) {
+__global__ __launch_bounds__(64 * kRedWaves) void slab_reduce_kernel(ReduceSegs segs) {
   __shared__ f32x4 part[kRedWaves][64];
   int blk = blockIdx.x, sidx = 0;
   while (sidx < segs.count - 1 && blk >= segs.seg[sidx].blocks) {
