@@ -1286,20 +1286,41 @@ struct C3Pre {
   }
 };
 
+// Rows 0..3 of one channel pair: d = bf16 pair (channel 2k low, 2k+1 high), t = their pool3 argmax
+// (0..3) in bits 0-1 of each halfword; row i keeps a channel iff its argmax == i.  The argmax bit planes
+// become halfword sign masks (two packed shifts each) and every row is one v_bitop3 - 9 VALU per 8
+// outputs instead of a compare + select per output.
+typedef short s16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void c3_rows(uint32_t d, uint32_t t, uint32_t& r0, uint32_t& r1, uint32_t& r2,
+                                        uint32_t& r3) {
+  const s16x2v ts = __builtin_bit_cast(s16x2v, t);
+  const uint32_t a0 = __builtin_bit_cast(uint32_t, (s16x2v)(ts << 15) >> 15);  // halfword = -(argmax bit 0)
+  const uint32_t a1 = __builtin_bit_cast(uint32_t, (s16x2v)(ts << 14) >> 15);  // halfword = -(argmax bit 1)
+  // v_bitop3 truth-table index = (S0 << 2) | (S1 << 1) | S2 with S0 = d, S1 = a0, S2 = a1
+  r0 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x10);  // d & ~a0 & ~a1
+  r1 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x40);  // d &  a0 & ~a1
+  r2 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x20);  // d & ~a0 &  a1
+  r3 = __builtin_amdgcn_bitop3_b32(d, a0, a1, 0x80);  // d &  a0 &  a1
+}
+
 // Expand compact item tid (window w = tid >> 4, channels cc..cc+7) to the 4 window-ordered rows.
 template <typename RowPtr>
 __device__ __forceinline__ void c3_expand(const C3Pre& p, int tid, RowPtr row_ptr) {
   if (tid < 256) {
     const int w = tid >> 4, cc = (tid & 15) * 8;
+    const uint4 dv = __builtin_bit_cast(uint4, p.da);
+    const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+    uint32_t r[4][4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = byte_of(p.id, j) == i ? p.da[j] : (bf16)0.f;
-      }
-      *reinterpret_cast<bf16x8*>(row_ptr(4 * w + i) + cc) = v;
+    for (int k = 0; k < 4; ++k) {
+      // argmax bytes 2k, 2k+1 -> the low bytes of the two halfwords
+      const uint32_t id4 = k < 2 ? p.id.x : p.id.y;
+      const uint32_t t = __builtin_amdgcn_perm(id4, id4, (k & 1) ? 0x0c030c02u : 0x0c010c00u);
+      c3_rows(dw[k], t, r[0][k], r[1][k], r[2][k], r[3][k]);
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      *reinterpret_cast<uint4*>(row_ptr(4 * w + i) + cc) = make_uint4(r[i][0], r[i][1], r[i][2], r[i][3]);
   }
 }
 
