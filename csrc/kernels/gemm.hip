@@ -1023,7 +1023,12 @@ static bool fp8_use_256(int M, int N, int Kbytes, int batch, int splits) {
   if (mode == 256) return true;
   const int64_t out_tiles = (int64_t)((M + 255) / 256) * ((N + 255) / 256) * batch;
   const int64_t tiles = out_tiles * std::max(1, splits);
-  if (tiles < 192 || fp8_256_fill(tiles) < 0.75) return false;
+  static const double min_fill = [] {
+    const char* v = getenv("RINGDP_FP8_256_FILL");
+    const double f = v ? atof(v) : 0.75;
+    return f > 0.0 && f <= 1.0 ? f : 0.75;
+  }();
+  if (tiles < 192 || fp8_256_fill(tiles) < min_fill) return false;
   // (single-pass GEMMs of any K: with the scalar-branch epilogue the 256 kernel wins at >= 75 % round fill,
   // e.g. 25216 x 3072 x 768 104 vs 126 us, x 2304 87 vs 98 us; profiles/r03/gemm_tiles.jsonl)
   return splits > 1 ? out_tiles >= 16 : true;
