@@ -56,3 +56,35 @@ def test_shared_weight_gradient_is_sum_of_both_uses():
             ref.w.grad = None
     finally:
         dist.destroy_process_group()
+
+
+def test_last_bucket_marks_follow_the_bucket_layout():
+    """DDP marks the parameters of the bucket it all-reduces last (`_ringdp_last_bucket`): the ConvNet ops
+    may defer those parameters' final gradient reduction into a later op of the same backward
+    (ringdp/ops/convnet.py _defer_reduce).  One bucket: every parameter; small buckets: only the last
+    bucket's, re-marked after the rebuild that follows the gradient-ready order."""
+    from ringdp.parallel import DistributedDataParallel as DDP
+
+    dist.init_process_group("fake", rank=0, world_size=2)
+    try:
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, 10))
+        ddp = DDP(m)
+        assert all(p._ringdp_last_bucket for p in m.parameters())
+        m2 = nn.Sequential(nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, 64), nn.Tanh(), nn.Linear(64, 10))
+        ddp2 = DDP(m2, bucket_cap_mb=0.01, first_bucket_mb=0.01)
+        for _ in range(3):  # the rebuild happens after the first iteration
+            ddp2(torch.randn(4, 64)).sum().backward()
+            for p in m2.parameters():
+                p.grad = None
+        buckets = [list(b) for b in ddp2.reducer.bucket_indices()]
+        assert len(buckets) > 1
+        params = list(m2.parameters())
+        last = set(buckets[-1])
+        for i, p in enumerate(params):
+            assert p._ringdp_last_bucket == (i in last), i
+        # autograd readies the output layer first: after the rebuild it sits in the first bucket
+        assert not params[-1]._ringdp_last_bucket
+        del ddp, ddp2
+    finally:
+        dist.destroy_process_group()
