@@ -211,6 +211,27 @@ __global__ __launch_bounds__(1024) void amax_roll_kernel(float* __restrict__ his
   }
 }
 
+// amax_roll_kernel for many sites: workgroup i rolls hists[i] (n = ns[i] tile maxima)
+__global__ __launch_bounds__(256) void amax_roll_many_kernel(float* const* __restrict__ hists, const int* __restrict__ ns) {
+  __shared__ float red[4];
+  float* hist = hists[blockIdx.x];
+  const int n = ns[blockIdx.x];
+  float m0 = 0.f, m1 = 0.f;
+  int i = threadIdx.x;
+  for (; i + 256 < n; i += 512) {
+    m0 = fmaxf(m0, hist[1 + i]);
+    m1 = fmaxf(m1, hist[1 + i + 256]);
+  }
+  if (i < n) m0 = fmaxf(m0, hist[1 + i]);
+  const float m = wave_max(fmaxf(m0, m1));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float a = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (a > 0.f) hist[0] = a;
+  }
+}
+
 // part[blockIdx.y][c] = sum of x[r][c] over rows [blockIdx.y * rows_per, +rows_per): 64 columns per block,
 // 32 row lanes x 8 columns per thread, a fixed-order tree at the end (deterministic).
 __global__ __launch_bounds__(256) void colsum_part_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
@@ -308,15 +329,20 @@ void fp8_quantize(const void* x, int64_t rows, int64_t cols, bool transpose, con
 }
 
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
-                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part, const void* gelu_pre) {
+                          float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part, const void* gelu_pre,
+                          bool roll) {
   dim3 grid((unsigned)((cols + kQT_C - 1) / kQT_C), (unsigned)((rows + kQT_R - 1) / kQT_R));
   if (init)
     fp8_amax(x, rows * cols, hist, s);  // first use of the site: the exact amax of this tensor
-  else
+  else if (roll)
     amax_roll_kernel<<<1, 1024, 0, s>>>(hist, (int)(grid.x * grid.y));
   quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, hist, static_cast<uint8_t*>(out_t),
                                       scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1),
                                       colsum_part, static_cast<const bf16*>(gelu_pre));
+}
+
+void fp8_roll_many(float* const* hists, const int* ns, int count, hipStream_t s) {
+  if (count > 0) amax_roll_many_kernel<<<count, 256, 0, s>>>(hists, ns);
 }
 
 }  // namespace kern

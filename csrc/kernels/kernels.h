@@ -309,7 +309,10 @@ int64_t fp8_quant_tiles(int64_t rows, int64_t cols);
 int64_t fp8_quant_row_tiles(int64_t rows);
 void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist, bool init, void* out_t,
                           float* scale, void* out_rowmajor, hipStream_t s, float* colsum_part = nullptr,
-                          const void* gelu_pre = nullptr);
+                          const void* gelu_pre = nullptr, bool roll = true);
+// the rolls of many sites in one launch (one workgroup per site): hist_i[0] <- max hist_i[1 .. 1+n_i) when
+// that is > 0.  A training step rolls every site once before its first quantisation (roll = false above)
+void fp8_roll_many(float* const* hists, const int* ns, int count, hipStream_t s);
 // column sums of a bf16 [rows][cols] matrix as colsum_parts(rows) fp32 partial rows (sum them with splitk_sum;
 // fp8_quantize_delayed's colsum_part has one partial row per 64-row tile instead)
 int colsum_parts(int64_t rows);

@@ -688,7 +688,8 @@ int64_t fp8_delayed_slots(int64_t rows, int64_t cols) { return kern::fp8_quant_t
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const at::Tensor& x, at::Tensor hist,
                                                                         bool init,
                                                                         const c10::optional<at::Tensor>& colsum,
-                                                                        const c10::optional<at::Tensor>& gelu_pre) {
+                                                                        const c10::optional<at::Tensor>& gelu_pre,
+                                                                        bool roll) {
   bf16_gpu(x, "fp8 quantize input");
   RINGDP_CHECK(x.dim() == 2 && x.size(0) % 16 == 0 && x.size(1) % 16 == 0,
                "fp8_quantize_both_delayed: expected a 2-D tensor with dims % 16 == 0");
@@ -719,10 +720,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const a
     }
   }
   kern::fp8_quantize_delayed(src.data_ptr(), R, Cc, hist.data_ptr<float>(), init, qt.data_ptr(), scale.data_ptr<float>(),
-                             q.data_ptr(), stream_of(x), part.defined() ? part.data_ptr<float>() : nullptr, pre);
+                             q.data_ptr(), stream_of(x), part.defined() ? part.data_ptr<float>() : nullptr, pre, roll);
   if (part.defined())
     kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), Cc, colsum->data_ptr<float>(), stream_of(x));
   return {q, qt, scale};
+}
+
+void fp8_roll_many(const at::Tensor& hists, const at::Tensor& ns) {
+  RINGDP_CHECK(hists.is_cuda() && ns.is_cuda() && hists.scalar_type() == at::kLong && ns.scalar_type() == at::kInt &&
+                   hists.dim() == 1 && hists.sizes() == ns.sizes() && hists.is_contiguous() && ns.is_contiguous(),
+               "fp8_roll_many: expected int64 pointer and int32 count vectors of one length on the GPU");
+  kern::fp8_roll_many(reinterpret_cast<float* const*>(hists.data_ptr<int64_t>()), ns.data_ptr<int>(),
+                      (int)hists.numel(), stream_of(hists));
 }
 
 void colsum_f32(const at::Tensor& x, at::Tensor out) {

@@ -70,7 +70,10 @@ int64_t fp8_delayed_slots(int64_t rows, int64_t cols);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const at::Tensor& x, at::Tensor hist,
                                                                         bool init,
                                                                         const c10::optional<at::Tensor>& colsum,
-                                                                        const c10::optional<at::Tensor>& gelu_pre);
+                                                                        const c10::optional<at::Tensor>& gelu_pre,
+                                                                        bool roll = true);
+// hists: int64 [count] device pointers to the sites' history tensors, ns: int32 [count] their tile counts
+void fp8_roll_many(const at::Tensor& hists, const at::Tensor& ns);
 void colsum_f32(const at::Tensor& x, at::Tensor out);
 at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
                     int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,

@@ -161,6 +161,39 @@ class LinearF(torch.autograd.Function):
 
 
 _FP8_DELAYED = os.environ.get("RINGDP_FP8_DELAYED", "1") == "1"
+_FP8_BATCH_ROLL = os.environ.get("RINGDP_FP8_BATCH_ROLL", "1") == "1"
+
+
+class _RollSet:
+    """The delayed-scaling sites of one device, rolled together: the first quantisation of a step that
+    finds its site already used since the last roll rolls EVERY site in one launch
+    (``fp8_roll_many``, one workgroup per site) instead of one ``amax_roll`` launch per quantisation
+    (ViT-B/16: 144 launches of ~5 us per step).  Each site's scale still comes from its own previous
+    call's tile maxima; a roll of a site not called since is a no-op (same maxima, same result)."""
+
+    def __init__(self):
+        self.sites = []          # (sites list on the weight, used flags on the weight, slot)
+        self.table = None        # (int64 pointers, int32 tile counts) of the current history tensors
+        self.dirty = True
+
+    def register(self, sites, used, slot):
+        if not any(s is sites and k == slot for s, _, k in self.sites):
+            self.sites.append((sites, used, slot))
+        self.dirty = True
+
+    def roll(self, device):
+        if self.dirty:
+            live = [(s[k]) for s, _, k in self.sites if s[k] is not None]
+            ptrs = torch.tensor([h.data_ptr() for h in live], dtype=torch.int64)
+            ns = torch.tensor([h.numel() - 1 for h in live], dtype=torch.int32)
+            self.table = (ptrs.to(device), ns.to(device), live)
+            self.dirty = False
+        C.fp8_roll_many(self.table[0], self.table[1])
+        for _, used, k in self.sites:
+            used[k] = False
+
+
+_ROLLS = {}
 
 
 def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[torch.Tensor] = None,
@@ -170,18 +203,31 @@ def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[tor
     the first quantisation of a site measures its exact amax; later ones scale by the amax the previous
     step measured (values clamped to the e4m3 range) and record the current one inside the same pass,
     which removes the separate amax pass over the tensor.  ``gelu_pre``: quantise ``t * GELU'(gelu_pre)``
-    instead (the GELU backward done inside the quantisation pass)."""
+    instead (the GELU backward done inside the quantisation pass).  The rolls of all sites run as one
+    launch per step (``_RollSet``)."""
     if not _FP8_DELAYED:
         return C.fp8_quantize_both(t if gelu_pre is None else C.gelu_bwd(t, gelu_pre))
     sites = getattr(w, "_ringdp_fp8", None)
     if sites is None:
         sites = w._ringdp_fp8 = [None, None, None]
+        w._ringdp_fp8_used = [False, False, False]
+    used = w._ringdp_fp8_used
     n = 1 + C.fp8_delayed_slots(t.shape[0], t.shape[1])
     hist = sites[slot]
     init = hist is None or hist.numel() != n
     if init:
         hist = sites[slot] = torch.zeros(n, device=t.device, dtype=torch.float32)
-    return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre)
+    if not _FP8_BATCH_ROLL:
+        return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre)
+    rs = _ROLLS.setdefault(t.device, _RollSet())
+    if init:
+        rs.register(sites, used, slot)
+    elif used[slot]:
+        if rs.dirty and torch.cuda.is_current_stream_capturing():  # no table upload inside a capture
+            return C.fp8_quantize_both_delayed(t, hist, False, colsum, gelu_pre)
+        rs.roll(t.device)
+    used[slot] = True
+    return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre, roll=False)
 
 
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):

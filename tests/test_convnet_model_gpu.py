@@ -344,3 +344,33 @@ def test_head_ce_fusion_and_deferred_reduce(world1, B, bucket_mb):
                 assert n1 == 0, (cfg, n1)
     finally:
         cn._HEAD_CE, cn._DEFER = True, True
+
+
+@pytest.mark.parametrize("kw", [{"reduction": "sum"}, {"reduction": "none"}, {"label_smoothing": 0.1},
+                                {"ignore_index": 3}])
+def test_head_ce_variants_match_separate_criterion(kw):
+    """The cross entropy fused into the fc1 backward honours reduction / label smoothing / ignore_index
+    exactly like the separate ce kernels (bit-identical loss and gradients)."""
+    import ringdp.ops.convnet as cn
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+
+    crit = CrossEntropyLoss(**kw)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    x = torch.randint(0, 256, (64, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g)
+    y = torch.randint(0, 10, (64,), device="cuda", generator=g)
+    res = []
+    try:
+        for fused in (False, True):
+            cn._HEAD_CE = fused
+            torch.manual_seed(0)
+            m = ConvNet().cuda()
+            loss = crit(m(x), y)
+            (loss.sum() if loss.dim() else loss).backward()
+            res.append((loss.detach(), [p.grad.clone() for p in m.parameters()]))
+    finally:
+        cn._HEAD_CE = True
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)

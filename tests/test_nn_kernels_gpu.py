@@ -647,3 +647,41 @@ def test_vit_fp8_training_trajectory_tracks_bf16():
     # chaotic enough that any perturbation moves individual windows, so the gate is absolute
     gap = float((w8 - w16).abs().max())
     assert gap < 0.15 * float(w16[0]), gap
+
+
+def test_fp8_batched_roll_matches_per_site_roll():
+    """Rolling every delayed-scaling site in one launch per step (``_RollSet``) gives bit-identical
+    training to one ``amax_roll`` per quantisation: the roll is a max over the same tile maxima."""
+    import copy
+
+    import ringdp.ops.transformer as tr
+    from ringdp.models import vit_tiny
+    from ringdp.optim import SGD
+
+    torch.manual_seed(0)
+    m = vit_tiny(num_classes=10).cuda()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    xs = [torch.randn(16, 3, 32, 32, device="cuda", generator=g) for _ in range(4)]
+    ys = [torch.randint(0, 10, (16,), device="cuda", generator=g) for _ in range(4)]
+    res = []
+    try:
+        tr.set_fp8(True)
+        for batched in (False, True):
+            tr._FP8_BATCH_ROLL = batched
+            tr._ROLLS.clear()
+            mm = copy.deepcopy(m)
+            opt = SGD(mm.parameters(), lr=0.05, momentum=0.9)
+            losses = []
+            for x, y in zip(xs, ys):
+                loss = F.cross_entropy(mm(x), y)
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                opt.step()
+                losses.append(loss.detach())
+            res.append((torch.stack(losses), [p.detach().clone() for p in mm.parameters()]))
+    finally:
+        tr.set_fp8(False)
+        tr._FP8_BATCH_ROLL = True
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
