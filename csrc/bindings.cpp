@@ -542,6 +542,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_quantize_both_delayed", &ops::fp8_quantize_both_delayed, py::arg("x"), py::arg("hist"), py::arg("init"),
         py::arg("colsum") = py::none(), py::arg("gelu_pre") = py::none(), py::arg("roll") = true);
   m.def("fp8_roll_many", &ops::fp8_roll_many, "delayed-scaling roll of many fp8 sites in one launch");
+  m.def("gemm_fp8_q8_slots", &ops::gemm_fp8_q8_slots);
+  m.def("fp8_roll", &ops::fp8_roll, "delayed-scaling roll of one fp8 site");
+  m.def("gemm_fp8_quant_out", &ops::gemm_fp8_quant_out, py::arg("a"), py::arg("b"), py::arg("scale_a"),
+        py::arg("scale_b"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bias") = py::none(), py::arg("act") = 0,
+        py::arg("preact") = py::none(), py::arg("hist"), py::arg("colsum") = py::none());
   m.def("colsum_f32", &ops::colsum_f32, "out[c] = sum_r x[r][c] (bf16 in, fp32 out, deterministic)");
   m.def("fp8_delayed_slots", &ops::fp8_delayed_slots);
   m.def("gemm_fp8", &ops::gemm_fp8, py::arg("a"), py::arg("b"), py::arg("scale_a"), py::arg("scale_b"), py::arg("M"),

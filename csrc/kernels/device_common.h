@@ -56,5 +56,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// tile id -> (tm, tn) of a tiles_m x tiles_n grid, group_m tile rows at a time (bijective): the tiles one
+// XCD runs at once (consecutive ids after xcd_remap) then share group_m A panels and a few B panels in
+// its L2 instead of 1 A panel and up to 32 B panels (row-major order)
+__device__ __forceinline__ void grouped_tile(int t, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+  if (group_m <= 1) {
+    tm = t / tiles_n;
+    tn = t - tm * tiles_n;
+    return;
+  }
+  const int gsz = group_m * tiles_n, g = t / gsz, first = g * group_m;
+  const int gm = min(tiles_m - first, group_m), w = t - g * gsz;
+  tm = first + w % gm;
+  tn = w / gm;
+}
+
 }  // namespace dev
 }  // namespace ringdp

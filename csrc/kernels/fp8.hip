@@ -341,6 +341,8 @@ void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist
                                       colsum_part, static_cast<const bf16*>(gelu_pre));
 }
 
+void fp8_roll(float* hist, int n, hipStream_t s) { amax_roll_kernel<<<1, 1024, 0, s>>>(hist, n); }
+
 void fp8_roll_many(float* const* hists, const int* ns, int count, hipStream_t s) {
   if (count > 0) amax_roll_many_kernel<<<count, 256, 0, s>>>(hists, ns);
 }

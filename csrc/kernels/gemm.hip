@@ -19,6 +19,7 @@
 //   optionally keeps the pre-activation, and emits deterministic per-channel sum / sum-of-squares
 //   partials (batch-norm statistics) or split-K fp32 partials.
 #include <algorithm>
+#include <cstdio>
 #include <type_traits>
 
 #include "device_common.h"
@@ -1056,6 +1057,13 @@ int gemm_fp8_pick_splits(int M, int N, int Kbytes, int requested) {
 
 void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int Kbytes, const GemmEpilogue& ep,
               int splits, hipStream_t s) {
+  if (ep.q8) {  // e4m3 outputs exist only in the 256x256 kernel's epilogue (the op layer checked the shape)
+    if (!gemm_fp8_256(A, B, batch, M, N, Kbytes, ep, splits, s)) {
+      fprintf(stderr, "gemm_fp8: e4m3-output GEMM %d x %d x %d not supported by the 256x256 kernel\n", M, N, Kbytes);
+      abort();
+    }
+    return;
+  }
   if (fp8_use_256(M, N, Kbytes, batch, splits) && gemm_fp8_256(A, B, batch, M, N, Kbytes, ep, splits, s)) return;
   // K-contiguous e4m3 operands viewed as bf16 "slots" of 2 bytes for the 16-B stagers
   const DenseLoader da{static_cast<const bf16*>(A.p), A.ld / 2, A.bstride / 2, M, Kbytes / 2};

@@ -55,7 +55,7 @@ __device__ __forceinline__ float gemm_gelu_grad(float x) {
 // every wave then runs every path of every element, the GELU's erf included).
 struct EpiFlags {
   int act, mode;
-  bool bias, res, pre, st_pre;
+  bool bias, res, pre, st_pre, q8;
 };
 __device__ __forceinline__ EpiFlags epi_flags(const GemmEpilogue& ep) {
   EpiFlags f;
@@ -65,6 +65,7 @@ __device__ __forceinline__ EpiFlags epi_flags(const GemmEpilogue& ep) {
   f.res = __builtin_amdgcn_readfirstlane(ep.residual != nullptr ? 1 : 0) != 0;
   f.pre = __builtin_amdgcn_readfirstlane(ep.preact != nullptr ? 1 : 0) != 0;
   f.st_pre = f.pre && f.act != 3;
+  f.q8 = __builtin_amdgcn_readfirstlane(ep.q8 != nullptr ? 1 : 0) != 0;
   return f;
 }
 
@@ -88,11 +89,160 @@ __device__ __forceinline__ void epi_finish(float (&v)[4], const dev::bf16x4& sid
   }
 }
 
+__device__ __forceinline__ uint32_t gemm_pack_e4m3(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+// e4m3 outputs (GemmEpilogue::q8).  The wave's 128 x 64 e4m3 tile goes to LDS as [128 rows][64 B] (16-B chunk
+// c of row r at c ^ ((r >> 3) & 3)), from which it is stored row-major as 16-B row pieces and transposed as in
+// quant_t_kernel (fp8.hip): a lane gathers 8 rows x 4 columns (b32 reads), 16 v_perm_b32 make 4 columns x 8
+// rows, and the 16 lanes of one column group write 128 contiguous bytes of an output row.  M % 16 == 0 and
+// N % 16 == 0 (checked by the launcher), so 16-B pieces and 8-row groups are wholly inside or outside.
+template <bool QUAD, int ACT>
+__device__ __forceinline__ void gemm256_store_q8(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep,
+                                                 const EpiFlags& fl, int M, int N, int mrow, int ncol, float sa,
+                                                 char* lds_wave) {
+  using namespace ringdp::dev;
+  auto mof = [&](int i) { return QUAD ? mrow + (i >> 2) * 64 + 16 * (i & 3) : mrow + 16 * i; };
+  auto nof = [&](int j) { return QUAD ? ncol + (j >> 1) * 32 + 16 * (j & 1) : ncol + 16 * j; };
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+  const float qs = fmaxf(ep.q8_amax[0], 1e-12f) / 448.f;  // the scale quant_t_kernel would use
+  const float inv = 1.f / qs;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) ep.q8_scale[0] = qs;
+  const bool want_cs = __builtin_amdgcn_readfirstlane(ep.q8_colsum != nullptr ? 1 : 0) != 0;
+  f32x4 bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = nof(j);
+    bias[j] = (fl.bias && n < N) ? *reinterpret_cast<const f32x4*>(ep.bias + n) : zero_f32x4();
+  }
+  const bool has_side = fl.res || ACT == 3;
+  const bf16* side = static_cast<const bf16*>(fl.res ? ep.residual : ep.preact);
+  float vmax = 0.f;
+  float cs[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[j][e] = 0.f;
+  // side inputs (residual / GELU pre-activation) preloaded half a wave tile at a time: all 32 quads at once
+  // next to the 128 accumulator registers spills
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    bf16x4 sv[4][4];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sv[ii][j] = bf16x4{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+        if (has_side) {
+          const int m = min(mof(4 * half + ii), M - 1), n = min(nof(j), N - 4);
+          sv[ii][j] = *reinterpret_cast<const bf16x4*>(side + (int64_t)m * ep.ldc + n);
+        }
+      }
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii) {
+    const int i = 4 * half + ii;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = mof(i), n = nof(j);
+      const bool ok = m < M && n < N;
+      float v[4];
+      epi_values<ACT>(acc[i][j], sa, bias[j], sv[ii][j], fl.res, v);
+      if (fl.st_pre && ok)
+        *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + (int64_t)m * ep.ldc + n) =
+            bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      epi_finish<ACT>(v, sv[ii][j], fl.res);
+      float q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float vb = ok ? (float)(bf16)v[e] : 0.f;  // rows past M hold clamped-row garbage
+        vmax = fmaxf(vmax, fabsf(vb));
+        cs[j][e] += vb;
+        q[e] = fminf(fmaxf(vb * inv, -448.f), 448.f);
+      }
+      // opaque running reductions: without these the unrolled max / sum chains are re-associated into trees
+      // over all 128 values, which keeps every value (and its accumulator) live at once and spills
+      asm volatile("" : "+v"(vmax), "+v"(cs[j][0]), "+v"(cs[j][1]), "+v"(cs[j][2]), "+v"(cs[j][3]));
+      const int r = (QUAD ? (i >> 2) * 64 + 16 * (i & 3) : 16 * i) + fr;
+      const int c = QUAD ? (j >> 1) * 32 + 16 * (j & 1) + 4 * fq : 16 * j + 4 * fq;  // byte column
+      *reinterpret_cast<uint32_t*>(lds_wave + r * 64 + (((c >> 4) ^ ((r >> 3) & 3)) << 4) + (c & 15)) =
+          gemm_pack_e4m3(q[0], q[1], q[2], q[3]);
+    }
+  }
+  }
+  const int m_base = mrow - fr, n_base = ncol - 4 * fq;  // the wave tile's first row / column
+  // (each wave reads back only what it wrote: LDS executes one wave's operations in order)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // row-major: lane -> row 16k + lane / 4, 16-B piece lane & 3
+    const int r = 16 * k + (lane >> 2), ch = lane & 3;
+    const uint4 w = *reinterpret_cast<const uint4*>(lds_wave + r * 64 + ((ch ^ ((r >> 3) & 3)) << 4));
+    const int m = m_base + r, n = n_base + 16 * ch;
+    if (m < M && n < N) *reinterpret_cast<uint4*>(ep.q8 + (int64_t)m * N + n) = w;
+  }
+  {  // transposed: lane -> rows 8 rg .. 8 rg + 7, columns 16 p + 4 (lane >> 4) + 0..3
+    const int rg = lane & 15;
+    const int m = m_base + 8 * rg;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int oc = 16 * p + 4 * fq;
+      uint32_t d[8];
+#pragma unroll
+      for (int ii = 0; ii < 8; ++ii) {
+        const int r = 8 * rg + ii;
+        d[ii] = *reinterpret_cast<const uint32_t*>(lds_wave + r * 64 + (((oc >> 4) ^ (rg & 3)) << 4) + (oc & 15));
+      }
+      uint32_t col[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t a = d[4 * h], b = d[4 * h + 1], c = d[4 * h + 2], e = d[4 * h + 3];
+        const uint32_t ab_lo = __builtin_amdgcn_perm(b, a, 0x05010400u), ab_hi = __builtin_amdgcn_perm(b, a, 0x07030602u);
+        const uint32_t ce_lo = __builtin_amdgcn_perm(e, c, 0x05010400u), ce_hi = __builtin_amdgcn_perm(e, c, 0x07030602u);
+        col[h][0] = __builtin_amdgcn_perm(ce_lo, ab_lo, 0x05040100u);
+        col[h][1] = __builtin_amdgcn_perm(ce_lo, ab_lo, 0x07060302u);
+        col[h][2] = __builtin_amdgcn_perm(ce_hi, ab_hi, 0x05040100u);
+        col[h][3] = __builtin_amdgcn_perm(ce_hi, ab_hi, 0x07060302u);
+      }
+      if (m < M) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int n = n_base + oc + jj;
+          if (n < N) *reinterpret_cast<uint2*>(ep.q8t + (int64_t)n * M + m) = make_uint2(col[0][jj], col[1][jj]);
+        }
+      }
+    }
+  }
+  vmax = wave_max(vmax);
+  if (lane == 0) ep.q8_tmax[(int64_t)blockIdx.x * 8 + (threadIdx.x >> 6)] = vmax;
+  if (want_cs) {  // the 16 lanes of one fq hold the same columns: xor 1 / 2 / 4 / 8 sums their rows
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t = cs[j][e];
+        t += __shfl_xor(t, 1, 64);
+        t += __shfl_xor(t, 2, 64);
+        t += __shfl_xor(t, 4, 64);
+        t += __shfl_xor(t, 8, 64);
+        cs[j][e] = t;
+      }
+    if (fr == 0) {
+      float* row = ep.q8_colsum + (int64_t)(m_base >> 7) * N;  // one partial row per 128-row wave tile
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nof(j);
+        if (n < N) *reinterpret_cast<f32x4*>(row + n) = f32x4{cs[j][0], cs[j][1], cs[j][2], cs[j][3]};
+      }
+    }
+  }
+}
+
 // QUAD: the phased kernel's tile order (acc[qm*4 + mt][qn*2 + nt], quadrants of 64 rows x 32 cols);
 // otherwise acc[i][j] covers rows mrow + 16 i, columns ncol + 16 j.
 // lds_wave: this wave's 16 KiB of the kernel's LDS (free once the main loop's last barrier has passed):
 // store mode 2 writes the wave's 128 x 64 bf16 tile there and stores it back as whole 128-B rows.
-template <bool QUAD, int ACT>
+template <bool QUAD, int ACT, bool Q8>
 __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep,
                                                    const EpiFlags& fl, int M, int N, int bidx, int mrow, int ncol,
                                                    float scale, char* lds_wave) {
@@ -101,6 +251,12 @@ __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4]
   auto nof = [&](int j) { return QUAD ? ncol + (j >> 1) * 32 + 16 * (j & 1) : ncol + 16 * j; };
   const int64_t cb = (int64_t)bidx * ep.c_bstride;
   const float sa = scale * ep.alpha;
+  if constexpr (Q8) {  // (the bf16 kernels compile without this path: it costs them registers)
+    if (fl.q8) {  // before the full-tile preloads below: its own loads are staged by halves
+      gemm256_store_q8<QUAD, ACT>(acc, ep, fl, M, N, mrow, ncol, sa, lds_wave);
+      return;
+    }
+  }
   // ---- all loads first
   f32x4 bias[4];
 #pragma unroll
@@ -236,7 +392,8 @@ __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4]
   }
 }
 
-template <bool QUAD>
+// Q8: the e4m3-output path (GemmEpilogue::q8) is compiled in (the fp8 kernel)
+template <bool QUAD, bool Q8 = false>
 __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep, int M, int N,
                                               int zid, int bidx, int mrow, int ncol, float scale, char* lds_wave) {
   using namespace ringdp::dev;
@@ -259,10 +416,10 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
   const EpiFlags fl = epi_flags(ep);
   // one specialised body per activation: the per-element code holds no branch on the epilogue kind
   switch (fl.act) {
-    case 1: gemm256_store_impl<QUAD, 1>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
-    case 2: gemm256_store_impl<QUAD, 2>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
-    case 3: gemm256_store_impl<QUAD, 3>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
-    default: gemm256_store_impl<QUAD, 0>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 1: gemm256_store_impl<QUAD, 1, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 2: gemm256_store_impl<QUAD, 2, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 3: gemm256_store_impl<QUAD, 3, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    default: gemm256_store_impl<QUAD, 0, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
   }
 }
 

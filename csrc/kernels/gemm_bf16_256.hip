@@ -82,14 +82,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256_kernel(const uint8_t* __
                                                               int64_t a_bs, const uint8_t* __restrict__ B,
                                                               int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
                                                               int N, int K, int tiles_m, int tiles_n, int splits,
-                                                              int k_per_split) {
+                                                              int k_per_split, int group_m) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int per_z = tiles_m * tiles_n;
   const int zid = blockIdx.y;
   const int t = xcd_remap(blockIdx.x, per_z);
-  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  int tm, tn;
+  grouped_tile(t, tiles_m, tiles_n, group_m, tm, tn);
   const int b = zid / splits, split = zid - b * splits;
   const int m0 = tm * TM, n0 = tn * TN;
   const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
@@ -220,14 +221,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* _
                                                                int64_t a_bs, const uint8_t* __restrict__ B,
                                                                int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
                                                                int N, int K, int tiles_m, int tiles_n, int splits,
-                                                               int k_per_split) {
+                                                               int k_per_split, int group_m) {
   __shared__ __attribute__((aligned(16))) char smem[2 * PBUF];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
   const int per_z = tiles_m * tiles_n;
   const int zid = blockIdx.y;
   const int t = xcd_remap(blockIdx.x, per_z);
-  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  int tm, tn;
+  grouped_tile(t, tiles_m, tiles_n, group_m, tm, tn);
   const int b = zid / splits, split = zid - b * splits;
   const int m0 = tm * TM, n0 = tn * TN;
   const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
@@ -355,7 +357,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256q_kernel(const uint8_t* _
                                                                int64_t a_bs, const uint8_t* __restrict__ B,
                                                                int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
                                                                int N, int K, int tiles_m, int tiles_n, int splits,
-                                                               int k_per_split, int total) {
+                                                               int k_per_split, int total, int group_m) {
   __shared__ __attribute__((aligned(16))) char smem[2 * PBUF];
   // wave index in an SGPR (readfirstlane): the per-wave terms of the DMA offsets and LDS addresses then cost
   // no VGPRs
@@ -375,7 +377,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256q_kernel(const uint8_t* _
     const int t = xcd_remap(w, total);
     z = t / per_z;
     const int tt = t - z * per_z;
-    const int tm = tt / tiles_n, tn = tt - tm * tiles_n;
+    int tm, tn;
+    grouped_tile(tt, tiles_m, tiles_n, group_m, tm, tn);
     b = z / splits;
     const int split = z - b * splits;
     tm0 = tm * TM;
@@ -655,10 +658,14 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   e2.store_rot = gemm_wide_store_mode() < 10;
   e2.store_cache = gemm_store_cache();
   e2.sink = store_sink();
+  static const int group_m = [] {  // tile rows per group of the tile order (1 = row-major, rounds 1-3)
+    const char* v = getenv("RINGDP_BF16_GROUP_M");
+    return v && *v ? atoi(v) : 4;
+  }();
   auto go = [&](auto kern) {
     kern<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
                               static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M, N, K * 2,
-                              tiles_m, tiles_n, splits, kps * 2);
+                              tiles_m, tiles_n, splits, kps * 2, group_m);
   };
   const bool wide_bf16 = N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 &&
                          ep.c_bstride % 8 == 0;
@@ -672,7 +679,7 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
       const int g = std::min(total, cu_count());
       gemm_bf16_256q_kernel<<<g, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
                                              static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M,
-                                             N, K * 2, tiles_m, tiles_n, splits, kps * 2, total);
+                                             N, K * 2, tiles_m, tiles_n, splits, kps * 2, total, group_m);
       return true;
     }
   }

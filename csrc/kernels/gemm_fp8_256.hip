@@ -50,20 +50,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_wave_ba
 // chunk swizzle of stage row r (see the header); swz = 0: the round-3 r & 7 (A/B knob RINGDP_FP8_SWZ)
 __device__ __forceinline__ int chunk_swz(int r, int swz) { return swz ? ((r & 6) | ((r >> 3) & 1)) : (r & 7); }
 
-// tile id -> (tm, tn), group_m tile rows at a time: the 32 tiles an XCD runs at once (consecutive ids after
-// xcd_remap) then share group_m A panels and 32 / group_m B panels instead of 1 and 32 (L2 hit rate)
-__device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
-  if (group_m <= 1) {
-    tm = t / tiles_n;
-    tn = t - tm * tiles_n;
-    return;
-  }
-  const int gsz = group_m * tiles_n, g = t / gsz, first = g * group_m;
-  const int gm = min(tiles_m - first, group_m), w = t - g * gsz;
-  tm = first + w % gm;
-  tn = w / gm;
-}
-
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -82,7 +68,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(const uint8_t* __r
   const int zid = blockIdx.y;
   const int t = xcd_remap(blockIdx.x, per_z);
   int tm, tn;
-  tile_of(t, tiles_m, tiles_n, group_m, tm, tn);
+  grouped_tile(t, tiles_m, tiles_n, group_m, tm, tn);  // L2 reuse across the XCD's concurrent tiles
   const int b = zid / splits, split = zid - b * splits;
   const int m0 = tm * TM, n0 = tn * TN;
   const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
@@ -171,10 +157,13 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(const uint8_t* __r
   const int mrow = m0 + wm * 128 + (lane & 15);
   const int ncol = n0 + wn * 64 + 4 * (lane >> 4);
   const float dscale = (ep.scale_a ? ep.scale_a[0] : 1.f) * (ep.scale_b ? ep.scale_b[0] : 1.f);
-  gemm256_store<false>(acc, ep, M, N, zid, b, mrow, ncol, dscale, smem + wave * 16384);
+  gemm256_store<false, true>(acc, ep, M, N, zid, b, mrow, ncol, dscale, smem + wave * 16384);
 }
 
 }  // namespace
+
+int64_t gemm_fp8_q8_slots(int M, int N) { return (int64_t)((M + TM - 1) / TM) * ((N + TN - 1) / TN) * 8; }
+int64_t gemm_fp8_q8_colsum_rows(int M) { return (int64_t)((M + TM - 1) / TM) * 2; }
 
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
@@ -185,6 +174,8 @@ bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M
                   const GemmEpilogue& ep, int splits, hipStream_t s) {
   // K-contiguous operands with 16-B aligned rows, whole 128-byte k-steps, whole 4-column runs, no
   // statistics epilogue (BN layers never run in fp8)
+  if (ep.q8 && (M % 16 != 0 || N % 16 != 0 || batch != 1 || splits > 1 || ep.mode != GemmEpilogue::kStore))
+    return false;
   if (A.row_contig || Bop.row_contig || Kbytes % TK != 0 || N % 4 != 0 || M <= 0 || N <= 0 || ep.stats ||
       A.ld % 16 != 0 || Bop.ld % 16 != 0 || (ep.mode != GemmEpilogue::kSplitK && ep.ldc % 4 != 0) ||
       reinterpret_cast<uintptr_t>(ep.bias) % 16 != 0)

@@ -266,6 +266,17 @@ struct GemmEpilogue {
   int store_cache;    // 256x256 kernels' 16-B output stores: 0 plain, 1 nontemporal, 2 write-through sc1
   void* sink;         // persistent 256x256 kernels: >= 16 B target of the stores past the M / N edge (set by
                       // the launcher)
+  // e4m3 outputs instead of C (256x256 fp8 kernel only): the final value v (after bias / GELU / GELU backward,
+  // rounded to bf16 as a stored C would be) is quantised with the delayed scale q8_amax[0] / 448 (clamped to
+  // +-448) into q8 [M][N] and its transpose q8t [N][M]; q8_scale[0] <- that scale; q8_tmax[tile * 8 + wave]
+  // <- |v|max of each wave's 128 x 64 outputs (the next roll); q8_colsum (nullable) [tiles_m * 2][N] <- the
+  // column sums of v over each wave's 128 rows (a bias gradient)
+  uint8_t* q8;
+  uint8_t* q8t;
+  const float* q8_amax;
+  float* q8_scale;
+  float* q8_tmax;
+  float* q8_colsum;
 };
 struct ConvGeom {
   int N, H, W, C;   // input NHWC (C padded to a multiple of 8)
@@ -281,6 +292,9 @@ void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int 
               int splits, hipStream_t s);
 // the 256x256 e4m3 kernel behind gemm_fp8 (false = shape not supported, nothing launched)
 void set_bf16_tile_mode(int mode);  // 0 auto, 128 / 256 forced (A/B measurements)
+// tile-maximum slots and colsum partial rows of a gemm_fp8 launch with e4m3 outputs (ep.q8)
+int64_t gemm_fp8_q8_slots(int M, int N);
+int64_t gemm_fp8_q8_colsum_rows(int M);
 // 256x256 bf16 kernel for K-contiguous A and B (gemm_bf16_256.hip); false when the shape/layout is not
 // supported (the caller falls back to the 128x128 core).  K in elements.
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K,
@@ -313,6 +327,7 @@ void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist
 // the rolls of many sites in one launch (one workgroup per site): hist_i[0] <- max hist_i[1 .. 1+n_i) when
 // that is > 0.  A training step rolls every site once before its first quantisation (roll = false above)
 void fp8_roll_many(float* const* hists, const int* ns, int count, hipStream_t s);
+void fp8_roll(float* hist, int n, hipStream_t s);  // one site: hist[0] <- max hist[1 .. 1+n) when > 0
 // column sums of a bf16 [rows][cols] matrix as colsum_parts(rows) fp32 partial rows (sum them with splitk_sum;
 // fp8_quantize_delayed's colsum_part has one partial row per 64-row tile instead)
 int colsum_parts(int64_t rows);

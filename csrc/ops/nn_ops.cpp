@@ -779,6 +779,66 @@ at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& 
   return c;
 }
 
+void fp8_roll(at::Tensor hist) {
+  f32_gpu(hist, "fp8 amax history");
+  RINGDP_CHECK(hist.is_contiguous() && hist.numel() >= 1, "fp8_roll: expected a contiguous history");
+  kern::fp8_roll(hist.data_ptr<float>(), (int)(hist.numel() - 1), stream_of(hist));
+}
+
+int64_t gemm_fp8_q8_slots(int64_t M, int64_t N) { return kern::gemm_fp8_q8_slots((int)M, (int)N); }
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_fp8_quant_out(
+    const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b, int64_t M,
+    int64_t N, int64_t K, const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& preact,
+    at::Tensor hist, const c10::optional<at::Tensor>& colsum) {
+  gpu(a, "fp8 A");
+  gpu(b, "fp8 B");
+  dtype(a, at::kByte, "fp8 A");
+  dtype(b, at::kByte, "fp8 B");
+  f32_gpu(scale_a, "fp8 scale A");
+  f32_gpu(scale_b, "fp8 scale B");
+  f32_gpu(hist, "fp8 amax history");
+  RINGDP_CHECK(M % 16 == 0 && N % 16 == 0 && K % 128 == 0, "gemm_fp8_quant_out: M, N % 16 and K % 128 must be 0");
+  RINGDP_CHECK(a.numel() >= M * K && b.numel() >= N * K, "gemm_fp8_quant_out: operand smaller than described");
+  RINGDP_CHECK(act == 0 || act == 2 || act == 3, "gemm_fp8_quant_out: act must be 0, 2 (GELU) or 3 (GELU backward)");
+  RINGDP_CHECK(hist.is_contiguous() && hist.numel() == 1 + kern::gemm_fp8_q8_slots((int)M, (int)N),
+               "gemm_fp8_quant_out: history must hold 1 + gemm_fp8_q8_slots(M, N) floats");
+  auto e = make_epi(nullptr, N, 0, true);
+  e.act = static_cast<int>(act);
+  e.scale_a = scale_a.data_ptr<float>();
+  e.scale_b = scale_b.data_ptr<float>();
+  if (bias.has_value() && bias->defined()) {
+    f32_gpu(*bias, "gemm bias");
+    RINGDP_CHECK(bias->numel() == N && reinterpret_cast<uintptr_t>(bias->data_ptr()) % 16 == 0, "gemm bias: [N], 16-B aligned");
+    e.bias = bias->data_ptr<float>();
+  }
+  if (act == 2 || act == 3) {
+    RINGDP_CHECK(preact.has_value() && preact->defined(), "gemm_fp8_quant_out: act 2 / 3 need the pre-activation");
+    bf16_gpu(*preact, "gemm preact");
+    RINGDP_CHECK(preact->numel() == M * N && preact->is_contiguous(), "gemm preact: [M][N] contiguous");
+    e.preact = preact->data_ptr();
+  }
+  at::Tensor q = at::empty({M, N}, a.options()), qt = at::empty({N, M}, a.options());
+  at::Tensor scale = at::empty({1}, a.options().dtype(at::kFloat));
+  at::Tensor part;
+  if (colsum.has_value() && colsum->defined()) {
+    f32_gpu(*colsum, "gemm colsum");
+    RINGDP_CHECK(colsum->numel() == N && colsum->is_contiguous(), "gemm colsum: [N] floats");
+    part = at::empty({kern::gemm_fp8_q8_colsum_rows((int)M), N}, a.options().dtype(at::kFloat));
+    e.q8_colsum = part.data_ptr<float>();
+  }
+  e.q8 = static_cast<uint8_t*>(q.data_ptr());
+  e.q8t = static_cast<uint8_t*>(qt.data_ptr());
+  e.q8_amax = hist.data_ptr<float>();
+  e.q8_scale = scale.data_ptr<float>();
+  e.q8_tmax = hist.data_ptr<float>() + 1;
+  kern::GemmOperand A{a.data_ptr(), K, 0, false}, B{b.data_ptr(), K, 0, false};
+  kern::gemm_fp8(A, B, 1, (int)M, (int)N, (int)K, e, 1, stream_of(a));
+  if (part.defined())
+    kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), N, colsum->data_ptr<float>(), stream_of(a));
+  return {q, qt, scale};
+}
+
 void set_fp8_tile_mode(int64_t mode) { kern::set_fp8_tile_mode((int)mode); }
 void set_bf16_tile_mode(int64_t mode) { kern::set_bf16_tile_mode((int)mode); }
 

@@ -74,6 +74,15 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> fp8_quantize_both_delayed(const a
                                                                         bool roll = true);
 // hists: int64 [count] device pointers to the sites' history tensors, ns: int32 [count] their tile counts
 void fp8_roll_many(const at::Tensor& hists, const at::Tensor& ns);
+// fp8 GEMM whose epilogue writes e4m3 (row-major and transposed) with delayed scaling instead of bf16 C:
+// hist = {amax to scale by, the launch's per-(tile, wave) maxima}; act 2 stores the pre-activation into
+// preact, act 3 reads it (GELU backward); colsum (nullable) <- column sums of the quantised-from values
+int64_t gemm_fp8_q8_slots(int64_t M, int64_t N);
+void fp8_roll(at::Tensor hist);
+std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_fp8_quant_out(
+    const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b, int64_t M,
+    int64_t N, int64_t K, const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& preact,
+    at::Tensor hist, const c10::optional<at::Tensor>& colsum);
 void colsum_f32(const at::Tensor& x, at::Tensor out);
 at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
                     int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,

@@ -18,8 +18,8 @@ from collections import OrderedDict
 import torch
 import torch.nn as nn
 
-from ..ops.transformer import (AttentionF, ClassRowsF, LayerNormF, LayerNormFork, MLPF, PatchTokensF, cast_weights,
-                                clear_weights, fp8_enabled, linear)
+from ..ops.transformer import (AttentionF, ClassRowsF, LayerNormF, LayerNormFork, MLPF, MLPF8, PatchTokensF,
+                                cast_weights, clear_weights, fp8_enabled, fp8_mlp_fusable, linear)
 
 
 class MLPBlock(nn.Sequential):
@@ -56,8 +56,11 @@ class EncoderBlock(nn.Module):
             o = AttentionF.apply(qkv, B, T, self.num_heads)
             x = linear(o, att.out_proj, residual=x)
             h, x = LayerNormFork.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
-            h = linear(h, self.mlp[0], act=2)
-            return linear(h, self.mlp[3], residual=x)
+            fc1, fc2 = self.mlp[0], self.mlp[3]
+            if fp8_mlp_fusable(h.shape[0], h.shape[1], fc1.weight.shape[0]):  # e4m3 from the GEMM epilogues
+                return MLPF8.apply(h, fc1.weight, fc1.bias, fc2.weight, fc2.bias, x)
+            h = linear(h, fc1, act=2)
+            return linear(h, fc2, residual=x)
         # bf16: the residual streams' gradients join in the LayerNorm backward kernels (LayerNormFork)
         # and the GELU backward runs in fc2's data-gradient epilogue (MLPF)
         h, x = LayerNormFork.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)

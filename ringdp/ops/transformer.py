@@ -196,6 +196,35 @@ class _RollSet:
 _ROLLS = {}
 
 
+def _site(w: torch.Tensor, slot: int, n: int, device) -> Tuple[torch.Tensor, bool, bool]:
+    """The delayed-scaling history of site ``slot`` on weight ``w`` ([amax to scale by, n - 1 tile maxima of
+    the last call]): returns (hist, init, roll_here).  Slots: 0 the linear's input, 1 its output gradient,
+    2 its weight, 3 (on fc2) the input fc1's epilogue quantises, 4 (on fc1) the output gradient fc2's
+    data-gradient epilogue quantises.  ``init``: first use (or a new shape) - the caller measures an exact
+    amax.  ``roll_here``: the caller rolls this site itself (per-site mode, or a capture that cannot
+    upload the batched roll's table); otherwise the batched roll already ran when needed."""
+    sites = getattr(w, "_ringdp_fp8", None)
+    if sites is None:
+        sites = w._ringdp_fp8 = [None] * 5
+        w._ringdp_fp8_used = [False] * 5
+    used = w._ringdp_fp8_used
+    hist = sites[slot]
+    init = hist is None or hist.numel() != n
+    if init:
+        hist = sites[slot] = torch.zeros(n, device=device, dtype=torch.float32)
+    if not _FP8_BATCH_ROLL:
+        return hist, init, not init
+    rs = _ROLLS.setdefault(device, _RollSet())
+    if init:
+        rs.register(sites, used, slot)
+    elif used[slot]:
+        if rs.dirty and torch.cuda.is_current_stream_capturing():  # no table upload inside a capture
+            return hist, init, True
+        rs.roll(device)
+    used[slot] = True
+    return hist, init, False
+
+
 def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[torch.Tensor] = None,
                gelu_pre: Optional[torch.Tensor] = None):
     """fp8 quantisation of an activation (slot 0: the linear's input x), output gradient (slot 1: dz) or
@@ -207,27 +236,88 @@ def _quant_act(t: torch.Tensor, w: torch.Tensor, slot: int, colsum: Optional[tor
     launch per step (``_RollSet``)."""
     if not _FP8_DELAYED:
         return C.fp8_quantize_both(t if gelu_pre is None else C.gelu_bwd(t, gelu_pre))
-    sites = getattr(w, "_ringdp_fp8", None)
-    if sites is None:
-        sites = w._ringdp_fp8 = [None, None, None]
-        w._ringdp_fp8_used = [False, False, False]
-    used = w._ringdp_fp8_used
-    n = 1 + C.fp8_delayed_slots(t.shape[0], t.shape[1])
-    hist = sites[slot]
-    init = hist is None or hist.numel() != n
-    if init:
-        hist = sites[slot] = torch.zeros(n, device=t.device, dtype=torch.float32)
-    if not _FP8_BATCH_ROLL:
-        return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre)
-    rs = _ROLLS.setdefault(t.device, _RollSet())
-    if init:
-        rs.register(sites, used, slot)
-    elif used[slot]:
-        if rs.dirty and torch.cuda.is_current_stream_capturing():  # no table upload inside a capture
-            return C.fp8_quantize_both_delayed(t, hist, False, colsum, gelu_pre)
-        rs.roll(t.device)
-    used[slot] = True
-    return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre, roll=False)
+    hist, init, roll = _site(w, slot, 1 + C.fp8_delayed_slots(t.shape[0], t.shape[1]), t.device)
+    return C.fp8_quantize_both_delayed(t, hist, init, colsum, gelu_pre, roll=roll)
+
+
+_FP8_MLP_FUSED = os.environ.get("RINGDP_FP8_MLP_FUSED", "1") == "1"
+
+
+def fp8_mlp_fusable(M: int, D: int, Hd: int) -> bool:
+    """MLPF8 needs whole 16-row / 16-column e4m3 pieces and whole 128-byte k-steps (K = D)."""
+    return _FP8_MLP_FUSED and _FP8_DELAYED and M % 16 == 0 and Hd % 16 == 0 and D % 128 == 0
+
+
+def _epilogue_site(w, slot, M, N, device, exact_from: int):
+    """History of an epilogue-quantised site; on its first use the caller takes the unfused path, whose
+    quant_t site ``exact_from`` on the same weight measures the exact amax this one then starts from."""
+    hist, init, roll = _site(w, slot, 1 + C.gemm_fp8_q8_slots(M, N), device)
+    if roll:
+        C.fp8_roll(hist)
+    return hist, init
+
+
+class MLPF8(torch.autograd.Function):
+    """The transformer MLP ``y = fc2(GELU(fc1(h))) + residual`` in e4m3 with the [tokens, 3072] tensors
+    quantised by the GEMM epilogues that produce them (ringdp's fp8 256x256 kernel, ``ep.q8``):
+      forward   fc1's epilogue applies bias + GELU, stores the bf16 pre-activation (for the backward) and
+                writes GELU(.) as e4m3 row-major (fc2's A) and transposed (fc2's weight gradient) - the bf16
+                activation never reaches memory and fc2's input needs no quant_t pass;
+      backward  fc2's data-gradient epilogue applies the GELU backward and writes dz1 as e4m3 (both
+                orientations) plus its column sums (fc1's bias gradient) - no bf16 dz1, no quant_t pass.
+    Scales are delayed (the sites' previous amax, rolled once per step) exactly like the quant_t sites;
+    the first call of each epilogue site runs the unfused path to measure an exact amax."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2, residual):
+        M, D = h.shape
+        Hd = w1.shape[0]
+        hq, hqt, sh = _quant_act(h, w1, 0)
+        w1q, w1qt, sw1 = _quant_act(_bf16(w1), w1, 2)
+        pre = torch.empty(M, Hd, device=h.device, dtype=torch.bfloat16)
+        hist3, init3 = _epilogue_site(w2, 3, M, Hd, h.device, 0)
+        if init3:
+            a = C.gemm_fp8(hq, w1q, sh, sw1, M, Hd, D, True, b1, 2, None, pre)
+            aq, aqt, sa = _quant_act(a, w2, 0)
+            hist3[:1].copy_(w2._ringdp_fp8[0][:1])
+        else:
+            aq, aqt, sa = C.gemm_fp8_quant_out(hq, w1q, sh, sw1, M, Hd, D, b1, 2, pre, hist3)
+        w2q, w2qt, sw2 = _quant_act(_bf16(w2), w2, 2)
+        y = C.gemm_fp8(aq, w2q, sa, sw2, M, D, Hd, True, b2, 0, residual)
+        ctx.save_for_backward(hqt, sh, w1qt, sw1, pre, aqt, sa, w2qt, sw2)
+        ctx.params = (w1, b1, w2, b2)
+        ctx.dims = (M, D, Hd)
+        ctx.has_res = residual is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        hqt, sh, w1qt, sw1, pre, aqt, sa, w2qt, sw2 = ctx.saved_tensors
+        w1, b1, w2, b2 = ctx.params
+        M, D, Hd = ctx.dims
+        n = ctx.needs_input_grad
+        dyb = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
+        db2 = grad_buffer(b2) if n[4] else None
+        dyq, dyqt, sdy = _quant_act(dyb, w2, 1, db2)
+        dw2 = None
+        if n[3]:
+            dw2 = grad_buffer(w2)
+            C.gemm_fp8_splitk_f32(dyqt, aqt, sdy, sa, D, Hd, M, _splits(M, D, Hd), dw2)
+        db1 = grad_buffer(b1) if n[2] else None
+        hist4, init4 = _epilogue_site(w1, 4, M, Hd, dy.device, 1)
+        if init4:
+            da = C.gemm_fp8(dyq, w2qt, sdy, sw2, M, Hd, D, True)
+            dzq, dztq, sdz = _quant_act(da, w1, 1, db1, pre)
+            hist4[:1].copy_(w1._ringdp_fp8[1][:1])
+        else:
+            dzq, dztq, sdz = C.gemm_fp8_quant_out(dyq, w2qt, sdy, sw2, M, Hd, D, None, 3, pre, hist4, db1)
+        dw1 = None
+        if n[1]:
+            dw1 = grad_buffer(w1)
+            C.gemm_fp8_splitk_f32(dztq, hqt, sdz, sh, Hd, D, M, _splits(M, Hd, D), dw1)
+        dh = C.gemm_fp8(dzq, w1qt, sdz, sw1, M, D, Hd, True) if n[0] else None
+        dres = dyb if ctx.has_res and n[5] else None
+        return dh, dw1, db1, dw2, db2, dres
 
 
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):

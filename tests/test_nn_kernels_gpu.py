@@ -685,3 +685,107 @@ def test_fp8_batched_roll_matches_per_site_roll():
     assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+def _e4m3_ref(v: torch.Tensor, scale: float) -> torch.Tensor:
+    """e4m3 bytes of bf16-rounded v at a per-tensor scale, clamped to +-448 (what quant_t_kernel stores)."""
+    x = (v.bfloat16().float() * (1.0 / scale)).clamp(-448.0, 448.0)
+    return x.to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+@pytest.mark.parametrize("act", [2, 3])
+def test_gemm_fp8_quant_out_matches_bf16_output_then_quantise(act):
+    """The e4m3-output epilogue (GemmEpilogue::q8) against the bf16-output GEMM of the same kernel followed
+    by per-tensor quantisation: row-major and transposed bytes, the scale, the tile maxima (roll) and, for
+    the GELU backward, the column sums."""
+    import ringdp
+
+    C = ringdp._C
+    torch.manual_seed(0)
+    M, N, K = 1040, 512, 256  # M not a multiple of 256: a partial tile row (and a wave tile past M)
+    a = (torch.randn(M, K, device="cuda") * 2).to(torch.float8_e4m3fn).view(torch.uint8)
+    b = (torch.randn(N, K, device="cuda") * 2).to(torch.float8_e4m3fn).view(torch.uint8)
+    sa = torch.tensor([0.05], device="cuda")
+    sb = torch.tensor([0.03], device="cuda")
+    bias = torch.randn(N, device="cuda") if act == 2 else None
+    pre_in = torch.randn(M, N, device="cuda").bfloat16()
+    C.set_fp8_tile_mode(256)
+    try:
+        if act == 2:
+            pre_ref = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+            v = C.gemm_fp8(a, b, sa, sb, M, N, K, True, bias, 2, None, pre_ref)
+        else:
+            v = C.gemm_fp8(a, b, sa, sb, M, N, K, False) * 1.0  # fp32, GELU backward applied below
+            x = pre_in.float()
+            cdf = 0.5 * (1 + torch.erf(x * 0.7071067811865476))
+            v = v * (cdf + x * 0.3989422804014327 * torch.exp(-0.5 * x * x))
+        amax = float(v.float().abs().max()) * 0.8  # delayed scale smaller than the true amax: exercises the clamp
+        hist = torch.zeros(1 + C.gemm_fp8_q8_slots(M, N), device="cuda")
+        hist[0] = amax
+        colsum = torch.empty(N, device="cuda") if act == 3 else None
+        pre = torch.empty(M, N, device="cuda", dtype=torch.bfloat16) if act == 2 else pre_in
+        q, qt, scale = C.gemm_fp8_quant_out(a, b, sa, sb, M, N, K, bias, act, pre, hist, colsum)
+    finally:
+        C.set_fp8_tile_mode(0)
+    torch.cuda.synchronize()
+    s = amax / 448.0
+    assert abs(float(scale) - s) <= 1e-6 * s
+    assert torch.equal(qt, q.t().contiguous())
+    ref = _e4m3_ref(v.float(), float(scale))
+    # act 2 runs the same epilogue arithmetic as the bf16 output: bit-identical; act 3 folds GELU' before
+    # the bf16 rounding (the reference rounds the fp32 GEMM output once, then multiplies): near-identical
+    # (torch's fp32 -> e4m3 conversion and v_cvt_pk_fp8_f32 may still differ on rare ties / subnormals)
+    diff = (q != ref).float().mean().item()
+    dq = (q.view(torch.float8_e4m3fn).float() - ref.view(torch.float8_e4m3fn).float()).abs()
+    assert float(dq.max()) <= 32.0  # at most one e4m3 step at the top of the range
+    if act == 2:
+        assert torch.equal(pre, pre_ref)
+        assert diff < 1e-3, diff
+    else:
+        assert diff < 0.02, diff
+        ref_cs = v.bfloat16().float().sum(0)
+        torch.testing.assert_close(colsum, ref_cs, rtol=2e-2, atol=2e-2 * float(ref_cs.abs().max()))
+    # tile maxima: the next roll gives the true |v|max (over the valid rows only)
+    assert abs(float(hist[1:].max()) - float(v.bfloat16().float().abs().max())) <= 2e-2 * float(v.abs().max())
+
+
+def test_vit_fp8_mlp_epilogue_quantisation_tracks_unfused():
+    """MLPF8 (fc1 / fc2-dgrad epilogues emit e4m3) against the per-linear fp8 path on a 128-wide ViT:
+    the first step is identical (epilogue sites start on the unfused path), later losses stay close."""
+    import copy
+
+    import ringdp.ops.transformer as tr
+    from ringdp.models.vit import VisionTransformer
+    from ringdp.optim import SGD
+
+    torch.manual_seed(0)
+    m = VisionTransformer(image_size=32, patch_size=4, num_layers=2, num_heads=2, hidden_dim=128, mlp_dim=256,
+                          num_classes=10).cuda()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xs = [torch.randn(16, 3, 32, 32, device="cuda", generator=g) for _ in range(6)]
+    ys = [torch.randint(0, 10, (16,), device="cuda", generator=g) for _ in range(6)]
+    res = []
+    try:
+        tr.set_fp8(True)
+        for fused in (False, True):
+            tr._FP8_MLP_FUSED = fused
+            tr._ROLLS.clear()
+            mm = copy.deepcopy(m)
+            opt = SGD(mm.parameters(), lr=0.05, momentum=0.9)
+            losses = []
+            for x, y in zip(xs, ys):
+                loss = F.cross_entropy(mm(x), y)
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                opt.step()
+                losses.append(float(loss))
+            res.append(losses)
+            if fused:
+                assert mm.encoder.layers[0].mlp[3].weight._ringdp_fp8[3] is not None  # the fused path ran
+    finally:
+        tr.set_fp8(False)
+        tr._FP8_MLP_FUSED = True
+    print("unfused", res[0], "fused", res[1])
+    assert res[0][0] == res[1][0]
+    for a, b in zip(res[0], res[1]):
+        assert abs(a - b) < 0.05 * abs(res[0][0]), (res[0], res[1])
