@@ -188,8 +188,11 @@ bool gemm_fp8_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M
   dim3 grid(tiles_m * tiles_n, batch * splits);
   static const int swz = env_int("RINGDP_FP8_SWZ", 1), group_m = env_int("RINGDP_FP8_GROUP_M", 4);
   GemmEpilogue e2 = ep;
-  e2.store_mode = gemm_wide_store_mode() % 10;
-  e2.store_rot = gemm_wide_store_mode() < 10;
+  // bf16 output: 16-B stores after a lane exchange (mode 1) measured +0.8 % on the ViT-B/16 fp8 step over the
+  // LDS-staged rows the bf16 kernels use (5957 / 5973 vs 5910 / 5928 img/s, profiles/r04/fp8/env_sweep.txt)
+  static const int wide = env_int("RINGDP_FP8_WIDE_STORE", 1);
+  e2.store_mode = wide % 10;
+  e2.store_rot = wide < 10;
   e2.store_cache = gemm_store_cache();
   gemm_fp8_256_kernel<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld, A.bstride,
                                            static_cast<const uint8_t*>(Bop.p), Bop.ld, Bop.bstride, e2, M, N, Kbytes,
