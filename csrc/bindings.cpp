@@ -526,7 +526,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_fwd", &ops::softmax_fwd);
   m.def("attn_bwd_ds", &ops::attn_bwd_ds, "fused dP = dO V^T + softmax backward -> dS (head dim 64, Tp <= 256)");
   m.def("attn_fwd_rows", &ops::attn_fwd_rows,
-        "fused attention forward on the qkv projection rows [B*T, 3*H*64]: returns [P, out rows [B*T, H*64]]");
+        "fused attention forward on the qkv projection rows [B*T, 3*H*64]: returns [P (or, recompute=True, the "
+        "per-query log-sum-exp), out rows [B*T, H*64]]",
+        py::arg("qkv"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("scale"), py::arg("recompute") = false);
   m.def("attn_bwd_rows", &ops::attn_bwd_rows, "fused attention backward from output-grad rows -> dqkv rows");
   m.def("attn_bwd", &ops::attn_bwd,
         "fused attention backward -> dqkv rows [B*T, 3*H*Dh] (query-side dQ kernel + key-side dK/dV kernel)");

@@ -457,6 +457,11 @@ bool attn_bwd(const void* dout, const void* q, const void* k, const void* v, con
 // (forward) / taking dO rows [B*T][H*64] (backward): no head-major split, merge or transposes
 bool attn_fwd_rows(const void* qkv, int B, int T, int H, int Tp, int Dh, float scale, void* p, void* out,
                    hipStream_t s);
+// P-recompute variants: the forward stores the per-query log-sum-exp lse [B*H][Tp] instead of P
+bool attn_fwd_rows_lse(const void* qkv, int B, int T, int H, int Tp, int Dh, float scale, float* lse, void* out,
+                       hipStream_t s);
+bool attn_bwd_rows_lse(const void* dout_rows, const void* qkv, const float* lse, int B, int T, int H, int Tp, int Dh,
+                       float scale, float* dsum, void* dqkv, hipStream_t s);
 bool attn_bwd_rows(const void* dout_rows, const void* qkv, const void* p, int B, int T, int H, int Tp, int Dh,
                    float scale, float* dsum, void* dqkv, hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);

@@ -554,9 +554,13 @@ __device__ __forceinline__ int att_vsw(int r, int d) {
   return r * ATT_D + ((((d >> 4) ^ ((r >> 1) & 3))) << 4) + (d & 15);
 }
 
-template <int NT>  // key tiles of 16 (Tp = 16 * NT)
+// LSE: instead of P, store each query's log-sum-exp (lse[bh][Tp], +inf for padded queries) - the backward
+// kernels recompute P = exp(scale S - lse) from Q and K (flash-attention style): P is 2 x Tp^2 bytes per head
+// written here and read twice in the backward, the largest HBM stream of the attention (ViT-B/16: 133 MB per
+// layer per pass, against 5.5 MFLOP of MFMA work per head to recompute it)
+template <int NT, bool LSE>  // key tiles of 16 (Tp = 16 * NT)
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnIn q, AttnIn k, AttnIn v, int T, int H, float scale,
-                                                       bf16* __restrict__ p, AttnOut o) {
+                                                       bf16* __restrict__ p, AttnOut o, float* __restrict__ lse) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
@@ -606,12 +610,14 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnIn q, AttnIn k, AttnI
     sum += __shfl_xor(sum, 32, 64);
     const float inv = qrow < T ? 1.f / sum : 0.f;  // padded query rows: P = 0
     bf16x4 pb[NT];
-    bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
       pb[t] = bf16x4{(bf16)(st[t][0] * inv), (bf16)(st[t][1] * inv), (bf16)(st[t][2] * inv), (bf16)(st[t][3] * inv)};
-    {  // tile pairs (t, t+1): lanes with g even store 8 keys of tile t, g odd 8 keys of tile t+1 (one xor-16
+    if constexpr (LSE) {
+      if (g == 0) lse[(int64_t)bh * Tp + qrow] = qrow < T ? mx + __logf(sum) : INFINITY;
+    } else {  // tile pairs (t, t+1): lanes with g even store 8 keys of tile t, g odd 8 keys of tile t+1 (one xor-16
        // exchange of 8 B): 16-B stores, 64 contiguous bytes of each of 16 rows per store instruction
+      bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp;
       const bool godd = g & 1;
 #pragma unroll
       for (int t = 0; t + 1 < NT; t += 2) {
@@ -710,10 +716,11 @@ __global__ __launch_bounds__(256) void attn_bwd_ds_kernel(const bf16* __restrict
 // pass - dQ^T = K^T dS^T with the dS registers as the MFMA B operand and K^T read from LDS with
 // ds_read_b64_tr_b16 (the forward's O^T = V^T P^T trick).  dQ rows go straight into the dqkv gradient
 // rows [B*T][3*H*Dh]; D = rowsum(dP * P) per query is stored for the key-side kernel.
-template <int NT>
+template <int NT, bool LSE>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k, AttnIn v,
                                                           const bf16* __restrict__ p, float scale, int T, int H,
-                                                          float* __restrict__ dsum, AttnOut dq) {
+                                                          float* __restrict__ dsum, AttnOut dq, AttnIn q,
+                                                          const float* __restrict__ lse) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
@@ -731,10 +738,25 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k,
     const int qrow = qt * 16 + qi;
     const bf16x8 of0 = dout.load8(bh, H, qrow, T, 8 * g);
     const bf16x8 of1 = dout.load8(bh, H, qrow, T, 32 + 8 * g);
-    const bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp + 4 * g;
     bf16x4 pv[NT];
+    if constexpr (LSE) {  // P recomputed: S^T tile by tile exactly as the forward (lane (g, q): keys 16t + 4g + i)
+      const bf16x8 qf0 = q.load8(bh, H, qrow, T, 8 * g);
+      const bf16x8 qf1 = q.load8(bh, H, qrow, T, 32 + 8 * g);
+      const float lq = lse[(int64_t)bh * Tp + qrow];  // +inf for padded queries: P = 0
 #pragma unroll
-    for (int t = 0; t < NT; ++t) pv[t] = *reinterpret_cast<const bf16x4*>(prow + 16 * t);
+      for (int t = 0; t < NT; ++t) {
+        const int kr = 16 * t + qi;
+        const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Ks + att_vsw(kr, 8 * g));
+        const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ks + att_vsw(kr, 32 + 8 * g));
+        const f32x4 sv = mfma16x16x32(a1, qf1, mfma16x16x32(a0, qf0, zero_f32x4()));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) pv[t][i] = (bf16)(16 * t + 4 * g + i < T ? __expf(sv[i] * scale - lq) : 0.f);
+      }
+    } else {
+      const bf16* prow = p + ((int64_t)bh * Tp + qrow) * Tp + 4 * g;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) pv[t] = *reinterpret_cast<const bf16x4*>(prow + 16 * t);
+    }
     // dP = dO V^T tile by tile, recomputed in the second pass instead of held: the NT x 4 fp32 dP
     // registers had pushed the kernel to 232 VGPRs (one wave per SIMD)
     auto dp_tile = [&](int t) {
@@ -795,10 +817,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k,
 //   dV^T[d][key] += dO^T P     and     dK^T[d][key] += Q^T dS
 // with those registers as the MFMA B operand (reduction over the query pair, permuted like the forward's
 // key pairs) and dO^T / Q^T read from LDS with ds_read_b64_tr_b16.  dK, dV rows go straight into dqkv.
-template <int NT>
+template <int NT, bool LSE>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn q, AttnIn v,
                                                             const bf16* __restrict__ p, const float* __restrict__ dsum,
-                                                            float scale, int T, int H, AttnOut dk, AttnOut dv) {
+                                                            float scale, int T, int H, AttnOut dk, AttnOut dv,
+                                                            AttnIn k, const float* __restrict__ lse) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Qs[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Os[Tp * ATT_D];  // dO
@@ -817,6 +840,12 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
     const int key = kt * 16 + ki;
     const bf16x8 vf0 = v.load8(bh, H, key, T, 8 * g);
     const bf16x8 vf1 = v.load8(bh, H, key, T, 32 + 8 * g);
+    bf16x8 kf0 = zero_bf16x8(), kf1 = zero_bf16x8();
+    if constexpr (LSE) {
+      kf0 = k.load8(bh, H, key, T, 8 * g);
+      kf1 = k.load8(bh, H, key, T, 32 + 8 * g);
+    }
+    const float* lq = lse + (int64_t)bh * Tp;
     const bf16* pcol = p + (int64_t)bh * Tp * Tp + key;
     f32x4 dva[4], dka[4];
 #pragma unroll
@@ -832,10 +861,20 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
         const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(Os + att_vsw(orow, 8 * g));
         const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Os + att_vsw(orow, 32 + 8 * g));
         const f32x4 dpv = mfma16x16x32(a1, vf1, mfma16x16x32(a0, vf0, zero_f32x4()));
+        f32x4 spv = zero_f32x4();
+        if constexpr (LSE) {  // S[q][key] for the same queries: A = Q rows (LDS image), B = K rows (registers)
+          const bf16x8 c0 = *reinterpret_cast<const bf16x8*>(Qs + att_vsw(orow, 8 * g));
+          const bf16x8 c1 = *reinterpret_cast<const bf16x8*>(Qs + att_vsw(orow, 32 + 8 * g));
+          spv = mfma16x16x32(c1, kf1, mfma16x16x32(c0, kf0, zero_f32x4()));
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qq = 16 * qp[u] + 4 * g + r;
-          const float pr = (u == 0 || has1) ? (float)pcol[(int64_t)qq * Tp] : 0.f;
+          float pr;
+          if constexpr (LSE)  // the bf16 value the forward would have stored
+            pr = (u == 0 || has1) && key < T ? (float)(bf16)__expf(spv[r] * scale - lq[qq]) : 0.f;
+          else
+            pr = (u == 0 || has1) ? (float)pcol[(int64_t)qq * Tp] : 0.f;
           pb[u][r] = (bf16)pr;
           sb[u][r] = (bf16)(scale * pr * (dpv[r] - db[qq]));
         }
@@ -868,9 +907,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
 
 template <int NT>
 void attn_bwd_launch(AttnIn dout, AttnIn q, AttnIn k, AttnIn v, const void* p, int BH, int T, int H, float scale,
-                     float* dsum, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s) {
-  attn_bwd_dq_kernel<NT><<<BH, 256, 0, s>>>(dout, k, v, static_cast<const bf16*>(p), scale, T, H, dsum, dq);
-  attn_bwd_dkdv_kernel<NT><<<BH, 256, 0, s>>>(dout, q, v, static_cast<const bf16*>(p), dsum, scale, T, H, dk, dv);
+                     float* dsum, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s, const float* lse = nullptr) {
+  if (lse) {
+    attn_bwd_dq_kernel<NT, true><<<BH, 256, 0, s>>>(dout, k, v, nullptr, scale, T, H, dsum, dq, q, lse);
+    attn_bwd_dkdv_kernel<NT, true><<<BH, 256, 0, s>>>(dout, q, v, nullptr, dsum, scale, T, H, dk, dv, k, lse);
+    return;
+  }
+  attn_bwd_dq_kernel<NT, false><<<BH, 256, 0, s>>>(dout, k, v, static_cast<const bf16*>(p), scale, T, H, dsum, dq, q,
+                                                   nullptr);
+  attn_bwd_dkdv_kernel<NT, false><<<BH, 256, 0, s>>>(dout, q, v, static_cast<const bf16*>(p), dsum, scale, T, H, dk, dv,
+                                                     k, nullptr);
 }
 
 template <int NT>
@@ -882,8 +928,11 @@ void attn_bwd_ds_launch(const void* dout, const void* v, const void* p, int BH, 
 
 template <int NT>
 void attn_fwd_launch(AttnIn q, AttnIn k, AttnIn v, int BH, int T, int H, float scale, void* p, AttnOut o,
-                     hipStream_t s) {
-  attn_fwd_kernel<NT><<<BH, 256, 0, s>>>(q, k, v, T, H, scale, static_cast<bf16*>(p), o);
+                     hipStream_t s, float* lse = nullptr) {
+  if (lse)
+    attn_fwd_kernel<NT, true><<<BH, 256, 0, s>>>(q, k, v, T, H, scale, nullptr, o, lse);
+  else
+    attn_fwd_kernel<NT, false><<<BH, 256, 0, s>>>(q, k, v, T, H, scale, static_cast<bf16*>(p), o, nullptr);
 }
 
 }  // namespace
@@ -931,6 +980,16 @@ bool attn_fwd_rows(const void* qkv, int B, int T, int H, int Tp, int Dh, float s
   return false;
 }
 
+bool attn_fwd_rows_lse(const void* qkv, int B, int T, int H, int Tp, int Dh, float scale, float* lse, void* out,
+                       hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
+  const int64_t w3 = (int64_t)3 * H * ATT_D, w1 = (int64_t)H * ATT_D;
+  RINGDP_ATT_SWITCH((attn_fwd_launch<n>(token_rows(qkv, T, w3, 0), token_rows(qkv, T, w3, w1),
+                                        token_rows(qkv, T, w3, 2 * w1), B * H, T, H, scale, nullptr,
+                                        token_rows_out(out, T, w1, 0), s, lse)))
+  return false;
+}
+
 bool attn_bwd_ds(const void* dout, const void* v, const void* p, int BH, int Tp, int Dh, float scale, void* ds,
                  hipStream_t s) {
   if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16) return false;
@@ -969,6 +1028,17 @@ bool attn_bwd_rows(const void* dout_rows, const void* qkv, const void* p, int B,
                                         token_rows(qkv, T, w3, w1), token_rows(qkv, T, w3, 2 * w1), p, B * H, T, H,
                                         scale, dsum, token_rows_out(dqkv, T, w3, 0), token_rows_out(dqkv, T, w3, w1),
                                         token_rows_out(dqkv, T, w3, 2 * w1), s)))
+  return false;
+}
+
+bool attn_bwd_rows_lse(const void* dout_rows, const void* qkv, const float* lse, int B, int T, int H, int Tp, int Dh,
+                       float scale, float* dsum, void* dqkv, hipStream_t s) {
+  if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
+  const int64_t w3 = (int64_t)3 * H * ATT_D, w1 = (int64_t)H * ATT_D;
+  RINGDP_ATT_SWITCH((attn_bwd_launch<n>(token_rows(dout_rows, T, w1, 0), token_rows(qkv, T, w3, 0),
+                                        token_rows(qkv, T, w3, w1), token_rows(qkv, T, w3, 2 * w1), nullptr, B * H, T,
+                                        H, scale, dsum, token_rows_out(dqkv, T, w3, 0), token_rows_out(dqkv, T, w3, w1),
+                                        token_rows_out(dqkv, T, w3, 2 * w1), s, lse)))
   return false;
 }
 

@@ -575,12 +575,20 @@ at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
   return dqkv;
 }
 
-std::vector<at::Tensor> attn_fwd_rows(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double scale) {
+std::vector<at::Tensor> attn_fwd_rows(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double scale,
+                                      bool recompute) {
   bf16_gpu(qkv, "attention qkv rows");
   RINGDP_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && qkv.size(1) % (3 * H) == 0, "attn_fwd_rows: qkv [B*T, 3*H*Dh]");
   const int64_t Dh = qkv.size(1) / (3 * H), Tp = (T + 15) / 16 * 16;
-  at::Tensor p = at::empty({B * H, Tp, Tp}, qkv.options());
   at::Tensor out = at::empty({B * T, H * Dh}, qkv.options());
+  if (recompute) {  // saved for the backward: per-query log-sum-exp [B*H][Tp] fp32 instead of P
+    at::Tensor lse = at::empty({B * H, Tp}, qkv.options().dtype(at::kFloat));
+    const bool ok = kern::attn_fwd_rows_lse(qkv.data_ptr(), (int)B, (int)T, (int)H, (int)Tp, (int)Dh, (float)scale,
+                                            lse.data_ptr<float>(), out.data_ptr(), stream_of(qkv));
+    RINGDP_CHECK(ok, "attn_fwd_rows: unsupported shape (needs head dim 64, T <= 256)");
+    return {lse, out};
+  }
+  at::Tensor p = at::empty({B * H, Tp, Tp}, qkv.options());
   const bool ok = kern::attn_fwd_rows(qkv.data_ptr(), (int)B, (int)T, (int)H, (int)Tp, (int)Dh, (float)scale,
                                       p.data_ptr(), out.data_ptr(), stream_of(qkv));
   RINGDP_CHECK(ok, "attn_fwd_rows: unsupported shape (needs head dim 64, T <= 256)");
@@ -591,8 +599,21 @@ at::Tensor attn_bwd_rows(const at::Tensor& dout, const at::Tensor& qkv, const at
                          int64_t H, double scale) {
   bf16_gpu(dout, "attention output grad rows");
   bf16_gpu(qkv, "attention qkv rows");
-  bf16_gpu(p, "attention probs");
   const int64_t Dh = qkv.size(1) / (3 * H), Tp = (T + 15) / 16 * 16;
+  if (p.scalar_type() == at::kFloat) {  // the forward saved the log-sum-exp: P is recomputed
+    f32_gpu(p, "attention log-sum-exp");
+    RINGDP_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && dout.dim() == 2 && dout.size(0) == B * T &&
+                     dout.size(1) == H * Dh && p.dim() == 2 && p.size(0) == B * H && p.size(1) == Tp,
+                 "attn_bwd_rows: shape mismatch");
+    at::Tensor dqkv = at::empty_like(qkv);
+    at::Tensor dsum = at::empty({B * H, Tp}, qkv.options().dtype(at::kFloat));
+    const bool ok = kern::attn_bwd_rows_lse(dout.data_ptr(), qkv.data_ptr(), p.data_ptr<float>(), (int)B, (int)T, (int)H,
+                                            (int)Tp, (int)Dh, (float)scale, dsum.data_ptr<float>(), dqkv.data_ptr(),
+                                            stream_of(qkv));
+    RINGDP_CHECK(ok, "attn_bwd_rows: unsupported shape (needs head dim 64, T <= 256)");
+    return dqkv;
+  }
+  bf16_gpu(p, "attention probs");
   RINGDP_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && dout.dim() == 2 && dout.size(0) == B * T &&
                    dout.size(1) == H * Dh && p.dim() == 3 && p.size(0) == B * H && p.size(1) == Tp && p.size(2) == Tp,
                "attn_bwd_rows: shape mismatch");

@@ -53,7 +53,8 @@ at::Tensor softmax_fwd(const at::Tensor& scores, int64_t T, double scale);
 at::Tensor attn_bwd_ds(const at::Tensor& dout, const at::Tensor& v, const at::Tensor& p, double scale);
 at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tensor& k, const at::Tensor& v,
                     const at::Tensor& p, int64_t B, int64_t T, int64_t H, double scale);
-std::vector<at::Tensor> attn_fwd_rows(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double scale);
+std::vector<at::Tensor> attn_fwd_rows(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double scale,
+                                      bool recompute = false);
 at::Tensor attn_bwd_rows(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& p, int64_t B, int64_t T,
                          int64_t H, double scale);
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t T,

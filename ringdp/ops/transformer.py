@@ -20,6 +20,8 @@ from . import grad_buffer
 # RINGDP_ATTN_UNFUSED=1: attention forward as two GEMMs + a softmax pass (the path the fused kernel replaced)
 _ATTN_UNFUSED = os.environ.get("RINGDP_ATTN_UNFUSED", "0") == "1"
 _ATTN_BWD_GEMMS = os.environ.get("RINGDP_ATTN_BWD_GEMMS", "0") == "1"  # dS kernel + batched GEMMs (A/B runs)
+# fused attention saves the per-query log-sum-exp and the backward recomputes P (RINGDP_ATTN_RECOMPUTE=0: store P)
+_ATTN_RECOMPUTE = os.environ.get("RINGDP_ATTN_RECOMPUTE", "1") == "1"
 _FP8 = {"on": False}
 
 
@@ -464,7 +466,7 @@ class AttentionF(torch.autograd.Function):
         if Dh == 64 and Tp <= 256 and not _ATTN_UNFUSED and not _ATTN_BWD_GEMMS:
             # fused kernels straight on the projection rows: no head-major split / merge passes
             scale = 1.0 / math.sqrt(Dh)
-            p, out = C.attn_fwd_rows(qkv, B, T, H, scale)
+            p, out = C.attn_fwd_rows(qkv, B, T, H, scale, _ATTN_RECOMPUTE)  # p: P, or the log-sum-exp
             ctx.save_for_backward(qkv, p)
             ctx.cfg = (B, T, H, Tp, scale)
             ctx.rows = True

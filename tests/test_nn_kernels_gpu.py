@@ -789,3 +789,34 @@ def test_vit_fp8_mlp_epilogue_quantisation_tracks_unfused():
     assert res[0][0] == res[1][0]
     for a, b in zip(res[0], res[1]):
         assert abs(a - b) < 0.05 * abs(res[0][0]), (res[0], res[1])
+
+
+@pytest.mark.parametrize("T", [197, 50])
+def test_attention_recompute_matches_stored_probabilities(T):
+    """Fused attention with P recomputed in the backward from the saved log-sum-exp against the path that
+    stores P: identical forward output, and dqkv within bf16 rounding of P (the recomputed P is rounded to
+    bf16 exactly where the stored one was)."""
+    import ringdp
+
+    C = ringdp._C
+    torch.manual_seed(0)
+    B, H = 4, 12
+    qkv = (torch.randn(B * T, 3 * H * 64, device="cuda") * 0.5).bfloat16()
+    dout = torch.randn(B * T, H * 64, device="cuda").bfloat16()
+    scale = 0.125
+    p, out_p = C.attn_fwd_rows(qkv, B, T, H, scale, False)
+    lse, out_l = C.attn_fwd_rows(qkv, B, T, H, scale, True)
+    assert lse.dtype == torch.float32 and lse.shape == (B * H, (T + 15) // 16 * 16)
+    assert torch.equal(out_p, out_l)
+    # lse reproduces the stored probabilities
+    Tp = lse.shape[1]
+    q = qkv.view(B, T, 3, H, 64)[:, :, 0].permute(0, 2, 1, 3).float()
+    k = qkv.view(B, T, 3, H, 64)[:, :, 1].permute(0, 2, 1, 3).float()
+    pr = torch.exp(q @ k.transpose(-1, -2) * scale - lse.view(B, H, Tp)[:, :, :T, None])
+    torch.testing.assert_close(pr, p.view(B, H, Tp, Tp)[:, :, :T, :T].float(), atol=4e-3, rtol=1e-2)
+    assert torch.isinf(lse.view(B, H, Tp)[:, :, T:]).all()
+    d_p = C.attn_bwd_rows(dout, qkv, p, B, T, H, scale)
+    d_l = C.attn_bwd_rows(dout, qkv, lse, B, T, H, scale)
+    torch.cuda.synchronize()
+    err = (d_l.float() - d_p.float()).norm() / d_p.float().norm()
+    assert err < 1e-2, err
