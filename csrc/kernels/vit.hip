@@ -835,7 +835,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
   __syncthreads();
   const int g = lane >> 4, ki = lane & 15;
   const int q4 = ki >> 2, p4 = ki & 3;
+  // per-query D = rowsum(dP * P) and log-sum-exp: a lane's 4 queries 16 qp + 4g + r are one 16-B load each
   const float* db = dsum + (int64_t)bh * Tp;
+  const float* lq = LSE ? lse + (int64_t)bh * Tp : nullptr;
   for (int kt = wave; kt < NT; kt += 4) {
     const int key = kt * 16 + ki;
     const bf16x8 vf0 = v.load8(bh, H, key, T, 8 * g);
@@ -845,11 +847,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
       kf0 = k.load8(bh, H, key, T, 8 * g);
       kf1 = k.load8(bh, H, key, T, 32 + 8 * g);
     }
-    const float* lq = lse + (int64_t)bh * Tp;
     const bf16* pcol = p + (int64_t)bh * Tp * Tp + key;
     f32x4 dva[4], dka[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dva[dt] = dka[dt] = zero_f32x4();
+#pragma unroll 1  // (unrolled, the hoisted per-pair loads take the kernel to 256 VGPRs)
     for (int ks = 0; ks < (NT + 1) / 2; ++ks) {
       const int qp[2] = {2 * ks, 2 * ks + 1 < NT ? 2 * ks + 1 : 2 * ks};
       const bool has1 = 2 * ks + 1 < NT;
@@ -867,16 +869,19 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
           const bf16x8 c1 = *reinterpret_cast<const bf16x8*>(Qs + att_vsw(orow, 32 + 8 * g));
           spv = mfma16x16x32(c1, kf1, mfma16x16x32(c0, kf0, zero_f32x4()));
         }
+        const f32x4 dq4 = *reinterpret_cast<const f32x4*>(db + 16 * qp[u] + 4 * g);
+        f32x4 lq4 = zero_f32x4();
+        if constexpr (LSE) lq4 = *reinterpret_cast<const f32x4*>(lq + 16 * qp[u] + 4 * g);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int qq = 16 * qp[u] + 4 * g + r;
           float pr;
           if constexpr (LSE)  // the bf16 value the forward would have stored
-            pr = (u == 0 || has1) && key < T ? (float)(bf16)__expf(spv[r] * scale - lq[qq]) : 0.f;
+            pr = (u == 0 || has1) && key < T ? (float)(bf16)__expf(spv[r] * scale - lq4[r]) : 0.f;
           else
             pr = (u == 0 || has1) ? (float)pcol[(int64_t)qq * Tp] : 0.f;
           pb[u][r] = (bf16)pr;
-          sb[u][r] = (bf16)(scale * pr * (dpv[r] - db[qq]));
+          sb[u][r] = (bf16)(scale * pr * (dpv[r] - dq4[r]));
         }
       }
       const bf16x8 pfr = bf16x8{pb[0][0], pb[0][1], pb[0][2], pb[0][3], pb[1][0], pb[1][1], pb[1][2], pb[1][3]};

@@ -1,0 +1,11 @@
+#!/bin/bash
+# dK/dV kernel: vector loads of the per-query D / lse, rolled pair loop; tests + profile + bench
+set -o pipefail
+O=gpurun_out/r4ak; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_nn_kernels_gpu.py -k "attention or attn" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/p_vit16 -o run -- python3 $R/bench.py --model vit_b_16 --steps 10 > $R/$O/p.log 2>&1 || { tail -5 $R/$O/p.log; exit 1; }
+cp $(find /tmp/p_vit16 -name "*kernel_stats.csv" | head -1) $R/$O/vit16_kernel_stats.csv
+grep metric $R/$O/p.log | cut -c1-150; echo ALLDONE
