@@ -498,7 +498,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("ldb"), py::arg("a_row") = false, py::arg("b_row") = false, py::arg("batch") = 1,
         py::arg("a_bstride") = 0, py::arg("b_bstride") = 0, py::arg("out_bf16") = true,
         py::arg("bias") = py::none(), py::arg("act") = 0, py::arg("residual") = py::none(),
-        py::arg("preact") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none());
+        py::arg("preact") = py::none(), py::arg("alpha") = 1.0, py::arg("out") = py::none(),
+        py::arg("colsum") = py::none());
   m.def("gemm_splitk_f32", &ops::gemm_splitk_f32);
   m.def("pack_conv_weight", &ops::pack_conv_weight);
   m.def("pack_conv_weights", &ops::pack_conv_weights);

@@ -111,7 +111,7 @@ __device__ __forceinline__ void gemm256_store_q8(const dev::f32x4 (&acc)[8][4], 
   const float qs = fmaxf(ep.q8_amax[0], 1e-12f) / 448.f;  // the scale quant_t_kernel would use
   const float inv = 1.f / qs;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) ep.q8_scale[0] = qs;
-  const bool want_cs = __builtin_amdgcn_readfirstlane(ep.q8_colsum != nullptr ? 1 : 0) != 0;
+  const bool want_cs = __builtin_amdgcn_readfirstlane(ep.colsum_part != nullptr ? 1 : 0) != 0;
   f32x4 bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -228,7 +228,7 @@ __device__ __forceinline__ void gemm256_store_q8(const dev::f32x4 (&acc)[8][4], 
         cs[j][e] = t;
       }
     if (fr == 0) {
-      float* row = ep.q8_colsum + (int64_t)(m_base >> 7) * N;  // one partial row per 128-row wave tile
+      float* row = ep.colsum_part + (int64_t)(m_base >> 7) * N;  // one partial row per 128-row wave tile
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nof(j);
@@ -242,7 +242,7 @@ __device__ __forceinline__ void gemm256_store_q8(const dev::f32x4 (&acc)[8][4], 
 // otherwise acc[i][j] covers rows mrow + 16 i, columns ncol + 16 j.
 // lds_wave: this wave's 16 KiB of the kernel's LDS (free once the main loop's last barrier has passed):
 // store mode 2 writes the wave's 128 x 64 bf16 tile there and stores it back as whole 128-B rows.
-template <bool QUAD, int ACT, bool Q8>
+template <bool QUAD, int ACT, bool Q8, bool CS>
 __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep,
                                                    const EpiFlags& fl, int M, int N, int bidx, int mrow, int ncol,
                                                    float scale, char* lds_wave) {
@@ -292,6 +292,11 @@ __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4]
     // final values -> bf16 -> LDS image [128 rows][64 cols] (128-B rows, 16-B chunk c of row r at c ^ (r & 7)),
     // then 8 lanes per row store whole 128-B rows
     const int fr = lane & 15, fq = lane >> 4;
+    float cs[4][4];  // CS: column sums of the stored values over this lane's rows
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[j][e] = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -303,6 +308,12 @@ __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4]
           *reinterpret_cast<bf16x4*>(static_cast<bf16*>(ep.preact) + cb + (int64_t)m * ep.ldc + n) =
               bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         epi_finish<ACT>(v, sv[i][j], fl.res);
+        if constexpr (CS) {
+          const bool ok = m < M && n < N;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cs[j][e] += ok ? (float)(bf16)v[e] : 0.f;
+          asm volatile("" : "+v"(cs[j][0]), "+v"(cs[j][1]), "+v"(cs[j][2]), "+v"(cs[j][3]));  // (see the q8 path)
+        }
         const int r = (QUAD ? (i >> 2) * 64 + 16 * (i & 3) : 16 * i) + fr;    // row in the wave tile
         const int c = QUAD ? (j >> 1) * 32 + 16 * (j & 1) + 4 * fq : 16 * j + 4 * fq;  // column
         *reinterpret_cast<bf16x4*>(lds_wave + r * 128 + ((((c >> 3) ^ (r & 7)) << 4) | ((c & 7) << 1))) =
@@ -325,6 +336,27 @@ __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4]
         // probe mode 4: the whole epilogue, but every store goes to one 16-B sink (no HBM write traffic)
         void* dst = fl.mode == 4 ? ep.sink : static_cast<void*>(cbase + (int64_t)m * ep.ldc + n);
         gemm_st16(dst, w, ep.store_cache);
+      }
+    }
+    if constexpr (CS) {  // the 16 lanes of one fq hold the same columns: xor 1 / 2 / 4 / 8 sums their rows
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float t = cs[j][e];
+          t += __shfl_xor(t, 1, 64);
+          t += __shfl_xor(t, 2, 64);
+          t += __shfl_xor(t, 4, 64);
+          t += __shfl_xor(t, 8, 64);
+          cs[j][e] = t;
+        }
+      if (fr == 0) {
+        float* row = ep.colsum_part + (int64_t)(m_base >> 7) * N;  // one partial row per 128-row wave tile
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = nof(j);
+          if (n < N) *reinterpret_cast<f32x4*>(row + n) = f32x4{cs[j][0], cs[j][1], cs[j][2], cs[j][3]};
+        }
       }
     }
     return;
@@ -392,8 +424,9 @@ __device__ __forceinline__ void gemm256_store_impl(const dev::f32x4 (&acc)[8][4]
   }
 }
 
-// Q8: the e4m3-output path (GemmEpilogue::q8) is compiled in (the fp8 kernel)
-template <bool QUAD, bool Q8 = false>
+// Q8: the e4m3-output path (GemmEpilogue::q8) is compiled in (the fp8 kernel); CS: the bf16 LDS-row store path
+// also writes column-sum partials (ep.colsum_part; the launcher forces store mode 2)
+template <bool QUAD, bool Q8 = false, bool CS = false>
 __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], const GemmEpilogue& ep, int M, int N,
                                               int zid, int bidx, int mrow, int ncol, float scale, char* lds_wave) {
   using namespace ringdp::dev;
@@ -416,10 +449,10 @@ __device__ __forceinline__ void gemm256_store(const dev::f32x4 (&acc)[8][4], con
   const EpiFlags fl = epi_flags(ep);
   // one specialised body per activation: the per-element code holds no branch on the epilogue kind
   switch (fl.act) {
-    case 1: gemm256_store_impl<QUAD, 1, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
-    case 2: gemm256_store_impl<QUAD, 2, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
-    case 3: gemm256_store_impl<QUAD, 3, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
-    default: gemm256_store_impl<QUAD, 0, Q8>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 1: gemm256_store_impl<QUAD, 1, Q8, CS>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 2: gemm256_store_impl<QUAD, 2, Q8, CS>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    case 3: gemm256_store_impl<QUAD, 3, Q8, CS>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
+    default: gemm256_store_impl<QUAD, 0, Q8, CS>(acc, ep, fl, M, N, bidx, mrow, ncol, scale, lds_wave); break;
   }
 }
 

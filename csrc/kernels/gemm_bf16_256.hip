@@ -217,6 +217,7 @@ __device__ __forceinline__ int half_row(int h, int j) {
   }
 }
 
+template <bool CS>  // CS: the epilogue also writes column-sum partials (ep.colsum_part)
 __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* __restrict__ A, int64_t lda,
                                                                int64_t a_bs, const uint8_t* __restrict__ B,
                                                                int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
@@ -336,8 +337,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256p_kernel(const uint8_t* _
 
   // ---------------- epilogue: acc[qm*4+mt][qn*2+nt] holds C[m][n..n+3],
   //   m = m0 + wr*128 + qm*64 + 16 mt + (lane & 15),  n = n0 + wc*64 + qn*32 + 16 nt + 4 (lane >> 4)
-  gemm256_store<true>(acc, ep, M, N, zid, b, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + 4 * (lane >> 4), 1.f,
-                      smem + wave * 16384);
+  gemm256_store<true, false, CS>(acc, ep, M, N, zid, b, m0 + wr * 128 + (lane & 15), n0 + wc * 64 + 4 * (lane >> 4),
+                                 1.f, smem + wave * 16384);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -638,6 +639,14 @@ int gemm_store_cache() {
 }
 void set_gemm_store_cache(int flavour) { g_store_cache = flavour; }
 
+static int bf16_group_m() {  // tile rows per group of the tile order (1 = row-major, rounds 1-3)
+  static const int g = [] {
+    const char* v = getenv("RINGDP_BF16_GROUP_M");
+    return v && *v ? atoi(v) : 4;
+  }();
+  return g;
+}
+
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int M, int N, int K,
                    const GemmEpilogue& ep, int splits, hipStream_t s) {
   // 16-B aligned rows, whole 64-element k-tiles (k-rows of a row-contiguous operand), whole 4-column
@@ -653,22 +662,34 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   kps = (kps + TKE - 1) / TKE * TKE;
   splits = (K + kps - 1) / kps;
   dim3 grid(tiles_m * tiles_n, batch * splits);
+  const bool wide_bf16 = N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 &&
+                         ep.c_bstride % 8 == 0;
+  if (ep.colsum_part) {  // column sums ride in the phased kernel's LDS-row bf16 stores only
+    if (A.row_contig || Bop.row_contig || !phased_mode() || batch != 1 || splits != 1 || !ep.out_bf16 || !wide_bf16 ||
+        ep.mode != GemmEpilogue::kStore)
+      return false;
+    GemmEpilogue e3 = ep;
+    e3.store_mode = 2;
+    e3.store_rot = gemm_wide_store_mode() < 10;
+    e3.store_cache = gemm_store_cache();
+    e3.sink = store_sink();
+    gemm_bf16_256p_kernel<true><<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
+                                                      static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2,
+                                                      e3, M, N, K * 2, tiles_m, tiles_n, splits, kps * 2,
+                                                      bf16_group_m());
+    return true;
+  }
   GemmEpilogue e2 = ep;
   e2.store_mode = gemm_wide_store_mode() % 10;
   e2.store_rot = gemm_wide_store_mode() < 10;
   e2.store_cache = gemm_store_cache();
   e2.sink = store_sink();
-  static const int group_m = [] {  // tile rows per group of the tile order (1 = row-major, rounds 1-3)
-    const char* v = getenv("RINGDP_BF16_GROUP_M");
-    return v && *v ? atoi(v) : 4;
-  }();
+  const int group_m = bf16_group_m();
   auto go = [&](auto kern) {
     kern<<<grid, 512, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
                               static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e2, M, N, K * 2,
                               tiles_m, tiles_n, splits, kps * 2, group_m);
   };
-  const bool wide_bf16 = N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 &&
-                         ep.c_bstride % 8 == 0;
   const bool off32 = (int64_t)M * A.ld * 2 + (int64_t)K * 2 < (1ll << 32) &&
                      (int64_t)N * Bop.ld * 2 + (int64_t)K * 2 < (1ll << 32);
   if (!A.row_contig && !Bop.row_contig && phased_mode() && persist_mode() && off32 &&
@@ -684,7 +705,7 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
     }
   }
   if (!A.row_contig && !Bop.row_contig) {
-    if (phased_mode()) go(gemm_bf16_256p_kernel);
+    if (phased_mode()) go(gemm_bf16_256p_kernel<false>);
     else go(gemm_bf16_256_kernel<false, false>);
   }
   else if (A.row_contig && Bop.row_contig) go(gemm_bf16_256_kernel<true, true>);

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(512, 1) void gemm_fp8_256_kernel(const uint8_t* __r
 }  // namespace
 
 int64_t gemm_fp8_q8_slots(int M, int N) { return (int64_t)((M + TM - 1) / TM) * ((N + TN - 1) / TN) * 8; }
-int64_t gemm_fp8_q8_colsum_rows(int M) { return (int64_t)((M + TM - 1) / TM) * 2; }
+int64_t gemm_fp8_colsum_part_rows(int M) { return (int64_t)((M + TM - 1) / TM) * 2; }
 
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);

@@ -269,14 +269,15 @@ struct GemmEpilogue {
   // e4m3 outputs instead of C (256x256 fp8 kernel only): the final value v (after bias / GELU / GELU backward,
   // rounded to bf16 as a stored C would be) is quantised with the delayed scale q8_amax[0] / 448 (clamped to
   // +-448) into q8 [M][N] and its transpose q8t [N][M]; q8_scale[0] <- that scale; q8_tmax[tile * 8 + wave]
-  // <- |v|max of each wave's 128 x 64 outputs (the next roll); q8_colsum (nullable) [tiles_m * 2][N] <- the
-  // column sums of v over each wave's 128 rows (a bias gradient)
+  // <- |v|max of each wave's 128 x 64 outputs (the next roll).
+  // colsum_part (nullable; the fp8 q8 path, and bf16 outputs of the 256x256 phased kernel) [tiles_m * 2][N] <- the
+  // column sums of the stored (bf16-rounded) values over each wave's 128 rows (a bias gradient)
   uint8_t* q8;
   uint8_t* q8t;
   const float* q8_amax;
   float* q8_scale;
   float* q8_tmax;
-  float* q8_colsum;
+  float* colsum_part;
 };
 struct ConvGeom {
   int N, H, W, C;   // input NHWC (C padded to a multiple of 8)
@@ -294,7 +295,7 @@ void gemm_fp8(const GemmOperand& A, const GemmOperand& B, int batch, int M, int 
 void set_bf16_tile_mode(int mode);  // 0 auto, 128 / 256 forced (A/B measurements)
 // tile-maximum slots and colsum partial rows of a gemm_fp8 launch with e4m3 outputs (ep.q8)
 int64_t gemm_fp8_q8_slots(int M, int N);
-int64_t gemm_fp8_q8_colsum_rows(int M);
+int64_t gemm_fp8_colsum_part_rows(int M);
 // 256x256 bf16 kernel for K-contiguous A and B (gemm_bf16_256.hip); false when the shape/layout is not
 // supported (the caller falls back to the 128x128 core).  K in elements.
 bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& B, int batch, int M, int N, int K,

@@ -55,7 +55,8 @@ kern::ConvGeom geom(const at::Tensor& x, int64_t K, int64_t R, int64_t S, int64_
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 bool a_row, bool b_row, int64_t batch, int64_t a_bstride, int64_t b_bstride, bool out_bf16,
                 const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& residual,
-                const c10::optional<at::Tensor>& preact, double alpha, const c10::optional<at::Tensor>& out) {
+                const c10::optional<at::Tensor>& preact, double alpha, const c10::optional<at::Tensor>& out,
+                const c10::optional<at::Tensor>& colsum) {
   bf16_gpu(a, "gemm A");
   bf16_gpu(b, "gemm B");
   // 16-B vectors run along K for K-contiguous operands and along the rows otherwise
@@ -99,6 +100,21 @@ at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, 
   if (M == 0 || N == 0) return c;
   kern::GemmOperand A{a.data_ptr(), lda, a_bstride, a_row};
   kern::GemmOperand B{b.data_ptr(), ldb, b_bstride, b_row};
+  if (colsum.has_value() && colsum->defined()) {  // out[n] = sum_m C[m][n] of the stored bf16 C (a bias gradient)
+    f32_gpu(*colsum, "gemm colsum");
+    RINGDP_CHECK(batch == 1 && out_bf16 && colsum->numel() == N && colsum->is_contiguous(),
+                 "gemm colsum: [N] floats, single bf16 GEMM");
+    at::Tensor part = at::empty({(M + 255) / 256 * 2, N}, a.options().dtype(at::kFloat));
+    e.colsum_part = part.data_ptr<float>();
+    if (kern::gemm_bf16_256(A, B, 1, (int)M, (int)N, (int)K, e, 1, stream_of(a))) {  // sums from the epilogue
+      kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), N, colsum->data_ptr<float>(), stream_of(a));
+      return c;
+    }
+    e.colsum_part = nullptr;  // shape the phased kernel does not take: a separate column-sum pass
+    kern::gemm_bf16(A, B, 1, (int)M, (int)N, (int)K, e, 1, stream_of(a));
+    colsum_f32(c.view({M, N}), *colsum);
+    return c;
+  }
   kern::gemm_bf16(A, B, (int)batch, (int)M, (int)N, (int)K, e, 1, stream_of(a));
   return c;
 }
@@ -845,8 +861,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_fp8_quant_out(
   if (colsum.has_value() && colsum->defined()) {
     f32_gpu(*colsum, "gemm colsum");
     RINGDP_CHECK(colsum->numel() == N && colsum->is_contiguous(), "gemm colsum: [N] floats");
-    part = at::empty({kern::gemm_fp8_q8_colsum_rows((int)M), N}, a.options().dtype(at::kFloat));
-    e.q8_colsum = part.data_ptr<float>();
+    part = at::empty({kern::gemm_fp8_colsum_part_rows((int)M), N}, a.options().dtype(at::kFloat));
+    e.colsum_part = part.data_ptr<float>();
   }
   e.q8 = static_cast<uint8_t*>(q.data_ptr());
   e.q8t = static_cast<uint8_t*>(qt.data_ptr());

@@ -11,7 +11,8 @@ namespace ops {
 at::Tensor gemm(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                 bool a_row, bool b_row, int64_t batch, int64_t a_bstride, int64_t b_bstride, bool out_bf16,
                 const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& residual,
-                const c10::optional<at::Tensor>& preact, double alpha, const c10::optional<at::Tensor>& out);
+                const c10::optional<at::Tensor>& preact, double alpha, const c10::optional<at::Tensor>& out,
+                const c10::optional<at::Tensor>& colsum = c10::nullopt);
 at::Tensor gemm_splitk_f32(const at::Tensor& a, const at::Tensor& b, int64_t M, int64_t N, int64_t K, int64_t lda,
                            int64_t ldb, bool a_row, bool b_row, int64_t splits, const at::Tensor& out);
 std::tuple<at::Tensor, at::Tensor> pack_conv_weight(const at::Tensor& w, int64_t cpad);

@@ -389,18 +389,20 @@ class MLPF(torch.autograd.Function):
         M, D = h.shape
         Hd = w1b.shape[0]
         dy = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
-        # d(fc1 output) = (dy W2) * GELU'(pre): the GELU backward rides in the GEMM epilogue (act 3)
+        db1 = grad_buffer(b1)
+        # d(fc1 output) = (dy W2) * GELU'(pre): the GELU backward rides in the GEMM epilogue (act 3), and so do
+        # the column sums of the stored dz1 (fc1's bias gradient: no separate pass over [tokens, 3072])
         if _DGRAD_WT:
             dz1 = C.gemm(dy, _bf16_t(w2b), M, Hd, D, D, D, False, False, 1, 0, 0, True, None, 3, None,
-                         pre).view(M, Hd)
+                         pre, colsum=db1).view(M, Hd)
         else:
-            dz1 = C.gemm(dy, w2b, M, Hd, D, D, Hd, False, True, 1, 0, 0, True, None, 3, None, pre).view(M, Hd)
+            dz1 = C.gemm(dy, w2b, M, Hd, D, D, Hd, False, True, 1, 0, 0, True, None, 3, None, pre,
+                         colsum=db1).view(M, Hd)
         dw2, db2 = grad_buffer(w2), grad_buffer(b2)
         C.gemm_splitk_f32(dy, a, D, Hd, M, D, Hd, True, True, _splits(M, D, Hd), dw2)
         C.colsum_f32(dy, db2)
-        dw1, db1 = grad_buffer(w1), grad_buffer(b1)
+        dw1 = grad_buffer(w1)
         C.gemm_splitk_f32(dz1, h, Hd, D, M, Hd, D, True, True, _splits(M, Hd, D), dw1)
-        C.colsum_f32(dz1, db1)
         dh = None
         if ctx.needs_input_grad[0]:
             if _DGRAD_WT:

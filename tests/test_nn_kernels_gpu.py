@@ -820,3 +820,26 @@ def test_attention_recompute_matches_stored_probabilities(T):
     torch.cuda.synchronize()
     err = (d_l.float() - d_p.float()).norm() / d_p.float().norm()
     assert err < 1e-2, err
+
+
+@pytest.mark.parametrize("M,N,K", [(1040, 768, 256), (4096, 3072, 768), (100, 40, 64)])
+def test_gemm_colsum_epilogue_matches_separate_pass(M, N, K):
+    """bf16 GEMM with the bias-gradient column sums from the 256x256 phased kernel's epilogue (act 3,
+    MLPF's fc1 gradient) against colsum_f32 over the stored output; (100, 40, 64) takes the fallback
+    (separate pass) path."""
+    import ringdp
+
+    C = ringdp._C
+    torch.manual_seed(0)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, K, device="cuda").bfloat16()
+    pre = torch.randn(M, N, device="cuda").bfloat16()
+    cs = torch.empty(N, device="cuda")
+    out = C.gemm(a, b, M, N, K, K, K, False, False, 1, 0, 0, True, None, 3, None, pre, colsum=cs).view(M, N)
+    ref_out = C.gemm(a, b, M, N, K, K, K, False, False, 1, 0, 0, True, None, 3, None, pre).view(M, N)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref_out)
+    ref = torch.empty(N, device="cuda")
+    C.colsum_f32(out, ref)
+    torch.testing.assert_close(cs, ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(cs, out.float().sum(0), rtol=1e-4, atol=1e-3)
