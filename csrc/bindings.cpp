@@ -530,7 +530,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "fused attention forward on the qkv projection rows [B*T, 3*H*64]: returns [P (or, recompute=True, the "
         "per-query log-sum-exp), out rows [B*T, H*64]]",
         py::arg("qkv"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("scale"), py::arg("recompute") = false);
-  m.def("attn_bwd_rows", &ops::attn_bwd_rows, "fused attention backward from output-grad rows -> dqkv rows");
+  m.def("attn_bwd_rows", &ops::attn_bwd_rows, "fused attention backward from output-grad rows -> dqkv rows",
+        py::arg("dout"), py::arg("qkv"), py::arg("p"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("scale"),
+        py::arg("colsum_part") = py::none());
+  m.def("rowsum_f32", &ops::rowsum_f32, "out[c] = sum_r part[r][c] (fp32, fixed order)");
   m.def("attn_bwd", &ops::attn_bwd,
         "fused attention backward -> dqkv rows [B*T, 3*H*Dh] (query-side dQ kernel + key-side dK/dV kernel)");
   m.def("attn_fwd", &ops::attn_fwd, "fused attention forward (head dim 64, Tp <= 256): returns [P, O]");

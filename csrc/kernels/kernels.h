@@ -461,8 +461,9 @@ bool attn_fwd_rows(const void* qkv, int B, int T, int H, int Tp, int Dh, float s
 // P-recompute variants: the forward stores the per-query log-sum-exp lse [B*H][Tp] instead of P
 bool attn_fwd_rows_lse(const void* qkv, int B, int T, int H, int Tp, int Dh, float scale, float* lse, void* out,
                        hipStream_t s);
+// colsum_part (nullable): [B][3*H*64] per-batch column sums of dqkv (the qkv bias gradient before the sum over B)
 bool attn_bwd_rows_lse(const void* dout_rows, const void* qkv, const float* lse, int B, int T, int H, int Tp, int Dh,
-                       float scale, float* dsum, void* dqkv, hipStream_t s);
+                       float scale, float* dsum, void* dqkv, hipStream_t s, float* colsum_part = nullptr);
 bool attn_bwd_rows(const void* dout_rows, const void* qkv, const void* p, int B, int T, int H, int Tp, int Dh,
                    float scale, float* dsum, void* dqkv, hipStream_t s);
 void softmax_bwd(const void* p, const float* dp, int64_t rows, int T, int Tp, float scale, void* ds, hipStream_t s);

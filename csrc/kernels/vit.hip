@@ -716,11 +716,38 @@ __global__ __launch_bounds__(256) void attn_bwd_ds_kernel(const bf16* __restrict
 // pass - dQ^T = K^T dS^T with the dS registers as the MFMA B operand and K^T read from LDS with
 // ds_read_b64_tr_b16 (the forward's O^T = V^T P^T trick).  dQ rows go straight into the dqkv gradient
 // rows [B*T][3*H*Dh]; D = rowsum(dP * P) per query is stored for the key-side kernel.
+// Column sums of a kernel's 64-wide output block (a bias gradient's partial): lane (g, i) holds sums for columns
+// 16 dt + 4g + e; reduced over the 16 lanes of each g, then over the 4 waves through `scratch` (>= 1 KiB of the
+// kernel's LDS, free once its main loop is done - the caller has passed a barrier), and stored as 64 floats.
+__device__ __forceinline__ void attn_colsum_store(float (&cs)[4][4], float* scratch, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float t = cs[dt][e];
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      t += __shfl_xor(t, 8, 64);
+      cs[dt][e] = t;
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) scratch[wave * 64 + 16 * dt + 4 * g + e] = cs[dt][e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64)
+    out[threadIdx.x] = (scratch[threadIdx.x] + scratch[64 + threadIdx.x]) + (scratch[128 + threadIdx.x] + scratch[192 + threadIdx.x]);
+}
+
 template <int NT, bool LSE>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k, AttnIn v,
                                                           const bf16* __restrict__ p, float scale, int T, int H,
                                                           float* __restrict__ dsum, AttnOut dq, AttnIn q,
-                                                          const float* __restrict__ lse) {
+                                                          const float* __restrict__ lse, float* __restrict__ cs_out) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Vs[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Ks[Tp * ATT_D];
@@ -734,6 +761,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k,
   __syncthreads();
   const int g = lane >> 4, qi = lane & 15;
   const int q4 = qi >> 2, p4 = qi & 3;
+  float csum[4][4] = {};  // cs_out: column sums of the stored dQ rows (the qkv bias gradient's q part)
   for (int qt = wave; qt < NT; qt += 4) {
     const int qrow = qt * 16 + qi;
     const bf16x8 of0 = dout.load8(bh, H, qrow, T, 8 * g);
@@ -804,10 +832,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnIn dout, AttnIn k,
     if (qrow < dq.rows) {
       bf16* drow = dq.row(bh, H, qrow) + 4 * g;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        *reinterpret_cast<bf16x4*>(drow + 16 * dt) =
-            bf16x4{(bf16)qt4[dt][0], (bf16)qt4[dt][1], (bf16)qt4[dt][2], (bf16)qt4[dt][3]};
+      for (int dt = 0; dt < 4; ++dt) {
+        const bf16x4 o = bf16x4{(bf16)qt4[dt][0], (bf16)qt4[dt][1], (bf16)qt4[dt][2], (bf16)qt4[dt][3]};
+        *reinterpret_cast<bf16x4*>(drow + 16 * dt) = o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) csum[dt][e] += (float)o[e];
+      }
     }
+  }
+  if (cs_out) {  // [B][3*H*64] partial row of batch bh / H, columns of head bh % H (q part)
+    __syncthreads();  // every wave is done with Vs
+    attn_colsum_store(csum, reinterpret_cast<float*>(Vs), cs_out + (int64_t)(bh / H) * 3 * H * ATT_D + (bh % H) * ATT_D);
   }
 }
 
@@ -821,7 +856,8 @@ template <int NT, bool LSE>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn q, AttnIn v,
                                                             const bf16* __restrict__ p, const float* __restrict__ dsum,
                                                             float scale, int T, int H, AttnOut dk, AttnOut dv,
-                                                            AttnIn k, const float* __restrict__ lse) {
+                                                            AttnIn k, const float* __restrict__ lse,
+                                                            float* __restrict__ cs_out) {
   constexpr int Tp = 16 * NT;
   __shared__ __attribute__((aligned(16))) bf16 Qs[Tp * ATT_D];
   __shared__ __attribute__((aligned(16))) bf16 Os[Tp * ATT_D];  // dO
@@ -838,6 +874,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
   // per-query D = rowsum(dP * P) and log-sum-exp: a lane's 4 queries 16 qp + 4g + r are one 16-B load each
   const float* db = dsum + (int64_t)bh * Tp;
   const float* lq = LSE ? lse + (int64_t)bh * Tp : nullptr;
+  float csk[4][4] = {}, csv[4][4] = {};  // cs_out: column sums of the stored dK / dV rows
   for (int kt = wave; kt < NT; kt += 4) {
     const int key = kt * 16 + ki;
     const bf16x8 vf0 = v.load8(bh, H, key, T, 8 * g);
@@ -901,27 +938,39 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(AttnIn dout, AttnIn 
       bf16* vrow = dv.row(bh, H, key) + 4 * g;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        *reinterpret_cast<bf16x4*>(krow + 16 * dt) =
-            bf16x4{(bf16)dka[dt][0], (bf16)dka[dt][1], (bf16)dka[dt][2], (bf16)dka[dt][3]};
-        *reinterpret_cast<bf16x4*>(vrow + 16 * dt) =
-            bf16x4{(bf16)dva[dt][0], (bf16)dva[dt][1], (bf16)dva[dt][2], (bf16)dva[dt][3]};
+        const bf16x4 ko = bf16x4{(bf16)dka[dt][0], (bf16)dka[dt][1], (bf16)dka[dt][2], (bf16)dka[dt][3]};
+        const bf16x4 vo = bf16x4{(bf16)dva[dt][0], (bf16)dva[dt][1], (bf16)dva[dt][2], (bf16)dva[dt][3]};
+        *reinterpret_cast<bf16x4*>(krow + 16 * dt) = ko;
+        *reinterpret_cast<bf16x4*>(vrow + 16 * dt) = vo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          csk[dt][e] += (float)ko[e];
+          csv[dt][e] += (float)vo[e];
+        }
       }
     }
+  }
+  if (cs_out) {  // k part, then v part of the [B][3*H*64] partial row
+    float* row = cs_out + (int64_t)(bh / H) * 3 * H * ATT_D + (bh % H) * ATT_D;
+    __syncthreads();  // every wave is done with Qs / Os
+    attn_colsum_store(csk, reinterpret_cast<float*>(Qs), row + H * ATT_D);
+    attn_colsum_store(csv, reinterpret_cast<float*>(Os), row + 2 * H * ATT_D);
   }
 }
 
 template <int NT>
 void attn_bwd_launch(AttnIn dout, AttnIn q, AttnIn k, AttnIn v, const void* p, int BH, int T, int H, float scale,
-                     float* dsum, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s, const float* lse = nullptr) {
+                     float* dsum, AttnOut dq, AttnOut dk, AttnOut dv, hipStream_t s, const float* lse = nullptr,
+                     float* cs = nullptr) {
   if (lse) {
-    attn_bwd_dq_kernel<NT, true><<<BH, 256, 0, s>>>(dout, k, v, nullptr, scale, T, H, dsum, dq, q, lse);
-    attn_bwd_dkdv_kernel<NT, true><<<BH, 256, 0, s>>>(dout, q, v, nullptr, dsum, scale, T, H, dk, dv, k, lse);
+    attn_bwd_dq_kernel<NT, true><<<BH, 256, 0, s>>>(dout, k, v, nullptr, scale, T, H, dsum, dq, q, lse, cs);
+    attn_bwd_dkdv_kernel<NT, true><<<BH, 256, 0, s>>>(dout, q, v, nullptr, dsum, scale, T, H, dk, dv, k, lse, cs);
     return;
   }
   attn_bwd_dq_kernel<NT, false><<<BH, 256, 0, s>>>(dout, k, v, static_cast<const bf16*>(p), scale, T, H, dsum, dq, q,
-                                                   nullptr);
+                                                   nullptr, cs);
   attn_bwd_dkdv_kernel<NT, false><<<BH, 256, 0, s>>>(dout, q, v, static_cast<const bf16*>(p), dsum, scale, T, H, dk, dv,
-                                                     k, nullptr);
+                                                     k, nullptr, cs);
 }
 
 template <int NT>
@@ -1037,13 +1086,13 @@ bool attn_bwd_rows(const void* dout_rows, const void* qkv, const void* p, int B,
 }
 
 bool attn_bwd_rows_lse(const void* dout_rows, const void* qkv, const float* lse, int B, int T, int H, int Tp, int Dh,
-                       float scale, float* dsum, void* dqkv, hipStream_t s) {
+                       float scale, float* dsum, void* dqkv, hipStream_t s, float* colsum_part) {
   if (Dh != ATT_D || Tp % 16 != 0 || Tp > 256 || Tp < 16 || T > Tp) return false;
   const int64_t w3 = (int64_t)3 * H * ATT_D, w1 = (int64_t)H * ATT_D;
   RINGDP_ATT_SWITCH((attn_bwd_launch<n>(token_rows(dout_rows, T, w1, 0), token_rows(qkv, T, w3, 0),
                                         token_rows(qkv, T, w3, w1), token_rows(qkv, T, w3, 2 * w1), nullptr, B * H, T,
                                         H, scale, dsum, token_rows_out(dqkv, T, w3, 0), token_rows_out(dqkv, T, w3, w1),
-                                        token_rows_out(dqkv, T, w3, 2 * w1), s, lse)))
+                                        token_rows_out(dqkv, T, w3, 2 * w1), s, lse, colsum_part)))
   return false;
 }
 

@@ -612,7 +612,7 @@ std::vector<at::Tensor> attn_fwd_rows(const at::Tensor& qkv, int64_t B, int64_t 
 }
 
 at::Tensor attn_bwd_rows(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& p, int64_t B, int64_t T,
-                         int64_t H, double scale) {
+                         int64_t H, double scale, const c10::optional<at::Tensor>& colsum_part) {
   bf16_gpu(dout, "attention output grad rows");
   bf16_gpu(qkv, "attention qkv rows");
   const int64_t Dh = qkv.size(1) / (3 * H), Tp = (T + 15) / 16 * 16;
@@ -623,12 +623,21 @@ at::Tensor attn_bwd_rows(const at::Tensor& dout, const at::Tensor& qkv, const at
                  "attn_bwd_rows: shape mismatch");
     at::Tensor dqkv = at::empty_like(qkv);
     at::Tensor dsum = at::empty({B * H, Tp}, qkv.options().dtype(at::kFloat));
+    float* csp = nullptr;
+    if (colsum_part.has_value() && colsum_part->defined()) {  // every entry is written by one workgroup
+      f32_gpu(*colsum_part, "attention dqkv column-sum partials");
+      RINGDP_CHECK(colsum_part->numel() == B * qkv.size(1) && colsum_part->is_contiguous(),
+                   "attn_bwd_rows: colsum_part must be [B, 3*H*Dh] floats");
+      csp = colsum_part->data_ptr<float>();
+    }
     const bool ok = kern::attn_bwd_rows_lse(dout.data_ptr(), qkv.data_ptr(), p.data_ptr<float>(), (int)B, (int)T, (int)H,
                                             (int)Tp, (int)Dh, (float)scale, dsum.data_ptr<float>(), dqkv.data_ptr(),
-                                            stream_of(qkv));
+                                            stream_of(qkv), csp);
     RINGDP_CHECK(ok, "attn_bwd_rows: unsupported shape (needs head dim 64, T <= 256)");
     return dqkv;
   }
+  RINGDP_CHECK(!(colsum_part.has_value() && colsum_part->defined()),
+               "attn_bwd_rows: column sums need the recompute (log-sum-exp) path");
   bf16_gpu(p, "attention probs");
   RINGDP_CHECK(qkv.dim() == 2 && qkv.size(0) == B * T && dout.dim() == 2 && dout.size(0) == B * T &&
                    dout.size(1) == H * Dh && p.dim() == 3 && p.size(0) == B * H && p.size(1) == Tp && p.size(2) == Tp,
@@ -769,6 +778,15 @@ void fp8_roll_many(const at::Tensor& hists, const at::Tensor& ns) {
                "fp8_roll_many: expected int64 pointer and int32 count vectors of one length on the GPU");
   kern::fp8_roll_many(reinterpret_cast<float* const*>(hists.data_ptr<int64_t>()), ns.data_ptr<int>(),
                       (int)hists.numel(), stream_of(hists));
+}
+
+void rowsum_f32(const at::Tensor& part, at::Tensor out) {
+  f32_gpu(part, "rowsum input");
+  f32_gpu(out, "rowsum output");
+  RINGDP_CHECK(part.dim() == 2 && part.is_contiguous() && part.size(1) % 4 == 0 && out.numel() == part.size(1) &&
+                   out.is_contiguous(),
+               "rowsum_f32: expected contiguous fp32 [rows, cols % 4 == 0] and fp32 [cols]");
+  kern::rowsum_f32(part.data_ptr<float>(), (int)part.size(0), part.size(1), out.data_ptr<float>(), stream_of(part));
 }
 
 void colsum_f32(const at::Tensor& x, at::Tensor out) {

@@ -57,7 +57,8 @@ at::Tensor attn_bwd(const at::Tensor& dout, const at::Tensor& q, const at::Tenso
 std::vector<at::Tensor> attn_fwd_rows(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H, double scale,
                                       bool recompute = false);
 at::Tensor attn_bwd_rows(const at::Tensor& dout, const at::Tensor& qkv, const at::Tensor& p, int64_t B, int64_t T,
-                         int64_t H, double scale);
+                         int64_t H, double scale,
+                         const c10::optional<at::Tensor>& colsum_part = c10::nullopt);
 std::vector<at::Tensor> attn_fwd(const at::Tensor& q, const at::Tensor& k, const at::Tensor& v, int64_t T,
                                  double scale);
 at::Tensor softmax_bwd(const at::Tensor& p, const at::Tensor& dp, int64_t T, double scale);
@@ -86,6 +87,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_fp8_quant_out(
     int64_t N, int64_t K, const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& preact,
     at::Tensor hist, const c10::optional<at::Tensor>& colsum);
 void colsum_f32(const at::Tensor& x, at::Tensor out);
+void rowsum_f32(const at::Tensor& part, at::Tensor out);  // out[c] = sum_r part[r][c] (fixed order)
 at::Tensor gemm_fp8(const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b,
                     int64_t M, int64_t N, int64_t K, bool out_bf16, const c10::optional<at::Tensor>& bias, int64_t act,
                     const c10::optional<at::Tensor>& residual, const c10::optional<at::Tensor>& preact);

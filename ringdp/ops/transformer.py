@@ -152,7 +152,10 @@ class LinearF(torch.autograd.Function):
                 dw.copy_(full_w[:n_out])
         if b is not None and ctx.needs_input_grad[2]:
             db = grad_buffer(b)
-            if N == n_out:
+            part = getattr(dy, "_ringdp_colsum_part", None)  # per-batch column sums from the attention backward
+            if part is not None and act != 2 and N == n_out and part.shape[1] == N:
+                C.rowsum_f32(part, db)
+            elif N == n_out:
                 C.colsum_f32(dz, db)  # bias gradient = column sums of dz (one read of dz)
             else:
                 full = torch.empty(N, device=dy.device, dtype=torch.float32)
@@ -495,6 +498,13 @@ class AttentionF(torch.autograd.Function):
         if ctx.rows:
             qkv, p = ctx.saved_tensors
             B, T, H, Tp, scale = ctx.cfg
+            if p.dtype == torch.float32 and not _FP8["on"]:
+                # the kernels also sum their dq / dk / dv rows per batch: the qkv projection's bias gradient is
+                # then one [B, 3D] -> [3D] reduction in LinearF's backward instead of a pass over dqkv
+                part = torch.empty(B, qkv.shape[1], device=qkv.device, dtype=torch.float32)
+                dqkv = C.attn_bwd_rows(dout.contiguous(), qkv, p, B, T, H, scale, part)
+                dqkv._ringdp_colsum_part = part
+                return dqkv, None, None, None
             return C.attn_bwd_rows(dout.contiguous(), qkv, p, B, T, H, scale), None, None, None
         q, k, v, p = ctx.saved_tensors
         B, T, H, Tp, scale = ctx.cfg

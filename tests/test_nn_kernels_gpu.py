@@ -843,3 +843,26 @@ def test_gemm_colsum_epilogue_matches_separate_pass(M, N, K):
     C.colsum_f32(out, ref)
     torch.testing.assert_close(cs, ref, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(cs, out.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_attention_backward_column_sums_match_dqkv():
+    """The per-batch dq / dk / dv column sums written by the attention backward kernels (the qkv bias
+    gradient's partials) against the column sums of the dqkv rows they stored."""
+    import ringdp
+
+    C = ringdp._C
+    torch.manual_seed(0)
+    B, T, H = 3, 197, 12
+    qkv = (torch.randn(B * T, 3 * H * 64, device="cuda") * 0.5).bfloat16()
+    dout = torch.randn(B * T, H * 64, device="cuda").bfloat16()
+    lse, _ = C.attn_fwd_rows(qkv, B, T, H, 0.125, True)
+    part = torch.full((B, 3 * H * 64), float("nan"), device="cuda")
+    dqkv = C.attn_bwd_rows(dout, qkv, lse, B, T, H, 0.125, part)
+    ref = C.attn_bwd_rows(dout, qkv, lse, B, T, H, 0.125)
+    torch.cuda.synchronize()
+    assert torch.equal(dqkv, ref)
+    assert torch.isfinite(part).all()  # every entry written
+    torch.testing.assert_close(part, dqkv.float().view(B, T, -1).sum(1), rtol=1e-4, atol=1e-3)
+    out = torch.empty(3 * H * 64, device="cuda")
+    C.rowsum_f32(part, out)
+    torch.testing.assert_close(out, dqkv.float().sum(0), rtol=1e-4, atol=2e-3)
