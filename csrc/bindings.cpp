@@ -550,6 +550,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_roll_many", &ops::fp8_roll_many, "delayed-scaling roll of many fp8 sites in one launch");
   m.def("gemm_fp8_q8_slots", &ops::gemm_fp8_q8_slots);
   m.def("fp8_roll", &ops::fp8_roll, "delayed-scaling roll of one fp8 site");
+  m.def("fp8_quantize_weights", &ops::fp8_quantize_weights,
+        "delayed-scaling e4m3 copies (q, q^T, scale) of many fp32 weights in one launch");
   m.def("gemm_fp8_quant_out", &ops::gemm_fp8_quant_out, py::arg("a"), py::arg("b"), py::arg("scale_a"),
         py::arg("scale_b"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("bias") = py::none(), py::arg("act") = 0,
         py::arg("preact") = py::none(), py::arg("hist"), py::arg("colsum") = py::none());

@@ -87,19 +87,28 @@ __global__ __launch_bounds__(256) void quant_kernel(const bf16* __restrict__ x, 
 // gpre (nullable): the tensor quantised is x * GELU'(gpre) - the GELU backward of an fp8 linear fused into
 // the quantisation of its output gradient (the bf16 dz never reaches memory)
 constexpr int kQT_R = 128, kQT_C = 64, kQT_RS = 68;  // 17-dword rows
-__global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
-                                                      const float* __restrict__ amax, uint8_t* __restrict__ out,
-                                                      float* __restrict__ scale, uint8_t* __restrict__ out_rm,
-                                                      unsigned* __restrict__ amax_next, float* __restrict__ colsum,
-                                                      const bf16* __restrict__ gpre) {
+
+__device__ __forceinline__ bf16x8 load_bf16x8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ bf16x8 load_bf16x8(const float* p) {  // fp32 master weights: the bf16 copy's values
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  return bf16x8{(bf16)a.x, (bf16)a.y, (bf16)a.z, (bf16)a.w, (bf16)b.x, (bf16)b.y, (bf16)b.z, (bf16)b.w};
+}
+
+// One 128 x 64 tile (bx, by) of the quantise(+transpose) pass; X = bf16 or fp32 (rounded to bf16 on load).
+template <typename X>
+__device__ __forceinline__ void quant_t_tile(const X* __restrict__ x, int64_t rows, int64_t cols,
+                                             const float* __restrict__ amax, uint8_t* __restrict__ out,
+                                             float* __restrict__ scale, uint8_t* __restrict__ out_rm,
+                                             unsigned* __restrict__ amax_next, float* __restrict__ colsum,
+                                             const bf16* __restrict__ gpre, int bx, int by, int gx) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[kQT_R * kQT_RS];
   __shared__ float red[4];
   __shared__ float csum[4][64];
   const float inv = 1.f / qscale(amax);
   const float lim = amax_next ? kE4M3Max : INFINITY;
   float bmax = 0.f;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) scale[0] = qscale(amax);
-  const int64_t r0 = (int64_t)blockIdx.y * kQT_R, c0 = (int64_t)blockIdx.x * kQT_C;
+  if (bx == 0 && by == 0 && threadIdx.x == 0) scale[0] = qscale(amax);
+  const int64_t r0 = (int64_t)by * kQT_R, c0 = (int64_t)bx * kQT_C;
   const int t = threadIdx.x, cv = t & 7, rr = t >> 3;
   const int64_t gc = c0 + cv * 8;
   bf16x8 v[4], pz[4];
@@ -109,7 +118,7 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
     v[p] = zero_bf16x8();
     pz[p] = zero_bf16x8();
     if (gr < rows && gc < cols) {
-      v[p] = *reinterpret_cast<const bf16x8*>(x + gr * cols + gc);
+      v[p] = load_bf16x8(x + gr * cols + gc);
       if (gpre) pz[p] = *reinterpret_cast<const bf16x8*>(gpre + gr * cols + gc);
     }
   }
@@ -179,15 +188,41 @@ __global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x
     }
     __syncthreads();
     if (t < 64 && c0 + t < cols)
-      colsum[(int64_t)blockIdx.y * cols + c0 + t] = (csum[0][t] + csum[1][t]) + (csum[2][t] + csum[3][t]);
+      colsum[(int64_t)by * cols + c0 + t] = (csum[0][t] + csum[1][t]) + (csum[2][t] + csum[3][t]);
   }
   if (amax_next) {  // this tile's |x|max -> its own slot (thousands of same-address atomics serialise)
     bmax = wave_max(bmax);
     if ((t & 63) == 0) red[t >> 6] = bmax;
     __syncthreads();
     if (t == 0)
-      amax_next[blockIdx.y * gridDim.x + blockIdx.x] = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+      amax_next[by * gx + bx] = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
   }
+}
+
+__global__ __launch_bounds__(256) void quant_t_kernel(const bf16* __restrict__ x, int64_t rows, int64_t cols,
+                                                      const float* __restrict__ amax, uint8_t* __restrict__ out,
+                                                      float* __restrict__ scale, uint8_t* __restrict__ out_rm,
+                                                      unsigned* __restrict__ amax_next, float* __restrict__ colsum,
+                                                      const bf16* __restrict__ gpre) {
+  quant_t_tile(x, rows, cols, amax, out, scale, out_rm, amax_next, colsum, gpre, blockIdx.x, blockIdx.y, gridDim.x);
+}
+
+// Many fp32 matrices (a model's weights, delayed scaling) in one launch: the table is a kernel argument copied
+// to LDS with compile-time indices (run-time indexing of the argument goes to scratch); block b belongs to
+// the last entry whose first tile <= b.
+__global__ __launch_bounds__(256) void quant_t_multi_kernel(QuantTTable tab) {
+  __shared__ QuantTEntry se[kQuantTMax];
+#pragma unroll
+  for (int i = 0; i < kQuantTMax; ++i)
+    if (threadIdx.x == i && i < tab.n) se[i] = tab.e[i];
+  __syncthreads();
+  int i = 0;
+  while (i + 1 < tab.n && (int)blockIdx.x >= se[i + 1].tile0) ++i;
+  const QuantTEntry& e = se[i];
+  const int gx = (int)((e.cols + kQT_C - 1) / kQT_C);
+  const int l = (int)blockIdx.x - e.tile0, by = l / gx, bx = l - by * gx;
+  quant_t_tile(e.src, e.rows, e.cols, e.hist, e.qt, e.scale, e.q, reinterpret_cast<unsigned*>(e.hist + 1), nullptr,
+               nullptr, bx, by, gx);
 }
 
 // Delayed-scaling roll: hist[0] (the amax the next quantisation scales by) <- max of the per-tile maxima
@@ -339,6 +374,10 @@ void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist
   quant_t_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), rows, cols, hist, static_cast<uint8_t*>(out_t),
                                       scale, static_cast<uint8_t*>(out_rowmajor), reinterpret_cast<unsigned*>(hist + 1),
                                       colsum_part, static_cast<const bf16*>(gelu_pre));
+}
+
+void fp8_quantize_multi(const QuantTTable& t, hipStream_t s) {
+  if (t.n > 0 && t.total_tiles > 0) quant_t_multi_kernel<<<t.total_tiles, 256, 0, s>>>(t);
 }
 
 void fp8_roll(float* hist, int n, hipStream_t s) { amax_roll_kernel<<<1, 1024, 0, s>>>(hist, n); }

@@ -328,7 +328,25 @@ void fp8_quantize_delayed(const void* x, int64_t rows, int64_t cols, float* hist
 // the rolls of many sites in one launch (one workgroup per site): hist_i[0] <- max hist_i[1 .. 1+n_i) when
 // that is > 0.  A training step rolls every site once before its first quantisation (roll = false above)
 void fp8_roll_many(float* const* hists, const int* ns, int count, hipStream_t s);
-void fp8_roll(float* hist, int n, hipStream_t s);  // one site: hist[0] <- max hist[1 .. 1+n) when > 0
+void fp8_roll(float* hist, int n, hipStream_t s);
+// delayed-scaling quantise + transpose of many fp32 matrices (a model's weights) in one launch: entry i covers
+// blocks [tile0, tile0 + its 128 x 64 tile count); hist as fp8_quantize_delayed's (already rolled)
+struct QuantTEntry {
+  const float* src;  // [rows][cols] fp32 (quantised from its bf16 rounding)
+  int64_t rows, cols;
+  float* hist;
+  uint8_t* q;   // [rows][cols] e4m3
+  uint8_t* qt;  // [cols][rows] e4m3
+  float* scale;
+  int tile0;
+};
+constexpr int kQuantTMax = 60;  // 60 x 64 B + header < the 4 KiB kernel-argument limit
+struct QuantTTable {
+  int n;
+  int total_tiles;
+  QuantTEntry e[kQuantTMax];
+};
+void fp8_quantize_multi(const QuantTTable& t, hipStream_t s);  // one site: hist[0] <- max hist[1 .. 1+n) when > 0
 // column sums of a bf16 [rows][cols] matrix as colsum_parts(rows) fp32 partial rows (sum them with splitk_sum;
 // fp8_quantize_delayed's colsum_part has one partial row per 64-row tile instead)
 int colsum_parts(int64_t rows);

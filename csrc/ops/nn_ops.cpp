@@ -840,6 +840,44 @@ void fp8_roll(at::Tensor hist) {
   kern::fp8_roll(hist.data_ptr<float>(), (int)(hist.numel() - 1), stream_of(hist));
 }
 
+std::vector<at::Tensor> fp8_quantize_weights(const std::vector<at::Tensor>& ws, const std::vector<at::Tensor>& hists) {
+  RINGDP_CHECK(ws.size() == hists.size() && !ws.empty(), "fp8_quantize_weights: one history per weight");
+  std::vector<at::Tensor> out;
+  kern::QuantTTable t{};
+  auto flush = [&](hipStream_t st) {
+    if (t.n > 0) kern::fp8_quantize_multi(t, st);
+    t = kern::QuantTTable{};
+  };
+  for (size_t i = 0; i < ws.size(); ++i) {
+    const at::Tensor& w = ws[i];
+    const at::Tensor& h = hists[i];
+    f32_gpu(w, "fp8 weight");
+    f32_gpu(h, "fp8 amax history");
+    RINGDP_CHECK(w.dim() == 2 && w.is_contiguous() && w.size(0) % 16 == 0 && w.size(1) % 16 == 0,
+                 "fp8_quantize_weights: contiguous fp32 [rows, cols] with dims % 16 == 0");
+    const int64_t R = w.size(0), Cc = w.size(1);
+    RINGDP_CHECK(h.is_contiguous() && h.numel() == 1 + fp8_delayed_slots(R, Cc), "fp8_quantize_weights: history size");
+    at::Tensor q = at::empty({R, Cc}, w.options().dtype(at::kByte)), qt = at::empty({Cc, R}, w.options().dtype(at::kByte));
+    at::Tensor scale = at::empty({1}, w.options());
+    out.push_back(q);
+    out.push_back(qt);
+    out.push_back(scale);
+    if (t.n == kern::kQuantTMax) flush(stream_of(w));
+    kern::QuantTEntry& e = t.e[t.n++];
+    e.src = w.data_ptr<float>();
+    e.rows = R;
+    e.cols = Cc;
+    e.hist = h.data_ptr<float>();
+    e.q = static_cast<uint8_t*>(q.data_ptr());
+    e.qt = static_cast<uint8_t*>(qt.data_ptr());
+    e.scale = scale.data_ptr<float>();
+    e.tile0 = t.total_tiles;
+    t.total_tiles += (int)kern::fp8_quant_tiles(R, Cc);
+  }
+  flush(stream_of(ws[0]));
+  return out;
+}
+
 int64_t gemm_fp8_q8_slots(int64_t M, int64_t N) { return kern::gemm_fp8_q8_slots((int)M, (int)N); }
 
 std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_fp8_quant_out(

@@ -82,6 +82,8 @@ void fp8_roll_many(const at::Tensor& hists, const at::Tensor& ns);
 // preact, act 3 reads it (GELU backward); colsum (nullable) <- column sums of the quantised-from values
 int64_t gemm_fp8_q8_slots(int64_t M, int64_t N);
 void fp8_roll(at::Tensor hist);
+// every weight's delayed-scaling e4m3 copy (row-major, transposed, scale) in one launch: returns [q, qt, scale] * n
+std::vector<at::Tensor> fp8_quantize_weights(const std::vector<at::Tensor>& ws, const std::vector<at::Tensor>& hists);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> gemm_fp8_quant_out(
     const at::Tensor& a, const at::Tensor& b, const at::Tensor& scale_a, const at::Tensor& scale_b, int64_t M,
     int64_t N, int64_t K, const c10::optional<at::Tensor>& bias, int64_t act, const c10::optional<at::Tensor>& preact,

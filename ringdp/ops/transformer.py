@@ -51,7 +51,10 @@ def cast_weights(ws) -> None:
     progress (see _bf16 / _bf16_t): the backward's data-gradient GEMMs take W^T K-contiguous."""
     ws = [w for w in ws if w.is_cuda and w.dtype == torch.float32 and w.dim() == 2]
     _BF16_WEIGHTS_T.clear()  # the previous step's backward has taken what it needed
-    if ws and _FP8["on"]:  # fp8 linears quantise W / W^T themselves: plain casts only
+    if ws and _FP8["on"]:
+        if _FP8_WQ_BATCH and _FP8_DELAYED and _fp8_weights_batched(ws):
+            return
+        # fp8 linears quantise W / W^T themselves: plain casts only
         for w, b in zip(ws, C.cast_bf16_multi([w.detach().contiguous() for w in ws])):
             _BF16_WEIGHTS[id(w)] = b
         return
@@ -65,6 +68,41 @@ def cast_weights(ws) -> None:
 
 def clear_weights() -> None:
     _BF16_WEIGHTS.clear()
+    _FP8_WEIGHTS.clear()
+
+
+# fp8: every linear weight's e4m3 copies (q, q^T, scale) from one launch per forward (cast_weights), instead of a
+# bf16 cast launch plus one quantisation launch per weight (RINGDP_FP8_WQ_BATCH=0: per weight)
+_FP8_WQ_BATCH = os.environ.get("RINGDP_FP8_WQ_BATCH", "0") == "1"
+_FP8_WEIGHTS: dict = {}  # {id(weight): (weight, (q, qt, scale))} for the forward in progress
+
+
+def _fp8_weights_batched(ws) -> bool:
+    """Quantise all of ``ws`` (slot 2 delayed-scaling sites) in one launch; False (nothing done) while any
+    site still needs its first, exact-amax quantisation (the per-weight path does that)."""
+    for w in ws:
+        sites = getattr(w, "_ringdp_fp8", None)
+        hist = sites[2] if sites is not None else None
+        if hist is None or hist.numel() != 1 + C.fp8_delayed_slots(w.shape[0], w.shape[1]):
+            return False
+    hists = []
+    for w in ws:
+        hist, init, roll = _site(w, 2, 1 + C.fp8_delayed_slots(w.shape[0], w.shape[1]), w.device)
+        if roll:
+            C.fp8_roll(hist)
+        hists.append(hist)
+    flat = C.fp8_quantize_weights([w.detach().contiguous() for w in ws], hists)
+    for i, w in enumerate(ws):
+        _FP8_WEIGHTS[id(w)] = (w, tuple(flat[3 * i:3 * i + 3]))
+    return True
+
+
+def _quant_weight(w: torch.Tensor):
+    """(q, q^T, scale) of a linear weight: from the forward's batched launch, or quantised here."""
+    e = _FP8_WEIGHTS.get(id(w))
+    if e is not None and e[0] is w:
+        return e[1]
+    return _quant_act(_bf16(w), w, 2)
 
 
 def _bf16_t(wb: torch.Tensor) -> torch.Tensor:
@@ -278,7 +316,7 @@ class MLPF8(torch.autograd.Function):
         M, D = h.shape
         Hd = w1.shape[0]
         hq, hqt, sh = _quant_act(h, w1, 0)
-        w1q, w1qt, sw1 = _quant_act(_bf16(w1), w1, 2)
+        w1q, w1qt, sw1 = _quant_weight(w1)
         pre = torch.empty(M, Hd, device=h.device, dtype=torch.bfloat16)
         hist3, init3 = _epilogue_site(w2, 3, M, Hd, h.device, 0)
         if init3:
@@ -287,7 +325,7 @@ class MLPF8(torch.autograd.Function):
             hist3[:1].copy_(w2._ringdp_fp8[0][:1])
         else:
             aq, aqt, sa = C.gemm_fp8_quant_out(hq, w1q, sh, sw1, M, Hd, D, b1, 2, pre, hist3)
-        w2q, w2qt, sw2 = _quant_act(_bf16(w2), w2, 2)
+        w2q, w2qt, sw2 = _quant_weight(w2)
         y = C.gemm_fp8(aq, w2q, sa, sw2, M, D, Hd, True, b2, 0, residual)
         ctx.save_for_backward(hqt, sh, w1qt, sw1, pre, aqt, sa, w2qt, sw2)
         ctx.params = (w1, b1, w2, b2)
@@ -328,9 +366,8 @@ class MLPF8(torch.autograd.Function):
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
     M, K = x.shape
     N = w.shape[0]
-    wb = _bf16(w)
     xq, xtq, sx = _quant_act(x, w, 0)    # row-major for this GEMM, transposed for the weight grad
-    wq, wtq, sw = _quant_act(wb, w, 2)   # ... and for the data grad
+    wq, wtq, sw = _quant_weight(w)       # ... and for the data grad
     pre = torch.empty(M, N, device=x.device, dtype=torch.bfloat16) if act == 2 else None
     y = C.gemm_fp8(xq, wq, sx, sw, M, N, K, not out_f32, b, act, residual, pre)
     ctx.fp8 = True

@@ -866,3 +866,41 @@ def test_attention_backward_column_sums_match_dqkv():
     out = torch.empty(3 * H * 64, device="cuda")
     C.rowsum_f32(part, out)
     torch.testing.assert_close(out, dqkv.float().sum(0), rtol=1e-4, atol=2e-3)
+
+
+def test_fp8_batched_weight_quantisation_matches_per_weight():
+    """Every linear weight quantised in one launch per forward (fp8_quantize_weights) trains bit-identically
+    to one bf16 cast plus one quantisation launch per weight."""
+    import copy
+
+    import ringdp.ops.transformer as tr
+    from ringdp.models import vit_tiny
+    from ringdp.optim import SGD
+
+    torch.manual_seed(0)
+    m = vit_tiny(num_classes=10).cuda()
+    g = torch.Generator(device="cuda").manual_seed(4)
+    xs = [torch.randn(16, 3, 32, 32, device="cuda", generator=g) for _ in range(4)]
+    ys = [torch.randint(0, 10, (16,), device="cuda", generator=g) for _ in range(4)]
+    res = []
+    try:
+        tr.set_fp8(True)
+        for batched in (False, True):
+            tr._FP8_WQ_BATCH = batched
+            tr._ROLLS.clear()
+            mm = copy.deepcopy(m)
+            opt = SGD(mm.parameters(), lr=0.05, momentum=0.9)
+            losses = []
+            for x, y in zip(xs, ys):
+                loss = F.cross_entropy(mm(x), y)
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                opt.step()
+                losses.append(loss.detach())
+            res.append((torch.stack(losses), [p.detach().clone() for p in mm.parameters()]))
+    finally:
+        tr.set_fp8(False)
+        tr._FP8_WQ_BATCH = True
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
