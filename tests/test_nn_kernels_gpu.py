@@ -883,6 +883,7 @@ def test_fp8_batched_weight_quantisation_matches_per_weight():
     xs = [torch.randn(16, 3, 32, 32, device="cuda", generator=g) for _ in range(4)]
     ys = [torch.randint(0, 10, (16,), device="cuda", generator=g) for _ in range(4)]
     res = []
+    saved = tr._FP8_WQ_BATCH
     try:
         tr.set_fp8(True)
         for batched in (False, True):
@@ -900,7 +901,7 @@ def test_fp8_batched_weight_quantisation_matches_per_weight():
             res.append((torch.stack(losses), [p.detach().clone() for p in mm.parameters()]))
     finally:
         tr.set_fp8(False)
-        tr._FP8_WQ_BATCH = True
+        tr._FP8_WQ_BATCH = saved
     assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
