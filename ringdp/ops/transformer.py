@@ -73,7 +73,7 @@ def clear_weights() -> None:
 
 # fp8: every linear weight's e4m3 copies (q, q^T, scale) from one launch per forward (cast_weights), instead of a
 # bf16 cast launch plus one quantisation launch per weight (RINGDP_FP8_WQ_BATCH=0: per weight)
-_FP8_WQ_BATCH = os.environ.get("RINGDP_FP8_WQ_BATCH", "0") == "1"
+_FP8_WQ_BATCH = os.environ.get("RINGDP_FP8_WQ_BATCH", "1") == "1"
 _FP8_WEIGHTS: dict = {}  # {id(weight): (weight, (q, qt, scale))} for the forward in progress
 
 
