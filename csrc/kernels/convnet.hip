@@ -2400,7 +2400,15 @@ static void c12_split(int B, int& nd, int& ws) {
 
 static int conv1_wslices(int B) { return clampi(cdiv(B, 4), 1, 3 * num_cus()); }
 
-int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, fc_imgs(B)) * FC_SLAB; }
+// images per fc1-backward workgroup (RINGDP_CN_FC_IMGS overrides the table for A/B runs)
+static int fc_imgs_host(int B) {
+  static const int forced = [] {
+    const char* v = getenv("RINGDP_CN_FC_IMGS");
+    return v && *v ? atoi(v) : 0;
+  }();
+  return forced > 0 ? std::min(forced, 128) : fc_imgs(B);  // <= 128: the CE logits-gradient LDS block
+}
+int64_t cn_fc_slab_floats(int B, bool) { return (int64_t)cdiv(B, fc_imgs_host(B)) * FC_SLAB; }
 int64_t cn_conv3_slab_floats(int B, bool dgrad) {
   int nd, ws;
   c3_split(B, dgrad, nd, ws);
@@ -2425,7 +2433,7 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
   (void)wfc;  // the data gradient uses the packed bf16 copy, like every other dgrad
   int nd, ws;
   c3_split(B, dz2 != nullptr, nd, ws);
-  const int fs = cdiv(B, fc_imgs(B));
+  const int fs = cdiv(B, fc_imgs_host(B));
   const bf16* a3b = static_cast<const bf16*>(a3);
   const bf16* pk = static_cast<const bf16*>(packed);
   const CeFuse cef = ce ? *ce : CeFuse{};
@@ -2433,12 +2441,12 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
     const C3Src src{nullptr, a3b, pk, ce ? nullptr : dl, cef};
     conv3_bwd_kernel<true><<<fs + nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
                                                              static_cast<bf16*>(dz2), B, c3_slabs, ws, nd,
-                                                             c3_dgrad_images(B, nd), fs, fc_slabs, fc_imgs(B));
+                                                             c3_dgrad_images(B, nd), fs, fc_slabs, fc_imgs_host(B));
   } else {
     if (ce)
-      fc_bwd_kernel<true><<<fs, 256, 0, s>>>(a3b, pk, nullptr, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), cef);
+      fc_bwd_kernel<true><<<fs, 256, 0, s>>>(a3b, pk, nullptr, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs_host(B), cef);
     else
-      fc_bwd_kernel<false><<<fs, 256, 0, s>>>(a3b, pk, dl, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs(B), cef);
+      fc_bwd_kernel<false><<<fs, 256, 0, s>>>(a3b, pk, dl, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs_host(B), cef);
     const C3Src src{static_cast<const bf16*>(da3m), a3b, pk, dl, cef};
     conv3_bwd_kernel<false><<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
                                                          static_cast<bf16*>(dz2), B, c3_slabs, ws, nd,
