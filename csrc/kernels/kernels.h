@@ -453,8 +453,11 @@ void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s);
 void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, void* y,
                    float* stats, hipStream_t s);
 int layernorm_bwd_scratch_floats(int64_t rows, int D);
+// cs_part (nullable): [layernorm_bwd_blocks(rows)][D] per-block column sums of dx (the bias gradient of the
+// linear whose output gradient dx is)
+int layernorm_bwd_blocks(int64_t rows);
 void layernorm_bwd(const void* dy, const void* x, const float* stats, const float* w, const void* dres, int64_t rows,
-                   int D, void* dx, float* scratch, float* dw, float* db, hipStream_t s);
+                   int D, void* dx, float* scratch, float* dw, float* db, hipStream_t s, float* cs_part = nullptr);
 void qkv_split(const void* qkv, int B, int T, int H, int Dh, int Tp, void* q, void* k, void* v, hipStream_t s);
 void qkv_merge(const void* dq, const void* dk, const void* dv, int B, int T, int H, int Dh, int Tp, void* dqkv,
                hipStream_t s);

@@ -88,14 +88,15 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restri
                                                             const float* __restrict__ stats,
                                                             const float* __restrict__ w, const bf16* __restrict__ dres,
                                                             int64_t rows, int D, int rows_per_block,
-                                                            bf16* __restrict__ dx, float* __restrict__ part) {
+                                                            bf16* __restrict__ dx, float* __restrict__ part,
+                                                            float* __restrict__ cs_part) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = D / 8;
-  float dw[VPL][8], db[VPL][8];
+  float dw[VPL][8], db[VPL][8], cs[VPL][8];  // cs (cs_part != null): column sums of the stored dx
 #pragma unroll
   for (int i = 0; i < VPL; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dw[i][j] = db[i][j] = 0.f;
+    for (int j = 0; j < 8; ++j) dw[i][j] = db[i][j] = cs[i][j] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
   const int64_t r1 = std::min<int64_t>(rows, r0 + rows_per_block);
   for (int64_t row = r0 + wave; row < r1; row += 4) {
@@ -132,24 +133,28 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restri
         if (dres) rv = reinterpret_cast<const bf16x8*>(dres + row * D)[vi];
         bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (bf16)(rstd * (gw[i][j] - m1 - xh[i][j] * m2) + (float)rv[j]);
+        for (int j = 0; j < 8; ++j) {
+          o[j] = (bf16)(rstd * (gw[i][j] - m1 - xh[i][j] * m2) + (float)rv[j]);
+          cs[i][j] += (float)o[j];
+        }
         dxr[vi] = o;
       }
     }
   }
   // combine the 4 waves (fixed order) and write this block's partial dw/db
   __shared__ float red[4][2048];
-  for (int pass = 0; pass < 2; ++pass) {
+  const int passes = cs_part ? 3 : 2;  // (a kernel argument: uniform)
+  for (int pass = 0; pass < passes; ++pass) {
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int vi = lane + 64 * i;
       if (vi < nv)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) red[wave][vi * 8 + j] = pass == 0 ? dw[i][j] : db[i][j];
+        for (int j = 0; j < 8; ++j) red[wave][vi * 8 + j] = pass == 0 ? dw[i][j] : (pass == 1 ? db[i][j] : cs[i][j]);
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < D; c += 256)
-      part[((int64_t)blockIdx.x * 2 + pass) * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    float* dst = pass < 2 ? part + ((int64_t)blockIdx.x * 2 + pass) * D : cs_part + (int64_t)blockIdx.x * D;
+    for (int c = threadIdx.x; c < D; c += 256) dst[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
     __syncthreads();
   }
 }
@@ -463,13 +468,13 @@ void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, 
 }
 
 void layernorm_bwd(const void* dy, const void* x, const float* stats, const float* w, const void* dres, int64_t rows,
-                   int D, void* dx, float* part, float* dw, float* db, hipStream_t s) {
+                   int D, void* dx, float* part, float* dw, float* db, hipStream_t s, float* cs_part) {
   const int nb = layernorm_bwd_blocks(rows);
   const int rpb = (int)((rows + nb - 1) / nb);
   const int nv = D / 8;
   auto args = [&](auto kern) {
     kern<<<nb, 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(x), stats, w,
-                            static_cast<const bf16*>(dres), rows, D, rpb, static_cast<bf16*>(dx), part);
+                            static_cast<const bf16*>(dres), rows, D, rpb, static_cast<bf16*>(dx), part, cs_part);
   };
   if (nv <= 64)
     args(layernorm_bwd_kernel<1>);

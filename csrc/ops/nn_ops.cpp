@@ -470,6 +470,31 @@ std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::
   return {y, stats};
 }
 
+std::vector<at::Tensor> layernorm_bwd_colsum(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats,
+                                             const at::Tensor& w, const c10::optional<at::Tensor>& dres, at::Tensor dw,
+                                             at::Tensor db) {
+  bf16_gpu(dy, "layernorm output grad");
+  bf16_gpu(x, "layernorm input");
+  f32_gpu(stats, "layernorm stats");
+  f32_gpu(dw, "layernorm dweight");
+  f32_gpu(db, "layernorm dbias");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  RINGDP_CHECK(dy.sizes() == x.sizes() && D % 4 == 0, "layernorm backward: shape mismatch");
+  const void* dr = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    bf16_gpu(*dres, "layernorm residual grad");
+    RINGDP_CHECK(dres->sizes() == x.sizes(), "layernorm residual grad: shape mismatch");
+    dr = dres->data_ptr();
+  }
+  at::Tensor dx = at::empty_like(x);
+  at::Tensor scratch = at::empty({kern::layernorm_bwd_scratch_floats(rows, (int)D)}, w.options());
+  at::Tensor cs = at::empty({kern::layernorm_bwd_blocks(rows), D}, w.options());
+  kern::layernorm_bwd(dy.data_ptr(), x.data_ptr(), stats.data_ptr<float>(), w.data_ptr<float>(), dr, rows, (int)D,
+                      dx.data_ptr(), scratch.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                      stream_of(x), cs.data_ptr<float>());
+  return {dx, cs};
+}
+
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats, const at::Tensor& w,
                          const c10::optional<at::Tensor>& dres, at::Tensor dw, at::Tensor db) {
   bf16_gpu(dy, "layernorm output grad");

@@ -43,6 +43,10 @@ at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b);
 
 std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                                                  double eps);
+// layernorm_bwd plus per-block column sums of dx: returns [dx, colsum partials [blocks][D]]
+std::vector<at::Tensor> layernorm_bwd_colsum(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats,
+                                             const at::Tensor& w, const c10::optional<at::Tensor>& dres, at::Tensor dw,
+                                             at::Tensor db);
 at::Tensor layernorm_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats, const at::Tensor& w,
                          const c10::optional<at::Tensor>& dres, at::Tensor dw, at::Tensor db);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> qkv_split(const at::Tensor& qkv, int64_t B, int64_t T, int64_t H,

@@ -22,6 +22,8 @@ _ATTN_UNFUSED = os.environ.get("RINGDP_ATTN_UNFUSED", "0") == "1"
 _ATTN_BWD_GEMMS = os.environ.get("RINGDP_ATTN_BWD_GEMMS", "0") == "1"  # dS kernel + batched GEMMs (A/B runs)
 # fused attention saves the per-query log-sum-exp and the backward recomputes P (RINGDP_ATTN_RECOMPUTE=0: store P)
 _ATTN_RECOMPUTE = os.environ.get("RINGDP_ATTN_RECOMPUTE", "1") == "1"
+# LayerNorm backward also emits the column sums of dx (the producing linear's bias gradient)
+_LN_COLSUM = os.environ.get("RINGDP_LN_COLSUM", "0") == "1"
 _FP8 = {"on": False}
 
 
@@ -428,6 +430,7 @@ class MLPF(torch.autograd.Function):
         w1, b1, w2, b2 = ctx.params
         M, D = h.shape
         Hd = w1b.shape[0]
+        dy_in = dy
         dy = dy.contiguous() if dy.dtype == torch.bfloat16 else _bf16(dy)
         db1 = grad_buffer(b1)
         # d(fc1 output) = (dy W2) * GELU'(pre): the GELU backward rides in the GEMM epilogue (act 3), and so do
@@ -440,7 +443,11 @@ class MLPF(torch.autograd.Function):
                          colsum=db1).view(M, Hd)
         dw2, db2 = grad_buffer(w2), grad_buffer(b2)
         C.gemm_splitk_f32(dy, a, D, Hd, M, D, Hd, True, True, _splits(M, D, Hd), dw2)
-        C.colsum_f32(dy, db2)
+        part = getattr(dy_in, "_ringdp_colsum_part", None)  # from the LayerNorm backward that produced dy
+        if part is not None and part.shape[1] == D:
+            C.rowsum_f32(part, db2)
+        else:
+            C.colsum_f32(dy, db2)
         dw1 = grad_buffer(w1)
         C.gemm_splitk_f32(dz1, h, Hd, D, M, Hd, D, True, True, _splits(M, Hd, D), dw1)
         dh = None
@@ -473,7 +480,13 @@ class LayerNormFork(torch.autograd.Function):
             return dres, None, None, None
         dw, db = grad_buffer(w), grad_buffer(b)
         res = dres.contiguous() if dres is not None else None
-        dx = C.layernorm_bwd(dy.contiguous(), x, stats, w, res, dw, db)
+        if _FP8["on"] or not _LN_COLSUM:  # (fp8 linears take their bias gradients from the quantisation pass)
+            dx = C.layernorm_bwd(dy.contiguous(), x, stats, w, res, dw, db)
+        else:
+            # dx is the output gradient of the linear that produced x (attention proj / fc2, residual fused):
+            # its bias gradient's column sums come from this kernel instead of a pass over dx
+            dx, part = C.layernorm_bwd_colsum(dy.contiguous(), x, stats, w, res, dw, db)
+            dx._ringdp_colsum_part = part
         return dx, dw, db, None
 
 

@@ -905,3 +905,27 @@ def test_fp8_batched_weight_quantisation_matches_per_weight():
     assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+def test_layernorm_backward_column_sums():
+    """layernorm_bwd_colsum: the same dx / dw / db as layernorm_bwd, plus per-block column sums of dx whose
+    row sum is the column sum of dx (the bias gradient of the linear that produced the LayerNorm input)."""
+    import ringdp
+
+    C = ringdp._C
+    torch.manual_seed(0)
+    rows, D = 3000, 768
+    x = torch.randn(rows, D, device="cuda").bfloat16()
+    dy = torch.randn(rows, D, device="cuda").bfloat16()
+    dres = torch.randn(rows, D, device="cuda").bfloat16()
+    w = torch.randn(D, device="cuda")
+    b = torch.randn(D, device="cuda")
+    _, stats = C.layernorm_fwd(x, w, b, 1e-6)
+    dw0, db0, dw1, db1 = (torch.empty(D, device="cuda") for _ in range(4))
+    dx0 = C.layernorm_bwd(dy, x, stats, w, dres, dw0, db0)
+    dx1, part = C.layernorm_bwd_colsum(dy, x, stats, w, dres, dw1, db1)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1) and torch.equal(dw0, dw1) and torch.equal(db0, db1)
+    cs = torch.empty(D, device="cuda")
+    C.rowsum_f32(part, cs)
+    torch.testing.assert_close(cs, dx1.float().sum(0), rtol=1e-4, atol=2e-3)
