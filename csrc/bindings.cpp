@@ -520,6 +520,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("add_bf16", &ops::add_bf16);
   m.def("layernorm_fwd", &ops::layernorm_fwd);
   m.def("layernorm_bwd", &ops::layernorm_bwd);
+  m.def("layernorm_fwd_q8", &ops::layernorm_fwd_q8, "layernorm forward with e4m3 outputs (q, q^T) at a delayed scale");
+  m.def("layernorm_q8_slots", &ops::layernorm_q8_slots);
   m.def("layernorm_bwd_colsum", &ops::layernorm_bwd_colsum,
         "layernorm backward that also returns per-block column sums of dx (a bias gradient's partials)");
   m.def("qkv_split", &ops::qkv_split);

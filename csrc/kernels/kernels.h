@@ -453,6 +453,11 @@ void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s);
 void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, void* y,
                    float* stats, hipStream_t s);
 int layernorm_bwd_scratch_floats(int64_t rows, int D);
+// LayerNorm forward with e4m3 outputs (q [rows][D], qt [D][rows]) at the delayed scale amax[0] / 448; tmax gets one
+// |y|max per 64-row block (layernorm_q8_blocks); rows % 16 == 0, D % 8 == 0, D <= 2048
+int64_t layernorm_q8_blocks(int64_t rows);
+void layernorm_fwd_q8(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, float* stats,
+                      const float* amax, void* q, void* qt, float* scale, float* tmax, hipStream_t s);
 // cs_part (nullable): [layernorm_bwd_blocks(rows)][D] per-block column sums of dx (the bias gradient of the
 // linear whose output gradient dx is)
 int layernorm_bwd_blocks(int64_t rows);

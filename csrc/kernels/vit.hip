@@ -82,6 +82,119 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16* __restri
   }
 }
 
+// LayerNorm forward that writes its output as e4m3 for the next fp8 linear instead of bf16: the normalised row
+// (the exact values layernorm_fwd_kernel would store, rounded to bf16) is quantised with the delayed scale
+// amax[0] / 448 (clamped to +-448) into q [rows][D] (8-B stores straight from the lanes) and, through an LDS
+// tile of the block's 64 rows (193-dword rows: conflict-free), transposed into qt [D][rows] (8 lanes of a column
+// group write 64 contiguous bytes).  tmax[block] <- the block's |y|max (the next roll); scale[0] <- the scale.
+// rows % 16 == 0 (8-row groups are wholly inside), D % 8 == 0, dynamic LDS 64 * (D + 4) bytes.
+constexpr int kLnQ8Rows = 64;
+__device__ __forceinline__ uint32_t ln_pack_e4m3(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+template <int VPL>
+__global__ __launch_bounds__(256) void layernorm_fwd_q8_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ b, int64_t rows, int D,
+                                                               float eps, float* __restrict__ stats,
+                                                               const float* __restrict__ amax, uint8_t* __restrict__ q,
+                                                               uint8_t* __restrict__ qt, float* __restrict__ scale,
+                                                               float* __restrict__ tmax) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lnq_tile[];
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nv = D / 8, ld = D + 4;
+  const float qs = fmaxf(amax[0], 1e-12f) / 448.f, inv = 1.f / qs;
+  if (blockIdx.x == 0 && threadIdx.x == 0) scale[0] = qs;
+  const int64_t r0 = (int64_t)blockIdx.x * kLnQ8Rows;
+  float vmax = 0.f;
+  for (int rl = wave; rl < kLnQ8Rows; rl += 4) {
+    const int64_t row = r0 + rl;
+    if (row >= rows) break;
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row * D);
+    float v[VPL][8];
+    float sm = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nv) {
+        const bf16x8 t = xr[vi];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          v[i][j] = (float)t[j];
+          sm += v[i][j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+      }
+    }
+    const float mean = wave_sum(sm) / (float)D;
+    float qq = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+      if (lane + 64 * i < nv)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[i][j] - mean;
+          qq += d * d;
+        }
+    const float rstd = rsqrtf(wave_sum(qq) / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vi = lane + 64 * i;
+      if (vi < nv) {
+        float e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = vi * 8 + j;
+          const float y = (float)(bf16)((v[i][j] - mean) * rstd * w[c] + b[c]);  // layernorm_fwd_kernel's value
+          vmax = fmaxf(vmax, fabsf(y));
+          e[j] = fminf(fmaxf(y * inv, -448.f), 448.f);
+        }
+        const uint32_t lo = ln_pack_e4m3(e[0], e[1], e[2], e[3]), hi = ln_pack_e4m3(e[4], e[5], e[6], e[7]);
+        *reinterpret_cast<uint2*>(q + row * D + vi * 8) = make_uint2(lo, hi);
+        uint32_t* tw = reinterpret_cast<uint32_t*>(lnq_tile + rl * ld + vi * 8);
+        tw[0] = lo;
+        tw[1] = hi;
+      }
+    }
+    if (lane == 0) {
+      stats[2 * row] = mean;
+      stats[2 * row + 1] = rstd;
+    }
+  }
+  vmax = wave_max(vmax);
+  if (lane == 0) red[wave] = vmax;
+  __syncthreads();
+  if (threadIdx.x == 0) tmax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  // transposed: item = (8-row group rg, 4-column group cg)
+  const int ncg = D / 4;
+  for (int it = threadIdx.x; it < 8 * ncg; it += 256) {
+    const int rg = it & 7, c = 4 * (it >> 3);
+    const int64_t m = r0 + 8 * rg;
+    if (m >= rows) continue;
+    uint32_t d[8];
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) d[ii] = *reinterpret_cast<const uint32_t*>(lnq_tile + (8 * rg + ii) * ld + c);
+    uint32_t col[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t a0 = d[4 * h], a1 = d[4 * h + 1], a2 = d[4 * h + 2], a3 = d[4 * h + 3];
+      const uint32_t ab_lo = __builtin_amdgcn_perm(a1, a0, 0x05010400u), ab_hi = __builtin_amdgcn_perm(a1, a0, 0x07030602u);
+      const uint32_t ce_lo = __builtin_amdgcn_perm(a3, a2, 0x05010400u), ce_hi = __builtin_amdgcn_perm(a3, a2, 0x07030602u);
+      col[h][0] = __builtin_amdgcn_perm(ce_lo, ab_lo, 0x05040100u);
+      col[h][1] = __builtin_amdgcn_perm(ce_lo, ab_lo, 0x07060302u);
+      col[h][2] = __builtin_amdgcn_perm(ce_hi, ab_hi, 0x05040100u);
+      col[h][3] = __builtin_amdgcn_perm(ce_hi, ab_hi, 0x07060302u);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+      *reinterpret_cast<uint2*>(qt + (int64_t)(c + jj) * rows + m) = make_uint2(col[0][jj], col[1][jj]);
+  }
+}
+
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)) (+ dres);  dw/db partials per block
 template <int VPL>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
@@ -465,6 +578,24 @@ void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, 
     layernorm_fwd_kernel<2><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, static_cast<bf16*>(y), stats);
   else
     layernorm_fwd_kernel<4><<<grid, 256, 0, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, static_cast<bf16*>(y), stats);
+}
+
+int64_t layernorm_q8_blocks(int64_t rows) { return (rows + kLnQ8Rows - 1) / kLnQ8Rows; }
+
+void layernorm_fwd_q8(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, float* stats,
+                      const float* amax, void* q, void* qt, float* scale, float* tmax, hipStream_t s) {
+  const int nb = (int)layernorm_q8_blocks(rows), nv = D / 8;
+  const size_t lds = (size_t)kLnQ8Rows * (D + 4);
+  auto go = [&](auto kern) {
+    kern<<<nb, 256, lds, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, stats, amax, static_cast<uint8_t*>(q),
+                              static_cast<uint8_t*>(qt), scale, tmax);
+  };
+  if (nv <= 64)
+    go(layernorm_fwd_q8_kernel<1>);
+  else if (nv <= 128)
+    go(layernorm_fwd_q8_kernel<2>);
+  else
+    go(layernorm_fwd_q8_kernel<4>);
 }
 
 void layernorm_bwd(const void* dy, const void* x, const float* stats, const float* w, const void* dres, int64_t rows,

@@ -470,6 +470,28 @@ std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::
   return {y, stats};
 }
 
+std::vector<at::Tensor> layernorm_fwd_q8(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps,
+                                         at::Tensor hist) {
+  bf16_gpu(x, "layernorm input");
+  f32_gpu(w, "layernorm weight");
+  f32_gpu(b, "layernorm bias");
+  f32_gpu(hist, "fp8 amax history");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  RINGDP_CHECK(D % 8 == 0 && D <= 2048 && w.numel() == D && b.numel() == D && rows % 16 == 0 && x.is_contiguous(),
+               "layernorm_fwd_q8: bad shapes");
+  RINGDP_CHECK(hist.is_contiguous() && hist.numel() == 1 + kern::layernorm_q8_blocks(rows),
+               "layernorm_fwd_q8: history must hold 1 + ceil(rows / 64) floats");
+  at::Tensor stats = at::empty({rows, 2}, w.options());
+  at::Tensor q = at::empty({rows, D}, x.options().dtype(at::kByte)), qt = at::empty({D, rows}, x.options().dtype(at::kByte));
+  at::Tensor scale = at::empty({1}, w.options());
+  kern::layernorm_fwd_q8(x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), rows, (int)D, (float)eps,
+                         stats.data_ptr<float>(), hist.data_ptr<float>(), q.data_ptr(), qt.data_ptr(),
+                         scale.data_ptr<float>(), hist.data_ptr<float>() + 1, stream_of(x));
+  return {stats, q, qt, scale};
+}
+
+int64_t layernorm_q8_slots(int64_t rows) { return kern::layernorm_q8_blocks(rows); }
+
 std::vector<at::Tensor> layernorm_bwd_colsum(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats,
                                              const at::Tensor& w, const c10::optional<at::Tensor>& dres, at::Tensor dw,
                                              at::Tensor db) {

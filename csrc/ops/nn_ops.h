@@ -43,6 +43,10 @@ at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b);
 
 std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,
                                                  double eps);
+// LayerNorm forward writing e4m3 (delayed scaling, hist = [amax, per-64-row-block maxima]): [stats, q, qt, scale]
+std::vector<at::Tensor> layernorm_fwd_q8(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b, double eps,
+                                         at::Tensor hist);
+int64_t layernorm_q8_slots(int64_t rows);
 // layernorm_bwd plus per-block column sums of dx: returns [dx, colsum partials [blocks][D]]
 std::vector<at::Tensor> layernorm_bwd_colsum(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& stats,
                                              const at::Tensor& w, const c10::optional<at::Tensor>& dres, at::Tensor dw,

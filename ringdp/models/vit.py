@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.transformer import (AttentionF, ClassRowsF, LayerNormF, LayerNormFork, MLPF, MLPF8, PatchTokensF,
-                                cast_weights, clear_weights, fp8_enabled, fp8_mlp_fusable, linear)
+                                cast_weights, clear_weights, fp8_enabled, fp8_mlp_fusable, layernorm_fork, linear)
 
 
 class MLPBlock(nn.Sequential):
@@ -51,12 +51,12 @@ class EncoderBlock(nn.Module):
     def forward_rows(self, x, B: int, T: int):  # ringdp path, x [B*T, D] bf16
         att = self.self_attention
         if fp8_enabled():  # fp8 linears (LinearF's quantised path); residual gradients join in the LN backward
-            h, x = LayerNormFork.apply(x, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps)
+            fc1, fc2 = self.mlp[0], self.mlp[3]
+            h, x = layernorm_fork(x, self.ln_1, att.in_proj_weight)
             qkv = _lin(h, att.in_proj_weight, att.in_proj_bias)
             o = AttentionF.apply(qkv, B, T, self.num_heads)
             x = linear(o, att.out_proj, residual=x)
-            h, x = LayerNormFork.apply(x, self.ln_2.weight, self.ln_2.bias, self.ln_2.eps)
-            fc1, fc2 = self.mlp[0], self.mlp[3]
+            h, x = layernorm_fork(x, self.ln_2, fc1.weight)
             if fp8_mlp_fusable(h.shape[0], h.shape[1], fc1.weight.shape[0]):  # e4m3 from the GEMM epilogues
                 return MLPF8.apply(h, fc1.weight, fc1.bias, fc2.weight, fc2.bias, x)
             h = linear(h, fc1, act=2)

@@ -245,13 +245,13 @@ def _site(w: torch.Tensor, slot: int, n: int, device) -> Tuple[torch.Tensor, boo
     """The delayed-scaling history of site ``slot`` on weight ``w`` ([amax to scale by, n - 1 tile maxima of
     the last call]): returns (hist, init, roll_here).  Slots: 0 the linear's input, 1 its output gradient,
     2 its weight, 3 (on fc2) the input fc1's epilogue quantises, 4 (on fc1) the output gradient fc2's
-    data-gradient epilogue quantises.  ``init``: first use (or a new shape) - the caller measures an exact
+    data-gradient epilogue quantises, 5 the input a LayerNorm forward quantises (LayerNormFork8).  ``init``: first use (or a new shape) - the caller measures an exact
     amax.  ``roll_here``: the caller rolls this site itself (per-site mode, or a capture that cannot
     upload the batched roll's table); otherwise the batched roll already ran when needed."""
     sites = getattr(w, "_ringdp_fp8", None)
     if sites is None:
-        sites = w._ringdp_fp8 = [None] * 5
-        w._ringdp_fp8_used = [False] * 5
+        sites = w._ringdp_fp8 = [None] * 6
+        w._ringdp_fp8_used = [False] * 6
     used = w._ringdp_fp8_used
     hist = sites[slot]
     init = hist is None or hist.numel() != n
@@ -317,7 +317,7 @@ class MLPF8(torch.autograd.Function):
     def forward(ctx, h, w1, b1, w2, b2, residual):
         M, D = h.shape
         Hd = w1.shape[0]
-        hq, hqt, sh = _quant_act(h, w1, 0)
+        hq, hqt, sh = _q8_of(h, w1)
         w1q, w1qt, sw1 = _quant_weight(w1)
         pre = torch.empty(M, Hd, device=h.device, dtype=torch.bfloat16)
         hist3, init3 = _epilogue_site(w2, 3, M, Hd, h.device, 0)
@@ -368,7 +368,7 @@ class MLPF8(torch.autograd.Function):
 def _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32):
     M, K = x.shape
     N = w.shape[0]
-    xq, xtq, sx = _quant_act(x, w, 0)    # row-major for this GEMM, transposed for the weight grad
+    xq, xtq, sx = _q8_of(x, w)           # row-major for this GEMM, transposed for the weight grad
     wq, wtq, sw = _quant_weight(w)       # ... and for the data grad
     pre = torch.empty(M, N, device=x.device, dtype=torch.bfloat16) if act == 2 else None
     y = C.gemm_fp8(xq, wq, sx, sw, M, N, K, not out_f32, b, act, residual, pre)
@@ -488,6 +488,55 @@ class LayerNormFork(torch.autograd.Function):
             dx, part = C.layernorm_bwd_colsum(dy.contiguous(), x, stats, w, res, dw, db)
             dx._ringdp_colsum_part = part
         return dx, dw, db, None
+
+
+_FP8_LN_Q8 = os.environ.get("RINGDP_FP8_LN_Q8", "0") == "1"
+
+
+class LayerNormFork8(torch.autograd.Function):
+    """LayerNormFork for an fp8 consumer: the forward writes the normalised rows as e4m3 (row-major and
+    transposed, delayed scale of the consumer weight's site 5) instead of bf16, so the consumer linear needs
+    no quantisation pass.  The returned ``y`` is an unwritten placeholder carrying the e4m3 triple
+    (``_ringdp_q8``), read only by LinearF / MLPF8; the backward is LayerNormFork's.  The first call of a site
+    runs the bf16 LayerNorm and measures the exact amax."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, eps: float, consumer_w):
+        rows = x.shape[0]
+        hist, init, roll = _site(consumer_w, 5, 1 + C.layernorm_q8_slots(rows), x.device)
+        ctx.params = (w, b)
+        if init:
+            y, stats = C.layernorm_fwd(x, w, b, eps)
+            hist[:1].copy_(y.float().abs().amax().reshape(1))
+            ctx.save_for_backward(x, stats)
+            return y, x
+        if roll:
+            C.fp8_roll(hist)
+        stats, q, qt, scale = C.layernorm_fwd_q8(x, w, b, eps, hist)
+        ctx.save_for_backward(x, stats)
+        y = torch.empty_like(x)
+        y._ringdp_q8 = (q, qt, scale)
+        return y, x
+
+    @staticmethod
+    def backward(ctx, dy, dres):
+        dx, dw, db, _ = LayerNormFork.backward(ctx, dy, dres)
+        return dx, dw, db, None, None
+
+
+def layernorm_fork(x, ln, consumer_w):
+    """``y, x_id`` of LayerNormFork, or of LayerNormFork8 when the consumer is an fp8 linear."""
+    if _FP8["on"] and _FP8_LN_Q8 and _FP8_DELAYED and x.shape[0] % 16 == 0:
+        return LayerNormFork8.apply(x, ln.weight, ln.bias, ln.eps, consumer_w)
+    return LayerNormFork.apply(x, ln.weight, ln.bias, ln.eps)
+
+
+def _q8_of(x, w, slot=0):
+    """(q, q^T, scale) of an fp8 GEMM input: from the producing LayerNorm (LayerNormFork8) or quantised here."""
+    e = getattr(x, "_ringdp_q8", None)
+    if e is not None:
+        return e
+    return _quant_act(x, w, slot)
 
 
 class LayerNormF(torch.autograd.Function):

@@ -929,3 +929,46 @@ def test_layernorm_backward_column_sums():
     cs = torch.empty(D, device="cuda")
     C.rowsum_f32(part, cs)
     torch.testing.assert_close(cs, dx1.float().sum(0), rtol=1e-4, atol=2e-3)
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_fp8_layernorm_e4m3_output_matches_separate_quantisation(wide):
+    """LayerNormFork8 (the LayerNorm forward writes the next fp8 linear's e4m3 input) trains like the
+    LayerNorm + quant_t pair: same LayerNorm values, same delayed scale (a max over the same tensor)."""
+    import copy
+
+    import ringdp.ops.transformer as tr
+    from ringdp.models import vit_tiny
+    from ringdp.models.vit import VisionTransformer
+    from ringdp.optim import SGD
+
+    torch.manual_seed(0)
+    m = (VisionTransformer(image_size=32, patch_size=4, num_layers=2, num_heads=2, hidden_dim=128, mlp_dim=256,
+                           num_classes=10) if wide else vit_tiny(num_classes=10)).cuda()
+    g = torch.Generator(device="cuda").manual_seed(6)
+    xs = [torch.randn(16, 3, 32, 32, device="cuda", generator=g) for _ in range(4)]
+    ys = [torch.randint(0, 10, (16,), device="cuda", generator=g) for _ in range(4)]
+    res = []
+    saved = tr._FP8_LN_Q8
+    try:
+        tr.set_fp8(True)
+        for on in (False, True):
+            tr._FP8_LN_Q8 = on
+            tr._ROLLS.clear()
+            mm = copy.deepcopy(m)
+            opt = SGD(mm.parameters(), lr=0.05, momentum=0.9)
+            losses = []
+            for x, y in zip(xs, ys):
+                loss = F.cross_entropy(mm(x), y)
+                opt.zero_grad(set_to_none=True)
+                loss.backward()
+                opt.step()
+                losses.append(loss.detach())
+            res.append((torch.stack(losses), [p.detach().clone() for p in mm.parameters()]))
+    finally:
+        tr.set_fp8(False)
+        tr._FP8_LN_Q8 = saved
+    print(res[0][0], res[1][0])
+    assert torch.equal(res[0][0], res[1][0]), (res[0][0], res[1][0])
+    for a, b in zip(res[0][1], res[1][1]):
+        assert torch.equal(a, b)
