@@ -88,28 +88,28 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const bf16* __restri
 // tile of the block's 64 rows (193-dword rows: conflict-free), transposed into qt [D][rows] (8 lanes of a column
 // group write 64 contiguous bytes).  tmax[block] <- the block's |y|max (the next roll); scale[0] <- the scale.
 // rows % 16 == 0 (8-row groups are wholly inside), D % 8 == 0, dynamic LDS 64 * (D + 4) bytes.
-constexpr int kLnQ8Rows = 64;
+constexpr int kLnQ8Rows = 64, kLnQ8Threads = 1024;  // 16 waves x 4 rows: the rows of a block in parallel
 __device__ __forceinline__ uint32_t ln_pack_e4m3(float a, float b, float c, float d) {
   int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
   w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
   return (uint32_t)w;
 }
 template <int VPL>
-__global__ __launch_bounds__(256) void layernorm_fwd_q8_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
+__global__ __launch_bounds__(kLnQ8Threads) void layernorm_fwd_q8_kernel(const bf16* __restrict__ x, const float* __restrict__ w,
                                                                const float* __restrict__ b, int64_t rows, int D,
                                                                float eps, float* __restrict__ stats,
                                                                const float* __restrict__ amax, uint8_t* __restrict__ q,
                                                                uint8_t* __restrict__ qt, float* __restrict__ scale,
                                                                float* __restrict__ tmax) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lnq_tile[];
-  __shared__ float red[4];
+  __shared__ float red[kLnQ8Threads / 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = D / 8, ld = D + 4;
   const float qs = fmaxf(amax[0], 1e-12f) / 448.f, inv = 1.f / qs;
   if (blockIdx.x == 0 && threadIdx.x == 0) scale[0] = qs;
   const int64_t r0 = (int64_t)blockIdx.x * kLnQ8Rows;
   float vmax = 0.f;
-  for (int rl = wave; rl < kLnQ8Rows; rl += 4) {
+  for (int rl = wave; rl < kLnQ8Rows; rl += kLnQ8Threads / 64) {
     const int64_t row = r0 + rl;
     if (row >= rows) break;
     const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + row * D);
@@ -168,10 +168,14 @@ __global__ __launch_bounds__(256) void layernorm_fwd_q8_kernel(const bf16* __res
   vmax = wave_max(vmax);
   if (lane == 0) red[wave] = vmax;
   __syncthreads();
-  if (threadIdx.x == 0) tmax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (threadIdx.x == 0) {
+    float m = 0.f;
+    for (int i = 0; i < kLnQ8Threads / 64; ++i) m = fmaxf(m, red[i]);
+    tmax[blockIdx.x] = m;
+  }
   // transposed: item = (8-row group rg, 4-column group cg)
   const int ncg = D / 4;
-  for (int it = threadIdx.x; it < 8 * ncg; it += 256) {
+  for (int it = threadIdx.x; it < 8 * ncg; it += kLnQ8Threads) {
     const int rg = it & 7, c = 4 * (it >> 3);
     const int64_t m = r0 + 8 * rg;
     if (m >= rows) continue;
@@ -587,7 +591,7 @@ void layernorm_fwd_q8(const void* x, const float* w, const float* b, int64_t row
   const int nb = (int)layernorm_q8_blocks(rows), nv = D / 8;
   const size_t lds = (size_t)kLnQ8Rows * (D + 4);
   auto go = [&](auto kern) {
-    kern<<<nb, 256, lds, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, stats, amax, static_cast<uint8_t*>(q),
+    kern<<<nb, kLnQ8Threads, lds, s>>>(static_cast<const bf16*>(x), w, b, rows, D, eps, stats, amax, static_cast<uint8_t*>(q),
                               static_cast<uint8_t*>(qt), scale, tmax);
   };
   if (nv <= 64)

@@ -490,7 +490,7 @@ class LayerNormFork(torch.autograd.Function):
         return dx, dw, db, None
 
 
-_FP8_LN_Q8 = os.environ.get("RINGDP_FP8_LN_Q8", "0") == "1"
+_FP8_LN_Q8 = os.environ.get("RINGDP_FP8_LN_Q8", "1") == "1"
 
 
 class LayerNormFork8(torch.autograd.Function):
