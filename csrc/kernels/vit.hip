@@ -200,7 +200,7 @@ __global__ __launch_bounds__(kLnQ8Threads) void layernorm_fwd_q8_kernel(const bf
 }
 
 // dx = rstd * (w*dy - mean(w*dy) - xhat * mean(w*dy*xhat)) (+ dres);  dw/db partials per block
-template <int VPL>
+template <int VPL, bool CS>  // CS: also the column sums of dx into cs_part (compiled out otherwise)
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                             const float* __restrict__ stats,
                                                             const float* __restrict__ w, const bf16* __restrict__ dres,
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restri
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           o[j] = (bf16)(rstd * (gw[i][j] - m1 - xh[i][j] * m2) + (float)rv[j]);
-          cs[i][j] += (float)o[j];
+          if constexpr (CS) cs[i][j] += (float)o[j];
         }
         dxr[vi] = o;
       }
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const bf16* __restri
   }
   // combine the 4 waves (fixed order) and write this block's partial dw/db
   __shared__ float red[4][2048];
-  const int passes = cs_part ? 3 : 2;  // (a kernel argument: uniform)
+  constexpr int passes = CS ? 3 : 2;
   for (int pass = 0; pass < passes; ++pass) {
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
@@ -611,12 +611,15 @@ void layernorm_bwd(const void* dy, const void* x, const float* stats, const floa
     kern<<<nb, 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(x), stats, w,
                             static_cast<const bf16*>(dres), rows, D, rpb, static_cast<bf16*>(dx), part, cs_part);
   };
-  if (nv <= 64)
-    args(layernorm_bwd_kernel<1>);
-  else if (nv <= 128)
-    args(layernorm_bwd_kernel<2>);
-  else
-    args(layernorm_bwd_kernel<4>);
+  if (cs_part) {
+    if (nv <= 64) args(layernorm_bwd_kernel<1, true>);
+    else if (nv <= 128) args(layernorm_bwd_kernel<2, true>);
+    else args(layernorm_bwd_kernel<4, true>);
+  } else {
+    if (nv <= 64) args(layernorm_bwd_kernel<1, false>);
+    else if (nv <= 128) args(layernorm_bwd_kernel<2, false>);
+    else args(layernorm_bwd_kernel<4, false>);
+  }
   // part [nb][2][D] -> dw = sum part[.][0], db = sum part[.][1]
   reduce_parts(part, nb, D, part + (int64_t)nb * 2 * D, dw, db, s);
 }
