@@ -33,8 +33,11 @@ _FUSE12 = os.environ.get("RINGDP_CN_FUSE12", "1") != "0"
 # RINGDP_CN_FUSED_FWD=0: the three-launch forward (conv1+pack / conv2 / conv3+fc1) instead of the
 # whole-forward kernel (weight pack + cn_forward_fused; B=65536: forward 1469 -> 1390 us, B=100: 28 -> 23 us)
 _FUSED_FWD = os.environ.get("RINGDP_CN_FUSED_FWD", "1") != "0"
-# RINGDP_CN_DEFER_REDUCE=0: conv3 / fc1 weight-gradient reduction in its own launch (A/B)
-_DEFER = os.environ.get("RINGDP_CN_DEFER_REDUCE", "1") != "0"
+# RINGDP_CN_DEFER_REDUCE=1: the conv3 / fc1 weight-gradient reduction rides in conv12's reduction launch.
+# Opt-in: while deferred, the DDP slots of w3/b3/wfc/bfc hold stale values, and nothing in autograd lets
+# this node prove that no other producer (an L2 term on the weights, a tied use) makes the engine sum the
+# slot before conv12's backward runs.
+_DEFER = os.environ.get("RINGDP_CN_DEFER_REDUCE", "0") == "1"
 # RINGDP_CN_HEAD_CE=0: ringdp's cross entropy on the ConvNet logits stays a separate node (A/B)
 _HEAD_CE = os.environ.get("RINGDP_CN_HEAD_CE", "1") != "0"
 
@@ -227,7 +230,13 @@ def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index:
         return None
     if target.dim() != 1 or target.shape[0] != logits.shape[0] or not target.is_cuda:
         return None
-    z2, a2, idx2, w3, b3, wfc, bfc, packed, a3, idx3 = head
+    z2, a2, idx2, w3, b3, wfc, bfc, packed, a3, idx3, version, node = head
+    # The fused loss reads logits.detach(): only exact when the logits are still the untouched output of
+    # _Conv3FC (an in-place edit bumps the version and replaces grad_fn) and nobody observes their gradient
+    # (tensor hooks, retain_grad) - otherwise the plain criterion, whose backward runs through _Conv3FC.
+    if logits._version != version or logits.grad_fn is not node or logits.retains_grad \
+            or logits._backward_hooks:
+        return None
     return _HeadCE.apply(z2, w3, b3, wfc, bfc, logits.detach(), target.long().contiguous(),
                          (a2, idx2, a3, idx3, packed), ignore_index, eps, reduction)
 
@@ -266,5 +275,6 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
                                       fused)
     if logits.requires_grad:
         # what ringdp's cross entropy needs to fuse itself into the head (head_cross_entropy)
-        logits._ringdp_head = (z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed, a3, idx3)
+        logits._ringdp_head = (z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed, a3, idx3,
+                               logits._version, logits.grad_fn)
     return logits

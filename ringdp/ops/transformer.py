@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -140,6 +141,9 @@ class LinearF(torch.autograd.Function):
         if _FP8["on"] and M % 16 == 0 and N % 16 == 0 and K % 16 == 0:
             return _linear_fp8_fwd(ctx, x, w, b, residual, act, out_f32)
         ctx.fp8 = False
+        if getattr(x, "_ringdp_q8", None) is not None:
+            raise RuntimeError("LinearF: x is an e4m3-only LayerNorm output (LayerNormFork8) but this linear "
+                               "is not on the fp8 path")
         Np = (N + 7) // 8 * 8  # the weight-gradient GEMM walks rows of W in 16-B vectors
         wb = _bf16(w)
         bb = b
@@ -217,25 +221,36 @@ class _RollSet:
     call's tile maxima; a roll of a site not called since is a no-op (same maxima, same result)."""
 
     def __init__(self):
-        self.sites = []          # (sites list on the weight, used flags on the weight, slot)
+        self.sites = []          # (weakref to the weight, slot): the history lives on the weight
         self.table = None        # (int64 pointers, int32 tile counts) of the current history tensors
         self.dirty = True
 
-    def register(self, sites, used, slot):
-        if not any(s is sites and k == slot for s, _, k in self.sites):
-            self.sites.append((sites, used, slot))
+    def register(self, w, slot):
+        self._prune()
+        if not any(r() is w and k == slot for r, k in self.sites):
+            self.sites.append((weakref.ref(w), slot))
         self.dirty = True
 
+    def _prune(self):
+        """Forget the sites of weights that no longer exist (models torn down between evals / sweeps)."""
+        alive = [(r, k) for r, k in self.sites if r() is not None]
+        if len(alive) != len(self.sites):
+            self.sites = alive
+            self.dirty = True
+
     def roll(self, device):
+        self._prune()
         if self.dirty:
-            live = [(s[k]) for s, _, k in self.sites if s[k] is not None]
+            live = [h for h in (r()._ringdp_fp8[k] for r, k in self.sites) if h is not None]
             ptrs = torch.tensor([h.data_ptr() for h in live], dtype=torch.int64)
             ns = torch.tensor([h.numel() - 1 for h in live], dtype=torch.int32)
             self.table = (ptrs.to(device), ns.to(device), live)
             self.dirty = False
         C.fp8_roll_many(self.table[0], self.table[1])
-        for _, used, k in self.sites:
-            used[k] = False
+        for r, k in self.sites:
+            w = r()
+            if w is not None:
+                w._ringdp_fp8_used[k] = False
 
 
 _ROLLS = {}
@@ -261,7 +276,7 @@ def _site(w: torch.Tensor, slot: int, n: int, device) -> Tuple[torch.Tensor, boo
         return hist, init, not init
     rs = _ROLLS.setdefault(device, _RollSet())
     if init:
-        rs.register(sites, used, slot)
+        rs.register(w, slot)
     elif used[slot]:
         if rs.dirty and torch.cuda.is_current_stream_capturing():  # no table upload inside a capture
             return hist, init, True
@@ -524,9 +539,18 @@ class LayerNormFork8(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+def _fork8_ok(x, consumer_w) -> bool:
+    """LayerNormFork8's placeholder ``y`` is only valid if the consumer takes the fp8 path: LinearF's
+    condition (rows, D and the consumer's out_features multiples of 16) and the e4m3 LayerNorm kernel's
+    D <= 2048."""
+    rows, d = x.shape[0], x.shape[-1]
+    return x.dim() == 2 and rows % 16 == 0 and d % 16 == 0 and d <= 2048 and consumer_w.shape[0] % 16 == 0 \
+        and consumer_w.shape[-1] == d
+
+
 def layernorm_fork(x, ln, consumer_w):
     """``y, x_id`` of LayerNormFork, or of LayerNormFork8 when the consumer is an fp8 linear."""
-    if _FP8["on"] and _FP8_LN_Q8 and _FP8_DELAYED and x.shape[0] % 16 == 0:
+    if _FP8["on"] and _FP8_LN_Q8 and _FP8_DELAYED and _fork8_ok(x, consumer_w):
         return LayerNormFork8.apply(x, ln.weight, ln.bias, ln.eps, consumer_w)
     return LayerNormFork.apply(x, ln.weight, ln.bias, ln.eps)
 

@@ -328,6 +328,7 @@ def test_head_ce_fusion_and_deferred_reduce(world1, B, bucket_mb):
         assert not C.cn_reduce_pending(0)
         return loss.detach(), [p.grad.clone() for p in m.parameters()], C.cn_merged_reductions() - merged0
 
+    saved = (cn._HEAD_CE, cn._DEFER)
     try:
         l0, g0, n0 = run(False, False, False)
         assert n0 == 0
@@ -343,7 +344,7 @@ def test_head_ce_fusion_and_deferred_reduce(world1, B, bucket_mb):
             else:
                 assert n1 == 0, (cfg, n1)
     finally:
-        cn._HEAD_CE, cn._DEFER = True, True
+        cn._HEAD_CE, cn._DEFER = saved
 
 
 @pytest.mark.parametrize("kw", [{"reduction": "sum"}, {"reduction": "none"}, {"label_smoothing": 0.1},
@@ -374,3 +375,86 @@ def test_head_ce_variants_match_separate_criterion(kw):
     assert torch.equal(res[0][0], res[1][0])
     for a, b in zip(res[0][1], res[1][1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("edit", ["mul", "clamp", "retain", "hook"])
+def test_head_ce_not_fused_over_edited_or_observed_logits(edit):
+    """An in-place edit of the logits between model and criterion (or a hook / retain_grad on them)
+    must turn the head fusion off: the gradients then equal the unfused criterion's."""
+    import ringdp.ops.convnet as cn
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+
+    crit = CrossEntropyLoss()
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = torch.randint(0, 256, (128, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g)
+    y = torch.randint(0, 10, (128,), device="cuda", generator=g)
+    seen = []
+
+    def run(fused):
+        cn._HEAD_CE = fused
+        torch.manual_seed(0)
+        m = ConvNet().cuda()
+        logits = m(x)
+        if edit == "mul":
+            logits.mul_(0.5)
+        elif edit == "clamp":
+            logits.clamp_(-0.05, 0.05)
+        elif edit == "retain":
+            logits.retain_grad()
+        else:
+            logits.register_hook(lambda t: seen.append(t.detach().clone()))
+        loss = crit(logits, y)
+        loss.backward()
+        lg = logits.grad.clone() if edit == "retain" else None
+        return loss.detach(), [p.grad.clone() for p in m.parameters()], lg
+
+    saved = cn._HEAD_CE
+    try:
+        l0, g0, lg0 = run(False)
+        l1, g1, lg1 = run(True)
+    finally:
+        cn._HEAD_CE = saved
+    assert torch.equal(l0, l1)
+    for a, b in zip(g0, g1):
+        assert torch.equal(a, b)
+    if edit == "retain":
+        assert lg1 is not None and torch.equal(lg0, lg1)
+    if edit == "hook":
+        assert len(seen) == 2 and torch.equal(seen[0], seen[1])
+
+
+def test_weight_penalty_under_ddp_matches_separate_path(world1):
+    """A loss with an L2 term on the head weights (a second autograd producer for w3 / wfc) under DDP
+    gives the same gradients on the default path as with head fusion and reduction deferral off."""
+    import ringdp.ops.convnet as cn
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+    from ringdp.parallel import DistributedDataParallel as DDP
+
+    crit = CrossEntropyLoss()
+    g = torch.Generator(device="cuda").manual_seed(13)
+    x = torch.randint(0, 256, (256, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g)
+    y = torch.randint(0, 10, (256,), device="cuda", generator=g)
+
+    def run(head_ce, defer):
+        cn._HEAD_CE, cn._DEFER = head_ce, defer
+        torch.manual_seed(0)
+        m = ConvNet().cuda()
+        mod = DDP(m, device_ids=[0])
+        for _ in range(3):
+            for p in m.parameters():
+                p.grad = None
+            loss = crit(mod(x), y) + 1e-2 * (m.conv3.weight.pow(2).sum() + m.fc1.weight.pow(2).sum())
+            loss.backward()
+        torch.cuda.synchronize()
+        return [p.grad.clone() for p in m.parameters()]
+
+    saved = (cn._HEAD_CE, cn._DEFER)
+    try:
+        g0 = run(False, False)
+        g1 = run(*saved)
+    finally:
+        cn._HEAD_CE, cn._DEFER = saved
+    for a, b in zip(g0, g1):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
