@@ -1205,15 +1205,15 @@ __global__ __launch_bounds__(256) void fc_bwd_kernel(const bf16* __restrict__ a3
 //          to the z2 position its pool2 code names (F2 forward) -> dz2 [B,11,11,64];
 //   wgrad: dW3t[n = tap*64 + ci][co] = sum_k D3[k][co] * a2[pos(k) + tap][ci], a workgroup pair per
 //          image slice (one half of the 576 n columns each).  db3 comes from fc1's backward.
-// Padded d(conv3) image (12x12 positions, 8x8 interior, ring of 2 zeros) in LDS: position (Y, X) at
-// Y*C3_PY + X*C3_PX bf16.  These strides (tools/scratch/lds_bank_model_conv3.py: 288-B positions, 3648-B rows)
-// make every B-fragment read of the dgrad GEMM conflict-free (4 LDS cycles per ds_read_b128, was 7.7
-// with 136-element rows) while each read stays a per-lane base plus an immediate tap offset.
+// d(conv3) image in LDS with two zero rows above and below (12 rows x 8 columns): position (Y, X) at
+// Y*C3_PY + X*C3_PX bf16.  288-B positions and unpadded 2304-B rows make every B-fragment read of the
+// dgrad GEMM (lanes = 2 rows x 8 columns of one 16-B channel chunk) conflict-free: 4 LDS cycles per
+// ds_read_b128 (tools/lds_bank_model.py; the 12x12 ring layout with 3648-B rows read these in 8).
 constexpr int C3_PX = 144;   // bf16 per position (128 + 16)
-constexpr int C3_PY = 1824;  // bf16 per row of positions (12 * 144 + 96)
+constexpr int C3_PY = 1152;  // bf16 per row of positions (8 * 144)
 constexpr int C3_DARS = 68;  // floats per da2 row (64 + 4)
 constexpr int C3_DRS = 136;  // bf16 per D3 row in LDS
-constexpr int C3D_P = (11 * C3_PY + 11 * C3_PX + 128) * 2;  // 43552
+constexpr int C3D_P = 12 * C3_PY * 2;                       // 27648
 constexpr int C3D_AM = 100 * 64;                            // 6400: pool2 codes of the current image
 constexpr int C3D_DA = 100 * C3_DARS * 4;                   // 27200
 constexpr int C3D_LDS = C3D_P + C3D_AM + C3D_DA;
@@ -1334,16 +1334,16 @@ __device__ __forceinline__ void codes_glds(const uint8_t* __restrict__ idx2, int
   }
 }
 
-// dgrad per image in scatter form (the transpose of the forward conv, without its zero taps):
-//   Y[ci][(tap, p)] = sum_co W3[co][ci][tap] * dz3[p][co],   da2[p + off(tap)][ci] += Y[ci][(tap, p)]
-// over the 64 positions p of the 8x8 dz3 image, K = 128 output channels: 9 x 4 x 4 = 144 MFMAs per wave
-// (the full correlation over the 10x10 a2 image with the 3x3 flipped kernel needed 252: 900 (position,
-// tap) pairs of which only 576 are non-zero, padded to 7 m-tiles).  Operands are swapped so a lane's 4
-// results are 4 consecutive input channels of one position: wave w owns input channels 16w..16w+15,
-// so its col2im accumulation into the fp32 da2 image never meets another wave's.  Per tap, the 4
-// m-tiles (dz3 row pairs) hit disjoint da2 rows, so their read-add-writes are independent; consecutive
-// taps may hit the same da2 words from different lanes, so a compiler barrier keeps tap t+1's reads
-// behind tap t's writes (LDS executes one wave's instructions in order).  Fixed order: deterministic.
+// dgrad per image, gathered over kernel rows and scattered over kernel columns:
+//   da2[y'][x + kx][ci] += sum_{ky, co} W3[co][ci][ky][kx] * dz3[y' - ky][x][co]
+// over the 8 dz3 columns x and the 10 da2 rows y', K = 128 output channels (the full correlation over
+// the 10x10 a2 image with the 3x3 flipped kernel needed 252 MFMAs per wave: 900 (position, tap) pairs
+// of which only 576 are non-zero; the pure scatter form 144 plus a col2im read-add-write per tap).
+// Operands are swapped so a lane's 4 results are 4 consecutive input channels of one position: wave w
+// owns input channels 16w..16w+15, so its col2im into the fp32 da2 image never meets another wave's.
+// The kx taps of an m-tile hit the same da2 words from different lanes, so a compiler barrier keeps
+// each read behind the previous write (LDS executes one wave's instructions in order).  Fixed order:
+// deterministic.
 template <bool kFC>
 __device__ __forceinline__ void conv3_dgrad_role(char* smem, const C3Src& src, const uint8_t* __restrict__ idx3,
                                  const uint8_t* __restrict__ idx2, const bf16* __restrict__ packed,
@@ -1357,44 +1357,45 @@ __device__ __forceinline__ void conv3_dgrad_role(char* smem, const C3Src& src, c
   bf16x8 aw[36];  // [tap][kstep] weight fragments of this wave's 16 input channels
 #pragma unroll
   for (int j = 0; j < 36; ++j) aw[j] = pk[(wave * 36 + j) * 64 + lane];
-  // dz3 position p = 16 mt + r16 = (2 mt + (r16 >> 3), r16 & 7); its tap-(0,0) da2 target is p's (y, x)
-  const int pbase = ((r16 >> 3) + 2) * C3_PY + ((r16 & 7) + 2) * C3_PX + q8;
+  // lane r16 of m-tile mt: da2 row 2 mt + (r16 >> 3), dz3 column r16 & 7 (its kx = 0 da2 column)
+  const int pbase = ((r16 >> 3) + 2) * C3_PY + (r16 & 7) * C3_PX + q8;
   const int dbase = ((r16 >> 3) * 10 + (r16 & 7)) * C3_DARS + 16 * wave + c4;
-  // the ring of the padded image stays zero; only the 8x8 interior is rewritten per image
+  // the zero rows of the image stay zero; only the 8x8 interior is rewritten per image
   for (int c = tid; c < C3D_P / 16; c += 256) reinterpret_cast<bf16x8*>(P)[c] = zero_bf16x8();
+  // Gather over the kernel row ky, scatter over the kernel column kx.  Output m-tile mt = da2 rows
+  // 2mt, 2mt+1 at the 8 dz3 columns x: for each ky the B fragments are the dz3 rows y' - ky (a row
+  // offset into the zero-ringed image), and the three kx taps accumulate in three register tiles that
+  // land on da2 columns x, x+1, x+2.  13 (mt, ky) pairs hold a non-zero row (mt 0 has no ky 2, mt 4
+  // no ky 0): 156 MFMAs per wave (pure scatter: 144), but the fp32 col2im is one store + two
+  // read-add-writes per m-tile (15 + 10 per wave) instead of a read-add-write per tap (72 + 72): the
+  // 13-cycle ds_write_b128 traffic of that col2im had been as long as the MFMA stream itself.
+  const int xcol = r16 & 7;
   auto mfma_phase = [&]() {
-    for (int i = lane; i < 400; i += 64)  // this wave's 16-channel slice of da2
-      *reinterpret_cast<f32x4*>(DA + (i >> 2) * C3_DARS + 16 * wave + 4 * (i & 3)) = zero_f32x4();
-    // two m-tiles (4 dz3 rows) at a time keeps the B fragments at 32 VGPRs beside the 144 of weights
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      bf16x8 bfr[2][4];
+    for (int mt = 0; mt < 5; ++mt) {
+      f32x4 acc[3] = {zero_f32x4(), zero_f32x4(), zero_f32x4()};
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int ky = 0; ky < 3; ++ky) {
+        if ((mt == 0 && ky == 2) || (mt == 4 && ky == 0)) continue;  // both rows in the zero ring
+        bf16x8 bfr[4];
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
-          bfr[m][ks] = *reinterpret_cast<const bf16x8*>(P + pbase + 2 * (2 * half + m) * C3_PY + ks * 32);
+          bfr[ks] = *reinterpret_cast<const bf16x8*>(P + pbase + (2 * mt - ky) * C3_PY + ks * 32);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        f32x4 acc[2];
+        for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          acc[m] = zero_f32x4();
+          for (int kx = 0; kx < 3; ++kx) acc[kx] = mfma16x16x32(aw[(3 * ky + kx) * 4 + ks], bfr[ks], acc[kx]);
+      }
+      // da2 column x + kx; the lanes of column 7 open columns 8 (kx 1) and 9 (kx 2), which no earlier
+      // tap of this image wrote: they add to zero instead of the previous image's value
+      f32x4* d = reinterpret_cast<f32x4*>(DA + dbase + 20 * mt * C3_DARS);
+      *d = acc[0];
 #pragma unroll
-          for (int ks = 0; ks < 4; ++ks) acc[m] = mfma16x16x32(aw[tap * 4 + ks], bfr[m][ks], acc[m]);
-        }
-        f32x4* d[2];
-        f32x4 old[2];
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          d[m] = reinterpret_cast<f32x4*>(DA + dbase + (20 * (2 * half + m) + (tap / 3) * 10 + tap % 3) * C3_DARS);
-          old[m] = *d[m];
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          *d[m] = old[m] + acc[m];
-        }
-        asm volatile("" ::: "memory");  // the next tap's reads stay behind these writes
+      for (int kx = 1; kx < 3; ++kx) {
+        asm volatile("" ::: "memory");  // the read below stays behind the other lanes' write above
+        f32x4 old = d[kx * (C3_DARS / 4)];
+        if (xcol == 7) old = zero_f32x4();
+        d[kx * (C3_DARS / 4)] = old + acc[kx];
       }
     }
   };
@@ -1418,7 +1419,7 @@ __device__ __forceinline__ void conv3_dgrad_role(char* smem, const C3Src& src, c
     __syncthreads();  // previous image fully consumed (P, DA, AM)
     c3_expand(pre, tid, [&](int r) {
       const int w = r >> 2, i = r & 3;
-      return P + (2 * (w >> 2) + (i >> 1) + 2) * C3_PY + (2 * (w & 3) + (i & 1) + 2) * C3_PX;
+      return P + (2 * (w >> 2) + (i >> 1) + 2) * C3_PY + (2 * (w & 3) + (i & 1)) * C3_PX;
     });
     codes_glds(idx2, b, AM, wave, lane);  // this image's codes land during the MFMA phase
     const int nb = b + b_step;
