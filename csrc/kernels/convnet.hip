@@ -1573,6 +1573,311 @@ __global__ __launch_bounds__(256, kFC ? 1 : 2) void conv3_bwd_kernel(const bf16*
   conv3_dgrad_role<kFC>(smem, src, idx3, idx2, packed, dz2, b_first, b_end, b_step);  // one call site: inlined
 }
 
+// ---- conv3 backward with 8-wave workgroups (batches above fc_in_c3_max_batch: the fc1 backward launch
+// leaves the compact gradient da3m).  One 512-thread workgroup per CU, in one of two roles:
+//   dgrad, wave-specialised: waves 0-3 hold the conv3 weights and only run image s's dgrad MFMAs and
+//     col2im (P[s&1] -> DA[s&1]); beside them waves 4-7 run the pool2 + ReLU backward of image s-1
+//     (DA, codes -> dz2), expand image s+1's compact gradient (stage -> P) and issue the LDS-DMA of
+//     later images.  One barrier per image: every buffer is written in one step and read in the next,
+//     so P, DA, the codes and the compact stage are double-buffered.  The 4-wave role above ran these
+//     phases one after the other, each behind a barrier of all four waves.
+//   wgrad: 8 waves cover the whole 128 x 576 dW3t of their image slice (36 tiles each, 2 x 4 waves), so
+//     an image is staged once (the 4-wave role needs a workgroup pair, each staging every image); image
+//     i+1's operands (compact gradient -> D, a2 -> X by LDS-DMA straight into the padded rows) are staged
+//     while image i's MFMAs run.
+// All global -> LDS traffic is LDS-DMA from inline asm (invisible to the compiler's vmcnt bookkeeping),
+// waited for explicitly before the barrier; the dz2 stores stay in flight across it.
+constexpr int C3S_B = 2048 * 2 + 2048;  // compact stage of one image: da3m row (bf16) + pool3 argmax bytes
+constexpr int C3V_DG = 2 * (C3D_P + C3D_DA + C3D_AM + C3S_B);  // 134784
+constexpr int C3V_WG = 2 * (C3W_D + C3W_X + C3S_B);             // 75904
+constexpr int C3V_LDS = C3V_DG > C3V_WG ? C3V_DG : C3V_WG;
+static_assert(C3V_LDS <= 160 * 1024 && C3D_DA % 16 == 0 && C3W_X % 16 == 0 && C3_XRS == 72,
+              "conv3 backward (8-wave) LDS");
+
+// barrier for LDS hand-offs: this wave's LDS operations drained, global stores left in flight (the release
+// fence of __syncthreads() would also wait for those)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// wave-instruction k (0..5) of the compact stage of image b: da3m row (4 KiB), then the argmax bytes (2 KiB)
+__device__ __forceinline__ void c3s_glds(const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3, int b,
+                                         char* S, int k, int lane) {
+  if (k < 4)
+    glds16_async(da3m + (int64_t)b * 2048 + (k * 64 + lane) * 8, S + k * 1024);
+  else
+    glds16_async(idx3 + (int64_t)b * 2048 + ((k - 4) * 64 + lane) * 16, S + k * 1024);
+}
+
+__device__ __forceinline__ void c3s_pre(const char* S, int tid, C3Pre& p) {
+  if (tid < 256) {
+    p.da = reinterpret_cast<const bf16x8*>(S)[tid];
+    p.id = reinterpret_cast<const uint2*>(S + 4096)[tid];
+  }
+}
+
+// wave-instruction k (0..14) of the a2 image b straight into C3_XRS rows: 9 16-B chunks per row, lane-linear
+// in LDS; chunk 8 of a row is its padding and re-reads the row's chunk 0
+__device__ __forceinline__ void a2_glds_rows(const bf16* __restrict__ a2, int b, bf16* X, int k, int lane) {
+  const int c = k * 64 + lane;
+  if (c < 900) {
+    const int row = c / 9, sub = c - 9 * row;
+    glds16_async(a2 + (int64_t)b * 6400 + row * 64 + (sub < 8 ? sub * 8 : 0), X + k * 512);
+  }
+}
+
+// pool2 + ReLU backward of one image (threads t < 176: output row t >> 4, channel quad (t & 15) * 4), as
+// in conv3_dgrad_role
+__device__ __forceinline__ void c3_pool2_bwd(const float* DA, const uint8_t* AM, bf16* __restrict__ dz2, int b,
+                                             int t) {
+  const int gy = t >> 4, gq = (t & 15) * 4;
+  const int rowA = min(gy, 9), rowB = max(gy - 1, 0);
+  const int sA = gy <= 9 ? 0 : 4, sB = gy >= 1 ? 2 : 4;
+  auto masked_add = [](f32x4& g, uint32_t cw, int sh, const f32x4& d) {
+    const uint32_t m = (cw >> sh) & 0x01010101u;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = fmaf(d[j], (float)((m >> (8 * j)) & 0xffu), g[j]);
+  };
+  const uint32_t* cA = reinterpret_cast<const uint32_t*>(AM + rowA * 640 + gq);
+  const uint32_t* cB = reinterpret_cast<const uint32_t*>(AM + rowB * 640 + gq);
+  const f32x4* dA = reinterpret_cast<const f32x4*>(DA + rowA * 10 * C3_DARS + gq);
+  const f32x4* dB = reinterpret_cast<const f32x4*>(DA + rowB * 10 * C3_DARS + gq);
+  bf16x4* dst = reinterpret_cast<bf16x4*>(dz2 + ((int64_t)b * 121 + gy * 11) * 64 + gq);
+  uint32_t pa = 0, pb = 0;
+  f32x4 qa = zero_f32x4(), qb = zero_f32x4();
+#pragma unroll
+  for (int x = 0; x < 11; ++x) {
+    uint32_t na = 0, nb2 = 0;
+    f32x4 ea = zero_f32x4(), eb = zero_f32x4();
+    if (x < 10) {
+      na = cA[x * 16];
+      nb2 = cB[x * 16];
+      ea = dA[x * (C3_DARS / 4)];
+      eb = dB[x * (C3_DARS / 4)];
+    }
+    f32x4 g = zero_f32x4();
+    if (x < 10) masked_add(g, na, sA, ea);
+    if (x > 0) masked_add(g, pa, sA + 1, qa);
+    if (x < 10) masked_add(g, nb2, sB, eb);
+    if (x > 0) masked_add(g, pb, sB + 1, qb);
+    dst[x * 16] = bf16x4{(bf16)g[0], (bf16)g[1], (bf16)g[2], (bf16)g[3]};
+    pa = na;
+    pb = nb2;
+    qa = ea;
+    qb = eb;
+  }
+}
+
+__device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __restrict__ da3m,
+                                                  const uint8_t* __restrict__ idx3, const uint8_t* __restrict__ idx2,
+                                                  const bf16* __restrict__ packed, bf16* __restrict__ dz2, int b_first,
+                                                  int b_end, int b_step) {
+  auto Pb = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3D_P); };
+  auto DAb = [&](int k) { return reinterpret_cast<float*>(smem + 2 * C3D_P + k * C3D_DA); };
+  auto AMb = [&](int k) { return reinterpret_cast<uint8_t*>(smem + 2 * (C3D_P + C3D_DA) + k * C3D_AM); };
+  auto Sb = [&](int k) { return smem + 2 * (C3D_P + C3D_DA + C3D_AM) + k * C3S_B; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = b_first < b_end ? (b_end - b_first + b_step - 1) / b_step : 0;
+  // the zero rows of both dz3 images stay zero; the interiors are rewritten per image
+  for (int c = tid; c < 2 * C3D_P / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
+  if (wave < 4) {
+    // ---- MFMA waves: wave w owns input channels 16w..16w+15 (as conv3_dgrad_role)
+    const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
+    const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P3D_OFF);
+    bf16x8 aw[36];
+#pragma unroll
+    for (int j = 0; j < 36; ++j) aw[j] = pk[(wave * 36 + j) * 64 + lane];
+    const int pbase = ((r16 >> 3) + 2) * C3_PY + (r16 & 7) * C3_PX + q8;
+    const int dbase = ((r16 >> 3) * 10 + (r16 & 7)) * C3_DARS + 16 * wave + c4;
+    const int xcol = r16 & 7;
+    lds_barrier();  // [B0] zero rows
+    lds_barrier();  // [B1] image 0 expanded
+    for (int s = 0; s <= n; ++s) {
+      if (s < n) {
+        const bf16* P = Pb(s & 1);
+        float* DA = DAb(s & 1);
+#pragma unroll
+        for (int mt = 0; mt < 5; ++mt) {
+          f32x4 acc[3] = {zero_f32x4(), zero_f32x4(), zero_f32x4()};
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            if ((mt == 0 && ky == 2) || (mt == 4 && ky == 0)) continue;
+            bf16x8 bfr[4];
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+              bfr[ks] = *reinterpret_cast<const bf16x8*>(P + pbase + (2 * mt - ky) * C3_PY + ks * 32);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+              for (int kx = 0; kx < 3; ++kx) acc[kx] = mfma16x16x32(aw[(3 * ky + kx) * 4 + ks], bfr[ks], acc[kx]);
+          }
+          f32x4* d = reinterpret_cast<f32x4*>(DA + dbase + 20 * mt * C3_DARS);
+          *d = acc[0];
+#pragma unroll
+          for (int kx = 1; kx < 3; ++kx) {
+            asm volatile("" ::: "memory");
+            f32x4 old = d[kx * (C3_DARS / 4)];
+            if (xcol == 7) old = zero_f32x4();
+            d[kx * (C3_DARS / 4)] = old + acc[kx];
+          }
+        }
+      }
+      lds_barrier();
+    }
+  } else {
+    // ---- VALU waves: thread vt of 256; wave 7 issues every LDS-DMA (it has no pool2 items, so its
+    // vmcnt covers exactly its DMAs)
+    const int vt = tid - 256;
+    const bool dma = wave == 7;
+    auto row_ptr = [&](bf16* P) {
+      return [P](int r) {
+        const int w = r >> 2, i = r & 3;
+        return P + (2 * (w >> 2) + (i >> 1) + 2) * C3_PY + (2 * (w & 3) + (i & 1)) * C3_PX;
+      };
+    };
+    if (dma && n > 0) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) c3s_glds(da3m, idx3, b_first, Sb(0), k, lane);
+      if (n > 1) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) c3s_glds(da3m, idx3, b_first + b_step, Sb(1), k, lane);
+      }
+      c_dma_wait();
+    }
+    lds_barrier();  // [B0]
+    if (n > 0) {
+      C3Pre pre;
+      c3s_pre(Sb(0), vt, pre);
+      c3_expand(pre, vt, row_ptr(Pb(0)));
+    }
+    lds_barrier();  // [B1]
+    for (int s = 0; s <= n; ++s) {
+      if (dma) {
+        if (s + 2 < n) {
+#pragma unroll
+          for (int k = 0; k < 6; ++k) c3s_glds(da3m, idx3, b_first + (s + 2) * b_step, Sb(s & 1), k, lane);
+        }
+        if (s < n) {
+          const uint8_t* src = idx2 + (int64_t)(b_first + s * b_step) * 6400;
+          uint8_t* AM = AMb(s & 1);
+#pragma unroll
+          for (int k = 0; k < 7; ++k)
+            if (k * 64 + lane < 400) glds16_async(src + (k * 64 + lane) * 16, AM + k * 1024);
+        }
+      }
+      if (s + 1 < n) {
+        C3Pre pre;
+        c3s_pre(Sb((s + 1) & 1), vt, pre);
+        c3_expand(pre, vt, row_ptr(Pb((s + 1) & 1)));
+      }
+      if (s >= 1 && vt < 176) c3_pool2_bwd(DAb((s - 1) & 1), AMb((s - 1) & 1), dz2, b_first + (s - 1) * b_step, vt);
+      if (dma) c_dma_wait();
+      lds_barrier();
+    }
+  }
+}
+
+__device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
+                                                  const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
+                                                  int nslices, int slice) {
+  auto Db = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3W_D); };
+  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C3W_D + k * C3W_X); };
+  auto Sb = [&](int k) { return smem + 2 * (C3W_D + C3W_X) + k * C3S_B; };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;  // m-tiles (co) 4wm..4wm+3, n-tiles 9wn..9wn+8
+  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) acc[i][j] = zero_f32x4();
+  const int per = cdiv(B, nslices);
+  const int b_lo = slice * per, n = max(0, min(B, b_lo + per) - b_lo);
+  if (n > 0) {  // prologue: image 0 staged (D0, X0), image 1's compact gradient in S1
+    if (wave < 6) {
+      c3s_glds(da3m, idx3, b_lo, Sb(0), wave, lane);
+      if (n > 1) c3s_glds(da3m, idx3, b_lo + 1, Sb(1), wave, lane);
+    }
+    for (int k = wave; k < 15; k += 8) a2_glds_rows(a2, b_lo, Xb(0), k, lane);
+    c_dma_wait();
+    lds_barrier();
+    C3Pre pre;
+    c3s_pre(Sb(0), tid, pre);
+    c3_expand(pre, tid, [&](int r) { return Db(0) + r * C3_DRS; });
+  }
+  lds_barrier();
+  for (int i = 0; i < n; ++i) {
+    const int cur = i & 1, nxt = cur ^ 1, b = b_lo + i;
+    if (i + 1 < n)
+      for (int k = wave; k < 15; k += 8) a2_glds_rows(a2, b + 1, Xb(nxt), k, lane);
+    if (i + 2 < n && wave < 6) c3s_glds(da3m, idx3, b + 2, Sb(cur), wave, lane);
+    const bf16* D = Db(cur);
+    const bf16* X = Xb(cur);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int kb = ks * 32 + grp * 8;
+      bf16x8 af[4];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int m0 = (4 * wm + mi) * 16;
+        const bf16x4 lo = lds_read_tr16(D + (kb + q) * C3_DRS + m0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(D + (kb + 4 + q) * C3_DRS + m0 + 4 * p);
+        af[mi] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int x0 = win_pos(kb + q, 10), x1 = win_pos(kb + 4 + q, 10);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) {
+        const int n0 = (9 * wn + j) * 16;  // n = tap*64 + ci
+        const int tap = n0 >> 6, c0 = n0 & 63;
+        const int shift = (tap / 3) * 10 + tap % 3;
+        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3_XRS + c0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C3_XRS + c0 + 4 * p);
+        const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[mi][j] = mfma16x16x32(af[mi], bf, acc[mi][j]);
+      }
+      if (ks == 0 && i + 1 < n) {  // image i+1's D between the two k-steps: the writes go out under MFMAs
+        C3Pre pre;
+        c3s_pre(Sb(nxt), tid, pre);
+        bf16* Dn = Db(nxt);
+        c3_expand(pre, tid, [&](int r) { return Dn + r * C3_DRS; });
+      }
+    }
+    c_dma_wait();
+    lds_barrier();
+  }
+  float* slab = slabs + (int64_t)slice * C3_WSLAB;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int co = (4 * wm + mi) * 16 + grp * 4;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int nn = (9 * wn + j) * 16 + g16;
+      *reinterpret_cast<f32x4*>(slab + (int64_t)nn * 128 + co) = acc[mi][j];
+    }
+  }
+}
+
+// blocks [0, n_dgrad): dgrad of images [0, b_dgrad) (strided); then n_wgrad wgrad slices, whose workgroups
+// go on to the dgrad of images [b_dgrad, B) (static split: deterministic)
+__global__ __launch_bounds__(512, 1) void conv3_bwd8_kernel(const bf16* __restrict__ a2, const uint8_t* __restrict__ idx2,
+                                                           const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
+                                                           const bf16* __restrict__ packed, bf16* __restrict__ dz2,
+                                                           int B, float* __restrict__ slabs, int n_wgrad, int n_dgrad,
+                                                           int b_dgrad) {
+  __shared__ __attribute__((aligned(16))) char smem[C3V_LDS];
+  const int blk = blockIdx.x;
+  if (blk < n_dgrad) {
+    conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, blk, b_dgrad, n_dgrad);
+    return;
+  }
+  const int w = blk - n_dgrad;
+  conv3_wgrad8_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w);
+  if (dz2 == nullptr || b_dgrad >= B) return;
+  __syncthreads();  // LDS changes role
+  conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, b_dgrad + w, B, n_wgrad);
+}
+
 __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
   const bf16 one = (bf16)((lane & 15) == 0 ? 1.f : 0.f);
   return bf16x8{one, one, one, one, one, one, one, one};
@@ -2345,9 +2650,31 @@ static int min_slab_images(const char* env, int dflt) {
   return n >= 1 && n <= 64 ? n : dflt;
 }
 
-// dgrad and wgrad do the same MFMA work per image since the scatter-form dgrad (576 each per
-// workgroup image / image pair); measured best split 0.5-0.6 of the workgroup slots (B=32768).
+// 8-wave conv3 backward (conv3_bwd8_kernel): batches above fc_in_c3_max_batch, RINGDP_C3_V3=0 keeps the
+// 4-wave kernel (A/B)
+static bool c3_v3(int B) {
+  static const bool on = [] {
+    const char* v = getenv("RINGDP_C3_V3");
+    return !(v && v[0] == '0');
+  }();
+  return on && B > fc_in_c3_max_batch();
+}
+
+// dgrad and wgrad do about the same MFMA work per image (624 / 576 MFMAs); measured best split 0.5-0.6 of
+// the workgroup slots (B=32768).
 static void c3_split(int B, bool dgrad, int& nd, int& ws) {
+  if (c3_v3(B)) {  // one 512-thread workgroup per CU; ws = wgrad slices, one workgroup each
+    const int cus = num_cus();
+    if (!dgrad) {
+      nd = 0;
+      ws = clampi(cdiv(B, 8), 1, cus);
+      return;
+    }
+    static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.55);
+    nd = clampi((int)(frac * cus), 1, cus - 1);
+    ws = clampi(cdiv(B, 8), 1, cus - nd);
+    return;
+  }
   // 256-thread workgroups, two per CU; ws = image slices, each served by a pair of workgroups
   const int slots = 2 * num_cus();
   if (!dgrad) {
@@ -2448,10 +2775,15 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
       fc_bwd_kernel<true><<<fs, 256, 0, s>>>(a3b, pk, nullptr, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs_host(B), cef);
     else
       fc_bwd_kernel<false><<<fs, 256, 0, s>>>(a3b, pk, dl, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs_host(B), cef);
-    const C3Src src{static_cast<const bf16*>(da3m), a3b, pk, dl, cef};
-    conv3_bwd_kernel<false><<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
+    if (c3_v3(B)) {
+      conv3_bwd8_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m), idx3,
+                                               pk, static_cast<bf16*>(dz2), B, c3_slabs, ws, nd, c3_dgrad_images(B, nd));
+    } else {
+      const C3Src src{static_cast<const bf16*>(da3m), a3b, pk, dl, cef};
+      conv3_bwd_kernel<false><<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
                                                          static_cast<bf16*>(dz2), B, c3_slabs, ws, nd,
                                                          c3_dgrad_images(B, nd), 0, nullptr, 0);
+    }
   }
   ReduceList r{seg(c3_slabs, C3_WSLAB, 0, 576 * 128, ws, dw3, 1, 64, 128),
                seg(fc_slabs, FC_SLAB, 20490, 128, fs, db3), seg(fc_slabs, FC_SLAB, 0, 20480, fs, dwfc, 2),

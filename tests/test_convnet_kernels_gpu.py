@@ -179,7 +179,9 @@ def test_conv3_fc_forward(B):
     assert int(idx3.max()) <= 3
 
 
-@pytest.mark.parametrize("B", [1, 3, 64, 257])
+# 3000 / 9000: above fc_in_c3_max_batch, the 8-wave conv3 backward (dgrad and wgrad workgroups, the wgrad
+# ones taking the last images of the data gradient)
+@pytest.mark.parametrize("B", [1, 3, 64, 257, 3000, 9000])
 @pytest.mark.parametrize("need_dz2", [True, False])
 def test_conv3_fc_backward(B, need_dz2):
     torch.manual_seed(7 + B)
@@ -195,8 +197,9 @@ def test_conv3_fc_backward(B, need_dz2):
     dz2 = C().cn_conv3_fc_bwd(a2, idx2, a3, idx3, wf, dl, pk, need_dz2, dw3, db3, dwf, dbf)
     # reference: fc backward in fp32, unpool through the kernel's own pool3 argmax
     a3_flat = a3.view(B, 4, 4, 128).permute(0, 3, 1, 2).reshape(B, 2048).float()
-    torch.testing.assert_close(dwf, dl.t() @ a3_flat, rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(dbf, dl.sum(0), rtol=1e-5, atol=1e-5)
+    tol = 1e-4 * max(1.0, (B / 256) ** 0.5)  # fp32 sums over B images in a different order than the matmul
+    torch.testing.assert_close(dwf, dl.t() @ a3_flat, rtol=1e-4, atol=tol)
+    torch.testing.assert_close(dbf, dl.sum(0), rtol=1e-5, atol=tol / 10)
     da3 = (dl @ wf).view(B, 128, 4, 4).permute(0, 2, 3, 1)
     dconv = bf(unpool2x2(da3, idx3.view(B, 4, 4, 128), a3.view(B, 4, 4, 128), 8)).permute(0, 3, 1, 2)
     z2f = z2.permute(0, 3, 1, 2).float().requires_grad_()
