@@ -1587,12 +1587,40 @@ __global__ __launch_bounds__(256, kFC ? 1 : 2) void conv3_bwd_kernel(const bf16*
 //     while image i's MFMAs run.
 // All global -> LDS traffic is LDS-DMA from inline asm (invisible to the compiler's vmcnt bookkeeping),
 // waited for explicitly before the barrier; the dz2 stores stay in flight across it.
+// LDS layouts (every fragment read, col2im access and pool2 read modelled conflict-free with the lane
+// groups of MI355X_MICROARCH.md; the 4-wave kernel's layouts measured 30-46 % bank-conflict cycles):
+//   da2 (fp32): 256-B position rows, the 16-B chunk k of position (y, x) at slot k ^ 2(x & 7);
+//   D (wgrad): rows of 144 bf16 in blocks of 8 rows, 1216 bf16 per block (tr16 reads of rows k..k+3 and
+//     k+8..k+11 then cover the 64 banks once);  X (wgrad): a2 rows of 80 bf16 (10 16-B chunks).
 constexpr int C3S_B = 2048 * 2 + 2048;  // compact stage of one image: da3m row (bf16) + pool3 argmax bytes
-constexpr int C3V_DG = 2 * (C3D_P + C3D_DA + C3D_AM + C3S_B);  // 134784
-constexpr int C3V_WG = 2 * (C3W_D + C3W_X + C3S_B);             // 75904
+constexpr int C3V_DA = 100 * 64 * 4;    // 25600
+constexpr int C3V_D = 8 * 1216 * 2;     // 19456
+constexpr int C3V_XRS = 80;
+constexpr int C3V_X = 100 * C3V_XRS * 2;  // 16000
+constexpr int C3V_DG = 2 * (C3D_P + C3V_DA + C3D_AM + C3S_B);  // 131584
+constexpr int C3V_WG = 2 * (C3V_D + C3V_X + C3S_B);            // 83200
 constexpr int C3V_LDS = C3V_DG > C3V_WG ? C3V_DG : C3V_WG;
-static_assert(C3V_LDS <= 160 * 1024 && C3D_DA % 16 == 0 && C3W_X % 16 == 0 && C3_XRS == 72,
-              "conv3 backward (8-wave) LDS");
+static_assert(C3V_LDS <= 160 * 1024 && C3V_D % 16 == 0 && C3V_X % 16 == 0, "conv3 backward (8-wave) LDS");
+__device__ __forceinline__ int c3v_drow(int r) { return (r >> 3) * 1216 + (r & 7) * 144; }
+// float offset of 16-B chunk k (channels 4k..4k+3) of da2 position p = y * 10 + x
+__device__ __forceinline__ int c3v_da(int p, int x, int k) { return p * 64 + ((k ^ (2 * (x & 7))) << 2); }
+// exact 0.0 / 1.0 of byte J of v (one v_cvt_f32_ubyteJ; the compiler's form of (v >> 8J) & 0xff was a shift,
+// an and and v_cvt_f32_ubyte0 per byte)
+template <int J>
+__device__ __forceinline__ float ubyte_f32(uint32_t v) {
+  float r;
+  if constexpr (J == 0) asm("v_cvt_f32_ubyte0 %0, %1" : "=v"(r) : "v"(v));
+  else if constexpr (J == 1) asm("v_cvt_f32_ubyte1 %0, %1" : "=v"(r) : "v"(v));
+  else if constexpr (J == 2) asm("v_cvt_f32_ubyte2 %0, %1" : "=v"(r) : "v"(v));
+  else asm("v_cvt_f32_ubyte3 %0, %1" : "=v"(r) : "v"(v));
+  return r;
+}
+
+// v shifted right by N lanes inside each 16-lane DPP row (0 into the row's first N lanes)
+template <int N>
+__device__ __forceinline__ float dpp_row_shr(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x110 + N, 0xf, 0xf, true));
+}
 
 // barrier for LDS hand-offs: this wave's LDS operations drained, global stores left in flight (the release
 // fence of __syncthreads() would also wait for those)
@@ -1614,32 +1642,32 @@ __device__ __forceinline__ void c3s_pre(const char* S, int tid, C3Pre& p) {
   }
 }
 
-// wave-instruction k (0..14) of the a2 image b straight into C3_XRS rows: 9 16-B chunks per row, lane-linear
-// in LDS; chunk 8 of a row is its padding and re-reads the row's chunk 0
+// wave-instruction k (0..15) of the a2 image b straight into C3V_XRS rows: 10 16-B chunks per row, lane-linear
+// in LDS; chunks 8, 9 of a row are its padding and re-read the row's first chunks
 __device__ __forceinline__ void a2_glds_rows(const bf16* __restrict__ a2, int b, bf16* X, int k, int lane) {
   const int c = k * 64 + lane;
-  if (c < 900) {
-    const int row = c / 9, sub = c - 9 * row;
-    glds16_async(a2 + (int64_t)b * 6400 + row * 64 + (sub < 8 ? sub * 8 : 0), X + k * 512);
+  if (c < 1000) {
+    const int row = c / 10, sub = c - 10 * row;
+    glds16_async(a2 + (int64_t)b * 6400 + row * 64 + (sub & 7) * 8, X + k * 512);
   }
 }
 
-// pool2 + ReLU backward of one image (threads t < 176: output row t >> 4, channel quad (t & 15) * 4), as
-// in conv3_dgrad_role
+// pool2 + ReLU backward of one image (threads t < 176: output row t >> 4, channel quad t & 15), as in
+// conv3_dgrad_role, from the swizzled da2 image
 __device__ __forceinline__ void c3_pool2_bwd(const float* DA, const uint8_t* AM, bf16* __restrict__ dz2, int b,
                                              int t) {
-  const int gy = t >> 4, gq = (t & 15) * 4;
+  const int gy = t >> 4, k = t & 15, gq = k * 4;
   const int rowA = min(gy, 9), rowB = max(gy - 1, 0);
   const int sA = gy <= 9 ? 0 : 4, sB = gy >= 1 ? 2 : 4;
   auto masked_add = [](f32x4& g, uint32_t cw, int sh, const f32x4& d) {
     const uint32_t m = (cw >> sh) & 0x01010101u;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) g[j] = fmaf(d[j], (float)((m >> (8 * j)) & 0xffu), g[j]);
+    g[0] = fmaf(d[0], ubyte_f32<0>(m), g[0]);
+    g[1] = fmaf(d[1], ubyte_f32<1>(m), g[1]);
+    g[2] = fmaf(d[2], ubyte_f32<2>(m), g[2]);
+    g[3] = fmaf(d[3], ubyte_f32<3>(m), g[3]);
   };
   const uint32_t* cA = reinterpret_cast<const uint32_t*>(AM + rowA * 640 + gq);
   const uint32_t* cB = reinterpret_cast<const uint32_t*>(AM + rowB * 640 + gq);
-  const f32x4* dA = reinterpret_cast<const f32x4*>(DA + rowA * 10 * C3_DARS + gq);
-  const f32x4* dB = reinterpret_cast<const f32x4*>(DA + rowB * 10 * C3_DARS + gq);
   bf16x4* dst = reinterpret_cast<bf16x4*>(dz2 + ((int64_t)b * 121 + gy * 11) * 64 + gq);
   uint32_t pa = 0, pb = 0;
   f32x4 qa = zero_f32x4(), qb = zero_f32x4();
@@ -1650,8 +1678,8 @@ __device__ __forceinline__ void c3_pool2_bwd(const float* DA, const uint8_t* AM,
     if (x < 10) {
       na = cA[x * 16];
       nb2 = cB[x * 16];
-      ea = dA[x * (C3_DARS / 4)];
-      eb = dB[x * (C3_DARS / 4)];
+      ea = *reinterpret_cast<const f32x4*>(DA + c3v_da(rowA * 10 + x, x, k));
+      eb = *reinterpret_cast<const f32x4*>(DA + c3v_da(rowB * 10 + x, x, k));
     }
     f32x4 g = zero_f32x4();
     if (x < 10) masked_add(g, na, sA, ea);
@@ -1671,9 +1699,9 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
                                                   const bf16* __restrict__ packed, bf16* __restrict__ dz2, int b_first,
                                                   int b_end, int b_step) {
   auto Pb = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3D_P); };
-  auto DAb = [&](int k) { return reinterpret_cast<float*>(smem + 2 * C3D_P + k * C3D_DA); };
-  auto AMb = [&](int k) { return reinterpret_cast<uint8_t*>(smem + 2 * (C3D_P + C3D_DA) + k * C3D_AM); };
-  auto Sb = [&](int k) { return smem + 2 * (C3D_P + C3D_DA + C3D_AM) + k * C3S_B; };
+  auto DAb = [&](int k) { return reinterpret_cast<float*>(smem + 2 * C3D_P + k * C3V_DA); };
+  auto AMb = [&](int k) { return reinterpret_cast<uint8_t*>(smem + 2 * (C3D_P + C3V_DA) + k * C3D_AM); };
+  auto Sb = [&](int k) { return smem + 2 * (C3D_P + C3V_DA + C3D_AM) + k * C3S_B; };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = b_first < b_end ? (b_end - b_first + b_step - 1) / b_step : 0;
@@ -1687,8 +1715,10 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
 #pragma unroll
     for (int j = 0; j < 36; ++j) aw[j] = pk[(wave * 36 + j) * 64 + lane];
     const int pbase = ((r16 >> 3) + 2) * C3_PY + (r16 & 7) * C3_PX + q8;
-    const int dbase = ((r16 >> 3) * 10 + (r16 & 7)) * C3_DARS + 16 * wave + c4;
-    const int xcol = r16 & 7;
+    const int xcol = r16 & 7, chunk = 4 * wave + (c4 >> 2);
+    // da2 targets of m-tile 0: (row r16 >> 3, column xcol); lanes of column 7 also columns 8 and 9
+    const int dcol = c3v_da((r16 >> 3) * 10 + xcol, xcol, chunk);
+    const int dc8 = c3v_da((r16 >> 3) * 10 + 8, 8, chunk), dc9 = c3v_da((r16 >> 3) * 10 + 9, 9, chunk);
     lds_barrier();  // [B0] zero rows
     lds_barrier();  // [B1] image 0 expanded
     for (int s = 0; s <= n; ++s) {
@@ -1710,14 +1740,21 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
 #pragma unroll
               for (int kx = 0; kx < 3; ++kx) acc[kx] = mfma16x16x32(aw[(3 * ky + kx) * 4 + ks], bfr[ks], acc[kx]);
           }
-          f32x4* d = reinterpret_cast<f32x4*>(DA + dbase + 20 * mt * C3_DARS);
-          *d = acc[0];
+          // col2im along the row in registers: da2(x) = acc0(x) + acc1(x-1) + acc2(x-2), the shifted terms
+          // by DPP row shifts inside each 16-lane group (= 2 dz3 rows x 8 columns; a term that would cross
+          // into the next row is zeroed at its source lane); column 8 = acc1(7) + acc2(6), column 9 =
+          // acc2(7) go out from the column-7 lanes.  One plain store per target, no read-add-write.
+          f32x4 out, e8;
 #pragma unroll
-          for (int kx = 1; kx < 3; ++kx) {
-            asm volatile("" ::: "memory");
-            f32x4 old = d[kx * (C3_DARS / 4)];
-            if (xcol == 7) old = zero_f32x4();
-            d[kx * (C3_DARS / 4)] = old + acc[kx];
+          for (int j = 0; j < 4; ++j) {
+            const float a1 = xcol == 7 ? 0.f : acc[1][j], a2 = xcol >= 6 ? 0.f : acc[2][j];
+            out[j] = (acc[0][j] + dpp_row_shr<1>(a1)) + dpp_row_shr<2>(a2);
+            e8[j] = acc[1][j] + dpp_row_shr<1>(acc[2][j]);
+          }
+          *reinterpret_cast<f32x4*>(DA + dcol + 20 * mt * 64) = out;
+          if (xcol == 7) {
+            *reinterpret_cast<f32x4*>(DA + dc8 + 20 * mt * 64) = e8;
+            *reinterpret_cast<f32x4*>(DA + dc9 + 20 * mt * 64) = acc[2];
           }
         }
       }
@@ -1779,9 +1816,9 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
 __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
                                                   const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
                                                   int nslices, int slice) {
-  auto Db = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3W_D); };
-  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C3W_D + k * C3W_X); };
-  auto Sb = [&](int k) { return smem + 2 * (C3W_D + C3W_X) + k * C3S_B; };
+  auto Db = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3V_D); };
+  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C3V_D + k * C3V_X); };
+  auto Sb = [&](int k) { return smem + 2 * (C3V_D + C3V_X) + k * C3S_B; };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;  // m-tiles (co) 4wm..4wm+3, n-tiles 9wn..9wn+8
@@ -1798,18 +1835,18 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
       c3s_glds(da3m, idx3, b_lo, Sb(0), wave, lane);
       if (n > 1) c3s_glds(da3m, idx3, b_lo + 1, Sb(1), wave, lane);
     }
-    for (int k = wave; k < 15; k += 8) a2_glds_rows(a2, b_lo, Xb(0), k, lane);
+    for (int k = wave; k < 16; k += 8) a2_glds_rows(a2, b_lo, Xb(0), k, lane);
     c_dma_wait();
     lds_barrier();
     C3Pre pre;
     c3s_pre(Sb(0), tid, pre);
-    c3_expand(pre, tid, [&](int r) { return Db(0) + r * C3_DRS; });
+    c3_expand(pre, tid, [&](int r) { return Db(0) + c3v_drow(r); });
   }
   lds_barrier();
   for (int i = 0; i < n; ++i) {
     const int cur = i & 1, nxt = cur ^ 1, b = b_lo + i;
     if (i + 1 < n)
-      for (int k = wave; k < 15; k += 8) a2_glds_rows(a2, b + 1, Xb(nxt), k, lane);
+      for (int k = wave; k < 16; k += 8) a2_glds_rows(a2, b + 1, Xb(nxt), k, lane);
     if (i + 2 < n && wave < 6) c3s_glds(da3m, idx3, b + 2, Sb(cur), wave, lane);
     const bf16* D = Db(cur);
     const bf16* X = Xb(cur);
@@ -1820,8 +1857,8 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int m0 = (4 * wm + mi) * 16;
-        const bf16x4 lo = lds_read_tr16(D + (kb + q) * C3_DRS + m0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(D + (kb + 4 + q) * C3_DRS + m0 + 4 * p);
+        const bf16x4 lo = lds_read_tr16(D + c3v_drow(kb + q) + m0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(D + c3v_drow(kb + 4 + q) + m0 + 4 * p);
         af[mi] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
       const int x0 = win_pos(kb + q, 10), x1 = win_pos(kb + 4 + q, 10);
@@ -1830,8 +1867,8 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
         const int n0 = (9 * wn + j) * 16;  // n = tap*64 + ci
         const int tap = n0 >> 6, c0 = n0 & 63;
         const int shift = (tap / 3) * 10 + tap % 3;
-        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3_XRS + c0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C3_XRS + c0 + 4 * p);
+        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3V_XRS + c0 + 4 * p);
+        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C3V_XRS + c0 + 4 * p);
         const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) acc[mi][j] = mfma16x16x32(af[mi], bf, acc[mi][j]);
@@ -1840,7 +1877,7 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
         C3Pre pre;
         c3s_pre(Sb(nxt), tid, pre);
         bf16* Dn = Db(nxt);
-        c3_expand(pre, tid, [&](int r) { return Dn + r * C3_DRS; });
+        c3_expand(pre, tid, [&](int r) { return Dn + c3v_drow(r); });
       }
     }
     c_dma_wait();
@@ -2406,6 +2443,324 @@ __global__ __launch_bounds__(512) void conv12_bwd_kernel(const void* __restrict_
     conv2_wgrad_role(smem, a1, dz2, slabs2, B, nslices, blockIdx.x - n_dgrad);
 }
 
+// ---- conv2 backward + conv1 wgrad with wave-specialised / pipelined 8-wave workgroups (the conv3 bwd8
+// scheme; batches above fc_in_c3_max_batch).  One 512-thread workgroup per CU:
+//   dgrad: waves 0-3 run conv2's data gradient of image s (both 16-channel n-tiles per wave, so every
+//     A-fragment read feeds 2 MFMAs: half the LDS reads of conv12_dgrad_role) into da1 O[s&1]; beside them
+//     waves 4-7 run conv1's weight gradient of image s-1 (from O[(s-1)&1]) and stage image s+1 (dz2 ->
+//     P, input copies, pool1 codes; registers loaded one step ahead).  One barrier per image.  The
+//     input copies and codes of image s-1 are still read while image s+1 is staged: three of those.
+//   wgrad: conv2's weight gradient, 8 waves each 2 co tiles x 4-5 n-tiles (14 tr16 reads per 10 MFMAs per
+//     k-step instead of 20 per 9), image i+1 staged from registers while image i's MFMAs run.
+constexpr int C12V_DG = 2 * (C2D_P + C12_O) + 3 * (C12_XS + C1I_IMG);  // 155104
+constexpr int C12V_WG = 2 * (C2W_D + C2W_X);                           // 72096
+constexpr int C12V_LDS = C12V_DG > C12V_WG ? C12V_DG : C12V_WG;
+static_assert(C12V_LDS <= 160 * 1024 && C1I_IMG % 16 == 0, "conv12 backward (8-wave) LDS");
+
+template <bool U8>
+__device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __restrict__ xin,
+                                                   const uint8_t* __restrict__ idx1, const bf16* __restrict__ dz2,
+                                                   const bf16* __restrict__ packed, int B, int block, int nblocks,
+                                                   float mean, float inv_std, float in_scale,
+                                                   float* __restrict__ slabs1) {
+  auto Pb = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C2D_P); };
+  auto Ob = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C2D_P + k * C12_O); };
+  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * (C2D_P + C12_O) + k * C12_XS); };
+  auto Cb = [&](int k) { return reinterpret_cast<uint8_t*>(smem + 2 * (C2D_P + C12_O) + 3 * C12_XS + k * C1I_IMG); };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = block < B ? (B - block + nblocks - 1) / nblocks : 0;
+  // zero rings of both dz2 images, the zero windows 169..171 of both da1 images, the rings of the copies
+  for (int c = tid; c < (2 * (C2D_P + C12_O) + 3 * C12_XS) / 16; c += 512)
+    reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
+  __syncthreads();
+  if (wave < 4) {
+    // ---- MFMA waves: m-tiles wave, wave + 4, wave + 8 (< 11), both n-tiles.  Weights are the A operand
+    // (the B-fragment pack read as A: the same lane -> (channel, k) map), so a lane's 4 results are 4
+    // consecutive input channels of one position: one 8-byte store each.
+    const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
+    const bf16x8* pk = reinterpret_cast<const bf16x8*>(packed + P2D_OFF);
+    bf16x8 bw[2][18];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) bw[nt][ks] = pk[(nt * 18 + ks) * 64 + lane];
+    int base[3], opos[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int mt = min(wave + 4 * k, 10);
+      const int mm = c2d_tile_pos[mt * 16 + r16];
+      opos[k] = mm;
+      base[k] = mm == 255 ? 0 : (mm / 13) * C2_PW + mm % 13;
+    }
+    auto phase = [&](auto nk_c, const bf16* P, bf16* O) {
+      constexpr int NK = decltype(nk_c)::value;
+      f32x4 acc[NK][2];
+#pragma unroll
+      for (int k = 0; k < NK; ++k) acc[k][0] = acc[k][1] = zero_f32x4();
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int tapp = ks >> 1, c0 = (ks & 1) * 32;
+        const int shift = (tapp / 3) * C2_PW + tapp % 3;
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(P + (base[k] + shift) * C2_PRS + c0 + q8);
+          acc[k][0] = mfma16x16x32(bw[0][ks], a, acc[k][0]);
+          acc[k][1] = mfma16x16x32(bw[1][ks], a, acc[k][1]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        if (opos[k] < 169) {
+#pragma unroll
+          for (int nt = 0; nt < 2; ++nt)
+            *reinterpret_cast<bf16x4*>(O + opos[k] * C2_ORS + nt * 16 + c4) =
+                bf16x4{(bf16)acc[k][nt][0], (bf16)acc[k][nt][1], (bf16)acc[k][nt][2], (bf16)acc[k][nt][3]};
+        }
+      }
+    };
+    lds_barrier();  // [B1] image 0 staged
+    for (int s = 0; s <= n; ++s) {
+      if (s < n) {
+        if (wave < 3)
+          phase(std::integral_constant<int, 3>{}, Pb(s & 1), Ob(s & 1));
+        else
+          phase(std::integral_constant<int, 2>{}, Pb(s & 1), Ob(s & 1));
+      }
+      lds_barrier();
+    }
+    __syncthreads();  // [R0] the V waves' conv1 reduction reuses P
+    __syncthreads();  // [R1]
+  } else {
+    // ---- conv1-wgrad / staging waves: thread vt of 256
+    const int vt = tid - 256, vw = wave - 4;
+    const int i16 = lane & 15, g = lane >> 4, q = i16 >> 2, p = i16 & 3;
+    const int t1 = 16 + i16;
+    const int xoff0 = (i16 % 5) * C1W_CS + (i16 / 5) * C1W_RS + 8 * g;
+    const int xoff1 = t1 < 25 ? (t1 % 5) * C1W_CS + (t1 / 5) * C1W_RS + 8 * g : 0;
+    const uint32_t b1fill = t1 == 25 ? 0x3f803f80u : 0u;
+    const int dy = vw & 1;  // k-steps vw, vw + 4, ...: one window-row half per wave
+    f32x4 acc1[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) acc1[m][0] = acc1[m][1] = zero_f32x4();
+    bf16x8 pz[4];
+    uint4 pc = make_uint4(0, 0, 0, 0);
+    uint32_t xu = 0;
+    float4 xf = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](int bb) {
+      const bf16x8* src = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (vt + 256 * j < 968) pz[j] = src[vt + 256 * j];
+      if (vt < C1I_IMG / 16) pc = reinterpret_cast<const uint4*>(idx1 + (int64_t)bb * C1I_IMG)[vt];
+      c1_load<U8>(xin, bb, vt, xu, xf);
+    };
+    auto stage = [&](int k2, int k3) {
+      bf16* P = Pb(k2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = vt + 256 * j;
+        if (c < 968) {
+          const int pos = c >> 3, cc = (c & 7) * 8;
+          *reinterpret_cast<bf16x8*>(P + ((pos / 11 + 2) * C2_PW + pos % 11 + 2) * C2_PRS + cc) = pz[j];
+        }
+      }
+      if (vt < C1I_IMG / 16) reinterpret_cast<uint4*>(Cb(k3))[vt] = pc;
+      c1_store<U8, 5, C1W_RS, C1W_CS>(Xb(k3), vt, xu, xf, mean, inv_std, in_scale);
+    };
+    auto c1_step = [&](int ks, const bf16* O, const bf16* xs, const uint8_t* CB) {
+      const int py = ks >> 1;
+      bf16x8 A[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const uint2 d = __builtin_bit_cast(uint2, lds_read_tr16(O + (py * 13 + 4 * g + q) * C2_ORS + m * 16 + 4 * p));
+        const int co = m * 16 + i16;
+        const uint32_t cu = *reinterpret_cast<const uint32_t*>(CB + py * 256 + (co >> 1) * 16 + 4 * g);
+        const int csh = 4 * (co & 1) + 2 * dy;
+        uint32_t pr[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t dv = e & 1 ? (e < 2 ? d.x : d.y) >> 16 : (e < 2 ? d.x : d.y) & 0xffffu;
+          const uint32_t sel = __builtin_amdgcn_ubfe(cu, 8 * e + csh, 2);
+          pr[e] = dv * ((sel * 0x8001u) & 0x10001u);
+        }
+        A[m] = __builtin_bit_cast(bf16x8, make_uint4(pr[0], pr[1], pr[2], pr[3]));
+      }
+      const bf16x8 B0 = *reinterpret_cast<const bf16x8*>(xs + xoff0 + ks * C1W_RS);
+      bf16x8 B1 = *reinterpret_cast<const bf16x8*>(xs + xoff1 + ks * C1W_RS);
+      if (t1 >= 25) B1 = __builtin_bit_cast(bf16x8, make_uint4(b1fill, b1fill, b1fill, b1fill));
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        acc1[m][0] = mfma16x16x32(A[m], B0, acc1[m][0]);
+        acc1[m][1] = mfma16x16x32(A[m], B1, acc1[m][1]);
+      }
+    };
+    if (n > 0) {
+      load(block);
+      stage(0, 0);
+      if (n > 1) load(block + nblocks);
+    }
+    lds_barrier();  // [B1]
+    for (int s = 0; s <= n; ++s) {
+      if (s + 1 < n) {
+        stage((s + 1) & 1, (s + 1) % 3);
+        if (s + 2 < n) load(block + (s + 2) * nblocks);
+      }
+      if (s >= 1) {
+        const bf16* O = Ob((s - 1) & 1);
+        const bf16* xs = Xb((s - 1) % 3);
+        const uint8_t* CB = Cb((s - 1) % 3);
+        for (int ks = vw; ks < 26; ks += 4) c1_step(ks, O, xs, CB);
+      }
+      lds_barrier();
+    }
+    // combine the 4 K-groups in a fixed order (deterministic) and write this workgroup's conv1 slab
+    __syncthreads();  // [R0]
+    float* red = reinterpret_cast<float*>(smem);  // [vw][tile][lane][4]: 16 KiB over P
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int nn = 0; nn < 2; ++nn)
+        *reinterpret_cast<f32x4*>(red + ((vw * 4 + m * 2 + nn) * 64 + lane) * 4) = acc1[m][nn];
+    __syncthreads();  // [R1]
+    const int tile = vw;
+    f32x4 sum = *reinterpret_cast<const f32x4*>(red + (tile * 64 + lane) * 4);
+#pragma unroll
+    for (int w = 1; w < 4; ++w) sum += *reinterpret_cast<const f32x4*>(red + ((w * 4 + tile) * 64 + lane) * 4);
+    float* slab = slabs1 + (int64_t)block * C1_WSLAB;
+    const int tap = (tile & 1) * 16 + i16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = (tile >> 1) * 16 + g * 4 + r;
+      if (tap < 25) slab[co * 25 + tap] = sum[r];
+      if (tap == 25) slab[800 + co] = sum[r];
+    }
+  }
+}
+
+// conv2 wgrad, 8 waves: wave (wm2 = wave & 1, wn = wave >> 1) owns co tiles 2wm2, 2wm2+1 x n-tiles
+// [c2v_n0(wn), c2v_n0(wn + 1)) of dW2t [288][64] (5, 5, 4, 4); the wn = 0 waves also the bias column sums
+__device__ __forceinline__ int c2v_n0(int wn) { return wn <= 2 ? 5 * wn : 14; }
+
+__device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ dz2,
+                                                  float* __restrict__ slabs, int B, int nslices, int slice) {
+  auto Db = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C2W_D); };
+  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C2W_D + k * C2W_X); };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm2 = wave & 1, wn = wave >> 1;
+  const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
+  const bf16x8 onesf = ones_column_frag(lane);
+  f32x4 acc[2][5], accb[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    accb[m] = zero_f32x4();
+#pragma unroll
+    for (int j = 0; j < 5; ++j) acc[m][j] = zero_f32x4();
+  }
+  // rows >= 121 of both D images stay zero
+  for (int c = tid; c < 2 * C2W_D / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
+  const int per = cdiv(B, nslices);
+  const int b_lo = slice * per, n = max(0, min(B, b_lo + per) - b_lo);
+  bf16x8 pz[2], pa[2];
+  auto load = [&](int bb) {
+    const bf16x8* zs = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
+    const bf16x8* as = reinterpret_cast<const bf16x8*>(a1 + (int64_t)bb * 169 * 32);
+    pz[0] = zs[tid];
+    if (tid + 512 < 968) pz[1] = zs[tid + 512];
+    pa[0] = as[tid];
+    if (tid + 512 < 676) pa[1] = as[tid + 512];
+  };
+  auto stage = [&](int k) {
+    bf16* D = Db(k);
+    bf16* X = Xb(k);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = tid + 512 * j;
+      if (c < 968) *reinterpret_cast<bf16x8*>(D + c2_drow(c >> 3) + (c & 7) * 8) = pz[j];
+      if (c < 676) *reinterpret_cast<bf16x8*>(X + (c >> 2) * C2_XRS + (c & 3) * 8) = pa[j];
+    }
+  };
+  __syncthreads();  // zero fill before the first stage
+  if (n > 0) {
+    load(b_lo);
+    stage(0);
+    if (n > 1) load(b_lo + 1);
+  }
+  lds_barrier();
+  const int nj = wn <= 1 ? 5 : 4, n0 = c2v_n0(wn);
+  for (int i = 0; i < n; ++i) {
+    const int cur = i & 1;
+    if (i + 1 < n) {  // image i+1 into the other buffers; its registers refilled with image i+2
+      stage(cur ^ 1);
+      if (i + 2 < n) load(b_lo + i + 2);
+    }
+    const bf16* D = Db(cur);
+    const bf16* X = Xb(cur);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kb = ks * 32 + grp * 8;
+      bf16x8 af[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int m0 = (2 * wm2 + m) * 16;
+        const bf16x4 alo = lds_read_tr16(D + c2_drow(kb + q) + m0 + 4 * p);
+        const bf16x4 ahi = lds_read_tr16(D + c2_drow(kb + 4 + q) + m0 + 4 * p);
+        af[m] = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+      }
+      const int k0 = min(kb + q, 120), k1 = min(kb + 4 + q, 120);  // rows >= 121 of D are zero
+      const int x0 = (k0 / 11) * 13 + k0 % 11, x1 = (k1 / 11) * 13 + k1 % 11;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) {
+        if (j < nj) {
+          const int n0j = (n0 + j) * 16;  // n = tap*32 + ci
+          const int tap = n0j >> 5, c0 = n0j & 31;
+          const int shift = (tap / 3) * 13 + tap % 3;
+          const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C2_XRS + c0 + 4 * p);
+          const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C2_XRS + c0 + 4 * p);
+          const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+          for (int m = 0; m < 2; ++m) acc[m][j] = mfma16x16x32(af[m], bf, acc[m][j]);
+        }
+      }
+      if (wn == 0) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) accb[m] = mfma16x16x32(af[m], onesf, accb[m]);
+      }
+    }
+    lds_barrier();
+  }
+  float* slab = slabs + (int64_t)slice * C2_WSLAB;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int co = (2 * wm2 + m) * 16 + grp * 4;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (j < nj) {
+        const int nn = (n0 + j) * 16 + g16;
+        *reinterpret_cast<f32x4*>(slab + (int64_t)nn * 64 + co) = acc[m][j];
+      }
+    }
+    if (wn == 0 && g16 == 0) *reinterpret_cast<f32x4*>(slab + 288 * 64 + co) = accb[m];
+  }
+}
+
+template <bool U8>
+__global__ __launch_bounds__(512, 1) void conv12_bwd8_kernel(const void* __restrict__ xin,
+                                                            const uint8_t* __restrict__ idx1,
+                                                            const bf16* __restrict__ a1,
+                                                            const bf16* __restrict__ dz2,
+                                                            const bf16* __restrict__ packed, int B, float mean,
+                                                            float inv_std, float in_scale,
+                                                            float* __restrict__ slabs2, int nslices,
+                                                            float* __restrict__ slabs1, int n_dgrad) {
+  __shared__ __attribute__((aligned(16))) char smem[C12V_LDS];
+  if ((int)blockIdx.x < n_dgrad)
+    conv12_dgrad8_role<U8>(smem, xin, idx1, dz2, packed, B, blockIdx.x, n_dgrad, mean, inv_std, in_scale, slabs1);
+  else
+    conv2_wgrad8_role(smem, a1, dz2, slabs2, B, nslices, blockIdx.x - n_dgrad);
+}
+
 // ================================================================== fixed-order slab reductions
 // ReduceSeg: kernels.h
 constexpr int kMaxRedSegs = 8;
@@ -2717,8 +3072,24 @@ static void c2_split(int B, bool dgrad, int& nd, int& ws) {
 
 // fused conv2 backward + conv1 wgrad: the dgrad role also does conv1 wgrad (104 MFMAs per image on top
 // of conv2 dgrad's 396; conv2 wgrad: 304)
+// 8-wave conv2 backward + conv1 wgrad (conv12_bwd8_kernel): the conv3 bwd8 batches; RINGDP_C12_V3=0 keeps the
+// 8-wave unpipelined kernel (A/B)
+static bool c12_v3(int B) {
+  static const bool on = [] {
+    const char* v = getenv("RINGDP_C12_V3");
+    return !(v && v[0] == '0');
+  }();
+  return on && B > fc_in_c3_max_batch();
+}
+
 static void c12_split(int B, int& nd, int& ws) {
   const int cus = num_cus();
+  if (c12_v3(B)) {
+    static const double frac3 = split_frac("RINGDP_C12_DGRAD_FRAC", 0.6);
+    nd = clampi((int)(frac3 * cus), 1, cus - 1);
+    ws = clampi(cdiv(B, 8), 1, cus - nd);
+    return;
+  }
   static const double frac = split_frac("RINGDP_C12_DGRAD_FRAC", 0.64);
   static const int wmin = min_slab_images("RINGDP_C12_WMIN", 2);
   nd = clampi(B, 1, (int)(frac * cus));
@@ -2817,7 +3188,14 @@ void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, 
   const bf16* a1b = static_cast<const bf16*>(a1);
   const bf16* dzb = static_cast<const bf16*>(dz2);
   const bf16* pk = static_cast<const bf16*>(packed);
-  if (u8)
+  if (c12_v3(B)) {
+    if (u8)
+      conv12_bwd8_kernel<true><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
+                                                       slabs1, nd);
+    else
+      conv12_bwd8_kernel<false><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
+                                                        slabs1, nd);
+  } else if (u8)
     conv12_bwd_kernel<true><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
                                                     slabs1, nd);
   else

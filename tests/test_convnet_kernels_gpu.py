@@ -255,7 +255,8 @@ def test_conv1_wgrad(B, u8):
     assert rel_err(db, bq.grad) < 5e-3
 
 
-@pytest.mark.parametrize("B", [1, 7, 100, 513])
+# 3000: above fc_in_c3_max_batch, the wave-specialised 8-wave kernel (conv12_bwd8_kernel)
+@pytest.mark.parametrize("B", [1, 7, 100, 513, 3000])
 @pytest.mark.parametrize("u8", [True, False])
 def test_conv12_backward_fused(B, u8):
     """Fused conv2 backward + conv1 wgrad (da1 kept in LDS) against the fp32 PyTorch reference of both
