@@ -1598,7 +1598,7 @@ constexpr int C3V_D = 8 * 1216 * 2;     // 19456
 constexpr int C3V_XRS = 80;
 constexpr int C3V_X = 100 * C3V_XRS * 2;  // 16000
 constexpr int C3V_DG = 2 * (C3D_P + C3V_DA + C3D_AM + C3S_B);  // 131584
-constexpr int C3V_WG = 2 * (C3V_D + C3V_X + C3S_B);            // 83200
+constexpr int C3V_WG = 3 * (C3V_D + C3V_X) + 2 * C3S_B;        // 118656
 constexpr int C3V_LDS = C3V_DG > C3V_WG ? C3V_DG : C3V_WG;
 static_assert(C3V_LDS <= 160 * 1024 && C3V_D % 16 == 0 && C3V_X % 16 == 0, "conv3 backward (8-wave) LDS");
 __device__ __forceinline__ int c3v_drow(int r) { return (r >> 3) * 1216 + (r & 7) * 144; }
@@ -1697,7 +1697,7 @@ __device__ __forceinline__ void c3_pool2_bwd(const float* DA, const uint8_t* AM,
 __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __restrict__ da3m,
                                                   const uint8_t* __restrict__ idx3, const uint8_t* __restrict__ idx2,
                                                   const bf16* __restrict__ packed, bf16* __restrict__ dz2, int b_first,
-                                                  int b_end, int b_step) {
+                                                  int b_end, int b_step, int ablate) {
   auto Pb = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3D_P); };
   auto DAb = [&](int k) { return reinterpret_cast<float*>(smem + 2 * C3D_P + k * C3V_DA); };
   auto AMb = [&](int k) { return reinterpret_cast<uint8_t*>(smem + 2 * (C3D_P + C3V_DA) + k * C3D_AM); };
@@ -1722,7 +1722,7 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
     lds_barrier();  // [B0] zero rows
     lds_barrier();  // [B1] image 0 expanded
     for (int s = 0; s <= n; ++s) {
-      if (s < n) {
+      if (s < n && !(ablate & 2)) {
         const bf16* P = Pb(s & 1);
         float* DA = DAb(s & 1);
 #pragma unroll
@@ -1806,7 +1806,7 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
         c3s_pre(Sb((s + 1) & 1), vt, pre);
         c3_expand(pre, vt, row_ptr(Pb((s + 1) & 1)));
       }
-      if (s >= 1 && vt < 176) c3_pool2_bwd(DAb((s - 1) & 1), AMb((s - 1) & 1), dz2, b_first + (s - 1) * b_step, vt);
+      if (s >= 1 && vt < 176 && !(ablate & 1)) c3_pool2_bwd(DAb((s - 1) & 1), AMb((s - 1) & 1), dz2, b_first + (s - 1) * b_step, vt);
       if (dma) c_dma_wait();
       lds_barrier();
     }
@@ -1816,69 +1816,90 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
 __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __restrict__ a2, const bf16* __restrict__ da3m,
                                                   const uint8_t* __restrict__ idx3, float* __restrict__ slabs, int B,
                                                   int nslices, int slice) {
+  // three D / X image buffers: image i computes from buffer i % 3 while image i+2 is staged into (i+2) % 3,
+  // so image i+1's first fragments can be read before the barrier that ends image i
   auto Db = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3V_D); };
-  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C3V_D + k * C3V_X); };
-  auto Sb = [&](int k) { return smem + 2 * (C3V_D + C3V_X) + k * C3S_B; };
+  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 3 * C3V_D + k * C3V_X); };
+  auto Sb = [&](int k) { return smem + 3 * (C3V_D + C3V_X) + k * C3S_B; };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;  // m-tiles (co) 4wm..4wm+3, n-tiles 9wn..9wn+8
+  // wave (wm, wn): m-tiles (co) 4wm..4wm+3 x n-tiles 4j + wn (j < 9), n = tap*64 + ci, i.e. tap j and channels
+  // 16wn..16wn+15: the tap part of every X address is then an immediate offset
+  const int wm = wave & 1, wn = wave >> 1;
   const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
   f32x4 acc[4][9];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[i][j] = zero_f32x4();
-  const int per = cdiv(B, nslices);
-  const int b_lo = slice * per, n = max(0, min(B, b_lo + per) - b_lo);
-  if (n > 0) {  // prologue: image 0 staged (D0, X0), image 1's compact gradient in S1
-    if (wave < 6) {
-      c3s_glds(da3m, idx3, b_lo, Sb(0), wave, lane);
-      if (n > 1) c3s_glds(da3m, idx3, b_lo + 1, Sb(1), wave, lane);
+  // images slice, slice + nslices, ...: the dgrad workgroups stride the batch the same way, so with both counts
+  // multiples of 8 an image's two readers of the compact gradient run on one XCD at about the same time
+  const int n = slice < B ? (B - slice + nslices - 1) / nslices : 0;
+  auto img = [&](int i) { return slice + i * nslices; };
+  auto expand = [&](const char* S, bf16* D) {
+    C3Pre pre;
+    c3s_pre(S, tid, pre);
+    c3_expand(pre, tid, [&](int r) { return D + c3v_drow(r); });
+  };
+  auto readA = [&](int buf, int ks, bf16x8 (&af)[4]) {
+    const bf16* D = Db(buf) + 64 * wm + 4 * p;
+    const int kb = ks * 32 + grp * 8;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const bf16x4 lo = lds_read_tr16(D + c3v_drow(kb + q) + mi * 16);
+      const bf16x4 hi = lds_read_tr16(D + c3v_drow(kb + 4 + q) + mi * 16);
+      af[mi] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
-    for (int k = wave; k < 16; k += 8) a2_glds_rows(a2, b_lo, Xb(0), k, lane);
+  };
+  if (n > 0) {  // prologue: images 0 and 1 staged, image 2's compact gradient in S0
+    if (wave < 6) {
+      c3s_glds(da3m, idx3, img(0), Sb(0), wave, lane);
+      if (n > 1) c3s_glds(da3m, idx3, img(1), Sb(1), wave, lane);
+    }
+    for (int k = wave; k < 16; k += 8) {
+      a2_glds_rows(a2, img(0), Xb(0), k, lane);
+      if (n > 1) a2_glds_rows(a2, img(1), Xb(1), k, lane);
+    }
     c_dma_wait();
     lds_barrier();
-    C3Pre pre;
-    c3s_pre(Sb(0), tid, pre);
-    c3_expand(pre, tid, [&](int r) { return Db(0) + c3v_drow(r); });
+    expand(Sb(0), Db(0));
+    if (n > 1) expand(Sb(1), Db(1));
+    lds_barrier();  // S0, S1 free
+    if (n > 2 && wave < 6) c3s_glds(da3m, idx3, img(2), Sb(0), wave, lane);
+    c_dma_wait();
   }
   lds_barrier();
+  bf16x8 af[4], afn[4];
+  if (n > 0) readA(0, 0, af);
   for (int i = 0; i < n; ++i) {
-    const int cur = i & 1, nxt = cur ^ 1, b = b_lo + i;
-    if (i + 1 < n)
-      for (int k = wave; k < 16; k += 8) a2_glds_rows(a2, b + 1, Xb(nxt), k, lane);
-    if (i + 2 < n && wave < 6) c3s_glds(da3m, idx3, b + 2, Sb(cur), wave, lane);
-    const bf16* D = Db(cur);
-    const bf16* X = Xb(cur);
+    const int cur = i % 3;
+    const int st = (i + 2) % 3;  // staging buffer of image i+2
+    if (i + 2 < n)
+      for (int k = wave; k < 16; k += 8) a2_glds_rows(a2, img(i + 2), Xb(st), k, lane);
+    if (i + 3 < n && wave < 6) c3s_glds(da3m, idx3, img(i + 3), Sb((i + 1) & 1), wave, lane);
+    const bf16* X = Xb(cur) + 16 * wn + 4 * p;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = ks * 32 + grp * 8;
-      bf16x8 af[4];
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int m0 = (4 * wm + mi) * 16;
-        const bf16x4 lo = lds_read_tr16(D + c3v_drow(kb + q) + m0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(D + c3v_drow(kb + 4 + q) + m0 + 4 * p);
-        af[mi] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      const int x0 = win_pos(kb + q, 10), x1 = win_pos(kb + 4 + q, 10);
+      const int x0 = win_pos(kb + q, 10) * C3V_XRS, x1 = win_pos(kb + 4 + q, 10) * C3V_XRS;
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
-        const int n0 = (9 * wn + j) * 16;  // n = tap*64 + ci
-        const int tap = n0 >> 6, c0 = n0 & 63;
-        const int shift = (tap / 3) * 10 + tap % 3;
-        const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C3V_XRS + c0 + 4 * p);
-        const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C3V_XRS + c0 + 4 * p);
+        const int shift = ((j / 3) * 10 + j % 3) * C3V_XRS;  // tap j
+        const bf16x4 lo = lds_read_tr16(X + x0 + shift);
+        const bf16x4 hi = lds_read_tr16(X + x1 + shift);
         const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        if (j == 4) {  // next k-step's A fragments (image i+1's first, when ks = 1: its buffer is complete)
+          if (ks == 0)
+            readA(cur, 1, afn);
+          else if (i + 1 < n)
+            readA((i + 1) % 3, 0, afn);
+        }
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) acc[mi][j] = mfma16x16x32(af[mi], bf, acc[mi][j]);
       }
-      if (ks == 0 && i + 1 < n) {  // image i+1's D between the two k-steps: the writes go out under MFMAs
-        C3Pre pre;
-        c3s_pre(Sb(nxt), tid, pre);
-        bf16* Dn = Db(nxt);
-        c3_expand(pre, tid, [&](int r) { return Dn + c3v_drow(r); });
-      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) af[mi] = afn[mi];
+      if (ks == 0 && i + 2 < n) expand(Sb(i & 1), Db(st));  // image i+2's D, under the second k-step
     }
     c_dma_wait();
     lds_barrier();
@@ -1889,7 +1910,7 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
     const int co = (4 * wm + mi) * 16 + grp * 4;
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
-      const int nn = (9 * wn + j) * 16 + g16;
+      const int nn = (4 * j + wn) * 16 + g16;
       *reinterpret_cast<f32x4*>(slab + (int64_t)nn * 128 + co) = acc[mi][j];
     }
   }
@@ -1901,18 +1922,18 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd8_kernel(const bf16* __restri
                                                            const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3,
                                                            const bf16* __restrict__ packed, bf16* __restrict__ dz2,
                                                            int B, float* __restrict__ slabs, int n_wgrad, int n_dgrad,
-                                                           int b_dgrad) {
+                                                           int b_dgrad, int ablate) {
   __shared__ __attribute__((aligned(16))) char smem[C3V_LDS];
   const int blk = blockIdx.x;
   if (blk < n_dgrad) {
-    conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, blk, b_dgrad, n_dgrad);
+    conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, blk, b_dgrad, n_dgrad, ablate);
     return;
   }
   const int w = blk - n_dgrad;
   conv3_wgrad8_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w);
   if (dz2 == nullptr || b_dgrad >= B) return;
   __syncthreads();  // LDS changes role
-  conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, b_dgrad + w, B, n_wgrad);
+  conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, b_dgrad + w, B, n_wgrad, ablate);
 }
 
 __device__ __forceinline__ bf16x8 ones_column_frag(int lane) {
@@ -2453,7 +2474,7 @@ __global__ __launch_bounds__(512) void conv12_bwd_kernel(const void* __restrict_
 //   wgrad: conv2's weight gradient, 8 waves each 2 co tiles x 4-5 n-tiles (14 tr16 reads per 10 MFMAs per
 //     k-step instead of 20 per 9), image i+1 staged from registers while image i's MFMAs run.
 constexpr int C12V_DG = 2 * (C2D_P + C12_O) + 3 * (C12_XS + C1I_IMG);  // 155104
-constexpr int C12V_WG = 2 * (C2W_D + C2W_X);                           // 72096
+constexpr int C12V_WG = 3 * (C2W_D + C2W_X);                           // 108144
 constexpr int C12V_LDS = C12V_DG > C12V_WG ? C12V_DG : C12V_WG;
 static_assert(C12V_LDS <= 160 * 1024 && C1I_IMG % 16 == 0, "conv12 backward (8-wave) LDS");
 
@@ -2462,7 +2483,7 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
                                                    const uint8_t* __restrict__ idx1, const bf16* __restrict__ dz2,
                                                    const bf16* __restrict__ packed, int B, int block, int nblocks,
                                                    float mean, float inv_std, float in_scale,
-                                                   float* __restrict__ slabs1) {
+                                                   float* __restrict__ slabs1, int ablate) {
   auto Pb = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C2D_P); };
   auto Ob = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C2D_P + k * C12_O); };
   auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * (C2D_P + C12_O) + k * C12_XS); };
@@ -2521,7 +2542,7 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
     };
     lds_barrier();  // [B1] image 0 staged
     for (int s = 0; s <= n; ++s) {
-      if (s < n) {
+      if (s < n && !(ablate & 2)) {
         if (wave < 3)
           phase(std::integral_constant<int, 3>{}, Pb(s & 1), Ob(s & 1));
         else
@@ -2606,7 +2627,7 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
         stage((s + 1) & 1, (s + 1) % 3);
         if (s + 2 < n) load(block + (s + 2) * nblocks);
       }
-      if (s >= 1) {
+      if (s >= 1 && !(ablate & 1)) {
         const bf16* O = Ob((s - 1) & 1);
         const bf16* xs = Xb((s - 1) % 3);
         const uint8_t* CB = Cb((s - 1) % 3);
@@ -2638,17 +2659,20 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
   }
 }
 
-// conv2 wgrad, 8 waves: wave (wm2 = wave & 1, wn = wave >> 1) owns co tiles 2wm2, 2wm2+1 x n-tiles
-// [c2v_n0(wn), c2v_n0(wn + 1)) of dW2t [288][64] (5, 5, 4, 4); the wn = 0 waves also the bias column sums
-__device__ __forceinline__ int c2v_n0(int wn) { return wn <= 2 ? 5 * wn : 14; }
-
+// conv2 wgrad, 8 waves: wave (wm2 = wave & 1, wn = wave >> 1) owns co tiles 2wm2, 2wm2+1 x the n-tiles
+// (tap, half) of dW2t [288][64] with half = wn & 1 (input channels 16 half ..) and taps h, h+2, .. (h = wn >> 1:
+// 5 taps for h = 0, 4 for h = 1); the tap part of every X address is an immediate offset (body<H>).  The
+// wn = 0 waves also form the bias column sums.  Three D / X image buffers, as conv3_wgrad8_role: image i+1's
+// first A fragments are read before the barrier that ends image i.  The inputs are staged from registers
+// loaded one image ahead (an LDS-DMA form with per-lane sources - 37 wave-instructions per image into the
+// padded layouts - measured 1044 vs 782 us for this role at B=65536).
 __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __restrict__ a1, const bf16* __restrict__ dz2,
                                                   float* __restrict__ slabs, int B, int nslices, int slice) {
   auto Db = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C2W_D); };
-  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 2 * C2W_D + k * C2W_X); };
+  auto Xb = [&](int k) { return reinterpret_cast<bf16*>(smem + 3 * C2W_D + k * C2W_X); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm2 = wave & 1, wn = wave >> 1;
+  const int wm2 = wave & 1, wn = wave >> 1, half = wn & 1, h = wn >> 1;
   const int g16 = lane & 15, grp = lane >> 4, q = g16 >> 2, p = g16 & 3;
   const bf16x8 onesf = ones_column_frag(lane);
   f32x4 acc[2][5], accb[2];
@@ -2658,10 +2682,11 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
 #pragma unroll
     for (int j = 0; j < 5; ++j) acc[m][j] = zero_f32x4();
   }
-  // rows >= 121 of both D images stay zero
-  for (int c = tid; c < 2 * C2W_D / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
-  const int per = cdiv(B, nslices);
-  const int b_lo = slice * per, n = max(0, min(B, b_lo + per) - b_lo);
+  // rows >= 121 of the three D images stay zero
+  for (int c = tid; c < 3 * C2W_D / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
+  // images slice, slice + nslices, ... (as the dgrad workgroups)
+  const int n = slice < B ? (B - slice + nslices - 1) / nslices : 0;
+  auto img = [&](int i) { return slice + i * nslices; };
   bf16x8 pz[2], pa[2];
   auto load = [&](int bb) {
     const bf16x8* zs = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
@@ -2681,63 +2706,83 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
       if (c < 676) *reinterpret_cast<bf16x8*>(X + (c >> 2) * C2_XRS + (c & 3) * 8) = pa[j];
     }
   };
+  auto readA = [&](int buf, int ks, bf16x8 (&af)[2]) {
+    const bf16* D = Db(buf) + 32 * wm2 + 4 * p;
+    const int kb = ks * 32 + grp * 8;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const bf16x4 alo = lds_read_tr16(D + c2_drow(kb + q) + m * 16);
+      const bf16x4 ahi = lds_read_tr16(D + c2_drow(kb + 4 + q) + m * 16);
+      af[m] = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+    }
+  };
   __syncthreads();  // zero fill before the first stage
   if (n > 0) {
-    load(b_lo);
+    load(img(0));
     stage(0);
-    if (n > 1) load(b_lo + 1);
+    if (n > 1) {
+      load(img(1));
+      stage(1);
+    }
+    if (n > 2) load(img(2));
   }
   lds_barrier();
-  const int nj = wn <= 1 ? 5 : 4, n0 = c2v_n0(wn);
-  for (int i = 0; i < n; ++i) {
-    const int cur = i & 1;
-    if (i + 1 < n) {  // image i+1 into the other buffers; its registers refilled with image i+2
-      stage(cur ^ 1);
-      if (i + 2 < n) load(b_lo + i + 2);
-    }
-    const bf16* D = Db(cur);
-    const bf16* X = Xb(cur);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int kb = ks * 32 + grp * 8;
-      bf16x8 af[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        const int m0 = (2 * wm2 + m) * 16;
-        const bf16x4 alo = lds_read_tr16(D + c2_drow(kb + q) + m0 + 4 * p);
-        const bf16x4 ahi = lds_read_tr16(D + c2_drow(kb + 4 + q) + m0 + 4 * p);
-        af[m] = bf16x8{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+  bf16x8 af[2], afn[2];
+  if (n > 0) readA(0, 0, af);
+  auto body = [&](auto h_c) {
+    constexpr int H = decltype(h_c)::value;
+    constexpr int NJ = H == 0 ? 5 : 4;
+    for (int i = 0; i < n; ++i) {
+      const int cur = i % 3;
+      if (i + 2 < n) {  // image i+2 into the buffers image i-1 used; its registers refilled with image i+3
+        stage((i + 2) % 3);
+        if (i + 3 < n) load(img(i + 3));
       }
-      const int k0 = min(kb + q, 120), k1 = min(kb + 4 + q, 120);  // rows >= 121 of D are zero
-      const int x0 = (k0 / 11) * 13 + k0 % 11, x1 = (k1 / 11) * 13 + k1 % 11;
+      const bf16* X = Xb(cur) + 16 * half + 4 * p;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        if (j < nj) {
-          const int n0j = (n0 + j) * 16;  // n = tap*32 + ci
-          const int tap = n0j >> 5, c0 = n0j & 31;
-          const int shift = (tap / 3) * 13 + tap % 3;
-          const bf16x4 lo = lds_read_tr16(X + (x0 + shift) * C2_XRS + c0 + 4 * p);
-          const bf16x4 hi = lds_read_tr16(X + (x1 + shift) * C2_XRS + c0 + 4 * p);
+      for (int ks = 0; ks < 4; ++ks) {
+        const int kb = ks * 32 + grp * 8;
+        const int k0 = min(kb + q, 120), k1 = min(kb + 4 + q, 120);  // rows >= 121 of D are zero
+        const int x0 = ((k0 / 11) * 13 + k0 % 11) * C2_XRS, x1 = ((k1 / 11) * 13 + k1 % 11) * C2_XRS;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int tap = 2 * j + H;
+          const int shift = ((tap / 3) * 13 + tap % 3) * C2_XRS;
+          const bf16x4 lo = lds_read_tr16(X + x0 + shift);
+          const bf16x4 hi = lds_read_tr16(X + x1 + shift);
           const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          if (j == 2) {  // next k-step's A fragments (image i+1's first after the last k-step)
+            if (ks < 3)
+              readA(cur, ks + 1, afn);
+            else if (i + 1 < n)
+              readA((i + 1) % 3, 0, afn);
+          }
 #pragma unroll
           for (int m = 0; m < 2; ++m) acc[m][j] = mfma16x16x32(af[m], bf, acc[m][j]);
         }
-      }
-      if (wn == 0) {
+        if (wn == 0) {
 #pragma unroll
-        for (int m = 0; m < 2; ++m) accb[m] = mfma16x16x32(af[m], onesf, accb[m]);
+          for (int m = 0; m < 2; ++m) accb[m] = mfma16x16x32(af[m], onesf, accb[m]);
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) af[m] = afn[m];
       }
+      lds_barrier();
     }
-    lds_barrier();
-  }
+  };
+  if (h == 0)
+    body(std::integral_constant<int, 0>{});
+  else
+    body(std::integral_constant<int, 1>{});
   float* slab = slabs + (int64_t)slice * C2_WSLAB;
+  const int nj = h == 0 ? 5 : 4;
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int co = (2 * wm2 + m) * 16 + grp * 4;
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       if (j < nj) {
-        const int nn = (n0 + j) * 16 + g16;
+        const int nn = ((2 * j + h) * 2 + half) * 16 + g16;  // n-tile (tap, half)
         *reinterpret_cast<f32x4*>(slab + (int64_t)nn * 64 + co) = acc[m][j];
       }
     }
@@ -2753,10 +2798,11 @@ __global__ __launch_bounds__(512, 1) void conv12_bwd8_kernel(const void* __restr
                                                             const bf16* __restrict__ packed, int B, float mean,
                                                             float inv_std, float in_scale,
                                                             float* __restrict__ slabs2, int nslices,
-                                                            float* __restrict__ slabs1, int n_dgrad) {
+                                                            float* __restrict__ slabs1, int n_dgrad, int ablate) {
   __shared__ __attribute__((aligned(16))) char smem[C12V_LDS];
   if ((int)blockIdx.x < n_dgrad)
-    conv12_dgrad8_role<U8>(smem, xin, idx1, dz2, packed, B, blockIdx.x, n_dgrad, mean, inv_std, in_scale, slabs1);
+    conv12_dgrad8_role<U8>(smem, xin, idx1, dz2, packed, B, blockIdx.x, n_dgrad, mean, inv_std, in_scale, slabs1,
+                           ablate);
   else
     conv2_wgrad8_role(smem, a1, dz2, slabs2, B, nslices, blockIdx.x - n_dgrad);
 }
@@ -3015,6 +3061,16 @@ static bool c3_v3(int B) {
   return on && B > fc_in_c3_max_batch();
 }
 
+// timing-only ablations of the 8-wave conv3 backward (wrong results): bit 0 skips the pool2 backward,
+// bit 1 the dgrad MFMA phase (RINGDP_C3_ABLATE)
+static int c3_ablate() {
+  static const int v = [] {
+    const char* e = getenv("RINGDP_C3_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 // dgrad and wgrad do about the same MFMA work per image (624 / 576 MFMAs); measured best split 0.5-0.6 of
 // the workgroup slots (B=32768).
 static void c3_split(int B, bool dgrad, int& nd, int& ws) {
@@ -3026,7 +3082,7 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
       return;
     }
     static const double frac = split_frac("RINGDP_C3_DGRAD_FRAC", 0.55);
-    nd = clampi((int)(frac * cus), 1, cus - 1);
+    nd = clampi(((int)(frac * cus) + 4) / 8 * 8, 8, cus - 8);  // multiples of 8: see conv3_wgrad8_role
     ws = clampi(cdiv(B, 8), 1, cus - nd);
     return;
   }
@@ -3082,11 +3138,21 @@ static bool c12_v3(int B) {
   return on && B > fc_in_c3_max_batch();
 }
 
+// timing-only ablations of the 8-wave conv12 dgrad role (wrong results): bit 0 skips conv1 wgrad, bit 1 the
+// conv2 dgrad MFMAs (RINGDP_C12_ABLATE)
+static int c12_ablate() {
+  static const int v = [] {
+    const char* e = getenv("RINGDP_C12_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static void c12_split(int B, int& nd, int& ws) {
   const int cus = num_cus();
   if (c12_v3(B)) {
     static const double frac3 = split_frac("RINGDP_C12_DGRAD_FRAC", 0.6);
-    nd = clampi((int)(frac3 * cus), 1, cus - 1);
+    nd = clampi(((int)(frac3 * cus) + 4) / 8 * 8, 8, cus - 8);  // multiples of 8: see conv2_wgrad8_role
     ws = clampi(cdiv(B, 8), 1, cus - nd);
     return;
   }
@@ -3148,7 +3214,8 @@ void cn_conv3_fc_bwd(const void* a2, const uint8_t* idx2, const void* a3, const 
       fc_bwd_kernel<false><<<fs, 256, 0, s>>>(a3b, pk, dl, static_cast<bf16*>(da3m), fc_slabs, B, fc_imgs_host(B), cef);
     if (c3_v3(B)) {
       conv3_bwd8_kernel<<<nd + ws, 512, 0, s>>>(static_cast<const bf16*>(a2), idx2, static_cast<const bf16*>(da3m), idx3,
-                                               pk, static_cast<bf16*>(dz2), B, c3_slabs, ws, nd, c3_dgrad_images(B, nd));
+                                               pk, static_cast<bf16*>(dz2), B, c3_slabs, ws, nd, c3_dgrad_images(B, nd),
+                                               c3_ablate());
     } else {
       const C3Src src{static_cast<const bf16*>(da3m), a3b, pk, dl, cef};
       conv3_bwd_kernel<false><<<nd + 2 * ws, 256, 0, s>>>(static_cast<const bf16*>(a2), idx2, src, idx3, pk,
@@ -3191,10 +3258,10 @@ void cn_conv12_bwd(const void* x, bool u8, const uint8_t* idx1, const void* a1, 
   if (c12_v3(B)) {
     if (u8)
       conv12_bwd8_kernel<true><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
-                                                       slabs1, nd);
+                                                       slabs1, nd, c12_ablate());
     else
       conv12_bwd8_kernel<false><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
-                                                        slabs1, nd);
+                                                        slabs1, nd, c12_ablate());
   } else if (u8)
     conv12_bwd_kernel<true><<<nd + ws, 512, 0, s>>>(x, idx1, a1b, dzb, pk, B, mean, inv_std, in_scale, slabs2, ws,
                                                     slabs1, nd);

@@ -30,6 +30,19 @@ def pytest_collection_modifyitems(config, items):
 
 
 def free_port() -> int:
+    """A port below the kernel's ephemeral range (32768+): a port the kernel hands out (bind to 0) can be
+    taken again by an outgoing connection of an earlier test before the store binds it."""
+    import random
+
+    rng = random.Random(os.getpid() ^ int.from_bytes(os.urandom(4), "little"))
+    for _ in range(200):
+        port = rng.randrange(20000, 32000)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
