@@ -200,6 +200,15 @@ __device__ __forceinline__ void glds16_async(const void* gsrc, void* lds_wave_ba
 }
 __device__ __forceinline__ void c_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// The same copy from a wave-uniform base (SGPR pair) plus a 32-bit per-lane byte offset: the per-lane part of
+// an image's copy is the same for every image, so it is computed once and no 64-bit address math runs per copy.
+__device__ __forceinline__ void glds16_sv(const void* sbase, uint32_t voff, void* lds_wave_base) {
+  const unsigned base = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)((__attribute__((address_space(3))) char*)(lds_wave_base)));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" ::"s"(base), "v"(voff), "s"(sbase)
+               : "memory");
+}
+
 // ================================================================== F1: conv1 (MFMA)
 // The zero-ringed 30x30 input is staged as 8 copies shifted by s = 0..7 columns (rows of 32):
 // copy s holds xpad[r][c + s].  Eight consecutive pixels xpad[r][ow .. ow+7] are then ONE aligned
@@ -929,7 +938,10 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
   const int tid = threadIdx.x - 256, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, q8 = (lane >> 4) * 8;
   if (PACK) ff_wait_packed(sync, npack);
-  {
+  // fc1 in this launch unless logits == nullptr (large batches: fc1_fwd_kernel, an MFMA pass over a3, takes
+  // its ~200 VALU per lane and image out of phase 1, where the producer's conv1 epilogue is VALU-bound too)
+  const bool fc = logits != nullptr;
+  if (fc) {
     const uint4* src = reinterpret_cast<const uint4*>(packed + PFC_OFF);
     for (int c = tid; c < C3F_FCW / 8; c += 256) reinterpret_cast<uint4*>(fw)[c] = src[c];
   }
@@ -998,6 +1010,7 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
           const int64_t o = ((int64_t)be * 16 + wc) * 128 + co;
           a3[o] = pb;
           idx3[o] = (uint8_t)g;
+          if (!fc) continue;
           const float pv = (float)pb;
           const uint32_t* wp = reinterpret_cast<const uint32_t*>(fw + (wc * 128 + co) * 10);
 #pragma unroll
@@ -1007,8 +1020,10 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
             part[2 * h + 1] = fmaf(pv, __uint_as_float(u & 0xffff0000u), part[2 * h + 1]);
           }
         }
+      if (fc) {
 #pragma unroll
-      for (int n = 0; n < 10; ++n) fred[n * 256 + tid] = part[n];
+        for (int n = 0; n < 10; ++n) fred[n * 256 + tid] = part[n];
+      }
     }
     if (live_m) {
 #pragma unroll
@@ -1017,7 +1032,7 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     }
     __syncthreads();  // [S1]
     // ---------------- phase 2
-    if (live_e) fc_reduce(be);
+    if (live_e && fc) fc_reduce(be);
     if (live_m) mfma_ks(xb, std::integral_constant<int, 4>{}, std::integral_constant<int, 11>{});
     __syncthreads();  // [S2]
     // ---------------- phase 3: the rest of the producer's pool2 (image s), k-steps 11-17
@@ -1629,10 +1644,11 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // wave-instruction k (0..5) of the compact stage of image b: da3m row (4 KiB), then the argmax bytes (2 KiB)
 __device__ __forceinline__ void c3s_glds(const bf16* __restrict__ da3m, const uint8_t* __restrict__ idx3, int b,
                                          char* S, int k, int lane) {
+  const uint32_t voff = ((k & 3) * 64 + lane) * 16;
   if (k < 4)
-    glds16_async(da3m + (int64_t)b * 2048 + (k * 64 + lane) * 8, S + k * 1024);
+    glds16_sv(da3m + (int64_t)b * 2048, voff, S + k * 1024);
   else
-    glds16_async(idx3 + (int64_t)b * 2048 + ((k - 4) * 64 + lane) * 16, S + k * 1024);
+    glds16_sv(idx3 + (int64_t)b * 2048, voff, S + k * 1024);
 }
 
 __device__ __forceinline__ void c3s_pre(const char* S, int tid, C3Pre& p) {
@@ -1642,14 +1658,17 @@ __device__ __forceinline__ void c3s_pre(const char* S, int tid, C3Pre& p) {
   }
 }
 
-// wave-instruction k (0..15) of the a2 image b straight into C3V_XRS rows: 10 16-B chunks per row, lane-linear
-// in LDS; chunks 8, 9 of a row are its padding and re-read the row's first chunks
-__device__ __forceinline__ void a2_glds_rows(const bf16* __restrict__ a2, int b, bf16* X, int k, int lane) {
+// a2 image -> C3V_XRS rows by LDS-DMA: wave-instruction k (0..15) covers LDS chunks 64k..64k+63, 10 16-B
+// chunks per row, chunks 8, 9 of a row its padding (re-reading the row's first chunks); a2_rows_off is a lane's
+// byte offset in the image (or ~0u past the 100 rows), a2_glds_rows issues the copy of image b
+__device__ __forceinline__ uint32_t a2_rows_off(int k, int lane) {
   const int c = k * 64 + lane;
-  if (c < 1000) {
-    const int row = c / 10, sub = c - 10 * row;
-    glds16_async(a2 + (int64_t)b * 6400 + row * 64 + (sub & 7) * 8, X + k * 512);
-  }
+  if (c >= 1000) return ~0u;
+  const int row = c / 10, sub = c - 10 * row;
+  return (row * 64 + (sub & 7) * 8) * 2;
+}
+__device__ __forceinline__ void a2_glds_rows(const bf16* __restrict__ a2, int b, bf16* X, int k, uint32_t voff) {
+  if (voff != ~0u) glds16_sv(a2 + (int64_t)b * 6400, voff, X + k * 512);
 }
 
 // pool2 + ReLU backward of one image (threads t < 176: output row t >> 4, channel quad t & 15), as in
@@ -1798,7 +1817,7 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
           uint8_t* AM = AMb(s & 1);
 #pragma unroll
           for (int k = 0; k < 7; ++k)
-            if (k * 64 + lane < 400) glds16_async(src + (k * 64 + lane) * 16, AM + k * 1024);
+            if (k * 64 + lane < 400) glds16_sv(src, (k * 64 + lane) * 16, AM + k * 1024);
         }
       }
       if (s + 1 < n) {
@@ -1836,6 +1855,12 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
   // multiples of 8 an image's two readers of the compact gradient run on one XCD at about the same time
   const int n = slice < B ? (B - slice + nslices - 1) / nslices : 0;
   auto img = [&](int i) { return slice + i * nslices; };
+  // this wave's a2 DMA instructions: k = wave, wave + 8
+  const uint32_t xo0 = a2_rows_off(wave, lane), xo1 = a2_rows_off(wave + 8, lane);
+  auto dma_x = [&](int b, bf16* X) {
+    a2_glds_rows(a2, b, X, wave, xo0);
+    a2_glds_rows(a2, b, X, wave + 8, xo1);
+  };
   auto expand = [&](const char* S, bf16* D) {
     C3Pre pre;
     c3s_pre(S, tid, pre);
@@ -1856,10 +1881,8 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
       c3s_glds(da3m, idx3, img(0), Sb(0), wave, lane);
       if (n > 1) c3s_glds(da3m, idx3, img(1), Sb(1), wave, lane);
     }
-    for (int k = wave; k < 16; k += 8) {
-      a2_glds_rows(a2, img(0), Xb(0), k, lane);
-      if (n > 1) a2_glds_rows(a2, img(1), Xb(1), k, lane);
-    }
+    dma_x(img(0), Xb(0));
+    if (n > 1) dma_x(img(1), Xb(1));
     c_dma_wait();
     lds_barrier();
     expand(Sb(0), Db(0));
@@ -1874,31 +1897,32 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
   for (int i = 0; i < n; ++i) {
     const int cur = i % 3;
     const int st = (i + 2) % 3;  // staging buffer of image i+2
-    if (i + 2 < n)
-      for (int k = wave; k < 16; k += 8) a2_glds_rows(a2, img(i + 2), Xb(st), k, lane);
+    if (i + 2 < n) dma_x(img(i + 2), Xb(st));
     if (i + 3 < n && wave < 6) c3s_glds(da3m, idx3, img(i + 3), Sb((i + 1) & 1), wave, lane);
-    const bf16* X = Xb(cur) + 16 * wn + 4 * p;
+    const int xb = (int)(Xb(cur) - reinterpret_cast<const bf16*>(smem)) + 16 * wn + 4 * p;  // element offset
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int kb = ks * 32 + grp * 8;
-      const int x0 = win_pos(kb + q, 10) * C3V_XRS, x1 = win_pos(kb + 4 + q, 10) * C3V_XRS;
+      int x0 = xb + win_pos(kb + q, 10) * C3V_XRS, x1 = xb + win_pos(kb + 4 + q, 10) * C3V_XRS;
+      // the whole per-lane part of the address opaque to the optimiser: otherwise it folds the tap offset into
+      // a per-tap SGPR or VGPR and pays one VALU add per fragment read instead of the immediate offset
+      asm("" : "+v"(x0), "+v"(x1));
+      const bf16* S0 = reinterpret_cast<const bf16*>(smem);
 #pragma unroll
       for (int j = 0; j < 9; ++j) {
         const int shift = ((j / 3) * 10 + j % 3) * C3V_XRS;  // tap j
-        const bf16x4 lo = lds_read_tr16(X + x0 + shift);
-        const bf16x4 hi = lds_read_tr16(X + x1 + shift);
+        const bf16x4 lo = lds_read_tr16(S0 + x0 + shift);
+        const bf16x4 hi = lds_read_tr16(S0 + x1 + shift);
         const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         if (j == 4) {  // next k-step's A fragments (image i+1's first, when ks = 1: its buffer is complete)
           if (ks == 0)
             readA(cur, 1, afn);
           else if (i + 1 < n)
-            readA((i + 1) % 3, 0, afn);
+            readA((i + 1) % 3, 0, af);
         }
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) acc[mi][j] = mfma16x16x32(af[mi], bf, acc[mi][j]);
+        for (int mi = 0; mi < 4; ++mi) acc[mi][j] = mfma16x16x32(ks == 0 ? af[mi] : afn[mi], bf, acc[mi][j]);
       }
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) af[mi] = afn[mi];
       if (ks == 0 && i + 2 < n) expand(Sb(i & 1), Db(st));  // image i+2's D, under the second k-step
     }
     c_dma_wait();
@@ -2738,34 +2762,39 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
         stage((i + 2) % 3);
         if (i + 3 < n) load(img(i + 3));
       }
-      const bf16* X = Xb(cur) + 16 * half + 4 * p;
+      const int xb = (int)(Xb(cur) - reinterpret_cast<const bf16*>(smem)) + 16 * half + 4 * p;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int kb = ks * 32 + grp * 8;
         const int k0 = min(kb + q, 120), k1 = min(kb + 4 + q, 120);  // rows >= 121 of D are zero
-        const int x0 = ((k0 / 11) * 13 + k0 % 11) * C2_XRS, x1 = ((k1 / 11) * 13 + k1 % 11) * C2_XRS;
+        int x0 = xb + ((k0 / 11) * 13 + k0 % 11) * C2_XRS, x1 = xb + ((k1 / 11) * 13 + k1 % 11) * C2_XRS;
+        asm("" : "+v"(x0), "+v"(x1));  // as conv3_wgrad8_role: one VGPR base + immediate tap offsets
+        const bf16* S0 = reinterpret_cast<const bf16*>(smem);
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
           const int tap = 2 * j + H;
           const int shift = ((tap / 3) * 13 + tap % 3) * C2_XRS;
-          const bf16x4 lo = lds_read_tr16(X + x0 + shift);
-          const bf16x4 hi = lds_read_tr16(X + x1 + shift);
+          const bf16x4 lo = lds_read_tr16(S0 + x0 + shift);
+          const bf16x4 hi = lds_read_tr16(S0 + x1 + shift);
           const bf16x8 bf = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          if (j == 2) {  // next k-step's A fragments (image i+1's first after the last k-step)
-            if (ks < 3)
-              readA(cur, ks + 1, afn);
-            else if (i + 1 < n)
-              readA((i + 1) % 3, 0, afn);
+          if (j == 2) {  // next k-step's A fragments (image i+1's first after the last k-step); af and afn
+                         // alternate by k-step parity, so nothing is copied
+            if (ks < 3) {
+              if (ks & 1)
+                readA(cur, ks + 1, af);
+              else
+                readA(cur, ks + 1, afn);
+            } else if (i + 1 < n) {
+              readA((i + 1) % 3, 0, af);
+            }
           }
 #pragma unroll
-          for (int m = 0; m < 2; ++m) acc[m][j] = mfma16x16x32(af[m], bf, acc[m][j]);
+          for (int m = 0; m < 2; ++m) acc[m][j] = mfma16x16x32((ks & 1) ? afn[m] : af[m], bf, acc[m][j]);
         }
         if (wn == 0) {
 #pragma unroll
-          for (int m = 0; m < 2; ++m) accb[m] = mfma16x16x32(af[m], onesf, accb[m]);
+          for (int m = 0; m < 2; ++m) accb[m] = mfma16x16x32((ks & 1) ? afn[m] : af[m], onesf, accb[m]);
         }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) af[m] = afn[m];
       }
       lds_barrier();
     }
@@ -3002,14 +3031,17 @@ void cn_forward_fused(const void* x, bool u8, const float* const* w, const float
     return;
   }
   pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(ws, pk);
+  const bool fc_in = B <= fc_fused_max_batch();  // else fc1 as its own MFMA pass over a3
+  float* lg = fc_in ? logits : nullptr;
   if (u8)
     fused_fwd_kernel<true, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
-                                                       idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
+                                                       idx2, a3b, idx3, lg, B, mean, inv_std, in_scale, ablate,
                                                        nullptr, p2split);
   else
     fused_fwd_kernel<false, false><<<conv, 512, 0, s>>>(x, pk, ws, nullptr, conv, b1, b2, b3, bfc, a1b, idx1, a2b,
-                                                        idx2, a3b, idx3, logits, B, mean, inv_std, in_scale, ablate,
+                                                        idx2, a3b, idx3, lg, B, mean, inv_std, in_scale, ablate,
                                                         nullptr, p2split);
+  if (!fc_in) fc1_fwd_kernel<<<cdiv(B, 16 * FC1_G), 256, 0, s>>>(a3b, pk, bfc, logits, B);
 }
 
 void cn_conv2_fwd(const void* a1, const void* packed, const float* b2, void* a2, uint8_t* idx2, int B,
@@ -3151,7 +3183,7 @@ static int c12_ablate() {
 static void c12_split(int B, int& nd, int& ws) {
   const int cus = num_cus();
   if (c12_v3(B)) {
-    static const double frac3 = split_frac("RINGDP_C12_DGRAD_FRAC", 0.6);
+    static const double frac3 = split_frac("RINGDP_C12_DGRAD_FRAC", 0.65);
     nd = clampi(((int)(frac3 * cus) + 4) / 8 * 8, 8, cus - 8);  // multiples of 8: see conv2_wgrad8_role
     ws = clampi(cdiv(B, 8), 1, cus - nd);
     return;
