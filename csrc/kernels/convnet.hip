@@ -1719,8 +1719,16 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
                                                   int b_end, int b_step, int ablate) {
   auto Pb = [&](int k) { return reinterpret_cast<bf16*>(smem + k * C3D_P); };
   auto DAb = [&](int k) { return reinterpret_cast<float*>(smem + 2 * C3D_P + k * C3V_DA); };
+  // pool2 codes of image j in AM[j & 1], issued in step j (pool2 of image j runs in step j+1)
   auto AMb = [&](int k) { return reinterpret_cast<uint8_t*>(smem + 2 * (C3D_P + C3V_DA) + k * C3D_AM); };
   auto Sb = [&](int k) { return smem + 2 * (C3D_P + C3V_DA + C3D_AM) + k * C3S_B; };
+  auto codes_dma = [&](int j, int lane) {
+    const uint8_t* src = idx2 + (int64_t)(b_first + j * b_step) * 6400;
+    uint8_t* AM = AMb(j & 1);
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      if (k * 64 + lane < 400) glds16_sv(src, (k * 64 + lane) * 16, AM + k * 1024);
+  };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = b_first < b_end ? (b_end - b_first + b_step - 1) / b_step : 0;
@@ -1744,21 +1752,32 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
       if (s < n && !(ablate & 2)) {
         const bf16* P = Pb(s & 1);
         float* DA = DAb(s & 1);
+        // the 13 (m-tile, ky) groups with a non-zero dz3 row, in order; group g+1's 4 B fragments are read
+        // while group g's 12 MFMAs run (the reads issued right before their MFMAs had exposed ~100 cycles per
+        // group)
+        constexpr int NG = 13;
+        auto gmt = [](int g) { return g < 2 ? 0 : (g < 11 ? (g - 2) / 3 + 1 : 4); };
+        auto gky = [](int g) { return g < 2 ? g : (g < 11 ? (g - 2) % 3 : g - 10); };
+        auto readB = [&](int g, bf16x8 (&b)[4]) {
 #pragma unroll
-        for (int mt = 0; mt < 5; ++mt) {
-          f32x4 acc[3] = {zero_f32x4(), zero_f32x4(), zero_f32x4()};
+          for (int ks = 0; ks < 4; ++ks)
+            b[ks] = *reinterpret_cast<const bf16x8*>(P + pbase + (2 * gmt(g) - gky(g)) * C3_PY + ks * 32);
+        };
+        bf16x8 bfa[4], bfb[4];
+        readB(0, bfa);
+        f32x4 acc[3];
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky) {
-            if ((mt == 0 && ky == 2) || (mt == 4 && ky == 0)) continue;
-            bf16x8 bfr[4];
+        for (int g = 0; g < NG; ++g) {
+          const int mt = gmt(g), ky = gky(g);
+          bf16x8(&bcur)[4] = (g & 1) ? bfb : bfa;
+          bf16x8(&bnxt)[4] = (g & 1) ? bfa : bfb;
+          if (g + 1 < NG) readB(g + 1, bnxt);
+          if (g == 0 || gmt(g - 1) != mt) acc[0] = acc[1] = acc[2] = zero_f32x4();
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-              bfr[ks] = *reinterpret_cast<const bf16x8*>(P + pbase + (2 * mt - ky) * C3_PY + ks * 32);
+          for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-              for (int kx = 0; kx < 3; ++kx) acc[kx] = mfma16x16x32(aw[(3 * ky + kx) * 4 + ks], bfr[ks], acc[kx]);
-          }
+            for (int kx = 0; kx < 3; ++kx) acc[kx] = mfma16x16x32(aw[(3 * ky + kx) * 4 + ks], bcur[ks], acc[kx]);
+          if (g + 1 < NG && gmt(g + 1) == mt) continue;
           // col2im along the row in registers: da2(x) = acc0(x) + acc1(x-1) + acc2(x-2), the shifted terms
           // by DPP row shifts inside each 16-lane group (= 2 dz3 rows x 8 columns; a term that would cross
           // into the next row is zeroed at its source lane); column 8 = acc1(7) + acc2(6), column 9 =
@@ -1812,13 +1831,7 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
 #pragma unroll
           for (int k = 0; k < 6; ++k) c3s_glds(da3m, idx3, b_first + (s + 2) * b_step, Sb(s & 1), k, lane);
         }
-        if (s < n) {
-          const uint8_t* src = idx2 + (int64_t)(b_first + s * b_step) * 6400;
-          uint8_t* AM = AMb(s & 1);
-#pragma unroll
-          for (int k = 0; k < 7; ++k)
-            if (k * 64 + lane < 400) glds16_sv(src, (k * 64 + lane) * 16, AM + k * 1024);
-        }
+        if (s < n) codes_dma(s, lane);
       }
       if (s + 1 < n) {
         C3Pre pre;
@@ -1826,6 +1839,7 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
         c3_expand(pre, vt, row_ptr(Pb((s + 1) & 1)));
       }
       if (s >= 1 && vt < 176 && !(ablate & 1)) c3_pool2_bwd(DAb((s - 1) & 1), AMb((s - 1) & 1), dz2, b_first + (s - 1) * b_step, vt);
+      // (issuing image s+1's codes a step earlier and leaving them in flight measured slower)
       if (dma) c_dma_wait();
       lds_barrier();
     }
@@ -1925,6 +1939,7 @@ __device__ __forceinline__ void conv3_wgrad8_role(char* smem, const bf16* __rest
       }
       if (ks == 0 && i + 2 < n) expand(Sb(i & 1), Db(st));  // image i+2's D, under the second k-step
     }
+    // (letting image i+2's a2 copies stay in flight across the barrier measured 50 us slower)
     c_dma_wait();
     lds_barrier();
   }
@@ -1954,7 +1969,7 @@ __global__ __launch_bounds__(512, 1) void conv3_bwd8_kernel(const bf16* __restri
     return;
   }
   const int w = blk - n_dgrad;
-  conv3_wgrad8_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w);
+  if (!(ablate & 4)) conv3_wgrad8_role(smem, a2, da3m, idx3, slabs, B, n_wgrad, w);
   if (dz2 == nullptr || b_dgrad >= B) return;
   __syncthreads();  // LDS changes role
   conv3_dgrad8_role(smem, da3m, idx3, idx2, packed, dz2, b_dgrad + w, B, n_wgrad, ablate);
@@ -2588,30 +2603,38 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
     f32x4 acc1[2][2];
 #pragma unroll
     for (int m = 0; m < 2; ++m) acc1[m][0] = acc1[m][1] = zero_f32x4();
-    bf16x8 pz[4];
-    uint4 pc = make_uint4(0, 0, 0, 0);
-    uint32_t xu = 0;
-    float4 xf = make_float4(0.f, 0.f, 0.f, 0.f);
-    auto load = [&](int bb) {
+    // the next images' inputs in registers, two sets: image j's set is j & 1, loaded two steps before it is
+    // staged (one step of latency hiding was not enough: staging alone ran at the per-CU latency bound)
+    // the next images' inputs in registers, two sets: image j's set is j & 1, loaded two steps before it is
+    // staged (one step of latency hiding was not enough: staging alone ran at the per-CU latency bound).
+    // (Staging dz2 from the MFMA waves instead measured 935 -> 1024 us: they are the critical path.)
+    struct Regs {
+      bf16x8 pz[4];
+      uint4 pc;
+      uint32_t xu;
+      float4 xf;
+    };
+    Regs r0, r1;
+    auto load = [&](Regs& r, int bb) {
       const bf16x8* src = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (vt + 256 * j < 968) pz[j] = src[vt + 256 * j];
-      if (vt < C1I_IMG / 16) pc = reinterpret_cast<const uint4*>(idx1 + (int64_t)bb * C1I_IMG)[vt];
-      c1_load<U8>(xin, bb, vt, xu, xf);
+        if (vt + 256 * j < 968) r.pz[j] = src[vt + 256 * j];
+      if (vt < C1I_IMG / 16) r.pc = reinterpret_cast<const uint4*>(idx1 + (int64_t)bb * C1I_IMG)[vt];
+      c1_load<U8>(xin, bb, vt, r.xu, r.xf);
     };
-    auto stage = [&](int k2, int k3) {
+    auto stage = [&](const Regs& r, int k2, int k3) {
       bf16* P = Pb(k2);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int c = vt + 256 * j;
         if (c < 968) {
           const int pos = c >> 3, cc = (c & 7) * 8;
-          *reinterpret_cast<bf16x8*>(P + ((pos / 11 + 2) * C2_PW + pos % 11 + 2) * C2_PRS + cc) = pz[j];
+          *reinterpret_cast<bf16x8*>(P + ((pos / 11 + 2) * C2_PW + pos % 11 + 2) * C2_PRS + cc) = r.pz[j];
         }
       }
-      if (vt < C1I_IMG / 16) reinterpret_cast<uint4*>(Cb(k3))[vt] = pc;
-      c1_store<U8, 5, C1W_RS, C1W_CS>(Xb(k3), vt, xu, xf, mean, inv_std, in_scale);
+      if (vt < C1I_IMG / 16) reinterpret_cast<uint4*>(Cb(k3))[vt] = r.pc;
+      c1_store<U8, 5, C1W_RS, C1W_CS>(Xb(k3), vt, r.xu, r.xf, mean, inv_std, in_scale);
     };
     auto c1_step = [&](int ks, const bf16* O, const bf16* xs, const uint8_t* CB) {
       const int py = ks >> 1;
@@ -2641,15 +2664,17 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
       }
     };
     if (n > 0) {
-      load(block);
-      stage(0, 0);
-      if (n > 1) load(block + nblocks);
+      load(r0, block);
+      stage(r0, 0, 0);
+      if (n > 1) load(r1, block + nblocks);
+      if (n > 2) load(r0, block + 2 * nblocks);
     }
     lds_barrier();  // [B1]
-    for (int s = 0; s <= n; ++s) {
+    // step s: stage image s+1 (its set (s+1) & 1), refill that set with image s+3, conv1 wgrad of image s-1
+    auto step = [&](int s, Regs& rs) {
       if (s + 1 < n) {
-        stage((s + 1) & 1, (s + 1) % 3);
-        if (s + 2 < n) load(block + (s + 2) * nblocks);
+        stage(rs, (s + 1) & 1, (s + 1) % 3);
+        if (s + 3 < n) load(rs, block + (s + 3) * nblocks);
       }
       if (s >= 1 && !(ablate & 1)) {
         const bf16* O = Ob((s - 1) & 1);
@@ -2658,6 +2683,10 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
         for (int ks = vw; ks < 26; ks += 4) c1_step(ks, O, xs, CB);
       }
       lds_barrier();
+    };
+    for (int s = 0; s <= n; s += 2) {  // unrolled by 2: register sets are not indexable
+      step(s, r1);
+      if (s + 1 <= n) step(s + 1, r0);
     }
     // combine the 4 K-groups in a fixed order (deterministic) and write this workgroup's conv1 slab
     __syncthreads();  // [R0]
@@ -2711,23 +2740,27 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
   // images slice, slice + nslices, ... (as the dgrad workgroups)
   const int n = slice < B ? (B - slice + nslices - 1) / nslices : 0;
   auto img = [&](int i) { return slice + i * nslices; };
-  bf16x8 pz[2], pa[2];
-  auto load = [&](int bb) {
+  // inputs of later images in registers, two sets (image j: set j & 1, loaded two images before it is staged)
+  struct Regs {
+    bf16x8 pz[2], pa[2];
+  };
+  Regs r0, r1;
+  auto load = [&](Regs& r, int bb) {
     const bf16x8* zs = reinterpret_cast<const bf16x8*>(dz2 + (int64_t)bb * 121 * 64);
     const bf16x8* as = reinterpret_cast<const bf16x8*>(a1 + (int64_t)bb * 169 * 32);
-    pz[0] = zs[tid];
-    if (tid + 512 < 968) pz[1] = zs[tid + 512];
-    pa[0] = as[tid];
-    if (tid + 512 < 676) pa[1] = as[tid + 512];
+    r.pz[0] = zs[tid];
+    if (tid + 512 < 968) r.pz[1] = zs[tid + 512];
+    r.pa[0] = as[tid];
+    if (tid + 512 < 676) r.pa[1] = as[tid + 512];
   };
-  auto stage = [&](int k) {
+  auto stage = [&](const Regs& r, int k) {
     bf16* D = Db(k);
     bf16* X = Xb(k);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int c = tid + 512 * j;
-      if (c < 968) *reinterpret_cast<bf16x8*>(D + c2_drow(c >> 3) + (c & 7) * 8) = pz[j];
-      if (c < 676) *reinterpret_cast<bf16x8*>(X + (c >> 2) * C2_XRS + (c & 3) * 8) = pa[j];
+      if (c < 968) *reinterpret_cast<bf16x8*>(D + c2_drow(c >> 3) + (c & 7) * 8) = r.pz[j];
+      if (c < 676) *reinterpret_cast<bf16x8*>(X + (c >> 2) * C2_XRS + (c & 3) * 8) = r.pa[j];
     }
   };
   auto readA = [&](int buf, int ks, bf16x8 (&af)[2]) {
@@ -2742,13 +2775,14 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
   };
   __syncthreads();  // zero fill before the first stage
   if (n > 0) {
-    load(img(0));
-    stage(0);
+    load(r0, img(0));
+    stage(r0, 0);
     if (n > 1) {
-      load(img(1));
-      stage(1);
+      load(r1, img(1));
+      stage(r1, 1);
     }
-    if (n > 2) load(img(2));
+    if (n > 2) load(r0, img(2));
+    if (n > 3) load(r1, img(3));
   }
   lds_barrier();
   bf16x8 af[2], afn[2];
@@ -2756,11 +2790,11 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
   auto body = [&](auto h_c) {
     constexpr int H = decltype(h_c)::value;
     constexpr int NJ = H == 0 ? 5 : 4;
-    for (int i = 0; i < n; ++i) {
+    auto image = [&](int i, Regs& rs) {
       const int cur = i % 3;
-      if (i + 2 < n) {  // image i+2 into the buffers image i-1 used; its registers refilled with image i+3
-        stage((i + 2) % 3);
-        if (i + 3 < n) load(img(i + 3));
+      if (i + 2 < n) {  // image i+2 (set rs) into the buffers image i-1 used; rs refilled with image i+4
+        stage(rs, (i + 2) % 3);
+        if (i + 4 < n) load(rs, img(i + 4));
       }
       const int xb = (int)(Xb(cur) - reinterpret_cast<const bf16*>(smem)) + 16 * half + 4 * p;
 #pragma unroll
@@ -2797,6 +2831,10 @@ __device__ __forceinline__ void conv2_wgrad8_role(char* smem, const bf16* __rest
         }
       }
       lds_barrier();
+    };
+    for (int i = 0; i < n; i += 2) {  // unrolled by 2: register sets are not indexable
+      image(i, r0);
+      if (i + 1 < n) image(i + 1, r1);
     }
   };
   if (h == 0)
@@ -2832,7 +2870,7 @@ __global__ __launch_bounds__(512, 1) void conv12_bwd8_kernel(const void* __restr
   if ((int)blockIdx.x < n_dgrad)
     conv12_dgrad8_role<U8>(smem, xin, idx1, dz2, packed, B, blockIdx.x, n_dgrad, mean, inv_std, in_scale, slabs1,
                            ablate);
-  else
+  else if (!(ablate & 4))
     conv2_wgrad8_role(smem, a1, dz2, slabs2, B, nslices, blockIdx.x - n_dgrad);
 }
 
@@ -3094,7 +3132,7 @@ static bool c3_v3(int B) {
 }
 
 // timing-only ablations of the 8-wave conv3 backward (wrong results): bit 0 skips the pool2 backward,
-// bit 1 the dgrad MFMA phase (RINGDP_C3_ABLATE)
+// bit 1 the dgrad MFMA phase, bit 2 the weight gradient (RINGDP_C3_ABLATE)
 static int c3_ablate() {
   static const int v = [] {
     const char* e = getenv("RINGDP_C3_ABLATE");
@@ -3170,8 +3208,8 @@ static bool c12_v3(int B) {
   return on && B > fc_in_c3_max_batch();
 }
 
-// timing-only ablations of the 8-wave conv12 dgrad role (wrong results): bit 0 skips conv1 wgrad, bit 1 the
-// conv2 dgrad MFMAs (RINGDP_C12_ABLATE)
+// timing-only ablations of the 8-wave conv12 backward (wrong results): bit 0 skips conv1 wgrad, bit 1 the
+// conv2 dgrad MFMAs, bit 2 the conv2 weight gradient (RINGDP_C12_ABLATE)
 static int c12_ablate() {
   static const int v = [] {
     const char* e = getenv("RINGDP_C12_ABLATE");
