@@ -661,47 +661,62 @@ __global__ __launch_bounds__(256, 2) void conv3_fwd_kernel(const bf16* __restric
 // One wave per 16 images; A fragments stream straight from global (16 B per lane, no LDS), the
 // 64 B-fragments (N = 10 padded to 16) sit in LDS.  Unfused from conv3 because reducing 10 logits
 // across 256 lanes per image cost the conv3 kernel more than this whole pass over a3.
-constexpr int FC1_G = 2;  // 16-image groups per workgroup
+constexpr int FC1_G = 8;  // 16-image groups per workgroup
 __global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf16* __restrict__ a3,
                                                       const bf16* __restrict__ packed,
                                                       const float* __restrict__ bfc,
                                                       float* __restrict__ logits, int B) {
   // The 4 waves split K (512 each) and hold their 16 B-fragments in VGPRs, loaded once from the
-  // L2-resident pack: no 64 KiB LDS fill per workgroup (which dominated the old one-wave-per-group
-  // kernel), 8 waves per CU instead of 4.  Partials are summed in a fixed order.
-  __shared__ f32x4 red[3][64];
+  // L2-resident pack.  A bandwidth-bound pass over a3 (4 KB per image): group g+1's A fragments are
+  // loaded while group g's MFMAs and cross-wave sum run (two register sets; one set in flight had run at
+  // ~2.9 TB/s).  Partials are summed in a fixed order.
+  __shared__ f32x4 red[2][3][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bf16x8* src = reinterpret_cast<const bf16x8*>(packed + PFF_OFF);
   bf16x8 w[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) w[j] = src[(wave * 16 + j) * 64 + lane];
-  for (int g = 0; g < FC1_G; ++g) {
-    const int b0 = (blockIdx.x * FC1_G + g) * 16;  // uniform over the workgroup
-    if (b0 >= B) break;
-    const int row = min(b0 + (lane & 15), B - 1);
+  const int g0 = blockIdx.x * FC1_G;
+  const int ng = min(FC1_G, cdiv(B, 16) - g0);
+  auto load = [&](int g, bf16x8 (&av)[16]) {
+    const int row = min((g0 + g) * 16 + (lane & 15), B - 1);
     const bf16x8* ap = reinterpret_cast<const bf16x8*>(a3 + (int64_t)row * 2048) + (lane >> 4) + wave * 64;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) av[j] = ap[j * 4];
+  };
+  auto group = [&](int g, const bf16x8 (&av)[16]) {
+    const int b0 = (g0 + g) * 16;
     f32x4 acc0 = zero_f32x4(), acc1 = zero_f32x4();
 #pragma unroll
     for (int j = 0; j < 16; j += 2) {
-      acc0 = mfma16x16x32(ap[j * 4], w[j], acc0);
-      acc1 = mfma16x16x32(ap[(j + 1) * 4], w[j + 1], acc1);
+      acc0 = mfma16x16x32(av[j], w[j], acc0);
+      acc1 = mfma16x16x32(av[j + 1], w[j + 1], acc1);
     }
     const f32x4 acc = acc0 + acc1;
-    if (wave > 0) red[wave - 1][lane] = acc;
+    if (wave > 0) red[g & 1][wave - 1][lane] = acc;  // two slots: one barrier per group
     __syncthreads();
     if (wave == 0) {
-      const f32x4 t = acc + red[0][lane] + red[1][lane] + red[2][lane];
-      const int n = lane & 15;
-      if (n < 10) {
-        const float bn = bfc[n];
+      const f32x4 t = acc + red[g & 1][0][lane] + red[g & 1][1][lane] + red[g & 1][2][lane];
+      const int nn = lane & 15;
+      if (nn < 10) {
+        const float bn = bfc[nn];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int bb = b0 + (lane >> 4) * 4 + i;
-          if (bb < B) logits[(int64_t)bb * 10 + n] = t[i] + bn;
+          if (bb < B) logits[(int64_t)bb * 10 + nn] = t[i] + bn;
         }
       }
     }
-    __syncthreads();
+  };
+  bf16x8 va[16], vb[16];
+  if (ng > 0) load(0, va);
+  for (int g = 0; g < ng; g += 2) {  // unrolled by 2: register sets are not indexable
+    if (g + 1 < ng) load(g + 1, vb);
+    group(g, va);
+    if (g + 1 < ng) {
+      if (g + 2 < ng) load(g + 2, va);
+      group(g + 1, vb);
+    }
   }
 }
 
