@@ -88,10 +88,12 @@ def parse(argv=None):
                          "fp32: the ConvNet at the reference's precision (fp32 MFMA kernels)")
     ap.add_argument("--no-force-comm", action="store_true",
                     help="at world size 1 skip the bucket all-reduce (default: run it, the N>1 code path)")
-    ap.add_argument("--comm-stream", type=str, default="auto", choices=["auto", "side", "same"],
-                    help="N>1 bucket collectives inside the captured step: side HIP stream (overlaps backward; "
-                         "any second stream costs the graph its batched launch), the compute stream, or auto: "
-                         "both are captured during warmup and the faster one (max over ranks) is timed")
+    ap.add_argument("--comm-stream", type=str, default="split", choices=["split", "side", "same"],
+                    help="placement of the bucket collectives of the captured step: split (default: the step is "
+                         "captured as linear single-stream graph segments cut where buckets become ready, and each "
+                         "bucket's collective runs between them on the comm stream, overlapping the rest of "
+                         "backward), side (inside one graph on a side stream: a forked graph loses HIP's batched "
+                         "launch, +1.2-2 us per kernel) or same (inside one graph on the compute stream: no overlap)")
     ap.add_argument("--comm-stats-steps", type=int, default=20,
                     help="after the timed region: eager steps with device-timed bucket collectives and "
                          "comm-free graph replays for the exposed-comm estimate (0 = skip)")
@@ -249,7 +251,7 @@ def worker(args):
         err = None
         graph = None
         try:
-            graph = StepGraph(static_step, warmup=2).capture()
+            graph = StepGraph(static_step, warmup=2, split_ddp=ddp if split_mode else None).capture()
         except Exception as e:  # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
             sync()
@@ -270,6 +272,12 @@ def worker(args):
 
     _phase(f"model {args.model} dtype {args.dtype} B={B} world={world}: warmup + capture")
     use_graph = on_gpu and not args.no_graph
+    nat_pg = getattr(ddp, "_native_pg", None)
+    # fork-free overlap: linear graph segments, bucket collectives between them on the comm stream
+    split_mode = (use_graph and (world > 1 or force_comm) and args.comm_stream == "split"
+                  and args.comm_hook == "allreduce" and hasattr(nat_pg, "set_same_stream"))
+    if use_graph and hasattr(nat_pg, "set_same_stream") and os.environ.get("RINGDP_COMM_SAME_STREAM") is None:
+        nat_pg.set_same_stream(args.comm_stream == "same")
     graph = None
     n_warm = max(args.warmup, 3)
     if use_graph:
@@ -277,43 +285,30 @@ def worker(args):
         for i in range(2):
             _, x, y = pool[i % len(pool)]
             step_on(x, y)
+        if split_mode and len(ddp.reducer.bucket_numels()) < 2:
+            # one bucket is ready only at the end of backward: nothing to overlap, and a segment boundary plus a
+            # cross-stream wait cost more than the collective on the compute stream inside the one graph
+            split_mode = False
+            if os.environ.get("RINGDP_COMM_SAME_STREAM") is None:
+                nat_pg.set_same_stream(True)
         static_buf.copy_(pool[0][0])
         graph = capture()
         use_graph = graph is not None
 
     comm_stream_note = None
-    nat_pg = getattr(ddp, "_native_pg", None)
-    if use_graph and world > 1 and hasattr(nat_pg, "set_same_stream") and \
-            os.environ.get("RINGDP_COMM_SAME_STREAM") is None and args.comm_stream != "side":
-        # Placement of the bucket collectives in the captured step (a side stream forks
-        # the graph, and a forked graph loses HIP's batched packet launch: +1.2-2 us per kernel).
-        def time_graph(g, n=20):
-            sync()
-            dist.barrier()
-            sync()
-            t0 = time.perf_counter()
-            for i in range(n):
-                static_buf.copy_(pool[i % len(pool)][0], non_blocking=True)
-                g.replay()
-            sync()
-            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            return float(t.item()) / n
-        t_side = time_graph(graph) if args.comm_stream == "auto" else None
-        nat_pg.set_same_stream(True)
-        g_same = capture()
-        if g_same is None:
-            nat_pg.set_same_stream(False)
+    if use_graph and (world > 1 or force_comm) and hasattr(nat_pg, "same_stream"):
+        if split_mode and graph is not None and graph.segments:
+            n_split = sum(1 for p in graph.plan for i in p if i >= 0)
+            comm_stream_note = (
+                f"comm stream between {len(graph.segments)} linear graph segments for {n_split} bucket(s) "
+                "(issued as their gradients are final, overlapping the rest of backward; no fork inside any "
+                "graph), the other bucket(s) inline on the compute stream (estimated shorter than a segment "
+                "boundary, or the last)" if n_split else
+                "compute stream inside the graph (split placement: every bucket collective estimated shorter "
+                "than a segment boundary)")
         else:
-            t_same = time_graph(g_same)
-            if t_side is not None and t_side < t_same:
-                nat_pg.set_same_stream(False)
-                del g_same
-            else:
-                graph = g_same
-            comm_stream_note = ("compute stream" if nat_pg.same_stream() else "side stream") + (
-                f" (autotuned: side {t_side * 1e3:.3f} ms, same {t_same * 1e3:.3f} ms per step)"
-                if t_side is not None else " (--comm-stream same)")
+            comm_stream_note = "compute stream (no overlap)" if nat_pg.same_stream() else \
+                "side stream inside the graph (overlaps backward; forked graph)"
 
     def run_steps(n, g):
         loss = None
@@ -378,17 +373,12 @@ def worker(args):
         sizes_kb = ",".join(f"{b / 1024:.0f}" for b in comm_stats["bucket_bytes"])
         lib = {"rccl": "RCCL", "xgmi": "ringdp xGMI kernels (IPC peer memory)"}.get(nat.backend_name(), nat.backend_name()) \
             if on_gpu else "host ring (gloo)"
+        where = f"collectives on the {comm_stream_note}" if comm_stream_note else (
+            "compute stream" if getattr(nat, "same_stream", lambda: False)() else "side HIP stream")
         if world > 1:
-            where = ""
-            if on_gpu:
-                where = (f", collectives on the {comm_stream_note}" if comm_stream_note else
-                         (", compute stream" if getattr(nat, "same_stream", lambda: False)()
-                          else ", side HIP stream overlapped with backward"))
             comm = (f"{lib} {args.comm_hook} (avg) over {world} ranks, {n_buckets} bucket(s) [{sizes_kb}] KB, "
-                    f"cap {args.bucket_mb} MB" + where)
+                    f"cap {args.bucket_mb} MB, " + where)
         elif force_comm:
-            where = ("on the compute stream (a one-rank collective has nothing to overlap)"
-                     if getattr(nat, "same_stream", lambda: False)() else "on the side stream")
             comm = (f"{lib} {args.comm_hook} (avg) over 1 rank, forced so N=1 runs the reducer + collective "
                     f"path of N>1, {where}; {n_buckets} bucket(s) [{sizes_kb}] KB, cap {args.bucket_mb} MB")
         else:

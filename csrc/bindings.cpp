@@ -437,6 +437,23 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
                return std::make_shared<PyWork>(res);
              });
            })
+      .def("set_capture_split",
+           [](Reducer& r, py::object fn) {
+             if (fn.is_none()) {
+               r.set_capture_split(nullptr);
+               return;
+             }
+             auto holder = std::shared_ptr<py::function>(new py::function(fn.cast<py::function>()),
+                                                         [](py::function* f) {
+                                                           py::gil_scoped_acquire gil;
+                                                           delete f;
+                                                         });
+             r.set_capture_split([holder](int64_t idx) -> bool {
+               py::gil_scoped_acquire gil;
+               return (*holder)(idx).cast<bool>();
+             });
+           })
+      .def("launch_collective", &Reducer::launch_collective, py::call_guard<py::gil_scoped_release>())
       .def("grad_slots", &Reducer::grad_slots)
       .def("flat_buffers", &Reducer::flat_buffers)
       .def("param_offsets", &Reducer::param_offsets)

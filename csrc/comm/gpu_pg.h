@@ -80,12 +80,15 @@ class GpuPG : public ProcessGroup {
   hipStream_t comm_stream() const { return comm_stream_.stream(); }
   std::chrono::milliseconds timeout() const { return timeout_; }
   bool same_stream() const { return same_stream_; }
+  void set_caller_stream_ops(bool on) override { caller_ops_ = on; }
+  // ops go to the caller's stream: same-stream mode, or an inline op (set_caller_stream_ops)
+  bool on_caller_stream() const { return same_stream_ || caller_ops_; }
   // Switch between the caller's stream and the side stream for later ops (drains the device first:
   // nothing issued under the old placement is still in flight).  For A/B placement tuning.
   void set_same_stream(bool v);
   // the stream the next op will be issued on (the caller's in same-stream mode, else the comm stream)
   c10::hip::HIPStreamMasqueradingAsCUDA op_stream() const {
-    return same_stream_ ? c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_) : comm_stream_;
+    return on_caller_stream() ? c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(device_) : comm_stream_;
   }
 
   // Host-blocks until every eagerly issued op has completed and clears the watchdog list, so
@@ -141,6 +144,7 @@ class GpuPG : public ProcessGroup {
   bool eager_aux_since_join_ = false;
   bool timing_ = false;
   bool same_stream_ = false;  // issue collectives on the caller's stream (see init_common)
+  bool caller_ops_ = false;   // ... for the ops issued while set_caller_stream_ops(true)
   bool async_error_handling_ = true;
   std::atomic<bool> stopped_{false};
 
@@ -182,7 +186,7 @@ std::shared_ptr<Work> GpuPG::launch(OpType op, const std::vector<at::Tensor>& te
   RINGDP_HIP_CHECK(hipStreamIsCapturing(cur.stream(), &cap));
   const bool captured = cap == hipStreamCaptureStatusActive;
   auto work = std::make_shared<GpuWork>(op, next_seq(), this, captured, timing_ && !captured);
-  const bool same_stream = same_stream_;
+  const bool same_stream = on_caller_stream();
   hipStream_t cs = same_stream ? cur.stream() : comm_stream_.stream();
   // Fence: the comm stream waits for everything queued so far on the producer stream.
   if (!same_stream) {

@@ -130,6 +130,9 @@ class ProcessGroup : public std::enable_shared_from_this<ProcessGroup> {
   int rank() const { return rank_; }
   int size() const { return size_; }
   virtual std::string backend_name() const = 0;
+  // While on, collectives are issued on the caller's current stream even in side-stream mode (GPU groups;
+  // the reducer's inline buckets inside a segmented hipGraph capture).  No-op elsewhere.
+  virtual void set_caller_stream_ops(bool /*on*/) {}
 
   virtual std::shared_ptr<Work> allreduce(std::vector<at::Tensor>& tensors, ReduceOp op) = 0;
   // Many tensors reduced as one fused op (one flat buffer / one RCCL group).

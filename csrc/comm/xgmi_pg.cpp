@@ -91,7 +91,7 @@ std::string XgmiPG::backend_failure() {
 
 at::Tensor XgmiPG::scratch(int64_t nbytes) {
   auto opts = at::TensorOptions().dtype(at::kByte).device(at::kCUDA, device_);
-  if (same_stream_) return at::empty({std::max<int64_t>(nbytes, 16)}, opts);
+  if (on_caller_stream()) return at::empty({std::max<int64_t>(nbytes, 16)}, opts);
   c10::hip::HIPStreamGuardMasqueradingAsCUDA g(comm_stream_);
   return at::empty({std::max<int64_t>(nbytes, 16)}, opts);
 }
@@ -338,7 +338,7 @@ std::shared_ptr<Work> XgmiPG::send(at::Tensor& tensor, int dst, int /*tag*/) {
   RINGDP_CHECK(dst >= 0 && dst < size_ && dst != rank_, "send: invalid peer ", dst);
   return launch(OpType::SEND, {tensor}, [&](hipStream_t s) -> hipStream_t {
     const int64_t nb = tensor.numel() * static_cast<int64_t>(tensor.element_size());
-    if (same_stream_) {  // one stream by request: the caller orders sends and receives
+    if (on_caller_stream()) {  // one stream by request: the caller orders sends and receives
       eng_->send(tensor.data_ptr(), nb, dst, s);
       return s;
     }

@@ -344,6 +344,23 @@ void Reducer::launch_bucket(Bucket& b, int64_t index) {
     b.work.reset();
     return;
   }
+  if (split_ && hook_ == CommHook::ALLREDUCE) {  // segmented capture
+    split_this_iter_ = true;
+    if (split_(index)) {  // the replay issues the collective between segments
+      b.work.reset();
+      return;
+    }
+    std::vector<at::Tensor> v{b.flat};  // inline: captured on the compute stream
+    pg_->set_caller_stream_ops(true);
+    try {
+      b.work = pg_->allreduce(v, ReduceOp::AVG);
+    } catch (...) {
+      pg_->set_caller_stream_ops(false);
+      throw;
+    }
+    pg_->set_caller_stream_ops(false);
+    return;
+  }
   switch (hook_) {
     case CommHook::ALLREDUCE: {
       std::vector<at::Tensor> v{b.flat};
@@ -424,7 +441,17 @@ void Reducer::finalize_backward() {
       }
     }
   }
+  if (split_this_iter_) {  // segmented capture: the join point before the optimizer
+    split_this_iter_ = false;
+    split_(-1);
+  }
   ++iteration_;
+}
+
+std::shared_ptr<Work> Reducer::launch_collective(int64_t index) {
+  RINGDP_CHECK(index >= 0 && index < static_cast<int64_t>(buckets_.size()), "reducer: bad bucket index ", index);
+  std::vector<at::Tensor> v{buckets_[index].flat};
+  return pg_->allreduce(v, ReduceOp::AVG);
 }
 
 }  // namespace ringdp

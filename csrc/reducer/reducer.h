@@ -85,6 +85,20 @@ class Reducer {
   // also folds the samples into stats().
   std::vector<double> collect_comm_times();
 
+  // Segmented hipGraph capture (ringdp.utils.graph.StepGraph, split mode): while a split function is set,
+  // each bucket whose collective would be issued (ALLREDUCE hook) asks split(index) first.  true: the capture
+  // ended its current graph segment there and the replay issues the collective between segments on the
+  // comm stream (launch_collective), overlapping the rest of backward; false: the collective is captured
+  // inline on the compute stream (worth less than a segment boundary, or the last bucket, which nothing
+  // follows).  The end of backward calls split(-1), the join point before the optimizer segment.  Every
+  // segment stays a single-stream chain: no fork inside a graph.
+  using SplitFn = std::function<bool(int64_t)>;
+  void set_capture_split(SplitFn fn) {
+    std::lock_guard<std::mutex> lk(mu_);
+    split_ = std::move(fn);
+  }
+  std::shared_ptr<Work> launch_collective(int64_t index);
+
   // Internal: invoked from the AccumulateGrad post hook.
   void autograd_hook(int64_t index);
 
@@ -126,6 +140,8 @@ class Reducer {
   std::mutex mu_;
   CommHook hook_ = CommHook::ALLREDUCE;
   PyHook py_hook_;
+  SplitFn split_;
+  bool split_this_iter_ = false;
   bool expect_hooks_ = false;
   bool require_sync_ = true;
   bool finalize_queued_ = false;

@@ -144,14 +144,17 @@ def test_hipgraph_step_matches_eager(world1):
         torch.testing.assert_close(pa, pb, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("hook,stream", [("allreduce", "side"), ("bf16", "side"), ("allreduce", "same")])
+@pytest.mark.parametrize("hook,stream", [("allreduce", "side"), ("bf16", "side"), ("allreduce", "same"),
+                                         ("allreduce", "split")])
 def test_forced_comm_eager_and_graph(world1, monkeypatch, hook, stream):
     """RINGDP_DDP_FORCE_COMM=1 runs the bucket all-reduces on the one-rank RCCL group: the side
     stream, the event fork/join and RCCL inside hipGraph capture are exercised on one GPU (the N>1
     configuration, forced with RINGDP_COMM_SAME_STREAM=0), as is the compute-stream issue a one-rank
     group uses by default; the result must match the no-communication run (AVG over one rank is the
-    identity)."""
-    monkeypatch.setenv("RINGDP_COMM_SAME_STREAM", "0" if stream == "side" else "1")
+    identity).  ``split``: the step captured as linear graph segments with each bucket's collective
+    issued between them on the comm stream at replay (fork-free overlap)."""
+    monkeypatch.setenv("RINGDP_COMM_SAME_STREAM", "1" if stream == "same" else "0")
+    monkeypatch.setenv("RINGDP_SPLIT_MIN_US", "0")  # split at every bucket (the one-rank estimate is tiny)
     from ringdp.models import ConvNet
     from ringdp.nn import CrossEntropyLoss
     from ringdp.optim import SGD
@@ -195,7 +198,11 @@ def test_forced_comm_eager_and_graph(world1, monkeypatch, hook, stream):
         sx.copy_(x)
         sy.copy_(y)
         step()
-    g = StepGraph(step, warmup=0).capture()
+    g = StepGraph(step, warmup=0, split_ddp=d1 if stream == "split" else None).capture()
+    if stream == "split":  # forced split: a segment per non-last bucket + the join before the last one
+        nb = len(d1.reducer.bucket_numels())
+        assert nb >= 2 and len(g.segments) == nb + 1, (len(g.segments), nb, g.plan)
+        assert [i for p in g.plan for i in p] == list(range(nb - 1)) + [-1], g.plan
     for x, y in data[3:]:
         sx.copy_(x)
         sy.copy_(y)

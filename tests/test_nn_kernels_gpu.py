@@ -83,7 +83,15 @@ def _nhwc(x, cp):
     return out.bfloat16().contiguous()
 
 
-@pytest.mark.parametrize("case", CONV_CASES + [(4, 64, 64, 256, 1, 1, 0), (2, 256, 64, 64, 1, 1, 0)])
+SPLITK_CASES = [
+    # ResNet-18 CIFAR-shape layers 3-4 (few output tiles: split-K with the in-kernel last-arriver sum)
+    (256, 256, 4, 512, 3, 2, 1),
+    (64, 128, 4, 256, 3, 1, 1),
+    (32, 512, 2, 512, 1, 1, 0),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES + SPLITK_CASES + [(4, 64, 64, 256, 1, 1, 0), (2, 256, 64, 64, 1, 1, 0)])
 def test_conv_fwd_dgrad_wgrad(case):
     """Implicit-GEMM conv forward (+ BN statistics), data and weight gradient; the last two cases are
     large pointwise convs (M >= 8192 rows), plain GEMMs on the same kernels."""
@@ -118,11 +126,34 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert rel(dw, wr.grad) < 5e-3
 
 
+def test_splitk_repeatable():
+    """Split-K conv data / weight gradients (fixed-order partial sums): bitwise equal across runs."""
+    N, Cin, H, K, R, stride, pad = SPLITK_CASES[0]
+    torch.manual_seed(3)
+    dev = "cuda"
+    x = _nhwc(torch.randn(N, Cin, H, H, device=dev), Cin)
+    w = torch.randn(K, Cin, R, R, device=dev) * 0.1
+    _, crsk = C().pack_conv_weight(w, Cin)
+    P = (H + 2 * pad - R) // stride + 1
+    dz = torch.randn(N, P, P, K, device=dev).bfloat16()
+    res = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    dx1 = C().conv2d_dgrad(dz, crsk, H, H, stride, pad, 1, res)
+    dx2 = C().conv2d_dgrad(dz, crsk, H, H, stride, pad, 1, res)
+    assert torch.equal(dx1, dx2)
+    dw1, dw2 = torch.empty_like(w), torch.empty_like(w)
+    C().conv2d_wgrad(dz, x, dw1, stride, pad, 1)
+    C().conv2d_wgrad(dz, x, dw2, stride, pad, 1)
+    assert torch.equal(dw1, dw2)
+
+
+@pytest.mark.parametrize("shape", [(6, 7, 64), (256, 2, 256), (256, 1, 512), (64, 32, 64)])
 @pytest.mark.parametrize("relu,resid", [(True, False), (True, True), (False, False)])
-def test_batchnorm_fwd_bwd(relu, resid):
+def test_batchnorm_fwd_bwd(relu, resid, shape):
+    """BN forward / backward over the ResNet-18 CIFAR-shape sizes (few partial rows: the apply kernel sums
+    them itself) and a 65536-row tensor (two-level reduction)."""
     torch.manual_seed(int(relu) * 2 + int(resid))
     dev = "cuda"
-    N, H, Cc = 6, 7, 64
+    N, H, Cc = shape
     z = (torch.randn(N, H, H, Cc, device=dev) * 2 + 0.5).bfloat16()
     gamma = torch.rand(Cc, device=dev) + 0.5
     beta = torch.randn(Cc, device=dev) * 0.1

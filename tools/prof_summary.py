@@ -5,6 +5,10 @@ import sys
 
 
 def short(name: str) -> str:
+    if "gemm_kernel<" in name:  # keep the loader pair: the instantiations are different convolutions
+        args = name.split("gemm_kernel<", 1)[1].split(">(", 1)[0]
+        args = re.sub(r"ringdp::kern::|\(anonymous namespace\)::", "", args)
+        return f"gemm_kernel<{args}>"
     m = re.search(r"(\w+_kernel)(?:<[^>]*>)?", name.replace("EEv", "E"))
     if m:
         k = m.group(1)
