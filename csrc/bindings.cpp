@@ -490,7 +490,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_bf16", &ops::transpose_bf16);
   m.def("sgd_flat", &ops::sgd_flat, py::arg("param"), py::arg("grad"), py::arg("momentum_buf"),
         py::arg("hyper"), py::arg("first_step"), py::arg("lr_tensor") = py::none(),
-        py::arg("grad_scale") = py::none());
+        py::arg("grad_scale") = py::none(), py::arg("packed") = py::none(),
+        py::arg("pack_offsets") = std::vector<int64_t>{});
   m.def("sgd_multi", &ops::sgd_multi, py::arg("params"), py::arg("grads"), py::arg("bufs"),
         py::arg("hyper"), py::arg("first_step"), py::arg("lr_tensor") = py::none(),
         py::arg("grad_scale") = py::none());
@@ -608,7 +609,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv1_fwd_pack", &ops::cn_conv1_fwd_pack);
   m.def("cn_forward_buffers", &ops::cn_forward_buffers);
-  m.def("cn_forward_fused", &ops::cn_forward_fused);
+  m.def("cn_forward_fused", &ops::cn_forward_fused, py::arg("x"), py::arg("w1"), py::arg("b1"), py::arg("w2"),
+        py::arg("b2"), py::arg("w3"), py::arg("b3"), py::arg("wfc"), py::arg("bfc"), py::arg("mean"), py::arg("std"),
+        py::arg("in_scale"), py::arg("a1"), py::arg("idx1"), py::arg("a2"), py::arg("idx2"), py::arg("packed"),
+        py::arg("do_pack") = true);
   m.def("cn_conv2_fwd", &ops::cn_conv2_fwd);
   m.def("cn_conv3_fc_fwd", &ops::cn_conv3_fc_fwd);
   m.def("cn_conv3_fc_bwd", &ops::cn_conv3_fc_bwd, py::arg("a2"), py::arg("idx2"), py::arg("a3"), py::arg("idx3"),

@@ -36,6 +36,7 @@
 
 #include "device_common.h"
 #include "kernels.h"
+#include "sgd_device.h"
 
 namespace ringdp {
 namespace kern {
@@ -124,6 +125,79 @@ static_assert(PACK_TOTAL % 4 == 0 && P2F_OFF % 4 == 0, "packed regions in whole 
 
 __global__ __launch_bounds__(256) void pack_weights_kernel(PackSrc ws, bf16* __restrict__ out) {
   pack_range(ws, out, 0, blockIdx.x, gridDim.x);
+}
+
+// The inverse of pack_value: the packed slots of one master weight element (conv1: 1, conv2 / conv3 / fc1: the
+// forward and the backward copy), so the optimizer can write next step's fragments as it updates the fp32
+// masters (no pack launch per forward).  `which`: 0 conv1 [32][1][5][5], 1 conv2 [64][32][3][3],
+// 2 conv3 [128][64][3][3], 3 fc1 [10][2048]; l: the element's index in its tensor.  Padding slots (conv1
+// taps past 5x5, fc1 columns past 10) never change: the first pack zeroed them.
+__device__ __forceinline__ int frag_slot(int ks, int lane, int j, int nt, int KS) { return ((nt * KS + ks) * 64 + lane) * 8 + j; }
+__device__ __forceinline__ void pack_scatter(int which, int l, bf16 v, bf16* __restrict__ out) {
+  if (which == 0) {
+    const int co = l / 25, r = l - co * 25, kh = r / 5, kw = r - kh * 5;
+    out[P1_OFF + frag_slot(kh >> 2, ((kh & 3) << 4) | (co >> 1), kw, co & 1, 2)] = v;
+  } else if (which == 1) {  // forward: k = tap*32 + ci; data gradient: k = (8 - tap)*64 + co, n = ci
+    const int co = l / 288, ci = (l / 9) & 31, t = l % 9;
+    const int kf = t * 32 + ci, kd = (8 - t) * 64 + co;
+    out[P2F_OFF + frag_slot(kf >> 5, (((kf >> 3) & 3) << 4) | (co & 15), kf & 7, co >> 4, 9)] = v;
+    out[P2D_OFF + frag_slot(kd >> 5, (((kd >> 3) & 3) << 4) | (ci & 15), kd & 7, ci >> 4, 18)] = v;
+  } else if (which == 2) {  // forward: k = tap*64 + ci; data gradient (scatter form): ks = tap*4 + co/32
+    const int co = l / 576, ci = (l / 9) & 63, t = l % 9;
+    const int kf = t * 64 + ci;
+    out[P3F_OFF + frag_slot(kf >> 5, (((kf >> 3) & 3) << 4) | (co & 15), kf & 7, co >> 4, 18)] = v;
+    out[P3D_OFF + frag_slot(t * 4 + (co >> 5), (((co >> 3) & 3) << 4) | (ci & 15), co & 7, ci >> 4, 36)] = v;
+  } else {  // fc1 column c = co*16 + window: backward [window][co][n], forward B fragments k = window*128 + co
+    const int n = l >> 11, c = l & 2047, co = c >> 4, wd = c & 15;
+    out[PFC_OFF + wd * 1280 + co * 10 + n] = v;
+    const int k = wd * 128 + co;
+    out[PFF_OFF + frag_slot(k >> 5, (((k >> 3) & 3) << 4) | n, k & 7, 0, 0)] = v;
+  }
+}
+
+struct PackDst {
+  bf16* out;
+  int64_t off[4];  // each weight's first element in the flat parameter range
+};
+constexpr int kPackLen[4] = {32 * 25, 64 * 32 * 9, 128 * 64 * 9, 10 * 2048};
+
+// SGD over a flat fp32 range (params / grads / momentum laid out identically, as elementwise.hip's
+// sgd_flat_kernel) that also stores every updated ConvNet weight into its packed bf16 slots.
+template <bool MOM>
+__global__ __launch_bounds__(256) void cn_sgd_pack_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                          float* __restrict__ m, int64_t n, SgdArgs a, PackDst d) {
+  const SgdDev sd = load_sgd(a);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pv = reinterpret_cast<float4*>(p)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float4 mv = MOM ? reinterpret_cast<float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    sgd_elem<MOM>(pv.x, gv.x, mv.x, sd);
+    sgd_elem<MOM>(pv.y, gv.y, mv.y, sd);
+    sgd_elem<MOM>(pv.z, gv.z, mv.z, sd);
+    sgd_elem<MOM>(pv.w, gv.w, mv.w, sd);
+    reinterpret_cast<float4*>(p)[i] = pv;
+    if (MOM) reinterpret_cast<float4*>(m)[i] = mv;
+    const float v[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int64_t l0 = 4 * i - d.off[w];
+      if (l0 + 3 < 0 || l0 >= kPackLen[w]) continue;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (l0 + k >= 0 && l0 + k < kPackLen[w]) pack_scatter(w, (int)(l0 + k), (bf16)v[k], d.out);
+    }
+  }
+  for (int64_t i = n4 * 4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pv = p[i], mv = MOM ? m[i] : 0.f;
+    sgd_elem<MOM>(pv, g[i], mv, sd);
+    p[i] = pv;
+    if (MOM) m[i] = mv;
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      if (i >= d.off[w] && i - d.off[w] < kPackLen[w]) pack_scatter(w, (int)(i - d.off[w]), (bf16)pv, d.out);
+  }
 }
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -3053,10 +3127,21 @@ void cn_conv1_fwd(const void* x, bool u8, const void* packed, const float* b1, v
     conv1_fwd_kernel<false, false><<<grid, 256, 0, s>>>(x, pk, b1, a1b, idx1, B, mean, inv_std, in_scale, none, nullptr, grid);
 }
 
+void cn_sgd_flat_pack(float* p, const float* g, float* m, int64_t n, const SgdArgs& a, const int64_t* offsets,
+                      void* packed, hipStream_t s) {
+  if (n <= 0) return;
+  PackDst d{static_cast<bf16*>(packed), {offsets[0], offsets[1], offsets[2], offsets[3]}};
+  const int grid = std::max<int64_t>(1, std::min<int64_t>((n / 4 + 256) / 256, 2048));
+  if (m && a.momentum != 0.f)
+    cn_sgd_pack_kernel<true><<<grid, 256, 0, s>>>(p, g, m, n, a, d);
+  else
+    cn_sgd_pack_kernel<false><<<grid, 256, 0, s>>>(p, g, m, n, a, d);
+}
+
 void cn_forward_fused(const void* x, bool u8, const float* const* w, const float* b1, const float* b2,
                       const float* b3, const float* bfc, void* packed, void* a1, uint8_t* idx1, void* a2,
                       uint8_t* idx2, void* a3, uint8_t* idx3, float* logits, int B, float mean, float inv_std,
-                      float in_scale, unsigned* sync, hipStream_t s) {
+                      float in_scale, unsigned* sync, hipStream_t s, bool do_pack) {
   const int conv = clampi(B, 1, wpc("FF", 1) * num_cus());  // 121 KiB LDS: one 512-thread workgroup per CU
   const PackSrc ws{w[0], w[1], w[2], w[3]};
   bf16* pk = static_cast<bf16*>(packed);
@@ -3083,7 +3168,8 @@ void cn_forward_fused(const void* x, bool u8, const float* const* w, const float
                                                          sync, p2split);
     return;
   }
-  pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(ws, pk);
+  // (do_pack false: the optimizer wrote these fragments when it last updated the weights)
+  if (do_pack) pack_weights_kernel<<<cdiv(PACK_TOTAL, 1024), 256, 0, s>>>(ws, pk);
   const bool fc_in = B <= fc_fused_max_batch();  // else fc1 as its own MFMA pass over a3
   float* lg = fc_in ? logits : nullptr;
   if (u8)

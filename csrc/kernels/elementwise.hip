@@ -8,6 +8,7 @@
 //    fixed order) and backward (softmax - target).
 #include "device_common.h"
 #include "kernels.h"
+#include "sgd_device.h"
 
 namespace ringdp {
 namespace kern {
@@ -130,36 +131,6 @@ __global__ void cast_f16_f32_kernel(const _Float16* __restrict__ src, float* __r
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     dst[i] = (float)src[i];
-}
-
-struct SgdDev {
-  float lr, momentum, dampening, weight_decay, inv_scale;
-  bool nesterov, maximize, first;
-};
-
-__device__ __forceinline__ SgdDev load_sgd(const SgdArgs& a) {
-  SgdDev d;
-  d.lr = a.lr_ptr ? *a.lr_ptr : a.lr;
-  d.inv_scale = a.grad_scale_ptr ? 1.0f / *a.grad_scale_ptr : 1.0f;
-  d.momentum = a.momentum;
-  d.dampening = a.dampening;
-  d.weight_decay = a.weight_decay;
-  d.nesterov = a.nesterov;
-  d.maximize = a.maximize;
-  d.first = a.first_step;
-  return d;
-}
-
-template <bool MOM>
-__device__ __forceinline__ void sgd_elem(float& p, float g, float& m, const SgdDev& d) {
-  g *= d.inv_scale;
-  if (d.maximize) g = -g;
-  if (d.weight_decay != 0.f) g = fmaf(d.weight_decay, p, g);
-  if (MOM) {
-    m = d.first ? g : fmaf(d.momentum, m, (1.f - d.dampening) * g);
-    g = d.nesterov ? fmaf(d.momentum, m, g) : m;
-  }
-  p = fmaf(-d.lr, g, p);
 }
 
 template <bool MOM>

@@ -177,7 +177,11 @@ void cn_conv3_fc_fwd(const void* a2, const void* packed, const float* b3, const 
 void cn_forward_fused(const void* x, bool u8, const float* const* w, const float* b1, const float* b2,
                       const float* b3, const float* bfc, void* packed, void* a1, uint8_t* idx1, void* a2,
                       uint8_t* idx2, void* a3, uint8_t* idx3, float* logits, int B, float mean, float inv_std,
-                      float in_scale, unsigned* sync, hipStream_t s);  // sync: 2 zeroed words, self re-arming
+                      float in_scale, unsigned* sync, hipStream_t s, bool do_pack = true);
+// SGD over the flat parameter range that also writes the updated ConvNet weights into their packed bf16
+// fragments (cn_pack_weights layout); offsets[4]: first flat element of conv1 / conv2 / conv3 / fc1 weight
+void cn_sgd_flat_pack(float* p, const float* g, float* m, int64_t n, const SgdArgs& a, const int64_t* offsets,
+                      void* packed, hipStream_t s);  // sync: 2 zeroed words, self re-arming
 
 // Workspace sizes (floats) of the backward weight-gradient slabs.
 int64_t cn_fc_slab_floats(int B, bool dgrad);

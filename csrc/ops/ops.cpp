@@ -169,7 +169,8 @@ void cast_copy(at::Tensor dst, const at::Tensor& src) {
 // ------------------------------------------------------------------ SGD
 void sgd_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& buf_opt, const SgdHyper& h,
               bool first_step, const c10::optional<at::Tensor>& lr_t,
-              const c10::optional<at::Tensor>& scale_t) {
+              const c10::optional<at::Tensor>& scale_t, const c10::optional<at::Tensor>& packed,
+              const std::vector<int64_t>& pack_offsets) {
   check_cuda(param, "sgd param");
   check_cuda(grad, "sgd grad");
   check_dtype(param, at::kFloat, "sgd param");
@@ -184,6 +185,21 @@ void sgd_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::
   }
   RINGDP_CHECK(aligned16(param) && aligned16(grad) && (!m || aligned16(buf)),
                "sgd_flat: buffers must be 16-byte aligned");
+  if (packed.has_value() && packed->defined()) {
+    // the ConvNet's packed bf16 fragments, written as the weights are updated
+    check_cuda(*packed, "packed convnet weights");
+    check_dtype(*packed, at::kBFloat16, "packed convnet weights");
+    RINGDP_CHECK(packed->numel() == kern::cn_packed_elems(), "packed convnet weights: wrong size");
+    RINGDP_CHECK(pack_offsets.size() == 4, "sgd_flat: pack_offsets needs the 4 ConvNet weight offsets");
+    const int64_t lens[4] = {32 * 25, 64 * 32 * 9, 128 * 64 * 9, 10 * 2048};
+    for (int i = 0; i < 4; ++i)
+      RINGDP_CHECK(pack_offsets[i] >= 0 && pack_offsets[i] + lens[i] <= param.numel(),
+                   "sgd_flat: pack offset ", i, " outside the flat parameter range");
+    kern::cn_sgd_flat_pack(param.data_ptr<float>(), grad.data_ptr<float>(), m, param.numel(),
+                           make_args(h, first_step, lr_t, scale_t), pack_offsets.data(), packed->data_ptr(),
+                           cur_stream(param));
+    return;
+  }
   kern::sgd_flat(param.data_ptr<float>(), grad.data_ptr<float>(), m, param.numel(),
                  make_args(h, first_step, lr_t, scale_t), cur_stream(param));
 }
@@ -390,7 +406,8 @@ std::vector<at::Tensor> cn_forward_buffers(const at::Tensor& x) {
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_forward_fused(
     const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
     const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& wfc, const at::Tensor& bfc, double mean, double std,
-    double in_scale, at::Tensor a1, at::Tensor idx1, at::Tensor a2, at::Tensor idx2, at::Tensor packed) {
+    double in_scale, at::Tensor a1, at::Tensor idx1, at::Tensor a2, at::Tensor idx2, at::Tensor packed,
+    bool do_pack) {
   int64_t B;
   bool u8;
   check_input(x, B, u8);
@@ -422,7 +439,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_forward_fused(
                          a2.data_ptr(), idx2.data_ptr<uint8_t>(), a3.data_ptr(), idx3.data_ptr<uint8_t>(),
                          logits.data_ptr<float>(), static_cast<int>(B), static_cast<float>(mean),
                          static_cast<float>(1.0 / std), static_cast<float>(in_scale), next_counter(x),
-                         cur_stream(x));
+                         cur_stream(x), do_pack);
   return {logits, a3, idx3};
 }
 

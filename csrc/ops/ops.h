@@ -28,7 +28,8 @@ struct SgdHyper {
 // One fused SGD step over flat fp32 buffers (momentum_buf may be undefined when momentum == 0).
 void sgd_flat(at::Tensor param, const at::Tensor& grad, const c10::optional<at::Tensor>& momentum_buf,
               const SgdHyper& h, bool first_step, const c10::optional<at::Tensor>& lr_tensor,
-              const c10::optional<at::Tensor>& grad_scale);
+              const c10::optional<at::Tensor>& grad_scale,
+              const c10::optional<at::Tensor>& packed, const std::vector<int64_t>& pack_offsets);
 // Multi-tensor SGD: one launch for lists of (possibly non-adjacent) fp32 tensors.
 void sgd_multi(std::vector<at::Tensor> params, std::vector<at::Tensor> grads,
                std::vector<at::Tensor> bufs, const SgdHyper& h, bool first_step,
@@ -70,7 +71,8 @@ std::vector<at::Tensor> cn_forward_buffers(const at::Tensor& x);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_forward_fused(
     const at::Tensor& x, const at::Tensor& w1, const at::Tensor& b1, const at::Tensor& w2, const at::Tensor& b2,
     const at::Tensor& w3, const at::Tensor& b3, const at::Tensor& wfc, const at::Tensor& bfc, double mean, double std,
-    double in_scale, at::Tensor a1, at::Tensor idx1, at::Tensor a2, at::Tensor idx2, at::Tensor packed);
+    double in_scale, at::Tensor a1, at::Tensor idx1, at::Tensor a2, at::Tensor idx2, at::Tensor packed,
+    bool do_pack);
 std::tuple<at::Tensor, at::Tensor, at::Tensor> cn_conv1_fwd_pack(const at::Tensor& x, const at::Tensor& w1,
                                                                  const at::Tensor& w2, const at::Tensor& w3,
                                                                  const at::Tensor& wfc, const at::Tensor& b1,

@@ -13,9 +13,9 @@ conv2's pre-activation z2 is never materialised.  ``_Conv2`` returns a zero-stri
 for it (autograd's handle on "the gradient of conv2's output") next to the real activations;
 ``_Conv3FC``'s backward scatters d(a2) through the pool2 codes straight into dz2, so conv2's
 backward is a plain linear-layer backward and pool2/ReLU backward costs no extra pass over
-memory.  Weights are packed
-once per forward into bf16 MFMA fragments (``C.cn_pack_weights``); the fp32 masters stay the
-parameters (packed inside conv1's launch on the default path).  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
+memory.  Weights live as bf16 MFMA fragments (``C.cn_pack_weights`` layout) next to the fp32 master
+parameters; on the default path ringdp.optim.SGD writes the fragments as it updates the masters
+(``PackState``), so the forward packs only after an outside change of the weights.  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
 ``_Conv3FC.backward`` - so ringdp's reducer starts the first bucket all-reduce while conv2/conv1
 backward kernels still run.
 """
@@ -160,10 +160,10 @@ class _Conv12(torch.autograd.Function):
 class _Conv3FC(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z2, a2, idx2, w3, b3, wfc, bfc, packed, fused=None):
-        if fused is not None:  # (x, w1, b1, w2, b2, mean, std, in_scale, a1, idx1): the whole forward here
-            x, w1, b1, w2, b2, mean, std, in_scale, a1, idx1 = fused
+        if fused is not None:  # (x, w1, b1, w2, b2, mean, std, in_scale, a1, idx1, do_pack): the whole forward
+            x, w1, b1, w2, b2, mean, std, in_scale, a1, idx1, do_pack = fused
             logits, a3, idx3 = C.cn_forward_fused(x, w1, b1, w2, b2, w3, b3, wfc, bfc, mean, std, in_scale,
-                                                  a1, idx1, a2, idx2, packed)
+                                                  a1, idx1, a2, idx2, packed, do_pack)
         else:
             logits, a3, idx3 = C.cn_conv3_fc_fwd(a2, packed, b3, bfc)
         ctx.mark_non_differentiable(a3, idx3)
@@ -241,6 +241,39 @@ def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index:
                          (a2, idx2, a3, idx3, packed), ignore_index, eps, reduction)
 
 
+class PackState:
+    """The ConvNet's packed bf16 MFMA weight fragments, kept across steps.
+
+    The forward packs only when the weights changed under the fragments: ``key`` holds the weights'
+    (version, address) at the last pack, so a version bump (load_state_dict, an in-place edit, any
+    torch optimizer) repacks.  ringdp.optim.SGD's flat step writes the fragments of every weight it
+    updates (``C.sgd_flat(..., packed=buf)``) and then refreshes ``key``; a ringdp step that updates
+    the weights without writing them clears ``key`` (its kernels do not bump versions)."""
+
+    __slots__ = ("buf", "key")
+
+    def __init__(self):
+        self.buf = None
+        self.key = None
+
+    @staticmethod
+    def key_of(ws):
+        return tuple((w._version, w.data_ptr()) for w in ws)
+
+
+def _pack_state(conv1, conv2, conv3, fc1):
+    st = conv1.__dict__.get("_ringdp_pack_state")
+    if st is None:
+        st = PackState()
+        conv1.__dict__["_ringdp_pack_state"] = st
+    ws = (conv1.weight, conv2.weight, conv3.weight, fc1.weight)
+    for slot, w in enumerate(ws):  # the optimizer finds the fragments through the parameters
+        t = getattr(w, "_ringdp_pack", None)
+        if t is None or t[0] is not st or t[1] != slot:
+            w._ringdp_pack = (st, slot)
+    return st, ws
+
+
 def pack_weights(conv1, conv2, conv3, fc1) -> torch.Tensor:
     with torch.no_grad():
         return C.cn_pack_weights(conv1.weight, conv2.weight, conv3.weight, fc1.weight)
@@ -259,11 +292,18 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
     x = x.contiguous()
     fused = None
     if _FUSE12 and _FUSED_FWD:
+        st, ws = _pack_state(conv1, conv2, conv3, fc1)
         bufs = C.cn_forward_buffers(x)
+        if st.buf is None or st.buf.device != x.device:
+            st.buf, st.key = bufs[4], None
+        bufs = (bufs[0], bufs[1], bufs[2], bufs[3], st.buf)
+        key = PackState.key_of(ws)
+        do_pack = st.key != key  # else the optimizer already wrote these weights' fragments
+        st.key = key
         z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
                                              conv3.weight.detach(), fc1.weight.detach(), mean, std, scale, bufs)
         fused = (x, conv1.weight.detach(), conv1.bias.detach(), conv2.weight.detach(), conv2.bias.detach(),
-                 mean, std, scale, bufs[0], bufs[1])
+                 mean, std, scale, bufs[0], bufs[1], do_pack)
     elif _FUSE12:
         z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
                                              conv3.weight.detach(), fc1.weight.detach(), mean, std, scale)

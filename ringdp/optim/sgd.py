@@ -6,7 +6,8 @@ lr 0.02, momentum 0.9, wd 1e-4, nesterov).
 
 GPU paths (one launch per step, no per-tensor foreach chains):
 * flat  - when the parameters were flattened by ringdp's DDP into one buffer whose layout matches
-          the gradient bucket buffer, a single float4 kernel updates the entire range;
+          the gradient bucket buffer, a single float4 kernel updates the entire range (for the
+          ConvNet it also writes next step's bf16 MFMA weight fragments: no pack launch per forward);
 * multi - otherwise one multi-tensor kernel over a pointer table.
 CPU: the same math with ATen foreach ops.
 
@@ -15,6 +16,7 @@ captured hipGraph step picks up learning-rate schedule changes without re-captur
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -22,6 +24,38 @@ from torch.optim.optimizer import Optimizer
 
 from .._native import C
 from ..utils import tracing as _tracing
+
+
+# RINGDP_CN_PACK_IN_SGD=0: the ConvNet forward packs its weights itself every step (A/B measurements)
+_PACK_IN_SGD = os.environ.get("RINGDP_CN_PACK_IN_SGD", "1") != "0"
+
+
+def _pack_target(params):
+    """(state, flat offsets, weights) when the flat step can keep one model's packed weight fragments current
+    (ringdp.ops.convnet.PackState: all 4 ConvNet weights in this group, their fragments built once)."""
+    if not _PACK_IN_SGD:
+        return None
+    st, offs, ws = None, {}, {}
+    for p in params:
+        t = getattr(p, "_ringdp_pack", None)
+        if t is None:
+            continue
+        if st is not None and t[0] is not st:
+            return None
+        st = t[0]
+        offs[t[1]] = p._ringdp_flat[2]
+        ws[t[1]] = p
+    if st is None or st.buf is None or sorted(offs) != [0, 1, 2, 3]:
+        return None
+    return st, [offs[i] for i in range(4)], tuple(ws[i] for i in range(4))
+
+
+def _invalidate_packs(params):
+    """The step's kernels changed weights without bumping their versions: their fragments are stale."""
+    for p in params:
+        t = getattr(p, "_ringdp_pack", None)
+        if t is not None:
+            t[0].key = None
 
 
 class SGD(Optimizer):
@@ -127,8 +161,16 @@ class SGD(Optimizer):
         flat = self._flat_layout(group, params)
         if flat is not None:
             fp, fg, mom, first = flat
+            tgt = _pack_target(params)
+            if tgt is not None:  # also write the ConvNet's bf16 fragments of the updated weights
+                st, offs, ws = tgt
+                C.sgd_flat(fp, fg, mom if mom_on else None, h, first, lr_t, None, st.buf, offs)
+                st.key = type(st).key_of(ws)
+                return
             C.sgd_flat(fp, fg, mom if mom_on else None, h, first, lr_t, None)
+            _invalidate_packs(params)
             return
+        _invalidate_packs(params)
         bufs = []
         if mom_on:
             for p in params:

@@ -163,7 +163,8 @@ def ddp_train_worker(rank, world, port, result_dir, mode, name, graph, perturb):
     """DDP training over `world` ranks; rank 0 then replays the same global batches in a single
     process (per-rank chunks accumulated at 1/world, which is DDP's averaging also for BN models)
     and stores both parameter vectors.  `perturb`: rank-dependent delays inside backward (bucket
-    launch order must not depend on readiness).  `graph`: steps 3.. are hipGraph replays."""
+    launch order must not depend on readiness).  `graph`: steps 3.. are hipGraph replays ("split": of the
+    segmented capture whose bucket collectives run between linear graph segments)."""
     dist, dev = _init(rank, world, port, mode)
     if mode != "cpu" and world == 1:
         os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
@@ -203,7 +204,11 @@ def ddp_train_worker(rank, world, port, result_dir, mode, name, graph, perturb):
             sx.copy_(x)
             sy.copy_(y)
             if g is None:  # capture records the step without running it
-                g = StepGraph(lambda: step(sx, sy), warmup=0).capture()
+                # graph == "split": linear segments with the bucket collectives between them (every
+                # bucket split off: RINGDP_SPLIT_MIN_US=0)
+                if graph == "split":
+                    os.environ["RINGDP_SPLIT_MIN_US"] = "0"
+                g = StepGraph(lambda: step(sx, sy), warmup=0, split_ddp=ddp if graph == "split" else None).capture()
             g.replay()
         else:
             step(x, y)

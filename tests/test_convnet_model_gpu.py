@@ -465,3 +465,43 @@ def test_weight_penalty_under_ddp_matches_separate_path(world1):
         cn._HEAD_CE, cn._DEFER = saved
     for a, b in zip(g0, g1):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_optimizer_writes_packed_weights(world1):
+    """ringdp.optim.SGD's flat step writes the ConvNet's bf16 MFMA fragments of the weights it updates
+    (no pack launch in the next forward): after every step they equal a fresh pack bit for bit, the
+    forward then skips the pack, and an outside weight change (version bump) makes it pack again."""
+    from ringdp._native import C
+    from ringdp.models import ConvNet
+    from ringdp.nn import CrossEntropyLoss
+    from ringdp.optim import SGD
+    from ringdp.ops.convnet import PackState
+    from ringdp.parallel import DistributedDataParallel as DDP
+
+    torch.manual_seed(5)
+    m = ConvNet().cuda()
+    d = DDP(m, device_ids=[0])
+    opt = SGD(d.parameters(), lr=0.05, momentum=0.9, nesterov=True, weight_decay=1e-4)
+    crit = CrossEntropyLoss()
+    x = torch.randint(0, 256, (96, 1, 28, 28), dtype=torch.uint8, device="cuda")
+    y = torch.randint(0, 10, (96,), device="cuda")
+    ws = (m.conv1.weight, m.conv2.weight, m.conv3.weight, m.fc1.weight)
+    for i in range(4):
+        loss = crit(d(x), y)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        st = m.conv1._ringdp_pack_state
+        assert st.key == PackState.key_of(ws), i  # kept current by the optimizer
+        ref = C.cn_pack_weights(*ws)
+        torch.cuda.synchronize()
+        assert torch.equal(st.buf, ref), (i, (st.buf.float() - ref.float()).abs().max())
+    with torch.no_grad():
+        m.conv3.weight.mul_(0.5)  # version bump: the next forward packs again
+    assert st.key != PackState.key_of(ws)
+    out = d(x)
+    assert st.key == PackState.key_of(ws)
+    torch.cuda.synchronize()
+    assert torch.equal(st.buf, C.cn_pack_weights(*ws))
+    with torch.no_grad():
+        torch.testing.assert_close(out, m.reference_forward(x), rtol=5e-2, atol=5e-2)

@@ -67,7 +67,8 @@ def _check_train(tmp_path, world, rel):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("name,graph", [("convnet", False), ("convnet", True), ("resnet18", False), ("resnet18", True)])
+@pytest.mark.parametrize("name,graph", [("convnet", False), ("convnet", True), ("resnet18", False), ("resnet18", True),
+                                        ("resnet18", "split")])
 def test_xgmi_ddp_equivalence(tmp_path, world, name, graph):
     spawn(MW.ddp_train_worker, args=(world, free_port(), str(tmp_path), "xgmi", name, graph, False), nprocs=world)
     # the same bf16 kernels on the same per-rank chunks; only the fp32 averaging order differs
