@@ -94,6 +94,10 @@ def parse(argv=None):
                          "bucket's collective runs between them on the comm stream, overlapping the rest of "
                          "backward), side (inside one graph on a side stream: a forked graph loses HIP's batched "
                          "launch, +1.2-2 us per kernel) or same (inside one graph on the compute stream: no overlap)")
+    ap.add_argument("--comm-tuning", type=str, default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                     "comm_tuning.json"),
+                    help="settings from tools/comm_bench.py --recommend, adopted when measured at this world size "
+                         "(environment variables already set win)")
     ap.add_argument("--comm-stats-steps", type=int, default=20,
                     help="after the timed region: eager steps with device-timed bucket collectives and "
                          "comm-free graph replays for the exposed-comm estimate (0 = skip)")
@@ -168,6 +172,14 @@ def worker(args):
         dev = torch.device("cpu")
         backend = "gloo"
         torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(world_env, 1)))
+    comm_tuning = None
+    if on_gpu and args.comm_tuning and os.path.exists(args.comm_tuning):
+        # RCCL / small-message settings measured by tools/comm_bench.py --recommend at this world size;
+        # they must be in the environment before the communicator exists
+        with open(args.comm_tuning) as f:
+            tun = json.load(f)
+        if int(tun.get("world", -1)) == world_env:
+            comm_tuning = {k: os.environ.setdefault(k, str(v)) for k, v in tun.get("env", {}).items()}
     if launched:
         dist.init_process_group(backend=backend)
     else:
@@ -421,6 +433,7 @@ def worker(args):
                     "comm_world_size": int(nat.size()),
                     "comm_backend": nat.backend_name(),
                     "hipgraph": use_graph,
+                    "comm_tuning": comm_tuning,
                     "master_weights": "fp32",
                     "device": "cpu" if not on_gpu else torch.cuda.get_device_properties(dev).gcnArchName,
                 },

@@ -11,10 +11,13 @@ what a captured training step sees) and reports the max over ranks as us/op plus
   python tools/comm_bench.py --gpus 8                        # launches 8 ranks itself (ringdp.run)
   python tools/comm_bench.py --gpus 8 --sweep                # + NCCL_ALGO / channel variants
   python -m ringdp.run --nproc-per-node 8 tools/comm_bench.py
+  python tools/comm_bench.py --gpus 8 --sweep --recommend comm_tuning.json   # + the settings bench.py adopts
 
 The "rccl+xgmi_small" rows exist when RINGDP_P2P_ALLREDUCE_MAX_BYTES is set (this tool sets 4 MiB
 unless told otherwise); the crossover between them and the "rccl" rows is the threshold to use for
-RINGDP_P2P_ALLREDUCE_MAX_BYTES in training.  ``--backend xgmi``: every all-reduce on the xgmi backend
+RINGDP_P2P_ALLREDUCE_MAX_BYTES in training; ``--recommend PATH`` writes that threshold and the fastest RCCL
+variant of the sweep as environment settings, which ``bench.py`` adopts at the same world size (its
+``--comm-tuning``, default ``comm_tuning.json``).  ``--backend xgmi``: every all-reduce on the xgmi backend
 (ranks may share a GPU: rank r uses GPU r % device_count, so a one-GPU box runs --gpus 2/4, which RCCL
 refuses).  Rank 0 prints one JSON line per measurement.
 """
@@ -50,6 +53,8 @@ def parse():
     ap.add_argument("--reps", type=int, default=20, help="all-reduces per graph")
     ap.add_argument("--iters", type=int, default=20, help="timed graph replays")
     ap.add_argument("--sweep", action="store_true", help="repeat under each RCCL env variant (parent mode)")
+    ap.add_argument("--recommend", type=str, default=None,
+                    help="write the recommended RINGDP_P2P_ALLREDUCE_MAX_BYTES / RCCL settings (JSON) here")
     ap.add_argument("--backend", type=str, default=None, choices=["rccl", "xgmi"],
                     help="GPU backend (default: RINGDP_GPU_BACKEND, else rccl)")
     return ap.parse_args()
@@ -127,14 +132,46 @@ def worker(args):
                 ok = bool(torch.all(t == 1).item())  # average of ones stays one
                 if rank == 0:
                     algbw = nbytes / (us * 1e-6) / 1e9
-                    print(json.dumps({"impl": impl, "world": world, "dtype": dt_name, "bytes": nbytes,
-                                      "us_per_op": round(us, 2), "algbw_GBps": round(algbw, 2),
-                                      "busbw_GBps": round(algbw * 2 * (world - 1) / max(world, 1), 2),
-                                      "correct": ok, "rccl_env": variant}), flush=True)
+                    line = json.dumps({"impl": impl, "world": world, "dtype": dt_name, "bytes": nbytes,
+                                       "us_per_op": round(us, 2), "algbw_GBps": round(algbw, 2),
+                                       "busbw_GBps": round(algbw * 2 * (world - 1) / max(world, 1), 2),
+                                       "correct": ok, "rccl_env": variant})
+                    print(line, flush=True)
+                    if os.environ.get("RINGDP_COMM_BENCH_OUT"):  # the parent's --recommend collects these
+                        with open(os.environ["RINGDP_COMM_BENCH_OUT"], "a") as f:
+                            f.write(line + "\n")
                 del g
     if pg.backend_name() != "xgmi":
         pg.set_p2p_enabled(True)
     dist.destroy_process_group()
+
+
+def recommend(rows, world):
+    """Settings for training from the sweep's rows (fp32, correct results only): the RCCL variant with the
+    least total time over the measured sizes, and the largest size up to which the xGMI one-shot kernel
+    beats RCCL at every size (0: RCCL for every size)."""
+    rows = [r for r in rows if r["dtype"] == "fp32" and r["correct"] and r["world"] == world]
+    variants = {}
+    for r in rows:
+        if r["impl"] == "rccl":
+            key = json.dumps(r["rccl_env"], sort_keys=True)
+            variants.setdefault(key, {})[r["bytes"]] = r["us_per_op"]
+    sizes = sorted({b for v in variants.values() for b in v})
+    full = {k: v for k, v in variants.items() if sorted(v) == sizes}
+    best = min(full, key=lambda k: sum(full[k].values())) if full else "{}"
+    env = dict(json.loads(best))
+    small = {r["bytes"]: r["us_per_op"] for r in rows if r["impl"] == "rccl+xgmi_small"
+             and json.dumps(r["rccl_env"], sort_keys=True) == best}
+    thresh = 0
+    for b in sizes:
+        if b in small and b in full.get(best, {}) and small[b] < full[best][b]:
+            thresh = b
+        else:
+            break
+    env["RINGDP_P2P_ALLREDUCE_MAX_BYTES"] = str(thresh)
+    return {"world": world, "env": env,
+            "evidence": {"rccl_us_by_variant": {k: full[k] for k in full},
+                         "xgmi_small_us": small, "chosen_variant": best}}
 
 
 def main():
@@ -146,9 +183,21 @@ def main():
         from ringdp.run import launch_local
 
         argv = [a for a in sys.argv[1:] if a != "--sweep"]
+        out = None
+        if args.recommend:
+            out = os.path.abspath(args.recommend) + ".rows.jsonl"
+            if os.path.exists(out):
+                os.remove(out)
         rc = 0
         for env in (SWEEP if args.sweep else [{}]):
+            env = dict(env, RINGDP_COMM_BENCH_OUT=out) if out else env
             rc = launch_local(os.path.abspath(__file__), argv, args.gpus, env=env) or rc
+        if out and os.path.exists(out):
+            rows = [json.loads(ln) for ln in open(out) if ln.strip()]
+            rec = recommend(rows, args.gpus)
+            with open(args.recommend, "w") as f:
+                json.dump(rec, f, indent=1)
+            print(json.dumps({"recommendation": rec["env"], "path": args.recommend}), flush=True)
         sys.exit(rc)
     worker(args)
 
