@@ -92,6 +92,29 @@ __global__ __launch_bounds__(256) void cast_t_multi_kernel(CastTTable t) {
   const int r0 = (tb / tiles_c) * 64, c0 = (tb % tiles_c) * 64;
   bf16* w = static_cast<bf16*>(d.dst);
   bf16* wt = static_cast<bf16*>(d.dst_t);
+  if (r0 + 64 <= d.R && c0 + 64 <= d.C && (d.R & 3) == 0 && (d.C & 3) == 0) {
+    // whole tile: 16-B loads, 8-B stores on both sides (16 lanes = one 128-B row segment); the scalar form
+    // below moved ~2.7 TB/s
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = threadIdx.x + 256 * k, rr = idx >> 4, c4 = (idx & 15) * 4;
+      const int64_t o = (int64_t)(r0 + rr) * d.C + c0 + c4;
+      const float4 x = *reinterpret_cast<const float4*>(d.src + o);
+      *reinterpret_cast<bf16x4*>(w + o) = bf16x4{(bf16)x.x, (bf16)x.y, (bf16)x.z, (bf16)x.w};
+      tile[rr][c4] = x.x;
+      tile[rr][c4 + 1] = x.y;
+      tile[rr][c4 + 2] = x.z;
+      tile[rr][c4 + 3] = x.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = threadIdx.x + 256 * k, cc = idx >> 4, r4 = (idx & 15) * 4;
+      *reinterpret_cast<bf16x4*>(wt + (int64_t)(c0 + cc) * d.R + r0 + r4) =
+          bf16x4{(bf16)tile[r4][cc], (bf16)tile[r4 + 1][cc], (bf16)tile[r4 + 2][cc], (bf16)tile[r4 + 3][cc]};
+    }
+    return;
+  }
   for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
     const int rr = idx >> 6, cc = idx & 63;
     const int r = r0 + rr, c = c0 + cc;
