@@ -728,29 +728,35 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnIn q, AttnIn k, AttnI
       const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(Ks + att_ksw(kr, 32 + 8 * g));
       st[t] = mfma16x16x32(a1, qf1, mfma16x16x32(a0, qf0, zero_f32x4()));
     }
-    // softmax over keys for query qrow: lane holds keys 16t + 4g + i
-    float mx = -INFINITY;
+    // softmax over keys for query qrow: lane holds keys 16t + 4g + i.  Only tiles that reach past T are masked
+    // (a scalar test per tile; ViT-B/16: the last one): masking every score kept 52 lane masks live at once,
+    // which the compiler spilled through v_writelane / v_readlane (248 extra VALU per query tile).
+    // exp(s*scale - m) = exp2(s*c - m*c) with c = scale * log2(e): one fma + v_exp per score, and a masked
+    // -inf score gives exp2(-inf) = 0.
 #pragma unroll
     for (int t = 0; t < NT; ++t)
+      if (16 * t + 16 > T)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float x = 16 * t + 4 * g + i < T ? st[t][i] * scale : -INFINITY;
-        st[t][i] = x;
-        mx = fmaxf(mx, x);
-      }
+        for (int i = 0; i < 4; ++i)
+          if (!(16 * t + 4 * g + i < T)) st[t][i] = -INFINITY;
+    float mx = -INFINITY;  // of the raw scores (scale > 0)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) mx = fmaxf(mx, fmaxf(fmaxf(st[t][0], st[t][1]), fmaxf(st[t][2], st[t][3])));
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float c2 = scale * 1.4426950408889634f, mc = mx * c2;
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float e = 16 * t + 4 * g + i < T ? __expf(st[t][i] - mx) : 0.f;
+        const float e = __builtin_amdgcn_exp2f(fmaf(st[t][i], c2, -mc));
         st[t][i] = e;
         sum += e;
       }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
+    mx *= scale;  // the scaled maximum (the log-sum-exp below)
     const float inv = qrow < T ? 1.f / sum : 0.f;  // padded query rows: P = 0
     bf16x4 pb[NT];
 #pragma unroll
