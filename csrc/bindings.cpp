@@ -585,6 +585,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_fp8_splitk_f32", &ops::gemm_fp8_splitk_f32);
   m.def("set_bf16_tile_mode", &ops::set_bf16_tile_mode, "0 auto, 128 / 256: force the bf16 GEMM tile kernel");
   m.def("set_gemm256_phased", &kern::set_gemm256_phased, "K-contiguous 256x256 GEMM: 1 phased pipeline, 0 older kernel");
+  m.def("set_gemm_two_wg", &kern::set_gemm_two_wg, "bf16 K-contiguous GEMMs on the 2-workgroup 256x128 kernel: 0 never (default), 1 always, 2 N <= 1024; group_m > 0 sets its tile-order group",
+        py::arg("mode"), py::arg("group_m") = 0);
   m.def("set_gemm_store_cache", &kern::set_gemm_store_cache, "256x256 GEMM 16-B output stores: 0 plain, 1 nt, 2 sc1");
   m.def("set_gemm256_persist", &kern::set_gemm256_persist, "K-contiguous 256x256 GEMM: 1 persistent phased kernel, 0 one workgroup per tile");
   m.def("set_gemm_wide_store", &kern::set_gemm_wide_store, "256x256 GEMM epilogue: 1 16-B bf16 stores, 0 8-B stores");

@@ -569,6 +569,136 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_256q_kernel(const uint8_t* _
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Two workgroups per CU: 256x128 tiles, 4 waves (2 (M) x 2 (N), the same 128x64 wave tile and 32
+// accumulator tiles as above), 32-k stages of 24 KiB (A 256 x 64 B, B 128 x 64 B), three of them: 72 KiB
+// per workgroup, so two fit in the 160 KiB LDS and the CU holds the same 8 waves as the one-workgroup
+// kernels.  What the second workgroup buys: one tile's cold prologue (the first DMA round trip) and its
+// output drain (128 KiB of stores per 256x256 of output) run while the other workgroup's MFMAs issue - in
+// the one-workgroup kernels both are exposed on every tile (profiles/r03/gemm_epilogue.md).
+// Stage image: 64-B rows, physical 16-B chunk p of row r holds logical chunk p ^ f(r), f(r) = (r >> 2) & 2:
+// a ds_read_b128 lane group ({0-3,12-15,20-27}, ...) reads rows {j, 12+j, 4+j, 8+j} at two chunks, and
+// that f sends each group's 16 reads to 16 distinct 16-B bank slots (conflict-free).  One barrier per
+// stage; stage kt+2 is issued right after it (into the buffer stage kt-1 was read from).
+constexpr int N2_TN = 128, N2_TK = 64;  // N2_TK in bytes (32 bf16: one MFMA k-step)
+constexpr int N2_STAGE = (TM + N2_TN) * N2_TK;  // 24 KiB
+constexpr int N2_NBUF = 3;
+__device__ __forceinline__ int n2_swz(int r) { return (r >> 2) & 2; }
+
+template <bool CS>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_256n_kernel(const uint8_t* __restrict__ A, int64_t lda,
+                                                               int64_t a_bs, const uint8_t* __restrict__ B,
+                                                               int64_t ldb, int64_t b_bs, GemmEpilogue ep, int M,
+                                                               int N, int K, int tiles_m, int tiles_n, int splits,
+                                                               int k_per_split, int group_m) {
+  __shared__ __attribute__((aligned(16))) char smem[N2_NBUF * N2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int per_z = tiles_m * tiles_n;
+  const int zid = blockIdx.y;
+  const int t = xcd_remap(blockIdx.x, per_z);
+  int tm, tn;
+  grouped_tile(t, tiles_m, tiles_n, group_m, tm, tn);
+  const int b = zid / splits, split = zid - b * splits;
+  const int m0 = tm * TM, n0 = tn * N2_TN;
+  const int kbeg = split * k_per_split, kend = min(K, kbeg + k_per_split);
+  const int nkt = max(0, (kend - kbeg) / N2_TK);
+
+  // this lane's 6 DMA sources per stage: 4 of A (stage rows 64 wave + 16 j + lane / 4), 2 of B (stage rows
+  // 256 + 32 wave + 16 j + lane / 4); lane -> physical chunk lane & 3, logical chunk (lane & 3) ^ f(row)
+  const uint8_t* src[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const bool a_part = j < 4;
+    const int r = a_part ? 64 * wave + 16 * j + (lane >> 2) : 32 * wave + 16 * (j - 4) + (lane >> 2);
+    const int lc = (lane & 3) ^ n2_swz(r);
+    const uint8_t* base = a_part ? A + (int64_t)b * a_bs : B + (int64_t)b * b_bs;
+    const int64_t ld = a_part ? lda : ldb;
+    const int rr = min((a_part ? m0 : n0) + r, (a_part ? M : N) - 1);  // past the edge: re-read, dropped on store
+    src[j] = base + (int64_t)rr * ld + kbeg + lc * 16;
+  }
+  auto issue = [&](int kt) {
+    char* st = smem + (kt % N2_NBUF) * N2_STAGE;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      char* dst = j < 4 ? st + (64 * wave + 16 * j) * N2_TK : st + TM * N2_TK + (32 * wave + 16 * (j - 4)) * N2_TK;
+      glds16(src[j] + (int64_t)kt * N2_TK, dst);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = zero_f32x4();
+
+  // fragment reads: row R = 16 tile + (lane & 15) (so f(R) = f(lane & 15)), logical chunk lane >> 4
+  const int fr = lane & 15;
+  const int frag = fr * N2_TK + (((lane >> 4) ^ n2_swz(fr)) << 4);
+  const int a_off = wm * 128 * N2_TK + frag;
+  const int b_off = TM * N2_TK + wn * 64 * N2_TK + frag;
+
+  // Fragments are register double-buffered: stage kt + 1 is read into the other set while stage kt's MFMAs
+  // issue, so a buffer is free as soon as every wave has READ it (the barrier of the next stage), and the
+  // DMA runs three stages ahead (stage kt + 3 goes into stage kt's buffer).
+  struct Frags {
+    bf16x8 a[8], b[4];
+  };
+  auto load = [&](Frags& f, int kt) {
+    const char* st = smem + (kt % N2_NBUF) * N2_STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f.b[j] = *reinterpret_cast<const bf16x8*>(st + b_off + j * 16 * N2_TK);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.a[i] = *reinterpret_cast<const bf16x8*>(st + a_off + i * 16 * N2_TK);
+  };
+  auto mfmas = [&](const Frags& f) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32(f.b[j], f.a[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // stage kt: publish stage kt + 1 (its copies landed: only kt + 2 may still be in flight), refill the buffer
+  // of stage kt (every wave's reads of it retired before the barrier), read kt + 1, multiply kt
+  auto step = [&](int kt, const Frags& cur, Frags& nxt) {
+    if (kt + 1 < nkt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (kt + 2 < nkt)
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      raw_barrier();
+      if (kt + 3 < nkt) issue(kt + 3);
+      load(nxt, kt + 1);
+    }
+    mfmas(cur);
+  };
+
+  if (nkt > 0) issue(0);
+  if (nkt > 1) issue(1);
+  if (nkt > 2) issue(2);
+  Frags f0, f1;
+  if (nkt > 0) {
+    if (nkt > 2)
+      asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (nkt > 1)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    load(f0, 0);
+  }
+  for (int kt = 0; kt < nkt; kt += 2) {
+    step(kt, f0, f1);
+    if (kt + 1 < nkt) step(kt + 1, f1, f0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  raw_barrier();  // the epilogue reuses the stage buffers as per-wave scratch
+  gemm256_store<false, false, CS>(acc, ep, M, N, zid, b, m0 + wm * 128 + (lane & 15), n0 + wn * 64 + 4 * (lane >> 4),
+                                  1.f, smem + wave * 16384);
+}
+
 int g_phased = -1;
 int phased_mode() {
   if (g_phased < 0) {
@@ -638,6 +768,29 @@ int gemm_store_cache() {
   return g_store_cache;
 }
 void set_gemm_store_cache(int flavour) { g_store_cache = flavour; }
+// K-contiguous bf16 GEMMs on the two-workgroups-per-CU 256x128 kernel: 0 (default) never, 1 always, 2 when
+// N <= 1024; its tile-order group (tile rows per group, RINGDP_GEMM_2WG_GROUP, default 4).  Measured
+// (profiles/r05/two_wg/): 2-7 % faster than the 256x256 kernel on the N <= 1024 shapes back to back, 5-13 %
+// slower on N >= 2048 and at 8192^3, and neutral in the ViT-B/16 and ResNet-50 steps, so it stays opt-in.
+static int g_two_wg = -1, g_two_wg_group = -1;
+static int two_wg_mode() {
+  if (g_two_wg < 0) {
+    const char* v = getenv("RINGDP_GEMM_2WG");
+    g_two_wg = v && *v ? atoi(v) : 0;
+  }
+  return g_two_wg;
+}
+static int two_wg_group() {
+  if (g_two_wg_group < 0) {
+    const char* v = getenv("RINGDP_GEMM_2WG_GROUP");
+    g_two_wg_group = v && *v ? std::max(1, atoi(v)) : 4;
+  }
+  return g_two_wg_group;
+}
+void set_gemm_two_wg(int mode, int group_m) {
+  g_two_wg = mode;
+  if (group_m > 0) g_two_wg_group = group_m;
+}
 
 static int bf16_group_m() {  // tile rows per group of the tile order (1 = row-major, rounds 1-3)
   static const int g = [] {
@@ -664,6 +817,25 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& Bop, int batch, int 
   dim3 grid(tiles_m * tiles_n, batch * splits);
   const bool wide_bf16 = N % 8 == 0 && ep.ldc % 8 == 0 && (reinterpret_cast<uintptr_t>(ep.C) & 15) == 0 &&
                          ep.c_bstride % 8 == 0;
+  const int twm = two_wg_mode();
+  if (!A.row_contig && !Bop.row_contig && (twm == 1 || (twm == 2 && N <= 1024)) &&
+      (!ep.colsum_part || (batch == 1 && splits == 1 && ep.out_bf16 && wide_bf16 && ep.mode == GemmEpilogue::kStore))) {
+    const int tiles_n2 = (N + N2_TN - 1) / N2_TN;
+    GemmEpilogue e3 = ep;
+    e3.store_mode = ep.colsum_part ? 2 : gemm_wide_store_mode() % 10;
+    e3.store_rot = gemm_wide_store_mode() < 10;
+    e3.store_cache = gemm_store_cache();
+    e3.sink = store_sink();
+    dim3 grid2(tiles_m * tiles_n2, batch * splits);
+    auto go2 = [&](auto kern) {
+      kern<<<grid2, 256, 0, s>>>(static_cast<const uint8_t*>(A.p), A.ld * 2, A.bstride * 2,
+                                 static_cast<const uint8_t*>(Bop.p), Bop.ld * 2, Bop.bstride * 2, e3, M, N, K * 2,
+                                 tiles_m, tiles_n2, splits, kps * 2, two_wg_group());
+    };
+    if (ep.colsum_part) go2(gemm_bf16_256n_kernel<true>);
+    else go2(gemm_bf16_256n_kernel<false>);
+    return true;
+  }
   if (ep.colsum_part) {  // column sums ride in the phased kernel's LDS-row bf16 stores only
     if (A.row_contig || Bop.row_contig || !phased_mode() || batch != 1 || splits != 1 || !ep.out_bf16 || !wide_bf16 ||
         ep.mode != GemmEpilogue::kStore)

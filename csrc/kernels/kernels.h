@@ -307,6 +307,7 @@ bool gemm_bf16_256(const GemmOperand& A, const GemmOperand& B, int batch, int M,
 void set_gemm256_persist(int on);  // A/B: 1 persistent phased kernel (default), 0 one workgroup per tile
 void set_gemm256_phased(int on);  // A/B: 1 phased pipeline (default), 0 the single-stage-wait kernel
 void set_gemm_wide_store(int mode);
+void set_gemm_two_wg(int mode, int group_m);  // bf16 K-contiguous GEMMs on the 2-workgroup 256x128 kernel: 0 never (default), 1 always, 2 N <= 1024
 void set_gemm_store_cache(int flavour);  // A/B: GemmEpilogue::store_cache of the 256x256 kernels  // A/B: epilogue store mode of the 256x256 kernels (GemmEpilogue::store_mode)
 int gemm_wide_store_mode();         // RINGDP_GEMM_WIDE_STORE (default 2)
 int gemm_store_cache();             // RINGDP_GEMM_STORE_CACHE (default 0)

@@ -59,14 +59,21 @@ def _gelu_grad(x):
     return 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * 0.3989422804014327 * torch.exp(-0.5 * x * x)
 
 
-@pytest.mark.parametrize("persist", [1, 0])
+def _select(C, kern):
+    C.set_gemm256_persist(1 if kern == "persist" else 0)
+    C.set_gemm_two_wg(1 if kern == "2wg" else 0)
+
+
+@pytest.mark.parametrize("kern", ["persist", "1wg", "2wg"])
 @pytest.mark.parametrize("epi", ["bf16_bias", "gelu_preact", "residual", "gelu_bwd", "f32_plain"])
 @pytest.mark.parametrize("M,N,K,batch", [(4200, 4104, 128, 1), (1000, 776, 192, 3), (264, 256, 64, 1)])
-def test_gemm256_persistent_epilogues(C, persist, epi, M, N, K, batch):
+def test_gemm256_persistent_epilogues(C, kern, epi, M, N, K, batch):
     """The persistent phased kernel (several tiles per workgroup once tiles > CUs, next tile's first k-tile
     landing during the epilogue, exact-count edge stores into a sink) against fp32 references, for every
-    epilogue kind it serves; persist=0 is the one-workgroup-per-tile kernel on the same inputs."""
-    C.set_gemm256_persist(persist)
+    epilogue kind it serves; 1wg is the one-workgroup-per-tile kernel on the same inputs, 2wg the
+    two-workgroups-per-CU 256x128 kernel (gemm_bf16_256n: 3-stage DMA ring, register double-buffered
+    fragments; K = 64 and 192 give it 2 and 6 stages)."""
+    _select(C, kern)
     try:
         g = torch.Generator().manual_seed(M * 3 + N + K + batch)
         a, ad = _operand(M, K, False, batch, g)
@@ -97,13 +104,13 @@ def test_gemm256_persistent_epilogues(C, persist, epi, M, N, K, batch):
         err = (got - want).abs().max() / want.abs().max()
         assert err < (2e-3 if epi == "f32_plain" else 8e-3), float(err)
     finally:
-        C.set_gemm256_persist(0)
+        _select(C, "1wg")
 
 
-@pytest.mark.parametrize("persist", [1, 0])
-def test_gemm256_persistent_splitk(C, persist):
-    """K-contiguous split-K through the persistent kernel (work items = tiles x splits)."""
-    C.set_gemm256_persist(persist)
+@pytest.mark.parametrize("kern", ["persist", "1wg", "2wg"])
+def test_gemm256_persistent_splitk(C, kern):
+    """K-contiguous split-K through the persistent kernel (work items = tiles x splits) and the 2-WG kernel."""
+    _select(C, kern)
     try:
         M, N, K = 1032, 1288, 4096
         g = torch.Generator().manual_seed(11)
@@ -115,4 +122,20 @@ def test_gemm256_persistent_splitk(C, persist):
         err = (out.cpu() - ref).abs().max() / ref.abs().max()
         assert err < 1e-4, float(err)
     finally:
-        C.set_gemm256_persist(0)
+        _select(C, "1wg")
+
+
+@pytest.mark.parametrize("M,N,K", [(520, 264, 640), (304, 696, 64), (8, 8, 64), (256, 128, 96 * 2)])
+def test_gemm256_two_wg_shapes(C, M, N, K):
+    """2-WG kernel on ragged edges (M, N not multiples of 256 / 128) and stage counts 1, 2, 6, 10, 20."""
+    _select(C, "2wg")
+    try:
+        g = torch.Generator().manual_seed(M + 3 * N + K)
+        a, ad = _operand(M, K, False, 1, g)
+        b, bd = _operand(N, K, False, 1, g)
+        out = C.gemm(ad, bd, M, N, K, K, K, False, False, 1, M * K, N * K, False)
+        ref = a[0] @ b[0].t()
+        err = (out.cpu().view(M, N) - ref).abs().max() / ref.abs().max()
+        assert err < 2e-3, float(err)
+    finally:
+        _select(C, "1wg")
