@@ -3,6 +3,7 @@
 #include "xgmi_engine.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -51,8 +52,10 @@ int64_t round16(int64_t x) { return (x + 15) / 16 * 16; }
 
 XgmiConfig XgmiConfig::from_env() {
   XgmiConfig c;
+  c.blocks_set = getenv("RINGDP_XGMI_BLOCKS") && *getenv("RINGDP_XGMI_BLOCKS");
+  c.slot_set = getenv("RINGDP_XGMI_SLOT_MB") && *getenv("RINGDP_XGMI_SLOT_MB");
   c.nblocks = static_cast<int>(std::clamp<int64_t>(env_i64("RINGDP_XGMI_BLOCKS", c.nblocks), 1, 1024));
-  c.slot_bytes = round16(std::max<int64_t>(env_i64("RINGDP_XGMI_SLOT_MB", 4), 1) << 20);
+  c.slot_bytes = round16(std::max<int64_t>(env_i64("RINGDP_XGMI_SLOT_MB", c.slot_bytes >> 20), 1) << 20);
   c.p2p_slot_bytes = round16(std::max<int64_t>(env_i64("RINGDP_XGMI_P2P_SLOT_MB", 1), 1) << 20);
   c.oneshot_max = std::max<int64_t>(env_i64("RINGDP_XGMI_ONESHOT_KB", 512), 0) << 10;
   return c;
@@ -72,16 +75,28 @@ std::unique_ptr<XgmiEngine> XgmiEngine::create(const std::shared_ptr<Store>& sto
   for (int r = 0; r < world; ++r) same_host &= store->get("xgmi/host/" + std::to_string(r)) == me;
   if (!all_agree(store, "xgmi/samehost", rank, world, same_host)) return say("ranks are not on one host");
 
+  // ranks sharing a device (same PCI bus id): the shared-GPU defaults unless the environment says otherwise
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, device) != hipSuccess) std::snprintf(bus, sizeof(bus), "dev%d", device);
+  store->set("xgmi/bus/" + std::to_string(rank), bus);
+  bool shared = false;
+  for (int r = 0; r < world; ++r)
+    if (r != rank) shared |= store->get("xgmi/bus/" + std::to_string(r)) == std::string(bus);
+  shared = !all_agree(store, "xgmi/distinct", rank, world, !shared);
+  XgmiConfig c = cfg;
+  if (shared && !c.blocks_set) c.nblocks = 64;
+  if (shared && !c.slot_set) c.slot_bytes = 4 << 20;
+
   std::unique_ptr<XgmiEngine> p(new XgmiEngine());
   p->rank_ = rank;
   p->world_ = world;
   p->device_ = device;
-  p->cfg_ = cfg;
-  p->cfg_.oneshot_max = std::min(cfg.oneshot_max, cfg.slot_bytes);
-  const int G = cfg.nblocks;
-  const int64_t region = 2 * static_cast<int64_t>(world) * cfg.slot_bytes;
+  p->cfg_ = c;
+  p->cfg_.oneshot_max = std::min(c.oneshot_max, c.slot_bytes);
+  const int G = c.nblocks;
+  const int64_t region = 2 * static_cast<int64_t>(world) * c.slot_bytes;
   const int64_t off_a = 0, off_b = region, off_p2p = 2 * region;
-  const int64_t stage_bytes = off_p2p + static_cast<int64_t>(kern::kXgMaxRanks) * 2 * cfg.p2p_slot_bytes;
+  const int64_t stage_bytes = off_p2p + static_cast<int64_t>(kern::kXgMaxRanks) * 2 * c.p2p_slot_bytes;
   const size_t flag_bytes = static_cast<size_t>(4) * G * kern::kXgMaxRanks * sizeof(unsigned);
   const size_t epoch_bytes = static_cast<size_t>(1 + 2 * kern::kXgMaxRanks) * G * sizeof(unsigned);
 
@@ -164,8 +179,8 @@ std::unique_ptr<XgmiEngine> XgmiEngine::create(const std::shared_ptr<Store>& sto
   a.world = world;
   a.rank = rank;
   a.nblocks = G;
-  a.slot = cfg.slot_bytes;
-  a.p2p_slot = cfg.p2p_slot_bytes;
+  a.slot = c.slot_bytes;
+  a.p2p_slot = c.p2p_slot_bytes;
   a.off_a = off_a;
   a.off_b = off_b;
   a.off_p2p = off_p2p;
