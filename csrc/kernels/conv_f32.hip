@@ -269,6 +269,19 @@ struct NCHWOut {  // C[m = (b, p)][n] (+ bias[n]) -> out[b, n, p]
   }
 };
 
+// split-K data gradient (small batches): slice z stores its partial dx, NCHW, into slab plane z
+struct NCHWSlabOut {
+  static constexpr bool kPool = false, kPoolS1 = false;
+  float* out;
+  int N, M, plane;  // plane = M * N elements
+  FastDiv hw;
+  __device__ int row(int m) const {
+    const int b = fdiv(m, hw);
+    return static_cast<int>(blockIdx.z) * plane + b * N * static_cast<int>(hw.d) + (m - b * static_cast<int>(hw.d));
+  }
+  __device__ void store(int rowoff, int n, float v) const { out[rowoff + n * static_cast<int>(hw.d)] = v; }
+};
+
 struct SlabOut {  // split-K slice z: slab[z][m][n]
   static constexpr bool kPool = false, kPoolS1 = false;
   float* slab;
@@ -801,6 +814,23 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// dx = sum over the split-K planes of NCHWSlabOut, in plane order (deterministic); n4 = plane / 4
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float4* __restrict__ slab, int slices, int n4,
+                                                       float4* __restrict__ out) {
+  for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < n4;
+       i += static_cast<int>(gridDim.x * blockDim.x)) {
+    float4 acc = slab[i];
+    for (int z = 1; z < slices; ++z) {
+      const float4 v = slab[static_cast<int64_t>(z) * n4 + i];
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    out[i] = acc;
+  }
+}
+
 int grid_1d(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -822,13 +852,23 @@ int64_t batch_chunk(int64_t B, std::initializer_list<int64_t> per_image) {
   return std::max<int64_t>(1, std::min(B, cap));
 }
 
+// RINGDP_F32_WGRAD_MIN_K: shallowest k slice of a weight gradient.  512 (was 1024): B=100 step 318 -> 296 us
+// (256: 297, 128: 306); B=65536 unchanged (profiles/r05/fp32/).
+int wgrad_min_depth() {
+  static const int d = [] {
+    const char* e = std::getenv("RINGDP_F32_WGRAD_MIN_K");
+    return e && *e ? std::max(BK, std::atoi(e)) : 512;
+  }();
+  return d;
+}
+
 int wgrad_slices(int M, int N, int64_t K) {
-  // enough slices to put >= ~2048 workgroups on the 256 CUs, each slice >= 1024 deep
+  // enough slices to put >= ~2048 workgroups on the 256 CUs, each slice >= wgrad_min_depth() deep
   const Layout l = pick_layout(M, N, 1 << 20);  // the big-tile layout (the launch may still pick 32x32)
   const int bm = layout_bm(l), bn = layout_bn(l);
   const int64_t tiles = static_cast<int64_t>((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   int64_t s = (2048 + tiles - 1) / tiles;
-  const int64_t cap = (K + 1023) / 1024;
+  const int64_t cap = (K + wgrad_min_depth() - 1) / wgrad_min_depth();
   if (s > cap) s = cap;
   return static_cast<int>(s < 1 ? 1 : (s > 1024 ? 1024 : s));
 }
@@ -965,9 +1005,48 @@ void conv_f32_fwd_pool_s1(const ConvF32Geom& g, const float* x, const float* w, 
   }
 }
 
-void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, hipStream_t s) {
+// Small batches (the reference's 100 images): the data-gradient GEMM has few workgroups, each with one long k
+// loop that is latency-bound (B=100 conv3: 626 workgroups of 32x32 x 72 k-tiles, 63 us).  Split K into slices
+// of ~8 k-tiles (at most 8 slices): the grid then takes the big-tile layouts again (fewer gathers per MFMA)
+// and the slices' partial dx planes are summed in order by slab_sum_kernel.  B=100 step, forced counts
+// (profiles/r05/fp32/): 1 slice 353 us, 2: 353, 3: 342, 4: 329, 6: 313, 8: 312, 12: 317.  Big batches (>= 8
+// 32x32 tiles per CU) and chunked batches keep one slice.  RINGDP_F32_DGRAD_SLICES=n forces n (1: off).
+int conv_f32_dgrad_slices(const ConvF32Geom& g) {
   const int K = g.Kout * g.R * g.R;
   const int64_t zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW, xout = static_cast<int64_t>(g.C) * g.H * g.W;
+  if (batch_chunk(g.B, {zin, xout}) < g.B) return 1;
+  const int64_t M = g.B * g.H * g.W, plane = M * g.C;
+  if (plane % 4 != 0) return 1;
+  const int64_t tiles32 = ((M + 31) / 32) * ((g.C + 31) / 32);
+  int s = tiles32 >= 8 * f32_num_cus() ? 1 : std::min(8, (K + 8 * BK - 1) / (8 * BK));
+  if (const char* e = std::getenv("RINGDP_F32_DGRAD_SLICES")) {
+    const int v = std::atoi(e);
+    if (v > 0) s = v;
+  }
+  s = std::max(1, std::min(s, std::min(16, (K + BK - 1) / BK)));
+  if (static_cast<int64_t>(s) * plane >= (int64_t{1} << 29)) return 1;
+  return s;
+}
+
+void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* slab, int slices,
+                    hipStream_t s) {
+  const int K = g.Kout * g.R * g.R;
+  const int64_t zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW, xout = static_cast<int64_t>(g.C) * g.H * g.W;
+  if (slab && slices > 1) {  // conv_f32_dgrad_slices(g) > 1: one chunk, plane % 4 == 0
+    const int M = static_cast<int>(g.B * g.H * g.W);
+    const int plane = M * g.C;
+    int per = (K + slices - 1) / slices;
+    per = (per + BK - 1) / BK * BK;
+    const int used = (K + per - 1) / per;
+    DgradA la{{dz, static_cast<int>(g.B * zin * 4), 0.f, 1.f}, g.Kout, g.W, g.R, g.OH, g.OW, g.pad, K, M,
+              make_fdiv(g.H * g.W), make_fdiv(g.W)};
+    DgradB lb{{w, K * g.C * 4, 0.f, 1.f}, g.C, g.R * g.R, K, make_fdiv(g.R * g.R)};
+    NCHWSlabOut epi{slab, g.C, M, plane, make_fdiv(g.H * g.W)};
+    launch_gemm(M, g.C, K, per, used, -1, la, lb, epi, s);
+    hipLaunchKernelGGL(slab_sum_kernel, dim3(grid_1d(plane / 4)), dim3(256), 0, s, reinterpret_cast<const float4*>(slab),
+                       used, plane / 4, reinterpret_cast<float4*>(dx));
+    return;
+  }
   const int64_t chunk = batch_chunk(g.B, {zin, xout});
   for (int64_t b0 = 0; b0 < g.B; b0 += chunk) {
     const int nb = static_cast<int>(std::min(chunk, g.B - b0));

@@ -72,6 +72,26 @@ def test_conv_f32_many_tiles_and_slices(B, Cin, H, K, R, pad):
         _close(a, r, rtol=tol)
 
 
+@pytest.mark.parametrize("slices", ["1", "3", "8", ""])
+@pytest.mark.parametrize("B,Cin,H,K,R,pad", [(100, 64, 10, 128, 3, 0), (100, 32, 13, 64, 3, 0), (6, 3, 9, 5, 3, 1),
+                                             (700, 64, 10, 128, 3, 0)])
+def test_conv_f32_dgrad_split_k(monkeypatch, slices, B, Cin, H, K, R, pad):
+    """Small-batch data gradients split K into slices whose partial dx planes are summed in order
+    (conv_f32_dgrad_slices: the reference's B=100 conv3 / conv2 shapes take 8 / 5); forced counts, the
+    unsplit path (1) and the automatic choice ("": B=700 conv3 has enough tiles to stay unsplit)."""
+    if slices:
+        monkeypatch.setenv("RINGDP_F32_DGRAD_SLICES", slices)
+    else:
+        monkeypatch.delenv("RINGDP_F32_DGRAD_SLICES", raising=False)
+    g = torch.Generator(device=DEV).manual_seed(B + Cin)
+    w = torch.randn(K, Cin, R, R, device=DEV, generator=g) * 0.1
+    OH = H + 2 * pad - R + 1
+    dz = torch.randn(B, K, OH, OH, device=DEV, generator=g)
+    dx = C.f32_conv_dgrad(dz, w, H, H, pad)
+    ref = torch.nn.grad.conv2d_input((B, Cin, H, H), w.double(), dz.double(), padding=pad).float()
+    _close(dx, ref)
+
+
 def test_conv_f32_batch_chunks(monkeypatch):
     """The host launchers split the batch so every index stays 32-bit; a lowered limit runs that path
     (conv2 shape: 7744 output elements per image, limit 3 images -> chunks of 3, 3, 2)."""
