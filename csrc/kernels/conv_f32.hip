@@ -831,6 +831,40 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float4* __restrict_
   }
 }
 
+// ReLU + 2x2 max-pool (stride st) over the split-K planes of a plain NCHW conv output: each window value is
+// the in-order sum of its slices plus the bias (bias before the max, as PoolOut / PoolS1Out), the first maximum
+// in window order wins, code 255 where the result is 0.  One thread per pooled output.
+__global__ __launch_bounds__(256) void pool_slab_fwd_kernel(const float* __restrict__ slab, int slices, int plane,
+                                                            const float* __restrict__ bias, int C, int OH, int OW,
+                                                            int st, int PH, int PW, int total, float* __restrict__ a,
+                                                            unsigned char* __restrict__ code) {
+  const int o = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x);
+  if (o >= total) return;
+  const int px = o % PW;
+  int t = o / PW;
+  const int py = t % PH;
+  t /= PH;
+  const int n = t % C;
+  const int base = t * OH * OW + py * st * OW + px * st;  // t = b * C + n
+  const float bn = bias ? bias[n] : 0.f;
+  float best = 0.f;
+  int bt = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = base + (u >> 1) * OW + (u & 1);
+    float v = slab[i];
+    for (int z = 1; z < slices; ++z) v += slab[static_cast<int64_t>(z) * plane + i];
+    v += bn;
+    if (u == 0 || v > best) {
+      best = v;
+      bt = u;
+    }
+  }
+  const bool live = best > 0.f;
+  a[o] = live ? best : 0.f;
+  code[o] = live ? static_cast<unsigned char>(bt) : 255;
+}
+
 int grid_1d(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return static_cast<int>(g < 1 ? 1 : (g > 8192 ? 8192 : g));
@@ -1003,6 +1037,47 @@ void conv_f32_fwd_pool_s1(const ConvF32Geom& g, const float* x, const float* w, 
       launch_layout<4, 1, 2, 4>(M, g.Kout, K, K, 1, -1, la, lb, epi, s);
     }
   }
+}
+
+// Small batches, valid convs with a fused pool (the ConvNet's conv2 / conv3 at B=100: 100 one-image tiles x 18
+// k-tiles, 800 32x32 tiles x 36 k-tiles, ~30 us each): the same k split as the data gradient below, into planes
+// of the plain conv output, then pool_slab_fwd_kernel sums, adds the bias and pools.  RINGDP_F32_FWD_SLICES=n
+// forces n (1: the one-launch fused kernels).
+int conv_f32_fwd_slices(const ConvF32Geom& g) {
+  if (g.pad != 0) return 1;
+  const int K = g.C * g.R * g.R;
+  const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zout = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
+  if (batch_chunk(g.B, {xin, zout}) < g.B) return 1;
+  const int64_t M = g.B * g.OH * g.OW, plane = M * g.Kout;
+  const int64_t tiles32 = ((M + 31) / 32) * ((g.Kout + 31) / 32);
+  int s = tiles32 >= 8 * f32_num_cus() ? 1 : std::min(8, (K + 8 * BK - 1) / (8 * BK));
+  if (const char* e = std::getenv("RINGDP_F32_FWD_SLICES")) {
+    const int v = std::atoi(e);
+    if (v > 0) s = v;
+  }
+  s = std::max(1, std::min(s, std::min(16, (K + BK - 1) / BK)));
+  if (static_cast<int64_t>(s) * plane >= (int64_t{1} << 29)) return 1;
+  return s;
+}
+
+void conv_f32_fwd_pool_split(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* slab,
+                             int slices, int st, float* a, unsigned char* code, hipStream_t s) {
+  const int K = g.C * g.R * g.R;
+  const int M = static_cast<int>(g.B * g.OH * g.OW);
+  const int plane = M * g.Kout;
+  int per = (K + slices - 1) / slices;
+  per = (per + BK - 1) / BK * BK;
+  const int used = (K + per - 1) / per;
+  const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W;
+  WeightB lb{{w, K * g.Kout * 4, 0.f, 1.f}, K, g.Kout};
+  FwdA<false, false> la{{x, static_cast<int>(g.B * xin * 4), 0.f, 1.f}, g.C, g.H, g.W, g.R, g.pad, g.OW, K, M,
+                        make_fdiv(g.OH * g.OW), make_fdiv(g.OW)};
+  NCHWSlabOut epi{slab, g.Kout, M, plane, make_fdiv(g.OH * g.OW)};
+  launch_gemm(M, g.Kout, K, per, used, -1, la, lb, epi, s);
+  const int PH = st == 2 ? g.OH / 2 : g.OH - 1, PW = st == 2 ? g.OW / 2 : g.OW - 1;
+  const int total = static_cast<int>(g.B) * g.Kout * PH * PW;
+  hipLaunchKernelGGL(pool_slab_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, slab, used, plane, bias, g.Kout,
+                     g.OH, g.OW, st, PH, PW, total, a, code);
 }
 
 // Small batches (the reference's 100 images): the data-gradient GEMM has few workgroups, each with one long k

@@ -111,6 +111,10 @@ void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char
 // Same with the overlapping 2x2/s1 pool (fp32 input, OH * OW <= 128): one image per 128-row tile.
 void conv_f32_fwd_pool_s1(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* a,
                           unsigned char* code, hipStream_t s);
+// small-batch valid conv + ReLU + 2x2 pool (stride st) by split K: slab = conv_f32_fwd_slices(g) x B*Kout*OH*OW floats
+int conv_f32_fwd_slices(const ConvF32Geom& g);
+void conv_f32_fwd_pool_split(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* slab,
+                             int slices, int st, float* a, unsigned char* code, hipStream_t s);
 // slab: conv_f32_dgrad_slices(g) x B*C*H*W floats of split-K partials when that count is > 1 (else unused)
 int conv_f32_dgrad_slices(const ConvF32Geom& g);
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* slab, int slices,

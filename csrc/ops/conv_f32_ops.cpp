@@ -70,6 +70,20 @@ std::tuple<at::Tensor, at::Tensor> f32_conv_pool_fwd(const at::Tensor& x, const 
     RINGDP_CHECK(bias->numel() == g.Kout, "conv_f32 bias: wrong size");
     b = bias->data_ptr<float>();
   }
+  RINGDP_CHECK(stride == 1 || stride == 2, "conv_f32 + pool: 2x2 windows with stride 1 or 2");
+  if (x.scalar_type() == at::kFloat) {  // small batches: split K, then sum + bias + ReLU + pool in one pass
+    const int sl = kern::conv_f32_fwd_slices(g);
+    if (sl > 1) {
+      const int64_t PH = stride == 2 ? g.OH / 2 : g.OH - 1, PW = stride == 2 ? g.OW / 2 : g.OW - 1;
+      auto a = at::empty({g.B, g.Kout, PH, PW}, w.options());
+      auto code = at::empty({g.B, g.Kout, PH, PW}, w.options().dtype(at::kByte));
+      auto slab = at::empty({static_cast<int64_t>(sl) * g.B * g.Kout * g.OH * g.OW}, w.options());
+      kern::conv_f32_fwd_pool_split(g, x.data_ptr<float>(), w.data_ptr<float>(), b, slab.data_ptr<float>(), sl,
+                                    static_cast<int>(stride), a.data_ptr<float>(), code.data_ptr<uint8_t>(),
+                                    util::stream_of(w));
+      return {a, code};
+    }
+  }
   if (stride == 1) {
     RINGDP_CHECK(x.scalar_type() == at::kFloat && g.OH * g.OW <= 128,
                  "conv_f32 + 2x2/s1 pool: fp32 input and at most 128 output pixels per image");

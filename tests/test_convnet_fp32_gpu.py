@@ -92,6 +92,29 @@ def test_conv_f32_dgrad_split_k(monkeypatch, slices, B, Cin, H, K, R, pad):
     _close(dx, ref)
 
 
+@pytest.mark.parametrize("slices", ["1", "2", "5", ""])
+@pytest.mark.parametrize("B,Cin,H,K,st", [(100, 64, 10, 128, 2), (100, 32, 13, 64, 1), (3, 16, 6, 24, 2), (900, 64, 10, 128, 2)])
+def test_conv_f32_pool_split_k(monkeypatch, slices, B, Cin, H, K, st):
+    """Small-batch valid conv + ReLU + 2x2 pool by split K (conv_f32_fwd_slices: B=100 conv3 / conv2 take 5 / 3
+    slices; B=900 conv3 stays one fused launch) against fp64, and against conv-then-pool."""
+    if slices:
+        monkeypatch.setenv("RINGDP_F32_FWD_SLICES", slices)
+    else:
+        monkeypatch.delenv("RINGDP_F32_FWD_SLICES", raising=False)
+    g = torch.Generator(device=DEV).manual_seed(B + K + st)
+    x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+    w = torch.randn(K, Cin, 3, 3, device=DEV, generator=g) * 0.2
+    b = torch.randn(K, device=DEV, generator=g) * 0.1
+    a, code = C.f32_conv_pool_fwd(x, w, b, 0, 0.0, 1.0, st)
+    ref = F.max_pool2d(F.relu(F.conv2d(x.double(), w.double(), b.double())), 2, st).float()
+    _close(a, ref, rtol=1e-5, atol=1e-5)
+    a2, code2 = C.f32_pool_relu_fwd(C.f32_conv_fwd(x, w, b, 0, 0.0, 1.0), 2, st)
+    # another fp32 summation order than the unsplit conv (K = 576 products of magnitude ~5): a few ulp
+    torch.testing.assert_close(a, a2, rtol=1e-5, atol=1e-5)
+    assert float((code == code2).float().mean()) > 0.995
+    assert bool(((code == 255) == (a == 0)).all())
+
+
 def test_conv_f32_batch_chunks(monkeypatch):
     """The host launchers split the batch so every index stays 32-bit; a lowered limit runs that path
     (conv2 shape: 7744 output elements per image, limit 3 images -> chunks of 3, 3, 2)."""
