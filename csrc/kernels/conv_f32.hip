@@ -902,7 +902,9 @@ int wgrad_slices(int M, int N, int64_t K) {
   const int bm = layout_bm(l), bn = layout_bn(l);
   const int64_t tiles = static_cast<int64_t>((M + bm - 1) / bm) * ((N + bn - 1) / bn);
   int64_t s = (2048 + tiles - 1) / tiles;
-  const int64_t cap = (K + wgrad_min_depth() - 1) / wgrad_min_depth();
+  // K below one minimum-depth slice on a grid of < 64 tiles (fc1 at B=100: 16 tiles, K = 100): 2-k-tile slices
+  const int depth = (K < wgrad_min_depth() && tiles < 64) ? 2 * BK : wgrad_min_depth();
+  const int64_t cap = (K + depth - 1) / depth;
   if (s > cap) s = cap;
   return static_cast<int>(s < 1 ? 1 : (s > 1024 ? 1024 : s));
 }
@@ -945,6 +947,40 @@ __global__ __launch_bounds__(256) void linear_skinny_f32_kernel(const float* __r
   }
 }
 
+// The same with one 256-thread workgroup per row and 16-B loads (K % 4 == 0, 16-B aligned rows): each
+// thread's chain is K / 1024 float4 steps instead of K / 64 scalar ones (B=100 fc1: 14.8 us -> see
+// profiles/r05/fp32/); per-wave sums, then the 4 waves in order (deterministic).
+template <int N>
+__global__ __launch_bounds__(256) void linear_row_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                             const float* __restrict__ bias, float* __restrict__ z,
+                                                             int K) {
+  __shared__ float red[4][N];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = blockIdx.x;
+  const float4* xr = reinterpret_cast<const float4*>(x + (int64_t)row * K);
+  const int K4 = K >> 2;
+  float acc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = 0.f;
+  for (int k = tid; k < K4; k += 256) {
+    const float4 v = xr[k];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const float4 q = reinterpret_cast<const float4*>(w + (int64_t)n * K)[k];
+      acc[n] = fmaf(v.x, q.x, fmaf(v.y, q.y, fmaf(v.z, q.z, fmaf(v.w, q.w, acc[n]))));
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float v = acc[n];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wave][n] = v;
+  }
+  __syncthreads();
+  if (tid < N) z[(int64_t)row * N + tid] = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) + (bias ? bias[tid] : 0.f);
+}
+
 }  // namespace
 
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
@@ -959,8 +995,11 @@ void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8
                   const float* w, const float* bias, float* z, hipStream_t s) {
   const int K = g.C * g.R * g.R;
   if (!xu8 && g.R == 1 && g.H == 1 && g.W == 1 && g.Kout == 10 && g.B <= 8192) {  // fc1 at small batches
-    linear_skinny_f32_kernel<10><<<static_cast<unsigned>((g.B + 3) / 4), 256, 0, s>>>(x, w, bias, z,
-                                                                                     static_cast<int>(g.B), K);
+    if (K % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(w) & 15) == 0)
+      linear_row_f32_kernel<10><<<static_cast<unsigned>(g.B), 256, 0, s>>>(x, w, bias, z, K);
+    else
+      linear_skinny_f32_kernel<10><<<static_cast<unsigned>((g.B + 3) / 4), 256, 0, s>>>(x, w, bias, z,
+                                                                                       static_cast<int>(g.B), K);
     return;
   }
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zout = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
