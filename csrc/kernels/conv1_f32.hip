@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 #include "kernels.h"
@@ -111,7 +112,10 @@ __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restr
     if (b >= B) continue;
     float* ab = a1 + static_cast<int64_t>(b) * C1 * NWIN;
     unsigned char* cb = code1 + static_cast<int64_t>(b) * C1 * NWIN;
-    for (int g = split ? wave : 0; g < (4 * NWIN + 15) / 16; g += split ? WAVES : 1) {
+    // split mode with gridDim.y > 1 parts: workgroup (b, part) takes pixel groups part * WAVES + wave, step
+    // WAVES * parts (every part stages the whole image: 784 B)
+    const int gstep = split ? WAVES * static_cast<int>(gridDim.y) : 1;
+    for (int g = split ? static_cast<int>(blockIdx.y) * WAVES + wave : 0; g < (4 * NWIN + 15) / 16; g += gstep) {
       const int m = 16 * g + lr;
       const int base = m < 4 * NWIN ? pix_base(m) : 0;
       f32x4 acc[2] = {dev::zero_f32x4(), dev::zero_f32x4()};
@@ -258,14 +262,25 @@ int conv1_blocks(int64_t B) {
 
 int conv1_f32_wgrad_blocks(int64_t B) { return conv1_blocks(B); }
 
+// forward parts per image in split mode (RINGDP_F32_CONV1_PARTS overrides): B=100 -> 4 (400 workgroups)
+static int conv1_parts(int64_t B) {
+  if (!split_mode(B)) return 1;
+  if (const char* e = std::getenv("RINGDP_F32_CONV1_PARTS")) {
+    const int v = std::atoi(e);
+    if (v > 0) return std::min(v, 11);
+  }
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(4, 512 / std::max<int64_t>(B, 1))));
+}
+
 void conv1_pool_f32_fwd(const float* x, const unsigned char* xu8, int64_t B, float mean, float inv_std,
                         const float* w1, const float* b1, float* a1, unsigned char* code1, hipStream_t s) {
   const int nb = conv1_blocks(B);
+  const dim3 grid(nb, conv1_parts(B));
   if (xu8)
-    hipLaunchKernelGGL(conv1_pool_f32_kernel<true>, dim3(nb), dim3(256), 0, s, xu8, w1, b1, a1, code1,
+    hipLaunchKernelGGL(conv1_pool_f32_kernel<true>, grid, dim3(256), 0, s, xu8, w1, b1, a1, code1,
                        static_cast<int>(B), mean, inv_std);
   else
-    hipLaunchKernelGGL(conv1_pool_f32_kernel<false>, dim3(nb), dim3(256), 0, s, x, w1, b1, a1, code1,
+    hipLaunchKernelGGL(conv1_pool_f32_kernel<false>, grid, dim3(256), 0, s, x, w1, b1, a1, code1,
                        static_cast<int>(B), mean, inv_std);
 }
 
