@@ -201,7 +201,9 @@ __global__ __launch_bounds__(256) void conv1_wgrad_f32_kernel(const void* __rest
     const float* db = da1 + static_cast<int64_t>(b) * C1 * NWIN;
     const unsigned char* cbp = code1 + static_cast<int64_t>(b) * C1 * NWIN;
     // one pooled row (13 windows) at a time: its 52 gradient / code loads are issued together
-    for (int py = split ? wave : 0; py < PW1; py += split ? WAVES : 1) {
+    // split mode with gridDim.y parts: workgroup (b, part) takes pooled rows part * WAVES + wave, step WAVES * parts
+    const int rstep = split ? WAVES * static_cast<int>(gridDim.y) : 1;
+    for (int py = split ? static_cast<int>(blockIdx.y) * WAVES + wave : 0; py < PW1; py += rstep) {
       float dv[PW1][2];
       int cv[PW1][2];
 #pragma unroll
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(256) void conv1_wgrad_f32_kernel(const void* __rest
   for (int w = 0; w < WAVES - 1; ++w)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[q >> 1][q & 1] += red[w][q][lane];
-  float* out = slab + static_cast<int64_t>(blockIdx.x) * C1 * (TAPS + 1);
+  float* out = slab + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * C1 * (TAPS + 1);
 #pragma unroll
   for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
@@ -260,22 +262,25 @@ int conv1_blocks(int64_t B) {
 
 }  // namespace
 
-int conv1_f32_wgrad_blocks(int64_t B) { return conv1_blocks(B); }
-
-// forward parts per image in split mode (RINGDP_F32_CONV1_PARTS overrides): B=100 -> 4 (400 workgroups)
-static int conv1_parts(int64_t B) {
+// workgroups per image in split mode (RINGDP_F32_CONV1_PARTS / _WPARTS override the forward's / the weight
+// gradient's): B=100 -> 4 (400 workgroups; forward 22.5 -> 11.9 us)
+static int conv1_parts(int64_t B, const char* env) {
   if (!split_mode(B)) return 1;
-  if (const char* e = std::getenv("RINGDP_F32_CONV1_PARTS")) {
+  if (const char* e = std::getenv(env)) {
     const int v = std::atoi(e);
     if (v > 0) return std::min(v, 11);
   }
   return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(4, 512 / std::max<int64_t>(B, 1))));
 }
+static int conv1_wparts(int64_t B) { return std::min(conv1_parts(B, "RINGDP_F32_CONV1_WPARTS"), 4); }
+
+// weight-gradient partials (slab rows): one per workgroup, part-major
+int conv1_f32_wgrad_blocks(int64_t B) { return conv1_blocks(B) * conv1_wparts(B); }
 
 void conv1_pool_f32_fwd(const float* x, const unsigned char* xu8, int64_t B, float mean, float inv_std,
                         const float* w1, const float* b1, float* a1, unsigned char* code1, hipStream_t s) {
   const int nb = conv1_blocks(B);
-  const dim3 grid(nb, conv1_parts(B));
+  const dim3 grid(nb, conv1_parts(B, "RINGDP_F32_CONV1_PARTS"));
   if (xu8)
     hipLaunchKernelGGL(conv1_pool_f32_kernel<true>, grid, dim3(256), 0, s, xu8, w1, b1, a1, code1,
                        static_cast<int>(B), mean, inv_std);
@@ -287,11 +292,12 @@ void conv1_pool_f32_fwd(const float* x, const unsigned char* xu8, int64_t B, flo
 void conv1_wgrad_f32(const float* x, const unsigned char* xu8, int64_t B, float mean, float inv_std, const float* da1,
                      const unsigned char* code1, float* slab, hipStream_t s) {
   const int nb = conv1_blocks(B);
+  const dim3 grid(nb, conv1_wparts(B));  // conv1_f32_wgrad_blocks(B) = nb * parts slab rows
   if (xu8)
-    hipLaunchKernelGGL(conv1_wgrad_f32_kernel<true>, dim3(nb), dim3(256), 0, s, xu8, da1, code1, slab,
+    hipLaunchKernelGGL(conv1_wgrad_f32_kernel<true>, grid, dim3(256), 0, s, xu8, da1, code1, slab,
                        static_cast<int>(B), mean, inv_std);
   else
-    hipLaunchKernelGGL(conv1_wgrad_f32_kernel<false>, dim3(nb), dim3(256), 0, s, x, da1, code1, slab,
+    hipLaunchKernelGGL(conv1_wgrad_f32_kernel<false>, grid, dim3(256), 0, s, x, da1, code1, slab,
                        static_cast<int>(B), mean, inv_std);
 }
 
