@@ -2,7 +2,7 @@
 # round-5 closing evidence: the full GPU suite + smoke, then every bench config on the final tree
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r5final3; mkdir -p $O
+O=gpurun_out/r5final5; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/tests.log 2>&1; rc=$?
 tail -3 $O/tests.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error" $O/tests.log | head -20; exit 1; }
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
