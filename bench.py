@@ -43,6 +43,7 @@ import argparse
 import faulthandler
 import json
 import os
+import socket
 import sys
 import time
 
@@ -124,6 +125,32 @@ def _store_agree(dist, key: str, ok: bool, rank: int, world: int) -> bool:
     return all(st.get(k) == b"1" for k in keys)
 
 
+def _identity(dev) -> dict:
+    """Where this run executes, as tools/comm_bench.py records it next to its measurements."""
+    return {"arch": torch.cuda.get_device_properties(dev).gcnArchName, "host": socket.gethostname(),
+            "rccl": ".".join(str(v) for v in torch.cuda.nccl.version())}
+
+
+def _adopt_comm_tuning(path: str, world: int, here: dict) -> dict:
+    """RCCL / small-message settings measured by tools/comm_bench.py --recommend.  Adopted (into the
+    environment, before the communicator exists; variables already set win) only when the file was measured
+    at this world size on this device type, host and RCCL version - a file left over from another box or
+    setup must not silently change this run.  Returns what happened, for the result line."""
+    with open(path) as f:
+        tun = json.load(f)
+    ident = tun.get("identity") or {}
+    if int(tun.get("world", -1)) != world:
+        return {"adopted": False, "reason": f"measured at world {tun.get('world')}, this run has {world}"}
+    bad = [k for k in here if ident.get(k) != here[k]]
+    if bad:
+        return {"adopted": False, "reason": "identity mismatch: " + ", ".join(
+            f"{k} {ident.get(k)!r} != {here[k]!r}" for k in bad)}
+    env = {k: os.environ.setdefault(k, str(v)) for k, v in tun.get("env", {}).items()}
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench] adopted {path}: {env}", file=sys.stderr, flush=True)
+    return {"adopted": True, "env": env, "identity": here}
+
+
 def _pack_batch(x: torch.Tensor, y: torch.Tensor):
     """(buffer, x view, y view): copies of x and y in one uint8 buffer (x bytes first, 8-aligned)."""
     nx = x.numel() * x.element_size()
@@ -174,12 +201,7 @@ def worker(args):
         torch.set_num_threads(max(1, (os.cpu_count() or 2) // max(world_env, 1)))
     comm_tuning = None
     if on_gpu and args.comm_tuning and os.path.exists(args.comm_tuning):
-        # RCCL / small-message settings measured by tools/comm_bench.py --recommend at this world size;
-        # they must be in the environment before the communicator exists
-        with open(args.comm_tuning) as f:
-            tun = json.load(f)
-        if int(tun.get("world", -1)) == world_env:
-            comm_tuning = {k: os.environ.setdefault(k, str(v)) for k, v in tun.get("env", {}).items()}
+        comm_tuning = _adopt_comm_tuning(args.comm_tuning, world_env, _identity(dev))
     if launched:
         dist.init_process_group(backend=backend)
     else:
@@ -287,7 +309,7 @@ def worker(args):
     nat_pg = getattr(ddp, "_native_pg", None)
     # fork-free overlap: linear graph segments, bucket collectives between them on the comm stream
     split_mode = (use_graph and (world > 1 or force_comm) and args.comm_stream == "split"
-                  and args.comm_hook == "allreduce" and hasattr(nat_pg, "set_same_stream"))
+                  and hasattr(nat_pg, "set_same_stream"))
     if use_graph and hasattr(nat_pg, "set_same_stream") and os.environ.get("RINGDP_COMM_SAME_STREAM") is None:
         nat_pg.set_same_stream(args.comm_stream == "same")
     graph = None
@@ -321,6 +343,19 @@ def worker(args):
         else:
             comm_stream_note = "compute stream (no overlap)" if nat_pg.same_stream() else \
                 "side stream inside the graph (overlaps backward; forked graph)"
+
+    # where each bucket's collective runs in the captured step, and its modelled time (ringdp.utils.comm_model)
+    from ringdp.utils import comm_model
+
+    if graph is not None and graph.split_info:
+        split_plan = graph.split_info
+    else:
+        wire = 2 if args.comm_hook != "allreduce" else 4
+        same = bool(getattr(nat_pg, "same_stream", lambda: True)()) if use_graph else False
+        split_plan = [{"bucket": i, "bytes": wire * n, "est_us": round(comm_model.est_us(wire * n, world), 2),
+                       "placement": ("inline (compute stream, one graph)" if same else
+                                     "side stream" if use_graph else "side stream (eager)")}
+                      for i, n in enumerate(ddp.reducer.bucket_numels())]
 
     def run_steps(n, g):
         loss = None
@@ -440,6 +475,9 @@ def worker(args):
                 "comm_stats": comm_stats,
                 "final_loss": round(final_loss, 5),
             }
+            if world > 1 or force_comm:
+                res["split_plan"] = split_plan
+                res["modelled_exposed_us"] = comm_model.scaling_model(split_plan, ms_per_step * 1000.0, world)
             if on_gpu and world > torch.cuda.device_count():
                 res["config"]["ranks_per_gpu"] = world / torch.cuda.device_count()
             if text_only:

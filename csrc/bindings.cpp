@@ -14,6 +14,8 @@
 #include "store/store.h"
 #include "trace/trace.h"
 
+#include <execinfo.h>
+#include <signal.h>
 #include <unistd.h>
 
 #include <condition_variable>
@@ -122,7 +124,22 @@ class PyWork : public Work {
 
 }  // namespace
 
+namespace {
+// RINGDP_ABORT_BACKTRACE=1: a SIGABRT (std::terminate, failed asserts) prints the native stack to stderr before
+// the default action - diagnosis of aborts that happen outside any Python frame (e.g. at process teardown).
+void abort_backtrace(int sig) {
+  static const char kMsg[] = "[ringdp] SIGABRT, native stack:\n";
+  (void)!::write(2, kMsg, sizeof(kMsg) - 1);
+  void* frames[64];
+  const int n = ::backtrace(frames, 64);
+  ::backtrace_symbols_fd(frames, n, 2);
+  ::signal(sig, SIG_DFL);
+  ::raise(sig);
+}
+}  // namespace
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  if (const char* e = std::getenv("RINGDP_ABORT_BACKTRACE"); e && *e && *e != '0') ::signal(SIGABRT, abort_backtrace);
   m.doc() = "ringdp native runtime for AMD MI355X (gfx950): stores, RCCL/host-ring process "
             "groups, gradient reducer and CDNA4 HIP kernels";
 
@@ -607,7 +624,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("std"), py::arg("dw"), py::arg("db"));
   m.def("f32_pool_relu_fwd", &ops::f32_pool_relu_fwd);
   m.def("f32_pool_relu_bwd", &ops::f32_pool_relu_bwd);
-  m.def("cn_pack_weights", &ops::cn_pack_weights);
+  m.def("cn_pack_weights", &ops::cn_pack_weights, py::arg("w1"), py::arg("w2"), py::arg("w3"), py::arg("wfc"),
+        py::arg("out") = py::none());
   m.def("cn_conv1_fwd", &ops::cn_conv1_fwd);
   m.def("cn_conv1_fwd_pack", &ops::cn_conv1_fwd_pack);
   m.def("cn_forward_buffers", &ops::cn_forward_buffers);

@@ -133,6 +133,7 @@ void GpuPG::stop_common() {
     }
     std::lock_guard<std::mutex> lk(wd_mu_);
     inflight_.clear();
+    retired_.clear();
     if (ready_) hipEventDestroy(ready_);
     if (last_) hipEventDestroy(last_);
     if (last_aux_) hipEventDestroy(last_aux_);
@@ -147,6 +148,7 @@ void GpuPG::drain() {
   DeviceScope ds(device_);
   for (auto& w : inflight_) (void)hipEventSynchronize(w->done_);
   inflight_.clear();
+  retired_.clear();
 }
 
 void GpuPG::watch_beacon(const std::shared_ptr<ReplayBeacon>& beacon) {
@@ -201,6 +203,7 @@ void GpuPG::watchdog_loop() {
         auto& w = inflight_.front();
         hipError_t q = hipEventQuery(w->done_);
         if (q == hipSuccess) {
+          retired_.push_back(std::move(w));  // freed on the caller's thread (see retired_)
           inflight_.pop_front();
           continue;
         }

@@ -152,6 +152,10 @@ class GpuPG : public ProcessGroup {
   std::mutex wd_mu_;
   std::condition_variable wd_cv_;
   std::deque<std::shared_ptr<GpuWork>> inflight_;
+  // Works the watchdog saw complete.  They keep their output tensors; the watchdog thread never drops the
+  // last reference (that may release a tensor's Python object, which needs the GIL - fatal for a native
+  // thread while the interpreter finalises).  Freed on the caller's thread by the next launch / drain.
+  std::vector<std::shared_ptr<GpuWork>> retired_;
   std::mutex beacon_mu_;
   std::vector<std::weak_ptr<ReplayBeacon>> beacons_;
   std::thread watchdog_;
@@ -217,8 +221,12 @@ std::shared_ptr<Work> GpuPG::launch(OpType op, const std::vector<at::Tensor>& te
       else eager_aux_since_join_ = true;
     }
     work->deadline_us_ = now_us() + timeout_.count() * 1000;
-    std::lock_guard<std::mutex> wl(wd_mu_);
-    inflight_.push_back(work);
+    std::vector<std::shared_ptr<GpuWork>> retired;
+    {
+      std::lock_guard<std::mutex> wl(wd_mu_);
+      inflight_.push_back(work);
+      retired.swap(retired_);
+    }
   }
   return work;
 }

@@ -295,6 +295,8 @@ void HostRingPG::start_queue(Queue& q) {
         q.tasks.pop_front();
       }
       task();
+      std::lock_guard<std::mutex> lk(q.mu);
+      q.done.push_back(std::move(task));  // freed by the caller's thread (see Queue::done)
     }
   });
 }
@@ -306,13 +308,16 @@ void HostRingPG::stop_queue(Queue& q) {
   }
   q.cv.notify_all();
   if (q.th.joinable()) q.th.join();
+  q.done.clear();
 }
 
 std::shared_ptr<Work> HostRingPG::enqueue(Queue& q, OpType op, std::function<void(HostWork&)> fn) {
   RINGDP_CHECK(!shut_, "process group has been shut down");
   auto work = std::make_shared<HostWork>(op, next_seq());
+  std::vector<std::function<void()>> finished;
   {
     std::lock_guard<std::mutex> lk(q.mu);
+    finished.swap(q.done);  // destroyed on this (the caller's) thread, outside the lock
     q.tasks.emplace_back([work, fn = std::move(fn)] {
       try {
         fn(*work);

@@ -46,6 +46,12 @@ class HostRingPG : public ProcessGroup {
     std::mutex mu;
     std::condition_variable cv;
     std::deque<std::function<void()>> tasks;
+    // Finished tasks, still holding their captures (tensors, the Work).  The worker thread never destroys
+    // them: the last reference to a tensor whose Python object was already dropped must be released on a
+    // thread that may take the GIL, and a worker taking it while the interpreter finalises is terminated
+    // (pthread_exit through a noexcept frame: "terminate called without an active exception").  The
+    // caller's thread frees them on its next enqueue and at shutdown.
+    std::vector<std::function<void()>> done;
     std::thread th;
     bool stop = false;
   };

@@ -97,8 +97,9 @@ void RcclPG::setup_small_path(const std::shared_ptr<Store>& store) {
   const int64_t max_bytes = e ? std::atoll(e) : 0;
   if (max_bytes <= 0) return;
   XgmiConfig cfg = XgmiConfig::from_env();
-  // one-shot only: the slot must hold the largest routed message
-  cfg.slot_bytes = std::max(cfg.slot_bytes, (max_bytes + 15) / 16 * 16);
+  // one-shot only: the slot holds exactly the largest routed message (staging 4 x world x slot)
+  cfg.slot_bytes = (max_bytes + 15) / 16 * 16;
+  cfg.slot_set = true;
   cfg.oneshot_max = cfg.slot_bytes;
   cfg.p2p_slot_bytes = 16;
   auto sub = std::make_shared<PrefixStore>("xgmi_small", store);

@@ -86,6 +86,15 @@ std::unique_ptr<XgmiEngine> XgmiEngine::create(const std::shared_ptr<Store>& sto
   XgmiConfig c = cfg;
   if (shared && !c.blocks_set) c.nblocks = 64;
   if (shared && !c.slot_set) c.slot_bytes = 4 << 20;
+  if (!c.slot_set) {
+    // cap the two staging regions (4 x world x slot per rank, plus every peer's IPC mapping of them) at
+    // RINGDP_XGMI_STAGING_MB (256): 16 MiB slots are 128 MiB at ws2 but would be 512 MiB at ws8, and
+    // small sub-groups from new_group get their own engine; above the cap the slot shrinks (ws8: 8 MiB,
+    // a 26 MB bucket then takes one two-shot pass in world x slot = 64 MiB pieces - still one piece)
+    const int64_t cap = std::max<int64_t>(env_i64("RINGDP_XGMI_STAGING_MB", 256), 4) << 20;
+    const int64_t per = cap / (4 * static_cast<int64_t>(world));
+    if (c.slot_bytes > per) c.slot_bytes = std::max<int64_t>(1 << 20, per >> 20 << 20);
+  }
 
   std::unique_ptr<XgmiEngine> p(new XgmiEngine());
   p->rank_ = rank;

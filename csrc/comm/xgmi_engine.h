@@ -29,7 +29,8 @@ struct XgmiConfig {
   // defaults from the ws2 sweep (profiles/r05/xgmi/): 26 MB all-reduce 164 us at 64 blocks / 4 MiB slots,
   // 82 us at 128 / 16 MiB (69 us at 256 blocks, whose per-workgroup handshakes cost small messages +50 %)
   int nblocks = 128;                 // RINGDP_XGMI_BLOCKS
-  int64_t slot_bytes = 16 << 20;     // RINGDP_XGMI_SLOT_MB (staging: 2 x world x slot per rank)
+  int64_t slot_bytes = 16 << 20;     // RINGDP_XGMI_SLOT_MB (staging: 4 x world x slot per rank, capped at
+                                     // RINGDP_XGMI_STAGING_MB = 256 unless the slot size is set explicitly)
   int64_t p2p_slot_bytes = 1 << 20;  // RINGDP_XGMI_P2P_SLOT_MB
   int64_t oneshot_max = 512 << 10;   // RINGDP_XGMI_ONESHOT_KB: all-reduces up to this size are one-shot
   // set from the environment: otherwise ranks that SHARE a GPU (a one-GPU box running the multi-process

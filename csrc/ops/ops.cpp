@@ -335,12 +335,19 @@ void check_packed(const at::Tensor& p) {
 }
 
 at::Tensor cn_pack_weights(const at::Tensor& w1, const at::Tensor& w2, const at::Tensor& w3,
-                           const at::Tensor& wfc) {
+                           const at::Tensor& wfc, const c10::optional<at::Tensor>& out_opt) {
   check_f32_out(w1, {32, 1, 5, 5}, "conv1 weight");
   check_f32_out(w2, {64, 32, 3, 3}, "conv2 weight");
   check_f32_out(w3, {128, 64, 3, 3}, "conv3 weight");
   check_f32_out(wfc, {10, 2048}, "fc1 weight");
-  at::Tensor out = at::empty({kern::cn_packed_elems()}, w1.options().dtype(at::kBFloat16));
+  at::Tensor out;
+  if (out_opt.has_value() && out_opt->defined()) {  // repack in place (a captured step reads this buffer)
+    out = *out_opt;
+    check_packed(out);
+    RINGDP_CHECK(out.device() == w1.device(), "cn_pack_weights: out on another device");
+  } else {
+    out = at::empty({kern::cn_packed_elems()}, w1.options().dtype(at::kBFloat16));
+  }
   kern::cn_pack_weights(w1.data_ptr<float>(), w2.data_ptr<float>(), w3.data_ptr<float>(),
                         wfc.data_ptr<float>(), out.data_ptr(), cur_stream(w1));
   return out;

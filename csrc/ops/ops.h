@@ -58,7 +58,7 @@ at::Tensor cross_entropy_bwd(const at::Tensor& logits, const at::Tensor& labels,
 
 // MNIST ConvNet blocks (see csrc/kernels/convnet.hip for the F1/F2/F3 split).
 at::Tensor cn_pack_weights(const at::Tensor& w1, const at::Tensor& w2, const at::Tensor& w3,
-                           const at::Tensor& wfc);
+                           const at::Tensor& wfc, const c10::optional<at::Tensor>& out);
 std::tuple<at::Tensor, at::Tensor> cn_conv1_fwd(const at::Tensor& x, const at::Tensor& packed,
                                                 const at::Tensor& b1, double mean, double std,
                                                 double in_scale);

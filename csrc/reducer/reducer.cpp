@@ -344,13 +344,21 @@ void Reducer::launch_bucket(Bucket& b, int64_t index) {
     b.work.reset();
     return;
   }
-  if (split_ && hook_ == CommHook::ALLREDUCE) {  // segmented capture
+  const bool compress = hook_ == CommHook::BF16_COMPRESS || hook_ == CommHook::FP16_COMPRESS;
+  if (split_ && (hook_ == CommHook::ALLREDUCE || compress)) {  // segmented capture
     split_this_iter_ = true;
+    if (compress) {  // the wire copy rides in the segment that produced the gradients
+      auto dt = hook_ == CommHook::BF16_COMPRESS ? at::kBFloat16 : at::kHalf;
+      if (!b.wire.defined() || b.wire.numel() != b.flat.numel() || b.wire.scalar_type() != dt)
+        b.wire = at::empty({b.flat.numel()}, b.flat.options().dtype(dt));
+      ops::cast_copy(b.wire, b.flat);
+    }
     if (split_(index)) {  // the replay issues the collective between segments
       b.work.reset();
+      b.split_wire = compress;
       return;
     }
-    std::vector<at::Tensor> v{b.flat};  // inline: captured on the compute stream
+    std::vector<at::Tensor> v{compress ? b.wire : b.flat};  // inline: captured on the compute stream
     pg_->set_caller_stream_ops(true);
     try {
       b.work = pg_->allreduce(v, ReduceOp::AVG);
@@ -444,13 +452,23 @@ void Reducer::finalize_backward() {
   if (split_this_iter_) {  // segmented capture: the join point before the optimizer
     split_this_iter_ = false;
     split_(-1);
+    // compressed buckets whose collective runs between segments: decompress after the join
+    for (auto& b : buckets_) {
+      if (b.split_wire) {
+        ops::cast_copy(b.flat, b.wire);
+        b.split_wire = false;
+      }
+    }
   }
   ++iteration_;
 }
 
 std::shared_ptr<Work> Reducer::launch_collective(int64_t index) {
   RINGDP_CHECK(index >= 0 && index < static_cast<int64_t>(buckets_.size()), "reducer: bad bucket index ", index);
-  std::vector<at::Tensor> v{buckets_[index].flat};
+  const Bucket& b = buckets_[index];
+  const bool compress = hook_ == CommHook::BF16_COMPRESS || hook_ == CommHook::FP16_COMPRESS;
+  RINGDP_CHECK(!compress || b.wire.defined(), "reducer: bucket ", index, " has no wire buffer");
+  std::vector<at::Tensor> v{compress ? b.wire : b.flat};
   return pg_->allreduce(v, ReduceOp::AVG);
 }
 

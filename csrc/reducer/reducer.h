@@ -86,12 +86,15 @@ class Reducer {
   std::vector<double> collect_comm_times();
 
   // Segmented hipGraph capture (ringdp.utils.graph.StepGraph, split mode): while a split function is set,
-  // each bucket whose collective would be issued (ALLREDUCE hook) asks split(index) first.  true: the capture
-  // ended its current graph segment there and the replay issues the collective between segments on the
-  // comm stream (launch_collective), overlapping the rest of backward; false: the collective is captured
-  // inline on the compute stream (worth less than a segment boundary, or the last bucket, which nothing
-  // follows).  The end of backward calls split(-1), the join point before the optimizer segment.  Every
-  // segment stays a single-stream chain: no fork inside a graph.
+  // each bucket whose collective would be issued (ALLREDUCE / BF16 / FP16 hook) asks split(index) first.
+  // true: the capture ended its current graph segment there (or defers the bucket to the next boundary) and
+  // the replay issues the collective between segments on the comm stream (launch_collective), overlapping
+  // the rest of backward; false: the collective is captured inline on the compute stream (worth less than a
+  // segment boundary, or the last bucket, which nothing follows).  The end of backward calls split(-1), the
+  // join point before the optimizer segment.  Every segment stays a single-stream chain: no fork inside a
+  // graph.  Compressed hooks keep their casts on the compute stream: the bf16/fp16 wire copy is captured in
+  // the segment that produced the gradients, the split collective all-reduces the wire buffer, and the
+  // decompression is captured after the join (finalize_backward), ahead of the optimizer.
   using SplitFn = std::function<bool(int64_t)>;
   void set_capture_split(SplitFn fn) {
     std::lock_guard<std::mutex> lk(mu_);
@@ -109,6 +112,7 @@ class Reducer {
     at::Tensor wire;       // compressed copy for BF16/FP16 hooks
     int64_t pending = 0;
     bool launched = false;
+    bool split_wire = false;  // split capture of a compressed bucket: decompress after the join
     std::shared_ptr<Work> work;
     BucketStats st;
   };

@@ -17,11 +17,13 @@ from ringdp.utils.logging import Meter, log
 
 
 def train(local_rank: int, global_rank: int, use_gpu: bool, args) -> None:
-    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    # the device the caller bound (set_device): consistent even when local_rank >= device_count
+    # (the reference pairs set_device(rank % count) with cuda:local_rank)
+    device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")
     print(f"[init] == local rank: {local_rank}, global rank: {global_rank} ==")
     net = resnet18(num_classes=10).to(device)
-    net = ringdp.DistributedDataParallel(net, device_ids=[local_rank] if use_gpu else None,
-                                         output_device=local_rank if use_gpu else None)
+    net = ringdp.DistributedDataParallel(net, device_ids=[device.index] if use_gpu else None,
+                                         output_device=device.index if use_gpu else None)
     mean, std = CIFAR10.mean, CIFAR10.std
     if use_gpu:
         data, synthetic = cifar10_or_synthetic(args.data)

@@ -45,12 +45,14 @@ def main(argv=None):
         torch.cuda.set_device(local_rank % torch.cuda.device_count())
     dist.init_process_group("nccl" if use_gpu else "gloo")
     torch.manual_seed(0)
-    device = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    # the device bound above (the reference uses cuda:local_rank here, which disagrees with set_device(rank %
+    # count) whenever local_rank >= device_count - SURVEY §2.8-2)
+    device = torch.device("cuda", torch.cuda.current_device()) if use_gpu else torch.device("cpu")
     model = ConvNet().to(device)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), lr=args.lr)
-    model = ringdp.DistributedDataParallel(model, device_ids=[local_rank] if use_gpu else None,
-                                           output_device=local_rank if use_gpu else None)
+    model = ringdp.DistributedDataParallel(model, device_ids=[device.index] if use_gpu else None,
+                                           output_device=device.index if use_gpu else None)
     world = dist.get_world_size()
     if use_gpu:
         data, synthetic = mnist_or_synthetic(args.data)

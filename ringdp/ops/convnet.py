@@ -15,13 +15,15 @@ for it (autograd's handle on "the gradient of conv2's output") next to the real 
 backward is a plain linear-layer backward and pool2/ReLU backward costs no extra pass over
 memory.  Weights live as bf16 MFMA fragments (``C.cn_pack_weights`` layout) next to the fp32 master
 parameters; on the default path ringdp.optim.SGD writes the fragments as it updates the masters
-(``PackState``), so the forward packs only after an outside change of the weights.  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
+(``PackState``), so the forward packs only when no optimizer step wrote them since the last forward
+(``invalidate_pack`` covers raw writes in between).  Autograd fires parameter hooks block by block - fc1/conv3 grads are final after
 ``_Conv3FC.backward`` - so ringdp's reducer starts the first bucket all-reduce while conv2/conv1
 backward kernels still run.
 """
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -244,21 +246,75 @@ def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index:
 class PackState:
     """The ConvNet's packed bf16 MFMA weight fragments, kept across steps.
 
-    The forward packs only when the weights changed under the fragments: ``key`` holds the weights'
-    (version, address) at the last pack, so a version bump (load_state_dict, an in-place edit, any
-    torch optimizer) repacks.  ringdp.optim.SGD's flat step writes the fragments of every weight it
-    updates (``C.sgd_flat(..., packed=buf)``) and then refreshes ``key``; a ringdp step that updates
-    the weights without writing them clears ``key`` (its kernels do not bump versions)."""
+    ringdp.optim.SGD's flat step writes the fragments of every weight it updates
+    (``C.sgd_flat(..., packed=buf)``) and then marks them written (``mark_written``: ``fresh`` plus the
+    weights' (version, address) ``key``).  A forward skips packing only when BOTH hold - the fragments were
+    written by the optimizer since the last forward, and no version bump happened since - and consumes
+    ``fresh``.  So any change of the masters between two forwards without an optimizer step between them
+    repacks, including writes that bump no version (``p.data.mul_``, a broadcast into the raw storage).  The
+    one window left, an outside write between ``optimizer.step()`` and the next forward that bumps no version,
+    is closed by ``invalidate_pack(model)``; ringdp's own raw writers (checkpoint.load, DDP.join) call it.
 
-    __slots__ = ("buf", "key")
+    Captured steps: a forward captured with the optimizer's fragments never packs at replay, so
+    ``StepGraph.replay`` repacks eagerly (``repack``) when a weight's version moved or the state was
+    invalidated since the capture (load_state_dict, an EMA copy, ``invalidate_pack``)."""
+
+    __slots__ = ("buf", "key", "fresh", "ws", "__weakref__")
 
     def __init__(self):
         self.buf = None
         self.key = None
+        self.fresh = False
+        self.ws = ()
 
     @staticmethod
     def key_of(ws):
         return tuple((w._version, w.data_ptr()) for w in ws)
+
+    def mark_written(self, ws):
+        """The optimizer wrote every fragment from the updated masters."""
+        self.key = self.key_of(ws)
+        self.fresh = True
+
+    def invalidate(self):
+        """The masters changed behind the fragments' back: the next forward (or replay) repacks."""
+        self.key = None
+        self.fresh = False
+
+    def consume(self, ws) -> bool:
+        """Forward: True when it must pack the fragments itself."""
+        key = self.key_of(ws)
+        do_pack = not (self.fresh and self.key == key)
+        self.key, self.fresh = key, False
+        return do_pack
+
+    def stale(self) -> bool:
+        return self.buf is not None and bool(self.ws) and self.key != self.key_of(self.ws)
+
+    def repack(self):
+        """Rebuild the fragments from the masters now (stream-ordered on the current stream)."""
+        with torch.no_grad():
+            C.cn_pack_weights(*self.ws, out=self.buf)
+        self.mark_written(self.ws)
+
+
+_PACK_STATES: "weakref.WeakSet[PackState]" = weakref.WeakSet()
+
+
+def pack_states():
+    """Every live ConvNet fragment cache (StepGraph checks them before each replay)."""
+    return [st for st in list(_PACK_STATES) if st.buf is not None]
+
+
+def invalidate_pack(model_or_params) -> None:
+    """Declare that ConvNet weights were written without a version bump (``p.data`` in-place edits, raw
+    broadcasts): the next forward, or the next replay of a captured step, repacks their bf16 fragments.
+    Accepts a module (DDP wrappers included) or an iterable of parameters."""
+    params = model_or_params.parameters() if hasattr(model_or_params, "parameters") else model_or_params
+    for p in params:
+        t = getattr(p, "_ringdp_pack", None)
+        if t is not None:
+            t[0].invalidate()
 
 
 def _pack_state(conv1, conv2, conv3, fc1):
@@ -266,7 +322,10 @@ def _pack_state(conv1, conv2, conv3, fc1):
     if st is None:
         st = PackState()
         conv1.__dict__["_ringdp_pack_state"] = st
+        _PACK_STATES.add(st)
     ws = (conv1.weight, conv2.weight, conv3.weight, fc1.weight)
+    if len(st.ws) != 4 or any(a is not b for a, b in zip(st.ws, ws)):
+        st.ws = ws
     for slot, w in enumerate(ws):  # the optimizer finds the fragments through the parameters
         t = getattr(w, "_ringdp_pack", None)
         if t is None or t[0] is not st or t[1] != slot:
@@ -295,11 +354,10 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         st, ws = _pack_state(conv1, conv2, conv3, fc1)
         bufs = C.cn_forward_buffers(x)
         if st.buf is None or st.buf.device != x.device:
-            st.buf, st.key = bufs[4], None
+            st.buf = bufs[4]
+            st.invalidate()
         bufs = (bufs[0], bufs[1], bufs[2], bufs[3], st.buf)
-        key = PackState.key_of(ws)
-        do_pack = st.key != key  # else the optimizer already wrote these weights' fragments
-        st.key = key
+        do_pack = st.consume(ws)  # False: the optimizer wrote these weights' fragments since the last forward
         z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
                                              conv3.weight.detach(), fc1.weight.detach(), mean, std, scale, bufs)
         fused = (x, conv1.weight.detach(), conv1.bias.detach(), conv2.weight.detach(), conv2.bias.detach(),

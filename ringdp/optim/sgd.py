@@ -55,7 +55,7 @@ def _invalidate_packs(params):
     for p in params:
         t = getattr(p, "_ringdp_pack", None)
         if t is not None:
-            t[0].key = None
+            t[0].invalidate()
 
 
 class SGD(Optimizer):
@@ -165,7 +165,7 @@ class SGD(Optimizer):
             if tgt is not None:  # also write the ConvNet's bf16 fragments of the updated weights
                 st, offs, ws = tgt
                 C.sgd_flat(fp, fg, mom if mom_on else None, h, first, lr_t, None, st.buf, offs)
-                st.key = type(st).key_of(ws)
+                st.mark_written(ws)
                 return
             C.sgd_flat(fp, fg, mom if mom_on else None, h, first, lr_t, None)
             _invalidate_packs(params)

@@ -34,6 +34,7 @@ from .. import distributed as dist
 from .. import ops as _ops
 from .._native import C
 from . import comm_hooks as default_hooks
+from ..ops.convnet import invalidate_pack
 from ..utils import tracing as _tracing
 
 _DEFAULT_FIRST_BUCKET_BYTES = 1024 * 1024
@@ -441,6 +442,10 @@ class DistributedDataParallel(nn.Module):
         src = g.ranks[int(key.item()) % g.size()]
         with torch.no_grad():
             self._broadcast_coalesced([p.data for p in self._params] + list(self._buffers_list), src=src)
+        # raw writes: no version bump, so also drop the ConvNet's packed weight fragments (PackState)
+        for t in list(self._params) + list(self._buffers_list):
+            torch.autograd.graph.increment_version(t)
+        invalidate_pack(self._params)
 
     def register_comm_hook(self, state: Any, hook: Callable):
         """Builtin hooks (allreduce / bf16_compress / fp16_compress from

@@ -23,6 +23,16 @@ def _unwrap(model):
     return getattr(model, "module", model)
 
 
+def _mark_written(module, tensors) -> None:
+    """A broadcast into ``t.data`` bumps no version counter: bump them (saved-tensor checks, version-keyed
+    caches) and drop ringdp's packed ConvNet weight fragments, which would otherwise keep the old weights."""
+    from ..ops.convnet import invalidate_pack
+
+    for t in tensors:
+        torch.autograd.graph.increment_version(t)
+    invalidate_pack(module)
+
+
 def _rank() -> int:
     return dist.get_rank() if dist.is_initialized() else 0
 
@@ -51,9 +61,11 @@ def load(path: str, model, optimizer=None, broadcast: bool = True, map_location=
             optimizer.load_state_dict(state["optimizer"])
         meta = state.get("meta", {})
     if broadcast and dist.is_initialized() and dist.get_world_size() > 1:
+        written = list(m.parameters()) + list(m.buffers())
         with torch.no_grad():
-            for t in list(m.parameters()) + list(m.buffers()):
+            for t in written:
                 dist.broadcast(t.data, src=0)
+        _mark_written(m, written)
         # meta (epoch, step, sampler epoch) always travels: ranks must agree on where they resume
         # or their loops (and collective sequences) diverge; optimizer state only when given
         box = [meta, optimizer.state_dict() if (optimizer is not None and _rank() == 0) else None]

@@ -29,6 +29,12 @@ def _gpu_groups() -> List:
     return [pg for g in list(w.groups.values()) for pg in list(g._gpu.values())]
 
 
+def _pack_states() -> List:
+    from ..ops.convnet import pack_states
+
+    return pack_states()
+
+
 def drain_comms():
     """Block until every in-flight GPU collective of every group has completed."""
     for pg in _gpu_groups():
@@ -60,6 +66,8 @@ class StepGraph:
         self._split = [split_ddp] if split_ddp is not None else []
         self.segments: List[torch.cuda.CUDAGraph] = []
         self.plan: List[List] = []  # plan[k]: what the replay does after segment k (bucket indices / -1 join)
+        self.split_info: List[dict] = []  # per bucket: bytes, modelled collective time, placement
+        self._packs: List = []  # ConvNet fragment caches the captured forward may read without packing
 
     def capture(self):
         if self._split:
@@ -77,13 +85,7 @@ class StepGraph:
         if dump:
             self.graph.enable_debug_mode()
         dev = torch.cuda.current_device()
-        mode = os.environ.get("RINGDP_GRAPH_WATCHDOG", "auto")
-        watch = []
-        if mode != "0":
-            # auto: groups with peers only (a one-rank group has no peer to die; its beacon node would
-            # only add a launch to the step)
-            watch = [pg for pg in _gpu_groups() if pg.device == dev and (mode == "1" or pg.size() > 1)]
-        beacon = ReplayBeacon(dev) if watch else None
+        watch, beacon = self._watch_beacon()
         with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
             out = self.step_fn()
             if beacon is not None:
@@ -98,7 +100,19 @@ class StepGraph:
             pg.watch_beacon(beacon)
         self._beacon = beacon
         self._groups = [pg for pg in _gpu_groups() if pg.device == dev]
+        self._packs = _pack_states()
         return self
+
+    def _watch_beacon(self):
+        """(groups to watch, beacon) for a capture on the current device (see the class docstring)."""
+        dev = torch.cuda.current_device()
+        mode = os.environ.get("RINGDP_GRAPH_WATCHDOG", "auto")
+        watch = []
+        if mode != "0":
+            # auto: groups with peers only (a one-rank group has no peer to die; its beacon node would
+            # only add a launch to the step)
+            watch = [pg for pg in _gpu_groups() if pg.device == dev and (mode == "1" or pg.size() > 1)]
+        return watch, (ReplayBeacon(dev) if watch else None)
 
     def capture_split(self):
         """Fork-free overlap of the bucket collectives with backward.
@@ -112,9 +126,20 @@ class StepGraph:
         segments); before the last bucket's collective and the optimizer the compute stream waits for
         them.  A segment boundary plus two cross-queue waits cost ~15-45 us on MI355X (kernel traces,
         profiles/r05/split/), so a bucket is split off only when its collective is estimated to take
-        longer than ``RINGDP_SPLIT_MIN_US`` (30); the others, and always the last bucket (nothing
-        follows it to overlap), are captured inline on the compute stream.  The segments share one
-        memory pool and always replay in capture order."""
+        longer than ``RINGDP_SPLIT_MIN_US`` (``comm_model.est_us``); the others, and always the last
+        bucket (nothing follows it to overlap), are captured inline on the compute stream - except
+        after a bucket was split: a later bucket then never goes inline before the join (its collective
+        would run on the compute stream while the split one still runs on the comm stream, two
+        collectives of one group at once); it is deferred to the next segment boundary instead and
+        issued there, in bucket order, on the comm stream.  ``RINGDP_SPLIT_BUCKETS`` (comma list of
+        bucket indices) forces the split set (tests).  The segments share one memory pool and always
+        replay in capture order.
+
+        Watchdog: the last segment (the one holding the optimizer) ends with the replay beacon, as
+        ``capture()``'s graph does, so the collectives captured inline are watched too; the ones issued
+        between segments are ordinary eager collectives with their own deadlines."""
+        from . import comm_model
+
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -127,23 +152,22 @@ class StepGraph:
         segs = [torch.cuda.CUDAGraph()]
         plan: List[List] = [[]]
         ddp = self._split[0]
-        nbytes = [4 * n for n in ddp.reducer.bucket_numels()]
+        hook = ddp.reducer.comm_hook()
+        wire = 2 if hook in (C.CommHook.BF16_COMPRESS, C.CommHook.FP16_COMPRESS) else 4
+        nbytes = [wire * n for n in ddp.reducer.bucket_numels()]
         last = len(nbytes) - 1
         world = ddp._native_pg.size()
-        min_us = float(os.environ.get("RINGDP_SPLIT_MIN_US", "30"))
-        state = {"split": False, "joined": False}
+        min_us = float(os.environ.get("RINGDP_SPLIT_MIN_US", str(comm_model.SPLIT_MIN_US)))
+        forced = os.environ.get("RINGDP_SPLIT_BUCKETS")
+        forced = {int(t) for t in forced.split(",") if t.strip()} if forced is not None else None
+        state = {"split": False, "joined": False, "pending": []}
+        info = [{"bucket": i, "bytes": nb, "est_us": round(comm_model.est_us(nb, world), 2), "placement": None}
+                for i, nb in enumerate(nbytes)]
 
-        def est_us(nb):
-            # bucket collective estimate: one rank = a local copy (~1.5 TB/s); else a ring over xGMI at
-            # ~100 GB/s per rank plus a launch / latency term
-            if world <= 1:
-                return nb / 1.5e6
-            return 10.0 + 2.0 * (world - 1) / world * nb / 1.0e5
-
-        def cut(tag):
+        def cut(tags):
             with torch.cuda.stream(s):
                 segs[-1].capture_end()
-                plan[-1].append(tag)
+                plan[-1].extend(tags)
                 segs.append(torch.cuda.CUDAGraph())
                 plan.append([])
                 segs[-1].capture_begin(pool=pool, capture_error_mode="relaxed")
@@ -154,15 +178,28 @@ class StepGraph:
                 # the join: the earlier buckets' collectives before the optimizer (and before the last
                 # bucket's collective, which is captured inline: nothing follows it to overlap)
                 if state["split"] and not state["joined"]:
-                    cut(-1)
+                    cut(state["pending"] + [-1])
+                    state["pending"] = []
                     state["joined"] = True
+                if idx >= 0:
+                    info[idx]["placement"] = "inline (last)"
                 return False
-            if est_us(nbytes[idx]) < min_us:  # cheaper than the segment boundary it would need
-                return False
-            cut(idx)
+            want = (idx in forced) if forced is not None else comm_model.est_us(nbytes[idx], world) >= min_us
+            if not want:
+                if not state["split"]:  # cheaper than the segment boundary it would need
+                    info[idx]["placement"] = "inline"
+                    return False
+                # a split collective may still run on the comm stream: queue this one behind it
+                state["pending"].append(idx)
+                info[idx]["placement"] = "deferred to the next boundary"
+                return True
+            cut(state["pending"] + [idx])
+            state["pending"] = []
             state["split"] = True
+            info[idx]["placement"] = "split"
             return True
 
+        watch, beacon = self._watch_beacon()
         for d in self._split:
             d.reducer.set_capture_split(split)
         try:
@@ -170,6 +207,8 @@ class StepGraph:
                 segs[0].capture_begin(pool=pool, capture_error_mode="relaxed")
                 try:
                     out = self.step_fn()
+                    if beacon is not None:
+                        beacon.mark(s.cuda_stream)
                 finally:
                     segs[-1].capture_end()
         finally:
@@ -177,10 +216,16 @@ class StepGraph:
                 d.reducer.set_capture_split(None)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        assert not state["pending"], "split capture: deferred buckets never issued"
         self.segments, self.plan = segs, plan
+        self.split_info = info
         self.graph = segs[0]
         self.output = out.detach() if torch.is_tensor(out) else out
+        for pg in watch:
+            pg.watch_beacon(beacon)
+        self._beacon = beacon
         self._groups = [pg for pg in _gpu_groups() if pg.device == torch.cuda.current_device()]
+        self._packs = _pack_states()
         return self
 
     def _replay_split(self):
@@ -199,9 +244,16 @@ class StepGraph:
                     works = []
         for w in works:
             w.wait(False)
+        if self._beacon is not None:
+            self._beacon.issued()
         return self.output
 
     def replay(self):
+        for st in self._packs:
+            # weights changed since the capture behind the captured forward's back (a version bump, or
+            # ringdp.ops.convnet.invalidate_pack): rebuild the fragments it reads
+            if st.stale():
+                st.repack()
         if self.segments:
             if self._groups:
                 stream = torch.cuda.current_stream().cuda_stream

@@ -20,13 +20,17 @@ from ringdp.utils.graph import StepGraph  # noqa: E402
 
 def main():
     stall_cycles = int(sys.argv[1])
+    split = len(sys.argv) > 2 and sys.argv[2] == "split"  # the segmented capture (bench.py's default placement)
+    if split:
+        os.environ["RINGDP_SPLIT_BUCKETS"] = "1"  # bucket 0 inline, bucket 1 between segments, the last inline
     os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
     os.environ["RINGDP_GRAPH_WATCHDOG"] = "1"  # one rank: watched only when forced
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
     dist.init_process_group("nccl", timeout=datetime.timedelta(milliseconds=int(os.environ["WD_TIMEOUT_MS"])))
     torch.manual_seed(0)
     model = ConvNet().cuda()
-    ddp = DDP(model, device_ids=[torch.cuda.current_device()])
+    ddp = DDP(model, device_ids=[torch.cuda.current_device()], bucket_cap_mb=0.1 if split else 25.0,
+              first_bucket_mb=0.05 if split else None)
     opt = SGD(ddp.parameters(), lr=1e-3)
     crit = CrossEntropyLoss()
     x = torch.randint(0, 256, (64, 1, 28, 28), dtype=torch.uint8, device="cuda")
@@ -46,7 +50,9 @@ def main():
         step()
     torch.cuda.synchronize()
     stall["on"] = True
-    g = StepGraph(step, warmup=0).capture()
+    g = StepGraph(step, warmup=0, split_ddp=ddp if split else None).capture()
+    if split:
+        print("split plan", [b["placement"] for b in g.split_info], flush=True)
     print("captured; replaying", flush=True)
     g.replay()
     torch.cuda.synchronize()  # the watchdog ends the process while we wait here

@@ -1,7 +1,8 @@
 """One rank of a 2-rank xGMI DDP run whose rank 1 dies in the middle of hipGraph replays.
 
 Env: RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT (torchrun contract), FAULT_TIMEOUT_MS (group
-timeout), FAULT_AT (replay index at which rank 1 hard-exits).  Rank 0 keeps replaying: its kernels
+timeout), FAULT_AT (replay index at which rank 1 hard-exits), FAULT_SPLIT (set: the segmented capture,
+StepGraph(split_ddp=...), with RINGDP_SPLIT_BUCKETS=<its value> - e.g. "1" or "" for all inline).  Rank 0 keeps replaying: its kernels
 wait for a peer that never arrives, give up after the timeout, and the watchdog must end the process
 non-zero (SURVEY.md §4.3 Fault row).  Prints "SURVIVED" if rank 0 ever gets past its loop (a bug)."""
 import datetime
@@ -45,7 +46,12 @@ def main():
 
     for _ in range(2):
         step()
-    g = StepGraph(step, warmup=1).capture()
+    split = os.environ.get("FAULT_SPLIT")
+    if split is not None:
+        os.environ["RINGDP_SPLIT_BUCKETS"] = split
+    g = StepGraph(step, warmup=1, split_ddp=ddp if split is not None else None).capture()
+    if split is not None:
+        print(f"rank {rank}: split plan {[b['placement'] for b in g.split_info]}", file=sys.stderr, flush=True)
     for i in range(10_000):
         if rank == 1 and i == fault_at:
             torch.cuda.synchronize()

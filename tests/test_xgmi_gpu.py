@@ -75,6 +75,35 @@ def test_xgmi_ddp_equivalence(tmp_path, world, name, graph):
     _check_train(tmp_path, world, rel=1e-3)
 
 
+@pytest.mark.parametrize("graph,want", [
+    ("split_mix", ["inline", "split", "inline (last)"]),
+    ("split_defer", ["split", "deferred to the next boundary", "inline (last)"]),
+    ("split_bf16", ["split", "deferred to the next boundary", "inline (last)"]),
+])
+def test_xgmi_split_placements(tmp_path, graph, want):
+    """The segmented capture with mixed placements at ws2 (a bucket captured inline while an
+    earlier split bucket's collective may still run on the comm stream would put two collectives of one
+    group in flight at once; it is deferred behind it instead), and bf16-compressed buckets under split
+    (wire cast in the producing segment, wire all-reduce between segments, decompression after the join)."""
+    spawn(MW.ddp_train_worker, args=(2, free_port(), str(tmp_path), "xgmi", "convnet", graph, False), nprocs=2)
+    r0 = _check_train(tmp_path, 2, rel=3e-2 if graph == "split_bf16" else 1e-3)
+    assert r0["placements"] == want, r0["placements"]
+
+
+@pytest.mark.parametrize("case", ["ckpt", "join"])
+def test_xgmi_packed_weights_after_raw_writes(tmp_path, case):
+    """VERDICT r5 next #1b (ii)/(iii): checkpoint.load and DDP.join write the fp32 masters through raw
+    broadcasts (no version bump) right after an optimizer step wrote fresh bf16 fragments; the next forward
+    must repack: logits equal a freshly packed model's bit for bit, on every rank."""
+    spawn(MW.pack_sync_worker, args=(2, free_port(), str(tmp_path), "xgmi", case), nprocs=2)
+    for r in range(2):
+        res = eval((tmp_path / f"r{r}").read_text())  # noqa: S307 - our own repr of a dict of bools/floats
+        assert res["equal"], (r, res)
+        assert res["replicas"], (r, res)
+        if case == "ckpt":
+            assert res["loaded"], (r, res)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_xgmi_bucket_order_under_perturbed_readiness(tmp_path, world):
     spawn(MW.ddp_train_worker, args=(world, free_port(), str(tmp_path), "xgmi", "convnet", True, True), nprocs=world)
@@ -82,18 +111,25 @@ def test_xgmi_bucket_order_under_perturbed_readiness(tmp_path, world):
     assert r0["n_buckets"] > 1
 
 
-def _fault_env(port, rank, world=2):
-    return dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
-                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FAULT_TIMEOUT_MS="4000", FAULT_AT="3",
-                PYTHONPATH=ROOT)
+def _fault_env(port, rank, world=2, split=None):
+    env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), FAULT_TIMEOUT_MS="4000", FAULT_AT="3",
+               PYTHONPATH=ROOT)
+    if split is not None:
+        env["FAULT_SPLIT"] = split
+    return env
 
 
-def test_xgmi_rank_killed_mid_replay_survivor_exits_nonzero():
+@pytest.mark.parametrize("split", [None, "1", ""])
+def test_xgmi_rank_killed_mid_replay_survivor_exits_nonzero(split):
     """No launcher in between: the survivor itself must notice (kernel timeout word / replay beacon)
-    and end non-zero within the group timeout plus slack, with the watchdog's message."""
+    and end non-zero within the group timeout plus slack, with the watchdog's message.  ``split``: the
+    segmented capture (bench.py's default placement) - "1": bucket 0 inline, bucket 1 between segments,
+    the last inline; "": every collective inline (what the cost model picks for the ConvNet's small
+    buckets), watched only through the replay beacon at the end of the last segment."""
     port = free_port()
-    procs = [subprocess.Popen([sys.executable, FAULT], cwd=ROOT, env=_fault_env(port, r), stdout=subprocess.PIPE,
-                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, FAULT], cwd=ROOT, env=_fault_env(port, r, split=split),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
     t0 = time.time()
     try:
         out1, err1 = procs[1].communicate(timeout=240)

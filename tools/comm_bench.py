@@ -26,6 +26,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -81,6 +82,9 @@ def worker(args):
     else:
         impls = ["rccl"] + (["rccl+xgmi_small"] if pg.p2p_max_bytes() > 0 else [])
     variant = {k: os.environ[k] for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MIN_NCHANNELS") if k in os.environ}
+    # where the numbers were measured: bench.py adopts a recommendation only on the same device / host / RCCL
+    ident = {"arch": torch.cuda.get_device_properties(dev).gcnArchName, "host": socket.gethostname(),
+             "rccl": ".".join(str(v) for v in torch.cuda.nccl.version())}
     # The first timed measurement of a process ran several times slower whatever its size (ranks sharing
     # a GPU settle their queues / clocks): one untimed pass of the first size goes before the sweep.
     first = max(1, int(args.sizes.split(",")[0]) // 4)
@@ -135,7 +139,7 @@ def worker(args):
                     line = json.dumps({"impl": impl, "world": world, "dtype": dt_name, "bytes": nbytes,
                                        "us_per_op": round(us, 2), "algbw_GBps": round(algbw, 2),
                                        "busbw_GBps": round(algbw * 2 * (world - 1) / max(world, 1), 2),
-                                       "correct": ok, "rccl_env": variant})
+                                       "correct": ok, "rccl_env": variant, "identity": ident})
                     print(line, flush=True)
                     if os.environ.get("RINGDP_COMM_BENCH_OUT"):  # the parent's --recommend collects these
                         with open(os.environ["RINGDP_COMM_BENCH_OUT"], "a") as f:
@@ -169,7 +173,9 @@ def recommend(rows, world):
         else:
             break
     env["RINGDP_P2P_ALLREDUCE_MAX_BYTES"] = str(thresh)
-    return {"world": world, "env": env,
+    idents = {json.dumps(r.get("identity"), sort_keys=True) for r in rows}
+    ident = json.loads(idents.pop()) if len(idents) == 1 else None  # mixed or unknown: adopt nowhere
+    return {"world": world, "env": env, "identity": ident,
             "evidence": {"rccl_us_by_variant": {k: full[k] for k in full},
                          "xgmi_small_us": small, "chosen_variant": best}}
 
