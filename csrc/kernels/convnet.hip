@@ -204,30 +204,81 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned char u8x8 __attribute__((ext_vector_type(8)));
 
+// Packed 16-bit VALU ops (two channels per instruction).  The constant 1 of min(m - v, 1) is made opaque
+// to the optimiser (an empty asm that "defines" it): with a visible constant, LLVM turns the min into a
+// per-element compare + select and scalarises the whole chain (the pool2 loop of the fused forward was
+// 130 VALU + 40 SALU per 8 channels; this form is ~66 v_pk_* VALU).  (Every op as inline asm instead
+// compiles to the same VALU count plus an s_nop between dependent asm statements.)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 opaque_u16x2(uint32_t v) {
+  asm volatile("" : "+v"(v));
+  return __builtin_bit_cast(u16x2, v);
+}
+
 // relu(max over a 2x2 window) of 8 bf16 channels, plus the pool2 code byte per channel: one-hot bit
 // dy*2+dx of the first maximum in (0,0),(0,1),(1,0),(1,1) order (torch max_pool2d semantics), 0 = the
 // pooled value is 0 (no gradient flows).  Done on the raw bf16 bit patterns with packed int16
-// ops (v_pk_max_i16 & co, 2 channels per instruction): for values >= 0 the integer order is the float
-// order and any negative value is a negative int16, so max(v0..v3, 0) over int16 IS relu(max).
+// ops (2 channels per instruction): for values >= 0 the integer order is the float order and any
+// negative value is a negative int16, so max(v0..v3, 0) over int16 IS relu(max).  Per channel pair:
+// k_i = min(m - v_i, 1) is 0 iff v_i == m (u16 difference; a negative v_i wraps to non-zero), the first
+// index with v_i == m is k0 + k0 k1 + k0 k1 k2 = k0 + (k0 k1)(1 + k2), and the code is (1 << idx) * min(m, 1).
 __device__ __forceinline__ void pool2_code8(const bf16* r0, int rs, int w, bf16x8& out, uint2& code) {
-  const s16x8 v0 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0));
-  const s16x8 v1 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0 + rs));
-  const s16x8 v2 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0 + w * rs));
-  const s16x8 v3 = __builtin_bit_cast(s16x8, *reinterpret_cast<const bf16x8*>(r0 + (w + 1) * rs));
-  const s16x8 zero = (s16x8)0;
-  const s16x8 m = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_elementwise_max(v0, v1),
-                                                                      __builtin_elementwise_max(v2, v3)),
-                                            zero);
-  const u16x8 mu = __builtin_bit_cast(u16x8, m), one = (u16x8)1;
-  // k_i = 0 iff v_i == m (u16 difference; a negative v_i wraps to a non-zero value)
-  const u16x8 k0 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v0), one);
-  const u16x8 k1 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v1), one);
-  const u16x8 k2 = __builtin_elementwise_min(mu - __builtin_bit_cast(u16x8, v2), one);
-  const u16x8 t1 = k0 * k1;
-  const u16x8 idx = k0 + t1 + t1 * k2;                                    // first i with v_i == m
-  const u16x8 live = __builtin_elementwise_min(mu, one);                  // 0 iff m == 0
-  out = __builtin_bit_cast(bf16x8, m);
-  code = __builtin_bit_cast(uint2, __builtin_convertvector((one << idx) * live, u8x8));
+  const uint4 v0 = *reinterpret_cast<const uint4*>(r0);
+  const uint4 v1 = *reinterpret_cast<const uint4*>(r0 + rs);
+  const uint4 v2 = *reinterpret_cast<const uint4*>(r0 + w * rs);
+  const uint4 v3 = *reinterpret_cast<const uint4*>(r0 + (w + 1) * rs);
+  const u16x2 one = opaque_u16x2(0x00010001u);
+  const uint32_t a[4] = {v0.x, v0.y, v0.z, v0.w}, b[4] = {v1.x, v1.y, v1.z, v1.w},
+                 c[4] = {v2.x, v2.y, v2.z, v2.w}, d[4] = {v3.x, v3.y, v3.z, v3.w};
+  // stage-major over the 4 channel pairs: dependent packed ops are never adjacent (gfx950 pads a packed
+  // 16-bit result read by the next instruction with an s_nop, 4 cycles each)
+  s16x2 sa[4], sb[4], sc[4], x0[4], x1[4], sm[4];
+  u16x2 k0[4], k1[4], k2[4], t1[4], idx[4];
+  uint32_t m[4], cd[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sa[j] = __builtin_bit_cast(s16x2, a[j]);
+    sb[j] = __builtin_bit_cast(s16x2, b[j]);
+    sc[j] = __builtin_bit_cast(s16x2, c[j]);
+    x0[j] = __builtin_elementwise_max(sa[j], sb[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) x1[j] = __builtin_elementwise_max(sc[j], __builtin_bit_cast(s16x2, d[j]));
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sm[j] = __builtin_elementwise_max(x0[j], x1[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) sm[j] = __builtin_elementwise_max(sm[j], (s16x2)0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) k0[j] = __builtin_bit_cast(u16x2, sm[j]) - __builtin_bit_cast(u16x2, sa[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) k1[j] = __builtin_bit_cast(u16x2, sm[j]) - __builtin_bit_cast(u16x2, sb[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) k2[j] = __builtin_bit_cast(u16x2, sm[j]) - __builtin_bit_cast(u16x2, sc[j]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    k0[j] = __builtin_elementwise_min(k0[j], one);
+    k1[j] = __builtin_elementwise_min(k1[j], one);
+    k2[j] = __builtin_elementwise_min(k2[j], one);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t1[j] = k0[j] * k1[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) k2[j] = k2[j] + one;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) idx[j] = t1[j] * k2[j] + k0[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t1[j] = __builtin_elementwise_min(__builtin_bit_cast(u16x2, sm[j]), one);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) idx[j] = one << idx[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    m[j] = __builtin_bit_cast(uint32_t, sm[j]);
+    cd[j] = __builtin_bit_cast(uint32_t, idx[j] * t1[j]);
+  }
+  out = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
+  // codes (one per 16-bit half, < 16) -> 8 bytes: v_perm_b32 picks bytes 0 / 2 of two registers each
+  code = make_uint2(__builtin_amdgcn_perm(cd[1], cd[0], 0x06040200u), __builtin_amdgcn_perm(cd[3], cd[2], 0x06040200u));
 }
 
 // First-max argmax over the 4 registers of a window + bias + ReLU (torch max_pool2d semantics:
@@ -364,9 +415,9 @@ __device__ __forceinline__ uint32_t pool4_key(const f32x4& c, uint32_t& code) {
   const int k1 = (int)__builtin_amdgcn_bitop3_b32(__float_as_uint(c[1]), 3u, 2u, 0xBA);
   const int k2 = (int)__builtin_amdgcn_bitop3_b32(__float_as_uint(c[2]), 3u, 1u, 0xBA);
   const int k3 = (int)(__float_as_uint(c[3]) & ~3u);
-  const int km = max(max(k0, k1), max(k2, k3));
+  const int km = max(max(max(k0, k1), k2), max(k3, 0));  // two v_max3_i32
   code = km > 0 ? 1u << (~(uint32_t)km & 3u) : 0u;  // one-hot: bit dy*2+dx = where the gradient goes
-  return (uint32_t)max(km, 0);
+  return (uint32_t)km;
 }
 
 // F1: 4 waves; per image 43 m-tiles of 16 window-ordered rows (169 windows), 2 n-tiles (channel pairs),
@@ -860,13 +911,19 @@ __device__ __forceinline__ void ff_wait_packed(unsigned* sync, int npack) {
 // 400 / 480 / 560 / 800 -> 1402 / 1387 / 1342 / 1363 us at B=65536)
 __device__ __forceinline__ void ff_pool2(const bf16* Cs, bf16* X3b, bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
                                          int b, int t, int lo, int hi) {
+  // uniform per-image bases, 32-bit per-item offsets (no 64-bit address math per item); at most 3 items
+  // per thread (hi - lo <= 800, 256 threads per role)
   bf16x8* da = reinterpret_cast<bf16x8*>(a2 + (int64_t)b * 6400);
   uint2* di = reinterpret_cast<uint2*>(idx2 + (int64_t)b * 6400);
-  for (int it = lo + t; it < hi; it += 256) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int it = lo + t + 256 * k;
+    if (it >= hi) break;
     const int p = it >> 3, c = (it & 7) * 8;
+    const int y = (p * 205) >> 11;  // p / 10 for p < 100
     bf16x8 v;
     uint2 code;
-    pool2_code8(Cs + ((p / 10) * 11 + p % 10) * C2_CRS + c, C2_CRS, 11, v, code);
+    pool2_code8(Cs + (p + y) * C2_CRS + c, C2_CRS, 11, v, code);  // row y * 11 + (p - 10 y) = p + y
     da[it] = v;
     di[it] = code;
     *reinterpret_cast<bf16x8*>(X3b + p * C3F_XRS + c) = v;

@@ -42,6 +42,11 @@ _FUSED_FWD = os.environ.get("RINGDP_CN_FUSED_FWD", "1") != "0"
 _DEFER = os.environ.get("RINGDP_CN_DEFER_REDUCE", "0") == "1"
 # RINGDP_CN_HEAD_CE=0: ringdp's cross entropy on the ConvNet logits stays a separate node (A/B)
 _HEAD_CE = os.environ.get("RINGDP_CN_HEAD_CE", "1") != "0"
+# Batches up to RINGDP_CN_NET_NODE_MAX_B (4096; 0 disables): the fused cross entropy is ONE autograd node over
+# the whole network (_NetCE), whose backward is conv3 (+fc1 +CE) backward, conv12 backward and a single
+# weight-gradient reduction launch.  Above it the head and conv1/conv2 stay separate nodes, so the fc1/conv3
+# gradient bucket can be all-reduced while conv2/conv1 backward still run.
+_NET_NODE_MAX_B = int(os.environ.get("RINGDP_CN_NET_NODE_MAX_B", "4096"))
 
 
 def _defer_reduce(params, grads, need_in: bool) -> bool:
@@ -223,6 +228,42 @@ class _HeadCE(torch.autograd.Function):
                 dwfc if n[3] else None, dbfc if n[4] else None) + (None,) * 6
 
 
+class _NetCE(torch.autograd.Function):
+    """Cross entropy on the ConvNet logits as ONE node over every layer (small batches, see _NET_NODE_MAX_B).
+
+    The forward reuses the logits and activations of the fused forward.  The backward forms d(logits) inside
+    the fc1 backward, runs conv3's backward with its weight-gradient reduction deferred, then conv2's backward +
+    conv1's weight gradient, whose reduction launch also reduces the deferred conv3 / fc1 slabs: one reduction
+    launch per step instead of two.  Deferral is safe by construction here: every gradient slot
+    it leaves pending is written before this node returns, and autograd reads a node's gradients only after
+    it returns, so another producer of the same weight (a penalty term, a tied use) is summed with the final
+    values in stream order."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3, wfc, bfc, logits, target, saved, ignore_index, eps, reduction):
+        loss, lse, ws = C.cross_entropy_fwd(logits, target, ignore_index, eps, reduction)
+        ctx.save_for_backward(logits, target, lse, ws)
+        ctx.saved_acts = saved
+        ctx.params = (w1, b1, w2, b2, w3, b3, wfc, bfc)
+        ctx.cfg = (ignore_index, eps, reduction)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, target, lse, ws = ctx.saved_tensors
+        x, idx1, a1, a2, idx2, a3, idx3, packed, norm = ctx.saved_acts
+        w1, b1, w2, b2, w3, b3, wfc, bfc = ctx.params
+        n = ctx.needs_input_grad
+        g3 = [grad_buffer(p) for p in (w3, b3, wfc, bfc)]
+        dz2 = C.cn_conv3_fc_ce_bwd(a2, idx2, a3, idx3, wfc.detach(), logits, target, lse, ws,
+                                   grad_out.contiguous(), *ctx.cfg, packed, True, *g3, True)
+        dw1, db1, dw2, db2 = (grad_buffer(t) for t in (w1, b1, w2, b2))
+        # also launches the reduction of the deferred conv3 / fc1 weight-gradient slabs
+        C.cn_conv12_bwd(x, idx1, a1, dz2, packed, dw2, db2, dw1, db1, *norm)
+        grads = (dw1, db1, dw2, db2) + tuple(g3)
+        return (None,) + tuple(g if need else None for g, need in zip(grads, n[1:9])) + (None,) * 6
+
+
 def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int, eps: float,
                        reduction: int):
     """Fused head + cross entropy when ``logits`` is a ConvNet head output (see ``_HeadCE``), else
@@ -232,13 +273,19 @@ def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index:
         return None
     if target.dim() != 1 or target.shape[0] != logits.shape[0] or not target.is_cuda:
         return None
-    z2, a2, idx2, w3, b3, wfc, bfc, packed, a3, idx3, version, node = head
+    z2, a2, idx2, w3, b3, wfc, bfc, packed, a3, idx3, version, node, net = head
     # The fused loss reads logits.detach(): only exact when the logits are still the untouched output of
     # _Conv3FC (an in-place edit bumps the version and replaces grad_fn) and nobody observes their gradient
     # (tensor hooks, retain_grad) - otherwise the plain criterion, whose backward runs through _Conv3FC.
     if logits._version != version or logits.grad_fn is not node or logits.retains_grad \
             or logits._backward_hooks:
         return None
+    if net is not None and logits.shape[0] <= _NET_NODE_MAX_B:
+        x, idx1, a1, w1, b1, w2, b2, norm = net
+        # every weight must want a gradient: partially frozen models keep the per-block nodes
+        if all(p.requires_grad for p in (w1, b1, w2, b2, w3, b3, wfc, bfc)):
+            return _NetCE.apply(x, w1, b1, w2, b2, w3, b3, wfc, bfc, logits.detach(), target.long().contiguous(),
+                                (x, idx1, a1, a2, idx2, a3, idx3, packed, norm), ignore_index, eps, reduction)
     return _HeadCE.apply(z2, w3, b3, wfc, bfc, logits.detach(), target.long().contiguous(),
                          (a2, idx2, a3, idx3, packed), ignore_index, eps, reduction)
 
@@ -350,6 +397,7 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
         mean, std, scale = 0.0, 1.0, 1.0
     x = x.contiguous()
     fused = None
+    net = None
     if _FUSE12 and _FUSED_FWD:
         st, ws = _pack_state(conv1, conv2, conv3, fc1)
         bufs = C.cn_forward_buffers(x)
@@ -362,6 +410,7 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
                                              conv3.weight.detach(), fc1.weight.detach(), mean, std, scale, bufs)
         fused = (x, conv1.weight.detach(), conv1.bias.detach(), conv2.weight.detach(), conv2.bias.detach(),
                  mean, std, scale, bufs[0], bufs[1], do_pack)
+        net = (x, bufs[1], bufs[0], conv1.weight, conv1.bias, conv2.weight, conv2.bias, (mean, std, scale))
     elif _FUSE12:
         z2, a2, idx2, packed = _Conv12.apply(x, conv1.weight, conv1.bias, conv2.weight, conv2.bias,
                                              conv3.weight.detach(), fc1.weight.detach(), mean, std, scale)
@@ -374,5 +423,5 @@ def convnet_forward(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
     if logits.requires_grad:
         # what ringdp's cross entropy needs to fuse itself into the head (head_cross_entropy)
         logits._ringdp_head = (z2, a2, idx2, conv3.weight, conv3.bias, fc1.weight, fc1.bias, packed, a3, idx3,
-                               logits._version, logits.grad_fn)
+                               logits._version, logits.grad_fn, net)
     return logits
