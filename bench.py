@@ -477,7 +477,8 @@ def worker(args):
             }
             if world > 1 or force_comm:
                 res["split_plan"] = split_plan
-                res["modelled_exposed_us"] = comm_model.scaling_model(split_plan, ms_per_step * 1000.0, world)
+                res["modelled_exposed_us"] = comm_model.scaling_model(
+                    split_plan, ms_per_step * 1000.0, world, split=bool(graph is not None and graph.split_info))
             if on_gpu and world > torch.cuda.device_count():
                 res["config"]["ranks_per_gpu"] = world / torch.cuda.device_count()
             if text_only:

@@ -55,15 +55,34 @@ def exposed_us(plan: List[Dict], world: int, algo: str = "ring") -> float:
                if str(b.get("placement", "inline")).startswith("inline"))
 
 
-def scaling_model(plan: List[Dict], step_us: float, world_now: int, worlds=(2, 4, 8)) -> Dict:
+def replan(plan: List[Dict], world: int, min_us: float = SPLIT_MIN_US) -> List[Dict]:
+    """The placement the split capture (ringdp.utils.graph.StepGraph.capture_split) would choose for the
+    same buckets at ``world`` ranks: split where the modelled collective is at least ``min_us`` (never the
+    last bucket), deferred behind an earlier split, else inline."""
+    out, split = [], False
+    for i, b in enumerate(plan):
+        if i == len(plan) - 1:
+            pl = "inline (last)"
+        elif est_us(b["bytes"], world) >= min_us:
+            pl, split = "split", True
+        else:
+            pl = "deferred to the next boundary" if split else "inline"
+        out.append(dict(b, placement=pl))
+    return out
+
+
+def scaling_model(plan: List[Dict], step_us: float, world_now: int, worlds=(2, 4, 8), split: bool = True) -> Dict:
     """Modelled exposed comm and weak-scaling efficiency at other world sizes, from this run's plan and
-    step time.  The comm-free step time is the measured step minus this run's modelled inline comm."""
+    step time.  The comm-free step time is the measured step minus this run's modelled inline comm.  With
+    ``split`` (the captured step is segment-split), each world size gets its own placement (``replan``)."""
     base = max(step_us - exposed_us(plan, world_now), 1e-3)
     out: Dict = {"comm_free_step_us": round(base, 2), "assumptions": "ringdp.utils.comm_model (fitted on "
                  "ranks sharing one MI355X; no multi-GPU measurement behind the N>1 terms)"}
     for n in worlds:
-        ring = exposed_us(plan, n, "ring")
-        one = exposed_us(plan, n, "oneshot")
-        out[str(n)] = {"exposed_us_ring": round(ring, 2), "exposed_us_oneshot": round(one, 2),
+        p = replan(plan, n) if split else plan
+        ring = exposed_us(p, n, "ring")
+        one = exposed_us(p, n, "oneshot")
+        out[str(n)] = {"placement": [b["placement"] for b in p],
+                       "exposed_us_ring": round(ring, 2), "exposed_us_oneshot": round(one, 2),
                        "E_ring": round(base / (base + ring), 3), "E_oneshot": round(base / (base + one), 3)}
     return out

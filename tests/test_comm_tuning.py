@@ -90,8 +90,9 @@ def test_comm_model_placement_and_scaling():
 
     assert abs(cm.est_us(77312, 2) - 8.55) < 1.0 and abs(cm.est_us(77312, 4) - 15.1) < 1.5
     assert cm.est_us(369_000, 8) > cm.SPLIT_MIN_US > cm.est_us(76_000, 1)
-    plan = [{"bytes": 369_000, "placement": "split"}, {"bytes": 76_000, "placement": "inline (last)"}]
-    m = cm.scaling_model(plan, 3400.0, 1)
+    plan = [{"bytes": 369_000, "placement": "inline"}, {"bytes": 76_000, "placement": "inline (last)"}]
+    m = cm.scaling_model(plan, 3400.0, 1)  # the one-rank run captured both inline; at N=8 bucket 0 splits
+    assert m["8"]["placement"] == ["split", "inline (last)"] and m["2"]["placement"] == ["inline", "inline (last)"]
     assert m["8"]["exposed_us_ring"] == round(cm.est_us(76_000, 8), 2)
     assert m["8"]["E_ring"] > 0.98
     one = cm.scaling_model([{"bytes": 454_720, "placement": "inline (last)"}], 80.0, 1)

@@ -302,7 +302,7 @@ def test_convnet_bf16_trajectory_b4096():
     assert d < 5e-3, d
 
 
-@pytest.mark.parametrize("B,bucket_mb", [(100, None), (4096, None), (100, 0.05)])
+@pytest.mark.parametrize("B,bucket_mb", [(100, None), (4096, None), (100, 0.05), (5000, None), (5000, 0.05)])
 def test_head_ce_fusion_and_deferred_reduce(world1, B, bucket_mb):
     """The cross entropy fused into the fc1 backward (no ce_bwd launch) and the conv3 / fc1
     weight-gradient reduction folded into conv12's reduction launch give bit-identical losses and
@@ -344,7 +344,10 @@ def test_head_ce_fusion_and_deferred_reduce(world1, B, bucket_mb):
             assert torch.equal(l1, l0), cfg
             for a, b in zip(g1, g0):
                 assert torch.equal(a, b), cfg
-            if cfg[1] and cfg[2]:  # deferral only under DDP, and only into the last bucket: with small
+            if cfg[0] and B <= cn._NET_NODE_MAX_B:
+                # the whole-network node (_NetCE): one merged reduction per backward, with or without DDP
+                assert n1 == 3, (cfg, n1)
+            elif cfg[1] and cfg[2]:  # deferral only under DDP, and only into the last bucket: with small
                 # buckets conv3 / fc1 sit in the first one once the buckets follow the ready order
                 # (iteration 0's registration-order buckets may still allow it)
                 assert (n1 <= 1) if bucket_mb is not None else (n1 >= 2), (cfg, n1)
