@@ -20,9 +20,11 @@ from ringdp.utils.graph import StepGraph  # noqa: E402
 
 def main():
     stall_cycles = int(sys.argv[1])
-    split = len(sys.argv) > 2 and sys.argv[2] == "split"  # the segmented capture (bench.py's default placement)
+    # split=<buckets>: the segmented capture (bench.py's default placement) with RINGDP_SPLIT_BUCKETS=<buckets>
+    # ("1": bucket 0 inline, bucket 1 between segments, the last inline; "": every bucket inline)
+    split = len(sys.argv) > 2 and sys.argv[2].startswith("split=")
     if split:
-        os.environ["RINGDP_SPLIT_BUCKETS"] = "1"  # bucket 0 inline, bucket 1 between segments, the last inline
+        os.environ["RINGDP_SPLIT_BUCKETS"] = sys.argv[2][len("split="):]
     os.environ["RINGDP_DDP_FORCE_COMM"] = "1"
     os.environ["RINGDP_GRAPH_WATCHDOG"] = "1"  # one rank: watched only when forced
     torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
