@@ -198,7 +198,7 @@ def ddp_train_worker(rank, world, port, result_dir, mode, name, graph, perturb):
         opt.step()
         return loss
 
-    if graph == "split_bf16":
+    if graph in ("split_bf16", "graph_bf16"):  # graph_bf16: the same hook in the one-graph capture
         ddp._set_builtin_hook("bf16_compress")
     g = None
     placements = None
