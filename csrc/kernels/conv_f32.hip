@@ -1142,6 +1142,158 @@ int conv_f32_dgrad_slices(const ConvF32Geom& g) {
   return s;
 }
 
+// ---------------------------------------------------------------- conv3 data gradient, scatter form
+// The ConvNet's conv3 (64 -> 128 channels, 3x3 valid, 10x10 -> 8x8) data gradient as one GEMM per kernel tap
+// over the LIVE positions only: P_t[p][ci] = sum_co dz[co][p] * w[co][ci][t] (p over the 8x8 dz positions),
+// scattered into dx[ci][p + (kh, kw)].  The implicit-GEMM path correlates the zero-padded 12x12 dz against
+// the 10x10 output, and 36 % of its MACs multiply padding (profiles/r05/fp32/).
+// One 256-thread workgroup per CU, persistent over images; wave w owns the 16 input channels
+// [16 w, 16 w + 16) for all 9 taps and all 64 positions, so every A fragment (4 co x 16 positions) read from
+// LDS feeds 9 MFMAs and no two waves write the same dx element.  The weights stay in L2: a lane streams its
+// 9 tap values per k-step (3 x 16 B, repacked once per call into [wave][k-step][lane][12]) two k-steps ahead.
+// col2im: tap by tap (fixed order: deterministic) into a wave-private fp32 LDS image, then stored
+// coalesced - the wave's 16 x 100 outputs are one contiguous NCHW run.  The next image's dz (32 KB) is loaded
+// into registers while this one multiplies and stashed to the other LDS buffer behind the same barrier.
+// Exact fp32 MFMA (v_mfma_f32_16x16x4_f32): results differ from the GEMM path only by summation order.
+constexpr int D3_AS = 80;   // floats per co row of the staged dz image (64 + 16: the 2 k rows of a b32 read
+                            // land 16 banks apart)
+constexpr int D3_XS = 101;  // floats per channel row of a wave's dx image (odd: the 16 channel rows of a
+                            // b32 RMW hit 16 distinct banks)
+constexpr int D3_WP = 4 * 32 * 9 * 64;  // repacked weights (floats): [wave][k-step][tap][lane]
+
+__global__ __launch_bounds__(256) void d3_repack_kernel(const float* __restrict__ w, float* __restrict__ wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= D3_WP) return;
+  const int lane = i & 63, t = (i >> 6) % 9, ks = (i / 576) & 31, ct = i / 18432;
+  const int co = ks * 4 + (lane >> 4), ci = ct * 16 + (lane & 15);
+  wp[i] = w[(co * 64 + ci) * 9 + t];
+}
+
+__global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __restrict__ dz,
+                                                                  const float* __restrict__ wp,
+                                                                  float* __restrict__ dx, int B) {
+  __shared__ __attribute__((aligned(16))) float A[2][128 * D3_AS];   // 80 KB
+  __shared__ __attribute__((aligned(16))) float X[4][16 * D3_XS];   // 25.9 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const float* wl = wp + wave * 32 * 576 + lane;  // + (k-step * 9 + tap) * 64
+  float* xw = X[wave];
+  // this thread's 8 float4 of an image's dz (2048 float4: co = e / 16, column 4 (e % 16))
+  auto load_img = [&](int b, float4 (&r)[8]) {
+    const float4* src = reinterpret_cast<const float4*>(dz + (int64_t)b * 8192);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = src[tid + 256 * u];
+  };
+  auto stash_img = [&](float* buf, const float4 (&r)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u;
+      *reinterpret_cast<float4*>(buf + (e >> 4) * D3_AS + (e & 15) * 4) = r[u];
+    }
+  };
+  float4 nxt[8];
+  int b = blockIdx.x;
+  if (b < B) {
+    load_img(b, nxt);
+    stash_img(A[0], nxt);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; b < B; b += gridDim.x) {
+    const int nb = b + gridDim.x;
+    if (nb < B) load_img(nb, nxt);
+    const float* a_img = A[cur];
+    f32x4 acc[9][4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][i] = dev::zero_f32x4();
+    // weights: two register sets, each reloaded right after its MFMAs were issued, for the k-step two ahead
+    // (one coalesced 256-B dword load per tap, straight into the registers the MFMAs read).  The reloads are
+    // unconditional (the last two read past this wave's k-steps: the next wave's, or the buffer's pad) and
+    // pinned behind their k-step's MFMAs (sched_barrier), so each wait covers only the set about to be used
+    // and every load has a whole k-step (36 MFMAs, ~1150 cycles) to arrive.
+    float wa[9], wb[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      wa[t] = wl[t * 64];
+      wb[t] = wl[(9 + t) * 64];
+    }
+    auto kstep = [&](int ks, const float (&wt)[9]) {
+      float a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = a_img[(ks * 4 + lk) * D3_AS + 16 * i + lr];
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)  // rows: positions 16 i + (lane & 15); columns: channels
+          acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], wt[t], acc[t][i], 0, 0, 0);
+    };
+#pragma unroll 1
+    for (int ks = 0; ks < 32; ks += 2) {
+      kstep(ks, wa);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wa[t] = wl[((ks + 2) * 9 + t) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+      kstep(ks + 1, wb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wb[t] = wl[((ks + 3) * 9 + t) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // col2im into the wave's dx image: lane holds P_t[p = 16 i + 4 lk + r][ci = lr]
+    for (int e = lane; e < 16 * D3_XS; e += 64) xw[e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * i + 4 * lk + r;
+          v[4 * i + r] = xw[lr * D3_XS + ((p >> 3) + kh) * 10 + (p & 7) + kw];
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int p = 16 * i + 4 * lk + r;
+          xw[lr * D3_XS + ((p >> 3) + kh) * 10 + (p & 7) + kw] = v[4 * i + r] + acc[t][i][r];
+        }
+    }
+    // the wave's 16 channels x 100 positions: one contiguous run of dx
+    float* out = dx + (int64_t)b * 6400 + wave * 1600;
+    for (int e = lane; e < 1600; e += 64) {
+      const int c = e / 100;
+      out[e] = xw[c * D3_XS + (e - 100 * c)];
+    }
+    if (nb < B) stash_img(A[cur ^ 1], nxt);
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+bool conv3_dgrad_f32_scatter_ok(const ConvF32Geom& g) {
+  static const bool on = [] {
+    const char* v = std::getenv("RINGDP_F32_DGRAD_SCATTER");
+    return !(v && v[0] == '0');
+  }();
+  // the persistent one-image-per-workgroup form needs images for every CU; small batches keep split K
+  return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
+         g.B >= 2 * f32_num_cus() && g.B * 8192 < (int64_t{1} << 31);
+}
+
+void conv3_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
+                             hipStream_t s) {
+  hipLaunchKernelGGL(d3_repack_kernel, dim3((D3_WP + 255) / 256), dim3(256), 0, s, w, wp);
+  const int grid = static_cast<int>(std::min<int64_t>(g.B, f32_num_cus()));
+  hipLaunchKernelGGL(conv3_dgrad_f32_kernel, dim3(grid), dim3(256), 0, s, dz, wp, dx, static_cast<int>(g.B));
+}
+
+int conv3_dgrad_f32_scratch() { return D3_WP + 2 * 576; }  // + the prefetch pad
+
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* slab, int slices,
                     hipStream_t s) {
   const int K = g.Kout * g.R * g.R;

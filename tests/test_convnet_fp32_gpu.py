@@ -274,3 +274,19 @@ def test_convergence_200_steps_fp32_and_bf16():
     print(f"max |loss - aten fp32| over {steps} steps: fp32 {d32:.2e}, bf16 {d16:.2e}")
     assert d32 < 1e-3, d32  # measured 1.9e-4
     assert d16 < 5e-3, d16  # bf16 activations/weights, fp32 accumulation and masters (measured 3.7e-4)
+
+
+@pytest.mark.parametrize("B", [600, 1024])
+def test_conv3_dgrad_f32_scatter(B):
+    """conv3's data gradient over the live taps only (scatter form, csrc/kernels/conv_f32.hip
+    conv3_dgrad_f32_kernel: batches of at least 2 images per CU) against fp64, against the implicit-GEMM
+    path that 100-image batches take (same values up to summation order), and bit-identical across runs."""
+    g = torch.Generator(device=DEV).manual_seed(B)
+    w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.1
+    dz = torch.randn(B, 128, 8, 8, device=DEV, generator=g)
+    dx = C.f32_conv_dgrad(dz, w, 10, 10, 0)
+    ref = torch.nn.grad.conv2d_input((B, 64, 10, 10), w.double(), dz.double()).float()
+    _close(dx, ref)
+    assert torch.equal(dx, C.f32_conv_dgrad(dz, w, 10, 10, 0))
+    small = C.f32_conv_dgrad(dz[:100].contiguous(), w, 10, 10, 0)  # the split-K implicit GEMM
+    _close(small, dx[:100], rtol=1e-5, atol=1e-5)
