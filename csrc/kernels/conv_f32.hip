@@ -1242,10 +1242,14 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
       for (int t = 0; t < 9; ++t) wb[t] = wl[((ks + 3) * 9 + t) * 64];
       __builtin_amdgcn_sched_barrier(0);
     }
-    // col2im into the wave's dx image: lane holds P_t[p = 16 i + 4 lk + r][ci = lr]
+    // col2im into the wave's dx image: lane holds P_t[p = 16 i + 4 lk + r][ci = lr].  Lanes share
+    // destinations across taps (the x = 4, 5 columns of lanes with lk even and odd), which the compiler's
+    // per-thread alias analysis cannot see: a memory clobber between the phases keeps the wave's LDS
+    // operations in program order (one wave's LDS operations then complete in order).
     for (int e = lane; e < 16 * D3_XS; e += 64) xw[e] = 0.f;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
+      asm volatile("" ::: "memory");
       const int kh = t / 3, kw = t % 3;
       float v[16];
 #pragma unroll
@@ -1263,12 +1267,14 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
           xw[lr * D3_XS + ((p >> 3) + kh) * 10 + (p & 7) + kw] = v[4 * i + r] + acc[t][i][r];
         }
     }
+    asm volatile("" ::: "memory");
     // the wave's 16 channels x 100 positions: one contiguous run of dx
     float* out = dx + (int64_t)b * 6400 + wave * 1600;
     for (int e = lane; e < 1600; e += 64) {
       const int c = e / 100;
       out[e] = xw[c * D3_XS + (e - 100 * c)];
     }
+    asm volatile("" ::: "memory");
     if (nb < B) stash_img(A[cur ^ 1], nxt);
     __syncthreads();
     cur ^= 1;
