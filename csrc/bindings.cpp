@@ -620,22 +620,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("std"), py::arg("dw1"), py::arg("db1"),
         "ConvNet conv1 weight + bias gradient at fp32 from the pooled gradient (pool backward folded in)");
   m.def("f32_conv_dgrad", &ops::f32_conv_dgrad);
-  m.def("f32_conv3_scatter_ok", [](int64_t B) {
-    kern::ConvF32Geom g;
-    g.B = B;
-    g.Kout = 128;
-    g.C = 64;
-    g.R = 3;
-    g.H = g.W = 10;
-    g.pad = 0;
-    g.OH = g.OW = 8;
-    return kern::conv3_dgrad_f32_scatter_ok(g);
-  });
-  m.def("f32_conv3_dgrad_pool2", [](const at::Tensor& dz3, const at::Tensor& w3, const at::Tensor& code2) -> py::object {
-    at::Tensor r = ops::f32_conv3_dgrad_pool2(dz3, w3, code2);
-    if (!r.defined()) return py::none();
-    return py::cast(r);
-  });
   m.def("f32_conv_wgrad", &ops::f32_conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("pad"), py::arg("mean"),
         py::arg("std"), py::arg("dw"), py::arg("db"));
   m.def("f32_pool_relu_fwd", &ops::f32_pool_relu_fwd);

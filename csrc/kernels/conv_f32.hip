@@ -1169,17 +1169,11 @@ __global__ __launch_bounds__(256) void d3_repack_kernel(const float* __restrict_
   wp[i] = w[(co * 64 + ci) * 9 + t];
 }
 
-// POOL: the output is conv2's pre-pool gradient instead - the overlapping 2x2/s1 max-pool + ReLU backward of
-// pool2 (pool2s1_bwd_kernel's gather, same fixed order) applied to the wave's dx image in LDS, with the image's
-// pool2 codes staged next to its dz: out = dz2 [B, 64, 11, 11], and dx never reaches memory.
-template <bool POOL>
 __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __restrict__ dz,
                                                                   const float* __restrict__ wp,
-                                                                  float* __restrict__ dx,
-                                                                  const unsigned char* __restrict__ code2, int B) {
+                                                                  float* __restrict__ dx, int B) {
   __shared__ __attribute__((aligned(16))) float A[2][128 * D3_AS];   // 80 KB
   __shared__ __attribute__((aligned(16))) float X[4][16 * D3_XS];   // 25.9 KB
-  __shared__ __attribute__((aligned(16))) unsigned char CD[POOL ? 2 : 1][POOL ? 6400 : 16];  // pool2 codes
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const float* wl = wp + wave * 32 * 576 + lane;  // + (k-step * 9 + tap) * 64
@@ -1197,37 +1191,17 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
       *reinterpret_cast<float4*>(buf + (e >> 4) * D3_AS + (e & 15) * 4) = r[u];
     }
   };
-  // the image's pool2 codes (6400 B = 400 x 16 B): threads 0..143 carry two 16-B pieces, the rest one
-  auto load_codes = [&](int b, uint4 (&r)[2]) {
-    if constexpr (POOL) {
-      const uint4* src = reinterpret_cast<const uint4*>(code2 + (int64_t)b * 6400);
-      r[0] = src[tid];
-      if (tid < 144) r[1] = src[256 + tid];
-    }
-  };
-  auto stash_codes = [&](unsigned char* buf, const uint4 (&r)[2]) {
-    if constexpr (POOL) {
-      reinterpret_cast<uint4*>(buf)[tid] = r[0];
-      if (tid < 144) reinterpret_cast<uint4*>(buf)[256 + tid] = r[1];
-    }
-  };
   float4 nxt[8];
-  uint4 nxc[2];
   int b = blockIdx.x;
   if (b < B) {
     load_img(b, nxt);
-    load_codes(b, nxc);
     stash_img(A[0], nxt);
-    stash_codes(CD[0], nxc);
   }
   __syncthreads();
   int cur = 0;
   for (; b < B; b += gridDim.x) {
     const int nb = b + gridDim.x;
-    if (nb < B) {
-      load_img(nb, nxt);
-      load_codes(nb, nxc);
-    }
+    if (nb < B) load_img(nb, nxt);
     const float* a_img = A[cur];
     f32x4 acc[9][4];
 #pragma unroll
@@ -1294,35 +1268,14 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
         }
     }
     asm volatile("" ::: "memory");
-    if constexpr (POOL) {
-      // dz2[ci][y][x] = sum over the 4 windows (py, px) = (y - (q >> 1), x - (q & 1)) whose code is q of
-      // dx[ci][py][px], q = 0..3 in order; the wave's 16 channels x 121 positions are one contiguous run
-      const unsigned char* cw = CD[cur & (POOL ? 1 : 0)] + wave * 1600;
-      float* out = dx + (int64_t)b * 7744 + wave * 1936;
-      for (int e = lane; e < 1936; e += 64) {
-        const int c = e / 121, pos = e - 121 * c, y = pos / 11, x = pos - 11 * y;
-        float g = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int py = y - (q >> 1), px = x - (q & 1);
-          if (static_cast<unsigned>(py) < 10u && static_cast<unsigned>(px) < 10u && cw[c * 100 + py * 10 + px] == q)
-            g += xw[c * D3_XS + py * 10 + px];
-        }
-        out[e] = g;
-      }
-    } else {
-      // the wave's 16 channels x 100 positions: one contiguous run of dx
-      float* out = dx + (int64_t)b * 6400 + wave * 1600;
-      for (int e = lane; e < 1600; e += 64) {
-        const int c = e / 100;
-        out[e] = xw[c * D3_XS + (e - 100 * c)];
-      }
+    // the wave's 16 channels x 100 positions: one contiguous run of dx
+    float* out = dx + (int64_t)b * 6400 + wave * 1600;
+    for (int e = lane; e < 1600; e += 64) {
+      const int c = e / 100;
+      out[e] = xw[c * D3_XS + (e - 100 * c)];
     }
     asm volatile("" ::: "memory");
-    if (nb < B) {
-      stash_img(A[cur ^ 1], nxt);
-      stash_codes(CD[(cur ^ 1) & (POOL ? 1 : 0)], nxc);
-    }
+    if (nb < B) stash_img(A[cur ^ 1], nxt);
     __syncthreads();
     cur ^= 1;
   }
@@ -1339,15 +1292,10 @@ bool conv3_dgrad_f32_scatter_ok(const ConvF32Geom& g) {
 }
 
 void conv3_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
-                             hipStream_t s, const unsigned char* code2) {
+                             hipStream_t s) {
   hipLaunchKernelGGL(d3_repack_kernel, dim3((D3_WP + 255) / 256), dim3(256), 0, s, w, wp);
   const int grid = static_cast<int>(std::min<int64_t>(g.B, f32_num_cus()));
-  if (code2)
-    hipLaunchKernelGGL(conv3_dgrad_f32_kernel<true>, dim3(grid), dim3(256), 0, s, dz, wp, dx, code2,
-                       static_cast<int>(g.B));
-  else
-    hipLaunchKernelGGL(conv3_dgrad_f32_kernel<false>, dim3(grid), dim3(256), 0, s, dz, wp, dx, code2,
-                       static_cast<int>(g.B));
+  hipLaunchKernelGGL(conv3_dgrad_f32_kernel, dim3(grid), dim3(256), 0, s, dz, wp, dx, static_cast<int>(g.B));
 }
 
 int conv3_dgrad_f32_scratch() { return D3_WP + 2 * 576; }  // + the prefetch pad

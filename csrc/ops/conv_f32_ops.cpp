@@ -180,30 +180,6 @@ at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, 
   return dx;
 }
 
-at::Tensor f32_conv3_dgrad_pool2(const at::Tensor& dz3, const at::Tensor& w3, const at::Tensor& code2) {
-  util::f32_gpu(dz3, "conv3 dz");
-  util::f32_gpu(w3, "conv3 weight");
-  RINGDP_CHECK(code2.is_cuda() && code2.scalar_type() == at::kByte && code2.is_contiguous(), "pool2 codes: uint8 GPU");
-  kern::ConvF32Geom g;
-  g.B = dz3.size(0);
-  g.Kout = static_cast<int>(w3.size(0));
-  g.C = static_cast<int>(w3.size(1));
-  g.R = static_cast<int>(w3.size(2));
-  g.H = g.W = 10;
-  g.pad = 0;
-  g.OH = g.OW = 8;
-  if (!kern::conv3_dgrad_f32_scatter_ok(g) || !dz3.is_contiguous() || !w3.is_contiguous()) return at::Tensor();
-  RINGDP_CHECK(dz3.dim() == 4 && dz3.size(1) == 128 && dz3.size(2) == 8 && dz3.size(3) == 8, "conv3 dz: shape ",
-               dz3.sizes());
-  RINGDP_CHECK(code2.dim() == 4 && code2.size(0) == g.B && code2.size(1) == 64 && code2.size(2) == 10 &&
-                   code2.size(3) == 10, "pool2 codes: shape ", code2.sizes());
-  auto dz2 = at::empty({g.B, 64, 11, 11}, dz3.options());
-  at::Tensor wp = at::empty({kern::conv3_dgrad_f32_scratch()}, w3.options());
-  kern::conv3_dgrad_f32_scatter(g, dz3.data_ptr<float>(), w3.data_ptr<float>(), dz2.data_ptr<float>(),
-                                wp.data_ptr<float>(), util::stream_of(dz3), code2.data_ptr<uint8_t>());
-  return dz2;
-}
-
 void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
                     at::Tensor& dw, const c10::optional<at::Tensor>& db) {
   check_input(x);

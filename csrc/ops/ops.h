@@ -126,9 +126,6 @@ std::tuple<at::Tensor, at::Tensor> f32_conv1_pool_fwd(const at::Tensor& x, const
 void f32_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tensor& code1, double mean, double std,
                      at::Tensor& dw1, at::Tensor& db1);
 at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad);
-// conv3's data gradient with pool2's 2x2/s1 backward fused: conv2's pre-pool gradient [B, 64, 11, 11], or an
-// undefined tensor when the fused kernel does not apply (shape, batch)
-at::Tensor f32_conv3_dgrad_pool2(const at::Tensor& dz3, const at::Tensor& w3, const at::Tensor& code2);
 void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
                     at::Tensor& dw, const c10::optional<at::Tensor>& db);
 std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_t k, int64_t stride);

@@ -81,50 +81,6 @@ class _ConvPoolF32(torch.autograd.Function):
                 db if (b is not None and ctx.needs_input_grad[2]) else None, None, None, None, None)
 
 
-class _Conv23PoolF32(torch.autograd.Function):
-    """conv2 + ReLU + pool2 (2x2/s1) and conv3 + ReLU + pool3 (2x2/s2) as one node: the forward is the two fused
-    conv+pool launches; the backward forms conv2's pre-pool gradient inside conv3's data-gradient kernel (the
-    scatter kernel applies pool2's backward to its LDS image, csrc/kernels/conv_f32.hip), so conv3's input
-    gradient never reaches memory and the pool2 backward pass is gone.  Used where that kernel applies (the
-    ConvNet's shapes, >= 2 images per CU); otherwise the per-layer nodes."""
-
-    @staticmethod
-    def forward(ctx, a1, w2, b2, w3, b3):
-        a2, code2 = C.f32_conv_pool_fwd(a1, w2, b2, 0, 0.0, 1.0, 1)
-        a3, code3 = C.f32_conv_pool_fwd(a2, w3, b3, 0, 0.0, 1.0, 2)
-        ctx.save_for_backward(a1, a2, code2, code3)
-        ctx.params = (w2, b2, w3, b3)
-        ctx.mark_non_differentiable(code2, code3)
-        return a3
-
-    @staticmethod
-    def backward(ctx, da3):
-        a1, a2, code2, code3 = ctx.saved_tensors
-        w2, b2, w3, b3 = ctx.params
-        n = ctx.needs_input_grad
-        dz3 = C.f32_pool_relu_bwd(da3.contiguous(), code3, 8, 8, 2, 2)
-        dz2 = C.f32_conv3_dgrad_pool2(dz3, w3, code2)
-        if dz2 is None:  # (checked at forward time; kept as a guard) the unfused pair
-            dz2 = C.f32_pool_relu_bwd(C.f32_conv_dgrad(dz3, w3, 10, 10, 0), code2, 11, 11, 2, 1)
-        dw3, db3 = grad_buffer(w3), grad_buffer(b3)
-        C.f32_conv_wgrad(dz3, a2, 0, 0.0, 1.0, dw3, db3)
-        da1 = C.f32_conv_dgrad(dz2, w2, 13, 13, 0) if n[0] else None
-        dw2, db2 = grad_buffer(w2), grad_buffer(b2)
-        C.f32_conv_wgrad(dz2, a1, 0, 0.0, 1.0, dw2, db2)
-        return (da1, dw2 if n[1] else None, db2 if n[2] else None, dw3 if n[3] else None,
-                db3 if n[4] else None)
-
-
-def _fuse23_ok(a1: torch.Tensor, conv2, conv3) -> bool:
-    """The fused conv2 + conv3 node applies: the ConvNet's shapes, biases on both, and a batch the scatter
-    kernel takes (two images per CU; RINGDP_F32_DGRAD_SCATTER=0 disables it)."""
-    if a1.shape[1:] != (32, 13, 13) or conv2.bias is None or conv3.bias is None:
-        return False
-    if tuple(conv2.weight.shape) != (64, 32, 3, 3) or tuple(conv3.weight.shape) != (128, 64, 3, 3):
-        return False
-    return C.f32_conv3_scatter_ok(a1.shape[0])
-
-
 class _Conv1PoolF32(torch.autograd.Function):
     """The ConvNet's conv1 + ReLU + pool1 (csrc/kernels/conv1_f32.hip): one wave per image from an LDS
     copy; backward = the weight / bias gradient straight from the pooled gradient and the code (the
@@ -177,9 +133,6 @@ def convnet_forward_fp32(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Ten
         a = _Conv1PoolF32.apply(x, conv1.weight, conv1.bias, mean, std)
     else:
         a = _ConvPoolF32.apply(x, conv1.weight, conv1.bias, 1, mean, std)
-    if _fuse23_ok(a, conv2, conv3):
-        a = _Conv23PoolF32.apply(a, conv2.weight, conv2.bias, conv3.weight, conv3.bias)
-    else:
-        a = _ConvPoolF32.apply(a, conv2.weight, conv2.bias, 0, 0.0, 1.0, 1)
-        a = _ConvPoolF32.apply(a, conv3.weight, conv3.bias, 0, 0.0, 1.0)
+    a = _ConvPoolF32.apply(a, conv2.weight, conv2.bias, 0, 0.0, 1.0, 1)
+    a = _ConvPoolF32.apply(a, conv3.weight, conv3.bias, 0, 0.0, 1.0)
     return _ConvF32.apply(a.reshape(a.shape[0], -1), fc1.weight, fc1.bias, 0, 0.0, 1.0)

@@ -290,34 +290,3 @@ def test_conv3_dgrad_f32_scatter(B):
     assert torch.equal(dx, C.f32_conv_dgrad(dz, w, 10, 10, 0))
     small = C.f32_conv_dgrad(dz[:100].contiguous(), w, 10, 10, 0)  # the split-K implicit GEMM
     _close(small, dx[:100], rtol=1e-5, atol=1e-5)
-
-
-def test_fp32_convnet_fused_conv23_matches_aten_and_layer_nodes(monkeypatch):
-    """B=600: conv2 + conv3 as one node whose backward forms conv2's pre-pool gradient inside conv3's
-    scatter data-gradient kernel (pool2's backward fused) - against the ATen fp32 model and against the
-    per-layer nodes (RINGDP: _fuse23_ok forced off)."""
-    import ringdp.ops.convnet_fp32 as f32
-
-    B = 600
-    g = torch.Generator(device=DEV).manual_seed(21)
-    x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device=DEV, generator=g)
-    y = torch.randint(0, 10, (B,), device=DEV, generator=g)
-
-    def grads(fused):
-        m32, ref = _models()
-        if not fused:
-            monkeypatch.setattr(f32, "_fuse23_ok", lambda *a: False)
-        out = m32(x)
-        F.cross_entropy(out, y).backward()
-        monkeypatch.undo()
-        return out.detach(), [p.grad.clone() for p in m32.parameters()], ref
-
-    out_f, g_f, ref = grads(True)
-    assert C.f32_conv3_scatter_ok(B)
-    out_l, g_l, _ = grads(False)
-    assert torch.equal(out_f, out_l)  # same forward kernels
-    rout = ref.reference_forward(x)
-    F.cross_entropy(rout, y).backward()
-    for a, b, q in zip(g_f, g_l, ref.parameters()):
-        _close(a, b, rtol=1e-5, atol=1e-6)
-        _close(a, q.grad, rtol=1e-4, atol=1e-6)
