@@ -1281,24 +1281,159 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
   }
 }
 
-bool conv3_dgrad_f32_scatter_ok(const ConvF32Geom& g) {
+// conv2 (32 -> 64 channels, 3x3 valid, 13x13 -> 11x11): its data gradient in the same scatter form.  dz2 has
+// 121 positions (8 tiles of 16, the last 7 rows padding: never scattered); wave w owns input channels
+// [16 (w & 1), +16) for positions [64 (w >> 1), +64), so the two waves of a channel tile write overlapping
+// output rows: each scatters into its own LDS image and the pair is summed in a fixed order on the way out.
+constexpr int D2_XS = 171;                  // floats per channel row of a wave's 13x13 image (odd)
+constexpr int D2_WP = 2 * 16 * 9 * 64;      // repacked weights: [ci tile][k-step][tap][lane]
+
+__global__ __launch_bounds__(256) void d2_repack_kernel(const float* __restrict__ w, float* __restrict__ wp) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= D2_WP) return;
+  const int lane = i & 63, t = (i >> 6) % 9, ks = (i / 576) & 15, ct = i / 9216;
+  const int co = ks * 4 + (lane >> 4), ci = ct * 16 + (lane & 15);
+  wp[i] = w[(co * 32 + ci) * 9 + t];
+}
+
+__global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __restrict__ dz,
+                                                                  const float* __restrict__ wp,
+                                                                  float* __restrict__ dx, int B) {
+  __shared__ __attribute__((aligned(16))) float A[2][64 * 121 + 128];  // 62 KB (+ readable padding rows)
+  __shared__ __attribute__((aligned(16))) float X[4][16 * D2_XS + 32];  // 44.3 KB (+ a dump row per wave)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4, ct = wave & 1, half = wave >> 1;
+  const float* wl = wp + ct * 16 * 576 + lane;  // + (k-step * 9 + tap) * 64
+  float* xw = X[wave];
+  // per (tile i, row r) of this lane: the image offset (channel row included) of its dz position
+  // p = 64 half + 16 i + 4 lk + r; past the 121 real positions the wave's dump row (branch-free col2im)
+  int dst[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p = 64 * half + 16 * i + 4 * lk + r;
+      dst[4 * i + r] = p < 121 ? lr * D2_XS + (p / 11) * 13 + p % 11 : 16 * D2_XS;
+    }
+  // an image of dz is 7744 contiguous floats = 1936 float4: threads take 7 or 8 of them
+  auto load_img = [&](int b, float4 (&r)[8]) {
+    const float4* src = reinterpret_cast<const float4*>(dz + (int64_t)b * 7744);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (tid + 256 * u < 1936) r[u] = src[tid + 256 * u];
+  };
+  auto stash_img = [&](float* buf, const float4 (&r)[8]) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (tid + 256 * u < 1936) reinterpret_cast<float4*>(buf)[tid + 256 * u] = r[u];
+  };
+  float4 nxt[8];
+  int b = blockIdx.x;
+  if (b < B) {
+    load_img(b, nxt);
+    stash_img(A[0], nxt);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; b < B; b += gridDim.x) {
+    const int nb = b + gridDim.x;
+    if (nb < B) load_img(nb, nxt);
+    const float* a_img = A[cur] + 64 * half;
+    f32x4 acc[9][4];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[t][i] = dev::zero_f32x4();
+    float wa[9], wb[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      wa[t] = wl[t * 64];
+      wb[t] = wl[(9 + t) * 64];
+    }
+    // rows of dz: co = 4 ks + lk at 121 floats; positions 16 i + lr of this half (rows 121.. of the last
+    // tile read padding / the next channel: their products are never scattered)
+    auto kstep = [&](int ks, const float (&wt)[9]) {
+      float a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = a_img[(ks * 4 + lk) * 121 + 16 * i + lr];
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[t][i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], wt[t], acc[t][i], 0, 0, 0);
+    };
+#pragma unroll 1
+    for (int ks = 0; ks < 16; ks += 2) {  // as conv3_dgrad_f32_kernel: pinned, unconditional weight reloads
+      kstep(ks, wa);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wa[t] = wl[((ks + 2) * 9 + t) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+      kstep(ks + 1, wb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) wb[t] = wl[((ks + 3) * 9 + t) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // col2im into this wave's image (cross-lane shared destinations: keep program order, see conv3)
+    for (int e = lane; e < 16 * D2_XS; e += 64) xw[e] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      asm volatile("" ::: "memory");
+      const int off = (t / 3) * 13 + t % 3;
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = xw[dst[q] + off];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) xw[dst[q] + off] = v[q] + acc[t][q >> 2][q & 3];
+    }
+    __syncthreads();  // both halves of every channel tile scattered
+    {
+      // channel tile ct, elements [1352 half, +1352) of its 16 x 169 run: half 0's image + half 1's, in order
+      const float* x0 = X[ct];
+      const float* x1 = X[ct + 2];
+      float* out = dx + (int64_t)b * 5408 + ct * 2704;
+      for (int e = 1352 * half + lane; e < 1352 * (half + 1); e += 64) {
+        const int c = e / 169, q = e - 169 * c;
+        out[e] = x0[c * D2_XS + q] + x1[c * D2_XS + q];
+      }
+    }
+    if (nb < B) stash_img(A[cur ^ 1], nxt);
+    __syncthreads();  // images read out, next dz staged
+    cur ^= 1;
+  }
+}
+
+static bool is_conv3_dgrad(const ConvF32Geom& g) {
+  return g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10;
+}
+static bool is_conv2_dgrad(const ConvF32Geom& g) {
+  return g.Kout == 64 && g.C == 32 && g.R == 3 && g.pad == 0 && g.H == 13 && g.W == 13;
+}
+
+bool conv_dgrad_f32_scatter_ok(const ConvF32Geom& g) {
   static const bool on = [] {
     const char* v = std::getenv("RINGDP_F32_DGRAD_SCATTER");
     return !(v && v[0] == '0');
   }();
   // the persistent one-image-per-workgroup form needs images for every CU; small batches keep split K
-  return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
-         g.B >= 2 * f32_num_cus() && g.B * 8192 < (int64_t{1} << 31);
+  return on && (is_conv3_dgrad(g) || is_conv2_dgrad(g)) && g.B >= 2 * f32_num_cus() &&
+         g.B * 8192 < (int64_t{1} << 31);
 }
 
-void conv3_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
-                             hipStream_t s) {
-  hipLaunchKernelGGL(d3_repack_kernel, dim3((D3_WP + 255) / 256), dim3(256), 0, s, w, wp);
+void conv_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
+                            hipStream_t s) {
   const int grid = static_cast<int>(std::min<int64_t>(g.B, f32_num_cus()));
-  hipLaunchKernelGGL(conv3_dgrad_f32_kernel, dim3(grid), dim3(256), 0, s, dz, wp, dx, static_cast<int>(g.B));
+  if (is_conv3_dgrad(g)) {
+    hipLaunchKernelGGL(d3_repack_kernel, dim3((D3_WP + 255) / 256), dim3(256), 0, s, w, wp);
+    hipLaunchKernelGGL(conv3_dgrad_f32_kernel, dim3(grid), dim3(256), 0, s, dz, wp, dx, static_cast<int>(g.B));
+  } else {
+    hipLaunchKernelGGL(d2_repack_kernel, dim3((D2_WP + 255) / 256), dim3(256), 0, s, w, wp);
+    hipLaunchKernelGGL(conv2_dgrad_f32_kernel, dim3(grid), dim3(256), 0, s, dz, wp, dx, static_cast<int>(g.B));
+  }
 }
 
-int conv3_dgrad_f32_scratch() { return D3_WP + 2 * 576; }  // + the prefetch pad
+int conv_dgrad_f32_scratch() { return D3_WP + 2 * 576; }  // the larger repack + the prefetch pad
 
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* slab, int slices,
                     hipStream_t s) {

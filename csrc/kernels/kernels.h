@@ -117,12 +117,13 @@ void conv_f32_fwd_pool_split(const ConvF32Geom& g, const float* x, const float* 
                              int slices, int st, float* a, unsigned char* code, hipStream_t s);
 // slab: conv_f32_dgrad_slices(g) x B*C*H*W floats of split-K partials when that count is > 1 (else unused)
 int conv_f32_dgrad_slices(const ConvF32Geom& g);
-// The ConvNet conv3 data gradient (128 -> 64 channels, 3x3 valid, 8x8 -> 10x10) over the live taps only
-// (scatter form, conv_f32.hip); ok: this geometry and batch; wp: conv3_dgrad_f32_scratch() floats
-bool conv3_dgrad_f32_scatter_ok(const ConvF32Geom& g);
-int conv3_dgrad_f32_scratch();
-void conv3_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
-                             hipStream_t s);
+// The ConvNet's conv3 (128 -> 64 channels, 8x8 -> 10x10) and conv2 (64 -> 32, 11x11 -> 13x13) data gradients
+// over the live taps only (scatter form, conv_f32.hip); ok: one of these geometries and a batch of at least two
+// images per CU; wp: conv_dgrad_f32_scratch() floats
+bool conv_dgrad_f32_scatter_ok(const ConvF32Geom& g);
+int conv_dgrad_f32_scratch();
+void conv_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
+                            hipStream_t s);
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* slab, int slices,
                     hipStream_t s);
 // split-K weight (+ bias, when db != nullptr) gradient; slab: slices * Kout * (C*R*R + 1) floats

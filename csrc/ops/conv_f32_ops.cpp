@@ -166,9 +166,9 @@ at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, 
   RINGDP_CHECK(dz.dim() == 4 && dz.size(1) == g.Kout && dz.size(2) == g.OH && dz.size(3) == g.OW,
                "conv_f32 dgrad: dz has shape ", dz.sizes());
   auto dx = at::empty({g.B, g.C, g.H, g.W}, dz.options());
-  if (kern::conv3_dgrad_f32_scatter_ok(g) && dz.is_contiguous() && w.is_contiguous()) {
-    at::Tensor wp = at::empty({kern::conv3_dgrad_f32_scratch()}, w.options());
-    kern::conv3_dgrad_f32_scatter(g, dz.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(),
+  if (kern::conv_dgrad_f32_scatter_ok(g) && dz.is_contiguous() && w.is_contiguous()) {
+    at::Tensor wp = at::empty({kern::conv_dgrad_f32_scratch()}, w.options());
+    kern::conv_dgrad_f32_scatter(g, dz.data_ptr<float>(), w.data_ptr<float>(), dx.data_ptr<float>(),
                                   wp.data_ptr<float>(), util::stream_of(dz));
     return dx;
   }

@@ -277,16 +277,18 @@ def test_convergence_200_steps_fp32_and_bf16():
 
 
 @pytest.mark.parametrize("B", [600, 1024])
-def test_conv3_dgrad_f32_scatter(B):
-    """conv3's data gradient over the live taps only (scatter form, csrc/kernels/conv_f32.hip
-    conv3_dgrad_f32_kernel: batches of at least 2 images per CU) against fp64, against the implicit-GEMM
-    path that 100-image batches take (same values up to summation order), and bit-identical across runs."""
-    g = torch.Generator(device=DEV).manual_seed(B)
-    w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.1
-    dz = torch.randn(B, 128, 8, 8, device=DEV, generator=g)
-    dx = C.f32_conv_dgrad(dz, w, 10, 10, 0)
-    ref = torch.nn.grad.conv2d_input((B, 64, 10, 10), w.double(), dz.double()).float()
+@pytest.mark.parametrize("Cin,H,K", [(64, 10, 128), (32, 13, 64)])
+def test_conv_dgrad_f32_scatter(B, Cin, H, K):
+    """conv3's and conv2's data gradients over the live taps only (scatter form, csrc/kernels/conv_f32.hip
+    conv3_dgrad_f32_kernel / conv2_dgrad_f32_kernel: batches of at least 2 images per CU) against fp64,
+    against the implicit-GEMM path that 100-image batches take (same values up to summation order), and
+    bit-identical across runs."""
+    g = torch.Generator(device=DEV).manual_seed(B + K)
+    w = torch.randn(K, Cin, 3, 3, device=DEV, generator=g) * 0.1
+    dz = torch.randn(B, K, H - 2, H - 2, device=DEV, generator=g)
+    dx = C.f32_conv_dgrad(dz, w, H, H, 0)
+    ref = torch.nn.grad.conv2d_input((B, Cin, H, H), w.double(), dz.double()).float()
     _close(dx, ref)
-    assert torch.equal(dx, C.f32_conv_dgrad(dz, w, 10, 10, 0))
-    small = C.f32_conv_dgrad(dz[:100].contiguous(), w, 10, 10, 0)  # the split-K implicit GEMM
+    assert torch.equal(dx, C.f32_conv_dgrad(dz, w, H, H, 0))
+    small = C.f32_conv_dgrad(dz[:100].contiguous(), w, H, H, 0)  # the split-K implicit GEMM
     _close(small, dx[:100], rtol=1e-5, atol=1e-5)
