@@ -1153,7 +1153,9 @@ int conv_f32_dgrad_slices(const ConvF32Geom& g) {
 // 9 tap values per k-step (3 x 16 B, repacked once per call into [wave][k-step][lane][12]) two k-steps ahead.
 // col2im: tap by tap (fixed order: deterministic) into a wave-private fp32 LDS image, then stored
 // coalesced - the wave's 16 x 100 outputs are one contiguous NCHW run.  The next image's dz (32 KB) is loaded
-// into registers during the col2im and stashed to the other LDS buffer behind the same barrier.
+// into registers while this one multiplies and stashed to the other LDS buffer behind the same barrier (loads
+// are counted in order, so the first weight wait also waits for that HBM round trip; issued after the k-loop
+// instead, the stash waited for it: 5.9 -> 6.6 ms at B=65536).
 // Exact fp32 MFMA (v_mfma_f32_16x16x4_f32): results differ from the GEMM path only by summation order.
 constexpr int D3_AS = 80;   // floats per co row of the staged dz image (64 + 16: the 2 k rows of a b32 read
                             // land 16 banks apart)
@@ -1201,6 +1203,7 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
   int cur = 0;
   for (; b < B; b += gridDim.x) {
     const int nb = b + gridDim.x;
+    if (nb < B) load_img(nb, nxt);
     const float* a_img = A[cur];
     f32x4 acc[9][4];
 #pragma unroll
@@ -1241,10 +1244,6 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
       for (int t = 0; t < 9; ++t) wb[t] = wl[((ks + 3) * 9 + t) * 64];
       __builtin_amdgcn_sched_barrier(0);
     }
-    // the next image's dz, issued only now: loads are counted in order (vmcnt), so a prefetch issued before
-    // the k-loop made the first weight wait also wait for its HBM round trip; from here it has the col2im and
-    // the store-out to arrive
-    if (nb < B) load_img(nb, nxt);
     // col2im into the wave's dx image: lane holds P_t[p = 16 i + 4 lk + r][ci = lr].  Lanes share
     // destinations across taps (the x = 4, 5 columns of lanes with lk even and odd), which the compiler's
     // per-thread alias analysis cannot see: a memory clobber between the phases keeps the wave's LDS
@@ -1377,7 +1376,7 @@ __global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __
       for (int t = 0; t < 9; ++t) wb[t] = wl[((ks + 3) * 9 + t) * 64];
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (nb < B) load_img(nb, nxt);  // the next image's dz: after the k-loop (see conv3_dgrad_f32_kernel)
+    if (nb < B) load_img(nb, nxt);  // the next image's dz after the k-loop here (4.39 -> 4.31 ms; conv3: slower)
     // col2im into this wave's image (cross-lane shared destinations: keep program order, see conv3)
     for (int e = lane; e < 16 * D2_XS; e += 64) xw[e] = 0.f;
 #pragma unroll
