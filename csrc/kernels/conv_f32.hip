@@ -983,7 +983,11 @@ __global__ __launch_bounds__(256) void linear_row_f32_kernel(const float* __rest
 
 }  // namespace
 
+bool conv3_wgrad_f32_ok(const ConvF32Geom& g);  // (below, with its kernel)
+constexpr int W3_SLICES = 64;                     // its image slices (slab rows)
+
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
+  if (conv3_wgrad_f32_ok(g)) return W3_SLICES + (W3_SLICES + kSlabGroup - 1) / kSlabGroup;
   const int64_t chunk = wgrad_chunk(g);
   const int64_t nchunks = (g.B + chunk - 1) / chunk;
   const int slices = static_cast<int>(nchunks) *
@@ -1406,6 +1410,128 @@ __global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __
   }
 }
 
+// ---------------------------------------------------------------- conv3 weight gradient
+// dW3[co][ci][t] = sum over images b and the 8x8 positions p of dz3[b][co][p] * a2[b][ci][p + t] (+ the bias
+// gradient db3[co] = sum dz3): a dedicated kernel instead of the implicit GEMM's per-element gathers.  Workgroup
+// (ct, slice) owns input channels [16 ct, +16) and images [B slice / S, B (slice + 1) / S); wave w owns output
+// channels [32 w, +32) x 16 channels x 9 taps (18 MFMA tiles).  Per image both operands come from LDS with
+// compile-time offsets: dz3 staged transposed (positions x co, so a 16-co A fragment is one conflict-free
+// row read) and the 16-channel a2 tile (the tap shift is an immediate).  The bias sums ride in the staging
+// (ct = 0 workgroups, VALU).  Each workgroup writes its slice's partial dW into slab[slice][co][ci 9 + t]
+// (+ the bias column), reduced by the same fixed-order f32_slab_reduce as the GEMM path: deterministic.
+constexpr int W3_DS = 144;  // floats per position row of the transposed dz3 (128 co + 16: 16 banks apart)
+constexpr int W3_AS = 101;  // floats per channel row of the a2 tile (odd)
+
+__global__ __launch_bounds__(256, 1) void conv3_wgrad_f32_kernel(const float* __restrict__ dz,
+                                                                  const float* __restrict__ a2,
+                                                                  float* __restrict__ slab, int B) {
+  __shared__ __attribute__((aligned(16))) float DZ[2][64 * W3_DS];  // 73.7 KB
+  __shared__ __attribute__((aligned(16))) float AX[2][16 * W3_AS];  // 12.9 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int ct = blockIdx.x & 3, slice = blockIdx.x >> 2;
+  const int b0 = static_cast<int>((int64_t)B * slice / W3_SLICES), b1 = static_cast<int>((int64_t)B * (slice + 1) / W3_SLICES);
+  const bool bias = ct == 0;
+  // staging: dz3 = 2048 float4 (co = e >> 4, positions 4 (e & 15) ..), 8 per thread; the a2 tile = 400 float4
+  // (channel 4 e / 100, never crossing a row), 1-2 per thread
+  auto load = [&](int b, float4 (&rz)[8], float4 (&ra)[2]) {
+    const float4* z4 = reinterpret_cast<const float4*>(dz + (int64_t)b * 8192);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) rz[u] = z4[tid + 256 * u];
+    const float4* a4 = reinterpret_cast<const float4*>(a2 + (int64_t)b * 6400 + ct * 1600);
+    ra[0] = a4[tid];
+    if (tid < 144) ra[1] = a4[256 + tid];
+  };
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bias partials of co (tid >> 4) + 16 u
+  auto stash = [&](int buf, const float4 (&rz)[8], const float4 (&ra)[2]) {
+    float* d = DZ[buf];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, co = e >> 4, p = (e & 15) * 4;
+      d[(p + 0) * W3_DS + co] = rz[u].x;
+      d[(p + 1) * W3_DS + co] = rz[u].y;
+      d[(p + 2) * W3_DS + co] = rz[u].z;
+      d[(p + 3) * W3_DS + co] = rz[u].w;
+      if (bias) bsum[u] += (rz[u].x + rz[u].y) + (rz[u].z + rz[u].w);
+    }
+    float* x = AX[buf];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = tid + 256 * u;
+      if (u == 0 || tid < 144) {
+        const int c = (4 * e) / 100, q = 4 * e - 100 * c;
+        x[c * W3_AS + q + 0] = ra[u].x;
+        x[c * W3_AS + q + 1] = ra[u].y;
+        x[c * W3_AS + q + 2] = ra[u].z;
+        x[c * W3_AS + q + 3] = ra[u].w;
+      }
+    }
+  };
+  f32x4 acc[2][9];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[j][t] = dev::zero_f32x4();
+  float4 rz[8], ra[2];
+  if (b0 < b1) {
+    load(b0, rz, ra);
+    stash(0, rz, ra);
+  }
+  __syncthreads();
+  int cur = 0;
+  const int abase = lk * W3_DS + 32 * wave + lr;  // A: position 4 ks + lk, output channel 32 w + 16 j + lr
+  const int xbase = lr * W3_AS + lk;              // B: channel lr, position (ks >> 1, 4 (ks & 1) + lk) + tap
+  for (int b = b0; b < b1; ++b) {
+    if (b + 1 < b1) load(b + 1, rz, ra);
+    const float* d = DZ[cur];
+    const float* x = AX[cur];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      float a[2], w[9];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) a[j] = d[abase + 4 * ks * W3_DS + 16 * j];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) w[t] = x[xbase + ((ks >> 1) + t / 3) * 10 + 4 * (ks & 1) + t % 3];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], w[t], acc[j][t], 0, 0, 0);
+    }
+    if (b + 1 < b1) stash(cur ^ 1, rz, ra);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // partial dW of this slice: lane holds D[co = 32 w + 16 j + 4 lk + r][ci = 16 ct + lr] per tap
+  constexpr int NCOL = 64 * 9 + 1;
+  float* out = slab + (int64_t)slice * 128 * NCOL;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 32 * wave + 16 * j + 4 * lk + r;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) out[co * NCOL + (16 * ct + lr) * 9 + t] = acc[j][t][r];
+    }
+  if (bias) {  // the 16 threads sharing co (tid >> 4) + 16 u hold the 4-position partials of all 64 positions
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float v = bsum[u];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+      if ((tid & 15) == 0) out[((tid >> 4) + 16 * u) * NCOL + 576] = v;
+    }
+  }
+}
+
+bool conv3_wgrad_f32_ok(const ConvF32Geom& g) {
+  static const bool on = [] {
+    const char* v = std::getenv("RINGDP_F32_WGRAD3");
+    return !(v && v[0] == '0');
+  }();
+  return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
+         g.B >= 16 * W3_SLICES && g.B * 8192 < (int64_t{1} << 31);
+}
+
 static bool is_conv3_dgrad(const ConvF32Geom& g) {
   return g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10;
 }
@@ -1472,6 +1598,12 @@ void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const
                     float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s) {
   const int Nw = g.C * g.R * g.R;
   const int ncol = Nw + (db ? 1 : 0);
+  if (!xu8 && db && conv3_wgrad_f32_ok(g)) {  // the ConvNet's conv3 at large batches: the dedicated kernel
+    hipLaunchKernelGGL(conv3_wgrad_f32_kernel, dim3(4 * W3_SLICES), dim3(256), 0, s, dz, x, slab,
+                       static_cast<int>(g.B));
+    f32_slab_reduce(slab, W3_SLICES, g.Kout, Nw, ncol, dw, db, s);
+    return;
+  }
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
   const int64_t chunk = wgrad_chunk(g);
   const int ohw = g.OH * g.OW;

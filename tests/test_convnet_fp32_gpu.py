@@ -292,3 +292,23 @@ def test_conv_dgrad_f32_scatter(B, Cin, H, K):
     assert torch.equal(dx, C.f32_conv_dgrad(dz, w, H, H, 0))
     small = C.f32_conv_dgrad(dz[:100].contiguous(), w, H, H, 0)  # the split-K implicit GEMM
     _close(small, dx[:100], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B", [1024, 1500])
+def test_conv3_wgrad_f32_dedicated(B):
+    """conv3's weight + bias gradient on the dedicated kernel (csrc/kernels/conv_f32.hip conv3_wgrad_f32_kernel:
+    64 image slices x 4 channel tiles, slab + fixed-order reduction) against fp64 and bit-identical across runs."""
+    g = torch.Generator(device=DEV).manual_seed(B + 3)
+    x = torch.randn(B, 64, 10, 10, device=DEV, generator=g)
+    w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.1
+    dz = torch.randn(B, 128, 8, 8, device=DEV, generator=g)
+    dw, db = torch.empty_like(w), torch.empty(128, device=DEV)
+    C.f32_conv_wgrad(dz, x, 0, 0.0, 1.0, dw, db)
+    xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
+    br = torch.zeros(128, device=DEV, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr, br).backward(dz.double())
+    _close(dw, wr.grad.float(), rtol=2e-5)
+    _close(db, br.grad.float(), rtol=2e-5)
+    dw2, db2 = torch.empty_like(w), torch.empty(128, device=DEV)
+    C.f32_conv_wgrad(dz, x, 0, 0.0, 1.0, dw2, db2)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
