@@ -1059,8 +1059,114 @@ void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char
   }
 }
 
+// ---------------------------------------------------------------- conv2 + ReLU + pool2 forward (fp32)
+// The ConvNet's conv2 (32 -> 64 channels, 3x3 valid, 13x13 -> 11x11) with bias, ReLU and the overlapping 2x2/s1
+// max-pool (+ its argmax code, pool2s1_fwd_kernel semantics) as one persistent kernel, two 256-thread
+// workgroups per CU.  Wave w owns output channels [16 w, +16) with its 16 x 288 weights resident in registers
+// (72 per lane); K runs tap-major (k = 32 tap + ci), so an A fragment - 16 positions x 4 input channels of one
+// tap - is one b32 read of the LDS image at a per-lane base + a compile-time offset (no index math in the
+// loop).  The 121 positions are 8 tiles of 16 (the last 7 rows read the image's tail and are never stored).
+// Epilogue: conv + bias to an LDS tile, then pool + ReLU + code, 4 outputs (float4 / 4 code bytes) per thread.
+namespace {
+constexpr int C2F_ZS = 121 + 3;  // floats per channel row of the conv output tile
+
+__global__ __launch_bounds__(256, 1) void conv2_pool_f32_kernel(const float* __restrict__ x,
+                                                                 const float* __restrict__ w,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ a,
+                                                                 unsigned char* __restrict__ code, int B) {
+  __shared__ __attribute__((aligned(16))) float XI[5408 + 128];     // 22.1 KB: the input image (+ tail)
+  __shared__ __attribute__((aligned(16))) float Z[64 * C2F_ZS];     // 31.7 KB: conv + bias
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  // weights: lane holds B[k = 4 ks + lk][co = 16 wave + lr] = w[co][ci = (4 ks + lk) & 31][tap = ks >> 3]
+  float wr[72];
+  {
+    const float* wc = w + (16 * wave + lr) * 288;
+#pragma unroll
+    for (int ks = 0; ks < 72; ++ks) wr[ks] = wc[((4 * ks + lk) & 31) * 9 + (ks >> 3)];
+  }
+  const float bv = bias[16 * wave + lr];
+  // A base per position tile: lane row p = 16 i + lr -> (oy, ox); + the input channel lk
+  int pbase[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = min(16 * i + lr, 120);  // rows past 120: a real pixel, product never stored
+    pbase[i] = lk * 169 + (p / 11) * 13 + p % 11;
+  }
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    // stage the image (5408 floats = 1352 float4)
+    const float4* src = reinterpret_cast<const float4*>(x + (int64_t)b * 5408);
+    for (int e = tid; e < 1352; e += 256) reinterpret_cast<float4*>(XI)[e] = src[e];
+    __syncthreads();
+    f32x4 acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = dev::zero_f32x4();
+#pragma unroll
+    for (int ks = 0; ks < 72; ++ks) {
+      const int tap = ks >> 3, koff = 4 * (ks & 7) * 169 + (tap / 3) * 13 + tap % 3;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(XI[pbase[i] + koff], wr[ks], acc[i], 0, 0, 0);
+    }
+    // lane holds D[p = 16 i + 4 lk + r][co = 16 wave + lr]
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int p = 16 * i + 4 * lk + r;
+        if (p < 121) Z[(16 * wave + lr) * C2F_ZS + p] = acc[i][r] + bv;
+      }
+    __syncthreads();
+    // pool: quads of 4 consecutive outputs of one channel (100 per channel: never crossing a channel)
+    float4* ao = reinterpret_cast<float4*>(a + (int64_t)b * 6400);
+    uint32_t* co = reinterpret_cast<uint32_t*>(code + (int64_t)b * 6400);
+    for (int qd = tid; qd < 1600; qd += 256) {
+      const int ch = qd / 25, q0 = 4 * (qd - 25 * ch);
+      float o[4];
+      uint32_t cw = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = q0 + j, py = q / 10, px = q - 10 * py;
+        const float* t = Z + ch * C2F_ZS + py * 11 + px;
+        const float v0 = t[0], v1 = t[1], v2 = t[11], v3 = t[12];
+        float best = v0;
+        uint32_t arg = 0;
+        if (v1 > best) { best = v1; arg = 1; }
+        if (v2 > best) { best = v2; arg = 2; }
+        if (v3 > best) { best = v3; arg = 3; }
+        const bool live = best > 0.f;
+        o[j] = live ? best : 0.f;
+        cw |= (live ? arg : 255u) << (8 * j);
+      }
+      ao[qd] = make_float4(o[0], o[1], o[2], o[3]);
+      co[qd] = cw;
+    }
+    __syncthreads();  // Z and XI free for the next image
+  }
+}
+}  // namespace
+
+bool conv2_pool_f32_ok(const ConvF32Geom& g) {
+  static const bool on = [] {
+    const char* v = std::getenv("RINGDP_F32_CONV2_FWD");
+    return !(v && v[0] == '0');
+  }();
+  return on && g.Kout == 64 && g.C == 32 && g.R == 3 && g.pad == 0 && g.H == 13 && g.W == 13 &&
+         g.B >= 4 * f32_num_cus() && g.B * 6400 < (int64_t{1} << 31);
+}
+
+void conv2_pool_f32(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* a,
+                    unsigned char* code, hipStream_t s) {
+  const int grid = static_cast<int>(std::min<int64_t>(g.B, 2 * f32_num_cus()));
+  hipLaunchKernelGGL(conv2_pool_f32_kernel, dim3(grid), dim3(256), 0, s, x, w, bias, a, code, static_cast<int>(g.B));
+}
+
 void conv_f32_fwd_pool_s1(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* a,
                           unsigned char* code, hipStream_t s) {
+  if (bias && conv2_pool_f32_ok(g)) {  // the ConvNet's conv2 at large batches: the dedicated kernel
+    conv2_pool_f32(g, x, w, bias, a, code, s);
+    return;
+  }
   const int K = g.C * g.R * g.R;
   const int PH = g.OH - 1, PW = g.OW - 1, phw = PH * PW;
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, aout = static_cast<int64_t>(g.Kout) * phw;

@@ -312,3 +312,27 @@ def test_conv3_wgrad_f32_dedicated(B):
     dw2, db2 = torch.empty_like(w), torch.empty(128, device=DEV)
     C.f32_conv_wgrad(dz, x, 0, 0.0, 1.0, dw2, db2)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("B", [1024, 1100])
+def test_conv2_pool_f32_dedicated(B):
+    """conv2 + bias + ReLU + overlapping 2x2/s1 max-pool on the dedicated forward kernel
+    (csrc/kernels/conv_f32.hip conv2_pool_f32_kernel: batches of >= 4 images per CU) against fp64: pooled
+    values, and the argmax codes wherever the window's maximum is not a near-tie."""
+    g = torch.Generator(device=DEV).manual_seed(B + 5)
+    x = torch.randn(B, 32, 13, 13, device=DEV, generator=g)
+    w = torch.randn(64, 32, 3, 3, device=DEV, generator=g) * 0.1
+    b = torch.randn(64, device=DEV, generator=g) * 0.1
+    a, code = C.f32_conv_pool_fwd(x, w, b, 0, 0.0, 1.0, 1)
+    z = F.conv2d(x.double(), w.double(), b.double())  # [B, 64, 11, 11]
+    win = torch.stack([z[..., :-1, :-1], z[..., :-1, 1:], z[..., 1:, :-1], z[..., 1:, 1:]], -1)
+    best, arg = win.max(-1)
+    ref = best.clamp_min(0).float()
+    _close(a, ref, rtol=1e-5, atol=1e-5)
+    top2 = win.topk(2, -1).values
+    clear = ((top2[..., 0] - top2[..., 1]) > 1e-4 * (1 + top2[..., 0].abs())) & (best > 1e-4)
+    want = torch.where(best > 0, arg, torch.full_like(arg, 255)).to(torch.uint8)
+    assert torch.equal(code[clear], want[clear])
+    assert torch.equal(code[best < -1e-4], want[best < -1e-4])  # dead windows: 255
+    a2, code2 = C.f32_conv_pool_fwd(x, w, b, 0, 0.0, 1.0, 1)
+    assert torch.equal(a, a2) and torch.equal(code, code2)
