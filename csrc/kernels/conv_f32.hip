@@ -984,7 +984,7 @@ __global__ __launch_bounds__(256) void linear_row_f32_kernel(const float* __rest
 }  // namespace
 
 bool conv3_wgrad_f32_ok(const ConvF32Geom& g);  // (below, with its kernel)
-constexpr int W3_SLICES = 64;                     // its image slices (slab rows)
+constexpr int W3_SLICES = 128;                    // its image slices (slab rows): 512 workgroups, 2 per CU
 
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
   if (conv3_wgrad_f32_ok(g)) return W3_SLICES + (W3_SLICES + kSlabGroup - 1) / kSlabGroup;
@@ -1528,11 +1528,12 @@ __global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __
 constexpr int W3_DS = 144;  // floats per position row of the transposed dz3 (128 co + 16: 16 banks apart)
 constexpr int W3_AS = 101;  // floats per channel row of the a2 tile (odd)
 
-__global__ __launch_bounds__(256, 1) void conv3_wgrad_f32_kernel(const float* __restrict__ dz,
+__global__ __launch_bounds__(256, 2) void conv3_wgrad_f32_kernel(const float* __restrict__ dz,
                                                                   const float* __restrict__ a2,
                                                                   float* __restrict__ slab, int B) {
-  __shared__ __attribute__((aligned(16))) float DZ[2][64 * W3_DS];  // 73.7 KB
-  __shared__ __attribute__((aligned(16))) float AX[2][16 * W3_AS];  // 12.9 KB
+  // single-buffered (49.3 KB): two workgroups per CU, so one stages while the other multiplies
+  __shared__ __attribute__((aligned(16))) float DZ[1][64 * W3_DS];  // 36.9 KB
+  __shared__ __attribute__((aligned(16))) float AX[1][16 * W3_AS];  // 6.5 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int ct = blockIdx.x & 3, slice = blockIdx.x >> 2;
@@ -1579,18 +1580,14 @@ __global__ __launch_bounds__(256, 1) void conv3_wgrad_f32_kernel(const float* __
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[j][t] = dev::zero_f32x4();
   float4 rz[8], ra[2];
-  if (b0 < b1) {
-    load(b0, rz, ra);
-    stash(0, rz, ra);
-  }
-  __syncthreads();
-  int cur = 0;
   const int abase = lk * W3_DS + 32 * wave + lr;  // A: position 4 ks + lk, output channel 32 w + 16 j + lr
   const int xbase = lr * W3_AS + lk;              // B: channel lr, position (ks >> 1, 4 (ks & 1) + lk) + tap
   for (int b = b0; b < b1; ++b) {
-    if (b + 1 < b1) load(b + 1, rz, ra);
-    const float* d = DZ[cur];
-    const float* x = AX[cur];
+    load(b, rz, ra);
+    stash(0, rz, ra);
+    __syncthreads();
+    const float* d = DZ[0];
+    const float* x = AX[0];
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       float a[2], w[9];
@@ -1603,9 +1600,7 @@ __global__ __launch_bounds__(256, 1) void conv3_wgrad_f32_kernel(const float* __
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[j][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], w[t], acc[j][t], 0, 0, 0);
     }
-    if (b + 1 < b1) stash(cur ^ 1, rz, ra);
-    __syncthreads();
-    cur ^= 1;
+    __syncthreads();  // the tile is read out before the next image's stash
   }
   // partial dW of this slice: lane holds D[co = 32 w + 16 j + 4 lk + r][ci = 16 ct + lr] per tap
   constexpr int NCOL = 64 * 9 + 1;
@@ -1635,7 +1630,7 @@ bool conv3_wgrad_f32_ok(const ConvF32Geom& g) {
     return !(v && v[0] == '0');
   }();
   return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
-         g.B >= 16 * W3_SLICES && g.B * 8192 < (int64_t{1} << 31);
+         g.B >= 8 * W3_SLICES && g.B * 8192 < (int64_t{1} << 31);
 }
 
 static bool is_conv3_dgrad(const ConvF32Geom& g) {

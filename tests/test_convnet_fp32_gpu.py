@@ -297,7 +297,7 @@ def test_conv_dgrad_f32_scatter(B, Cin, H, K):
 @pytest.mark.parametrize("B", [1024, 1500])
 def test_conv3_wgrad_f32_dedicated(B):
     """conv3's weight + bias gradient on the dedicated kernel (csrc/kernels/conv_f32.hip conv3_wgrad_f32_kernel:
-    64 image slices x 4 channel tiles, slab + fixed-order reduction) against fp64 and bit-identical across runs."""
+    128 image slices x 4 channel tiles, slab + fixed-order reduction) against fp64 and bit-identical across runs."""
     g = torch.Generator(device=DEV).manual_seed(B + 3)
     x = torch.randn(B, 64, 10, 10, device=DEV, generator=g)
     w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.1
