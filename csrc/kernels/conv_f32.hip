@@ -983,11 +983,12 @@ __global__ __launch_bounds__(256) void linear_row_f32_kernel(const float* __rest
 
 }  // namespace
 
-bool conv3_wgrad_f32_ok(const ConvF32Geom& g);  // (below, with its kernel)
+bool conv3_wgrad_f32_ok(const ConvF32Geom& g);  // (below, with their kernels)
+bool conv2_wgrad_f32_ok(const ConvF32Geom& g);
 constexpr int W3_SLICES = 128;                    // its image slices (slab rows): 512 workgroups, 2 per CU
 
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
-  if (conv3_wgrad_f32_ok(g)) return W3_SLICES + (W3_SLICES + kSlabGroup - 1) / kSlabGroup;
+  if (conv3_wgrad_f32_ok(g) || conv2_wgrad_f32_ok(g)) return W3_SLICES + (W3_SLICES + kSlabGroup - 1) / kSlabGroup;
   const int64_t chunk = wgrad_chunk(g);
   const int64_t nchunks = (g.B + chunk - 1) / chunk;
   const int slices = static_cast<int>(nchunks) *
@@ -1070,7 +1071,7 @@ void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char
 namespace {
 constexpr int C2F_ZS = 121 + 3;  // floats per channel row of the conv output tile
 
-__global__ __launch_bounds__(256, 1) void conv2_pool_f32_kernel(const float* __restrict__ x,
+__global__ __launch_bounds__(256, 2) void conv2_pool_f32_kernel(const float* __restrict__ x,
                                                                  const float* __restrict__ w,
                                                                  const float* __restrict__ bias,
                                                                  float* __restrict__ a,
@@ -1102,11 +1103,28 @@ __global__ __launch_bounds__(256, 1) void conv2_pool_f32_kernel(const float* __r
     f32x4 acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = dev::zero_f32x4();
+    // k-step-major with the next k-step's 8 A reads issued ahead of this one's 8 MFMAs (independent
+    // accumulators back to back; left to itself the scheduler ran one position tile's 72 dependent MFMAs
+    // in a row: 4.27 ms at B=65536)
+    auto koff = [](int ks) { const int tap = ks >> 3; return 4 * (ks & 7) * 169 + (tap / 3) * 13 + tap % 3; };
+    float av[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) av[i] = XI[pbase[i] + koff(0)];
 #pragma unroll
     for (int ks = 0; ks < 72; ++ks) {
-      const int tap = ks >> 3, koff = 4 * (ks & 7) * 169 + (tap / 3) * 13 + tap % 3;
+      float an[8];
+      if (ks + 1 < 72) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(XI[pbase[i] + koff], wr[ks], acc[i], 0, 0, 0);
+        for (int i = 0; i < 8; ++i) an[i] = XI[pbase[i] + koff(ks + 1)];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], wr[ks], acc[i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < 72) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) av[i] = an[i];
+      }
     }
     // lane holds D[p = 16 i + 4 lk + r][co = 16 wave + lr]
 #pragma unroll
@@ -1624,13 +1642,117 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_f32_kernel(const float* __
   }
 }
 
-bool conv3_wgrad_f32_ok(const ConvF32Geom& g) {
+// conv2's weight gradient (64 <- 32 channels, 13x13 -> 11x11) the same way: workgroup (ct of 2, slice) owns
+// input channels [16 ct, +16), wave w output channels [16 w, +16) x 16 x 9 taps.  The 121 positions are 31
+// k-steps of 4 (the 3 padding rows of the transposed dz2 tile are zero); a position's 13x13 offset is a
+// per-lane table (the 11-wide rows do not split on k-step boundaries).
+constexpr int W2_DS = 80;   // floats per position row of the transposed dz2 (64 co + 16)
+constexpr int W2_AS = 171;  // floats per channel row of the a1 tile (odd)
+
+__global__ __launch_bounds__(256, 2) void conv2_wgrad_f32_kernel(const float* __restrict__ dz,
+                                                                  const float* __restrict__ a1,
+                                                                  float* __restrict__ slab, int B) {
+  __shared__ __attribute__((aligned(16))) float DZ[124 * W2_DS];  // 38.8 KB
+  __shared__ __attribute__((aligned(16))) float AX[16 * W2_AS];   // 10.9 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int ct = blockIdx.x & 1, slice = blockIdx.x >> 1;
+  const int b0 = static_cast<int>((int64_t)B * slice / W3_SLICES), b1 = static_cast<int>((int64_t)B * (slice + 1) / W3_SLICES);
+  const bool bias = ct == 0;
+  // padding positions 121..123 of the transposed tile: zero once (never written by the staging)
+  for (int e = tid; e < 3 * W2_DS; e += 256) DZ[121 * W2_DS + e] = 0.f;
+  int xoff[31];  // per k-step: the 13x13 offset of this lane's position 4 ks + lk (clamped past 120)
+#pragma unroll
+  for (int ks = 0; ks < 31; ++ks) {
+    const int p = min(4 * ks + lk, 120);
+    xoff[ks] = (p / 11) * 13 + p % 11;
+  }
+  f32x4 acc[9], accb = dev::zero_f32x4();  // accb: the bias sums (ct = 0), one MFMA against ones per k-step
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = dev::zero_f32x4();
+  const int abase = lk * W2_DS + 16 * wave + lr;
+  const int xbase = lr * W2_AS;
+  for (int b = b0; b < b1; ++b) {
+    // dz2 image: 7744 floats = 1936 float4 (a row of 121 does not hold whole float4s: scalar scatter)
+    const float4* z4 = reinterpret_cast<const float4*>(dz + (int64_t)b * 7744);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u;
+      if (e < 1936) {
+        const float4 v = z4[e];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int f = 4 * e + j, co = f / 121, p = f - 121 * co;
+          DZ[p * W2_DS + co] = vv[j];
+        }
+      }
+    }
+    // a1 tile of this channel tile: 16 x 169 = 2704 floats = 676 float4
+    const float4* a4 = reinterpret_cast<const float4*>(a1 + (int64_t)b * 5408 + ct * 2704);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + 256 * u;
+      if (e < 676) {
+        const float4 v = a4[e];
+        const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int f = 4 * e + j, c = f / 169, q = f - 169 * c;
+          AX[c * W2_AS + q] = vv[j];
+        }
+      }
+    }
+    __syncthreads();
+    // one straight k-loop per workgroup kind (a uniform branch outside it, not one per k-step)
+    auto kloop = [&](auto with_bias) {
+#pragma unroll
+      for (int ks = 0; ks < 31; ++ks) {
+        const float a = DZ[abase + 4 * ks * W2_DS];
+        float w[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) w[t] = AX[xbase + xoff[ks] + (t / 3) * 13 + t % 3];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w[t], acc[t], 0, 0, 0);
+        if constexpr (decltype(with_bias)::value) accb = __builtin_amdgcn_mfma_f32_16x16x4f32(a, 1.f, accb, 0, 0, 0);
+      }
+    };
+    if (bias)
+      kloop(std::true_type{});
+    else
+      kloop(std::false_type{});
+    __syncthreads();
+  }
+  constexpr int NCOL = 32 * 9 + 1;
+  float* out = slab + (int64_t)slice * 64 * NCOL;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int co = 16 * wave + 4 * lk + r;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) out[co * NCOL + (16 * ct + lr) * 9 + t] = acc[t][r];
+  }
+  if (bias && lr == 0) {  // every column of accb holds the row sums
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(16 * wave + 4 * lk + r) * NCOL + 288] = accb[r];
+  }
+}
+
+static bool wgrad_dedicated_on() {
   static const bool on = [] {
-    const char* v = std::getenv("RINGDP_F32_WGRAD3");
+    const char* v = std::getenv("RINGDP_F32_WGRAD_DEDICATED");
     return !(v && v[0] == '0');
   }();
-  return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
-         g.B >= 8 * W3_SLICES && g.B * 8192 < (int64_t{1} << 31);
+  return on;
+}
+
+bool conv3_wgrad_f32_ok(const ConvF32Geom& g) {
+  return wgrad_dedicated_on() && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 &&
+         g.W == 10 && g.B >= 8 * W3_SLICES && g.B * 8192 < (int64_t{1} << 31);
+}
+
+bool conv2_wgrad_f32_ok(const ConvF32Geom& g) {
+  return wgrad_dedicated_on() && g.Kout == 64 && g.C == 32 && g.R == 3 && g.pad == 0 && g.H == 13 &&
+         g.W == 13 && g.B >= 8 * W3_SLICES && g.B * 7744 < (int64_t{1} << 31);
 }
 
 static bool is_conv3_dgrad(const ConvF32Geom& g) {
@@ -1699,8 +1821,14 @@ void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const
                     float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s) {
   const int Nw = g.C * g.R * g.R;
   const int ncol = Nw + (db ? 1 : 0);
-  if (!xu8 && db && conv3_wgrad_f32_ok(g)) {  // the ConvNet's conv3 at large batches: the dedicated kernel
+  if (!xu8 && db && conv3_wgrad_f32_ok(g)) {  // the ConvNet's conv3 / conv2 at large batches: dedicated kernels
     hipLaunchKernelGGL(conv3_wgrad_f32_kernel, dim3(4 * W3_SLICES), dim3(256), 0, s, dz, x, slab,
+                       static_cast<int>(g.B));
+    f32_slab_reduce(slab, W3_SLICES, g.Kout, Nw, ncol, dw, db, s);
+    return;
+  }
+  if (!xu8 && db && conv2_wgrad_f32_ok(g)) {
+    hipLaunchKernelGGL(conv2_wgrad_f32_kernel, dim3(2 * W3_SLICES), dim3(256), 0, s, dz, x, slab,
                        static_cast<int>(g.B));
     f32_slab_reduce(slab, W3_SLICES, g.Kout, Nw, ncol, dw, db, s);
     return;

@@ -295,21 +295,23 @@ def test_conv_dgrad_f32_scatter(B, Cin, H, K):
 
 
 @pytest.mark.parametrize("B", [1024, 1500])
-def test_conv3_wgrad_f32_dedicated(B):
-    """conv3's weight + bias gradient on the dedicated kernel (csrc/kernels/conv_f32.hip conv3_wgrad_f32_kernel:
-    128 image slices x 4 channel tiles, slab + fixed-order reduction) against fp64 and bit-identical across runs."""
-    g = torch.Generator(device=DEV).manual_seed(B + 3)
-    x = torch.randn(B, 64, 10, 10, device=DEV, generator=g)
-    w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.1
-    dz = torch.randn(B, 128, 8, 8, device=DEV, generator=g)
-    dw, db = torch.empty_like(w), torch.empty(128, device=DEV)
+@pytest.mark.parametrize("Cin,H,K", [(64, 10, 128), (32, 13, 64)])
+def test_conv_wgrad_f32_dedicated(B, Cin, H, K):
+    """conv3's and conv2's weight + bias gradients on the dedicated kernels (csrc/kernels/conv_f32.hip
+    conv3_wgrad_f32_kernel / conv2_wgrad_f32_kernel: 128 image slices x the 16-channel tiles, slab + fixed-order
+    reduction) against fp64 and bit-identical across runs."""
+    g = torch.Generator(device=DEV).manual_seed(B + K)
+    x = torch.randn(B, Cin, H, H, device=DEV, generator=g)
+    w = torch.randn(K, Cin, 3, 3, device=DEV, generator=g) * 0.1
+    dz = torch.randn(B, K, H - 2, H - 2, device=DEV, generator=g)
+    dw, db = torch.empty_like(w), torch.empty(K, device=DEV)
     C.f32_conv_wgrad(dz, x, 0, 0.0, 1.0, dw, db)
     xr, wr = x.double().requires_grad_(), w.double().requires_grad_()
-    br = torch.zeros(128, device=DEV, dtype=torch.float64, requires_grad=True)
+    br = torch.zeros(K, device=DEV, dtype=torch.float64, requires_grad=True)
     F.conv2d(xr, wr, br).backward(dz.double())
     _close(dw, wr.grad.float(), rtol=2e-5)
     _close(db, br.grad.float(), rtol=2e-5)
-    dw2, db2 = torch.empty_like(w), torch.empty(128, device=DEV)
+    dw2, db2 = torch.empty_like(w), torch.empty(K, device=DEV)
     C.f32_conv_wgrad(dz, x, 0, 0.0, 1.0, dw2, db2)
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
