@@ -986,9 +986,11 @@ __global__ __launch_bounds__(256) void linear_row_f32_kernel(const float* __rest
 bool conv3_wgrad_f32_ok(const ConvF32Geom& g);  // (below, with their kernels)
 bool conv2_wgrad_f32_ok(const ConvF32Geom& g);
 constexpr int W3_SLICES = 128;                    // its image slices (slab rows): 512 workgroups, 2 per CU
+constexpr int W2_SLICES = 256;                    // conv2's (2 channel tiles): 512 workgroups
 
 int conv_f32_wgrad_slices(const ConvF32Geom& g) {
-  if (conv3_wgrad_f32_ok(g) || conv2_wgrad_f32_ok(g)) return W3_SLICES + (W3_SLICES + kSlabGroup - 1) / kSlabGroup;
+  if (conv3_wgrad_f32_ok(g)) return W3_SLICES + (W3_SLICES + kSlabGroup - 1) / kSlabGroup;
+  if (conv2_wgrad_f32_ok(g)) return W2_SLICES + (W2_SLICES + kSlabGroup - 1) / kSlabGroup;
   const int64_t chunk = wgrad_chunk(g);
   const int64_t nchunks = (g.B + chunk - 1) / chunk;
   const int slices = static_cast<int>(nchunks) *
@@ -1644,23 +1646,26 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_f32_kernel(const float* __
 
 // conv2's weight gradient (64 <- 32 channels, 13x13 -> 11x11) the same way: workgroup (ct of 2, slice) owns
 // input channels [16 ct, +16), wave w output channels [16 w, +16) x 16 x 9 taps.  The 121 positions are 31
-// k-steps of 4 (the 3 padding rows of the transposed dz2 tile are zero); a position's 13x13 offset is a
-// per-lane table (the 11-wide rows do not split on k-step boundaries).
-constexpr int W2_DS = 80;   // floats per position row of the transposed dz2 (64 co + 16)
+// k-steps of 4 (positions 121..123 of the dz2 tile are zero); a position's 13x13 offset is a per-lane table
+// (the 11-wide rows do not split on k-step boundaries).  dz2 stays in its natural [co][p] order with a row
+// stride of 2 mod 32 banks, so the A fragment (16 co x 4 positions) is a conflict-free read and the staging
+// writes run along rows.  256 slices (512 workgroups, 2 per CU) and the next image's loads in flight during
+// the k loop: with 256 workgroups and no prefetch the staging was exposed (4.49 ms vs the GEMM's 4.19).
+constexpr int W2_S = 130;   // floats per output-channel row of the dz2 tile (121 + 9; 130 = 2 mod 32)
 constexpr int W2_AS = 171;  // floats per channel row of the a1 tile (odd)
 
 __global__ __launch_bounds__(256, 2) void conv2_wgrad_f32_kernel(const float* __restrict__ dz,
                                                                   const float* __restrict__ a1,
                                                                   float* __restrict__ slab, int B) {
-  __shared__ __attribute__((aligned(16))) float DZ[124 * W2_DS];  // 38.8 KB
-  __shared__ __attribute__((aligned(16))) float AX[16 * W2_AS];   // 10.9 KB
+  __shared__ __attribute__((aligned(16))) float DZ[64 * W2_S];   // 33.3 KB
+  __shared__ __attribute__((aligned(16))) float AX[16 * W2_AS];  // 10.9 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int ct = blockIdx.x & 1, slice = blockIdx.x >> 1;
-  const int b0 = static_cast<int>((int64_t)B * slice / W3_SLICES), b1 = static_cast<int>((int64_t)B * (slice + 1) / W3_SLICES);
+  const int b0 = static_cast<int>((int64_t)B * slice / W2_SLICES), b1 = static_cast<int>((int64_t)B * (slice + 1) / W2_SLICES);
   const bool bias = ct == 0;
-  // padding positions 121..123 of the transposed tile: zero once (never written by the staging)
-  for (int e = tid; e < 3 * W2_DS; e += 256) DZ[121 * W2_DS + e] = 0.f;
+  // padding positions 121..123 of every row: zero once (never written by the staging)
+  for (int e = tid; e < 64 * 3; e += 256) DZ[(e / 3) * W2_S + 121 + e % 3] = 0.f;
   int xoff[31];  // per k-step: the 13x13 offset of this lane's position 4 ks + lk (clamped past 120)
 #pragma unroll
   for (int ks = 0; ks < 31; ++ks) {
@@ -1670,32 +1675,36 @@ __global__ __launch_bounds__(256, 2) void conv2_wgrad_f32_kernel(const float* __
   f32x4 acc[9], accb = dev::zero_f32x4();  // accb: the bias sums (ct = 0), one MFMA against ones per k-step
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = dev::zero_f32x4();
-  const int abase = lk * W2_DS + 16 * wave + lr;
-  const int xbase = lr * W2_AS;
-  for (int b = b0; b < b1; ++b) {
-    // dz2 image: 7744 floats = 1936 float4 (a row of 121 does not hold whole float4s: scalar scatter)
+  // staging registers: dz2 image = 7744 floats = 1936 float4 (8 per thread), a1 tile 16 x 169 = 676 float4 (3)
+  float4 rz[8], ra[3];
+  auto load = [&](int b) {
     const float4* z4 = reinterpret_cast<const float4*>(dz + (int64_t)b * 7744);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (tid + 256 * u < 1936) rz[u] = z4[tid + 256 * u];
+    const float4* a4 = reinterpret_cast<const float4*>(a1 + (int64_t)b * 5408 + ct * 2704);
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (tid + 256 * u < 676) ra[u] = a4[tid + 256 * u];
+  };
+  auto stash = [&]() {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u;
       if (e < 1936) {
-        const float4 v = z4[e];
-        const float vv[4] = {v.x, v.y, v.z, v.w};
+        const float vv[4] = {rz[u].x, rz[u].y, rz[u].z, rz[u].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int f = 4 * e + j, co = f / 121, p = f - 121 * co;
-          DZ[p * W2_DS + co] = vv[j];
+          DZ[co * W2_S + p] = vv[j];
         }
       }
     }
-    // a1 tile of this channel tile: 16 x 169 = 2704 floats = 676 float4
-    const float4* a4 = reinterpret_cast<const float4*>(a1 + (int64_t)b * 5408 + ct * 2704);
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
       const int e = tid + 256 * u;
       if (e < 676) {
-        const float4 v = a4[e];
-        const float vv[4] = {v.x, v.y, v.z, v.w};
+        const float vv[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int f = 4 * e + j, c = f / 169, q = f - 169 * c;
@@ -1703,12 +1712,19 @@ __global__ __launch_bounds__(256, 2) void conv2_wgrad_f32_kernel(const float* __
         }
       }
     }
+  };
+  const int abase = (16 * wave + lr) * W2_S + lk;  // A: output channel 16 w + lr, position 4 ks + lk
+  const int xbase = lr * W2_AS;                    // B: channel lr, position offset xoff[ks] + tap
+  if (b0 < b1) load(b0);
+  for (int b = b0; b < b1; ++b) {
+    stash();
     __syncthreads();
+    if (b + 1 < b1) load(b + 1);  // in flight during the k loop
     // one straight k-loop per workgroup kind (a uniform branch outside it, not one per k-step)
     auto kloop = [&](auto with_bias) {
 #pragma unroll
       for (int ks = 0; ks < 31; ++ks) {
-        const float a = DZ[abase + 4 * ks * W2_DS];
+        const float a = DZ[abase + 4 * ks];
         float w[9];
 #pragma unroll
         for (int t = 0; t < 9; ++t) w[t] = AX[xbase + xoff[ks] + (t / 3) * 13 + t % 3];
@@ -1752,7 +1768,7 @@ bool conv3_wgrad_f32_ok(const ConvF32Geom& g) {
 
 bool conv2_wgrad_f32_ok(const ConvF32Geom& g) {
   return wgrad_dedicated_on() && g.Kout == 64 && g.C == 32 && g.R == 3 && g.pad == 0 && g.H == 13 &&
-         g.W == 13 && g.B >= 8 * W3_SLICES && g.B * 7744 < (int64_t{1} << 31);
+         g.W == 13 && g.B >= 4 * W2_SLICES && g.B * 7744 < (int64_t{1} << 31);
 }
 
 static bool is_conv3_dgrad(const ConvF32Geom& g) {
@@ -1828,9 +1844,9 @@ void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const
     return;
   }
   if (!xu8 && db && conv2_wgrad_f32_ok(g)) {
-    hipLaunchKernelGGL(conv2_wgrad_f32_kernel, dim3(2 * W3_SLICES), dim3(256), 0, s, dz, x, slab,
+    hipLaunchKernelGGL(conv2_wgrad_f32_kernel, dim3(2 * W2_SLICES), dim3(256), 0, s, dz, x, slab,
                        static_cast<int>(g.B));
-    f32_slab_reduce(slab, W3_SLICES, g.Kout, Nw, ncol, dw, db, s);
+    f32_slab_reduce(slab, W2_SLICES, g.Kout, Nw, ncol, dw, db, s);
     return;
   }
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
