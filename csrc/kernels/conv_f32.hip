@@ -1301,40 +1301,38 @@ __global__ __launch_bounds__(256) void d3_repack_kernel(const float* __restrict_
   wp[i] = w[(co * 64 + ci) * 9 + t];
 }
 
-__global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __restrict__ dz,
+__global__ __launch_bounds__(256, 2) void conv3_dgrad_f32_kernel(const float* __restrict__ dz,
                                                                   const float* __restrict__ wp,
                                                                   float* __restrict__ dx, int B) {
-  __shared__ __attribute__((aligned(16))) float A[2][128 * D3_AS];   // 80 KB
+  __shared__ __attribute__((aligned(16))) float A[1][128 * D3_AS];   // 40 KB (two workgroups per CU)
   __shared__ __attribute__((aligned(16))) float X[4][16 * D3_XS];   // 25.9 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const float* wl = wp + wave * 32 * 576 + lane;  // + (k-step * 9 + tap) * 64
   float* xw = X[wave];
-  // this thread's 8 float4 of an image's dz (2048 float4: co = e / 16, column 4 (e % 16))
-  auto load_img = [&](int b, float4 (&r)[8]) {
-    const float4* src = reinterpret_cast<const float4*>(dz + (int64_t)b * 8192);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) r[u] = src[tid + 256 * u];
+  // an image's dz into the staging buffer: this thread's 8 float4 (2048 float4: co = e / 16, column 4 (e % 16)),
+  // all loads issued before the first store
+  auto copy_img = [&](int b, float* buf) {
+    const float4* src = reinterpret_cast<const float4*>(dz + (int64_t)b * 8192) + tid;
+    // named registers, not an array: the array form was left on the scratch stack
+    const float4 r0 = src[0], r1 = src[256], r2 = src[512], r3 = src[768], r4 = src[1024], r5 = src[1280],
+                 r6 = src[1536], r7 = src[1792];
+    float* d = buf + (tid >> 4) * D3_AS + (tid & 15) * 4;  // + 16 co rows per 256 float4
+    *reinterpret_cast<float4*>(d + 0 * 16 * D3_AS) = r0;
+    *reinterpret_cast<float4*>(d + 1 * 16 * D3_AS) = r1;
+    *reinterpret_cast<float4*>(d + 2 * 16 * D3_AS) = r2;
+    *reinterpret_cast<float4*>(d + 3 * 16 * D3_AS) = r3;
+    *reinterpret_cast<float4*>(d + 4 * 16 * D3_AS) = r4;
+    *reinterpret_cast<float4*>(d + 5 * 16 * D3_AS) = r5;
+    *reinterpret_cast<float4*>(d + 6 * 16 * D3_AS) = r6;
+    *reinterpret_cast<float4*>(d + 7 * 16 * D3_AS) = r7;
   };
-  auto stash_img = [&](float* buf, const float4 (&r)[8]) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int e = tid + 256 * u;
-      *reinterpret_cast<float4*>(buf + (e >> 4) * D3_AS + (e & 15) * 4) = r[u];
-    }
-  };
-  float4 nxt[8];
   int b = blockIdx.x;
-  if (b < B) {
-    load_img(b, nxt);
-    stash_img(A[0], nxt);
-  }
+  if (b < B) copy_img(b, A[0]);
   __syncthreads();
-  int cur = 0;
   for (; b < B; b += gridDim.x) {
     const int nb = b + gridDim.x;
-    if (nb < B) load_img(nb, nxt);
-    const float* a_img = A[cur];
+    const float* a_img = A[0];
     f32x4 acc[9][4];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -1407,9 +1405,11 @@ __global__ __launch_bounds__(256, 1) void conv3_dgrad_f32_kernel(const float* __
       out[e] = xw[c * D3_XS + (e - 100 * c)];
     }
     asm volatile("" ::: "memory");
-    if (nb < B) stash_img(A[cur ^ 1], nxt);
+    __syncthreads();  // every wave's k loop has read this image
+    // the next image's dz straight through registers into the single buffer: the round trip is exposed to
+    // this workgroup only; the CU's other workgroup keeps the matrix cores busy meanwhile
+    if (nb < B) copy_img(nb, A[0]);
     __syncthreads();
-    cur ^= 1;
   }
 }
 
@@ -1428,10 +1428,10 @@ __global__ __launch_bounds__(256) void d2_repack_kernel(const float* __restrict_
   wp[i] = w[(co * 32 + ci) * 9 + t];
 }
 
-__global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __restrict__ dz,
+__global__ __launch_bounds__(256, 2) void conv2_dgrad_f32_kernel(const float* __restrict__ dz,
                                                                   const float* __restrict__ wp,
                                                                   float* __restrict__ dx, int B) {
-  __shared__ __attribute__((aligned(16))) float A[2][64 * 121 + 128];  // 62 KB (+ readable padding rows)
+  __shared__ __attribute__((aligned(16))) float A[1][64 * 121 + 128];  // 31 KB (+ readable padding rows)
   __shared__ __attribute__((aligned(16))) float X[4][16 * D2_XS + 32];  // 44.3 KB (+ a dump row per wave)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4, ct = wave & 1, half = wave >> 1;
@@ -1447,29 +1447,29 @@ __global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __
       const int p = 64 * half + 16 * i + 4 * lk + r;
       dst[4 * i + r] = p < 121 ? lr * D2_XS + (p / 11) * 13 + p % 11 : 16 * D2_XS;
     }
-  // an image of dz is 7744 contiguous floats = 1936 float4: threads take 7 or 8 of them
-  auto load_img = [&](int b, float4 (&r)[8]) {
-    const float4* src = reinterpret_cast<const float4*>(dz + (int64_t)b * 7744);
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (tid + 256 * u < 1936) r[u] = src[tid + 256 * u];
+  // an image of dz is 7744 contiguous floats = 1936 float4: threads take 7 or 8 of them (the loads are
+  // unconditional, clamped to the image, so they all issue before the first store)
+  auto copy_img = [&](int b, float* buf) {
+    const float4* src = reinterpret_cast<const float4*>(dz + (int64_t)b * 7744) + tid;
+    float4* d = reinterpret_cast<float4*>(buf) + tid;
+    // named registers (an array was left on the scratch stack); the last one exists for tid < 144
+    const float4 r0 = src[0], r1 = src[256], r2 = src[512], r3 = src[768], r4 = src[1024], r5 = src[1280],
+                 r6 = src[1536], r7 = src[tid < 144 ? 1792 : 0];
+    d[0] = r0;
+    d[256] = r1;
+    d[512] = r2;
+    d[768] = r3;
+    d[1024] = r4;
+    d[1280] = r5;
+    d[1536] = r6;
+    if (tid < 144) d[1792] = r7;
   };
-  auto stash_img = [&](float* buf, const float4 (&r)[8]) {
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (tid + 256 * u < 1936) reinterpret_cast<float4*>(buf)[tid + 256 * u] = r[u];
-  };
-  float4 nxt[8];
   int b = blockIdx.x;
-  if (b < B) {
-    load_img(b, nxt);
-    stash_img(A[0], nxt);
-  }
+  if (b < B) copy_img(b, A[0]);
   __syncthreads();
-  int cur = 0;
   for (; b < B; b += gridDim.x) {
     const int nb = b + gridDim.x;
-    const float* a_img = A[cur] + 64 * half;
+    const float* a_img = A[0] + 64 * half;
     f32x4 acc[9][4];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
@@ -1506,7 +1506,6 @@ __global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __
       for (int t = 0; t < 9; ++t) wb[t] = wl[((ks + 3) * 9 + t) * 64];
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (nb < B) load_img(nb, nxt);  // the next image's dz after the k-loop here (4.39 -> 4.31 ms; conv3: slower)
     // col2im into this wave's image (cross-lane shared destinations: keep program order, see conv3)
     for (int e = lane; e < 16 * D2_XS; e += 64) xw[e] = 0.f;
 #pragma unroll
@@ -1530,9 +1529,8 @@ __global__ __launch_bounds__(256, 1) void conv2_dgrad_f32_kernel(const float* __
         out[e] = x0[c * D2_XS + q] + x1[c * D2_XS + q];
       }
     }
-    if (nb < B) stash_img(A[cur ^ 1], nxt);
+    if (nb < B) copy_img(nb, A[0]);  // every k loop finished before the barrier above (see conv3)
     __syncthreads();  // images read out, next dz staged
-    cur ^= 1;
   }
 }
 
@@ -1790,7 +1788,8 @@ bool conv_dgrad_f32_scatter_ok(const ConvF32Geom& g) {
 
 void conv_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* wp,
                             hipStream_t s) {
-  const int grid = static_cast<int>(std::min<int64_t>(g.B, f32_num_cus()));
+  // two persistent workgroups per CU (single-buffered dz): one's col2im runs beside the other's MFMAs
+  const int grid = static_cast<int>(std::min<int64_t>(g.B, 2 * f32_num_cus()));
   if (is_conv3_dgrad(g)) {
     hipLaunchKernelGGL(d3_repack_kernel, dim3((D3_WP + 255) / 256), dim3(256), 0, s, w, wp);
     hipLaunchKernelGGL(conv3_dgrad_f32_kernel, dim3(grid), dim3(256), 0, s, dz, wp, dx, static_cast<int>(g.B));
