@@ -83,7 +83,10 @@ __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restr
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, lr = lane & 15, lk = lane >> 4;
   float* im = img[wave];
   for (int i = lane; i < LDS_IMG; i += 64) im[i] = 0.f;
-  // A operand (row = n): w1[16 j + lr][4 s + lk]; B operand (col = pixel m): img[pix(m) + tap(4 s + lk)]
+  // A operand (row = pixel m): img[pix(m) + tap(4 s + lk)]; B operand (col = n): w1[16 j + lr][4 s + lk].
+  // D[m][n] then leaves the 4 pixels of a pooling window (window-major m) in one lane's 4 accumulator
+  // registers: the pool is a register reduction, no cross-lane exchange (the DPP quad form spent ~70 VALU
+  // per lane and m-tile)
   float wreg[7][2];
   int tapoff[7];
 #pragma unroll
@@ -93,12 +96,7 @@ __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restr
 #pragma unroll
     for (int j = 0; j < 2; ++j) wreg[s][j] = k < TAPS ? w1[(16 * j + lr) * TAPS + k] : 0.f;
   }
-  float bias[2][4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bias[j][r] = b1[16 * j + 4 * lk + r];
-  const int tap = lr & 3;
+  const float bias[2] = {b1[lr], b1[16 + lr]};
 
   // small batches (split_mode): the 4 waves share one image per round, each taking every 4th pixel group
   const bool split = split_mode(B);
@@ -118,44 +116,28 @@ __global__ __launch_bounds__(256) void conv1_pool_f32_kernel(const void* __restr
     for (int g = split ? static_cast<int>(blockIdx.y) * WAVES + wave : 0; g < (4 * NWIN + 15) / 16; g += gstep) {
       const int m = 16 * g + lr;
       const int base = m < 4 * NWIN ? pix_base(m) : 0;
-      f32x4 acc[2] = {dev::zero_f32x4(), dev::zero_f32x4()};
+      f32x4 acc[2] = {{bias[0], bias[0], bias[0], bias[0]}, {bias[1], bias[1], bias[1], bias[1]}};
 #pragma unroll
       for (int s = 0; s < 7; ++s) {
         const float p = im[base + tapoff[s]];
-        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(wreg[s][0], p, acc[0], 0, 0, 0);
-        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(wreg[s][1], p, acc[1], 0, 0, 0);
+        acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, wreg[s][0], acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(p, wreg[s][1], acc[1], 0, 0, 0);
       }
-      // D[n][m]: lane holds m = 16 g + lr, n = 16 j + 4 lk + r; a window = lanes 4q..4q+3
-      const int win = m >> 2;
+      // lane holds D[m = 16 g + 4 lk + r][n = 16 j + lr]: window 4 g + lk, its tap r
+      const int win = 4 * g + lk;
+      if (win < NWIN) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float best = acc[j][r] + bias[j][r];
-          int bt = tap;
-          {  // first maximum in window order wins, as max_pool2d
-            const float ov = quad_xor<1>(best);
-            const int ot = quad_xor<1>(bt);
-            if (ov > best || (ov == best && ot < bt)) {
-              best = ov;
-              bt = ot;
-            }
-          }
-          {
-            const float ov = quad_xor<2>(best);
-            const int ot = quad_xor<2>(bt);
-            if (ov > best || (ov == best && ot < bt)) {
-              best = ov;
-              bt = ot;
-            }
-          }
-          if (tap == 0 && win < NWIN) {
-            const int n = 16 * j + 4 * lk + r;
-            const bool live = best > 0.f;
-            ab[n * NWIN + win] = live ? best : 0.f;
-            cb[n * NWIN + win] = live ? static_cast<unsigned char>(bt) : 255;
-          }
+        for (int j = 0; j < 2; ++j) {
+          const f32x4 v = acc[j];
+          const float best = fmaxf(fmaxf(fmaxf(v[0], v[1]), v[2]), v[3]);  // v_max3 + v_max
+          // first maximum in window order wins, as max_pool2d
+          const int bt = v[0] == best ? 0 : v[1] == best ? 1 : v[2] == best ? 2 : 3;
+          const bool live = best > 0.f;
+          const int n = 16 * j + lr;
+          ab[n * NWIN + win] = live ? best : 0.f;
+          cb[n * NWIN + win] = live ? static_cast<unsigned char>(bt) : 255;
         }
+      }
     }
   }
 }
