@@ -1033,9 +1033,135 @@ void conv_f32_fwd(const ConvF32Geom& g, const float* x, const unsigned char* xu8
   }
 }
 
+// ---------------------------------------------------------------- conv3 + ReLU + pool3 forward (fp32)
+// The ConvNet's conv3 (64 -> 128 channels, 3x3 valid, 10x10 -> 8x8) with bias, ReLU and the 2x2/s2 max-pool
+// (-> 4x4, + the argmax code of pool_relu / PoolOut) as one persistent 512-thread workgroup per CU.  Its
+// 128 x 576 weights (295 KB) do not fit in LDS but do fit in the 8 waves' registers: wave w owns output
+// channels [16 w, +16) and holds their whole K (144 k-steps of 4, tap-major: k = 64 tap + ci) as B operands,
+// 144 VGPRs per lane, loaded once per launch.  Per image the waves share one LDS copy of the input (64
+// channels x 10 x 10, row stride 112 floats = 16 banks apart, so the two channel rows of a b32 read never
+// collide) and each runs 4 m-tiles x 144 k-steps with 4 independent accumulators.  The m-tile rows are
+// window-major (row r of tile t: window 4 (r / 4) + t, tap r % 4), so a lane's 4 accumulator registers of
+// tile t are the 4 pixels of window 4 lk + t: the pool is a register reduction and a lane's 4 tiles give 4
+// consecutive pooled outputs of one channel (one float4 + one dword of codes per lane and image).
+// The next image's input is loaded into registers during the k loop and stored to the other LDS buffer.
+namespace {
+constexpr int C3P_S = 112;  // floats per input channel row in LDS (100 + 12; 112 = 16 mod 32)
+
+__global__ __launch_bounds__(512, 1) void conv3_pool_f32_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bias,
+                                                                float* __restrict__ a,
+                                                                unsigned char* __restrict__ code, int B) {
+  __shared__ __attribute__((aligned(16))) float XI[2][64 * C3P_S];  // 2 x 28 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int co = 16 * wave + lr;
+  // B[k = 4 ks + lk][n = lr] = w[co][ci = 4 (ks & 15) + lk][tap = ks >> 4]
+  float wr[144];
+  {
+    const float* wc = w + co * 576;
+#pragma unroll
+    for (int ks = 0; ks < 144; ++ks) wr[ks] = wc[(4 * (ks & 15) + lk) * 9 + (ks >> 4)];
+  }
+  const float bv = bias[co];
+  // A: row lr of m-tile t = pixel (2 (lr >> 2) + ((lr >> 1) & 1), 2 t + (lr & 1)) of channel 4 (ks & 15) + lk
+  int abase[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) abase[t] = lk * C3P_S + (2 * (lr >> 2) + ((lr >> 1) & 1)) * 10 + 2 * t + (lr & 1);
+  auto koff = [](int ks) { const int tap = ks >> 4; return 4 * (ks & 15) * C3P_S + (tap / 3) * 10 + tap % 3; };
+  // staging: an image is 1600 float4 (channel e / 25, column 4 (e % 25)); threads take 3 or 4 (named
+  // registers: an array of them was left on the scratch stack)
+  float4 st0, st1, st2, st3;
+  auto load = [&](int b) {
+    const float4* src = reinterpret_cast<const float4*>(x + (int64_t)b * 6400) + tid;
+    st0 = src[0];
+    st1 = src[512];
+    st2 = src[1024];
+    st3 = src[tid < 64 ? 1536 : 0];
+  };
+  auto put = [&](float* buf, int e, const float4& v) {
+    const int c = e / 25, q = 4 * (e - 25 * c);
+    *reinterpret_cast<float4*>(buf + c * C3P_S + q) = v;
+  };
+  auto stash = [&](float* buf) {
+    put(buf, tid, st0);
+    put(buf, tid + 512, st1);
+    put(buf, tid + 1024, st2);
+    if (tid < 64) put(buf, tid + 1536, st3);
+  };
+  int b = blockIdx.x;
+  if (b < B) {
+    load(b);
+    stash(XI[0]);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; b < B; b += gridDim.x) {
+    const int nb = b + gridDim.x;
+    if (nb < B) load(nb);  // lands during the k loop
+    const float* X = XI[cur];
+    f32x4 acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = f32x4{bv, bv, bv, bv};
+    // k-step-major: the next k-step's 4 A reads issued ahead of this one's 4 MFMAs
+    float av[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) av[t] = X[abase[t] + koff(0)];
+#pragma unroll
+    for (int ks = 0; ks < 144; ++ks) {
+      float an[4];
+      if (ks + 1 < 144) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) an[t] = X[abase[t] + koff(ks + 1)];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], wr[ks], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < 144) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) av[t] = an[t];
+      }
+    }
+    // lane: D[row 4 lk + r][co] of tile t = window 4 lk + t, tap r (row-major in the window)
+    float o[4];
+    uint32_t cw = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const f32x4 v = acc[t];
+      const float best = fmaxf(fmaxf(fmaxf(v[0], v[1]), v[2]), v[3]);
+      const uint32_t arg = v[0] == best ? 0u : v[1] == best ? 1u : v[2] == best ? 2u : 3u;  // first maximum
+      const bool live = best > 0.f;
+      o[t] = live ? best : 0.f;
+      cw |= (live ? arg : 255u) << (8 * t);
+    }
+    reinterpret_cast<float4*>(a + (int64_t)b * 2048 + co * 16)[lk] = make_float4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<uint32_t*>(code + (int64_t)b * 2048 + co * 16)[lk] = cw;
+    if (nb < B) stash(XI[cur ^ 1]);
+    __syncthreads();  // the next image staged; this one's reads done before it is overwritten next round
+    cur ^= 1;
+  }
+}
+}  // namespace
+
+bool conv3_pool_f32_ok(const ConvF32Geom& g) {
+  static const bool on = [] {
+    const char* v = std::getenv("RINGDP_F32_CONV3_FWD");
+    return !(v && v[0] == '0');
+  }();
+  return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
+         g.B >= 4 * f32_num_cus() && g.B * 6400 < (int64_t{1} << 31);
+}
+
 void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
                        const float* w, const float* bias, float* a, unsigned char* code, hipStream_t s) {
   const int K = g.C * g.R * g.R;
+  if (bias && !xu8 && conv3_pool_f32_ok(g)) {  // the ConvNet's conv3 at large batches: the dedicated kernel
+    const int grid = static_cast<int>(std::min<int64_t>(g.B, f32_num_cus()));
+    hipLaunchKernelGGL(conv3_pool_f32_kernel, dim3(grid), dim3(512), 0, s, x, w, bias, a, code, static_cast<int>(g.B));
+    return;
+  }
   const int phw = (g.OH / 2) * (g.OW / 2);
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, aout = static_cast<int64_t>(g.Kout) * phw;
   const int64_t chunk = batch_chunk(g.B, {xin, static_cast<int64_t>(g.Kout) * g.OH * g.OW});

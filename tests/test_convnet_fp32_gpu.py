@@ -338,3 +338,29 @@ def test_conv2_pool_f32_dedicated(B):
     assert torch.equal(code[best < -1e-4], want[best < -1e-4])  # dead windows: 255
     a2, code2 = C.f32_conv_pool_fwd(x, w, b, 0, 0.0, 1.0, 1)
     assert torch.equal(a, a2) and torch.equal(code, code2)
+
+
+@pytest.mark.parametrize("B", [1024, 1100])
+def test_conv3_pool_f32_dedicated(B):
+    """conv3 + bias + ReLU + 2x2/s2 max-pool on the dedicated forward kernel (csrc/kernels/conv_f32.hip
+    conv3_pool_f32_kernel: weights resident in 8 waves' registers, window-major m-tiles pooled in registers)
+    against fp64: pooled values, argmax codes wherever the window maximum is not a near-tie, dead windows 255,
+    and against the implicit-GEMM path at a batch below the dedicated kernel's threshold."""
+    g = torch.Generator(device=DEV).manual_seed(B + 7)
+    x = torch.randn(B, 64, 10, 10, device=DEV, generator=g)
+    w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.05
+    b = torch.randn(128, device=DEV, generator=g) * 0.1
+    a, code = C.f32_conv_pool_fwd(x, w, b, 0, 0.0, 1.0, 2)
+    z = F.conv2d(x.double(), w.double(), b.double())  # [B, 128, 8, 8]
+    win = torch.stack([z[..., 0::2, 0::2], z[..., 0::2, 1::2], z[..., 1::2, 0::2], z[..., 1::2, 1::2]], -1)
+    best, arg = win.max(-1)
+    _close(a, best.clamp_min(0).float(), rtol=1e-5, atol=1e-5)
+    top2 = win.topk(2, -1).values
+    clear = ((top2[..., 0] - top2[..., 1]) > 1e-4 * (1 + top2[..., 0].abs())) & (best > 1e-4)
+    want = torch.where(best > 0, arg, torch.full_like(arg, 255)).to(torch.uint8)
+    assert torch.equal(code[clear], want[clear])
+    assert torch.equal(code[best < -1e-4], want[best < -1e-4])
+    a2, code2 = C.f32_conv_pool_fwd(x, w, b, 0, 0.0, 1.0, 2)
+    assert torch.equal(a, a2) and torch.equal(code, code2)
+    small, _ = C.f32_conv_pool_fwd(x[:100].contiguous(), w, b, 0, 0.0, 1.0, 2)  # the GEMM path
+    _close(small, a[:100], rtol=1e-5, atol=1e-5)
