@@ -786,6 +786,45 @@ __global__ __launch_bounds__(256) void pool2s1_bwd_kernel(const float* __restric
   }
 }
 
+// The same over tiles of 16 planes staged in LDS (16-B loads of da and the codes, coalesced stores of dz): the
+// per-element form issues 8 scalar loads per output and ran at ~2.6 TB/s (conv2's pool2 backward at B=65536:
+// 1.58 ms).  Needs PH * PW <= 128, PH * PW % 4 == 0 and a multiple of 16 planes.
+constexpr int kP2Tile = 16;
+// CPH / CPW > 0: compile-time window grid (the ConvNet's 10 x 10: the output index divisions become multiplies)
+template <int CPH, int CPW>
+__global__ __launch_bounds__(256) void pool2s1_bwd_tile_kernel(const float* __restrict__ da,
+                                                               const unsigned char* __restrict__ code,
+                                                               float* __restrict__ dz, int ntiles, int PH_, int PW_) {
+  const int PH = CPH > 0 ? CPH : PH_, PW = CPW > 0 ? CPW : PW_;
+  __shared__ __attribute__((aligned(16))) float D[kP2Tile * 128];
+  __shared__ __attribute__((aligned(16))) unsigned char Cd[kP2Tile * 128];
+  const int tid = threadIdx.x, W = PW + 1, hw = (PH + 1) * W, phw = PH * PW;
+  const int n4 = kP2Tile * phw / 4, n16 = kP2Tile * phw / 16, nout = kP2Tile * hw;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t p0 = (int64_t)t * kP2Tile;
+    const float4* src = reinterpret_cast<const float4*>(da + p0 * phw);
+    for (int e = tid; e < n4; e += 256) reinterpret_cast<float4*>(D)[e] = src[e];
+    const uint4* cs = reinterpret_cast<const uint4*>(code + p0 * phw);
+    for (int e = tid; e < n16; e += 256) reinterpret_cast<uint4*>(Cd)[e] = cs[e];
+    __syncthreads();
+    float* out = dz + p0 * hw;
+    for (int o = tid; o < nout; o += 256) {
+      const int pl = o / hw, r = o - pl * hw, y = r / W, x = r - y * W;
+      float g = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int py = y - (q >> 1), px = x - (q & 1);
+        if (static_cast<unsigned>(py) < static_cast<unsigned>(PH) && static_cast<unsigned>(px) < static_cast<unsigned>(PW)) {
+          const int i = pl * phw + py * PW + px;
+          if (Cd[i] == q) g += D[i];
+        }
+      }
+      out[o] = g;
+    }
+    __syncthreads();  // the tile is consumed before the next one is staged
+  }
+}
+
 // Fixed-order sums of the split-K slabs [slices][Kout][Nw + has_bias]: stage 1 sums groups of
 // kSlabGroup consecutive slices into part[group] (grid.y = groups), stage 2 sums the groups into
 // dw [Kout][Nw] and db [Kout].  Two stages keep each thread's serial chain short.
@@ -2059,6 +2098,18 @@ void pool_relu_f32_bwd(const float* da, const unsigned char* code, float* dz, in
       const int wins = static_cast<int>(nbc * PH * PW);
       hipLaunchKernelGGL(pool2s2_bwd_kernel, dim3(grid_elems(wins)), dim3(256), 0, s, da + c0 * PH * PW,
                          code + c0 * PH * PW, dz + c0 * H * W, wins, make_fdiv(PH * PW), make_fdiv(PW), H, W);
+      continue;
+    }
+    if (k == 2 && st == 1 && PH * PW <= 128 && (PH * PW) % 4 == 0 && nbc % kP2Tile == 0 &&
+        !(std::getenv("RINGDP_F32_P2BWD_TILE") && std::getenv("RINGDP_F32_P2BWD_TILE")[0] == '0')) {
+      const int ntiles = static_cast<int>(nbc / kP2Tile);
+      const dim3 grid(std::min(ntiles, 8 * f32_num_cus()));
+      if (PH == 10 && PW == 10)
+        hipLaunchKernelGGL((pool2s1_bwd_tile_kernel<10, 10>), grid, dim3(256), 0, s, da + c0 * PH * PW,
+                           code + c0 * PH * PW, dz + c0 * H * W, ntiles, PH, PW);
+      else
+        hipLaunchKernelGGL((pool2s1_bwd_tile_kernel<0, 0>), grid, dim3(256), 0, s, da + c0 * PH * PW,
+                           code + c0 * PH * PW, dz + c0 * H * W, ntiles, PH, PW);
       continue;
     }
     if (k == 2 && st == 1) {

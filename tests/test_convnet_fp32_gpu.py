@@ -364,3 +364,20 @@ def test_conv3_pool_f32_dedicated(B):
     assert torch.equal(a, a2) and torch.equal(code, code2)
     small, _ = C.f32_conv_pool_fwd(x[:100].contiguous(), w, b, 0, 0.0, 1.0, 2)  # the GEMM path
     _close(small, a[:100], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("planes,H", [((64, 64), 11), ((4, 8), 9), ((3, 5), 11)])
+def test_pool2s1_bwd_tile_matches_elementwise(planes, H):
+    """The LDS-tiled overlapping-pool backward (csrc/kernels/conv_f32.hip pool2s1_bwd_tile_kernel, 16 planes per
+    tile) against autograd through max_pool2d: (64, 64) planes take the tiled path with the compile-time 10 x 10
+    window grid, 9 x 9 inputs its runtime-size variant, (3, 5) = 15 planes the per-element kernel."""
+    n, c = planes
+    g = torch.Generator(device=DEV).manual_seed(n + c)
+    z = torch.randn(n, c, H, H, device=DEV, generator=g)
+    a, code = C.f32_pool_relu_fwd(z, 2, 1)
+    zr = z.clone().requires_grad_()
+    ref = F.max_pool2d(F.relu(zr), 2, 1)
+    da = torch.randn_like(a)
+    ref.backward(da)
+    dz = C.f32_pool_relu_bwd(da, code, H, H, 2, 1)
+    _close(dz, zr.grad, rtol=0, atol=1e-6)
