@@ -1704,19 +1704,21 @@ __global__ __launch_bounds__(256, 2) void conv2_dgrad_f32_kernel(const float* __
 // gradient db3[co] = sum dz3): a dedicated kernel instead of the implicit GEMM's per-element gathers.  Workgroup
 // (ct, slice) owns input channels [16 ct, +16) and images [B slice / S, B (slice + 1) / S); wave w owns output
 // channels [32 w, +32) x 16 channels x 9 taps (18 MFMA tiles).  Per image both operands come from LDS with
-// compile-time offsets: dz3 staged transposed (positions x co, so a 16-co A fragment is one conflict-free
-// row read) and the 16-channel a2 tile (the tap shift is an immediate).  The bias sums ride in the staging
-// (ct = 0 workgroups, VALU).  Each workgroup writes its slice's partial dW into slab[slice][co][ci 9 + t]
-// (+ the bias column), reduced by the same fixed-order f32_slab_reduce as the GEMM path: deterministic.
-constexpr int W3_DS = 144;  // floats per position row of the transposed dz3 (128 co + 16: 16 banks apart)
+// compile-time offsets: dz3 in its natural [co][p] order with a row stride of 2 mod 32 banks (the A fragment,
+// 16 co x 4 positions, is a conflict-free b32 read; the transposed layout it replaces made every staging
+// store a 16-way bank conflict) and the 16-channel a2 tile (the tap shift is an immediate).  The bias sums
+// ride in the staging (ct = 0 workgroups, VALU).  The next image's operands are loaded into registers during
+// the k loop.  Each workgroup writes its slice's partial dW into slab[slice][co][ci 9 + t] (+ the bias
+// column), reduced by the same fixed-order f32_slab_reduce as the GEMM path: deterministic.
+constexpr int W3_DS = 66;   // floats per co row of the dz3 tile (64 positions + 2; 66 = 2 mod 32)
 constexpr int W3_AS = 101;  // floats per channel row of the a2 tile (odd)
 
 __global__ __launch_bounds__(256, 2) void conv3_wgrad_f32_kernel(const float* __restrict__ dz,
                                                                   const float* __restrict__ a2,
                                                                   float* __restrict__ slab, int B) {
-  // single-buffered (49.3 KB): two workgroups per CU, so one stages while the other multiplies
-  __shared__ __attribute__((aligned(16))) float DZ[1][64 * W3_DS];  // 36.9 KB
-  __shared__ __attribute__((aligned(16))) float AX[1][16 * W3_AS];  // 6.5 KB
+  // single-buffered (40.3 KB): two workgroups per CU, so one stages while the other multiplies
+  __shared__ __attribute__((aligned(16))) float DZ[128 * W3_DS];  // 33.8 KB
+  __shared__ __attribute__((aligned(16))) float AX[16 * W3_AS];   // 6.5 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lk = lane >> 4;
   const int ct = blockIdx.x & 3, slice = blockIdx.x >> 2;
@@ -1724,36 +1726,34 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_f32_kernel(const float* __
   const bool bias = ct == 0;
   // staging: dz3 = 2048 float4 (co = e >> 4, positions 4 (e & 15) ..), 8 per thread; the a2 tile = 400 float4
   // (channel 4 e / 100, never crossing a row), 1-2 per thread
-  auto load = [&](int b, float4 (&rz)[8], float4 (&ra)[2]) {
+  float4 rz[8], ra[2];
+  auto load = [&](int b) {
     const float4* z4 = reinterpret_cast<const float4*>(dz + (int64_t)b * 8192);
 #pragma unroll
     for (int u = 0; u < 8; ++u) rz[u] = z4[tid + 256 * u];
     const float4* a4 = reinterpret_cast<const float4*>(a2 + (int64_t)b * 6400 + ct * 1600);
     ra[0] = a4[tid];
-    if (tid < 144) ra[1] = a4[256 + tid];
+    ra[1] = a4[tid < 144 ? 256 + tid : tid];
   };
   float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // bias partials of co (tid >> 4) + 16 u
-  auto stash = [&](int buf, const float4 (&rz)[8], const float4 (&ra)[2]) {
-    float* d = DZ[buf];
+  auto stash = [&]() {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int e = tid + 256 * u, co = e >> 4, p = (e & 15) * 4;
-      d[(p + 0) * W3_DS + co] = rz[u].x;
-      d[(p + 1) * W3_DS + co] = rz[u].y;
-      d[(p + 2) * W3_DS + co] = rz[u].z;
-      d[(p + 3) * W3_DS + co] = rz[u].w;
+      float2* d = reinterpret_cast<float2*>(DZ + co * W3_DS + p);  // 8-B aligned (W3_DS even)
+      d[0] = make_float2(rz[u].x, rz[u].y);
+      d[1] = make_float2(rz[u].z, rz[u].w);
       if (bias) bsum[u] += (rz[u].x + rz[u].y) + (rz[u].z + rz[u].w);
     }
-    float* x = AX[buf];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int e = tid + 256 * u;
       if (u == 0 || tid < 144) {
         const int c = (4 * e) / 100, q = 4 * e - 100 * c;
-        x[c * W3_AS + q + 0] = ra[u].x;
-        x[c * W3_AS + q + 1] = ra[u].y;
-        x[c * W3_AS + q + 2] = ra[u].z;
-        x[c * W3_AS + q + 3] = ra[u].w;
+        AX[c * W3_AS + q + 0] = ra[u].x;
+        AX[c * W3_AS + q + 1] = ra[u].y;
+        AX[c * W3_AS + q + 2] = ra[u].z;
+        AX[c * W3_AS + q + 3] = ra[u].w;
       }
     }
   };
@@ -1762,22 +1762,20 @@ __global__ __launch_bounds__(256, 2) void conv3_wgrad_f32_kernel(const float* __
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[j][t] = dev::zero_f32x4();
-  float4 rz[8], ra[2];
-  const int abase = lk * W3_DS + 32 * wave + lr;  // A: position 4 ks + lk, output channel 32 w + 16 j + lr
-  const int xbase = lr * W3_AS + lk;              // B: channel lr, position (ks >> 1, 4 (ks & 1) + lk) + tap
+  const int abase = (32 * wave + lr) * W3_DS + lk;  // A: output channel 32 w + 16 j + lr, position 4 ks + lk
+  const int xbase = lr * W3_AS + lk;                // B: channel lr, position (ks >> 1, 4 (ks & 1) + lk) + tap
+  if (b0 < b1) load(b0);
   for (int b = b0; b < b1; ++b) {
-    load(b, rz, ra);
-    stash(0, rz, ra);
+    stash();
     __syncthreads();
-    const float* d = DZ[0];
-    const float* x = AX[0];
+    if (b + 1 < b1) load(b + 1);  // in flight during the k loop
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       float a[2], w[9];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) a[j] = d[abase + 4 * ks * W3_DS + 16 * j];
+      for (int j = 0; j < 2; ++j) a[j] = DZ[abase + 4 * ks + 16 * j * W3_DS];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) w[t] = x[xbase + ((ks >> 1) + t / 3) * 10 + 4 * (ks & 1) + t % 3];
+      for (int t = 0; t < 9; ++t) w[t] = AX[xbase + ((ks >> 1) + t / 3) * 10 + 4 * (ks & 1) + t % 3];
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
