@@ -226,17 +226,30 @@ def _models(seed=0):
     return m32, ref
 
 
-def test_fp32_convnet_matches_aten():
+@pytest.mark.parametrize("B", [64, 2048])
+def test_fp32_convnet_matches_aten(B):
+    """Forward + gradients of the fp32 model against ATen fp32.  B=2048 runs the large-batch kernels of
+    csrc/kernels/conv_f32.hip in the model (scatter data gradients, dedicated weight gradients, the conv2 / conv3
+    + pool forwards, the tiled pool2 backward); B=64 the small-batch split-K path."""
     m32, ref = _models()
-    x = torch.randint(0, 256, (64, 1, 28, 28), dtype=torch.uint8, device=DEV)
-    y = torch.randint(0, 10, (64,), device=DEV)
+    x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device=DEV)
+    y = torch.randint(0, 10, (B,), device=DEV)
     out = m32(x)
     rout = ref.reference_forward(x)
     _close(out.detach(), rout.detach(), rtol=1e-4, atol=1e-5)
     F.cross_entropy(out, y).backward()
     F.cross_entropy(rout, y).backward()
     for (n, p), q in zip(m32.named_parameters(), ref.parameters()):
-        _close(p.grad, q.grad, rtol=1e-4, atol=1e-6)
+        if B <= 64:
+            _close(p.grad, q.grad, rtol=1e-4, atol=1e-6)
+        else:
+            # tens of millions of pooling windows: a few near-ties (top-2 gap below the ~1e-7 summation-order
+            # difference) pick the other argmax than ATen and route one element's gradient elsewhere, so the
+            # per-element bound does not hold; the relative L2 error stays ~1e-3 or below (measured: conv1.weight
+            # 1.6e-3, the rest <= 5e-4, conv3.bias / fc1 ~2e-7 - the same with every large-batch kernel switched
+            # off, i.e. the generic implicit GEMMs: tools/scratch/fp32_diag.py)
+            rel = float((p.grad - q.grad).norm() / q.grad.norm())
+            assert rel < 5e-3, (n, rel)
 
 
 def _trajectory(model, forward, steps, xs, ys, lr):
@@ -253,14 +266,16 @@ def _trajectory(model, forward, steps, xs, ys, lr):
     return torch.tensor(out)
 
 
-def test_convergence_200_steps_fp32_and_bf16():
+@pytest.mark.parametrize("B", [128, 2048])
+def test_convergence_200_steps_fp32_and_bf16(B):
+    """200 SGD steps of the fp32 and bf16 models against ATen fp32; B=2048 takes the large-batch fp32 kernels."""
     from ringdp.models import ConvNet
 
     g = torch.Generator(device=DEV).manual_seed(7)
-    xs = [torch.randint(0, 256, (128, 1, 28, 28), dtype=torch.uint8, device=DEV, generator=g) for _ in range(8)]
+    xs = [torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device=DEV, generator=g) for _ in range(8)]
     # learnable labels: a fixed random linear map of the pixels, so the loss really falls
     proj = torch.randn(784, 10, device=DEV, generator=g)
-    ys = [(x.float().view(128, -1) @ proj).argmax(1) for x in xs]
+    ys = [(x.float().view(B, -1) @ proj).argmax(1) for x in xs]
     lr, steps = 0.01, 200
     m32, ref = _models(1)
     l_ref = _trajectory(ref, ref.reference_forward, steps, xs, ys, lr)
