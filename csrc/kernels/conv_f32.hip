@@ -1262,11 +1262,35 @@ __global__ __launch_bounds__(256, 2) void conv2_pool_f32_kernel(const float* __r
     const int p = min(16 * i + lr, 120);  // rows past 120: a real pixel, product never stored
     pbase[i] = lk * 169 + (p / 11) * 13 + p % 11;
   }
+  // staging: the image is 5408 floats = 1352 float4, 5 or 6 per thread, loaded into named registers one image
+  // ahead (in flight during the k loop) and stored after the pool phase
+  float4 s0, s1, s2, s3, s4, s5;
+  auto load = [&](int b) {
+    const float4* src = reinterpret_cast<const float4*>(x + (int64_t)b * 5408) + tid;
+    s0 = src[0];
+    s1 = src[256];
+    s2 = src[512];
+    s3 = src[768];
+    s4 = src[1024];
+    s5 = src[tid < 72 ? 1280 : 0];
+  };
+  auto stash = [&]() {
+    float4* d = reinterpret_cast<float4*>(XI) + tid;
+    d[0] = s0;
+    d[256] = s1;
+    d[512] = s2;
+    d[768] = s3;
+    d[1024] = s4;
+    if (tid < 72) d[1280] = s5;
+  };
+  if (blockIdx.x < B) {
+    load(blockIdx.x);
+    stash();
+  }
+  __syncthreads();
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
-    // stage the image (5408 floats = 1352 float4)
-    const float4* src = reinterpret_cast<const float4*>(x + (int64_t)b * 5408);
-    for (int e = tid; e < 1352; e += 256) reinterpret_cast<float4*>(XI)[e] = src[e];
-    __syncthreads();
+    const int nb = b + gridDim.x;
+    if (nb < B) load(nb);
     f32x4 acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = dev::zero_f32x4();
@@ -1326,7 +1350,8 @@ __global__ __launch_bounds__(256, 2) void conv2_pool_f32_kernel(const float* __r
       ao[qd] = make_float4(o[0], o[1], o[2], o[3]);
       co[qd] = cw;
     }
-    __syncthreads();  // Z and XI free for the next image
+    if (nb < B) stash();  // XI was last read by the k loop, before the barrier above
+    __syncthreads();  // Z free, the next image staged
   }
 }
 }  // namespace
