@@ -1071,6 +1071,13 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
   }
 }
 
+// the consumer's conv3 k-steps per phase: [0, KA) beside conv1, [KA, KB) beside conv2, [KB, 18) beside pool2
+#ifndef RINGDP_FF_KA
+#define RINGDP_FF_KA 4
+#endif
+#ifndef RINGDP_FF_KB
+#define RINGDP_FF_KB 11
+#endif
 template <bool PACK>
 __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__ packed, const PackSrc& ws,
                             const float* __restrict__ b3, const float* __restrict__ bfc, bf16* __restrict__ a3,
@@ -1174,19 +1181,19 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     if (live_m) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
-      mfma_ks(xb, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+      mfma_ks(xb, std::integral_constant<int, 0>{}, std::integral_constant<int, RINGDP_FF_KA>{});
     }
     __syncthreads();  // [S1]
     // ---------------- phase 2
     if (live_e && fc) fc_reduce(be);
-    if (live_m) mfma_ks(xb, std::integral_constant<int, 4>{}, std::integral_constant<int, 11>{});
+    if (live_m) mfma_ks(xb, std::integral_constant<int, RINGDP_FF_KA>{}, std::integral_constant<int, RINGDP_FF_KB>{});
     __syncthreads();  // [S2]
     // ---------------- phase 3: the rest of the producer's pool2 (image s), k-steps 11-17
     {
       const int bpr = b0 + s * bstep;
       if (bpr < Bp) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, bpr, tid, p2split, 800);
     }
-    if (live_m) mfma_ks(xb, std::integral_constant<int, 11>{}, std::integral_constant<int, 18>{});
+    if (live_m) mfma_ks(xb, std::integral_constant<int, RINGDP_FF_KB>{}, std::integral_constant<int, 18>{});
     __syncthreads();  // [S3]
   }
 }
