@@ -552,6 +552,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool2d_bwd", &ops::maxpool2d_bwd);
   m.def("avgpool_fwd", &ops::avgpool_fwd);
   m.def("avgpool_bwd", &ops::avgpool_bwd);
+  m.def("head_ok", [](int64_t C, int64_t J) { return kern::head_ok((int)C, (int)J); });
+  m.def("head_fwd", &ops::head_fwd);
+  m.def("head_bwd", &ops::head_bwd);
   m.def("add_bf16", &ops::add_bf16);
   m.def("layernorm_fwd", &ops::layernorm_fwd);
   m.def("layernorm_bwd", &ops::layernorm_bwd);

@@ -1184,13 +1184,23 @@ __global__ __launch_bounds__(512, 1) void conv3_pool_f32_kernel(const float* __r
 }
 }  // namespace
 
+// smallest batch that takes the dedicated conv2 / conv3 forward kernels (one image per workgroup at a time)
+// instead of split K + pool_slab_fwd (RINGDP_F32_FWD_MIN_B overrides; default 4 images per CU)
+static int f32_fwd_dedicated_min_b() {
+  static const int v = [] {
+    const char* e = std::getenv("RINGDP_F32_FWD_MIN_B");
+    return e && *e ? std::atoi(e) : 4 * f32_num_cus();
+  }();
+  return v;
+}
+
 bool conv3_pool_f32_ok(const ConvF32Geom& g) {
   static const bool on = [] {
     const char* v = std::getenv("RINGDP_F32_CONV3_FWD");
     return !(v && v[0] == '0');
   }();
   return on && g.Kout == 128 && g.C == 64 && g.R == 3 && g.pad == 0 && g.H == 10 && g.W == 10 &&
-         g.B >= 4 * f32_num_cus() && g.B * 6400 < (int64_t{1} << 31);
+         g.B >= f32_fwd_dedicated_min_b() && g.B * 6400 < (int64_t{1} << 31);
 }
 
 void conv_f32_fwd_pool(const ConvF32Geom& g, const float* x, const unsigned char* xu8, float mean, float inv_std,
@@ -1362,7 +1372,7 @@ bool conv2_pool_f32_ok(const ConvF32Geom& g) {
     return !(v && v[0] == '0');
   }();
   return on && g.Kout == 64 && g.C == 32 && g.R == 3 && g.pad == 0 && g.H == 13 && g.W == 13 &&
-         g.B >= 4 * f32_num_cus() && g.B * 6400 < (int64_t{1} << 31);
+         g.B >= f32_fwd_dedicated_min_b() && g.B * 6400 < (int64_t{1} << 31);
 }
 
 void conv2_pool_f32(const ConvF32Geom& g, const float* x, const float* w, const float* bias, float* a,
@@ -1403,7 +1413,7 @@ void conv_f32_fwd_pool_s1(const ConvF32Geom& g, const float* x, const float* w, 
 // of the plain conv output, then pool_slab_fwd_kernel sums, adds the bias and pools.  RINGDP_F32_FWD_SLICES=n
 // forces n (1: the one-launch fused kernels).
 int conv_f32_fwd_slices(const ConvF32Geom& g) {
-  if (g.pad != 0) return 1;
+  if (g.pad != 0 || conv2_pool_f32_ok(g) || conv3_pool_f32_ok(g)) return 1;
   const int K = g.C * g.R * g.R;
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zout = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
   if (batch_chunk(g.B, {xin, zout}) < g.B) return 1;

@@ -876,6 +876,24 @@ static_assert(FF_OFF_X2 % 16 == 0 && FF_OFF_CT % 16 == 0 && FF_OFF_CS % 16 == 0 
                   FF_OFF_FW % 16 == 0 && FF_LDS <= 160 * 1024,
               "fused forward LDS");
 
+// RINGDP_FF_STAMPS (diagnostic builds only, tools/build_variant.py): lane 0 of every wave records s_memtime at
+// the 7 phase points of steps [FF_ST_S0, FF_ST_S0 + 8) into LDS past FF_LDS; workgroup FF_ST_BLK prints them
+// at the end (per-phase time of the producer and consumer roles)
+#ifdef RINGDP_FF_STAMPS
+constexpr int FF_ST_S0 = 100, FF_ST_BLK = 5, FF_ST_BYTES = 8 * 8 * 8 * 8;
+#define FF_ST(k)                                                                                           \
+  do {                                                                                                     \
+    if (s >= FF_ST_S0 && s < FF_ST_S0 + 8 && (threadIdx.x & 63) == 0)                                      \
+      reinterpret_cast<unsigned long long*>(smem + FF_LDS)[((threadIdx.x >> 6) * 8 + (s - FF_ST_S0)) * 8 + (k)] = \
+          __builtin_amdgcn_s_memtime();                                                                    \
+  } while (0)
+#else
+constexpr int FF_ST_BYTES = 0;
+#define FF_ST(k) \
+  do {           \
+  } while (0)
+#endif
+
 template <bool PACK>
 __device__ __forceinline__ bf16x8 ff_frag(const bf16* __restrict__ packed, const PackSrc& ws, int off, int lane) {
   bf16x8 v;
@@ -907,8 +925,9 @@ __device__ __forceinline__ void ff_wait_packed(unsigned* sync, int npack) {
 // pool2 + ReLU of items [lo, hi) (item = position p, 8-channel chunk) of the staged conv2 tile -> a2 /
 // idx2 in HBM and the conv3 operand rows of buffer X3b.  Phase 3 splits the items between the producer
 // and the consumer (the producer is the long pole: 1103 vs 808 us alone at B=65536).
-// items [0, p2split) are the producer's (kernel argument; RINGDP_FF_P2, default 560 of 800: measured
-// 400 / 480 / 560 / 800 -> 1402 / 1387 / 1342 / 1363 us at B=65536)
+// items [0, p2split) are the producer's (kernel argument; RINGDP_FF_P2, default 800 of 800 since the packed
+// pool2: phase 3 is consumer-bound (profiles/r06/fwd_stamps.md), and step times of 560 / 704 / 800 were
+// 3.335 / 3.333 / 3.325 ms, two runs each, profiles/r06/fwd_pool2/p2_resweep.txt)
 __device__ __forceinline__ void ff_pool2(const bf16* Cs, bf16* X3b, bf16* __restrict__ a2, uint8_t* __restrict__ idx2,
                                          int b, int t, int lo, int hi) {
   // uniform per-image bases, 32-bit per-item offsets (no 64-bit address math per item); at most 3 items
@@ -997,6 +1016,7 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
     const int b = b0 + s * bstep;
     const bool live = b < B;
     const int nb = b + bstep;
+    FF_ST(0);
     // ---------------- phase 1: conv1 -> X2 / CT
     if (live) {
       if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
@@ -1027,7 +1047,9 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
         p1 = c1;
       }
     }
+    FF_ST(1);
     __syncthreads();  // [S1] X2 / CT complete, XS free
+    FF_ST(2);
     // ---------------- phase 2: next input; a1 / idx1 out; conv2 -> Cs
     f32x4 acc[4][2];
     if (live) {
@@ -1064,10 +1086,14 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
         }
       }
     }
+    FF_ST(3);
     __syncthreads();  // [S2] Cs complete
+    FF_ST(4);
     // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3 (items [0, FF_P2_PROD); the consumer pools the rest)
     if (live) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, b, tid, 0, p2split);
+    FF_ST(5);
     __syncthreads();  // [S3] X3 complete; Cs, X2, CT free
+    FF_ST(6);
   }
 }
 
@@ -1148,6 +1174,7 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     const int bm = b0 + (s - 1) * bstep, be = bm - bstep;
     const bool live_m = s >= 1 && bm < B, live_e = s >= 2 && be < B;
     const bf16* xb = X3 + ((s - 1) & 1) * FF_X3H;
+    FF_ST(0);
     // ---------------- phase 1
     if (live_e) {
       float part[10];
@@ -1183,18 +1210,24 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
       for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
       mfma_ks(xb, std::integral_constant<int, 0>{}, std::integral_constant<int, RINGDP_FF_KA>{});
     }
+    FF_ST(1);
     __syncthreads();  // [S1]
+    FF_ST(2);
     // ---------------- phase 2
     if (live_e && fc) fc_reduce(be);
     if (live_m) mfma_ks(xb, std::integral_constant<int, RINGDP_FF_KA>{}, std::integral_constant<int, RINGDP_FF_KB>{});
+    FF_ST(3);
     __syncthreads();  // [S2]
+    FF_ST(4);
     // ---------------- phase 3: the rest of the producer's pool2 (image s), k-steps 11-17
     {
       const int bpr = b0 + s * bstep;
       if (bpr < Bp) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, bpr, tid, p2split, 800);
     }
     if (live_m) mfma_ks(xb, std::integral_constant<int, RINGDP_FF_KB>{}, std::integral_constant<int, 18>{});
+    FF_ST(5);
     __syncthreads();  // [S3]
+    FF_ST(6);
   }
 }
 
@@ -1218,7 +1251,7 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
     if (threadIdx.x == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
-  __shared__ __attribute__((aligned(16))) char ff_smem[FF_LDS];
+  __shared__ __attribute__((aligned(16))) char ff_smem[FF_LDS + FF_ST_BYTES];
   const int b0 = blockIdx.x, bstep = conv_blocks;
   const int nimg = b0 < B ? (B - b0 + bstep - 1) / bstep : 0;
   const int nsteps = nimg + 2;  // the consumer's MFMAs trail by one step, its epilogue by two
@@ -1230,6 +1263,20 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
   else
     ff_consumer<PACK>(ff_smem, PACK ? pack_out : packed, ws, b3, bfc, a3, idx3, logits, a2, idx2,
                       (ablate & 1) ? 0 : B, (ablate & 2) ? 0 : B, b0, bstep, nsteps, sync, npack, p2split);
+#ifdef RINGDP_FF_STAMPS
+  __syncthreads();
+  if (blockIdx.x == FF_ST_BLK && threadIdx.x == 0 && nsteps > FF_ST_S0 + 8) {
+    const unsigned long long* st = reinterpret_cast<const unsigned long long*>(ff_smem + FF_LDS);
+    for (int w = 0; w < 8; ++w)
+      for (int k = 0; k < 8; ++k) {
+        const unsigned long long* r = st + (w * 8 + k) * 8;
+        const unsigned long long t0 = st[k * 8];  // wave 0's step start
+        printf("FFST w%d s%d %lld %lld %lld %lld %lld %lld %lld\n", w, k, (long long)(r[0] - t0),
+               (long long)(r[1] - t0), (long long)(r[2] - t0), (long long)(r[3] - t0), (long long)(r[4] - t0),
+               (long long)(r[5] - t0), (long long)(r[6] - t0));
+      }
+  }
+#endif
   if (PACK) {  // the last conv workgroup out re-arms the counters
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -3211,8 +3258,8 @@ void cn_forward_fused(const void* x, bool u8, const float* const* w, const float
   bf16* pk = static_cast<bf16*>(packed);
   bf16 *a1b = static_cast<bf16*>(a1), *a2b = static_cast<bf16*>(a2), *a3b = static_cast<bf16*>(a3);
   static const int ablate = [] { const char* v = getenv("RINGDP_FF_ABLATE"); return v ? atoi(v) : 0; }();
-  static const int p2split = [] { const char* v = getenv("RINGDP_FF_P2"); const int n = v ? atoi(v) : 560;
-                                  return n >= 0 && n <= 800 ? n : 560; }();
+  static const int p2split = [] { const char* v = getenv("RINGDP_FF_P2"); const int n = v ? atoi(v) : 800;
+                                  return n >= 0 && n <= 800 ? n : 800; }();
   // In-launch packing (RINGDP_FF_INPACK=1) is correct but slow on MI355X: the pack workgroups' agent-scope
   // release has to write their XCD's L2 back before the other XCDs may read the fragments (measured
   // B=100: 114 us against 23 us with the separate pack launch), so it is off by default.

@@ -450,6 +450,12 @@ void bn_prepare(const float* sums, int G, int64_t M, int C, const float* gamma, 
                 int64_t* num_batches_tracked, hipStream_t s);
 void bn_act_fwd(const void* z, const float* scale_shift, const void* res, bool relu, int64_t M, int C, void* y,
                 hipStream_t s);
+// bn_prepare + bn_act_fwd as one launch when the group partials are few (G * C <= 8192): every workgroup forms
+// the scale / shift itself (same fixed order, same bits); save / running stats / nbt written once
+bool bn_fold_ok(int G, int C);
+void bn_fold_act_fwd(const float* sums, int G, int64_t M, int C, const float* gamma, const float* beta, float eps,
+                     float momentum, float* running_mean, float* running_var, float* save,
+                     int64_t* num_batches_tracked, const void* z, const void* res, bool relu, void* y, hipStream_t s);
 // backward part 1: g = dy * (y > 0 if relu); partial sums of g and g*zhat per channel -> part
 // BN statistics of a stored bf16 z [M][C] (C % 8 == 0, C <= 2048): partials [bn_bwd_parts(M, C)][2][C]
 // (sum, sum of squares); returns the partial count.
@@ -467,6 +473,14 @@ void maxpool_bwd(const void* dy, const uint8_t* arg, int N, int H, int W, int C,
 void avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t s);
 void avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t s);
 void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s);
+// classifier head, few classes (J <= 16, C % 8 == 0, C/8 divides 256): x [N][HW][C] bf16 -> pooled [N][C] fp32
+// (window mean) and logits [N][J] fp32 = pooled W^T + b; backward from dl [N][J] or a fused cross entropy (ce):
+// dx [N][HW][C] bf16, dw [J][C], db [J] (written, not accumulated)
+bool head_ok(int C, int J);
+void head_fwd(const void* x, int N, int HW, int C, int J, const float* w, const float* b, float* pooled,
+              float* logits, hipStream_t s);
+void head_bwd(const float* dl, const CeFuse* ce, const float* pooled, const float* w, int N, int HW, int C, int J,
+              void* dx, float* dw, float* db, hipStream_t s);
 
 // ---------------------------------------------------------------- transformer layers (vit.hip)
 void layernorm_fwd(const void* x, const float* w, const float* b, int64_t rows, int D, float eps, void* y,

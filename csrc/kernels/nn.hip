@@ -123,18 +123,16 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const void* __restric
 
 // sums = G group partials [G][2][C] of the conv epilogue's per-tile statistics (first level of
 // reduce_parts); the second level is summed here in the same fixed order (one launch fewer per BN).
-// nbt: BatchNorm.num_batches_tracked, incremented on device (one launch fewer again).
-__global__ __launch_bounds__(256) void bn_prepare_kernel(const float* __restrict__ sums, int G, int64_t M, int C,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, float eps, float momentum,
-                                                         float* __restrict__ running_mean,
-                                                         float* __restrict__ running_var, float* __restrict__ ss,
-                                                         float* __restrict__ save, int64_t* __restrict__ nbt) {
-  // block = 64 channels; wave w sums groups w, w+4, .. and the 4 wave totals combine in a fixed order
-  __shared__ float red[4][2][64];
+// 64 channels [c0, c0 + 64) per call, 256 threads: wave w sums groups w, w+4, .. and the 4 wave totals
+// combine in a fixed order; wave 0 then forms the per-channel scale / shift (-> sc_out / sh_out, either
+// may be LDS) and, if write_stats, save / running statistics.  red: [4][2][64] floats.
+__device__ __forceinline__ void bn_stats64(const float* __restrict__ sums, int G, int64_t M, int C, int c0,
+                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                           float eps, float momentum, float* __restrict__ running_mean,
+                                           float* __restrict__ running_var, float* sc_out, float* sh_out,
+                                           float* __restrict__ save, bool write_stats, float (*red)[2][64]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  const int c = c0 + lane;
   // 4 independent partial chains per wave (loads of 4 groups in flight): the serial chain over G/4 groups
   // was latency-bound (10 us at G = 64 for a ResNet-18 layer-2 conv); combined in a fixed order
   float a4[4] = {0.f, 0.f, 0.f, 0.f}, q4[4] = {0.f, 0.f, 0.f, 0.f};
@@ -155,23 +153,40 @@ __global__ __launch_bounds__(256) void bn_prepare_kernel(const float* __restrict
   red[wave][0][lane] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
   red[wave][1][lane] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
   __syncthreads();
-  if (wave != 0 || c >= C) return;
-  const float s1 = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
-  const float s2 = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
-  const double inv = 1.0 / (double)M;
-  const double mean = s1 * inv;
-  const double var = fmax(s2 * inv - mean * mean, 0.0);  // biased (normalisation)
-  const float invstd = (float)(1.0 / sqrt(var + eps));
-  const float sc = gamma[c] * invstd;
-  ss[c] = sc;
-  ss[C + c] = beta[c] - (float)mean * sc;
-  save[c] = (float)mean;
-  save[C + c] = invstd;
-  if (running_mean) {
-    const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  if (wave == 0 && c < C) {
+    const float s1 = (red[0][0][lane] + red[1][0][lane]) + (red[2][0][lane] + red[3][0][lane]);
+    const float s2 = (red[0][1][lane] + red[1][1][lane]) + (red[2][1][lane] + red[3][1][lane]);
+    const double inv = 1.0 / (double)M;
+    const double mean = s1 * inv;
+    const double var = fmax(s2 * inv - mean * mean, 0.0);  // biased (normalisation)
+    const float invstd = (float)(1.0 / sqrt(var + eps));
+    const float sc = gamma[c] * invstd;
+    sc_out[c] = sc;
+    sh_out[c] = beta[c] - (float)mean * sc;
+    if (write_stats) {
+      save[c] = (float)mean;
+      save[C + c] = invstd;
+      if (running_mean) {
+        const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+        running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+      }
+    }
   }
+  __syncthreads();  // red reusable
+}
+
+// nbt: BatchNorm.num_batches_tracked, incremented on device (one launch fewer again).
+__global__ __launch_bounds__(256) void bn_prepare_kernel(const float* __restrict__ sums, int G, int64_t M, int C,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps, float momentum,
+                                                         float* __restrict__ running_mean,
+                                                         float* __restrict__ running_var, float* __restrict__ ss,
+                                                         float* __restrict__ save, int64_t* __restrict__ nbt) {
+  __shared__ float red[4][2][64];
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) nbt[0] += 1;
+  bn_stats64(sums, G, M, C, blockIdx.x * 64, gamma, beta, eps, momentum, running_mean, running_var, ss, ss + C, save,
+             true, red);
 }
 
 __global__ __launch_bounds__(256) void bn_act_fwd_kernel(const bf16* __restrict__ z, const float* __restrict__ ss,
@@ -236,6 +251,68 @@ __global__ __launch_bounds__(256) void bn_act_fwd_col_kernel(const bf16* __restr
           if (kRes) f += (float)rv[u][j];
           if (kRelu) f = fmaxf(f, 0.f);
           o[j] = (bf16)f;
+        }
+        reinterpret_cast<bf16x8*>(y)[rr * cv + col] = o;
+      }
+    }
+  }
+}
+
+// BN forward with the statistics step folded in (few groups: kBnFoldMax): every workgroup forms the
+// scale / shift of all C channels from the G group partials itself (bn_stats64, the prepare kernel's fixed
+// order, so bit-identical to the two-launch path) into LDS; workgroup 0 also writes save / running
+// statistics / num_batches_tracked.  One launch per BN instead of two.
+struct BnFold {
+  const float* sums;
+  int G;
+  const float* gamma;
+  const float* beta;
+  float eps, momentum;
+  float* running_mean;
+  float* running_var;
+  float* save;
+  int64_t* nbt;
+};
+constexpr int kBnFoldMax = 8192;  // G * C at most (the partials every workgroup re-reads from L2)
+
+template <bool kRes, bool kRelu>
+__global__ __launch_bounds__(256) void bn_fold_act_fwd_kernel(const bf16* __restrict__ z, BnFold f,
+                                                              const bf16* __restrict__ res, int64_t M, int C,
+                                                              bf16* __restrict__ y) {
+  __shared__ float red[4][2][64];
+  __shared__ __attribute__((aligned(16))) float sss[2][2048];
+  const bool w0 = blockIdx.x == 0;
+  if (f.nbt && w0 && threadIdx.x == 0) f.nbt[0] += 1;
+  for (int c0 = 0; c0 < C; c0 += 64)
+    bn_stats64(f.sums, f.G, M, C, c0, f.gamma, f.beta, f.eps, f.momentum, f.running_mean, f.running_var, sss[0],
+               sss[1], f.save, w0, red);
+  const int cv = C >> 3, rpb = 256 / cv;
+  const int col = threadIdx.x % cv, rsub = threadIdx.x / cv;
+  float sc[8], sh[8];
+  load8(sss[0] + col * 8, sc);
+  load8(sss[1] + col * 8, sh);
+  const int64_t rstride = (int64_t)gridDim.x * rpb;
+  for (int64_t r = (int64_t)blockIdx.x * rpb + rsub; r < M; r += kBnUnroll * rstride) {
+    bf16x8 zv[kBnUnroll], rv[kBnUnroll];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      const int64_t rr = r + u * rstride;
+      if (rr < M) {
+        zv[u] = reinterpret_cast<const bf16x8*>(z)[rr * cv + col];
+        if (kRes) rv[u] = reinterpret_cast<const bf16x8*>(res)[rr * cv + col];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      const int64_t rr = r + u * rstride;
+      if (rr < M) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float v = fmaf((float)zv[u][j], sc[j], sh[j]);
+          if (kRes) v += (float)rv[u][j];
+          if (kRelu) v = fmaxf(v, 0.f);
+          o[j] = (bf16)v;
         }
         reinterpret_cast<bf16x8*>(y)[rr * cv + col] = o;
       }
@@ -557,6 +634,162 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16* __restrict
   }
 }
 
+// ---------------------------------------------------------------- classifier head (avgpool + fc, J <= 16)
+// ResNet's head at few classes (CIFAR: 10) as one launch each way instead of the ~19 launches of
+// avgpool -> bf16 weight copy / row padding -> MFMA GEMM -> slice, and their backward (ref/example_mp.py:50:
+// torchvision resnet18(num_classes=10)).  The work is tiny (N x C x J MACs); what costs is launches.
+// Thread layout: 8 channels per thread, C/8 threads per image, 256/(C/8) images per pass.
+constexpr int kHeadMaxJ = 16;
+__global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ x, int N, int HW, int C, int J,
+                                                       const float* __restrict__ w, const float* __restrict__ b,
+                                                       float* __restrict__ pooled, float* __restrict__ logits) {
+  __shared__ float part[256][kHeadMaxJ + 1];
+  const int cv = C >> 3, ipp = 256 / cv;
+  const int col = threadIdx.x % cv, sub = threadIdx.x / cv;
+  const int n = blockIdx.x * ipp + sub;
+  const bool live = sub < ipp && n < N;
+  float acc[kHeadMaxJ];
+#pragma unroll
+  for (int j = 0; j < kHeadMaxJ; ++j) acc[j] = 0.f;
+  if (live) {
+    float s[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = 0.f;
+    const bf16x8* xr = reinterpret_cast<const bf16x8*>(x + (int64_t)n * HW * C) + col;
+    for (int i = 0; i < HW; ++i) {  // fixed order over the window
+      const bf16x8 v = xr[(int64_t)i * cv];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[k] += (float)v[k];
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] *= inv;
+    float4* pr = reinterpret_cast<float4*>(pooled + (int64_t)n * C + col * 8);
+    pr[0] = make_float4(s[0], s[1], s[2], s[3]);
+    pr[1] = make_float4(s[4], s[5], s[6], s[7]);
+#pragma unroll
+    for (int j = 0; j < kHeadMaxJ; ++j) {
+      if (j < J) {
+        float wv[8];
+        load8(w + (int64_t)j * C + col * 8, wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[j] = fmaf(s[k], wv[k], acc[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kHeadMaxJ; ++j) part[threadIdx.x][j] = acc[j];
+  __syncthreads();
+  // one thread per (image, class): the image's cv partials in column order (fixed)
+  for (int o = threadIdx.x; o < ipp * J; o += 256) {
+    const int si = o / J, j = o - si * J, nn = blockIdx.x * ipp + si;
+    if (nn >= N) continue;
+    float a = 0.f;
+    for (int c = 0; c < cv; ++c) a += part[si * cv + c][j];
+    logits[(int64_t)nn * J + j] = a + b[j];
+  }
+}
+
+// logits gradient of row r, class j: from a materialised dl, or formed from the cross-entropy forward (ce,
+// the expression of ce_bwd_kernel)
+// (branch-free: every load is issued before any of them is used - a load behind the ignore_index branch made
+// each call two dependent round trips to L2, 20 us for the dW role's 10 calls per thread)
+__device__ __forceinline__ float head_dl(const float* __restrict__ dl, const CeFuse& ce, int J, int r, int j) {
+  if (dl) return dl[(int64_t)r * J + j];
+  const int64_t y = ce.labels[r];
+  const float x = ce.logits[(int64_t)r * J + j], l = ce.lse[r];
+  const float go = ce.reduction == 0 ? ce.grad_out[r] : ce.grad_out[0] / ce.denom[0];
+  const float p = __expf(x - l);
+  const float q = (j == y ? (1.f - ce.eps) : 0.f) + ce.eps / (float)J;
+  return y == ce.ignore_index ? 0.f : (p - q) * go;
+}
+
+// Backward: workgroups [0, nb_dx) form dx (d(pooled) = dl W / HW, broadcast over the window), the
+// C/16 workgroups after them dW (16 channels each, the batch summed by 16 row groups combined in a fixed
+// order) and, in the first of those, db.  No partial sums cross workgroups: one launch, deterministic.
+constexpr int kHeadRows = 256;  // logits-gradient rows staged in LDS per chunk (dW role)
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl, CeFuse ce,
+                                                       const float* __restrict__ pooled, const float* __restrict__ w,
+                                                       int N, int HW, int C, int J, int nb_dx, bf16* __restrict__ dx,
+                                                       float* __restrict__ dw, float* __restrict__ db) {
+  __shared__ float g[kHeadRows][kHeadMaxJ];
+  if ((int)blockIdx.x < nb_dx) {
+    const int cv = C >> 3, ipp = 256 / cv;
+    const int col = threadIdx.x % cv, sub = threadIdx.x / cv;
+    const int n0 = blockIdx.x * ipp, n = n0 + sub;
+    // this workgroup's ipp x J logits gradients first (independent loads in flight), then W from L2
+    for (int o = threadIdx.x; o < ipp * J; o += 256) {
+      const int si = o / J, j = o - si * J;
+      if (n0 + si < N) g[si][j] = head_dl(dl, ce, J, n0 + si, j);
+    }
+    __syncthreads();
+    if (sub >= ipp || n >= N) return;
+    float d[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kHeadMaxJ; ++j) {
+      if (j < J) {
+        const float gj = g[sub][j];
+        float wv[8];
+        load8(w + (int64_t)j * C + col * 8, wv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = fmaf(gj, wv[k], d[k]);
+      }
+    }
+    const float inv = 1.f / (float)HW;
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (bf16)(d[k] * inv);
+    bf16x8* xr = reinterpret_cast<bf16x8*>(dx + (int64_t)n * HW * C) + col;
+    for (int i = 0; i < HW; ++i) xr[(int64_t)i * cv] = o;
+    return;
+  }
+  // dW role: 16 channels per workgroup; thread (cl = t & 15, rq = t >> 4) sums rows r = rq, rq + 16, .. of
+  // its channel for every class (independent row loads in flight), then the 16 row-group partials of each
+  // (class, channel) are combined in a fixed order through LDS
+  float (*red)[16][kHeadMaxJ] = reinterpret_cast<float (*)[16][kHeadMaxJ]>(&g[0][0]);  // [16 rq][16 cl][J]
+  const int c0 = ((int)blockIdx.x - nb_dx) * 16, cl = threadIdx.x & 15, rq = threadIdx.x >> 4;
+  const int c = c0 + cl;
+  float a[kHeadMaxJ], bsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < kHeadMaxJ; ++j) a[j] = 0.f;
+  for (int r0 = 0; r0 < N; r0 += kHeadRows) {
+    const int rows = min(kHeadRows, N - r0);
+    __syncthreads();  // the previous chunk's readers are done
+#pragma unroll 4
+    for (int e = threadIdx.x; e < rows * J; e += 256) {
+      const int r = e / J, j = e - r * J;
+      g[r][j] = head_dl(dl, ce, J, r0 + r, j);
+    }
+    __syncthreads();
+    if (c < C) {
+#pragma unroll 4
+      for (int r = rq; r < rows; r += 16) {
+        const float p = pooled[(int64_t)(r0 + r) * C + c];
+#pragma unroll
+        for (int j = 0; j < kHeadMaxJ; ++j)
+          if (j < J) a[j] = fmaf(g[r][j], p, a[j]);
+      }
+    }
+    if (blockIdx.x == nb_dx && threadIdx.x < J)
+      for (int r = 0; r < rows; ++r) bsum += g[r][threadIdx.x];
+  }
+  __syncthreads();  // g is reused as red
+#pragma unroll
+  for (int j = 0; j < kHeadMaxJ; ++j)
+    if (j < J) red[rq][cl][j] = a[j];
+  __syncthreads();
+  for (int o = threadIdx.x; o < 16 * J; o += 256) {
+    const int j = o >> 4, cc = o & 15;
+    if (c0 + cc >= C) continue;
+    float v = 0.f;
+    for (int q = 0; q < 16; ++q) v += red[q][cc][j];
+    dw[(int64_t)j * C + c0 + cc] = v;
+  }
+  if (blockIdx.x == nb_dx && threadIdx.x < J) db[threadIdx.x] = bsum;
+}
+
 __global__ __launch_bounds__(256) void add_bf16_kernel(const bf16* __restrict__ a, const bf16* __restrict__ b,
                                                        int64_t nvec, bf16* __restrict__ y) {
   for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * 256) {
@@ -649,6 +882,25 @@ void bn_prepare(const float* sums, int G, int64_t M, int C, const float* gamma, 
                                                     running_var, scale_shift, save, num_batches_tracked);
 }
 
+bool bn_fold_ok(int G, int C) {
+  return C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0 && (int64_t)G * C <= kBnFoldMax;
+}
+
+void bn_fold_act_fwd(const float* sums, int G, int64_t M, int C, const float* gamma, const float* beta, float eps,
+                     float momentum, float* running_mean, float* running_var, float* save,
+                     int64_t* num_batches_tracked, const void* z, const void* res, bool relu, void* y, hipStream_t s) {
+  const BnFold f{sums, G, gamma, beta, eps, momentum, running_mean, running_var, save, num_batches_tracked};
+  const int rpb = 256 / (C / 8);
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((M + rpb * kBnUnroll - 1) / (rpb * kBnUnroll), 2048));
+  const bf16* zb = static_cast<const bf16*>(z);
+  const bf16* rb = static_cast<const bf16*>(res);
+  bf16* yb = static_cast<bf16*>(y);
+  if (res && relu) bn_fold_act_fwd_kernel<true, true><<<grid, 256, 0, s>>>(zb, f, rb, M, C, yb);
+  else if (res) bn_fold_act_fwd_kernel<true, false><<<grid, 256, 0, s>>>(zb, f, rb, M, C, yb);
+  else if (relu) bn_fold_act_fwd_kernel<false, true><<<grid, 256, 0, s>>>(zb, f, rb, M, C, yb);
+  else bn_fold_act_fwd_kernel<false, false><<<grid, 256, 0, s>>>(zb, f, rb, M, C, yb);
+}
+
 void bn_act_fwd(const void* z, const float* ss, const void* res, bool relu, int64_t M, int C, void* y,
                 hipStream_t s) {
   const int64_t nvec = M * C / 8;
@@ -726,6 +978,22 @@ void avgpool_fwd(const void* x, int N, int HW, int C, void* y, hipStream_t s) {
 void avgpool_bwd(const void* dy, int N, int HW, int C, void* dx, hipStream_t s) {
   avgpool_bwd_kernel<<<grid_for((int64_t)N * HW * C), 256, 0, s>>>(static_cast<const bf16*>(dy), N, HW, C,
                                                                    static_cast<bf16*>(dx));
+}
+
+bool head_ok(int C, int J) { return J >= 1 && J <= kHeadMaxJ && C % 8 == 0 && C >= 8 && C <= 2048 && 256 % (C / 8) == 0; }
+
+void head_fwd(const void* x, int N, int HW, int C, int J, const float* w, const float* b, float* pooled,
+              float* logits, hipStream_t s) {
+  const int ipp = 256 / (C / 8);
+  head_fwd_kernel<<<(N + ipp - 1) / ipp, 256, 0, s>>>(static_cast<const bf16*>(x), N, HW, C, J, w, b, pooled, logits);
+}
+
+void head_bwd(const float* dl, const CeFuse* ce, const float* pooled, const float* w, int N, int HW, int C, int J,
+              void* dx, float* dw, float* db, hipStream_t s) {
+  const int ipp = 256 / (C / 8), nb_dx = (N + ipp - 1) / ipp;
+  const CeFuse c = ce ? *ce : CeFuse{};
+  head_bwd_kernel<<<nb_dx + (C + 15) / 16, 256, 0, s>>>(dl, c, pooled, w, N, HW, C, J, nb_dx, static_cast<bf16*>(dx),
+                                                        dw, db);
 }
 
 void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s) {

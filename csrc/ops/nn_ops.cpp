@@ -360,8 +360,19 @@ std::tuple<at::Tensor, at::Tensor> bn_fwd_train(const at::Tensor& z, const at::T
     RINGDP_CHECK(residual->sizes() == z.sizes(), "bn residual: shape mismatch");
     res = residual->data_ptr();
   }
-  at::Tensor ss = at::empty({2, C}, gamma.options());
   at::Tensor save = at::empty({2, C}, gamma.options());
+  // RINGDP_BN_FOLD=1: one launch, every workgroup forms the scale / shift itself.  Opt-in: the redundant
+  // per-workgroup statistics cost more than the launch they save (ResNet-18 B=256 1.913 -> 1.934 ms, ResNet-50
+  // 34.05 -> 34.43 ms; profiles/r06/rejected/bn_fold.md)
+  static const bool fold = [] { const char* v = std::getenv("RINGDP_BN_FOLD"); return v && std::atoi(v) != 0; }();
+  if (fold && kern::bn_fold_ok(G, (int)C)) {
+    at::Tensor y = at::empty_like(z);
+    kern::bn_fold_act_fwd(sums.data_ptr<float>(), G, M, (int)C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                          (float)eps, (float)momentum, rm, rv, save.data_ptr<float>(), nbt, z.data_ptr(), res, relu,
+                          y.data_ptr(), stream_of(z));
+    return {y, save};
+  }
+  at::Tensor ss = at::empty({2, C}, gamma.options());
   kern::bn_prepare(sums.data_ptr<float>(), G, M, (int)C, gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
                    (float)momentum, rm, rv, ss.data_ptr<float>(), save.data_ptr<float>(), nbt, stream_of(z));
   at::Tensor y = at::empty_like(z);
@@ -443,6 +454,55 @@ at::Tensor avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W) {
   const int64_t N = dy.size(0), C = dy.size(1);
   at::Tensor dx = at::empty({N, H, W, C}, dy.options());
   kern::avgpool_bwd(dy.data_ptr(), (int)N, (int)(H * W), (int)C, dx.data_ptr(), stream_of(dy));
+  return dx;
+}
+
+std::tuple<at::Tensor, at::Tensor> head_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b) {
+  bf16_gpu(x, "head input");
+  f32_gpu(w, "head weight");
+  f32_gpu(b, "head bias");
+  const int64_t N = x.size(0), C = x.size(-1), HW = x.numel() / (N * C), J = w.size(0);
+  RINGDP_CHECK(kern::head_ok((int)C, (int)J) && w.dim() == 2 && w.size(1) == C && b.numel() == J,
+               "head: unsupported shape (C ", C, ", classes ", J, ")");
+  at::Tensor logits = at::empty({N, J}, w.options());
+  at::Tensor pooled = at::empty({N, C}, w.options());
+  kern::head_fwd(x.data_ptr(), (int)N, (int)HW, (int)C, (int)J, w.data_ptr<float>(), b.data_ptr<float>(),
+                 pooled.data_ptr<float>(), logits.data_ptr<float>(), stream_of(x));
+  return {logits, pooled};
+}
+
+at::Tensor head_bwd(const c10::optional<at::Tensor>& dl, const c10::optional<at::Tensor>& logits,
+                    const c10::optional<at::Tensor>& labels, const c10::optional<at::Tensor>& lse,
+                    const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& grad_out,
+                    int64_t ignore_index, double eps, int64_t reduction, const at::Tensor& pooled,
+                    const at::Tensor& w, int64_t H, int64_t W, at::Tensor dw, at::Tensor db) {
+  f32_gpu(pooled, "head pooled");
+  f32_gpu(w, "head weight");
+  f32_gpu(dw, "head dweight");
+  f32_gpu(db, "head dbias");
+  const int64_t N = pooled.size(0), C = pooled.size(1), J = w.size(0);
+  RINGDP_CHECK(kern::head_ok((int)C, (int)J) && dw.sizes() == w.sizes() && db.numel() == J,
+               "head backward: unsupported shape");
+  const float* dlp = nullptr;
+  kern::CeFuse ce{};
+  at::Tensor g;
+  if (dl.has_value() && dl->defined()) {
+    f32_gpu(*dl, "head logits grad");
+    RINGDP_CHECK(dl->dim() == 2 && dl->size(0) == N && dl->size(1) == J, "head backward: dl must be [N, J]");
+    dlp = dl->data_ptr<float>();
+  } else {
+    RINGDP_CHECK(logits && labels && lse && ws && grad_out, "head backward: dl or the cross-entropy tensors");
+    f32_gpu(*logits, "head logits");
+    RINGDP_CHECK(logits->size(0) == N && logits->size(1) == J && labels->numel() == N, "head backward: CE shapes");
+    g = grad_out->to(at::kFloat).contiguous();
+    const int64_t nparts = (ws->numel() - 4) / 2;
+    ce = kern::CeFuse{logits->data_ptr<float>(), labels->data_ptr<int64_t>(), lse->data_ptr<float>(),
+                      g.data_ptr<float>(), ws->data_ptr<float>() + 2 * nparts, (int)ignore_index, (float)eps,
+                      (int)reduction};
+  }
+  at::Tensor dx = at::empty({N, H, W, C}, w.options().dtype(at::kBFloat16));
+  kern::head_bwd(dlp, dlp ? nullptr : &ce, pooled.data_ptr<float>(), w.data_ptr<float>(), (int)N, (int)(H * W),
+                 (int)C, (int)J, dx.data_ptr(), dw.data_ptr<float>(), db.data_ptr<float>(), stream_of(pooled));
   return dx;
 }
 

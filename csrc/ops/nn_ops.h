@@ -39,6 +39,15 @@ at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H,
                          int64_t stride, int64_t pad);
 at::Tensor avgpool_fwd(const at::Tensor& x);
 at::Tensor avgpool_bwd(const at::Tensor& dy, int64_t H, int64_t W);
+// classifier head at few classes (kern::head_ok): (logits fp32 [N, J], pooled fp32 [N, C])
+std::tuple<at::Tensor, at::Tensor> head_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b);
+// backward from dl [N, J], or (dl undefined) from the cross-entropy forward's (logits, labels, lse, ws, grad_out);
+// returns dx [N, H, W, C] bf16, writes dw / db
+at::Tensor head_bwd(const c10::optional<at::Tensor>& dl, const c10::optional<at::Tensor>& logits,
+                    const c10::optional<at::Tensor>& labels, const c10::optional<at::Tensor>& lse,
+                    const c10::optional<at::Tensor>& ws, const c10::optional<at::Tensor>& grad_out,
+                    int64_t ignore_index, double eps, int64_t reduction, const at::Tensor& pooled,
+                    const at::Tensor& w, int64_t H, int64_t W, at::Tensor dw, at::Tensor db);
 at::Tensor add_bf16(const at::Tensor& a, const at::Tensor& b);
 
 std::tuple<at::Tensor, at::Tensor> layernorm_fwd(const at::Tensor& x, const at::Tensor& w, const at::Tensor& b,

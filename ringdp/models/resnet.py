@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.nhwc import (AvgPoolLinear, ConvBNAct, ConvBNActFork, ConvBNActPair, MaxPoolNHWC, pack_conv_weights,
+from ..ops.nhwc import (ConvBNAct, ConvBNActFork, ConvBNActPair, MaxPoolNHWC, classifier_head, pack_conv_weights,
                         to_nhwc)
 
 # {id(conv): (krsc, crsk)} of the forward in progress (ResNet.forward_nhwc packs every conv weight in one
@@ -199,7 +199,7 @@ class ResNet(nn.Module):
                     h = blk.forward_nhwc(h)
         finally:
             _PACKED.clear()
-        return AvgPoolLinear.apply(h, self.fc.weight, self.fc.bias)
+        return classifier_head(h, self.fc)
 
 
 def resnet18(num_classes: int = 1000, **kw) -> ResNet:

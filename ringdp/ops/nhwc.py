@@ -189,6 +189,80 @@ def _pad_rows(t: torch.Tensor, rows: int) -> torch.Tensor:
     return out
 
 
+class _Head(torch.autograd.Function):
+    """Global average pool + fc at few classes (``C.head_ok``): one launch each way (nn.hip head_*_kernel).
+    Returns (logits, pooled); pooled (fp32) is what a fused cross entropy's backward needs."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        logits, pooled = C.head_fwd(x, w.detach(), b.detach())
+        ctx.mark_non_differentiable(pooled)
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(pooled, w, b)
+        ctx.hw = (x.shape[1], x.shape[2])
+        return logits, pooled
+
+    @staticmethod
+    def backward(ctx, dl, _dpooled):
+        if dl is None:
+            return None, None, None
+        pooled, w, b = ctx.saved_tensors
+        dw, db = grad_buffer(w), grad_buffer(b)
+        dx = C.head_bwd(dl.float().contiguous(), None, None, None, None, None, -100, 0.0, 1, pooled, w.detach(),
+                        *ctx.hw, dw, db)
+        n = ctx.needs_input_grad
+        return dx if n[0] else None, dw if n[1] else None, db if n[2] else None
+
+
+class _HeadCE(torch.autograd.Function):
+    """Cross entropy straight on the head (``loss = CE(fc(avgpool(x)), y)``) as one node: the backward forms
+    d(logits) inside the head's backward kernel (no ce_bwd launch, no [N, J] gradient tensor).  The forward
+    reuses the logits ``_Head`` computed; that node stays in the graph for any other use of the logits."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, logits, target, pooled, ignore_index, eps, reduction):
+        loss, lse, ws = C.cross_entropy_fwd(logits, target, ignore_index, eps, reduction)
+        ctx.save_for_backward(logits, target, lse, ws, pooled, w, b)
+        ctx.cfg = (ignore_index, eps, reduction)
+        ctx.hw = (x.shape[1], x.shape[2])
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, target, lse, ws, pooled, w, b = ctx.saved_tensors
+        dw, db = grad_buffer(w), grad_buffer(b)
+        dx = C.head_bwd(None, logits, target, lse, ws, grad_out.contiguous(), *ctx.cfg, pooled, w.detach(), *ctx.hw,
+                        dw, db)
+        n = ctx.needs_input_grad
+        return (dx if n[0] else None, dw if n[1] else None, db if n[2] else None) + (None,) * 6
+
+
+def classifier_head(x: torch.Tensor, fc) -> torch.Tensor:
+    """avgpool + fc of NHWC bf16 ``x`` -> fp32 logits: the one-launch head at few classes, else the GEMM path."""
+    if fc.bias is not None and C.head_ok(x.shape[-1], fc.out_features):
+        logits, pooled = _Head.apply(x, fc.weight, fc.bias)
+        if logits.requires_grad:
+            # what ringdp's cross entropy needs to fuse itself into the head (head_cross_entropy)
+            logits._ringdp_rhead = (x, fc.weight, fc.bias, pooled, logits._version, logits.grad_fn)
+        return logits
+    return AvgPoolLinear.apply(x, fc.weight, fc.bias)
+
+
+def head_cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int, eps: float,
+                       reduction: int):
+    """The fused head + cross entropy node when ``logits`` is the untouched output of ``classifier_head``'s
+    one-launch head, else None.  Called by ringdp.ops.loss.cross_entropy."""
+    head = getattr(logits, "_ringdp_rhead", None)
+    if head is None or not torch.is_grad_enabled() or not logits.requires_grad:
+        return None
+    if target.dim() != 1 or target.shape[0] != logits.shape[0] or not target.is_cuda:
+        return None
+    x, w, b, pooled, version, node = head
+    if logits._version != version or logits.grad_fn is not node or logits.retains_grad or logits._backward_hooks:
+        return None
+    return _HeadCE.apply(x, w, b, logits.detach(), target.long().contiguous(), pooled, ignore_index, eps, reduction)
+
+
 class AvgPoolLinear(torch.autograd.Function):
     """Global average pool (NHWC bf16) + fully connected head -> fp32 logits."""
 

@@ -207,6 +207,41 @@ def test_pools():
                                atol=1e-3)
 
 
+@pytest.mark.parametrize("N,HW,Cc,J", [(256, 1, 512, 10), (37, 16, 512, 10), (64, 49, 2048, 16), (300, 4, 64, 3)])
+@pytest.mark.parametrize("fused_ce", [False, True])
+def test_classifier_head_matches_fp32(N, HW, Cc, J, fused_ce):
+    """One-launch avgpool + fc head (nn.hip head_fwd / head_bwd) against fp32 PyTorch; with ringdp's cross
+    entropy the loss is the fused head node (d(logits) formed inside the head backward)."""
+    from ringdp.ops.loss import cross_entropy
+    from ringdp.ops.nhwc import classifier_head
+
+    torch.manual_seed(5)
+    h = int(HW ** 0.5)
+    fc = torch.nn.Linear(Cc, J).cuda()
+    x = torch.randn(N, h, h, Cc, device="cuda").bfloat16().requires_grad_()
+    y = torch.randint(0, J, (N,), device="cuda")
+    y[3] = -100  # an ignored row
+    logits = classifier_head(x, fc)
+    xr = x.detach().float().requires_grad_()
+    fr = torch.nn.Linear(Cc, J).cuda()
+    fr.load_state_dict(fc.state_dict())
+    ref = fr(xr.mean((1, 2)))
+    torch.testing.assert_close(logits, ref, rtol=1e-4, atol=1e-4)
+    if fused_ce:
+        loss = cross_entropy(logits, y, label_smoothing=0.1)
+        assert type(loss.grad_fn).__name__ == "_HeadCEBackward", loss.grad_fn
+    else:
+        loss = F.cross_entropy(logits, y, label_smoothing=0.1)
+    lref = F.cross_entropy(ref, y, label_smoothing=0.1)
+    torch.testing.assert_close(loss, lref, rtol=1e-4, atol=1e-5)
+    loss.backward()
+    lref.backward()
+    torch.testing.assert_close(fc.weight.grad, fr.weight.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(fc.bias.grad, fr.bias.grad, rtol=1e-4, atol=1e-6)
+    # dx is bf16 (one rounding of an fp32 value)
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=1e-2, atol=1e-6)
+
+
 def _cos(a, b):
     return float(F.cosine_similarity(a.reshape(1, -1).float(), b.reshape(1, -1).float()))
 
