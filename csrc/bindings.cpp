@@ -625,6 +625,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("f32_conv_dgrad", &ops::f32_conv_dgrad);
   m.def("f32_conv_wgrad", &ops::f32_conv_wgrad, py::arg("dz"), py::arg("x"), py::arg("pad"), py::arg("mean"),
         py::arg("std"), py::arg("dw"), py::arg("db"));
+  m.def("f32_conv_wgrad_slab", &ops::f32_conv_wgrad_slab, py::arg("dz"), py::arg("x"), py::arg("pad"),
+        py::arg("mean"), py::arg("std"), py::arg("dw"), py::arg("with_bias"),
+        "weight-gradient GEMM with its reduction deferred: (slab, [slices, Kout, Nw, ncol])");
+  m.def("f32_conv1_wgrad_slab", &ops::f32_conv1_wgrad_slab);
+  m.def("f32_slab_reduce_multi", &ops::f32_slab_reduce_multi,
+        "the deferred weight-gradient reductions of several layers in one launch");
   m.def("f32_pool_relu_fwd", &ops::f32_pool_relu_fwd);
   m.def("f32_pool_relu_bwd", &ops::f32_pool_relu_bwd);
   m.def("cn_pack_weights", &ops::cn_pack_weights, py::arg("w1"), py::arg("w2"), py::arg("w3"), py::arg("wfc"),

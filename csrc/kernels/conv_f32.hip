@@ -853,6 +853,53 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// f32_slab_reduce of up to kF32RedMax segments in one launch: element e of a segment is the sum of its slices in
+// the two-stage order of slab_group_kernel + wgrad_reduce_kernel (groups of kSlabGroup slices summed from 0.f,
+// then the group sums in order; one group: the slices in order) - the same bits, done by one thread.
+struct F32RedArgs {
+  F32RedSeg seg[kF32RedMax];
+  int start[kF32RedMax + 1];
+  int n;
+};
+__global__ __launch_bounds__(256) void f32_reduce_multi_kernel(F32RedArgs a) {
+  __shared__ F32RedSeg ss[kF32RedMax];
+  __shared__ int st[kF32RedMax + 1];
+  // compile-time indices into the by-value argument (a run-time index would copy it to scratch per thread)
+#pragma unroll
+  for (int i = 0; i < kF32RedMax; ++i)
+    if ((int)threadIdx.x == i) ss[i] = a.seg[i];
+#pragma unroll
+  for (int i = 0; i <= kF32RedMax; ++i)
+    if ((int)threadIdx.x == i) st[i] = a.start[i];
+  __syncthreads();
+  const int total_all = st[a.n];
+  int k = 0;
+  for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < total_all;
+       i += static_cast<int>(gridDim.x * blockDim.x)) {
+    while (k + 1 < a.n && i >= st[k + 1]) ++k;
+    const F32RedSeg sg = ss[k];
+    const int e = i - st[k], total = sg.Kout * sg.ncol;
+    float acc;
+    if (sg.slices > kSlabGroup) {
+      acc = 0.f;
+      for (int g0 = 0; g0 < sg.slices; g0 += kSlabGroup) {
+        const int g1 = min(g0 + kSlabGroup, sg.slices);
+        float p = 0.f;
+#pragma unroll 8
+        for (int z = g0; z < g1; ++z) p += sg.slab[static_cast<int64_t>(z) * total + e];
+        acc = g0 == 0 ? p : acc + p;
+      }
+    } else {
+      acc = sg.slab[e];
+#pragma unroll 8
+      for (int z = 1; z < sg.slices; ++z) acc += sg.slab[static_cast<int64_t>(z) * total + e];
+    }
+    const int m = e / sg.ncol, n = e - m * sg.ncol;
+    if (n < sg.Nw) sg.dw[m * sg.Nw + n] = acc;
+    else sg.db[m] = acc;
+  }
+}
+
 // dx = sum over the split-K planes of NCHWSlabOut, in plane order (deterministic); n4 = plane / 4
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float4* __restrict__ slab, int slices, int n4,
                                                        float4* __restrict__ out) {
@@ -2031,19 +2078,25 @@ void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float
 }
 
 void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const unsigned char* xu8, float mean,
-                    float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s) {
+                    float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s, F32RedList* defer) {
+  auto reduce = [&](int n, int Kout, int Nw, int ncol) {
+    if (defer)
+      defer->push_back(F32RedSeg{slab, n, Kout, Nw, ncol, dw, db});
+    else
+      f32_slab_reduce(slab, n, Kout, Nw, ncol, dw, db, s);
+  };
   const int Nw = g.C * g.R * g.R;
   const int ncol = Nw + (db ? 1 : 0);
   if (!xu8 && db && conv3_wgrad_f32_ok(g)) {  // the ConvNet's conv3 / conv2 at large batches: dedicated kernels
     hipLaunchKernelGGL(conv3_wgrad_f32_kernel, dim3(4 * W3_SLICES), dim3(256), 0, s, dz, x, slab,
                        static_cast<int>(g.B));
-    f32_slab_reduce(slab, W3_SLICES, g.Kout, Nw, ncol, dw, db, s);
+    reduce(W3_SLICES, g.Kout, Nw, ncol);
     return;
   }
   if (!xu8 && db && conv2_wgrad_f32_ok(g)) {
     hipLaunchKernelGGL(conv2_wgrad_f32_kernel, dim3(2 * W2_SLICES), dim3(256), 0, s, dz, x, slab,
                        static_cast<int>(g.B));
-    f32_slab_reduce(slab, W2_SLICES, g.Kout, Nw, ncol, dw, db, s);
+    reduce(W2_SLICES, g.Kout, Nw, ncol);
     return;
   }
   const int64_t xin = static_cast<int64_t>(g.C) * g.H * g.W, zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
@@ -2079,7 +2132,7 @@ void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const
   }
   // the slab holds conv_f32_wgrad_slices(g) = (slices of all chunks) + their group count >= used + groups
   (void)slices;
-  f32_slab_reduce(slab, used, g.Kout, Nw, ncol, dw, db, s);
+  reduce(used, g.Kout, Nw, ncol);
 }
 
 int f32_slab_capacity(int slices) { return slices + (slices + kSlabGroup - 1) / kSlabGroup; }
@@ -2096,6 +2149,24 @@ void f32_slab_reduce(float* slab, int slices, int Kout, int Nw, int ncol, float*
     src = part;
   }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_1d(total)), dim3(256), 0, s, src, nsum, Kout, Nw, ncol, dw, db);
+}
+
+void f32_slab_reduce_multi(const F32RedList& segs, hipStream_t s) {
+  if (segs.empty()) return;
+  if ((int)segs.size() > kF32RedMax) {
+    for (const auto& g : segs)
+      f32_slab_reduce(const_cast<float*>(g.slab), g.slices, g.Kout, g.Nw, g.ncol, g.dw, g.db, s);
+    return;
+  }
+  F32RedArgs a{};
+  a.n = static_cast<int>(segs.size());
+  a.start[0] = 0;
+  for (int i = 0; i < a.n; ++i) {
+    a.seg[i] = segs[i];
+    a.start[i + 1] = a.start[i] + segs[i].Kout * segs[i].ncol;
+  }
+  for (int i = a.n + 1; i <= kF32RedMax; ++i) a.start[i] = a.start[a.n];
+  hipLaunchKernelGGL(f32_reduce_multi_kernel, dim3(grid_1d(a.start[a.n])), dim3(256), 0, s, a);
 }
 
 void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,

@@ -949,6 +949,13 @@ __device__ __forceinline__ void ff_pool2(const bf16* Cs, bf16* X3b, bf16* __rest
   }
 }
 
+// software-pipelined A-fragment reads in the conv2 (producer) / conv3 (consumer) k-step loops (A/B build macros)
+#ifndef RINGDP_FF_KPIPE
+#define RINGDP_FF_KPIPE 0
+#endif
+#ifndef RINGDP_FF_PPIPE
+#define RINGDP_FF_PPIPE 0
+#endif
 template <bool U8, bool PACK>
 __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__ xin, const bf16* __restrict__ packed,
                             const PackSrc& ws, const float* __restrict__ b1, const float* __restrict__ b2,
@@ -1056,6 +1063,36 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
       if (nb < B) c1_store<U8, 8, XC_W, C1F_CS>(XS, tid, pu, pf, mean, inv_std, in_scale);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) acc[mt][0] = acc[mt][1] = zero_f32x4();
+#if RINGDP_FF_PPIPE
+      // software-pipelined as the consumer's conv3 k-steps (RINGDP_FF_KPIPE)
+      {
+        auto a2_of = [&](int ks, int mt) {
+          const int shift = (ks / 3) * 13 + ks % 3;
+          return *reinterpret_cast<const bf16x8*>(X2 + (base2[mt] + shift) * C2_XRS + q8);
+        };
+        bf16x8 cur[4], nxt[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) cur[mt] = a2_of(0, mt);
+#pragma unroll
+        for (int ks = 0; ks < 9; ++ks) {
+          if (ks + 1 < 9) {
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) nxt[mt] = a2_of(ks + 1, mt);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int mt = 0; mt < 4; ++mt) {
+            acc[mt][0] = mfma16x16x32(bw2[0][ks], cur[mt], acc[mt][0]);
+            acc[mt][1] = mfma16x16x32(bw2[1][ks], cur[mt], acc[mt][1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 1 < 9) {
+#pragma unroll
+            for (int mt = 0; mt < 4; ++mt) cur[mt] = nxt[mt];
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int ks = 0; ks < 9; ++ks) {
         const int shift = (ks / 3) * 13 + ks % 3;
@@ -1066,6 +1103,7 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
           acc[mt][1] = mfma16x16x32(bw2[1][ks], a, acc[mt][1]);
         }
       }
+#endif
       // a1 / idx1 to HBM while the MFMAs drain
       uint4* og = reinterpret_cast<uint4*>(a1 + (int64_t)b * C1A_IMG);
       for (int c = tid; c < C1A_IMG / 8; c += 256)
@@ -1154,6 +1192,39 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
   };
   f32x4 acc[4][2];
   // conv3 k-steps [k0, k1) of the image in buffer xb
+#if RINGDP_FF_KPIPE
+  // software-pipelined: the next k-step's 4 A fragments are read before this k-step's 8 MFMAs (sched_barrier
+  // pins the order), so each LDS read has 8 MFMAs (128 cycles) to land instead of being waited on at once
+  auto a_of = [&](const bf16* xb, int ks, int mt) {
+    const int tap = ks >> 1, c0 = (ks & 1) * 32;
+    const int shift = (tap / 3) * 10 + tap % 3;
+    return *reinterpret_cast<const bf16x8*>(xb + (base[mt] + shift) * C3F_XRS + c0 + q8);
+  };
+  auto mfma_ks = [&](const bf16* xb, auto k0c, auto k1c) {
+    constexpr int k0 = decltype(k0c)::value, k1 = decltype(k1c)::value;
+    bf16x8 cur[4], nxt[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) cur[mt] = a_of(xb, k0, mt);
+#pragma unroll
+    for (int ks = k0; ks < k1; ++ks) {
+      if (ks + 1 < k1) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) nxt[mt] = a_of(xb, ks + 1, mt);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        acc[mt][0] = mfma16x16x32(cur[mt], bw[0][ks], acc[mt][0]);
+        acc[mt][1] = mfma16x16x32(cur[mt], bw[1][ks], acc[mt][1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < k1) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) cur[mt] = nxt[mt];
+      }
+    }
+  };
+#else
   auto mfma_ks = [&](const bf16* xb, auto k0c, auto k1c) {
 #pragma unroll
     for (int ks = decltype(k0c)::value; ks < decltype(k1c)::value; ++ks) {
@@ -1167,6 +1238,7 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
       }
     }
   };
+#endif
   // Step s: pool3 / fc1-partials epilogue of image s-2 and the first 4 k-steps of image s-1 (phase 1,
   // beside the producer's MFMA-light conv1), fc1 reduction of s-2 + k-steps 4-10 (phase 2), k-steps
   // 11-17 (phase 3, beside the producer's VALU-only pool2): the MFMA pipe has work in every phase.

@@ -128,12 +128,25 @@ void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float
                     hipStream_t s);
 // split-K weight (+ bias, when db != nullptr) gradient; slab: slices * Kout * (C*R*R + 1) floats
 int conv_f32_wgrad_slices(const ConvF32Geom& g);
+// One fixed-order slab reduction (f32_slab_reduce) as a segment of a multi-segment launch
+struct F32RedSeg {
+  const float* slab;
+  int slices, Kout, Nw, ncol;
+  float* dw;
+  float* db;
+};
+using F32RedList = std::vector<F32RedSeg>;
+// defer != null: the reduction is appended to *defer instead of launched (f32_slab_reduce_multi later)
 void conv_f32_wgrad(const ConvF32Geom& g, const float* dz, const float* x, const unsigned char* xu8, float mean,
-                    float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s);
+                    float inv_std, float* slab, int slices, float* dw, float* db, hipStream_t s,
+                    F32RedList* defer = nullptr);
 // Fixed-order sum of split-K slabs [slices][Kout][ncol] into dw [Kout][Nw] and (column Nw) db;
 // the slab must hold f32_slab_capacity(slices) slices (room for the stage-1 group sums).
 int f32_slab_capacity(int slices);
 void f32_slab_reduce(float* slab, int slices, int Kout, int Nw, int ncol, float* dw, float* db, hipStream_t s);
+// every segment's f32_slab_reduce in ONE launch (at most kF32RedMax segments), bit-identical to the two-stage form
+constexpr int kF32RedMax = 8;
+void f32_slab_reduce_multi(const F32RedList& segs, hipStream_t s);
 // The ConvNet's conv1 (1->32, 5x5, pad 1, 28x28) + bias + ReLU + 2x2/s2 max-pool at fp32
 // (conv1_f32.hip): a1 [B][32][13][13] and its argmax code; and its weight + bias gradient from the
 // pooled gradient da1 and the code (the pool backward is folded in): per-workgroup partials in slab

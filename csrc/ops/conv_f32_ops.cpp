@@ -204,6 +204,81 @@ void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, doub
                        util::stream_of(dz));
 }
 
+// Deferred weight gradients (the whole-network fp32 cross-entropy node, ringdp/ops/convnet_fp32.py): the GEMM /
+// kernel runs now, its fixed-order slab reduction is returned as (slab, [slices, Kout, Nw, ncol]) and launched
+// later by f32_slab_reduce_multi together with the other layers' (one launch per backward).
+std::tuple<at::Tensor, std::vector<int64_t>> f32_conv_wgrad_slab(const at::Tensor& dz, const at::Tensor& x,
+                                                                 int64_t pad, double mean, double std,
+                                                                 const at::Tensor& dw, bool with_bias) {
+  check_input(x);
+  util::f32_gpu(dz, "conv_f32 dz");
+  util::f32_gpu(dw, "conv_f32 dw");
+  auto g = geom(x, dw, pad);
+  RINGDP_CHECK(dz.dim() == 4 && dz.size(0) == g.B && dz.size(1) == g.Kout && dz.size(2) == g.OH &&
+                   dz.size(3) == g.OW,
+               "conv_f32 wgrad: dz has shape ", dz.sizes());
+  const int slices = kern::conv_f32_wgrad_slices(g);
+  auto slab = at::empty({static_cast<int64_t>(slices) * g.Kout * (g.C * g.R * g.R + 1)}, dz.options());
+  const bool u8 = x.scalar_type() == at::kByte;
+  kern::F32RedList segs;
+  // dw / db pointers are not used by a deferred call (f32_slab_reduce_multi gets them from the caller)
+  float dummy_db = 0.f;
+  kern::conv_f32_wgrad(g, dz.data_ptr<float>(), u8 ? nullptr : x.data_ptr<float>(),
+                       u8 ? x.data_ptr<uint8_t>() : nullptr, static_cast<float>(mean), static_cast<float>(1.0 / std),
+                       slab.data_ptr<float>(), slices, nullptr, with_bias ? &dummy_db : nullptr, util::stream_of(dz),
+                       &segs);
+  RINGDP_CHECK(segs.size() == 1, "conv_f32 wgrad: expected one deferred reduction");
+  const auto& q = segs[0];
+  return {slab, {q.slices, q.Kout, q.Nw, q.ncol}};
+}
+
+std::tuple<at::Tensor, std::vector<int64_t>> f32_conv1_wgrad_slab(const at::Tensor& x, const at::Tensor& da1,
+                                                                  const at::Tensor& code1, double mean, double std) {
+  check_input(x);
+  RINGDP_CHECK(x.dim() == 4 && x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28,
+               "f32 conv1: [B, 1, 28, 28] input expected, got ", x.sizes());
+  util::f32_gpu(da1, "conv1 pooled grad");
+  const int64_t B = x.size(0);
+  RINGDP_CHECK(da1.sizes() == at::IntArrayRef({B, 32, 13, 13}) && code1.sizes() == da1.sizes() &&
+                   code1.scalar_type() == at::kByte,
+               "f32 conv1 wgrad: pooled grad / code must be [B, 32, 13, 13]");
+  const int blocks = kern::conv1_f32_wgrad_blocks(B);
+  auto slab = at::empty({static_cast<int64_t>(kern::f32_slab_capacity(blocks)) * 32 * 26}, da1.options());
+  const bool u8 = x.scalar_type() == at::kByte;
+  auto xc = x.contiguous();
+  auto dac = da1.contiguous();
+  kern::conv1_wgrad_f32(u8 ? nullptr : xc.data_ptr<float>(), u8 ? xc.data_ptr<uint8_t>() : nullptr, B,
+                        static_cast<float>(mean), static_cast<float>(1.0 / std), dac.data_ptr<float>(),
+                        code1.data_ptr<uint8_t>(), slab.data_ptr<float>(), util::stream_of(da1));
+  return {slab, {blocks, 32, 25, 26}};
+}
+
+void f32_slab_reduce_multi(const std::vector<at::Tensor>& slabs, const std::vector<std::vector<int64_t>>& meta,
+                           const std::vector<at::Tensor>& dws, const std::vector<c10::optional<at::Tensor>>& dbs) {
+  RINGDP_CHECK(slabs.size() == meta.size() && slabs.size() == dws.size() && slabs.size() == dbs.size(),
+               "f32_slab_reduce_multi: one slab, meta, dw and db per segment");
+  if (slabs.empty()) return;
+  kern::F32RedList segs;
+  for (size_t i = 0; i < slabs.size(); ++i) {
+    const auto& m = meta[i];
+    RINGDP_CHECK(m.size() == 4, "f32_slab_reduce_multi: meta is [slices, Kout, Nw, ncol]");
+    util::f32_gpu(slabs[i], "slab");
+    util::f32_gpu(dws[i], "dw");
+    RINGDP_CHECK(dws[i].numel() == m[1] * m[2] && slabs[i].numel() >= m[0] * m[1] * m[3],
+                 "f32_slab_reduce_multi: segment ", i, " does not match its slab / dw");
+    float* db = nullptr;
+    if (m[3] > m[2]) {
+      RINGDP_CHECK(dbs[i].has_value() && dbs[i]->defined() && dbs[i]->numel() == m[1],
+                   "f32_slab_reduce_multi: segment ", i, " has a bias column but no db");
+      util::f32_gpu(*dbs[i], "db");
+      db = dbs[i]->data_ptr<float>();
+    }
+    segs.push_back(kern::F32RedSeg{slabs[i].data_ptr<float>(), static_cast<int>(m[0]), static_cast<int>(m[1]),
+                                   static_cast<int>(m[2]), static_cast<int>(m[3]), dws[i].data_ptr<float>(), db});
+  }
+  kern::f32_slab_reduce_multi(segs, util::stream_of(slabs[0]));
+}
+
 std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_t k, int64_t stride) {
   util::f32_gpu(z, "pool_relu_f32 input");
   RINGDP_CHECK(z.dim() == 4, "pool_relu_f32: 4-d input expected");

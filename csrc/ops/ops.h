@@ -128,6 +128,13 @@ void f32_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tenso
 at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad);
 void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
                     at::Tensor& dw, const c10::optional<at::Tensor>& db);
+std::tuple<at::Tensor, std::vector<int64_t>> f32_conv_wgrad_slab(const at::Tensor& dz, const at::Tensor& x,
+                                                                 int64_t pad, double mean, double std,
+                                                                 const at::Tensor& dw, bool with_bias);
+std::tuple<at::Tensor, std::vector<int64_t>> f32_conv1_wgrad_slab(const at::Tensor& x, const at::Tensor& da1,
+                                                                  const at::Tensor& code1, double mean, double std);
+void f32_slab_reduce_multi(const std::vector<at::Tensor>& slabs, const std::vector<std::vector<int64_t>>& meta,
+                           const std::vector<at::Tensor>& dws, const std::vector<c10::optional<at::Tensor>>& dbs);
 std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_t k, int64_t stride);
 at::Tensor f32_pool_relu_bwd(const at::Tensor& da, const at::Tensor& code, int64_t H, int64_t W, int64_t k,
                              int64_t stride);

@@ -13,6 +13,8 @@ the fused bf16 fast path; this module is what ``ConvNet(precision="fp32")`` and
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .._native import C
@@ -64,10 +66,13 @@ class _ConvPoolF32(torch.autograd.Function):
         ctx.params = (w, b)
         ctx.cfg = (pad, mean, std, stride)
         ctx.mark_non_differentiable(code)
-        return a
+        ctx.set_materialize_grads(False)
+        return a, code
 
     @staticmethod
-    def backward(ctx, da):
+    def backward(ctx, da, _dcode):
+        if da is None:
+            return (None,) * 7
         x, code = ctx.saved_tensors
         w, b = ctx.params
         pad, mean, std, stride = ctx.cfg
@@ -93,10 +98,13 @@ class _Conv1PoolF32(torch.autograd.Function):
         ctx.params = (w, b)
         ctx.cfg = (mean, std)
         ctx.mark_non_differentiable(code)
-        return a
+        ctx.set_materialize_grads(False)
+        return a, code
 
     @staticmethod
-    def backward(ctx, da):
+    def backward(ctx, da, _dcode):
+        if da is None:
+            return (None,) * 5
         x, code = ctx.saved_tensors
         w, b = ctx.params
         mean, std = ctx.cfg
@@ -120,6 +128,80 @@ class _PoolReLUF32(torch.autograd.Function):
         return C.f32_pool_relu_bwd(da.contiguous(), code, H, W, k, st), None, None
 
 
+# Batches up to RINGDP_F32_NET_NODE_MAX_B (4096; 0 disables): ringdp's cross entropy on these logits is ONE autograd
+# node over the whole network (_NetCEF32) whose backward runs every layer's gradient kernels and then a single
+# launch for all of their weight-gradient reductions (instead of one or two per layer).  Above it the per-layer
+# nodes stay, so DDP can all-reduce the fc1 / conv3 bucket while conv2 / conv1 backward still run.
+_NET_NODE_MAX_B = int(os.environ.get("RINGDP_F32_NET_NODE_MAX_B", "4096"))
+
+
+class _NetCEF32(torch.autograd.Function):
+    """Cross entropy on the fp32 ConvNet's logits as one node over every layer (small batches).
+
+    The forward reuses the logits and activations of the per-layer forward.  The backward is the per-layer
+    backward's kernel sequence (cross-entropy gradient, fc1, pool3, conv3, pool2, conv2, conv1 - same kernels,
+    same fixed-order reductions, so the same bits), except that the weight-gradient reductions of all four
+    layers run as one launch at the end.  Deferral is safe by construction: every gradient this node returns
+    is written before it returns, and autograd reads a node's gradients only after it returns."""
+
+    @staticmethod
+    def forward(ctx, w1, b1, w2, b2, w3, b3, wfc, bfc, logits, target, saved, ignore_index, eps, reduction):
+        loss, lse, ws = C.cross_entropy_fwd(logits, target, ignore_index, eps, reduction)
+        ctx.save_for_backward(logits, target, lse, ws)
+        ctx.saved_acts = saved
+        ctx.params = (w1, b1, w2, b2, w3, b3, wfc, bfc)
+        ctx.cfg = (ignore_index, eps, reduction)
+        return loss
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        logits, target, lse, ws = ctx.saved_tensors
+        x, a1, code1, a2, code2, a3, code3, mean, std = ctx.saved_acts
+        w1, b1, w2, b2, w3, b3, wfc, bfc = ctx.params
+        B = logits.shape[0]
+        grads = [grad_buffer(p) for p in (w1, b1, w2, b2, w3, b3, wfc, bfc)]
+        dw1, db1, dw2, db2, dw3, db3, dwfc, dbfc = grads
+        dl = C.cross_entropy_bwd(logits, target, lse, ws, grad_out.contiguous(), *ctx.cfg)
+        segs = []
+        # fc1 (a 1x1 conv over the flattened 2048-vector)
+        dz = dl.view(B, -1, 1, 1)
+        x3 = a3.reshape(B, -1, 1, 1)
+        wfc4 = wfc.detach().view(wfc.shape[0], -1, 1, 1)
+        da3 = C.f32_conv_dgrad(dz, wfc4, 1, 1, 0)
+        segs.append(C.f32_conv_wgrad_slab(dz, x3, 0, 0.0, 1.0, dwfc.view(wfc4.shape), True) + (dwfc, dbfc))
+        # pool3 + conv3
+        dz3 = C.f32_pool_relu_bwd(da3.view(a3.shape), code3, 2 * a3.shape[2], 2 * a3.shape[3], 2, 2)
+        da2 = C.f32_conv_dgrad(dz3, w3.detach(), a2.shape[2], a2.shape[3], 0)
+        segs.append(C.f32_conv_wgrad_slab(dz3, a2, 0, 0.0, 1.0, dw3, True) + (dw3, db3))
+        # pool2 (2x2 / s1) + conv2
+        dz2 = C.f32_pool_relu_bwd(da2, code2, a2.shape[2] + 1, a2.shape[3] + 1, 2, 1)
+        da1 = C.f32_conv_dgrad(dz2, w2.detach(), a1.shape[2], a1.shape[3], 0)
+        segs.append(C.f32_conv_wgrad_slab(dz2, a1, 0, 0.0, 1.0, dw2, True) + (dw2, db2))
+        # conv1 (+ pool1, folded into its weight gradient)
+        segs.append(C.f32_conv1_wgrad_slab(x, da1, code1, mean, std) + (dw1, db1))
+        C.f32_slab_reduce_multi([sg[0] for sg in segs], [sg[1] for sg in segs], [sg[2] for sg in segs],
+                                [sg[3] for sg in segs])
+        n = ctx.needs_input_grad
+        return tuple(g if need else None for g, need in zip(grads, n[:8])) + (None,) * 6
+
+
+def head_cross_entropy_fp32(logits: torch.Tensor, target: torch.Tensor, ignore_index: int, eps: float,
+                            reduction: int):
+    """The whole-network fp32 node when ``logits`` is the untouched output of ``convnet_forward_fp32`` at a small
+    batch, else None.  Called by ringdp.ops.loss.cross_entropy."""
+    net = getattr(logits, "_ringdp_net32", None)
+    if net is None or not torch.is_grad_enabled() or not logits.requires_grad:
+        return None
+    if target.dim() != 1 or target.shape[0] != logits.shape[0] or not target.is_cuda:
+        return None
+    params, saved, version, node = net
+    if logits._version != version or logits.grad_fn is not node or logits.retains_grad or logits._backward_hooks:
+        return None
+    if not all(p.requires_grad for p in params):
+        return None
+    return _NetCEF32.apply(*params, logits.detach(), target.long().contiguous(), saved, ignore_index, eps, reduction)
+
+
 def convnet_forward_fp32(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Tensor:
     """fp32 GPU forward of the reference ConvNet (ref/launch_dist.py:35-41): uint8 pixels
     (normalised in conv1's loads) or already-normalised float input; fp32 logits [B, 10]."""
@@ -129,10 +211,18 @@ def convnet_forward_fp32(x: torch.Tensor, conv1, conv2, conv3, fc1) -> torch.Ten
         x = x.float()
         mean, std = 0.0, 1.0
     x = x.contiguous()
-    if x.shape[1:] == (1, 28, 28) and conv1.bias is not None and not x.requires_grad:
-        a = _Conv1PoolF32.apply(x, conv1.weight, conv1.bias, mean, std)
+    dedicated1 = x.shape[1:] == (1, 28, 28) and conv1.bias is not None and not x.requires_grad
+    if dedicated1:
+        a1, code1 = _Conv1PoolF32.apply(x, conv1.weight, conv1.bias, mean, std)
     else:
-        a = _ConvPoolF32.apply(x, conv1.weight, conv1.bias, 1, mean, std)
-    a = _ConvPoolF32.apply(a, conv2.weight, conv2.bias, 0, 0.0, 1.0, 1)
-    a = _ConvPoolF32.apply(a, conv3.weight, conv3.bias, 0, 0.0, 1.0)
-    return _ConvF32.apply(a.reshape(a.shape[0], -1), fc1.weight, fc1.bias, 0, 0.0, 1.0)
+        a1, code1 = _ConvPoolF32.apply(x, conv1.weight, conv1.bias, 1, mean, std)
+    a2, code2 = _ConvPoolF32.apply(a1, conv2.weight, conv2.bias, 0, 0.0, 1.0, 1)
+    a3, code3 = _ConvPoolF32.apply(a2, conv3.weight, conv3.bias, 0, 0.0, 1.0)
+    logits = _ConvF32.apply(a3.reshape(a3.shape[0], -1), fc1.weight, fc1.bias, 0, 0.0, 1.0)
+    if (logits.requires_grad and dedicated1 and x.shape[0] <= _NET_NODE_MAX_B and a3.shape[1:] == (128, 4, 4)
+            and all(m.bias is not None for m in (conv2, conv3, fc1))):
+        # what ringdp's cross entropy needs to run the whole backward as one node (head_cross_entropy_fp32)
+        params = (conv1.weight, conv1.bias, conv2.weight, conv2.bias, conv3.weight, conv3.bias, fc1.weight, fc1.bias)
+        saved = (x, a1.detach(), code1, a2.detach(), code2, a3.detach(), code3, mean, std)
+        logits._ringdp_net32 = (params, saved, logits._version, logits.grad_fn)
+    return logits

@@ -29,8 +29,9 @@ def cross_entropy(logits: torch.Tensor, target: torch.Tensor, ignore_index: int 
                   label_smoothing: float = 0.0, reduction: str = "mean") -> torch.Tensor:
     if logits.is_cuda and logits.dim() == 2 and target.dim() == 1:
         from .convnet import head_cross_entropy
+        from .convnet_fp32 import head_cross_entropy_fp32
         from .nhwc import head_cross_entropy as classifier_head_cross_entropy
-        for hook in (head_cross_entropy, classifier_head_cross_entropy):
+        for hook in (head_cross_entropy, head_cross_entropy_fp32, classifier_head_cross_entropy):
             fused = hook(logits, target, ignore_index, float(label_smoothing), _RED[reduction])
             if fused is not None:
                 return fused

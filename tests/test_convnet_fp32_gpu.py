@@ -252,6 +252,34 @@ def test_fp32_convnet_matches_aten(B):
             assert rel < 5e-3, (n, rel)
 
 
+@pytest.mark.parametrize("B", [100, 700])
+def test_fp32_net_node_matches_per_layer_backward(B):
+    """ringdp's cross entropy on the fp32 model at a small batch is ONE node over the whole network (one
+    weight-gradient reduction launch); its gradients must equal the per-layer backward's bit for bit (same kernels,
+    same fixed-order reductions), and the loss value too."""
+    from ringdp.ops.loss import _CrossEntropy, cross_entropy
+
+    m_a, _ = _models(3)
+    m_b, _ = _models(3)
+    x = torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device=DEV)
+    y = torch.randint(0, 10, (B,), device=DEV)
+    y[1] = -100
+    la = cross_entropy(m_a(x), y, label_smoothing=0.05)
+    assert type(la.grad_fn).__name__ == "_NetCEF32Backward", la.grad_fn
+    # the same cross-entropy kernels without the fusion hook: the per-layer nodes
+    lb = _CrossEntropy.apply(m_b(x), y, -100, 0.05, "mean")
+    la.backward()
+    lb.backward()
+    assert torch.equal(la.detach(), lb.detach())
+    for (n, p), q in zip(m_a.named_parameters(), m_b.parameters()):
+        assert torch.equal(p.grad, q.grad), n
+    # another use of the logits keeps the per-layer path (gradients through both are summed by autograd)
+    m_c, _ = _models(3)
+    out = m_c(x)
+    (cross_entropy(out, y) + out.square().mean()).backward()
+    assert all(p.grad is not None for p in m_c.parameters())
+
+
 def _trajectory(model, forward, steps, xs, ys, lr):
     from ringdp.optim import SGD
 
