@@ -861,9 +861,15 @@ struct F32RedArgs {
   int start[kF32RedMax + 1];
   int n;
 };
+// Work item = (element, group of kSlabGroup slices): 32 elements x 8 group lanes per workgroup; lane q sums groups
+// q, q + 8, .. (each group's slices loaded at once, added in order from 0.f) into LDS, then lane 0 adds the group
+// sums in order - the two-stage arithmetic of slab_group_kernel + wgrad_reduce_kernel, with the groups' L2 round
+// trips in parallel instead of one serial chain per element.
+constexpr int kRedLanes = 8, kRedElems = 256 / kRedLanes, kRedMaxGroups = 64;
 __global__ __launch_bounds__(256) void f32_reduce_multi_kernel(F32RedArgs a) {
   __shared__ F32RedSeg ss[kF32RedMax];
   __shared__ int st[kF32RedMax + 1];
+  __shared__ float part[kRedMaxGroups][kRedElems];
   // compile-time indices into the by-value argument (a run-time index would copy it to scratch per thread)
 #pragma unroll
   for (int i = 0; i < kF32RedMax; ++i)
@@ -873,30 +879,48 @@ __global__ __launch_bounds__(256) void f32_reduce_multi_kernel(F32RedArgs a) {
     if ((int)threadIdx.x == i) st[i] = a.start[i];
   __syncthreads();
   const int total_all = st[a.n];
-  int k = 0;
-  for (int i = static_cast<int>(blockIdx.x * blockDim.x + threadIdx.x); i < total_all;
-       i += static_cast<int>(gridDim.x * blockDim.x)) {
+  const int el = threadIdx.x % kRedElems, q = threadIdx.x / kRedElems;
+  for (int base = blockIdx.x * kRedElems; base < total_all; base += gridDim.x * kRedElems) {
+    const int i = base + el;
+    int k = 0;
     while (k + 1 < a.n && i >= st[k + 1]) ++k;
+    const bool live = i < total_all;
     const F32RedSeg sg = ss[k];
     const int e = i - st[k], total = sg.Kout * sg.ncol;
-    float acc;
-    if (sg.slices > kSlabGroup) {
-      acc = 0.f;
-      for (int g0 = 0; g0 < sg.slices; g0 += kSlabGroup) {
-        const int g1 = min(g0 + kSlabGroup, sg.slices);
-        float p = 0.f;
-#pragma unroll 8
-        for (int z = g0; z < g1; ++z) p += sg.slab[static_cast<int64_t>(z) * total + e];
-        acc = g0 == 0 ? p : acc + p;
-      }
-    } else {
-      acc = sg.slab[e];
-#pragma unroll 8
-      for (int z = 1; z < sg.slices; ++z) acc += sg.slab[static_cast<int64_t>(z) * total + e];
+    const int ngroups = (sg.slices + kSlabGroup - 1) / kSlabGroup;
+    const bool staged = ngroups <= kRedMaxGroups;
+    for (int g = q; live && staged && g < ngroups; g += kRedLanes) {
+      const int z0 = g * kSlabGroup, nz = min(kSlabGroup, sg.slices - z0);
+      float v[kSlabGroup];
+#pragma unroll
+      for (int z = 0; z < kSlabGroup; ++z)
+        v[z] = z < nz ? sg.slab[static_cast<int64_t>(z0 + z) * total + e] : 0.f;
+      float p = 0.f;
+#pragma unroll
+      for (int z = 0; z < kSlabGroup; ++z)
+        if (z < nz) p += v[z];
+      part[g][el] = p;
     }
-    const int m = e / sg.ncol, n = e - m * sg.ncol;
-    if (n < sg.Nw) sg.dw[m * sg.Nw + n] = acc;
-    else sg.db[m] = acc;
+    __syncthreads();
+    if (q == 0 && live) {
+      float t;
+      if (staged) {
+        t = part[0][el];
+        for (int g = 1; g < ngroups; ++g) t += part[g][el];
+      } else {  // more slices than the LDS stage holds: every group in order by this thread
+        t = 0.f;
+        for (int g = 0; g < ngroups; ++g) {
+          const int z0 = g * kSlabGroup, z1 = min(z0 + kSlabGroup, sg.slices);
+          float p = 0.f;
+          for (int z = z0; z < z1; ++z) p += sg.slab[static_cast<int64_t>(z) * total + e];
+          t = g == 0 ? p : t + p;
+        }
+      }
+      const int m = e / sg.ncol, n = e - m * sg.ncol;
+      if (n < sg.Nw) sg.dw[m * sg.Nw + n] = t;
+      else sg.db[m] = t;
+    }
+    __syncthreads();  // part reusable
   }
 }
 
@@ -2166,7 +2190,8 @@ void f32_slab_reduce_multi(const F32RedList& segs, hipStream_t s) {
     a.start[i + 1] = a.start[i] + segs[i].Kout * segs[i].ncol;
   }
   for (int i = a.n + 1; i <= kF32RedMax; ++i) a.start[i] = a.start[a.n];
-  hipLaunchKernelGGL(f32_reduce_multi_kernel, dim3(grid_1d(a.start[a.n])), dim3(256), 0, s, a);
+  const int grid = std::max(1, std::min((a.start[a.n] + kRedElems - 1) / kRedElems, 8192));
+  hipLaunchKernelGGL(f32_reduce_multi_kernel, dim3(grid), dim3(256), 0, s, a);
 }
 
 void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,

@@ -446,11 +446,16 @@ struct PackEntry {
   int64_t start;       // first KRSC element of this weight in the launch's flat index space
   int64_t start_tile;  // first 64x64 CRSK transpose tile
   int K, C, R, S, Cp, ldk;
+  int start_tile2;     // first (32 k x kPackCt(Cp) c x R*S) tile of the one-launch pack (pack_both_multi_kernel)
 };
-constexpr int kPackMax = 48;  // 48 x 64 B + header < the 4 KiB kernel-argument limit
+// channels per tile of the one-launch pack: every channel of the stem (7x7, Cp = 8), 32 otherwise
+inline int pack_ct(int Cp) { return Cp < 32 ? Cp : 32; }
+inline int pack_tiles2(int K, int Cp) { return ((K + 31) / 32) * ((Cp + pack_ct(Cp) - 1) / pack_ct(Cp)); }
+constexpr int kPackMax = 48;  // 48 x 72 B + header < the 4 KiB kernel-argument limit
 struct PackTable {
   int n;
   int64_t total, total_tiles;
+  int total_tiles2;
   PackEntry e[kPackMax];
 };
 void pack_conv_weights(const PackTable& t, hipStream_t s);

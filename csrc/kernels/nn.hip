@@ -7,6 +7,7 @@
 // (ReLU mask + the two channel sums) and one apply pass that also emits the residual branch's grad.
 // Every kernel moves 16-B vectors of 8 channels.
 #include <algorithm>
+#include <cstdlib>
 
 #include "device_common.h"
 #include "kernels.h"
@@ -101,6 +102,71 @@ __global__ __launch_bounds__(256) void pack_crsk_multi_kernel(PackTable t) {
     const int cc = idx >> 6, kk = idx & 63;
     const int k = k0 + kk, crs = crs0 + cc;
     if (k < d.K && crs < crs_all) out[(int64_t)crs * d.K + k] = (bf16)tile[kk][cc];
+  }
+}
+
+// Both bf16 layouts from ONE read of each fp32 weight (the two kernels above read it twice, the KRSC one with
+// a strided gather): a tile of 32 output channels x ct input channels x all R*S taps - a contiguous run of each
+// source row - is staged in LDS, then written as KRSC rows (runs of ct channels) and CRSK rows (runs of 32
+// output channels).  Padded channels (c >= C) and the stem's row tail (ldk > R*S*Cp) are written as zeros.
+constexpr int kPackTileFloats = 32 * 8 * 49;  // the largest tile: the 7x7 stem, Cp = 8 (3x3: 32 x 32 x 9)
+__device__ __forceinline__ int pack_ct_dev(int Cp) { return Cp < 32 ? Cp : 32; }  // = kern::pack_ct
+__global__ __launch_bounds__(256) void pack_both_multi_kernel(PackTable t) {
+  __shared__ PackEntry se[kPackMax];
+  __shared__ float tile[kPackTileFloats];
+  pack_table_to_lds(t, se);
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < t.n && b >= se[i + 1].start_tile2) ++i;
+  const PackEntry d = se[i];
+  const int RS = d.R * d.S, ct = pack_ct_dev(d.Cp), nct = (d.Cp + ct - 1) / ct;
+  const int tb = b - d.start_tile2;
+  const int k0 = (tb / nct) * 32, c0 = (tb % nct) * ct;
+  const int run = ct * RS;  // floats of one source row in this tile
+  // load: tile[kk][cc * RS + rs] = w[k0 + kk][c0 + cc][rs] (contiguous in the source)
+  for (int idx = threadIdx.x; idx < 32 * run; idx += 256) {
+    const int kk = idx / run, r = idx - kk * run, c = c0 + r / RS, k = k0 + kk;
+    tile[idx] = (k < d.K && c < d.C) ? d.w[(int64_t)k * d.C * RS + (int64_t)c0 * RS + r] : 0.f;
+  }
+  __syncthreads();
+  bf16* krsc = static_cast<bf16*>(d.krsc);
+  bf16* crsk = static_cast<bf16*>(d.crsk);
+  // KRSC: row k, element rs * Cp + c (runs of ct consecutive channels), 8 channels (one 16-B store) per thread;
+  // ct, Cp and ldk are multiples of 8
+  const int cv = ct >> 3;
+  for (int idx = threadIdx.x; idx < 32 * RS * cv; idx += 256) {
+    const int kk = idx / (RS * cv), r = idx - kk * RS * cv, rs = r / cv, cc = (r - rs * cv) * 8, k = k0 + kk;
+    if (k >= d.K || c0 + cc >= d.Cp) continue;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (bf16)tile[kk * run + (cc + j) * RS + rs];
+    *reinterpret_cast<bf16x8*>(krsc + (int64_t)k * d.ldk + rs * d.Cp + c0 + cc) = v;
+  }
+  // CRSK: row (c, rs), element k (runs of 32 output channels): 8 per thread when K % 8 == 0
+  if ((d.K & 7) == 0) {
+    for (int idx = threadIdx.x; idx < 4 * run; idx += 256) {
+      const int crs = idx >> 2, kk = (idx & 3) * 8, cc = crs / RS, rs = crs - cc * RS, k = k0 + kk;
+      if (k >= d.K || c0 + cc >= d.Cp) continue;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (bf16)tile[(kk + j) * run + cc * RS + rs];
+      *reinterpret_cast<bf16x8*>(crsk + ((int64_t)(c0 + cc) * RS + rs) * d.K + k) = v;
+    }
+  } else {
+    for (int idx = threadIdx.x; idx < 32 * run; idx += 256) {
+      const int crs = idx >> 5, kk = idx & 31, cc = crs / RS, rs = crs - cc * RS, k = k0 + kk;
+      if (k < d.K && c0 + cc < d.Cp)
+        crsk[((int64_t)(c0 + cc) * RS + rs) * d.K + k] = (bf16)tile[kk * run + cc * RS + rs];
+    }
+  }
+  // the zero tail of KRSC rows padded to whole 64-wide k-tiles (the stem)
+  const int kd = RS * d.Cp;
+  if (c0 == 0 && d.ldk > kd) {
+    const int tail = d.ldk - kd;
+    for (int idx = threadIdx.x; idx < 32 * tail; idx += 256) {
+      const int kk = idx / tail, j = kd + idx - kk * tail, k = k0 + kk;
+      if (k < d.K) krsc[(int64_t)k * d.ldk + j] = (bf16)0.f;
+    }
   }
 }
 
@@ -873,6 +939,14 @@ void pack_conv_weight(const float* w, int K, int C, int R, int S, int Cp, int ld
 
 void pack_conv_weights(const PackTable& t, hipStream_t s) {
   if (t.total <= 0) return;
+  // RINGDP_PACK_SPLIT=1: the two-launch form (A/B)
+  static const bool split = [] { const char* v = std::getenv("RINGDP_PACK_SPLIT"); return v && std::atoi(v) != 0; }();
+  bool fits = true;  // every entry's tile must fit the LDS stage
+  for (int i = 0; i < t.n; ++i) fits = fits && 32 * pack_ct(t.e[i].Cp) * t.e[i].R * t.e[i].S <= kPackTileFloats;
+  if (!split && fits) {
+    pack_both_multi_kernel<<<t.total_tiles2, 256, 0, s>>>(t);
+    return;
+  }
   pack_krsc_multi_kernel<<<grid_for(t.total), 256, 0, s>>>(t);
   pack_crsk_multi_kernel<<<(int)t.total_tiles, 256, 0, s>>>(t);
 }

@@ -181,6 +181,8 @@ std::vector<at::Tensor> pack_conv_weights(const std::vector<at::Tensor>& ws, con
     e.ldk = (int)ldk;
     t.total += K * ldk;
     t.total_tiles += ((cpad * R * S + 63) / 64) * ((K + 63) / 64);
+    e.start_tile2 = t.total_tiles2;
+    t.total_tiles2 += kern::pack_tiles2((int)K, (int)cpad);
   }
   if (t.n > 0) flush(stream_of(ws[0]));
   return out;

@@ -578,7 +578,9 @@ def test_fused_attention_forward(T):
 def test_pack_conv_weights_multi_matches_single():
     """One-launch packing of many conv weights == the per-weight pack (KRSC with padded rows, CRSK)."""
     torch.manual_seed(3)
-    shapes = [(64, 3, 7, 7, 8), (64, 64, 3, 3, 64), (256, 64, 1, 1, 64), (512, 256, 3, 3, 256), (10, 5, 3, 3, 8)]
+    # (the one-launch pack tiles 32 output x min(Cp, 32) input channels: ragged K and Cp included)
+    shapes = [(64, 3, 7, 7, 8), (64, 64, 3, 3, 64), (256, 64, 1, 1, 64), (512, 256, 3, 3, 256), (10, 5, 3, 3, 8),
+              (40, 20, 3, 3, 24), (33, 70, 1, 1, 72), (2048, 512, 1, 1, 512)]
     ws = [torch.randn(k, c, r, s, device="cuda") for k, c, r, s, _ in shapes]
     flat = C().pack_conv_weights(ws, [cp for *_, cp in shapes])
     for i, w in enumerate(ws):
