@@ -953,6 +953,14 @@ __device__ __forceinline__ void ff_pool2(const bf16* Cs, bf16* X3b, bf16* __rest
 #ifndef RINGDP_FF_KPIPE
 #define RINGDP_FF_KPIPE 0
 #endif
+// issue priority between the two waves of a SIMD: 0 none (age decides: the producer wins), 1 the consumer at
+// priority 1 in phase 3, 2 the consumer at priority 1 throughout, 3 = 1 plus the producer at 1 in phases 1-2
+#ifndef RINGDP_FF_PRIO
+#define RINGDP_FF_PRIO 0
+#endif
+#ifndef RINGDP_BWD_PRIO
+#define RINGDP_BWD_PRIO 0  // 1: the 8-wave dgrad roles' VALU / DMA waves (4-7) at issue priority 1
+#endif
 #ifndef RINGDP_FF_PPIPE
 #define RINGDP_FF_PPIPE 0
 #endif
@@ -1024,6 +1032,9 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
     const bool live = b < B;
     const int nb = b + bstep;
     FF_ST(0);
+#if RINGDP_FF_PRIO == 3
+    __builtin_amdgcn_s_setprio(1);
+#endif
     // ---------------- phase 1: conv1 -> X2 / CT
     if (live) {
       if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
@@ -1127,6 +1138,9 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
     FF_ST(3);
     __syncthreads();  // [S2] Cs complete
     FF_ST(4);
+#if RINGDP_FF_PRIO == 3
+    __builtin_amdgcn_s_setprio(0);
+#endif
     // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3 (items [0, FF_P2_PROD); the consumer pools the rest)
     if (live) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, b, tid, 0, p2split);
     FF_ST(5);
@@ -1179,6 +1193,9 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
   }
   __syncthreads();  // [S0a]
   __syncthreads();  // [S0b]  (fw is complete past these)
+#if RINGDP_FF_PRIO == 2
+  __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (MI355X_MICROARCH: two waves per SIMD)
+#endif
   auto fc_reduce = [&](int bb) {  // after a barrier that follows the fred writes of image bb
     if (tid < 160) {
       const int n = tid >> 4, c = tid & 15;
@@ -1292,6 +1309,10 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     __syncthreads();  // [S2]
     FF_ST(4);
     // ---------------- phase 3: the rest of the producer's pool2 (image s), k-steps 11-17
+#if RINGDP_FF_PRIO == 1 || RINGDP_FF_PRIO == 3
+    // phase 3 is the consumer's (fwd_stamps.md): win the SIMD's issue arbitration against the older producer wave
+    __builtin_amdgcn_s_setprio(1);
+#endif
     {
       const int bpr = b0 + s * bstep;
       if (bpr < Bp) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, bpr, tid, p2split, 800);
@@ -1300,6 +1321,9 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     FF_ST(5);
     __syncthreads();  // [S3]
     FF_ST(6);
+#if RINGDP_FF_PRIO == 1 || RINGDP_FF_PRIO == 3
+    __builtin_amdgcn_s_setprio(0);
+#endif
   }
 }
 
@@ -2006,6 +2030,9 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
   const int n = b_first < b_end ? (b_end - b_first + b_step - 1) / b_step : 0;
   // the zero rows of both dz3 images stay zero; the interiors are rewritten per image
   for (int c = tid; c < 2 * C3D_P / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
+#if RINGDP_BWD_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger (VALU / DMA) half
+#endif
   if (wave < 4) {
     // ---- MFMA waves: wave w owns input channels 16w..16w+15 (as conv3_dgrad_role)
     const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
@@ -2806,6 +2833,9 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
   for (int c = tid; c < (2 * (C2D_P + C12_O) + 3 * C12_XS) / 16; c += 512)
     reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
   __syncthreads();
+#if RINGDP_BWD_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger (VALU / DMA) half
+#endif
   if (wave < 4) {
     // ---- MFMA waves: m-tiles wave, wave + 4, wave + 8 (< 11), both n-tiles.  Weights are the A operand
     // (the B-fragment pack read as A: the same lane -> (channel, k) map), so a lane's 4 results are 4

@@ -756,15 +756,16 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
   }
 }
 
-// logits gradient of row r, class j: from a materialised dl, or formed from the cross-entropy forward (ce,
-// the expression of ce_bwd_kernel)
-// (branch-free: every load is issued before any of them is used - a load behind the ignore_index branch made
-// each call two dependent round trips to L2, 20 us for the dW role's 10 calls per thread)
-__device__ __forceinline__ float head_dl(const float* __restrict__ dl, const CeFuse& ce, int J, int r, int j) {
-  if (dl) return dl[(int64_t)r * J + j];
+// logits gradient of row r, class j: from a materialised dl (kCE false), or formed from the cross-entropy forward
+// (ce, the expression of ce_bwd_kernel).  Branch-free: every load is unconditional (the reduction picks an index,
+// not a path), so a call's loads issue together - conditional loads had made each call several dependent L2
+// round trips.  sc: 1 (reduction none) or 1 / denom.
+template <bool kCE>
+__device__ __forceinline__ float head_dl(const float* __restrict__ dl, const CeFuse& ce, float sc, int J, int r, int j) {
+  if (!kCE) return dl[(int64_t)r * J + j];
   const int64_t y = ce.labels[r];
   const float x = ce.logits[(int64_t)r * J + j], l = ce.lse[r];
-  const float go = ce.reduction == 0 ? ce.grad_out[r] : ce.grad_out[0] / ce.denom[0];
+  const float go = ce.grad_out[ce.reduction == 0 ? r : 0] * sc;
   const float p = __expf(x - l);
   const float q = (j == y ? (1.f - ce.eps) : 0.f) + ce.eps / (float)J;
   return y == ce.ignore_index ? 0.f : (p - q) * go;
@@ -774,11 +775,13 @@ __device__ __forceinline__ float head_dl(const float* __restrict__ dl, const CeF
 // C/16 workgroups after them dW (16 channels each, the batch summed by 16 row groups combined in a fixed
 // order) and, in the first of those, db.  No partial sums cross workgroups: one launch, deterministic.
 constexpr int kHeadRows = 256;  // logits-gradient rows staged in LDS per chunk (dW role)
+template <bool kCE>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl, CeFuse ce,
                                                        const float* __restrict__ pooled, const float* __restrict__ w,
                                                        int N, int HW, int C, int J, int nb_dx, bf16* __restrict__ dx,
                                                        float* __restrict__ dw, float* __restrict__ db) {
   __shared__ float g[kHeadRows][kHeadMaxJ];
+  const float sc = kCE ? (ce.reduction == 0 ? 1.f : 1.f / ce.denom[0]) : 1.f;
   if ((int)blockIdx.x < nb_dx) {
     const int cv = C >> 3, ipp = 256 / cv;
     const int col = threadIdx.x % cv, sub = threadIdx.x / cv;
@@ -786,7 +789,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     // this workgroup's ipp x J logits gradients first (independent loads in flight), then W from L2
     for (int o = threadIdx.x; o < ipp * J; o += 256) {
       const int si = o / J, j = o - si * J;
-      if (n0 + si < N) g[si][j] = head_dl(dl, ce, J, n0 + si, j);
+      if (n0 + si < N) g[si][j] = head_dl<kCE>(dl, ce, sc, J, n0 + si, j);
     }
     __syncthreads();
     if (sub >= ipp || n >= N) return;
@@ -830,7 +833,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int e = e0 + 256 * u, r = e / J, j = e - r * J;
-        v[u] = e < rows * J ? head_dl(dl, ce, J, r0 + r, j) : 0.f;
+        v[u] = e < rows * J ? head_dl<kCE>(dl, ce, sc, J, r0 + r, j) : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -1076,8 +1079,11 @@ void head_bwd(const float* dl, const CeFuse* ce, const float* pooled, const floa
               void* dx, float* dw, float* db, hipStream_t s) {
   const int ipp = 256 / (C / 8), nb_dx = (N + ipp - 1) / ipp;
   const CeFuse c = ce ? *ce : CeFuse{};
-  head_bwd_kernel<<<nb_dx + (C + 15) / 16, 256, 0, s>>>(dl, c, pooled, w, N, HW, C, J, nb_dx, static_cast<bf16*>(dx),
-                                                        dw, db);
+  const int grid = nb_dx + (C + 15) / 16;
+  if (ce)
+    head_bwd_kernel<true><<<grid, 256, 0, s>>>(nullptr, c, pooled, w, N, HW, C, J, nb_dx, static_cast<bf16*>(dx), dw, db);
+  else
+    head_bwd_kernel<false><<<grid, 256, 0, s>>>(dl, c, pooled, w, N, HW, C, J, nb_dx, static_cast<bf16*>(dx), dw, db);
 }
 
 void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s) {
