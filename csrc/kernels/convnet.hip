@@ -950,17 +950,18 @@ __device__ __forceinline__ void ff_pool2(const bf16* Cs, bf16* X3b, bf16* __rest
 }
 
 // software-pipelined A-fragment reads in the conv2 (producer) / conv3 (consumer) k-step loops (A/B build macros)
+// RINGDP_FF_P2_ALL (default): the producer pools all 800 pool2 items and the consumer's phase 3 holds no pool2
+// code at all (fewer live registers beside conv3's 144 weight registers); 0: the split is the run-time
+// p2split argument (RINGDP_FF_P2)
+#ifndef RINGDP_FF_P2_ALL
+#define RINGDP_FF_P2_ALL 1
+#endif
 #ifndef RINGDP_FF_KPIPE
 #define RINGDP_FF_KPIPE 0
 #endif
-// issue priority between the two waves of a SIMD: 0 none (age decides: the producer wins), 1 the consumer at
-// priority 1 in phase 3, 2 the consumer at priority 1 throughout, 3 = 1 plus the producer at 1 in phases 1-2
-#ifndef RINGDP_FF_PRIO
-#define RINGDP_FF_PRIO 0
-#endif
-#ifndef RINGDP_BWD_PRIO
-#define RINGDP_BWD_PRIO 0  // 1: the 8-wave dgrad roles' VALU / DMA waves (4-7) at issue priority 1
-#endif
+// issue priority between the two waves of a SIMD (scheduling A/B through RINGDP_FF_ABLATE, results unchanged):
+// by default age decides (the older producer wave wins); bit 4: the consumer at priority 1 in phase 3; bit 5:
+// the producer at priority 1 in phases 1-2
 #ifndef RINGDP_FF_PPIPE
 #define RINGDP_FF_PPIPE 0
 #endif
@@ -969,7 +970,7 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
                             const PackSrc& ws, const float* __restrict__ b1, const float* __restrict__ b2,
                             bf16* __restrict__ a1, uint8_t* __restrict__ idx1, bf16* __restrict__ a2,
                             uint8_t* __restrict__ idx2, int B, int b0, int bstep, int nsteps, float mean,
-                            float inv_std, float in_scale, unsigned* sync, int npack, int p2split) {
+                            float inv_std, float in_scale, unsigned* sync, int npack, int p2split, int prio) {
   bf16* XS = reinterpret_cast<bf16*>(smem);
   bf16* X2 = reinterpret_cast<bf16*>(smem + FF_OFF_X2);
   uint32_t* X2u = reinterpret_cast<uint32_t*>(X2);
@@ -1032,9 +1033,7 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
     const bool live = b < B;
     const int nb = b + bstep;
     FF_ST(0);
-#if RINGDP_FF_PRIO == 3
-    __builtin_amdgcn_s_setprio(1);
-#endif
+    if (prio & 2) __builtin_amdgcn_s_setprio(1);
     // ---------------- phase 1: conv1 -> X2 / CT
     if (live) {
       if (nb < B) c1_load<U8>(xin, nb, tid, pu, pf);
@@ -1138,11 +1137,13 @@ __device__ __forceinline__ void ff_producer(char* smem, const void* __restrict__
     FF_ST(3);
     __syncthreads();  // [S2] Cs complete
     FF_ST(4);
-#if RINGDP_FF_PRIO == 3
-    __builtin_amdgcn_s_setprio(0);
-#endif
+    if (prio & 2) __builtin_amdgcn_s_setprio(0);
     // ---------------- phase 3: pool2 -> a2 / idx2 (HBM) + X3 (items [0, FF_P2_PROD); the consumer pools the rest)
+#if RINGDP_FF_P2_ALL
+    if (live) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, b, tid, 0, 800);
+#else
     if (live) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, b, tid, 0, p2split);
+#endif
     FF_ST(5);
     __syncthreads();  // [S3] X3 complete; Cs, X2, CT free
     FF_ST(6);
@@ -1161,7 +1162,7 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
                             const float* __restrict__ b3, const float* __restrict__ bfc, bf16* __restrict__ a3,
                             uint8_t* __restrict__ idx3, float* __restrict__ logits, bf16* __restrict__ a2,
                             uint8_t* __restrict__ idx2, int Bp, int B, int b0, int bstep, int nsteps,
-                            unsigned* sync, int npack, int p2split) {
+                            unsigned* sync, int npack, int p2split, int prio) {
   bf16* X3 = reinterpret_cast<bf16*>(smem + FF_OFF_X3);
   const bf16* Cs = reinterpret_cast<const bf16*>(smem + FF_OFF_CS);
   bf16* fw = reinterpret_cast<bf16*>(smem + FF_OFF_FW);
@@ -1193,9 +1194,6 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
   }
   __syncthreads();  // [S0a]
   __syncthreads();  // [S0b]  (fw is complete past these)
-#if RINGDP_FF_PRIO == 2
-  __builtin_amdgcn_s_setprio(1);  // static priority for the younger half (MI355X_MICROARCH: two waves per SIMD)
-#endif
   auto fc_reduce = [&](int bb) {  // after a barrier that follows the fred writes of image bb
     if (tid < 160) {
       const int n = tid >> 4, c = tid & 15;
@@ -1309,21 +1307,19 @@ __device__ __forceinline__ void ff_consumer(char* smem, const bf16* __restrict__
     __syncthreads();  // [S2]
     FF_ST(4);
     // ---------------- phase 3: the rest of the producer's pool2 (image s), k-steps 11-17
-#if RINGDP_FF_PRIO == 1 || RINGDP_FF_PRIO == 3
     // phase 3 is the consumer's (fwd_stamps.md): win the SIMD's issue arbitration against the older producer wave
-    __builtin_amdgcn_s_setprio(1);
-#endif
+    if (prio & 1) __builtin_amdgcn_s_setprio(1);
+#if !RINGDP_FF_P2_ALL
     {
       const int bpr = b0 + s * bstep;
       if (bpr < Bp) ff_pool2(Cs, X3 + (s & 1) * FF_X3H, a2, idx2, bpr, tid, p2split, 800);
     }
+#endif
     if (live_m) mfma_ks(xb, std::integral_constant<int, RINGDP_FF_KB>{}, std::integral_constant<int, 18>{});
     FF_ST(5);
     __syncthreads();  // [S3]
     FF_ST(6);
-#if RINGDP_FF_PRIO == 1 || RINGDP_FF_PRIO == 3
-    __builtin_amdgcn_s_setprio(0);
-#endif
+    if (prio & 1) __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -1355,10 +1351,12 @@ __global__ __launch_bounds__(512, 1) void fused_fwd_kernel(const void* __restric
   // exec-masked sequence whose live ranges the register allocator would have to overlap)
   if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < 4)
     ff_producer<U8, PACK>(ff_smem, xin, PACK ? pack_out : packed, ws, b1, b2, a1, idx1, a2, idx2,
-                          (ablate & 1) ? 0 : B, b0, bstep, nsteps, mean, inv_std, in_scale, sync, npack, p2split);
+                          (ablate & 1) ? 0 : B, b0, bstep, nsteps, mean, inv_std, in_scale, sync, npack, p2split,
+                          __builtin_amdgcn_readfirstlane(ablate >> 4));
   else
     ff_consumer<PACK>(ff_smem, PACK ? pack_out : packed, ws, b3, bfc, a3, idx3, logits, a2, idx2,
-                      (ablate & 1) ? 0 : B, (ablate & 2) ? 0 : B, b0, bstep, nsteps, sync, npack, p2split);
+                      (ablate & 1) ? 0 : B, (ablate & 2) ? 0 : B, b0, bstep, nsteps, sync, npack, p2split,
+                      __builtin_amdgcn_readfirstlane(ablate >> 4));
 #ifdef RINGDP_FF_STAMPS
   __syncthreads();
   if (blockIdx.x == FF_ST_BLK && threadIdx.x == 0 && nsteps > FF_ST_S0 + 8) {
@@ -2030,9 +2028,9 @@ __device__ __forceinline__ void conv3_dgrad8_role(char* smem, const bf16* __rest
   const int n = b_first < b_end ? (b_end - b_first + b_step - 1) / b_step : 0;
   // the zero rows of both dz3 images stay zero; the interiors are rewritten per image
   for (int c = tid; c < 2 * C3D_P / 16; c += 512) reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
-#if RINGDP_BWD_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger (VALU / DMA) half
-#endif
+  // RINGDP_C3_ABLATE / RINGDP_C12_ABLATE bit 3 (a scheduling A/B, results unchanged): the younger (VALU / DMA)
+  // half at issue priority 1 (MI355X_MICROARCH: two waves per SIMD, static priority)
+  if ((ablate & 8) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   if (wave < 4) {
     // ---- MFMA waves: wave w owns input channels 16w..16w+15 (as conv3_dgrad_role)
     const int r16 = lane & 15, q8 = (lane >> 4) * 8, c4 = (lane >> 4) * 4;
@@ -2833,9 +2831,9 @@ __device__ __forceinline__ void conv12_dgrad8_role(char* smem, const void* __res
   for (int c = tid; c < (2 * (C2D_P + C12_O) + 3 * C12_XS) / 16; c += 512)
     reinterpret_cast<bf16x8*>(smem)[c] = zero_bf16x8();
   __syncthreads();
-#if RINGDP_BWD_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // static priority for the younger (VALU / DMA) half
-#endif
+  // RINGDP_C3_ABLATE / RINGDP_C12_ABLATE bit 3 (a scheduling A/B, results unchanged): the younger (VALU / DMA)
+  // half at issue priority 1 (MI355X_MICROARCH: two waves per SIMD, static priority)
+  if ((ablate & 8) && wave >= 4) __builtin_amdgcn_s_setprio(1);
   if (wave < 4) {
     // ---- MFMA waves: m-tiles wave, wave + 4, wave + 8 (< 11), both n-tiles.  Weights are the A operand
     // (the B-fragment pack read as A: the same lane -> (channel, k) map), so a lane's 4 results are 4
