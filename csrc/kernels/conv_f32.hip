@@ -891,10 +891,14 @@ __global__ __launch_bounds__(256) void f32_reduce_multi_kernel(F32RedArgs a) {
     const bool staged = ngroups <= kRedMaxGroups;
     for (int g = q; live && staged && g < ngroups; g += kRedLanes) {
       const int z0 = g * kSlabGroup, nz = min(kSlabGroup, sg.slices - z0);
+      // unconditional loads (the index clamped into the group): a guarded load is a branch the compiler will not
+      // hoist past, which serialises the group's round trips
       float v[kSlabGroup];
+      // (a global-address-space pointer: the slab pointer read back from LDS would otherwise be a flat access)
+      const __attribute__((address_space(1))) float* src =
+          (const __attribute__((address_space(1))) float*)(sg.slab + static_cast<int64_t>(z0) * total + e);
 #pragma unroll
-      for (int z = 0; z < kSlabGroup; ++z)
-        v[z] = z < nz ? sg.slab[static_cast<int64_t>(z0 + z) * total + e] : 0.f;
+      for (int z = 0; z < kSlabGroup; ++z) v[z] = src[static_cast<int64_t>(min(z, nz - 1)) * total];
       float p = 0.f;
 #pragma unroll
       for (int z = 0; z < kSlabGroup; ++z)
@@ -2214,6 +2218,53 @@ void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC
     hipLaunchKernelGGL(pool_relu_fwd_kernel, dim3(grid_elems(total)), dim3(256), 0, s, z + c0 * H * W,
                        a + c0 * PH * PW, code + c0 * PH * PW, total, H, W, make_fdiv(PH * PW), make_fdiv(PW), k, st);
   }
+}
+
+// The fp32 ConvNet head backward at small batches (the whole-network cross-entropy node): the logits gradient
+// (ce_bwd_kernel's expression, same bits) -> dl for fc1's weight gradient, fc1's data gradient
+// da3[f] = sum_j dl[j] W[j][f] (an fmaf chain in j order) and pool3's backward (2x2/s2, code = dy*2+dx, 255 =
+// no gradient) straight into dz3 [128][8][8] - one launch for the cross-entropy backward, fc1 data gradient and
+// pool3 backward launches.  Workgroup = 256 features of one image; 8 per image.
+__global__ __launch_bounds__(256) void fc_ce_pool3_bwd_f32_kernel(const float* __restrict__ logits,
+                                                                  const int64_t* __restrict__ labels,
+                                                                  const float* __restrict__ lse,
+                                                                  const float* __restrict__ grad_out,
+                                                                  const float* __restrict__ denom, int ignore_index,
+                                                                  float eps, int reduction,
+                                                                  const float* __restrict__ wfc,
+                                                                  const unsigned char* __restrict__ code3,
+                                                                  float* __restrict__ dl, float* __restrict__ dz3) {
+  __shared__ float g[10];
+  const int n = blockIdx.x >> 3, f = (blockIdx.x & 7) * 256 + threadIdx.x;
+  if (threadIdx.x < 10) {
+    const int c = threadIdx.x;
+    const int64_t y = labels[n];
+    float v = 0.f;
+    if (y != ignore_index) {
+      const float p = __expf(logits[n * 10 + c] - lse[n]);
+      const float q = (c == y ? (1.f - eps) : 0.f) + eps / 10.f;
+      v = (p - q) * (reduction == 0 ? grad_out[n] : grad_out[0] / denom[0]);
+    }
+    g[c] = v;
+    if ((blockIdx.x & 7) == 0) dl[n * 10 + c] = v;
+  }
+  __syncthreads();
+  float a = 0.f;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) a = fmaf(g[j], wfc[j * 2048 + f], a);
+  const int code = code3[n * 2048 + f];
+  const int c = f >> 4, py = (f >> 2) & 3, px = f & 3;
+  float* o = dz3 + (int64_t)n * 8192 + c * 64 + 2 * py * 8 + 2 * px;
+  *reinterpret_cast<float2*>(o) = make_float2(code == 0 ? a : 0.f, code == 1 ? a : 0.f);
+  *reinterpret_cast<float2*>(o + 8) = make_float2(code == 2 ? a : 0.f, code == 3 ? a : 0.f);
+}
+
+void fc_ce_pool3_bwd_f32(const float* logits, const int64_t* labels, const float* lse, const float* grad_out,
+                         const float* denom, int ignore_index, float eps, int reduction, const float* wfc,
+                         const unsigned char* code3, int B, float* dl, float* dz3, hipStream_t s) {
+  if (B <= 0) return;
+  hipLaunchKernelGGL(fc_ce_pool3_bwd_f32_kernel, dim3(8 * B), dim3(256), 0, s, logits, labels, lse, grad_out, denom,
+                     ignore_index, eps, reduction, wfc, code3, dl, dz3);
 }
 
 void pool_relu_f32_bwd(const float* da, const unsigned char* code, float* dz, int64_t BC, int H, int W, int k,

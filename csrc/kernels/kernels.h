@@ -156,6 +156,11 @@ void conv1_pool_f32_fwd(const float* x, const unsigned char* xu8, int64_t B, flo
                         const float* w1, const float* b1, float* a1, unsigned char* code1, hipStream_t s);
 void conv1_wgrad_f32(const float* x, const unsigned char* xu8, int64_t B, float mean, float inv_std, const float* da1,
                      const unsigned char* code1, float* slab, hipStream_t s);
+// The fp32 ConvNet's cross-entropy backward + fc1 data gradient + pool3 backward in one launch (10 classes, 2048
+// features = [128][4][4]): dl [B][10] (for fc1's weight gradient) and dz3 [B][128][8][8]
+void fc_ce_pool3_bwd_f32(const float* logits, const int64_t* labels, const float* lse, const float* grad_out,
+                         const float* denom, int ignore_index, float eps, int reduction, const float* wfc,
+                         const unsigned char* code3, int B, float* dl, float* dz3, hipStream_t s);
 // a = relu(maxpool_k,st(z)) with a 1-byte argmax code (255: no gradient); backward is a gather
 void pool_relu_f32_fwd(const float* z, float* a, unsigned char* code, int64_t BC, int H, int W, int k, int st,
                        hipStream_t s);

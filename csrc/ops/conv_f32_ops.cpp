@@ -253,6 +253,32 @@ std::tuple<at::Tensor, std::vector<int64_t>> f32_conv1_wgrad_slab(const at::Tens
   return {slab, {blocks, 32, 25, 26}};
 }
 
+std::tuple<at::Tensor, at::Tensor> f32_fc_ce_pool3_bwd(const at::Tensor& logits, const at::Tensor& labels,
+                                                       const at::Tensor& lse, const at::Tensor& ws,
+                                                       const at::Tensor& grad_out, int64_t ignore_index, double eps,
+                                                       int64_t reduction, const at::Tensor& wfc,
+                                                       const at::Tensor& code3) {
+  util::f32_gpu(logits, "logits");
+  util::f32_gpu(wfc, "fc1 weight");
+  const int64_t B = logits.size(0);
+  RINGDP_CHECK(logits.dim() == 2 && logits.size(1) == 10 && labels.numel() == B && lse.numel() == B &&
+                   wfc.numel() == 10 * 2048 && wfc.is_contiguous() && logits.is_contiguous(),
+               "fc_ce_pool3_bwd: the ConvNet head (10 classes, 2048 features) expected");
+  RINGDP_CHECK(code3.scalar_type() == at::kByte && code3.numel() == B * 2048 && code3.is_contiguous(),
+               "fc_ce_pool3_bwd: code3 must be [B, 128, 4, 4] uint8");
+  RINGDP_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "fc_ce_pool3_bwd: int64 labels");
+  at::Tensor g = grad_out.to(at::kFloat).contiguous();
+  const int64_t nparts = (ws.numel() - 4) / 2;
+  at::Tensor dl = at::empty({B, 10}, logits.options());
+  at::Tensor dz3 = at::empty({B, 128, 8, 8}, logits.options());
+  kern::fc_ce_pool3_bwd_f32(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                            g.data_ptr<float>(), ws.data_ptr<float>() + 2 * nparts, static_cast<int>(ignore_index),
+                            static_cast<float>(eps), static_cast<int>(reduction), wfc.data_ptr<float>(),
+                            code3.data_ptr<uint8_t>(), static_cast<int>(B), dl.data_ptr<float>(), dz3.data_ptr<float>(),
+                            util::stream_of(logits));
+  return {dl, dz3};
+}
+
 void f32_slab_reduce_multi(const std::vector<at::Tensor>& slabs, const std::vector<std::vector<int64_t>>& meta,
                            const std::vector<at::Tensor>& dws, const std::vector<c10::optional<at::Tensor>>& dbs) {
   RINGDP_CHECK(slabs.size() == meta.size() && slabs.size() == dws.size() && slabs.size() == dbs.size(),

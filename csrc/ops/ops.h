@@ -133,6 +133,11 @@ std::tuple<at::Tensor, std::vector<int64_t>> f32_conv_wgrad_slab(const at::Tenso
                                                                  const at::Tensor& dw, bool with_bias);
 std::tuple<at::Tensor, std::vector<int64_t>> f32_conv1_wgrad_slab(const at::Tensor& x, const at::Tensor& da1,
                                                                   const at::Tensor& code1, double mean, double std);
+std::tuple<at::Tensor, at::Tensor> f32_fc_ce_pool3_bwd(const at::Tensor& logits, const at::Tensor& labels,
+                                                       const at::Tensor& lse, const at::Tensor& ws,
+                                                       const at::Tensor& grad_out, int64_t ignore_index, double eps,
+                                                       int64_t reduction, const at::Tensor& wfc,
+                                                       const at::Tensor& code3);
 void f32_slab_reduce_multi(const std::vector<at::Tensor>& slabs, const std::vector<std::vector<int64_t>>& meta,
                            const std::vector<at::Tensor>& dws, const std::vector<c10::optional<at::Tensor>>& dbs);
 std::tuple<at::Tensor, at::Tensor> f32_pool_relu_fwd(const at::Tensor& z, int64_t k, int64_t stride);

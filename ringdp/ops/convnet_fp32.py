@@ -139,9 +139,9 @@ class _NetCEF32(torch.autograd.Function):
     """Cross entropy on the fp32 ConvNet's logits as one node over every layer (small batches).
 
     The forward reuses the logits and activations of the per-layer forward.  The backward is the per-layer
-    backward's kernel sequence (cross-entropy gradient, fc1, pool3, conv3, pool2, conv2, conv1 - same kernels,
-    same fixed-order reductions, so the same bits), except that the weight-gradient reductions of all four
-    layers run as one launch at the end.  Deferral is safe by construction: every gradient this node returns
+    backward's sequence (cross-entropy gradient, fc1, pool3, conv3, pool2, conv2, conv1) with two fusions: the
+    cross-entropy backward, fc1's data gradient and pool3's backward are one launch, and the weight-gradient
+    reductions of all four layers run as one launch at the end (the same fixed-order sums as the per-layer path).  Deferral is safe by construction: every gradient this node returns
     is written before it returns, and autograd reads a node's gradients only after it returns."""
 
     @staticmethod
@@ -161,16 +161,15 @@ class _NetCEF32(torch.autograd.Function):
         B = logits.shape[0]
         grads = [grad_buffer(p) for p in (w1, b1, w2, b2, w3, b3, wfc, bfc)]
         dw1, db1, dw2, db2, dw3, db3, dwfc, dbfc = grads
-        dl = C.cross_entropy_bwd(logits, target, lse, ws, grad_out.contiguous(), *ctx.cfg)
+        # cross-entropy backward + fc1 data gradient + pool3 backward: one launch (the logits gradient dl is also
+        # written, for fc1's weight gradient)
+        dl, dz3 = C.f32_fc_ce_pool3_bwd(logits, target, lse, ws, grad_out.contiguous(), *ctx.cfg, wfc.detach(), code3)
         segs = []
-        # fc1 (a 1x1 conv over the flattened 2048-vector)
+        # fc1's weight gradient (a 1x1 conv over the flattened 2048-vector)
         dz = dl.view(B, -1, 1, 1)
         x3 = a3.reshape(B, -1, 1, 1)
-        wfc4 = wfc.detach().view(wfc.shape[0], -1, 1, 1)
-        da3 = C.f32_conv_dgrad(dz, wfc4, 1, 1, 0)
-        segs.append(C.f32_conv_wgrad_slab(dz, x3, 0, 0.0, 1.0, dwfc.view(wfc4.shape), True) + (dwfc, dbfc))
-        # pool3 + conv3
-        dz3 = C.f32_pool_relu_bwd(da3.view(a3.shape), code3, 2 * a3.shape[2], 2 * a3.shape[3], 2, 2)
+        segs.append(C.f32_conv_wgrad_slab(dz, x3, 0, 0.0, 1.0, dwfc.view(wfc.shape[0], -1, 1, 1), True) + (dwfc, dbfc))
+        # conv3
         da2 = C.f32_conv_dgrad(dz3, w3.detach(), a2.shape[2], a2.shape[3], 0)
         segs.append(C.f32_conv_wgrad_slab(dz3, a2, 0, 0.0, 1.0, dw3, True) + (dw3, db3))
         # pool2 (2x2 / s1) + conv2

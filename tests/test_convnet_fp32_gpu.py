@@ -255,8 +255,9 @@ def test_fp32_convnet_matches_aten(B):
 @pytest.mark.parametrize("B", [100, 700])
 def test_fp32_net_node_matches_per_layer_backward(B):
     """ringdp's cross entropy on the fp32 model at a small batch is ONE node over the whole network (one
-    weight-gradient reduction launch); its gradients must equal the per-layer backward's bit for bit (same kernels,
-    same fixed-order reductions), and the loss value too."""
+    weight-gradient reduction launch; cross entropy + fc1 data gradient + pool3 backward fused).  The loss and fc1's
+    gradients (same logits gradient, same GEMM, same fixed-order reduction) equal the per-layer backward's bit for
+    bit; the conv layers' to fp32 rounding (fc1's data gradient is an fmaf chain instead of the GEMM's MFMAs)."""
     from ringdp.ops.loss import _CrossEntropy, cross_entropy
 
     m_a, _ = _models(3)
@@ -272,7 +273,11 @@ def test_fp32_net_node_matches_per_layer_backward(B):
     lb.backward()
     assert torch.equal(la.detach(), lb.detach())
     for (n, p), q in zip(m_a.named_parameters(), m_b.parameters()):
-        assert torch.equal(p.grad, q.grad), n
+        if n.startswith("fc1"):
+            assert torch.equal(p.grad, q.grad), n
+        else:
+            rel = float((p.grad - q.grad).norm() / q.grad.norm())
+            assert rel < 1e-5, (n, rel)
     # another use of the logits keeps the per-layer path (gradients through both are summed by autograd)
     m_c, _ = _models(3)
     out = m_c(x)
