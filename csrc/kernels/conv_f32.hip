@@ -858,74 +858,78 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // then the group sums in order; one group: the slices in order) - the same bits, done by one thread.
 struct F32RedArgs {
   F32RedSeg seg[kF32RedMax];
-  int start[kF32RedMax + 1];
+  int bstart[kF32RedMax];  // first workgroup of each segment
   int n;
 };
-// Work item = (element, group of kSlabGroup slices): 32 elements x 8 group lanes per workgroup; lane q sums groups
-// q, q + 8, .. (each group's slices loaded at once, added in order from 0.f) into LDS, then lane 0 adds the group
-// sums in order - the two-stage arithmetic of slab_group_kernel + wgrad_reduce_kernel, with the groups' L2 round
-// trips in parallel instead of one serial chain per element.
+// Two kinds of workgroup, chosen per segment on the host: a segment of at most kSlabGroup slices (one group) gets
+// 256 elements per workgroup, one thread each summing the slices in order (unconditional loads, all in flight);
+// a segment with more slices gets 32 elements x 8 group lanes: lane q sums groups q, q + 8, .. into LDS and lane 0
+// adds the group sums in order.  Both are the two-stage arithmetic of slab_group_kernel + wgrad_reduce_kernel.
+// (One 32-element workgroup kind for every segment was 3553 workgroups at B=100 and ~20 us of dispatch; the
+// serial one-thread form before it spent 20 us in conv1's 400-slice chain.)
 constexpr int kRedLanes = 8, kRedElems = 256 / kRedLanes, kRedMaxGroups = 64;
+
+__device__ __forceinline__ float red_group(const F32RedSeg& sg, int total, int e, int z0) {
+  // unconditional loads (index clamped into the group) from a global-address-space pointer: a guarded load is a
+  // branch the compiler will not hoist past, and the slab pointer read back from LDS would be a flat access
+  const int nz = min(kSlabGroup, sg.slices - z0);
+  const __attribute__((address_space(1))) float* src =
+      (const __attribute__((address_space(1))) float*)(sg.slab + static_cast<int64_t>(z0) * total + e);
+  float v[kSlabGroup];
+#pragma unroll
+  for (int z = 0; z < kSlabGroup; ++z) v[z] = src[static_cast<int64_t>(min(z, nz - 1)) * total];
+  float p = 0.f;
+#pragma unroll
+  for (int z = 0; z < kSlabGroup; ++z)
+    if (z < nz) p += v[z];
+  return p;
+}
+
+__device__ __forceinline__ void red_store_f32(const F32RedSeg& sg, int e, float t) {
+  const int m = e / sg.ncol, n = e - m * sg.ncol;
+  if (n < sg.Nw) sg.dw[m * sg.Nw + n] = t;
+  else sg.db[m] = t;
+}
+
 __global__ __launch_bounds__(256) void f32_reduce_multi_kernel(F32RedArgs a) {
-  __shared__ F32RedSeg ss[kF32RedMax];
-  __shared__ int st[kF32RedMax + 1];
   __shared__ float part[kRedMaxGroups][kRedElems];
-  // compile-time indices into the by-value argument (a run-time index would copy it to scratch per thread)
+  // the segment of this workgroup: compile-time indices into the by-value argument (a run-time index would copy
+  // it to scratch per thread)
+  int k = 0;
 #pragma unroll
-  for (int i = 0; i < kF32RedMax; ++i)
-    if ((int)threadIdx.x == i) ss[i] = a.seg[i];
+  for (int i = 1; i < kF32RedMax; ++i)
+    if (i < a.n && (int)blockIdx.x >= a.bstart[i]) k = i;
+  F32RedSeg sg = a.seg[0];
+  int b0 = a.bstart[0];
 #pragma unroll
-  for (int i = 0; i <= kF32RedMax; ++i)
-    if ((int)threadIdx.x == i) st[i] = a.start[i];
-  __syncthreads();
-  const int total_all = st[a.n];
-  const int el = threadIdx.x % kRedElems, q = threadIdx.x / kRedElems;
-  for (int base = blockIdx.x * kRedElems; base < total_all; base += gridDim.x * kRedElems) {
-    const int i = base + el;
-    int k = 0;
-    while (k + 1 < a.n && i >= st[k + 1]) ++k;
-    const bool live = i < total_all;
-    const F32RedSeg sg = ss[k];
-    const int e = i - st[k], total = sg.Kout * sg.ncol;
-    const int ngroups = (sg.slices + kSlabGroup - 1) / kSlabGroup;
-    const bool staged = ngroups <= kRedMaxGroups;
-    for (int g = q; live && staged && g < ngroups; g += kRedLanes) {
-      const int z0 = g * kSlabGroup, nz = min(kSlabGroup, sg.slices - z0);
-      // unconditional loads (the index clamped into the group): a guarded load is a branch the compiler will not
-      // hoist past, which serialises the group's round trips
-      float v[kSlabGroup];
-      // (a global-address-space pointer: the slab pointer read back from LDS would otherwise be a flat access)
-      const __attribute__((address_space(1))) float* src =
-          (const __attribute__((address_space(1))) float*)(sg.slab + static_cast<int64_t>(z0) * total + e);
-#pragma unroll
-      for (int z = 0; z < kSlabGroup; ++z) v[z] = src[static_cast<int64_t>(min(z, nz - 1)) * total];
-      float p = 0.f;
-#pragma unroll
-      for (int z = 0; z < kSlabGroup; ++z)
-        if (z < nz) p += v[z];
-      part[g][el] = p;
+  for (int i = 1; i < kF32RedMax; ++i)
+    if (i == k) {
+      sg = a.seg[i];
+      b0 = a.bstart[i];
     }
-    __syncthreads();
-    if (q == 0 && live) {
-      float t;
-      if (staged) {
-        t = part[0][el];
-        for (int g = 1; g < ngroups; ++g) t += part[g][el];
-      } else {  // more slices than the LDS stage holds: every group in order by this thread
-        t = 0.f;
-        for (int g = 0; g < ngroups; ++g) {
-          const int z0 = g * kSlabGroup, z1 = min(z0 + kSlabGroup, sg.slices);
-          float p = 0.f;
-          for (int z = z0; z < z1; ++z) p += sg.slab[static_cast<int64_t>(z) * total + e];
-          t = g == 0 ? p : t + p;
-        }
-      }
-      const int m = e / sg.ncol, n = e - m * sg.ncol;
-      if (n < sg.Nw) sg.dw[m * sg.Nw + n] = t;
-      else sg.db[m] = t;
-    }
-    __syncthreads();  // part reusable
+  const int total = sg.Kout * sg.ncol, blk = (int)blockIdx.x - b0;
+  const int ngroups = (sg.slices + kSlabGroup - 1) / kSlabGroup;
+  if (ngroups == 1) {  // 256 elements, one thread each
+    const int e = blk * 256 + (int)threadIdx.x;
+    if (e < total) red_store_f32(sg, e, red_group(sg, total, e, 0));
+    return;
   }
+  const int el = threadIdx.x % kRedElems, q = threadIdx.x / kRedElems;
+  const int e = blk * kRedElems + el;
+  const bool live = e < total;
+  const bool staged = ngroups <= kRedMaxGroups;
+  for (int g = q; live && staged && g < ngroups; g += kRedLanes) part[g][el] = red_group(sg, total, e, g * kSlabGroup);
+  __syncthreads();
+  if (q != 0 || !live) return;
+  float t;
+  if (staged) {
+    t = part[0][el];
+    for (int g = 1; g < ngroups; ++g) t += part[g][el];
+  } else {  // more slices than the LDS stage holds: every group in order by this thread
+    t = red_group(sg, total, e, 0);
+    for (int g = 1; g < ngroups; ++g) t += red_group(sg, total, e, g * kSlabGroup);
+  }
+  red_store_f32(sg, e, t);
 }
 
 // dx = sum over the split-K planes of NCHWSlabOut, in plane order (deterministic); n4 = plane / 4
@@ -2188,13 +2192,16 @@ void f32_slab_reduce_multi(const F32RedList& segs, hipStream_t s) {
   }
   F32RedArgs a{};
   a.n = static_cast<int>(segs.size());
-  a.start[0] = 0;
+  int blocks = 0;
   for (int i = 0; i < a.n; ++i) {
     a.seg[i] = segs[i];
-    a.start[i + 1] = a.start[i] + segs[i].Kout * segs[i].ncol;
+    a.bstart[i] = blocks;
+    const int total = segs[i].Kout * segs[i].ncol;
+    const int per = segs[i].slices <= kSlabGroup ? 256 : kRedElems;  // the kernel's two workgroup kinds
+    blocks += (total + per - 1) / per;
   }
-  for (int i = a.n + 1; i <= kF32RedMax; ++i) a.start[i] = a.start[a.n];
-  const int grid = std::max(1, std::min((a.start[a.n] + kRedElems - 1) / kRedElems, 8192));
+  for (int i = a.n; i < kF32RedMax; ++i) a.bstart[i] = blocks;
+  const int grid = blocks;
   hipLaunchKernelGGL(f32_reduce_multi_kernel, dim3(grid), dim3(256), 0, s, a);
 }
 
