@@ -629,6 +629,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean"), py::arg("std"), py::arg("dw"), py::arg("with_bias"),
         "weight-gradient GEMM with its reduction deferred: (slab, [slices, Kout, Nw, ncol])");
   m.def("f32_conv1_wgrad_slab", &ops::f32_conv1_wgrad_slab);
+  m.def("f32_conv_dgrad_pool2s1_bwd", &ops::f32_conv_dgrad_pool2s1_bwd,
+        "conv data gradient + the 2x2/s1 pool backward of its input in one pass over the split-K planes");
   m.def("f32_fc_ce_pool3_bwd", &ops::f32_fc_ce_pool3_bwd,
         "fp32 ConvNet head backward: cross entropy + fc1 data gradient + pool3 backward in one launch -> (dl, dz3)");
   m.def("f32_slab_reduce_multi", &ops::f32_slab_reduce_multi,

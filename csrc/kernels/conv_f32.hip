@@ -792,9 +792,12 @@ __global__ __launch_bounds__(256) void pool2s1_bwd_kernel(const float* __restric
 constexpr int kP2Tile = 16;
 // CPH / CPW > 0: compile-time window grid (the ConvNet's 10 x 10: the output index divisions become multiplies)
 template <int CPH, int CPW>
+// slices > 1: da is the data-gradient GEMM's split-K planes (slices x plane floats), summed in slice order while the
+// tile is staged - the same sums as slab_sum_kernel, without its launch and the da round trip
 __global__ __launch_bounds__(256) void pool2s1_bwd_tile_kernel(const float* __restrict__ da,
                                                                const unsigned char* __restrict__ code,
-                                                               float* __restrict__ dz, int ntiles, int PH_, int PW_) {
+                                                               float* __restrict__ dz, int ntiles, int PH_, int PW_,
+                                                               int slices, int64_t plane) {
   const int PH = CPH > 0 ? CPH : PH_, PW = CPW > 0 ? CPW : PW_;
   __shared__ __attribute__((aligned(16))) float D[kP2Tile * 128];
   __shared__ __attribute__((aligned(16))) unsigned char Cd[kP2Tile * 128];
@@ -803,7 +806,17 @@ __global__ __launch_bounds__(256) void pool2s1_bwd_tile_kernel(const float* __re
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t p0 = (int64_t)t * kP2Tile;
     const float4* src = reinterpret_cast<const float4*>(da + p0 * phw);
-    for (int e = tid; e < n4; e += 256) reinterpret_cast<float4*>(D)[e] = src[e];
+    for (int e = tid; e < n4; e += 256) {
+      float4 acc = src[e];
+      for (int z = 1; z < slices; ++z) {
+        const float4 v = reinterpret_cast<const float4*>(da + z * plane + p0 * phw)[e];
+        acc.x += v.x;
+        acc.y += v.y;
+        acc.z += v.z;
+        acc.w += v.w;
+      }
+      reinterpret_cast<float4*>(D)[e] = acc;
+    }
     const uint4* cs = reinterpret_cast<const uint4*>(code + p0 * phw);
     for (int e = tid; e < n16; e += 256) reinterpret_cast<uint4*>(Cd)[e] = cs[e];
     __syncthreads();
@@ -2274,6 +2287,33 @@ void fc_ce_pool3_bwd_f32(const float* logits, const int64_t* labels, const float
                      ignore_index, eps, reduction, wfc, code3, dl, dz3);
 }
 
+bool conv_f32_dgrad_pool2s1_ok(const ConvF32Geom& g) {
+  const int64_t BC = g.B * g.C;
+  return conv_f32_dgrad_slices(g) > 1 && !conv_dgrad_f32_scatter_ok(g) && g.H == 10 && g.W == 10 && BC % kP2Tile == 0;
+}
+
+void conv_f32_dgrad_pool2s1_bwd(const ConvF32Geom& g, const float* dz, const float* w, float* slab, int slices,
+                                const unsigned char* code, float* dzp, hipStream_t s) {
+  // conv_f32_dgrad's split-K GEMM into slab (its planes are the pool's da), then the tiled 2x2/s1 pool backward
+  // summing the planes as it stages them: one launch fewer than dgrad + slab_sum + pool backward
+  const int K = g.Kout * g.R * g.R;
+  const int64_t zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW;
+  const int M = static_cast<int>(g.B * g.H * g.W);
+  const int plane = M * g.C;
+  int per = (K + slices - 1) / slices;
+  per = (per + BK - 1) / BK * BK;
+  const int used = (K + per - 1) / per;
+  DgradA la{{dz, static_cast<int>(g.B * zin * 4), 0.f, 1.f}, g.Kout, g.W, g.R, g.OH, g.OW, g.pad, K, M,
+            make_fdiv(g.H * g.W), make_fdiv(g.W)};
+  DgradB lb{{w, K * g.C * 4, 0.f, 1.f}, g.C, g.R * g.R, K, make_fdiv(g.R * g.R)};
+  NCHWSlabOut epi{slab, g.C, M, plane, make_fdiv(g.H * g.W)};
+  launch_gemm(M, g.C, K, per, used, -1, la, lb, epi, s);
+  const int ntiles = static_cast<int>(g.B * g.C / kP2Tile);
+  const dim3 grid(std::min(ntiles, 8 * f32_num_cus()));
+  hipLaunchKernelGGL((pool2s1_bwd_tile_kernel<10, 10>), grid, dim3(256), 0, s, slab, code, dzp, ntiles, 10, 10, used,
+                     static_cast<int64_t>(plane));
+}
+
 void pool_relu_f32_bwd(const float* da, const unsigned char* code, float* dz, int64_t BC, int H, int W, int k,
                        int st, hipStream_t s) {
   const int PH = (H - k) / st + 1, PW = (W - k) / st + 1;
@@ -2293,10 +2333,10 @@ void pool_relu_f32_bwd(const float* da, const unsigned char* code, float* dz, in
       const dim3 grid(std::min(ntiles, 8 * f32_num_cus()));
       if (PH == 10 && PW == 10)
         hipLaunchKernelGGL((pool2s1_bwd_tile_kernel<10, 10>), grid, dim3(256), 0, s, da + c0 * PH * PW,
-                           code + c0 * PH * PW, dz + c0 * H * W, ntiles, PH, PW);
+                           code + c0 * PH * PW, dz + c0 * H * W, ntiles, PH, PW, 1, int64_t{0});
       else
         hipLaunchKernelGGL((pool2s1_bwd_tile_kernel<0, 0>), grid, dim3(256), 0, s, da + c0 * PH * PW,
-                           code + c0 * PH * PW, dz + c0 * H * W, ntiles, PH, PW);
+                           code + c0 * PH * PW, dz + c0 * H * W, ntiles, PH, PW, 1, int64_t{0});
       continue;
     }
     if (k == 2 && st == 1) {

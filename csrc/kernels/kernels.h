@@ -126,6 +126,12 @@ void conv_dgrad_f32_scatter(const ConvF32Geom& g, const float* dz, const float* 
                             hipStream_t s);
 void conv_f32_dgrad(const ConvF32Geom& g, const float* dz, const float* w, float* dx, float* slab, int slices,
                     hipStream_t s);
+// The data gradient of a conv whose input came from a 2x2/s1 max-pool of a 11x11 map (the ConvNet's conv3 at small
+// batches: split K) with that pool's backward in the same pass over the split-K planes: dzp [B][C][11][11].
+// ok: split K applies, H = W = 10 and B*C a multiple of the pool tile; slab: conv_f32_dgrad_slices(g) planes.
+bool conv_f32_dgrad_pool2s1_ok(const ConvF32Geom& g);
+void conv_f32_dgrad_pool2s1_bwd(const ConvF32Geom& g, const float* dz, const float* w, float* slab, int slices,
+                                const unsigned char* code, float* dzp, hipStream_t s);
 // split-K weight (+ bias, when db != nullptr) gradient; slab: slices * Kout * (C*R*R + 1) floats
 int conv_f32_wgrad_slices(const ConvF32Geom& g);
 // One fixed-order slab reduction (f32_slab_reduce) as a segment of a multi-segment launch

@@ -706,17 +706,21 @@ __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16* __restrict
 // torchvision resnet18(num_classes=10)).  The work is tiny (N x C x J MACs); what costs is launches.
 // Thread layout: 8 channels per thread, C/8 threads per image, 256/(C/8) images per pass.
 constexpr int kHeadMaxJ = 16;
-__global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ x, int N, int HW, int C, int J,
+// JT: the class count at compile time (10: CIFAR), 0: run-time J <= kHeadMaxJ (per-class guards become branches)
+template <int JT>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ x, int N, int HW, int C, int Jr,
                                                        const float* __restrict__ w, const float* __restrict__ b,
                                                        float* __restrict__ pooled, float* __restrict__ logits) {
   __shared__ float part[256][kHeadMaxJ + 1];
+  constexpr int JM = JT > 0 ? JT : kHeadMaxJ;
+  const int J = JT > 0 ? JT : Jr;
   const int cv = C >> 3, ipp = 256 / cv;
   const int col = threadIdx.x % cv, sub = threadIdx.x / cv;
   const int n = blockIdx.x * ipp + sub;
   const bool live = sub < ipp && n < N;
-  float acc[kHeadMaxJ];
+  float acc[JM];
 #pragma unroll
-  for (int j = 0; j < kHeadMaxJ; ++j) acc[j] = 0.f;
+  for (int j = 0; j < JM; ++j) acc[j] = 0.f;
   if (live) {
     float s[8];
 #pragma unroll
@@ -734,8 +738,8 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
     pr[0] = make_float4(s[0], s[1], s[2], s[3]);
     pr[1] = make_float4(s[4], s[5], s[6], s[7]);
 #pragma unroll
-    for (int j = 0; j < kHeadMaxJ; ++j) {
-      if (j < J) {
+    for (int j = 0; j < JM; ++j) {
+      if (JT > 0 || j < J) {
         float wv[8];
         load8(w + (int64_t)j * C + col * 8, wv);
 #pragma unroll
@@ -744,7 +748,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16* __restrict__ 
     }
   }
 #pragma unroll
-  for (int j = 0; j < kHeadMaxJ; ++j) part[threadIdx.x][j] = acc[j];
+  for (int j = 0; j < JM; ++j) part[threadIdx.x][j] = acc[j];
   __syncthreads();
   // one thread per (image, class): the image's cv partials in column order (fixed)
   for (int o = threadIdx.x; o < ipp * J; o += 256) {
@@ -775,11 +779,13 @@ __device__ __forceinline__ float head_dl(const float* __restrict__ dl, const CeF
 // C/16 workgroups after them dW (16 channels each, the batch summed by 16 row groups combined in a fixed
 // order) and, in the first of those, db.  No partial sums cross workgroups: one launch, deterministic.
 constexpr int kHeadRows = 256;  // logits-gradient rows staged in LDS per chunk (dW role)
-template <bool kCE>
+template <bool kCE, int JT>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dl, CeFuse ce,
                                                        const float* __restrict__ pooled, const float* __restrict__ w,
-                                                       int N, int HW, int C, int J, int nb_dx, bf16* __restrict__ dx,
+                                                       int N, int HW, int C, int Jr, int nb_dx, bf16* __restrict__ dx,
                                                        float* __restrict__ dw, float* __restrict__ db) {
+  constexpr int JM = JT > 0 ? JT : kHeadMaxJ;
+  const int J = JT > 0 ? JT : Jr;
   __shared__ float g[kHeadRows][kHeadMaxJ];
   const float sc = kCE ? (ce.reduction == 0 ? 1.f : 1.f / ce.denom[0]) : 1.f;
   if ((int)blockIdx.x < nb_dx) {
@@ -797,8 +803,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = 0.f;
 #pragma unroll
-    for (int j = 0; j < kHeadMaxJ; ++j) {
-      if (j < J) {
+    for (int j = 0; j < JM; ++j) {
+      if (JT > 0 || j < J) {
         const float gj = g[sub][j];
         float wv[8];
         load8(w + (int64_t)j * C + col * 8, wv);
@@ -820,9 +826,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
   float (*red)[16][kHeadMaxJ] = reinterpret_cast<float (*)[16][kHeadMaxJ]>(&g[0][0]);  // [16 rq][16 cl][J]
   const int c0 = ((int)blockIdx.x - nb_dx) * 16, cl = threadIdx.x & 15, rq = threadIdx.x >> 4;
   const int c = c0 + cl;
-  float a[kHeadMaxJ], bsum = 0.f;
+  float a[JM], bsum = 0.f;
 #pragma unroll
-  for (int j = 0; j < kHeadMaxJ; ++j) a[j] = 0.f;
+  for (int j = 0; j < JM; ++j) a[j] = 0.f;
   for (int r0 = 0; r0 < N; r0 += kHeadRows) {
     const int rows = min(kHeadRows, N - r0);
     __syncthreads();  // the previous chunk's readers are done
@@ -847,8 +853,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
       for (int r = rq; r < rows; r += 16) {
         const float p = pooled[(int64_t)(r0 + r) * C + c];
 #pragma unroll
-        for (int j = 0; j < kHeadMaxJ; ++j)
-          if (j < J) a[j] = fmaf(g[r][j], p, a[j]);
+        for (int j = 0; j < JM; ++j)
+          if (JT > 0 || j < J) a[j] = fmaf(g[r][j], p, a[j]);
       }
     }
     if (blockIdx.x == nb_dx && threadIdx.x < J)
@@ -856,8 +862,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
   }
   __syncthreads();  // g is reused as red
 #pragma unroll
-  for (int j = 0; j < kHeadMaxJ; ++j)
-    if (j < J) red[rq][cl][j] = a[j];
+  for (int j = 0; j < JM; ++j)
+    if (JT > 0 || j < J) red[rq][cl][j] = a[j];
   __syncthreads();
   for (int o = threadIdx.x; o < 16 * J; o += 256) {
     const int j = o >> 4, cc = o & 15;
@@ -1072,7 +1078,11 @@ bool head_ok(int C, int J) { return J >= 1 && J <= kHeadMaxJ && C % 8 == 0 && C 
 void head_fwd(const void* x, int N, int HW, int C, int J, const float* w, const float* b, float* pooled,
               float* logits, hipStream_t s) {
   const int ipp = 256 / (C / 8);
-  head_fwd_kernel<<<(N + ipp - 1) / ipp, 256, 0, s>>>(static_cast<const bf16*>(x), N, HW, C, J, w, b, pooled, logits);
+  const bf16* xb = static_cast<const bf16*>(x);
+  if (J == 10)
+    head_fwd_kernel<10><<<(N + ipp - 1) / ipp, 256, 0, s>>>(xb, N, HW, C, J, w, b, pooled, logits);
+  else
+    head_fwd_kernel<0><<<(N + ipp - 1) / ipp, 256, 0, s>>>(xb, N, HW, C, J, w, b, pooled, logits);
 }
 
 void head_bwd(const float* dl, const CeFuse* ce, const float* pooled, const float* w, int N, int HW, int C, int J,
@@ -1080,10 +1090,15 @@ void head_bwd(const float* dl, const CeFuse* ce, const float* pooled, const floa
   const int ipp = 256 / (C / 8), nb_dx = (N + ipp - 1) / ipp;
   const CeFuse c = ce ? *ce : CeFuse{};
   const int grid = nb_dx + (C + 15) / 16;
-  if (ce)
-    head_bwd_kernel<true><<<grid, 256, 0, s>>>(nullptr, c, pooled, w, N, HW, C, J, nb_dx, static_cast<bf16*>(dx), dw, db);
+  bf16* dxb = static_cast<bf16*>(dx);
+  if (ce && J == 10)
+    head_bwd_kernel<true, 10><<<grid, 256, 0, s>>>(nullptr, c, pooled, w, N, HW, C, J, nb_dx, dxb, dw, db);
+  else if (ce)
+    head_bwd_kernel<true, 0><<<grid, 256, 0, s>>>(nullptr, c, pooled, w, N, HW, C, J, nb_dx, dxb, dw, db);
+  else if (J == 10)
+    head_bwd_kernel<false, 10><<<grid, 256, 0, s>>>(dl, c, pooled, w, N, HW, C, J, nb_dx, dxb, dw, db);
   else
-    head_bwd_kernel<false><<<grid, 256, 0, s>>>(dl, c, pooled, w, N, HW, C, J, nb_dx, static_cast<bf16*>(dx), dw, db);
+    head_bwd_kernel<false, 0><<<grid, 256, 0, s>>>(dl, c, pooled, w, N, HW, C, J, nb_dx, dxb, dw, db);
 }
 
 void add_bf16(const void* a, const void* b, int64_t n, void* y, hipStream_t s) {

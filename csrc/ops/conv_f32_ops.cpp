@@ -3,6 +3,7 @@
 #include <torch/extension.h>
 
 #include "../kernels/kernels.h"
+#include "ops.h"
 #include "util.h"
 
 namespace ringdp {
@@ -207,6 +208,38 @@ void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, doub
 // Deferred weight gradients (the whole-network fp32 cross-entropy node, ringdp/ops/convnet_fp32.py): the GEMM /
 // kernel runs now, its fixed-order slab reduction is returned as (slab, [slices, Kout, Nw, ncol]) and launched
 // later by f32_slab_reduce_multi together with the other layers' (one launch per backward).
+// conv3's data gradient + pool2's (2x2/s1) backward at small batches: dz2 [B, C, 11, 11] from dz3, with the split-K
+// planes summed inside the pool backward (falls back to the two ops where that form does not apply)
+at::Tensor f32_conv_dgrad_pool2s1_bwd(const at::Tensor& dz, const at::Tensor& w, const at::Tensor& code) {
+  util::f32_gpu(dz, "conv_f32 dz");
+  util::f32_gpu(w, "conv_f32 weight");
+  kern::ConvF32Geom g;
+  g.B = dz.size(0);
+  g.Kout = static_cast<int>(w.size(0));
+  g.C = static_cast<int>(w.size(1));
+  g.R = static_cast<int>(w.size(2));
+  g.pad = 0;
+  g.OH = static_cast<int>(dz.size(2));
+  g.OW = static_cast<int>(dz.size(3));
+  g.H = g.OH + g.R - 1;
+  g.W = g.OW + g.R - 1;
+  RINGDP_CHECK(dz.dim() == 4 && dz.size(1) == g.Kout && dz.is_contiguous() && w.is_contiguous(),
+               "conv_f32 dgrad + pool: dz has shape ", dz.sizes());
+  RINGDP_CHECK(code.scalar_type() == at::kByte && code.dim() == 4 && code.size(0) == g.B && code.size(1) == g.C &&
+                   code.size(2) == g.H && code.size(3) == g.W && code.is_contiguous(),
+               "conv_f32 dgrad + pool: code must be [B, C, H, W] of the pooled map");
+  if (!kern::conv_f32_dgrad_pool2s1_ok(g)) {
+    at::Tensor dx = f32_conv_dgrad(dz, w, g.H, g.W, 0);
+    return f32_pool_relu_bwd(dx, code, g.H + 1, g.W + 1, 2, 1);
+  }
+  const int slices = kern::conv_f32_dgrad_slices(g);
+  at::Tensor slab = at::empty({static_cast<int64_t>(slices) * g.B * g.C * g.H * g.W}, dz.options());
+  at::Tensor dzp = at::empty({g.B, g.C, g.H + 1, g.W + 1}, dz.options());
+  kern::conv_f32_dgrad_pool2s1_bwd(g, dz.data_ptr<float>(), w.data_ptr<float>(), slab.data_ptr<float>(), slices,
+                                   code.data_ptr<uint8_t>(), dzp.data_ptr<float>(), util::stream_of(dz));
+  return dzp;
+}
+
 std::tuple<at::Tensor, std::vector<int64_t>> f32_conv_wgrad_slab(const at::Tensor& dz, const at::Tensor& x,
                                                                  int64_t pad, double mean, double std,
                                                                  const at::Tensor& dw, bool with_bias) {

@@ -128,6 +128,7 @@ void f32_conv1_wgrad(const at::Tensor& x, const at::Tensor& da1, const at::Tenso
 at::Tensor f32_conv_dgrad(const at::Tensor& dz, const at::Tensor& w, int64_t H, int64_t W, int64_t pad);
 void f32_conv_wgrad(const at::Tensor& dz, const at::Tensor& x, int64_t pad, double mean, double std,
                     at::Tensor& dw, const c10::optional<at::Tensor>& db);
+at::Tensor f32_conv_dgrad_pool2s1_bwd(const at::Tensor& dz, const at::Tensor& w, const at::Tensor& code);
 std::tuple<at::Tensor, std::vector<int64_t>> f32_conv_wgrad_slab(const at::Tensor& dz, const at::Tensor& x,
                                                                  int64_t pad, double mean, double std,
                                                                  const at::Tensor& dw, bool with_bias);

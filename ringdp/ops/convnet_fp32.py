@@ -169,11 +169,10 @@ class _NetCEF32(torch.autograd.Function):
         dz = dl.view(B, -1, 1, 1)
         x3 = a3.reshape(B, -1, 1, 1)
         segs.append(C.f32_conv_wgrad_slab(dz, x3, 0, 0.0, 1.0, dwfc.view(wfc.shape[0], -1, 1, 1), True) + (dwfc, dbfc))
-        # conv3
-        da2 = C.f32_conv_dgrad(dz3, w3.detach(), a2.shape[2], a2.shape[3], 0)
+        # conv3 (its data gradient's split-K planes summed inside pool2's 2x2 / s1 backward)
         segs.append(C.f32_conv_wgrad_slab(dz3, a2, 0, 0.0, 1.0, dw3, True) + (dw3, db3))
-        # pool2 (2x2 / s1) + conv2
-        dz2 = C.f32_pool_relu_bwd(da2, code2, a2.shape[2] + 1, a2.shape[3] + 1, 2, 1)
+        dz2 = C.f32_conv_dgrad_pool2s1_bwd(dz3, w3.detach(), code2)
+        # conv2
         da1 = C.f32_conv_dgrad(dz2, w2.detach(), a1.shape[2], a1.shape[3], 0)
         segs.append(C.f32_conv_wgrad_slab(dz2, a1, 0, 0.0, 1.0, dw2, True) + (dw2, db2))
         # conv1 (+ pool1, folded into its weight gradient)

@@ -285,6 +285,21 @@ def test_fp32_net_node_matches_per_layer_backward(B):
     assert all(p.grad is not None for p in m_c.parameters())
 
 
+@pytest.mark.parametrize("B", [100, 64, 37])
+def test_conv_dgrad_pool2s1_fused_matches_two_ops(B):
+    """conv3's data gradient with pool2's 2x2/s1 backward summing the split-K planes as it stages them == the
+    data gradient (planes summed by slab_sum) followed by the pool backward, bit for bit (B=37: B*C not a multiple
+    of the pool tile -> the two-op fallback)."""
+    g = torch.Generator(device=DEV).manual_seed(B)
+    w = torch.randn(128, 64, 3, 3, device=DEV, generator=g) * 0.1
+    dz = torch.randn(B, 128, 8, 8, device=DEV, generator=g)
+    code = torch.randint(0, 4, (B, 64, 10, 10), dtype=torch.uint8, device=DEV, generator=g)
+    code[torch.rand(code.shape, device=DEV, generator=g) < 0.3] = 255
+    fused = C.f32_conv_dgrad_pool2s1_bwd(dz, w, code)
+    ref = C.f32_pool_relu_bwd(C.f32_conv_dgrad(dz, w, 10, 10, 0), code, 11, 11, 2, 1)
+    assert torch.equal(fused, ref)
+
+
 def _trajectory(model, forward, steps, xs, ys, lr):
     from ringdp.optim import SGD
 
