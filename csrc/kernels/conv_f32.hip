@@ -965,7 +965,9 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float4* __restrict_
 // ReLU + 2x2 max-pool (stride st) over the split-K planes of a plain NCHW conv output: each window value is
 // the in-order sum of its slices plus the bias (bias before the max, as PoolOut / PoolS1Out), the first maximum
 // in window order wins, code 255 where the result is 0.  One thread per pooled output.
-__global__ __launch_bounds__(256) void pool_slab_fwd_kernel(const float* __restrict__ slab, int slices, int plane,
+// SC: the slice count at compile time (all 4 x SC loads of a window issued together), 0: run-time slices
+template <int SC>
+__global__ __launch_bounds__(256) void pool_slab_fwd_kernel(const float* __restrict__ slab, int slices_rt, int plane,
                                                             const float* __restrict__ bias, int C, int OH, int OW,
                                                             int st, int PH, int PW, int total, float* __restrict__ a,
                                                             unsigned char* __restrict__ code) {
@@ -978,13 +980,17 @@ __global__ __launch_bounds__(256) void pool_slab_fwd_kernel(const float* __restr
   const int n = t % C;
   const int base = t * OH * OW + py * st * OW + px * st;  // t = b * C + n
   const float bn = bias ? bias[n] : 0.f;
+  const int slices = SC > 0 ? SC : slices_rt;
   float best = 0.f;
   int bt = 0;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = base + (u >> 1) * OW + (u & 1);
     float v = slab[i];
-    for (int z = 1; z < slices; ++z) v += slab[static_cast<int64_t>(z) * plane + i];
+#pragma unroll
+    for (int z = 1; z < (SC > 0 ? SC : 1); ++z) v += slab[static_cast<int64_t>(z) * plane + i];
+    if (SC == 0)
+      for (int z = 1; z < slices; ++z) v += slab[static_cast<int64_t>(z) * plane + i];
     v += bn;
     if (u == 0 || v > best) {
       best = v;
@@ -1537,8 +1543,20 @@ void conv_f32_fwd_pool_split(const ConvF32Geom& g, const float* x, const float* 
   launch_gemm(M, g.Kout, K, per, used, -1, la, lb, epi, s);
   const int PH = st == 2 ? g.OH / 2 : g.OH - 1, PW = st == 2 ? g.OW / 2 : g.OW - 1;
   const int total = static_cast<int>(g.B) * g.Kout * PH * PW;
-  hipLaunchKernelGGL(pool_slab_fwd_kernel, dim3((total + 255) / 256), dim3(256), 0, s, slab, used, plane, bias, g.Kout,
-                     g.OH, g.OW, st, PH, PW, total, a, code);
+  const dim3 grid((total + 255) / 256);
+#define RINGDP_POOL_SLAB(SCV)                                                                                         \
+  hipLaunchKernelGGL(pool_slab_fwd_kernel<SCV>, grid, dim3(256), 0, s, slab, used, plane, bias, g.Kout, g.OH, g.OW, st, \
+                     PH, PW, total, a, code)
+  switch (used) {
+    case 2: RINGDP_POOL_SLAB(2); break;
+    case 3: RINGDP_POOL_SLAB(3); break;
+    case 4: RINGDP_POOL_SLAB(4); break;
+    case 5: RINGDP_POOL_SLAB(5); break;
+    case 6: RINGDP_POOL_SLAB(6); break;
+    case 8: RINGDP_POOL_SLAB(8); break;
+    default: RINGDP_POOL_SLAB(0); break;
+  }
+#undef RINGDP_POOL_SLAB
 }
 
 // Small batches (the reference's 100 images): the data-gradient GEMM has few workgroups, each with one long k
