@@ -1024,11 +1024,13 @@ int64_t batch_chunk(int64_t B, std::initializer_list<int64_t> per_image) {
 }
 
 // RINGDP_F32_WGRAD_MIN_K: shallowest k slice of a weight gradient.  512 (was 1024): B=100 step 318 -> 296 us
-// (256: 297, 128: 306); B=65536 unchanged (profiles/r05/fp32/).
+// (256: 297, 128: 306); B=65536 unchanged (profiles/r05/fp32/).  320 on the round-6 step (every slab reduced by
+// one launch, so more slices cost little): 216 -> 209 us (192: 217, 256: 211, 384: 212, 1024: 241;
+// profiles/r06/fp32/b100_wgrad_depth_sweep.txt).
 int wgrad_min_depth() {
   static const int d = [] {
     const char* e = std::getenv("RINGDP_F32_WGRAD_MIN_K");
-    return e && *e ? std::max(BK, std::atoi(e)) : 512;
+    return e && *e ? std::max(BK, std::atoi(e)) : 320;
   }();
   return d;
 }
