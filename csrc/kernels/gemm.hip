@@ -1082,11 +1082,19 @@ static bool is_pointwise(const ConvGeom& g) {
 // Split count for a conv GEMM with few output tiles (ResNet-18 CIFAR layers 2-4 run 8-32 tiles of 128x128
 // on 256 CUs with 18-72 serial k-tiles each): enough splits to give ~2 workgroups per CU, >= 4 k-tiles per
 // split.  Returns the count the launcher will actually use (its rounding of the k-range per split).
+// RINGDP_CONV_SPLIT_WGS / RINGDP_CONV_SPLIT_MINKT / RINGDP_WGRAD_SPLIT_WGS / RINGDP_WGRAD_SPLIT_MINKT override the
+// workgroup targets and minimum k-tiles per split of the two split counts below (sweeps).
+static int split_knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? std::max(1, atoi(v)) : dflt;
+}
+
 int conv_gemm_splits(int M, int N, int K) {
+  static const int wgs = split_knob("RINGDP_CONV_SPLIT_WGS", 512), minkt = split_knob("RINGDP_CONV_SPLIT_MINKT", 4);
   const int64_t tiles = (int64_t)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   const int nkt = K / BK;
-  if (tiles >= 128 || nkt < 8) return 1;
-  int S = (int)std::min<int64_t>(nkt / 4, (512 + tiles - 1) / tiles);
+  if (tiles >= 128 || nkt < 2 * minkt) return 1;
+  int S = (int)std::min<int64_t>(nkt / minkt, (wgs + tiles - 1) / tiles);
   S = std::max(1, std::min(S, 32));
   int kps = (K + S - 1) / S;
   kps = (kps + BK - 1) / BK * BK;
@@ -1197,9 +1205,11 @@ void conv_wgrad_bf16(const void* dy, const void* x, const ConvGeom& g, int split
 
 int conv_wgrad_splits(const ConvGeom& g, int cus) {
   const int Mpos = g.N * g.P * g.Q, Kd = g.R * g.S * g.C;
+  static const int wgs = split_knob("RINGDP_WGRAD_SPLIT_WGS", 0), minkt = split_knob("RINGDP_WGRAD_SPLIT_MINKT", 4);
+  const int target = wgs > 0 ? wgs : 2 * cus;
   const int tiles = ((g.K + BM - 1) / BM) * ((Kd + BN - 1) / BN);
-  const int want = std::max(1, (2 * cus + tiles - 1) / tiles);
-  const int max_split = std::max(1, Mpos / (4 * BK));
+  const int want = std::max(1, (target + tiles - 1) / tiles);
+  const int max_split = std::max(1, Mpos / (minkt * BK));
   return std::min(want, max_split);
 }
 
