@@ -1565,8 +1565,10 @@ void conv_f32_fwd_pool_split(const ConvF32Geom& g, const float* x, const float* 
 // loop that is latency-bound (B=100 conv3: 626 workgroups of 32x32 x 72 k-tiles, 63 us).  Split K into slices
 // of ~8 k-tiles (at most 8 slices): the grid then takes the big-tile layouts again (fewer gathers per MFMA)
 // and the slices' partial dx planes are summed in order by slab_sum_kernel.  B=100 step, forced counts
-// (profiles/r05/fp32/): 1 slice 353 us, 2: 353, 3: 342, 4: 329, 6: 313, 8: 312, 12: 317.  Big batches (>= 8
-// 32x32 tiles per CU) and chunked batches keep one slice.  RINGDP_F32_DGRAD_SLICES=n forces n (1: off).
+// (profiles/r05/fp32/): 1 slice 353 us, 2: 353, 3: 342, 4: 329, 6: 313, 8: 312, 12: 317.  At least 6 slices on the
+// round-6 step (conv2's 18 k-tiles had 3): 209 -> 207 us (forced 4: 220, 10: 207;
+// profiles/r06/fp32/b100_slices_sweep.txt).  Big batches (>= 8 32x32 tiles per CU) and chunked batches keep one
+// slice.  RINGDP_F32_DGRAD_SLICES=n forces n (1: off).
 int conv_f32_dgrad_slices(const ConvF32Geom& g) {
   const int K = g.Kout * g.R * g.R;
   const int64_t zin = static_cast<int64_t>(g.Kout) * g.OH * g.OW, xout = static_cast<int64_t>(g.C) * g.H * g.W;
@@ -1574,7 +1576,7 @@ int conv_f32_dgrad_slices(const ConvF32Geom& g) {
   const int64_t M = g.B * g.H * g.W, plane = M * g.C;
   if (plane % 4 != 0) return 1;
   const int64_t tiles32 = ((M + 31) / 32) * ((g.C + 31) / 32);
-  int s = tiles32 >= 8 * f32_num_cus() ? 1 : std::min(8, (K + 8 * BK - 1) / (8 * BK));
+  int s = tiles32 >= 8 * f32_num_cus() ? 1 : std::min(8, std::max(6, (K + 8 * BK - 1) / (8 * BK)));
   if (const char* e = std::getenv("RINGDP_F32_DGRAD_SLICES")) {
     const int v = std::atoi(e);
     if (v > 0) s = v;
