@@ -3484,12 +3484,13 @@ static void c3_split(int B, bool dgrad, int& nd, int& ws) {
 
 // Images [0, result) of the conv3 data gradient run on the dgrad workgroups, the rest on the wgrad
 // workgroups after their weight-gradient slice (RINGDP_C3_STEAL = that share; large batches only, where
-// each dgrad workgroup has many images).
+// each dgrad workgroup has many images).  0.07 (was 0.1): B=65536 step 3.304-3.315 -> 3.259-3.292 ms, three
+// passes each of 0.06 / 0.07 / 0.08 all ahead of 0.1, 0.0 behind it (profiles/r06/c3_steal_sweep.txt).
 static int c3_dgrad_images(int B, int nd) {
   static const double steal = [] {
     const char* v = getenv("RINGDP_C3_STEAL");
-    const double f = v ? atof(v) : 0.1;
-    return f >= 0.0 && f < 0.9 ? f : 0.1;
+    const double f = v ? atof(v) : 0.07;
+    return f >= 0.0 && f < 0.9 ? f : 0.07;
   }();
   if (nd <= 0 || B < 32 * nd) return B;
   return B - (int)(steal * B);
