@@ -547,7 +547,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("running_mean"), py::arg("running_var"), py::arg("eps"), py::arg("momentum"), py::arg("residual"),
         py::arg("relu"), py::arg("num_batches_tracked") = py::none());
   m.def("bn_fwd_eval", &ops::bn_fwd_eval);
-  m.def("bn_bwd", &ops::bn_bwd);
+  m.def("bn_bwd", &ops::bn_bwd, py::arg("dy"), py::arg("y"), py::arg("z"), py::arg("save"), py::arg("gamma"),
+        py::arg("relu"), py::arg("dgamma"), py::arg("dbeta"), py::arg("need_g") = true);
   m.def("maxpool2d_fwd", &ops::maxpool2d_fwd);
   m.def("maxpool2d_bwd", &ops::maxpool2d_bwd);
   m.def("avgpool_fwd", &ops::avgpool_fwd);

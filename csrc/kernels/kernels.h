@@ -490,11 +490,16 @@ void bn_fold_act_fwd(const float* sums, int G, int64_t M, int C, const float* ga
 // (sum, sum of squares); returns the partial count.
 int bn_col_stats(const void* z, int64_t M, int C, float* part, hipStream_t s);
 int bn_bwd_parts(int64_t M, int C);
-void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
-                   float* part, void* g_out, hipStream_t s);
-// part 2: dgamma/dbeta and dz = scale*(g - mean(g) - zhat*mean(g*zhat))/..., plus d(residual) = g
+// ss != nullptr (bn_bwd_zmask_ok(C)): the ReLU mask from z and the forward's scale / shift instead of y; g_out may
+// be nullptr (the masked gradient is not stored)
+void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, const float* ss, bool relu,
+                   int64_t M, int C, float* part, void* g_out, hipStream_t s);
+bool bn_bwd_zmask_ok(int C);
+// part 2: dgamma/dbeta and dz = scale*(g - mean(g) - zhat*mean(g*zhat))/..., plus d(residual) = g.  With ss, g is
+// the unmasked dy and the mask is re-derived from z as in part 1.
 void bn_bwd_apply(const float* part, int nparts, float* scratch, const void* g, const void* z, const float* save,
-                  const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s);
+                  const float* ss, const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz,
+                  hipStream_t s);
 void maxpool_fwd(const void* x, int N, int H, int W, int C, int k, int stride, int pad, int P, int Q, void* y,
                  uint8_t* arg, hipStream_t s);
 void maxpool_bwd(const void* dy, const uint8_t* arg, int N, int H, int W, int C, int k, int stride, int pad, int P,

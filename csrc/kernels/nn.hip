@@ -391,8 +391,11 @@ __global__ __launch_bounds__(256) void bn_fold_act_fwd_kernel(const bf16* __rest
 // part != null (few partial rows, see kBnFewParts): every workgroup sums the [nparts][2][C] partials of
 // its channels itself in a fixed order and workgroup 0 stores dgamma / dbeta - two launches fewer than
 // the two-level reduction; otherwise dgamma / dbeta are inputs.
+// kZMask: g is the unmasked dy and the ReLU mask is re-derived from z and ss (see bn_bwd_reduce_kernel)
+template <bool kZMask>
 __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __restrict__ g, const bf16* __restrict__ z,
                                                                const float* __restrict__ save,
+                                                               const float* __restrict__ ss,
                                                                const float* __restrict__ gamma,
                                                                float* __restrict__ dgamma,
                                                                float* __restrict__ dbeta, const float* __restrict__ part,
@@ -400,10 +403,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __res
   const int cv = C >> 3, rpb = 256 / cv;
   const int col = threadIdx.x % cv, rsub = threadIdx.x / cv;
   const float invM = 1.f / (float)M;
-  float mean[8], inv[8], ga[8], dg[8], db[8], A[8], Bz[8], Cc[8];
+  float mean[8], inv[8], ga[8], dg[8], db[8], A[8], Bz[8], Cc[8], sc[8], sh[8];
   load8(save + col * 8, mean);
   load8(save + C + col * 8, inv);
   load8(gamma + col * 8, ga);
+  if constexpr (kZMask) {
+    load8(ss + col * 8, sc);
+    load8(ss + C + col * 8, sh);
+  }
   if (part) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) dg[j] = db[j] = 0.f;
@@ -477,7 +484,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __res
       if (rr < M) {
         bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = (bf16)fmaf(A[j], (float)gv[u][j], fmaf(Bz[j], (float)zv[u][j], Cc[j]));
+        for (int j = 0; j < 8; ++j) {
+          float gj = (float)gv[u][j];
+          if constexpr (kZMask) {
+            const bf16 yv = (bf16)fmaxf(fmaf((float)zv[u][j], sc[j], sh[j]), 0.f);
+            if (!((float)yv > 0.f)) gj = 0.f;
+          }
+          o[j] = (bf16)fmaf(A[j], gj, fmaf(Bz[j], (float)zv[u][j], Cc[j]));
+        }
         reinterpret_cast<bf16x8*>(dz)[rr * cv + col] = o;
       }
     }
@@ -496,8 +510,13 @@ inline int64_t bn_rows_per_part(int64_t M, int C) {
   return std::max<int64_t>(64, (M + 1023) / 1024);
 }
 
+// kZMask: the ReLU mask re-derived from z and the forward's scale / shift (ss: the same fmaf and bf16 rounding
+// as bn_act_fwd_col_kernel, so bit-identical to reading y) - a BN + ReLU without a residual add reads dy and z only.
+// g_out == nullptr: the masked gradient is not stored (nobody but the apply pass needs it, and that pass re-masks).
+template <bool kZMask>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restrict__ dy, const bf16* __restrict__ y,
                                                             const bf16* __restrict__ z, const float* __restrict__ save,
+                                                            const float* __restrict__ ss,
                                                             int relu, int64_t M, int C, int64_t rows_per_part,
                                                             float* __restrict__ part, bf16* __restrict__ g_out) {
   const int cv = C / 8;
@@ -511,11 +530,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
 #pragma unroll
   for (int j = 0; j < 8; ++j) sg[j] = sgz[j] = 0.f;
   if (rsub < rows_in_flight && col < lanes_per_row) {
-    float mean[8], inv[8];
+    float mean[8], inv[8], sc[8], sh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       mean[j] = save[col * 8 + j];
       inv[j] = save[C + col * 8 + j];
+      sc[j] = kZMask ? ss[col * 8 + j] : 0.f;
+      sh[j] = kZMask ? ss[C + col * 8 + j] : 0.f;
     }
     // kBnUnroll rows per step: 12 16-B loads in flight per thread (rows accumulate in a fixed order)
     for (int64_t r = r0 + rsub; r < r1; r += kBnUnroll * rows_in_flight) {
@@ -527,7 +548,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
           const int64_t v = rr * cv + col;
           d[u] = reinterpret_cast<const bf16x8*>(dy)[v];
           zz[u] = reinterpret_cast<const bf16x8*>(z)[v];
-          yy[u] = relu ? reinterpret_cast<const bf16x8*>(y)[v] : zero_bf16x8();
+          yy[u] = (relu && !kZMask) ? reinterpret_cast<const bf16x8*>(y)[v] : zero_bf16x8();
         }
       }
 #pragma unroll
@@ -537,13 +558,20 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const bf16* __restri
           bf16x8 go;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float g = (relu && !((float)yy[u][j] > 0.f)) ? 0.f : (float)d[u][j];
+            bool off;
+            if constexpr (kZMask) {
+              const bf16 yv = (bf16)fmaxf(fmaf((float)zz[u][j], sc[j], sh[j]), 0.f);
+              off = !((float)yv > 0.f);
+            } else {
+              off = relu && !((float)yy[u][j] > 0.f);
+            }
+            const float g = off ? 0.f : (float)d[u][j];
             go[j] = (bf16)g;
             const float gq = (float)go[j];
             sg[j] += gq;
             sgz[j] += gq * ((float)zz[u][j] - mean[j]) * inv[j];
           }
-          reinterpret_cast<bf16x8*>(g_out)[rr * cv + col] = go;
+          if (g_out) reinterpret_cast<bf16x8*>(g_out)[rr * cv + col] = go;
         }
       }
     }
@@ -1024,26 +1052,40 @@ int bn_col_stats(const void* z, int64_t M, int C, float* part, hipStream_t s) {
   return nparts;
 }
 
-void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, bool relu, int64_t M, int C,
-                   float* part, void* g_out, hipStream_t s) {
-  bn_bwd_reduce_kernel<<<bn_bwd_parts(M, C), 256, 0, s>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(y),
-                                                       static_cast<const bf16*>(z), save, relu ? 1 : 0, M, C,
-                                                       bn_rows_per_part(M, C), part, static_cast<bf16*>(g_out));
+void bn_bwd_reduce(const void* dy, const void* y, const void* z, const float* save, const float* ss, bool relu,
+                   int64_t M, int C, float* part, void* g_out, hipStream_t s) {
+  if (ss)
+    bn_bwd_reduce_kernel<true><<<bn_bwd_parts(M, C), 256, 0, s>>>(
+        static_cast<const bf16*>(dy), nullptr, static_cast<const bf16*>(z), save, ss, 1, M, C, bn_rows_per_part(M, C),
+        part, static_cast<bf16*>(g_out));
+  else
+    bn_bwd_reduce_kernel<false><<<bn_bwd_parts(M, C), 256, 0, s>>>(
+        static_cast<const bf16*>(dy), static_cast<const bf16*>(y), static_cast<const bf16*>(z), save, nullptr,
+        relu ? 1 : 0, M, C, bn_rows_per_part(M, C), part, static_cast<bf16*>(g_out));
 }
 
+bool bn_bwd_zmask_ok(int C) { return C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0; }
+
 void bn_bwd_apply(const float* part, int nparts, float* scratch, const void* g, const void* z, const float* save,
-                  const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz, hipStream_t s) {
+                  const float* ss, const float* gamma, int64_t M, int C, float* dgamma, float* dbeta, void* dz,
+                  hipStream_t s) {
   const int64_t nvec = M * C / 8;
-  if (C % 8 == 0 && C <= 2048 && 256 % (C / 8) == 0) {
+  if (bn_bwd_zmask_ok(C)) {
     const bool few = nparts <= kBnFewParts;  // the apply kernel sums the partials itself
     if (!few) reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);  // part[p][0] = sum g, [1] = sum g*zhat
     const int rpb = 256 / (C / 8);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((M + rpb * kBnUnroll - 1) / (rpb * kBnUnroll), 2048));
-    bn_bwd_apply_col_kernel<<<grid, 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save, gamma,
-                                                 dgamma, dbeta, few ? part : nullptr, nparts, M, C,
-                                                 static_cast<bf16*>(dz));
+    if (ss)
+      bn_bwd_apply_col_kernel<true><<<grid, 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save,
+                                                         ss, gamma, dgamma, dbeta, few ? part : nullptr, nparts, M, C,
+                                                         static_cast<bf16*>(dz));
+    else
+      bn_bwd_apply_col_kernel<false><<<grid, 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z),
+                                                          save, nullptr, gamma, dgamma, dbeta, few ? part : nullptr,
+                                                          nparts, M, C, static_cast<bf16*>(dz));
     return;
   }
+  // (ss is only passed when bn_bwd_zmask_ok(C): this fallback never sees the z-mask form)
   reduce_parts(part, nparts, C, scratch, dbeta, dgamma, s);
   bn_bwd_apply_kernel<<<grid_for(nvec), 256, 0, s>>>(static_cast<const bf16*>(g), static_cast<const bf16*>(z), save,
                                                      gamma, dgamma, dbeta, M, C, nvec, static_cast<bf16*>(dz));

@@ -374,12 +374,15 @@ std::tuple<at::Tensor, at::Tensor> bn_fwd_train(const at::Tensor& z, const at::T
                           y.data_ptr(), stream_of(z));
     return {y, save};
   }
-  at::Tensor ss = at::empty({2, C}, gamma.options());
+  // save4 = [mean, inv_std, scale, shift]: the backward of a BN + ReLU without a residual re-derives the ReLU mask
+  // from z and the scale / shift (bn_bwd need_g = false) instead of reading y
+  at::Tensor save4 = at::empty({4, C}, gamma.options());
+  float* ss = save4.data_ptr<float>() + 2 * C;
   kern::bn_prepare(sums.data_ptr<float>(), G, M, (int)C, gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)eps,
-                   (float)momentum, rm, rv, ss.data_ptr<float>(), save.data_ptr<float>(), nbt, stream_of(z));
+                   (float)momentum, rm, rv, ss, save4.data_ptr<float>(), nbt, stream_of(z));
   at::Tensor y = at::empty_like(z);
-  kern::bn_act_fwd(z.data_ptr(), ss.data_ptr<float>(), res, relu, M, (int)C, y.data_ptr(), stream_of(z));
-  return {y, save};
+  kern::bn_act_fwd(z.data_ptr(), ss, res, relu, M, (int)C, y.data_ptr(), stream_of(z));
+  return {y, save4};
 }
 
 at::Tensor bn_fwd_eval(const at::Tensor& z, const at::Tensor& scale_shift, const c10::optional<at::Tensor>& residual,
@@ -399,25 +402,31 @@ at::Tensor bn_fwd_eval(const at::Tensor& z, const at::Tensor& scale_shift, const
 
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& z,
                                           const at::Tensor& save, const at::Tensor& gamma, bool relu,
-                                          at::Tensor dgamma, at::Tensor dbeta) {
+                                          at::Tensor dgamma, at::Tensor dbeta, bool need_g) {
   bf16_gpu(dy, "bn output grad");
   bf16_gpu(z, "bn input");
-  if (relu) bf16_gpu(y, "bn output");
   const int64_t C = z.size(-1), M = z.numel() / C;
   RINGDP_CHECK(C % 8 == 0 && C <= 2048, "bn backward: channels must be a multiple of 8 and <= 2048");
   f32_gpu(dgamma, "bn dweight");
   f32_gpu(dbeta, "bn dbias");
+  f32_gpu(save, "bn save");
+  // need_g = false (no residual consumes the pre-activation gradient): nothing stores it.  Without ReLU the apply
+  // pass reads dy itself; with ReLU and bn_fwd_train's [4, C] save the mask comes from z and the forward's
+  // scale / shift (bit-identical to y > 0), so y is not read either.
+  const bool zmask = !need_g && relu && save.dim() == 2 && save.size(0) == 4 && kern::bn_bwd_zmask_ok((int)C);
+  const bool store_g = need_g || (relu && !zmask);
+  if (relu && !zmask) bf16_gpu(y, "bn output");
+  const float* ss = zmask ? save.data_ptr<float>() + 2 * C : nullptr;
   const int nparts = kern::bn_bwd_parts(M, (int)C);
   at::Tensor part = at::empty({nparts, 2, C}, gamma.options());
-  at::Tensor g = at::empty_like(z);  // dL/d(pre-activation) = the residual branch's gradient
-  kern::bn_bwd_reduce(dy.data_ptr(), relu ? y.data_ptr() : nullptr, z.data_ptr(), save.data_ptr<float>(), relu, M,
-                      (int)C, part.data_ptr<float>(), g.data_ptr(), stream_of(z));
+  at::Tensor g = store_g ? at::empty_like(z) : at::Tensor();  // dL/d(pre-activation): the residual's gradient
+  kern::bn_bwd_reduce(dy.data_ptr(), (relu && !zmask) ? y.data_ptr() : nullptr, z.data_ptr(), save.data_ptr<float>(),
+                      ss, relu, M, (int)C, part.data_ptr<float>(), store_g ? g.data_ptr() : nullptr, stream_of(z));
   at::Tensor dz = at::empty_like(z);
   at::Tensor scratch = at::empty({kern::reduce_parts_scratch_floats(nparts, (int)C)}, part.options());
-  kern::bn_bwd_apply(part.data_ptr<float>(), nparts, scratch.data_ptr<float>(), g.data_ptr(), z.data_ptr(),
-                     save.data_ptr<float>(),
-                     gamma.data_ptr<float>(), M, (int)C, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-                     dz.data_ptr(), stream_of(z));
+  kern::bn_bwd_apply(part.data_ptr<float>(), nparts, scratch.data_ptr<float>(), store_g ? g.data_ptr() : dy.data_ptr(),
+                     z.data_ptr(), save.data_ptr<float>(), ss, gamma.data_ptr<float>(), M, (int)C,
+                     dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), dz.data_ptr(), stream_of(z));
   return {dz, g};
 }
 

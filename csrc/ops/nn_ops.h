@@ -33,7 +33,7 @@ at::Tensor bn_fwd_eval(const at::Tensor& z, const at::Tensor& scale_shift, const
                        bool relu);
 std::tuple<at::Tensor, at::Tensor> bn_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& z,
                                           const at::Tensor& save, const at::Tensor& gamma, bool relu,
-                                          at::Tensor dgamma, at::Tensor dbeta);
+                                          at::Tensor dgamma, at::Tensor dbeta, bool need_g);
 std::tuple<at::Tensor, at::Tensor> maxpool2d_fwd(const at::Tensor& x, int64_t k, int64_t stride, int64_t pad);
 at::Tensor maxpool2d_bwd(const at::Tensor& dy, const at::Tensor& arg, int64_t H, int64_t W, int64_t k,
                          int64_t stride, int64_t pad);

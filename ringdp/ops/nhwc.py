@@ -57,15 +57,18 @@ def _cba_forward(x, w, gamma, beta, residual, running_mean, running_var, stride,
     return y, (z, y, save, crsk)
 
 
-def _cba_backward(saved, x, dy, w, gamma, beta, cfg, need_dx: bool, need_dw: bool, dx_residual=None):
+def _cba_backward(saved, x, dy, w, gamma, beta, cfg, need_dx: bool, need_dw: bool, dx_residual=None,
+                  need_g: bool = False):
     """BN backward, then the data gradient (+ dx_residual, summed in the GEMM epilogue) and the weight
-    gradient.  Returns (dx, dw, dgamma, dbeta, g) with g = d(pre-activation) (the residual's gradient)."""
+    gradient.  Returns (dx, dw, dgamma, dbeta, g) with g = d(pre-activation) (the residual's gradient), None
+    unless ``need_g``: then the BN backward neither stores it nor (BN + ReLU) reads y - the ReLU mask is
+    re-derived from z and the forward's scale / shift, bit-identically."""
     z, y, save, crsk = saved
     stride, pad, relu, training = cfg
     if not training:
         raise RuntimeError("ConvBNAct: backward through eval-mode batch norm is not supported")
     dgamma, dbeta = grad_buffer(gamma), grad_buffer(beta)
-    dz, g = C.bn_bwd(dy.contiguous(), y, z, save, gamma, relu, dgamma, dbeta)
+    dz, g = C.bn_bwd(dy.contiguous(), y, z, save, gamma, relu, dgamma, dbeta, need_g)
     dx = None
     if need_dx:
         res = dx_residual.contiguous() if dx_residual is not None else None
@@ -93,8 +96,9 @@ class ConvBNAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, *saved = ctx.saved_tensors
         w, gamma, beta = ctx.params
+        # with a residual in the forward the ReLU mask needs y (z alone does not give it): the stored-g form
         dx, dw, dgamma, dbeta, g = _cba_backward(saved, x, dy, w, gamma, beta, ctx.cfg, ctx.needs_input_grad[0],
-                                                 ctx.needs_input_grad[1])
+                                                 ctx.needs_input_grad[1], need_g=ctx.has_res)
         dres = g if (ctx.has_res and ctx.needs_input_grad[4]) else None
         return dx, dw, dgamma, dbeta, dres, None, None, None, None, None, None, None, None, None, None
 

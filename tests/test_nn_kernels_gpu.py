@@ -185,6 +185,13 @@ def test_batchnorm_fwd_bwd(relu, resid, shape):
     assert rel(dbeta, b_.grad) < 1e-2
     if resid:
         assert rel(g.permute(0, 3, 1, 2), resr.grad) < 1e-2
+    else:
+        # need_g=False: no stored pre-activation gradient; with ReLU the mask comes from z and the forward's
+        # scale / shift instead of y - bit-identical results
+        dg2, db2 = torch.empty_like(gamma), torch.empty_like(beta)
+        dz2, g2 = C().bn_bwd(dy.permute(0, 2, 3, 1).contiguous(), y, z, save, gamma, relu, dg2, db2, False)
+        assert g2 is None
+        assert torch.equal(dz2, dz) and torch.equal(dg2, dgamma) and torch.equal(db2, dbeta)
 
 
 def test_pools():
