@@ -505,9 +505,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_col_kernel(const bf16* __res
 // row slices so the reduction spreads over the whole chip (16 slices of a 50k x 1024 tensor took 7 ms per
 // ResNet-50 step more).
 constexpr int kBnFewParts = 32;
+// RINGDP_BN_MAX_PARTS / RINGDP_BN_MIN_ROWS: partial-row count and rows per part of the large tensors (sweeps)
 inline int64_t bn_rows_per_part(int64_t M, int C) {
+  static const int64_t max_parts = [] { const char* v = getenv("RINGDP_BN_MAX_PARTS"); return v && *v ? std::max(1, atoi(v)) : 1024; }();
+  static const int64_t min_rows = [] { const char* v = getenv("RINGDP_BN_MIN_ROWS"); return v && *v ? std::max(1, atoi(v)) : 64; }();
   if (M * C <= (int64_t)1 << 19) return std::max<int64_t>(32, (M + kBnFewParts - 1) / kBnFewParts);
-  return std::max<int64_t>(64, (M + 1023) / 1024);
+  return std::max<int64_t>(min_rows, (M + max_parts - 1) / max_parts);
 }
 
 // kZMask: the ReLU mask re-derived from z and the forward's scale / shift (ss: the same fmaf and bf16 rounding
